@@ -1,0 +1,398 @@
+// Exact ring GEMM over Z_2^64 / Z_2^128 on the gfx950 int8 matrix cores.
+//
+// There is no 64-bit integer MFMA, so every ring element is split into L signed 8-bit
+// limbs (L = 8 for Z_2^64, 16 for Z_2^128) in the *balanced* representation
+// x = sum_l d_l 256^l, d_l in [-128, 127] (carry propagated low to high; the carry out of
+// the top limb vanishes mod 2^(8L)).  Then
+//
+//     x . y  =  sum_{d < L} 256^d  sum_{i + j = d} (X_i . Y_j)      (mod 2^(8L))
+//
+// so the product needs the L(L+1)/2 limb-pair GEMMs on or below the anti-diagonal (36 for
+// Z_2^64, 136 for Z_2^128), each an i8 x i8 -> i32 MFMA (v_mfma_i32_32x32x32_i8).  Pairs on
+// the same anti-diagonal d accumulate into ONE i32 accumulator tile, so a wave holds L
+// accumulator tiles (16 regs each).  Diagonal d contributes S_d * 2^(8d) and only needs S_d
+// mod 2^(8(L-d)); for the low diagonals |S_d| <= (d+1) K' 2^14 < 2^31 whenever K' <= 8192
+// (Z_2^128) / 16384 (Z_2^64), and the high diagonals (8(L-d) <= 32) may wrap freely.
+// Longer K is split into chunks accumulated in the output.
+//
+// The RSS multiplication needs z_i = x_i.(y_i + y_{i+1}) + x_{i+1}.y_i per party.  That is
+// ONE GEMM with a doubled K: A' = [x_i | x_{i+1}], B' = [y_i + y_{i+1} ; y_i]  (mode 1).
+// The three parties of a stacked session are the batch dimension of one launch.
+//
+// Pipeline per call:
+//   1. prep_a / prep_b (memory-bound): limb-split A' and B' into a blocked, swizzled int8
+//      layout [batch][tile][k-step][limb][64 rows][32 bytes] so that each 64x32 tile of a
+//      limb plane is a contiguous 2 KB image whose 16-byte fragment reads are LDS
+//      bank-conflict free (halves of rows r and r+8 are swapped).
+//   2. gemm (MFMA-bound): 256-thread blocks (4 waves as 2x2), 64x64 output tile, each wave
+//      32x32 with L diagonal accumulators; K advances 32 limb-bytes per step, staged in LDS
+//      with a register prefetch of the next step.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <mutex>
+
+#include "moosex.h"
+
+using u64 = uint64_t;
+using u128 = unsigned __int128;
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+namespace {
+
+constexpr int TM = 64;  // rows of the block tile (A side)
+constexpr int TN = 64;  // cols of the block tile (B side)
+constexpr int TK = 32;  // limb-bytes per k-step (one MFMA K)
+constexpr int kTileBytes = 64 * TK;  // one limb plane of one tile per k-step: 2 KB
+
+__device__ __host__ inline int swz(int r, int h) { return r * TK + 16 * (h ^ ((r >> 3) & 1)); }
+
+template <class T>
+struct Limbs;
+template <>
+struct Limbs<u64> {
+  static constexpr int L = 8;
+};
+template <>
+struct Limbs<u128> {
+  static constexpr int L = 16;
+};
+
+// balanced signed limb split
+template <class T>
+__device__ inline void split_limbs(T x, int8_t* d) {
+  constexpr int L = Limbs<T>::L;
+#pragma unroll
+  for (int l = 0; l < L; ++l) {
+    int v = (int)(x & 0xff);
+    x >>= 8;
+    if (v >= 128) {
+      v -= 256;
+      x += 1;
+    }
+    d[l] = (int8_t)v;
+  }
+}
+
+// A' [batch, M, K'] (K' = K or 2K) -> blocked limbs. One thread: one row, 16 consecutive k'.
+template <class T>
+__global__ void k_prep_a(const T* __restrict__ A0, const T* __restrict__ A1, int64_t M,
+                         int64_t K, int mode, int8_t* __restrict__ out, int64_t Mp, int64_t Kp) {
+  constexpr int L = Limbs<T>::L;
+  const int64_t groups_k = Kp / 16;
+  const int64_t total = Mp * groups_k;
+  const int64_t b = blockIdx.y;
+  const T* a0 = A0 + b * M * K;
+  const T* a1 = mode ? A1 + b * M * K : nullptr;
+  const int64_t nkb = Kp / TK;
+  int8_t* ob = out + b * (Mp / TM) * nkb * (int64_t)L * kTileBytes;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = g / groups_k;
+    const int64_t k0 = (g % groups_k) * 16;
+    alignas(16) int8_t limbs[L][16];
+#pragma unroll 4
+    for (int j = 0; j < 16; ++j) {
+      int64_t k = k0 + j;
+      T v = 0;
+      if (m < M) {
+        if (k < K)
+          v = a0[m * K + k];
+        else if (mode && k < 2 * K)
+          v = a1[m * K + (k - K)];
+      }
+      int8_t d[L];
+      split_limbs<T>(v, d);
+#pragma unroll
+      for (int l = 0; l < L; ++l) limbs[l][j] = d[l];
+    }
+    const int64_t mb = m / TM, kb = k0 / TK;
+    const int r = (int)(m % TM), h = (int)((k0 % TK) / 16);
+    int8_t* base = ob + (mb * nkb + kb) * (int64_t)L * kTileBytes + swz(r, h);
+#pragma unroll
+    for (int l = 0; l < L; ++l) *(v4i*)(base + l * kTileBytes) = *(const v4i*)limbs[l];
+  }
+}
+
+// B' [batch, K', N] -> blocked limbs with n as the tile row.  mode 1: rows k < K hold
+// B0 + B1, rows K <= k < 2K hold B0.  One thread: one column, 16 consecutive k'.
+template <class T>
+__global__ void k_prep_b(const T* __restrict__ B0, const T* __restrict__ B1, int64_t K,
+                         int64_t N, int mode, int8_t* __restrict__ out, int64_t Np, int64_t Kp) {
+  constexpr int L = Limbs<T>::L;
+  const int64_t groups_k = Kp / 16;
+  const int64_t total = Np * groups_k;
+  const int64_t b = blockIdx.y;
+  const T* b0 = B0 + b * K * N;
+  const T* b1 = mode ? B1 + b * K * N : nullptr;
+  const int64_t nkb = Kp / TK;
+  int8_t* ob = out + b * (Np / TN) * nkb * (int64_t)L * kTileBytes;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    // consecutive threads take consecutive columns (coalesced row reads of B)
+    const int64_t n = g % Np;
+    const int64_t k0 = (g / Np) * 16;
+    alignas(16) int8_t limbs[L][16];
+#pragma unroll 4
+    for (int j = 0; j < 16; ++j) {
+      int64_t k = k0 + j;
+      T v = 0;
+      if (n < N) {
+        if (k < K) {
+          v = b0[k * N + n];
+          if (mode) v += b1[k * N + n];
+        } else if (mode && k < 2 * K) {
+          v = b0[(k - K) * N + n];
+        }
+      }
+      int8_t d[L];
+      split_limbs<T>(v, d);
+#pragma unroll
+      for (int l = 0; l < L; ++l) limbs[l][j] = d[l];
+    }
+    const int64_t nb = n / TN, kb = k0 / TK;
+    const int r = (int)(n % TN), h = (int)((k0 % TK) / 16);
+    int8_t* base = ob + (nb * nkb + kb) * (int64_t)L * kTileBytes + swz(r, h);
+#pragma unroll
+    for (int l = 0; l < L; ++l) *(v4i*)(base + l * kTileBytes) = *(const v4i*)limbs[l];
+  }
+}
+
+template <int L>
+__device__ inline void mfma_diagonals(const int8_t* __restrict__ As,
+                                      const int8_t* __restrict__ Bs, int arow, int brow,
+                                      int half, v16i (&acc)[L]) {
+  v4i bf[L];
+#pragma unroll
+  for (int j = 0; j < L; ++j) bf[j] = *(const v4i*)(Bs + j * kTileBytes + swz(brow, half));
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    v4i af = *(const v4i*)(As + i * kTileBytes + swz(arow, half));
+#pragma unroll
+    for (int j = 0; j < L - i; ++j)
+      acc[i + j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af, bf[j], acc[i + j], 0, 0, 0);
+  }
+}
+
+// XCD-aware remap of the flattened tile index: consecutive tiles of the same row band
+// land on the same XCD (blocks b and b+8 share an XCD under round-robin dispatch).
+__device__ inline int64_t xcd_remap(int64_t bid, int64_t nwg) {
+  const int64_t q = nwg / 8, r = nwg % 8;
+  const int64_t x = bid % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
+template <class T>
+__global__ void __launch_bounds__(256, 1)
+    k_gemm_limb(const int8_t* __restrict__ LA, const int8_t* __restrict__ LB,
+                T* __restrict__ C, int64_t M, int64_t N, int64_t Mp, int64_t Np, int64_t Kp,
+                int accumulate) {
+  constexpr int L = Limbs<T>::L;
+  constexpr int STAGE = L * kTileBytes;  // bytes per operand per k-step
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+  int8_t* As = smem;
+  int8_t* Bs = smem + STAGE;
+
+  const int64_t tiles_n = Np / TN, tiles_m = Mp / TM;
+  const int64_t ntiles = tiles_n * tiles_m;
+  const int64_t tid_flat = xcd_remap(blockIdx.x, ntiles);
+  const int64_t tm = tid_flat / tiles_n, tn = tid_flat % tiles_n;
+  const int64_t b = blockIdx.y;
+  const int64_t nkb = Kp / TK;
+
+  const int8_t* ga = LA + (b * tiles_m + tm) * nkb * (int64_t)STAGE;
+  const int8_t* gb = LB + (b * tiles_n + tn) * nkb * (int64_t)STAGE;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int arow = wr * 32 + (lane & 31);
+  const int brow = wc * 32 + (lane & 31);
+  const int half = lane >> 5;
+
+  v16i acc[L];
+#pragma unroll
+  for (int d = 0; d < L; ++d) acc[d] = v16i{0};
+
+  constexpr int PER_THREAD = STAGE / (256 * 16);  // 16-byte chunks per thread per operand
+  v4i pa[PER_THREAD], pb[PER_THREAD];
+#pragma unroll
+  for (int c = 0; c < PER_THREAD; ++c) {
+    pa[c] = *(const v4i*)(ga + (c * 256 + threadIdx.x) * 16);
+    pb[c] = *(const v4i*)(gb + (c * 256 + threadIdx.x) * 16);
+  }
+  for (int64_t kb = 0; kb < nkb; ++kb) {
+#pragma unroll
+    for (int c = 0; c < PER_THREAD; ++c) {
+      *(v4i*)(As + (c * 256 + threadIdx.x) * 16) = pa[c];
+      *(v4i*)(Bs + (c * 256 + threadIdx.x) * 16) = pb[c];
+    }
+    __syncthreads();
+    if (kb + 1 < nkb) {
+      const int8_t* na = ga + (kb + 1) * STAGE;
+      const int8_t* nb = gb + (kb + 1) * STAGE;
+#pragma unroll
+      for (int c = 0; c < PER_THREAD; ++c) {
+        pa[c] = *(const v4i*)(na + (c * 256 + threadIdx.x) * 16);
+        pb[c] = *(const v4i*)(nb + (c * 256 + threadIdx.x) * 16);
+      }
+    }
+    mfma_diagonals<L>(As, Bs, arow, brow, half, acc);
+    __syncthreads();
+  }
+
+  // epilogue: C[row][col] = sum_d sext(acc_d) << 8d
+  const int col = lane & 31;
+  const int64_t gcol = tn * TN + wc * 32 + col;
+  T* cb = C + b * M * N;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    const int64_t grow = tm * TM + wr * 32 + row;
+    T v = 0;
+#pragma unroll
+    for (int d = 0; d < L; ++d) v += ((T)(int64_t)acc[d][r]) << (8 * d);
+    if (grow < M && gcol < N) {
+      T* p = cb + grow * N + gcol;
+      *p = accumulate ? (T)(*p + v) : v;
+    }
+  }
+}
+
+struct Workspace {
+  void* ptr = nullptr;
+  int64_t bytes = 0;
+  int device = -1;
+};
+std::mutex g_ws_mu;
+Workspace g_ws[16];
+
+void* get_workspace(int64_t bytes) {
+  int dev = 0;
+  hipGetDevice(&dev);
+  if (dev < 0 || dev >= 16) return nullptr;
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  Workspace& w = g_ws[dev];
+  if (w.bytes < bytes) {
+    if (w.ptr) {
+      hipDeviceSynchronize();
+      hipFree(w.ptr);
+    }
+    w.ptr = nullptr;
+    if (hipMalloc(&w.ptr, bytes) != hipSuccess) {
+      w.ptr = nullptr;
+      w.bytes = 0;
+      return nullptr;
+    }
+    w.bytes = bytes;
+  }
+  return w.ptr;
+}
+
+inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+struct Plan {
+  int L;
+  int64_t Mp, Np, Kp, la_bytes, lb_bytes;
+};
+
+Plan make_plan(int words, int64_t batch, int64_t M, int64_t N, int64_t Kchunk, int mode) {
+  Plan p;
+  p.L = words == 1 ? 8 : 16;
+  p.Mp = round_up(M, TM);
+  p.Np = round_up(N, TN);
+  p.Kp = round_up(mode ? 2 * Kchunk : Kchunk, TK);
+  p.la_bytes = batch * p.Mp * p.Kp * p.L;
+  p.lb_bytes = batch * p.Np * p.Kp * p.L;
+  return p;
+}
+
+int64_t max_k_chunk(int words, int mode) {
+  // K' limit keeping the low diagonals exact in i32 (see header comment)
+  int64_t kp = words == 1 ? 16384 : 8192;
+  return mode ? kp / 2 : kp;
+}
+
+template <class T>
+int run(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T* A1, const T* B0,
+        const T* B1, int mode, T* C, int accumulate, void* ws, int64_t ws_bytes,
+        hipStream_t st) {
+  constexpr int L = Limbs<T>::L;
+  const int64_t kc = max_k_chunk(sizeof(T) == 8 ? 1 : 2, mode);
+  for (int64_t k0 = 0; k0 < K || (K == 0 && k0 == 0); k0 += kc) {
+    const int64_t kk = std::min(kc, K - k0);
+    Plan p = make_plan(sizeof(T) == 8 ? 1 : 2, batch, M, N, kk, mode);
+    if (p.la_bytes + p.lb_bytes > ws_bytes) return -5;
+    int8_t* la = (int8_t*)ws;
+    int8_t* lb = la + p.la_bytes;
+    // A chunk: columns [k0, k0+kk) of A0/A1 -> sub-matrix view with row stride K
+    // (handled by offsetting and passing K as the row stride through a temporary view)
+    const int threads = 256;
+    {
+      int64_t work = p.Mp * (p.Kp / 16);
+      int gx = (int)std::min<int64_t>((work + threads - 1) / threads, 4096);
+      if (kk == K) {
+        hipLaunchKernelGGL(k_prep_a<T>, dim3(gx, (unsigned)batch), dim3(threads), 0, st, A0, A1,
+                           M, K, mode, la, p.Mp, p.Kp);
+      } else {
+        return -6;  // chunked K handled by the caller (mx_gemm splits K)
+      }
+    }
+    {
+      int64_t work = p.Np * (p.Kp / 16);
+      int gx = (int)std::min<int64_t>((work + threads - 1) / threads, 4096);
+      hipLaunchKernelGGL(k_prep_b<T>, dim3(gx, (unsigned)batch), dim3(threads), 0, st, B0, B1,
+                         K, N, mode, lb, p.Np, p.Kp);
+    }
+    {
+      const int64_t ntiles = (p.Mp / TM) * (p.Np / TN);
+      const size_t lds = 2 * (size_t)L * kTileBytes;
+      hipLaunchKernelGGL(k_gemm_limb<T>, dim3((unsigned)ntiles, (unsigned)batch), dim3(256),
+                         lds, st, la, lb, C, M, N, p.Mp, p.Np, p.Kp, accumulate);
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return -100 - (int)e;
+    break;
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t mx_gemm_workspace_bytes(int words, int64_t batch, int64_t M, int64_t N, int64_t K,
+                                int mode) {
+  if (words != 1 && words != 2) return 0;
+  int64_t kk = std::min(K, max_k_chunk(words, mode));
+  Plan p = make_plan(words, batch, M, N, kk, mode);
+  return p.la_bytes + p.lb_bytes;
+}
+
+int mx_gemm_ws(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
+               const void* A1, const void* B0, const void* B1, int mode, void* C,
+               int accumulate, void* workspace, int64_t ws_bytes, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (words == 1)
+    return run<u64>(batch, M, N, K, (const u64*)A0, (const u64*)A1, (const u64*)B0,
+                    (const u64*)B1, mode, (u64*)C, accumulate, workspace, ws_bytes, st);
+  if (words == 2)
+    return run<u128>(batch, M, N, K, (const u128*)A0, (const u128*)A1, (const u128*)B0,
+                     (const u128*)B1, mode, (u128*)C, accumulate, workspace, ws_bytes, st);
+  return -2;
+}
+
+int mxh_gemm_mfma(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
+                  const void* A1, const void* B0, const void* B1, int mode, void* C,
+                  int accumulate, void* stream) {
+  if (K > max_k_chunk(words, mode)) return -6;  // caller splits long K
+  int64_t bytes = mx_gemm_workspace_bytes(words, batch, M, N, K, mode);
+  void* ws = get_workspace(bytes);
+  if (!ws) return -4;
+  return mx_gemm_ws(words, batch, M, N, K, A0, A1, B0, B1, mode, C, accumulate, ws, bytes,
+                    stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,95 @@
+// moosex native core: C ABI shared by the CPU (ring_cpu.cpp) and the gfx950 HIP
+// (ring_hip.hip, gemm_mfma.hip) implementations.
+//
+// Ring tensors: Z_2^64 elements are uint64 words; Z_2^128 elements are two little-endian
+// uint64 words (lo, hi) == the in-memory layout of unsigned __int128 on x86-64 and
+// AMDGPU.  "words" below is 1 (Z_2^64), 2 (Z_2^128) or 0 (one byte per element, used for
+// bit tensors holding 0/1).
+//
+// Every entry point returns 0 on success, a negative error code otherwise; `dev` is
+// 0 for host memory and 1 for device memory (then `stream` is a hipStream_t).
+#pragma once
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum mx_binop { MX_ADD = 0, MX_SUB = 1, MX_MUL = 2, MX_AND = 3, MX_OR = 4, MX_XOR = 5 };
+enum mx_unop { MX_NEG = 0, MX_NOT = 1, MX_SHL = 2, MX_SHR = 3, MX_SAR = 4 };
+enum mx_cmpop { MX_LT = 0, MX_GT = 1, MX_EQ = 2, MX_MSB = 3 };
+// RSS cross-term kinds: arithmetic (x0*y0 + x0*y1 + x1*y0 + a - b) or boolean (& and ^)
+enum mx_cross { MX_CROSS_ARITH = 0, MX_CROSS_BOOL = 1 };
+
+// AES-128 key schedule: 11 round keys of 4 big-endian-packed words (FIPS-197 layout)
+typedef struct {
+  uint32_t rk[44];
+} mx_aes_key;
+
+int mx_version(void);
+int mx_device_count(void);
+
+// out[i] = a[i] op b[i]; na, nb in {n, 1} (scalar broadcast)
+int mx_ew_binary(int dev, int op, int words, const void* a, int64_t na, const void* b,
+                 int64_t nb, void* out, int64_t n, void* stream);
+// out[i] = op(a[i], param)
+int mx_ew_unary(int dev, int op, int words, const void* a, void* out, int64_t n,
+                int64_t param, void* stream);
+// out[i] = (a[i] cmp b[i]) as 0/1 bytes, signed two's-complement comparison
+int mx_ew_compare(int dev, int op, int words, const void* a, int64_t na, const void* b,
+                  int64_t nb, uint8_t* out, int64_t n, void* stream);
+// out[i] = (a[i] >> bit) & 1
+int mx_bit_extract(int dev, int words, const void* a, uint8_t* out, int64_t n, int bit,
+                   void* stream);
+// out[i] = (ring) bits[i] << bit
+int mx_ring_inject(int dev, int words, const uint8_t* bits, void* out, int64_t n, int bit,
+                   void* stream);
+// out[i] = round(x[i] * 2^frac) mod 2^(64*words)
+int mx_encode(int dev, int words, const double* x, void* out, int64_t n, int frac,
+              void* stream);
+// out[i] = signed(x[i]) / 2^frac
+int mx_decode(int dev, int words, const void* x, double* out, int64_t n, int frac,
+              void* stream);
+// out[o, i] = sum_r a[o, r, i]
+int mx_sum_axis(int dev, int words, const void* a, void* out, int64_t outer, int64_t red,
+                int64_t inner, void* stream);
+// AES-128 in counter mode: block c (c = ctr0, ctr0+1, ...) = AES_k(nonce_le64 || c_le64);
+// writes nbytes bytes of the keystream
+int mx_prg(int dev, const uint8_t* key16, uint64_t nonce, uint64_t ctr0, void* out,
+           int64_t nbytes, void* stream);
+// AES-128 encryption of single 16-byte blocks (ECB) on the host; used for seed derivation
+int mx_aes_encrypt_blocks(const uint8_t* key16, const uint8_t* in, uint8_t* out,
+                          int64_t nblocks);
+// RSS local step for `nparties` stacked parties of n elements each:
+//   party p, element i: out = x0*y0 + x0*y1 + x1*y0 + PRF(key[p])_i - PRF(key[p+1])_i
+// (boolean flavour: & and ^).  keys has nparties+1 entries.  x1 or y1 may be null
+// (then those terms are dropped: used for local products with public values).  keys may be
+// null (no zero share).
+int mx_rss_cross(int dev, int kind, int words, const void* x0, const void* x1,
+                 const void* y0, const void* y1, void* out, int64_t n, int nparties,
+                 const uint8_t* keys16, uint64_t nonce, void* stream);
+// zero share only: out[p, i] = PRF(key[p])_i - PRF(key[p+1])_i (xor for kind BOOL)
+int mx_zero_share(int dev, int kind, int words, void* out, int64_t n, int nparties,
+                  const uint8_t* keys16, uint64_t nonce, void* stream);
+// PRF expansion of several keys: out[p, i] = PRF(key[p])_i (words 0 -> bytes & 1)
+int mx_prf_expand(int dev, int words, void* out, int64_t n, int nkeys,
+                  const uint8_t* keys16, uint64_t nonce, void* stream);
+// Batched ring GEMM.  mode 0: C = A0 . B0.  mode 1 (RSS cross): C = A0.(B0+B1) + A1.B0.
+// A* are [batch, M, K] row-major, B* are [batch, K, N] row-major, C is [batch, M, N].
+// accumulate != 0 -> C += result.
+int mx_gemm(int dev, int words, int64_t batch, int64_t M, int64_t N, int64_t K,
+            const void* A0, const void* A1, const void* B0, const void* B1, int mode,
+            void* C, int accumulate, void* stream);
+// Scratch for the MFMA GEMM (device only): bytes needed for the given problem
+int64_t mx_gemm_workspace_bytes(int words, int64_t batch, int64_t M, int64_t N,
+                                int64_t K, int mode);
+// GEMM variant using caller-provided device workspace (graph-capture friendly)
+int mx_gemm_ws(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
+               const void* A1, const void* B0, const void* B1, int mode, void* C,
+               int accumulate, void* workspace, int64_t ws_bytes, void* stream);
+// select the GEMM kernel: 0 = auto, 1 = force VALU reference kernel, 2 = force MFMA
+void mx_set_gemm_impl(int impl);
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,476 @@
+// Host (CPU) implementation of the moosex ring kernels.
+//
+// These are the correctness oracles for the gfx950 kernels (bit-exact ring arithmetic)
+// and the execution path of the CPU-only LocalMooseRuntime.  Z_2^128 uses the compiler's
+// unsigned __int128; AES uses AES-NI.  Work is split over a small pool of std::threads.
+#include <immintrin.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <thread>
+#include <vector>
+
+#include "aes_core.h"
+#include "moosex.h"
+#include "ring_common.h"
+
+namespace {
+
+using u64 = uint64_t;
+using u128 = unsigned __int128;
+using i128 = __int128;
+
+int num_threads() {
+  static int n = [] {
+    const char* e = getenv("MOOSEX_CPU_THREADS");
+    int v = e ? atoi(e) : (int)std::thread::hardware_concurrency();
+    return std::max(1, std::min(v, 32));
+  }();
+  return n;
+}
+
+template <class F>
+void parallel_for(int64_t n, int64_t grain, F f) {
+  int nt = num_threads();
+  if (n <= grain || nt == 1) {
+    if (n > 0) f(0, n);
+    return;
+  }
+  int64_t chunks = std::min<int64_t>(nt, (n + grain - 1) / grain);
+  int64_t per = (n + chunks - 1) / chunks;
+  std::vector<std::thread> ts;
+  ts.reserve(chunks - 1);
+  for (int64_t c = 1; c < chunks; ++c) {
+    int64_t b = c * per, e = std::min(n, b + per);
+    if (b < e) ts.emplace_back([=] { f(b, e); });
+  }
+  f(0, std::min(n, per));
+  for (auto& t : ts) t.join();
+}
+
+// ---------------------------------------------------------------------------
+// AES-NI keystream
+// ---------------------------------------------------------------------------
+struct NiKey {
+  __m128i rk[11];
+};
+
+__attribute__((target("aes,sse4.1"))) void ni_expand(const uint8_t* key, NiKey* k) {
+  uint32_t w[44];
+  mx::expand_key(key, w);
+  for (int r = 0; r < 11; ++r) {
+    uint8_t b[16];
+    for (int i = 0; i < 4; ++i) {
+      uint32_t x = w[4 * r + i];
+      b[4 * i] = x >> 24;
+      b[4 * i + 1] = x >> 16;
+      b[4 * i + 2] = x >> 8;
+      b[4 * i + 3] = x;
+    }
+    k->rk[r] = _mm_loadu_si128((const __m128i*)b);
+  }
+}
+
+__attribute__((target("aes,sse4.1"))) inline __m128i ni_encrypt(const NiKey& k, __m128i b) {
+  b = _mm_xor_si128(b, k.rk[0]);
+  for (int r = 1; r < 10; ++r) b = _mm_aesenc_si128(b, k.rk[r]);
+  return _mm_aesenclast_si128(b, k.rk[10]);
+}
+
+bool have_aesni() {
+  static bool v = __builtin_cpu_supports("aes");
+  return v;
+}
+
+struct SwKey {
+  uint32_t rk[44];
+};
+
+uint32_t g_T0[256];
+struct TInit {
+  TInit() {
+    for (int i = 0; i < 256; ++i) g_T0[i] = mx::t0_entry(mx::kSbox[i]);
+  }
+} g_tinit;
+
+// Fill `nblocks` keystream blocks starting at counter ctr into out (16 bytes each)
+__attribute__((target("aes,sse4.1"))) void keystream_ni(const NiKey& k, uint64_t nonce,
+                                                        uint64_t ctr, uint8_t* out,
+                                                        int64_t nblocks) {
+  for (int64_t i = 0; i < nblocks; ++i) {
+    __m128i in = _mm_set_epi64x((long long)(ctr + i), (long long)nonce);
+    _mm_storeu_si128((__m128i*)(out + 16 * i), ni_encrypt(k, in));
+  }
+}
+
+void keystream_sw(const SwKey& k, uint64_t nonce, uint64_t ctr, uint8_t* out, int64_t nblocks) {
+  for (int64_t i = 0; i < nblocks; ++i) {
+    uint32_t w[4], o[4];
+    mx::ctr_block_words(nonce, ctr + i, w);
+    mx::encrypt_block_tt(k.rk, g_T0, mx::kSbox, w[0], w[1], w[2], w[3], o);
+    uint64_t lo, hi;
+    mx::block_to_u64(o, &lo, &hi);
+    memcpy(out + 16 * i, &lo, 8);
+    memcpy(out + 16 * i + 8, &hi, 8);
+  }
+}
+
+struct Prf {
+  NiKey ni;
+  SwKey sw;
+  bool use_ni;
+  explicit Prf(const uint8_t* key) {
+    use_ni = have_aesni();
+    if (use_ni)
+      ni_expand(key, &ni);
+    else
+      mx::expand_key(key, sw.rk);
+  }
+  void blocks(uint64_t nonce, uint64_t ctr, uint8_t* out, int64_t n) const {
+    if (use_ni)
+      keystream_ni(ni, nonce, ctr, out, n);
+    else
+      keystream_sw(sw, nonce, ctr, out, n);
+  }
+};
+
+// keystream bytes [byte0, byte0 + nbytes) into out
+void keystream_range(const Prf& p, uint64_t nonce, int64_t byte0, int64_t nbytes, uint8_t* out) {
+  int64_t b0 = byte0 / 16, b1 = (byte0 + nbytes + 15) / 16;
+  uint8_t tmp[16 * 64];
+  int64_t pos = 0;
+  for (int64_t b = b0; b < b1; b += 64) {
+    int64_t nb = std::min<int64_t>(64, b1 - b);
+    p.blocks(nonce, (uint64_t)b, tmp, nb);
+    int64_t start = (b == b0) ? byte0 - b0 * 16 : 0;
+    int64_t avail = nb * 16 - start;
+    int64_t take = std::min(avail, nbytes - pos);
+    memcpy(out + pos, tmp + start, take);
+    pos += take;
+  }
+}
+
+// PRF element i of a ring with `words` words (0 -> 1 byte masked to a bit)
+template <class T>
+void prf_elements(const Prf& p, uint64_t nonce, int64_t i0, int64_t n, T* out) {
+  if constexpr (sizeof(T) == 1) {
+    keystream_range(p, nonce, i0, n, (uint8_t*)out);
+    for (int64_t i = 0; i < n; ++i) out[i] &= 1;
+  } else {
+    keystream_range(p, nonce, i0 * (int64_t)sizeof(T), n * (int64_t)sizeof(T), (uint8_t*)out);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// generic elementwise templates
+// ---------------------------------------------------------------------------
+template <class T>
+int binary_t(int op, const T* a, int64_t na, const T* b, int64_t nb, T* out, int64_t n) {
+  parallel_for(n, 1 << 16, [&](int64_t s, int64_t e) {
+    for (int64_t i = s; i < e; ++i) {
+      T x = a[na == 1 ? 0 : i], y = b[nb == 1 ? 0 : i];
+      out[i] = mxr::binop<T>(op, x, y);
+    }
+  });
+  return 0;
+}
+
+template <class T>
+int unary_t(int op, const T* a, T* out, int64_t n, int64_t param) {
+  parallel_for(n, 1 << 16, [&](int64_t s, int64_t e) {
+    for (int64_t i = s; i < e; ++i) out[i] = mxr::unop<T>(op, a[i], (int)param);
+  });
+  return 0;
+}
+
+template <class T>
+int compare_t(int op, const T* a, int64_t na, const T* b, int64_t nb, uint8_t* out, int64_t n) {
+  parallel_for(n, 1 << 16, [&](int64_t s, int64_t e) {
+    for (int64_t i = s; i < e; ++i)
+      out[i] = mxr::cmpop<T>(op, a[na == 1 ? 0 : i], b ? b[nb == 1 ? 0 : i] : (T)0);
+  });
+  return 0;
+}
+
+template <class T>
+int rss_cross_t(int kind, const T* x0, const T* x1, const T* y0, const T* y1, T* out, int64_t n,
+                int nparties, const uint8_t* keys, uint64_t nonce) {
+  for (int p = 0; p < nparties; ++p) {
+    const int64_t off = (int64_t)p * n;
+    Prf* ka = keys ? new Prf(keys + 16 * p) : nullptr;
+    Prf* kb = keys ? new Prf(keys + 16 * (p + 1)) : nullptr;
+    parallel_for(n, 1 << 14, [&](int64_t s, int64_t e) {
+      const int64_t CH = 1024;
+      T ra[CH], rb[CH];
+      for (int64_t c = s; c < e; c += CH) {
+        int64_t m = std::min(CH, e - c);
+        if (ka) {
+          prf_elements<T>(*ka, nonce, c, m, ra);
+          prf_elements<T>(*kb, nonce, c, m, rb);
+        }
+        for (int64_t j = 0; j < m; ++j) {
+          int64_t i = off + c + j;
+          T v;
+          if (x0 && y0) {
+            v = mxr::cross<T>(kind, x0[i], x1 ? x1[i] : (T)0, y0[i], y1 ? y1[i] : (T)0,
+                              x1 != nullptr, y1 != nullptr);
+          } else {
+            v = 0;
+          }
+          if (ka) v = mxr::zs_combine<T>(kind, v, ra[j], rb[j]);
+          out[i] = v;
+        }
+      }
+    });
+    delete ka;
+    delete kb;
+  }
+  return 0;
+}
+
+template <class T>
+int prf_expand_t(T* out, int64_t n, int nkeys, const uint8_t* keys, uint64_t nonce) {
+  for (int p = 0; p < nkeys; ++p) {
+    Prf k(keys + 16 * p);
+    parallel_for(n, 1 << 14, [&](int64_t s, int64_t e) {
+      prf_elements<T>(k, nonce, s, e - s, out + (int64_t)p * n + s);
+    });
+  }
+  return 0;
+}
+
+template <class T>
+int sum_axis_t(const T* a, T* out, int64_t outer, int64_t red, int64_t inner) {
+  parallel_for(outer * inner, 1 << 14, [&](int64_t s, int64_t e) {
+    for (int64_t oi = s; oi < e; ++oi) {
+      int64_t o = oi / inner, i = oi % inner;
+      T acc = 0;
+      const T* p = a + o * red * inner + i;
+      for (int64_t r = 0; r < red; ++r) acc += p[r * inner];
+      out[oi] = acc;
+    }
+  });
+  return 0;
+}
+
+template <class T>
+void gemm_plain(const T* A, const T* B, T* C, int64_t M, int64_t N, int64_t K, bool acc) {
+  parallel_for(M, 4, [&](int64_t s, int64_t e) {
+    std::vector<T> row(N);
+    for (int64_t i = s; i < e; ++i) {
+      std::fill(row.begin(), row.end(), (T)0);
+      const T* a = A + i * K;
+      for (int64_t k = 0; k < K; ++k) {
+        T av = a[k];
+        const T* b = B + k * N;
+        for (int64_t j = 0; j < N; ++j) row[j] += av * b[j];
+      }
+      T* c = C + i * N;
+      if (acc)
+        for (int64_t j = 0; j < N; ++j) c[j] += row[j];
+      else
+        for (int64_t j = 0; j < N; ++j) c[j] = row[j];
+    }
+  });
+}
+
+template <class T>
+int gemm_t(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T* A1,
+           const T* B0, const T* B1, int mode, T* C, int accumulate) {
+  for (int64_t b = 0; b < batch; ++b) {
+    const T* a0 = A0 + b * M * K;
+    const T* b0 = B0 + b * K * N;
+    T* c = C + b * M * N;
+    if (mode == 0) {
+      gemm_plain(a0, b0, c, M, N, K, accumulate != 0);
+    } else {
+      const T* a1 = A1 + b * M * K;
+      const T* b1 = B1 + b * K * N;
+      std::vector<T> bs(K * N);
+      for (int64_t i = 0; i < K * N; ++i) bs[i] = b0[i] + b1[i];
+      gemm_plain(a0, bs.data(), c, M, N, K, accumulate != 0);
+      gemm_plain(a1, b0, c, M, N, K, true);
+    }
+  }
+  return 0;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C ABI (host side); device variants live in ring_hip.hip and are reached through
+// the mxh_* symbols declared in ring_common.h
+// ---------------------------------------------------------------------------
+#define DISPATCH_WORDS(words, T, ...)                 \
+  switch (words) {                                    \
+    case 0: { using T = uint8_t; __VA_ARGS__; }        \
+    case 1: { using T = u64; __VA_ARGS__; }            \
+    case 2: { using T = u128; __VA_ARGS__; }           \
+    default: return -2;                               \
+  }
+
+extern "C" {
+
+int mx_version(void) { return 3; }
+
+int mx_ew_binary(int dev, int op, int words, const void* a, int64_t na, const void* b,
+                 int64_t nb, void* out, int64_t n, void* stream) {
+  if (dev) return mxh_ew_binary(op, words, a, na, b, nb, out, n, stream);
+  DISPATCH_WORDS(words, T,
+                 return binary_t<T>(op, (const T*)a, na, (const T*)b, nb, (T*)out, n));
+}
+
+int mx_ew_unary(int dev, int op, int words, const void* a, void* out, int64_t n,
+                int64_t param, void* stream) {
+  if (dev) return mxh_ew_unary(op, words, a, out, n, param, stream);
+  DISPATCH_WORDS(words, T, return unary_t<T>(op, (const T*)a, (T*)out, n, param));
+}
+
+int mx_ew_compare(int dev, int op, int words, const void* a, int64_t na, const void* b,
+                  int64_t nb, uint8_t* out, int64_t n, void* stream) {
+  if (dev) return mxh_ew_compare(op, words, a, na, b, nb, out, n, stream);
+  DISPATCH_WORDS(words, T,
+                 return compare_t<T>(op, (const T*)a, na, (const T*)b, nb, out, n));
+}
+
+int mx_bit_extract(int dev, int words, const void* a, uint8_t* out, int64_t n, int bit,
+                   void* stream) {
+  if (dev) return mxh_bit_extract(words, a, out, n, bit, stream);
+  DISPATCH_WORDS(words, T, {
+    const T* x = (const T*)a;
+    parallel_for(n, 1 << 16, [&](int64_t s, int64_t e) {
+      for (int64_t i = s; i < e; ++i) out[i] = (uint8_t)((x[i] >> bit) & 1);
+    });
+    return 0;
+  });
+}
+
+int mx_ring_inject(int dev, int words, const uint8_t* bits, void* out, int64_t n, int bit,
+                   void* stream) {
+  if (dev) return mxh_ring_inject(words, bits, out, n, bit, stream);
+  DISPATCH_WORDS(words, T, {
+    T* o = (T*)out;
+    parallel_for(n, 1 << 16, [&](int64_t s, int64_t e) {
+      for (int64_t i = s; i < e; ++i) o[i] = ((T)(bits[i] & 1)) << bit;
+    });
+    return 0;
+  });
+}
+
+int mx_encode(int dev, int words, const double* x, void* out, int64_t n, int frac,
+              void* stream) {
+  if (dev) return mxh_encode(words, x, out, n, frac, stream);
+  if (words == 1) {
+    u64* o = (u64*)out;
+    parallel_for(n, 1 << 16, [&](int64_t s, int64_t e) {
+      for (int64_t i = s; i < e; ++i) o[i] = (u64)mxr::f64_to_i128(x[i] * std::ldexp(1.0, frac));
+    });
+    return 0;
+  }
+  if (words == 2) {
+    u128* o = (u128*)out;
+    parallel_for(n, 1 << 16, [&](int64_t s, int64_t e) {
+      for (int64_t i = s; i < e; ++i) o[i] = (u128)mxr::f64_to_i128(x[i] * std::ldexp(1.0, frac));
+    });
+    return 0;
+  }
+  return -2;
+}
+
+int mx_decode(int dev, int words, const void* x, double* out, int64_t n, int frac,
+              void* stream) {
+  if (dev) return mxh_decode(words, x, out, n, frac, stream);
+  double scale = std::ldexp(1.0, -frac);
+  if (words == 1) {
+    const u64* a = (const u64*)x;
+    parallel_for(n, 1 << 16, [&](int64_t s, int64_t e) {
+      for (int64_t i = s; i < e; ++i) out[i] = (double)(int64_t)a[i] * scale;
+    });
+    return 0;
+  }
+  if (words == 2) {
+    const u128* a = (const u128*)x;
+    parallel_for(n, 1 << 16, [&](int64_t s, int64_t e) {
+      for (int64_t i = s; i < e; ++i) out[i] = mxr::i128_to_f64(a[i]) * scale;
+    });
+    return 0;
+  }
+  return -2;
+}
+
+int mx_sum_axis(int dev, int words, const void* a, void* out, int64_t outer, int64_t red,
+                int64_t inner, void* stream) {
+  if (dev) return mxh_sum_axis(words, a, out, outer, red, inner, stream);
+  DISPATCH_WORDS(words, T, return sum_axis_t<T>((const T*)a, (T*)out, outer, red, inner));
+}
+
+int mx_prg(int dev, const uint8_t* key16, uint64_t nonce, uint64_t ctr0, void* out,
+           int64_t nbytes, void* stream) {
+  if (dev) return mxh_prg(key16, nonce, ctr0, out, nbytes, stream);
+  Prf p(key16);
+  parallel_for((nbytes + 15) / 16, 1 << 12, [&](int64_t s, int64_t e) {
+    int64_t b0 = s * 16, b1 = std::min(nbytes, e * 16);
+    keystream_range(p, nonce, (int64_t)ctr0 * 16 + b0, b1 - b0, (uint8_t*)out + b0);
+  });
+  return 0;
+}
+
+int mx_aes_encrypt_blocks(const uint8_t* key16, const uint8_t* in, uint8_t* out,
+                          int64_t nblocks) {
+  uint32_t rk[44];
+  mx::expand_key(key16, rk);
+  for (int64_t b = 0; b < nblocks; ++b) {
+    const uint8_t* p = in + 16 * b;
+    uint32_t w[4], o[4];
+    for (int i = 0; i < 4; ++i)
+      w[i] = ((uint32_t)p[4 * i] << 24) | ((uint32_t)p[4 * i + 1] << 16) |
+             ((uint32_t)p[4 * i + 2] << 8) | p[4 * i + 3];
+    mx::encrypt_block_tt(rk, g_T0, mx::kSbox, w[0], w[1], w[2], w[3], o);
+    for (int i = 0; i < 4; ++i) {
+      out[16 * b + 4 * i] = o[i] >> 24;
+      out[16 * b + 4 * i + 1] = o[i] >> 16;
+      out[16 * b + 4 * i + 2] = o[i] >> 8;
+      out[16 * b + 4 * i + 3] = o[i];
+    }
+  }
+  return 0;
+}
+
+int mx_rss_cross(int dev, int kind, int words, const void* x0, const void* x1,
+                 const void* y0, const void* y1, void* out, int64_t n, int nparties,
+                 const uint8_t* keys16, uint64_t nonce, void* stream) {
+  if (dev)
+    return mxh_rss_cross(kind, words, x0, x1, y0, y1, out, n, nparties, keys16, nonce, stream);
+  DISPATCH_WORDS(words, T,
+                 return rss_cross_t<T>(kind, (const T*)x0, (const T*)x1, (const T*)y0,
+                                       (const T*)y1, (T*)out, n, nparties, keys16, nonce));
+}
+
+int mx_zero_share(int dev, int kind, int words, void* out, int64_t n, int nparties,
+                  const uint8_t* keys16, uint64_t nonce, void* stream) {
+  return mx_rss_cross(dev, kind, words, nullptr, nullptr, nullptr, nullptr, out, n, nparties,
+                      keys16, nonce, stream);
+}
+
+int mx_prf_expand(int dev, int words, void* out, int64_t n, int nkeys, const uint8_t* keys16,
+                  uint64_t nonce, void* stream) {
+  if (dev) return mxh_prf_expand(words, out, n, nkeys, keys16, nonce, stream);
+  DISPATCH_WORDS(words, T, return prf_expand_t<T>((T*)out, n, nkeys, keys16, nonce));
+}
+
+int mx_gemm(int dev, int words, int64_t batch, int64_t M, int64_t N, int64_t K,
+            const void* A0, const void* A1, const void* B0, const void* B1, int mode, void* C,
+            int accumulate, void* stream) {
+  if (dev) return mxh_gemm(words, batch, M, N, K, A0, A1, B0, B1, mode, C, accumulate, stream);
+  if (words == 1)
+    return gemm_t<u64>(batch, M, N, K, (const u64*)A0, (const u64*)A1, (const u64*)B0,
+                       (const u64*)B1, mode, (u64*)C, accumulate);
+  if (words == 2)
+    return gemm_t<u128>(batch, M, N, K, (const u128*)A0, (const u128*)A1, (const u128*)B0,
+                        (const u128*)B1, mode, (u128*)C, accumulate);
+  return -2;
+}
+
+}  // extern "C"

@@ -1,0 +1,509 @@
+// gfx950 kernels for the moosex ring dialect: elementwise Z_2^64 / Z_2^128 / Z_2 ops,
+// the AES-128-CTR correlated-randomness generator, the fused RSS local step
+// (cross terms + zero share in one pass), fixed-point encode/decode, reductions.
+//
+// Design notes (MI355X):
+//  * every elementwise kernel is a grid-stride loop over 16-byte elements (one u128, two
+//    u64) so each lane issues dwordx4 loads; the grid is capped at 256 CUs x 8 blocks.
+//  * AES uses a T0 table + S-box staged in LDS by each block (1.25 KB), rotations give
+//    T1..T3; one AES block yields one u128 / two u64 / sixteen bits.
+//  * the fused RSS kernel (mxh_rss_cross) reads the four share streams once and writes
+//    z_i + alpha_i once: the whole local half of an RSS multiplication is one launch, for
+//    all three parties at once when they are stacked on one device.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "aes_core.h"
+#include "moosex.h"
+#include "ring_common.h"
+
+using mxr::u128;
+using u64 = uint64_t;
+
+namespace {
+
+__constant__ uint8_t c_sbox[256] = MX_SBOX_INIT;
+
+constexpr int kBlock = 256;
+
+inline int grid_for(int64_t n, int per_thread = 1) {
+  int64_t blocks = (n + (int64_t)kBlock * per_thread - 1) / ((int64_t)kBlock * per_thread);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(blocks, 256 * 8));
+}
+
+inline hipStream_t S(void* s) { return (hipStream_t)s; }
+
+#define MX_LAUNCH_CHECK()                               \
+  do {                                                  \
+    hipError_t _e = hipGetLastError();                  \
+    if (_e != hipSuccess) return -100 - (int)_e;        \
+  } while (0)
+
+template <class T>
+__global__ void k_binary(int op, const T* __restrict__ a, int64_t na, const T* __restrict__ b,
+                         int64_t nb, T* __restrict__ out, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    out[i] = mxr::binop<T>(op, a[na == 1 ? 0 : i], b[nb == 1 ? 0 : i]);
+  }
+}
+
+template <class T>
+__global__ void k_unary(int op, const T* __restrict__ a, T* __restrict__ out, int64_t n, int k) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = mxr::unop<T>(op, a[i], k);
+}
+
+template <class T>
+__global__ void k_compare(int op, const T* __restrict__ a, int64_t na, const T* __restrict__ b,
+                          int64_t nb, uint8_t* __restrict__ out, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = mxr::cmpop<T>(op, a[na == 1 ? 0 : i], b ? b[nb == 1 ? 0 : i] : (T)0);
+}
+
+template <class T>
+__global__ void k_bit_extract(const T* __restrict__ a, uint8_t* __restrict__ out, int64_t n,
+                              int bit) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (uint8_t)((a[i] >> bit) & 1);
+}
+
+template <class T>
+__global__ void k_ring_inject(const uint8_t* __restrict__ bits, T* __restrict__ out, int64_t n,
+                              int bit) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = ((T)(bits[i] & 1)) << bit;
+}
+
+template <class T>
+__global__ void k_encode(const double* __restrict__ x, T* __restrict__ out, int64_t n,
+                         double scale) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (T)mxr::f64_to_i128(x[i] * scale);
+}
+
+template <class T>
+__global__ void k_decode(const T* __restrict__ x, double* __restrict__ out, int64_t n,
+                         double scale) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if constexpr (sizeof(T) == 8)
+      out[i] = (double)(int64_t)x[i] * scale;
+    else
+      out[i] = mxr::i128_to_f64(x[i]) * scale;
+  }
+}
+
+// one thread per output when the reduced axis is short; a block per output otherwise
+template <class T>
+__global__ void k_sum_axis(const T* __restrict__ a, T* __restrict__ out, int64_t outer,
+                           int64_t red, int64_t inner) {
+  int64_t total = outer * inner;
+  for (int64_t oi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; oi < total;
+       oi += (int64_t)gridDim.x * blockDim.x) {
+    int64_t o = oi / inner, i = oi % inner;
+    const T* p = a + o * red * inner + i;
+    T acc = 0;
+    for (int64_t r = 0; r < red; ++r) acc += p[r * inner];
+    out[oi] = acc;
+  }
+}
+
+template <class T>
+__global__ void k_sum_axis_wide(const T* __restrict__ a, T* __restrict__ out, int64_t red,
+                                int64_t inner) {
+  __shared__ T part[kBlock];
+  int64_t oi = blockIdx.x;
+  int64_t o = oi / inner, i = oi % inner;
+  const T* p = a + o * red * inner + i;
+  T acc = 0;
+  for (int64_t r = threadIdx.x; r < red; r += blockDim.x) acc += p[r * inner];
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) part[threadIdx.x] += part[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[oi] = part[0];
+}
+
+// ---------------------------------------------------------------------------
+// AES
+// ---------------------------------------------------------------------------
+struct RK {
+  uint32_t rk[44];
+};
+struct Keys4 {
+  uint32_t rk[4][44];
+};
+
+__device__ inline void stage_tables(uint32_t* T, uint8_t* Sb) {
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    uint8_t s = c_sbox[i];
+    Sb[i] = s;
+    T[i] = mx::t0_entry(s);
+  }
+  __syncthreads();
+}
+
+__device__ inline void aes_ctr(const uint32_t* rk, const uint32_t* T, const uint8_t* Sb,
+                               uint64_t nonce, uint64_t ctr, uint64_t* lo, uint64_t* hi) {
+  uint32_t w[4], o[4];
+  mx::ctr_block_words(nonce, ctr, w);
+  mx::encrypt_block_tt(rk, T, Sb, w[0], w[1], w[2], w[3], o);
+  mx::block_to_u64(o, lo, hi);
+}
+
+__global__ void k_prg(RK key, uint64_t nonce, uint64_t ctr0, uint8_t* __restrict__ out,
+                      int64_t nbytes) {
+  __shared__ uint32_t T[256];
+  __shared__ uint8_t Sb[256];
+  stage_tables(T, Sb);
+  int64_t nblocks = (nbytes + 15) / 16;
+  for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < nblocks;
+       b += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t lo, hi;
+    aes_ctr(key.rk, T, Sb, nonce, ctr0 + b, &lo, &hi);
+    if ((b + 1) * 16 <= nbytes) {
+      uint64_t* o = (uint64_t*)(out + b * 16);
+      o[0] = lo;
+      o[1] = hi;
+    } else {
+      uint8_t tmp[16];
+      memcpy(tmp, &lo, 8);
+      memcpy(tmp + 8, &hi, 8);
+      for (int64_t j = 0; j < nbytes - b * 16; ++j) out[b * 16 + j] = tmp[j];
+    }
+  }
+}
+
+// Element e of type T lives in keystream block e / (16 / sizeof(T)); one thread per block.
+template <class T>
+struct Lane {
+  static constexpr int kPer = 16 / (int)sizeof(T);  // elements per AES block
+};
+
+template <class T>
+__device__ inline T pick(uint64_t lo, uint64_t hi, int j) {
+  if constexpr (sizeof(T) == 16) {
+    return ((T)hi << 64) | (T)lo;
+  } else if constexpr (sizeof(T) == 8) {
+    return j == 0 ? lo : hi;
+  } else {
+    uint64_t w = j < 8 ? lo : hi;
+    return (T)((w >> (8 * (j & 7))) & 1);
+  }
+}
+
+template <class T>
+__global__ void k_rss_cross(int kind, const T* __restrict__ x0, const T* __restrict__ x1,
+                            const T* __restrict__ y0, const T* __restrict__ y1,
+                            T* __restrict__ out, int64_t n, int nparties, int has_keys,
+                            Keys4 keys, uint64_t nonce) {
+  __shared__ uint32_t Tt[256];
+  __shared__ uint8_t Sb[256];
+  if (has_keys) stage_tables(Tt, Sb);
+  constexpr int P = Lane<T>::kPer;
+  const int64_t nb = (n + P - 1) / P;  // keystream blocks per party
+  const int64_t total = nb * nparties;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const int p = (int)(g / nb);
+    const int64_t b = g % nb;
+    uint64_t alo = 0, ahi = 0, blo = 0, bhi = 0;
+    if (has_keys) {
+      aes_ctr(keys.rk[p], Tt, Sb, nonce, (uint64_t)b, &alo, &ahi);
+      aes_ctr(keys.rk[p + 1], Tt, Sb, nonce, (uint64_t)b, &blo, &bhi);
+    }
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      int64_t e = b * P + j;
+      if (e >= n) break;
+      int64_t i = (int64_t)p * n + e;
+      T v = 0;
+      if (x0 != nullptr)
+        v = mxr::cross<T>(kind, x0[i], x1 ? x1[i] : (T)0, y0[i], y1 ? y1[i] : (T)0,
+                          x1 != nullptr, y1 != nullptr);
+      if (has_keys) v = mxr::zs_combine<T>(kind, v, pick<T>(alo, ahi, j), pick<T>(blo, bhi, j));
+      out[i] = v;
+    }
+  }
+}
+
+template <class T>
+__global__ void k_prf_expand(T* __restrict__ out, int64_t n, int nkeys, Keys4 keys,
+                             uint64_t nonce) {
+  __shared__ uint32_t Tt[256];
+  __shared__ uint8_t Sb[256];
+  stage_tables(Tt, Sb);
+  constexpr int P = Lane<T>::kPer;
+  const int64_t nb = (n + P - 1) / P;
+  const int64_t total = nb * nkeys;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const int p = (int)(g / nb);
+    const int64_t b = g % nb;
+    uint64_t lo, hi;
+    aes_ctr(keys.rk[p], Tt, Sb, nonce, (uint64_t)b, &lo, &hi);
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      int64_t e = b * P + j;
+      if (e < n) out[(int64_t)p * n + e] = pick<T>(lo, hi, j);
+    }
+  }
+}
+
+// Reference (VALU) ring GEMM: 16x16 output tile per block, K staged through LDS.
+template <class T, int TS>
+__global__ void k_gemm_valu(int64_t M, int64_t N, int64_t K, const T* __restrict__ A0,
+                            const T* __restrict__ A1, const T* __restrict__ B0,
+                            const T* __restrict__ B1, int mode, T* __restrict__ C,
+                            int accumulate) {
+  __shared__ T As[TS][TS + 1];
+  __shared__ T Bs[TS][TS + 1];
+  const int64_t b = blockIdx.z;
+  const int64_t row = blockIdx.y * TS + threadIdx.y;
+  const int64_t col = blockIdx.x * TS + threadIdx.x;
+  const T* a0 = A0 + b * M * K;
+  const T* b0 = B0 + b * K * N;
+  const T* a1 = mode ? A1 + b * M * K : nullptr;
+  const T* b1 = mode ? B1 + b * K * N : nullptr;
+  T acc = 0;
+  const int passes = mode ? 2 : 1;
+  for (int pass = 0; pass < passes; ++pass) {
+    for (int64_t k0 = 0; k0 < K; k0 += TS) {
+      int64_t ka = k0 + threadIdx.x, kb = k0 + threadIdx.y;
+      T av = 0, bv = 0;
+      if (row < M && ka < K) av = (pass == 0 ? a0 : a1)[row * K + ka];
+      if (col < N && kb < K) {
+        bv = b0[kb * N + col];
+        if (mode && pass == 0) bv += b1[kb * N + col];
+      }
+      As[threadIdx.y][threadIdx.x] = av;
+      Bs[threadIdx.y][threadIdx.x] = bv;
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < TS; ++k) acc += As[threadIdx.y][k] * Bs[k][threadIdx.x];
+      __syncthreads();
+    }
+  }
+  if (row < M && col < N) {
+    T* c = C + b * M * N + row * N + col;
+    *c = accumulate ? (T)(*c + acc) : acc;
+  }
+}
+
+template <class T>
+int launch_gemm_valu(int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
+                     const void* A1, const void* B0, const void* B1, int mode, void* C,
+                     int accumulate, hipStream_t st) {
+  constexpr int TS = 16;
+  dim3 grid((unsigned)((N + TS - 1) / TS), (unsigned)((M + TS - 1) / TS), (unsigned)batch);
+  dim3 block(TS, TS);
+  hipLaunchKernelGGL((k_gemm_valu<T, TS>), grid, block, 0, st, M, N, K, (const T*)A0,
+                     (const T*)A1, (const T*)B0, (const T*)B1, mode, (T*)C, accumulate);
+  MX_LAUNCH_CHECK();
+  return 0;
+}
+
+Keys4 load_keys(const uint8_t* keys16, int nkeys) {
+  Keys4 k;
+  memset(&k, 0, sizeof(k));
+  for (int i = 0; i < nkeys && i < 4; ++i) mx::expand_key(keys16 + 16 * i, k.rk[i]);
+  return k;
+}
+
+}  // namespace
+
+// from gemm_mfma.hip
+extern "C" int mxh_gemm_mfma(int words, int64_t batch, int64_t M, int64_t N, int64_t K,
+                             const void* A0, const void* A1, const void* B0, const void* B1,
+                             int mode, void* C, int accumulate, void* stream);
+
+static int g_gemm_impl = 0;
+
+#define DEV_DISPATCH(words, T, ...)            \
+  switch (words) {                             \
+    case 0: { using T = uint8_t; __VA_ARGS__; } \
+    case 1: { using T = u64; __VA_ARGS__; }     \
+    case 2: { using T = u128; __VA_ARGS__; }    \
+    default: return -2;                        \
+  }
+
+extern "C" {
+
+void mx_set_gemm_impl(int impl) { g_gemm_impl = impl; }
+
+int mx_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int mxh_ew_binary(int op, int words, const void* a, int64_t na, const void* b, int64_t nb,
+                  void* out, int64_t n, void* stream) {
+  if (n == 0) return 0;
+  DEV_DISPATCH(words, T, {
+    hipLaunchKernelGGL(k_binary<T>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream), op,
+                       (const T*)a, na, (const T*)b, nb, (T*)out, n);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mxh_ew_unary(int op, int words, const void* a, void* out, int64_t n, int64_t param,
+                 void* stream) {
+  if (n == 0) return 0;
+  DEV_DISPATCH(words, T, {
+    hipLaunchKernelGGL(k_unary<T>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream), op,
+                       (const T*)a, (T*)out, n, (int)param);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mxh_ew_compare(int op, int words, const void* a, int64_t na, const void* b, int64_t nb,
+                   uint8_t* out, int64_t n, void* stream) {
+  if (n == 0) return 0;
+  DEV_DISPATCH(words, T, {
+    hipLaunchKernelGGL(k_compare<T>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream), op,
+                       (const T*)a, na, (const T*)b, nb, out, n);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mxh_bit_extract(int words, const void* a, uint8_t* out, int64_t n, int bit, void* stream) {
+  if (n == 0) return 0;
+  DEV_DISPATCH(words, T, {
+    hipLaunchKernelGGL(k_bit_extract<T>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
+                       (const T*)a, out, n, bit);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mxh_ring_inject(int words, const uint8_t* bits, void* out, int64_t n, int bit,
+                    void* stream) {
+  if (n == 0) return 0;
+  DEV_DISPATCH(words, T, {
+    hipLaunchKernelGGL(k_ring_inject<T>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream), bits,
+                       (T*)out, n, bit);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mxh_encode(int words, const double* x, void* out, int64_t n, int frac, void* stream) {
+  if (n == 0) return 0;
+  double scale = ldexp(1.0, frac);
+  if (words == 1)
+    hipLaunchKernelGGL(k_encode<u64>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream), x,
+                       (u64*)out, n, scale);
+  else if (words == 2)
+    hipLaunchKernelGGL(k_encode<u128>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream), x,
+                       (u128*)out, n, scale);
+  else
+    return -2;
+  MX_LAUNCH_CHECK();
+  return 0;
+}
+
+int mxh_decode(int words, const void* x, double* out, int64_t n, int frac, void* stream) {
+  if (n == 0) return 0;
+  double scale = ldexp(1.0, -frac);
+  if (words == 1)
+    hipLaunchKernelGGL(k_decode<u64>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
+                       (const u64*)x, out, n, scale);
+  else if (words == 2)
+    hipLaunchKernelGGL(k_decode<u128>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
+                       (const u128*)x, out, n, scale);
+  else
+    return -2;
+  MX_LAUNCH_CHECK();
+  return 0;
+}
+
+int mxh_sum_axis(int words, const void* a, void* out, int64_t outer, int64_t red, int64_t inner,
+                 void* stream) {
+  int64_t total = outer * inner;
+  if (total == 0) return 0;
+  DEV_DISPATCH(words, T, {
+    if (red >= 1024 && total <= 65536) {
+      hipLaunchKernelGGL(k_sum_axis_wide<T>, dim3((unsigned)total), dim3(kBlock), 0, S(stream),
+                         (const T*)a, (T*)out, red, inner);
+    } else {
+      hipLaunchKernelGGL(k_sum_axis<T>, dim3(grid_for(total)), dim3(kBlock), 0, S(stream),
+                         (const T*)a, (T*)out, outer, red, inner);
+    }
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mxh_prg(const uint8_t* key16, uint64_t nonce, uint64_t ctr0, void* out, int64_t nbytes,
+            void* stream) {
+  if (nbytes == 0) return 0;
+  RK k;
+  mx::expand_key(key16, k.rk);
+  hipLaunchKernelGGL(k_prg, dim3(grid_for((nbytes + 15) / 16)), dim3(kBlock), 0, S(stream), k,
+                     nonce, ctr0, (uint8_t*)out, nbytes);
+  MX_LAUNCH_CHECK();
+  return 0;
+}
+
+int mxh_rss_cross(int kind, int words, const void* x0, const void* x1, const void* y0,
+                  const void* y1, void* out, int64_t n, int nparties, const uint8_t* keys16,
+                  uint64_t nonce, void* stream) {
+  if (n == 0) return 0;
+  if (nparties < 1 || nparties > 3) return -3;
+  Keys4 k = keys16 ? load_keys(keys16, nparties + 1) : Keys4{};
+  DEV_DISPATCH(words, T, {
+    constexpr int P = 16 / (int)sizeof(T);
+    int64_t work = ((n + P - 1) / P) * nparties;
+    hipLaunchKernelGGL(k_rss_cross<T>, dim3(grid_for(work)), dim3(kBlock), 0, S(stream), kind,
+                       (const T*)x0, (const T*)x1, (const T*)y0, (const T*)y1, (T*)out, n,
+                       nparties, keys16 != nullptr, k, nonce);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mxh_prf_expand(int words, void* out, int64_t n, int nkeys, const uint8_t* keys16,
+                   uint64_t nonce, void* stream) {
+  if (n == 0) return 0;
+  if (nkeys < 1 || nkeys > 4) return -3;
+  Keys4 k = load_keys(keys16, nkeys);
+  DEV_DISPATCH(words, T, {
+    constexpr int P = 16 / (int)sizeof(T);
+    int64_t work = ((n + P - 1) / P) * nkeys;
+    hipLaunchKernelGGL(k_prf_expand<T>, dim3(grid_for(work)), dim3(kBlock), 0, S(stream),
+                       (T*)out, n, nkeys, k, nonce);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mxh_gemm(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
+             const void* A1, const void* B0, const void* B1, int mode, void* C, int accumulate,
+             void* stream) {
+  if (M == 0 || N == 0 || batch == 0) return 0;
+  bool big = M >= 64 && N >= 64 && K >= 32;
+  if ((g_gemm_impl == 2 || (g_gemm_impl == 0 && big)) && (words == 1 || words == 2))
+    return mxh_gemm_mfma(words, batch, M, N, K, A0, A1, B0, B1, mode, C, accumulate, stream);
+  if (words == 1)
+    return launch_gemm_valu<u64>(batch, M, N, K, A0, A1, B0, B1, mode, C, accumulate,
+                                 S(stream));
+  if (words == 2)
+    return launch_gemm_valu<u128>(batch, M, N, K, A0, A1, B0, B1, mode, C, accumulate,
+                                  S(stream));
+  return -2;
+}
+
+}  // extern "C"

@@ -1,0 +1,109 @@
+"""ctypes binding of the native core ``libmoosex.so`` (built in-tree on first use).
+
+On a GPU box the device kernels are mandatory: if the library cannot be loaded we raise
+instead of silently falling back to a slower path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+from moose_amd._native import build as _build
+
+_LIB = None
+_LOCK = threading.Lock()
+
+c_i64 = ctypes.c_int64
+c_int = ctypes.c_int
+c_u64 = ctypes.c_uint64
+c_vp = ctypes.c_void_p
+
+_SIGS = {
+    "mx_version": (c_int, []),
+    "mx_device_count": (c_int, []),
+    "mx_ew_binary": (c_int, [c_int, c_int, c_int, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "mx_ew_unary": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_i64, c_i64, c_vp]),
+    "mx_ew_compare": (c_int, [c_int, c_int, c_int, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "mx_bit_extract": (c_int, [c_int, c_int, c_vp, c_vp, c_i64, c_int, c_vp]),
+    "mx_ring_inject": (c_int, [c_int, c_int, c_vp, c_vp, c_i64, c_int, c_vp]),
+    "mx_encode": (c_int, [c_int, c_int, c_vp, c_vp, c_i64, c_int, c_vp]),
+    "mx_decode": (c_int, [c_int, c_int, c_vp, c_vp, c_i64, c_int, c_vp]),
+    "mx_sum_axis": (c_int, [c_int, c_int, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
+    "mx_prg": (c_int, [c_int, c_vp, c_u64, c_u64, c_vp, c_i64, c_vp]),
+    "mx_aes_encrypt_blocks": (c_int, [c_vp, c_vp, c_vp, c_i64]),
+    "mx_rss_cross": (
+        c_int,
+        [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_u64, c_vp],
+    ),
+    "mx_zero_share": (c_int, [c_int, c_int, c_int, c_vp, c_i64, c_int, c_vp, c_u64, c_vp]),
+    "mx_prf_expand": (c_int, [c_int, c_int, c_vp, c_i64, c_int, c_vp, c_u64, c_vp]),
+    "mx_gemm": (
+        c_int,
+        [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp],
+    ),
+    "mx_gemm_workspace_bytes": (c_i64, [c_int, c_i64, c_i64, c_i64, c_i64, c_int]),
+    "mx_gemm_ws": (
+        c_int,
+        [c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp,
+         c_i64, c_vp],
+    ),
+    "mx_set_gemm_impl": (None, [c_int]),
+}
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib():
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    with _LOCK:
+        if _LIB is not None:
+            return _LIB
+        if _build.needs_build() and os.environ.get("MOOSEX_NO_BUILD") != "1":
+            _build.build()
+        path = str(_build.LIB)
+        try:
+            handle = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        except OSError as e:
+            raise NativeError(f"cannot load {path}: {e}") from e
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = handle
+        return _LIB
+
+
+def loaded_path():
+    return str(_build.LIB)
+
+
+def check(rc, what):
+    if rc != 0:
+        raise NativeError(f"{what} failed with code {rc}")
+
+
+def dev_of(t: torch.Tensor) -> int:
+    return 1 if t.is_cuda else 0
+
+
+def stream_of(t: torch.Tensor):
+    if t.is_cuda:
+        return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+    return None
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def key_buffer(keys) -> ctypes.Array:
+    """Pack a list of 16-byte keys into a C buffer."""
+    raw = b"".join(bytes(k) for k in keys)
+    return ctypes.create_string_buffer(raw, len(raw))

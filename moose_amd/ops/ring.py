@@ -1,0 +1,707 @@
+"""Ring tensors: Z_2^64, Z_2^128 and Z_2 (bits) on CPU or MI355X.
+
+``RT`` wraps a torch tensor:
+
+* Z_2^64  -> ``torch.int64`` of the logical shape (two's complement = u64 bits),
+* Z_2^128 -> ``torch.int64`` of shape ``(*shape, 2)`` holding (lo, hi) words, i.e. the
+  in-memory layout of ``unsigned __int128``; the native kernels read it as such,
+* Z_2     -> ``torch.uint8`` holding 0/1.
+
+Elementwise Z_2^64 / Z_2 arithmetic uses torch's wrapping integer kernels; everything
+that torch cannot express (Z_2^128 arithmetic, exact ring GEMM, AES-CTR PRG, the fused RSS
+step) goes to ``libmoosex`` (``csrc/``), on the tensor's device and current HIP stream.
+
+Axis arguments are *logical*: ``nb`` leading batch dimensions (e.g. the party axis of a
+stacked 3-party session) are skipped.
+
+Parity: reference host ring kernels ``moose/src/host/ops.rs:1709-2036``.
+"""
+from __future__ import annotations
+
+import math
+from typing import List
+from typing import Sequence
+
+import numpy as np
+import torch
+
+from moose_amd.ops import native as nat
+
+MASK64 = (1 << 64) - 1
+MASK128 = (1 << 128) - 1
+
+_BIN = {"add": 0, "sub": 1, "mul": 2, "and": 3, "or": 4, "xor": 5}
+_UN = {"neg": 0, "not": 1, "shl": 2, "shr": 3, "sar": 4}
+_CMP = {"lt": 0, "gt": 1, "eq": 2, "msb": 3}
+
+
+def _words(bits):
+    return {1: 0, 64: 1, 128: 2}[bits]
+
+
+class RT:
+    """A ring tensor (see module docstring)."""
+
+    __slots__ = ("data", "bits")
+
+    def __init__(self, data: torch.Tensor, bits: int):
+        self.data = data
+        self.bits = bits
+
+    # -- shape -------------------------------------------------------------
+    @property
+    def shape(self):
+        s = tuple(self.data.shape)
+        return s[:-1] if self.bits == 128 else s
+
+    @property
+    def ndim(self):
+        return len(self.shape)
+
+    @property
+    def device(self):
+        return self.data.device
+
+    def numel(self):
+        return math.prod(self.shape)
+
+    def __repr__(self):
+        return f"RT(bits={self.bits}, shape={self.shape}, device={self.device})"
+
+    def contiguous(self):
+        return RT(self.data.contiguous(), self.bits)
+
+    def clone(self):
+        return RT(self.data.clone(), self.bits)
+
+    # -- arithmetic --------------------------------------------------------
+    def __add__(self, o):
+        return binary("add", self, o)
+
+    def __sub__(self, o):
+        return binary("sub", self, o)
+
+    def __mul__(self, o):
+        return binary("mul", self, o)
+
+    def __and__(self, o):
+        return binary("and", self, o)
+
+    def __or__(self, o):
+        return binary("or", self, o)
+
+    def __xor__(self, o):
+        return binary("xor", self, o)
+
+    def __neg__(self):
+        return unary("neg", self)
+
+    def __invert__(self):
+        return unary("not", self)
+
+    def shl(self, k):
+        return unary("shl", self, k)
+
+    def shr(self, k):
+        return unary("shr", self, k)
+
+    def sar(self, k):
+        return unary("sar", self, k)
+
+
+# ---------------------------------------------------------------------------
+# construction / conversion
+# ---------------------------------------------------------------------------
+def empty(shape, bits, device) -> RT:
+    shape = tuple(shape)
+    if bits == 128:
+        return RT(torch.empty(shape + (2,), dtype=torch.int64, device=device), 128)
+    if bits == 64:
+        return RT(torch.empty(shape, dtype=torch.int64, device=device), 64)
+    return RT(torch.empty(shape, dtype=torch.uint8, device=device), 1)
+
+
+def zeros(shape, bits, device) -> RT:
+    r = empty(shape, bits, device)
+    r.data.zero_()
+    return r
+
+
+def fill(shape, value: int, bits, device) -> RT:
+    """Constant ring tensor (``value`` taken mod 2^bits)."""
+    shape = tuple(shape)
+    if bits == 1:
+        return RT(torch.full(shape, int(value) & 1, dtype=torch.uint8, device=device), 1)
+    if bits == 64:
+        v = _to_i64(int(value) & MASK64)
+        return RT(torch.full(shape, v, dtype=torch.int64, device=device), 64)
+    v = int(value) & MASK128
+    lo, hi = _to_i64(v & MASK64), _to_i64(v >> 64)
+    d = torch.empty(shape + (2,), dtype=torch.int64, device=device)
+    d[..., 0] = lo
+    d[..., 1] = hi
+    return RT(d, 128)
+
+
+def _to_i64(u):
+    u &= MASK64
+    return u - (1 << 64) if u >= (1 << 63) else u
+
+
+def from_ints(values, bits, device="cpu") -> RT:
+    """Build from python ints / nested lists (values reduced mod 2^bits)."""
+    arr = np.array(values, dtype=object)
+    shape = arr.shape
+    flat = [int(x) for x in arr.reshape(-1)]
+    if bits == 1:
+        t = torch.tensor([v & 1 for v in flat], dtype=torch.uint8).reshape(shape)
+        return RT(t.to(device), 1)
+    if bits == 64:
+        t = torch.tensor([_to_i64(v) for v in flat], dtype=torch.int64).reshape(shape)
+        return RT(t.to(device), 64)
+    pairs = [[_to_i64(v & MASK64), _to_i64((v >> 64) & MASK64)] for v in flat]
+    t = torch.tensor(pairs, dtype=torch.int64).reshape(shape + (2,))
+    return RT(t.to(device), 128)
+
+
+def to_ints(x: RT) -> np.ndarray:
+    """Unsigned python-int view (object ndarray) -- test/inspection helper."""
+    d = x.data.detach().cpu()
+    if x.bits == 1:
+        return d.numpy().astype(object)
+    if x.bits == 64:
+        return np.vectorize(lambda v: int(v) & MASK64, otypes=[object])(d.numpy())
+    a = d.numpy()
+    lo = np.vectorize(lambda v: int(v) & MASK64, otypes=[object])(a[..., 0])
+    hi = np.vectorize(lambda v: int(v) & MASK64, otypes=[object])(a[..., 1])
+    return lo + hi * (1 << 64)
+
+
+def to_signed_ints(x: RT) -> np.ndarray:
+    u = to_ints(x)
+    half = 1 << (x.bits - 1)
+    return np.vectorize(lambda v: v - (1 << x.bits) if v >= half else v, otypes=[object])(u)
+
+
+# ---------------------------------------------------------------------------
+# elementwise
+# ---------------------------------------------------------------------------
+def _as_rt(o, like: RT) -> RT:
+    if isinstance(o, RT):
+        return o
+    if isinstance(o, int):
+        return fill((), o, like.bits, like.device)
+    raise TypeError(f"cannot combine RT with {type(o)}")
+
+
+def _broadcast(a: RT, b: RT):
+    if a.shape == b.shape:
+        return a, b
+    shp = torch.broadcast_shapes(a.shape, b.shape)
+    return expand(a, shp), expand(b, shp)
+
+
+def expand(a: RT, shape) -> RT:
+    shape = tuple(shape)
+    if a.shape == shape:
+        return a
+    if a.bits == 128:
+        return RT(a.data.expand(shape + (2,)), 128)
+    return RT(a.data.expand(shape), a.bits)
+
+
+def binary(op: str, a, b) -> RT:
+    if not isinstance(a, RT):
+        a = _as_rt(a, b)
+    b = _as_rt(b, a)
+    if a.bits != b.bits:
+        raise TypeError(f"ring width mismatch {a.bits} vs {b.bits}")
+    bits = a.bits
+    if bits == 1:
+        x, y = a.data, b.data
+        if op in ("add", "sub", "xor"):
+            return RT(x ^ y, 1)
+        if op in ("mul", "and"):
+            return RT(x & y, 1)
+        if op == "or":
+            return RT(x | y, 1)
+    if bits == 64:
+        x, y = a.data, b.data
+        if op == "add":
+            return RT(x + y, 64)
+        if op == "sub":
+            return RT(x - y, 64)
+        if op == "mul":
+            return RT(x * y, 64)
+        if op == "and":
+            return RT(x & y, 64)
+        if op == "or":
+            return RT(x | y, 64)
+        if op == "xor":
+            return RT(x ^ y, 64)
+    # Z_2^128: native kernel; scalar operands broadcast natively
+    na, nb_ = a.numel(), b.numel()
+    if na != nb_ and na != 1 and nb_ != 1:
+        a, b = _broadcast(a, b)
+        na = nb_ = a.numel()
+    n = max(na, nb_)
+    out_shape = a.shape if na >= nb_ else b.shape
+    out = empty(out_shape, 128, a.device)
+    ad, bd = a.data.contiguous(), b.data.contiguous()
+    nat.check(
+        nat.lib().mx_ew_binary(
+            nat.dev_of(ad), _BIN[op], 2, nat.ptr(ad), na, nat.ptr(bd), nb_, nat.ptr(out.data), n,
+            nat.stream_of(ad),
+        ),
+        f"ring128 {op}",
+    )
+    return out
+
+
+def unary(op: str, a: RT, k: int = 0) -> RT:
+    bits = a.bits
+    if bits == 1:
+        if op == "neg":
+            return RT(a.data.clone(), 1)
+        if op == "not":
+            return RT(a.data ^ 1, 1)
+        return RT(a.data.clone() if k == 0 else torch.zeros_like(a.data), 1)
+    if bits == 64:
+        x = a.data
+        if op == "neg":
+            return RT(-x, 64)
+        if op == "not":
+            return RT(~x, 64)
+        if op == "shl":
+            return RT(torch.zeros_like(x) if k >= 64 else (x << k), 64)
+        if op == "shr":
+            if k == 0:
+                return RT(x.clone(), 64)
+            if k >= 64:
+                return RT(torch.zeros_like(x), 64)
+            return RT((x >> k) & ((1 << (64 - k)) - 1), 64)
+        if op == "sar":
+            return RT(x >> min(k, 63), 64)
+    out = empty(a.shape, 128, a.device)
+    ad = a.data.contiguous()
+    nat.check(
+        nat.lib().mx_ew_unary(
+            nat.dev_of(ad), _UN[op], 2, nat.ptr(ad), nat.ptr(out.data), a.numel(), int(k),
+            nat.stream_of(ad),
+        ),
+        f"ring128 {op}",
+    )
+    return out
+
+
+def compare(op: str, a: RT, b: RT = None) -> RT:
+    """Signed comparison -> bit tensor (op: lt, gt, eq, msb)."""
+    if a.bits == 64 and op != "msb":
+        x, y = a.data, b.data
+        r = {"lt": x < y, "gt": x > y, "eq": x == y}[op]
+        return RT(r.to(torch.uint8), 1)
+    if a.bits == 64:
+        return RT(((a.data >> 63) & 1).to(torch.uint8), 1)
+    if b is not None and a.shape != b.shape and b.numel() != 1 and a.numel() != 1:
+        a, b = _broadcast(a, b)
+    n = max(a.numel(), b.numel() if b is not None else 0)
+    shape = a.shape if b is None or a.numel() >= b.numel() else b.shape
+    out = torch.empty(shape, dtype=torch.uint8, device=a.device)
+    ad = a.data.contiguous()
+    bd = b.data.contiguous() if b is not None else None
+    nat.check(
+        nat.lib().mx_ew_compare(
+            nat.dev_of(ad), _CMP[op], _words(a.bits), nat.ptr(ad), a.numel(), nat.ptr(bd),
+            b.numel() if b is not None else 0, nat.ptr(out), n, nat.stream_of(ad),
+        ),
+        f"compare {op}",
+    )
+    return RT(out, 1)
+
+
+def bit_extract(a: RT, bit: int) -> RT:
+    if a.bits == 64:
+        return RT(((a.data >> bit) & 1).to(torch.uint8), 1)
+    w = a.data[..., bit // 64]
+    return RT(((w >> (bit % 64)) & 1).to(torch.uint8), 1)
+
+
+def ring_inject(bitsrt: RT, bit: int, ring_bits: int) -> RT:
+    """bit tensor -> ring tensor with the bit placed at position ``bit``."""
+    b = bitsrt.data.to(torch.int64) & 1
+    if ring_bits == 64:
+        return RT(b << bit if bit < 64 else torch.zeros_like(b), 64)
+    out = torch.zeros(tuple(b.shape) + (2,), dtype=torch.int64, device=b.device)
+    if bit < 64:
+        out[..., 0] = b << bit
+    else:
+        out[..., 1] = b << (bit - 64)
+    return RT(out, 128)
+
+
+def cast(a: RT, bits: int) -> RT:
+    """Ring width change: truncation 128->64, zero extension 64->128, bit->ring."""
+    if a.bits == bits:
+        return a
+    if a.bits == 128 and bits == 64:
+        return RT(a.data[..., 0].contiguous(), 64)
+    if a.bits == 64 and bits == 128:
+        out = torch.zeros(tuple(a.data.shape) + (2,), dtype=torch.int64, device=a.device)
+        out[..., 0] = a.data
+        return RT(out, 128)
+    if a.bits == 1:
+        return ring_inject(a, 0, bits)
+    if bits == 1:
+        return bit_extract(a, 0)
+    raise TypeError(f"cannot cast ring {a.bits} -> {bits}")
+
+
+def sign_extend(a: RT, from_bits: int, bits: int) -> RT:
+    """64 -> 128 with sign extension."""
+    assert a.bits == 64 and bits == 128
+    out = torch.empty(tuple(a.data.shape) + (2,), dtype=torch.int64, device=a.device)
+    out[..., 0] = a.data
+    out[..., 1] = a.data >> 63
+    return RT(out, 128)
+
+
+# ---------------------------------------------------------------------------
+# fixed-point encode / decode (reference host/fixedpoint.rs: truncating `as i128`)
+# ---------------------------------------------------------------------------
+def encode(x: torch.Tensor, frac: int, bits: int) -> RT:
+    x = x.to(torch.float64).contiguous()
+    out = empty(tuple(x.shape), bits, x.device)
+    nat.check(
+        nat.lib().mx_encode(
+            nat.dev_of(x), _words(bits), nat.ptr(x), nat.ptr(out.data), x.numel(), int(frac),
+            nat.stream_of(x),
+        ),
+        "encode",
+    )
+    return out
+
+
+def decode(a: RT, frac: int) -> torch.Tensor:
+    ad = a.data.contiguous()
+    out = torch.empty(a.shape, dtype=torch.float64, device=a.device)
+    nat.check(
+        nat.lib().mx_decode(
+            nat.dev_of(ad), _words(a.bits), nat.ptr(ad), nat.ptr(out), a.numel(), int(frac),
+            nat.stream_of(ad),
+        ),
+        "decode",
+    )
+    return out
+
+
+# ---------------------------------------------------------------------------
+# shape ops (logical axes after `nb` batch dims)
+# ---------------------------------------------------------------------------
+def _ax(a: RT, axis: int, nb: int) -> int:
+    nd = a.ndim - nb
+    if axis < 0:
+        axis += nd
+    if not 0 <= axis < max(nd, 1):
+        raise IndexError(f"axis {axis} out of range for logical rank {nd}")
+    return axis + nb
+
+
+def reshape(a: RT, shape, nb=0) -> RT:
+    shape = tuple(int(s) for s in shape)
+    full = a.shape[:nb] + shape
+    if a.bits == 128:
+        return RT(a.data.reshape(full + (2,)), 128)
+    return RT(a.data.reshape(full), a.bits)
+
+
+def transpose(a: RT, nb=0, perm=None) -> RT:
+    nd = a.ndim - nb
+    perm = list(range(nd))[::-1] if perm is None else list(perm)
+    full = list(range(nb)) + [p + nb for p in perm]
+    if a.bits == 128:
+        full.append(a.ndim)
+    return RT(a.data.permute(full).contiguous(), a.bits)
+
+
+def expand_dims(a: RT, axes, nb=0) -> RT:
+    d = a.data
+    nd = a.ndim - nb
+    for ax in sorted(int(x) for x in axes):
+        if ax < 0:
+            ax += nd + 1
+        d = d.unsqueeze(ax + nb)
+        nd += 1
+    return RT(d, a.bits)
+
+
+def squeeze(a: RT, axis=None, nb=0) -> RT:
+    if axis is None:
+        shape = a.shape[:nb] + tuple(s for s in a.shape[nb:] if s != 1)
+        return reshape(a, shape[nb:], nb)
+    ax = _ax(a, axis, nb)
+    return RT(a.data.squeeze(ax), a.bits)
+
+
+def concat(xs: Sequence[RT], axis=0, nb=0) -> RT:
+    ax = _ax(xs[0], axis, nb)
+    return RT(torch.cat([x.data for x in xs], dim=ax), xs[0].bits)
+
+
+def index_axis(a: RT, axis: int, index: int, nb=0) -> RT:
+    ax = _ax(a, axis, nb)
+    return RT(a.data.select(ax, index).contiguous(), a.bits)
+
+
+def slice_axis(a: RT, axis: int, start, end, step=None, nb=0) -> RT:
+    ax = _ax(a, axis, nb)
+    idx = [slice(None)] * a.data.dim()
+    idx[ax] = slice(start, end, step)
+    return RT(a.data[tuple(idx)].contiguous(), a.bits)
+
+
+def strided_slice(a: RT, slices, nb=0) -> RT:
+    idx = [slice(None)] * nb + list(slices)
+    d = a.data
+    # torch lacks negative steps: emulate with flip
+    for i, s in enumerate(idx):
+        if isinstance(s, slice) and s.step is not None and s.step < 0:
+            raise NotImplementedError("negative slice steps")
+    return RT(d[tuple(idx)].contiguous(), a.bits)
+
+
+def select_mask(a: RT, axis: int, mask: torch.Tensor, nb=0) -> RT:
+    ax = _ax(a, axis, nb)
+    keep = torch.nonzero(mask.reshape(-1).to(torch.bool)).reshape(-1).to(a.device)
+    return RT(a.data.index_select(ax, keep).contiguous(), a.bits)
+
+
+def diag(a: RT, nb=0) -> RT:
+    d = a.data
+    if a.bits == 128:
+        return RT(torch.diagonal(d, dim1=nb, dim2=nb + 1).movedim(-1, -2).contiguous(), 128)
+    return RT(torch.diagonal(d, dim1=nb, dim2=nb + 1).contiguous(), a.bits)
+
+
+def broadcast_to(a: RT, shape, nb=0) -> RT:
+    full = a.shape[:nb] + tuple(shape)
+    return expand(a, full).contiguous()
+
+
+def atleast_2d(a: RT, to_column_vector=False, nb=0) -> RT:
+    nd = a.ndim - nb
+    if nd >= 2:
+        return a
+    if nd == 0:
+        return reshape(a, (1, 1), nb)
+    n = a.shape[nb]
+    return reshape(a, (n, 1) if to_column_vector else (1, n), nb)
+
+
+# ---------------------------------------------------------------------------
+# reductions
+# ---------------------------------------------------------------------------
+def sum(a: RT, axis=None, nb=0) -> RT:  # noqa: A001 - mirrors the Moose op name
+    if axis is None:
+        # reduce all logical dims
+        flat = reshape(a, (a.numel() // max(1, math.prod(a.shape[:nb])),), nb)
+        return sum(flat, 0, nb)
+    ax = _ax(a, axis, nb)
+    if a.bits == 1:
+        return RT((a.data.to(torch.int64).sum(dim=ax) & 1).to(torch.uint8), 1)
+    if a.bits == 64:
+        return RT(a.data.sum(dim=ax), 64)
+    shape = a.shape
+    outer = math.prod(shape[:ax])
+    red = shape[ax]
+    inner = math.prod(shape[ax + 1 :])
+    out = empty(shape[:ax] + shape[ax + 1 :], 128, a.device)
+    ad = a.data.contiguous()
+    nat.check(
+        nat.lib().mx_sum_axis(
+            nat.dev_of(ad), 2, nat.ptr(ad), nat.ptr(out.data), outer, red, inner,
+            nat.stream_of(ad),
+        ),
+        "ring128 sum",
+    )
+    return out
+
+
+def add_n(xs: List[RT]) -> RT:
+    acc = xs[0]
+    for x in xs[1:]:
+        acc = acc + x
+    return acc
+
+
+# ---------------------------------------------------------------------------
+# GEMM
+# ---------------------------------------------------------------------------
+def _gemm_call(bits, batch, M, N, K, a0, a1, b0, b1, mode, out, accumulate=0):
+    lib = nat.lib()
+    limit = (16384 if bits == 64 else 8192) // (2 if mode else 1)
+    if out.is_cuda and K > limit:
+        # split K so every limb diagonal stays exact in the i32 accumulators
+        for k0 in range(0, K, limit):
+            k1 = min(K, k0 + limit)
+            A0c = _kslice_rows(a0, batch, M, K, k0, k1, bits)
+            A1c = _kslice_rows(a1, batch, M, K, k0, k1, bits) if a1 is not None else None
+            B0c = _kslice_cols(b0, batch, K, N, k0, k1, bits)
+            B1c = _kslice_cols(b1, batch, K, N, k0, k1, bits) if b1 is not None else None
+            _gemm_call(bits, batch, M, N, k1 - k0, A0c, A1c, B0c, B1c, mode, out,
+                       accumulate if k0 == 0 else 1)
+        return
+    nat.check(
+        lib.mx_gemm(
+            nat.dev_of(out), _words(bits), batch, M, N, K, nat.ptr(a0), nat.ptr(a1), nat.ptr(b0),
+            nat.ptr(b1), mode, nat.ptr(out), accumulate, nat.stream_of(out),
+        ),
+        "ring gemm",
+    )
+
+
+def _kslice_rows(t, batch, M, K, k0, k1, bits):
+    v = t.reshape(batch, M, K, -1) if bits == 128 else t.reshape(batch, M, K)
+    return v[:, :, k0:k1].contiguous()
+
+
+def _kslice_cols(t, batch, K, N, k0, k1, bits):
+    v = t.reshape(batch, K, N, -1) if bits == 128 else t.reshape(batch, K, N)
+    return v[:, k0:k1].contiguous()
+
+
+def _dot_shapes(xs, ys, nb):
+    """Normalise rank-1/2 operands to [batch, M, K] x [batch, K, N]."""
+    xl, yl = xs[nb:], ys[nb:]
+    bshape = xs[:nb]
+    if len(xl) == 1 and len(yl) == 1:
+        M, K, N = 1, xl[0], 1
+        out = ()
+    elif len(xl) == 1:
+        M, K, N = 1, xl[0], yl[1]
+        out = (N,)
+    elif len(yl) == 1:
+        M, K, N = xl[0], xl[1], 1
+        out = (M,)
+    else:
+        M, K, N = xl[0], xl[1], yl[1]
+        out = (M, N)
+    if K != (yl[0]):
+        raise ValueError(f"dot shape mismatch {xl} . {yl}")
+    return bshape, M, K, N, out
+
+
+def dot(x: RT, y: RT, nb=0) -> RT:
+    """Ring matrix product (np.dot semantics for logical ranks 1/2), batched over nb dims."""
+    bits = x.bits
+    bshape, M, K, N, oshape = _dot_shapes(x.shape, y.shape, nb)
+    batch = math.prod(bshape)
+    out = empty(bshape + (M, N), bits, x.device)
+    if bits == 1:
+        r = (x.data.reshape(batch, M, K).to(torch.int64) @ y.data.reshape(batch, K, N).to(torch.int64)) & 1
+        return RT(r.to(torch.uint8).reshape(bshape + oshape), 1)
+    a0 = x.data.contiguous()
+    b0 = y.data.contiguous()
+    _gemm_call(bits, batch, M, N, K, a0, None, b0, None, 0, out.data)
+    return reshape(out, oshape, nb) if oshape != (M, N) else out
+
+
+def dot_cross(x0: RT, x1: RT, y0: RT, y1: RT, nb=0) -> RT:
+    """RSS cross terms of a matrix product: x0.(y0+y1) + x1.y0 in one K-doubled GEMM."""
+    bits = x0.bits
+    bshape, M, K, N, oshape = _dot_shapes(x0.shape, y0.shape, nb)
+    batch = math.prod(bshape)
+    out = empty(bshape + (M, N), bits, x0.device)
+    _gemm_call(
+        bits, batch, M, N, K, x0.data.contiguous(), x1.data.contiguous(), y0.data.contiguous(),
+        y1.data.contiguous(), 1, out.data,
+    )
+    return reshape(out, oshape, nb) if oshape != (M, N) else out
+
+
+# ---------------------------------------------------------------------------
+# randomness (AES-128-CTR)
+# ---------------------------------------------------------------------------
+def prf_expand(keys: Sequence[bytes], nonce: int, shape, bits, device) -> RT:
+    """out[p] = PRF(keys[p], nonce) of the given logical shape; stacked over keys."""
+    shape = tuple(shape)
+    n = math.prod(shape)
+    out = empty((len(keys),) + shape, bits, device)
+    kb = nat.key_buffer(keys)
+    if len(keys) > 4:
+        raise ValueError("at most 4 keys per call")
+    nat.check(
+        nat.lib().mx_prf_expand(
+            nat.dev_of(out.data), _words(bits), nat.ptr(out.data), n, len(keys), kb,
+            nonce & MASK64, nat.stream_of(out.data),
+        ),
+        "prf_expand",
+    )
+    return out
+
+
+def prg_bytes(key: bytes, nonce: int, nbytes: int, device="cpu", ctr0=0) -> torch.Tensor:
+    out = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    kb = nat.key_buffer([key])
+    nat.check(
+        nat.lib().mx_prg(nat.dev_of(out), kb, nonce & MASK64, ctr0, nat.ptr(out), nbytes,
+                         nat.stream_of(out)),
+        "prg",
+    )
+    return out
+
+
+def aes_encrypt(key: bytes, block: bytes) -> bytes:
+    import ctypes
+
+    kb = nat.key_buffer([key])
+    inp = ctypes.create_string_buffer(bytes(block), 16)
+    out = ctypes.create_string_buffer(16)
+    nat.check(nat.lib().mx_aes_encrypt_blocks(kb, inp, out, 1), "aes")
+    return out.raw
+
+
+def rss_cross(kind: str, x0: RT, x1, y0: RT, y1, keys, nonce: int, nparties: int) -> RT:
+    """Fused RSS local step.  Stacked layout: x* are [nparties, *shape]; party p gets
+    x0*y0 + x0*y1 + x1*y0 + PRF(k_p) - PRF(k_{p+1}) (boolean: & / ^).  ``keys`` is a list
+    of nparties+1 keys (or None for no zero share)."""
+    bits = x0.bits
+    shp = x0.shape
+    if y0.shape != shp:
+        x0, y0 = _broadcast(x0, y0)
+        shp = x0.shape
+    parts = [x0, x1, y0, y1]
+    datas = []
+    for p in parts:
+        if p is None:
+            datas.append(None)
+        else:
+            if p.shape != shp:
+                p = expand(p, shp)
+            datas.append(p.data.contiguous())
+    n_total = math.prod(shp)
+    n = n_total // nparties
+    out = empty(shp, bits, x0.device)
+    kbuf = nat.key_buffer(keys) if keys is not None else None
+    nat.check(
+        nat.lib().mx_rss_cross(
+            nat.dev_of(out.data), 1 if kind == "bool" else 0, _words(bits),
+            nat.ptr(datas[0]), nat.ptr(datas[1]), nat.ptr(datas[2]), nat.ptr(datas[3]),
+            nat.ptr(out.data), n, nparties, kbuf, nonce & MASK64, nat.stream_of(out.data),
+        ),
+        "rss_cross",
+    )
+    return out
+
+
+def zero_share(kind: str, shape, bits, keys, nonce: int, nparties: int, device) -> RT:
+    shape = tuple(shape)
+    out = empty(shape, bits, device)
+    n = math.prod(shape) // nparties
+    nat.check(
+        nat.lib().mx_zero_share(
+            nat.dev_of(out.data), 1 if kind == "bool" else 0, _words(bits), nat.ptr(out.data), n,
+            nparties, nat.key_buffer(keys), nonce & MASK64, nat.stream_of(out.data),
+        ),
+        "zero_share",
+    )
+    return out

@@ -1,0 +1,130 @@
+"""Bit-exact checks of every gfx950 ring kernel against the host (CPU) kernels, which
+are in turn checked against python-int arithmetic in test_ring_cpu.py."""
+import random
+
+import pytest
+import torch
+
+from moose_amd.ops import native as nat
+from moose_amd.ops import ring as R
+
+pytestmark = pytest.mark.gpu
+
+M64, M128 = (1 << 64) - 1, (1 << 128) - 1
+
+
+def rand_rt(shape, bits, seed):
+    g = torch.Generator().manual_seed(seed)
+    if bits == 1:
+        return R.RT(torch.randint(0, 2, shape, generator=g, dtype=torch.uint8), 1)
+    lo = torch.randint(-(2**63), 2**63 - 1, shape + ((2,) if bits == 128 else ()),
+                       generator=g, dtype=torch.int64)
+    return R.RT(lo, bits)
+
+
+def gpu(x):
+    return R.RT(x.data.cuda(), x.bits)
+
+
+def same(a, b):
+    assert a.bits == b.bits
+    assert torch.equal(a.data.cpu(), b.data.cpu())
+
+
+def test_library_is_native_and_gpu_visible():
+    assert nat.lib().mx_device_count() >= 1
+    assert nat.loaded_path().endswith("libmoosex.so")
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+@pytest.mark.parametrize("op", ["add", "sub", "mul", "and", "or", "xor"])
+def test_binary(bits, op):
+    a, b = rand_rt((1000,), bits, 1), rand_rt((1000,), bits, 2)
+    same(R.binary(op, a, b), R.binary(op, gpu(a), gpu(b)))
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+def test_unary_and_compare(bits):
+    a, b = rand_rt((777,), bits, 3), rand_rt((777,), bits, 4)
+    for op in ("neg", "not"):
+        same(R.unary(op, a), R.unary(op, gpu(a)))
+    for k in (0, 1, 31, 63, bits - 1):
+        same(a.shl(k), gpu(a).shl(k))
+        same(a.shr(k), gpu(a).shr(k))
+    for op in ("lt", "gt", "eq"):
+        same(R.compare(op, a, b), R.compare(op, gpu(a), gpu(b)))
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+def test_encode_decode_sum(bits):
+    x = torch.randn(513, dtype=torch.float64) * 1000
+    same(R.encode(x, 23, bits), R.encode(x.cuda(), 23, bits))
+    e = R.encode(x, 23, bits)
+    assert torch.equal(R.decode(e, 23), R.decode(gpu(e), 23).cpu())
+    a = rand_rt((7, 300, 5), bits, 5)
+    for ax in (0, 1, 2):
+        same(R.sum(a, ax), R.sum(gpu(a), ax))
+    big = rand_rt((4096, 3), bits, 6)
+    same(R.sum(big, 0), R.sum(gpu(big), 0))
+
+
+def test_prg_matches_host():
+    key = bytes(range(16))
+    for n in (1, 15, 16, 17, 1000, 4099):
+        h = R.prg_bytes(key, 123, n, "cpu")
+        d = R.prg_bytes(key, 123, n, "cuda")
+        assert torch.equal(h, d.cpu())
+
+
+@pytest.mark.parametrize("bits", [1, 64, 128])
+@pytest.mark.parametrize("kind", ["arith", "bool"])
+def test_rss_cross_fused(bits, kind):
+    if bits == 1 and kind == "arith":
+        pytest.skip("bits use the boolean flavour")
+    keys = [bytes([i] * 16) for i in range(3)]
+    keys = keys + keys[:1]
+    xs = [rand_rt((3, 1001), bits, s) for s in range(4)]
+    h = R.rss_cross(kind, *xs, keys, 99, 3)
+    d = R.rss_cross(kind, *[gpu(x) for x in xs], keys, 99, 3)
+    same(h, d)
+    z1 = R.prf_expand(keys[:3], 5, (333,), bits, "cpu")
+    z2 = R.prf_expand(keys[:3], 5, (333,), bits, "cuda")
+    same(z1, z2)
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+@pytest.mark.parametrize("shape", [(3, 5, 4), (64, 64, 64), (70, 130, 96), (128, 256, 192)])
+def test_gemm_matches_host(bits, shape):
+    M, K, N = shape
+    a, b = rand_rt((2, M, K), bits, 10), rand_rt((2, K, N), bits, 11)
+    same(R.dot(a, b, nb=1), R.dot(gpu(a), gpu(b), nb=1))
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+def test_gemm_cross_matches_host(bits):
+    M, K, N = 96, 160, 128
+    xs = [rand_rt((3, M, K), bits, 20 + i) for i in range(2)]
+    ys = [rand_rt((3, K, N), bits, 30 + i) for i in range(2)]
+    h = R.dot_cross(xs[0], xs[1], ys[0], ys[1], nb=1)
+    d = R.dot_cross(gpu(xs[0]), gpu(xs[1]), gpu(ys[0]), gpu(ys[1]), nb=1)
+    same(h, d)
+
+
+def test_gemm_mfma_asymmetric_identity():
+    # A = I with an asymmetric B catches a transposed C write (guide §3)
+    n = 64
+    eye = R.from_ints([[1 if i == j else 0 for j in range(n)] for i in range(n)], 128, "cuda")
+    vals = [[random.Random(i * n + j).getrandbits(128) for j in range(n)] for i in range(n)]
+    b = R.from_ints(vals, 128, "cuda")
+    nat.lib().mx_set_gemm_impl(2)
+    try:
+        c = R.dot(eye, b)
+    finally:
+        nat.lib().mx_set_gemm_impl(0)
+    assert (R.to_ints(c) == R.to_ints(b)).all()
+
+
+def test_gemm_long_k_split():
+    bits = 128
+    a, b = rand_rt((1, 64, 9000), bits, 40), rand_rt((1, 9000, 64), bits, 41)
+    same(R.dot(a, b, nb=1), R.dot(gpu(a), gpu(b), nb=1))
