@@ -63,8 +63,8 @@ int mx_aes_encrypt_blocks(const uint8_t* key16, const uint8_t* in, uint8_t* out,
 // RSS local step for `nparties` stacked parties of n elements each:
 //   party p, element i: out = x0*y0 + x0*y1 + x1*y0 + PRF(key[p])_i - PRF(key[p+1])_i
 // (boolean flavour: & and ^).  keys has nparties+1 entries.  x1 or y1 may be null
-// (then those terms are dropped: used for local products with public values).  keys may be
-// null (no zero share).
+// (then those terms are dropped: used for local products with public values).  y0 == null
+// means out = x0 + zero share.  keys may be null (no zero share).
 int mx_rss_cross(int dev, int kind, int words, const void* x0, const void* x1,
                  const void* y0, const void* y1, void* out, int64_t n, int nparties,
                  const uint8_t* keys16, uint64_t nonce, void* stream);

@@ -216,6 +216,8 @@ int rss_cross_t(int kind, const T* x0, const T* x1, const T* y0, const T* y1, T*
           if (x0 && y0) {
             v = mxr::cross<T>(kind, x0[i], x1 ? x1[i] : (T)0, y0[i], y1 ? y1[i] : (T)0,
                               x1 != nullptr, y1 != nullptr);
+          } else if (x0) {
+            v = x0[i];  // add-zero-share mode
           } else {
             v = 0;
           }

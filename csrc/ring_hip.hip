@@ -227,9 +227,11 @@ __global__ void k_rss_cross(int kind, const T* __restrict__ x0, const T* __restr
       if (e >= n) break;
       int64_t i = (int64_t)p * n + e;
       T v = 0;
-      if (x0 != nullptr)
+      if (x0 != nullptr && y0 != nullptr)
         v = mxr::cross<T>(kind, x0[i], x1 ? x1[i] : (T)0, y0[i], y1 ? y1[i] : (T)0,
                           x1 != nullptr, y1 != nullptr);
+      else if (x0 != nullptr)
+        v = x0[i];  // add-zero-share mode
       if (has_keys) v = mxr::zs_combine<T>(kind, v, pick<T>(alo, ahi, j), pick<T>(blo, bhi, j));
       out[i] = v;
     }

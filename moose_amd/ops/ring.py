@@ -666,7 +666,7 @@ def rss_cross(kind: str, x0: RT, x1, y0: RT, y1, keys, nonce: int, nparties: int
     of nparties+1 keys (or None for no zero share)."""
     bits = x0.bits
     shp = x0.shape
-    if y0.shape != shp:
+    if y0 is not None and y0.shape != shp:
         x0, y0 = _broadcast(x0, y0)
         shp = x0.shape
     parts = [x0, x1, y0, y1]

@@ -1,0 +1,470 @@
+"""Three-party replicated secret sharing (RSS) over Z_2^64, Z_2^128 and Z_2.
+
+A secret x = x_0 + x_1 + x_2 (XOR for boolean sharings) is held as ``slots``: party p
+holds (x_p, x_{p+1}).  A :class:`RepTensor` keeps the two party vectors ``s0`` (x_p at
+party p) and ``s1`` (x_{p+1} at party p); ``s1`` is ``s0`` shifted by one party.
+
+Correlated randomness: party p holds PRF keys k_p and k_{p+1} (so slot s can be sampled
+by exactly the two parties holding slot s) and one key k_all common to all three.
+
+Parity with the reference (``moose/src/replicated``):
+
+=====================  =====================================  =========================
+protocol               reference                              rounds here
+=====================  =====================================  =========================
+share (owner member)   convert.rs:74-125                      1 msg (x_j -> P_{j+2})
+share (outsider)       convert.rs:126-156                     1 (x sent + seeds)
+reveal                 convert.rs:280-313                     1
+add/sub/neg/sum/shape  arith.rs:7-314, ops.rs                 0
+mul                    arith.rs:317-367                       1 (fused kernel + roll)
+dot                    arith.rs:436-492                       1 (one K-doubled GEMM)
+trunc_pr               fixedpoint.rs:80-103, additive/trunc   2 (dealer msgs overlap)
+bit_decompose          bits.rs:6-21, misc.rs:181-243          1 + 1 + log2(k)
+msb / less / greater   arith.rs:611-653, compare.rs           bit_decompose + 2
+b2a (ring_inject)      convert.rs:316-390                     2
+equal_zero / equal     compare.rs:24-89                       bit_decompose + log2(k)
+mux                    control_flow.rs:9-45                   1 (+2 for a bit selector)
+=====================  =====================================  =========================
+
+Boolean sharings of k-bit words keep the k bits packed in one ring word (a Z_2^64 /
+Z_2^128 element), so a Kogge-Stone level is ONE boolean multiplication of whole words
+instead of k bit tensors (reference bits.rs stacks a [k, ...] bit array).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+from moose_amd.ir.computation import ReplicatedPlacement
+from moose_amd.ops import ring as R
+from moose_amd.runtime.session import HV
+from moose_amd.runtime.session import PV
+from moose_amd.utils.telemetry import span
+
+
+@dataclass
+class RepTensor:
+    plc: ReplicatedPlacement
+    bits: int  # 1, 64 or 128
+    kind: str  # "arith" (additive) or "bool" (xor)
+    s0: PV
+    s1: PV
+
+    @property
+    def add_prim(self):
+        return "Add" if self.kind == "arith" else "Xor"
+
+
+def _owner_index(plc, host):
+    try:
+        return plc.owners.index(host)
+    except ValueError:
+        return None
+
+
+# ---------------------------------------------------------------------------
+# input / output
+# ---------------------------------------------------------------------------
+def share(sess, plc, x: HV, kind="arith") -> RepTensor:
+    """Secret-share a ring tensor held by one host."""
+    bits = x.v.bits if hasattr(x.v, "bits") else None
+    with span("rep.share"):
+        sess.setup(plc)
+        shape = sess.h("Shape", x.host, x)
+        j = _owner_index(plc, x.host)
+        if j is None:
+            return _share_outsider(sess, plc, x, kind, bits, shape)
+        sub = "Sub" if kind == "arith" else "Xor"
+        o = plc.owners
+        j1, j2 = (j + 1) % 3, (j + 2) % 3
+        n1, na = sess.nonce(), sess.nonce()
+        # slot_{j+1} = PRF(k_{j+1}) [P_j, P_{j+1}]; slot_{j+2} = PRF(k_all); slot_j = rest
+        r1_j = sess.h_prf(plc, o[j], j1, shape, bits, n1)
+        r1_j1 = sess.h_prf(plc, o[j1], j1, shape, bits, n1)
+        ra_j = sess.h_prf(plc, o[j], "all", shape, bits, na)
+        ra_j1 = sess.h_prf(plc, o[j1], "all", shape, bits, na)
+        ra_j2 = sess.h_prf(plc, o[j2], "all", shape, bits, na)
+        xj = sess.h(sub, o[j], sess.h(sub, o[j], x, r1_j), ra_j)
+        comp0 = {j: xj, j1: r1_j1, j2: ra_j2}
+        comp1 = {j: r1_j, j1: ra_j1, j2: sess.move(xj, o[j2])}
+        s0 = sess.gather(plc, [comp0[i] for i in range(3)])
+        s1 = sess.gather(plc, [comp1[i] for i in range(3)])
+        return RepTensor(plc, bits, kind, s0, s1)
+
+
+def _share_outsider(sess, plc, x, kind, bits, shape):
+    """Owner outside the placement: two fresh seeds go to the slot holders, the third
+    slot x - PRG(seed0) - PRG(seed1) is sent to its two holders."""
+    o = plc.owners
+    sub = "Sub" if kind == "arith" else "Xor"
+    seed0, seed1 = sess.h_fresh_seed(x.host), sess.h_fresh_seed(x.host)
+    r0 = sess.h("SampleSeeded", x.host, shape, seed0, bits=bits)
+    r1 = sess.h("SampleSeeded", x.host, shape, seed1, bits=bits)
+    x2 = sess.h(sub, x.host, sess.h(sub, x.host, x, r0), r1)
+
+    def expand(seed, host):
+        return sess.h("SampleSeeded", host, sess.move(shape, host), sess.move(seed, host),
+                      bits=bits)
+
+    # slot0 = PRG(seed0) at P0, P2 ; slot1 = PRG(seed1) at P0, P1 ; slot2 = x2 at P1, P2
+    s0 = sess.gather(plc, [expand(seed0, o[0]), expand(seed1, o[1]), sess.move(x2, o[2])])
+    s1 = sess.gather(plc, [expand(seed1, o[0]), sess.move(x2, o[1]), expand(seed0, o[2])])
+    return RepTensor(plc, bits, kind, s0, s1)
+
+
+def reveal(sess, x: RepTensor, host: str) -> HV:
+    """Open x to ``host`` (a party of x.plc or an outsider)."""
+    with span("rep.reveal"):
+        add = x.add_prim
+        j = _owner_index(x.plc, host)
+        if j is not None:
+            # P_j holds (x_j, x_{j+1}); x_{j+2} comes from P_{j+1} (its s1)
+            a = sess.h(add, host, sess.take(x.s0, j), sess.take(x.s1, j))
+            c = sess.move(sess.take(x.s1, (j + 1) % 3), host)
+            return sess.h(add, host, a, c)
+        a = sess.move(sess.take(x.s0, 0), host)
+        b = sess.move(sess.take(x.s1, 0), host)
+        c = sess.move(sess.take(x.s1, 1), host)
+        return sess.h(add, host, sess.h(add, host, a, b), c)
+
+
+def from_public(sess, plc, value, bits, kind="arith") -> RepTensor:
+    """Trivial sharing of a value every party knows: slots (v, 0, 0)."""
+    s0 = sess.p_public_slot(plc, value, 0, bits)
+    s1 = sess.p_public_slot(plc, value, 2, bits)
+    return RepTensor(plc, bits, kind, s0, s1)
+
+
+def from_slot_holders(sess, plc, slot: int, x_h0: HV, x_h1: HV, like: PV,
+                      kind="arith") -> RepTensor:
+    """Sharing of a value known to both holders of ``slot`` (party ``slot`` holds it as
+    s0 -> ``x_h0``; party ``slot-1`` as s1 -> ``x_h1``): that slot = x, the others 0.
+    No communication (e.g. x_2 of an arithmetic sharing in bit decomposition).  ``like``
+    is any party vector of the same shape (each party takes its zeros' shape from it)."""
+    bits = x_h0.v.bits if hasattr(x_h0.v, "bits") else None
+    o = plc.owners
+    h0, h1 = slot, (slot - 1) % 3
+    comps0, comps1 = [], []
+    for p in range(3):
+        zero = None
+        if p != h0 or p != h1:
+            shape = sess.h("Shape", o[p], sess.take(like, p))
+            zero = sess.h("Fill", o[p], shape, value=0, bits=bits)
+        comps0.append(x_h0 if p == h0 else zero)
+        comps1.append(x_h1 if p == h1 else zero)
+    return RepTensor(plc, bits, kind, sess.gather(plc, comps0), sess.gather(plc, comps1))
+
+
+# ---------------------------------------------------------------------------
+# local (communication-free) operations
+# ---------------------------------------------------------------------------
+def local(sess, x: RepTensor, prim, **attrs) -> RepTensor:
+    """Apply a linear / shape primitive share-wise."""
+    return RepTensor(x.plc, x.bits, x.kind, sess.p(prim, x.plc, x.s0, **attrs),
+                     sess.p(prim, x.plc, x.s1, **attrs))
+
+
+def add(sess, x: RepTensor, y: RepTensor) -> RepTensor:
+    a = x.add_prim
+    return RepTensor(x.plc, x.bits, x.kind, sess.p(a, x.plc, x.s0, y.s0),
+                     sess.p(a, x.plc, x.s1, y.s1))
+
+
+def sub(sess, x: RepTensor, y: RepTensor) -> RepTensor:
+    a = "Sub" if x.kind == "arith" else "Xor"
+    return RepTensor(x.plc, x.bits, x.kind, sess.p(a, x.plc, x.s0, y.s0),
+                     sess.p(a, x.plc, x.s1, y.s1))
+
+
+def neg(sess, x: RepTensor) -> RepTensor:
+    if x.kind == "bool":
+        return x
+    return local(sess, x, "Neg")
+
+
+def add_public(sess, x: RepTensor, c) -> RepTensor:
+    """x + c for a public c (added to slot 0 only)."""
+    a = x.add_prim
+    s0 = sess.p_apply_at(a, x.plc, x.s0, 0, c)
+    s1 = sess.p_apply_at(a, x.plc, x.s1, 2, c)
+    return RepTensor(x.plc, x.bits, x.kind, s0, s1)
+
+
+def sub_public(sess, x: RepTensor, c) -> RepTensor:
+    a = "Sub" if x.kind == "arith" else "Xor"
+    s0 = sess.p_apply_at(a, x.plc, x.s0, 0, c)
+    s1 = sess.p_apply_at(a, x.plc, x.s1, 2, c)
+    return RepTensor(x.plc, x.bits, x.kind, s0, s1)
+
+
+def public_sub(sess, c, x: RepTensor) -> RepTensor:
+    return add_public(sess, neg(sess, x), c) if x.kind == "arith" else add_public(sess, x, c)
+
+
+def mul_public(sess, x: RepTensor, c) -> RepTensor:
+    m = "Mul" if x.kind == "arith" else "And"
+    pc = sess.public(x.plc, c)
+    return RepTensor(x.plc, x.bits, x.kind, sess.p(m, x.plc, x.s0, pc),
+                     sess.p(m, x.plc, x.s1, pc))
+
+
+def dot_public(sess, x: RepTensor, c, public_left=False) -> RepTensor:
+    pc = sess.public(x.plc, c)
+    if public_left:
+        return RepTensor(x.plc, x.bits, x.kind, sess.p("Dot", x.plc, pc, x.s0),
+                         sess.p("Dot", x.plc, pc, x.s1))
+    return RepTensor(x.plc, x.bits, x.kind, sess.p("Dot", x.plc, x.s0, pc),
+                     sess.p("Dot", x.plc, x.s1, pc))
+
+
+def shl(sess, x: RepTensor, k: int) -> RepTensor:
+    return local(sess, x, "Shl", amount=k)
+
+
+def sum(sess, x: RepTensor, axis=None) -> RepTensor:  # noqa: A001
+    return local(sess, x, "Sum", axis=axis)
+
+
+# ---------------------------------------------------------------------------
+# multiplication
+# ---------------------------------------------------------------------------
+def _reshare(sess, plc, z: PV, bits, kind) -> RepTensor:
+    """z_p (already masked by a zero share) -> P_{p-1}: one communication round."""
+    return RepTensor(plc, bits, kind, z, sess.shift(z, 1))
+
+
+def mul(sess, x: RepTensor, y: RepTensor) -> RepTensor:
+    """Elementwise product (AND for boolean sharings): one fused kernel + one round."""
+    with span("rep.mul"):
+        kind = x.kind
+        z = sess.p_cross(kind, x.plc, x.s0, x.s1, y.s0, y.s1, zero_share=True)
+        return _reshare(sess, x.plc, z, x.bits, kind)
+
+
+def and_(sess, x: RepTensor, y: RepTensor) -> RepTensor:
+    assert x.kind == "bool"
+    return mul(sess, x, y)
+
+
+def xor(sess, x: RepTensor, y: RepTensor) -> RepTensor:
+    assert x.kind == "bool"
+    return add(sess, x, y)
+
+
+def dot(sess, x: RepTensor, y: RepTensor) -> RepTensor:
+    """Matrix product: z_p = x_p.(y_p + y_{p+1}) + x_{p+1}.y_p as ONE K-doubled MFMA
+    GEMM (all parties batched when stacked), + zero share, + reshare."""
+    with span("rep.dot"):
+        v = sess.p_dot_cross(x.plc, x.s0, x.s1, y.s0, y.s1)
+        z = sess.p_add_zero_share(x.plc, v, x.kind)
+        return _reshare(sess, x.plc, z, x.bits, x.kind)
+
+
+# ---------------------------------------------------------------------------
+# probabilistic truncation (dealer-assisted, P2 = dealer)
+# ---------------------------------------------------------------------------
+def trunc_pr(sess, x: RepTensor, m: int) -> RepTensor:
+    """y ~= x / 2^m (probabilistic rounding, error <= 1 ulp), for |x| < 2^(k-2).
+
+    Escudero et al. (as in reference additive/trunc.rs:114-170) with dealer P2 and all
+    masks derived from PRF keys instead of shipped tensors where possible:
+      * r = r0 + r1 with r0 = PRF(k_0) [P0,P2] and r1 = PRF(k_2) [P1,P2]: no message;
+      * shares of r_top, r_msb for P1 are the only dealer messages (input independent);
+      * round 1: P0 and P1 exchange their masked shares -> both know c = x + r + 2^(k-2);
+      * round 2: additive -> replicated exchange (w_0, w_1).
+    """
+    if m == 0:
+        return x
+    with span("rep.trunc_pr"):
+        plc, bits = x.plc, x.bits
+        p0, p1, p2 = plc.owners
+        k = bits - 1
+        sh = [sess.h("Shape", plc.owners[i], sess.take(x.s0, i)) for i in range(3)]
+        nr0, nr1, nt, nm = sess.nonce(), sess.nonce(), sess.nonce(), sess.nonce()
+        # dealer P2
+        r = sess.h("Add", p2, sess.h_prf(plc, p2, 0, sh[2], bits, nr0),
+                   sess.h_prf(plc, p2, 2, sh[2], bits, nr1))
+        r_msb = sess.h("Shr", p2, r, amount=bits - 1)
+        r_top = sess.h("Shr", p2, sess.h("Shl", p2, r, amount=1), amount=m + 1)
+        rt1 = sess.move(sess.h("Sub", p2, r_top, sess.h_prf(plc, p2, 0, sh[2], bits, nt)), p1)
+        rm1 = sess.move(sess.h("Sub", p2, r_msb, sess.h_prf(plc, p2, 0, sh[2], bits, nm)), p1)
+        # P0 re-derives its mask shares from k_0, P1 its r1 from k_2
+        r0 = sess.h_prf(plc, p0, 0, sh[0], bits, nr0)
+        rt0 = sess.h_prf(plc, p0, 0, sh[0], bits, nt)
+        rm0 = sess.h_prf(plc, p0, 0, sh[0], bits, nm)
+        r1 = sess.h_prf(plc, p1, 2, sh[1], bits, nr1)
+        # replicated -> additive: a0 = x0 + x1 at P0, a1 = x2 at P1
+        a0 = sess.h("Add", p0, sess.take(x.s0, 0), sess.take(x.s1, 0))
+        a1 = sess.take(x.s1, 1)
+        mk0 = sess.h("Add", p0, sess.h("AddConst", p0, a0, value=1 << (k - 1), bits=bits), r0)
+        mk1 = sess.h("Add", p1, a1, r1)
+        c_at0 = sess.h("Add", p0, mk0, sess.move(mk1, p0))
+        c_at1 = sess.h("Add", p1, mk1, sess.move(mk0, p1))
+        outs = []
+        for host, c, rt, rm, first in ((p0, c_at0, rt0, rm0, True), (p1, c_at1, rt1, rm1, False)):
+            c_msb = sess.h("Shr", host, c, amount=bits - 1)
+            # share of overflow = r_msb XOR c_msb = rm + [first] c_msb - 2 c_msb rm
+            ov = sess.h("Sub", host, rm,
+                        sess.h("Shl", host, sess.h("Mul", host, c_msb, rm), amount=1))
+            if first:
+                ov = sess.h("Add", host, ov, c_msb)
+            y = sess.h("Sub", host, sess.h("Shl", host, ov, amount=k - m), rt)
+            if first:
+                c_top = sess.h("Shr", host, sess.h("Shl", host, c, amount=1), amount=m + 1)
+                y = sess.h("Add", host, y, c_top)
+                y = sess.h("AddConst", host, y, value=-(1 << (k - 1 - m)), bits=bits)
+            outs.append(y)
+        return _adt_to_rep(sess, plc, outs[0], outs[1], sh, bits)
+
+
+def _adt_to_rep(sess, plc, y0: HV, y1: HV, sh, bits) -> RepTensor:
+    """2-party additive (P0: y0, P1: y1) -> RSS: z0 = PRF(k_0) [P0,P2], z2 = PRF(k_2)
+    [P1,P2], z1 = (y0 - z0) + (y1 - z2) exchanged between P0 and P1 (one round)."""
+    p0, p1, p2 = plc.owners
+    n0, n2 = sess.nonce(), sess.nonce()
+    z0_at0 = sess.h_prf(plc, p0, 0, sh[0], bits, n0)
+    z2_at1 = sess.h_prf(plc, p1, 2, sh[1], bits, n2)
+    z0_at2 = sess.h_prf(plc, p2, 0, sh[2], bits, n0)
+    z2_at2 = sess.h_prf(plc, p2, 2, sh[2], bits, n2)
+    w0 = sess.h("Sub", p0, y0, z0_at0)
+    w1 = sess.h("Sub", p1, y1, z2_at1)
+    z1_at0 = sess.h("Add", p0, w0, sess.move(w1, p0))
+    z1_at1 = sess.h("Add", p1, w1, sess.move(w0, p1))
+    s0 = sess.gather(plc, [z0_at0, z1_at1, z2_at2])
+    s1 = sess.gather(plc, [z1_at0, z2_at1, z0_at2])
+    return RepTensor(plc, bits, "arith", s0, s1)
+
+
+# ---------------------------------------------------------------------------
+# bit decomposition & comparisons (packed boolean words)
+# ---------------------------------------------------------------------------
+def bit_decompose(sess, x: RepTensor) -> RepTensor:
+    """Arithmetic sharing of x in Z_2^k -> boolean sharing of its k bits packed in one
+    word.  y = x_0 + x_1 is boolean-shared by P0, x_2 is a trivial boolean sharing
+    (slot 2), and a packed Kogge-Stone adder computes y + x_2 (log2 k AND rounds)."""
+    with span("rep.bit_decompose"):
+        plc, bits = x.plc, x.bits
+        o = plc.owners
+        y = sess.h("Add", o[0], sess.take(x.s0, 0), sess.take(x.s1, 0))
+        yb = share(sess, plc, y, kind="bool")
+        x2 = from_slot_holders(sess, plc, 2, sess.take(x.s0, 2), sess.take(x.s1, 1), x.s0,
+                               kind="bool")
+        return binary_adder(sess, yb, x2)
+
+
+def binary_adder(sess, a: RepTensor, b: RepTensor) -> RepTensor:
+    """Packed-word Kogge-Stone: bits of a + b for boolean sharings a, b."""
+    bits = a.bits
+    p = xor(sess, a, b)
+    g = and_(sess, a, b)
+    pk = p
+    d = 1
+    while d < bits:
+        # batch the two independent ANDs of this level in one round
+        gs = shl(sess, g, d)
+        ps = shl(sess, pk, d)
+        if 2 * d < bits:
+            both = _stack2(sess, pk, pk)
+            other = _stack2(sess, gs, ps)
+            prod = and_(sess, both, other)
+            t, pk_new = _unstack2(sess, prod)
+            pk = pk_new
+        else:
+            t = and_(sess, pk, gs)
+        g = xor(sess, g, t)
+        d *= 2
+    carry = shl(sess, g, 1)
+    return xor(sess, p, carry)
+
+
+def _stack2(sess, x: RepTensor, y: RepTensor) -> RepTensor:
+    return RepTensor(x.plc, x.bits, x.kind, sess.p_stack2(x.s0, y.s0), sess.p_stack2(x.s1, y.s1))
+
+
+def _unstack2(sess, x: RepTensor):
+    a0, b0 = sess.p_unstack2(x.s0)
+    a1, b1 = sess.p_unstack2(x.s1)
+    return (RepTensor(x.plc, x.bits, x.kind, a0, a1), RepTensor(x.plc, x.bits, x.kind, b0, b1))
+
+
+def bit_extract(sess, x: RepTensor, i: int) -> RepTensor:
+    """Bit i of a packed boolean sharing -> boolean bit sharing (Z_2)."""
+    assert x.kind == "bool"
+    return RepTensor(x.plc, 1, "bool", sess.p("BitExtract", x.plc, x.s0, bit_idx=i),
+                     sess.p("BitExtract", x.plc, x.s1, bit_idx=i))
+
+
+def b2a(sess, b: RepTensor, ring_bits: int) -> RepTensor:
+    """Boolean bit -> arithmetic bit in Z_2^ring_bits (2 rounds):
+    b = a XOR b2 with a = b0 ^ b1 known to P0 and b2 known to P1, P2;
+    [b] = [a] + [b2] - 2 [a][b2]."""
+    with span("rep.b2a"):
+        plc = b.plc
+        o = plc.owners
+        if b.bits != 1:
+            raise TypeError("b2a expects a bit sharing")
+        a_bit = sess.h("Xor", o[0], sess.take(b.s0, 0), sess.take(b.s1, 0))
+        a_ring = sess.h("RingInject", o[0], a_bit, bit_idx=0, bits=ring_bits)
+        A = share(sess, plc, a_ring, kind="arith")
+        b2_h0 = sess.h("RingInject", o[2], sess.take(b.s0, 2), bit_idx=0, bits=ring_bits)
+        b2_h1 = sess.h("RingInject", o[1], sess.take(b.s1, 1), bit_idx=0, bits=ring_bits)
+        B = from_slot_holders(sess, plc, 2, b2_h0, b2_h1, b.s0, kind="arith")
+        AB = mul(sess, A, B)
+        return sub(sess, add(sess, A, B), shl(sess, AB, 1))
+
+
+def msb(sess, x: RepTensor) -> RepTensor:
+    """Boolean sharing of the sign bit."""
+    bd = bit_decompose(sess, x)
+    return bit_extract(sess, bd, x.bits - 1)
+
+
+def less_than_zero_arith(sess, x: RepTensor) -> RepTensor:
+    return b2a(sess, msb(sess, x), x.bits)
+
+
+def less(sess, x: RepTensor, y: RepTensor) -> RepTensor:
+    """[x < y] as a boolean bit sharing (msb of x - y)."""
+    return msb(sess, sub(sess, x, y))
+
+
+def greater(sess, x: RepTensor, y: RepTensor) -> RepTensor:
+    return msb(sess, sub(sess, y, x))
+
+
+def equal_zero(sess, x: RepTensor) -> RepTensor:
+    """[x == 0] as a boolean bit: AND-tree over the complemented packed bits."""
+    bd = bit_decompose(sess, x)
+    z = add_public(sess, bd, R.fill((), (1 << x.bits) - 1, x.bits, sess.device))  # NOT
+    w = x.bits
+    while w > 1:
+        w //= 2
+        z = and_(sess, z, local(sess, z, "Shr", amount=w))
+    return bit_extract(sess, z, 0)
+
+
+def equal(sess, x: RepTensor, y: RepTensor) -> RepTensor:
+    return equal_zero(sess, sub(sess, x, y))
+
+
+def mux(sess, s: RepTensor, x: RepTensor, y: RepTensor) -> RepTensor:
+    """s ? x : y ; s is an arithmetic 0/1 sharing or a boolean bit sharing."""
+    if s.kind == "bool":
+        s = b2a(sess, s, x.bits)
+    return add(sess, mul(sess, s, sub(sess, x, y)), y)
+
+
+def abs_(sess, x: RepTensor) -> RepTensor:
+    s = less_than_zero_arith(sess, x)
+    # |x| = x - 2 s x
+    return sub(sess, x, shl(sess, mul(sess, s, x), 1))
+
+
+def relu(sess, x: RepTensor) -> RepTensor:
+    s = b2a(sess, msb(sess, x), x.bits)  # 1 if negative
+    return sub(sess, x, mul(sess, s, x))
+
+
+def ring_cast(sess, x: RepTensor, bits: int) -> RepTensor:
+    """Z_2^128 -> Z_2^64 (share-wise truncation; valid for values that fit)."""
+    return RepTensor(x.plc, bits, x.kind, sess.p("RingCast", x.plc, x.s0, bits=bits),
+                     sess.p("RingCast", x.plc, x.s1, bits=bits))

@@ -1,0 +1,433 @@
+"""Host-level primitive operations (the leaf kernels of a lowered graph).
+
+Each primitive has a name -- the operator kind it becomes in a lowered computation
+(``Add``, ``Dot``, ``SampleSeeded`` ... and this framework's fused extensions
+``RingMulCross``/``RingDotCross``/``BitAndCross``/``ZeroShare``) -- an eager
+implementation on python/torch values, and a result-type rule used by the symbolic
+session.  Eager values are:
+
+* :class:`moose_amd.ops.ring.RT` for ring / bit tensors,
+* ``torch.Tensor`` for plaintext host tensors (float, int, uint, bool),
+* ``tuple`` for shapes, ``bytes`` for PRF keys / seeds, ``str`` for strings.
+
+Implementations take ``nb`` -- the number of leading batch dims (1 when the three
+parties of a session are stacked on one device) -- so axis attributes stay logical.
+
+Parity: the ``runtime`` flavour rows of the reference dispatch tables
+(``moose/src/kernels/*.rs``) are the host kernels in ``moose/src/host/ops.rs``.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from moose_amd.ir import types as T
+from moose_amd.ops import ring as R
+
+
+class Prim:
+    __slots__ = ("name", "impl", "ty")
+
+    def __init__(self, name, impl, ty=None):
+        self.name = name
+        self.impl = impl
+        self.ty = ty or (lambda tys, **a: tys[0])
+
+
+PRIMS = {}
+
+
+def prim(name, ty=None):
+    def deco(fn):
+        PRIMS[name] = Prim(name, fn, ty)
+        return fn
+
+    return deco
+
+
+def _is_rt(x):
+    return isinstance(x, R.RT)
+
+
+def _tensorish(x):
+    return isinstance(x, (R.RT, torch.Tensor))
+
+
+# ---------------------------------------------------------------------------
+# arithmetic (ring or plaintext)
+# ---------------------------------------------------------------------------
+def _arith(op):
+    def impl(nb, a, b):
+        if _is_rt(a) or _is_rt(b):
+            return R.binary(op, a, b)
+        if op == "add":
+            return a + b
+        if op == "sub":
+            return a - b
+        if op == "mul":
+            return a * b
+        if op == "and":
+            return a & b
+        if op == "or":
+            return a | b
+        if op == "xor":
+            return a ^ b
+        raise AssertionError(op)
+
+    return impl
+
+
+prim("Add")(_arith("add"))
+prim("Sub")(_arith("sub"))
+prim("Mul")(_arith("mul"))
+prim("And")(_arith("and"))
+prim("Or")(_arith("or"))
+prim("Xor")(_arith("xor"))
+
+
+@prim("Neg")
+def _neg(nb, a):
+    if _is_rt(a):
+        return -a
+    if a.dtype == torch.bool:
+        return ~a
+    return -a
+
+
+@prim("Div")
+def _div(nb, a, b):
+    if a.dtype in (torch.float32, torch.float64):
+        return a / b
+    return torch.div(a, b, rounding_mode="trunc")
+
+
+@prim("Shl")
+def _shl(nb, a, amount):
+    return a.shl(amount)
+
+
+@prim("Shr")
+def _shr(nb, a, amount):
+    return a.shr(amount)
+
+
+@prim("Sar")
+def _sar(nb, a, amount):
+    return a.sar(amount)
+
+
+@prim("Dot")
+def _dot(nb, a, b):
+    if _is_rt(a):
+        return R.dot(a, b, nb)
+    if nb:
+        return torch.matmul(a, b)
+    if a.dim() <= 2 and b.dim() <= 2:
+        return a @ b if (a.dim() > 0 and b.dim() > 0) else a * b
+    return torch.tensordot(a, b, dims=([a.dim() - 1], [0]))
+
+
+@prim("Sum", ty=lambda tys, **a: tys[0])
+def _sum(nb, a, axis=None):
+    if _is_rt(a):
+        return R.sum(a, axis, nb)
+    if axis is None:
+        return a.reshape(a.shape[:nb] + (-1,)).sum(dim=nb) if nb else a.sum()
+    return a.sum(dim=_lax(a.dim(), axis, nb))
+
+
+def _lax(ndim, axis, nb):
+    nd = ndim - nb
+    return (axis + nd if axis < 0 else axis) + nb
+
+
+@prim("AddN")
+def _addn(nb, *xs):
+    acc = xs[0]
+    for x in xs[1:]:
+        acc = _arith("add")(nb, acc, x)
+    return acc
+
+
+@prim("Mean")
+def _mean(nb, a, axis=None):
+    if axis is None:
+        return a.mean() if not nb else a.reshape(a.shape[:nb] + (-1,)).mean(dim=nb)
+    return a.mean(dim=_lax(a.dim(), axis, nb))
+
+
+# ---------------------------------------------------------------------------
+# shapes
+# ---------------------------------------------------------------------------
+@prim("Shape", ty=lambda tys, **a: T.HOST_SHAPE)
+def _shape(nb, a):
+    if _is_rt(a):
+        return tuple(a.shape[nb:])
+    return tuple(a.shape[nb:])
+
+
+@prim("Reshape")
+def _reshape(nb, a, shape):
+    if _is_rt(a):
+        return R.reshape(a, shape, nb)
+    return a.reshape(tuple(a.shape[:nb]) + tuple(shape))
+
+
+@prim("ExpandDims")
+def _expand_dims(nb, a, axis):
+    if _is_rt(a):
+        return R.expand_dims(a, axis, nb)
+    d = a
+    nd = a.dim() - nb
+    for ax in sorted(axis):
+        if ax < 0:
+            ax += nd + 1
+        d = d.unsqueeze(ax + nb)
+        nd += 1
+    return d
+
+
+@prim("Squeeze")
+def _squeeze(nb, a, axis=None):
+    if _is_rt(a):
+        return R.squeeze(a, axis, nb)
+    if axis is None:
+        keep = list(a.shape[:nb]) + [s for s in a.shape[nb:] if s != 1]
+        return a.reshape(keep)
+    return a.squeeze(_lax(a.dim(), axis, nb))
+
+
+@prim("Transpose")
+def _transpose(nb, a):
+    if _is_rt(a):
+        return R.transpose(a, nb)
+    nd = a.dim() - nb
+    perm = list(range(nb)) + [nb + i for i in reversed(range(nd))]
+    return a.permute(perm).contiguous()
+
+
+@prim("Concat")
+def _concat(nb, *xs, axis=0):
+    if _is_rt(xs[0]):
+        return R.concat(xs, axis, nb)
+    return torch.cat(xs, dim=_lax(xs[0].dim(), axis, nb))
+
+
+@prim("IndexAxis")
+def _index_axis(nb, a, axis, index):
+    if _is_rt(a):
+        return R.index_axis(a, axis, index, nb)
+    return a.select(_lax(a.dim(), axis, nb), index).contiguous()
+
+
+@prim("Slice")
+def _slice(nb, a, slice):
+    start, end, step = slice
+    if _is_rt(a):
+        return R.slice_axis(a, 0, start, end, step, nb)
+    idx = [builtins_slice(None)] * nb + [builtins_slice(start, end, step)]
+    return a[tuple(idx)].contiguous()
+
+
+builtins_slice = slice
+
+
+@prim("StridedSlice")
+def _strided_slice(nb, a, slices):
+    if _is_rt(a):
+        return R.strided_slice(a, slices, nb)
+    idx = [builtins_slice(None)] * nb + list(slices)
+    return a[tuple(idx)].contiguous()
+
+
+@prim("Select")
+def _select(nb, a, mask, axis):
+    m = mask.data if _is_rt(mask) else mask
+    if _is_rt(a):
+        return R.select_mask(a, axis, m, nb)
+    keep = torch.nonzero(m.reshape(-1).to(torch.bool)).reshape(-1).to(a.device)
+    return a.index_select(_lax(a.dim(), axis, nb), keep).contiguous()
+
+
+@prim("Diag")
+def _diag(nb, a):
+    if _is_rt(a):
+        return R.diag(a, nb)
+    return torch.diagonal(a, dim1=nb, dim2=nb + 1).contiguous()
+
+
+@prim("Broadcast")
+def _broadcast(nb, a, shape):
+    if _is_rt(a):
+        return R.broadcast_to(a, shape, nb)
+    return a.expand(tuple(a.shape[:nb]) + tuple(shape)).contiguous()
+
+
+@prim("AtLeast2D")
+def _atleast_2d(nb, a, to_column_vector=False):
+    if _is_rt(a):
+        return R.atleast_2d(a, to_column_vector, nb)
+    nd = a.dim() - nb
+    if nd >= 2:
+        return a
+    if nd == 0:
+        return a.reshape(tuple(a.shape[:nb]) + (1, 1))
+    n = a.shape[nb]
+    return a.reshape(tuple(a.shape[:nb]) + ((n, 1) if to_column_vector else (1, n)))
+
+
+# ---------------------------------------------------------------------------
+# constants / randomness
+# ---------------------------------------------------------------------------
+@prim("Fill")
+def _fill(nb, shape, value, bits, device="cpu"):
+    return R.fill(shape, value, bits, device)
+
+
+@prim("AddConst")
+def _add_const(nb, x, value, bits):
+    """x + value (mod 2^bits); lowers to Fill + Add."""
+    return R.binary("add", x, R.fill((), int(value), bits, x.device))
+
+
+@prim("SampleSeeded")
+def _sample_seeded(nb, shape, seed, bits, device="cpu"):
+    """Uniform ring tensor expanded from a 16-byte seed with AES-128-CTR."""
+    out = R.prf_expand([bytes(seed)], 0, tuple(shape), bits, device)
+    return R.RT(out.data[0], bits)
+
+
+@prim("Sample")
+def _sample(nb, shape, bits, device="cpu"):
+    import os
+
+    return _sample_seeded(nb, shape, os.urandom(16), bits, device)
+
+
+@prim("Zeros")
+def _zeros(nb, shape, dtype, device):
+    return torch.zeros(tuple(shape), dtype=dtype, device=device)
+
+
+@prim("Ones")
+def _ones(nb, shape, dtype, device):
+    return torch.ones(tuple(shape), dtype=dtype, device=device)
+
+
+# ---------------------------------------------------------------------------
+# ring <-> plaintext
+# ---------------------------------------------------------------------------
+@prim("RingFixedpointEncode")
+def _encode(nb, x, scaling_exp, bits):
+    return R.encode(x, scaling_exp, bits)
+
+
+@prim("RingFixedpointDecode")
+def _decode(nb, x, scaling_exp):
+    return R.decode(x, scaling_exp)
+
+
+@prim("BitExtract")
+def _bit_extract(nb, x, bit_idx):
+    return R.bit_extract(x, bit_idx)
+
+
+@prim("RingInject")
+def _ring_inject(nb, x, bit_idx, bits):
+    return R.ring_inject(x, bit_idx, bits)
+
+
+@prim("RingCast")
+def _ring_cast(nb, x, bits):
+    return R.cast(x, bits)
+
+
+@prim("Less")
+def _less(nb, a, b):
+    if _is_rt(a):
+        return R.compare("lt", a, b)
+    return a < b
+
+
+@prim("Greater")
+def _greater(nb, a, b):
+    if _is_rt(a):
+        return R.compare("gt", a, b)
+    return a > b
+
+
+@prim("Equal")
+def _equal(nb, a, b):
+    if _is_rt(a):
+        return R.compare("eq", a, b)
+    return a == b
+
+
+@prim("Msb")
+def _msb(nb, a):
+    return R.compare("msb", a)
+
+
+@prim("Mux")
+def _mux(nb, s, x, y):
+    if _is_rt(x):
+        sel = s if _is_rt(s) else R.RT(s.to(torch.uint8), 1)
+        m = R.ring_inject(sel, 0, x.bits) if sel.bits == 1 else sel
+        return R.binary("add", R.binary("mul", m, R.binary("sub", x, y)), y)
+    return torch.where(s.to(torch.bool), x, y)
+
+
+# ---------------------------------------------------------------------------
+# plaintext float math (host placements)
+# ---------------------------------------------------------------------------
+def _f(fn):
+    def impl(nb, a, **kw):
+        return fn(a, **kw)
+
+    return impl
+
+
+prim("Exp")(_f(torch.exp))
+prim("Log")(_f(torch.log))
+prim("Log2")(_f(torch.log2))
+prim("Sqrt")(_f(torch.sqrt))
+prim("Sigmoid")(_f(torch.sigmoid))
+prim("Relu")(_f(torch.relu))
+prim("Abs")(_f(torch.abs))
+prim("Sign")(_f(torch.sign))
+prim("Inverse")(_f(torch.linalg.inv))
+
+
+@prim("Softmax")
+def _softmax(nb, a, axis, upmost_index):
+    ax = _lax(a.dim(), axis, nb)
+    return torch.softmax(a, dim=ax)
+
+
+@prim("Argmax", ty=lambda tys, **a: T.Ty("HostUint64Tensor"))
+def _argmax(nb, a, axis, upmost_index):
+    ax = _lax(a.dim(), axis, nb)
+    return torch.argmax(a, dim=ax)
+
+
+@prim("Maximum")
+def _maximum(nb, *xs):
+    acc = xs[0]
+    for x in xs[1:]:
+        acc = torch.maximum(acc, x)
+    return acc
+
+
+@prim("Cast")
+def _cast(nb, x, dtype):
+    return x.to(dtype)
+
+
+@prim("Identity")
+def _identity(nb, x):
+    return x
+
+
+def numel_of(shape):
+    return math.prod(shape)

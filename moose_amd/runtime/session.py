@@ -1,0 +1,247 @@
+"""Execution sessions: where party-local work runs and how shares move.
+
+All MPC protocols (``moose_amd.protocols``) are written once against this API and run
+under three sessions:
+
+* :class:`StackedSession` -- all parties in one process on one device.  A party vector
+  (``PV``) is a single tensor with a leading party axis of size 3, so one kernel launch
+  does the local work of all three parties and a reshare is a roll of that axis.  This
+  is the single-MI355X mode (and the CPU mode for tests); it plays the role of the
+  reference's ``SyncSession``/``AsyncTestRuntime`` (``execution/synchronous.rs``,
+  ``execution/asynchronous.rs:634-773``).
+* :class:`moose_amd.parallel.spmd.SPMDSession` -- one process per party (one MI355X per
+  party); every reshare is an RCCL send/recv over xGMI.
+* :class:`moose_amd.compiler.symbolic.SymbolicSession` -- records host-level operations
+  instead of executing them (compile-time lowering, reference ``execution/symbolic.rs``).
+
+Vocabulary:
+
+* ``HV`` -- a value living on one host (``host`` = role name).
+* ``PV`` -- one component per party of a replicated placement ``plc``; component ``p``
+  lives on ``plc.owners[p]``.
+
+Keys: for every replicated placement the session holds k_0, k_1, k_2 (party p holds k_p
+and k_{p+1}, so PRF(k_s) is computable by exactly the two holders of slot s) and k_all.
+"""
+from __future__ import annotations
+
+import math
+import os
+from dataclasses import dataclass
+from typing import Any
+from typing import List
+from typing import Optional
+
+import torch
+
+from moose_amd.ir.computation import ReplicatedPlacement
+from moose_amd.ops import ring as R
+from moose_amd.runtime.prims import PRIMS
+from moose_amd.utils import telemetry
+
+
+@dataclass
+class HV:
+    host: str
+    v: Any
+
+
+@dataclass
+class PV:
+    plc: ReplicatedPlacement
+    v: Any
+
+
+class Public:
+    """Marks a value every party of a placement knows (no party axis)."""
+
+    __slots__ = ("v",)
+
+    def __init__(self, v):
+        self.v = v
+
+
+# primitives whose eager implementation needs the session's device
+_DEVICE_PRIMS = {"Fill", "Zeros", "Ones", "SampleSeeded", "Sample"}
+
+
+def _nbytes(v):
+    if isinstance(v, R.RT):
+        return v.data.numel() * v.data.element_size()
+    if isinstance(v, torch.Tensor):
+        return v.numel() * v.element_size()
+    if isinstance(v, (bytes, bytearray)):
+        return len(v)
+    return 8
+
+
+class Session:
+    """Common bookkeeping; see subclasses."""
+
+    nb_party = 0
+
+    def __init__(self, device="cpu", seed: Optional[int] = None):
+        self.device = torch.device(device)
+        self._nonce = 0
+        self.seed = seed
+        self.stats = telemetry.SessionStats()
+        self._keys = {}
+        self._rng = torch.Generator().manual_seed(seed) if seed is not None else None
+
+    def nonce(self) -> int:
+        """Fresh PRF nonce; all parties draw the same sequence (deterministic order)."""
+        self._nonce += 1
+        return self._nonce
+
+    def _random_bytes(self, n=16) -> bytes:
+        if self._rng is not None:
+            return bytes(torch.randint(0, 256, (n,), generator=self._rng,
+                                       dtype=torch.uint8).tolist())
+        return os.urandom(n)
+
+    def _attrs(self, prim, attrs):
+        if prim in _DEVICE_PRIMS and "device" not in attrs:
+            attrs = dict(attrs, device=self.device)
+        return attrs
+
+
+class StackedSession(Session):
+    """All three parties of every replicated placement on one device (module doc)."""
+
+    nb_party = 1
+    is_simulated = True
+
+    # -- keys ------------------------------------------------------------------
+    def setup(self, plc) -> List[bytes]:
+        ks = self._keys.get(plc)
+        if ks is None:
+            ks = [self._random_bytes() for _ in range(4)]  # k0, k1, k2, k_all
+            self._keys[plc] = ks
+        return ks
+
+    def party_keys(self, plc):
+        k = self.setup(plc)
+        return [k[0], k[1], k[2], k[0]]
+
+    # -- host ops ----------------------------------------------------------------
+    def h(self, prim, host, *args, **attrs):
+        vals = []
+        for a in args:
+            if isinstance(a, HV):
+                if a.host != host:
+                    a = self.move(a, host)
+                vals.append(a.v)
+            elif isinstance(a, PV):
+                raise TypeError("party vector passed to a host op")
+            else:
+                vals.append(a)
+        return HV(host, PRIMS[prim].impl(0, *vals, **self._attrs(prim, attrs)))
+
+    def move(self, x, host):
+        if x.host != host:
+            self.stats.record_send(x.host, host, _nbytes(x.v))
+        return HV(host, x.v)
+
+    def h_prf(self, plc, host, key_id, shape: HV, bits, nonce):
+        """PRF(k_key_id, nonce) sampled on ``host`` (which must hold that key)."""
+        keys = self.setup(plc)
+        k = keys[3] if key_id == "all" else keys[key_id]
+        out = R.prf_expand([k], nonce, tuple(shape.v), bits, self.device)
+        return HV(host, R.RT(out.data[0], bits))
+
+    def h_fresh_seed(self, host):
+        return HV(host, self._random_bytes())
+
+    # -- party vectors -------------------------------------------------------------
+    def p(self, prim, plc, *args, **attrs):
+        vals = []
+        for a in args:
+            if isinstance(a, PV):
+                vals.append(a.v)
+            elif isinstance(a, Public):
+                v = a.v
+                if prim in ("Dot", "Concat"):
+                    v = _stack3(v)
+                vals.append(v)
+            elif isinstance(a, HV):
+                raise TypeError("host value passed to a party-vector op; use public()")
+            else:
+                vals.append(a)
+        return PV(plc, PRIMS[prim].impl(1, *vals, **self._attrs(prim, attrs)))
+
+    def public(self, plc, value):
+        return Public(value)
+
+    def shift(self, x, k=1):
+        """Component p <- component p+k (one communication round)."""
+        self.stats.record_round(_nbytes(x.v))
+        v = x.v
+        if isinstance(v, R.RT):
+            return PV(x.plc, R.RT(torch.roll(v.data, -k, dims=0), v.bits))
+        return PV(x.plc, torch.roll(v, -k, dims=0))
+
+    def take(self, x, i):
+        v = x.v
+        if isinstance(v, R.RT):
+            return HV(x.plc.owners[i], R.RT(v.data[i], v.bits))
+        return HV(x.plc.owners[i], v[i])
+
+    def gather(self, plc, xs):
+        for i, x in enumerate(xs):
+            if x.host != plc.owners[i]:
+                self.stats.record_send(x.host, plc.owners[i], _nbytes(x.v))
+        vs = [x.v for x in xs]
+        if isinstance(vs[0], R.RT):
+            return PV(plc, R.RT(torch.stack([v.data for v in vs]), vs[0].bits))
+        return PV(plc, torch.stack(vs))
+
+    def p_public_slot(self, plc, value, slot, bits):
+        v = value if isinstance(value, R.RT) else R.fill((), int(value), bits, self.device)
+        d = torch.zeros((3,) + tuple(v.data.shape), dtype=v.data.dtype, device=self.device)
+        d[slot] = v.data
+        return PV(plc, R.RT(d, bits))
+
+    def p_apply_at(self, prim, plc, x, which, c):
+        """Apply ``prim(component, c)`` on party ``which`` only."""
+        v = x.v
+        part = PRIMS[prim].impl(0, R.RT(v.data[which], v.bits), c)
+        d = v.data.clone() if part.data.shape == v.data.shape[1:] else None
+        if d is None:  # broadcasting changed the shape
+            shp = (3,) + tuple(part.data.shape)
+            d = v.data.expand(shp).clone()
+        d[which] = part.data
+        return PV(plc, R.RT(d, v.bits))
+
+    def p_stack2(self, a, b):
+        return PV(a.plc, R.RT(torch.stack([a.v.data, b.v.data], dim=1), a.v.bits))
+
+    def p_unstack2(self, x):
+        return (PV(x.plc, R.RT(x.v.data[:, 0], x.v.bits)),
+                PV(x.plc, R.RT(x.v.data[:, 1], x.v.bits)))
+
+    # -- fused RSS kernels -----------------------------------------------------------
+    def p_cross(self, kind, plc, x0, x1, y0, y1, zero_share=True):
+        """Party p: x0*y0 + x0*y1 + x1*y0 (+ alpha_p with sum alpha = 0), one kernel."""
+        keys = self.party_keys(plc) if zero_share else None
+        out = R.rss_cross(kind, x0.v, x1.v if x1 is not None else None, y0.v,
+                          y1.v if y1 is not None else None, keys, self.nonce(), 3)
+        return PV(plc, out)
+
+    def p_dot_cross(self, plc, x0, x1, y0, y1):
+        return PV(plc, R.dot_cross(x0.v, x1.v, y0.v, y1.v, nb=1))
+
+    def p_add_zero_share(self, plc, z, kind="arith"):
+        keys = self.party_keys(plc)
+        return PV(plc, R.rss_cross(kind, z.v, None, None, None, keys, self.nonce(), 3))
+
+    def p_shape(self, x: PV):
+        return tuple(x.v.shape[1:])
+
+    def materialized(self, x) -> bool:
+        return True
+
+
+def _stack3(v):
+    if isinstance(v, R.RT):
+        return R.RT(v.data.unsqueeze(0).expand((3,) + tuple(v.data.shape)).contiguous(), v.bits)
+    return v.unsqueeze(0).expand((3,) + tuple(v.shape)).contiguous()

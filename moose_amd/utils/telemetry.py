@@ -1,0 +1,112 @@
+"""Tracing, counters and per-session metrics.
+
+* :class:`SessionStats` -- bytes sent per (sender, receiver) pair, communication rounds,
+  elapsed time per role (the reference only reports per-role ``elapsed_time``,
+  ``choreography/grpc.rs:150,187-192``).
+* :func:`span` -- a context manager recording a Chrome-trace event and, on GPU, a roctx
+  range (``torch.cuda.nvtx`` maps to roctx on ROCm) so protocol steps show up in
+  ``rocprofv3 --marker-trace`` timelines.
+* ``MOOSEX_TRACE=path.json`` dumps all spans at exit; ``MOOSEX_LOG`` sets the log level.
+"""
+from __future__ import annotations
+
+import atexit
+import json
+import logging
+import os
+import threading
+import time
+from collections import defaultdict
+from contextlib import contextmanager
+
+_LOG = logging.getLogger("moose_amd")
+if os.environ.get("MOOSEX_LOG"):
+    logging.basicConfig(level=os.environ["MOOSEX_LOG"].upper())
+
+
+def get_logger():
+    return _LOG
+
+
+class SessionStats:
+    def __init__(self):
+        self.bytes = defaultdict(int)
+        self.messages = defaultdict(int)
+        self.rounds = 0
+        self.round_bytes = 0
+        self.elapsed = {}
+
+    def record_send(self, src, dst, nbytes):
+        self.bytes[(src, dst)] += int(nbytes)
+        self.messages[(src, dst)] += 1
+
+    def record_round(self, nbytes):
+        self.rounds += 1
+        self.round_bytes += int(nbytes)
+
+    def as_dict(self):
+        return {
+            "rounds": self.rounds,
+            "reshare_bytes": self.round_bytes,
+            "bytes": {f"{a}->{b}": v for (a, b), v in self.bytes.items()},
+            "messages": {f"{a}->{b}": v for (a, b), v in self.messages.items()},
+            "elapsed_us": dict(self.elapsed),
+        }
+
+
+_EVENTS = []
+_EV_LOCK = threading.Lock()
+_TRACE_PATH = os.environ.get("MOOSEX_TRACE")
+
+
+def _nvtx():
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            return torch.cuda.nvtx
+    except Exception:  # pragma: no cover
+        pass
+    return None
+
+
+@contextmanager
+def span(name, **args):
+    """Record a named interval (Chrome trace + roctx range when on GPU)."""
+    nv = _nvtx() if _TRACE_PATH or os.environ.get("MOOSEX_ROCTX") else None
+    if nv is not None:
+        nv.range_push(name)
+    t0 = time.perf_counter_ns()
+    try:
+        yield
+    finally:
+        t1 = time.perf_counter_ns()
+        if nv is not None:
+            nv.range_pop()
+        if _TRACE_PATH:
+            with _EV_LOCK:
+                _EVENTS.append(
+                    {
+                        "name": name,
+                        "ph": "X",
+                        "ts": t0 / 1e3,
+                        "dur": (t1 - t0) / 1e3,
+                        "pid": os.getpid(),
+                        "tid": threading.get_ident() % 100000,
+                        "args": args,
+                    }
+                )
+
+
+def dump_trace(path=None):
+    path = path or _TRACE_PATH
+    if not path:
+        return
+    with _EV_LOCK:
+        evs = list(_EVENTS)
+    with open(path, "w") as f:
+        json.dump({"traceEvents": evs}, f)
+
+
+if _TRACE_PATH:
+    atexit.register(dump_trace)
