@@ -1,0 +1,533 @@
+"""Replicated fixed-point arithmetic and the non-linear functions built on it.
+
+Parity: reference ``moose/src/fixedpoint/ops.rs`` (precision bookkeeping, TruncPr after
+mul/dot) and ``moose/src/replicated/{division,exp,log,sqrt,softmax,argmax}.rs``.
+
+A :class:`RepFixed` is an arithmetic RSS tensor whose ring elements encode
+``value * 2^frac``.  Non-linear functions share one normalisation primitive:
+
+* :func:`_top_bit_onehot` -- bit-decompose |x| (packed words), prefix-OR from the top
+  (log2 k boolean ANDs), one-hot of the leading bit, then ONE batched B2A of the relevant
+  bit planes.  From the arithmetic one-hot bits t_j any public function of the exponent
+  (2^-j, 2^(j/2), j ...) is a local weighted sum.
+* mantissa m in [0.5, 1) = x * 2^(f-1-j)  ->  polynomial (Estrin/power-tree, log depth)
+  for 1/m, sqrt(m), log2(m).
+
+This replaces the reference's Goldschmidt reciprocal (division.rs:5-86) and int2fl log
+(log.rs:9-106) with fewer sequential rounds.  exp uses 2^x = 2^int * 2^frac with the
+integer part from B2A'd exponent bits (product tree, log depth -- the reference folds
+sequentially, exp.rs:155) and a polynomial for the fraction; negative inputs use the
+2^-int factors directly instead of a reciprocal.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from functools import lru_cache
+
+import numpy as np
+
+from moose_amd.ops import ring as R
+from moose_amd.protocols import replicated as rep
+from moose_amd.protocols.replicated import RepTensor
+from moose_amd.runtime.values import MV
+
+
+@dataclass
+class RepFixed:
+    t: RepTensor
+    frac: int
+    integ: int
+
+    @property
+    def bits(self):
+        return self.t.bits
+
+    @property
+    def plc(self):
+        return self.t.plc
+
+
+def _pub(v):
+    """Public operand payload: MV -> its value."""
+    return v.v if isinstance(v, MV) else v
+
+
+def _encode_const(sess, value: float, frac: int, bits: int):
+    return R.fill((), int(round(value * (1 << frac))), bits, sess.device)
+
+
+def _with(x: RepFixed, t: RepTensor) -> RepFixed:
+    return RepFixed(t, x.frac, x.integ)
+
+
+# ---------------------------------------------------------------------------
+# linear ops
+# ---------------------------------------------------------------------------
+def local(sess, x, prim, *extra, **attrs):
+    if isinstance(x, RepFixed):
+        return _with(x, local(sess, x.t, prim, *extra, **attrs))
+    if extra:
+        # extra positional (e.g. Select mask) are public values
+        pub = [sess.public(x.plc, e) for e in extra]
+        return RepTensor(x.plc, x.bits, x.kind, sess.p(prim, x.plc, x.s0, *pub, **attrs),
+                         sess.p(prim, x.plc, x.s1, *pub, **attrs))
+    return rep.local(sess, x, prim, **attrs)
+
+
+def add(sess, x, y, px=None, py=None):
+    if px is not None:
+        return _with(y, rep.add_public(sess, y.t, px))
+    if py is not None:
+        return _with(x, rep.add_public(sess, x.t, py))
+    return _with(x, rep.add(sess, x.t, y.t))
+
+
+def sub(sess, x, y, px=None, py=None):
+    if px is not None:
+        return _with(y, rep.add_public(sess, rep.neg(sess, y.t), px))
+    if py is not None:
+        return _with(x, rep.sub_public(sess, x.t, py))
+    return _with(x, rep.sub(sess, x.t, y.t))
+
+
+def neg(sess, x: RepFixed) -> RepFixed:
+    return _with(x, rep.neg(sess, x.t))
+
+
+def mul(sess, x, y, px=None, py=None, f=None):
+    if px is not None:
+        x, y, px, py = y, MV(None, px), None, px
+    if py is not None:
+        z = rep.mul_public(sess, x.t, _pub(py))
+    else:
+        z = rep.mul(sess, x.t, y.t)
+    return _with(x, rep.trunc_pr(sess, z, f if f is not None else x.frac))
+
+
+def dot(sess, x, y, px=None, py=None, f=None):
+    if px is not None:
+        z = rep.dot_public(sess, y.t, px, public_left=True)
+        base = y
+    elif py is not None:
+        z = rep.dot_public(sess, x.t, py)
+        base = x
+    else:
+        z = rep.dot(sess, x.t, y.t)
+        base = x
+    return _with(base, rep.trunc_pr(sess, z, f if f is not None else base.frac))
+
+
+def mul_const(sess, x: RepFixed, c: float) -> RepFixed:
+    """x * c for a public real constant (one truncation)."""
+    z = rep.mul_public(sess, x.t, _encode_const(sess, c, x.frac, x.bits))
+    return _with(x, rep.trunc_pr(sess, z, x.frac))
+
+
+def add_const(sess, x: RepFixed, c: float) -> RepFixed:
+    return _with(x, rep.add_public(sess, x.t, _encode_const(sess, c, x.frac, x.bits)))
+
+
+def ring_binary(sess, kind, x, y, px=None, py=None):
+    if kind == "Add":
+        if px is not None:
+            return rep.add_public(sess, y, px)
+        if py is not None:
+            return rep.add_public(sess, x, py)
+        return rep.add(sess, x, y)
+    if kind == "Sub":
+        if py is not None:
+            return rep.sub_public(sess, x, py)
+        if px is not None:
+            return rep.add_public(sess, rep.neg(sess, y), px)
+        return rep.sub(sess, x, y)
+    if kind == "Mul":
+        if py is not None:
+            return rep.mul_public(sess, x, py)
+        if px is not None:
+            return rep.mul_public(sess, y, px)
+        return rep.mul(sess, x, y)
+    if kind == "Dot":
+        if py is not None:
+            return rep.dot_public(sess, x, py)
+        if px is not None:
+            return rep.dot_public(sess, y, px, public_left=True)
+        return rep.dot(sess, x, y)
+    raise NotImplementedError(kind)
+
+
+def cast(sess, x: RepFixed, target) -> RepFixed:
+    bits = target.ring_bits
+    t = x.t
+    df = target.fractional_precision - x.frac
+    if df < 0:
+        t = rep.trunc_pr(sess, t, -df)
+    if bits != t.bits:
+        if bits < t.bits:
+            t = rep.ring_cast(sess, t, bits)
+        else:
+            raise NotImplementedError("replicated ring extension 64 -> 128")
+    if df > 0:
+        t = rep.shl(sess, t, df)
+    return RepFixed(t, target.fractional_precision, target.integral_precision)
+
+
+def mean(sess, x: RepFixed, axis):
+    s = local(sess, x, "Sum", axis=axis)
+    shape = shape_of(sess, x)
+    n = math.prod(shape) if axis is None else shape[axis]
+    return mul_const(sess, s, 1.0 / n)
+
+
+def concat(sess, xs, axis):
+    ts = [x.t if isinstance(x, RepFixed) else x for x in xs]
+    plc = ts[0].plc
+    s0 = sess.p("Concat", plc, *[t.s0 for t in ts], axis=axis)
+    s1 = sess.p("Concat", plc, *[t.s1 for t in ts], axis=axis)
+    t = RepTensor(plc, ts[0].bits, ts[0].kind, s0, s1)
+    return _with(xs[0], t) if isinstance(xs[0], RepFixed) else t
+
+
+def shape_of(sess, x):
+    t = x.t if isinstance(x, RepFixed) else x
+    if isinstance(t, MV):
+        return tuple(t.v.shape)
+    return sess.p_shape(t.s0)
+
+
+# ---------------------------------------------------------------------------
+# comparisons and selection
+# ---------------------------------------------------------------------------
+def _as_rep(sess, x, like: RepFixed):
+    if isinstance(x, RepFixed):
+        return x
+    return RepFixed(rep.from_public(sess, like.plc, _pub(x), like.bits), like.frac, like.integ)
+
+
+def compare(sess, kind, x, y, px=None, py=None) -> RepTensor:
+    """[x < y] / [x > y] as a boolean bit sharing."""
+    if px is not None:
+        diff = rep.add_public(sess, rep.neg(sess, _t(y)), px)  # px - y
+    elif py is not None:
+        diff = rep.sub_public(sess, _t(x), py)  # x - py
+    else:
+        diff = rep.sub(sess, _t(x), _t(y))
+    if kind == "Less":
+        return rep.msb(sess, diff)
+    # x > y  <=>  y - x < 0
+    return rep.msb(sess, rep.neg(sess, diff))
+
+
+def _t(x):
+    return x.t if isinstance(x, RepFixed) else x
+
+
+def mux(sess, s, x, y):
+    """s ? x : y  (s boolean bit or arithmetic 0/1)."""
+    if isinstance(x, RepFixed):
+        return _with(x, rep.mux(sess, s, x.t, y.t))
+    return rep.mux(sess, s, x, y)
+
+
+def sign_bit(sess, x: RepFixed) -> RepTensor:
+    """Arithmetic 0/1 sharing of [x < 0]."""
+    return rep.b2a(sess, rep.msb(sess, x.t), x.bits)
+
+
+def relu(sess, x: RepFixed) -> RepFixed:
+    s = sign_bit(sess, x)
+    return _with(x, rep.sub(sess, x.t, rep.mul(sess, s, x.t)))
+
+
+def abs_(sess, x: RepFixed) -> RepFixed:
+    s = sign_bit(sess, x)
+    return _with(x, rep.sub(sess, x.t, rep.shl(sess, rep.mul(sess, s, x.t), 1)))
+
+
+def maximum(sess, xs):
+    """Elementwise maximum of a list: tree of (less, mux)."""
+    xs = list(xs)
+    while len(xs) > 1:
+        nxt = []
+        for i in range(0, len(xs) - 1, 2):
+            a, b = xs[i], xs[i + 1]
+            lt = rep.msb(sess, rep.sub(sess, a.t, b.t))  # a < b
+            nxt.append(mux(sess, lt, b, a))
+        if len(xs) % 2:
+            nxt.append(xs[-1])
+        xs = nxt
+    return xs[0]
+
+
+# ---------------------------------------------------------------------------
+# normalisation: leading-bit one-hot
+# ---------------------------------------------------------------------------
+def _or(sess, a: RepTensor, b: RepTensor) -> RepTensor:
+    return rep.xor(sess, rep.xor(sess, a, b), rep.and_(sess, a, b))
+
+
+def _top_bit_onehot(sess, x: RepTensor, lo: int, hi: int) -> RepTensor:
+    """For x >= 0 (arithmetic): arithmetic 0/1 sharings t_j, j in [lo, hi), stacked on a
+    new leading axis, with t_j = 1 iff bit j is the leading one of x."""
+    bits = x.bits
+    bd = rep.bit_decompose(sess, x)
+    p = bd
+    d = 1
+    while d < bits:
+        p = _or(sess, p, rep.local(sess, p, "Shr", amount=d))
+        d *= 2
+    onehot = rep.xor(sess, p, rep.local(sess, p, "Shr", amount=1))
+    planes = RepTensor(x.plc, 1, "bool", sess.p("BitSplit", x.plc, onehot.s0, start=lo, count=hi - lo),
+                       sess.p("BitSplit", x.plc, onehot.s1, start=lo, count=hi - lo))
+    return rep.b2a(sess, planes, bits)
+
+
+def _weighted(sess, t: RepTensor, weights, bits) -> RepTensor:
+    """sum_j w_j t_j over the leading axis (public integer weights, mod 2^bits)."""
+    w = [int(v) % (1 << bits) for v in weights]
+    return RepTensor(t.plc, bits, "arith", sess.p("WeightedSum", t.plc, t.s0, weights=w, bits=bits),
+                     sess.p("WeightedSum", t.plc, t.s1, weights=w, bits=bits))
+
+
+def _normalize(sess, x: RepFixed):
+    """x > 0 -> (m, t, lo) with m = x * 2^(f-1-j) in [0.5, 1) (fixed, frac f) and t the
+    arithmetic one-hot of the leading bit position j in [lo, lo + len)."""
+    f, bits = x.frac, x.bits
+    hi = min(bits - 1, f + x.integ + 1)
+    lo = 0
+    t = _top_bit_onehot(sess, x.t, lo, hi)
+    # scale factor 2^(f-1-j) as fixed point: weight 2^(2f-1-j) (needs j <= 2f-1)
+    weights = [(1 << (2 * f - 1 - j)) if 2 * f - 1 - j >= 0 else 0 for j in range(lo, hi)]
+    F = RepFixed(_weighted(sess, t, weights, bits), f, x.integ)
+    m = mul(sess, x, F)
+    return m, t, lo, hi
+
+
+# ---------------------------------------------------------------------------
+# polynomials (log-depth power tree, public coefficients)
+# ---------------------------------------------------------------------------
+def poly_eval(sess, x: RepFixed, coeffs) -> RepFixed:
+    """sum_k c_k x^k.  Powers x^2..x^n are computed level by level (x^(a+b) from x^a,
+    x^b with a, b <= 2^level), so depth is ceil(log2 n) multiplication rounds; all powers
+    of one level are batched into one stacked multiplication."""
+    n = len(coeffs) - 1
+    powers = {1: x}
+    have = 1
+    while have < n:
+        targets = [k for k in range(have + 1, min(2 * have, n) + 1)]
+        lefts = [powers[have] for _ in targets]
+        rights = [powers[k - have] for k in targets]
+        prods = _batched_mul(sess, lefts, rights)
+        for k, pr in zip(targets, prods):
+            powers[k] = pr
+        have = min(2 * have, n)
+    f, bits = x.frac, x.bits
+    acc = None
+    for k in range(1, n + 1):
+        c = coeffs[k]
+        if c == 0:
+            continue
+        term = rep.mul_public(sess, powers[k].t, _encode_const(sess, c, f, bits))
+        acc = term if acc is None else rep.add(sess, acc, term)
+    acc = rep.trunc_pr(sess, acc, f)
+    out = RepFixed(acc, f, x.integ)
+    return add_const(sess, out, coeffs[0])
+
+
+def _batched_mul(sess, xs, ys):
+    """Several independent fixed-point products in one round (stacked on a new axis)."""
+    if len(xs) == 1:
+        return [mul(sess, xs[0], ys[0])]
+    X = concat(sess, [local(sess, v, "ExpandDims", axis=[0]) for v in xs], 0)
+    Y = concat(sess, [local(sess, v, "ExpandDims", axis=[0]) for v in ys], 0)
+    Z = mul(sess, X, Y)
+    return [local(sess, Z, "IndexAxis", axis=0, index=i) for i in range(len(xs))]
+
+
+@lru_cache(maxsize=None)
+def _fit(fn_name: str, lo: float, hi: float, degree: int):
+    """Least-squares Chebyshev fit -> monomial coefficients (float64)."""
+    xs = np.cos(np.linspace(0, np.pi, 4001)) * (hi - lo) / 2 + (hi + lo) / 2
+    fn = {
+        "recip": lambda v: 1.0 / v,
+        "sqrt": np.sqrt,
+        "rsqrt": lambda v: 1.0 / np.sqrt(v),
+        "log2": np.log2,
+        "exp2": np.exp2,
+    }[fn_name]
+    poly = np.polynomial.Polynomial.fit(xs, fn(xs), degree).convert()
+    return tuple(float(c) for c in poly.coef)
+
+
+# ---------------------------------------------------------------------------
+# reciprocal / division / sqrt / log
+# ---------------------------------------------------------------------------
+def _newton_recip(sess, m: RepFixed, w: RepFixed, iters: int) -> RepFixed:
+    for _ in range(iters):
+        e = add_const(sess, neg(sess, mul(sess, m, w)), 2.0)  # 2 - m w
+        w = mul(sess, w, e)
+    return w
+
+
+def reciprocal_positive(sess, x: RepFixed) -> RepFixed:
+    m, t, lo, hi = _normalize(sess, x)
+    f = x.frac
+    w = poly_eval(sess, m, _fit("recip", 0.5, 1.0, 4))
+    w = _newton_recip(sess, m, w, 2 if f > 24 else 1)
+    weights = [(1 << (2 * f - 1 - j)) if 2 * f - 1 - j >= 0 else 0 for j in range(lo, hi)]
+    F = RepFixed(_weighted(sess, t, weights, x.bits), f, x.integ)
+    return mul(sess, w, F)
+
+
+def reciprocal(sess, x: RepFixed) -> RepFixed:
+    s = sign_bit(sess, x)
+    ax = _with(x, rep.sub(sess, x.t, rep.shl(sess, rep.mul(sess, s, x.t), 1)))
+    r = reciprocal_positive(sess, ax)
+    return _with(r, rep.sub(sess, r.t, rep.shl(sess, rep.mul(sess, s, r.t), 1)))
+
+
+def div(sess, x, y, px=None, py=None):
+    if py is not None:
+        # public divisor: multiply by its reciprocal computed in the clear
+        yv = R.decode(_pub(py), x.frac)
+        inv = R.encode(1.0 / yv, x.frac, x.bits)
+        return _with(x, rep.trunc_pr(sess, rep.mul_public(sess, x.t, inv), x.frac))
+    r = reciprocal(sess, y)
+    if px is not None:
+        return _with(r, rep.trunc_pr(sess, rep.mul_public(sess, r.t, _pub(px)), r.frac))
+    return mul(sess, x, r)
+
+
+def sqrt(sess, x: RepFixed) -> RepFixed:
+    """sqrt(x) = sqrt(m) * 2^((j - f + 1) / 2) for x = m * 2^(j-f+1), m in [0.5, 1)."""
+    m, t, lo, hi = _normalize(sess, x)
+    f = x.frac
+    sm = poly_eval(sess, m, _fit("sqrt", 0.5, 1.0, 5))
+    weights = [int(round(2.0 ** ((j - f + 1) / 2.0) * (1 << f))) for j in range(lo, hi)]
+    G = RepFixed(_weighted(sess, t, weights, x.bits), f, x.integ)
+    return mul(sess, sm, G)
+
+
+def log2(sess, x: RepFixed) -> RepFixed:
+    """log2(x) = log2(m) + (j - f + 1)."""
+    m, t, lo, hi = _normalize(sess, x)
+    f = x.frac
+    lm = poly_eval(sess, m, _fit("log2", 0.5, 1.0, 8))
+    weights = [((j - f + 1) << f) for j in range(lo, hi)]
+    E = _weighted(sess, t, weights, x.bits)
+    return _with(lm, rep.add(sess, lm.t, E))
+
+
+def log(sess, x: RepFixed) -> RepFixed:
+    return mul_const(sess, log2(sess, x), math.log(2.0))
+
+
+# ---------------------------------------------------------------------------
+# exponentials
+# ---------------------------------------------------------------------------
+def _exp2_parts(sess, a: RepFixed, negative: bool):
+    """2^a (or 2^-a) for a >= 0: integer part from B2A'd bits (product tree of public
+    factors), fraction via polynomial."""
+    f, bits, integ = a.frac, a.bits, a.integ
+    nint = max(1, min(6, int(math.ceil(math.log2(max(2, integ + 1))))))
+    bd = rep.bit_decompose(sess, a.t)
+    planes = RepTensor(a.plc, 1, "bool", sess.p("BitSplit", a.plc, bd.s0, start=0, count=f + nint),
+                       sess.p("BitSplit", a.plc, bd.s1, start=0, count=f + nint))
+    ab = rep.b2a(sess, planes, bits)  # arithmetic bits, leading axis
+    frac_w = [(1 << j) for j in range(f)] + [0] * nint
+    r = RepFixed(_weighted(sess, ab, frac_w, bits), f, integ)
+    if negative:
+        # 2^-r for r in [0,1) = 2^(1-r) / 2 -> fit exp2 on [0, 1] of (1 - r)
+        one_minus = add_const(sess, neg(sess, r), 1.0)
+        p = mul_const(sess, poly_eval(sess, one_minus, _fit("exp2", 0.0, 1.0, 7)), 0.5)
+    else:
+        p = poly_eval(sess, r, _fit("exp2", 0.0, 1.0, 7))
+    # integer part factors: 1 + b_j (c_j - 1), c_j = 2^(+-2^j)
+    factors = []
+    for j in range(nint):
+        bj = local(sess, ab, "IndexAxis", axis=0, index=f + j)
+        c = 2.0 ** (-(2 ** j) if negative else (2 ** j))
+        fac = rep.mul_public(sess, bj, _encode_const(sess, c - 1.0, f, bits))
+        fac = rep.add_public(sess, fac, _encode_const(sess, 1.0, f, bits))
+        factors.append(RepFixed(fac, f, integ))
+    while len(factors) > 1:
+        nxt = _batched_mul(sess, factors[0::2][: len(factors) // 2], factors[1::2])
+        if len(factors) % 2:
+            nxt.append(factors[-1])
+        factors = nxt
+    return mul(sess, p, factors[0])
+
+
+def exp2(sess, x: RepFixed) -> RepFixed:
+    s = sign_bit(sess, x)
+    ax = _with(x, rep.sub(sess, x.t, rep.shl(sess, rep.mul(sess, s, x.t), 1)))
+    pos = _exp2_parts(sess, ax, negative=False)
+    negv = _exp2_parts(sess, ax, negative=True)
+    return _with(pos, rep.mux(sess, s, negv.t, pos.t))
+
+
+def exp(sess, x: RepFixed) -> RepFixed:
+    return exp2(sess, mul_const(sess, x, 1.0 / math.log(2.0)))
+
+
+def exp_nonpositive(sess, x: RepFixed) -> RepFixed:
+    """e^x for x <= 0 (softmax after max subtraction, sigmoid): no sign mux."""
+    a = mul_const(sess, neg(sess, x), 1.0 / math.log(2.0))
+    return _exp2_parts(sess, a, negative=True)
+
+
+def sigmoid(sess, x: RepFixed) -> RepFixed:
+    """sigma(x) = 1 / (1 + e^-|x|) mirrored for x < 0; 1 + e^-|x| is in [1, 2] so the
+    reciprocal needs no normalisation."""
+    s = sign_bit(sess, x)
+    ax = _with(x, rep.sub(sess, x.t, rep.shl(sess, rep.mul(sess, s, x.t), 1)))
+    e = exp_nonpositive(sess, neg(sess, ax))
+    d = add_const(sess, e, 1.0)  # in [1, 2]
+    half = mul_const(sess, d, 0.5)  # in [0.5, 1]
+    w = poly_eval(sess, half, _fit("recip", 0.5, 1.0, 4))
+    w = _newton_recip(sess, half, w, 1)
+    pos = mul_const(sess, w, 0.5)  # 1/d
+    one_minus = add_const(sess, neg(sess, pos), 1.0)
+    return _with(pos, rep.mux(sess, s, one_minus.t, pos.t))
+
+
+def softmax(sess, x: RepFixed, axis: int, upmost_index: int) -> RepFixed:
+    n = shape_of(sess, x)[axis]
+    cols = [local(sess, x, "IndexAxis", axis=axis, index=i) for i in range(min(n, upmost_index))]
+    mx = maximum(sess, cols)
+    mxe = local(sess, mx, "ExpandDims", axis=[axis])
+    shifted = _with(x, rep.sub(sess, x.t, _bcast(sess, mxe.t, x.t)))
+    e = exp_nonpositive(sess, shifted)
+    ssum = local(sess, e, "Sum", axis=axis)  # >= 1 (the max term is e^0)
+    inv = reciprocal_positive(sess, ssum)
+    inve = local(sess, inv, "ExpandDims", axis=[axis])
+    return mul(sess, e, _with(inve, _bcast(sess, inve.t, e.t)))
+
+
+def _bcast(sess, small: RepTensor, big: RepTensor) -> RepTensor:
+    shape = sess.p_shape(big.s0)
+    return rep.local(sess, small, "Broadcast", shape=shape)
+
+
+def argmax(sess, x: RepFixed, axis: int, upmost_index: int) -> RepTensor:
+    """Index of the maximum along ``axis`` as an arithmetic Z_2^64 sharing: tree of
+    (value, index) pairs reduced with less + mux (reference argmax.rs:6-96)."""
+    n = min(shape_of(sess, x)[axis], upmost_index)
+    vals = [local(sess, x, "IndexAxis", axis=axis, index=i) for i in range(n)]
+    bits = x.bits
+    idx = [rep.from_public(sess, x.plc, R.fill(shape_of(sess, vals[0]), i, bits, sess.device),
+                           bits) for i in range(n)]
+    pairs = list(zip(vals, idx))
+    while len(pairs) > 1:
+        nxt = []
+        for i in range(0, len(pairs) - 1, 2):
+            (va, ia), (vb, ib) = pairs[i], pairs[i + 1]
+            lt = rep.b2a(sess, rep.msb(sess, rep.sub(sess, va.t, vb.t)), bits)  # a < b
+            v = _with(va, rep.mux(sess, lt, vb.t, va.t))
+            ix = rep.mux(sess, lt, ib, ia)
+            nxt.append((v, ix))
+        if len(pairs) % 2:
+            nxt.append(pairs[-1])
+        pairs = nxt
+    out = pairs[0][1]
+    return rep.ring_cast(sess, out, 64) if bits != 64 else out

@@ -1,0 +1,731 @@
+"""Logical interpreter: evaluate a (logical-level) native-IR computation on a session.
+
+Each logical operator is dispatched on its placement kind, exactly like the
+reference's logical kernels (``moose/src/logical/ops.rs``: ``logical_host_kernel`` /
+``logical_rep_kernel``) and fixed-point kernels (``moose/src/fixedpoint/ops.rs``):
+inputs are implicitly converted to the op's placement (share host values onto a
+replicated placement, reveal replicated values to a host, mirror/demirror), fixed-point
+products are followed by a truncation, and comparisons return boolean sharings.
+
+Unlike the reference, the replicated path is *not* first lowered to thousands of host
+ops: every replicated op runs its fused protocol directly on the session (one stacked
+kernel per local step on a single MI355X, RCCL send/recv between MI355Xs), which is the
+fast path used by ``LocalMooseRuntime`` and the benchmarks.  Lowering to a host graph
+is still available (``moose_amd.compiler``) and runs the same protocol code on a
+symbolic session.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict
+
+import numpy as np
+import torch
+
+from moose_amd.ir import types as T
+from moose_amd.ir.computation import Computation
+from moose_amd.ir.computation import Constant
+from moose_amd.ir.computation import HostPlacement
+from moose_amd.ir.computation import Mirrored3Placement
+from moose_amd.ir.computation import Operation
+from moose_amd.ir.computation import ReplicatedPlacement
+from moose_amd.ops import ring as R
+from moose_amd.protocols import fixedpoint as fxp
+from moose_amd.protocols import replicated as rep
+from moose_amd.protocols.fixedpoint import RepFixed
+from moose_amd.runtime.session import HV
+from moose_amd.runtime.values import LV
+from moose_amd.runtime.values import MV
+from moose_amd.utils.telemetry import span
+
+_FLOAT = {"Float32": torch.float32, "Float64": torch.float64}
+
+
+class MooseRuntimeError(RuntimeError):
+    pass
+
+
+def torch_dtype_of(dtype: T.TensorDType):
+    k = dtype.kind
+    if k in _FLOAT:
+        return _FLOAT[k]
+    if k == "Bool":
+        return torch.bool
+    if k == "Uint64":
+        return torch.int64
+    raise MooseRuntimeError(f"no plaintext torch dtype for {dtype}")
+
+
+def dtype_of_numpy(a: np.ndarray) -> T.TensorDType:
+    m = {
+        np.dtype("float64"): T.FLOAT64,
+        np.dtype("float32"): T.FLOAT32,
+        np.dtype("bool"): T.BOOL,
+        np.dtype("uint64"): T.UINT64,
+    }
+    if a.dtype in m:
+        return m[a.dtype]
+    if np.issubdtype(a.dtype, np.integer):
+        return T.TensorDType("Uint64") if a.dtype.kind == "u" else T.TensorDType("Int64")
+    raise MooseRuntimeError(f"unsupported numpy dtype {a.dtype}")
+
+
+def numpy_to_torch(a, device):
+    a = np.asarray(a)
+    if a.dtype == np.uint64:
+        return torch.from_numpy(a.view(np.int64).copy()).to(device)
+    if a.dtype == np.uint32:
+        a = a.astype(np.int64)
+    if a.dtype == object:
+        raise MooseRuntimeError("object arrays are not tensors")
+    return torch.from_numpy(np.ascontiguousarray(a)).to(device)
+
+
+class Interpreter:
+    def __init__(self, sess, storage=None, fixedpoint_ring: int = None):
+        self.sess = sess
+        self.storage = storage if storage is not None else {}
+        self.env: Dict[str, LV] = {}
+        self.fixed_ring = fixedpoint_ring  # override Fixed128 -> Fixed64 if 64
+        self.outputs = {}
+
+    # ------------------------------------------------------------------------
+    # driver
+    # ------------------------------------------------------------------------
+    def run(self, comp: Computation, arguments: dict) -> dict:
+        self.arguments = arguments or {}
+        comp = comp.toposorted()
+        for op in comp.operations:
+            handler = getattr(self, f"op_{op.kind}", None)
+            if handler is None:
+                raise MooseRuntimeError(f"operator {op.kind} is not supported by the interpreter")
+            ins = [self.env[n] for n in op.inputs]
+            with span(f"op.{op.kind}", op=op.name):
+                try:
+                    self.env[op.name] = handler(op, ins)
+                except MooseRuntimeError:
+                    raise
+                except Exception as e:  # annotate with the failing op
+                    raise MooseRuntimeError(f"{op.name} = {op.kind} failed: {e}") from e
+        return self.outputs
+
+    # ------------------------------------------------------------------------
+    # dtype helpers
+    # ------------------------------------------------------------------------
+    def _dtype(self, d: T.TensorDType) -> T.TensorDType:
+        if d is not None and d.kind == "Fixed128" and self.fixed_ring == 64:
+            return T.TensorDType("Fixed64", d.integral_precision, d.fractional_precision)
+        return d
+
+    def _ret_dtype(self, op):
+        return self._dtype(op.sig.ret.dtype) if op.sig.ret.name == "Tensor" else None
+
+    # ------------------------------------------------------------------------
+    # placement conversions
+    # ------------------------------------------------------------------------
+    def to_host(self, x: LV, host: str) -> LV:
+        sess = self.sess
+        hp = HostPlacement(host)
+        if x.is_host:
+            if x.host == host:
+                return x
+            return LV(hp, x.kind, x.dtype, sess.move(x.v, host))
+        if x.is_rep and isinstance(x.v, MV):
+            return LV(hp, x.kind, x.dtype, HV(host, x.v.v))
+        if x.is_mir:
+            return LV(hp, x.kind, x.dtype, HV(host, x.v.v))
+        if x.is_rep:
+            if x.kind != "tensor":
+                return LV(hp, x.kind, x.dtype, HV(host, x.v))
+            if isinstance(x.v, RepFixed):
+                ring = rep.reveal(sess, x.v.t, host)
+                return LV(hp, "tensor", x.dtype, ring)
+            opened = rep.reveal(sess, x.v, host)
+            if x.dtype.kind == "Bool":
+                return LV(hp, "tensor", x.dtype, sess.h("ToBool", host, opened))
+            if x.dtype.kind == "Uint64":
+                return LV(hp, "tensor", x.dtype, sess.h("RingToInt", host, opened))
+            return LV(hp, "tensor", x.dtype, opened)
+        raise MooseRuntimeError(f"cannot move {x} to host {host}")
+
+    def to_rep(self, x: LV, plc: ReplicatedPlacement) -> LV:
+        if x.is_rep and x.plc == plc:
+            return x
+        if x.kind != "tensor":
+            if x.kind == "shape":
+                return LV(plc, "shape", None, self._plain(x))
+            return x
+        if x.is_mir or (x.is_rep and isinstance(x.v, MV)):
+            return LV(plc, "tensor", x.dtype, MV(x.plc, x.v.v))
+        if x.is_rep:  # another replicated placement: reveal then re-share
+            x = self.to_host(x, plc.owners[0])
+        d = x.dtype
+        sess = self.sess
+        if d.is_fixed:
+            t = rep.share(sess, plc, x.v)
+            return LV(plc, "tensor", d, RepFixed(t, d.fractional_precision, d.integral_precision))
+        if d.kind == "Bool":
+            bits = sess.h("FromBool", x.host, x.v)
+            return LV(plc, "tensor", d, rep.share(sess, plc, bits, kind="bool"))
+        if d.kind == "Uint64":
+            ring = sess.h("IntToRing", x.host, x.v)
+            return LV(plc, "tensor", d, rep.share(sess, plc, ring))
+        raise MooseRuntimeError(
+            f"cannot secret-share a {d} tensor; cast it to a fixed-point dtype first"
+        )
+
+    def to_mir(self, x: LV, plc: Mirrored3Placement) -> LV:
+        if x.is_mir and x.plc == plc:
+            return x
+        if x.is_rep and isinstance(x.v, MV):
+            return LV(plc, x.kind, x.dtype, MV(plc, x.v.v))
+        h = self.to_host(x, plc.owners[0]) if not x.is_host else x
+        return LV(plc, h.kind, h.dtype, self.sess.mirror(h.v, plc))
+
+    def _plain(self, x: LV):
+        """Python/plaintext value of a non-secret LV (shapes, strings, scalars)."""
+        v = x.v
+        if isinstance(v, HV):
+            return v.v
+        if isinstance(v, MV):
+            return v.v
+        return v
+
+    def _public(self, x: LV):
+        return x.v.v if isinstance(x.v, MV) else None
+
+    def at(self, op, x: LV) -> LV:
+        plc = op.placement
+        if isinstance(plc, HostPlacement):
+            return self.to_host(x, plc.owner)
+        if isinstance(plc, ReplicatedPlacement):
+            return self.to_rep(x, plc)
+        if isinstance(plc, Mirrored3Placement):
+            return self.to_mir(x, plc)
+        raise MooseRuntimeError(f"unsupported placement {plc}")
+
+    # ------------------------------------------------------------------------
+    # IO
+    # ------------------------------------------------------------------------
+    def _host_value_from_python(self, host, value, want: T.Ty):
+        sess = self.sess
+        hp = HostPlacement(host)
+        if isinstance(value, str):
+            return LV(hp, "string", None, HV(host, value))
+        if isinstance(value, (tuple, list)) and want is not None and want.name in ("HostShape", "Shape"):
+            return LV(hp, "shape", None, HV(host, tuple(value)))
+        if isinstance(value, float) and not isinstance(value, np.ndarray):
+            if want is None or want.name != "Tensor":
+                return LV(hp, "float", None, HV(host, value))
+        if isinstance(value, int) and not isinstance(value, bool):
+            if want is None or want.name != "Tensor":
+                return LV(hp, "int", None, HV(host, value))
+        arr = np.asarray(value)
+        dtype = dtype_of_numpy(arr)
+        t = numpy_to_torch(arr, sess.device)
+        lv = LV(hp, "tensor", dtype, HV(host, t))
+        if want is not None and want.name == "Tensor" and want.dtype.kind not in ("Unknown",):
+            wd = self._dtype(want.dtype)
+            if wd != dtype:
+                lv = self._cast_host(lv, wd)
+        return lv
+
+    def op_Input(self, op, ins):
+        name = op.attrs.get("arg_name") or op.name
+        if name not in self.arguments:
+            raise MooseRuntimeError(f"missing argument {name}")
+        plc = op.placement
+        host = plc.owner if isinstance(plc, HostPlacement) else plc.owners[0]
+        lv = self._host_value_from_python(host, self.arguments[name], op.sig.ret)
+        return lv if isinstance(plc, HostPlacement) else self.at(op, lv)
+
+    def op_Constant(self, op, ins):
+        c: Constant = op.attrs["value"]
+        plc = op.placement
+        host = plc.owner if isinstance(plc, HostPlacement) else plc.owners[0]
+        want = op.sig.ret
+        hp = HostPlacement(host)
+        if c.kind == "HostShape":
+            lv = LV(hp, "shape", None, HV(host, tuple(c.value)))
+        elif c.kind == "HostString":
+            lv = LV(hp, "string", None, HV(host, c.value))
+        elif c.kind in ("Float32", "Float64"):
+            lv = self._host_value_from_python(host, np.array(c.value, dtype=np.float64)
+                                              if want.name == "Tensor" else float(c.value), want)
+        elif c.kind in ("HostRing64Tensor", "HostRing128Tensor"):
+            bits = 64 if "64" in c.kind else 128
+            lv = LV(hp, "tensor", None, HV(host, R.from_ints(c.value, bits, self.sess.device)))
+        else:
+            arr = np.asarray(c.value)
+            lv = self._host_value_from_python(host, arr, want)
+        if isinstance(plc, HostPlacement):
+            return lv
+        # constants on replicated / mirrored placements are public
+        if isinstance(plc, ReplicatedPlacement):
+            return LV(plc, lv.kind, lv.dtype, MV(plc, lv.v.v))
+        return LV(plc, lv.kind, lv.dtype, MV(plc, lv.v.v))
+
+    def op_Output(self, op, ins):
+        x = ins[0]
+        plc = op.placement
+        if isinstance(plc, HostPlacement):
+            x = self.to_host(x, plc.owner)
+        self.outputs[op.attrs.get("tag") or op.name] = x
+        return x
+
+    def op_Identity(self, op, ins):
+        return self.at(op, ins[0])
+
+    def op_Save(self, op, ins):
+        key, val = ins
+        host = op.placement.owner
+        val = self.to_host(val, host)
+        k = self._plain(key)
+        if self.sess.materialized(val.v):
+            self.storage.setdefault(host, {})[k] = self.to_numpy(val)
+        return LV(op.placement, "unit", None, HV(host, None))
+
+    def op_Load(self, op, ins):
+        key, query = ins
+        host = op.placement.owner
+        k = self._plain(key)
+        store = self.storage.get(host, {})
+        if k not in store:
+            from moose_amd.utils import storage as st
+
+            value = st.load_from_path(k, self._plain(query)) if st.looks_like_path(k) else None
+            if value is None:
+                raise MooseRuntimeError(f"key {k!r} not found in storage of {host}")
+        else:
+            value = store[k]
+        return self._host_value_from_python(host, value, op.sig.ret)
+
+    # ------------------------------------------------------------------------
+    # materialisation
+    # ------------------------------------------------------------------------
+    def to_numpy(self, x: LV):
+        v = self._plain(x)
+        if x.kind != "tensor":
+            return v
+        if isinstance(v, R.RT):
+            if x.dtype is not None and x.dtype.is_fixed:
+                return R.decode(v, x.dtype.fractional_precision).cpu().numpy()
+            return R.to_ints(v)
+        t = v.detach().cpu()
+        if x.dtype is not None and x.dtype.kind == "Uint64":
+            return t.numpy().view(np.uint64)
+        return t.numpy()
+
+    # ------------------------------------------------------------------------
+    # casts
+    # ------------------------------------------------------------------------
+    def _cast_host(self, x: LV, target: T.TensorDType) -> LV:
+        sess, host = self.sess, x.host
+        src = x.dtype
+        if src == target:
+            return x
+        if target.is_fixed:
+            bits = target.ring_bits
+            if src.is_fixed:
+                v = x.v
+                df = target.fractional_precision - src.fractional_precision
+                if src.ring_bits != bits:
+                    v = sess.h("RingCast", host, v, bits=bits)
+                if df > 0:
+                    v = sess.h("Shl", host, v, amount=df)
+                elif df < 0:
+                    v = sess.h("Sar", host, v, amount=-df)
+                return LV(x.plc, "tensor", target, v)
+            f = sess.h("Cast", host, x.v, dtype=torch.float64)
+            return LV(x.plc, "tensor", target,
+                      sess.h("RingFixedpointEncode", host, f,
+                             scaling_exp=target.fractional_precision, bits=bits))
+        if src is not None and src.is_fixed:
+            f = sess.h("RingFixedpointDecode", host, x.v, scaling_exp=src.fractional_precision)
+            if target.kind == "Float64":
+                return LV(x.plc, "tensor", target, f)
+            x = LV(x.plc, "tensor", T.FLOAT64, f)
+            src = T.FLOAT64
+        if src is None:  # raw ring tensor
+            raise MooseRuntimeError("cannot cast a raw ring tensor")
+        return LV(x.plc, "tensor", target, sess.h("Cast", host, x.v, dtype=torch_dtype_of(target)))
+
+    def op_Cast(self, op, ins):
+        target = self._ret_dtype(op)
+        x = self.at(op, ins[0])
+        if x.is_host:
+            return self._cast_host(x, target)
+        if x.is_rep and isinstance(x.v, MV):
+            h = self._cast_host(LV(HostPlacement(op.placement.owners[0]), x.kind, x.dtype,
+                                   HV(op.placement.owners[0], x.v.v)), target)
+            return LV(x.plc, "tensor", target, MV(x.plc, h.v.v))
+        if x.is_rep:
+            src = x.dtype
+            if src.is_fixed and target.is_fixed:
+                return LV(x.plc, "tensor", target, fxp.cast(self.sess, x.v, target))
+            if src.kind == "Bool" and target.is_fixed:
+                t = rep.b2a(self.sess, x.v, target.ring_bits)
+                f = target.fractional_precision
+                t = rep.shl(self.sess, t, f) if f else t
+                return LV(x.plc, "tensor", target,
+                          RepFixed(t, f, target.integral_precision))
+            raise MooseRuntimeError(f"replicated cast {src} -> {target} not supported")
+        if x.is_mir:
+            h = self._cast_host(LV(HostPlacement(x.plc.owners[0]), x.kind, x.dtype,
+                                   HV(x.plc.owners[0], x.v.v)), target)
+            return LV(x.plc, "tensor", target, MV(x.plc, h.v.v))
+        raise MooseRuntimeError("bad cast")
+
+    # ------------------------------------------------------------------------
+    # arithmetic
+    # ------------------------------------------------------------------------
+    def _binary(self, op, ins, kind):
+        x, y = (self.at(op, v) for v in ins)
+        if x.kind != "tensor" or y.kind != "tensor":
+            return self._scalar_binary(op, x, y, kind)
+        dtype = x.dtype if x.dtype is not None else y.dtype
+        if x.is_host:
+            return self._host_binary(op, x, y, kind, dtype)
+        if x.is_mir:
+            return self._mir_binary(op, x, y, kind, dtype)
+        return self._rep_binary(op, x, y, kind, dtype)
+
+    def _scalar_binary(self, op, x, y, kind):
+        a, b = self._plain(x), self._plain(y)
+        f = {"Add": lambda: a + b, "Sub": lambda: a - b, "Mul": lambda: a * b,
+             "Div": lambda: a / b}[kind]
+        return LV(x.plc, x.kind, None, HV(getattr(x.plc, "owner", None), f()))
+
+    def _host_binary(self, op, x, y, kind, dtype):
+        sess, host = self.sess, x.host
+        if dtype.is_fixed:
+            f = dtype.fractional_precision
+            if kind in ("Add", "Sub"):
+                return LV(x.plc, "tensor", dtype, sess.h(kind, host, x.v, y.v))
+            if kind in ("Mul", "Dot"):
+                z = sess.h(kind, host, x.v, y.v)
+                return LV(x.plc, "tensor", dtype, sess.h("Sar", host, z, amount=f))
+            if kind == "Div":
+                xf = sess.h("RingFixedpointDecode", host, x.v, scaling_exp=f)
+                yf = sess.h("RingFixedpointDecode", host, y.v, scaling_exp=f)
+                q = sess.h("Div", host, xf, yf)
+                return LV(x.plc, "tensor", dtype, sess.h("RingFixedpointEncode", host, q,
+                                                         scaling_exp=f, bits=dtype.ring_bits))
+        if kind in ("Less", "Greater"):
+            return LV(x.plc, "tensor", T.BOOL, sess.h(kind, host, x.v, y.v))
+        if kind in ("And", "Or"):
+            return LV(x.plc, "tensor", dtype, sess.h(kind, host, x.v, y.v))
+        return LV(x.plc, "tensor", dtype, sess.h(kind, host, x.v, y.v))
+
+    def _mir_binary(self, op, x, y, kind, dtype):
+        hx = LV(HostPlacement(x.plc.owners[0]), "tensor", x.dtype, HV(x.plc.owners[0], x.v.v))
+        hy = LV(HostPlacement(x.plc.owners[0]), "tensor", y.dtype, HV(x.plc.owners[0], y.v.v))
+        r = self._host_binary(op, hx, hy, kind, dtype)
+        return LV(x.plc, "tensor", r.dtype, MV(x.plc, r.v.v))
+
+    def _rep_binary(self, op, x, y, kind, dtype):
+        sess = self.sess
+        px, py = self._public(x), self._public(y)
+        if px is not None and py is not None:
+            h = self._mir_binary(op, LV(x.plc, "tensor", x.dtype, MV(x.plc, px)),
+                                 LV(x.plc, "tensor", y.dtype, MV(x.plc, py)), kind, dtype)
+            return LV(x.plc, "tensor", h.dtype, MV(x.plc, h.v.v))
+        if kind in ("Less", "Greater"):
+            a, b = x, y
+            return LV(x.plc, "tensor", T.BOOL, fxp.compare(sess, kind, a.v, b.v, px, py))
+        if kind in ("And", "Or"):
+            if px is not None or py is not None:
+                raise MooseRuntimeError("boolean ops with public operands not supported")
+            if kind == "And":
+                return LV(x.plc, "tensor", T.BOOL, rep.and_(sess, x.v, y.v))
+            # a | b = a ^ b ^ (a & b)
+            return LV(x.plc, "tensor", T.BOOL,
+                      rep.xor(sess, rep.xor(sess, x.v, y.v), rep.and_(sess, x.v, y.v)))
+        if dtype.kind == "Uint64":
+            return LV(x.plc, "tensor", dtype, fxp.ring_binary(sess, kind, x.v, y.v, px, py))
+        if not dtype.is_fixed:
+            raise MooseRuntimeError(f"replicated {kind} on {dtype}")
+        f = dtype.fractional_precision
+        if kind == "Add":
+            r = fxp.add(sess, x.v, y.v, px, py)
+        elif kind == "Sub":
+            r = fxp.sub(sess, x.v, y.v, px, py)
+        elif kind == "Mul":
+            r = fxp.mul(sess, x.v, y.v, px, py, f)
+        elif kind == "Dot":
+            r = fxp.dot(sess, x.v, y.v, px, py, f)
+        elif kind == "Div":
+            r = fxp.div(sess, x.v, y.v, px, py)
+        else:
+            raise MooseRuntimeError(kind)
+        return LV(x.plc, "tensor", dtype, r)
+
+    def op_Add(self, op, ins):
+        return self._binary(op, ins, "Add")
+
+    def op_Sub(self, op, ins):
+        return self._binary(op, ins, "Sub")
+
+    def op_Mul(self, op, ins):
+        return self._binary(op, ins, "Mul")
+
+    def op_Dot(self, op, ins):
+        return self._binary(op, ins, "Dot")
+
+    def op_Div(self, op, ins):
+        return self._binary(op, ins, "Div")
+
+    def op_Less(self, op, ins):
+        return self._binary(op, ins, "Less")
+
+    def op_Greater(self, op, ins):
+        return self._binary(op, ins, "Greater")
+
+    def op_And(self, op, ins):
+        return self._binary(op, ins, "And")
+
+    def op_Or(self, op, ins):
+        return self._binary(op, ins, "Or")
+
+    def op_AddN(self, op, ins):
+        acc = ins[0]
+        for x in ins[1:]:
+            acc = self._binary(op, [acc, x], "Add")
+        return acc
+
+    # ------------------------------------------------------------------------
+    # unary math
+    # ------------------------------------------------------------------------
+    def _host_float_unary(self, op, x, prim, **attrs):
+        """Host math; fixed-point host tensors go through float64."""
+        sess, host = self.sess, x.host
+        d = x.dtype
+        if d is not None and d.is_fixed:
+            f = sess.h("RingFixedpointDecode", host, x.v, scaling_exp=d.fractional_precision)
+            r = sess.h(prim, host, f, **attrs)
+            if prim == "Argmax":
+                return LV(x.plc, "tensor", T.UINT64, r)
+            return LV(x.plc, "tensor", d, sess.h("RingFixedpointEncode", host, r,
+                                                 scaling_exp=d.fractional_precision,
+                                                 bits=d.ring_bits))
+        r = sess.h(prim, host, x.v, **attrs)
+        return LV(x.plc, "tensor", T.UINT64 if prim == "Argmax" else d, r)
+
+    def _unary(self, op, ins, prim, rep_fn, **attrs):
+        x = self.at(op, ins[0])
+        if x.is_host:
+            return self._host_float_unary(op, x, prim, **attrs)
+        if x.is_mir or (x.is_rep and isinstance(x.v, MV)):
+            h = self._host_float_unary(op, LV(HostPlacement(x.plc.owners[0]), x.kind, x.dtype,
+                                              HV(x.plc.owners[0], x.v.v)), prim, **attrs)
+            return LV(x.plc, "tensor", h.dtype, MV(x.plc, h.v.v))
+        return rep_fn(x)
+
+    def _rep_fixed_unary(self, fn, out_dtype=None):
+        def apply(x):
+            if not x.dtype.is_fixed:
+                raise MooseRuntimeError(f"{fn.__name__} expects a fixed-point tensor, got {x.dtype}")
+            return LV(x.plc, "tensor", out_dtype or x.dtype, fn(self.sess, x.v))
+
+        return apply
+
+    def op_Exp(self, op, ins):
+        return self._unary(op, ins, "Exp", self._rep_fixed_unary(fxp.exp))
+
+    def op_Log(self, op, ins):
+        return self._unary(op, ins, "Log", self._rep_fixed_unary(fxp.log))
+
+    def op_Log2(self, op, ins):
+        return self._unary(op, ins, "Log2", self._rep_fixed_unary(fxp.log2))
+
+    def op_Sqrt(self, op, ins):
+        return self._unary(op, ins, "Sqrt", self._rep_fixed_unary(fxp.sqrt))
+
+    def op_Sigmoid(self, op, ins):
+        return self._unary(op, ins, "Sigmoid", self._rep_fixed_unary(fxp.sigmoid))
+
+    def op_Relu(self, op, ins):
+        return self._unary(op, ins, "Relu", self._rep_fixed_unary(fxp.relu))
+
+    def op_Abs(self, op, ins):
+        return self._unary(op, ins, "Abs", self._rep_fixed_unary(fxp.abs_))
+
+    def op_Neg(self, op, ins):
+        return self._unary(op, ins, "Neg", self._rep_fixed_unary(fxp.neg))
+
+    def op_Softmax(self, op, ins):
+        ax, up = op.attrs["axis"], op.attrs["upmost_index"]
+        return self._unary(op, ins, "Softmax",
+                           self._rep_fixed_unary(lambda s, v: fxp.softmax(s, v, ax, up)),
+                           axis=ax, upmost_index=up)
+
+    def op_Argmax(self, op, ins):
+        ax, up = op.attrs["axis"], op.attrs["upmost_index"]
+
+        def rep_fn(x):
+            return LV(x.plc, "tensor", T.UINT64, fxp.argmax(self.sess, x.v, ax, up))
+
+        return self._unary(op, ins, "Argmax", rep_fn, axis=ax, upmost_index=up)
+
+    def op_Maximum(self, op, ins):
+        xs = [self.at(op, v) for v in ins]
+        if xs[0].is_host:
+            r = self.sess.h("Maximum", xs[0].host, *[x.v for x in xs])
+            return LV(xs[0].plc, "tensor", xs[0].dtype, r)
+        return LV(xs[0].plc, "tensor", xs[0].dtype, fxp.maximum(self.sess, [x.v for x in xs]))
+
+    def op_Inverse(self, op, ins):
+        x = self.at(op, ins[0])
+        if not x.is_host:
+            raise MooseRuntimeError("Inverse is only supported on host placements")
+        return self._host_float_unary(op, x, "Inverse")
+
+    def op_Mux(self, op, ins):
+        s, x, y = (self.at(op, v) for v in ins)
+        if s.is_host:
+            return LV(s.plc, "tensor", x.dtype, self.sess.h("Mux", s.host, s.v, x.v, y.v))
+        return LV(s.plc, "tensor", x.dtype, fxp.mux(self.sess, s.v, x.v, y.v))
+
+    # ------------------------------------------------------------------------
+    # reductions
+    # ------------------------------------------------------------------------
+    def op_Sum(self, op, ins):
+        x = self.at(op, ins[0])
+        axis = op.attrs.get("axis")
+        if x.is_host:
+            return LV(x.plc, "tensor", x.dtype, self.sess.h("Sum", x.host, x.v, axis=axis))
+        if isinstance(x.v, MV):
+            return self._public_prim(x, "Sum", axis=axis)
+        return LV(x.plc, "tensor", x.dtype, fxp.local(self.sess, x.v, "Sum", axis=axis))
+
+    def op_Mean(self, op, ins):
+        x = self.at(op, ins[0])
+        axis = op.attrs.get("axis")
+        if x.is_host:
+            if x.dtype is not None and x.dtype.is_fixed:
+                return self._host_float_unary(op, x, "Mean", axis=axis)
+            return LV(x.plc, "tensor", x.dtype, self.sess.h("Mean", x.host, x.v, axis=axis))
+        return LV(x.plc, "tensor", x.dtype, fxp.mean(self.sess, x.v, axis))
+
+    # ------------------------------------------------------------------------
+    # shape ops (share-wise on replicated values)
+    # ------------------------------------------------------------------------
+    def _public_prim(self, x, prim, *extra, **attrs):
+        r = self.sess.h(prim, x.plc.owners[0], HV(x.plc.owners[0], x.v.v), *extra, **attrs)
+        return LV(x.plc, x.kind, x.dtype, MV(x.plc, r.v))
+
+    def _shape_op(self, op, x, prim, *extra, **attrs):
+        x = self.at(op, x)
+        if x.kind == "shape":
+            return x
+        if x.is_host:
+            return LV(x.plc, "tensor", x.dtype, self.sess.h(prim, x.host, x.v, *extra, **attrs))
+        if isinstance(x.v, MV):
+            return self._public_prim(x, prim, *extra, **attrs)
+        return LV(x.plc, "tensor", x.dtype, fxp.local(self.sess, x.v, prim, *extra, **attrs))
+
+    def op_Transpose(self, op, ins):
+        return self._shape_op(op, ins[0], "Transpose")
+
+    def op_ExpandDims(self, op, ins):
+        return self._shape_op(op, ins[0], "ExpandDims", axis=op.attrs["axis"])
+
+    def op_Squeeze(self, op, ins):
+        return self._shape_op(op, ins[0], "Squeeze", axis=op.attrs.get("axis"))
+
+    def op_IndexAxis(self, op, ins):
+        return self._shape_op(op, ins[0], "IndexAxis", axis=op.attrs["axis"],
+                              index=op.attrs["index"])
+
+    def op_AtLeast2D(self, op, ins):
+        return self._shape_op(op, ins[0], "AtLeast2D",
+                              to_column_vector=op.attrs["to_column_vector"])
+
+    def op_Diag(self, op, ins):
+        return self._shape_op(op, ins[0], "Diag")
+
+    def op_Reshape(self, op, ins):
+        shape = tuple(self._plain(ins[1]))
+        return self._shape_op(op, ins[0], "Reshape", shape=shape)
+
+    def op_Broadcast(self, op, ins):
+        shape = tuple(self._plain(ins[1]))
+        return self._shape_op(op, ins[0], "Broadcast", shape=shape)
+
+    def op_Slice(self, op, ins):
+        x = ins[0]
+        sl = op.attrs["slice"]
+        if x.kind == "shape":
+            start, end, step = sl[0] if isinstance(sl, list) else sl
+            v = tuple(self._plain(x))[start:end:step]
+            return LV(x.plc if isinstance(op.placement, HostPlacement) else op.placement,
+                      "shape", None, HV(getattr(op.placement, "owner", None), v)
+                      if isinstance(op.placement, HostPlacement) else v)
+        slices = sl if isinstance(sl, list) else [sl]
+        py = [slice(a, b, c) for (a, b, c) in slices]
+        return self._shape_op(op, x, "StridedSlice", slices=py)
+
+    def op_Select(self, op, ins):
+        mask = self.to_host(ins[1], self._some_host(op)) if not ins[1].is_host else ins[1]
+        m = self._plain(mask)
+        return self._shape_op(op, ins[0], "Select", m, axis=op.attrs["axis"])
+
+    def _some_host(self, op):
+        plc = op.placement
+        return plc.owner if isinstance(plc, HostPlacement) else plc.owners[0]
+
+    def op_Concat(self, op, ins):
+        xs = [self.at(op, v) for v in ins]
+        axis = op.attrs["axis"]
+        x0 = xs[0]
+        if x0.is_host:
+            return LV(x0.plc, "tensor", x0.dtype,
+                      self.sess.h("Concat", x0.host, *[x.v for x in xs], axis=axis))
+        if all(isinstance(x.v, MV) for x in xs):
+            r = self.sess.h("Concat", x0.plc.owners[0], *[HV(x0.plc.owners[0], x.v.v) for x in xs],
+                            axis=axis)
+            return LV(x0.plc, "tensor", x0.dtype, MV(x0.plc, r.v))
+        xs = [x if not isinstance(x.v, MV) else self._share_public(x) for x in xs]
+        return LV(x0.plc, "tensor", x0.dtype, fxp.concat(self.sess, [x.v for x in xs], axis))
+
+    def _share_public(self, x: LV) -> LV:
+        d = x.dtype
+        bits = d.ring_bits if d.is_fixed else 64
+        t = rep.from_public(self.sess, x.plc, x.v.v, bits)
+        if d.is_fixed:
+            return LV(x.plc, "tensor", d, RepFixed(t, d.fractional_precision, d.integral_precision))
+        return LV(x.plc, "tensor", d, t)
+
+    def op_Shape(self, op, ins):
+        x = ins[0]
+        plc = op.placement
+        if isinstance(plc, HostPlacement):
+            x = self.to_host(x, plc.owner) if x.is_host else x
+            if x.is_host:
+                return LV(plc, "shape", None, self.sess.h("Shape", plc.owner, x.v))
+        return LV(plc, "shape", None, fxp.shape_of(self.sess, x.v))
+
+    def _fill(self, op, ins, value):
+        shape = tuple(self._plain(ins[0]))
+        d = self._ret_dtype(op)
+        plc = op.placement
+        host = self._some_host(op)
+        if d.is_fixed:
+            v = R.fill(shape, value << d.fractional_precision, d.ring_bits, self.sess.device)
+        else:
+            v = torch.full(shape, value, dtype=torch_dtype_of(d), device=self.sess.device)
+        if isinstance(plc, HostPlacement):
+            return LV(plc, "tensor", d, HV(host, v))
+        return LV(plc, "tensor", d, MV(plc, v))
+
+    def op_Ones(self, op, ins):
+        return self._fill(op, ins, 1)
+
+    def op_Zeros(self, op, ins):
+        return self._fill(op, ins, 0)
+
+    def op_Decrypt(self, op, ins):
+        from moose_amd.protocols import aes
+
+        key, ct = ins
+        return aes.decrypt_logical(self, op, key, ct)

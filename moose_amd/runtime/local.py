@@ -1,0 +1,142 @@
+"""``LocalMooseRuntime``: all identities simulated in one process on one device.
+
+Parity: reference ``pymoose/pymoose/runtime.py:14-70`` + ``pymoose/src/bindings.rs:137-250``
+(``AsyncTestRuntime``, ``execution/asynchronous.rs:634-773``).  Here the three parties of
+each replicated placement are stacked on one device (an MI355X when available, else the
+CPU), so every protocol step is one kernel launch for all parties.
+"""
+from __future__ import annotations
+
+import os
+import time
+from typing import Dict
+from typing import List
+from typing import Optional
+
+import numpy as np
+import torch
+
+from moose_amd.computation import computation as ecomp
+from moose_amd.ir.computation import Computation
+from moose_amd.runtime.interpreter import Interpreter
+from moose_amd.runtime.session import StackedSession
+
+
+def default_device():
+    dev = os.environ.get("MOOSEX_DEVICE")
+    if dev:
+        return dev
+    return "cuda" if torch.cuda.is_available() else "cpu"
+
+
+def to_native(computation, fixedpoint_ring=128) -> Computation:
+    """Accept an AbstractComputation, an eDSL Computation, a native Computation, a
+    MooseComputation, or serialized bytes; return a native-IR Computation."""
+    from moose_amd.compiler.from_edsl import convert
+    from moose_amd.edsl import base as edsl
+    from moose_amd.edsl import tracer
+
+    if isinstance(computation, Computation):
+        return computation
+    if hasattr(computation, "native"):  # MooseComputation
+        return computation.native
+    if isinstance(computation, edsl.AbstractComputation):
+        computation = tracer.trace(computation)
+    if isinstance(computation, (bytes, bytearray)):
+        from moose_amd.computation import utils
+
+        try:
+            return Computation.from_msgpack(bytes(computation))
+        except Exception:
+            computation = utils.deserialize_computation(bytes(computation))
+    if isinstance(computation, ecomp.Computation):
+        return convert(computation, fixedpoint_ring)
+    raise ValueError(f"cannot evaluate object of type {type(computation)}")
+
+
+class LocalMooseRuntime:
+    """Locally simulated runtime with optional per-identity storage."""
+
+    def __init__(
+        self,
+        identities: List[str],
+        storage_mapping: Optional[Dict[str, Dict]] = None,
+        device=None,
+        fixedpoint_ring: int = 128,
+        seed: Optional[int] = None,
+    ):
+        identities = [getattr(i, "name", i) for i in identities]
+        storage_mapping = dict(storage_mapping or {})
+        for ident in storage_mapping:
+            if ident not in identities:
+                raise ValueError(
+                    f"Found unknown identity {ident} in `storage_mapping` arg, "
+                    f"must be one of {identities}."
+                )
+        self.identities = identities
+        self.storage = {i: dict(storage_mapping.get(i, {})) for i in identities}
+        self.device = torch.device(device or default_device())
+        self.fixedpoint_ring = fixedpoint_ring
+        self.seed = seed
+        self.last_stats = None
+        self.last_timings = None
+
+    def set_default(self):
+        from moose_amd.edsl.base import set_current_runtime
+
+        set_current_runtime(self)
+
+    # ------------------------------------------------------------------
+    def evaluate_computation(self, computation, arguments=None, compiler_passes=None):
+        comp = to_native(computation, self.fixedpoint_ring)
+        if compiler_passes:
+            from moose_amd.compiler import passes
+
+            comp = passes.compile(comp, compiler_passes)
+        return self.evaluate_compiled(comp, arguments)
+
+    def evaluate_compiled(self, comp, arguments=None):
+        comp = to_native(comp, self.fixedpoint_ring)
+        arguments = dict(arguments or {})
+        if _is_lowered(comp):
+            from moose_amd.runtime.graph_executor import GraphExecutor
+
+            ex = GraphExecutor(self.device, self.storage)
+            t0 = time.perf_counter()
+            outs = ex.run(comp, arguments)
+            self.last_timings = {i: int((time.perf_counter() - t0) * 1e6) for i in self.identities}
+            return outs
+        sess = StackedSession(self.device, seed=self.seed)
+        interp = Interpreter(sess, self.storage, self.fixedpoint_ring)
+        t0 = time.perf_counter()
+        outs = interp.run(comp, arguments)
+        result = {}
+        for tag, lv in outs.items():
+            if lv.kind == "unit":
+                continue
+            result[tag] = interp.to_numpy(lv)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        elapsed = int((time.perf_counter() - t0) * 1e6)
+        self.last_timings = {i: elapsed for i in self.identities}
+        self.last_stats = sess.stats
+        return result
+
+    def read_value_from_storage(self, identity, key):
+        if identity not in self.storage:
+            raise RuntimeError(f"unknown identity {identity}")
+        return self.storage[identity][key]
+
+    def write_value_to_storage(self, identity, key, value):
+        if identity not in self.storage:
+            raise RuntimeError(f"unknown identity {identity}")
+        self.storage[identity][key] = np.asarray(value) if not isinstance(value, str) else value
+
+
+def _is_lowered(comp: Computation) -> bool:
+    """A computation is host-level when every op is on a host placement."""
+    from moose_amd.ir.computation import HostPlacement
+
+    return all(isinstance(op.placement, HostPlacement) for op in comp.operations) and any(
+        op.kind in ("Send", "Receive", "PrfKeyGen", "RingFixedpointEncode") for op in comp.operations
+    )

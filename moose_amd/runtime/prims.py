@@ -343,6 +343,52 @@ def _ring_cast(nb, x, bits):
     return R.cast(x, bits)
 
 
+@prim("BitSplit")
+def _bit_split(nb, x, start, count):
+    """Packed word -> bit tensor with a new logical leading axis: out[j] = bit start+j."""
+    d = x.data
+    outs = []
+    for j in range(start, start + count):
+        w = d if x.bits == 64 else d[..., j // 64]
+        outs.append(((w >> (j % 64)) & 1).to(torch.uint8))
+    return R.RT(torch.stack(outs, dim=nb), 1)
+
+
+@prim("WeightedSum")
+def _weighted_sum(nb, x, weights, bits):
+    """sum_j weights[j] * x[j] over the leading logical axis (public integer weights)."""
+    acc = None
+    for j, w in enumerate(weights):
+        if w == 0:
+            continue
+        xj = R.index_axis(x, 0, j, nb)
+        t = R.binary("mul", xj, R.fill((), int(w), bits, x.device))
+        acc = t if acc is None else R.binary("add", acc, t)
+    if acc is None:
+        return R.zeros(R.index_axis(x, 0, 0, nb).shape, bits, x.device)
+    return acc
+
+
+@prim("ToBool")
+def _to_bool(nb, x):
+    return x.data.to(torch.bool) if _is_rt(x) else x.to(torch.bool)
+
+
+@prim("FromBool")
+def _from_bool(nb, x):
+    return R.RT(x.to(torch.uint8), 1)
+
+
+@prim("RingToInt")
+def _ring_to_int(nb, x):
+    return R.cast(x, 64).data
+
+
+@prim("IntToRing")
+def _int_to_ring(nb, x):
+    return R.RT(x.to(torch.int64), 64)
+
+
 @prim("Less")
 def _less(nb, a, b):
     if _is_rt(a):

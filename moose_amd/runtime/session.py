@@ -237,6 +237,15 @@ class StackedSession(Session):
     def p_shape(self, x: PV):
         return tuple(x.v.shape[1:])
 
+    def mirror(self, x: HV, plc):
+        """Host value -> mirrored (public on the 3 hosts of ``plc``)."""
+        from moose_amd.runtime.values import MV
+
+        for o in plc.owners:
+            if o != x.host:
+                self.stats.record_send(x.host, o, _nbytes(x.v))
+        return MV(plc, x.v)
+
     def materialized(self, x) -> bool:
         return True
 
