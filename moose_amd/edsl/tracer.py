@@ -63,11 +63,27 @@ _OPS = {
 }
 
 
+def _resolve_annotation(func, ann):
+    """Evaluate string annotations (``from __future__ import annotations``) in the
+    function's globals plus its closure."""
+    if not isinstance(ann, str):
+        return ann
+    scope = dict(func.__globals__)
+    if func.__closure__:
+        for name, cell in zip(func.__code__.co_freevars, func.__closure__):
+            try:
+                scope[name] = cell.cell_contents
+            except ValueError:
+                pass
+    return eval(ann, scope)  # noqa: S307 - annotations are user code
+
+
 def trace(abstract_computation):
-    params = inspect.signature(abstract_computation.func).parameters
+    func = abstract_computation.func
+    params = inspect.signature(func).parameters
     symbolic_args = []
     for arg_name, p in params.items():
-        ann = p.annotation
+        ann = _resolve_annotation(func, p.annotation)
         if not isinstance(ann, expr.Argument):
             raise TypeError(f"Parameter `{arg_name}` must be annotated with pm.Argument")
         symbolic_args.append(

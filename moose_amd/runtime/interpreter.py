@@ -220,9 +220,14 @@ class Interpreter:
         if isinstance(value, int) and not isinstance(value, bool):
             if want is None or want.name != "Tensor":
                 return LV(hp, "int", None, HV(host, value))
-        arr = np.asarray(value)
-        dtype = dtype_of_numpy(arr)
-        t = numpy_to_torch(arr, sess.device)
+        if isinstance(value, torch.Tensor):  # device-resident argument (no host copy)
+            t = value.to(sess.device)
+            dtype = {torch.float64: T.FLOAT64, torch.float32: T.FLOAT32,
+                     torch.bool: T.BOOL}.get(t.dtype, T.UINT64)
+        else:
+            arr = np.asarray(value)
+            dtype = dtype_of_numpy(arr)
+            t = numpy_to_torch(arr, sess.device)
         lv = LV(hp, "tensor", dtype, HV(host, t))
         if want is not None and want.name == "Tensor" and want.dtype.kind not in ("Unknown",):
             wd = self._dtype(want.dtype)
@@ -270,6 +275,9 @@ class Interpreter:
         plc = op.placement
         if isinstance(plc, HostPlacement):
             x = self.to_host(x, plc.owner)
+        elif x.kind == "tensor":
+            # outputs pinned to a replicated / mirrored placement open to its first owner
+            x = self.to_host(x, plc.owners[0])
         self.outputs[op.attrs.get("tag") or op.name] = x
         return x
 
