@@ -429,7 +429,8 @@ def _exp2_parts(sess, a: RepFixed, negative: bool):
     """2^a (or 2^-a) for a >= 0: integer part from B2A'd bits (product tree of public
     factors), fraction via polynomial."""
     f, bits, integ = a.frac, a.bits, a.integ
-    nint = max(1, min(6, int(math.ceil(math.log2(max(2, integ + 1))))))
+    # every integer bit of a must be inspected (a < 2^(integ+1) after the log2(e) scale)
+    nint = max(1, min(bits - 2 - f, integ + 1))
     bd = rep.bit_decompose(sess, a.t)
     planes = RepTensor(a.plc, 1, "bool", sess.p("BitSplit", a.plc, bd.s0, start=0, count=f + nint),
                        sess.p("BitSplit", a.plc, bd.s1, start=0, count=f + nint))
@@ -446,7 +447,11 @@ def _exp2_parts(sess, a: RepFixed, negative: bool):
     factors = []
     for j in range(nint):
         bj = local(sess, ab, "IndexAxis", axis=0, index=f + j)
-        c = 2.0 ** (-(2 ** j) if negative else (2 ** j))
+        e = 2 ** j
+        if negative:
+            c = 2.0 ** (-e) if e <= f + 2 else 0.0  # underflows to 0 at precision f
+        else:
+            c = 2.0 ** min(e, integ + 1)  # saturate: larger results overflow anyway
         fac = rep.mul_public(sess, bj, _encode_const(sess, c - 1.0, f, bits))
         fac = rep.add_public(sess, fac, _encode_const(sess, 1.0, f, bits))
         factors.append(RepFixed(fac, f, integ))

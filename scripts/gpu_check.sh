@@ -1,12 +1,31 @@
 #!/bin/bash
 # One GPU-box session: tests, smoke, headline bench (both rings), kernel profile.
-set -o pipefail
+# A step that fails an assertion (rc 1) does not stop the session; a crash, abort,
+# fault or timeout (any other non-zero rc) ends it immediately.
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export PYTHONPATH=$PWD
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 && echo "pytest ok" \
-&& timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1 && echo "smoke ok" \
-&& timeout -k 10 600 python bench.py --steps 5 --warmup 2 --check > gpurun_out/bench128.log 2>&1 && cat gpurun_out/bench128.log \
-&& timeout -k 10 600 python bench.py --steps 5 --warmup 2 --ring 64 --check > gpurun_out/bench64.log 2>&1 && cat gpurun_out/bench64.log \
-&& cd /tmp && export TMPDIR=/tmp && cd - >/dev/null \
-&& timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 > gpurun_out/prof.log 2>&1 && echo "prof ok"
+
+run() {  # run <name> <timeout> <cmd...>
+  local name=$1 t=$2
+  shift 2
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  tail -3 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+    echo "stopping after $name (rc=$rc)"
+    exit $rc
+  fi
+}
+
+STEPS=${STEPS:-all}
+[[ $STEPS == *test* || $STEPS == all ]] && run pytest_gpu 900 python -m pytest tests -m gpu -x -q
+[[ $STEPS == *smoke* || $STEPS == all ]] && run smoke 300 python __graft_entry__.py smoke
+[[ $STEPS == *bench* || $STEPS == all ]] && run bench128 600 python bench.py --steps 5 --warmup 2 --check
+[[ $STEPS == *bench* || $STEPS == all ]] && run bench64 600 python bench.py --steps 5 --warmup 2 --ring 64 --check
+if [[ $STEPS == *prof* || $STEPS == all ]]; then
+  export TMPDIR=/tmp
+  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1
+fi
+exit 0
