@@ -1,0 +1,138 @@
+"""RSS protocols on the stacked 3-party session (all parties simulated in-process):
+share -> op -> reveal compared with plaintext (reference replicated/mod.rs:281-1360)."""
+import numpy as np
+import pytest
+import torch
+
+from moose_amd.ir.computation import ReplicatedPlacement
+from moose_amd.ops import ring as R
+from moose_amd.protocols import replicated as rep
+from moose_amd.runtime.session import HV
+from moose_amd.runtime.session import StackedSession
+
+PLC = ReplicatedPlacement(("alice", "bob", "carole"))
+F = 23
+
+
+def enc(x, bits, host="alice"):
+    return HV(host, R.encode(torch.as_tensor(x, dtype=torch.float64), F, bits))
+
+
+def dec(sess, t, frac=F, host="carole"):
+    return R.decode(rep.reveal(sess, t, host).v, frac)
+
+
+@pytest.fixture(params=[64, 128])
+def bits(request):
+    return request.param
+
+
+@pytest.fixture
+def sess():
+    return StackedSession("cpu", seed=42)
+
+
+def test_share_reveal_all_owners(sess, bits):
+    x = np.array([[1.5, -2.0], [0.0, 7.25]])
+    for owner in ("alice", "bob", "carole", "dave"):
+        X = rep.share(sess, PLC, enc(x, bits, owner))
+        for to in ("alice", "bob", "carole", "eve"):
+            np.testing.assert_allclose(dec(sess, X, host=to), x)
+
+
+def test_shares_look_random(sess, bits):
+    x = np.zeros((64,))
+    X = rep.share(sess, PLC, enc(x, bits))
+    s = R.to_ints(R.RT(X.s0.v.data[0], bits))
+    assert len(set(s.tolist())) > 60  # masked, not the encoded zeros
+
+
+def test_reshare_invariant(sess, bits):
+    x = np.array([3.0, -1.0])
+    X = rep.share(sess, PLC, enc(x, bits))
+    Y = rep.mul(sess, X, X)
+    # party p's second share equals party p+1's first share
+    assert torch.equal(Y.s1.v.data, torch.roll(Y.s0.v.data, -1, dims=0))
+
+
+def test_linear_ops(sess, bits):
+    x, y = np.array([1.0, -2.5, 3.0]), np.array([0.5, 4.0, -1.0])
+    X, Y = rep.share(sess, PLC, enc(x, bits)), rep.share(sess, PLC, enc(y, bits, "bob"))
+    np.testing.assert_allclose(dec(sess, rep.add(sess, X, Y)), x + y)
+    np.testing.assert_allclose(dec(sess, rep.sub(sess, X, Y)), x - y)
+    np.testing.assert_allclose(dec(sess, rep.neg(sess, X)), -x)
+    c = R.encode(torch.tensor([1.0, 1.0, 1.0], dtype=torch.float64), F, bits)
+    np.testing.assert_allclose(dec(sess, rep.add_public(sess, X, c)), x + 1)
+    np.testing.assert_allclose(dec(sess, rep.sub_public(sess, X, c)), x - 1)
+    np.testing.assert_allclose(dec(sess, rep.sum(sess, X, 0)), x.sum())
+
+
+def test_mul_dot_trunc(sess, bits):
+    rng = np.random.default_rng(0)
+    x, y = rng.uniform(-4, 4, (5, 7)), rng.uniform(-4, 4, (7, 3))
+    X, Y = rep.share(sess, PLC, enc(x, bits)), rep.share(sess, PLC, enc(y, bits, "bob"))
+    D = rep.dot(sess, X, Y)
+    np.testing.assert_allclose(dec(sess, D, 2 * F), x @ y, atol=1e-5)
+    T = rep.trunc_pr(sess, D, F)
+    np.testing.assert_allclose(dec(sess, T), x @ y, atol=1e-5)
+    XX = rep.mul(sess, X, X)
+    np.testing.assert_allclose(dec(sess, rep.trunc_pr(sess, XX, F)), x * x, atol=1e-5)
+
+
+def test_trunc_pr_error_bound(sess, bits):
+    x = np.linspace(-1000, 1000, 4001)
+    X = rep.share(sess, PLC, enc(x, bits))
+    T = rep.trunc_pr(sess, X, 10)
+    got = R.to_signed_ints(rep.reveal(sess, T, "alice").v).astype(np.float64)
+    want = np.floor(R.to_signed_ints(R.encode(torch.tensor(x), F, bits)).astype(np.float64) / 2**10)
+    assert np.abs(got - want).max() <= 1
+
+
+def test_bit_decompose(sess, bits):
+    vals = [0, 1, 5, 2**40 + 3, (-7) & ((1 << bits) - 1)]
+    X = rep.share(sess, PLC, HV("alice", R.from_ints(vals, bits)))
+    B = rep.bit_decompose(sess, X)
+    assert B.kind == "bool"
+    opened = R.to_ints(rep.reveal(sess, B, "bob").v)
+    assert list(opened) == vals
+
+
+def test_comparisons_and_mux(sess, bits):
+    x, y = np.array([1.5, -2.0, 3.0, -1.0]), np.array([-1.0, 4.0, 3.0, -0.5])
+    X, Y = rep.share(sess, PLC, enc(x, bits)), rep.share(sess, PLC, enc(y, bits, "bob"))
+    lt = rep.reveal(sess, rep.less(sess, X, Y), "alice").v.data.numpy()
+    gt = rep.reveal(sess, rep.greater(sess, X, Y), "alice").v.data.numpy()
+    eq = rep.reveal(sess, rep.equal(sess, X, Y), "alice").v.data.numpy()
+    np.testing.assert_array_equal(lt, (x < y).astype(np.uint8))
+    np.testing.assert_array_equal(gt, (x > y).astype(np.uint8))
+    np.testing.assert_array_equal(eq, (x == y).astype(np.uint8))
+    m = rep.mux(sess, rep.less(sess, X, Y), X, Y)
+    np.testing.assert_allclose(dec(sess, m), np.minimum(x, y))
+    np.testing.assert_allclose(dec(sess, rep.abs_(sess, X)), np.abs(x))
+    np.testing.assert_allclose(dec(sess, rep.relu(sess, X)), np.maximum(x, 0))
+
+
+def test_b2a(sess, bits):
+    b = np.array([1, 0, 1, 1, 0], dtype=np.uint8)
+    B = rep.share(sess, PLC, HV("alice", R.RT(torch.from_numpy(b), 1)), kind="bool")
+    A = rep.b2a(sess, B, bits)
+    assert list(R.to_ints(rep.reveal(sess, A, "carole").v)) == b.tolist()
+
+
+def test_boolean_and_xor(sess):
+    a = np.array([1, 0, 1, 0], dtype=np.uint8)
+    b = np.array([1, 1, 0, 0], dtype=np.uint8)
+    A = rep.share(sess, PLC, HV("alice", R.RT(torch.from_numpy(a), 1)), kind="bool")
+    B = rep.share(sess, PLC, HV("bob", R.RT(torch.from_numpy(b), 1)), kind="bool")
+    np.testing.assert_array_equal(rep.reveal(sess, rep.and_(sess, A, B), "carole").v.data.numpy(), a & b)
+    np.testing.assert_array_equal(rep.reveal(sess, rep.xor(sess, A, B), "carole").v.data.numpy(), a ^ b)
+
+
+def test_round_accounting(sess):
+    X = rep.share(sess, PLC, enc(np.ones(4), 128))
+    r0 = sess.stats.rounds
+    rep.mul(sess, X, X)
+    assert sess.stats.rounds - r0 == 1  # one reshare round
+    r0 = sess.stats.rounds
+    rep.dot(sess, rep.local(sess, X, "Reshape", shape=(2, 2)), rep.local(sess, X, "Reshape", shape=(2, 2)))
+    assert sess.stats.rounds - r0 == 1
