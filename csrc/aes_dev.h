@@ -1,0 +1,71 @@
+// Device-side AES-128-CTR helpers shared by the gfx950 translation units.
+//
+// Each block stages the T0 table and S-box into LDS (1.25 KB) once; T1..T3 are byte
+// rotations of T0.  A keystream block yields one u128, two u64 or sixteen bits.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include "aes_core.h"
+
+namespace mxd {
+
+static __constant__ uint8_t c_sbox[256] = MX_SBOX_INIT;
+
+struct RK {
+  uint32_t rk[44];
+};
+struct Keys4 {
+  uint32_t rk[4][44];
+};
+
+__device__ inline void stage_tables(uint32_t* T, uint8_t* Sb) {
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    uint8_t s = c_sbox[i];
+    Sb[i] = s;
+    T[i] = mx::t0_entry(s);
+  }
+  __syncthreads();
+}
+
+__device__ inline void aes_ctr(const uint32_t* rk, const uint32_t* T, const uint8_t* Sb,
+                               uint64_t nonce, uint64_t ctr, uint64_t* lo, uint64_t* hi) {
+  uint32_t w[4], o[4];
+  mx::ctr_block_words(nonce, ctr, w);
+  mx::encrypt_block_tt(rk, T, Sb, w[0], w[1], w[2], w[3], o);
+  mx::block_to_u64(o, lo, hi);
+}
+
+// elements of type T per AES block
+template <class T>
+struct Lane {
+  static constexpr int kPer = 16 / (int)sizeof(T);
+};
+
+template <class T>
+__device__ inline T pick(uint64_t lo, uint64_t hi, int j) {
+  if constexpr (sizeof(T) == 16) {
+    return ((T)hi << 64) | (T)lo;
+  } else if constexpr (sizeof(T) == 8) {
+    return j == 0 ? lo : hi;
+  } else {
+    uint64_t w = j < 8 ? lo : hi;
+    return (T)((w >> (8 * (j & 7))) & 1);
+  }
+}
+
+inline Keys4 load_keys(const uint8_t* keys16, int nkeys) {
+  Keys4 k;
+  memset(&k, 0, sizeof(k));
+  for (int i = 0; i < nkeys && i < 4; ++i) mx::expand_key(keys16 + 16 * i, k.rk[i]);
+  return k;
+}
+
+inline int grid_for(int64_t n, int block = 256) {
+  int64_t blocks = (n + block - 1) / block;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 256 * 8) blocks = 256 * 8;
+  return (int)blocks;
+}
+
+}  // namespace mxd

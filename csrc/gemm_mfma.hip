@@ -192,8 +192,8 @@ __global__ void __launch_bounds__(256, 1)
   constexpr int L = Limbs<T>::L;
   constexpr int STAGE = L * kTileBytes;  // bytes per operand per k-step
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
-  int8_t* As = smem;
-  int8_t* Bs = smem + STAGE;
+  // two LDS buffers, each holding the A and B stage of one k-step
+  int8_t* buf[2] = {smem, smem + 2 * STAGE};
 
   const int64_t tiles_n = Np / TN, tiles_m = Mp / TM;
   const int64_t ntiles = tiles_n * tiles_m;
@@ -218,28 +218,36 @@ __global__ void __launch_bounds__(256, 1)
 
   constexpr int PER_THREAD = STAGE / (256 * 16);  // 16-byte chunks per thread per operand
   v4i pa[PER_THREAD], pb[PER_THREAD];
-#pragma unroll
-  for (int c = 0; c < PER_THREAD; ++c) {
-    pa[c] = *(const v4i*)(ga + (c * 256 + threadIdx.x) * 16);
-    pb[c] = *(const v4i*)(gb + (c * 256 + threadIdx.x) * 16);
-  }
-  for (int64_t kb = 0; kb < nkb; ++kb) {
+  auto load_stage = [&](int64_t kb) {
+    const int8_t* na = ga + kb * STAGE;
+    const int8_t* nb = gb + kb * STAGE;
 #pragma unroll
     for (int c = 0; c < PER_THREAD; ++c) {
-      *(v4i*)(As + (c * 256 + threadIdx.x) * 16) = pa[c];
-      *(v4i*)(Bs + (c * 256 + threadIdx.x) * 16) = pb[c];
+      pa[c] = *(const v4i*)(na + (c * 256 + threadIdx.x) * 16);
+      pb[c] = *(const v4i*)(nb + (c * 256 + threadIdx.x) * 16);
     }
-    __syncthreads();
-    if (kb + 1 < nkb) {
-      const int8_t* na = ga + (kb + 1) * STAGE;
-      const int8_t* nb = gb + (kb + 1) * STAGE;
+  };
+  auto store_stage = [&](int8_t* dst) {
 #pragma unroll
-      for (int c = 0; c < PER_THREAD; ++c) {
-        pa[c] = *(const v4i*)(na + (c * 256 + threadIdx.x) * 16);
-        pb[c] = *(const v4i*)(nb + (c * 256 + threadIdx.x) * 16);
-      }
+    for (int c = 0; c < PER_THREAD; ++c) {
+      *(v4i*)(dst + (c * 256 + threadIdx.x) * 16) = pa[c];
+      *(v4i*)(dst + STAGE + (c * 256 + threadIdx.x) * 16) = pb[c];
     }
-    mfma_diagonals<L>(As, Bs, arow, brow, half, acc);
+  };
+  // software pipeline: LDS double buffer + one k-step of register prefetch; one barrier
+  // per k-step.  Stage kb+1 is written to the idle buffer after computing stage kb, and
+  // the global loads of stage kb+2 are in flight during the next compute phase.
+  load_stage(0);
+  store_stage(buf[0]);
+  __syncthreads();
+  if (nkb > 1) load_stage(1);
+  for (int64_t kb = 0; kb < nkb; ++kb) {
+    const int cur = (int)(kb & 1);
+    mfma_diagonals<L>(buf[cur], buf[cur] + STAGE, arow, brow, half, acc);
+    if (kb + 1 < nkb) {
+      store_stage(buf[cur ^ 1]);
+      if (kb + 2 < nkb) load_stage(kb + 2);
+    }
     __syncthreads();
   }
 
@@ -348,7 +356,13 @@ int run(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T* A1
     }
     {
       const int64_t ntiles = (p.Mp / TM) * (p.Np / TN);
-      const size_t lds = 2 * (size_t)L * kTileBytes;
+      const size_t lds = 4 * (size_t)L * kTileBytes;  // 2 buffers x (A + B) stages
+      static bool attr_set = false;
+      if (!attr_set) {
+        hipFuncSetAttribute((const void*)k_gemm_limb<T>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr_set = true;
+      }
       hipLaunchKernelGGL(k_gemm_limb<T>, dim3((unsigned)ntiles, (unsigned)batch), dim3(256),
                          lds, st, la, lb, C, M, N, p.Mp, p.Np, p.Kp, accumulate);
     }

@@ -90,6 +90,16 @@ int mx_gemm_ws(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const 
 // select the GEMM kernel: 0 = auto, 1 = force VALU reference kernel, 2 = force MFMA
 void mx_set_gemm_impl(int impl);
 
+// Fused stacked-session protocols (rss_fused.h).  s0/out0/out1 are [3, n] slot
+// vectors (party p holds out0[p] = z_p and out1[p] = z_{p+1}).
+// trunc_pr3 nonces: r0, r1, r_top, r_msb, z0, z2 (dealer keys k0, k2).
+int mx_trunc_pr3(int dev, int words, const void* s0, void* out0, void* out1, int64_t n, int m,
+                 const uint8_t* k0, const uint8_t* k2, const uint64_t* nonces, void* stream);
+// share3: owner party j; slot_{j+1} = PRF(k_next, n1), slot_{j+2} = PRF(k_all, na).
+int mx_share3(int dev, int kind, int words, const void* x, void* out0, void* out1, int64_t n,
+              int j, const uint8_t* k_next, const uint8_t* k_all, uint64_t n1, uint64_t na,
+              void* stream);
+
 #ifdef __cplusplus
 }
 #endif

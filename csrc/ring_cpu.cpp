@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <functional>
 #include <thread>
 #include <vector>
 
@@ -300,6 +301,20 @@ int gemm_t(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T*
 }
 
 }  // namespace
+
+// host PRF expansion used by the fused host kernels (rss_fused_cpu.cpp)
+void mx_cpu_prf_range(const uint8_t* key, uint64_t nonce, int words, int64_t i0, int64_t n,
+                      void* out) {
+  Prf p(key);
+  if (words == 0) prf_elements<uint8_t>(p, nonce, i0, n, (uint8_t*)out);
+  if (words == 1) prf_elements<u64>(p, nonce, i0, n, (u64*)out);
+  if (words == 2) prf_elements<u128>(p, nonce, i0, n, (u128*)out);
+}
+
+void mx_cpu_parallel_for(int64_t n, int64_t grain,
+                         const std::function<void(int64_t, int64_t)>& f) {
+  parallel_for(n, grain, f);
+}
 
 // ---------------------------------------------------------------------------
 // C ABI (host side); device variants live in ring_hip.hip and are reached through

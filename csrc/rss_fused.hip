@@ -1,0 +1,150 @@
+// gfx950 versions of the fused stacked-session protocol kernels (rss_fused.h).
+//
+// trunc_pr3: one pass per element computes the dealer's masks, both parties' masked
+// openings, the local truncation and the additive->replicated conversion for all three
+// parties -- six AES-CTR blocks and ~40 integer ops per element, one read of the three
+// input slots, one write of the two output share vectors.
+// share3: input sharing by a member party (two AES blocks per element).
+#include <hip/hip_runtime.h>
+
+#include "aes_dev.h"
+#include "moosex.h"
+#include "rss_fused.h"
+
+using u64 = uint64_t;
+using u128 = unsigned __int128;
+
+namespace {
+
+template <class T>
+__global__ void k_trunc_pr3(const T* __restrict__ s0, T* __restrict__ out0, T* __restrict__ out1,
+                            int64_t n, int m, mxd::Keys4 keys, uint64_t n_r0, uint64_t n_r1,
+                            uint64_t n_t, uint64_t n_m, uint64_t n_z0, uint64_t n_z2) {
+  __shared__ uint32_t Tt[256];
+  __shared__ uint8_t Sb[256];
+  mxd::stage_tables(Tt, Sb);
+  constexpr int P = mxd::Lane<T>::kPer;
+  const int64_t nb = (n + P - 1) / P;
+  const uint32_t* k0 = keys.rk[0];
+  const uint32_t* k2 = keys.rk[1];
+  for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < nb;
+       b += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t r0l, r0h, r1l, r1h, tl, th, ml, mh, z0l, z0h, z2l, z2h;
+    mxd::aes_ctr(k0, Tt, Sb, n_r0, b, &r0l, &r0h);
+    mxd::aes_ctr(k2, Tt, Sb, n_r1, b, &r1l, &r1h);
+    mxd::aes_ctr(k0, Tt, Sb, n_t, b, &tl, &th);
+    mxd::aes_ctr(k0, Tt, Sb, n_m, b, &ml, &mh);
+    mxd::aes_ctr(k0, Tt, Sb, n_z0, b, &z0l, &z0h);
+    mxd::aes_ctr(k2, Tt, Sb, n_z2, b, &z2l, &z2h);
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const int64_t i = b * P + j;
+      if (i >= n) break;
+      const T z0 = mxd::pick<T>(z0l, z0h, j);
+      const T z2 = mxd::pick<T>(z2l, z2h, j);
+      const T z1 = mxf::trunc_pr_z1<T>(s0[i], s0[n + i], s0[2 * n + i], mxd::pick<T>(r0l, r0h, j),
+                                       mxd::pick<T>(r1l, r1h, j), mxd::pick<T>(tl, th, j),
+                                       mxd::pick<T>(ml, mh, j), z0, z2, m);
+      out0[i] = z0;
+      out0[n + i] = z1;
+      out0[2 * n + i] = z2;
+      out1[i] = z1;
+      out1[n + i] = z2;
+      out1[2 * n + i] = z0;
+    }
+  }
+}
+
+template <class T>
+__global__ void k_share3(int kind, const T* __restrict__ x, T* __restrict__ out0,
+                         T* __restrict__ out1, int64_t n, int j0, mxd::Keys4 keys, uint64_t n1,
+                         uint64_t na) {
+  __shared__ uint32_t Tt[256];
+  __shared__ uint8_t Sb[256];
+  mxd::stage_tables(Tt, Sb);
+  constexpr int P = mxd::Lane<T>::kPer;
+  const int64_t nb = (n + P - 1) / P;
+  for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < nb;
+       b += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t al, ah, bl, bh;
+    mxd::aes_ctr(keys.rk[0], Tt, Sb, n1, b, &al, &ah);
+    mxd::aes_ctr(keys.rk[1], Tt, Sb, na, b, &bl, &bh);
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const int64_t i = b * P + j;
+      if (i >= n) break;
+      const T r1 = mxd::pick<T>(al, ah, j);
+      const T ra = mxd::pick<T>(bl, bh, j);
+      const T xj = kind == MX_CROSS_BOOL ? (T)(x[i] ^ r1 ^ ra) : (T)(x[i] - r1 - ra);
+      T slot[3];
+      slot[j0] = xj;
+      slot[(j0 + 1) % 3] = r1;
+      slot[(j0 + 2) % 3] = ra;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        out0[p * n + i] = slot[p];
+        out1[p * n + i] = slot[(p + 1) % 3];
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int mxh_trunc_pr3(int words, const void* s0, void* out0, void* out1, int64_t n, int m,
+                  const uint8_t* k0, const uint8_t* k2, const uint64_t* nn, void* stream) {
+  if (n == 0) return 0;
+  uint8_t kk[32];
+  memcpy(kk, k0, 16);
+  memcpy(kk + 16, k2, 16);
+  mxd::Keys4 keys = mxd::load_keys(kk, 2);
+  hipStream_t st = (hipStream_t)stream;
+  if (words == 1) {
+    int64_t nb = (n + 1) / 2;
+    hipLaunchKernelGGL(k_trunc_pr3<u64>, dim3(mxd::grid_for(nb)), dim3(256), 0, st,
+                       (const u64*)s0, (u64*)out0, (u64*)out1, n, m, keys, nn[0], nn[1], nn[2],
+                       nn[3], nn[4], nn[5]);
+  } else if (words == 2) {
+    hipLaunchKernelGGL(k_trunc_pr3<u128>, dim3(mxd::grid_for(n)), dim3(256), 0, st,
+                       (const u128*)s0, (u128*)out0, (u128*)out1, n, m, keys, nn[0], nn[1], nn[2],
+                       nn[3], nn[4], nn[5]);
+  } else {
+    return -2;
+  }
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : -100 - (int)e;
+}
+
+int mxh_share3(int kind, int words, const void* x, void* out0, void* out1, int64_t n, int j,
+               const uint8_t* k_next, const uint8_t* k_all, uint64_t n1, uint64_t na,
+               void* stream) {
+  if (n == 0) return 0;
+  uint8_t kk[32];
+  memcpy(kk, k_next, 16);
+  memcpy(kk + 16, k_all, 16);
+  mxd::Keys4 keys = mxd::load_keys(kk, 2);
+  hipStream_t st = (hipStream_t)stream;
+  switch (words) {
+    case 0:
+      hipLaunchKernelGGL(k_share3<uint8_t>, dim3(mxd::grid_for((n + 15) / 16)), dim3(256), 0, st,
+                         kind, (const uint8_t*)x, (uint8_t*)out0, (uint8_t*)out1, n, j, keys, n1,
+                         na);
+      break;
+    case 1:
+      hipLaunchKernelGGL(k_share3<u64>, dim3(mxd::grid_for((n + 1) / 2)), dim3(256), 0, st, kind,
+                         (const u64*)x, (u64*)out0, (u64*)out1, n, j, keys, n1, na);
+      break;
+    case 2:
+      hipLaunchKernelGGL(k_share3<u128>, dim3(mxd::grid_for(n)), dim3(256), 0, st, kind,
+                         (const u128*)x, (u128*)out0, (u128*)out1, n, j, keys, n1, na);
+      break;
+    default:
+      return -2;
+  }
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : -100 - (int)e;
+}
+
+}  // extern "C"

@@ -51,6 +51,13 @@ _SIGS = {
          c_i64, c_vp],
     ),
     "mx_set_gemm_impl": (None, [c_int]),
+    "mx_trunc_pr3": (
+        c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_vp],
+    ),
+    "mx_share3": (
+        c_int,
+        [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_u64, c_u64, c_vp],
+    ),
 }
 
 

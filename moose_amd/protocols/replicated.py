@@ -77,6 +77,9 @@ def share(sess, plc, x: HV, kind="arith") -> RepTensor:
         o = plc.owners
         j1, j2 = (j + 1) % 3, (j + 2) % 3
         n1, na = sess.nonce(), sess.nonce()
+        if getattr(sess, "fused", False):
+            s0, s1 = sess.fused_share(plc, x, j, kind, n1, na)
+            return RepTensor(plc, bits, kind, s0, s1)
         # slot_{j+1} = PRF(k_{j+1}) [P_j, P_{j+1}]; slot_{j+2} = PRF(k_all); slot_j = rest
         r1_j = sess.h_prf(plc, o[j], j1, shape, bits, n1)
         r1_j1 = sess.h_prf(plc, o[j1], j1, shape, bits, n1)
@@ -278,8 +281,12 @@ def trunc_pr(sess, x: RepTensor, m: int) -> RepTensor:
         plc, bits = x.plc, x.bits
         p0, p1, p2 = plc.owners
         k = bits - 1
-        sh = [sess.h("Shape", plc.owners[i], sess.take(x.s0, i)) for i in range(3)]
         nr0, nr1, nt, nm = sess.nonce(), sess.nonce(), sess.nonce(), sess.nonce()
+        if getattr(sess, "fused", False):
+            n0, n2 = sess.nonce(), sess.nonce()
+            s0, s1 = sess.fused_trunc_pr(x, m, (nr0, nr1, nt, nm, n0, n2))
+            return RepTensor(plc, bits, "arith", s0, s1)
+        sh = [sess.h("Shape", plc.owners[i], sess.take(x.s0, i)) for i in range(3)]
         # dealer P2
         r = sess.h("Add", p2, sess.h_prf(plc, p2, 0, sh[2], bits, nr0),
                    sess.h_prf(plc, p2, 2, sh[2], bits, nr1))

@@ -237,6 +237,57 @@ class StackedSession(Session):
     def p_shape(self, x: PV):
         return tuple(x.v.shape[1:])
 
+    # -- fused whole-protocol kernels (same shares as the generic protocol code) ------
+    fused = os.environ.get("MOOSEX_FUSED", "1") != "0"
+
+    def fused_trunc_pr(self, x, m, nonces):
+        """All three parties' TruncPr in one kernel (see replicated.trunc_pr)."""
+        import ctypes
+
+        from moose_amd.ops import native as nat
+
+        keys = self.setup(x.plc)
+        s0 = x.s0.v.data.contiguous()
+        out0, out1 = torch.empty_like(s0), torch.empty_like(s0)
+        n = x.s0.v.numel() // 3
+        nn = (ctypes.c_uint64 * 6)(*[v & ((1 << 64) - 1) for v in nonces])
+        nat.check(
+            nat.lib().mx_trunc_pr3(
+                nat.dev_of(s0), R._words(x.bits), nat.ptr(s0), nat.ptr(out0), nat.ptr(out1), n, m,
+                nat.key_buffer([keys[0]]), nat.key_buffer([keys[2]]), nn, nat.stream_of(s0),
+            ),
+            "trunc_pr3",
+        )
+        nbytes = out0.numel() * out0.element_size() // 3
+        o = x.plc.owners
+        # messages of the protocol: dealer -> P1 (2 tensors), P0 <-> P1 (two rounds)
+        for src, dst, k in ((o[2], o[1], 2), (o[0], o[1], 2), (o[1], o[0], 2)):
+            for _ in range(k):
+                self.stats.record_send(src, dst, nbytes)
+        self.stats.record_round(2 * nbytes)
+        self.stats.record_round(2 * nbytes)
+        return PV(x.plc, R.RT(out0, x.bits)), PV(x.plc, R.RT(out1, x.bits))
+
+    def fused_share(self, plc, x: HV, j, kind, n1, na):
+        from moose_amd.ops import native as nat
+
+        keys = self.setup(plc)
+        xd = x.v.data.contiguous()
+        shape = (3,) + tuple(xd.shape)
+        out0 = torch.empty(shape, dtype=xd.dtype, device=xd.device)
+        out1 = torch.empty_like(out0)
+        nat.check(
+            nat.lib().mx_share3(
+                nat.dev_of(xd), 1 if kind == "bool" else 0, R._words(x.v.bits), nat.ptr(xd),
+                nat.ptr(out0), nat.ptr(out1), x.v.numel(), j,
+                nat.key_buffer([keys[(j + 1) % 3]]), nat.key_buffer([keys[3]]), n1, na,
+                nat.stream_of(xd),
+            ),
+            "share3",
+        )
+        self.stats.record_send(x.host, plc.owners[(j + 2) % 3], _nbytes(x.v))
+        return PV(plc, R.RT(out0, x.v.bits)), PV(plc, R.RT(out1, x.v.bits))
+
     def mirror(self, x: HV, plc):
         """Host value -> mirrored (public on the 3 hosts of ``plc``)."""
         from moose_amd.runtime.values import MV

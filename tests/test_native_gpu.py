@@ -128,3 +128,21 @@ def test_gemm_long_k_split():
     bits = 128
     a, b = rand_rt((1, 64, 9000), bits, 40), rand_rt((1, 9000, 64), bits, 41)
     same(R.dot(a, b, nb=1), R.dot(gpu(a), gpu(b), nb=1))
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+def test_fused_protocol_kernels_match_host(bits):
+    from moose_amd.ir.computation import ReplicatedPlacement
+    from moose_amd.protocols import replicated as rep
+    from moose_amd.runtime.session import HV, StackedSession
+
+    plc = ReplicatedPlacement(("a", "b", "c"))
+    res = []
+    for dev in ("cpu", "cuda"):
+        s = StackedSession(dev, seed=9)
+        x = HV("b", R.encode(torch.linspace(-20, 20, 4099, dtype=torch.float64).to(dev), 23, bits))
+        X = rep.share(s, plc, x)
+        T = rep.trunc_pr(s, rep.mul(s, X, X), 23)
+        res.append([t.cpu() for t in (X.s0.v.data, X.s1.v.data, T.s0.v.data, T.s1.v.data)])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)

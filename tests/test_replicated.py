@@ -136,3 +136,19 @@ def test_round_accounting(sess):
     r0 = sess.stats.rounds
     rep.dot(sess, rep.local(sess, X, "Reshape", shape=(2, 2)), rep.local(sess, X, "Reshape", shape=(2, 2)))
     assert sess.stats.rounds - r0 == 1
+
+
+@pytest.mark.parametrize("owner", ["alice", "bob", "carole"])
+def test_fused_kernels_match_generic_protocol(bits, owner):
+    """The stacked session's one-pass Share/TruncPr kernels produce exactly the shares
+    of the generic (per-host) protocol code."""
+    outs = []
+    for fused in (False, True):
+        s = StackedSession("cpu", seed=5)
+        s.fused = fused
+        x = HV(owner, R.encode(torch.linspace(-50, 50, 301, dtype=torch.float64), F, bits))
+        X = rep.share(s, PLC, x)
+        T = rep.trunc_pr(s, rep.mul(s, X, X), F)
+        outs.append([X.s0.v.data, X.s1.v.data, T.s0.v.data, T.s1.v.data])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
