@@ -193,7 +193,7 @@ __global__ void __launch_bounds__(256, 1)
   constexpr int STAGE = L * kTileBytes;  // bytes per operand per k-step
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
   // two LDS buffers, each holding the A and B stage of one k-step
-  int8_t* buf[2] = {smem, smem + 2 * STAGE};
+  auto buf = [&](int i) -> int8_t* { return smem + i * 2 * STAGE; };
 
   const int64_t tiles_n = Np / TN, tiles_m = Mp / TM;
   const int64_t ntiles = tiles_n * tiles_m;
@@ -238,14 +238,14 @@ __global__ void __launch_bounds__(256, 1)
   // per k-step.  Stage kb+1 is written to the idle buffer after computing stage kb, and
   // the global loads of stage kb+2 are in flight during the next compute phase.
   load_stage(0);
-  store_stage(buf[0]);
+  store_stage(buf(0));
   __syncthreads();
   if (nkb > 1) load_stage(1);
   for (int64_t kb = 0; kb < nkb; ++kb) {
     const int cur = (int)(kb & 1);
-    mfma_diagonals<L>(buf[cur], buf[cur] + STAGE, arow, brow, half, acc);
+    mfma_diagonals<L>(buf(cur), buf(cur) + STAGE, arow, brow, half, acc);
     if (kb + 1 < nkb) {
-      store_stage(buf[cur ^ 1]);
+      store_stage(buf(cur ^ 1));
       if (kb + 2 < nkb) load_stage(kb + 2);
     }
     __syncthreads();
