@@ -25,8 +25,8 @@
 //      limb plane is a contiguous 2 KB image whose 16-byte fragment reads are LDS
 //      bank-conflict free (halves of rows r and r+8 are swapped).
 //   2. gemm (MFMA-bound): 256-thread blocks (4 waves as 2x2), 64x64 output tile, each wave
-//      32x32 with L diagonal accumulators; K advances 32 limb-bytes per step, staged in LDS
-//      with a register prefetch of the next step.
+//      32x32 with L diagonal accumulators; K advances 32 limb-bytes per step, streamed
+//      global->LDS by LDS-DMA (global_load_lds) into a double buffer.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -60,103 +60,105 @@ struct Limbs<u128> {
   static constexpr int L = 16;
 };
 
-// balanced signed limb split
-template <class T>
-__device__ inline void split_limbs(T x, int8_t* d) {
+// Pack the balanced limbs of 16 consecutive k' of one tile row into L 16-byte vectors
+// (word j/4, byte j%4); fully unrolled so everything stays in registers.
+template <class T, class Load>
+__device__ inline void split16(Load load, v4i (&w)[Limbs<T>::L]) {
   constexpr int L = Limbs<T>::L;
 #pragma unroll
-  for (int l = 0; l < L; ++l) {
-    int v = (int)(x & 0xff);
-    x >>= 8;
-    if (v >= 128) {
-      v -= 256;
-      x += 1;
+  for (int l = 0; l < L; ++l) w[l] = v4i{0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    T x = load(j);
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      int v = (int)(x & 0xff);
+      x >>= 8;
+      if (v >= 128) x += 1;  // balanced digit v - 256, carry one into the next limb
+      w[l][j >> 2] |= (v & 0xff) << (8 * (j & 3));
     }
-    d[l] = (int8_t)v;
   }
 }
 
-// A' [batch, M, K'] (K' = K or 2K) -> blocked limbs. One thread: one row, 16 consecutive k'.
+// One thread = (tile, k-step, tile row r, k-half h); a wave covers 32 rows x both halves of
+// one (tile, k-step), so every limb-plane store of the wave is one contiguous 1 KB run.
+__device__ inline void prep_coords(int64_t g, int64_t nkb, int64_t& t, int64_t& kb, int& r,
+                                   int& h) {
+  h = (int)(g & 1);
+  r = (int)((g >> 1) & 63);
+  const int64_t q = g >> 7;
+  kb = q % nkb;
+  t = q / nkb;
+}
+
+// A' [batch, M, K'] (K' = K or 2K: mode 1 concatenates A0 | A1) -> blocked limbs.
 template <class T>
-__global__ void k_prep_a(const T* __restrict__ A0, const T* __restrict__ A1, int64_t M,
-                         int64_t K, int mode, int8_t* __restrict__ out, int64_t Mp, int64_t Kp) {
+__global__ void __launch_bounds__(256) k_prep_a(const T* __restrict__ A0, const T* __restrict__ A1,
+                                                int64_t M, int64_t K, int mode,
+                                                int8_t* __restrict__ out, int64_t Mp, int64_t Kp) {
   constexpr int L = Limbs<T>::L;
-  const int64_t groups_k = Kp / 16;
-  const int64_t total = Mp * groups_k;
+  const int64_t nkb = Kp / TK;
+  const int64_t total = (Mp / TM) * nkb * 128;
   const int64_t b = blockIdx.y;
   const T* a0 = A0 + b * M * K;
-  const T* a1 = mode ? A1 + b * M * K : nullptr;
-  const int64_t nkb = Kp / TK;
+  const T* a1 = mode ? A1 + b * M * K : a0;
   int8_t* ob = out + b * (Mp / TM) * nkb * (int64_t)L * kTileBytes;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total;
        g += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t m = g / groups_k;
-    const int64_t k0 = (g % groups_k) * 16;
-    alignas(16) int8_t limbs[L][16];
-#pragma unroll 4
-    for (int j = 0; j < 16; ++j) {
-      int64_t k = k0 + j;
-      T v = 0;
-      if (m < M) {
-        if (k < K)
-          v = a0[m * K + k];
-        else if (mode && k < 2 * K)
-          v = a1[m * K + (k - K)];
-      }
-      int8_t d[L];
-      split_limbs<T>(v, d);
-#pragma unroll
-      for (int l = 0; l < L; ++l) limbs[l][j] = d[l];
-    }
-    const int64_t mb = m / TM, kb = k0 / TK;
-    const int r = (int)(m % TM), h = (int)((k0 % TK) / 16);
+    int64_t mb, kb;
+    int r, h;
+    prep_coords(g, nkb, mb, kb, r, h);
+    const int64_t m = mb * TM + r;
+    const int64_t k0 = kb * TK + h * 16;
+    v4i w[L];
+    split16<T>(
+        [&](int j) -> T {
+          const int64_t k = k0 + j;
+          if (m >= M) return 0;
+          if (k < K) return a0[m * K + k];
+          if (mode && k < 2 * K) return a1[m * K + (k - K)];
+          return 0;
+        },
+        w);
     int8_t* base = ob + (mb * nkb + kb) * (int64_t)L * kTileBytes + swz(r, h);
 #pragma unroll
-    for (int l = 0; l < L; ++l) *(v4i*)(base + l * kTileBytes) = *(const v4i*)limbs[l];
+    for (int l = 0; l < L; ++l) *(v4i*)(base + l * kTileBytes) = w[l];
   }
 }
 
 // B' [batch, K', N] -> blocked limbs with n as the tile row.  mode 1: rows k < K hold
-// B0 + B1, rows K <= k < 2K hold B0.  One thread: one column, 16 consecutive k'.
+// B0 + B1, rows K <= k < 2K hold B0.  Lanes of a wave read 32 consecutive columns.
 template <class T>
-__global__ void k_prep_b(const T* __restrict__ B0, const T* __restrict__ B1, int64_t K,
-                         int64_t N, int mode, int8_t* __restrict__ out, int64_t Np, int64_t Kp) {
+__global__ void __launch_bounds__(256) k_prep_b(const T* __restrict__ B0, const T* __restrict__ B1,
+                                                int64_t K, int64_t N, int mode,
+                                                int8_t* __restrict__ out, int64_t Np, int64_t Kp) {
   constexpr int L = Limbs<T>::L;
-  const int64_t groups_k = Kp / 16;
-  const int64_t total = Np * groups_k;
+  const int64_t nkb = Kp / TK;
+  const int64_t total = (Np / TN) * nkb * 128;
   const int64_t b = blockIdx.y;
   const T* b0 = B0 + b * K * N;
-  const T* b1 = mode ? B1 + b * K * N : nullptr;
-  const int64_t nkb = Kp / TK;
+  const T* b1 = mode ? B1 + b * K * N : b0;
   int8_t* ob = out + b * (Np / TN) * nkb * (int64_t)L * kTileBytes;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total;
        g += (int64_t)gridDim.x * blockDim.x) {
-    // consecutive threads take consecutive columns (coalesced row reads of B)
-    const int64_t n = g % Np;
-    const int64_t k0 = (g / Np) * 16;
-    alignas(16) int8_t limbs[L][16];
-#pragma unroll 4
-    for (int j = 0; j < 16; ++j) {
-      int64_t k = k0 + j;
-      T v = 0;
-      if (n < N) {
-        if (k < K) {
-          v = b0[k * N + n];
-          if (mode) v += b1[k * N + n];
-        } else if (mode && k < 2 * K) {
-          v = b0[(k - K) * N + n];
-        }
-      }
-      int8_t d[L];
-      split_limbs<T>(v, d);
-#pragma unroll
-      for (int l = 0; l < L; ++l) limbs[l][j] = d[l];
-    }
-    const int64_t nb = n / TN, kb = k0 / TK;
-    const int r = (int)(n % TN), h = (int)((k0 % TK) / 16);
+    int64_t nb, kb;
+    int r, h;
+    prep_coords(g, nkb, nb, kb, r, h);
+    const int64_t n = nb * TN + r;
+    const int64_t k0 = kb * TK + h * 16;
+    v4i w[L];
+    split16<T>(
+        [&](int j) -> T {
+          const int64_t k = k0 + j;
+          if (n >= N) return 0;
+          if (k < K) return mode ? (T)(b0[k * N + n] + b1[k * N + n]) : b0[k * N + n];
+          if (mode && k < 2 * K) return b0[(k - K) * N + n];
+          return 0;
+        },
+        w);
     int8_t* base = ob + (nb * nkb + kb) * (int64_t)L * kTileBytes + swz(r, h);
 #pragma unroll
-    for (int l = 0; l < L; ++l) *(v4i*)(base + l * kTileBytes) = *(const v4i*)limbs[l];
+    for (int l = 0; l < L; ++l) *(v4i*)(base + l * kTileBytes) = w[l];
   }
 }
 
@@ -164,15 +166,19 @@ template <int L>
 __device__ inline void mfma_diagonals(const int8_t* __restrict__ As,
                                       const int8_t* __restrict__ Bs, int arow, int brow,
                                       int half, v16i (&acc)[L]) {
-  v4i bf[L];
+  // All fragments of the k-step are requested up front so the LDS latency is paid once
+  // (hipcc then emits counted lgkmcnt waits instead of a full drain before every A limb);
+  // with one wave per SIMD nothing else would hide a per-limb wait.
+  v4i bf[L], af[L];
 #pragma unroll
   for (int j = 0; j < L; ++j) bf[j] = *(const v4i*)(Bs + j * kTileBytes + swz(brow, half));
 #pragma unroll
+  for (int i = 0; i < L; ++i) af[i] = *(const v4i*)(As + i * kTileBytes + swz(arow, half));
+#pragma unroll
   for (int i = 0; i < L; ++i) {
-    v4i af = *(const v4i*)(As + i * kTileBytes + swz(arow, half));
 #pragma unroll
     for (int j = 0; j < L - i; ++j)
-      acc[i + j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af, bf[j], acc[i + j], 0, 0, 0);
+      acc[i + j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[i], bf[j], acc[i + j], 0, 0, 0);
   }
 }
 
@@ -216,39 +222,38 @@ __global__ void __launch_bounds__(256, 1)
 #pragma unroll
   for (int d = 0; d < L; ++d) acc[d] = v16i{0};
 
-  constexpr int PER_THREAD = STAGE / (256 * 16);  // 16-byte chunks per thread per operand
-  v4i pa[PER_THREAD], pb[PER_THREAD];
-  auto load_stage = [&](int64_t kb) {
-    const int8_t* na = ga + kb * STAGE;
-    const int8_t* nb = gb + kb * STAGE;
+  // Stage k-step kb of both operands straight into LDS with global_load_lds (16 B per
+  // lane, 1 KiB per wave-instruction): the blocked limb layout makes each stage one
+  // contiguous image, so the lane-linear LDS destination of LDS-DMA matches exactly and no
+  // VGPRs are spent on staging (they hold the 2 x L MFMA fragments instead).
+  constexpr int PIECES = STAGE / 1024;  // 1 KiB pieces per operand per stage
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  auto issue_stage = [&](int64_t kb, int8_t* dst) {
+    const int8_t* sa = ga + kb * STAGE + lane * 16;
+    const int8_t* sb = gb + kb * STAGE + lane * 16;
 #pragma unroll
-    for (int c = 0; c < PER_THREAD; ++c) {
-      pa[c] = *(const v4i*)(na + (c * 256 + threadIdx.x) * 16);
-      pb[c] = *(const v4i*)(nb + (c * 256 + threadIdx.x) * 16);
+    for (int c = wave_u; c < PIECES; c += 4) {
+      __builtin_amdgcn_global_load_lds((const void*)(sa + c * 1024),
+                                       (__attribute__((address_space(3))) void*)(dst + c * 1024),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(sb + c * 1024),
+                                       (__attribute__((address_space(3))) void*)(dst + STAGE + c * 1024),
+                                       16, 0, 0);
     }
   };
-  auto store_stage = [&](int8_t* dst) {
-#pragma unroll
-    for (int c = 0; c < PER_THREAD; ++c) {
-      *(v4i*)(dst + (c * 256 + threadIdx.x) * 16) = pa[c];
-      *(v4i*)(dst + STAGE + (c * 256 + threadIdx.x) * 16) = pb[c];
-    }
-  };
-  // software pipeline: LDS double buffer + one k-step of register prefetch; one barrier
-  // per k-step.  Stage kb+1 is written to the idle buffer after computing stage kb, and
-  // the global loads of stage kb+2 are in flight during the next compute phase.
-  load_stage(0);
-  store_stage(buf(0));
+  // two LDS buffers; the DMA of stage kb+1 is in flight while stage kb is multiplied.  One
+  // barrier per k-step: after it every wave has finished reading buffer kb&1 (so it may be
+  // refilled with stage kb+2) and every wave's DMA of stage kb+1 has landed (vmcnt(0)).
+  issue_stage(0, buf(0));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (nkb > 1) load_stage(1);
+  if (nkb > 1) issue_stage(1, buf(1));
   for (int64_t kb = 0; kb < nkb; ++kb) {
     const int cur = (int)(kb & 1);
     mfma_diagonals<L>(buf(cur), buf(cur) + STAGE, arow, brow, half, acc);
-    if (kb + 1 < nkb) {
-      store_stage(buf(cur ^ 1));
-      if (kb + 2 < nkb) load_stage(kb + 2);
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (kb + 2 < nkb) issue_stage(kb + 2, buf(cur));
   }
 
   // epilogue: C[row][col] = sum_d sext(acc_d) << 8d
@@ -340,7 +345,7 @@ int run(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T* A1
     const int threads = 256;
     {
       int64_t work = p.Mp * (p.Kp / 16);
-      int gx = (int)std::min<int64_t>((work + threads - 1) / threads, 4096);
+      int gx = (int)std::min<int64_t>((work + threads - 1) / threads, 8192);
       if (kk == K) {
         hipLaunchKernelGGL(k_prep_a<T>, dim3(gx, (unsigned)batch), dim3(threads), 0, st, A0, A1,
                            M, K, mode, la, p.Mp, p.Kp);
@@ -350,7 +355,7 @@ int run(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T* A1
     }
     {
       int64_t work = p.Np * (p.Kp / 16);
-      int gx = (int)std::min<int64_t>((work + threads - 1) / threads, 4096);
+      int gx = (int)std::min<int64_t>((work + threads - 1) / threads, 8192);
       hipLaunchKernelGGL(k_prep_b<T>, dim3(gx, (unsigned)batch), dim3(threads), 0, st, B0, B1,
                          K, N, mode, lb, p.Np, p.Kp);
     }

@@ -27,5 +27,6 @@ STEPS=${STEPS:-all}
 if [[ $STEPS == *prof* || $STEPS == all ]]; then
   export TMPDIR=/tmp
   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1
+  run prof64 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof64 -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --ring 64
 fi
 exit 0
