@@ -46,6 +46,7 @@ constexpr int TM = 64;  // rows of the block tile (A side)
 constexpr int TN = 64;  // cols of the block tile (B side)
 constexpr int TK = 32;  // limb-bytes per k-step (one MFMA K)
 constexpr int kTileBytes = 64 * TK;  // one limb plane of one tile per k-step: 2 KB
+constexpr int kGroupM = 4;           // row bands per L2 tile group
 
 __device__ __host__ inline int swz(int r, int h) { return r * TK + 16 * (h ^ ((r >> 3) & 1)); }
 
@@ -203,8 +204,15 @@ __global__ void __launch_bounds__(256, 1)
 
   const int64_t tiles_n = Np / TN, tiles_m = Mp / TM;
   const int64_t ntiles = tiles_n * tiles_m;
+  // XCD-contiguous tile ranges, walked in groups of kGroupM row bands so the ~32 blocks
+  // co-resident on one XCD cover a 4 x 8 patch of output tiles: they share 4 A and 8 B
+  // k-streams in that XCD's L2 instead of 1 A and 32 B streams.
   const int64_t tid_flat = xcd_remap(blockIdx.x, ntiles);
-  const int64_t tm = tid_flat / tiles_n, tn = tid_flat % tiles_n;
+  const int64_t group = tid_flat / (kGroupM * tiles_n);
+  const int64_t first_m = group * kGroupM;
+  const int64_t gm = tiles_m - first_m < kGroupM ? tiles_m - first_m : kGroupM;
+  const int64_t in_group = tid_flat % (kGroupM * tiles_n);
+  const int64_t tm = first_m + in_group % gm, tn = in_group / gm;
   const int64_t b = blockIdx.y;
   const int64_t nkb = Kp / TK;
 

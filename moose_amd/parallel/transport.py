@@ -1,0 +1,225 @@
+"""Point-to-point value transport between party processes over ``torch.distributed``.
+
+This replaces the reference's networking layer (``moose/src/networking``: the
+``AsyncNetworking{send, receive}`` trait keyed by (SessionId, RendezvousKey), gRPC in
+``networking/grpc.rs:98-170`` and TCP streams in ``networking/tcpstream.rs:160-284``).
+On a MI355X node every party is one process on its own GPU and every message is an
+RCCL ``send``/``recv`` over xGMI (backend ``"nccl"`` is RCCL on ROCm); CPU tests use the
+``gloo`` backend with the same code.
+
+Matching: all party processes execute the same protocol program in the same order
+(SPMD), so the n-th message from A to B is always the n-th receive B posts from A --
+the role the reference's rendezvous keys play.  Messages whose shape the receiver
+already knows (the hot reshare path, :meth:`Transport.shift`) go without a header;
+everything else is preceded by a fixed-size int64 header describing the payload
+(kind, dtype, ring width, shape) so that no Python object is ever pickled.
+"""
+from __future__ import annotations
+
+import math
+import struct
+from typing import List
+
+import torch
+import torch.distributed as dist
+
+from moose_amd.ops import ring as R
+
+HEADER_WORDS = 24
+MAX_DIMS = HEADER_WORDS - 4
+
+# payload kinds
+K_RT, K_TENSOR, K_BYTES, K_SHAPE, K_INT, K_FLOAT, K_NONE, K_STR, K_BOOL = range(9)
+
+_DTYPES = [torch.float64, torch.float32, torch.int64, torch.int32, torch.uint8, torch.bool,
+           torch.int8, torch.int16, torch.float16, torch.bfloat16]
+_DTYPE_CODE = {d: i for i, d in enumerate(_DTYPES)}
+
+
+class TransportError(RuntimeError):
+    pass
+
+
+class Transport:
+    """Typed send/recv between the ranks of a process group.
+
+    ``device`` is where payload tensors travel (a CUDA device for RCCL, CPU for gloo).
+    """
+
+    def __init__(self, rank: int, world: int, device, group=None):
+        self.rank = rank
+        self.world = world
+        self.device = torch.device(device)
+        self.group = group
+        self.bytes_sent = 0
+        self.messages = 0
+
+    # -- encoding -----------------------------------------------------------------
+    def _header(self, v):
+        h = [0] * HEADER_WORDS
+        payload = None
+        if isinstance(v, R.RT):
+            h[0], h[2] = K_RT, v.bits
+            data = v.data
+            payload = data
+            shape = tuple(data.shape)
+            h[1] = _DTYPE_CODE[data.dtype]
+        elif isinstance(v, torch.Tensor):
+            h[0] = K_TENSOR
+            data = v
+            if data.dtype == torch.bool:  # RCCL has no bool reduction type; ship bytes
+                h[2] = 1
+                data = data.to(torch.uint8)
+            h[1] = _DTYPE_CODE[data.dtype]
+            payload = data
+            shape = tuple(data.shape)
+        elif isinstance(v, (bytes, bytearray)):
+            h[0], h[1] = K_BYTES, _DTYPE_CODE[torch.uint8]
+            payload = torch.tensor(list(v), dtype=torch.uint8)
+            shape = (len(v),)
+        elif isinstance(v, str):
+            h[0], h[1] = K_STR, _DTYPE_CODE[torch.uint8]
+            b = v.encode()
+            payload = torch.tensor(list(b), dtype=torch.uint8)
+            shape = (len(b),)
+        elif isinstance(v, bool):
+            h[0], h[4] = K_BOOL, int(v)
+            return h, None
+        elif isinstance(v, int):
+            h[0] = K_INT
+            # two's-complement 128-bit split (Python ints used as ring constants)
+            u = v & ((1 << 128) - 1)
+            h[4], h[5] = _s64(u & ((1 << 64) - 1)), _s64(u >> 64)
+            h[6] = 1 if v < 0 else 0
+            return h, None
+        elif isinstance(v, float):
+            h[0] = K_FLOAT
+            h[4] = struct.unpack("<q", struct.pack("<d", v))[0]
+            return h, None
+        elif v is None:
+            h[0] = K_NONE
+            return h, None
+        elif isinstance(v, tuple) and all(isinstance(d, int) for d in v):
+            h[0] = K_SHAPE
+            if len(v) > MAX_DIMS:
+                raise TransportError(f"shape {v} has too many dimensions")
+            h[3] = len(v)
+            h[4:4 + len(v)] = list(v)
+            return h, None
+        else:
+            raise TransportError(f"cannot transport a {type(v).__name__}")
+        if len(shape) > MAX_DIMS:
+            raise TransportError(f"tensor of rank {len(shape)} is too large to transport")
+        h[3] = len(shape)
+        h[4:4 + len(shape)] = list(shape)
+        return h, payload
+
+    def _decode_header(self, h: List[int]):
+        kind = h[0]
+        if kind == K_BOOL:
+            return kind, None, bool(h[4])
+        if kind == K_INT:
+            u = (h[4] & ((1 << 64) - 1)) | ((h[5] & ((1 << 64) - 1)) << 64)
+            return kind, None, u - (1 << 128) if h[6] else u
+        if kind == K_FLOAT:
+            return kind, None, struct.unpack("<d", struct.pack("<q", h[4]))[0]
+        if kind == K_NONE:
+            return kind, None, None
+        shape = tuple(h[4:4 + h[3]])
+        if kind == K_SHAPE:
+            return kind, None, shape
+        return kind, shape, None
+
+    # -- raw tensors ----------------------------------------------------------------
+    def _send_tensor(self, t: torch.Tensor, dst: int):
+        t = t.contiguous()
+        if t.device != self.device:
+            t = t.to(self.device)
+        if t.numel() == 0:
+            return
+        dist.send(t, dst, group=self.group)
+        self.bytes_sent += t.numel() * t.element_size()
+        self.messages += 1
+
+    def _recv_tensor(self, shape, dtype, src: int) -> torch.Tensor:
+        t = torch.empty(shape, dtype=dtype, device=self.device)
+        if t.numel() == 0:
+            return t
+        dist.recv(t, src, group=self.group)
+        return t
+
+    # -- typed values -----------------------------------------------------------------
+    def send(self, v, dst: int):
+        h, payload = self._header(v)
+        self._send_tensor(torch.tensor(h, dtype=torch.int64), dst)
+        if payload is not None:
+            self._send_tensor(payload, dst)
+
+    def recv(self, src: int, device=None):
+        h = self._recv_tensor((HEADER_WORDS,), torch.int64, src).cpu().tolist()
+        kind, shape, scalar = self._decode_header(h)
+        if shape is None:
+            return scalar
+        dtype = _DTYPES[h[1]]
+        data = self._recv_tensor(shape, dtype, src)
+        if device is not None:
+            data = data.to(device)
+        if kind == K_RT:
+            return R.RT(data, h[2])
+        if kind == K_TENSOR:
+            return data.to(torch.bool) if h[2] == 1 else data
+        if kind == K_BYTES:
+            return bytes(data.cpu().tolist())
+        if kind == K_STR:
+            return bytes(data.cpu().tolist()).decode()
+        raise TransportError(f"bad header kind {kind}")
+
+    # -- structured exchanges ------------------------------------------------------------
+    def shift(self, t: torch.Tensor, to_rank: int, from_rank: int) -> torch.Tensor:
+        """Send ``t`` to ``to_rank`` while receiving a same-shaped tensor from
+        ``from_rank`` (the RSS reshare ring).  One grouped RCCL call."""
+        t = t.contiguous()
+        if t.device != self.device:
+            t = t.to(self.device)
+        out = torch.empty_like(t)
+        if t.numel() == 0:
+            return out
+        ops = [dist.P2POp(dist.isend, t, to_rank, group=self.group),
+               dist.P2POp(dist.irecv, out, from_rank, group=self.group)]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        self.bytes_sent += t.numel() * t.element_size()
+        self.messages += 1
+        return out
+
+    def broadcast_from(self, v, src: int, dsts: List[int], me: int):
+        """``src`` sends ``v`` to every rank in ``dsts``; returns the value at ``me``."""
+        if me == src:
+            for d in dsts:
+                if d != src:
+                    self.send(v, d)
+            return v
+        if me in dsts:
+            return self.recv(src)
+        return None
+
+
+def _s64(u: int) -> int:
+    return u - (1 << 64) if u >= (1 << 63) else u
+
+
+def payload_bytes(v) -> int:
+    if isinstance(v, R.RT):
+        return v.data.numel() * v.data.element_size()
+    if isinstance(v, torch.Tensor):
+        return v.numel() * v.element_size()
+    if isinstance(v, (bytes, bytearray, str)):
+        return len(v)
+    return 8
+
+
+def numel(shape) -> int:
+    return int(math.prod(shape)) if shape else 1
+
+
+__all__ = ["Transport", "TransportError", "payload_bytes", "numel"]

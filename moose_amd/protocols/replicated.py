@@ -76,7 +76,7 @@ def share(sess, plc, x: HV, kind="arith") -> RepTensor:
         sub = "Sub" if kind == "arith" else "Xor"
         o = plc.owners
         j1, j2 = (j + 1) % 3, (j + 2) % 3
-        n1, na = sess.nonce(), sess.nonce()
+        n1, na = sess.nonce(plc), sess.nonce(plc)
         if getattr(sess, "fused", False):
             s0, s1 = sess.fused_share(plc, x, j, kind, n1, na)
             return RepTensor(plc, bits, kind, s0, s1)
@@ -281,9 +281,9 @@ def trunc_pr(sess, x: RepTensor, m: int) -> RepTensor:
         plc, bits = x.plc, x.bits
         p0, p1, p2 = plc.owners
         k = bits - 1
-        nr0, nr1, nt, nm = sess.nonce(), sess.nonce(), sess.nonce(), sess.nonce()
+        nr0, nr1, nt, nm = (sess.nonce(plc) for _ in range(4))
         if getattr(sess, "fused", False):
-            n0, n2 = sess.nonce(), sess.nonce()
+            n0, n2 = sess.nonce(plc), sess.nonce(plc)
             s0, s1 = sess.fused_trunc_pr(x, m, (nr0, nr1, nt, nm, n0, n2))
             return RepTensor(plc, bits, "arith", s0, s1)
         sh = [sess.h("Shape", plc.owners[i], sess.take(x.s0, i)) for i in range(3)]
@@ -327,7 +327,7 @@ def _adt_to_rep(sess, plc, y0: HV, y1: HV, sh, bits) -> RepTensor:
     """2-party additive (P0: y0, P1: y1) -> RSS: z0 = PRF(k_0) [P0,P2], z2 = PRF(k_2)
     [P1,P2], z1 = (y0 - z0) + (y1 - z2) exchanged between P0 and P1 (one round)."""
     p0, p1, p2 = plc.owners
-    n0, n2 = sess.nonce(), sess.nonce()
+    n0, n2 = sess.nonce(plc), sess.nonce(plc)
     z0_at0 = sess.h_prf(plc, p0, 0, sh[0], bits, n0)
     z2_at1 = sess.h_prf(plc, p1, 2, sh[1], bits, n2)
     z0_at2 = sess.h_prf(plc, p2, 0, sh[2], bits, n0)

@@ -45,6 +45,10 @@ class MooseRuntimeError(RuntimeError):
     pass
 
 
+def _owners(plc):
+    return (plc.owner,) if isinstance(plc, HostPlacement) else tuple(plc.owners)
+
+
 def torch_dtype_of(dtype: T.TensorDType):
     k = dtype.kind
     if k in _FLOAT:
@@ -95,6 +99,7 @@ class Interpreter:
     def run(self, comp: Computation, arguments: dict) -> dict:
         self.arguments = arguments or {}
         comp = comp.toposorted()
+        me = getattr(self.sess, "me", None)  # set for one-process-per-party sessions
         for op in comp.operations:
             handler = getattr(self, f"op_{op.kind}", None)
             if handler is None:
@@ -102,12 +107,51 @@ class Interpreter:
             ins = [self.env[n] for n in op.inputs]
             with span(f"op.{op.kind}", op=op.name):
                 try:
-                    self.env[op.name] = handler(op, ins)
+                    if me is not None and me not in _owners(op.placement):
+                        self.env[op.name] = self._foreign_op(op, ins, me)
+                    else:
+                        self.env[op.name] = handler(op, ins)
                 except MooseRuntimeError:
                     raise
                 except Exception as e:  # annotate with the failing op
                     raise MooseRuntimeError(f"{op.name} = {op.kind} failed: {e}") from e
         return self.outputs
+
+    # ------------------------------------------------------------------------
+    # SPMD: operations placed on other parties
+    # ------------------------------------------------------------------------
+    def _foreign_op(self, op, ins, me):
+        """This process does not own ``op``'s placement.  It takes part only in moving
+        its own operands there (sharing a host input, revealing a share, ...), in the
+        order the owners' handler converts them, and keeps a typed placeholder."""
+        for x in ins:
+            if me in _owners(x.plc) and x.kind in ("tensor", "shape"):
+                self.at(op, x)
+        return self._placeholder(op)
+
+    def _placeholder(self, op) -> LV:
+        from moose_amd.parallel.spmd import Remote
+        from moose_amd.runtime.session import PV
+
+        plc = op.placement
+        ret = op.sig.ret
+        name = ret.name
+        kind = ("shape" if "Shape" in name else "string" if "String" in name
+                else "unit" if name == "Unit" else "tensor")
+        dtype = self._ret_dtype(op) if kind == "tensor" else None
+        bits = None
+        if dtype is not None:
+            bits = (dtype.ring_bits if dtype.is_fixed else 1 if dtype.kind == "Bool"
+                    else 64 if dtype.kind == "Uint64" else None)
+        if isinstance(plc, HostPlacement):
+            return LV(plc, kind, dtype, HV(plc.owner, Remote(bits)))
+        if isinstance(plc, ReplicatedPlacement) and kind == "tensor" and bits is not None:
+            rkind = "bool" if bits == 1 else "arith"
+            t = rep.RepTensor(plc, bits, rkind, PV(plc, Remote(bits)), PV(plc, Remote(bits)))
+            if dtype.is_fixed:
+                t = RepFixed(t, dtype.fractional_precision, dtype.integral_precision)
+            return LV(plc, kind, dtype, t)
+        return LV(plc, kind, dtype, MV(plc, Remote(bits)))
 
     # ------------------------------------------------------------------------
     # dtype helpers

@@ -82,16 +82,20 @@ class Session:
 
     def __init__(self, device="cpu", seed: Optional[int] = None):
         self.device = torch.device(device)
-        self._nonce = 0
+        self._nonces = {}
         self.seed = seed
         self.stats = telemetry.SessionStats()
         self._keys = {}
         self._rng = torch.Generator().manual_seed(seed) if seed is not None else None
 
-    def nonce(self) -> int:
-        """Fresh PRF nonce; all parties draw the same sequence (deterministic order)."""
-        self._nonce += 1
-        return self._nonce
+    def nonce(self, plc=None) -> int:
+        """Fresh PRF nonce of replicated placement ``plc``.  Every member of ``plc``
+        executes every protocol step on ``plc`` in program order, so all members draw the
+        same sequence; keeping one counter per placement keeps it aligned even when a
+        party also works on other placements (SPMD execution)."""
+        n = self._nonces.get(plc, 0) + 1
+        self._nonces[plc] = n
+        return n
 
     def _random_bytes(self, n=16) -> bytes:
         if self._rng is not None:
@@ -224,7 +228,7 @@ class StackedSession(Session):
         """Party p: x0*y0 + x0*y1 + x1*y0 (+ alpha_p with sum alpha = 0), one kernel."""
         keys = self.party_keys(plc) if zero_share else None
         out = R.rss_cross(kind, x0.v, x1.v if x1 is not None else None, y0.v,
-                          y1.v if y1 is not None else None, keys, self.nonce(), 3)
+                          y1.v if y1 is not None else None, keys, self.nonce(plc), 3)
         return PV(plc, out)
 
     def p_dot_cross(self, plc, x0, x1, y0, y1):
@@ -232,7 +236,7 @@ class StackedSession(Session):
 
     def p_add_zero_share(self, plc, z, kind="arith"):
         keys = self.party_keys(plc)
-        return PV(plc, R.rss_cross(kind, z.v, None, None, None, keys, self.nonce(), 3))
+        return PV(plc, R.rss_cross(kind, z.v, None, None, None, keys, self.nonce(plc), 3))
 
     def p_shape(self, x: PV):
         return tuple(x.v.shape[1:])

@@ -1,0 +1,144 @@
+"""One process per identity (SPMD session over torch.distributed/gloo): results equal the
+single-process stacked runtime, including bitwise-equal shares under fixed seeds.
+
+Reference strategy: the reference tests its gRPC/TCP networking with multi-worker
+integration tests (``moose/tests/integration_test.rs``, ``pymoose`` examples on
+``GrpcMooseRuntime``); here the workers are local processes on the gloo backend."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import moose_amd as pm
+from moose_amd.ir.computation import ReplicatedPlacement
+from moose_amd.ops import ring as R
+from moose_amd.runtime.distributed import DistributedMooseRuntime
+from moose_amd.runtime.local import LocalMooseRuntime
+
+FP = pm.fixed(14, 23)
+
+
+def _comp(with_outsider=False):
+    alice = pm.host_placement("alice")
+    bob = pm.host_placement("bob")
+    carole = pm.host_placement("carole")
+    dave = pm.host_placement("dave")
+    rep = pm.replicated_placement("rep", players=[alice, bob, carole])
+    src = dave if with_outsider else alice
+
+    @pm.computation
+    def f(x: pm.Argument(placement=src, vtype=pm.TensorType(pm.float64)),
+          y: pm.Argument(placement=bob, vtype=pm.TensorType(pm.float64))):
+        with src:
+            xf = pm.cast(x, dtype=FP)
+        with bob:
+            yf = pm.cast(y, dtype=FP)
+        with rep:
+            z = pm.dot(xf, yf)
+            s = pm.sigmoid(z)
+            m = pm.mul(z, z)
+            c = pm.less(z, m)
+        with carole:
+            zo = pm.cast(z, dtype=pm.float64)
+            so = pm.cast(s, dtype=pm.float64)
+        with alice:
+            mo = pm.cast(m, dtype=pm.float64)
+        with (dave if with_outsider else carole):
+            co = pm.identity(c)
+        return zo, so, mo, co
+
+    return f
+
+
+def _args():
+    rng = np.random.default_rng(3)
+    return {"x": rng.uniform(-1, 1, (4, 5)), "y": rng.uniform(-1, 1, (5, 3))}
+
+
+@pytest.mark.parametrize("outsider", [False, True])
+def test_distributed_runtime_matches_local(outsider):
+    comp = _comp(outsider)
+    idents = ["alice", "bob", "carole"] + (["dave"] if outsider else [])
+    args = _args()
+    local = LocalMooseRuntime(idents, device="cpu", seed=1).evaluate_computation(comp, args)
+    rt = DistributedMooseRuntime(idents, backend="gloo", seed=1, timeout=300)
+    got = rt.evaluate_computation(comp, args)
+    assert set(got) == set(local)
+    for k in local:
+        np.testing.assert_allclose(np.asarray(got[k], dtype=np.float64),
+                                   np.asarray(local[k], dtype=np.float64), atol=1e-5)
+    z = args["x"] @ args["y"]
+    vals = sorted(local.values(), key=lambda a: np.asarray(a).size)
+    assert any(np.allclose(np.asarray(v, dtype=np.float64), z, atol=1e-4) for v in vals)
+    assert set(rt.last_timings) == set(idents)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _shares_worker(rank, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=3)
+    from moose_amd.parallel.spmd import SPMDSession
+    from moose_amd.parallel.transport import Transport
+    from moose_amd.protocols import replicated as rep
+    from moose_amd.runtime.session import HV
+
+    plc = ReplicatedPlacement(("a", "b", "c"))
+    s = SPMDSession(plc.owners[rank], {"a": 0, "b": 1, "c": 2}, Transport(rank, 3, "cpu"),
+                    seed=9)
+    out = {}
+    for bits in (64, 128):
+        enc = R.encode(torch.linspace(-20, 20, 257, dtype=torch.float64), 23, bits)
+        x = HV("b", enc if rank == 1 else _remote(bits))
+        X = rep.share(s, plc, x)
+        Y = rep.trunc_pr(s, rep.mul(s, X, X), 23)
+        D = rep.dot(s, rep.local(s, X, "Reshape", shape=(1, 257)),
+                    rep.local(s, X, "Reshape", shape=(257, 1)))
+        out[bits] = [t.s0.v.data.clone() for t in (X, Y, D)] + [t.s1.v.data.clone() for t in (X, Y, D)]
+    q.put((rank, {b: [t.numpy() for t in v] for b, v in out.items()}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _remote(bits):
+    from moose_amd.parallel.spmd import Remote
+
+    return Remote(bits)
+
+
+def test_spmd_shares_bitwise_equal_stacked():
+    from moose_amd.protocols import replicated as rep
+    from moose_amd.runtime.session import HV
+    from moose_amd.runtime.session import StackedSession
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_shares_worker, args=(r, port, q)) for r in range(3)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(3))
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    plc = ReplicatedPlacement(("a", "b", "c"))
+    s = StackedSession("cpu", seed=9)
+    s.fused = False
+    for bits in (64, 128):
+        enc = R.encode(torch.linspace(-20, 20, 257, dtype=torch.float64), 23, bits)
+        X = rep.share(s, plc, HV("b", enc))
+        Y = rep.trunc_pr(s, rep.mul(s, X, X), 23)
+        D = rep.dot(s, rep.local(s, X, "Reshape", shape=(1, 257)),
+                    rep.local(s, X, "Reshape", shape=(257, 1)))
+        stacked = [t.s0.v.data for t in (X, Y, D)] + [t.s1.v.data for t in (X, Y, D)]
+        for i, st in enumerate(stacked):
+            for p in range(3):
+                assert np.array_equal(res[p][bits][i], st[p].numpy()), (bits, i, p)
