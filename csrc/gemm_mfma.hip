@@ -163,26 +163,6 @@ __global__ void __launch_bounds__(256) k_prep_b(const T* __restrict__ B0, const 
   }
 }
 
-template <int L>
-__device__ inline void mfma_diagonals(const int8_t* __restrict__ As,
-                                      const int8_t* __restrict__ Bs, int arow, int brow,
-                                      int half, v16i (&acc)[L]) {
-  // All fragments of the k-step are requested up front so the LDS latency is paid once
-  // (hipcc then emits counted lgkmcnt waits instead of a full drain before every A limb);
-  // with one wave per SIMD nothing else would hide a per-limb wait.
-  v4i bf[L], af[L];
-#pragma unroll
-  for (int j = 0; j < L; ++j) bf[j] = *(const v4i*)(Bs + j * kTileBytes + swz(brow, half));
-#pragma unroll
-  for (int i = 0; i < L; ++i) af[i] = *(const v4i*)(As + i * kTileBytes + swz(arow, half));
-#pragma unroll
-  for (int i = 0; i < L; ++i) {
-#pragma unroll
-    for (int j = 0; j < L - i; ++j)
-      acc[i + j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[i], bf[j], acc[i + j], 0, 0, 0);
-  }
-}
-
 // XCD-aware remap of the flattened tile index: consecutive tiles of the same row band
 // land on the same XCD (blocks b and b+8 share an XCD under round-robin dispatch).
 __device__ inline int64_t xcd_remap(int64_t bid, int64_t nwg) {
@@ -249,19 +229,58 @@ __global__ void __launch_bounds__(256, 1)
                                        16, 0, 0);
     }
   };
-  // two LDS buffers; the DMA of stage kb+1 is in flight while stage kb is multiplied.  One
-  // barrier per k-step: after it every wave has finished reading buffer kb&1 (so it may be
-  // refilled with stage kb+2) and every wave's DMA of stage kb+1 has landed (vmcnt(0)).
+  // Two LDS buffers; the DMA of stage kb+1 is in flight while stage kb is multiplied.
+  // Within a k-step the A limbs are walked from L-1 down to 0 (1, 2, ..., L MFMAs each),
+  // so the step ends with the longest MFMA run (A_0 x all B).  The single barrier of the
+  // step sits right before that run: every wave has then finished reading buffer kb&1
+  // and its DMA of stage kb+1 has landed, so the B fragments of stage kb+1 (a second
+  // register set) and its first A fragment are read -- and stage kb+2's DMA is issued --
+  // while the last L MFMAs of stage kb execute.
+  const int aoff = swz(arow, half), boff = swz(brow, half);
+  constexpr int AP = 4;  // A limbs in flight ahead of their MFMAs
+  v4i bf0[L], bf1[L];
+  v4i ar[AP];            // ar[i % AP] holds A limb i of the current step
+  auto read_a = [&](const int8_t* As, int i) -> v4i {
+    return *(const v4i*)(As + i * kTileBytes + aoff);
+  };
+  auto kstep = [&](int64_t kb, v4i (&bc)[L], v4i (&bnx)[L]) {
+    const int cur = (int)(kb & 1);
+    const int8_t* As = buf(cur);
+#pragma unroll
+    for (int i = L - 1; i >= 1; --i) {
+      const v4i a = ar[i % AP];
+      if (i - AP >= 0) ar[(i - AP) % AP] = read_a(As, i - AP);
+#pragma unroll
+      for (int j = 0; j < L - i; ++j)
+        acc[i + j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bc[j], acc[i + j], 0, 0, 0);
+    }
+    const v4i a0 = ar[0];
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kb + 1 < nkb) {
+      const int8_t* nx = buf(cur ^ 1);
+#pragma unroll
+      for (int j = 0; j < L; ++j) bnx[j] = *(const v4i*)(nx + STAGE + j * kTileBytes + boff);
+#pragma unroll
+      for (int i = L - 1; i >= L - AP; --i) ar[i % AP] = read_a(nx, i);
+    }
+    if (kb + 2 < nkb) issue_stage(kb + 2, buf(cur));
+#pragma unroll
+    for (int j = 0; j < L; ++j)
+      acc[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bc[j], acc[j], 0, 0, 0);
+  };
   issue_stage(0, buf(0));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (nkb > 1) issue_stage(1, buf(1));
+#pragma unroll
+  for (int j = 0; j < L; ++j) bf0[j] = *(const v4i*)(buf(0) + STAGE + j * kTileBytes + boff);
+#pragma unroll
+  for (int i = L - 1; i >= L - AP; --i) ar[i % AP] = read_a(buf(0), i);
   for (int64_t kb = 0; kb < nkb; ++kb) {
-    const int cur = (int)(kb & 1);
-    mfma_diagonals<L>(buf(cur), buf(cur) + STAGE, arow, brow, half, acc);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (kb + 2 < nkb) issue_stage(kb + 2, buf(cur));
+    kstep(kb, bf0, bf1);
+#pragma unroll
+    for (int j = 0; j < L; ++j) bf0[j] = bf1[j];
   }
 
   // epilogue: C[row][col] = sum_d sext(acc_d) << 8d
