@@ -293,9 +293,27 @@ def _add_const(nb, x, value, bits):
 
 @prim("SampleSeeded")
 def _sample_seeded(nb, shape, seed, bits, device="cpu"):
-    """Uniform ring tensor expanded from a 16-byte seed with AES-128-CTR."""
-    out = R.prf_expand([bytes(seed)], 0, tuple(shape), bits, device)
+    """Uniform ring tensor expanded with AES-128-CTR from a seed: a fresh 16-byte key
+    (nonce 0) or a 32-byte ``DeriveSeed`` output key || nonce (reference
+    ``host/ops.rs:1883-2036`` + ``host/prim.rs:123-150``)."""
+    seed = bytes(seed)
+    key, nonce = seed[:16], int.from_bytes(seed[16:24], "little") if len(seed) > 16 else 0
+    out = R.prf_expand([key], nonce, tuple(shape), bits, device)
     return R.RT(out.data[0], bits)
+
+
+@prim("DeriveSeed")
+def _derive_seed(nb, key, sync_key):
+    """Seed for PRF(key, nonce): the key and the 16-byte sync key (nonce, little endian).
+    The PRF itself is keyed AES-CTR, so no hash is needed to separate streams."""
+    return bytes(key) + bytes(sync_key)
+
+
+@prim("PrfKeyGen")
+def _prf_key_gen(nb):
+    import os
+
+    return os.urandom(16)
 
 
 @prim("Sample")
