@@ -19,7 +19,7 @@ OPERATORS = {
     "And": [],
     "AtLeast2D": [("to_column_vector", "bool")],
     "BitExtract": [("bit_idx", "int")],
-    "Broadcast": [],
+    "Broadcast": [("shape", "opt_ints")],
     "Cast": [],
     "Concat": [("axis", "int")],
     "Constant": [("value", "const")],
@@ -40,7 +40,7 @@ OPERATORS = {
     "Ones": [],
     "Or": [],
     "PrfKeyGen": [],
-    "Reshape": [],
+    "Reshape": [("shape", "opt_ints")],
     "Receive": [("rendezvous_key", "key"), ("sender", "str")],
     "Relu": [],
     "RingFixedpointArgmax": [("axis", "int"), ("upmost_index", "int")],
@@ -115,6 +115,17 @@ EXTENSION_OPERATORS = {
     # logical right shift of a packed boolean word tensor along the bit axis
     "ShrWord": [("amount", "int")],
     "ShlWord": [("amount", "int")],
+    # host primitives of lowered graphs that the reference expresses with other ops
+    "Sar": [("amount", "int")],                      # arithmetic right shift
+    "AddConst": [("value", "const")],                # x + public ring constant
+    "RingCast": [],                                  # Z_2^128 -> Z_2^64 (width = ret type)
+    "FromBool": [],
+    "ToBool": [],
+    "RingToInt": [],
+    "IntToRing": [],
+    "BitSplit": [("start", "int"), ("count", "int")],  # packed word -> bit planes
+    "WeightedSum": [("weights", "ints"), ("bits", "int")],
+    "StridedSlice": [("slices", "ints")],
 }
 
 ALL_OPERATORS = {**OPERATORS, **EXTENSION_OPERATORS}

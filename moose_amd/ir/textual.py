@@ -175,7 +175,9 @@ def _parse_value(c: _Cursor, kind: str):
             c.eat("None")
             return None
         return int(c.match(_INT, "integer").group(0))
-    if kind == "ints":
+    if kind in ("ints", "opt_ints"):
+        if kind == "opt_ints" and c.eat("None"):
+            return None
         return [int(x) for x in _parse_nested(c, _num)]
     if kind == "const":
         if c.peek('"'):
@@ -246,7 +248,7 @@ def _parse_operation(c: _Cursor) -> Operation:
             c.eat(",")
     for an, ak in schema:
         if an not in attrs:
-            if ak == "opt_int":
+            if ak in ("opt_int", "opt_ints"):
                 attrs[an] = None
             elif kind == "Output" and an == "tag":
                 attrs[an] = name  # older files omit the tag (examples/test.moose)
@@ -324,7 +326,7 @@ def _print_value(v, kind):
         return "true" if v else "false"
     if kind in ("int", "opt_int"):
         return str(int(v))
-    if kind == "ints":
+    if kind in ("ints", "opt_ints"):
         return "[" + ", ".join(str(int(x)) for x in v) + "]"
     if kind == "const":
         return v.to_textual()

@@ -229,11 +229,14 @@ class Interpreter:
     def _plain(self, x: LV):
         """Python/plaintext value of a non-secret LV (shapes, strings, scalars)."""
         v = x.v
-        if isinstance(v, HV):
-            return v.v
-        if isinstance(v, MV):
-            return v.v
-        return v
+        if isinstance(v, (HV, MV)):
+            v = v.v
+        const = getattr(v, "const", None)  # symbolic value with a statically known value
+        return const if const is not None else v
+
+    @property
+    def symbolic(self) -> bool:
+        return getattr(self.sess, "symbolic", False)
 
     def _public(self, x: LV):
         return x.v.v if isinstance(x.v, MV) else None
@@ -281,6 +284,8 @@ class Interpreter:
 
     def op_Input(self, op, ins):
         name = op.attrs.get("arg_name") or op.name
+        if self.symbolic:
+            return self._symbolic_input(op, name)
         if name not in self.arguments:
             raise MooseRuntimeError(f"missing argument {name}")
         plc = op.placement
@@ -322,8 +327,41 @@ class Interpreter:
         elif x.kind == "tensor":
             # outputs pinned to a replicated / mirrored placement open to its first owner
             x = self.to_host(x, plc.owners[0])
-        self.outputs[op.attrs.get("tag") or op.name] = x
+        tag = op.attrs.get("tag") or op.name
+        if self.symbolic:
+            sess = self.sess
+            v = x.v.v if isinstance(x.v, (HV, MV)) else x.v
+            sess.output(x.plc.owner if x.is_host else plc.owners[0], tag,
+                        sess.lit(x.plc.owner if x.is_host else plc.owners[0], v))
+        self.outputs[tag] = x
         return x
+
+    def _symbolic_input(self, op, name):
+        """Lowering: an Input op of the lowered graph with the shape from ``arg_specs``."""
+        from moose_amd.compiler.symbolic import ring_ty
+
+        spec = self.arg_specs.get(name) if getattr(self, "arg_specs", None) else None
+        if spec is None:
+            raise MooseRuntimeError(
+                f"lowering needs the shape of argument {name!r} (pass arg_specs)")
+        shape, dtype = spec
+        plc = op.placement
+        host = plc.owner if isinstance(plc, HostPlacement) else plc.owners[0]
+        hp = HostPlacement(host)
+        want = op.sig.ret
+        d = dtype if dtype is not None else (want.dtype if want.name == "Tensor" else T.FLOAT64)
+        d = self._dtype(d)
+        if d.is_fixed:
+            ty, bits = ring_ty(d.ring_bits), d.ring_bits
+        else:
+            ty, bits = T.Ty({"Float64": "HostFloat64Tensor", "Float32": "HostFloat32Tensor",
+                             "Bool": "HostBitTensor", "Uint64": "HostUint64Tensor"}[d.kind]), None
+        lv = LV(hp, "tensor", d, HV(host, self.sess.input(host, name, ty, shape, bits)))
+        if want.name == "Tensor" and want.dtype.kind != "Unknown":
+            wd = self._dtype(want.dtype)
+            if wd != d:
+                lv = self._cast_host(lv, wd)
+        return lv if isinstance(plc, HostPlacement) else self.at(op, lv)
 
     def op_Identity(self, op, ins):
         return self.at(op, ins[0])

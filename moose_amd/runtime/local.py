@@ -92,7 +92,8 @@ class LocalMooseRuntime:
         if compiler_passes:
             from moose_amd.compiler import passes
 
-            comp = passes.compile(comp, compiler_passes)
+            comp = passes.compile(comp, compiler_passes, arg_specs=arg_specs_of(arguments),
+                                  fixedpoint_ring=self.fixedpoint_ring)
         return self.evaluate_compiled(comp, arguments)
 
     def evaluate_compiled(self, comp, arguments=None):
@@ -134,9 +135,19 @@ class LocalMooseRuntime:
 
 
 def _is_lowered(comp: Computation) -> bool:
-    """A computation is host-level when every op is on a host placement."""
-    from moose_amd.ir.computation import HostPlacement
+    """A computation is host-level when every op is on a host placement and no op
+    carries a logical (Tensor/Shape) type."""
+    from moose_amd.compiler.passes import is_lowered
 
-    return all(isinstance(op.placement, HostPlacement) for op in comp.operations) and any(
-        op.kind in ("Send", "Receive", "PrfKeyGen", "RingFixedpointEncode") for op in comp.operations
-    )
+    return is_lowered(comp)
+
+
+def arg_specs_of(arguments) -> dict:
+    """Shapes of concrete arguments (lowering is shape-specialised)."""
+    specs = {}
+    for k, v in (arguments or {}).items():
+        if isinstance(v, (str, bytes)):
+            continue
+        shape = tuple(v.shape) if hasattr(v, "shape") else tuple(np.shape(v))
+        specs[k] = (shape, None)
+    return specs

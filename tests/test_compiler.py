@@ -1,0 +1,149 @@
+"""Compiler passes (reference ``moose/src/compilation/*`` unit tests and the
+``tutorials/dotprod*.moose`` pipeline): lowering to a host graph + networking, then the
+lowered graph executes to the same values as the logical interpreter."""
+import io
+
+import numpy as np
+import pytest
+
+import moose_amd as pm
+from moose_amd.compiler import passes
+from moose_amd.ir import types as T
+from moose_amd.ir.computation import Computation
+from moose_amd.runtime.local import LocalMooseRuntime
+from moose_amd.runtime.local import to_native
+
+# the reference tutorial's logical dot product (tutorials/dotprod.moose)
+DOTPROD = """
+constant_0 = Constant{value = HostFloat64Tensor([[1.0, 2.0, 3.0]])}: () -> Tensor<Float64> () @Host(player0)
+cast_0 = Cast: (Tensor<Float64>) -> Tensor<Fixed128(24, 40)> (constant_0) @Host(player0)
+constant_1 = Constant{value = HostFloat64Tensor([[4.0], [5.0], [6.0]])}: () -> Tensor<Float64> () @Host(player1)
+cast_1 = Cast: (Tensor<Float64>) -> Tensor<Fixed128(24, 40)> (constant_1) @Host(player1)
+dot_0 = Dot: (Tensor<Fixed128(24, 40)>, Tensor<Fixed128(24, 40)>) -> Tensor<Fixed128(24, 40)> (cast_0, cast_1) @Replicated(player0, player1, player2)
+cast_2 = Cast: (Tensor<Fixed128(24, 40)>) -> Tensor<Float64> (dot_0) @Host(player2)
+output_0 = Output{tag = "output_0"}: (Tensor<Float64>) -> Tensor<Float64> (cast_2) @Host(player2)
+"""
+
+ROLES = ["player0", "player1", "player2"]
+
+
+def test_dotprod_tutorial_compiles_and_runs():
+    comp = Computation.from_textual(DOTPROD)
+    low = passes.compile(comp)
+    kinds = {op.kind for op in low.operations}
+    assert {"PrfKeyGen", "DeriveSeed", "SampleSeeded", "Send", "Receive"} <= kinds
+    assert passes.is_lowered(low)
+    passes.well_formed(low)
+    # the textual form of the lowered graph round-trips
+    txt = low.to_textual()
+    assert Computation.from_textual(txt).to_textual() == txt
+    rt = LocalMooseRuntime(ROLES, device="cpu")
+    out = rt.evaluate_compiled(Computation.from_textual(txt), {})
+    np.testing.assert_allclose(out["output_0"], [[32.0]], atol=1e-9)
+    # every Send has exactly one Receive and both ends are on different hosts
+    sends = {bytes(o.attrs["rendezvous_key"]): o for o in low.operations if o.kind == "Send"}
+    recvs = {bytes(o.attrs["rendezvous_key"]): o for o in low.operations if o.kind == "Receive"}
+    assert sends.keys() == recvs.keys()
+    for k, s in sends.items():
+        assert s.placement.owner != recvs[k].placement.owner
+        assert s.attrs["receiver"] == recvs[k].placement.owner
+
+
+def _nonlinear():
+    fp = pm.fixed(14, 23)
+    alice, bob, carole = (pm.host_placement(n) for n in ("alice", "bob", "carole"))
+    rep = pm.replicated_placement("rep", players=[alice, bob, carole])
+
+    @pm.computation
+    def f(x: pm.Argument(placement=alice, vtype=pm.TensorType(pm.float64)),
+          y: pm.Argument(placement=bob, vtype=pm.TensorType(pm.float64))):
+        with alice:
+            xf = pm.cast(x, dtype=fp)
+        with bob:
+            yf = pm.cast(y, dtype=fp)
+        with rep:
+            z = pm.dot(xf, yf)
+            s = pm.sigmoid(z)
+            c = pm.less(z, s)
+            am = pm.argmax(z, axis=1, upmost_index=2)
+            r = pm.relu(z)
+        with carole:
+            return (pm.cast(z, dtype=pm.float64), pm.cast(s, dtype=pm.float64),
+                    pm.cast(r, dtype=pm.float64), pm.identity(c), pm.identity(am))
+
+    return f
+
+
+def test_lowered_graph_matches_interpreter():
+    f = _nonlinear()
+    rng = np.random.default_rng(0)
+    args = {"x": rng.uniform(-1, 1, (3, 4)), "y": rng.uniform(-1, 1, (4, 2))}
+    rt = LocalMooseRuntime(["alice", "bob", "carole"], device="cpu")
+    ref = rt.evaluate_computation(f, args)
+    got = rt.evaluate_computation(f, args, compiler_passes=passes.DEFAULT_PASSES)
+    assert set(got) == set(ref)
+    for k in ref:
+        np.testing.assert_allclose(np.asarray(got[k], dtype=float),
+                                   np.asarray(ref[k], dtype=float), atol=1e-5)
+
+
+def test_lowering_requires_input_shapes():
+    with pytest.raises(Exception, match="shape"):
+        passes.compile(to_native(_nonlinear()))
+
+
+def test_typing_fills_unknown_argument_types():
+    src = """
+x = Constant{value = HostFloat64Tensor([1.0, 2.0])}: () -> Tensor<Float64> () @Host(alice)
+y = Add: (Tensor, Tensor) -> Tensor<Float64> (x, x) @Host(alice)
+"""
+    comp = passes.typing_pass(Computation.from_textual(src))
+    y = comp.by_name()["y"]
+    assert y.sig.args == (T.Ty("Tensor", T.FLOAT64), T.Ty("Tensor", T.FLOAT64))
+
+
+def test_deprecated_shape():
+    src = ('shape_0 = Shape: (Tensor<Fixed128(24, 40)>) -> HostShape (x) @Host(bob)\n'
+           'x = Constant{value = HostFloat64Tensor([1.0])}: () -> Tensor<Fixed128(24, 40)> () @Host(bob)')
+    comp = passes.deprecated_shape(Computation.from_textual(src))
+    assert comp.by_name()["shape_0"].sig.ret == T.Ty("Shape", "Host")
+
+
+def test_prune_and_toposort_and_dot():
+    src = """
+z = Output{tag = "z"}: (HostFloat64Tensor) -> HostFloat64Tensor (b) @Host(alice)
+b = Add: (HostFloat64Tensor, HostFloat64Tensor) -> HostFloat64Tensor (a, a) @Host(alice)
+a = Constant{value = HostFloat64Tensor([1.0])}: () -> HostFloat64Tensor () @Host(alice)
+dead = Constant{value = HostFloat64Tensor([2.0])}: () -> HostFloat64Tensor () @Host(alice)
+"""
+    comp = passes.prune(Computation.from_textual(src))
+    assert [op.name for op in comp.operations if op.name == "dead"] == []
+    comp = passes.toposort(comp)
+    assert [op.name for op in comp.operations] == ["a", "b", "z"]
+    passes.well_formed(comp)
+    buf = io.StringIO()
+    passes.print_graph(comp, out=buf)
+    assert buf.getvalue().startswith("digraph {") and '"a" -> "b"' in buf.getvalue()
+
+
+def test_well_formed_rejects_bad_order_and_unknown_pass():
+    src = """
+b = Add: (HostFloat64Tensor, HostFloat64Tensor) -> HostFloat64Tensor (a, a) @Host(alice)
+a = Constant{value = HostFloat64Tensor([1.0])}: () -> HostFloat64Tensor () @Host(alice)
+"""
+    with pytest.raises(passes.CompilationError):
+        passes.well_formed(Computation.from_textual(src))
+    with pytest.raises(passes.CompilationError, match="Unknown pass"):
+        passes.compile(Computation.from_textual(src), ["nope"])
+
+
+def test_networking_dedups_per_destination():
+    src = """
+a = Constant{value = HostFloat64Tensor([1.0])}: () -> HostFloat64Tensor () @Host(alice)
+b = Add: (HostFloat64Tensor, HostFloat64Tensor) -> HostFloat64Tensor (a, a) @Host(bob)
+c = Add: (HostFloat64Tensor, HostFloat64Tensor) -> HostFloat64Tensor (a, b) @Host(bob)
+d = Add: (HostFloat64Tensor, HostFloat64Tensor) -> HostFloat64Tensor (a, a) @Host(carole)
+"""
+    comp = passes.networking(Computation.from_textual(src))
+    assert sum(op.kind == "Send" for op in comp.operations) == 2  # a->bob once, a->carole once
+    passes.well_formed(comp.toposorted())
