@@ -41,13 +41,21 @@ def _enc_attr(v):
             return {"__c": v.kind, "nd": payload}
         if isinstance(val, tuple):
             val = list(val)
-        return {"__c": v.kind, "v": val}
+        return {"__c": v.kind, "v": _enc_attr(val)}
     if isinstance(v, tuple):
-        return {"__t": list(v)}
+        return {"__t": [_enc_attr(x) for x in v]}
+    if isinstance(v, list):
+        return [_enc_attr(x) for x in v]
+    if isinstance(v, int) and not isinstance(v, bool) and not -(1 << 63) <= v < (1 << 64):
+        return {"__i": str(v)}  # ring constants / weights wider than msgpack ints
     return v
 
 
 def _dec_attr(v):
+    if isinstance(v, list):
+        return [_dec_attr(x) for x in v]
+    if isinstance(v, dict) and "__i" in v:
+        return int(v["__i"])
     if isinstance(v, dict) and "__c" in v:
         if "nd" in v:
             p = v["nd"]
@@ -56,12 +64,12 @@ def _dec_attr(v):
             else:
                 arr = np.frombuffer(p["b"], dtype=np.dtype(p["dt"])).reshape(p["shape"]).copy()
             return Constant(v["__c"], arr)
-        val = v["v"]
+        val = _dec_attr(v["v"])
         if v["__c"] == "HostShape" or v["__c"] == "Fixed":
             val = tuple(val)
         return Constant(v["__c"], val)
     if isinstance(v, dict) and "__t" in v:
-        return tuple(v["__t"])
+        return tuple(_dec_attr(x) for x in v["__t"])
     return v
 
 

@@ -68,12 +68,29 @@ def run_spmd(comp: Computation, arguments: dict, identities: List[str], *, rank:
     from moose_amd.parallel.transport import Transport
     from moose_amd.runtime.interpreter import Interpreter
 
+    from moose_amd.compiler.passes import is_lowered
+
     identity = identities[rank]
     role_ranks = {r: i for i, r in enumerate(identities)}
     device = torch.device(device) if device is not None else torch.device("cpu")
     tr = Transport(rank, len(identities), device, group=group)
-    sess = SPMDSession(identity, role_ranks, tr, device=device, seed=seed)
     store = storage if storage is not None else {}
+    if is_lowered(comp):
+        # a compiled host graph: run this identity's operations, Send/Receive over RCCL
+        # (the reference's per-identity AsyncExecutor on a lowered computation)
+        from moose_amd.runtime.graph_executor import GraphExecutor
+
+        ex = GraphExecutor(device, store, identity=identity, transport=tr, role_ranks=role_ranks)
+        dist.barrier(group=group)
+        t0 = time.perf_counter()
+        raw = ex.run(comp, arguments)
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        elapsed = int((time.perf_counter() - t0) * 1e6)
+        from moose_amd.utils.telemetry import SessionStats
+
+        return {k: _host_numpy(v) for k, v in raw.items()}, SessionStats(), elapsed
+    sess = SPMDSession(identity, role_ranks, tr, device=device, seed=seed)
     interp = Interpreter(sess, store, fixedpoint_ring)
     dist.barrier(group=group)
     t0 = time.perf_counter()
@@ -127,7 +144,10 @@ class DistributedMooseRuntime:
         if compiler_passes:
             from moose_amd.compiler import passes
 
-            comp = passes.compile(comp, compiler_passes)
+            from moose_amd.runtime.local import arg_specs_of
+
+            comp = passes.compile(comp, compiler_passes, arg_specs=arg_specs_of(arguments),
+                                  fixedpoint_ring=self.fixedpoint_ring)
         return self._launch(comp, dict(arguments or {}))
 
     # mirrors pymoose's GrpcMooseRuntime.run_computation -> (outputs, timings)
@@ -192,6 +212,17 @@ class DistributedMooseRuntime:
 
     def write_value_to_storage(self, identity, key, value):
         self.storage[identity][key] = np.asarray(value) if not isinstance(value, str) else value
+
+
+def _host_numpy(v):
+    """Output value of a lowered graph -> numpy (ring tensors as integers)."""
+    from moose_amd.ops import ring as R
+
+    if isinstance(v, R.RT):
+        return np.asarray(R.to_ints(v))
+    if isinstance(v, torch.Tensor):
+        return v.detach().cpu().numpy()
+    return v
 
 
 def _encodable(d: dict) -> dict:

@@ -105,8 +105,12 @@ class LocalMooseRuntime:
             ex = GraphExecutor(self.device, self.storage)
             t0 = time.perf_counter()
             outs = ex.run(comp, arguments)
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
             self.last_timings = {i: int((time.perf_counter() - t0) * 1e6) for i in self.identities}
-            return outs
+            from moose_amd.runtime.distributed import _host_numpy
+
+            return {k: _host_numpy(v) for k, v in outs.items()}
         sess = StackedSession(self.device, seed=self.seed)
         interp = Interpreter(sess, self.storage, self.fixedpoint_ring)
         t0 = time.perf_counter()
