@@ -1,0 +1,287 @@
+"""Choreography: long-running party workers that execute sessions on request.
+
+Parity:
+
+* gRPC choreography + ``comet`` worker (``choreography/grpc.rs:34-233``,
+  ``bin/comet/comet.rs``): ``launch_computation`` (duplicate session ids rejected),
+  ``retrieve_results`` (blocks until done, returns outputs + elapsed time),
+  ``abort_computation``;
+* ``cometctl`` client (``bin/comet/cometctl.rs``) and ``GrpcMooseRuntime``;
+* filesystem choreography (``choreography/filesystem.rs:28-259``, ``rudolph``): a
+  directory of ``<session-id>.session`` TOML files (``[computation] path, format`` and
+  ``[[roles]] name, endpoint``) is watched and every new file is launched.
+
+MI355X design: the control plane is a ``torch.distributed.TCPStore`` (native C++
+key-value server hosted by worker rank 0); the data plane is the workers' process
+group (RCCL between GPUs, gloo on CPU) -- the same one the SPMD session uses, so a
+session costs no connection setup.  Keys::
+
+    moosex/worker/<rank>            -> identity of that worker
+    moosex/launch_count             -> number of launched sessions (atomic add)
+    moosex/session/<n>              -> n-th job (valuecodec: sid, computation, args, ...)
+    moosex/result/<sid>/<identity>  -> that identity's outputs / error / elapsed_us
+    moosex/abort/<sid>              -> abort request
+"""
+from __future__ import annotations
+
+import glob
+import os
+import threading
+import time
+import traceback
+from datetime import timedelta
+from typing import Dict
+from typing import List
+from typing import Optional
+
+import numpy as np
+
+from moose_amd.utils import valuecodec
+
+PREFIX = "moosex"
+
+
+def _store(addr: str, is_master: bool, world: Optional[int] = None, timeout=3600):
+    import torch.distributed as dist
+
+    host, _, port = addr.rpartition(":")
+    return dist.TCPStore(host or "127.0.0.1", int(port), world_size=world, is_master=is_master,
+                         timeout=timedelta(seconds=timeout), wait_for_workers=False)
+
+
+def _get(store, key: str) -> bytes:
+    return bytes(store.get(key))
+
+
+def _has(store, key: str) -> bool:
+    return store.check([key])
+
+
+# ---------------------------------------------------------------------------
+# worker
+# ---------------------------------------------------------------------------
+class Worker:
+    """One identity of a group of choreographed workers (rank 0 hosts the store)."""
+
+    def __init__(self, identity: str, rank: int, world: int, store_addr: str,
+                 backend: str = "gloo", storage_dir: Optional[str] = None):
+        import torch
+        import torch.distributed as dist
+
+        from moose_amd.runtime.distributed import party_device
+
+        self.identity = identity
+        self.rank = rank
+        self.world = world
+        self.store = _store(store_addr, rank == 0, world)
+        self.store.set(f"{PREFIX}/worker/{rank}", identity)
+        self.backend = backend
+        self.device = party_device(backend, int(os.environ.get("LOCAL_RANK", rank)))
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        if not dist.is_initialized():
+            dist.init_process_group(backend, store=dist.PrefixStore("pg", self.store),
+                                    rank=rank, world_size=world)
+        self.identities = [_get(self.store, f"{PREFIX}/worker/{r}").decode() for r in range(world)]
+        self.storage_dir = storage_dir
+        self.storage: Dict[str, object] = {}
+        self.seen = set()
+
+    def serve(self, max_sessions: Optional[int] = None, poll_s: float = 0.05) -> int:
+        n = 0
+        while max_sessions is None or n < max_sessions:
+            key = f"{PREFIX}/session/{n}"
+            while not _has(self.store, key):
+                time.sleep(poll_s)
+            job = valuecodec.loads(_get(self.store, key))
+            n += 1
+            if job.get("shutdown"):
+                break
+            self._run(job)
+        return 0
+
+    def _run(self, job):
+        import torch.distributed as dist
+
+        from moose_amd.ir.computation import Computation
+        from moose_amd.runtime.distributed import run_spmd
+
+        sid = job["session_id"]
+        rkey = f"{PREFIX}/result/{sid}/{self.identity}"
+        if sid in self.seen:  # choreography/grpc.rs:114-118
+            self.store.set(rkey, valuecodec.dumps({"error": f"session {sid} already exists"}))
+            return
+        self.seen.add(sid)
+        # rank 0 decides whether an abort request arrived before the start, so every
+        # worker takes the same branch
+        import torch
+
+        flag = torch.tensor([1 if (self.rank == 0 and _has(self.store, f"{PREFIX}/abort/{sid}"))
+                             else 0], device=self.device)
+        dist.broadcast(flag, 0)
+        if int(flag.item()):
+            self.store.set(rkey, valuecodec.dumps({"error": "aborted"}))
+            return
+        try:
+            comp = Computation.from_msgpack(job["computation"])
+            roles = job.get("role_assignment") or {}
+            # identities in rank order, renamed to the computation's roles
+            inv = {ident: role for role, ident in roles.items()}
+            idents = [inv.get(i, i) for i in self.identities]
+            storage = {idents[self.rank]: self._load_storage()}
+            outs, stats, elapsed = run_spmd(comp, job.get("arguments", {}), idents,
+                                            rank=self.rank, device=self.device,
+                                            fixedpoint_ring=job.get("fixedpoint_ring", 128),
+                                            storage=storage)
+            self._save_storage(storage.get(idents[self.rank], {}))
+            res = {"outputs": {k: np.asarray(v) for k, v in outs.items()},
+                   "elapsed_us": elapsed, "rounds": stats.rounds}
+        except Exception as e:  # report, keep serving
+            res = {"error": f"{type(e).__name__}: {e}", "trace": traceback.format_exc()[-4000:]}
+        self.store.set(rkey, valuecodec.dumps(res))
+
+    def _load_storage(self):
+        if self.storage_dir is None:
+            return dict(self.storage)
+        from moose_amd.utils.storage import load_from_path
+
+        out = {}
+        for p in glob.glob(os.path.join(self.storage_dir, "*.npy")):
+            out[os.path.basename(p)[:-4]] = load_from_path(p)
+        return out
+
+    def _save_storage(self, store):
+        for k, v in store.items():
+            if self.storage_dir is None:
+                self.storage[k] = v
+            elif isinstance(v, np.ndarray):
+                np.save(os.path.join(self.storage_dir, f"{k}.npy"), v, allow_pickle=False)
+
+
+# ---------------------------------------------------------------------------
+# client
+# ---------------------------------------------------------------------------
+class ChoreographyClient:
+    """``cometctl`` / ``GrpcMooseRuntime`` analogue talking to the workers' store."""
+
+    def __init__(self, store_addr: str, timeout: float = 3600):
+        self.store = _store(store_addr, False, None, timeout)
+        self.timeout = timeout
+
+    def worker_identities(self, world: int) -> List[str]:
+        return [_get(self.store, f"{PREFIX}/worker/{r}").decode() for r in range(world)]
+
+    def launch_computation(self, session_id: str, computation, arguments=None,
+                           role_assignment=None, fixedpoint_ring: int = 128):
+        from moose_amd.runtime.local import to_native
+
+        if self.store.add(f"{PREFIX}/sid/{session_id}", 1) > 1:  # choreography/grpc.rs:114
+            raise RuntimeError(f"session {session_id} already exists")
+        comp = to_native(computation, fixedpoint_ring)
+        job = {"session_id": str(session_id), "computation": comp.to_msgpack(),
+               "arguments": _plain_args(arguments or {}),
+               "role_assignment": dict(role_assignment or {}),
+               "fixedpoint_ring": fixedpoint_ring}
+        n = self.store.add(f"{PREFIX}/launch_count", 1) - 1
+        self.store.set(f"{PREFIX}/session/{n}", valuecodec.dumps(job))
+        return n
+
+    def retrieve_results(self, session_id: str, identities: List[str], timeout=None):
+        deadline = time.time() + (timeout or self.timeout)
+        outputs, timings = {}, {}
+        for ident in identities:
+            key = f"{PREFIX}/result/{session_id}/{ident}"
+            while not _has(self.store, key):
+                if time.time() > deadline:
+                    raise TimeoutError(f"no result from {ident} for session {session_id}")
+                time.sleep(0.05)
+            res = valuecodec.loads(_get(self.store, key))
+            if "error" in res:
+                raise RuntimeError(f"{ident}: {res['error']}\n{res.get('trace', '')}")
+            outputs.update(res["outputs"])
+            timings[ident] = res["elapsed_us"]
+        return outputs, timings
+
+    def abort_computation(self, session_id: str):
+        self.store.set(f"{PREFIX}/abort/{session_id}", b"1")
+
+    def run_computation(self, session_id, computation, arguments, identities, role_assignment=None):
+        self.launch_computation(session_id, computation, arguments, role_assignment)
+        return self.retrieve_results(session_id, identities)
+
+    def shutdown(self):
+        n = self.store.add(f"{PREFIX}/launch_count", 1) - 1
+        self.store.set(f"{PREFIX}/session/{n}", valuecodec.dumps({"shutdown": True}))
+
+
+def _plain_args(d):
+    import torch
+
+    out = {}
+    for k, v in d.items():
+        if isinstance(v, torch.Tensor):
+            v = v.detach().cpu().numpy()
+        elif isinstance(v, list):
+            v = np.asarray(v)
+        out[k] = v
+    return out
+
+
+# ---------------------------------------------------------------------------
+# filesystem choreography
+# ---------------------------------------------------------------------------
+def parse_session_file(path: str) -> dict:
+    """``[computation] path = ..., format = "textual"|"msgpack"`` and
+    ``[[roles]] name = ..., endpoint = ...`` (reference examples/test.session)."""
+    import tomli
+
+    with open(path, "rb") as f:
+        d = tomli.load(f)
+    comp = d.get("computation", {})
+    cpath = comp["path"]
+    if not os.path.isabs(cpath):
+        cpath = os.path.join(os.path.dirname(os.path.abspath(path)), cpath)
+    roles = {r["name"]: r.get("endpoint", r["name"]) for r in d.get("roles", [])}
+    return {"session_id": os.path.splitext(os.path.basename(path))[0],
+            "computation_path": cpath, "format": comp.get("format", "textual"), "roles": roles}
+
+
+def watch_sessions(sessions_dir: str, client: ChoreographyClient, world: int,
+                   stop: threading.Event, poll_s: float = 0.2, log=print):
+    """Launch every new ``*.session`` file in ``sessions_dir`` (session id = stem) and log
+    its outputs when done (choreography/filesystem.rs)."""
+    from moose_amd.cli.common import read_computation
+
+    launched = set()
+    idents = client.worker_identities(world)
+    while not stop.is_set():
+        for p in sorted(glob.glob(os.path.join(sessions_dir, "*.session"))):
+            if p in launched:
+                continue
+            launched.add(p)
+            try:
+                s = parse_session_file(p)
+                comp = read_computation(s["computation_path"], s["format"])
+                # roles are mapped to the workers whose identity is the role's endpoint name
+                ra = {role: ep.split(":")[0] if ep not in idents else ep
+                      for role, ep in s["roles"].items()}
+                ra = {role: (ident if ident in idents else role) for role, ident in ra.items()}
+                client.launch_computation(s["session_id"], comp, {}, ra)
+                outs, timings = client.retrieve_results(s["session_id"], idents)
+                log(f"session {s['session_id']}: outputs {sorted(outs)} timings {timings}")
+                for k, v in outs.items():
+                    np.save(os.path.join(sessions_dir, f"{s['session_id']}.{k}.npy"),
+                            np.asarray(v), allow_pickle=False)
+            except Exception as e:
+                log(f"session {os.path.basename(p)} failed: {e}")
+        stop.wait(poll_s)
+
+
+def serve(identity: Optional[str], backend: Optional[str]) -> int:
+    """Entry used by ``python -m moose_amd.runtime.worker --serve`` (env: RANK,
+    WORLD_SIZE, MOOSEX_STORE=host:port)."""
+    rank = int(os.environ["RANK"])
+    world = int(os.environ["WORLD_SIZE"])
+    addr = os.environ.get("MOOSEX_STORE", "127.0.0.1:29600")
+    w = Worker(identity or f"worker{rank}", rank, world, addr, backend or "gloo")
+    return w.serve()
