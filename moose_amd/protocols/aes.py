@@ -1,0 +1,213 @@
+"""AES-GCM-128 single-block decryption, on a host or inside the replicated placement.
+
+Parity: reference ``encrypted/ops.rs:312-393`` (``aesgcm``) + ``replicated/aes.rs`` +
+``host`` AES kernels.  The ciphertext of a fixed-point value is 224 bits: a 96-bit
+nonce followed by the 128-bit masked plaintext ``m ^ AES_k(nonce || 0^30 10)`` (GCM
+counter value 2).  The plaintext bit string, MSB first, is the Z_2^128 encoding of the
+fixed-point value.
+
+* host: one native AES-128 call over all counter blocks (AES-NI on the CPU);
+* replicated: the key is a boolean sharing of its 128 bits, the ciphertext is shared by
+  its owner, AES runs as the levelled circuit of :mod:`moose_amd.protocols.aes_circuit`
+  (40 AND rounds for any batch size), and the 128 plaintext bits are converted to one
+  arithmetic Z_2^128 sharing with a single batched B2A plus a local weighted sum.
+"""
+from __future__ import annotations
+
+from functools import lru_cache
+
+import numpy as np
+import torch
+
+from moose_amd.ir.computation import HostPlacement
+from moose_amd.ir.computation import ReplicatedPlacement
+from moose_amd.ops import ring as R
+from moose_amd.protocols import replicated as rep
+from moose_amd.runtime.session import HV
+from moose_amd.runtime.values import LV
+
+NONCE_BITS = 96
+BLOCK_BITS = 128
+CT_BITS = NONCE_BITS + BLOCK_BITS
+
+
+@lru_cache(maxsize=1)
+def levelled_aes():
+    from moose_amd.protocols.aes_circuit import aes128_circuit
+    from moose_amd.protocols.bristol import LevelledCircuit
+
+    return LevelledCircuit(aes128_circuit())
+
+
+def _bits_to_bytes(bits: np.ndarray) -> np.ndarray:
+    """[..., 8k] {0,1} MSB-first -> [..., k] uint8."""
+    return np.packbits(bits.astype(np.uint8), axis=-1)
+
+
+def _bytes_to_bits(b: np.ndarray) -> np.ndarray:
+    return np.unpackbits(b.astype(np.uint8), axis=-1)
+
+
+def counter_blocks(nonce_bits: np.ndarray) -> np.ndarray:
+    """[..., 96] nonce bits -> [..., 16] counter-block bytes (nonce || 00 00 00 02)."""
+    nb = _bits_to_bytes(nonce_bits)
+    ctr = np.zeros(nb.shape[:-1] + (4,), dtype=np.uint8)
+    ctr[..., 3] = 2
+    return np.concatenate([nb, ctr], axis=-1)
+
+
+def bits_msb_to_ring128(bits: np.ndarray, device) -> R.RT:
+    """[..., 128] plaintext bits (MSB first) -> Z_2^128 ring tensor of shape [...]."""
+    by = _bits_to_bytes(bits)  # [..., 16] big endian
+    hi = by[..., :8].copy().view(">u8")[..., 0].astype(np.uint64)
+    lo = by[..., 8:].copy().view(">u8")[..., 0].astype(np.uint64)
+    d = np.stack([lo.view(np.int64), hi.view(np.int64)], axis=-1)
+    return R.RT(torch.as_tensor(d, device=device), 128)
+
+
+def host_decrypt(key_bits, ct_bits, device="cpu") -> R.RT:
+    """Plaintext AES-GCM single-block decryption of a [..., 224]-bit ciphertext."""
+    key_bits = np.asarray(key_bits.cpu() if isinstance(key_bits, torch.Tensor) else key_bits)
+    ct = np.asarray(ct_bits.cpu() if isinstance(ct_bits, torch.Tensor) else ct_bits).astype(np.uint8)
+    if key_bits.shape[-1] != 128 or ct.shape[-1] != CT_BITS:
+        raise ValueError("AES-GCM decrypt expects a 128-bit key and 224-bit ciphertexts")
+    key = bytes(_bits_to_bytes(key_bits.reshape(128)).tolist())
+    blocks = counter_blocks(ct[..., :NONCE_BITS])
+    flat = np.ascontiguousarray(blocks.reshape(-1, 16))
+    import ctypes
+
+    from moose_amd.ops import native as nat
+
+    out = ctypes.create_string_buffer(flat.size)
+    nat.check(nat.lib().mx_aes_encrypt_blocks(nat.key_buffer([key]), flat.ctypes.data, out,
+                                              flat.shape[0]), "aes")
+    ks = np.frombuffer(out.raw, dtype=np.uint8).reshape(blocks.shape)
+    m = _bytes_to_bits(_bits_to_bytes(ct[..., NONCE_BITS:]) ^ ks)
+    return bits_msb_to_ring128(m, device)
+
+
+def encrypt_fixed(key: bytes, values: np.ndarray, frac: int, nonces=None) -> np.ndarray:
+    """Test/helper: encode floats as Z_2^128 fixed-point and encrypt them into
+    [..., 224]-bit ciphertexts (the client-side counterpart of decrypt)."""
+    values = np.asarray(values, dtype=np.float64)
+    enc = R.to_ints(R.encode(torch.as_tensor(values), frac, 128))
+    plain = np.asarray([int(v).to_bytes(16, "big") for v in np.asarray(enc).reshape(-1)],
+                       dtype=object)
+    pb = np.frombuffer(b"".join(plain.tolist()), dtype=np.uint8).reshape(values.shape + (16,))
+    if nonces is None:
+        nonces = np.random.default_rng().integers(0, 256, values.shape + (12,), dtype=np.uint8)
+    ctr = np.concatenate([nonces, np.zeros(values.shape + (4,), np.uint8)], axis=-1)
+    ctr[..., 15] = 2
+    ks = np.frombuffer(b"".join(R.aes_encrypt(key, bytes(b)) for b in ctr.reshape(-1, 16)),
+                       dtype=np.uint8).reshape(ctr.shape)
+    return np.concatenate([_bytes_to_bits(nonces), _bytes_to_bits(pb ^ ks)], axis=-1)
+
+
+def rep_decrypt(sess, plc: ReplicatedPlacement, key: rep.RepTensor, ct: rep.RepTensor) -> rep.RepTensor:
+    """Secure decryption: key [128] and ciphertext [..., 224] are boolean bit sharings;
+    returns the arithmetic Z_2^128 sharing of the plaintexts [...]."""
+    lc = levelled_aes()
+    batch = sess.p_shape(ct.s0)[:-1]
+    # circuit input [256, *batch]: key bits broadcast + counter block bits
+    kb = rep.local(sess, key, "Reshape", shape=(128,) + (1,) * len(batch))
+    kb = rep.local(sess, kb, "Broadcast", shape=(128,) + tuple(batch))
+    ctw = rep.local(sess, ct, "Transpose") if len(batch) == 1 else _wire_major(sess, ct)
+    nonce = _slice_rows(sess, ctw, 0, NONCE_BITS)
+    rm = _slice_rows(sess, ctw, NONCE_BITS, CT_BITS)
+    ctr = np.zeros((32,) + tuple(batch), dtype=np.uint8)
+    ctr[30] = 1  # counter value 2 in the last 32 bits (MSB first)
+    ctr_sh = rep.from_public(sess, plc, R.RT(torch.as_tensor(ctr, device=sess.device), 1), 1,
+                             kind="bool")
+    inp = _concat_rows(sess, [kb, nonce, ctr_sh])
+    r = lc.eval_shared(sess, inp)  # [128, *batch]
+    m = rep.xor(sess, rm, r)
+    a = rep.b2a(sess, m, 128)  # one batched B2A over all 128 bit planes
+    weights = [1 << (127 - i) for i in range(128)]
+    return rep.RepTensor(plc, 128, "arith",
+                         sess.p("WeightedSum", plc, a.s0, weights=weights, bits=128),
+                         sess.p("WeightedSum", plc, a.s1, weights=weights, bits=128))
+
+
+def _wire_major(sess, ct):
+    n = len(sess.p_shape(ct.s0))
+    perm = (n - 1,) + tuple(range(n - 1))
+    return rep.local(sess, ct, "Permute", perm=perm)
+
+
+def _slice_rows(sess, x, a, b):
+    return rep.local(sess, x, "Slice", slice=(a, b, None))
+
+
+def _concat_rows(sess, xs):
+    plc = xs[0].plc
+    return rep.RepTensor(plc, 1, "bool", sess.p("Concat", plc, *[x.s0 for x in xs], axis=0),
+                         sess.p("Concat", plc, *[x.s1 for x in xs], axis=0))
+
+
+# ---------------------------------------------------------------------------
+# interpreter hooks
+# ---------------------------------------------------------------------------
+def key_input(interp, op, name):
+    """AesKey argument: on a host a [128] bit array; on a replicated placement the
+    pre-shared ``name/<role>/share<i>`` bit arrays (reference replicated/input.rs)."""
+    plc = op.placement
+    sess = interp.sess
+    args = interp.arguments
+    if isinstance(plc, HostPlacement):
+        v = _bit_rt(args[name], sess.device)
+        return LV(plc, "aeskey", None, HV(plc.owner, v))
+    o = plc.owners
+    comps0, comps1 = [], []
+    for p in range(3):
+        a = args.get(f"{name}/{o[p]}/share{p}")
+        b = args.get(f"{name}/{o[p]}/share{(p + 1) % 3}")
+        if a is None or b is None:
+            raise KeyError(f"missing pre-shared key argument {name}/{o[p]}/share*")
+        comps0.append(HV(o[p], _bit_rt(a, sess.device)))
+        comps1.append(HV(o[p], _bit_rt(b, sess.device)))
+    t = rep.RepTensor(plc, 1, "bool", sess.gather(plc, comps0), sess.gather(plc, comps1))
+    return LV(plc, "aeskey", None, t)
+
+
+def tensor_input(interp, op, name):
+    plc = op.placement
+    host = plc.owner if isinstance(plc, HostPlacement) else plc.owners[0]
+    v = _bit_rt(interp.arguments[name], interp.sess.device)
+    return LV(HostPlacement(host), "aestensor", None, HV(host, v))
+
+
+def _bit_rt(a, device):
+    t = torch.as_tensor(np.asarray(a).astype(np.uint8), device=device)
+    return R.RT(t, 1)
+
+
+def decrypt_logical(interp, op, key: LV, ct: LV) -> LV:
+    from moose_amd.protocols.fixedpoint import RepFixed
+
+    sess = interp.sess
+    plc = op.placement
+    dtype = interp._ret_dtype(op)
+    if isinstance(plc, HostPlacement):
+        host = plc.owner
+        kv = _key_on_host(interp, key, host)
+        cv = sess.move(ct.v, host) if ct.is_host else None
+        pt = host_decrypt(kv.v.data, cv.v.data, sess.device)
+        return LV(plc, "tensor", dtype, HV(host, pt))
+    if not isinstance(plc, ReplicatedPlacement):
+        raise NotImplementedError("decrypt is supported on host and replicated placements")
+    k = key.v if key.is_rep else rep.share(sess, plc, key.v, kind="bool")
+    c = rep.share(sess, plc, ct.v, kind="bool") if ct.is_host else ct.v
+    t = rep_decrypt(sess, plc, k, c)
+    if dtype is not None and dtype.is_fixed:
+        if dtype.ring_bits != 128:
+            t = rep.ring_cast(sess, t, dtype.ring_bits)
+        return LV(plc, "tensor", dtype, RepFixed(t, dtype.fractional_precision,
+                                                  dtype.integral_precision))
+    return LV(plc, "tensor", dtype, t)
+
+
+def _key_on_host(interp, key: LV, host):
+    sess = interp.sess
+    if key.is_host:
+        return sess.move(key.v, host)
+    return rep.reveal(sess, key.v, host)

@@ -286,6 +286,15 @@ class Interpreter:
         name = op.attrs.get("arg_name") or op.name
         if self.symbolic:
             return self._symbolic_input(op, name)
+        rname = op.sig.ret.name
+        if rname in ("AesKey", "HostAesKey", "ReplicatedAesKey"):
+            from moose_amd.protocols import aes
+
+            return aes.key_input(self, op, name)
+        if rname in ("AesTensor", "Fixed128AesTensor", "HostFixed128AesTensor"):
+            from moose_amd.protocols import aes
+
+            return aes.tensor_input(self, op, name)
         if name not in self.arguments:
             raise MooseRuntimeError(f"missing argument {name}")
         plc = op.placement

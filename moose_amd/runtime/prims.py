@@ -233,6 +233,13 @@ def _slice(nb, a, slice):
 builtins_slice = slice
 
 
+@prim("Permute")
+def _permute(nb, a, perm):
+    if _is_rt(a):
+        return R.transpose(a, nb, perm)
+    return a.permute(list(range(nb)) + [p + nb for p in perm]).contiguous()
+
+
 @prim("StridedSlice")
 def _strided_slice(nb, a, slices):
     if _is_rt(a):
@@ -385,6 +392,19 @@ def _weighted_sum(nb, x, weights, bits):
     if acc is None:
         return R.zeros(R.index_axis(x, 0, 0, nb).shape, bits, x.device)
     return acc
+
+
+@prim("BitAffine")
+def _bit_affine(nb, x, aff):
+    """Linear part of a GF(2) affine map over the leading logical axis of a bit tensor
+    (``aff`` is a ``bristol._SparseAffine``; one sparse GEMM, see protocols/bristol)."""
+    d = x.data
+    if nb:
+        d = d.movedim(0, 1)  # party axis behind the wire axis
+    y = aff.linear(d)
+    if nb:
+        y = y.movedim(1, 0)
+    return R.RT(y.contiguous(), 1)
 
 
 @prim("ToBool")
