@@ -188,6 +188,13 @@ def concat(sess, xs, axis):
     return _with(xs[0], t) if isinstance(xs[0], RepFixed) else t
 
 
+def broadcast_to(sess, x, shape):
+    """Share-wise broadcast of a (fixed-point) sharing to ``shape`` (no-op if equal)."""
+    if tuple(shape_of(sess, x)) == tuple(shape):
+        return x
+    return local(sess, x, "Broadcast", shape=tuple(shape))
+
+
 def shape_of(sess, x):
     t = x.t if isinstance(x, RepFixed) else x
     if isinstance(t, MV):

@@ -683,7 +683,14 @@ class Interpreter:
         s, x, y = (self.at(op, v) for v in ins)
         if s.is_host:
             return LV(s.plc, "tensor", x.dtype, self.sess.h("Mux", s.host, s.v, x.v, y.v))
-        return LV(s.plc, "tensor", x.dtype, fxp.mux(self.sess, s.v, x.v, y.v))
+        # public (mirrored / constant) branches become trivial sharings (no messages)
+        x, y = (v if not isinstance(v.v, MV) else self._share_public(v) for v in (x, y))
+        if isinstance(s.v, MV):
+            raise MooseRuntimeError("mux with a public selector on a replicated placement")
+        xv, yv = x.v, y.v
+        shp = fxp.shape_of(self.sess, s.v)
+        xv, yv = (fxp.broadcast_to(self.sess, v, shp) for v in (xv, yv))
+        return LV(s.plc, "tensor", x.dtype, fxp.mux(self.sess, s.v, xv, yv))
 
     # ------------------------------------------------------------------------
     # reductions
