@@ -102,9 +102,9 @@ def __getattr__(name):
 
         return MooseComputation
     if name == "elk_compiler":
-        from moose_amd import elk_compiler
+        import importlib
 
-        return elk_compiler
+        return importlib.import_module("moose_amd.elk_compiler")
     if name == "predictors":
         from moose_amd.models import predictors
 

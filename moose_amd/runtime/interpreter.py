@@ -809,6 +809,8 @@ class Interpreter:
             x = self.to_host(x, plc.owner) if x.is_host else x
             if x.is_host:
                 return LV(plc, "shape", None, self.sess.h("Shape", plc.owner, x.v))
+        if x.is_host:  # shapes are public: the owner's view of its tensor's shape
+            return LV(plc, "shape", None, self.sess.h("Shape", x.host, x.v))
         return LV(plc, "shape", None, fxp.shape_of(self.sess, x.v))
 
     def _fill(self, op, ins, value):

@@ -414,6 +414,8 @@ def _to_bool(nb, x):
 
 @prim("FromBool")
 def _from_bool(nb, x):
+    if _is_rt(x):  # already a bit tensor (e.g. a host comparison result)
+        return R.RT(x.data.to(torch.uint8), 1)
     return R.RT(x.to(torch.uint8), 1)
 
 
