@@ -279,66 +279,18 @@ def trunc_pr(sess, x: RepTensor, m: int) -> RepTensor:
         return x
     with span("rep.trunc_pr"):
         plc, bits = x.plc, x.bits
-        p0, p1, p2 = plc.owners
-        k = bits - 1
         nr0, nr1, nt, nm = (sess.nonce(plc) for _ in range(4))
         if getattr(sess, "fused", False):
             n0, n2 = sess.nonce(plc), sess.nonce(plc)
             s0, s1 = sess.fused_trunc_pr(x, m, (nr0, nr1, nt, nm, n0, n2))
             return RepTensor(plc, bits, "arith", s0, s1)
+        from moose_amd.protocols import additive
+
+        # every party takes the shape from its own share: no metadata messages
         sh = [sess.h("Shape", plc.owners[i], sess.take(x.s0, i)) for i in range(3)]
-        # dealer P2
-        r = sess.h("Add", p2, sess.h_prf(plc, p2, 0, sh[2], bits, nr0),
-                   sess.h_prf(plc, p2, 2, sh[2], bits, nr1))
-        r_msb = sess.h("Shr", p2, r, amount=bits - 1)
-        r_top = sess.h("Shr", p2, sess.h("Shl", p2, r, amount=1), amount=m + 1)
-        rt1 = sess.move(sess.h("Sub", p2, r_top, sess.h_prf(plc, p2, 0, sh[2], bits, nt)), p1)
-        rm1 = sess.move(sess.h("Sub", p2, r_msb, sess.h_prf(plc, p2, 0, sh[2], bits, nm)), p1)
-        # P0 re-derives its mask shares from k_0, P1 its r1 from k_2
-        r0 = sess.h_prf(plc, p0, 0, sh[0], bits, nr0)
-        rt0 = sess.h_prf(plc, p0, 0, sh[0], bits, nt)
-        rm0 = sess.h_prf(plc, p0, 0, sh[0], bits, nm)
-        r1 = sess.h_prf(plc, p1, 2, sh[1], bits, nr1)
-        # replicated -> additive: a0 = x0 + x1 at P0, a1 = x2 at P1
-        a0 = sess.h("Add", p0, sess.take(x.s0, 0), sess.take(x.s1, 0))
-        a1 = sess.take(x.s1, 1)
-        mk0 = sess.h("Add", p0, sess.h("AddConst", p0, a0, value=1 << (k - 1), bits=bits), r0)
-        mk1 = sess.h("Add", p1, a1, r1)
-        c_at0 = sess.h("Add", p0, mk0, sess.move(mk1, p0))
-        c_at1 = sess.h("Add", p1, mk1, sess.move(mk0, p1))
-        outs = []
-        for host, c, rt, rm, first in ((p0, c_at0, rt0, rm0, True), (p1, c_at1, rt1, rm1, False)):
-            c_msb = sess.h("Shr", host, c, amount=bits - 1)
-            # share of overflow = r_msb XOR c_msb = rm + [first] c_msb - 2 c_msb rm
-            ov = sess.h("Sub", host, rm,
-                        sess.h("Shl", host, sess.h("Mul", host, c_msb, rm), amount=1))
-            if first:
-                ov = sess.h("Add", host, ov, c_msb)
-            y = sess.h("Sub", host, sess.h("Shl", host, ov, amount=k - m), rt)
-            if first:
-                c_top = sess.h("Shr", host, sess.h("Shl", host, c, amount=1), amount=m + 1)
-                y = sess.h("Add", host, y, c_top)
-                y = sess.h("AddConst", host, y, value=-(1 << (k - 1 - m)), bits=bits)
-            outs.append(y)
-        return _adt_to_rep(sess, plc, outs[0], outs[1], sh, bits)
-
-
-def _adt_to_rep(sess, plc, y0: HV, y1: HV, sh, bits) -> RepTensor:
-    """2-party additive (P0: y0, P1: y1) -> RSS: z0 = PRF(k_0) [P0,P2], z2 = PRF(k_2)
-    [P1,P2], z1 = (y0 - z0) + (y1 - z2) exchanged between P0 and P1 (one round)."""
-    p0, p1, p2 = plc.owners
-    n0, n2 = sess.nonce(plc), sess.nonce(plc)
-    z0_at0 = sess.h_prf(plc, p0, 0, sh[0], bits, n0)
-    z2_at1 = sess.h_prf(plc, p1, 2, sh[1], bits, n2)
-    z0_at2 = sess.h_prf(plc, p2, 0, sh[2], bits, n0)
-    z2_at2 = sess.h_prf(plc, p2, 2, sh[2], bits, n2)
-    w0 = sess.h("Sub", p0, y0, z0_at0)
-    w1 = sess.h("Sub", p1, y1, z2_at1)
-    z1_at0 = sess.h("Add", p0, w0, sess.move(w1, p0))
-    z1_at1 = sess.h("Add", p1, w1, sess.move(w0, p1))
-    s0 = sess.gather(plc, [z0_at0, z1_at1, z2_at2])
-    s1 = sess.gather(plc, [z1_at0, z2_at1, z0_at2])
-    return RepTensor(plc, bits, "arith", s0, s1)
+        a = additive.from_rep(sess, x)  # P0: x0 + x1, P1: x2 (local)
+        y = additive.trunc_pr(sess, plc, a, m, (nr0, nr1, nt, nm), shapes=sh)
+        return additive.to_rep(sess, plc, y, shapes=sh)
 
 
 # ---------------------------------------------------------------------------
