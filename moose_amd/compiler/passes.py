@@ -234,12 +234,50 @@ PASSES: Dict[str, Callable] = {
 }
 
 
+_PLAN_CACHE: Dict[str, Computation] = {}
+_PLAN_CACHE_MAX = 32
+
+
+def _plan_key(comp, names, arg_specs, fixedpoint_ring):
+    import hashlib
+
+    spec = sorted((k, str(v)) for k, v in (arg_specs or {}).items())
+    h = hashlib.blake2b(digest_size=16)
+    for part in (comp.digest(), ",".join(names), repr(spec), str(fixedpoint_ring)):
+        h.update(part.encode())
+    return h.hexdigest()
+
+
 def compile(comp: Computation, passes: Optional[List[str]] = None,  # noqa: A001
-            arg_specs=None, fixedpoint_ring: int = 128) -> Computation:
+            arg_specs=None, fixedpoint_ring: int = 128, cache: bool = True) -> Computation:
+    """Run the pass pipeline.  Lowered plans are deterministic (PRF nonces are counters,
+    not random sync keys), so results are cached by (computation digest, passes, input
+    shapes, ring) in memory and, with ``MOOSEX_PLAN_CACHE=<dir>``, on disk."""
+    import os
+
     names = DEFAULT_PASSES if passes is None else list(passes)
     for name in names:
-        fn = PASSES.get(name)
-        if fn is None:
+        if name not in PASSES:
             raise CompilationError(f"Unknown pass requested: {name}")
-        comp = fn(comp, arg_specs=arg_specs, fixedpoint_ring=fixedpoint_ring)
+    side_effects = any(n in ("print", "dump") for n in names)
+    key = _plan_key(comp, names, arg_specs, fixedpoint_ring) if cache and not side_effects else None
+    if key is not None:
+        hit = _PLAN_CACHE.get(key)
+        if hit is not None:
+            return hit
+        disk = os.environ.get("MOOSEX_PLAN_CACHE")
+        if disk and os.path.exists(os.path.join(disk, key + ".msgpack")):
+            plan = Computation.from_disk(os.path.join(disk, key + ".msgpack"))
+            _PLAN_CACHE[key] = plan
+            return plan
+    for name in names:
+        comp = PASSES[name](comp, arg_specs=arg_specs, fixedpoint_ring=fixedpoint_ring)
+    if key is not None:
+        if len(_PLAN_CACHE) >= _PLAN_CACHE_MAX:
+            _PLAN_CACHE.pop(next(iter(_PLAN_CACHE)))
+        _PLAN_CACHE[key] = comp
+        disk = os.environ.get("MOOSEX_PLAN_CACHE")
+        if disk:
+            os.makedirs(disk, exist_ok=True)
+            comp.to_disk(os.path.join(disk, key + ".msgpack"))
     return comp

@@ -17,7 +17,9 @@ everything else is preceded by a fixed-size int64 header describing the payload
 from __future__ import annotations
 
 import math
+import os
 import struct
+import time
 from typing import List
 
 import torch
@@ -46,13 +48,18 @@ class Transport:
     ``device`` is where payload tensors travel (a CUDA device for RCCL, CPU for gloo).
     """
 
-    def __init__(self, rank: int, world: int, device, group=None):
+    def __init__(self, rank: int, world: int, device, group=None, fault=None):
         self.rank = rank
         self.world = world
         self.device = torch.device(device)
         self.group = group
         self.bytes_sent = 0
         self.messages = 0
+        # test-only fault injection: MOOSEX_FAULT="drop:<k>@<rank>" drops this rank's
+        # k-th outgoing message, "delay:<seconds>@<rank>" delays every send
+        self.fault = fault if fault is not None else _parse_fault(os.environ.get("MOOSEX_FAULT"),
+                                                                   rank)
+        self._sends = 0
 
     # -- encoding -----------------------------------------------------------------
     def _header(self, v):
@@ -137,6 +144,13 @@ class Transport:
             t = t.to(self.device)
         if t.numel() == 0:
             return
+        self._sends += 1
+        if self.fault is not None:
+            kind, val = self.fault
+            if kind == "drop" and self._sends == val:
+                return  # the receiver waits until the session deadline
+            if kind == "delay":
+                time.sleep(val)
         dist.send(t, dst, group=self.group)
         self.bytes_sent += t.numel() * t.element_size()
         self.messages += 1
@@ -202,6 +216,20 @@ class Transport:
         if me in dsts:
             return self.recv(src)
         return None
+
+
+def _parse_fault(spec, rank):
+    if not spec:
+        return None
+    what, _, who = spec.partition("@")
+    if who and int(who) != rank:
+        return None
+    kind, _, val = what.partition(":")
+    if kind == "drop":
+        return ("drop", int(val))
+    if kind == "delay":
+        return ("delay", float(val))
+    raise ValueError(f"bad MOOSEX_FAULT spec {spec!r}")
 
 
 def _s64(u: int) -> int:

@@ -116,7 +116,8 @@ class DistributedMooseRuntime:
     def __init__(self, identities, backend: Optional[str] = None,
                  storage_mapping: Optional[Dict[str, Dict]] = None, fixedpoint_ring: int = 128,
                  seed: Optional[int] = None, timeout: float = 900.0,
-                 master_addr: str = "127.0.0.1"):
+                 master_addr: str = "127.0.0.1", session_timeout: Optional[float] = None,
+                 retries: int = 0, worker_env: Optional[Dict[str, str]] = None):
         if isinstance(identities, dict):  # GrpcMooseRuntime-style {role: endpoint}
             identities = list(identities.keys())
         self.identities = [getattr(i, "name", i) for i in identities]
@@ -129,6 +130,11 @@ class DistributedMooseRuntime:
         self.seed = seed
         self.timeout = timeout
         self.master_addr = master_addr
+        # per-session deadline inside the workers (process-group timeout) and automatic
+        # re-launch with a fresh session (new keys, new rendezvous) on failure
+        self.session_timeout = session_timeout
+        self.retries = retries
+        self.worker_env = dict(worker_env or {})
         self.last_timings = None
         self.last_stats = None
 
@@ -148,7 +154,12 @@ class DistributedMooseRuntime:
 
             comp = passes.compile(comp, compiler_passes, arg_specs=arg_specs_of(arguments),
                                   fixedpoint_ring=self.fixedpoint_ring)
-        return self._launch(comp, dict(arguments or {}))
+        for attempt in range(self.retries + 1):
+            try:
+                return self._launch(comp, dict(arguments or {}))
+            except DistributedRuntimeError:
+                if attempt == self.retries:
+                    raise
 
     # mirrors pymoose's GrpcMooseRuntime.run_computation -> (outputs, timings)
     def run_computation(self, computation, arguments=None):
@@ -173,6 +184,9 @@ class DistributedMooseRuntime:
             env = dict(os.environ)
             env.update(MASTER_ADDR=self.master_addr, MASTER_PORT=str(port),
                        WORLD_SIZE=str(n), HSA_ENABLE_IPC_MODE_LEGACY="0")
+            if self.session_timeout is not None:
+                env["MOOSEX_SESSION_TIMEOUT"] = str(self.session_timeout)
+            env.update(self.worker_env)
             pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
             env["PYTHONPATH"] = pkg_root + os.pathsep + env.get("PYTHONPATH", "")
             procs = []

@@ -87,6 +87,7 @@ class GraphExecutor:
 
         arguments = arguments or {}
         comp = comp.toposorted()
+        self._used = set()
         env: Dict[str, object] = {}
         parked: Dict[bytes, object] = {}
         outputs = {}
@@ -98,6 +99,10 @@ class GraphExecutor:
             if op.kind == "Send":
                 key = bytes(op.attrs["rendezvous_key"])
                 dst = op.attrs["receiver"]
+                if key in parked or key in self._used:
+                    # each (session, rendezvous key) is sent and received exactly once
+                    raise GraphExecutionError(f"{op.name}: duplicate send for rendezvous key "
+                                              f"{key.hex()}")
                 if me is None:
                     parked[key] = env[op.inputs[0]]
                 elif me == host:
@@ -139,7 +144,9 @@ class GraphExecutor:
         if kind == "Receive":
             key = bytes(attrs["rendezvous_key"])
             if key not in parked:
-                raise GraphExecutionError(f"receive {op.name}: no value for its rendezvous key")
+                raise GraphExecutionError(f"receive {op.name}: no value for its rendezvous key"
+                                          + (" (already received)" if key in self._used else ""))
+            self._used.add(key)
             return parked.pop(key)
         if kind == "PrfKeyGen":
             return os.urandom(16)

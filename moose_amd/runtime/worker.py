@@ -26,7 +26,12 @@ def _init_group(backend: str):
     import torch.distributed as dist
 
     if not dist.is_initialized():
-        dist.init_process_group(backend=backend)
+        from datetime import timedelta
+
+        # per-session deadline: a party that never receives (dead peer, dropped message)
+        # fails after MOOSEX_SESSION_TIMEOUT seconds instead of hanging
+        timeout = timedelta(seconds=float(os.environ.get("MOOSEX_SESSION_TIMEOUT", "1800")))
+        dist.init_process_group(backend=backend, timeout=timeout)
     return dist.get_rank(), dist.get_world_size()
 
 
