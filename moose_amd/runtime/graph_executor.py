@@ -169,6 +169,8 @@ class GraphExecutor:
             attrs["device"] = self.device
         if kind in ("Cast", "Zeros", "Ones"):
             attrs["dtype"] = _TY_DTYPE.get(op.sig.ret.name, torch.float64)
+        if kind == "BitDecompose":
+            attrs["to_bits"] = bits == 1
         if kind in ("RingMulCross", "BitAndCross", "RingDotCross"):
             return _cross(kind, *vals)
         params = _params(prim.impl)

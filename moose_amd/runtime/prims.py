@@ -394,6 +394,33 @@ def _weighted_sum(nb, x, weights, bits):
     return acc
 
 
+@prim("BitDecompose")
+def _bit_decompose(nb, x, to_bits=True):
+    """Ring tensor -> its bits stacked on a new leading logical axis (LSB first), as a
+    bit tensor or as 0/1 ring elements (reference host/ops.rs:855-937)."""
+    bits = x.bits
+    d = x.data
+    planes = []
+    for j in range(bits):
+        w = d if bits == 64 else d[..., j // 64]
+        planes.append(((w >> (j % 64)) & 1).to(torch.uint8))
+    out = torch.stack(planes, dim=nb)
+    if to_bits:
+        return R.RT(out, 1)
+    return R.ring_inject(R.RT(out, 1), 0, bits)
+
+
+@prim("ShlDim")
+def _shl_dim(nb, x, amount, bit_length):
+    """Shift along the leading (bit) axis: out[i] = x[i - amount], zeros below
+    (reference host/ops.rs:835-853)."""
+    d = x.data if _is_rt(x) else x
+    ax = nb
+    head = torch.zeros_like(d.narrow(ax, 0, amount))
+    out = torch.cat([head, d.narrow(ax, 0, bit_length - amount)], dim=ax)
+    return R.RT(out, x.bits) if _is_rt(x) else out
+
+
 @prim("BitAffine")
 def _bit_affine(nb, x, aff):
     """Linear part of a GF(2) affine map over the leading logical axis of a bit tensor
