@@ -69,6 +69,10 @@ def main():
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--ring", type=int, default=128, choices=[64, 128])
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--layout", default="stacked", choices=["stacked", "spmd"],
+                    help="stacked: 3 parties per GPU, N data-parallel sessions (default, "
+                         "highest throughput); spmd: each party on its own GPU, N/3 sessions, "
+                         "every reshare an RCCL send/recv")
     ap.add_argument("--check", action="store_true", help="verify against float64 numpy")
     args = ap.parse_args()
 
@@ -89,20 +93,42 @@ def main():
 
     comp = build_computation(args.ring)
     n = args.size
-    g = torch.Generator(device="cpu").manual_seed(1234 + rank)
+    spmd = args.layout == "spmd"
+    if spmd and (world < 3 or world % 3):
+        raise SystemExit("--layout spmd needs a multiple of 3 GPUs (one per party)")
+    n_sessions = world // 3 if spmd else world
+    session = rank // 3 if spmd else rank
+    g = torch.Generator(device="cpu").manual_seed(1234 + session)
     x = (torch.rand(n, n, generator=g, dtype=torch.float64) * 8 - 4).to(device)
     y = (torch.rand(n, n, generator=g, dtype=torch.float64) * 8 - 4).to(device)
-    gather_buf = None
-    if world > 1 and not args.no_gather:
-        gather_buf = torch.empty((world, n, n), dtype=torch.float64, device=device)
+    gather_buf, gather_group = None, None
+    if n_sessions > 1 and not args.no_gather:
+        # replicas' revealed outputs concatenated along rows (the layout every backend accepts)
+        gather_buf = torch.empty((n_sessions * n, n), dtype=torch.float64, device=device)
+        if spmd:  # the output owners (carole = party 2) of every session
+            gather_group = dist.new_group([3 * s + 2 for s in range(n_sessions)])
+    out_owner = (rank % 3 == 2) if spmd else True
+
+    if spmd:
+        from moose_amd.parallel.spmd import SPMDSession
+        from moose_amd.parallel.transport import Transport
+
+        roles = {r: 3 * session + i for i, r in enumerate(("alice", "bob", "carole"))}
+        transport = Transport(rank, world, device)
+
+        def new_session():
+            return SPMDSession(("alice", "bob", "carole")[rank % 3], roles, transport, device)
+    else:
+        def new_session():
+            return StackedSession(device)
 
     def step():
-        sess = StackedSession(device)
+        sess = new_session()
         interp = Interpreter(sess, {}, fixedpoint_ring=args.ring)
         outs = interp.run(comp, {"x": x, "y": y})
-        z = outs["output_0"].v.v
-        if gather_buf is not None:
-            dist.all_gather_into_tensor(gather_buf, z.contiguous())
+        z = outs["output_0"].v.v if out_owner else None
+        if gather_buf is not None and out_owner:
+            dist.all_gather_into_tensor(gather_buf, z.contiguous(), group=gather_group)
         return z
 
     for _ in range(args.warmup):
@@ -124,10 +150,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1e3
-    value = world * n * n * args.steps / elapsed
+    value = n_sessions * n * n * args.steps / elapsed
 
     check = None
-    if args.check:
+    if args.check and out_owner:
         ref = (x.double() @ y.double())
         err = (z - ref).abs().max().item()
         check = {"max_abs_err": err}
@@ -148,9 +174,11 @@ def main():
             "data": "synthetic uniform[-4,4) inputs, device resident",
             "config": {
                 "model": f"replicated fixed(14,23) RingDot {n}x{n} (share+dot+trunc_pr+reveal)",
-                "global_batch": world,
+                "global_batch": n_sessions,
                 "seq_len": n,
-                "parallelism": f"dp{world} (one stacked 3-party session per GPU)",
+                "parallelism": (f"dp{n_sessions} x 3-party sessions, one party per GPU "
+                                "(RCCL reshare)" if spmd else
+                                f"dp{world} (one stacked 3-party session per GPU)"),
             },
         }
         if check:

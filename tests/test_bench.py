@@ -1,0 +1,39 @@
+"""bench.py contract on CPU (gloo): one JSON line from rank 0 with the driver's fields, for
+the default stacked data-parallel layout and the party-per-GPU (SPMD) layout."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FIELDS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+          "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"}
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(n, *extra):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py",
+           "--gpus", str(n), "--steps", "2", "--warmup", "1", "--size", "64", *extra]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n,layout", [(2, "stacked"), (3, "spmd")])
+def test_bench_json_line(n, layout):
+    d = _run(n, "--layout", layout)
+    assert FIELDS <= set(d)
+    assert d["n_gpus"] == n and d["steps"] == 2 and d["warmup"] == 1
+    assert d["value"] > 0 and d["higher_is_better"] is True
+    assert {"model", "global_batch", "seq_len", "parallelism"} <= set(d["config"])
