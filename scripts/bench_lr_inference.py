@@ -1,0 +1,70 @@
+"""Private logistic-regression inference latency (BASELINE config 4, the reference's
+``tutorials/ml-inference-with-onnx`` setup): sklearn LogisticRegression on
+make_classification(1000 samples, 10 features, 2 classes, random_state=5), 80/20 split;
+the 200 test rows are secret-shared from alice, scored on the replicated placement
+(public weights, secure sigmoid) and the probabilities opened to bob.
+
+Prints one JSON line with p50/p90 latency of the whole computation (share -> predict ->
+reveal) over ``--runs`` evaluations, and the max deviation from sklearn's
+``predict_proba``.  Single process: the three parties are stacked on one device.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--runs", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--device", default=None)
+    ap.add_argument("--ring", type=int, default=128, choices=(64, 128))
+    a = ap.parse_args()
+    import torch
+    from sklearn.datasets import make_classification
+    from sklearn.linear_model import LogisticRegression
+    from sklearn.model_selection import train_test_split
+
+    from moose_amd.models import predictors
+    from moose_amd.runtime.local import LocalMooseRuntime
+
+    X, y = make_classification(n_samples=1000, n_features=10, n_classes=2, random_state=5)
+    X_train, X_test, y_train, _ = train_test_split(X, y, test_size=0.2, random_state=5)
+    lg = LogisticRegression().fit(X_train, y_train)
+    w, b = lg.coef_[0], lg.intercept_[0]
+    # the ONNX export of a binary sklearn LR: two score rows (-w, w), LOGISTIC transform
+    model = predictors.LinearClassifier(np.stack([-w, w]), np.array([-b, b]),
+                                        predictors.PostTransform.SIGMOID)
+    comp = model.predictor_factory(predictors.DEFAULT_FIXED_DTYPE)
+    dev = a.device or ("cuda" if torch.cuda.is_available() else "cpu")
+    rt = LocalMooseRuntime(["alice", "bob", "carole"], device=dev, fixedpoint_ring=a.ring)
+    args = {"x": X_test}
+    for _ in range(a.warmup):
+        out = rt.evaluate_computation(comp, args)
+    lat = []
+    for _ in range(a.runs):
+        t0 = time.perf_counter()
+        out = rt.evaluate_computation(comp, args)
+        lat.append(time.perf_counter() - t0)
+    pred = np.asarray(list(out.values())[0])
+    err = float(np.abs(pred - lg.predict_proba(X_test)).max())
+    lat = np.sort(np.asarray(lat)) * 1e3
+    print(json.dumps({
+        "metric": "private LR inference p50 latency", "value": float(np.median(lat)),
+        "unit": "ms", "p90_ms": float(lat[int(0.9 * (len(lat) - 1))]), "runs": a.runs,
+        "higher_is_better": False, "batch": int(X_test.shape[0]), "features": 10,
+        "device": dev, "ring": a.ring, "max_abs_err_vs_sklearn": err,
+        "data": "make_classification(random_state=5), sklearn LogisticRegression",
+    }))
+
+
+if __name__ == "__main__":
+    main()
