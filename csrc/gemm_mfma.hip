@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <mutex>
 
 #include "moosex.h"
@@ -244,17 +245,26 @@ __global__ void __launch_bounds__(256, Limbs<T>::L == 8 ? 2 : 1)
     const int cur = (int)(kb & 1);
     const int8_t* As = buf(cur);
     const int8_t* Bs = As + STAGE;
-    // all fragments of the step are requested up front so the LDS latency is paid once
+    // B fragments of the step stay resident; A limbs are consumed one per round, so only
+    // two are requested ahead of their round (the rest stream in behind the MFMAs).
     v4i bf[L], af[L];
 #pragma unroll
     for (int j = 0; j < L; ++j) bf[j] = *(const v4i*)(Bs + j * kTileBytes + boff);
 #pragma unroll
-    for (int i = 0; i < L; ++i) af[i] = *(const v4i*)(As + i * kTileBytes + aoff);
+    for (int i = 0; i < 2; ++i) af[i] = *(const v4i*)(As + i * kTileBytes + aoff);
+    // Issue order: round i multiplies A limb i into diagonals d = L-1 .. i (j = d - i),
+    // so consecutive MFMAs never share an accumulator and two updates of the same
+    // diagonal are >= 2 MFMAs apart (no back-to-back SrcC dependency); the scheduling
+    // barriers keep the compiler from regrouping them.
 #pragma unroll
     for (int i = 0; i < L; ++i) {
+      if (i + 2 < L) af[i + 2] = *(const v4i*)(As + (i + 2) * kTileBytes + aoff);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int j = 0; j < L - i; ++j)
-        acc[i + j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[i], bf[j], acc[i + j], 0, 0, 0);
+      for (int d = L - 1; d >= i; --d) {
+        acc[d] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[i], bf[d - i], acc[d], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -277,6 +287,146 @@ __global__ void __launch_bounds__(256, Limbs<T>::L == 8 ? 2 : 1)
       *p = accumulate ? (T)(*p + v) : v;
     }
   }
+}
+
+// Z_2^128 variant with TWO waves per SIMD.  The 16 diagonal accumulators of a 32x32 tile
+// (256 registers) pin k_gemm_limb to one wave per SIMD, so every LDS wait and barrier
+// idles the matrix core.  Here each 32x32 tile is owned by a pair of waves that split the
+// anti-diagonals: the "low" wave sums d = 0..kSplit-1 (55 MFMAs, 10 accumulators), the
+// "high" wave d = kSplit..15 (81 MFMAs, 6 accumulators), each within 256 registers, so
+// 8 waves share the CU and one wave's MFMAs cover the other's waits.  B fragments a wave
+// needs stay resident; A fragments stream limb by limb.  The high wave hands its partial
+// sums to the low wave through LDS at the end.
+constexpr int kSplit = 10;
+
+__global__ void __launch_bounds__(512, 1)
+    k_gemm_limb128_split(const int8_t* __restrict__ LA, const int8_t* __restrict__ LB,
+                         u128* __restrict__ C, int64_t M, int64_t N, int64_t Mp, int64_t Np,
+                         int64_t Kp, int accumulate) {
+  constexpr int L = 16;
+  constexpr int STAGE = L * kTileBytes;
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+  auto buf = [&](int i) -> int8_t* { return smem + i * 2 * STAGE; };
+
+  const int64_t tiles_n = Np / TN, tiles_m = Mp / TM;
+  const int64_t ntiles = tiles_n * tiles_m;
+  const int64_t tid_flat = xcd_remap(blockIdx.x, ntiles);
+  const int64_t group = tid_flat / (kGroupM * tiles_n);
+  const int64_t first_m = group * kGroupM;
+  const int64_t gm = tiles_m - first_m < kGroupM ? tiles_m - first_m : kGroupM;
+  const int64_t in_group = tid_flat % (kGroupM * tiles_n);
+  const int64_t tm = first_m + in_group % gm, tn = in_group / gm;
+  const int64_t b = blockIdx.y;
+  const int64_t nkb = Kp / TK;
+  const int8_t* ga = LA + (b * tiles_m + tm) * nkb * (int64_t)STAGE;
+  const int8_t* gb = LB + (b * tiles_n + tn) * nkb * (int64_t)STAGE;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;  // 0..7
+  const int tile = wave & 3;          // which 32x32 quarter of the 64x64 block tile
+  const bool high = wave >= 4;        // diagonal half
+  const int wr = tile >> 1, wc = tile & 1;
+  const int half = lane >> 5;
+  const int aoff = swz(wr * 32 + (lane & 31), half);
+  const int boff = swz(wc * 32 + (lane & 31), half);
+
+  constexpr int PIECES = STAGE / 1024;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  auto issue_stage = [&](int64_t kb, int8_t* dst) {
+    const int8_t* sa = ga + kb * STAGE + lane * 16;
+    const int8_t* sb = gb + kb * STAGE + lane * 16;
+#pragma unroll
+    for (int c = wave_u; c < PIECES; c += 8) {
+      __builtin_amdgcn_global_load_lds((const void*)(sa + c * 1024),
+                                       (__attribute__((address_space(3))) void*)(dst + c * 1024),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(sb + c * 1024),
+                                       (__attribute__((address_space(3))) void*)(dst + STAGE + c * 1024),
+                                       16, 0, 0);
+    }
+  };
+
+  constexpr int NLO = kSplit, NHI = L - kSplit;
+  v16i acc[NLO > NHI ? NLO : NHI];
+#pragma unroll
+  for (int d = 0; d < (NLO > NHI ? NLO : NHI); ++d) acc[d] = v16i{0};
+
+  issue_stage(0, buf(0));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (nkb > 1) issue_stage(1, buf(1));
+  for (int64_t kb = 0; kb < nkb; ++kb) {
+    const int cur = (int)(kb & 1);
+    const int8_t* As = buf(cur);
+    const int8_t* Bs = As + STAGE;
+    if (!high) {
+      v4i bf[NLO];
+#pragma unroll
+      for (int j = 0; j < NLO; ++j) bf[j] = *(const v4i*)(Bs + j * kTileBytes + boff);
+#pragma unroll
+      for (int i = 0; i < NLO; ++i) {
+        const v4i a = *(const v4i*)(As + i * kTileBytes + aoff);
+#pragma unroll
+        for (int j = 0; j < NLO - i; ++j)
+          acc[i + j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bf[j], acc[i + j], 0, 0, 0);
+      }
+    } else {
+      v4i bf[L];
+#pragma unroll
+      for (int j = 0; j < L; ++j) bf[j] = *(const v4i*)(Bs + j * kTileBytes + boff);
+#pragma unroll
+      for (int i = 0; i < L; ++i) {
+        const v4i a = *(const v4i*)(As + i * kTileBytes + aoff);
+#pragma unroll
+        for (int j = (kSplit - i > 0 ? kSplit - i : 0); j < L - i; ++j)
+          acc[i + j - kSplit] =
+              __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bf[j], acc[i + j - kSplit], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kb + 2 < nkb) issue_stage(kb + 2, buf(cur));
+  }
+
+  // epilogue: the high wave parks its partial sums in LDS (free now), the low wave adds
+  // its own and writes C.  16 rows x 64 lanes x 16 B = 16 KB per tile.
+  u128* part = (u128*)smem + tile * (16 * 64);
+  if (high) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      u128 v = 0;
+#pragma unroll
+      for (int d = 0; d < NHI; ++d) v += ((u128)(int64_t)acc[d][r]) << (8 * (d + kSplit));
+      part[r * 64 + lane] = v;
+    }
+  }
+  __syncthreads();
+  if (!high) {
+    const int col = lane & 31;
+    const int64_t gcol = tn * TN + wc * 32 + col;
+    u128* cb = C + b * M * N;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int64_t grow = tm * TM + wr * 32 + row;
+      u128 v = part[r * 64 + lane];
+#pragma unroll
+      for (int d = 0; d < NLO; ++d) v += ((u128)(int64_t)acc[d][r]) << (8 * d);
+      if (grow < M && gcol < N) {
+        u128* p = cb + grow * N + gcol;
+        *p = accumulate ? (u128)(*p + v) : v;
+      }
+    }
+  }
+}
+
+// MOOSEX_GEMM_SPLIT=0 selects the one-wave-per-SIMD kernel for Z_2^128 (A/B testing)
+bool use_split_kernel() {
+  static const bool on = [] {
+    const char* e = std::getenv("MOOSEX_GEMM_SPLIT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 struct Workspace {
@@ -371,10 +521,18 @@ int run(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T* A1
       if (!attr_set) {
         hipFuncSetAttribute((const void*)k_gemm_limb<T>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipFuncSetAttribute((const void*)k_gemm_limb128_split,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr_set = true;
       }
-      hipLaunchKernelGGL(k_gemm_limb<T>, dim3((unsigned)ntiles, (unsigned)batch), dim3(256),
-                         lds, st, la, lb, C, M, N, p.Mp, p.Np, p.Kp, accumulate);
+      if (sizeof(T) == 16 && use_split_kernel()) {
+        hipLaunchKernelGGL(k_gemm_limb128_split, dim3((unsigned)ntiles, (unsigned)batch),
+                           dim3(512), lds, st, la, lb, (u128*)C, M, N, p.Mp, p.Np, p.Kp,
+                           accumulate);
+      } else {
+        hipLaunchKernelGGL(k_gemm_limb<T>, dim3((unsigned)ntiles, (unsigned)batch), dim3(256),
+                           lds, st, la, lb, C, M, N, p.Mp, p.Np, p.Kp, accumulate);
+      }
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return -100 - (int)e;
@@ -384,6 +542,37 @@ int run(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T* A1
 }
 
 }  // namespace
+
+namespace {
+
+// Register-only MFMA throughput probe: the ceiling the limb GEMM is measured against
+// (same instruction, same clock behaviour, no memory traffic).
+__global__ void __launch_bounds__(256, 1) k_mfma_peak(int iters, int* __restrict__ sink) {
+  v16i acc[8];
+#pragma unroll
+  for (int d = 0; d < 8; ++d) acc[d] = v16i{0};
+  v4i a = v4i{(int)threadIdx.x, 1, 2, 3}, b = v4i{3, 2, 1, (int)blockIdx.x};
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int d = 0; d < 8; ++d) acc[d] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, acc[d], 0, 0, 0);
+  }
+  int s = 0;
+#pragma unroll
+  for (int d = 0; d < 8; ++d) s += acc[d][threadIdx.x & 15];
+  if (s == 0x7fffffff) sink[0] = s;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mx_mfma_peak(int blocks, int iters, void* sink, void* stream) {
+  hipLaunchKernelGGL(k_mfma_peak, dim3(blocks), dim3(256), 0, (hipStream_t)stream, iters,
+                     (int*)sink);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // extern "C"
 
 extern "C" {
 

@@ -45,6 +45,7 @@ _SIGS = {
         [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp],
     ),
     "mx_gemm_workspace_bytes": (c_i64, [c_int, c_i64, c_i64, c_i64, c_i64, c_int]),
+    "mx_mfma_peak": (c_int, [c_int, c_int, c_vp, c_vp]),
     "mx_gemm_ws": (
         c_int,
         [c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp,

@@ -12,7 +12,10 @@ def main():
     ap.add_argument("--n", type=int, default=4096)
     ap.add_argument("--bits", type=int, default=128)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--peak", action="store_true", help="also run the MFMA peak probe")
     a = ap.parse_args()
+    if a.peak:
+        mfma_peak()
     n, bits = a.n, a.bits
     shp = (3, n, n) + ((2,) if bits == 128 else ())
     g = torch.Generator(device="cuda").manual_seed(0)
@@ -27,6 +30,23 @@ def main():
     L = 16 if bits == 128 else 8
     ops = 2 * 3 * n * n * 2 * n * L * (L + 1) / 2
     print(f"n={n} bits={bits} {dt*1e3:.2f} ms/call  {ops/dt/1e15:.2f} int8 POPS")
+
+
+
+def mfma_peak(blocks=1024, iters=20000):
+    """Register-only v_mfma_i32_32x32x32_i8 rate (the ceiling for the limb GEMM)."""
+    from moose_amd.ops import native as nat
+
+    sink = torch.zeros(1, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    nat.lib().mx_mfma_peak(blocks, 10, nat.ptr(sink), st)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    nat.lib().mx_mfma_peak(blocks, iters, nat.ptr(sink), st)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t
+    ops = blocks * 4 * iters * 8 * 2 * 32 * 32 * 32
+    print(f"mfma peak probe: {ops / dt / 1e15:.2f} int8 POPS ({blocks} blocks x 4 waves)")
 
 
 if __name__ == "__main__":
