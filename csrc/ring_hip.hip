@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
 
 #include "aes_core.h"
 #include "moosex.h"
@@ -234,6 +235,44 @@ __global__ void k_rss_cross(int kind, const T* __restrict__ x0, const T* __restr
         v = x0[i];  // add-zero-share mode
       if (has_keys) v = mxr::zs_combine<T>(kind, v, pick<T>(alo, ahi, j), pick<T>(blo, bhi, j));
       out[i] = v;
+    }
+  }
+}
+
+// Stacked three-party ring (keys k0, k1, k2, k3 == k0): party p needs PRF(k_p) and
+// PRF(k_{p+1}), so each of the three keystreams is used by two parties.  One thread per
+// keystream block evaluates the three AES blocks once and finishes all three parties'
+// elements: 3 AES per block instead of 6 (the shares are identical to k_rss_cross).
+template <class T>
+__global__ void k_rss_cross_ring3(int kind, const T* __restrict__ x0, const T* __restrict__ x1,
+                                  const T* __restrict__ y0, const T* __restrict__ y1,
+                                  T* __restrict__ out, int64_t n, Keys4 keys, uint64_t nonce) {
+  __shared__ uint32_t Tt[256];
+  __shared__ uint8_t Sb[256];
+  stage_tables(Tt, Sb);
+  constexpr int P = Lane<T>::kPer;
+  const int64_t nb = (n + P - 1) / P;
+  for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < nb;
+       b += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t lo[3], hi[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) aes_ctr(keys.rk[q], Tt, Sb, nonce, (uint64_t)b, &lo[q], &hi[q]);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      const int q = p == 2 ? 0 : p + 1;
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const int64_t e = b * P + j;
+        if (e >= n) break;
+        const int64_t i = (int64_t)p * n + e;
+        T v = 0;
+        if (x0 != nullptr && y0 != nullptr)
+          v = mxr::cross<T>(kind, x0[i], x1 ? x1[i] : (T)0, y0[i], y1 ? y1[i] : (T)0,
+                            x1 != nullptr, y1 != nullptr);
+        else if (x0 != nullptr)
+          v = x0[i];
+        out[i] = mxr::zs_combine<T>(kind, v, pick<T>(lo[p], hi[p], j), pick<T>(lo[q], hi[q], j));
+      }
     }
   }
 }
@@ -466,8 +505,17 @@ int mxh_rss_cross(int kind, int words, const void* x0, const void* x1, const voi
   if (n == 0) return 0;
   if (nparties < 1 || nparties > 3) return -3;
   Keys4 k = keys16 ? load_keys(keys16, nparties + 1) : Keys4{};
+  const bool ring3 = keys16 && nparties == 3 && std::memcmp(keys16, keys16 + 48, 16) == 0;
   DEV_DISPATCH(words, T, {
     constexpr int P = 16 / (int)sizeof(T);
+    if (ring3) {
+      const int64_t blocks = (n + P - 1) / P;
+      hipLaunchKernelGGL(k_rss_cross_ring3<T>, dim3(grid_for(blocks)), dim3(kBlock), 0,
+                         S(stream), kind, (const T*)x0, (const T*)x1, (const T*)y0,
+                         (const T*)y1, (T*)out, n, k, nonce);
+      MX_LAUNCH_CHECK();
+      return 0;
+    }
     int64_t work = ((n + P - 1) / P) * nparties;
     hipLaunchKernelGGL(k_rss_cross<T>, dim3(grid_for(work)), dim3(kBlock), 0, S(stream), kind,
                        (const T*)x0, (const T*)x1, (const T*)y0, (const T*)y1, (T*)out, n,
