@@ -483,8 +483,11 @@ def diag(a: RT, nb=0) -> RT:
 
 
 def broadcast_to(a: RT, shape, nb=0) -> RT:
-    full = a.shape[:nb] + tuple(shape)
-    return expand(a, full).contiguous()
+    shape = tuple(shape)
+    lead = len(shape) - (a.ndim - nb)
+    if lead > 0:  # numpy rule: missing dims are prepended (after the batch axes)
+        a = reshape(a, (1,) * lead + a.shape[nb:], nb)
+    return expand(a, a.shape[:nb] + shape).contiguous()
 
 
 def atleast_2d(a: RT, to_column_vector=False, nb=0) -> RT:

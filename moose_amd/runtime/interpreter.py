@@ -522,6 +522,32 @@ class Interpreter:
         r = self._host_binary(op, hx, hy, kind, dtype)
         return LV(x.plc, "tensor", r.dtype, MV(x.plc, r.v.v))
 
+    def _broadcast_secret(self, x, y, px, py):
+        """Numpy-broadcast the secret operand(s) of an elementwise op to the common shape.
+
+        Shares carry a leading party axis (stacked) or live per process (SPMD), so rank
+        differences must be resolved on the logical shapes before the share-wise kernels
+        (e.g. a shared scalar learning rate times a (100, 1) gradient)."""
+        def shape(v, pub):
+            if pub is not None:
+                s = getattr(pub, "shape", None)
+                return tuple(s) if s is not None else ()
+            try:
+                s = fxp.shape_of(self.sess, v.v)
+            except RuntimeError:
+                return None
+            return None if s is None or any(d is None for d in s) else tuple(s)
+
+        sx, sy = shape(x, px), shape(y, py)
+        if sx is None or sy is None or sx == sy:
+            return x, y
+        target = tuple(np.broadcast_shapes(sx, sy))
+        if px is None and sx != target:
+            x = LV(x.plc, x.kind, x.dtype, fxp.broadcast_to(self.sess, x.v, target))
+        if py is None and sy != target:
+            y = LV(y.plc, y.kind, y.dtype, fxp.broadcast_to(self.sess, y.v, target))
+        return x, y
+
     def _rep_binary(self, op, x, y, kind, dtype):
         sess = self.sess
         px, py = self._public(x), self._public(y)
@@ -529,6 +555,8 @@ class Interpreter:
             h = self._mir_binary(op, LV(x.plc, "tensor", x.dtype, MV(x.plc, px)),
                                  LV(x.plc, "tensor", y.dtype, MV(x.plc, py)), kind, dtype)
             return LV(x.plc, "tensor", h.dtype, MV(x.plc, h.v.v))
+        if kind != "Dot":
+            x, y = self._broadcast_secret(x, y, px, py)
         if kind in ("Less", "Greater"):
             a, b = x, y
             return LV(x.plc, "tensor", T.BOOL, fxp.compare(sess, kind, a.v, b.v, px, py))

@@ -268,6 +268,9 @@ def _diag(nb, a):
 def _broadcast(nb, a, shape):
     if _is_rt(a):
         return R.broadcast_to(a, shape, nb)
+    lead = len(shape) - (a.dim() - nb)
+    if lead > 0:
+        a = a.reshape(tuple(a.shape[:nb]) + (1,) * lead + tuple(a.shape[nb:]))
     return a.expand(tuple(a.shape[:nb]) + tuple(shape)).contiguous()
 
 

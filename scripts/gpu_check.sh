@@ -24,6 +24,16 @@ STEPS=${STEPS:-all}
 [[ $STEPS == *smoke* || $STEPS == all ]] && run smoke 300 python __graft_entry__.py smoke
 [[ $STEPS == *bench* || $STEPS == all ]] && run bench128 600 python bench.py --steps 5 --warmup 2 --check
 [[ $STEPS == *bench* || $STEPS == all ]] && run bench64 600 python bench.py --steps 5 --warmup 2 --ring 64 --check
+if [[ $STEPS == *logreg* ]]; then
+  rm -f gpurun_out/logreg.jsonl
+  for it in 10 50 100; do for bs in 128 256 512 1024 2048; do
+    run logreg_${bs}_${it} 600 python benchmarks/logreg_train.py --batch_size $bs --n_iter $it --n_exp 3 --json gpurun_out/logreg.jsonl
+  done; done
+fi
+if [[ $STEPS == *dots* ]]; then
+  rm -f gpurun_out/dots.jsonl
+  run dots 900 python benchmarks/dot_product.py --sweep --n 3 --json gpurun_out/dots.jsonl
+fi
 if [[ $STEPS == *prof* || $STEPS == all ]]; then
   export TMPDIR=/tmp
   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1
