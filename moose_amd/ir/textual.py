@@ -185,6 +185,12 @@ def _parse_value(c: _Cursor, kind: str):
         name = c.match(_IDENT, "constant kind").group(0)
         return _parse_constant_literal(c, name)
     if kind == "slice":
+        if c.eat("["):  # multi-axis slice: [{start = ..}, {..}] (one element per axis)
+            out = []
+            while not c.eat("]"):
+                out.append(_parse_value(c, "slice"))
+                c.eat(",")
+            return out
         c.expect("{")
         d = {"start": 0, "end": None, "step": None}
         while not c.eat("}"):
@@ -331,6 +337,11 @@ def _print_value(v, kind):
     if kind == "const":
         return v.to_textual()
     if kind == "slice":
+        if isinstance(v, list):
+            if len(v) == 1:
+                v = v[0]
+            else:
+                return "[" + ", ".join(_print_value(e, "slice") for e in v) + "]"
         start, end, step = v
         s = f"{{start = {start}"
         if end is not None:

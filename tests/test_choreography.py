@@ -26,11 +26,14 @@ def _start(port, sessions_dir=None):
     env = dict(os.environ, PYTHONPATH=ROOT, WORLD_SIZE="3")
     procs = []
     for r, ident in enumerate(IDS):
-        cmd = [sys.executable, "-m", "moose_amd.cli.comet", "--identity", ident,
-               "--store", f"127.0.0.1:{port}", "--rank", str(r), "--world", "3",
-               "--backend", "gloo"]
-        if sessions_dir and r == 0:
-            cmd += ["--sessions-dir", sessions_dir]
+        if sessions_dir:  # filesystem choreography worker (rank 0 watches the dir)
+            cmd = [sys.executable, "-m", "moose_amd.cli.rudolph", "--identity", ident,
+                   "--store", f"127.0.0.1:{port}", "--sessions", sessions_dir,
+                   "--backend", "gloo"]
+        else:
+            cmd = [sys.executable, "-m", "moose_amd.cli.comet", "--identity", ident,
+                   "--store", f"127.0.0.1:{port}", "--rank", str(r), "--world", "3",
+                   "--backend", "gloo"]
         procs.append(subprocess.Popen(cmd, env=dict(env, RANK=str(r)), stdout=subprocess.PIPE,
                                       stderr=subprocess.STDOUT))
         if r == 0:

@@ -1,0 +1,65 @@
+"""The reference's benchmark workloads (``benchmarks/pymoose/logreg.py``,
+``benchmarks/pymoose/dot_product.py``) run end to end on small shapes and match fp64."""
+import importlib.util
+import os
+
+import numpy as np
+import pytest
+
+import moose_amd as pm
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _load(name):
+    spec = importlib.util.spec_from_file_location(name, os.path.join(ROOT, "benchmarks",
+                                                                     f"{name}.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_logreg_training_matches_fp64():
+    L = _load("logreg_train")
+    bs, n_it, nf = 16, 3, 100
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal((bs * n_it, nf))
+    y = rng.integers(2, size=(bs * n_it, 1)).astype(np.float64)
+    comp = L.build_training(bs, n_it, n_features=nf)
+    rt = pm.LocalMooseRuntime(["alice", "bob", "carole"], device="cpu")
+    outs = rt.evaluate_computation(comp, {"x": x, "y": y, "w_0": np.zeros((nf, 1)),
+                                          "b_0": np.zeros((1, 1))})
+    w_ref, b_ref = L.plaintext_training(x, y, bs, n_it)
+    vals = sorted(outs.values(), key=lambda v: -np.asarray(v).size)
+    np.testing.assert_allclose(vals[0].reshape(w_ref.shape), w_ref, atol=1e-5)
+    np.testing.assert_allclose(vals[1].reshape(b_ref.shape), b_ref, atol=1e-5)
+
+
+@pytest.mark.parametrize("mode,k", [("seq", 3), ("parallel", 4)])
+def test_dot_benchmark_graphs(mode, k):
+    D = _load("dot_product")
+    rt = pm.LocalMooseRuntime(["alice", "bob", "carole"], device="cpu")
+    res = D.run_one(rt, mode, 7, k, 1)
+    assert res["max_abs_err"] < 1e-6
+
+
+def test_secret_scalar_broadcasts_against_matrix():
+    alice, bob, carole = (pm.host_placement(n) for n in ("alice", "bob", "carole"))
+    rep = pm.replicated_placement("rep", [alice, bob, carole])
+    fx = pm.fixed(14, 23)
+
+    @pm.computation
+    def comp(a: pm.Argument(alice, dtype=pm.float64), s: pm.Argument(bob, dtype=pm.float64)):
+        with alice:
+            af = pm.cast(a, dtype=fx)
+        with bob:
+            sf = pm.cast(s, dtype=fx)
+        with rep:
+            z = pm.mul(af, sf) + sf - pm.mul(sf, af)
+        with carole:
+            return pm.cast(z, dtype=pm.float64)
+
+    rt = pm.LocalMooseRuntime(["alice", "bob", "carole"], device="cpu")
+    a = np.arange(6.0).reshape(3, 2) / 4
+    out = rt.evaluate_computation(comp, {"a": a, "s": np.array(0.5)})
+    np.testing.assert_allclose(next(iter(out.values())), np.full((3, 2), 0.5), atol=1e-5)
