@@ -88,8 +88,8 @@ prim("Xor")(_arith("xor"))
 
 @prim("Neg")
 def _neg(nb, a):
-    if _is_rt(a):
-        return -a
+    if _is_rt(a):  # on bit tensors Neg is NOT (reference host/ops.rs:1519-1527)
+        return ~a if a.bits == 1 else -a
     if a.dtype == torch.bool:
         return ~a
     return -a
