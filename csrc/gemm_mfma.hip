@@ -437,6 +437,8 @@ struct Workspace {
 std::mutex g_ws_mu;
 Workspace g_ws[16];
 
+// Grow-only per-device scratch.  A replaced buffer is retired, never freed: a captured
+// hipGraph may still reference it, and freeing would need a device-wide sync.
 void* get_workspace(int64_t bytes) {
   int dev = 0;
   hipGetDevice(&dev);
@@ -444,17 +446,12 @@ void* get_workspace(int64_t bytes) {
   std::lock_guard<std::mutex> lk(g_ws_mu);
   Workspace& w = g_ws[dev];
   if (w.bytes < bytes) {
-    if (w.ptr) {
-      hipDeviceSynchronize();
-      hipFree(w.ptr);
-    }
-    w.ptr = nullptr;
-    if (hipMalloc(&w.ptr, bytes) != hipSuccess) {
-      w.ptr = nullptr;
-      w.bytes = 0;
-      return nullptr;
-    }
-    w.bytes = bytes;
+    int64_t want = 1 << 20;
+    while (want < bytes) want <<= 1;
+    void* p = nullptr;
+    if (hipMalloc(&p, want) != hipSuccess) return nullptr;
+    w.ptr = p;  // the previous buffer (if any) stays allocated
+    w.bytes = want;
   }
   return w.ptr;
 }

@@ -100,6 +100,28 @@ int mx_share3(int dev, int kind, int words, const void* x, void* out0, void* out
               int j, const uint8_t* k_next, const uint8_t* k_all, uint64_t n1, uint64_t na,
               void* stream);
 
+// ---- PRF keys held in key slots (graph-capture friendly) -----------------------------
+// A key slot is MX_KEY_SLOT_WORDS uint32 words: the raw 16-byte key (words 0..3) followed
+// by its expanded AES-128 schedule (words 4..47).  Slots live in the memory named by
+// `dev`; kernels read them at run time, so the keys are not baked into launch parameters.
+#define MX_KEY_SLOT_WORDS 48
+// host: fill n consecutive slots from n raw keys
+void mx_key_slots(const uint8_t* keys16, int n, uint32_t* out);
+// mx_rss_cross with keys from slots: party p uses slot p % nslots and (p + 1) % nslots
+// (nslots == nparties: the ring of an RSS zero share; nslots == nparties + 1: explicit)
+int mx_rss_cross_k(int dev, int kind, int words, const void* x0, const void* x1,
+                   const void* y0, const void* y1, void* out, int64_t n, int nparties,
+                   const uint32_t* slots, int nslots, uint64_t nonce, void* stream);
+// mx_prf_expand with nkeys consecutive key slots
+int mx_prf_expand_k(int dev, int words, void* out, int64_t n, int nkeys, const uint32_t* slots,
+                    uint64_t nonce, void* stream);
+int mx_trunc_pr3_k(int dev, int words, const void* s0, void* out0, void* out1, int64_t n, int m,
+                   const uint32_t* slot_k0, const uint32_t* slot_k2, const uint64_t* nonces,
+                   void* stream);
+int mx_share3_k(int dev, int kind, int words, const void* x, void* out0, void* out1, int64_t n,
+                int j, const uint32_t* slot_next, const uint32_t* slot_all, uint64_t n1,
+                uint64_t na, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -176,6 +176,11 @@ int mxh_rss_cross(int kind, int words, const void* x0, const void* x1, const voi
                   uint64_t nonce, void* stream);
 int mxh_prf_expand(int words, void* out, int64_t n, int nkeys, const uint8_t* keys16,
                    uint64_t nonce, void* stream);
+int mxh_rss_cross_k(int kind, int words, const void* x0, const void* x1, const void* y0,
+                    const void* y1, void* out, int64_t n, int nparties, const uint32_t* slots,
+                    int nslots, uint64_t nonce, void* stream);
+int mxh_prf_expand_k(int words, void* out, int64_t n, int nkeys, const uint32_t* slots,
+                     uint64_t nonce, void* stream);
 int mxh_gemm(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
              const void* A1, const void* B0, const void* B1, int mode, void* C, int accumulate,
              void* stream);

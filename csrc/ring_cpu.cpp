@@ -490,4 +490,37 @@ int mx_gemm(int dev, int words, int64_t batch, int64_t M, int64_t N, int64_t K,
   return -2;
 }
 
+// ---- key slots ---------------------------------------------------------------------
+void mx_key_slots(const uint8_t* keys16, int n, uint32_t* out) {
+  for (int i = 0; i < n; ++i) {
+    uint32_t* slot = out + (int64_t)MX_KEY_SLOT_WORDS * i;
+    memcpy(slot, keys16 + 16 * i, 16);
+    mx::expand_key(keys16 + 16 * i, slot + 4);
+  }
+}
+
+int mx_rss_cross_k(int dev, int kind, int words, const void* x0, const void* x1,
+                   const void* y0, const void* y1, void* out, int64_t n, int nparties,
+                   const uint32_t* slots, int nslots, uint64_t nonce, void* stream) {
+  if (nslots < 1 || nparties < 1 || nparties > 3) return -3;
+  if (dev)
+    return mxh_rss_cross_k(kind, words, x0, x1, y0, y1, out, n, nparties, slots, nslots, nonce,
+                           stream);
+  uint8_t keys[16 * 4];  // host slots: the raw keys lead each slot
+  for (int i = 0; i <= nparties; ++i)
+    memcpy(keys + 16 * i, slots + MX_KEY_SLOT_WORDS * (i % nslots), 16);
+  DISPATCH_WORDS(words, T,
+                 return rss_cross_t<T>(kind, (const T*)x0, (const T*)x1, (const T*)y0,
+                                       (const T*)y1, (T*)out, n, nparties, keys, nonce));
+}
+
+int mx_prf_expand_k(int dev, int words, void* out, int64_t n, int nkeys, const uint32_t* slots,
+                    uint64_t nonce, void* stream) {
+  if (nkeys < 1 || nkeys > 4) return -3;
+  if (dev) return mxh_prf_expand_k(words, out, n, nkeys, slots, nonce, stream);
+  uint8_t keys[16 * 4];
+  for (int i = 0; i < nkeys; ++i) memcpy(keys + 16 * i, slots + MX_KEY_SLOT_WORDS * i, 16);
+  DISPATCH_WORDS(words, T, return prf_expand_t<T>((T*)out, n, nkeys, keys, nonce));
+}
+
 }  // extern "C"

@@ -16,6 +16,7 @@
 #include <cstring>
 
 #include "aes_core.h"
+#include "aes_dev.h"
 #include "moosex.h"
 #include "ring_common.h"
 
@@ -23,8 +24,6 @@ using mxr::u128;
 using u64 = uint64_t;
 
 namespace {
-
-__constant__ uint8_t c_sbox[256] = MX_SBOX_INIT;
 
 constexpr int kBlock = 256;
 
@@ -137,29 +136,13 @@ __global__ void k_sum_axis_wide(const T* __restrict__ a, T* __restrict__ out, in
 // ---------------------------------------------------------------------------
 // AES
 // ---------------------------------------------------------------------------
-struct RK {
-  uint32_t rk[44];
-};
-struct Keys4 {
-  uint32_t rk[4][44];
-};
-
-__device__ inline void stage_tables(uint32_t* T, uint8_t* Sb) {
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
-    uint8_t s = c_sbox[i];
-    Sb[i] = s;
-    T[i] = mx::t0_entry(s);
-  }
-  __syncthreads();
-}
-
-__device__ inline void aes_ctr(const uint32_t* rk, const uint32_t* T, const uint8_t* Sb,
-                               uint64_t nonce, uint64_t ctr, uint64_t* lo, uint64_t* hi) {
-  uint32_t w[4], o[4];
-  mx::ctr_block_words(nonce, ctr, w);
-  mx::encrypt_block_tt(rk, T, Sb, w[0], w[1], w[2], w[3], o);
-  mx::block_to_u64(o, lo, hi);
-}
+using mxd::aes_ctr;
+using mxd::KeySrc;
+using mxd::Lane;
+using mxd::pick;
+using mxd::RK;
+using mxd::stage_keys;
+using mxd::stage_tables;
 
 __global__ void k_prg(RK key, uint64_t nonce, uint64_t ctr0, uint8_t* __restrict__ out,
                       int64_t nbytes) {
@@ -185,31 +168,20 @@ __global__ void k_prg(RK key, uint64_t nonce, uint64_t ctr0, uint8_t* __restrict
 }
 
 // Element e of type T lives in keystream block e / (16 / sizeof(T)); one thread per block.
-template <class T>
-struct Lane {
-  static constexpr int kPer = 16 / (int)sizeof(T);  // elements per AES block
-};
-
-template <class T>
-__device__ inline T pick(uint64_t lo, uint64_t hi, int j) {
-  if constexpr (sizeof(T) == 16) {
-    return ((T)hi << 64) | (T)lo;
-  } else if constexpr (sizeof(T) == 8) {
-    return j == 0 ? lo : hi;
-  } else {
-    uint64_t w = j < 8 ? lo : hi;
-    return (T)((w >> (8 * (j & 7))) & 1);
-  }
-}
-
+// Key schedules are staged in LDS next to the T-table (from launch parameters or from
+// key slots in device memory, see aes_dev.h).
 template <class T>
 __global__ void k_rss_cross(int kind, const T* __restrict__ x0, const T* __restrict__ x1,
                             const T* __restrict__ y0, const T* __restrict__ y1,
                             T* __restrict__ out, int64_t n, int nparties, int has_keys,
-                            Keys4 keys, uint64_t nonce) {
+                            KeySrc keys, uint64_t nonce) {
   __shared__ uint32_t Tt[256];
   __shared__ uint8_t Sb[256];
-  if (has_keys) stage_tables(Tt, Sb);
+  __shared__ uint32_t rks[4][44];
+  if (has_keys) {
+    stage_keys(rks, keys, nparties + 1);
+    stage_tables(Tt, Sb);
+  }
   constexpr int P = Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;  // keystream blocks per party
   const int64_t total = nb * nparties;
@@ -219,8 +191,8 @@ __global__ void k_rss_cross(int kind, const T* __restrict__ x0, const T* __restr
     const int64_t b = g % nb;
     uint64_t alo = 0, ahi = 0, blo = 0, bhi = 0;
     if (has_keys) {
-      aes_ctr(keys.rk[p], Tt, Sb, nonce, (uint64_t)b, &alo, &ahi);
-      aes_ctr(keys.rk[p + 1], Tt, Sb, nonce, (uint64_t)b, &blo, &bhi);
+      aes_ctr(rks[p], Tt, Sb, nonce, (uint64_t)b, &alo, &ahi);
+      aes_ctr(rks[p + 1], Tt, Sb, nonce, (uint64_t)b, &blo, &bhi);
     }
 #pragma unroll
     for (int j = 0; j < P; ++j) {
@@ -246,9 +218,11 @@ __global__ void k_rss_cross(int kind, const T* __restrict__ x0, const T* __restr
 template <class T>
 __global__ void k_rss_cross_ring3(int kind, const T* __restrict__ x0, const T* __restrict__ x1,
                                   const T* __restrict__ y0, const T* __restrict__ y1,
-                                  T* __restrict__ out, int64_t n, Keys4 keys, uint64_t nonce) {
+                                  T* __restrict__ out, int64_t n, KeySrc keys, uint64_t nonce) {
   __shared__ uint32_t Tt[256];
   __shared__ uint8_t Sb[256];
+  __shared__ uint32_t rks[3][44];
+  stage_keys(rks, keys, 3);
   stage_tables(Tt, Sb);
   constexpr int P = Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;
@@ -256,7 +230,7 @@ __global__ void k_rss_cross_ring3(int kind, const T* __restrict__ x0, const T* _
        b += (int64_t)gridDim.x * blockDim.x) {
     uint64_t lo[3], hi[3];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) aes_ctr(keys.rk[q], Tt, Sb, nonce, (uint64_t)b, &lo[q], &hi[q]);
+    for (int q = 0; q < 3; ++q) aes_ctr(rks[q], Tt, Sb, nonce, (uint64_t)b, &lo[q], &hi[q]);
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
       const int q = p == 2 ? 0 : p + 1;
@@ -278,10 +252,12 @@ __global__ void k_rss_cross_ring3(int kind, const T* __restrict__ x0, const T* _
 }
 
 template <class T>
-__global__ void k_prf_expand(T* __restrict__ out, int64_t n, int nkeys, Keys4 keys,
+__global__ void k_prf_expand(T* __restrict__ out, int64_t n, int nkeys, KeySrc keys,
                              uint64_t nonce) {
   __shared__ uint32_t Tt[256];
   __shared__ uint8_t Sb[256];
+  __shared__ uint32_t rks[4][44];
+  stage_keys(rks, keys, nkeys);
   stage_tables(Tt, Sb);
   constexpr int P = Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;
@@ -291,7 +267,7 @@ __global__ void k_prf_expand(T* __restrict__ out, int64_t n, int nkeys, Keys4 ke
     const int p = (int)(g / nb);
     const int64_t b = g % nb;
     uint64_t lo, hi;
-    aes_ctr(keys.rk[p], Tt, Sb, nonce, (uint64_t)b, &lo, &hi);
+    aes_ctr(rks[p], Tt, Sb, nonce, (uint64_t)b, &lo, &hi);
 #pragma unroll
     for (int j = 0; j < P; ++j) {
       int64_t e = b * P + j;
@@ -353,12 +329,6 @@ int launch_gemm_valu(int64_t batch, int64_t M, int64_t N, int64_t K, const void*
   return 0;
 }
 
-Keys4 load_keys(const uint8_t* keys16, int nkeys) {
-  Keys4 k;
-  memset(&k, 0, sizeof(k));
-  for (int i = 0; i < nkeys && i < 4; ++i) mx::expand_key(keys16 + 16 * i, k.rk[i]);
-  return k;
-}
 
 }  // namespace
 
@@ -499,13 +469,15 @@ int mxh_prg(const uint8_t* key16, uint64_t nonce, uint64_t ctr0, void* out, int6
   return 0;
 }
 
-int mxh_rss_cross(int kind, int words, const void* x0, const void* x1, const void* y0,
-                  const void* y1, void* out, int64_t n, int nparties, const uint8_t* keys16,
-                  uint64_t nonce, void* stream) {
+}  // extern "C"
+
+namespace {
+
+int launch_rss_cross(int kind, int words, const void* x0, const void* x1, const void* y0,
+                     const void* y1, void* out, int64_t n, int nparties, bool has_keys,
+                     bool ring3, const KeySrc& k, uint64_t nonce, void* stream) {
   if (n == 0) return 0;
   if (nparties < 1 || nparties > 3) return -3;
-  Keys4 k = keys16 ? load_keys(keys16, nparties + 1) : Keys4{};
-  const bool ring3 = keys16 && nparties == 3 && std::memcmp(keys16, keys16 + 48, 16) == 0;
   DEV_DISPATCH(words, T, {
     constexpr int P = 16 / (int)sizeof(T);
     if (ring3) {
@@ -519,17 +491,16 @@ int mxh_rss_cross(int kind, int words, const void* x0, const void* x1, const voi
     int64_t work = ((n + P - 1) / P) * nparties;
     hipLaunchKernelGGL(k_rss_cross<T>, dim3(grid_for(work)), dim3(kBlock), 0, S(stream), kind,
                        (const T*)x0, (const T*)x1, (const T*)y0, (const T*)y1, (T*)out, n,
-                       nparties, keys16 != nullptr, k, nonce);
+                       nparties, has_keys ? 1 : 0, k, nonce);
     MX_LAUNCH_CHECK();
     return 0;
   });
 }
 
-int mxh_prf_expand(int words, void* out, int64_t n, int nkeys, const uint8_t* keys16,
-                   uint64_t nonce, void* stream) {
+int launch_prf_expand(int words, void* out, int64_t n, int nkeys, const KeySrc& k,
+                      uint64_t nonce, void* stream) {
   if (n == 0) return 0;
   if (nkeys < 1 || nkeys > 4) return -3;
-  Keys4 k = load_keys(keys16, nkeys);
   DEV_DISPATCH(words, T, {
     constexpr int P = 16 / (int)sizeof(T);
     int64_t work = ((n + P - 1) / P) * nkeys;
@@ -538,6 +509,44 @@ int mxh_prf_expand(int words, void* out, int64_t n, int nkeys, const uint8_t* ke
     MX_LAUNCH_CHECK();
     return 0;
   });
+}
+
+}  // namespace
+
+extern "C" {
+
+int mxh_rss_cross(int kind, int words, const void* x0, const void* x1, const void* y0,
+                  const void* y1, void* out, int64_t n, int nparties, const uint8_t* keys16,
+                  uint64_t nonce, void* stream) {
+  KeySrc k = keys16 ? mxd::keysrc_host(keys16, nparties + 1) : mxd::keysrc_slots(nullptr, 0);
+  const bool ring3 = keys16 && nparties == 3 && std::memcmp(keys16, keys16 + 48, 16) == 0;
+  return launch_rss_cross(kind, words, x0, x1, y0, y1, out, n, nparties, keys16 != nullptr,
+                          ring3, k, nonce, stream);
+}
+
+int mxh_rss_cross_k(int kind, int words, const void* x0, const void* x1, const void* y0,
+                    const void* y1, void* out, int64_t n, int nparties, const uint32_t* slots,
+                    int nslots, uint64_t nonce, void* stream) {
+  if (nslots < 1 || nparties + 1 > 4) return -3;
+  const uint32_t* ptrs[4];
+  for (int i = 0; i <= nparties; ++i) ptrs[i] = slots + MX_KEY_SLOT_WORDS * (i % nslots);
+  const bool ring3 = nparties == 3 && nslots == 3;
+  KeySrc k = mxd::keysrc_slots(ptrs, ring3 ? 3 : nparties + 1);
+  return launch_rss_cross(kind, words, x0, x1, y0, y1, out, n, nparties, true, ring3, k, nonce,
+                          stream);
+}
+
+int mxh_prf_expand(int words, void* out, int64_t n, int nkeys, const uint8_t* keys16,
+                   uint64_t nonce, void* stream) {
+  return launch_prf_expand(words, out, n, nkeys, mxd::keysrc_host(keys16, nkeys), nonce, stream);
+}
+
+int mxh_prf_expand_k(int words, void* out, int64_t n, int nkeys, const uint32_t* slots,
+                     uint64_t nonce, void* stream) {
+  if (nkeys < 1 || nkeys > 4) return -3;
+  const uint32_t* ptrs[4];
+  for (int i = 0; i < nkeys; ++i) ptrs[i] = slots + MX_KEY_SLOT_WORDS * i;
+  return launch_prf_expand(words, out, n, nkeys, mxd::keysrc_slots(ptrs, nkeys), nonce, stream);
 }
 
 int mxh_gemm(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,

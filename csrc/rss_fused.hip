@@ -18,15 +18,17 @@ namespace {
 
 template <class T>
 __global__ void k_trunc_pr3(const T* __restrict__ s0, T* __restrict__ out0, T* __restrict__ out1,
-                            int64_t n, int m, mxd::Keys4 keys, uint64_t n_r0, uint64_t n_r1,
+                            int64_t n, int m, mxd::KeySrc keys, uint64_t n_r0, uint64_t n_r1,
                             uint64_t n_t, uint64_t n_m, uint64_t n_z0, uint64_t n_z2) {
   __shared__ uint32_t Tt[256];
   __shared__ uint8_t Sb[256];
+  __shared__ uint32_t rks[2][44];
+  mxd::stage_keys(rks, keys, 2);
   mxd::stage_tables(Tt, Sb);
   constexpr int P = mxd::Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;
-  const uint32_t* k0 = keys.rk[0];
-  const uint32_t* k2 = keys.rk[1];
+  const uint32_t* k0 = rks[0];
+  const uint32_t* k2 = rks[1];
   for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < nb;
        b += (int64_t)gridDim.x * blockDim.x) {
     uint64_t r0l, r0h, r1l, r1h, tl, th, ml, mh, z0l, z0h, z2l, z2h;
@@ -57,18 +59,20 @@ __global__ void k_trunc_pr3(const T* __restrict__ s0, T* __restrict__ out0, T* _
 
 template <class T>
 __global__ void k_share3(int kind, const T* __restrict__ x, T* __restrict__ out0,
-                         T* __restrict__ out1, int64_t n, int j0, mxd::Keys4 keys, uint64_t n1,
+                         T* __restrict__ out1, int64_t n, int j0, mxd::KeySrc keys, uint64_t n1,
                          uint64_t na) {
   __shared__ uint32_t Tt[256];
   __shared__ uint8_t Sb[256];
+  __shared__ uint32_t rks[2][44];
+  mxd::stage_keys(rks, keys, 2);
   mxd::stage_tables(Tt, Sb);
   constexpr int P = mxd::Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;
   for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < nb;
        b += (int64_t)gridDim.x * blockDim.x) {
     uint64_t al, ah, bl, bh;
-    mxd::aes_ctr(keys.rk[0], Tt, Sb, n1, b, &al, &ah);
-    mxd::aes_ctr(keys.rk[1], Tt, Sb, na, b, &bl, &bh);
+    mxd::aes_ctr(rks[0], Tt, Sb, n1, b, &al, &ah);
+    mxd::aes_ctr(rks[1], Tt, Sb, na, b, &bl, &bh);
 #pragma unroll
     for (int j = 0; j < P; ++j) {
       const int64_t i = b * P + j;
@@ -89,17 +93,9 @@ __global__ void k_share3(int kind, const T* __restrict__ x, T* __restrict__ out0
   }
 }
 
-}  // namespace
-
-extern "C" {
-
-int mxh_trunc_pr3(int words, const void* s0, void* out0, void* out1, int64_t n, int m,
-                  const uint8_t* k0, const uint8_t* k2, const uint64_t* nn, void* stream) {
+int launch_trunc_pr3(int words, const void* s0, void* out0, void* out1, int64_t n, int m,
+                     const mxd::KeySrc& keys, const uint64_t* nn, void* stream) {
   if (n == 0) return 0;
-  uint8_t kk[32];
-  memcpy(kk, k0, 16);
-  memcpy(kk + 16, k2, 16);
-  mxd::Keys4 keys = mxd::load_keys(kk, 2);
   hipStream_t st = (hipStream_t)stream;
   if (words == 1) {
     int64_t nb = (n + 1) / 2;
@@ -117,14 +113,9 @@ int mxh_trunc_pr3(int words, const void* s0, void* out0, void* out1, int64_t n, 
   return e == hipSuccess ? 0 : -100 - (int)e;
 }
 
-int mxh_share3(int kind, int words, const void* x, void* out0, void* out1, int64_t n, int j,
-               const uint8_t* k_next, const uint8_t* k_all, uint64_t n1, uint64_t na,
-               void* stream) {
+int launch_share3(int kind, int words, const void* x, void* out0, void* out1, int64_t n, int j,
+                  const mxd::KeySrc& keys, uint64_t n1, uint64_t na, void* stream) {
   if (n == 0) return 0;
-  uint8_t kk[32];
-  memcpy(kk, k_next, 16);
-  memcpy(kk + 16, k_all, 16);
-  mxd::Keys4 keys = mxd::load_keys(kk, 2);
   hipStream_t st = (hipStream_t)stream;
   switch (words) {
     case 0:
@@ -145,6 +136,43 @@ int mxh_share3(int kind, int words, const void* x, void* out0, void* out1, int64
   }
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : -100 - (int)e;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mxh_trunc_pr3(int words, const void* s0, void* out0, void* out1, int64_t n, int m,
+                  const uint8_t* k0, const uint8_t* k2, const uint64_t* nn, void* stream) {
+  uint8_t kk[32];
+  memcpy(kk, k0, 16);
+  memcpy(kk + 16, k2, 16);
+  return launch_trunc_pr3(words, s0, out0, out1, n, m, mxd::keysrc_host(kk, 2), nn, stream);
+}
+
+int mxh_trunc_pr3_k(int words, const void* s0, void* out0, void* out1, int64_t n, int m,
+                    const uint32_t* slot_k0, const uint32_t* slot_k2, const uint64_t* nn,
+                    void* stream) {
+  const uint32_t* ptrs[2] = {slot_k0, slot_k2};
+  return launch_trunc_pr3(words, s0, out0, out1, n, m, mxd::keysrc_slots(ptrs, 2), nn, stream);
+}
+
+int mxh_share3(int kind, int words, const void* x, void* out0, void* out1, int64_t n, int j,
+               const uint8_t* k_next, const uint8_t* k_all, uint64_t n1, uint64_t na,
+               void* stream) {
+  uint8_t kk[32];
+  memcpy(kk, k_next, 16);
+  memcpy(kk + 16, k_all, 16);
+  return launch_share3(kind, words, x, out0, out1, n, j, mxd::keysrc_host(kk, 2), n1, na,
+                       stream);
+}
+
+int mxh_share3_k(int kind, int words, const void* x, void* out0, void* out1, int64_t n, int j,
+                 const uint32_t* slot_next, const uint32_t* slot_all, uint64_t n1, uint64_t na,
+                 void* stream) {
+  const uint32_t* ptrs[2] = {slot_next, slot_all};
+  return launch_share3(kind, words, x, out0, out1, n, j, mxd::keysrc_slots(ptrs, 2), n1, na,
+                       stream);
 }
 
 }  // extern "C"

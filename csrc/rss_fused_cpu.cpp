@@ -17,6 +17,12 @@ extern "C" int mxh_trunc_pr3(int words, const void* s0, void* out0, void* out1, 
 extern "C" int mxh_share3(int kind, int words, const void* x, void* out0, void* out1, int64_t n,
                           int j, const uint8_t* k_next, const uint8_t* k_all, uint64_t n1,
                           uint64_t na, void* stream);
+extern "C" int mxh_trunc_pr3_k(int words, const void* s0, void* out0, void* out1, int64_t n,
+                               int m, const uint32_t* slot_k0, const uint32_t* slot_k2,
+                               const uint64_t* nonces, void* stream);
+extern "C" int mxh_share3_k(int kind, int words, const void* x, void* out0, void* out1,
+                            int64_t n, int j, const uint32_t* slot_next,
+                            const uint32_t* slot_all, uint64_t n1, uint64_t na, void* stream);
 
 namespace {
 
@@ -112,6 +118,25 @@ int mx_share3(int dev, int kind, int words, const void* x, void* out0, void* out
                                             j, k_next, k_all, n1, na);
   }
   return -2;
+}
+
+// key-slot variants: host slots lead with the raw key (moosex.h)
+int mx_trunc_pr3_k(int dev, int words, const void* s0, void* out0, void* out1, int64_t n, int m,
+                   const uint32_t* slot_k0, const uint32_t* slot_k2, const uint64_t* nonces,
+                   void* stream) {
+  if (dev)
+    return mxh_trunc_pr3_k(words, s0, out0, out1, n, m, slot_k0, slot_k2, nonces, stream);
+  return mx_trunc_pr3(0, words, s0, out0, out1, n, m, (const uint8_t*)slot_k0,
+                      (const uint8_t*)slot_k2, nonces, stream);
+}
+
+int mx_share3_k(int dev, int kind, int words, const void* x, void* out0, void* out1, int64_t n,
+                int j, const uint32_t* slot_next, const uint32_t* slot_all, uint64_t n1,
+                uint64_t na, void* stream) {
+  if (dev)
+    return mxh_share3_k(kind, words, x, out0, out1, n, j, slot_next, slot_all, n1, na, stream);
+  return mx_share3(0, kind, words, x, out0, out1, n, j, (const uint8_t*)slot_next,
+                   (const uint8_t*)slot_all, n1, na, stream);
 }
 
 }  // extern "C"

@@ -55,6 +55,20 @@ _SIGS = {
     "mx_trunc_pr3": (
         c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_vp],
     ),
+    "mx_key_slots": (None, [ctypes.c_char_p, c_int, c_vp]),
+    "mx_rss_cross_k": (
+        c_int,
+        [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_u64,
+         c_vp],
+    ),
+    "mx_prf_expand_k": (c_int, [c_int, c_int, c_vp, c_i64, c_int, c_vp, c_u64, c_vp]),
+    "mx_trunc_pr3_k": (
+        c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_vp],
+    ),
+    "mx_share3_k": (
+        c_int,
+        [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_u64, c_u64, c_vp],
+    ),
     "mx_share3": (
         c_int,
         [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_u64, c_u64, c_vp],

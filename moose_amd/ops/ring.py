@@ -18,6 +18,7 @@ Parity: reference host ring kernels ``moose/src/host/ops.rs:1709-2036``.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from typing import List
 from typing import Sequence
@@ -642,6 +643,21 @@ def prf_expand(keys: Sequence[bytes], nonce: int, shape, bits, device) -> RT:
     return out
 
 
+def prf_expand_k(slot_ptr: int, nkeys: int, nonce: int, shape, bits, device) -> RT:
+    """``prf_expand`` with the keys read from ``nkeys`` consecutive key slots."""
+    shape = tuple(shape)
+    n = math.prod(shape)
+    out = empty((nkeys,) + shape, bits, device)
+    nat.check(
+        nat.lib().mx_prf_expand_k(
+            nat.dev_of(out.data), _words(bits), nat.ptr(out.data), n, nkeys,
+            ctypes.c_void_p(slot_ptr), nonce & MASK64, nat.stream_of(out.data),
+        ),
+        "prf_expand_k",
+    )
+    return out
+
+
 def prg_bytes(key: bytes, nonce: int, nbytes: int, device="cpu", ctr0=0) -> torch.Tensor:
     out = torch.empty(nbytes, dtype=torch.uint8, device=device)
     kb = nat.key_buffer([key])
@@ -663,7 +679,15 @@ def aes_encrypt(key: bytes, block: bytes) -> bytes:
     return out.raw
 
 
-def rss_cross(kind: str, x0: RT, x1, y0: RT, y1, keys, nonce: int, nparties: int) -> RT:
+def rss_cross_k(kind: str, x0: RT, x1, y0, y1, slot_ptr: int, nslots: int, nonce: int,
+                nparties: int) -> RT:
+    """``rss_cross`` with the zero-share keys read from key slots: party p uses slots
+    p % nslots and (p + 1) % nslots."""
+    return rss_cross(kind, x0, x1, y0, y1, None, nonce, nparties, _slots=(slot_ptr, nslots))
+
+
+def rss_cross(kind: str, x0: RT, x1, y0: RT, y1, keys, nonce: int, nparties: int,
+              _slots=None) -> RT:
     """Fused RSS local step.  Stacked layout: x* are [nparties, *shape]; party p gets
     x0*y0 + x0*y1 + x1*y0 + PRF(k_p) - PRF(k_{p+1}) (boolean: & / ^).  ``keys`` is a list
     of nparties+1 keys (or None for no zero share)."""
@@ -684,6 +708,17 @@ def rss_cross(kind: str, x0: RT, x1, y0: RT, y1, keys, nonce: int, nparties: int
     n_total = math.prod(shp)
     n = n_total // nparties
     out = empty(shp, bits, x0.device)
+    if _slots is not None:
+        nat.check(
+            nat.lib().mx_rss_cross_k(
+                nat.dev_of(out.data), 1 if kind == "bool" else 0, _words(bits),
+                nat.ptr(datas[0]), nat.ptr(datas[1]), nat.ptr(datas[2]), nat.ptr(datas[3]),
+                nat.ptr(out.data), n, nparties, ctypes.c_void_p(_slots[0]), _slots[1],
+                nonce & MASK64, nat.stream_of(out.data),
+            ),
+            "rss_cross_k",
+        )
+        return out
     kbuf = nat.key_buffer(keys) if keys is not None else None
     nat.check(
         nat.lib().mx_rss_cross(

@@ -1,0 +1,104 @@
+"""Session PRF keys held in device memory ("key slots").
+
+Every PRF evaluation of a stacked session -- zero shares, input sharing, the dealer masks
+of TruncPr, seeded sampling -- is an AES-128-CTR keystream under one of the session's
+keys.  Instead of expanding the key on the host and passing the schedule as a launch
+parameter, the session keeps its keys in a :class:`KeyTable`: one device tensor of
+``MX_KEY_SLOT_WORDS``-word slots (raw key + expanded schedule, ``csrc/moosex.h``) that the
+kernels read at run time.  Two things follow:
+
+* a hipGraph captured from an evaluation does not bake the keys in: refreshing the table
+  before each replay gives every replay fresh, independent randomness
+  (:mod:`moose_amd.runtime.graphs`);
+* setup costs one small host->device copy per placement instead of a key expansion per
+  kernel launch.
+
+Parity: the keys play the role of the reference's ``RepSetup`` PRF keys
+(``replicated/setup.rs:39-58``) and the seeds of ``PrfKeyGen``/``DeriveSeed``
+(``host/prim.rs:113-150``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+import torch
+
+from moose_amd.ops import native as nat
+
+SLOT_WORDS = 48  # MX_KEY_SLOT_WORDS
+
+
+class KeyRef:
+    """A seed that lives in a key slot (what ``h_fresh_seed`` hands out)."""
+
+    __slots__ = ("table", "slot")
+
+    def __init__(self, table: "KeyTable", slot: int):
+        self.table = table
+        self.slot = slot
+
+    @property
+    def ptr(self):
+        return self.table.ptr(self.slot)
+
+    def __len__(self):
+        return 16
+
+
+def slot_words(keys) -> np.ndarray:
+    """Host image of ``len(keys)`` slots."""
+    raw = b"".join(bytes(k) for k in keys)
+    out = np.zeros((len(keys), SLOT_WORDS), dtype=np.uint32)
+    nat.lib().mx_key_slots(ctypes.c_char_p(raw), len(keys),
+                           out.ctypes.data_as(ctypes.c_void_p))
+    return out
+
+
+class KeyTable:
+    """Fixed-capacity table of key slots on ``device``.
+
+    ``alloc`` hands out consecutive slots and (unless the table is *frozen*) fills them
+    with fresh keys.  A frozen table -- the state during hipGraph capture -- never writes:
+    its contents were filled by :meth:`refresh` beforehand and are refreshed again before
+    each replay.
+    """
+
+    def __init__(self, device, capacity: int = 256, random_bytes=None):
+        self.device = torch.device(device)
+        self.capacity = capacity
+        self.t = torch.zeros((capacity, SLOT_WORDS), dtype=torch.int32, device=self.device)
+        self.n = 0
+        self.frozen = False
+        self._rand = random_bytes or os.urandom
+
+    def alloc(self, n: int) -> int:
+        base = self.n
+        if base + n > self.capacity:
+            if self.frozen:
+                raise RuntimeError("key table exhausted during graph capture")
+            grown = torch.zeros((max(2 * self.capacity, base + n), SLOT_WORDS),
+                                dtype=torch.int32, device=self.device)
+            grown[:self.capacity].copy_(self.t)
+            self.t, self.capacity = grown, grown.shape[0]
+        self.n = base + n
+        if not self.frozen:
+            self._write(base, [self._rand(16) for _ in range(n)])
+        return base
+
+    def _write(self, base: int, keys):
+        img = torch.from_numpy(slot_words(keys).view(np.int32))
+        self.t[base:base + len(keys)].copy_(img)
+
+    def refresh(self, upto: int = None):
+        """Fresh random keys for slots ``[0, upto)`` (default: every slot)."""
+        n = self.capacity if upto is None else upto
+        self._write(0, [os.urandom(16) for _ in range(n)])
+
+    def ptr(self, slot: int) -> int:
+        return self.t.data_ptr() + slot * SLOT_WORDS * 4
+
+    def raw_key(self, slot: int) -> bytes:
+        """The raw 16-byte key of a slot (reads device memory; host-side uses only)."""
+        return self.t[slot, :4].cpu().numpy().astype(np.int32).tobytes()

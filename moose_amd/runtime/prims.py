@@ -306,6 +306,9 @@ def _sample_seeded(nb, shape, seed, bits, device="cpu"):
     """Uniform ring tensor expanded with AES-128-CTR from a seed: a fresh 16-byte key
     (nonce 0) or a 32-byte ``DeriveSeed`` output key || nonce (reference
     ``host/ops.rs:1883-2036`` + ``host/prim.rs:123-150``)."""
+    if hasattr(seed, "table"):  # a KeyRef: the seed lives in a device key slot
+        out = R.prf_expand_k(seed.ptr, 1, 0, tuple(shape), bits, device)
+        return R.RT(out.data[0], bits)
     seed = bytes(seed)
     key, nonce = seed[:16], int.from_bytes(seed[16:24], "little") if len(seed) > 16 else 0
     out = R.prf_expand([key], nonce, tuple(shape), bits, device)

@@ -72,6 +72,8 @@ def _nbytes(v):
         return v.numel() * v.element_size()
     if isinstance(v, (bytes, bytearray)):
         return len(v)
+    if type(v).__name__ == "KeyRef":
+        return 16
     return 8
 
 
@@ -116,16 +118,30 @@ class StackedSession(Session):
     is_simulated = True
 
     # -- keys ------------------------------------------------------------------
-    def setup(self, plc) -> List[bytes]:
-        ks = self._keys.get(plc)
-        if ks is None:
-            ks = [self._random_bytes() for _ in range(4)]  # k0, k1, k2, k_all
-            self._keys[plc] = ks
-        return ks
+    # Keys live in a device key table (runtime/keys.py): placement plc owns four slots
+    # k0, k1, k2, k_all at self._keys[plc]; party p holds k_p and k_{p+1}.
+    @property
+    def keytable(self):
+        kt = getattr(self, "_keytable", None)
+        if kt is None:
+            from moose_amd.runtime.keys import KeyTable
 
-    def party_keys(self, plc):
-        k = self.setup(plc)
-        return [k[0], k[1], k[2], k[0]]
+            kt = self._keytable = KeyTable(self.device, random_bytes=self._random_bytes)
+        return kt
+
+    def use_keytable(self, kt):
+        """Run on a caller-provided key table (graph capture: a frozen, refreshed one)."""
+        self._keytable = kt
+
+    def setup(self, plc) -> int:
+        base = self._keys.get(plc)
+        if base is None:
+            base = self.keytable.alloc(4)  # k0, k1, k2, k_all
+            self._keys[plc] = base
+        return base
+
+    def key_ptr(self, plc, i) -> int:
+        return self.keytable.ptr(self.setup(plc) + i)
 
     # -- host ops ----------------------------------------------------------------
     def h(self, prim, host, *args, **attrs):
@@ -148,13 +164,15 @@ class StackedSession(Session):
 
     def h_prf(self, plc, host, key_id, shape: HV, bits, nonce):
         """PRF(k_key_id, nonce) sampled on ``host`` (which must hold that key)."""
-        keys = self.setup(plc)
-        k = keys[3] if key_id == "all" else keys[key_id]
-        out = R.prf_expand([k], nonce, tuple(shape.v), bits, self.device)
+        ptr = self.key_ptr(plc, 3 if key_id == "all" else key_id)
+        out = R.prf_expand_k(ptr, 1, nonce, tuple(shape.v), bits, self.device)
         return HV(host, R.RT(out.data[0], bits))
 
     def h_fresh_seed(self, host):
-        return HV(host, self._random_bytes())
+        from moose_amd.runtime.keys import KeyRef
+
+        kt = self.keytable
+        return HV(host, KeyRef(kt, kt.alloc(1)))
 
     # -- party vectors -------------------------------------------------------------
     def p(self, prim, plc, *args, **attrs):
@@ -226,17 +244,20 @@ class StackedSession(Session):
     # -- fused RSS kernels -----------------------------------------------------------
     def p_cross(self, kind, plc, x0, x1, y0, y1, zero_share=True):
         """Party p: x0*y0 + x0*y1 + x1*y0 (+ alpha_p with sum alpha = 0), one kernel."""
-        keys = self.party_keys(plc) if zero_share else None
-        out = R.rss_cross(kind, x0.v, x1.v if x1 is not None else None, y0.v,
-                          y1.v if y1 is not None else None, keys, self.nonce(plc), 3)
+        x1v = x1.v if x1 is not None else None
+        y1v = y1.v if y1 is not None else None
+        if not zero_share:
+            return PV(plc, R.rss_cross(kind, x0.v, x1v, y0.v, y1v, None, self.nonce(plc), 3))
+        out = R.rss_cross_k(kind, x0.v, x1v, y0.v, y1v, self.key_ptr(plc, 0), 3,
+                            self.nonce(plc), 3)
         return PV(plc, out)
 
     def p_dot_cross(self, plc, x0, x1, y0, y1):
         return PV(plc, R.dot_cross(x0.v, x1.v, y0.v, y1.v, nb=1))
 
     def p_add_zero_share(self, plc, z, kind="arith"):
-        keys = self.party_keys(plc)
-        return PV(plc, R.rss_cross(kind, z.v, None, None, None, keys, self.nonce(plc), 3))
+        return PV(plc, R.rss_cross_k(kind, z.v, None, None, None, self.key_ptr(plc, 0), 3,
+                                     self.nonce(plc), 3))
 
     def p_shape(self, x: PV):
         return tuple(x.v.shape[1:])
@@ -250,15 +271,15 @@ class StackedSession(Session):
 
         from moose_amd.ops import native as nat
 
-        keys = self.setup(x.plc)
         s0 = x.s0.v.data.contiguous()
         out0, out1 = torch.empty_like(s0), torch.empty_like(s0)
         n = x.s0.v.numel() // 3
         nn = (ctypes.c_uint64 * 6)(*[v & ((1 << 64) - 1) for v in nonces])
         nat.check(
-            nat.lib().mx_trunc_pr3(
+            nat.lib().mx_trunc_pr3_k(
                 nat.dev_of(s0), R._words(x.bits), nat.ptr(s0), nat.ptr(out0), nat.ptr(out1), n, m,
-                nat.key_buffer([keys[0]]), nat.key_buffer([keys[2]]), nn, nat.stream_of(s0),
+                ctypes.c_void_p(self.key_ptr(x.plc, 0)), ctypes.c_void_p(self.key_ptr(x.plc, 2)),
+                nn, nat.stream_of(s0),
             ),
             "trunc_pr3",
         )
@@ -273,19 +294,20 @@ class StackedSession(Session):
         return PV(x.plc, R.RT(out0, x.bits)), PV(x.plc, R.RT(out1, x.bits))
 
     def fused_share(self, plc, x: HV, j, kind, n1, na):
+        import ctypes
+
         from moose_amd.ops import native as nat
 
-        keys = self.setup(plc)
         xd = x.v.data.contiguous()
         shape = (3,) + tuple(xd.shape)
         out0 = torch.empty(shape, dtype=xd.dtype, device=xd.device)
         out1 = torch.empty_like(out0)
         nat.check(
-            nat.lib().mx_share3(
+            nat.lib().mx_share3_k(
                 nat.dev_of(xd), 1 if kind == "bool" else 0, R._words(x.v.bits), nat.ptr(xd),
                 nat.ptr(out0), nat.ptr(out1), x.v.numel(), j,
-                nat.key_buffer([keys[(j + 1) % 3]]), nat.key_buffer([keys[3]]), n1, na,
-                nat.stream_of(xd),
+                ctypes.c_void_p(self.key_ptr(plc, (j + 1) % 3)),
+                ctypes.c_void_p(self.key_ptr(plc, 3)), n1, na, nat.stream_of(xd),
             ),
             "share3",
         )

@@ -1,0 +1,78 @@
+"""Key slots (runtime/keys.py, csrc/moosex.h): PRF evaluations with keys read from a
+device key table are bit-identical to the same PRFs with host-expanded keys, and a
+refreshed table yields different randomness."""
+import os
+
+import pytest
+import torch
+
+from moose_amd.ops import ring as R
+from moose_amd.runtime.keys import KeyTable
+
+
+
+def _table(device, keys):
+    kt = KeyTable(device, capacity=8)
+    kt._write(0, keys)
+    kt.n = len(keys)
+    return kt
+
+
+def _devices():
+    return [pytest.param("cpu")] + [pytest.param("cuda", marks=pytest.mark.gpu)]
+
+
+@pytest.mark.parametrize("device", _devices())
+@pytest.mark.parametrize("bits", [1, 64, 128])
+def test_rss_cross_slots_match_host_keys(device, bits):
+    if device == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    keys = [os.urandom(16) for _ in range(3)]
+    kt = _table(device, keys)
+    shape = (3, 37, 5)
+    x0, x1, y0, y1 = (R.prf_expand([os.urandom(16)], 1, shape, bits, device) for _ in range(4))
+    x0, x1, y0, y1 = (R.RT(t.data[0], bits) for t in (x0, x1, y0, y1))
+    kind = "bool" if bits == 1 else "arith"
+    ref = R.rss_cross(kind, x0, x1, y0, y1, keys + [keys[0]], 7, 3)
+    got = R.rss_cross_k(kind, x0, x1, y0, y1, kt.ptr(0), 3, 7, 3)
+    assert torch.equal(ref.data.cpu(), got.data.cpu())
+    zs = R.rss_cross_k(kind, R.zeros(shape, bits, device), None, None, None, kt.ptr(0), 3, 9, 3)
+    ref_zs = R.rss_cross(kind, R.zeros(shape, bits, device), None, None, None,
+                         keys + [keys[0]], 9, 3)
+    assert torch.equal(zs.data.cpu(), ref_zs.data.cpu())
+
+
+@pytest.mark.parametrize("device", _devices())
+@pytest.mark.parametrize("bits", [1, 64, 128])
+def test_prf_expand_slots_match_host_keys(device, bits):
+    if device == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    keys = [os.urandom(16) for _ in range(2)]
+    kt = _table(device, keys)
+    ref = R.prf_expand(keys, 5, (10, 3), bits, device)
+    got = R.prf_expand_k(kt.ptr(0), 2, 5, (10, 3), bits, device)
+    assert torch.equal(ref.data.cpu(), got.data.cpu())
+    one = R.prf_expand_k(kt.ptr(1), 1, 5, (10, 3), bits, device)
+    assert torch.equal(one.data[0].cpu(), ref.data[1].cpu())
+
+
+def test_refresh_changes_keys_and_randomness():
+    kt = KeyTable("cpu", capacity=4)
+    base = kt.alloc(2)
+    before = kt.raw_key(base)
+    a = R.prf_expand_k(kt.ptr(base), 1, 1, (64,), 64, "cpu")
+    kt.refresh()
+    assert kt.raw_key(base) != before
+    b = R.prf_expand_k(kt.ptr(base), 1, 1, (64,), 64, "cpu")
+    assert not torch.equal(a.data, b.data)
+
+
+def test_frozen_table_does_not_write():
+    kt = KeyTable("cpu", capacity=4)
+    kt.refresh()
+    snap = kt.t.clone()
+    kt.frozen = True
+    kt.alloc(3)
+    assert torch.equal(snap, kt.t)
+    with pytest.raises(RuntimeError):
+        kt.alloc(2)
