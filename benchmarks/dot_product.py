@@ -101,12 +101,14 @@ def main(argv=None):
     ap.add_argument("--max_n", type=int, default=1000)
     ap.add_argument("--runtime", choices=["local", "distributed"], default="local")
     ap.add_argument("--device", default=None)
+    ap.add_argument("--graphs", action="store_true",
+                    help="replay each evaluation as a captured hipGraph (runtime/graphs.py)")
     ap.add_argument("--json", default=None)
     args = ap.parse_args(argv)
 
     ids = ["alice", "bob", "carole"]
     if args.runtime == "local":
-        runtime = pm.LocalMooseRuntime(ids, device=args.device)
+        runtime = pm.LocalMooseRuntime(ids, device=args.device, use_graphs=args.graphs)
     else:
         runtime = pm.DistributedMooseRuntime(ids, timeout=1800)
     if args.sweep:
@@ -117,7 +119,7 @@ def main(argv=None):
     results = []
     for mode, k, n in cases:
         res = run_one(runtime, mode, n, k, args.n_iter)
-        res["runtime"] = args.runtime
+        res["runtime"] = args.runtime + ("+graphs" if args.graphs else "")
         res["device"] = str(getattr(runtime, "device", "distributed"))
         results.append(res)
         print(json.dumps(res), flush=True)

@@ -119,6 +119,8 @@ def main(argv=None):
     ap.add_argument("--n_exp", type=int, default=3)
     ap.add_argument("--runtime", choices=["local", "distributed"], default="local")
     ap.add_argument("--device", default=None)
+    ap.add_argument("--graphs", action="store_true",
+                    help="replay each evaluation as a captured hipGraph (runtime/graphs.py)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--json", default=None, help="append one JSON result line to this file")
     args = ap.parse_args(argv)
@@ -138,7 +140,7 @@ def main(argv=None):
     t_trace = time.perf_counter() - t_trace
     ids = ["alice", "bob", "carole"]
     if args.runtime == "local":
-        runtime = pm.LocalMooseRuntime(ids, device=args.device)
+        runtime = pm.LocalMooseRuntime(ids, device=args.device, use_graphs=args.graphs)
     else:
         runtime = pm.DistributedMooseRuntime(ids, timeout=1200)
     arguments = {"x": x, "y": y, "w_0": w0, "b_0": b0}
@@ -158,7 +160,7 @@ def main(argv=None):
     ref = REFERENCE_S.get((args.batch_size, args.n_iter))
     res = {
         "bench": "logreg_train", "batch_size": args.batch_size, "n_iter": args.n_iter,
-        "n_features": N_FEATURES, "dtype": "fixed(24,40)/ring128", "runtime": args.runtime,
+        "n_features": N_FEATURES, "dtype": "fixed(24,40)/ring128", "runtime": args.runtime + ("+graphs" if args.graphs else ""),
         "device": str(getattr(runtime, "device", runtime.__class__.__name__)),
         "session_s": {"min": min(session_s), "max": max(session_s),
                       "mean": statistics.mean(session_s)},

@@ -36,6 +36,20 @@ _UN = {"neg": 0, "not": 1, "shl": 2, "shr": 3, "sar": 4}
 _CMP = {"lt": 0, "gt": 1, "eq": 2, "msb": 3}
 
 
+# Every host->device copy made while a computation runs goes through to_device, so that
+# hipGraph capture (runtime/graphs.py) can substitute copies staged before the capture.
+_UPLOAD_HOOK = None
+
+
+def to_device(t: torch.Tensor, device) -> torch.Tensor:
+    device = torch.device(device)
+    if device.type == "cpu" or t.device == device:
+        return t
+    if _UPLOAD_HOOK is not None:
+        return _UPLOAD_HOOK(t, device)
+    return t.to(device)
+
+
 def _words(bits):
     return {1: 0, 64: 1, 128: 2}[bits]
 
@@ -156,13 +170,13 @@ def from_ints(values, bits, device="cpu") -> RT:
     flat = [int(x) for x in arr.reshape(-1)]
     if bits == 1:
         t = torch.tensor([v & 1 for v in flat], dtype=torch.uint8).reshape(shape)
-        return RT(t.to(device), 1)
+        return RT(to_device(t, device), 1)
     if bits == 64:
         t = torch.tensor([_to_i64(v) for v in flat], dtype=torch.int64).reshape(shape)
-        return RT(t.to(device), 64)
+        return RT(to_device(t, device), 64)
     pairs = [[_to_i64(v & MASK64), _to_i64((v >> 64) & MASK64)] for v in flat]
     t = torch.tensor(pairs, dtype=torch.int64).reshape(shape + (2,))
-    return RT(t.to(device), 128)
+    return RT(to_device(t, device), 128)
 
 
 def to_ints(x: RT) -> np.ndarray:

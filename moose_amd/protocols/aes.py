@@ -62,7 +62,7 @@ def bits_msb_to_ring128(bits: np.ndarray, device) -> R.RT:
     hi = by[..., :8].copy().view(">u8")[..., 0].astype(np.uint64)
     lo = by[..., 8:].copy().view(">u8")[..., 0].astype(np.uint64)
     d = np.stack([lo.view(np.int64), hi.view(np.int64)], axis=-1)
-    return R.RT(torch.as_tensor(d, device=device), 128)
+    return R.RT(R.to_device(torch.as_tensor(d), device), 128)
 
 
 def host_decrypt(key_bits, ct_bits, device="cpu") -> R.RT:
@@ -116,7 +116,7 @@ def rep_decrypt(sess, plc: ReplicatedPlacement, key: rep.RepTensor, ct: rep.RepT
     rm = _slice_rows(sess, ctw, NONCE_BITS, CT_BITS)
     ctr = np.zeros((32,) + tuple(batch), dtype=np.uint8)
     ctr[30] = 1  # counter value 2 in the last 32 bits (MSB first)
-    ctr_sh = rep.from_public(sess, plc, R.RT(torch.as_tensor(ctr, device=sess.device), 1), 1,
+    ctr_sh = rep.from_public(sess, plc, R.RT(R.to_device(torch.as_tensor(ctr), sess.device), 1), 1,
                              kind="bool")
     inp = _concat_rows(sess, [kb, nonce, ctr_sh])
     r = lc.eval_shared(sess, inp)  # [128, *batch]
@@ -177,7 +177,7 @@ def tensor_input(interp, op, name):
 
 
 def _bit_rt(a, device):
-    t = torch.as_tensor(np.asarray(a).astype(np.uint8), device=device)
+    t = R.to_device(torch.as_tensor(np.asarray(a).astype(np.uint8)), device)
     return R.RT(t, 1)
 
 

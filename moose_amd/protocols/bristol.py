@@ -28,6 +28,8 @@ from typing import Tuple
 import numpy as np
 import torch
 
+from moose_amd.ops import ring as R
+
 
 @dataclass
 class Gate:
@@ -190,7 +192,7 @@ class _SparseAffine:
     def matrix(self, device):
         m = self._cache.get(device)
         if m is None:
-            idx = torch.as_tensor(np.stack([self.row_idx, self.col_idx]), device=device)
+            idx = R.to_device(torch.as_tensor(np.stack([self.row_idx, self.col_idx])), device)
             vals = torch.ones(len(self.row_idx), dtype=torch.float32, device=device)
             m = torch.sparse_coo_tensor(idx, vals, (self.nrows, self.ncols)).coalesce()
             self._cache[device] = m
@@ -205,7 +207,7 @@ class _SparseAffine:
 
     def apply(self, base: torch.Tensor) -> torch.Tensor:
         y = self.linear(base)
-        c = torch.as_tensor(self.const, device=base.device).reshape((-1,) + (1,) * (y.dim() - 1))
+        c = R.to_device(torch.as_tensor(self.const), base.device).reshape((-1,) + (1,) * (y.dim() - 1))
         return y ^ c
 
 
@@ -220,6 +222,6 @@ def _affine_shared(sess, aff: _SparseAffine, x):
     y = rep.RepTensor(x.plc, 1, "bool", s0, s1)
     if aff.const.any():
         shape = (aff.nrows,) + (1,) * (len(sess.p_shape(x.s0)) - 1)
-        c = R.RT(torch.as_tensor(aff.const, device=sess.device).reshape(shape), 1)
+        c = R.RT(R.to_device(torch.as_tensor(aff.const), sess.device).reshape(shape), 1)
         y = rep.add_public(sess, y, c)
     return y

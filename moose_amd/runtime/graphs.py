@@ -1,0 +1,197 @@
+"""Whole-evaluation hipGraphs for the stacked (single-GPU) runtime.
+
+An evaluation of a computation on a :class:`StackedSession` is a long, fixed sequence of
+small kernels (a fixed-point sigmoid alone is ~100 launches), so at moderate tensor sizes
+it is bound by Python dispatch and launch latency, not by the GPU.  For a given
+(computation, argument signature) this module records the evaluation once into a HIP
+graph (``torch.cuda.CUDAGraph`` is hipGraph on ROCm) and afterwards replays it:
+
+1. **warm-up run** (eager): produces the first result, sizes every workspace, and records
+   each host->device upload made during the run (public constants; see
+   ``ring.to_device``);
+2. **capture run**: the same evaluation on a fresh session whose PRF keys live in a
+   *frozen* :class:`~moose_amd.runtime.keys.KeyTable` (the kernels read keys from device
+   memory, never from launch parameters), arguments in static device buffers, and every
+   upload served from a copy staged before the capture (checked against the warm-up's
+   bytes: a data-dependent upload aborts the capture);
+3. **replay**: copy the new arguments into the static buffers, refresh the key table
+   with fresh random keys (so each replay draws independent randomness -- the nonce
+   sequence is fixed, the keys are not), replay, decode the outputs.
+
+Anything that cannot be captured (host side effects such as Save/Load, data-dependent
+uploads, CPU devices) falls back to eager evaluation.
+"""
+from __future__ import annotations
+
+import warnings
+from typing import Dict
+
+import numpy as np
+import torch
+
+from moose_amd.ops import ring as R
+from moose_amd.runtime.interpreter import Interpreter
+from moose_amd.runtime.interpreter import dtype_of_numpy
+from moose_amd.runtime.interpreter import numpy_to_torch
+from moose_amd.runtime.keys import KeyTable
+from moose_amd.runtime.session import StackedSession
+
+_SIDE_EFFECTS = {"Save", "Load"}
+
+
+class CaptureError(RuntimeError):
+    pass
+
+
+class _Recorder:
+    def __init__(self):
+        self.items = []  # (host copy, device tensor)
+
+    def __call__(self, t, device):
+        d = t.to(device)
+        self.items.append((t.detach().clone(), d))
+        return d
+
+
+class _Stager:
+    def __init__(self, recorded, device):
+        self.host = [h for h, _ in recorded]
+        self.dev = [h.to(device) for h in self.host]  # staged before the capture begins
+        self.i = 0
+
+    def __call__(self, t, device):
+        i = self.i
+        if i >= len(self.host):
+            raise CaptureError("more uploads than in the warm-up run")
+        h = self.host[i]
+        if h.dtype != t.dtype or h.shape != t.shape or not torch.equal(h, t.cpu()):
+            raise CaptureError("data-dependent host->device upload")
+        self.i += 1
+        return self.dev[i]
+
+
+def _upload_hook(hook):
+    class _Ctx:
+        def __enter__(self):
+            self.prev = R._UPLOAD_HOOK
+            R._UPLOAD_HOOK = hook
+
+        def __exit__(self, *exc):
+            R._UPLOAD_HOOK = self.prev
+
+    return _Ctx()
+
+
+def signature(arguments: dict):
+    """Hashable description of the arguments a plan is specialised on."""
+    sig = []
+    for k in sorted(arguments):
+        v = arguments[k]
+        if isinstance(v, (np.ndarray, np.generic)) or (
+                isinstance(v, (list, tuple)) and v and not isinstance(v[0], (str, bytes))):
+            a = np.asarray(v)
+            sig.append((k, "array", a.shape, a.dtype.str))
+        elif isinstance(v, torch.Tensor):
+            sig.append((k, "tensor", tuple(v.shape), str(v.dtype)))
+        else:
+            sig.append((k, "value", repr(v)))
+    return tuple(sig)
+
+
+def capturable(comp) -> bool:
+    return not any(op.kind in _SIDE_EFFECTS for op in comp.operations)
+
+
+class GraphPlan:
+    """One captured evaluation (see module docstring)."""
+
+    def __init__(self, comp, arguments: dict, device, storage, fixedpoint_ring, seed=None):
+        self.comp = comp
+        self.device = torch.device(device)
+        self.ring = fixedpoint_ring
+        self.storage = storage
+        self.static = {}
+        for k, v in arguments.items():
+            if isinstance(v, (np.ndarray, np.generic)) or (
+                    isinstance(v, (list, tuple)) and v and not isinstance(v[0], (str, bytes))):
+                a = np.asarray(v)
+                t = numpy_to_torch(a, self.device)
+                t._moose_dtype = dtype_of_numpy(a)
+                self.static[k] = t
+            else:
+                self.static[k] = v
+        # 1. warm-up (eager): first result + recorded uploads
+        rec = _Recorder()
+        sess = StackedSession(self.device, seed=seed)
+        interp = Interpreter(sess, storage, fixedpoint_ring)
+        with _upload_hook(rec):
+            outs = interp.run(comp, self.static)
+            self.first = self._decode(interp, outs)
+        self.stats = sess.stats
+        torch.cuda.synchronize(self.device)
+        # 2. capture on a session with a frozen, refreshed key table
+        self.keys = KeyTable(self.device, capacity=max(256, sess.keytable.n + 16))
+        self.keys.refresh()
+        self.keys.frozen = True
+        self.sess = StackedSession(self.device, seed=seed)
+        self.sess.use_keytable(self.keys)
+        self.interp = Interpreter(self.sess, storage, fixedpoint_ring)
+        stager = _Stager(rec.items, self.device)
+        torch.cuda.synchronize(self.device)
+        self.graph = torch.cuda.CUDAGraph()
+        with _upload_hook(stager):
+            with torch.cuda.graph(self.graph):
+                self.outs = self.interp.run(comp, self.static)
+        if stager.i != len(stager.host):
+            raise CaptureError("fewer uploads than in the warm-up run")
+        self._stager = stager  # keep the staged constants alive
+        self.replays = 0
+
+    def _decode(self, interp, outs) -> Dict[str, np.ndarray]:
+        res = {}
+        for tag, lv in outs.items():
+            if lv.kind == "unit":
+                continue
+            res[tag] = interp.to_numpy(lv)
+        return res
+
+    def run(self, arguments: dict) -> Dict[str, np.ndarray]:
+        for k, v in arguments.items():
+            t = self.static.get(k)
+            if isinstance(t, torch.Tensor):
+                src = torch.from_numpy(np.ascontiguousarray(
+                    np.asarray(v).view(np.int64) if np.asarray(v).dtype == np.uint64
+                    else np.asarray(v)))
+                t.copy_(src)
+        self.keys.refresh()  # fresh randomness for this replay
+        self.graph.replay()
+        self.replays += 1
+        return self._decode(self.interp, self.outs)
+
+
+class GraphCache:
+    """Per-runtime cache of captured plans keyed by (computation, argument signature)."""
+
+    def __init__(self):
+        self.plans = {}
+        self.failed = set()
+
+    def evaluate(self, comp, arguments, device, storage, ring, seed=None):
+        key = (id(comp), signature(arguments))
+        plan = self.plans.get(key)
+        if plan is not None and plan.comp is comp:
+            return plan.run(arguments), plan.stats
+        if key in self.failed or not capturable(comp):
+            return None
+        try:
+            plan = GraphPlan(comp, arguments, device, storage, ring, seed)
+        except Exception as e:  # noqa: BLE001 - any capture failure means "run eagerly"
+            warnings.warn(f"hipGraph capture failed, evaluating eagerly: {e}")
+            self.failed.add(key)
+            try:
+                torch.cuda.synchronize()
+            except Exception:  # noqa: BLE001
+                pass
+            return None
+        self.plans[key] = plan
+        return plan.first, plan.stats

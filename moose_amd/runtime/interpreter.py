@@ -77,12 +77,12 @@ def dtype_of_numpy(a: np.ndarray) -> T.TensorDType:
 def numpy_to_torch(a, device):
     a = np.asarray(a)
     if a.dtype == np.uint64:
-        return torch.from_numpy(a.view(np.int64).copy()).to(device)
+        return R.to_device(torch.from_numpy(a.view(np.int64).copy()), device)
     if a.dtype == np.uint32:
         a = a.astype(np.int64)
     if a.dtype == object:
         raise MooseRuntimeError("object arrays are not tensors")
-    return torch.from_numpy(np.ascontiguousarray(a)).to(device)
+    return R.to_device(torch.from_numpy(np.ascontiguousarray(a)), device)
 
 
 class Interpreter:
@@ -269,8 +269,9 @@ class Interpreter:
                 return LV(hp, "int", None, HV(host, value))
         if isinstance(value, torch.Tensor):  # device-resident argument (no host copy)
             t = value.to(sess.device)
-            dtype = {torch.float64: T.FLOAT64, torch.float32: T.FLOAT32,
-                     torch.bool: T.BOOL}.get(t.dtype, T.UINT64)
+            dtype = getattr(value, "_moose_dtype", None) or {
+                torch.float64: T.FLOAT64, torch.float32: T.FLOAT32,
+                torch.bool: T.BOOL}.get(t.dtype, T.UINT64)
         else:
             arr = np.asarray(value)
             dtype = dtype_of_numpy(arr)

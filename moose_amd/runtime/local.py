@@ -1,5 +1,8 @@
 """``LocalMooseRuntime``: all identities simulated in one process on one device.
 
+With ``use_graphs=True`` (or ``MOOSEX_GRAPHS=1``) repeated evaluations of the same
+computation and argument signature replay a captured hipGraph (runtime/graphs.py).
+
 Parity: reference ``pymoose/pymoose/runtime.py:14-70`` + ``pymoose/src/bindings.rs:137-250``
 (``AsyncTestRuntime``, ``execution/asynchronous.rs:634-773``).  Here the three parties of
 each replicated placement are stacked on one device (an MI355X when available, else the
@@ -64,6 +67,7 @@ class LocalMooseRuntime:
         device=None,
         fixedpoint_ring: int = 128,
         seed: Optional[int] = None,
+        use_graphs: Optional[bool] = None,
     ):
         identities = [getattr(i, "name", i) for i in identities]
         storage_mapping = dict(storage_mapping or {})
@@ -80,6 +84,13 @@ class LocalMooseRuntime:
         self.seed = seed
         self.last_stats = None
         self.last_timings = None
+        # replay whole evaluations as hipGraphs (runtime/graphs.py); MOOSEX_GRAPHS=1
+        if use_graphs is None:
+            use_graphs = os.environ.get("MOOSEX_GRAPHS", "0") == "1"
+        self.use_graphs = use_graphs
+        from moose_amd.runtime.graphs import GraphCache
+
+        self._graphs = GraphCache()
 
     def set_default(self):
         from moose_amd.edsl.base import set_current_runtime
@@ -111,6 +122,16 @@ class LocalMooseRuntime:
             from moose_amd.runtime.distributed import _host_numpy
 
             return {k: _host_numpy(v) for k, v in outs.items()}
+        if self.use_graphs and self.device.type == "cuda":
+            t0 = time.perf_counter()
+            r = self._graphs.evaluate(comp, arguments, self.device, self.storage,
+                                      self.fixedpoint_ring, self.seed)
+            if r is not None:
+                result, self.last_stats = r
+                torch.cuda.synchronize(self.device)
+                elapsed = int((time.perf_counter() - t0) * 1e6)
+                self.last_timings = {i: elapsed for i in self.identities}
+                return result
         sess = StackedSession(self.device, seed=self.seed)
         interp = Interpreter(sess, self.storage, self.fixedpoint_ring)
         t0 = time.perf_counter()

@@ -34,6 +34,14 @@ if [[ $STEPS == *dots* ]]; then
   rm -f gpurun_out/dots.jsonl
   run dots 900 python benchmarks/dot_product.py --sweep --n 3 --json gpurun_out/dots.jsonl
 fi
+if [[ $STEPS == *graphs* ]]; then
+  run pytest_graphs 600 python -m pytest tests/test_graphs.py tests/test_keys.py -x -q
+  rm -f gpurun_out/logreg_graphs.jsonl gpurun_out/dots_graphs.jsonl
+  for it in 10 100; do for bs in 128 2048; do
+    run logreg_g_${bs}_${it} 900 python benchmarks/logreg_train.py --graphs --batch_size $bs --n_iter $it --n_exp 3 --json gpurun_out/logreg_graphs.jsonl
+  done; done
+  run dots_graphs 900 python benchmarks/dot_product.py --graphs --sweep --n 3 --json gpurun_out/dots_graphs.jsonl
+fi
 if [[ $STEPS == *prof* || $STEPS == all ]]; then
   export TMPDIR=/tmp
   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1

@@ -1,0 +1,82 @@
+"""Whole-evaluation hipGraph replay (runtime/graphs.py): replays with new inputs give the
+same results as eager evaluation, use fresh keys, and really run from the graph."""
+import importlib.util
+import os
+import warnings
+
+import numpy as np
+import pytest
+import torch
+
+import moose_amd as pm
+from moose_amd.runtime import graphs
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _load(name):
+    spec = importlib.util.spec_from_file_location(name, os.path.join(ROOT, "benchmarks",
+                                                                     f"{name}.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_signature_distinguishes_shapes_and_values():
+    a = graphs.signature({"x": np.zeros((2, 3)), "k": "key"})
+    b = graphs.signature({"x": np.zeros((3, 3)), "k": "key"})
+    c = graphs.signature({"x": np.ones((2, 3)), "k": "key"})
+    assert a != b and a == c
+
+
+def test_stager_rejects_data_dependent_uploads():
+    rec = graphs._Recorder()
+    rec(torch.arange(4), "cpu")
+    st = graphs._Stager(rec.items, "cpu")
+    st(torch.arange(4), "cpu")
+    with pytest.raises(graphs.CaptureError):
+        st(torch.arange(4), "cpu")
+    st = graphs._Stager(rec.items, "cpu")
+    with pytest.raises(graphs.CaptureError):
+        st(torch.arange(4) + 1, "cpu")
+
+
+@pytest.mark.gpu
+def test_logreg_training_replays_from_graph():
+    L = _load("logreg_train")
+    bs, n_it, nf = 64, 3, 100
+    from moose_amd.runtime.local import to_native
+
+    native = to_native(L.build_training(bs, n_it, n_features=nf))
+    rt = pm.LocalMooseRuntime(["alice", "bob", "carole"], device="cuda", use_graphs=True)
+    rng = np.random.default_rng(3)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")  # a capture failure would warn and fall back
+        for rep in range(3):
+            x = rng.standard_normal((bs * n_it, nf))
+            y = rng.integers(2, size=(bs * n_it, 1)).astype(np.float64)
+            outs = rt.evaluate_computation(native, {"x": x, "y": y,
+                                                    "w_0": np.zeros((nf, 1)),
+                                                    "b_0": np.zeros((1, 1))})
+            w_ref, b_ref = L.plaintext_training(x, y, bs, n_it)
+            vals = sorted(outs.values(), key=lambda v: -np.asarray(v).size)
+            np.testing.assert_allclose(vals[0].reshape(w_ref.shape), w_ref, atol=1e-5)
+            np.testing.assert_allclose(vals[1].reshape(b_ref.shape), b_ref, atol=1e-5)
+    plans = list(rt._graphs.plans.values())
+    assert len(plans) == 1 and plans[0].replays == 2
+
+
+@pytest.mark.gpu
+def test_graph_replay_refreshes_keys():
+    D = _load("dot_product")
+    from moose_amd.runtime.local import to_native
+
+    native = to_native(D.build("seq", 2))
+    rt = pm.LocalMooseRuntime(["alice", "bob", "carole"], device="cuda", use_graphs=True)
+    args = {"x_arg": np.ones((8, 8)), "y_arg": np.identity(8)}
+    rt.evaluate_computation(native, args)
+    plan = next(iter(rt._graphs.plans.values()))
+    k0 = plan.keys.t.clone()
+    out = rt.evaluate_computation(native, args)
+    assert not torch.equal(k0, plan.keys.t)
+    np.testing.assert_allclose(next(iter(out.values())), np.ones((8, 8)), atol=1e-6)
