@@ -27,6 +27,7 @@ from typing import Dict
 from typing import List
 from typing import Optional
 
+from moose_amd import errors
 from moose_amd.ir import types as T
 from moose_amd.ir.computation import Computation
 from moose_amd.ir.computation import HostPlacement
@@ -37,7 +38,7 @@ from moose_amd.ir.computation import rendezvous_key_from_counter
 DEFAULT_PASSES = ["typing", "deprecatedShape", "lowering", "prune", "networking", "toposort"]
 
 
-class CompilationError(RuntimeError):
+class CompilationError(errors.Compilation):
     pass
 
 

@@ -20,6 +20,7 @@ from typing import List
 
 import numpy as np
 
+from moose_amd import errors
 from moose_amd.ir.computation import Computation
 from moose_amd.ir.computation import Constant
 from moose_amd.ir.computation import Operation
@@ -42,7 +43,7 @@ _STRING = re.compile(r'"((?:[^"\\]|\\.)*)"')
 _TYPE = re.compile(r"[A-Za-z0-9]+(?:<[^>]*>)?")
 
 
-class ParseError(ValueError):
+class ParseError(errors.MalformedComputation, ValueError):
     pass
 
 

@@ -11,6 +11,7 @@ import threading
 
 import torch
 
+from moose_amd import errors
 from moose_amd._native import build as _build
 
 _LIB = None
@@ -76,7 +77,7 @@ _SIGS = {
 }
 
 
-class NativeError(RuntimeError):
+class NativeError(errors.KernelError):
     pass
 
 

@@ -25,6 +25,7 @@ from typing import List
 import torch
 import torch.distributed as dist
 
+from moose_amd import errors
 from moose_amd.ops import ring as R
 
 HEADER_WORDS = 24
@@ -38,7 +39,7 @@ _DTYPES = [torch.float64, torch.float32, torch.int64, torch.int32, torch.uint8, 
 _DTYPE_CODE = {d: i for i, d in enumerate(_DTYPES)}
 
 
-class TransportError(RuntimeError):
+class TransportError(errors.Networking):
     pass
 
 

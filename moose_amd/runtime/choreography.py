@@ -36,6 +36,7 @@ from typing import Optional
 
 import numpy as np
 
+from moose_amd import errors
 from moose_amd.utils import valuecodec
 
 PREFIX = "moosex"
@@ -176,7 +177,7 @@ class ChoreographyClient:
         from moose_amd.runtime.local import to_native
 
         if self.store.add(f"{PREFIX}/sid/{session_id}", 1) > 1:  # choreography/grpc.rs:114
-            raise RuntimeError(f"session {session_id} already exists")
+            raise errors.SessionAlreadyExists(f"session {session_id} already exists")
         comp = to_native(computation, fixedpoint_ring)
         job = {"session_id": str(session_id), "computation": comp.to_msgpack(),
                "arguments": _plain_args(arguments or {}),

@@ -34,11 +34,12 @@ from typing import Optional
 import numpy as np
 import torch
 
+from moose_amd import errors
 from moose_amd.ir.computation import Computation
 from moose_amd.utils import valuecodec
 
 
-class DistributedRuntimeError(RuntimeError):
+class DistributedRuntimeError(errors.Networking):
     pass
 
 

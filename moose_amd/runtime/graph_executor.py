@@ -24,6 +24,7 @@ from typing import Optional
 import numpy as np
 import torch
 
+from moose_amd import errors
 from moose_amd.compiler.symbolic import bits_of_ty
 from moose_amd.ir.computation import Computation
 from moose_amd.ir.computation import Constant
@@ -38,7 +39,7 @@ _TY_DTYPE = {"HostFloat64Tensor": torch.float64, "HostFloat32Tensor": torch.floa
              "HostBitTensor": torch.bool, "HostBoolTensor": torch.bool}
 
 
-class GraphExecutionError(RuntimeError):
+class GraphExecutionError(errors.KernelError):
     pass
 
 

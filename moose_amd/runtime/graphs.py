@@ -29,6 +29,7 @@ from typing import Dict
 import numpy as np
 import torch
 
+from moose_amd import errors
 from moose_amd.ops import ring as R
 from moose_amd.runtime.interpreter import Interpreter
 from moose_amd.runtime.interpreter import dtype_of_numpy
@@ -39,7 +40,7 @@ from moose_amd.runtime.session import StackedSession
 _SIDE_EFFECTS = {"Save", "Load"}
 
 
-class CaptureError(RuntimeError):
+class CaptureError(errors.Unexpected):
     pass
 
 

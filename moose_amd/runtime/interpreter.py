@@ -22,6 +22,7 @@ from typing import Dict
 import numpy as np
 import torch
 
+from moose_amd import errors
 from moose_amd.ir import types as T
 from moose_amd.ir.computation import Computation
 from moose_amd.ir.computation import Constant
@@ -41,7 +42,7 @@ from moose_amd.utils.telemetry import span
 _FLOAT = {"Float32": torch.float32, "Float64": torch.float64}
 
 
-class MooseRuntimeError(RuntimeError):
+class MooseRuntimeError(errors.KernelError):
     pass
 
 

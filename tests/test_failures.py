@@ -91,3 +91,23 @@ def test_lowered_plan_is_deterministic_textual():
         'o = Output{tag = "o"}: (Tensor<Fixed128(14, 23)>) -> Tensor<Fixed128(14, 23)> (m) @Host(b)\n'))
     assert comp.digest() == again.digest()
     assert os.environ.get("MOOSEX_FAULT") is None
+
+
+def test_error_model_variants():
+    """Reference error.rs:7-61: 17 variants; subsystem errors map onto them."""
+    from moose_amd import errors
+    from moose_amd.compiler.passes import CompilationError
+    from moose_amd.ir.textual import ParseError
+    from moose_amd.ops.native import NativeError
+    from moose_amd.parallel.transport import TransportError
+    from moose_amd.runtime.graph_executor import GraphExecutionError
+    from moose_amd.runtime.interpreter import MooseRuntimeError
+
+    assert len(errors.VARIANTS) == 17
+    assert all(issubclass(v, errors.MooseError) for v in errors.VARIANTS)
+    assert issubclass(CompilationError, errors.Compilation)
+    assert issubclass(ParseError, errors.MalformedComputation) and issubclass(ParseError, ValueError)
+    assert issubclass(NativeError, errors.KernelError)
+    assert issubclass(TransportError, errors.Networking)
+    assert issubclass(GraphExecutionError, errors.KernelError)
+    assert issubclass(MooseRuntimeError, errors.KernelError)
