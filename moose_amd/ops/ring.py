@@ -152,9 +152,10 @@ def fill(shape, value: int, bits, device) -> RT:
         return RT(torch.full(shape, v, dtype=torch.int64, device=device), 64)
     v = int(value) & MASK128
     lo, hi = _to_i64(v & MASK64), _to_i64(v >> 64)
-    d = torch.empty(shape + (2,), dtype=torch.int64, device=device)
-    d[..., 0] = lo
-    d[..., 1] = hi
+    # fill kernels only (slice assignment of a python int is a host->device copy, which
+    # is not allowed while a hipGraph is being captured)
+    d = torch.stack([torch.full(shape, lo, dtype=torch.int64, device=device),
+                     torch.full(shape, hi, dtype=torch.int64, device=device)], dim=-1)
     return RT(d, 128)
 
 

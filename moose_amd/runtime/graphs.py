@@ -23,6 +23,7 @@ uploads, CPU devices) falls back to eager evaluation.
 """
 from __future__ import annotations
 
+import os
 import warnings
 from typing import Dict
 
@@ -187,6 +188,11 @@ class GraphCache:
         try:
             plan = GraphPlan(comp, arguments, device, storage, ring, seed)
         except Exception as e:  # noqa: BLE001 - any capture failure means "run eagerly"
+            import traceback
+
+            self.last_error = traceback.format_exc()
+            if os.environ.get("MOOSEX_GRAPHS_DEBUG") == "1":
+                raise
             warnings.warn(f"hipGraph capture failed, evaluating eagerly: {e}")
             self.failed.add(key)
             try:
