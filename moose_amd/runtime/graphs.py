@@ -39,6 +39,7 @@ from moose_amd.runtime.keys import KeyTable
 from moose_amd.runtime.session import StackedSession
 
 _SIDE_EFFECTS = {"Save", "Load"}
+SEGMENT_OPS = int(os.environ.get("MOOSEX_GRAPH_SEGMENT_OPS", "32"))
 
 
 class CaptureError(errors.Unexpected):
@@ -140,10 +141,40 @@ class GraphPlan:
         self.interp = Interpreter(self.sess, storage, fixedpoint_ring)
         stager = _Stager(rec.items, self.device)
         torch.cuda.synchronize(self.device)
-        self.graph = torch.cuda.CUDAGraph()
-        with _upload_hook(stager):
-            with torch.cuda.graph(self.graph):
+        # The evaluation is captured as a chain of graphs of SEGMENT_OPS logical ops each
+        # (sharing one memory pool, replayed in capture order): a single graph of 10^5+
+        # kernel nodes is slow to instantiate and has crashed the HIP runtime.
+        self.graphs = []
+        pool = torch.cuda.graph_pool_handle()
+        stream = torch.cuda.Stream(self.device)
+        state = {"g": None, "n": 0}
+
+        def begin():
+            g = torch.cuda.CUDAGraph()
+            g.capture_begin(pool=pool)
+            state["g"], state["n"] = g, 0
+
+        def end():
+            state["g"].capture_end()
+            self.graphs.append(state["g"])
+
+        def rotate():  # called before each op: segments never end empty-handed
+            if state["g"] is None:
+                begin()
+            elif state["n"] >= SEGMENT_OPS:
+                end()
+                begin()
+            state["n"] += 1
+
+        self.interp.on_op = rotate
+        with _upload_hook(stager), torch.cuda.stream(stream):
+            try:
                 self.outs = self.interp.run(comp, self.static)
+            finally:
+                if state["g"] is not None:
+                    end()
+        self.interp.on_op = None
+        torch.cuda.synchronize(self.device)
         if stager.i != len(stager.host):
             raise CaptureError("fewer uploads than in the warm-up run")
         self._stager = stager  # keep the staged constants alive
@@ -166,7 +197,8 @@ class GraphPlan:
                     else np.asarray(v)))
                 t.copy_(src)
         self.keys.refresh()  # fresh randomness for this replay
-        self.graph.replay()
+        for g in self.graphs:
+            g.replay()
         self.replays += 1
         return self._decode(self.interp, self.outs)
 

@@ -93,6 +93,7 @@ class Interpreter:
         self.env: Dict[str, LV] = {}
         self.fixed_ring = fixedpoint_ring  # override Fixed128 -> Fixed64 if 64
         self.outputs = {}
+        self.on_op = None
 
     # ------------------------------------------------------------------------
     # driver
@@ -106,6 +107,8 @@ class Interpreter:
             if handler is None:
                 raise MooseRuntimeError(f"operator {op.kind} is not supported by the interpreter")
             ins = [self.env[n] for n in op.inputs]
+            if self.on_op is not None:  # e.g. graph capture segmentation (graphs.py)
+                self.on_op()
             with span(f"op.{op.kind}", op=op.name):
                 try:
                     if me is not None and me not in _owners(op.placement):

@@ -51,7 +51,7 @@ def test_logreg_training_replays_from_graph():
     rt = pm.LocalMooseRuntime(["alice", "bob", "carole"], device="cuda", use_graphs=True)
     rng = np.random.default_rng(3)
     with warnings.catch_warnings():
-        warnings.simplefilter("error")  # a capture failure would warn and fall back
+        warnings.filterwarnings("error", message="hipGraph capture failed")
         for rep in range(3):
             x = rng.standard_normal((bs * n_it, nf))
             y = rng.integers(2, size=(bs * n_it, 1)).astype(np.float64)
