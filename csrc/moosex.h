@@ -50,6 +50,14 @@ int mx_encode(int dev, int words, const double* x, void* out, int64_t n, int fra
 // out[i] = signed(x[i]) / 2^frac
 int mx_decode(int dev, int words, const void* x, double* out, int64_t n, int frac,
               void* stream);
+// out[i] = value (lo word, hi word for Z_2^128; low byte for bits)
+int mx_fill(int dev, int words, void* out, int64_t n, uint64_t lo, uint64_t hi, void* stream);
+// out[o, j, i] = bit (start + j) of a[o, i] (0/1 bytes)
+int mx_bit_planes(int dev, int words, const void* a, uint8_t* out, int64_t outer, int64_t inner,
+                  int start, int count, void* stream);
+// out[o, i] = sum_j w[j] * a[o, j, i] (w: k ring elements in the memory named by dev)
+int mx_weighted_sum(int dev, int words, const void* a, const void* w, void* out, int64_t outer,
+                    int64_t k, int64_t inner, void* stream);
 // out[o, i] = sum_r a[o, r, i]
 int mx_sum_axis(int dev, int words, const void* a, void* out, int64_t outer, int64_t red,
                 int64_t inner, void* stream);
@@ -112,6 +120,12 @@ void mx_key_slots(const uint8_t* keys16, int n, uint32_t* out);
 int mx_rss_cross_k(int dev, int kind, int words, const void* x0, const void* x1,
                    const void* y0, const void* y1, void* out, int64_t n, int nparties,
                    const uint32_t* slots, int nslots, uint64_t nonce, void* stream);
+// Stacked 3-party RSS product with the reshare fused in: out0[p] = z_p (cross terms +
+// zero share from slots p, p+1 mod 3) and out1[p] = z_{p+1}, i.e. both shares of every
+// party after the one-round reshare (x*/y*/out* are [3, n] slot vectors)
+int mx_rss_mul3_k(int dev, int kind, int words, const void* x0, const void* x1, const void* y0,
+                  const void* y1, void* out0, void* out1, int64_t n, const uint32_t* slots,
+                  uint64_t nonce, void* stream);
 // mx_prf_expand with nkeys consecutive key slots
 int mx_prf_expand_k(int dev, int words, void* out, int64_t n, int nkeys, const uint32_t* slots,
                     uint64_t nonce, void* stream);

@@ -167,6 +167,11 @@ int mxh_ring_inject(int words, const uint8_t* bits, void* out, int64_t n, int bi
                     void* stream);
 int mxh_encode(int words, const double* x, void* out, int64_t n, int frac, void* stream);
 int mxh_decode(int words, const void* x, double* out, int64_t n, int frac, void* stream);
+int mxh_fill(int words, void* out, int64_t n, uint64_t lo, uint64_t hi, void* stream);
+int mxh_bit_planes(int words, const void* a, uint8_t* out, int64_t outer, int64_t inner,
+                   int start, int count, void* stream);
+int mxh_weighted_sum(int words, const void* a, const void* w, void* out, int64_t outer,
+                     int64_t k, int64_t inner, void* stream);
 int mxh_sum_axis(int words, const void* a, void* out, int64_t outer, int64_t red, int64_t inner,
                  void* stream);
 int mxh_prg(const uint8_t* key16, uint64_t nonce, uint64_t ctr0, void* out, int64_t nbytes,
@@ -179,6 +184,9 @@ int mxh_prf_expand(int words, void* out, int64_t n, int nkeys, const uint8_t* ke
 int mxh_rss_cross_k(int kind, int words, const void* x0, const void* x1, const void* y0,
                     const void* y1, void* out, int64_t n, int nparties, const uint32_t* slots,
                     int nslots, uint64_t nonce, void* stream);
+int mxh_rss_mul3_k(int kind, int words, const void* x0, const void* x1, const void* y0,
+                   const void* y1, void* out0, void* out1, int64_t n, const uint32_t* slots,
+                   uint64_t nonce, void* stream);
 int mxh_prf_expand_k(int words, void* out, int64_t n, int nkeys, const uint32_t* slots,
                      uint64_t nonce, void* stream);
 int mxh_gemm(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,

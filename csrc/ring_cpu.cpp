@@ -417,6 +417,60 @@ int mx_decode(int dev, int words, const void* x, double* out, int64_t n, int fra
   return -2;
 }
 
+int mx_fill(int dev, int words, void* out, int64_t n, uint64_t lo, uint64_t hi, void* stream) {
+  if (dev) return mxh_fill(words, out, n, lo, hi, stream);
+  DISPATCH_WORDS(words, T, {
+    T v;
+    if constexpr (sizeof(T) == 16) {
+      v = ((T)hi << 64) | (T)lo;
+    } else {
+      v = (T)lo;
+    }
+    T* o = (T*)out;
+    parallel_for(n, 1 << 16, [&](int64_t s, int64_t e) {
+      for (int64_t i = s; i < e; ++i) o[i] = v;
+    });
+    return 0;
+  });
+}
+
+int mx_bit_planes(int dev, int words, const void* a, uint8_t* out, int64_t outer, int64_t inner,
+                  int start, int count, void* stream) {
+  if (dev) return mxh_bit_planes(words, a, out, outer, inner, start, count, stream);
+  DISPATCH_WORDS(words, T, {
+    const T* x = (const T*)a;
+    parallel_for(outer * inner, 1 << 12, [&](int64_t s, int64_t e) {
+      for (int64_t g = s; g < e; ++g) {
+        const int64_t o = g / inner, i = g - o * inner;
+        const T v = x[g];
+        uint8_t* dst = out + o * count * inner + i;
+        for (int j = 0; j < count; ++j) dst[(int64_t)j * inner] = (uint8_t)((v >> (start + j)) & 1);
+      }
+    });
+    return 0;
+  });
+}
+
+int mx_weighted_sum(int dev, int words, const void* a, const void* w, void* out, int64_t outer,
+                    int64_t k, int64_t inner, void* stream) {
+  if (dev) return mxh_weighted_sum(words, a, w, out, outer, k, inner, stream);
+  DISPATCH_WORDS(words, T, {
+    const T* x = (const T*)a;
+    const T* ww = (const T*)w;
+    T* o_ = (T*)out;
+    parallel_for(outer * inner, 1 << 12, [&](int64_t s, int64_t e) {
+      for (int64_t g = s; g < e; ++g) {
+        const int64_t o = g / inner, i = g - o * inner;
+        const T* src = x + o * k * inner + i;
+        T acc = 0;
+        for (int64_t j = 0; j < k; ++j) acc += ww[j] * src[j * inner];
+        o_[g] = acc;
+      }
+    });
+    return 0;
+  });
+}
+
 int mx_sum_axis(int dev, int words, const void* a, void* out, int64_t outer, int64_t red,
                 int64_t inner, void* stream) {
   if (dev) return mxh_sum_axis(words, a, out, outer, red, inner, stream);
@@ -512,6 +566,19 @@ int mx_rss_cross_k(int dev, int kind, int words, const void* x0, const void* x1,
   DISPATCH_WORDS(words, T,
                  return rss_cross_t<T>(kind, (const T*)x0, (const T*)x1, (const T*)y0,
                                        (const T*)y1, (T*)out, n, nparties, keys, nonce));
+}
+
+int mx_rss_mul3_k(int dev, int kind, int words, const void* x0, const void* x1, const void* y0,
+                  const void* y1, void* out0, void* out1, int64_t n, const uint32_t* slots,
+                  uint64_t nonce, void* stream) {
+  if (dev)
+    return mxh_rss_mul3_k(kind, words, x0, x1, y0, y1, out0, out1, n, slots, nonce, stream);
+  int rc = mx_rss_cross_k(0, kind, words, x0, x1, y0, y1, out0, n, 3, slots, 3, nonce, stream);
+  if (rc) return rc;
+  const int64_t bytes = n * (words == 0 ? 1 : 8 * words);
+  for (int p = 0; p < 3; ++p)  // out1[p] = out0[p + 1]
+    memcpy((uint8_t*)out1 + p * bytes, (const uint8_t*)out0 + ((p + 1) % 3) * bytes, bytes);
+  return 0;
 }
 
 int mx_prf_expand_k(int dev, int words, void* out, int64_t n, int nkeys, const uint32_t* slots,

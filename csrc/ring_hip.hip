@@ -57,6 +57,48 @@ __global__ void k_unary(int op, const T* __restrict__ a, T* __restrict__ out, in
 }
 
 template <class T>
+__global__ void k_fill(T* __restrict__ out, int64_t n, uint64_t lo, uint64_t hi) {
+  T v;
+  if constexpr (sizeof(T) == 16) {
+    v = ((T)hi << 64) | (T)lo;
+  } else {
+    v = (T)lo;
+  }
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = v;
+}
+
+// out[o, j, i] = bit (start + j) of a[o, i] as a 0/1 byte (bit decomposition / split)
+template <class T>
+__global__ void k_bit_planes(const T* __restrict__ a, uint8_t* __restrict__ out, int64_t outer,
+                             int64_t inner, int start, int count) {
+  const int64_t n = outer * inner;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < n;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t o = g / inner, i = g - o * inner;
+    const T v = a[g];
+    uint8_t* dst = out + o * count * inner + i;
+    for (int j = 0; j < count; ++j) dst[(int64_t)j * inner] = (uint8_t)((v >> (start + j)) & 1);
+  }
+}
+
+// out[o, i] = sum_j w[j] * a[o, j, i]  (public ring weights, bit composition)
+template <class T>
+__global__ void k_weighted_sum(const T* __restrict__ a, const T* __restrict__ w,
+                               T* __restrict__ out, int64_t outer, int64_t k, int64_t inner) {
+  const int64_t n = outer * inner;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < n;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t o = g / inner, i = g - o * inner;
+    const T* src = a + o * k * inner + i;
+    T acc = 0;
+    for (int64_t j = 0; j < k; ++j) acc += w[j] * src[j * inner];
+    out[g] = acc;
+  }
+}
+
+template <class T>
 __global__ void k_compare(int op, const T* __restrict__ a, int64_t na, const T* __restrict__ b,
                           int64_t nb, uint8_t* __restrict__ out, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
@@ -218,7 +260,8 @@ __global__ void k_rss_cross(int kind, const T* __restrict__ x0, const T* __restr
 template <class T>
 __global__ void k_rss_cross_ring3(int kind, const T* __restrict__ x0, const T* __restrict__ x1,
                                   const T* __restrict__ y0, const T* __restrict__ y1,
-                                  T* __restrict__ out, int64_t n, KeySrc keys, uint64_t nonce) {
+                                  T* __restrict__ out, T* __restrict__ out1, int64_t n,
+                                  KeySrc keys, uint64_t nonce) {
   __shared__ uint32_t Tt[256];
   __shared__ uint8_t Sb[256];
   __shared__ uint32_t rks[3][44];
@@ -245,7 +288,10 @@ __global__ void k_rss_cross_ring3(int kind, const T* __restrict__ x0, const T* _
                             x1 != nullptr, y1 != nullptr);
         else if (x0 != nullptr)
           v = x0[i];
-        out[i] = mxr::zs_combine<T>(kind, v, pick<T>(lo[p], hi[p], j), pick<T>(lo[q], hi[q], j));
+        const T z = mxr::zs_combine<T>(kind, v, pick<T>(lo[p], hi[p], j), pick<T>(lo[q], hi[q], j));
+        out[i] = z;
+        // fused reshare: z_p is party p-1's second share
+        if (out1 != nullptr) out1[(int64_t)(p == 0 ? 2 : p - 1) * n + e] = z;
       }
     }
   }
@@ -441,6 +487,38 @@ int mxh_decode(int words, const void* x, double* out, int64_t n, int frac, void*
   return 0;
 }
 
+int mxh_fill(int words, void* out, int64_t n, uint64_t lo, uint64_t hi, void* stream) {
+  if (n == 0) return 0;
+  DEV_DISPATCH(words, T, {
+    hipLaunchKernelGGL(k_fill<T>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream), (T*)out, n,
+                       lo, hi);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mxh_bit_planes(int words, const void* a, uint8_t* out, int64_t outer, int64_t inner,
+                   int start, int count, void* stream) {
+  if (outer * inner == 0 || count == 0) return 0;
+  DEV_DISPATCH(words, T, {
+    hipLaunchKernelGGL(k_bit_planes<T>, dim3(grid_for(outer * inner)), dim3(kBlock), 0,
+                       S(stream), (const T*)a, out, outer, inner, start, count);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mxh_weighted_sum(int words, const void* a, const void* w, void* out, int64_t outer,
+                     int64_t k, int64_t inner, void* stream) {
+  if (outer * inner == 0) return 0;
+  DEV_DISPATCH(words, T, {
+    hipLaunchKernelGGL(k_weighted_sum<T>, dim3(grid_for(outer * inner)), dim3(kBlock), 0,
+                       S(stream), (const T*)a, (const T*)w, (T*)out, outer, k, inner);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
 int mxh_sum_axis(int words, const void* a, void* out, int64_t outer, int64_t red, int64_t inner,
                  void* stream) {
   int64_t total = outer * inner;
@@ -475,7 +553,8 @@ namespace {
 
 int launch_rss_cross(int kind, int words, const void* x0, const void* x1, const void* y0,
                      const void* y1, void* out, int64_t n, int nparties, bool has_keys,
-                     bool ring3, const KeySrc& k, uint64_t nonce, void* stream) {
+                     bool ring3, const KeySrc& k, uint64_t nonce, void* stream,
+                     void* out1 = nullptr) {
   if (n == 0) return 0;
   if (nparties < 1 || nparties > 3) return -3;
   DEV_DISPATCH(words, T, {
@@ -484,7 +563,7 @@ int launch_rss_cross(int kind, int words, const void* x0, const void* x1, const 
       const int64_t blocks = (n + P - 1) / P;
       hipLaunchKernelGGL(k_rss_cross_ring3<T>, dim3(grid_for(blocks)), dim3(kBlock), 0,
                          S(stream), kind, (const T*)x0, (const T*)x1, (const T*)y0,
-                         (const T*)y1, (T*)out, n, k, nonce);
+                         (const T*)y1, (T*)out, (T*)out1, n, k, nonce);
       MX_LAUNCH_CHECK();
       return 0;
     }
@@ -534,6 +613,15 @@ int mxh_rss_cross_k(int kind, int words, const void* x0, const void* x1, const v
   KeySrc k = mxd::keysrc_slots(ptrs, ring3 ? 3 : nparties + 1);
   return launch_rss_cross(kind, words, x0, x1, y0, y1, out, n, nparties, true, ring3, k, nonce,
                           stream);
+}
+
+int mxh_rss_mul3_k(int kind, int words, const void* x0, const void* x1, const void* y0,
+                   const void* y1, void* out0, void* out1, int64_t n, const uint32_t* slots,
+                   uint64_t nonce, void* stream) {
+  const uint32_t* ptrs[3];
+  for (int i = 0; i < 3; ++i) ptrs[i] = slots + MX_KEY_SLOT_WORDS * i;
+  return launch_rss_cross(kind, words, x0, x1, y0, y1, out0, n, 3, true, true,
+                          mxd::keysrc_slots(ptrs, 3), nonce, stream, out1);
 }
 
 int mxh_prf_expand(int words, void* out, int64_t n, int nkeys, const uint8_t* keys16,

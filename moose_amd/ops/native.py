@@ -33,6 +33,9 @@ _SIGS = {
     "mx_encode": (c_int, [c_int, c_int, c_vp, c_vp, c_i64, c_int, c_vp]),
     "mx_decode": (c_int, [c_int, c_int, c_vp, c_vp, c_i64, c_int, c_vp]),
     "mx_sum_axis": (c_int, [c_int, c_int, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
+    "mx_fill": (c_int, [c_int, c_int, c_vp, c_i64, c_u64, c_u64, c_vp]),
+    "mx_bit_planes": (c_int, [c_int, c_int, c_vp, c_vp, c_i64, c_i64, c_int, c_int, c_vp]),
+    "mx_weighted_sum": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
     "mx_prg": (c_int, [c_int, c_vp, c_u64, c_u64, c_vp, c_i64, c_vp]),
     "mx_aes_encrypt_blocks": (c_int, [c_vp, c_vp, c_vp, c_i64]),
     "mx_rss_cross": (
@@ -63,6 +66,10 @@ _SIGS = {
          c_vp],
     ),
     "mx_prf_expand_k": (c_int, [c_int, c_int, c_vp, c_i64, c_int, c_vp, c_u64, c_vp]),
+    "mx_rss_mul3_k": (
+        c_int,
+        [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_u64, c_vp],
+    ),
     "mx_trunc_pr3_k": (
         c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_vp],
     ),

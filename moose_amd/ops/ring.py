@@ -142,9 +142,31 @@ def zeros(shape, bits, device) -> RT:
     return r
 
 
+_SCALARS = {}
+
+
 def fill(shape, value: int, bits, device) -> RT:
-    """Constant ring tensor (``value`` taken mod 2^bits)."""
+    """Constant ring tensor (``value`` taken mod 2^bits).
+
+    Scalars (shape ``()``) are the public constants of the protocols (encoded
+    coefficients, masks, 1/n ...); they are created once per device and shared -- callers
+    never write into a fill result.  Not while a hipGraph is being captured: the tensor
+    would live in the graph's private pool."""
     shape = tuple(shape)
+    if not shape:
+        key = (int(value), bits, str(device))
+        hit = _SCALARS.get(key)
+        if hit is not None:
+            return hit
+        t = _fill(shape, value, bits, device)
+        if torch.device(device).type == "cpu" or not torch.cuda.is_current_stream_capturing():
+            if len(_SCALARS) < 65536:
+                _SCALARS[key] = t
+        return t
+    return _fill(shape, value, bits, device)
+
+
+def _fill(shape, value: int, bits, device) -> RT:
     if bits == 1:
         return RT(torch.full(shape, int(value) & 1, dtype=torch.uint8, device=device), 1)
     if bits == 64:
@@ -152,11 +174,12 @@ def fill(shape, value: int, bits, device) -> RT:
         return RT(torch.full(shape, v, dtype=torch.int64, device=device), 64)
     v = int(value) & MASK128
     lo, hi = _to_i64(v & MASK64), _to_i64(v >> 64)
-    # fill kernels only (slice assignment of a python int is a host->device copy, which
-    # is not allowed while a hipGraph is being captured)
-    d = torch.stack([torch.full(shape, lo, dtype=torch.int64, device=device),
-                     torch.full(shape, hi, dtype=torch.int64, device=device)], dim=-1)
-    return RT(d, 128)
+    # one native fill kernel (slice assignment of a python int would be a host->device
+    # copy, which is not allowed while a hipGraph is being captured)
+    out = empty(shape, 128, device)
+    nat.check(nat.lib().mx_fill(nat.dev_of(out.data), 2, nat.ptr(out.data), math.prod(shape),
+                                lo & MASK64, hi & MASK64, nat.stream_of(out.data)), "fill")
+    return out
 
 
 def _to_i64(u):
@@ -658,6 +681,47 @@ def prf_expand(keys: Sequence[bytes], nonce: int, shape, bits, device) -> RT:
     return out
 
 
+def bit_planes(a: RT, start: int, count: int, nb=0) -> RT:
+    """Bits start..start+count-1 of ``a`` as a bit tensor with a new logical leading axis
+    (after ``nb`` batch axes): out[.., j, ..] = bit start+j.  One kernel."""
+    shp = a.shape
+    outer = math.prod(shp[:nb])
+    inner = math.prod(shp[nb:])
+    out = torch.empty(tuple(shp[:nb]) + (count,) + tuple(shp[nb:]), dtype=torch.uint8,
+                      device=a.device)
+    ad = a.data.contiguous()
+    nat.check(nat.lib().mx_bit_planes(nat.dev_of(ad), _words(a.bits), nat.ptr(ad), nat.ptr(out),
+                                      outer, inner, start, count, nat.stream_of(ad)),
+              "bit_planes")
+    return RT(out, 1)
+
+
+_WEIGHTS = {}
+
+
+def weighted_sum(a: RT, weights, nb=0) -> RT:
+    """sum_j weights[j] * a[.., j, ..] over the leading logical axis (public integer
+    weights, e.g. bit composition).  One kernel."""
+    bits = a.bits
+    key = (tuple(int(w) for w in weights), bits, str(a.device))
+    w = _WEIGHTS.get(key)
+    if w is None:
+        w = from_ints(np.array([int(v) for v in weights], dtype=object), bits, a.device)
+        if a.device.type == "cpu" or not torch.cuda.is_current_stream_capturing():
+            if len(_WEIGHTS) < 4096:
+                _WEIGHTS[key] = w
+    shp = a.shape
+    k = shp[nb]
+    outer = math.prod(shp[:nb])
+    inner = math.prod(shp[nb + 1:])
+    out = empty(tuple(shp[:nb]) + tuple(shp[nb + 1:]), bits, a.device)
+    ad = a.data.contiguous()
+    nat.check(nat.lib().mx_weighted_sum(nat.dev_of(ad), _words(bits), nat.ptr(ad),
+                                        nat.ptr(w.data), nat.ptr(out.data), outer, k, inner,
+                                        nat.stream_of(ad)), "weighted_sum")
+    return out
+
+
 def prf_expand_k(slot_ptr: int, nkeys: int, nonce: int, shape, bits, device) -> RT:
     """``prf_expand`` with the keys read from ``nkeys`` consecutive key slots."""
     shape = tuple(shape)
@@ -692,6 +756,30 @@ def aes_encrypt(key: bytes, block: bytes) -> bytes:
     out = ctypes.create_string_buffer(16)
     nat.check(nat.lib().mx_aes_encrypt_blocks(kb, inp, out, 1), "aes")
     return out.raw
+
+
+def rss_mul3_k(kind: str, x0: RT, x1: RT, y0: RT, y1: RT, slot_ptr: int, nonce: int):
+    """Stacked 3-party product with the reshare fused in: returns (s0, s1) with
+    s0[p] = z_p and s1[p] = z_{p+1} (one kernel, see mx_rss_mul3_k)."""
+    bits = x0.bits
+    shp = x0.shape
+    if y0 is not None and y0.shape != shp:
+        x0, y0 = _broadcast(x0, y0)
+        shp = x0.shape
+    # x1/y0/y1 may be None: y0 None -> out = x0 + zero share (then reshared)
+    datas = [None if p is None else (p if p.shape == shp else expand(p, shp)).data.contiguous()
+             for p in (x0, x1, y0, y1)]
+    n = math.prod(shp) // 3
+    out0, out1 = empty(shp, bits, x0.device), empty(shp, bits, x0.device)
+    nat.check(
+        nat.lib().mx_rss_mul3_k(
+            nat.dev_of(out0.data), 1 if kind == "bool" else 0, _words(bits),
+            *[nat.ptr(d) for d in datas], nat.ptr(out0.data), nat.ptr(out1.data), n,
+            ctypes.c_void_p(slot_ptr), nonce & MASK64, nat.stream_of(out0.data),
+        ),
+        "rss_mul3_k",
+    )
+    return out0, out1
 
 
 def rss_cross_k(kind: str, x0: RT, x1, y0, y1, slot_ptr: int, nslots: int, nonce: int,

@@ -239,6 +239,10 @@ def mul(sess, x: RepTensor, y: RepTensor) -> RepTensor:
     """Elementwise product (AND for boolean sharings): one fused kernel + one round."""
     with span("rep.mul"):
         kind = x.kind
+        fused = getattr(sess, "p_mul_reshare", None)
+        if fused is not None and getattr(sess, "fused", False):
+            s0, s1 = fused(kind, x.plc, x.s0, x.s1, y.s0, y.s1)
+            return RepTensor(x.plc, x.bits, kind, s0, s1)
         z = sess.p_cross(kind, x.plc, x.s0, x.s1, y.s0, y.s1, zero_share=True)
         return _reshare(sess, x.plc, z, x.bits, kind)
 
@@ -258,6 +262,10 @@ def dot(sess, x: RepTensor, y: RepTensor) -> RepTensor:
     GEMM (all parties batched when stacked), + zero share, + reshare."""
     with span("rep.dot"):
         v = sess.p_dot_cross(x.plc, x.s0, x.s1, y.s0, y.s1)
+        fused = getattr(sess, "p_zero_share_reshare", None)
+        if fused is not None and getattr(sess, "fused", False):
+            s0, s1 = fused(x.plc, v, x.kind)
+            return RepTensor(x.plc, x.bits, x.kind, s0, s1)
         z = sess.p_add_zero_share(x.plc, v, x.kind)
         return _reshare(sess, x.plc, z, x.bits, x.kind)
 

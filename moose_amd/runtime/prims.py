@@ -377,43 +377,23 @@ def _ring_cast(nb, x, bits):
 @prim("BitSplit")
 def _bit_split(nb, x, start, count):
     """Packed word -> bit tensor with a new logical leading axis: out[j] = bit start+j."""
-    d = x.data
-    outs = []
-    for j in range(start, start + count):
-        w = d if x.bits == 64 else d[..., j // 64]
-        outs.append(((w >> (j % 64)) & 1).to(torch.uint8))
-    return R.RT(torch.stack(outs, dim=nb), 1)
+    return R.bit_planes(x, start, count, nb)
 
 
 @prim("WeightedSum")
 def _weighted_sum(nb, x, weights, bits):
     """sum_j weights[j] * x[j] over the leading logical axis (public integer weights)."""
-    acc = None
-    for j, w in enumerate(weights):
-        if w == 0:
-            continue
-        xj = R.index_axis(x, 0, j, nb)
-        t = R.binary("mul", xj, R.fill((), int(w), bits, x.device))
-        acc = t if acc is None else R.binary("add", acc, t)
-    if acc is None:
-        return R.zeros(R.index_axis(x, 0, 0, nb).shape, bits, x.device)
-    return acc
+    return R.weighted_sum(x, weights, nb)
 
 
 @prim("BitDecompose")
 def _bit_decompose(nb, x, to_bits=True):
     """Ring tensor -> its bits stacked on a new leading logical axis (LSB first), as a
     bit tensor or as 0/1 ring elements (reference host/ops.rs:855-937)."""
-    bits = x.bits
-    d = x.data
-    planes = []
-    for j in range(bits):
-        w = d if bits == 64 else d[..., j // 64]
-        planes.append(((w >> (j % 64)) & 1).to(torch.uint8))
-    out = torch.stack(planes, dim=nb)
+    out = R.bit_planes(x, 0, x.bits, nb)
     if to_bits:
-        return R.RT(out, 1)
-    return R.ring_inject(R.RT(out, 1), 0, bits)
+        return out
+    return R.ring_inject(out, 0, x.bits)
 
 
 @prim("ShlDim")

@@ -252,6 +252,21 @@ class StackedSession(Session):
                             self.nonce(plc), 3)
         return PV(plc, out)
 
+    def p_mul_reshare(self, kind, plc, x0, x1, y0, y1):
+        """Both shares of x*y after the reshare, in one kernel (protocol of rep.mul:
+        cross terms + zero share, then z_p -> P_{p-1})."""
+        s0, s1 = R.rss_mul3_k(kind, x0.v, x1.v, y0.v, y1.v, self.key_ptr(plc, 0),
+                              self.nonce(plc))
+        self.stats.record_round(_nbytes(s0))
+        return PV(plc, s0), PV(plc, s1)
+
+    def p_zero_share_reshare(self, plc, z, kind="arith"):
+        """z_p + alpha_p, reshared (the tail of rep.dot), in one kernel."""
+        s0, s1 = R.rss_mul3_k(kind, z.v, None, None, None, self.key_ptr(plc, 0),
+                              self.nonce(plc))
+        self.stats.record_round(_nbytes(s0))
+        return PV(plc, s0), PV(plc, s1)
+
     def p_dot_cross(self, plc, x0, x1, y0, y1):
         return PV(plc, R.dot_cross(x0.v, x1.v, y0.v, y1.v, nb=1))
 

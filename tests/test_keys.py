@@ -76,3 +76,20 @@ def test_frozen_table_does_not_write():
     assert torch.equal(snap, kt.t)
     with pytest.raises(RuntimeError):
         kt.alloc(2)
+
+
+@pytest.mark.parametrize("device", _devices())
+@pytest.mark.parametrize("bits", [1, 64, 128])
+def test_fused_mul_reshare_matches_cross_then_shift(device, bits):
+    if device == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    keys = [os.urandom(16) for _ in range(3)]
+    kt = _table(device, keys)
+    shape = (3, 9, 4)
+    x0, x1, y0, y1 = (R.RT(R.prf_expand([os.urandom(16)], 1, shape, bits, device).data[0], bits)
+                      for _ in range(4))
+    kind = "bool" if bits == 1 else "arith"
+    z = R.rss_cross_k(kind, x0, x1, y0, y1, kt.ptr(0), 3, 11, 3)
+    s0, s1 = R.rss_mul3_k(kind, x0, x1, y0, y1, kt.ptr(0), 11)
+    assert torch.equal(s0.data.cpu(), z.data.cpu())
+    assert torch.equal(s1.data.cpu(), torch.roll(z.data, -1, dims=0).cpu())
