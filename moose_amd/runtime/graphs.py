@@ -63,14 +63,16 @@ class _Stager:
         self.i = 0
 
     def __call__(self, t, device):
-        i = self.i
-        if i >= len(self.host):
-            raise CaptureError("more uploads than in the warm-up run")
-        h = self.host[i]
-        if h.dtype != t.dtype or h.shape != t.shape or not torch.equal(h, t.cpu()):
-            raise CaptureError("data-dependent host->device upload")
-        self.i += 1
-        return self.dev[i]
+        # Uploads come in warm-up order; some warm-up uploads are served from constant
+        # caches during the capture (ring.fill / ring.weighted_sum), so skip forward to
+        # the next recorded upload with the same bytes.
+        tc = t.cpu()
+        for i in range(self.i, len(self.host)):
+            h = self.host[i]
+            if h.dtype == tc.dtype and h.shape == tc.shape and torch.equal(h, tc):
+                self.i = i + 1
+                return self.dev[i]
+        raise CaptureError("data-dependent host->device upload")
 
 
 def _upload_hook(hook):
@@ -175,8 +177,6 @@ class GraphPlan:
                     end()
         self.interp.on_op = None
         torch.cuda.synchronize(self.device)
-        if stager.i != len(stager.host):
-            raise CaptureError("fewer uploads than in the warm-up run")
         self._stager = stager  # keep the staged constants alive
         self.replays = 0
 

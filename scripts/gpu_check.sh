@@ -42,6 +42,13 @@ if [[ $STEPS == *graphs* ]]; then
   done; done
   run dots_graphs 900 python benchmarks/dot_product.py --graphs --sweep --n 3 --json gpurun_out/dots_graphs.jsonl
 fi
+if [[ $STEPS == *quick* ]]; then
+  rm -f gpurun_out/logreg_quick.jsonl
+  run lq_e_128_10 600 python benchmarks/logreg_train.py --batch_size 128 --n_iter 10 --n_exp 3 --json gpurun_out/logreg_quick.jsonl
+  run lq_e_128_100 600 python benchmarks/logreg_train.py --batch_size 128 --n_iter 100 --n_exp 2 --json gpurun_out/logreg_quick.jsonl
+  run lq_g_128_100 600 python benchmarks/logreg_train.py --graphs --batch_size 128 --n_iter 100 --n_exp 3 --json gpurun_out/logreg_quick.jsonl
+  run lq_g_2048_100 600 python benchmarks/logreg_train.py --graphs --batch_size 2048 --n_iter 100 --n_exp 3 --json gpurun_out/logreg_quick.jsonl
+fi
 if [[ $STEPS == *prof* || $STEPS == all ]]; then
   export TMPDIR=/tmp
   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1

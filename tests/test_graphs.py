@@ -32,10 +32,11 @@ def test_signature_distinguishes_shapes_and_values():
 def test_stager_rejects_data_dependent_uploads():
     rec = graphs._Recorder()
     rec(torch.arange(4), "cpu")
+    rec(torch.arange(3), "cpu")
     st = graphs._Stager(rec.items, "cpu")
-    st(torch.arange(4), "cpu")
+    assert torch.equal(st(torch.arange(3), "cpu"), torch.arange(3))  # skips a cached one
     with pytest.raises(graphs.CaptureError):
-        st(torch.arange(4), "cpu")
+        st(torch.arange(4), "cpu")  # already behind it
     st = graphs._Stager(rec.items, "cpu")
     with pytest.raises(graphs.CaptureError):
         st(torch.arange(4) + 1, "cpu")
