@@ -20,7 +20,7 @@ run() {  # run <name> <timeout> <cmd...>
 }
 
 STEPS=${STEPS:-all}
-[[ $STEPS == *test* || $STEPS == all ]] && run pytest_gpu 900 python -m pytest tests -m gpu -x -q
+[[ $STEPS == *test* || $STEPS == all ]] && run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
 [[ $STEPS == *smoke* || $STEPS == all ]] && run smoke 300 python __graft_entry__.py smoke
 [[ $STEPS == *bench* || $STEPS == all ]] && run bench128 600 python bench.py --steps 5 --warmup 2 --check
 [[ $STEPS == *bench* || $STEPS == all ]] && run bench64 600 python bench.py --steps 5 --warmup 2 --ring 64 --check
