@@ -11,6 +11,7 @@ import fcntl
 import os
 import subprocess
 import sys
+import sysconfig
 from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 
@@ -111,5 +112,40 @@ def needs_build() -> bool:
     return newest > lib_t
 
 
+RT_SRC = CSRC / "runtime"
+RT_EXT = HERE / ("_moosert" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def runtime_needs_build() -> bool:
+    srcs = list(RT_SRC.glob("*.cpp")) + list(RT_SRC.glob("*.h"))
+    if not RT_EXT.exists():
+        return True
+    return bool(srcs) and max(p.stat().st_mtime for p in srcs) > RT_EXT.stat().st_mtime
+
+
+def build_runtime(force: bool = False, verbose: bool = False) -> Path:
+    """Native runtime core (csrc/runtime: parser, graph passes, TCP networking, dataflow
+    scheduler, pybind11 bindings) -> moose_amd/_native/_moosert*.so (host C++)."""
+    import pybind11
+
+    BUILD.mkdir(parents=True, exist_ok=True)
+    with open(BUILD / ".lock_rt", "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        if not force and not runtime_needs_build():
+            return RT_EXT
+        tmp = RT_EXT.with_name(RT_EXT.name + ".tmp")
+        cmd = [CXX, "-O2", "-fPIC", "-std=c++17", "-pthread", "-shared",
+               "-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"]]
+        cmd += [str(s) for s in sorted(RT_SRC.glob("*.cpp"))] + ["-o", str(tmp)]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"runtime build failed\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, RT_EXT)
+    return RT_EXT
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    print(build_runtime(force="--force" in sys.argv, verbose=True))

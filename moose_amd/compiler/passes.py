@@ -115,7 +115,12 @@ def _norm_specs(specs):
 
 
 def prune(comp: Computation, **_) -> Computation:
-    """Keep only operations that Outputs (and Saves) transitively depend on."""
+    """Operations that Outputs (and Saves) transitively depend on, following
+    Send->Receive edges too (native graph core when available)."""
+    from moose_amd.runtime import native_rt
+
+    if native_rt.enabled():
+        return native_rt.prune(comp)
     by_name = comp.by_name()
     roots = [op.name for op in comp.operations if op.kind in ("Output", "Save")]
     keep = set()
@@ -173,6 +178,16 @@ def toposort(comp: Computation, **_) -> Computation:
 def well_formed(comp: Computation, **_) -> Computation:
     """Topological order + every operator known + every input defined earlier."""
     from moose_amd.ir.operators import ALL_OPERATORS
+    from moose_amd.runtime import native_rt
+
+    if native_rt.enabled():
+        try:
+            bad = native_rt.graph_of(comp).first_out_of_order()
+        except (native_rt.mod().NativeGraphError, KeyError) as e:
+            raise CompilationError(str(e)) from None
+        if bad >= 0:
+            op = comp.operations[bad]
+            raise CompilationError(f"{op.name}: an input is not defined before use")
 
     seen = set()
     sends = {bytes(op.attrs["rendezvous_key"]) for op in comp.operations if op.kind == "Send"}

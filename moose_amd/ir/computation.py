@@ -324,6 +324,19 @@ class Computation:
                     yield sends[k], j
 
     def toposorted(self) -> "Computation":
+        from moose_amd.runtime import native_rt
+
+        if native_rt.enabled():
+            try:
+                return native_rt.toposort(self)
+            except native_rt.mod().NativeGraphError as e:
+                msg = str(e)
+                if "unknown input" in msg:
+                    raise KeyError(msg) from None
+                raise ValueError(msg) from None
+        return self.toposorted_py()
+
+    def toposorted_py(self) -> "Computation":
         n = len(self.operations)
         succ = [[] for _ in range(n)]
         indeg = [0] * n

@@ -8,8 +8,9 @@ assignment::
 
 The parser is a regex-driven cursor parser; ``parse_computation(parallel=True)``
 splits large sources at line breaks and parses the chunks in a process pool (the
-analogue of the reference's rayon ``parallel_parse_computation``).  A native C++
-parser (``csrc/textual.cpp``) is used when the extension is built.
+analogue of the reference's rayon ``parallel_parse_computation``).  The native C++
+parser (``csrc/runtime/textual.cpp``, chunks on native threads) is used when the
+runtime extension is available; this Python one is its oracle.
 """
 from __future__ import annotations
 
@@ -302,6 +303,20 @@ def _parse_chunk(source: str) -> List[Operation]:
 
 
 def parse_computation(source: str, parallel: bool = True, chunks: int = 8) -> Computation:
+    from moose_amd.runtime import native_rt
+
+    if native_rt.enabled():
+        try:
+            return native_rt.parse(source, threads=chunks if parallel else 1)
+        except native_rt.mod().NativeParseError as e:
+            raise ParseError(str(e)) from None
+        except ValueError as e:  # bad type / placement text
+            raise ParseError(str(e)) from None
+    return parse_computation_py(source, parallel, chunks)
+
+
+def parse_computation_py(source: str, parallel: bool = True, chunks: int = 8) -> Computation:
+    """Pure-Python parser (oracle for the native one; ``MOOSEX_NATIVE_RUNTIME=0``)."""
     if not parallel or len(source) < 2_000_000:
         return Computation(_parse_chunk(source))
     # split at line breaks into `chunks` parts (reference parsing.rs:83-117)

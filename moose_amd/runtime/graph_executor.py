@@ -76,17 +76,38 @@ def _attr_value(v):
 
 class GraphExecutor:
     def __init__(self, device="cpu", storage: Optional[Dict[str, dict]] = None,
-                 identity: Optional[str] = None, transport=None, role_ranks=None):
+                 identity: Optional[str] = None, transport=None, role_ranks=None,
+                 workers: Optional[int] = None, timeout_s: Optional[float] = None):
         self.device = torch.device(device)
         self.storage = storage if storage is not None else {}
         self.identity = identity
         self.tr = transport
         self.role_ranks = role_ranks or {}
+        self.workers = workers
+        self.timeout_s = -1.0 if timeout_s is None else float(timeout_s)
+        self.last_run_stats = None
+
+    def _native_dataflow(self) -> bool:
+        """Native scheduler for in-process runs and TCP-networked identities; RCCL runs
+        keep the ordered walk (RCCL matches messages by order, not by key)."""
+        from moose_amd.runtime import native_rt
+
+        if os.environ.get("MOOSEX_DATAFLOW", "1") == "0" or not native_rt.enabled():
+            return False
+        if self.identity is None:
+            return True
+        from moose_amd.runtime.dataflow import TcpTransport
+
+        return isinstance(self.tr, TcpTransport)
 
     def run(self, comp: Computation, arguments: Optional[dict] = None) -> dict:
         from moose_amd.runtime.interpreter import numpy_to_torch
 
         arguments = arguments or {}
+        if self._native_dataflow():
+            from moose_amd.runtime.dataflow import run_dataflow
+
+            return run_dataflow(self, comp, arguments, self.workers, self.timeout_s)
         comp = comp.toposorted()
         self._used = set()
         env: Dict[str, object] = {}
