@@ -3,7 +3,7 @@ from __future__ import annotations
 
 from moose_amd.ir.computation import Computation
 
-FORMATS = ("textual", "msgpack")
+FORMATS = ("textual", "msgpack", "bincode")
 
 
 def read_computation(path, fmt="textual") -> Computation:
@@ -13,7 +13,10 @@ def read_computation(path, fmt="textual") -> Computation:
     if fmt == "msgpack":
         with open(path, "rb") as f:
             return Computation.from_msgpack(f.read())
-    raise ValueError(f"unsupported computation format {fmt!r} (bincode is Rust-only)")
+    if fmt == "bincode":
+        with open(path, "rb") as f:
+            return Computation.from_bincode(f.read())
+    raise ValueError(f"unsupported computation format {fmt!r}")
 
 
 def write_computation(comp: Computation, path, fmt="textual"):
@@ -30,6 +33,12 @@ def write_computation(comp: Computation, path, fmt="textual"):
             raise ValueError("msgpack output needs --output")
         with open(path, "wb") as f:
             f.write(comp.to_msgpack())
+        return
+    if fmt == "bincode":
+        if path is None:
+            raise ValueError("bincode output needs --output")
+        with open(path, "wb") as f:
+            f.write(comp.to_bincode())
         return
     raise ValueError(f"unsupported computation format {fmt!r}")
 

@@ -295,6 +295,18 @@ class Computation:
 
         return from_msgpack(data)
 
+    # bincode-style binary (reference computation.rs:1837-1844) -------------------
+    def to_bincode(self) -> bytes:
+        from moose_amd.ir.bincode import to_bincode
+
+        return to_bincode(self)
+
+    @staticmethod
+    def from_bincode(data: bytes) -> "Computation":
+        from moose_amd.ir.bincode import from_bincode
+
+        return from_bincode(data)
+
     def to_disk(self, path):
         with open(path, "wb") as f:
             f.write(self.to_msgpack())

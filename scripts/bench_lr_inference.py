@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--device", default=None)
     ap.add_argument("--ring", type=int, default=128, choices=(64, 128))
+    ap.add_argument("--graphs", action="store_true", help="replay captured hipGraphs")
     a = ap.parse_args()
     import torch
     from sklearn.datasets import make_classification
@@ -43,9 +44,15 @@ def main():
     # the ONNX export of a binary sklearn LR: two score rows (-w, w), LOGISTIC transform
     model = predictors.LinearClassifier(np.stack([-w, w]), np.array([-b, b]),
                                         predictors.PostTransform.SIGMOID)
-    comp = model.predictor_factory(predictors.DEFAULT_FIXED_DTYPE)
+    # fixed(24,40) needs Z_2^128 (pymoose's mapping); Z_2^64 uses the reference's
+    # canonical Fixed64 precision fixed(14,23) (replicated/input.rs:91-92)
+    import moose_amd as pm
+
+    dtype = predictors.DEFAULT_FIXED_DTYPE if a.ring == 128 else pm.fixed(14, 23)
+    comp = model.predictor_factory(dtype)
     dev = a.device or ("cuda" if torch.cuda.is_available() else "cpu")
-    rt = LocalMooseRuntime(["alice", "bob", "carole"], device=dev, fixedpoint_ring=a.ring)
+    rt = LocalMooseRuntime(["alice", "bob", "carole"], device=dev, fixedpoint_ring=a.ring,
+                           use_graphs=a.graphs)
     args = {"x": X_test}
     for _ in range(a.warmup):
         out = rt.evaluate_computation(comp, args)
@@ -61,7 +68,8 @@ def main():
         "metric": "private LR inference p50 latency", "value": float(np.median(lat)),
         "unit": "ms", "p90_ms": float(lat[int(0.9 * (len(lat) - 1))]), "runs": a.runs,
         "higher_is_better": False, "batch": int(X_test.shape[0]), "features": 10,
-        "device": dev, "ring": a.ring, "max_abs_err_vs_sklearn": err,
+        "device": dev, "ring": a.ring, "graphs": a.graphs,
+        "fixed": [dtype.integral_precision, dtype.fractional_precision], "max_abs_err_vs_sklearn": err,
         "data": "make_classification(random_state=5), sklearn LogisticRegression",
     }))
 

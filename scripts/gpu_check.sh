@@ -49,6 +49,14 @@ if [[ $STEPS == *quick* ]]; then
   run lq_g_128_100 600 python benchmarks/logreg_train.py --graphs --batch_size 128 --n_iter 100 --n_exp 3 --json gpurun_out/logreg_quick.jsonl
   run lq_g_2048_100 600 python benchmarks/logreg_train.py --graphs --batch_size 2048 --n_iter 100 --n_exp 3 --json gpurun_out/logreg_quick.jsonl
 fi
+if [[ $STEPS == *lrinf* ]]; then
+  run lrinf128 600 python scripts/bench_lr_inference.py --runs 50
+  run lrinf64 600 python scripts/bench_lr_inference.py --runs 50 --ring 64
+  run lrinf128g 600 python scripts/bench_lr_inference.py --runs 50 --graphs
+  run lrinf64g 600 python scripts/bench_lr_inference.py --runs 50 --ring 64 --graphs
+  export TMPDIR=/tmp
+  run lrinf_prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/lrinf_prof -o run --output-format csv -- python scripts/bench_lr_inference.py --runs 5 --warmup 1
+fi
 if [[ $STEPS == *prof* || $STEPS == all ]]; then
   export TMPDIR=/tmp
   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1
