@@ -213,14 +213,17 @@ PYBIND11_MODULE(_moosert, m) {
   py::class_<TcpNetworking, std::shared_ptr<TcpNetworking>>(m, "TcpNetworking")
       .def(py::init([](std::string own, std::map<std::string, std::string> endpoints,
                        std::shared_ptr<Mailbox> mb, double initial_s, double multiplier,
-                       double max_interval_s, double max_elapsed_s) {
+                       double max_interval_s, double max_elapsed_s, std::string cert_file,
+                       std::string key_file, std::string ca_file) {
              BackoffPolicy b{initial_s, multiplier, max_interval_s, max_elapsed_s};
+             TlsConfig tls{std::move(cert_file), std::move(key_file), std::move(ca_file)};
              return std::make_shared<TcpNetworking>(std::move(own), std::move(endpoints),
-                                                    std::move(mb), b);
+                                                    std::move(mb), b, std::move(tls));
            }),
            py::arg("own"), py::arg("endpoints"), py::arg("mailbox"), py::arg("initial_s") = 0.05,
            py::arg("multiplier") = 1.1, py::arg("max_interval_s") = 5.0,
-           py::arg("max_elapsed_s") = 300.0)
+           py::arg("max_elapsed_s") = 300.0, py::arg("cert_file") = "",
+           py::arg("key_file") = "", py::arg("ca_file") = "")
       .def("start", &TcpNetworking::start, py::call_guard<py::gil_scoped_release>())
       .def("send",
            [](TcpNetworking& t, const std::string& receiver, const std::string& key,

@@ -6,6 +6,9 @@
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <sys/socket.h>
+#include <openssl/err.h>
+#include <openssl/ssl.h>
+#include <openssl/x509.h>
 #include <unistd.h>
 
 #include <chrono>
@@ -130,6 +133,63 @@ bool read_all(int fd, char* p, size_t n) {
   return true;
 }
 
+std::string ssl_error() {
+  unsigned long e = ERR_get_error();
+  if (!e) return "unknown TLS error";
+  char buf[256];
+  ERR_error_string_n(e, buf, sizeof(buf));
+  return buf;
+}
+
+bool write_any(int fd, SSL* ssl, const char* p, size_t n) {
+  if (!ssl) return write_all(fd, p, n);
+  while (n) {
+    int w = SSL_write(ssl, p, static_cast<int>(std::min<size_t>(n, 1u << 30)));
+    if (w <= 0) return false;
+    p += w;
+    n -= static_cast<size_t>(w);
+  }
+  return true;
+}
+
+bool read_any(int fd, SSL* ssl, char* p, size_t n) {
+  if (!ssl) return read_all(fd, p, n);
+  while (n) {
+    int r = SSL_read(ssl, p, static_cast<int>(std::min<size_t>(n, 1u << 30)));
+    if (r <= 0) return false;
+    p += r;
+    n -= static_cast<size_t>(r);
+  }
+  return true;
+}
+
+// common name of the peer's (verified) certificate, "" if none
+std::string peer_common_name(SSL* ssl) {
+  X509* cert = SSL_get1_peer_certificate(ssl);
+  if (!cert) return "";
+  char buf[256] = {0};
+  int n = X509_NAME_get_text_by_NID(X509_get_subject_name(cert), NID_commonName, buf,
+                                    sizeof(buf));
+  X509_free(cert);
+  return n > 0 ? std::string(buf, static_cast<size_t>(n)) : "";
+}
+
+SSL_CTX* make_ctx(const TlsConfig& t, bool server) {
+  SSL_CTX* ctx = SSL_CTX_new(server ? TLS_server_method() : TLS_client_method());
+  if (!ctx) throw NetError("SSL_CTX_new: " + ssl_error());
+  SSL_CTX_set_min_proto_version(ctx, TLS1_2_VERSION);
+  if (SSL_CTX_use_certificate_chain_file(ctx, t.cert_file.c_str()) != 1 ||
+      SSL_CTX_use_PrivateKey_file(ctx, t.key_file.c_str(), SSL_FILETYPE_PEM) != 1 ||
+      SSL_CTX_check_private_key(ctx) != 1 ||
+      SSL_CTX_load_verify_locations(ctx, t.ca_file.c_str(), nullptr) != 1) {
+    std::string err = ssl_error();
+    SSL_CTX_free(ctx);
+    throw NetError("TLS setup failed (" + t.cert_file + "): " + err);
+  }
+  SSL_CTX_set_verify(ctx, SSL_VERIFY_PEER | SSL_VERIFY_FAIL_IF_NO_PEER_CERT, nullptr);
+  return ctx;
+}
+
 void split_endpoint(const std::string& ep, std::string& host, int& port) {
   auto c = ep.rfind(':');
   if (c == std::string::npos) throw NetError("endpoint must be host:port, got " + ep);
@@ -152,10 +212,12 @@ T get_le(const char* p) {
 }  // namespace
 
 TcpNetworking::TcpNetworking(std::string own, std::map<std::string, std::string> endpoints,
-                             std::shared_ptr<Mailbox> mailbox, BackoffPolicy backoff)
+                             std::shared_ptr<Mailbox> mailbox, BackoffPolicy backoff,
+                             TlsConfig tls)
     : own_(std::move(own)), endpoints_(std::move(endpoints)), mb_(std::move(mailbox)),
-      backoff_(backoff) {
+      backoff_(backoff), tls_(std::move(tls)) {
   if (!endpoints_.count(own_)) throw NetError("no endpoint for own identity " + own_);
+  if (tls_.enabled()) init_tls();
   for (auto& kv : endpoints_) {
     if (kv.first == own_) continue;
     auto p = std::make_unique<Peer>();
@@ -165,7 +227,22 @@ TcpNetworking::TcpNetworking(std::string own, std::map<std::string, std::string>
   }
 }
 
-TcpNetworking::~TcpNetworking() { close(); }
+TcpNetworking::~TcpNetworking() {
+  close();
+  if (server_ctx_) SSL_CTX_free(static_cast<SSL_CTX*>(server_ctx_));
+  if (client_ctx_) SSL_CTX_free(static_cast<SSL_CTX*>(client_ctx_));
+}
+
+void TcpNetworking::init_tls() {
+  server_ctx_ = make_ctx(tls_, true);
+  try {
+    client_ctx_ = make_ctx(tls_, false);
+  } catch (...) {
+    SSL_CTX_free(static_cast<SSL_CTX*>(server_ctx_));
+    server_ctx_ = nullptr;
+    throw;
+  }
+}
 
 void TcpNetworking::start() {
   std::string host;
@@ -209,12 +286,29 @@ void TcpNetworking::accept_loop() {
 
 void TcpNetworking::read_loop(int fd) {
   // frame: u64 body length | u16 sender len | sender | u32 key len | key | payload
+  SSL* ssl = nullptr;
+  std::string authenticated;
+  if (server_ctx_) {
+    ssl = SSL_new(static_cast<SSL_CTX*>(server_ctx_));
+    SSL_set_fd(ssl, fd);
+    if (SSL_accept(ssl) != 1) {  // unauthenticated peer: drop the connection
+      SSL_free(ssl);
+      return;
+    }
+    authenticated = peer_common_name(ssl);
+  }
+  struct Free {
+    SSL* s;
+    ~Free() {
+      if (s) SSL_free(s);
+    }
+  } free_ssl{ssl};
   while (!closing_) {
     char hdr[8];
-    if (!read_all(fd, hdr, 8)) return;
+    if (!read_any(fd, ssl, hdr, 8)) return;
     uint64_t n = get_le<uint64_t>(hdr);
     std::string body(n, '\0');
-    if (!read_all(fd, body.data(), n)) return;
+    if (!read_any(fd, ssl, body.data(), n)) return;
     size_t off = 0;
     if (n < 6) return;
     uint16_t sl = get_le<uint16_t>(body.data());
@@ -225,6 +319,11 @@ void TcpNetworking::read_loop(int fd) {
     off += 4;
     std::string key = body.substr(off, kl);
     off += kl;
+    if (ssl && sender != authenticated) {
+      mb_->abort("sender identity mismatch: connection authenticated as '" + authenticated +
+                 "' sent a frame as '" + sender + "'");
+      return;
+    }
     Message m{sender, body.substr(off)};
     {
       std::lock_guard<std::mutex> g(stats_mu_);
@@ -279,17 +378,30 @@ void TcpNetworking::send_loop(Peer* p) {
       p->busy = true;
     }
     bool ok = true;
+    std::string why;
     if (p->fd < 0) {
       p->fd = connect_with_backoff(p);
       ok = p->fd >= 0;
+      if (ok && client_ctx_) {
+        SSL* ssl = SSL_new(static_cast<SSL_CTX*>(client_ctx_));
+        SSL_set_fd(ssl, p->fd);
+        p->ssl = ssl;
+        if (SSL_connect(ssl) != 1) {
+          ok = false;
+          why = ": TLS handshake failed: " + ssl_error();
+        } else if (peer_common_name(ssl) != p->identity) {
+          ok = false;
+          why = ": server certificate names '" + peer_common_name(ssl) + "'";
+        }
+      }
     }
-    if (ok) ok = write_all(p->fd, frame.data(), frame.size());
+    if (ok) ok = write_any(p->fd, static_cast<SSL*>(p->ssl), frame.data(), frame.size());
     {
       std::lock_guard<std::mutex> g(p->mu);
       p->busy = false;
       if (!ok && p->error.empty())
         p->error = "could not send to " + p->identity + " at " + p->host + ":" +
-                   std::to_string(p->port);
+                   std::to_string(p->port) + why;
     }
     if (ok) {
       std::lock_guard<std::mutex> g(stats_mu_);
@@ -344,6 +456,10 @@ void TcpNetworking::close() {
   }
   for (auto& kv : peers_) {
     if (kv.second->th.joinable()) kv.second->th.join();
+    if (kv.second->ssl) {
+      SSL_free(static_cast<SSL*>(kv.second->ssl));
+      kv.second->ssl = nullptr;
+    }
     if (kv.second->fd >= 0) ::shutdown(kv.second->fd, SHUT_RDWR), ::close(kv.second->fd);
   }
   if (listen_fd_ >= 0) {

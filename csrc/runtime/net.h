@@ -13,6 +13,13 @@
 // (the dataflow scheduler) are notified on every arrival.  `TcpNetworking` feeds a
 // Mailbox from socket reader threads, so a Receive never blocks a compute thread: the
 // scheduler only runs it once its payload is present.
+//
+// Optional mutual TLS (reference networking/grpc.rs with grpc.rs:1-30 / reindeer.rs:41-78
+// TLS setup): every connection is authenticated both ways against one CA; a peer's
+// identity is the common name of its certificate.  An outgoing connection must reach a
+// server whose certificate names the intended receiver, and every incoming frame must
+// claim the sender identity its connection authenticated (grpc.rs:150-168) -- a
+// mismatch aborts the session.
 #pragma once
 
 #include <atomic>
@@ -73,6 +80,11 @@ class Mailbox {
   std::string abort_reason_;
 };
 
+struct TlsConfig {
+  std::string cert_file, key_file, ca_file;  // all empty: plain TCP
+  bool enabled() const { return !cert_file.empty(); }
+};
+
 struct BackoffPolicy {
   double initial_s = 0.05;
   double multiplier = 1.1;
@@ -84,7 +96,8 @@ class TcpNetworking {
  public:
   // endpoints: identity -> "host:port" (this identity's entry is the listen address)
   TcpNetworking(std::string own, std::map<std::string, std::string> endpoints,
-                std::shared_ptr<Mailbox> mailbox, BackoffPolicy backoff = {});
+                std::shared_ptr<Mailbox> mailbox, BackoffPolicy backoff = {},
+                TlsConfig tls = {});
   ~TcpNetworking();
 
   void start();  // bind + listen + accept loop
@@ -105,6 +118,7 @@ class TcpNetworking {
     std::string identity, host;
     int port = 0;
     int fd = -1;
+    void* ssl = nullptr;  // SSL* when TLS is on
     std::deque<std::string> queue;
     std::mutex mu;
     std::condition_variable cv;
@@ -116,7 +130,11 @@ class TcpNetworking {
   void accept_loop();
   void read_loop(int fd);
   int connect_with_backoff(Peer* p);
+  void init_tls();
 
+  TlsConfig tls_;
+  void* server_ctx_ = nullptr;  // SSL_CTX*
+  void* client_ctx_ = nullptr;
   std::string own_;
   std::map<std::string, std::string> endpoints_;
   std::shared_ptr<Mailbox> mb_;

@@ -137,6 +137,7 @@ def build_runtime(force: bool = False, verbose: bool = False) -> Path:
         cmd = [CXX, "-O2", "-fPIC", "-std=c++17", "-pthread", "-shared",
                "-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"]]
         cmd += [str(s) for s in sorted(RT_SRC.glob("*.cpp"))] + ["-o", str(tmp)]
+        cmd += ["-lssl", "-lcrypto"]  # mutual TLS of the TCP networking
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -65,7 +65,7 @@ def _run_tcp(a, comp, args) -> int:
     elif not any(op.kind == "Send" for op in comp.operations):
         comp = passes.compile(comp, ["networking", "toposort"])
     device = a.device or "cpu"
-    tr = TcpTransport(a.identity, hosts, session_id=a.session_id).start()
+    tr = TcpTransport(a.identity, hosts, session_id=a.session_id, certs_dir=a.certs).start()
     try:
         ex = GraphExecutor(device, identity=a.identity, transport=tr, timeout_s=a.timeout)
         t0 = time.perf_counter()
@@ -86,6 +86,7 @@ def main(argv=None) -> int:
     ap.add_argument("--identity", help="this process's identity (tcp transport)")
     ap.add_argument("--hosts", help='JSON {"identity": "host:port"} (tcp transport)')
     ap.add_argument("--session-id", default="vixen")
+    ap.add_argument("--certs", help="mutual TLS: directory with <identity>.crt/.key, ca.crt")
     ap.add_argument("--timeout", type=float, default=300.0, help="session deadline (s)")
     ap.add_argument("--device", default=None)
     ap.add_argument("--compile", action="store_true")

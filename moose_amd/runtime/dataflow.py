@@ -33,21 +33,36 @@ from moose_amd.parallel import transport as PT
 from moose_amd.runtime import native_rt as N
 
 
+def tls_files(identity: str, certs_dir: str):
+    """``{certs_dir}/{identity}.crt``, ``{identity}.key`` and ``ca.crt`` -- the layout of
+    the reference's ``load_identity_and_ca`` (reindeer.rs:65-78).  The certificate's
+    common name must be the identity."""
+    files = (os.path.join(certs_dir, f"{identity}.crt"), os.path.join(certs_dir, f"{identity}.key"),
+             os.path.join(certs_dir, "ca.crt"))
+    for f in files:
+        if not os.path.exists(f):
+            raise FileNotFoundError(f"TLS file missing: {f}")
+    return files
+
+
 class TcpTransport:
     """Typed value transport between identity processes over the native TCP networking.
 
     ``endpoints``: identity -> "host:port" for every identity (own entry = listen address;
-    port 0 picks a free one, see :attr:`port`).
+    port 0 picks a free one, see :attr:`port`).  ``certs_dir``: mutual TLS with the
+    certificates of :func:`tls_files`; peers are authenticated by certificate CN.
     """
 
     def __init__(self, identity: str, endpoints: Dict[str, str], session_id: str = "",
-                 connect_timeout_s: float = 300.0):
+                 connect_timeout_s: float = 300.0, certs_dir: Optional[str] = None):
         m = N.mod()
         self.identity = identity
         self.session_id = session_id
         self.mailbox = m.Mailbox()
+        tls = tls_files(identity, certs_dir) if certs_dir else ("", "", "")
         self.net = m.TcpNetworking(identity, dict(endpoints), self.mailbox,
-                                   max_elapsed_s=connect_timeout_s)
+                                   max_elapsed_s=connect_timeout_s, cert_file=tls[0],
+                                   key_file=tls[1], ca_file=tls[2])
         self._codec = PT.Transport(0, 1, "cpu")  # header encoder only
         self.started = False
 

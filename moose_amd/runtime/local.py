@@ -91,6 +91,7 @@ class LocalMooseRuntime:
         from moose_amd.runtime.graphs import GraphCache
 
         self._graphs = GraphCache()
+        self._native_cache = {}
 
     def set_default(self):
         from moose_amd.edsl.base import set_current_runtime
@@ -98,8 +99,23 @@ class LocalMooseRuntime:
         set_current_runtime(self)
 
     # ------------------------------------------------------------------
-    def evaluate_computation(self, computation, arguments=None, compiler_passes=None):
+    def _native(self, computation) -> Computation:
+        """to_native, memoised per traced object: re-evaluating the same
+        AbstractComputation skips tracing + conversion and keeps the Computation's
+        identity stable, so captured hipGraph plans are found again."""
+        if isinstance(computation, Computation):
+            return computation
+        hit = self._native_cache.get(id(computation))
+        if hit is not None and hit[0] is computation:
+            return hit[1]
         comp = to_native(computation, self.fixedpoint_ring)
+        if len(self._native_cache) >= 64:
+            self._native_cache.pop(next(iter(self._native_cache)))
+        self._native_cache[id(computation)] = (computation, comp)
+        return comp
+
+    def evaluate_computation(self, computation, arguments=None, compiler_passes=None):
+        comp = self._native(computation)
         if compiler_passes:
             from moose_amd.compiler import passes
 

@@ -270,3 +270,78 @@ def test_vixen_tcp_processes_run_networked_tutorial():
     outs = [p.communicate(timeout=240)[0] for p in procs]
     assert all(p.returncode == 0 for p in procs), outs
     assert "[player2] output_0 = [[32.]]" in outs[2]
+
+
+def _make_certs(d, names):
+    """CA + one certificate per name (CN = name) with the openssl CLI."""
+    import shutil
+    import subprocess
+
+    if shutil.which("openssl") is None:
+        pytest.skip("openssl CLI not available")
+
+    def run(*a):
+        subprocess.run(["openssl", *a], check=True, capture_output=True, cwd=d)
+
+    run("req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", "ca.key", "-out", "ca.crt",
+        "-days", "2", "-subj", "/CN=moosex-test-ca")
+    for n in names:
+        run("req", "-newkey", "rsa:2048", "-nodes", "-keyout", f"{n}.key", "-out", f"{n}.csr",
+            "-subj", f"/CN={n}")
+        run("x509", "-req", "-in", f"{n}.csr", "-CA", "ca.crt", "-CAkey", "ca.key",
+            "-CAcreateserial", "-out", f"{n}.crt", "-days", "2")
+    return str(d)
+
+
+def _run_parties(comp, ids, eps, certs_for):
+    results, errors = {}, []
+
+    def party(ident):
+        try:
+            tr = TcpTransport(ident, eps, session_id="tls", certs_dir=certs_for(ident),
+                              connect_timeout_s=5).start()
+        except Exception as e:
+            errors.append((ident, e))
+            return
+        try:
+            ex = GraphExecutor("cpu", identity=ident, transport=tr, timeout_s=10)
+            results[ident] = ex.run(comp, {})
+        except Exception as e:
+            errors.append((ident, e))
+        finally:
+            tr.close()
+
+    th = [threading.Thread(target=party, args=(i,)) for i in ids]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(60)
+    return results, errors
+
+
+@pytest.mark.skipif(not os.path.exists(NETWORKED), reason="reference checkout not available")
+def test_mutual_tls_networking(tmp_path):
+    """mTLS (reference grpc.rs:150-168): authenticated identities run the tutorial; an
+    identity whose certificate names someone else cannot join."""
+    comp = Computation.from_textual(open(NETWORKED).read())
+    ids = ["player0", "player1", "player2"]
+    certs = _make_certs(tmp_path, ids + ["mallory"])
+    eps = {r: f"127.0.0.1:{p}" for r, p in zip(ids, _free_ports(3))}
+    results, errors = _run_parties(comp, ids, eps, lambda i: certs)
+    assert not errors, errors
+    np.testing.assert_allclose(np.asarray(results["player2"]["output_0"]), [[32.0]], atol=1e-5)
+
+    # player1's endpoint is served with mallory's certificate: nobody may talk to it
+    bad = tmp_path / "bad"
+    bad.mkdir()
+    import shutil
+
+    shutil.copy(tmp_path / "ca.crt", bad / "ca.crt")
+    shutil.copy(tmp_path / "mallory.crt", bad / "player1.crt")
+    shutil.copy(tmp_path / "mallory.key", bad / "player1.key")
+    eps = {r: f"127.0.0.1:{p}" for r, p in zip(ids, _free_ports(3))}
+    results, errors = _run_parties(
+        comp, ids, eps, lambda i: str(bad) if i == "player1" else certs)
+    assert errors and "player2" not in results
+    assert any("names 'mallory'" in str(e) or "mismatch" in str(e) or "deadline" in str(e)
+               for _, e in errors), errors
