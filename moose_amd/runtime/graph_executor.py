@@ -181,24 +181,40 @@ class GraphExecutor:
             return self.storage[host][key]
         if kind in ("RingMulCross", "BitAndCross", "RingDotCross"):
             return _cross(kind, *vals)
-        prim = PRIMS.get(kind)
-        if prim is None:
-            raise GraphExecutionError(f"no host kernel for {kind}")
-        bits = bits_of_ty(op.sig.ret)
-        if kind in _NEEDS_BITS:
-            attrs["bits"] = bits
-        if kind in _NEEDS_DEVICE:
-            attrs["device"] = self.device
-        if kind in ("Cast", "Zeros", "Ones"):
-            attrs["dtype"] = _TY_DTYPE.get(op.sig.ret.name, torch.float64)
-        if kind == "BitDecompose":
-            attrs["to_bits"] = bits == 1
-        if kind in ("RingMulCross", "BitAndCross", "RingDotCross"):
-            return _cross(kind, *vals)
-        params = _params(prim.impl)
-        if params is not None:  # drop IR-only attributes (e.g. scaling_base)
-            attrs = {k: v for k, v in attrs.items() if k in params}
-        return prim.impl(0, *vals, **attrs)
+        return run_host_prim(op, vals, attrs, self.device)
+
+
+def run_host_prim(op, vals, attrs, device):
+    """One host-level operation as its primitive (shared with the interpreter's
+    dialect-level fallback)."""
+    kind = op.kind
+    if kind in ("RingMulCross", "BitAndCross", "RingDotCross"):
+        return _cross(kind, *vals)
+    prim = PRIMS.get(kind)
+    if prim is None:
+        raise GraphExecutionError(f"no host kernel for {kind}")
+    return prim.impl(0, *vals, **prim_attrs(op, attrs, device))
+
+
+def prim_attrs(op, attrs, device):
+    """Keyword arguments of ``op``'s primitive: IR attributes plus the ring width /
+    device / dtype its signature implies, minus IR-only attributes."""
+    kind = op.kind
+    prim = PRIMS[kind]
+    attrs = dict(attrs)
+    bits = bits_of_ty(op.sig.ret)
+    if kind in _NEEDS_BITS:
+        attrs["bits"] = bits
+    if kind in _NEEDS_DEVICE:
+        attrs["device"] = device
+    if kind in ("Cast", "Zeros", "Ones"):
+        attrs["dtype"] = _TY_DTYPE.get(op.sig.ret.name, torch.float64)
+    if kind == "BitDecompose":
+        attrs["to_bits"] = bits == 1
+    params = _params(prim.impl)
+    if params is not None:  # drop IR-only attributes (e.g. scaling_base)
+        attrs = {k: v for k, v in attrs.items() if k in params}
+    return attrs
 
 
 _PARAMS = {}

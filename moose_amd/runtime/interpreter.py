@@ -34,12 +34,23 @@ from moose_amd.ops import ring as R
 from moose_amd.protocols import fixedpoint as fxp
 from moose_amd.protocols import replicated as rep
 from moose_amd.protocols.fixedpoint import RepFixed
+from moose_amd.runtime import shares
 from moose_amd.runtime.session import HV
 from moose_amd.runtime.values import LV
 from moose_amd.runtime.values import MV
 from moose_amd.utils.telemetry import span
 
 _FLOAT = {"Float32": torch.float32, "Float64": torch.float64}
+
+
+# replicated dialect operators handled by Interpreter._rep_dialect (reference
+# replicated/{convert,arith,bits,compare}.rs; Share/TruncPr are special-cased there)
+_REP_DIALECT = {
+    "Share": None, "TruncPr": None,
+    "Msb": rep.msb, "BitDecompose": rep.bit_decompose, "EqualZero": rep.equal_zero,
+    "Xor": rep.xor, "And": rep.and_, "Shl": rep.shl, "BitExtract": rep.bit_extract,
+    "RingInject": rep.b2a,
+}
 
 
 class MooseRuntimeError(errors.KernelError):
@@ -103,7 +114,7 @@ class Interpreter:
         comp = comp.toposorted()
         me = getattr(self.sess, "me", None)  # set for one-process-per-party sessions
         for op in comp.operations:
-            handler = getattr(self, f"op_{op.kind}", None)
+            handler = getattr(self, f"op_{op.kind}", None) or self._dialect_handler(op)
             if handler is None:
                 raise MooseRuntimeError(f"operator {op.kind} is not supported by the interpreter")
             ins = [self.env[n] for n in op.inputs]
@@ -120,6 +131,79 @@ class Interpreter:
                 except Exception as e:  # annotate with the failing op
                     raise MooseRuntimeError(f"{op.name} = {op.kind} failed: {e}") from e
         return self.outputs
+
+    # ------------------------------------------------------------------------
+    # dialect-level operations (textual computations below the logical level)
+    # ------------------------------------------------------------------------
+    def _dialect_handler(self, op):
+        """Handler for an operator without a logical ``op_*`` method: replicated dialect
+        protocols (Share/Reveal/TruncPr/Msb/BitDecompose/...) or, on a host, the host
+        primitive itself -- the role of the reference's SyncSession dispatch tables
+        for host and replicated placements (``execution/synchronous.rs:149-237``)."""
+        if isinstance(op.placement, ReplicatedPlacement) and op.kind in _REP_DIALECT:
+            return self._rep_dialect
+        if isinstance(op.placement, HostPlacement):
+            from moose_amd.runtime.prims import PRIMS
+
+            if op.kind in PRIMS:
+                return self._host_prim
+        return None
+
+    def _host_prim(self, op, ins):
+        from moose_amd.runtime.graph_executor import _attr_value
+        from moose_amd.runtime.graph_executor import prim_attrs
+
+        host = op.placement.owner
+        hp = HostPlacement(host)
+        args = []
+        for x in ins:
+            x = self.to_host(x, host)
+            args.append(x.v if x.kind in ("tensor", "shape") else self._plain(x))
+        attrs = {k: _attr_value(v) for k, v in op.attrs.items()}
+        out = self.sess.h(op.kind, host, *args, **prim_attrs(op, attrs, self.sess.device))
+        ret = op.sig.ret.name
+        if ret == "HostShape":
+            return LV(hp, "shape", None, out)
+        dtype = {"HostFloat64Tensor": T.FLOAT64, "HostFloat32Tensor": T.FLOAT32,
+                 "HostBitTensor": None, "HostUint64Tensor": T.UINT64}.get(ret)
+        if ins and ins[0].dtype is not None and ins[0].dtype.is_fixed and ret.startswith(
+                "HostFixed"):
+            dtype = ins[0].dtype
+        return LV(hp, "tensor", dtype, out)
+
+    def _rep_dialect(self, op, ins):
+        plc = op.placement
+        sess = self.sess
+        kind = op.kind
+        if kind == "Share":
+            x = ins[0]
+            if x.is_host and x.dtype is None:  # raw ring / bit tensor
+                bits = getattr(x.v.v, "bits", None)
+                return LV(plc, "tensor", None,
+                          rep.share(sess, plc, x.v, kind="bool" if bits == 1 else "arith"))
+            return self.to_rep(x, plc)
+        xs = [self.to_rep(x, plc) for x in ins]
+        ts = [x.v.t if isinstance(x.v, RepFixed) else x.v for x in xs]
+        attrs = op.attrs
+        if kind == "TruncPr":
+            amount = int(attrs.get("amount", attrs.get("precision", 0)))
+            t = rep.trunc_pr(sess, ts[0], amount)
+            if isinstance(xs[0].v, RepFixed):
+                f = xs[0].v
+                return LV(plc, "tensor", xs[0].dtype, RepFixed(t, f.frac - amount, f.integ))
+            return LV(plc, "tensor", None, t)
+        fn = _REP_DIALECT[kind]
+        if kind == "Shl":
+            t = fn(sess, ts[0], int(attrs["amount"]))
+        elif kind == "BitExtract":
+            t = fn(sess, ts[0], int(attrs["bit_idx"]))
+        elif kind == "RingInject":
+            t = rep.shl(sess, fn(sess, ts[0], int(attrs.get("ring_bits", 0)) or
+                                 (128 if "128" in op.sig.ret.name else 64)),
+                        int(attrs.get("bit_idx", 0)))
+        else:
+            t = fn(sess, *ts)
+        return LV(plc, "tensor", None, t)
 
     # ------------------------------------------------------------------------
     # SPMD: operations placed on other parties
@@ -189,6 +273,8 @@ class Interpreter:
                 ring = rep.reveal(sess, x.v.t, host)
                 return LV(hp, "tensor", x.dtype, ring)
             opened = rep.reveal(sess, x.v, host)
+            if x.dtype is None:  # raw ring / bit sharing (dialect-level Reveal)
+                return LV(hp, "tensor", None, opened)
             if x.dtype.kind == "Bool":
                 return LV(hp, "tensor", x.dtype, sess.h("ToBool", host, opened))
             if x.dtype.kind == "Uint64":
@@ -287,6 +373,9 @@ class Interpreter:
                 lv = self._cast_host(lv, wd)
         return lv
 
+    def op_Reveal(self, op, ins):
+        return self.to_host(ins[0], op.placement.owner)
+
     def op_Input(self, op, ins):
         name = op.attrs.get("arg_name") or op.name
         if self.symbolic:
@@ -300,12 +389,94 @@ class Interpreter:
             from moose_amd.protocols import aes
 
             return aes.tensor_input(self, op, name)
+        plc = op.placement
+        if isinstance(plc, ReplicatedPlacement) and (
+                rname in shares.REP_TYPES or (name not in self.arguments and any(
+                    shares.share_name(name, r, i) in self.arguments
+                    for i, r in enumerate(plc.owners)))):
+            return self._preshared_input(op, name)
         if name not in self.arguments:
             raise MooseRuntimeError(f"missing argument {name}")
-        plc = op.placement
         host = plc.owner if isinstance(plc, HostPlacement) else plc.owners[0]
         lv = self._host_value_from_python(host, self.arguments[name], op.sig.ret)
         return lv if isinstance(plc, HostPlacement) else self.at(op, lv)
+
+    def _rep_type_info(self, op, meta=None):
+        """(bits, kind, dtype) of a replicated Input/Load from its type (or saved meta)."""
+        ret = op.sig.ret
+        if ret.name in shares.REP_TYPES:
+            bits, kind, dtype = shares.REP_TYPES[ret.name]
+            return bits, kind, (meta or {}).get("dtype", dtype)
+        if meta is not None:
+            return meta["bits"], meta["kind"], meta.get("dtype")
+        d = self._dtype(ret.dtype) if ret.name == "Tensor" else T.UNKNOWN_DTYPE
+        if d.is_fixed:
+            return d.ring_bits, "arith", d
+        if d.kind == "Bool":
+            return 1, "bool", d
+        if d.kind == "Uint64":
+            return 64, "arith", d
+        raise MooseRuntimeError(f"{op.name}: cannot infer the share type of {ret}")
+
+    def _rep_lv(self, plc, t, dtype):
+        if dtype is not None and dtype.is_fixed:
+            return LV(plc, "tensor", dtype, RepFixed(t, dtype.fractional_precision,
+                                                     dtype.integral_precision))
+        return LV(plc, "tensor", dtype, t)
+
+    def _preshared_input(self, op, name):
+        """Replicated Input from pre-shared ``name/<role>/share<i>`` arguments."""
+        plc = op.placement
+        bits, kind, dtype = self._rep_type_info(op)
+
+        def lookup(p, i):
+            k = shares.share_name(name, plc.owners[p], i)
+            if k not in self.arguments:
+                raise MooseRuntimeError(f"missing pre-shared argument {k}")
+            return self.arguments[k]
+
+        t = shares.rep_from_components(self.sess, plc, bits, kind, lookup)
+        return self._rep_lv(plc, t, dtype)
+
+    def _save_shares(self, plc, key, val: LV):
+        """Each party stores its own pair of shares in its own storage."""
+        v = val.v
+        if isinstance(v, MV):
+            raise MooseRuntimeError("saving a public value on a replicated placement; "
+                                    "save it on a host instead")
+        t = v.t if isinstance(v, RepFixed) else v
+        dtype = val.dtype
+        if isinstance(v, RepFixed) and (dtype is None or not dtype.is_fixed):
+            dtype = T.TensorDType("Fixed64" if t.bits == 64 else "Fixed128", v.integ, v.frac)
+        comps = shares.rep_components(self.sess, t)
+        for p, c in enumerate(comps):
+            if c is None:
+                continue
+            role = plc.owners[p]
+            store = self.storage.setdefault(role, {})
+            store[shares.share_name(key, role, p)] = shares.ring_to_python(c[0])
+            store[shares.share_name(key, role, (p + 1) % 3)] = shares.ring_to_python(c[1])
+            store[shares.meta_name(key, role)] = shares.meta_json(t.bits, t.kind, dtype)
+
+    def _load_shares(self, op, key):
+        plc = op.placement
+        me = getattr(self.sess, "me", None)
+        mine = [r for r in plc.owners if me is None or r == me]
+        meta_s = self.storage.get(mine[0], {}).get(shares.meta_name(key, mine[0]))
+        if meta_s is None:
+            raise MooseRuntimeError(f"no share checkpoint {key!r} in storage of {mine[0]}")
+        bits, kind, dtype = self._rep_type_info(op, shares.parse_meta(meta_s))
+
+        def lookup(p, i):
+            role = plc.owners[p]
+            k = shares.share_name(key, role, i)
+            store = self.storage.get(role, {})
+            if k not in store:
+                raise MooseRuntimeError(f"key {k!r} not found in storage of {role}")
+            return store[k]
+
+        t = shares.rep_from_components(self.sess, plc, bits, kind, lookup)
+        return self._rep_lv(plc, t, dtype)
 
     def op_Constant(self, op, ins):
         c: Constant = op.attrs["value"]
@@ -382,17 +553,23 @@ class Interpreter:
 
     def op_Save(self, op, ins):
         key, val = ins
+        k = self._plain(key)
+        if isinstance(op.placement, ReplicatedPlacement):
+            plc = op.placement
+            self._save_shares(plc, k, self.to_rep(val, plc))
+            return LV(plc, "unit", None, MV(plc, None))
         host = op.placement.owner
         val = self.to_host(val, host)
-        k = self._plain(key)
         if self.sess.materialized(val.v):
             self.storage.setdefault(host, {})[k] = self.to_numpy(val)
         return LV(op.placement, "unit", None, HV(host, None))
 
     def op_Load(self, op, ins):
         key, query = ins
-        host = op.placement.owner
         k = self._plain(key)
+        if isinstance(op.placement, ReplicatedPlacement):
+            return self._load_shares(op, k)
+        host = op.placement.owner
         store = self.storage.get(host, {})
         if k not in store:
             from moose_amd.utils import storage as st
