@@ -23,13 +23,16 @@ using Clock = std::chrono::steady_clock;
 // ---------------------------------------------------------------------------
 void Mailbox::put(const std::string& key, Message m) {
   std::vector<Listener> ls;
-  {
+  bool dup = false;
+  {  // errors are raised after the lock is released
     std::lock_guard<std::mutex> g(mu_);
-    if (slots_.count(key) || taken_.count(key))
-      throw NetError("duplicate delivery for rendezvous key " + key);
-    slots_.emplace(key, std::move(m));
-    for (auto& kv : listeners_) ls.push_back(kv.second);
+    dup = slots_.count(key) || taken_.count(key);
+    if (!dup) {
+      slots_.emplace(key, std::move(m));
+      for (auto& kv : listeners_) ls.push_back(kv.second);
+    }
   }
+  if (dup) throw NetError("duplicate delivery for rendezvous key " + key);
   cv_.notify_all();
   for (auto& l : ls) l(key);
 }
@@ -42,14 +45,21 @@ bool Mailbox::has(const std::string& key) {
 Message Mailbox::take(const std::string& key, double timeout_s) {
   std::unique_lock<std::mutex> lk(mu_);
   auto ready = [&] { return aborted_ || slots_.count(key) != 0; };
+  bool timed_out = false;
   if (timeout_s < 0) {
     cv_.wait(lk, ready);
-  } else if (!cv_.wait_for(lk, std::chrono::duration<double>(timeout_s), ready)) {
-    if (taken_.count(key)) throw NetError("rendezvous key " + key + " was already received");
-    throw NetTimeout("timed out waiting for rendezvous key " + key);
+  } else {
+    timed_out = !cv_.wait_for(lk, std::chrono::duration<double>(timeout_s), ready);
   }
   auto it = slots_.find(key);
-  if (it == slots_.end()) throw NetError("session aborted: " + abort_reason_);
+  if (timed_out || it == slots_.end()) {  // errors are raised after the lock is released
+    bool again = taken_.count(key) != 0;
+    std::string reason = abort_reason_;
+    lk.unlock();
+    if (!timed_out) throw NetError("session aborted: " + reason);
+    if (again) throw NetError("rendezvous key " + key + " was already received");
+    throw NetTimeout("timed out waiting for rendezvous key " + key);
+  }
   Message m = std::move(it->second);
   slots_.erase(it);
   taken_.insert(key);
