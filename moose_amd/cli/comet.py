@@ -29,7 +29,21 @@ def main(argv=None) -> int:
     ap.add_argument("--storage-dir", default=None, help="filesystem storage (*.npy)")
     ap.add_argument("--sessions-dir", default=None, help="watch *.session files (rank 0)")
     ap.add_argument("--max-sessions", type=int, default=None)
+    ap.add_argument("--port", type=int, default=None,
+                    help="control-plane port (overrides the port of --store)")
+    ap.add_argument("--telemetry", default=None, metavar="TRACE_JSON",
+                    help="write a Chrome trace of this worker's spans ({identity} expands)")
+    ap.add_argument("--ignore-existing", action="store_true",
+                    help="with --sessions-dir: only sessions that appear after start-up")
+    ap.add_argument("--no-listen", action="store_true",
+                    help="with --sessions-dir: run the existing sessions, then shut down")
     a = ap.parse_args(argv)
+    if a.port is not None:
+        a.store = f"{a.store.rsplit(':', 1)[0]}:{a.port}"
+    if a.telemetry:
+        from moose_amd.utils.telemetry import enable_tracing
+
+        enable_tracing(a.telemetry.replace("{identity}", a.identity))
     import torch
 
     from moose_amd.runtime.choreography import ChoreographyClient
@@ -43,7 +57,9 @@ def main(argv=None) -> int:
     if a.sessions_dir and a.rank == 0:
         client = ChoreographyClient(a.store)
         th = threading.Thread(target=watch_sessions,
-                              args=(a.sessions_dir, client, a.world, stop), daemon=True)
+                              args=(a.sessions_dir, client, a.world, stop),
+                              kwargs={"ignore_existing": a.ignore_existing,
+                                      "no_listen": a.no_listen}, daemon=True)
         th.start()
     try:
         return w.serve(a.max_sessions)

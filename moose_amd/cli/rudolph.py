@@ -27,8 +27,22 @@ def main(argv=None) -> int:
     ap.add_argument("--backend", default=None)
     ap.add_argument("--storage-dir", default=None)
     ap.add_argument("--max-sessions", type=int, default=None)
+    ap.add_argument("--port", type=int, default=None)
+    ap.add_argument("--ignore-existing", action="store_true",
+                    help="ignore sessions already in the directory; only run new ones")
+    ap.add_argument("--no-listen", action="store_true",
+                    help="exit once the existing sessions have been processed")
+    ap.add_argument("--telemetry", default=None, metavar="TRACE_JSON")
     a = ap.parse_args(argv)
     args = ["--identity", a.identity, "--store", a.store, "--sessions-dir", a.sessions]
+    if a.port is not None:
+        args += ["--port", str(a.port)]
+    if a.ignore_existing:
+        args.append("--ignore-existing")
+    if a.no_listen:
+        args.append("--no-listen")
+    if a.telemetry:
+        args += ["--telemetry", a.telemetry]
     if a.backend:
         args += ["--backend", a.backend]
     if a.storage_dir:

@@ -248,15 +248,19 @@ def parse_session_file(path: str) -> dict:
 
 
 def watch_sessions(sessions_dir: str, client: ChoreographyClient, world: int,
-                   stop: threading.Event, poll_s: float = 0.2, log=print):
+                   stop: threading.Event, poll_s: float = 0.2, log=print,
+                   ignore_existing: bool = False, no_listen: bool = False):
     """Launch every new ``*.session`` file in ``sessions_dir`` (session id = stem) and log
-    its outputs when done (choreography/filesystem.rs)."""
+    its outputs when done (choreography/filesystem.rs).  ``ignore_existing``: only files
+    that appear after start-up; ``no_listen``: process the existing files once, then shut
+    the workers down (rudolph ``--ignore-existing`` / ``--no-listen``, main.rs:29-37)."""
     from moose_amd.cli.common import read_computation
 
-    launched = set()
+    pattern = os.path.join(sessions_dir, "*.session")
+    launched = set(glob.glob(pattern)) if ignore_existing else set()
     idents = client.worker_identities(world)
     while not stop.is_set():
-        for p in sorted(glob.glob(os.path.join(sessions_dir, "*.session"))):
+        for p in sorted(glob.glob(pattern)):
             if p in launched:
                 continue
             launched.add(p)
@@ -275,6 +279,9 @@ def watch_sessions(sessions_dir: str, client: ChoreographyClient, world: int,
                             np.asarray(v), allow_pickle=False)
             except Exception as e:
                 log(f"session {os.path.basename(p)} failed: {e}")
+        if no_listen:
+            client.shutdown()
+            return
         stop.wait(poll_s)
 
 

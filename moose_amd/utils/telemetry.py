@@ -98,6 +98,16 @@ def span(name, **args):
                 )
 
 
+def enable_tracing(path: str):
+    """Turn span recording on at run time (CLI ``--telemetry``); dumped at exit.  The
+    reference exports spans to Jaeger (``reindeer.rs:6-30``); here a Chrome trace."""
+    global _TRACE_PATH
+    first = _TRACE_PATH is None
+    _TRACE_PATH = path
+    if first:
+        atexit.register(dump_trace)
+
+
 def dump_trace(path=None):
     path = path or _TRACE_PATH
     if not path:

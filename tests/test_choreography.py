@@ -22,14 +22,14 @@ def _port():
         return s.getsockname()[1]
 
 
-def _start(port, sessions_dir=None):
+def _start(port, sessions_dir=None, extra=()):
     env = dict(os.environ, PYTHONPATH=ROOT, WORLD_SIZE="3")
     procs = []
     for r, ident in enumerate(IDS):
         if sessions_dir:  # filesystem choreography worker (rank 0 watches the dir)
             cmd = [sys.executable, "-m", "moose_amd.cli.rudolph", "--identity", ident,
                    "--store", f"127.0.0.1:{port}", "--sessions", sessions_dir,
-                   "--backend", "gloo"]
+                   "--backend", "gloo", *extra]
         else:
             cmd = [sys.executable, "-m", "moose_amd.cli.comet", "--identity", ident,
                    "--store", f"127.0.0.1:{port}", "--rank", str(r), "--world", "3",
@@ -94,3 +94,28 @@ def test_filesystem_sessions(tmp_path):
         np.testing.assert_allclose(np.load(out), [[1.0], [10.5]], atol=1e-5)
     finally:
         _stop(procs, client)
+
+
+def test_rudolph_no_listen_exits_after_existing_sessions(tmp_path):
+    """``--no-listen``: run what is in the directory, then every worker exits by itself;
+    ``--telemetry`` writes each worker's Chrome trace."""
+    import json
+
+    for f in ("dot.moose", "dot.session"):
+        shutil.copy(os.path.join(ROOT, "examples", f), tmp_path / f)
+    trace = str(tmp_path / "trace_{identity}.json")
+    procs = _start(_port(), sessions_dir=str(tmp_path),
+                   extra=("--no-listen", "--telemetry", trace))
+    try:
+        for p in procs:
+            assert p.wait(180) == 0, p.stdout.read().decode()[-2000:]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    np.testing.assert_allclose(np.load(tmp_path / "dot.result.npy"), [[1.0], [10.5]],
+                               atol=1e-5)
+    for ident in IDS:
+        with open(tmp_path / f"trace_{ident}.json") as f:
+            evs = json.load(f)["traceEvents"]
+        assert any(e["name"].startswith("op.") for e in evs)
