@@ -83,7 +83,10 @@ def main(argv=None) -> int:
     ap.add_argument("-i", "--input-format", default="textual", choices=("textual", "msgpack"))
     ap.add_argument("--transport", default="rccl", choices=("rccl", "tcp"))
     ap.add_argument("--roles", help="comma-separated role per rank (rccl transport)")
-    ap.add_argument("--identity", help="this process's identity (tcp transport)")
+    ap.add_argument("--identity", "--placement", dest="identity",
+                    help="this process's identity (tcp transport)")
+    ap.add_argument("--role-assignment", default=None,
+                    help='JSON {"role": "identity"} applied to the computation\'s roles')
     ap.add_argument("--hosts", help='JSON {"identity": "host:port"} (tcp transport)')
     ap.add_argument("--session-id", default="vixen")
     ap.add_argument("--certs", help="mutual TLS: directory with <identity>.crt/.key, ca.crt")
@@ -96,6 +99,8 @@ def main(argv=None) -> int:
     from moose_amd.cli.common import read_computation
 
     comp = read_computation(a.comp, a.input_format)
+    if a.role_assignment:
+        comp = comp.with_roles(json.loads(a.role_assignment))
     args = _load_args(a.arg)
     if a.transport == "tcp":
         if not (a.identity and a.hosts):

@@ -271,6 +271,27 @@ class Computation:
                 roles.setdefault(o, None)
         return list(roles)
 
+    def with_roles(self, assignment: Dict[str, str]) -> "Computation":
+        """Copy with every role renamed to its identity (``role -> identity``; roles not
+        in ``assignment`` keep their name) -- the role assignment the reference's
+        executors apply when they pick an identity's operations
+        (``execution/asynchronous.rs:579-605``).  Send/Receive peers are renamed too."""
+        import dataclasses
+
+        def ren(plc):
+            if isinstance(plc, HostPlacement):
+                return HostPlacement(assignment.get(plc.owner, plc.owner))
+            return type(plc)(tuple(assignment.get(o, o) for o in plc.owners))
+
+        ops = []
+        for op in self.operations:
+            attrs = dict(op.attrs)
+            for k in ("sender", "receiver"):
+                if isinstance(attrs.get(k), str):
+                    attrs[k] = assignment.get(attrs[k], attrs[k])
+            ops.append(dataclasses.replace(op, placement=ren(op.placement), attrs=attrs))
+        return Computation(ops)
+
     # textual ---------------------------------------------------------------
     def to_textual(self) -> str:
         from moose_amd.ir.textual import print_computation

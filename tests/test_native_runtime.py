@@ -260,16 +260,20 @@ def test_vixen_tcp_processes_run_networked_tutorial():
     import subprocess
     import sys
 
-    ids = ["player0", "player1", "player2"]
+    # the reference's flags: --placement (own identity), --role-assignment, --hosts
+    roles = ["player0", "player1", "player2"]
+    ids = ["alice", "bob", "carole"]
+    ra = json.dumps(dict(zip(roles, ids)))
     hosts = json.dumps({r: f"127.0.0.1:{p}" for r, p in zip(ids, _free_ports(3))})
     env = dict(os.environ, PYTHONPATH=REPO)
     procs = [subprocess.Popen([sys.executable, "-m", "moose_amd.cli.vixen", "--transport", "tcp",
-                               "--identity", i, "--hosts", hosts, "--comp", NETWORKED,
-                               "--timeout", "120"], env=env, stdout=subprocess.PIPE,
-                              stderr=subprocess.STDOUT, text=True) for i in ids]
+                               "--placement", i, "--role-assignment", ra, "--hosts", hosts,
+                               "--comp", NETWORKED, "--timeout", "120"], env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+             for i in ids]
     outs = [p.communicate(timeout=240)[0] for p in procs]
     assert all(p.returncode == 0 for p in procs), outs
-    assert "[player2] output_0 = [[32.]]" in outs[2]
+    assert "[carole] output_0 = [[32.]]" in outs[2]
 
 
 def _make_certs(d, names):
