@@ -101,10 +101,13 @@ def main():
     g = torch.Generator(device="cpu").manual_seed(1234 + session)
     x = (torch.rand(n, n, generator=g, dtype=torch.float64) * 8 - 4).to(device)
     y = (torch.rand(n, n, generator=g, dtype=torch.float64) * 8 - 4).to(device)
-    gather_buf, gather_group = None, None
+    gather_bufs, gather_group, pending = None, None, []
     if n_sessions > 1 and not args.no_gather:
-        # replicas' revealed outputs concatenated along rows (the layout every backend accepts)
-        gather_buf = torch.empty((n_sessions * n, n), dtype=torch.float64, device=device)
+        # replicas' revealed outputs concatenated along rows (the layout every backend
+        # accepts).  Double-buffered: step k's all-gather runs on the RCCL stream while
+        # step k+1 computes; a buffer is reused only after its gather completed.
+        gather_bufs = [torch.empty((n_sessions * n, n), dtype=torch.float64, device=device)
+                       for _ in range(2)]
         if spmd:  # the output owners (carole = party 2) of every session
             gather_group = dist.new_group([3 * s + 2 for s in range(n_sessions)])
     out_owner = (rank % 3 == 2) if spmd else True
@@ -122,17 +125,29 @@ def main():
         def new_session():
             return StackedSession(device)
 
+    n_steps = [0]
+
     def step():
         sess = new_session()
         interp = Interpreter(sess, {}, fixedpoint_ring=args.ring)
         outs = interp.run(comp, {"x": x, "y": y})
         z = outs["output_0"].v.v if out_owner else None
-        if gather_buf is not None and out_owner:
-            dist.all_gather_into_tensor(gather_buf, z.contiguous(), group=gather_group)
+        if gather_bufs is not None and out_owner:
+            if len(pending) == 2:
+                pending.pop(0).wait()
+            buf = gather_bufs[n_steps[0] % 2]
+            pending.append(dist.all_gather_into_tensor(buf, z.contiguous(), group=gather_group,
+                                                       async_op=True))
+        n_steps[0] += 1
         return z
+
+    def drain():
+        while pending:
+            pending.pop(0).wait()
 
     for _ in range(args.warmup):
         step()
+    drain()
     if device.type == "cuda":
         torch.cuda.synchronize()
     if world > 1:
@@ -140,6 +155,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         z = step()
+    drain()  # every step's gather is complete inside the timed region
     if device.type == "cuda":
         torch.cuda.synchronize()
     if world > 1:
