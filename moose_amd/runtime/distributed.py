@@ -57,9 +57,11 @@ def party_device(backend: str, local_rank: int) -> torch.device:
 
 def run_spmd(comp: Computation, arguments: dict, identities: List[str], *, rank: int,
              device=None, seed: Optional[int] = None, fixedpoint_ring: int = 128,
-             storage: Optional[dict] = None, group=None):
+             storage: Optional[dict] = None, group=None, rank_offset: int = 0):
     """Evaluate ``comp`` as party ``identities[rank]`` of an initialised process group.
 
+    ``group``/``rank_offset``: the session runs on a sub-group whose parties are the
+    global ranks ``rank_offset + i`` (data-parallel replicas, :mod:`..parallel.replicas`).
     Returns ``(outputs, stats, elapsed_us)`` where ``outputs`` holds the numpy values of
     the outputs this identity owns.
     """
@@ -72,9 +74,9 @@ def run_spmd(comp: Computation, arguments: dict, identities: List[str], *, rank:
     from moose_amd.compiler.passes import is_lowered
 
     identity = identities[rank]
-    role_ranks = {r: i for i, r in enumerate(identities)}
+    role_ranks = {r: rank_offset + i for i, r in enumerate(identities)}
     device = torch.device(device) if device is not None else torch.device("cpu")
-    tr = Transport(rank, len(identities), device, group=group)
+    tr = Transport(rank_offset + rank, len(identities), device, group=group)
     store = storage if storage is not None else {}
     if is_lowered(comp):
         # a compiled host graph: run this identity's operations, Send/Receive over RCCL
@@ -118,13 +120,14 @@ class DistributedMooseRuntime:
                  storage_mapping: Optional[Dict[str, Dict]] = None, fixedpoint_ring: int = 128,
                  seed: Optional[int] = None, timeout: float = 900.0,
                  master_addr: str = "127.0.0.1", session_timeout: Optional[float] = None,
-                 retries: int = 0, worker_env: Optional[Dict[str, str]] = None):
+                 retries: int = 0, worker_env: Optional[Dict[str, str]] = None,
+                 replicas: int = 1, shard_args=None, device_map: Optional[List[int]] = None):
         if isinstance(identities, dict):  # GrpcMooseRuntime-style {role: endpoint}
             identities = list(identities.keys())
         self.identities = [getattr(i, "name", i) for i in identities]
         if backend is None:
             n = torch.cuda.device_count() if torch.cuda.is_available() else 0
-            backend = "nccl" if n >= len(self.identities) else "gloo"
+            backend = "nccl" if n >= len(self.identities) * max(int(replicas), 1) else "gloo"
         self.backend = backend
         self.storage = {i: dict((storage_mapping or {}).get(i, {})) for i in self.identities}
         self.fixedpoint_ring = fixedpoint_ring
@@ -136,6 +139,15 @@ class DistributedMooseRuntime:
         self.session_timeout = session_timeout
         self.retries = retries
         self.worker_env = dict(worker_env or {})
+        # data parallelism: `replicas` copies of the session on disjoint GPU groups
+        # (global rank = replica * n + party); `shard_args` are split along axis 0 and
+        # the outputs concatenated back (parallel/replicas.py).  `device_map[rank]` pins
+        # a rank to a GPU index (default: rank).
+        self.replicas = int(replicas)
+        self.shard_args = list(shard_args or [])
+        self.device_map = list(device_map) if device_map is not None else None
+        if self.replicas < 1:
+            raise ValueError("replicas must be >= 1")
         self.last_timings = None
         self.last_stats = None
 
@@ -168,7 +180,16 @@ class DistributedMooseRuntime:
         return outs, dict(self.last_timings or {})
 
     def _launch(self, comp: Computation, arguments: dict):
-        n = len(self.identities)
+        R = self.replicas
+        n = len(self.identities) * R
+        replica_args = None
+        if R > 1:
+            from moose_amd.parallel.replicas import shard_arguments
+
+            shards = shard_arguments(arguments, self.shard_args, R)
+            arguments = {k: v for k, v in arguments.items() if k not in self.shard_args}
+            replica_args = [{k: v for k, v in sh.items() if k in self.shard_args}
+                            for sh in shards]
         with tempfile.TemporaryDirectory(prefix="moosex_job_") as job:
             with open(os.path.join(job, "computation.msgpack"), "wb") as f:
                 f.write(comp.to_msgpack())
@@ -180,6 +201,8 @@ class DistributedMooseRuntime:
                     "fixedpoint_ring": self.fixedpoint_ring,
                     "seed": self.seed,
                     "backend": self.backend,
+                    "replicas": R,
+                    "replica_arguments": [_encodable(a) for a in replica_args or []],
                 }))
             port = free_port()
             env = dict(os.environ)
@@ -192,7 +215,8 @@ class DistributedMooseRuntime:
             env["PYTHONPATH"] = pkg_root + os.pathsep + env.get("PYTHONPATH", "")
             procs = []
             for r in range(n):
-                e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+                dev = self.device_map[r] if self.device_map is not None else r
+                e = dict(env, RANK=str(r), LOCAL_RANK=str(dev))
                 procs.append(subprocess.Popen(
                     [sys.executable, "-m", "moose_amd.runtime.worker", "--job", job],
                     env=e, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
@@ -204,21 +228,25 @@ class DistributedMooseRuntime:
                 except subprocess.TimeoutExpired:
                     for q in procs:
                         q.kill()
-                    raise DistributedRuntimeError(f"worker {self.identities[r]} timed out")
+                    raise DistributedRuntimeError(
+                        f"worker {self.identities[r % len(self.identities)]} timed out")
                 logs.append(out.decode(errors="replace"))
                 if p.returncode != 0:
                     failed.append(r)
             if failed:
-                msg = "\n".join(f"--- {self.identities[r]} (rc={procs[r].returncode})\n"
-                                f"{logs[r][-3000:]}" for r in failed)
+                msg = "\n".join(f"--- {self.identities[r % len(self.identities)]} rank {r} "
+                                f"(rc={procs[r].returncode})\n{logs[r][-3000:]}"
+                                for r in failed)
                 raise DistributedRuntimeError(f"worker(s) failed:\n{msg}")
             outputs, timings = {}, {}
-            for r, ident in enumerate(self.identities):
+            for r in range(n):
+                ident = self.identities[r % len(self.identities)]
                 with open(os.path.join(job, f"result_{r}.msgpack"), "rb") as f:
                     res = valuecodec.loads(f.read())
-                outputs.update(res["outputs"])
-                timings[ident] = res["elapsed_us"]
-                self.storage[ident].update(res.get("storage", {}))
+                outputs.update(res["outputs"])  # replica 0 holds the gathered outputs
+                timings[ident] = max(timings.get(ident, 0), res["elapsed_us"])
+                if r < len(self.identities):
+                    self.storage[ident].update(res.get("storage", {}))
             self.last_timings = timings
             return outputs
 

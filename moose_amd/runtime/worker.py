@@ -51,16 +51,33 @@ def run_job(job: str) -> int:
     backend = spec["backend"]
     rank, world = _init_group(backend)
     identities = spec["identities"]
-    if world != len(identities):
-        raise RuntimeError(f"world size {world} != {len(identities)} identities")
+    replicas = int(spec.get("replicas", 1))
+    n = len(identities)
+    if world != n * replicas:
+        raise RuntimeError(f"world size {world} != {n} identities x {replicas} replicas")
     device = party_device(backend, int(os.environ.get("LOCAL_RANK", rank)))
     if device.type == "cuda":
         torch.cuda.set_device(device)
-    ident = identities[rank]
+    replica, party = divmod(rank, n)
+    ident = identities[party]
     storage = {ident: dict(spec["storage"].get(ident, {}))}
-    outs, stats, elapsed = run_spmd(comp, spec["arguments"], identities, rank=rank,
+    arguments = dict(spec["arguments"])
+    group = owner_groups = None
+    if replicas > 1:
+        from moose_amd.parallel import replicas as REP
+
+        replica_groups, owner_groups = REP.make_groups(n, replicas)
+        group = replica_groups[replica]
+        arguments.update(spec["replica_arguments"][replica])
+    outs, stats, elapsed = run_spmd(comp, arguments, identities, rank=party,
                                     device=device, seed=spec["seed"],
-                                    fixedpoint_ring=spec["fixedpoint_ring"], storage=storage)
+                                    fixedpoint_ring=spec["fixedpoint_ring"], storage=storage,
+                                    group=group, rank_offset=replica * n)
+    if replicas > 1:
+        comm_dev = device if backend == "nccl" else torch.device("cpu")
+        outs = REP.gather_outputs(outs, owner_groups[party], replicas, comm_dev)
+        if replica > 0:
+            outs = {}
     res = {
         "outputs": {k: np.asarray(v) if not isinstance(v, (str, bytes)) else v
                     for k, v in outs.items()},
