@@ -126,6 +126,15 @@ int mx_rss_cross_k(int dev, int kind, int words, const void* x0, const void* x1,
 int mx_rss_mul3_k(int dev, int kind, int words, const void* x0, const void* x1, const void* y0,
                   const void* y1, void* out0, void* out1, int64_t n, const uint32_t* slots,
                   uint64_t nonce, void* stream);
+// One Kogge-Stone level of the packed boolean adder for three stacked parties, reshare
+// fused (x*, out* are [3, n] slot vectors of packed words):
+//   t = pk AND (g << d)                     (RSS AND: cross terms ^ zero share)
+//   g' = g ^ t ;  pk' = pk AND (pk << d) if both
+// zero shares: party p xors PRF(k_p) ^ PRF(k_{p+1}) at element e (t) and n + e (pk') of
+// ONE nonce -- the same values as the generic path's stacked [2, n] AND.
+int mx_ks_level3_k(int dev, int words, const void* g0, const void* g1, const void* p0,
+                   const void* p1, void* og0, void* og1, void* op0, void* op1, int64_t n,
+                   int d, int both, const uint32_t* slots, uint64_t nonce, void* stream);
 // mx_prf_expand with nkeys consecutive key slots
 int mx_prf_expand_k(int dev, int words, void* out, int64_t n, int nkeys, const uint32_t* slots,
                     uint64_t nonce, void* stream);

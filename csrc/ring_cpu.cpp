@@ -581,6 +581,52 @@ int mx_rss_mul3_k(int dev, int kind, int words, const void* x0, const void* x1, 
   return 0;
 }
 
+int mx_ks_level3_k(int dev, int words, const void* g0, const void* g1, const void* p0,
+                   const void* p1, void* og0, void* og1, void* op0, void* op1, int64_t n,
+                   int d, int both, const uint32_t* slots, uint64_t nonce, void* stream) {
+  if (dev)
+    return mxh_ks_level3_k(words, g0, g1, p0, p1, og0, og1, op0, op1, n, d, both, slots, nonce,
+                           stream);
+  if (words != 1 && words != 2) return -2;
+  DISPATCH_WORDS(words, T, {
+    const int64_t m = both ? 2 * n : n;
+    std::vector<T> r[3];
+    for (int k = 0; k < 3; ++k) {
+      r[k].resize(m);
+      mx_cpu_prf_range((const uint8_t*)(slots + MX_KEY_SLOT_WORDS * k), nonce, words, 0, m,
+                       r[k].data());
+    }
+    const T *G0 = (const T*)g0, *G1 = (const T*)g1, *A0 = (const T*)p0, *A1 = (const T*)p1;
+    T *OG0 = (T*)og0, *OG1 = (T*)og1, *OP0 = (T*)op0, *OP1 = (T*)op1;
+    parallel_for(n, 4096, [&](int64_t lo, int64_t hi) {
+      for (int64_t e = lo; e < hi; ++e) {
+        T t[3], q[3];
+        for (int p = 0; p < 3; ++p) {
+          const int64_t i = p * n + e;
+          const int pn = (p + 1) % 3;
+          const T s0 = G0[i] << d, s1 = G1[i] << d;
+          t[p] = (A0[i] & s0) ^ (A0[i] & s1) ^ (A1[i] & s0) ^ r[p][e] ^ r[pn][e];
+          if (both) {
+            const T u0 = A0[i] << d, u1 = A1[i] << d;
+            q[p] = (A0[i] & u0) ^ (A0[i] & u1) ^ (A1[i] & u0) ^ r[p][n + e] ^ r[pn][n + e];
+          }
+        }
+        for (int p = 0; p < 3; ++p) {
+          const int64_t i = p * n + e;
+          const int pn = (p + 1) % 3;
+          OG0[i] = G0[i] ^ t[p];
+          OG1[i] = G1[i] ^ t[pn];
+          if (both) {
+            OP0[i] = q[p];
+            OP1[i] = q[pn];
+          }
+        }
+      }
+    });
+    return 0;
+  });
+}
+
 int mx_prf_expand_k(int dev, int words, void* out, int64_t n, int nkeys, const uint32_t* slots,
                     uint64_t nonce, void* stream) {
   if (nkeys < 1 || nkeys > 4) return -3;

@@ -41,7 +41,7 @@ inline hipStream_t S(void* s) { return (hipStream_t)s; }
   } while (0)
 
 template <class T>
-__global__ void k_binary(int op, const T* __restrict__ a, int64_t na, const T* __restrict__ b,
+__global__ void __launch_bounds__(256) k_binary(int op, const T* __restrict__ a, int64_t na, const T* __restrict__ b,
                          int64_t nb, T* __restrict__ out, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -50,14 +50,14 @@ __global__ void k_binary(int op, const T* __restrict__ a, int64_t na, const T* _
 }
 
 template <class T>
-__global__ void k_unary(int op, const T* __restrict__ a, T* __restrict__ out, int64_t n, int k) {
+__global__ void __launch_bounds__(256) k_unary(int op, const T* __restrict__ a, T* __restrict__ out, int64_t n, int k) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
     out[i] = mxr::unop<T>(op, a[i], k);
 }
 
 template <class T>
-__global__ void k_fill(T* __restrict__ out, int64_t n, uint64_t lo, uint64_t hi) {
+__global__ void __launch_bounds__(256) k_fill(T* __restrict__ out, int64_t n, uint64_t lo, uint64_t hi) {
   T v;
   if constexpr (sizeof(T) == 16) {
     v = ((T)hi << 64) | (T)lo;
@@ -71,7 +71,7 @@ __global__ void k_fill(T* __restrict__ out, int64_t n, uint64_t lo, uint64_t hi)
 
 // out[o, j, i] = bit (start + j) of a[o, i] as a 0/1 byte (bit decomposition / split)
 template <class T>
-__global__ void k_bit_planes(const T* __restrict__ a, uint8_t* __restrict__ out, int64_t outer,
+__global__ void __launch_bounds__(256) k_bit_planes(const T* __restrict__ a, uint8_t* __restrict__ out, int64_t outer,
                              int64_t inner, int start, int count) {
   const int64_t n = outer * inner;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < n;
@@ -85,21 +85,27 @@ __global__ void k_bit_planes(const T* __restrict__ a, uint8_t* __restrict__ out,
 
 // out[o, i] = sum_j w[j] * a[o, j, i]  (public ring weights, bit composition)
 template <class T>
-__global__ void k_weighted_sum(const T* __restrict__ a, const T* __restrict__ w,
+__global__ void __launch_bounds__(256) k_weighted_sum(const T* __restrict__ a, const T* __restrict__ w,
                                T* __restrict__ out, int64_t outer, int64_t k, int64_t inner) {
   const int64_t n = outer * inner;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < n;
        g += (int64_t)gridDim.x * blockDim.x) {
     const int64_t o = g / inner, i = g - o * inner;
     const T* src = a + o * k * inner + i;
-    T acc = 0;
-    for (int64_t j = 0; j < k; ++j) acc += w[j] * src[j * inner];
-    out[g] = acc;
+    // independent partial sums so the k loads of a thread are in flight together
+    T acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int64_t j = 0;
+    for (; j + 8 <= k; j += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u] += w[j + u] * src[(j + u) * inner];
+    }
+    for (; j < k; ++j) acc[0] += w[j] * src[j * inner];
+    out[g] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   }
 }
 
 template <class T>
-__global__ void k_compare(int op, const T* __restrict__ a, int64_t na, const T* __restrict__ b,
+__global__ void __launch_bounds__(256) k_compare(int op, const T* __restrict__ a, int64_t na, const T* __restrict__ b,
                           int64_t nb, uint8_t* __restrict__ out, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -107,7 +113,7 @@ __global__ void k_compare(int op, const T* __restrict__ a, int64_t na, const T* 
 }
 
 template <class T>
-__global__ void k_bit_extract(const T* __restrict__ a, uint8_t* __restrict__ out, int64_t n,
+__global__ void __launch_bounds__(256) k_bit_extract(const T* __restrict__ a, uint8_t* __restrict__ out, int64_t n,
                               int bit) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -115,7 +121,7 @@ __global__ void k_bit_extract(const T* __restrict__ a, uint8_t* __restrict__ out
 }
 
 template <class T>
-__global__ void k_ring_inject(const uint8_t* __restrict__ bits, T* __restrict__ out, int64_t n,
+__global__ void __launch_bounds__(256) k_ring_inject(const uint8_t* __restrict__ bits, T* __restrict__ out, int64_t n,
                               int bit) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -123,7 +129,7 @@ __global__ void k_ring_inject(const uint8_t* __restrict__ bits, T* __restrict__ 
 }
 
 template <class T>
-__global__ void k_encode(const double* __restrict__ x, T* __restrict__ out, int64_t n,
+__global__ void __launch_bounds__(256) k_encode(const double* __restrict__ x, T* __restrict__ out, int64_t n,
                          double scale) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -131,7 +137,7 @@ __global__ void k_encode(const double* __restrict__ x, T* __restrict__ out, int6
 }
 
 template <class T>
-__global__ void k_decode(const T* __restrict__ x, double* __restrict__ out, int64_t n,
+__global__ void __launch_bounds__(256) k_decode(const T* __restrict__ x, double* __restrict__ out, int64_t n,
                          double scale) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -144,21 +150,26 @@ __global__ void k_decode(const T* __restrict__ x, double* __restrict__ out, int6
 
 // one thread per output when the reduced axis is short; a block per output otherwise
 template <class T>
-__global__ void k_sum_axis(const T* __restrict__ a, T* __restrict__ out, int64_t outer,
+__global__ void __launch_bounds__(256) k_sum_axis(const T* __restrict__ a, T* __restrict__ out, int64_t outer,
                            int64_t red, int64_t inner) {
   int64_t total = outer * inner;
   for (int64_t oi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; oi < total;
        oi += (int64_t)gridDim.x * blockDim.x) {
     int64_t o = oi / inner, i = oi % inner;
     const T* p = a + o * red * inner + i;
-    T acc = 0;
-    for (int64_t r = 0; r < red; ++r) acc += p[r * inner];
-    out[oi] = acc;
+    T acc[4] = {0, 0, 0, 0};
+    int64_t r = 0;
+    for (; r + 4 <= red; r += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] += p[(r + u) * inner];
+    }
+    for (; r < red; ++r) acc[0] += p[r * inner];
+    out[oi] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   }
 }
 
 template <class T>
-__global__ void k_sum_axis_wide(const T* __restrict__ a, T* __restrict__ out, int64_t red,
+__global__ void __launch_bounds__(256) k_sum_axis_wide(const T* __restrict__ a, T* __restrict__ out, int64_t red,
                                 int64_t inner) {
   __shared__ T part[kBlock];
   int64_t oi = blockIdx.x;
@@ -186,7 +197,7 @@ using mxd::RK;
 using mxd::stage_keys;
 using mxd::stage_tables;
 
-__global__ void k_prg(RK key, uint64_t nonce, uint64_t ctr0, uint8_t* __restrict__ out,
+__global__ void __launch_bounds__(256) k_prg(RK key, uint64_t nonce, uint64_t ctr0, uint8_t* __restrict__ out,
                       int64_t nbytes) {
   __shared__ uint32_t T[256];
   __shared__ uint8_t Sb[256];
@@ -213,7 +224,7 @@ __global__ void k_prg(RK key, uint64_t nonce, uint64_t ctr0, uint8_t* __restrict
 // Key schedules are staged in LDS next to the T-table (from launch parameters or from
 // key slots in device memory, see aes_dev.h).
 template <class T>
-__global__ void k_rss_cross(int kind, const T* __restrict__ x0, const T* __restrict__ x1,
+__global__ void __launch_bounds__(256) k_rss_cross(int kind, const T* __restrict__ x0, const T* __restrict__ x1,
                             const T* __restrict__ y0, const T* __restrict__ y1,
                             T* __restrict__ out, int64_t n, int nparties, int has_keys,
                             KeySrc keys, uint64_t nonce) {
@@ -258,7 +269,7 @@ __global__ void k_rss_cross(int kind, const T* __restrict__ x0, const T* __restr
 // keystream block evaluates the three AES blocks once and finishes all three parties'
 // elements: 3 AES per block instead of 6 (the shares are identical to k_rss_cross).
 template <class T>
-__global__ void k_rss_cross_ring3(int kind, const T* __restrict__ x0, const T* __restrict__ x1,
+__global__ void __launch_bounds__(256) k_rss_cross_ring3(int kind, const T* __restrict__ x0, const T* __restrict__ x1,
                                   const T* __restrict__ y0, const T* __restrict__ y1,
                                   T* __restrict__ out, T* __restrict__ out1, int64_t n,
                                   KeySrc keys, uint64_t nonce) {
@@ -297,8 +308,72 @@ __global__ void k_rss_cross_ring3(int kind, const T* __restrict__ x0, const T* _
   }
 }
 
+// One Kogge-Stone level for the three stacked parties (see mx_ks_level3_k).  One thread
+// per element: the 3 keystreams at counter e (and n + e) are computed once and serve the
+// zero shares of all three parties, whose reshared outputs are written directly.
 template <class T>
-__global__ void k_prf_expand(T* __restrict__ out, int64_t n, int nkeys, KeySrc keys,
+__global__ void __launch_bounds__(256) k_ks_level3(const T* __restrict__ g0, const T* __restrict__ g1,
+                                                   const T* __restrict__ p0, const T* __restrict__ p1,
+                                                   T* __restrict__ og0, T* __restrict__ og1,
+                                                   T* __restrict__ op0, T* __restrict__ op1,
+                                                   int64_t n, int d, int both, KeySrc keys,
+                                                   uint64_t nonce) {
+  __shared__ uint32_t Tt[256];
+  __shared__ uint8_t Sb[256];
+  __shared__ uint32_t rks[3][44];
+  stage_keys(rks, keys, 3);
+  stage_tables(Tt, Sb);
+  constexpr int P = Lane<T>::kPer;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    T rt[3], rq[3];
+    uint64_t lo, hi;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      aes_ctr(rks[k], Tt, Sb, nonce, (uint64_t)(e / P), &lo, &hi);
+      rt[k] = pick<T>(lo, hi, (int)(e % P));
+      rq[k] = 0;
+    }
+    if (both) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        aes_ctr(rks[k], Tt, Sb, nonce, (uint64_t)((n + e) / P), &lo, &hi);
+        rq[k] = pick<T>(lo, hi, (int)((n + e) % P));
+      }
+    }
+    T t[3], q[3], gv0[3], gv1[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      const int64_t i = (int64_t)p * n + e;
+      gv0[p] = g0[i];
+      gv1[p] = g1[i];
+      const T a0 = p0[i], a1 = p1[i];
+      const T s0 = gv0[p] << d, s1 = gv1[p] << d;
+      const int pn = p == 2 ? 0 : p + 1;
+      t[p] = (a0 & s0) ^ (a0 & s1) ^ (a1 & s0) ^ rt[p] ^ rt[pn];
+      if (both) {
+        const T u0 = a0 << d, u1 = a1 << d;
+        q[p] = (a0 & u0) ^ (a0 & u1) ^ (a1 & u0) ^ rq[p] ^ rq[pn];
+      } else {
+        q[p] = 0;
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      const int64_t i = (int64_t)p * n + e;
+      const int pn = p == 2 ? 0 : p + 1;
+      og0[i] = gv0[p] ^ t[p];
+      og1[i] = gv1[p] ^ t[pn];
+      if (both) {
+        op0[i] = q[p];
+        op1[i] = q[pn];
+      }
+    }
+  }
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) k_prf_expand(T* __restrict__ out, int64_t n, int nkeys, KeySrc keys,
                              uint64_t nonce) {
   __shared__ uint32_t Tt[256];
   __shared__ uint8_t Sb[256];
@@ -324,7 +399,7 @@ __global__ void k_prf_expand(T* __restrict__ out, int64_t n, int nkeys, KeySrc k
 
 // Reference (VALU) ring GEMM: 16x16 output tile per block, K staged through LDS.
 template <class T, int TS>
-__global__ void k_gemm_valu(int64_t M, int64_t N, int64_t K, const T* __restrict__ A0,
+__global__ void __launch_bounds__(256) k_gemm_valu(int64_t M, int64_t N, int64_t K, const T* __restrict__ A0,
                             const T* __restrict__ A1, const T* __restrict__ B0,
                             const T* __restrict__ B1, int mode, T* __restrict__ C,
                             int accumulate) {
@@ -622,6 +697,28 @@ int mxh_rss_mul3_k(int kind, int words, const void* x0, const void* x1, const vo
   for (int i = 0; i < 3; ++i) ptrs[i] = slots + MX_KEY_SLOT_WORDS * i;
   return launch_rss_cross(kind, words, x0, x1, y0, y1, out0, n, 3, true, true,
                           mxd::keysrc_slots(ptrs, 3), nonce, stream, out1);
+}
+
+int mxh_ks_level3_k(int words, const void* g0, const void* g1, const void* p0, const void* p1,
+                    void* og0, void* og1, void* op0, void* op1, int64_t n, int d, int both,
+                    const uint32_t* slots, uint64_t nonce, void* stream) {
+  if (n == 0) return 0;
+  const uint32_t* ptrs[3];
+  for (int i = 0; i < 3; ++i) ptrs[i] = slots + MX_KEY_SLOT_WORDS * i;
+  KeySrc k = mxd::keysrc_slots(ptrs, 3);
+  if (words == 1) {
+    hipLaunchKernelGGL(k_ks_level3<u64>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
+                       (const u64*)g0, (const u64*)g1, (const u64*)p0, (const u64*)p1,
+                       (u64*)og0, (u64*)og1, (u64*)op0, (u64*)op1, n, d, both, k, nonce);
+  } else if (words == 2) {
+    hipLaunchKernelGGL(k_ks_level3<u128>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
+                       (const u128*)g0, (const u128*)g1, (const u128*)p0, (const u128*)p1,
+                       (u128*)og0, (u128*)og1, (u128*)op0, (u128*)op1, n, d, both, k, nonce);
+  } else {
+    return -2;
+  }
+  MX_LAUNCH_CHECK();
+  return 0;
 }
 
 int mxh_prf_expand(int words, void* out, int64_t n, int nkeys, const uint8_t* keys16,

@@ -17,7 +17,7 @@ using u128 = unsigned __int128;
 namespace {
 
 template <class T>
-__global__ void k_trunc_pr3(const T* __restrict__ s0, T* __restrict__ out0, T* __restrict__ out1,
+__global__ void __launch_bounds__(256) k_trunc_pr3(const T* __restrict__ s0, T* __restrict__ out0, T* __restrict__ out1,
                             int64_t n, int m, mxd::KeySrc keys, uint64_t n_r0, uint64_t n_r1,
                             uint64_t n_t, uint64_t n_m, uint64_t n_z0, uint64_t n_z2) {
   __shared__ uint32_t Tt[256];
@@ -58,7 +58,7 @@ __global__ void k_trunc_pr3(const T* __restrict__ s0, T* __restrict__ out0, T* _
 }
 
 template <class T>
-__global__ void k_share3(int kind, const T* __restrict__ x, T* __restrict__ out0,
+__global__ void __launch_bounds__(256) k_share3(int kind, const T* __restrict__ x, T* __restrict__ out0,
                          T* __restrict__ out1, int64_t n, int j0, mxd::KeySrc keys, uint64_t n1,
                          uint64_t na) {
   __shared__ uint32_t Tt[256];

@@ -782,6 +782,29 @@ def rss_mul3_k(kind: str, x0: RT, x1: RT, y0: RT, y1: RT, slot_ptr: int, nonce: 
     return out0, out1
 
 
+def ks_level3_k(g0: RT, g1: RT, p0: RT, p1: RT, d: int, both: bool, slot_ptr: int,
+                nonce: int):
+    """One fused Kogge-Stone level for three stacked parties (mx_ks_level3_k): returns
+    the reshared (g0', g1', p0', p1') -- p0'/p1' are None unless ``both``."""
+    bits = g0.bits
+    shp = g0.shape
+    datas = [x.data.contiguous() for x in (g0, g1, p0, p1)]
+    n = math.prod(shp) // 3
+    outs = [empty(shp, bits, g0.device) for _ in range(4 if both else 2)]
+    dummy = outs[0].data
+    nat.check(
+        nat.lib().mx_ks_level3_k(
+            nat.dev_of(outs[0].data), _words(bits), *[nat.ptr(x) for x in datas],
+            nat.ptr(outs[0].data), nat.ptr(outs[1].data),
+            nat.ptr(outs[2].data if both else dummy), nat.ptr(outs[3].data if both else dummy),
+            n, int(d), 1 if both else 0, ctypes.c_void_p(slot_ptr), nonce & MASK64,
+            nat.stream_of(outs[0].data),
+        ),
+        "ks_level3_k",
+    )
+    return (outs[0], outs[1], outs[2], outs[3]) if both else (outs[0], outs[1], None, None)
+
+
 def rss_cross_k(kind: str, x0: RT, x1, y0, y1, slot_ptr: int, nslots: int, nonce: int,
                 nparties: int) -> RT:
     """``rss_cross`` with the zero-share keys read from key slots: party p uses slots

@@ -314,31 +314,24 @@ def _normalize(sess, x: RepFixed):
 # polynomials (log-depth power tree, public coefficients)
 # ---------------------------------------------------------------------------
 def poly_eval(sess, x: RepFixed, coeffs) -> RepFixed:
-    """sum_k c_k x^k.  Powers x^2..x^n are computed level by level (x^(a+b) from x^a,
-    x^b with a, b <= 2^level), so depth is ceil(log2 n) multiplication rounds; all powers
-    of one level are batched into one stacked multiplication."""
+    """sum_k c_k x^k.  The powers stay stacked on a leading axis P = [x, x^2, ...]: level
+    by level x^(h+1..h+m) = x^h * P[0:m] is ONE stacked multiplication (depth
+    ceil(log2 n) rounds), and the sum is one public weighted sum over P + one TruncPr."""
     n = len(coeffs) - 1
-    powers = {1: x}
+    f, bits = x.frac, x.bits
+    shape = tuple(shape_of(sess, x))
+    P = local(sess, x, "ExpandDims", axis=[0])
     have = 1
     while have < n:
-        targets = [k for k in range(have + 1, min(2 * have, n) + 1)]
-        lefts = [powers[have] for _ in targets]
-        rights = [powers[k - have] for k in targets]
-        prods = _batched_mul(sess, lefts, rights)
-        for k, pr in zip(targets, prods):
-            powers[k] = pr
-        have = min(2 * have, n)
-    f, bits = x.frac, x.bits
-    acc = None
-    for k in range(1, n + 1):
-        c = coeffs[k]
-        if c == 0:
-            continue
-        term = rep.mul_public(sess, powers[k].t, _encode_const(sess, c, f, bits))
-        acc = term if acc is None else rep.add(sess, acc, term)
+        m = min(2 * have, n) - have
+        xh = local(sess, P, "Slice", slice=(have - 1, have, None))
+        left = xh if m == 1 else local(sess, xh, "Broadcast", shape=(m,) + shape)
+        right = P if m == have else local(sess, P, "Slice", slice=(0, m, None))
+        P = concat(sess, [P, mul(sess, left, right)], 0)
+        have += m
+    acc = _weighted(sess, P.t, [int(round(c * (1 << f))) for c in coeffs[1:]], bits)
     acc = rep.trunc_pr(sess, acc, f)
-    out = RepFixed(acc, f, x.integ)
-    return add_const(sess, out, coeffs[0])
+    return add_const(sess, RepFixed(acc, f, x.integ), coeffs[0])
 
 
 def _batched_mul(sess, xs, ys):
@@ -450,24 +443,32 @@ def _exp2_parts(sess, a: RepFixed, negative: bool):
         p = mul_const(sess, poly_eval(sess, one_minus, _fit("exp2", 0.0, 1.0, 7)), 0.5)
     else:
         p = poly_eval(sess, r, _fit("exp2", 0.0, 1.0, 7))
-    # integer part factors: 1 + b_j (c_j - 1), c_j = 2^(+-2^j)
-    factors = []
+    # integer part factors 1 + b_j (c_j - 1), c_j = 2^(+-2^j), for all j at once: the
+    # integer bit planes stay stacked on the leading axis, scaled by a public vector
+    cs = []
     for j in range(nint):
-        bj = local(sess, ab, "IndexAxis", axis=0, index=f + j)
         e = 2 ** j
         if negative:
             c = 2.0 ** (-e) if e <= f + 2 else 0.0  # underflows to 0 at precision f
         else:
             c = 2.0 ** min(e, integ + 1)  # saturate: larger results overflow anyway
-        fac = rep.mul_public(sess, bj, _encode_const(sess, c - 1.0, f, bits))
-        fac = rep.add_public(sess, fac, _encode_const(sess, 1.0, f, bits))
-        factors.append(RepFixed(fac, f, integ))
-    while len(factors) > 1:
-        nxt = _batched_mul(sess, factors[0::2][: len(factors) // 2], factors[1::2])
-        if len(factors) % 2:
-            nxt.append(factors[-1])
-        factors = nxt
-    return mul(sess, p, factors[0])
+        cs.append(int(round((c - 1.0) * (1 << f))))
+    ints = local(sess, ab, "Slice", slice=(f, f + nint, None))
+    ndim = len(shape_of(sess, ints)) - 1
+    cvec = R.from_ints(np.array(cs, dtype=object).reshape((nint,) + (1,) * ndim), bits,
+                       sess.device)
+    fac = rep.mul_public(sess, ints, cvec)
+    fac = rep.add_public(sess, fac, _encode_const(sess, 1.0, f, bits))
+    # log-depth product over the leading axis: one stacked multiplication per level
+    F, n = RepFixed(fac, f, integ), nint
+    while n > 1:
+        h = n // 2
+        prod = mul(sess, local(sess, F, "Slice", slice=(0, h, None)),
+                   local(sess, F, "Slice", slice=(h, 2 * h, None)))
+        F = prod if n % 2 == 0 else concat(
+            sess, [prod, local(sess, F, "Slice", slice=(2 * h, n, None))], 0)
+        n = (n + 1) // 2
+    return mul(sess, p, local(sess, F, "IndexAxis", axis=0, index=0))
 
 
 def exp2(sess, x: RepFixed) -> RepFixed:

@@ -325,6 +325,17 @@ def binary_adder(sess, a: RepTensor, b: RepTensor) -> RepTensor:
     g = and_(sess, a, b)
     pk = p
     d = 1
+    level = getattr(sess, "p_ks_level", None) if getattr(sess, "fused", False) else None
+    if level is not None and bits in (64, 128):
+        # stacked session: each level (shifts, both ANDs, reshare, xor) is one kernel
+        while d < bits:
+            both = 2 * d < bits
+            g0, g1, q0, q1 = level(a.plc, g.s0, g.s1, pk.s0, pk.s1, d, both)
+            g = RepTensor(a.plc, bits, "bool", g0, g1)
+            if both:
+                pk = RepTensor(a.plc, bits, "bool", q0, q1)
+            d *= 2
+        return xor(sess, p, shl(sess, g, 1))
     while d < bits:
         # batch the two independent ANDs of this level in one round
         gs = shl(sess, g, d)

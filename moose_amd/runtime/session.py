@@ -260,6 +260,16 @@ class StackedSession(Session):
         self.stats.record_round(_nbytes(s0))
         return PV(plc, s0), PV(plc, s1)
 
+    def p_ks_level(self, plc, g0, g1, p0, p1, d, both):
+        """One Kogge-Stone level of rep.binary_adder (AND(s) + reshare + xor) in one
+        kernel; consumes the one nonce of the generic level's AND round."""
+        og0, og1, op0, op1 = R.ks_level3_k(g0.v, g1.v, p0.v, p1.v, d, both,
+                                           self.key_ptr(plc, 0), self.nonce(plc))
+        self.stats.record_round(_nbytes(og0) * (2 if both else 1))
+        if not both:
+            return PV(plc, og0), PV(plc, og1), None, None
+        return PV(plc, og0), PV(plc, og1), PV(plc, op0), PV(plc, op1)
+
     def p_zero_share_reshare(self, plc, z, kind="arith"):
         """z_p + alpha_p, reshared (the tail of rep.dot), in one kernel."""
         s0, s1 = R.rss_mul3_k(kind, z.v, None, None, None, self.key_ptr(plc, 0),

@@ -143,6 +143,8 @@ def test_fused_protocol_kernels_match_host(bits):
         x = HV("b", R.encode(torch.linspace(-20, 20, 4099, dtype=torch.float64).to(dev), 23, bits))
         X = rep.share(s, plc, x)
         T = rep.trunc_pr(s, rep.mul(s, X, X), 23)
-        res.append([t.cpu() for t in (X.s0.v.data, X.s1.v.data, T.s0.v.data, T.s1.v.data)])
+        B = rep.bit_decompose(s, X)  # fused Kogge-Stone levels (k_ks_level3)
+        res.append([t.cpu() for t in (X.s0.v.data, X.s1.v.data, T.s0.v.data, T.s1.v.data,
+                                      B.s0.v.data, B.s1.v.data)])
     for a, b in zip(*res):
         assert torch.equal(a, b)

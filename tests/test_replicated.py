@@ -152,3 +152,32 @@ def test_fused_kernels_match_generic_protocol(bits, owner):
         outs.append([X.s0.v.data, X.s1.v.data, T.s0.v.data, T.s1.v.data])
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+def test_fused_kogge_stone_level_bitwise_equals_generic(bits):
+    """The stacked session's one-kernel Kogge-Stone level (mx_ks_level3_k) produces the
+    same shares as the generic per-step protocol (shifts, stacked AND, reshare, xor)."""
+    import torch
+
+    from moose_amd.ir.computation import ReplicatedPlacement
+    from moose_amd.ops import ring as R
+    from moose_amd.protocols import replicated as rep
+    from moose_amd.runtime.session import HV
+    from moose_amd.runtime.session import StackedSession
+
+    plc = ReplicatedPlacement(("a", "b", "c"))
+    outs = []
+    for fused in (True, False):
+        s = StackedSession("cpu", seed=5)
+        s.fused = fused
+        x = R.encode(torch.linspace(-30, 30, 301, dtype=torch.float64), 23, bits)
+        X = rep.share(s, plc, HV("b", x))
+        B = rep.bit_decompose(s, X)
+        M = rep.msb(s, X)
+        outs.append([B.s0.v.data, B.s1.v.data, M.s0.v.data, M.s1.v.data])
+        opened = R.to_ints(rep.reveal(s, B, "c").v)
+        want = R.to_ints(x)
+        assert (opened == want).all()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
