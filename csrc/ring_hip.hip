@@ -308,9 +308,10 @@ __global__ void __launch_bounds__(256) k_rss_cross_ring3(int kind, const T* __re
   }
 }
 
-// One Kogge-Stone level for the three stacked parties (see mx_ks_level3_k).  One thread
-// per element: the 3 keystreams at counter e (and n + e) are computed once and serve the
-// zero shares of all three parties, whose reshared outputs are written directly.
+// One Kogge-Stone level for the three stacked parties (see mx_ks_level3_k).  A block
+// handles EPB elements: its NS = 3 (t) or 6 (t and pk') keystream values per element are
+// computed one AES per thread into LDS (one AES on the critical path), then EPB threads
+// finish all three parties' shares and write the reshared outputs directly.
 template <class T>
 __global__ void __launch_bounds__(256) k_ks_level3(const T* __restrict__ g0, const T* __restrict__ g1,
                                                    const T* __restrict__ p0, const T* __restrict__ p1,
@@ -318,57 +319,112 @@ __global__ void __launch_bounds__(256) k_ks_level3(const T* __restrict__ g0, con
                                                    T* __restrict__ op0, T* __restrict__ op1,
                                                    int64_t n, int d, int both, KeySrc keys,
                                                    uint64_t nonce) {
+  constexpr int EPB = 256 / 6;
   __shared__ uint32_t Tt[256];
   __shared__ uint8_t Sb[256];
   __shared__ uint32_t rks[3][44];
+  __shared__ T ks[6][EPB];
   stage_keys(rks, keys, 3);
   stage_tables(Tt, Sb);
   constexpr int P = Lane<T>::kPer;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    T rt[3], rq[3];
-    uint64_t lo, hi;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      aes_ctr(rks[k], Tt, Sb, nonce, (uint64_t)(e / P), &lo, &hi);
-      rt[k] = pick<T>(lo, hi, (int)(e % P));
-      rq[k] = 0;
+  const int NS = both ? 6 : 3;
+  const int tid = threadIdx.x, s = tid / EPB, le = tid % EPB;
+  for (int64_t e0 = (int64_t)blockIdx.x * EPB; e0 < n; e0 += (int64_t)gridDim.x * EPB) {
+    if (s < NS && e0 + le < n) {
+      const int64_t c = (s < 3 ? 0 : n) + e0 + le;  // t at e, pk' at n + e
+      uint64_t lo, hi;
+      aes_ctr(rks[s % 3], Tt, Sb, nonce, (uint64_t)(c / P), &lo, &hi);
+      ks[s][le] = pick<T>(lo, hi, (int)(c % P));
     }
-    if (both) {
+    __syncthreads();
+    const int64_t e = e0 + tid;
+    if (tid < EPB && e < n) {
+      T t[3], q[3], gv0[3], gv1[3];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        aes_ctr(rks[k], Tt, Sb, nonce, (uint64_t)((n + e) / P), &lo, &hi);
-        rq[k] = pick<T>(lo, hi, (int)((n + e) % P));
+      for (int p = 0; p < 3; ++p) {
+        const int64_t i = (int64_t)p * n + e;
+        gv0[p] = g0[i];
+        gv1[p] = g1[i];
+        const T a0 = p0[i], a1 = p1[i];
+        const T s0 = gv0[p] << d, s1 = gv1[p] << d;
+        const int pn = p == 2 ? 0 : p + 1;
+        t[p] = (a0 & s0) ^ (a0 & s1) ^ (a1 & s0) ^ ks[p][tid] ^ ks[pn][tid];
+        if (both) {
+          const T u0 = a0 << d, u1 = a1 << d;
+          q[p] = (a0 & u0) ^ (a0 & u1) ^ (a1 & u0) ^ ks[3 + p][tid] ^ ks[3 + pn][tid];
+        } else {
+          q[p] = 0;
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const int64_t i = (int64_t)p * n + e;
+        const int pn = p == 2 ? 0 : p + 1;
+        og0[i] = gv0[p] ^ t[p];
+        og1[i] = gv1[p] ^ t[pn];
+        if (both) {
+          op0[i] = q[p];
+          op1[i] = q[pn];
+        }
       }
     }
-    T t[3], q[3], gv0[3], gv1[3];
+    __syncthreads();
+  }
+}
+
+// Latency variant for small launches (few keystream blocks): the block's 3 x EPB AES
+// blocks are computed one per thread into LDS, then EPB threads finish the elements --
+// one AES on the critical path instead of three.
+template <class T>
+__global__ void __launch_bounds__(256) k_rss_cross_ring3_lat(int kind, const T* __restrict__ x0,
+                                                             const T* __restrict__ x1,
+                                                             const T* __restrict__ y0,
+                                                             const T* __restrict__ y1,
+                                                             T* __restrict__ out,
+                                                             T* __restrict__ out1, int64_t n,
+                                                             KeySrc keys, uint64_t nonce) {
+  constexpr int EPB = 256 / 3;
+  __shared__ uint32_t Tt[256];
+  __shared__ uint8_t Sb[256];
+  __shared__ uint32_t rks[3][44];
+  __shared__ uint64_t kl[3][EPB], kh[3][EPB];
+  stage_keys(rks, keys, 3);
+  stage_tables(Tt, Sb);
+  constexpr int P = Lane<T>::kPer;
+  const int64_t nb = (n + P - 1) / P;
+  const int tid = threadIdx.x, s = tid / EPB, lb = tid % EPB;
+  for (int64_t b0 = (int64_t)blockIdx.x * EPB; b0 < nb; b0 += (int64_t)gridDim.x * EPB) {
+    if (s < 3 && b0 + lb < nb) {
+      uint64_t lo, hi;
+      aes_ctr(rks[s], Tt, Sb, nonce, (uint64_t)(b0 + lb), &lo, &hi);
+      kl[s][lb] = lo;
+      kh[s][lb] = hi;
+    }
+    __syncthreads();
+    if (tid < EPB && b0 + tid < nb) {
+      const int64_t b = b0 + tid;
 #pragma unroll
-    for (int p = 0; p < 3; ++p) {
-      const int64_t i = (int64_t)p * n + e;
-      gv0[p] = g0[i];
-      gv1[p] = g1[i];
-      const T a0 = p0[i], a1 = p1[i];
-      const T s0 = gv0[p] << d, s1 = gv1[p] << d;
-      const int pn = p == 2 ? 0 : p + 1;
-      t[p] = (a0 & s0) ^ (a0 & s1) ^ (a1 & s0) ^ rt[p] ^ rt[pn];
-      if (both) {
-        const T u0 = a0 << d, u1 = a1 << d;
-        q[p] = (a0 & u0) ^ (a0 & u1) ^ (a1 & u0) ^ rq[p] ^ rq[pn];
-      } else {
-        q[p] = 0;
+      for (int p = 0; p < 3; ++p) {
+        const int q = p == 2 ? 0 : p + 1;
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+          const int64_t e = b * P + j;
+          if (e >= n) break;
+          const int64_t i = (int64_t)p * n + e;
+          T v = 0;
+          if (x0 != nullptr && y0 != nullptr)
+            v = mxr::cross<T>(kind, x0[i], x1 ? x1[i] : (T)0, y0[i], y1 ? y1[i] : (T)0,
+                              x1 != nullptr, y1 != nullptr);
+          else if (x0 != nullptr)
+            v = x0[i];
+          const T z = mxr::zs_combine<T>(kind, v, pick<T>(kl[p][tid], kh[p][tid], j),
+                                         pick<T>(kl[q][tid], kh[q][tid], j));
+          out[i] = z;
+          if (out1 != nullptr) out1[(int64_t)(p == 0 ? 2 : p - 1) * n + e] = z;
+        }
       }
     }
-#pragma unroll
-    for (int p = 0; p < 3; ++p) {
-      const int64_t i = (int64_t)p * n + e;
-      const int pn = p == 2 ? 0 : p + 1;
-      og0[i] = gv0[p] ^ t[p];
-      og1[i] = gv1[p] ^ t[pn];
-      if (both) {
-        op0[i] = q[p];
-        op1[i] = q[pn];
-      }
-    }
+    __syncthreads();
   }
 }
 
@@ -636,6 +692,14 @@ int launch_rss_cross(int kind, int words, const void* x0, const void* x1, const 
     constexpr int P = 16 / (int)sizeof(T);
     if (ring3) {
       const int64_t blocks = (n + P - 1) / P;
+      if (blocks <= 16384) {  // latency-bound launch: one AES per thread, via LDS
+        const int64_t g = (blocks + 84) / 85;
+        hipLaunchKernelGGL(k_rss_cross_ring3_lat<T>, dim3((unsigned)g), dim3(kBlock), 0,
+                           S(stream), kind, (const T*)x0, (const T*)x1, (const T*)y0,
+                           (const T*)y1, (T*)out, (T*)out1, n, k, nonce);
+        MX_LAUNCH_CHECK();
+        return 0;
+      }
       hipLaunchKernelGGL(k_rss_cross_ring3<T>, dim3(grid_for(blocks)), dim3(kBlock), 0,
                          S(stream), kind, (const T*)x0, (const T*)x1, (const T*)y0,
                          (const T*)y1, (T*)out, (T*)out1, n, k, nonce);
@@ -699,6 +763,11 @@ int mxh_rss_mul3_k(int kind, int words, const void* x0, const void* x1, const vo
                           mxd::keysrc_slots(ptrs, 3), nonce, stream, out1);
 }
 
+inline int ks_grid(int64_t items, int per_block = 256 / 6) {
+  int64_t b = (items + per_block - 1) / per_block;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(b, 8192));
+}
+
 int mxh_ks_level3_k(int words, const void* g0, const void* g1, const void* p0, const void* p1,
                     void* og0, void* og1, void* op0, void* op1, int64_t n, int d, int both,
                     const uint32_t* slots, uint64_t nonce, void* stream) {
@@ -707,11 +776,11 @@ int mxh_ks_level3_k(int words, const void* g0, const void* g1, const void* p0, c
   for (int i = 0; i < 3; ++i) ptrs[i] = slots + MX_KEY_SLOT_WORDS * i;
   KeySrc k = mxd::keysrc_slots(ptrs, 3);
   if (words == 1) {
-    hipLaunchKernelGGL(k_ks_level3<u64>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
+    hipLaunchKernelGGL(k_ks_level3<u64>, dim3(ks_grid(n)), dim3(kBlock), 0, S(stream),
                        (const u64*)g0, (const u64*)g1, (const u64*)p0, (const u64*)p1,
                        (u64*)og0, (u64*)og1, (u64*)op0, (u64*)op1, n, d, both, k, nonce);
   } else if (words == 2) {
-    hipLaunchKernelGGL(k_ks_level3<u128>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
+    hipLaunchKernelGGL(k_ks_level3<u128>, dim3(ks_grid(n)), dim3(kBlock), 0, S(stream),
                        (const u128*)g0, (const u128*)g1, (const u128*)p0, (const u128*)p1,
                        (u128*)og0, (u128*)og1, (u128*)op0, (u128*)op1, n, d, both, k, nonce);
   } else {

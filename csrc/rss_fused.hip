@@ -57,6 +57,60 @@ __global__ void __launch_bounds__(256) k_trunc_pr3(const T* __restrict__ s0, T* 
   }
 }
 
+// Latency variant (small n): the six keystream blocks of each of the block's EPB AES
+// blocks are computed one per thread into LDS; then EPB threads finish the elements.
+template <class T>
+__global__ void __launch_bounds__(256) k_trunc_pr3_lat(const T* __restrict__ s0, T* __restrict__ out0,
+                                                       T* __restrict__ out1, int64_t n, int m,
+                                                       mxd::KeySrc keys, uint64_t n_r0,
+                                                       uint64_t n_r1, uint64_t n_t, uint64_t n_m,
+                                                       uint64_t n_z0, uint64_t n_z2) {
+  constexpr int EPB = 256 / 6;
+  __shared__ uint32_t Tt[256];
+  __shared__ uint8_t Sb[256];
+  __shared__ uint32_t rks[2][44];
+  __shared__ uint64_t kl[6][EPB], kh[6][EPB];
+  mxd::stage_keys(rks, keys, 2);
+  mxd::stage_tables(Tt, Sb);
+  constexpr int P = mxd::Lane<T>::kPer;
+  const int64_t nb = (n + P - 1) / P;
+  const int tid = threadIdx.x, s = tid / EPB, lb = tid % EPB;
+  // stream s: (key, nonce) of r0, r1, t, m, z0, z2 -- as in k_trunc_pr3
+  const int key_of = (s == 1 || s == 5) ? 1 : 0;
+  const uint64_t nonce_of = s == 0 ? n_r0 : s == 1 ? n_r1 : s == 2 ? n_t : s == 3 ? n_m
+                            : s == 4 ? n_z0 : n_z2;
+  for (int64_t b0 = (int64_t)blockIdx.x * EPB; b0 < nb; b0 += (int64_t)gridDim.x * EPB) {
+    if (s < 6 && b0 + lb < nb) {
+      uint64_t lo, hi;
+      mxd::aes_ctr(rks[key_of], Tt, Sb, nonce_of, (uint64_t)(b0 + lb), &lo, &hi);
+      kl[s][lb] = lo;
+      kh[s][lb] = hi;
+    }
+    __syncthreads();
+    if (tid < EPB && b0 + tid < nb) {
+      const int64_t b = b0 + tid;
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const int64_t i = b * P + j;
+        if (i >= n) break;
+        const T z0 = mxd::pick<T>(kl[4][tid], kh[4][tid], j);
+        const T z2 = mxd::pick<T>(kl[5][tid], kh[5][tid], j);
+        const T z1 = mxf::trunc_pr_z1<T>(
+            s0[i], s0[n + i], s0[2 * n + i], mxd::pick<T>(kl[0][tid], kh[0][tid], j),
+            mxd::pick<T>(kl[1][tid], kh[1][tid], j), mxd::pick<T>(kl[2][tid], kh[2][tid], j),
+            mxd::pick<T>(kl[3][tid], kh[3][tid], j), z0, z2, m);
+        out0[i] = z0;
+        out0[n + i] = z1;
+        out0[2 * n + i] = z2;
+        out1[i] = z1;
+        out1[n + i] = z2;
+        out1[2 * n + i] = z0;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 template <class T>
 __global__ void __launch_bounds__(256) k_share3(int kind, const T* __restrict__ x, T* __restrict__ out0,
                          T* __restrict__ out1, int64_t n, int j0, mxd::KeySrc keys, uint64_t n1,
@@ -97,6 +151,20 @@ int launch_trunc_pr3(int words, const void* s0, void* out0, void* out1, int64_t 
                      const mxd::KeySrc& keys, const uint64_t* nn, void* stream) {
   if (n == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  const int64_t nblk = words == 1 ? (n + 1) / 2 : n;
+  if (nblk <= 8192 && (words == 1 || words == 2)) {  // latency-bound: one AES per thread
+    const unsigned g = (unsigned)((nblk + 41) / 42);
+    if (words == 1)
+      hipLaunchKernelGGL(k_trunc_pr3_lat<u64>, dim3(g), dim3(256), 0, st, (const u64*)s0,
+                         (u64*)out0, (u64*)out1, n, m, keys, nn[0], nn[1], nn[2], nn[3], nn[4],
+                         nn[5]);
+    else
+      hipLaunchKernelGGL(k_trunc_pr3_lat<u128>, dim3(g), dim3(256), 0, st, (const u128*)s0,
+                         (u128*)out0, (u128*)out1, n, m, keys, nn[0], nn[1], nn[2], nn[3],
+                         nn[4], nn[5]);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : -100 - (int)e;
+  }
   if (words == 1) {
     int64_t nb = (n + 1) / 2;
     hipLaunchKernelGGL(k_trunc_pr3<u64>, dim3(mxd::grid_for(nb)), dim3(256), 0, st,
