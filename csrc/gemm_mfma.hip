@@ -176,7 +176,7 @@ template <class T>
 __global__ void __launch_bounds__(256, Limbs<T>::L == 8 ? 2 : 1)
     k_gemm_limb(const int8_t* __restrict__ LA, const int8_t* __restrict__ LB,
                 T* __restrict__ C, int64_t M, int64_t N, int64_t Mp, int64_t Np, int64_t Kp,
-                int accumulate) {
+                int accumulate, int gM, int xcd) {
   constexpr int L = Limbs<T>::L;
   constexpr int STAGE = L * kTileBytes;  // bytes per operand per k-step
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
@@ -188,11 +188,11 @@ __global__ void __launch_bounds__(256, Limbs<T>::L == 8 ? 2 : 1)
   // XCD-contiguous tile ranges, walked in groups of kGroupM row bands so the ~32 blocks
   // co-resident on one XCD cover a 4 x 8 patch of output tiles: they share 4 A and 8 B
   // k-streams in that XCD's L2 instead of 1 A and 32 B streams.
-  const int64_t tid_flat = xcd_remap(blockIdx.x, ntiles);
-  const int64_t group = tid_flat / (kGroupM * tiles_n);
-  const int64_t first_m = group * kGroupM;
-  const int64_t gm = tiles_m - first_m < kGroupM ? tiles_m - first_m : kGroupM;
-  const int64_t in_group = tid_flat % (kGroupM * tiles_n);
+  const int64_t tid_flat = xcd ? xcd_remap(blockIdx.x, ntiles) : (int64_t)blockIdx.x;
+  const int64_t group = tid_flat / (gM * tiles_n);
+  const int64_t first_m = group * gM;
+  const int64_t gm = tiles_m - first_m < gM ? tiles_m - first_m : gM;
+  const int64_t in_group = tid_flat % (gM * tiles_n);
   const int64_t tm = first_m + in_group % gm, tn = in_group / gm;
   const int64_t b = blockIdx.y;
   const int64_t nkb = Kp / TK;
@@ -302,7 +302,7 @@ constexpr int kSplit = 10;
 __global__ void __launch_bounds__(512, 1)
     k_gemm_limb128_split(const int8_t* __restrict__ LA, const int8_t* __restrict__ LB,
                          u128* __restrict__ C, int64_t M, int64_t N, int64_t Mp, int64_t Np,
-                         int64_t Kp, int accumulate) {
+                         int64_t Kp, int accumulate, int gM, int xcd) {
   constexpr int L = 16;
   constexpr int STAGE = L * kTileBytes;
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
@@ -310,11 +310,11 @@ __global__ void __launch_bounds__(512, 1)
 
   const int64_t tiles_n = Np / TN, tiles_m = Mp / TM;
   const int64_t ntiles = tiles_n * tiles_m;
-  const int64_t tid_flat = xcd_remap(blockIdx.x, ntiles);
-  const int64_t group = tid_flat / (kGroupM * tiles_n);
-  const int64_t first_m = group * kGroupM;
-  const int64_t gm = tiles_m - first_m < kGroupM ? tiles_m - first_m : kGroupM;
-  const int64_t in_group = tid_flat % (kGroupM * tiles_n);
+  const int64_t tid_flat = xcd ? xcd_remap(blockIdx.x, ntiles) : (int64_t)blockIdx.x;
+  const int64_t group = tid_flat / (gM * tiles_n);
+  const int64_t first_m = group * gM;
+  const int64_t gm = tiles_m - first_m < gM ? tiles_m - first_m : gM;
+  const int64_t in_group = tid_flat % (gM * tiles_n);
   const int64_t tm = first_m + in_group % gm, tn = in_group / gm;
   const int64_t b = blockIdx.y;
   const int64_t nkb = Kp / TK;
@@ -421,6 +421,19 @@ __global__ void __launch_bounds__(512, 1)
 }
 
 // MOOSEX_GEMM_SPLIT=0 selects the one-wave-per-SIMD kernel for Z_2^128 (A/B testing)
+// Tile-order knobs (tuning experiments): MOOSEX_GEMM_GROUPM row bands per L2 group
+// (default kGroupM), MOOSEX_GEMM_XCD=0 disables the XCD-contiguous block remap.
+int gemm_group_m() {
+  const char* e = std::getenv("MOOSEX_GEMM_GROUPM");
+  int v = e ? std::atoi(e) : kGroupM;
+  return v >= 1 && v <= 64 ? v : kGroupM;
+}
+
+int gemm_xcd() {
+  const char* e = std::getenv("MOOSEX_GEMM_XCD");
+  return e && e[0] == '0' ? 0 : 1;
+}
+
 bool use_split_kernel() {
   static const bool on = [] {
     const char* e = std::getenv("MOOSEX_GEMM_SPLIT");
@@ -525,10 +538,11 @@ int run(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T* A1
       if (sizeof(T) == 16 && use_split_kernel()) {
         hipLaunchKernelGGL(k_gemm_limb128_split, dim3((unsigned)ntiles, (unsigned)batch),
                            dim3(512), lds, st, la, lb, (u128*)C, M, N, p.Mp, p.Np, p.Kp,
-                           accumulate);
+                           accumulate, gemm_group_m(), gemm_xcd());
       } else {
         hipLaunchKernelGGL(k_gemm_limb<T>, dim3((unsigned)ntiles, (unsigned)batch), dim3(256),
-                           lds, st, la, lb, C, M, N, p.Mp, p.Np, p.Kp, accumulate);
+                           lds, st, la, lb, C, M, N, p.Mp, p.Np, p.Kp, accumulate,
+                           gemm_group_m(), gemm_xcd());
       }
     }
     hipError_t e = hipGetLastError();

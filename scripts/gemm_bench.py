@@ -13,6 +13,8 @@ def main():
     ap.add_argument("--bits", type=int, default=128)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--peak", action="store_true", help="also run the MFMA peak probe")
+    ap.add_argument("--sweep", action="store_true",
+                    help="sweep the tile-order knobs (MOOSEX_GEMM_GROUPM / MOOSEX_GEMM_XCD)")
     a = ap.parse_args()
     if a.peak:
         mfma_peak()
@@ -30,6 +32,21 @@ def main():
     L = 16 if bits == 128 else 8
     ops = 2 * 3 * n * n * 2 * n * L * (L + 1) / 2
     print(f"n={n} bits={bits} {dt*1e3:.2f} ms/call  {ops/dt/1e15:.2f} int8 POPS")
+    if a.sweep:
+        import os
+
+        for xcd in ("1", "0"):
+            for gm in ("1", "2", "4", "8", "16"):
+                os.environ["MOOSEX_GEMM_GROUPM"], os.environ["MOOSEX_GEMM_XCD"] = gm, xcd
+                R.dot_cross(*xs, nb=1)
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                for _ in range(a.iters):
+                    R.dot_cross(*xs, nb=1)
+                torch.cuda.synchronize()
+                dt = (time.perf_counter() - t) / a.iters
+                print(f"  xcd={xcd} group_m={gm}: {dt*1e3:.2f} ms/call "
+                      f"{ops/dt/1e15:.2f} int8 POPS", flush=True)
 
 
 
