@@ -1,7 +1,7 @@
 // Device-side AES-128-CTR helpers shared by the gfx950 translation units.
 //
-// Each block stages the T0 table and S-box into LDS (1.25 KB) once; T1..T3 are byte
-// rotations of T0.  A keystream block yields one u128, two u64 or sixteen bits.
+// Each block stages the T0 table into LDS once (replicated for conflict-free lookups, see
+// kTTWords); T1..T3 are byte rotations of T0.  A keystream block yields one u128, two u64 or sixteen bits.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <string.h>
@@ -19,6 +19,38 @@ struct Keys4 {
   uint32_t rk[4][44];
 };
 
+// The T0 table is replicated 32 times in LDS, word i*32 + c for copy c: lane L of a
+// 32-lane ds_read_b32 group reads copy L & 31, so the 32 lanes of a group always hit 32
+// different banks ((a/4) mod 32 = c) -- random table lookups are bank-conflict free.
+// The S-box (last round) is byte 2 of T0.  32 KB of LDS per block.
+constexpr int kTTWords = 256 * 32;
+
+struct TRep {
+  const uint32_t* b;
+  int c;
+  __device__ uint32_t operator[](uint32_t i) const { return b[i * 32 + c]; }
+};
+struct SRep {
+  TRep t;
+  __device__ uint8_t operator[](uint32_t i) const { return (uint8_t)(t[i] >> 16); }
+};
+
+__device__ inline void stage_tables_rep(uint32_t* T) {
+  for (int i = threadIdx.x; i < kTTWords; i += blockDim.x) T[i] = mx::t0_entry(c_sbox[i >> 5]);
+  __syncthreads();
+}
+
+__device__ inline void aes_ctr_rep(const uint32_t* rk, const uint32_t* T, uint64_t nonce,
+                                   uint64_t ctr, uint64_t* lo, uint64_t* hi) {
+  uint32_t w[4], o[4];
+  mx::ctr_block_words(nonce, ctr, w);
+  const TRep tr{T, (int)(threadIdx.x & 31)};
+  mx::encrypt_block_tt(rk, tr, SRep{tr}, w[0], w[1], w[2], w[3], o);
+  mx::block_to_u64(o, lo, hi);
+}
+
+// Compact variant (1.25 KB: one T0 copy + S-box) for latency-bound launches that run one
+// AES per thread, where staging 32 KB would cost more than the bank conflicts.
 __device__ inline void stage_tables(uint32_t* T, uint8_t* Sb) {
   for (int i = threadIdx.x; i < 256; i += blockDim.x) {
     uint8_t s = c_sbox[i];

@@ -196,17 +196,18 @@ using mxd::pick;
 using mxd::RK;
 using mxd::stage_keys;
 using mxd::stage_tables;
+using mxd::stage_tables_rep;
+using mxd::aes_ctr_rep;
 
 __global__ void __launch_bounds__(256) k_prg(RK key, uint64_t nonce, uint64_t ctr0, uint8_t* __restrict__ out,
                       int64_t nbytes) {
-  __shared__ uint32_t T[256];
-  __shared__ uint8_t Sb[256];
-  stage_tables(T, Sb);
+  __shared__ uint32_t T[mxd::kTTWords];
+    stage_tables_rep(T);
   int64_t nblocks = (nbytes + 15) / 16;
   for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < nblocks;
        b += (int64_t)gridDim.x * blockDim.x) {
     uint64_t lo, hi;
-    aes_ctr(key.rk, T, Sb, nonce, ctr0 + b, &lo, &hi);
+    aes_ctr_rep(key.rk, T, nonce, ctr0 + b, &lo, &hi);
     if ((b + 1) * 16 <= nbytes) {
       uint64_t* o = (uint64_t*)(out + b * 16);
       o[0] = lo;
@@ -228,12 +229,11 @@ __global__ void __launch_bounds__(256) k_rss_cross(int kind, const T* __restrict
                             const T* __restrict__ y0, const T* __restrict__ y1,
                             T* __restrict__ out, int64_t n, int nparties, int has_keys,
                             KeySrc keys, uint64_t nonce) {
-  __shared__ uint32_t Tt[256];
-  __shared__ uint8_t Sb[256];
-  __shared__ uint32_t rks[4][44];
+  __shared__ uint32_t Tt[mxd::kTTWords];
+    __shared__ uint32_t rks[4][44];
   if (has_keys) {
     stage_keys(rks, keys, nparties + 1);
-    stage_tables(Tt, Sb);
+    stage_tables_rep(Tt);
   }
   constexpr int P = Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;  // keystream blocks per party
@@ -244,8 +244,8 @@ __global__ void __launch_bounds__(256) k_rss_cross(int kind, const T* __restrict
     const int64_t b = g % nb;
     uint64_t alo = 0, ahi = 0, blo = 0, bhi = 0;
     if (has_keys) {
-      aes_ctr(rks[p], Tt, Sb, nonce, (uint64_t)b, &alo, &ahi);
-      aes_ctr(rks[p + 1], Tt, Sb, nonce, (uint64_t)b, &blo, &bhi);
+      aes_ctr_rep(rks[p], Tt, nonce, (uint64_t)b, &alo, &ahi);
+      aes_ctr_rep(rks[p + 1], Tt, nonce, (uint64_t)b, &blo, &bhi);
     }
 #pragma unroll
     for (int j = 0; j < P; ++j) {
@@ -275,7 +275,7 @@ __global__ void __launch_bounds__(256) k_rss_cross_ring3(int kind, const T* __re
                                   KeySrc keys, uint64_t nonce) {
   __shared__ uint32_t Tt[256];
   __shared__ uint8_t Sb[256];
-  __shared__ uint32_t rks[3][44];
+    __shared__ uint32_t rks[3][44];
   stage_keys(rks, keys, 3);
   stage_tables(Tt, Sb);
   constexpr int P = Lane<T>::kPer;
@@ -431,11 +431,10 @@ __global__ void __launch_bounds__(256) k_rss_cross_ring3_lat(int kind, const T* 
 template <class T>
 __global__ void __launch_bounds__(256) k_prf_expand(T* __restrict__ out, int64_t n, int nkeys, KeySrc keys,
                              uint64_t nonce) {
-  __shared__ uint32_t Tt[256];
-  __shared__ uint8_t Sb[256];
-  __shared__ uint32_t rks[4][44];
+  __shared__ uint32_t Tt[mxd::kTTWords];
+    __shared__ uint32_t rks[4][44];
   stage_keys(rks, keys, nkeys);
-  stage_tables(Tt, Sb);
+  stage_tables_rep(Tt);
   constexpr int P = Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;
   const int64_t total = nb * nkeys;
@@ -444,7 +443,7 @@ __global__ void __launch_bounds__(256) k_prf_expand(T* __restrict__ out, int64_t
     const int p = (int)(g / nb);
     const int64_t b = g % nb;
     uint64_t lo, hi;
-    aes_ctr(rks[p], Tt, Sb, nonce, (uint64_t)b, &lo, &hi);
+    aes_ctr_rep(rks[p], Tt, nonce, (uint64_t)b, &lo, &hi);
 #pragma unroll
     for (int j = 0; j < P; ++j) {
       int64_t e = b * P + j;

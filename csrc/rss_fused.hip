@@ -20,11 +20,10 @@ template <class T>
 __global__ void __launch_bounds__(256) k_trunc_pr3(const T* __restrict__ s0, T* __restrict__ out0, T* __restrict__ out1,
                             int64_t n, int m, mxd::KeySrc keys, uint64_t n_r0, uint64_t n_r1,
                             uint64_t n_t, uint64_t n_m, uint64_t n_z0, uint64_t n_z2) {
-  __shared__ uint32_t Tt[256];
-  __shared__ uint8_t Sb[256];
-  __shared__ uint32_t rks[2][44];
+  __shared__ uint32_t Tt[mxd::kTTWords];
+    __shared__ uint32_t rks[2][44];
   mxd::stage_keys(rks, keys, 2);
-  mxd::stage_tables(Tt, Sb);
+  mxd::stage_tables_rep(Tt);
   constexpr int P = mxd::Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;
   const uint32_t* k0 = rks[0];
@@ -32,12 +31,12 @@ __global__ void __launch_bounds__(256) k_trunc_pr3(const T* __restrict__ s0, T* 
   for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < nb;
        b += (int64_t)gridDim.x * blockDim.x) {
     uint64_t r0l, r0h, r1l, r1h, tl, th, ml, mh, z0l, z0h, z2l, z2h;
-    mxd::aes_ctr(k0, Tt, Sb, n_r0, b, &r0l, &r0h);
-    mxd::aes_ctr(k2, Tt, Sb, n_r1, b, &r1l, &r1h);
-    mxd::aes_ctr(k0, Tt, Sb, n_t, b, &tl, &th);
-    mxd::aes_ctr(k0, Tt, Sb, n_m, b, &ml, &mh);
-    mxd::aes_ctr(k0, Tt, Sb, n_z0, b, &z0l, &z0h);
-    mxd::aes_ctr(k2, Tt, Sb, n_z2, b, &z2l, &z2h);
+    mxd::aes_ctr_rep(k0, Tt, n_r0, b, &r0l, &r0h);
+    mxd::aes_ctr_rep(k2, Tt, n_r1, b, &r1l, &r1h);
+    mxd::aes_ctr_rep(k0, Tt, n_t, b, &tl, &th);
+    mxd::aes_ctr_rep(k0, Tt, n_m, b, &ml, &mh);
+    mxd::aes_ctr_rep(k0, Tt, n_z0, b, &z0l, &z0h);
+    mxd::aes_ctr_rep(k2, Tt, n_z2, b, &z2l, &z2h);
 #pragma unroll
     for (int j = 0; j < P; ++j) {
       const int64_t i = b * P + j;
@@ -115,18 +114,17 @@ template <class T>
 __global__ void __launch_bounds__(256) k_share3(int kind, const T* __restrict__ x, T* __restrict__ out0,
                          T* __restrict__ out1, int64_t n, int j0, mxd::KeySrc keys, uint64_t n1,
                          uint64_t na) {
-  __shared__ uint32_t Tt[256];
-  __shared__ uint8_t Sb[256];
-  __shared__ uint32_t rks[2][44];
+  __shared__ uint32_t Tt[mxd::kTTWords];
+    __shared__ uint32_t rks[2][44];
   mxd::stage_keys(rks, keys, 2);
-  mxd::stage_tables(Tt, Sb);
+  mxd::stage_tables_rep(Tt);
   constexpr int P = mxd::Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;
   for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < nb;
        b += (int64_t)gridDim.x * blockDim.x) {
     uint64_t al, ah, bl, bh;
-    mxd::aes_ctr(rks[0], Tt, Sb, n1, b, &al, &ah);
-    mxd::aes_ctr(rks[1], Tt, Sb, na, b, &bl, &bh);
+    mxd::aes_ctr_rep(rks[0], Tt, n1, b, &al, &ah);
+    mxd::aes_ctr_rep(rks[1], Tt, na, b, &bl, &bh);
 #pragma unroll
     for (int j = 0; j < P; ++j) {
       const int64_t i = b * P + j;
