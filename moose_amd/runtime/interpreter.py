@@ -49,7 +49,7 @@ _REP_DIALECT = {
     "Share": None, "TruncPr": None,
     "Msb": rep.msb, "BitDecompose": rep.bit_decompose, "EqualZero": rep.equal_zero,
     "Xor": rep.xor, "And": rep.and_, "Shl": rep.shl, "BitExtract": rep.bit_extract,
-    "RingInject": rep.b2a,
+    "RingInject": rep.b2a, "Equal": rep.equal, "Index": rep.bit_extract,
 }
 
 
@@ -197,6 +197,8 @@ class Interpreter:
             t = fn(sess, ts[0], int(attrs["amount"]))
         elif kind == "BitExtract":
             t = fn(sess, ts[0], int(attrs["bit_idx"]))
+        elif kind == "Index":  # bit i of a replicated bit array (packed words here)
+            t = fn(sess, ts[0], int(attrs["index"]))
         elif kind == "RingInject":
             t = rep.shl(sess, fn(sess, ts[0], int(attrs.get("ring_bits", 0)) or
                                  (128 if "128" in op.sig.ret.name else 64)),
@@ -375,6 +377,32 @@ class Interpreter:
 
     def op_Reveal(self, op, ins):
         return self.to_host(ins[0], op.placement.owner)
+
+    # mirrored / fixed-point dialect conversions (reference kernels/conversion.rs)
+    def op_Mirror(self, op, ins):
+        return self.to_mir(ins[0], op.placement)
+
+    def op_Demirror(self, op, ins):
+        return self.to_host(ins[0], op.placement.owner)
+
+    def op_FixedpointEncode(self, op, ins):
+        kind = "Fixed64" if "64" in op.sig.ret.name else "Fixed128"
+        if self.fixed_ring == 64:
+            kind = "Fixed64"
+        d = T.TensorDType(kind, int(op.attrs.get("integral_precision", 0)),
+                          int(op.attrs["fractional_precision"]))
+        return self.at(op, self._cast_host(self.to_host(ins[0], _owners(op.placement)[0]), d))
+
+    def op_FixedpointDecode(self, op, ins):
+        want = T.FLOAT32 if "32" in op.sig.ret.name else T.FLOAT64
+        return self.at(op, self._cast_host(self.to_host(ins[0], _owners(op.placement)[0]), want))
+
+    def op_Pow2(self, op, ins):
+        plc = op.placement
+        x = self.to_rep(ins[0], plc) if isinstance(plc, ReplicatedPlacement) else ins[0]
+        if not (x.is_rep and isinstance(x.v, RepFixed)):
+            raise MooseRuntimeError("Pow2 is defined on replicated fixed-point tensors")
+        return LV(plc, "tensor", x.dtype, fxp.exp2(self.sess, x.v))
 
     def op_Input(self, op, ins):
         name = op.attrs.get("arg_name") or op.name

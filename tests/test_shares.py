@@ -193,3 +193,33 @@ o2 = Output{{tag = "m"}}: (HostBitTensor) -> HostBitTensor (mr) @Host(carole)
     want = [200 * 8, 400 * 8, -50 * 8]
     assert all(abs(a - b) <= 8 for a, b in zip(t, want)), t
     assert [int(v) for v in np.asarray(out["m"]).reshape(-1)] == [0, 0, 1]
+
+
+def test_dialect_equal_pow2_mirror_encode():
+    """More dialect-level operators reachable from textual computations: Equal / Index on
+    replicated rings, Pow2 on a replicated fixed-point tensor, Mirror/Demirror, and
+    FixedpointEncode/Decode on a host."""
+    plc = "@Replicated(alice, bob, carole)"
+    src = f"""
+a = Constant{{value = HostRing64Tensor([5, 7, 9])}}: () -> HostRing64Tensor @Host(alice)
+b = Constant{{value = HostRing64Tensor([5, 8, 9])}}: () -> HostRing64Tensor @Host(bob)
+ra = Share: (HostRing64Tensor) -> ReplicatedRing64Tensor (a) {plc}
+rb = Share: (HostRing64Tensor) -> ReplicatedRing64Tensor (b) {plc}
+eq = Equal: (ReplicatedRing64Tensor, ReplicatedRing64Tensor) -> ReplicatedBitTensor (ra, rb) {plc}
+eqo = Reveal: (ReplicatedBitTensor) -> HostBitTensor (eq) @Host(carole)
+x = Constant{{value = HostFloat64Tensor([0.5, -1.25, 2.0])}}: () -> HostFloat64Tensor @Host(alice)
+xf = FixedpointEncode{{fractional_precision = 23, integral_precision = 14}}: (HostFloat64Tensor) -> HostFixed128Tensor (x) @Host(alice)
+p = Pow2: (Tensor<Fixed128(14, 23)>) -> Tensor<Fixed128(14, 23)> (xf) {plc}
+po = FixedpointDecode{{fractional_precision = 23}}: (HostFixed128Tensor) -> HostFloat64Tensor (p) @Host(carole)
+m = Mirror: (HostFloat64Tensor) -> Mirrored3Float64 (x) @Mirrored3(alice, bob, carole)
+md = Demirror: (Mirrored3Float64) -> HostFloat64Tensor (m) @Host(bob)
+o1 = Output{{tag = "eq"}}: (HostBitTensor) -> HostBitTensor (eqo) @Host(carole)
+o2 = Output{{tag = "pow2"}}: (HostFloat64Tensor) -> HostFloat64Tensor (po) @Host(carole)
+o3 = Output{{tag = "mir"}}: (HostFloat64Tensor) -> HostFloat64Tensor (md) @Host(bob)
+"""
+    comp = Computation.from_textual(src)
+    out = LocalMooseRuntime(ROLES, device="cpu").evaluate_computation(comp, {})
+    assert [int(v) for v in np.asarray(out["eq"]).reshape(-1)] == [1, 0, 1]
+    np.testing.assert_allclose(np.asarray(out["pow2"], dtype=np.float64),
+                               2.0 ** np.array([0.5, -1.25, 2.0]), atol=1e-3)
+    np.testing.assert_allclose(np.asarray(out["mir"], dtype=np.float64), [0.5, -1.25, 2.0])
