@@ -135,6 +135,12 @@ int mx_rss_mul3_k(int dev, int kind, int words, const void* x0, const void* x1, 
 int mx_ks_level3_k(int dev, int words, const void* g0, const void* g1, const void* p0,
                    const void* p1, void* og0, void* og1, void* op0, void* op1, int64_t n,
                    int d, int both, const uint32_t* slots, uint64_t nonce, void* stream);
+// One party's share of a Kogge-Stone level (SPMD: one process per party), before the
+// reshare: z[e] = pk AND (g << d) cross terms ^ PRF(k0)[e] ^ PRF(k1)[e]; if both, also
+// z[n + e] for pk AND (pk << d).  keys16 = (k_p, k_{p+1}); z has (both ? 2n : n) words.
+int mx_ks_cross1(int dev, int words, const void* g0, const void* g1, const void* p0,
+                 const void* p1, void* z, int64_t n, int d, int both, const uint8_t* keys16,
+                 uint64_t nonce, void* stream);
 // mx_prf_expand with nkeys consecutive key slots
 int mx_prf_expand_k(int dev, int words, void* out, int64_t n, int nkeys, const uint32_t* slots,
                     uint64_t nonce, void* stream);

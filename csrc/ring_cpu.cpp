@@ -581,6 +581,32 @@ int mx_rss_mul3_k(int dev, int kind, int words, const void* x0, const void* x1, 
   return 0;
 }
 
+int mx_ks_cross1(int dev, int words, const void* g0, const void* g1, const void* p0,
+                 const void* p1, void* z, int64_t n, int d, int both, const uint8_t* keys16,
+                 uint64_t nonce, void* stream) {
+  if (dev) return mxh_ks_cross1(words, g0, g1, p0, p1, z, n, d, both, keys16, nonce, stream);
+  if (words != 1 && words != 2) return -2;
+  DISPATCH_WORDS(words, T, {
+    const int64_t m = both ? 2 * n : n;
+    std::vector<T> r0(m), r1(m);
+    mx_cpu_prf_range(keys16, nonce, words, 0, m, r0.data());
+    mx_cpu_prf_range(keys16 + 16, nonce, words, 0, m, r1.data());
+    const T *G0 = (const T*)g0, *G1 = (const T*)g1, *A0 = (const T*)p0, *A1 = (const T*)p1;
+    T* Z = (T*)z;
+    parallel_for(n, 4096, [&](int64_t lo, int64_t hi) {
+      for (int64_t e = lo; e < hi; ++e) {
+        const T s0 = G0[e] << d, s1 = G1[e] << d;
+        Z[e] = (A0[e] & s0) ^ (A0[e] & s1) ^ (A1[e] & s0) ^ r0[e] ^ r1[e];
+        if (both) {
+          const T u0 = A0[e] << d, u1 = A1[e] << d;
+          Z[n + e] = (A0[e] & u0) ^ (A0[e] & u1) ^ (A1[e] & u0) ^ r0[n + e] ^ r1[n + e];
+        }
+      }
+    });
+    return 0;
+  });
+}
+
 int mx_ks_level3_k(int dev, int words, const void* g0, const void* g1, const void* p0,
                    const void* p1, void* og0, void* og1, void* op0, void* op1, int64_t n,
                    int d, int both, const uint32_t* slots, uint64_t nonce, void* stream) {

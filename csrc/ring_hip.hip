@@ -372,6 +372,38 @@ __global__ void __launch_bounds__(256) k_ks_level3(const T* __restrict__ g0, con
   }
 }
 
+// One party's cross terms of a Kogge-Stone level (mx_ks_cross1): thread per element.
+template <class T>
+__global__ void __launch_bounds__(256) k_ks_cross1(const T* __restrict__ g0, const T* __restrict__ g1,
+                                                   const T* __restrict__ p0, const T* __restrict__ p1,
+                                                   T* __restrict__ z, int64_t n, int d, int both,
+                                                   KeySrc keys, uint64_t nonce) {
+  __shared__ uint32_t Tt[256];
+  __shared__ uint8_t Sb[256];
+  __shared__ uint32_t rks[2][44];
+  stage_keys(rks, keys, 2);
+  stage_tables(Tt, Sb);
+  constexpr int P = Lane<T>::kPer;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t l0, h0, l1, h1;
+    aes_ctr(rks[0], Tt, Sb, nonce, (uint64_t)(e / P), &l0, &h0);
+    aes_ctr(rks[1], Tt, Sb, nonce, (uint64_t)(e / P), &l1, &h1);
+    const T a0 = p0[e], a1 = p1[e];
+    const T s0 = g0[e] << d, s1 = g1[e] << d;
+    z[e] = (a0 & s0) ^ (a0 & s1) ^ (a1 & s0) ^ pick<T>(l0, h0, (int)(e % P)) ^
+           pick<T>(l1, h1, (int)(e % P));
+    if (both) {
+      const int64_t c = n + e;
+      aes_ctr(rks[0], Tt, Sb, nonce, (uint64_t)(c / P), &l0, &h0);
+      aes_ctr(rks[1], Tt, Sb, nonce, (uint64_t)(c / P), &l1, &h1);
+      const T u0 = a0 << d, u1 = a1 << d;
+      z[c] = (a0 & u0) ^ (a0 & u1) ^ (a1 & u0) ^ pick<T>(l0, h0, (int)(c % P)) ^
+             pick<T>(l1, h1, (int)(c % P));
+    }
+  }
+}
+
 // Latency variant for small launches (few keystream blocks): the block's 3 x EPB AES
 // blocks are computed one per thread into LDS, then EPB threads finish the elements --
 // one AES on the critical path instead of three.
@@ -760,6 +792,26 @@ int mxh_rss_mul3_k(int kind, int words, const void* x0, const void* x1, const vo
   for (int i = 0; i < 3; ++i) ptrs[i] = slots + MX_KEY_SLOT_WORDS * i;
   return launch_rss_cross(kind, words, x0, x1, y0, y1, out0, n, 3, true, true,
                           mxd::keysrc_slots(ptrs, 3), nonce, stream, out1);
+}
+
+int mxh_ks_cross1(int words, const void* g0, const void* g1, const void* p0, const void* p1,
+                  void* z, int64_t n, int d, int both, const uint8_t* keys16, uint64_t nonce,
+                  void* stream) {
+  if (n == 0) return 0;
+  KeySrc k = mxd::keysrc_host(keys16, 2);
+  if (words == 1) {
+    hipLaunchKernelGGL(k_ks_cross1<u64>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
+                       (const u64*)g0, (const u64*)g1, (const u64*)p0, (const u64*)p1, (u64*)z,
+                       n, d, both, k, nonce);
+  } else if (words == 2) {
+    hipLaunchKernelGGL(k_ks_cross1<u128>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
+                       (const u128*)g0, (const u128*)g1, (const u128*)p0, (const u128*)p1,
+                       (u128*)z, n, d, both, k, nonce);
+  } else {
+    return -2;
+  }
+  MX_LAUNCH_CHECK();
+  return 0;
 }
 
 inline int ks_grid(int64_t items, int per_block = 256 / 6) {

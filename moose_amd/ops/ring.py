@@ -782,6 +782,25 @@ def rss_mul3_k(kind: str, x0: RT, x1: RT, y0: RT, y1: RT, slot_ptr: int, nonce: 
     return out0, out1
 
 
+def ks_cross1(g0: RT, g1: RT, p0: RT, p1: RT, d: int, both: bool, keys, nonce: int) -> RT:
+    """One party's masked cross terms of a Kogge-Stone level (mx_ks_cross1): shape
+    ``[2, *shape]`` (t, pk') if ``both`` else ``shape``; ``keys`` = (k_p, k_{p+1})."""
+    bits = g0.bits
+    shp = g0.shape
+    datas = [x.data.contiguous() for x in (g0, g1, p0, p1)]
+    n = math.prod(shp)
+    z = empty(((2,) + tuple(shp)) if both else tuple(shp), bits, g0.device)
+    kbuf = nat.key_buffer(list(keys))
+    nat.check(
+        nat.lib().mx_ks_cross1(
+            nat.dev_of(z.data), _words(bits), *[nat.ptr(x) for x in datas], nat.ptr(z.data),
+            n, int(d), 1 if both else 0, kbuf, nonce & MASK64, nat.stream_of(z.data),
+        ),
+        "ks_cross1",
+    )
+    return z
+
+
 def ks_level3_k(g0: RT, g1: RT, p0: RT, p1: RT, d: int, both: bool, slot_ptr: int,
                 nonce: int):
     """One fused Kogge-Stone level for three stacked parties (mx_ks_level3_k): returns

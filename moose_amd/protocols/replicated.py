@@ -325,7 +325,8 @@ def binary_adder(sess, a: RepTensor, b: RepTensor) -> RepTensor:
     g = and_(sess, a, b)
     pk = p
     d = 1
-    level = getattr(sess, "p_ks_level", None) if getattr(sess, "fused", False) else None
+    fused = getattr(sess, "fused", False) or getattr(sess, "ks_fused", False)
+    level = getattr(sess, "p_ks_level", None) if fused else None
     if level is not None and bits in (64, 128):
         # stacked session: each level (shifts, both ANDs, reshare, xor) is one kernel
         while d < bits:

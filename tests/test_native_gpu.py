@@ -148,3 +148,14 @@ def test_fused_protocol_kernels_match_host(bits):
                                       B.s0.v.data, B.s1.v.data)])
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+@pytest.mark.parametrize("both", [True, False])
+def test_ks_cross1_matches_host(bits, both):
+    """SPMD per-party Kogge-Stone level kernel (k_ks_cross1): GPU == CPU bitwise."""
+    xs = [rand_rt((3, 37), bits, 60 + i) for i in range(4)]
+    keys = (bytes(range(16)), bytes(range(16, 32)))
+    cpu = R.ks_cross1(*xs, 3, both, keys, 11)
+    dev = R.ks_cross1(*[gpu(x) for x in xs], 3, both, keys, 11)
+    same(cpu, dev)

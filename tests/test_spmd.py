@@ -102,7 +102,9 @@ def _shares_worker(rank, port, q):
         Y = rep.trunc_pr(s, rep.mul(s, X, X), 23)
         D = rep.dot(s, rep.local(s, X, "Reshape", shape=(1, 257)),
                     rep.local(s, X, "Reshape", shape=(257, 1)))
-        out[bits] = [t.s0.v.data.clone() for t in (X, Y, D)] + [t.s1.v.data.clone() for t in (X, Y, D)]
+        B = rep.bit_decompose(s, X)  # per-party fused Kogge-Stone levels (SPMD p_ks_level)
+        out[bits] = ([t.s0.v.data.clone() for t in (X, Y, D, B)]
+                     + [t.s1.v.data.clone() for t in (X, Y, D, B)])
     q.put((rank, {b: [t.numpy() for t in v] for b, v in out.items()}))
     dist.barrier()
     dist.destroy_process_group()
@@ -138,7 +140,8 @@ def test_spmd_shares_bitwise_equal_stacked():
         Y = rep.trunc_pr(s, rep.mul(s, X, X), 23)
         D = rep.dot(s, rep.local(s, X, "Reshape", shape=(1, 257)),
                     rep.local(s, X, "Reshape", shape=(257, 1)))
-        stacked = [t.s0.v.data for t in (X, Y, D)] + [t.s1.v.data for t in (X, Y, D)]
+        B = rep.bit_decompose(s, X)  # generic per-step protocol (fused=False)
+        stacked = [t.s0.v.data for t in (X, Y, D, B)] + [t.s1.v.data for t in (X, Y, D, B)]
         for i, st in enumerate(stacked):
             for p in range(3):
                 assert np.array_equal(res[p][bits][i], st[p].numpy()), (bits, i, p)
