@@ -269,7 +269,9 @@ __global__ void __launch_bounds__(256) k_rss_cross(int kind, const T* __restrict
 // keystream block evaluates the three AES blocks once and finishes all three parties'
 // elements: 3 AES per block instead of 6 (the shares are identical to k_rss_cross).
 template <class T>
-__global__ void __launch_bounds__(256) k_rss_cross_ring3(int kind, const T* __restrict__ x0, const T* __restrict__ x1,
+// default launch bounds on purpose: at 128 VGPRs it spills a little but runs more waves,
+// which is faster for the large launches it serves (small ones use k_rss_cross_ring3_lat)
+__global__ void k_rss_cross_ring3(int kind, const T* __restrict__ x0, const T* __restrict__ x1,
                                   const T* __restrict__ y0, const T* __restrict__ y1,
                                   T* __restrict__ out, T* __restrict__ out1, int64_t n,
                                   KeySrc keys, uint64_t nonce) {
