@@ -43,6 +43,18 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 
 namespace {
 
+// MX_SETPRIO=1: raise the wave priority for the MFMA section of each k-step (tuning knob)
+#ifndef MX_SETPRIO
+#define MX_SETPRIO 0
+#endif
+#if MX_SETPRIO
+#define MX_PRIO_HI() __builtin_amdgcn_s_setprio(1)
+#define MX_PRIO_LO() __builtin_amdgcn_s_setprio(0)
+#else
+#define MX_PRIO_HI() ((void)0)
+#define MX_PRIO_LO() ((void)0)
+#endif
+
 constexpr int TM = 64;  // rows of the block tile (A side)
 constexpr int TN = 64;  // cols of the block tile (B side)
 constexpr int TK = 32;  // limb-bytes per k-step (one MFMA K)
@@ -363,6 +375,7 @@ __global__ void __launch_bounds__(512, 1)
       v4i bf[NLO];
 #pragma unroll
       for (int j = 0; j < NLO; ++j) bf[j] = *(const v4i*)(Bs + j * kTileBytes + boff);
+      MX_PRIO_HI();
 #pragma unroll
       for (int i = 0; i < NLO; ++i) {
         const v4i a = *(const v4i*)(As + i * kTileBytes + aoff);
@@ -374,6 +387,7 @@ __global__ void __launch_bounds__(512, 1)
       v4i bf[L];
 #pragma unroll
       for (int j = 0; j < L; ++j) bf[j] = *(const v4i*)(Bs + j * kTileBytes + boff);
+      MX_PRIO_HI();
 #pragma unroll
       for (int i = 0; i < L; ++i) {
         const v4i a = *(const v4i*)(As + i * kTileBytes + aoff);
@@ -383,6 +397,7 @@ __global__ void __launch_bounds__(512, 1)
               __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bf[j], acc[i + j - kSplit], 0, 0, 0);
       }
     }
+    MX_PRIO_LO();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (kb + 2 < nkb) issue_stage(kb + 2, buf(cur));

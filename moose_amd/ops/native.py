@@ -106,7 +106,7 @@ def lib():
             return _LIB
         if _build.needs_build() and os.environ.get("MOOSEX_NO_BUILD") != "1":
             _build.build()
-        path = str(_build.LIB)
+        path = os.environ.get("MOOSEX_LIB") or str(_build.LIB)  # tuning variants
         try:
             handle = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
         except OSError as e:
