@@ -32,6 +32,10 @@ int mx_device_count(void);
 // out[i] = a[i] op b[i]; na, nb in {n, 1} (scalar broadcast)
 int mx_ew_binary(int dev, int op, int words, const void* a, int64_t na, const void* b,
                  int64_t nb, void* out, int64_t n, void* stream);
+// Stacked party vectors a[nparties, m]: out[p, i] = p == which ? a[p, i] op b[i % nb]
+// : a[p, i] (a public operand applied to one party's share slot, in one pass); nb in {m, 1}
+int mx_ew_binary_slot(int dev, int op, int words, const void* a, const void* b, int64_t nb,
+                      void* out, int64_t m, int nparties, int which, void* stream);
 // out[i] = op(a[i], param)
 int mx_ew_unary(int dev, int op, int words, const void* a, void* out, int64_t n,
                 int64_t param, void* stream);

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstring>
 #include <functional>
 #include <thread>
 #include <vector>
@@ -337,6 +338,23 @@ int mx_ew_binary(int dev, int op, int words, const void* a, int64_t na, const vo
   if (dev) return mxh_ew_binary(op, words, a, na, b, nb, out, n, stream);
   DISPATCH_WORDS(words, T,
                  return binary_t<T>(op, (const T*)a, na, (const T*)b, nb, (T*)out, n));
+}
+
+int mx_ew_binary_slot(int dev, int op, int words, const void* a, const void* b, int64_t nb,
+                      void* out, int64_t m, int nparties, int which, void* stream) {
+  if (dev) return mxh_ew_binary_slot(op, words, a, b, nb, out, m, nparties, which, stream);
+  DISPATCH_WORDS(words, T, {
+    const T *A = (const T*)a, *B = (const T*)b;
+    T* O = (T*)out;
+    for (int p = 0; p < nparties; ++p) {
+      if (p == which) {
+        binary_t<T>(op, A + p * m, m, B, nb, O + p * m, m);
+      } else if (O != A) {
+        std::memcpy(O + p * m, A + p * m, sizeof(T) * m);
+      }
+    }
+    return 0;
+  });
 }
 
 int mx_ew_unary(int dev, int op, int words, const void* a, void* out, int64_t n,

@@ -50,6 +50,19 @@ __global__ void __launch_bounds__(256) k_binary(int op, const T* __restrict__ a,
 }
 
 template <class T>
+__global__ void __launch_bounds__(256) k_binary_slot(int op, const T* __restrict__ a,
+                                                     const T* __restrict__ b, int64_t nb,
+                                                     T* __restrict__ out, int64_t m, int np,
+                                                     int which) {
+  const int64_t n = m * np;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < n;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = g / m, i = g - p * m;
+    out[g] = p == which ? mxr::binop<T>(op, a[g], b[nb == 1 ? 0 : i]) : a[g];
+  }
+}
+
+template <class T>
 __global__ void __launch_bounds__(256) k_unary(int op, const T* __restrict__ a, T* __restrict__ out, int64_t n, int k) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -573,6 +586,18 @@ int mxh_ew_binary(int op, int words, const void* a, int64_t na, const void* b, i
   DEV_DISPATCH(words, T, {
     hipLaunchKernelGGL(k_binary<T>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream), op,
                        (const T*)a, na, (const T*)b, nb, (T*)out, n);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mxh_ew_binary_slot(int op, int words, const void* a, const void* b, int64_t nb, void* out,
+                       int64_t m, int nparties, int which, void* stream) {
+  if (m == 0) return 0;
+  DEV_DISPATCH(words, T, {
+    hipLaunchKernelGGL(k_binary_slot<T>, dim3(grid_for(m * nparties)), dim3(kBlock), 0,
+                       S(stream), op, (const T*)a, (const T*)b, nb, (T*)out, m, nparties,
+                       which);
     MX_LAUNCH_CHECK();
     return 0;
   });

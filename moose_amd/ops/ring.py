@@ -782,6 +782,28 @@ def rss_mul3_k(kind: str, x0: RT, x1: RT, y0: RT, y1: RT, slot_ptr: int, nonce: 
     return out0, out1
 
 
+def binary_slot(op: str, a: RT, b: RT, which: int):
+    """Stacked [nparties, *shape] ``a``: ``op`` with public ``b`` (same shape as one slot,
+    or a scalar) applied to slot ``which`` only, one kernel (mx_ew_binary_slot)."""
+    np_, m = a.shape[0], math.prod(a.shape[1:])
+    nb = b.numel()
+    if nb not in (1, m):
+        raise ValueError("binary_slot: operand must be a scalar or one slot's shape")
+    ad = a.data.contiguous()
+    bd = b.data.contiguous()
+    if bd.device != ad.device:
+        bd = bd.to(ad.device)
+    out = empty(a.shape, a.bits, a.device)
+    nat.check(
+        nat.lib().mx_ew_binary_slot(
+            nat.dev_of(ad), _BIN[op], _words(a.bits), nat.ptr(ad), nat.ptr(bd), nb,
+            nat.ptr(out.data), m, np_, int(which), nat.stream_of(ad),
+        ),
+        "binary_slot",
+    )
+    return out
+
+
 def ks_cross1(g0: RT, g1: RT, p0: RT, p1: RT, d: int, both: bool, keys, nonce: int) -> RT:
     """One party's masked cross terms of a Kogge-Stone level (mx_ks_cross1): shape
     ``[2, *shape]`` (t, pk') if ``both`` else ``shape``; ``keys`` = (k_p, k_{p+1})."""

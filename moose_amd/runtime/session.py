@@ -226,6 +226,11 @@ class StackedSession(Session):
     def p_apply_at(self, prim, plc, x, which, c):
         """Apply ``prim(component, c)`` on party ``which`` only."""
         v = x.v
+        op = {"Add": "add", "Sub": "sub", "Xor": "xor", "And": "and", "Mul": "mul"}.get(prim)
+        if op is not None and isinstance(c, R.RT) and c.bits == v.bits and v.bits in (1, 64, 128):
+            m = math.prod(v.shape[1:])
+            if c.numel() in (1, m) and (c.numel() == 1 or tuple(c.shape) == tuple(v.shape[1:])):
+                return PV(plc, R.binary_slot(op, v, c, which))  # one kernel
         part = PRIMS[prim].impl(0, R.RT(v.data[which], v.bits), c)
         d = v.data.clone() if part.data.shape == v.data.shape[1:] else None
         if d is None:  # broadcasting changed the shape

@@ -159,3 +159,12 @@ def test_ks_cross1_matches_host(bits, both):
     cpu = R.ks_cross1(*xs, 3, both, keys, 11)
     dev = R.ks_cross1(*[gpu(x) for x in xs], 3, both, keys, 11)
     same(cpu, dev)
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+def test_binary_slot_matches_host(bits):
+    """Public operand on one share slot in one kernel (k_binary_slot): GPU == CPU."""
+    a = rand_rt((3, 5, 7), bits, 70)
+    for b in (rand_rt((5, 7), bits, 71), rand_rt((), bits, 72)):
+        for which in (0, 2):
+            same(R.binary_slot("add", a, b, which), R.binary_slot("add", gpu(a), gpu(b), which))
