@@ -36,6 +36,10 @@ int mx_ew_binary(int dev, int op, int words, const void* a, int64_t na, const vo
 // : a[p, i] (a public operand applied to one party's share slot, in one pass); nb in {m, 1}
 int mx_ew_binary_slot(int dev, int op, int words, const void* a, const void* b, int64_t nb,
                       void* out, int64_t m, int nparties, int which, void* stream);
+// Zero share from precomputed keystreams + reshare, three stacked parties (arith):
+// out0[p, i] = v[p, i] + r[p, i] - r[p+1, i] ; out1[p, i] = out0[p+1, i]
+int mx_add_zs3(int dev, int words, const void* v, const void* r, void* out0, void* out1,
+               int64_t n, void* stream);
 // out[i] = op(a[i], param)
 int mx_ew_unary(int dev, int op, int words, const void* a, void* out, int64_t n,
                 int64_t param, void* stream);

@@ -189,6 +189,8 @@ int mxh_rss_mul3_k(int kind, int words, const void* x0, const void* x1, const vo
                    uint64_t nonce, void* stream);
 int mxh_ew_binary_slot(int op, int words, const void* a, const void* b, int64_t nb, void* out,
                        int64_t m, int nparties, int which, void* stream);
+int mxh_add_zs3(int words, const void* v, const void* r, void* out0, void* out1, int64_t n,
+                void* stream);
 int mxh_ks_cross1(int words, const void* g0, const void* g1, const void* p0, const void* p1,
                   void* z, int64_t n, int d, int both, const uint8_t* keys16, uint64_t nonce,
                   void* stream);

@@ -340,6 +340,24 @@ int mx_ew_binary(int dev, int op, int words, const void* a, int64_t na, const vo
                  return binary_t<T>(op, (const T*)a, na, (const T*)b, nb, (T*)out, n));
 }
 
+int mx_add_zs3(int dev, int words, const void* v, const void* r, void* out0, void* out1,
+               int64_t n, void* stream) {
+  if (dev) return mxh_add_zs3(words, v, r, out0, out1, n, stream);
+  DISPATCH_WORDS(words, T, {
+    const T *V = (const T*)v, *Rr = (const T*)r;
+    T *O0 = (T*)out0, *O1 = (T*)out1;
+    parallel_for(n, 1 << 14, [&](int64_t lo, int64_t hi) {
+      for (int64_t e = lo; e < hi; ++e) {
+        const T z0 = V[e] + Rr[e] - Rr[n + e], z1 = V[n + e] + Rr[n + e] - Rr[2 * n + e],
+                z2 = V[2 * n + e] + Rr[2 * n + e] - Rr[e];
+        O0[e] = z0; O0[n + e] = z1; O0[2 * n + e] = z2;
+        O1[e] = z1; O1[n + e] = z2; O1[2 * n + e] = z0;
+      }
+    });
+    return 0;
+  });
+}
+
 int mx_ew_binary_slot(int dev, int op, int words, const void* a, const void* b, int64_t nb,
                       void* out, int64_t m, int nparties, int which, void* stream) {
   if (dev) return mxh_ew_binary_slot(op, words, a, b, nb, out, m, nparties, which, stream);

@@ -63,6 +63,23 @@ __global__ void __launch_bounds__(256) k_binary_slot(int op, const T* __restrict
 }
 
 template <class T>
+__global__ void __launch_bounds__(256) k_add_zs3(const T* __restrict__ v, const T* __restrict__ r,
+                                                 T* __restrict__ out0, T* __restrict__ out1,
+                                                 int64_t n) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const T r0 = r[e], r1 = r[n + e], r2 = r[2 * n + e];
+    const T z0 = v[e] + r0 - r1, z1 = v[n + e] + r1 - r2, z2 = v[2 * n + e] + r2 - r0;
+    out0[e] = z0;
+    out0[n + e] = z1;
+    out0[2 * n + e] = z2;
+    out1[e] = z1;
+    out1[n + e] = z2;
+    out1[2 * n + e] = z0;
+  }
+}
+
+template <class T>
 __global__ void __launch_bounds__(256) k_unary(int op, const T* __restrict__ a, T* __restrict__ out, int64_t n, int k) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -586,6 +603,17 @@ int mxh_ew_binary(int op, int words, const void* a, int64_t na, const void* b, i
   DEV_DISPATCH(words, T, {
     hipLaunchKernelGGL(k_binary<T>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream), op,
                        (const T*)a, na, (const T*)b, nb, (T*)out, n);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mxh_add_zs3(int words, const void* v, const void* r, void* out0, void* out1, int64_t n,
+                void* stream) {
+  if (n == 0) return 0;
+  DEV_DISPATCH(words, T, {
+    hipLaunchKernelGGL(k_add_zs3<T>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
+                       (const T*)v, (const T*)r, (T*)out0, (T*)out1, n);
     MX_LAUNCH_CHECK();
     return 0;
   });

@@ -66,6 +66,7 @@ _SIGS = {
          c_vp],
     ),
     "mx_prf_expand_k": (c_int, [c_int, c_int, c_vp, c_i64, c_int, c_vp, c_u64, c_vp]),
+    "mx_add_zs3": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "mx_ew_binary_slot": (
         c_int, [c_int, c_int, c_int, c_vp, c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_vp]),
     "mx_ks_cross1": (

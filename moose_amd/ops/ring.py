@@ -782,6 +782,18 @@ def rss_mul3_k(kind: str, x0: RT, x1: RT, y0: RT, y1: RT, slot_ptr: int, nonce: 
     return out0, out1
 
 
+def add_zs3(v: RT, r: RT):
+    """Stacked arith zero share from precomputed keystreams ``r`` (= PRF(k_p) per party)
+    plus the reshare: returns (s0, s1) exactly like ``rss_mul3_k(arith, v)``."""
+    vd, rd = v.data.contiguous(), r.data.contiguous()
+    n = math.prod(v.shape) // 3
+    o0, o1 = empty(v.shape, v.bits, v.device), empty(v.shape, v.bits, v.device)
+    nat.check(nat.lib().mx_add_zs3(nat.dev_of(vd), _words(v.bits), nat.ptr(vd), nat.ptr(rd),
+                                   nat.ptr(o0.data), nat.ptr(o1.data), n, nat.stream_of(vd)),
+              "add_zs3")
+    return o0, o1
+
+
 def binary_slot(op: str, a: RT, b: RT, which: int):
     """Stacked [nparties, *shape] ``a``: ``op`` with public ``b`` (same shape as one slot,
     or a scalar) applied to slot ``which`` only, one kernel (mx_ew_binary_slot)."""

@@ -261,6 +261,11 @@ def dot(sess, x: RepTensor, y: RepTensor) -> RepTensor:
     """Matrix product: z_p = x_p.(y_p + y_{p+1}) + x_{p+1}.y_p as ONE K-doubled MFMA
     GEMM (all parties batched when stacked), + zero share, + reshare."""
     with span("rep.dot"):
+        over = getattr(sess, "p_dot_zs_reshare", None)
+        if over is not None and getattr(sess, "fused", False):
+            res = over(x.plc, x.s0, x.s1, y.s0, y.s1, x.kind)
+            if res is not None:
+                return RepTensor(x.plc, x.bits, x.kind, res[0], res[1])
         v = sess.p_dot_cross(x.plc, x.s0, x.s1, y.s0, y.s1)
         fused = getattr(sess, "p_zero_share_reshare", None)
         if fused is not None and getattr(sess, "fused", False):

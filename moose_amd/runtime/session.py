@@ -282,6 +282,36 @@ class StackedSession(Session):
         self.stats.record_round(_nbytes(s0))
         return PV(plc, s0), PV(plc, s1)
 
+    def p_dot_zs_reshare(self, plc, x0, x1, y0, y1, kind):
+        """rep.dot's local part + zero share + reshare with the zero-share keystreams
+        generated on a side stream WHILE the MFMA GEMM runs (AES is VALU/LDS work, the
+        GEMM is MFMA work; both fit on a CU).  Same nonce and values as
+        p_dot_cross + p_zero_share_reshare.  Returns None when not applicable."""
+        if (kind != "arith" or self.device.type != "cuda" or os.environ.get(
+                "MOOSEX_OVERLAP_ZS", "1") == "0"):
+            return None
+        shp, yshp = tuple(x0.v.shape), tuple(y0.v.shape)
+        if len(shp) != 3 or len(yshp) != 3:  # [party, M, K] . [party, K, N] only
+            return None
+        m, nout = shp[1], yshp[2]
+        if m * nout < (1 << 20):
+            return None
+        bits = x0.v.bits
+        nonce = self.nonce(plc)
+        main = torch.cuda.current_stream(self.device)
+        side = getattr(self, "_side_stream", None)
+        if side is None:
+            side = self._side_stream = torch.cuda.Stream(self.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            r = R.prf_expand_k(self.key_ptr(plc, 0), 3, nonce, (m, nout), bits, self.device)
+        v = R.dot_cross(x0.v, x1.v, y0.v, y1.v, nb=1)
+        main.wait_stream(side)
+        r.data.record_stream(main)
+        s0, s1 = R.add_zs3(v, r)
+        self.stats.record_round(_nbytes(s0))
+        return PV(plc, s0), PV(plc, s1)
+
     def p_dot_cross(self, plc, x0, x1, y0, y1):
         return PV(plc, R.dot_cross(x0.v, x1.v, y0.v, y1.v, nb=1))
 

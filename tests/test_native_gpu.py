@@ -168,3 +168,24 @@ def test_binary_slot_matches_host(bits):
     for b in (rand_rt((5, 7), bits, 71), rand_rt((), bits, 72)):
         for which in (0, 2):
             same(R.binary_slot("add", a, b, which), R.binary_slot("add", gpu(a), gpu(b), which))
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+def test_dot_zero_share_overlap_bitwise(bits, monkeypatch):
+    """rep.dot with the zero-share keystream generated on a side stream during the GEMM
+    (StackedSession.p_dot_zs_reshare) == the sequential fused path, bitwise."""
+    from moose_amd.ir.computation import ReplicatedPlacement
+    from moose_amd.protocols import replicated as rep
+    from moose_amd.runtime.session import HV, StackedSession
+
+    plc = ReplicatedPlacement(("a", "b", "c"))
+    res = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("MOOSEX_OVERLAP_ZS", flag)
+        s = StackedSession("cuda", seed=3)
+        x = R.encode(torch.rand(1024, 96, dtype=torch.float64, device="cuda"), 20, bits)
+        y = R.encode(torch.rand(96, 1024, dtype=torch.float64, device="cuda"), 20, bits)
+        X, Y = rep.share(s, plc, HV("a", x)), rep.share(s, plc, HV("b", y))
+        Z = rep.dot(s, X, Y)
+        res.append((Z.s0.v.data.cpu(), Z.s1.v.data.cpu()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
