@@ -288,7 +288,7 @@ class StackedSession(Session):
         GEMM is MFMA work; both fit on a CU).  Same nonce and values as
         p_dot_cross + p_zero_share_reshare.  Returns None when not applicable."""
         if (kind != "arith" or self.device.type != "cuda" or os.environ.get(
-                "MOOSEX_OVERLAP_ZS", "1") == "0"):
+                "MOOSEX_OVERLAP_ZS", "0") == "0"):  # opt-in until measured
             return None
         shp, yshp = tuple(x0.v.shape), tuple(y0.v.shape)
         if len(shp) != 3 or len(yshp) != 3:  # [party, M, K] . [party, K, N] only

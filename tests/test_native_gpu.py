@@ -180,11 +180,13 @@ def test_dot_zero_share_overlap_bitwise(bits, monkeypatch):
 
     plc = ReplicatedPlacement(("a", "b", "c"))
     res = []
+    g = torch.Generator(device="cpu").manual_seed(7)
+    xf = torch.rand(1024, 96, dtype=torch.float64, generator=g).cuda()
+    yf = torch.rand(96, 1024, dtype=torch.float64, generator=g).cuda()
     for flag in ("1", "0"):
         monkeypatch.setenv("MOOSEX_OVERLAP_ZS", flag)
         s = StackedSession("cuda", seed=3)
-        x = R.encode(torch.rand(1024, 96, dtype=torch.float64, device="cuda"), 20, bits)
-        y = R.encode(torch.rand(96, 1024, dtype=torch.float64, device="cuda"), 20, bits)
+        x, y = R.encode(xf, 20, bits), R.encode(yf, 20, bits)
         X, Y = rep.share(s, plc, HV("a", x)), rep.share(s, plc, HV("b", y))
         Z = rep.dot(s, X, Y)
         res.append((Z.s0.v.data.cpu(), Z.s1.v.data.cpu()))
