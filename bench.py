@@ -9,37 +9,46 @@ truncated (TruncPr) and revealed to carole, who decodes to float64.  As in pymoo
 fixed dtype runs over Z_2^128 (``--ring 64`` selects the Z_2^64 path).  Value = output
 elements per second over the whole job (all GPUs).
 
-Layout: one stacked 3-party session per GPU (all three parties' local work is one
-batched kernel per step on that MI355X); N GPUs run N data-parallel session replicas
-(weak scaling) and all-gather their revealed outputs over RCCL at the end of each step.
-Inputs are synthetic (uniform [-4, 4)), resident on the device; compilation (tracing and
-conversion) happens once before the timed region, like the reference's client-side
-compile.
+Layouts (``--layout``; default ``auto`` = stacked on 1 GPU, cyclic on N > 1):
+
+* ``stacked`` -- one 3-party session per GPU, all three parties' local work batched into
+  one kernel per protocol step; N GPUs = N data-parallel session replicas.
+* ``cyclic`` -- N sessions on N GPUs, every party of a session on a DIFFERENT GPU (role r
+  of session s on GPU (s + r) mod N, ``moose_amd/parallel/cyclic.py``): each GPU does one
+  session's worth of work and every reshare / dealer message / reveal is an RCCL
+  send/recv over xGMI.  Weak scaling with the same per-GPU work as the 1-GPU stacked run.
+* ``spmd`` -- one party per GPU, N/3 sessions (latency layout).
+
+All layouts all-gather the revealed outputs of every session over RCCL inside the timed
+region (overlapped with the next step).  Inputs are synthetic (uniform [-4, 4)),
+device-resident; tracing/conversion happens once before the timed region (the
+reference's client-side compile).  Every step creates a fresh session (fresh PRF keys).
+
+Launch: ``python bench.py --gpus N`` spawns N ranks itself (torch.distributed.run on
+127.0.0.1, before anything touches the GPU); under an external launcher (WORLD_SIZE set)
+it runs as one rank.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import numpy as np
-import torch
-import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 REFERENCE_ELEMS_PER_SEC = 1.0e6 / 5.910  # benchmarks/README.md:21, 1000x1000 Fixed128
+ROLES = ("alice", "bob", "carole")
 
 
 def build_computation(ring):
     import moose_amd as pm
     from moose_amd.compiler.from_edsl import convert
 
-    alice = pm.host_placement("alice")
-    bob = pm.host_placement("bob")
-    carole = pm.host_placement("carole")
+    alice, bob, carole = (pm.host_placement(r) for r in ROLES)
     rep = pm.replicated_placement("rep", players=[alice, bob, carole])
     fx = pm.fixed(14, 23)
 
@@ -61,7 +70,7 @@ def build_computation(ring):
     return convert(pm.trace(dot_product), fixedpoint_ring=ring)
 
 
-def main():
+def _parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -69,58 +78,114 @@ def main():
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--ring", type=int, default=128, choices=[64, 128])
     ap.add_argument("--no-gather", action="store_true")
-    ap.add_argument("--layout", default="stacked", choices=["stacked", "spmd"],
-                    help="stacked: 3 parties per GPU, N data-parallel sessions (default, "
-                         "highest throughput); spmd: each party on its own GPU, N/3 sessions, "
-                         "every reshare an RCCL send/recv")
-    ap.add_argument("--check", action="store_true", help="verify against float64 numpy")
-    args = ap.parse_args()
+    ap.add_argument("--layout", default="auto", choices=["auto", "stacked", "cyclic", "spmd"])
+    ap.add_argument("--check", action="store_true", help="verify against float64 torch")
+    return ap.parse_args()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _self_launch(args):
+    """N > 1 without a launcher: run N fresh ranks as child processes.  This process has
+    not touched the GPU (only argparse ran), and exits with the launcher's status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def _inputs(n, session, which, device):
+    import torch
+
+    g = torch.Generator(device="cpu").manual_seed(1234 + 2 * session + (which == "y"))
+    return (torch.rand(n, n, generator=g, dtype=torch.float64) * 8 - 4).to(device)
+
+
+def main():
+    args = _parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_self_launch(args))
+
+    import torch
+    import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but the launcher started {world} ranks")
+    # MOOSEX_SHARED_GPU=1: every rank on cuda:0 with gloo (rehearsing the multi-GPU
+    # layouts on a one-GPU box; RCCL refuses two ranks on one device)
+    shared = os.environ.get("MOOSEX_SHARED_GPU") == "1"
     if torch.cuda.is_available():
-        torch.cuda.set_device(local_rank)
-        device = torch.device("cuda", local_rank)
+        idx = 0 if shared else local_rank
+        torch.cuda.set_device(idx)
+        device = torch.device("cuda", idx)
     else:
         device = torch.device("cpu")
     if world > 1:
-        backend = "nccl" if device.type == "cuda" else "gloo"
-        dist.init_process_group(backend=backend, device_id=device if device.type == "cuda" else None)
+        backend = "nccl" if device.type == "cuda" and not shared else "gloo"
+        dist.init_process_group(backend=backend,
+                                device_id=device if backend == "nccl" else None)
+        dist.barrier()
 
     from moose_amd.runtime.interpreter import Interpreter
     from moose_amd.runtime.session import StackedSession
 
+    layout = args.layout
+    if layout == "auto":
+        layout = "stacked" if world == 1 else "cyclic"
+    if layout == "spmd" and (world < 3 or world % 3):
+        raise SystemExit("--layout spmd needs a multiple of 3 GPUs (one per party)")
+
     comp = build_computation(args.ring)
     n = args.size
-    spmd = args.layout == "spmd"
-    if spmd and (world < 3 or world % 3):
-        raise SystemExit("--layout spmd needs a multiple of 3 GPUs (one per party)")
-    n_sessions = world // 3 if spmd else world
-    session = rank // 3 if spmd else rank
-    g = torch.Generator(device="cpu").manual_seed(1234 + session)
-    x = (torch.rand(n, n, generator=g, dtype=torch.float64) * 8 - 4).to(device)
-    y = (torch.rand(n, n, generator=g, dtype=torch.float64) * 8 - 4).to(device)
+    if layout == "spmd":
+        n_sessions, out_owner = world // 3, rank % 3 == 2
+        xs, ys, out_session = rank // 3, rank // 3, rank // 3
+    elif layout == "cyclic":  # rank g hosts alice of session g, bob of g-1, carole of g-2
+        n_sessions, out_owner = world, True
+        xs, ys, out_session = rank, (rank - 1) % world, (rank - 2) % world
+    else:
+        n_sessions, out_owner = world, True
+        xs, ys, out_session = rank, rank, rank
+    x = _inputs(n, xs, "x", device)
+    y = _inputs(n, ys, "y", device)
+
     gather_bufs, gather_group, pending = None, None, []
     if n_sessions > 1 and not args.no_gather:
-        # replicas' revealed outputs concatenated along rows (the layout every backend
-        # accepts).  Double-buffered: step k's all-gather runs on the RCCL stream while
-        # step k+1 computes; a buffer is reused only after its gather completed.
+        # every session's revealed output, concatenated along rows.  Double-buffered:
+        # step k's all-gather runs on the RCCL stream while step k+1 computes.
         gather_bufs = [torch.empty((n_sessions * n, n), dtype=torch.float64, device=device)
                        for _ in range(2)]
-        if spmd:  # the output owners (carole = party 2) of every session
+        if layout == "spmd":  # the output owners (carole = party 2) of every session
             gather_group = dist.new_group([3 * s + 2 for s in range(n_sessions)])
-    out_owner = (rank % 3 == 2) if spmd else True
 
-    if spmd:
+    if layout == "spmd":
         from moose_amd.parallel.spmd import SPMDSession
         from moose_amd.parallel.transport import Transport
 
-        roles = {r: 3 * session + i for i, r in enumerate(("alice", "bob", "carole"))}
+        roles = {r: 3 * (rank // 3) + i for i, r in enumerate(ROLES)}
         transport = Transport(rank, world, device)
 
         def new_session():
-            return SPMDSession(("alice", "bob", "carole")[rank % 3], roles, transport, device)
+            return SPMDSession(ROLES[rank % 3], roles, transport, device)
+    elif layout == "cyclic":
+        from moose_amd.parallel.cyclic import CyclicSession
+        from moose_amd.parallel.cyclic import RingComm
+        from moose_amd.parallel.cyclic import default_offsets
+
+        comm = RingComm(rank, world, device)
+        offsets = default_offsets(ROLES)
+
+        def new_session():
+            return CyclicSession(comm, offsets, device)
     else:
         def new_session():
             return StackedSession(device)
@@ -145,36 +210,50 @@ def main():
         while pending:
             pending.pop(0).wait()
 
+    def sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
     for _ in range(args.warmup):
         step()
     drain()
-    if device.type == "cuda":
-        torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         z = step()
     drain()  # every step's gather is complete inside the timed region
-    if device.type == "cuda":
-        torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    sync()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    per_rank = [elapsed]
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+        tdev = device if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
+        allt = torch.empty(world, dtype=torch.float64, device=tdev)
+        dist.all_gather_into_tensor(allt, t)
+        per_rank = allt.cpu().tolist()
+    elapsed = max(per_rank)
     ms_per_step = elapsed / args.steps * 1e3
     value = n_sessions * n * n * args.steps / elapsed
 
     check = None
     if args.check and out_owner:
-        ref = (x.double() @ y.double())
-        err = (z - ref).abs().max().item()
-        check = {"max_abs_err": err}
+        ref = _inputs(n, out_session, "x", device) @ _inputs(n, out_session, "y", device)
+        check = {"max_abs_err": (z - ref).abs().max().item()}
+    checks = [check]
+    if world > 1 and args.check:
+        checks = [None] * world
+        dist.all_gather_object(checks, check)
 
     if rank == 0:
+        parallelism = {
+            "stacked": f"dp{world} (one stacked 3-party session per GPU, no inter-GPU reshare)",
+            "cyclic": (f"{n_sessions} 3-party sessions on {world} GPUs, each party on its own "
+                       "GPU (cyclic layout): every reshare an RCCL send/recv" if world > 1 else
+                       "1 stacked 3-party session"),
+            "spmd": f"dp{n_sessions} x 3-party sessions, one party per GPU (RCCL reshare)",
+        }[layout]
         line = {
             "metric": "replicated fixed(14,23) matmul elems/sec",
             "value": value,
@@ -192,13 +271,15 @@ def main():
                 "model": f"replicated fixed(14,23) RingDot {n}x{n} (share+dot+trunc_pr+reveal)",
                 "global_batch": n_sessions,
                 "seq_len": n,
-                "parallelism": (f"dp{n_sessions} x 3-party sessions, one party per GPU "
-                                "(RCCL reshare)" if spmd else
-                                f"dp{world} (one stacked 3-party session per GPU)"),
+                "parallelism": parallelism,
             },
+            "layout": layout,
+            "world_size": world,
+            "sessions": n_sessions,
+            "per_rank_ms_per_step": [t / args.steps * 1e3 for t in per_rank],
         }
-        if check:
-            line["check"] = check
+        if args.check:
+            line["check"] = [c for c in checks if c is not None]
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -97,22 +97,23 @@ inline Keys4 load_keys(const uint8_t* keys16, int nkeys) {
 // slots in device memory (MX_KEY_SLOT_WORDS words: raw key in words 0..3, schedule in
 // 4..47).  Slots keep the keys out of the launch parameters, so a captured hipGraph
 // replays with whatever keys the slots hold at replay time (fresh per evaluation).
+constexpr int kMaxKeySlots = 6;  // pairs mode: (k_p, k_p') for up to 3 parties
 struct KeySrc {
   Keys4 k;
-  const uint32_t* slot[4];
+  const uint32_t* slot[kMaxKeySlots];
 };
 
 inline KeySrc keysrc_host(const uint8_t* keys16, int nkeys) {
   KeySrc s;
   s.k = load_keys(keys16, nkeys);
-  for (int i = 0; i < 4; ++i) s.slot[i] = nullptr;
+  for (int i = 0; i < kMaxKeySlots; ++i) s.slot[i] = nullptr;
   return s;
 }
 
 inline KeySrc keysrc_slots(const uint32_t* const* slots, int nkeys) {
   KeySrc s;
   memset(&s.k, 0, sizeof(s.k));
-  for (int i = 0; i < 4; ++i) s.slot[i] = i < nkeys ? slots[i] : nullptr;
+  for (int i = 0; i < kMaxKeySlots; ++i) s.slot[i] = i < nkeys ? slots[i] : nullptr;
   return s;
 }
 
@@ -120,7 +121,7 @@ inline KeySrc keysrc_slots(const uint32_t* const* slots, int nkeys) {
 __device__ inline void stage_keys(uint32_t (*rks)[44], const KeySrc& src, int nkeys) {
   for (int i = threadIdx.x; i < nkeys * 44; i += blockDim.x) {
     const int q = i / 44, w = i - q * 44;
-    rks[q][w] = src.slot[q] ? src.slot[q][4 + w] : src.k.rk[q][w];
+    rks[q][w] = src.slot[q] ? src.slot[q][4 + w] : (q < 4 ? src.k.rk[q][w] : 0u);
   }
 }
 

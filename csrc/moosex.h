@@ -128,6 +128,12 @@ void mx_key_slots(const uint8_t* keys16, int n, uint32_t* out);
 int mx_rss_cross_k(int dev, int kind, int words, const void* x0, const void* x1,
                    const void* y0, const void* y1, void* out, int64_t n, int nparties,
                    const uint32_t* slots, int nslots, uint64_t nonce, void* stream);
+// mx_rss_cross with an explicit key PAIR per party: party p uses the key slots at
+// slot_ptrs[2p] and slot_ptrs[2p+1] (a host array of 2 * nparties slot addresses).  Used
+// when the stacked parties belong to different sessions (cyclic multi-GPU layout).
+int mx_rss_cross_kp(int dev, int kind, int words, const void* x0, const void* x1,
+                    const void* y0, const void* y1, void* out, int64_t n, int nparties,
+                    const uint32_t* const* slot_ptrs, uint64_t nonce, void* stream);
 // Stacked 3-party RSS product with the reshare fused in: out0[p] = z_p (cross terms +
 // zero share from slots p, p+1 mod 3) and out1[p] = z_{p+1}, i.e. both shares of every
 // party after the one-round reshare (x*/y*/out* are [3, n] slot vectors)

@@ -181,6 +181,9 @@ int mxh_rss_cross(int kind, int words, const void* x0, const void* x1, const voi
                   uint64_t nonce, void* stream);
 int mxh_prf_expand(int words, void* out, int64_t n, int nkeys, const uint8_t* keys16,
                    uint64_t nonce, void* stream);
+int mxh_rss_cross_kp(int kind, int words, const void* x0, const void* x1, const void* y0,
+                     const void* y1, void* out, int64_t n, int nparties,
+                     const uint32_t* const* slot_ptrs, uint64_t nonce, void* stream);
 int mxh_rss_cross_k(int kind, int words, const void* x0, const void* x1, const void* y0,
                     const void* y1, void* out, int64_t n, int nparties, const uint32_t* slots,
                     int nslots, uint64_t nonce, void* stream);

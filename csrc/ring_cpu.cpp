@@ -604,6 +604,40 @@ int mx_rss_cross_k(int dev, int kind, int words, const void* x0, const void* x1,
                                        (const T*)y1, (T*)out, n, nparties, keys, nonce));
 }
 
+int mx_rss_cross_kp(int dev, int kind, int words, const void* x0, const void* x1,
+                    const void* y0, const void* y1, void* out, int64_t n, int nparties,
+                    const uint32_t* const* slot_ptrs, uint64_t nonce, void* stream) {
+  if (nparties < 1 || nparties > 3) return -3;
+  if (dev)
+    return mxh_rss_cross_kp(kind, words, x0, x1, y0, y1, out, n, nparties, slot_ptrs, nonce,
+                            stream);
+  const int64_t es = words == 0 ? 1 : 8 * words;
+  auto at = [&](const void* b, int p) -> const void* {
+    return b ? (const uint8_t*)b + (int64_t)p * n * es : nullptr;
+  };
+  for (int p = 0; p < nparties; ++p) {
+    uint8_t keys[32];
+    memcpy(keys, slot_ptrs[2 * p], 16);
+    memcpy(keys + 16, slot_ptrs[2 * p + 1], 16);
+    void* o = (uint8_t*)out + (int64_t)p * n * es;
+    int rc = -2;
+    if (words == 0)
+      rc = rss_cross_t<uint8_t>(kind, (const uint8_t*)at(x0, p), (const uint8_t*)at(x1, p),
+                                (const uint8_t*)at(y0, p), (const uint8_t*)at(y1, p),
+                                (uint8_t*)o, n, 1, keys, nonce);
+    else if (words == 1)
+      rc = rss_cross_t<u64>(kind, (const u64*)at(x0, p), (const u64*)at(x1, p),
+                            (const u64*)at(y0, p), (const u64*)at(y1, p), (u64*)o, n, 1, keys,
+                            nonce);
+    else if (words == 2)
+      rc = rss_cross_t<u128>(kind, (const u128*)at(x0, p), (const u128*)at(x1, p),
+                             (const u128*)at(y0, p), (const u128*)at(y1, p), (u128*)o, n, 1,
+                             keys, nonce);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
 int mx_rss_mul3_k(int dev, int kind, int words, const void* x0, const void* x1, const void* y0,
                   const void* y1, void* out0, void* out1, int64_t n, const uint32_t* slots,
                   uint64_t nonce, void* stream) {

@@ -258,11 +258,13 @@ template <class T>
 __global__ void __launch_bounds__(256) k_rss_cross(int kind, const T* __restrict__ x0, const T* __restrict__ x1,
                             const T* __restrict__ y0, const T* __restrict__ y1,
                             T* __restrict__ out, int64_t n, int nparties, int has_keys,
-                            KeySrc keys, uint64_t nonce) {
+                            KeySrc keys, uint64_t nonce, int pairs) {
+  // pairs == 0: party p uses keys p and p+1 (one session, shared ring of keys);
+  // pairs == 1: party p uses keys 2p and 2p+1 (parties of independent sessions)
   __shared__ uint32_t Tt[mxd::kTTWords];
-    __shared__ uint32_t rks[4][44];
+  __shared__ uint32_t rks[mxd::kMaxKeySlots][44];
   if (has_keys) {
-    stage_keys(rks, keys, nparties + 1);
+    stage_keys(rks, keys, pairs ? 2 * nparties : nparties + 1);
     stage_tables_rep(Tt);
   }
   constexpr int P = Lane<T>::kPer;
@@ -274,8 +276,9 @@ __global__ void __launch_bounds__(256) k_rss_cross(int kind, const T* __restrict
     const int64_t b = g % nb;
     uint64_t alo = 0, ahi = 0, blo = 0, bhi = 0;
     if (has_keys) {
-      aes_ctr_rep(rks[p], Tt, nonce, (uint64_t)b, &alo, &ahi);
-      aes_ctr_rep(rks[p + 1], Tt, nonce, (uint64_t)b, &blo, &bhi);
+      const int ka = pairs ? 2 * p : p;
+      aes_ctr_rep(rks[ka], Tt, nonce, (uint64_t)b, &alo, &ahi);
+      aes_ctr_rep(rks[ka + 1], Tt, nonce, (uint64_t)b, &blo, &bhi);
     }
 #pragma unroll
     for (int j = 0; j < P; ++j) {
@@ -771,7 +774,7 @@ namespace {
 int launch_rss_cross(int kind, int words, const void* x0, const void* x1, const void* y0,
                      const void* y1, void* out, int64_t n, int nparties, bool has_keys,
                      bool ring3, const KeySrc& k, uint64_t nonce, void* stream,
-                     void* out1 = nullptr) {
+                     void* out1 = nullptr, int pairs = 0) {
   if (n == 0) return 0;
   if (nparties < 1 || nparties > 3) return -3;
   DEV_DISPATCH(words, T, {
@@ -795,7 +798,7 @@ int launch_rss_cross(int kind, int words, const void* x0, const void* x1, const 
     int64_t work = ((n + P - 1) / P) * nparties;
     hipLaunchKernelGGL(k_rss_cross<T>, dim3(grid_for(work)), dim3(kBlock), 0, S(stream), kind,
                        (const T*)x0, (const T*)x1, (const T*)y0, (const T*)y1, (T*)out, n,
-                       nparties, has_keys ? 1 : 0, k, nonce);
+                       nparties, has_keys ? 1 : 0, k, nonce, pairs);
     MX_LAUNCH_CHECK();
     return 0;
   });
@@ -838,6 +841,15 @@ int mxh_rss_cross_k(int kind, int words, const void* x0, const void* x1, const v
   KeySrc k = mxd::keysrc_slots(ptrs, ring3 ? 3 : nparties + 1);
   return launch_rss_cross(kind, words, x0, x1, y0, y1, out, n, nparties, true, ring3, k, nonce,
                           stream);
+}
+
+int mxh_rss_cross_kp(int kind, int words, const void* x0, const void* x1, const void* y0,
+                     const void* y1, void* out, int64_t n, int nparties,
+                     const uint32_t* const* slot_ptrs, uint64_t nonce, void* stream) {
+  if (nparties < 1 || 2 * nparties > mxd::kMaxKeySlots) return -3;
+  KeySrc k = mxd::keysrc_slots(slot_ptrs, 2 * nparties);
+  return launch_rss_cross(kind, words, x0, x1, y0, y1, out, n, nparties, true, false, k, nonce,
+                          stream, nullptr, 1);
 }
 
 int mxh_rss_mul3_k(int kind, int words, const void* x0, const void* x1, const void* y0,

@@ -865,6 +865,32 @@ def rss_cross_k(kind: str, x0: RT, x1, y0, y1, slot_ptr: int, nslots: int, nonce
     return rss_cross(kind, x0, x1, y0, y1, None, nonce, nparties, _slots=(slot_ptr, nslots))
 
 
+def rss_cross_kp(kind: str, x0: RT, x1, y0, y1, slot_ptrs, nonce: int) -> RT:
+    """``rss_cross`` for stacked parties with independent key PAIRS: party p masks with
+    PRF(slot_ptrs[2p]) - PRF(slot_ptrs[2p+1]) (``len(slot_ptrs) == 2 * nparties``).  The
+    parties of one stack may then belong to different sessions (mx_rss_cross_kp)."""
+    nparties = len(slot_ptrs) // 2
+    bits = x0.bits
+    shp = x0.shape
+    if y0 is not None and y0.shape != shp:
+        x0, y0 = _broadcast(x0, y0)
+        shp = x0.shape
+    datas = [None if p is None else (p if p.shape == shp else expand(p, shp)).data.contiguous()
+             for p in (x0, x1, y0, y1)]
+    n = math.prod(shp) // nparties
+    out = empty(shp, bits, x0.device)
+    arr = (ctypes.c_void_p * len(slot_ptrs))(*slot_ptrs)
+    nat.check(
+        nat.lib().mx_rss_cross_kp(
+            nat.dev_of(out.data), 1 if kind == "bool" else 0, _words(bits),
+            *[nat.ptr(d) for d in datas], nat.ptr(out.data), n, nparties, arr,
+            nonce & MASK64, nat.stream_of(out.data),
+        ),
+        "rss_cross_kp",
+    )
+    return out
+
+
 def rss_cross(kind: str, x0: RT, x1, y0: RT, y1, keys, nonce: int, nparties: int,
               _slots=None) -> RT:
     """Fused RSS local step.  Stacked layout: x* are [nparties, *shape]; party p gets

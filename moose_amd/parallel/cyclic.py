@@ -1,0 +1,304 @@
+"""Cyclic multi-GPU layout: N concurrent 3-party sessions on N GPUs, every party of a
+session on its own GPU, every reshare an RCCL send/recv over xGMI.
+
+Placement rule: role ``r`` (offset ``o(r)``: 0, 1, 2 for the three parties of the
+replicated placement, further roles after them) of session ``s`` lives on GPU
+``(s + o(r)) mod N``.  So GPU ``g`` hosts role ``r`` of session ``(g - o(r)) mod N`` --
+one instance of EVERY role, each from a different session (for N >= 3):
+
+    N = 4      GPU0          GPU1          GPU2          GPU3
+    alice      s0            s1            s2            s3
+    bob        s3            s0            s1            s2
+    carole     s2            s3            s0            s1
+
+Every GPU therefore does exactly the work of one stacked 3-party session (the weak-scaling
+unit of the 1-GPU bench), with the SAME batched kernels: a party vector is still one
+``[3, ...]`` tensor whose component ``p`` is party ``p`` -- of session ``g - o(owner_p)``.
+What changes is data movement, which becomes real inter-GPU traffic:
+
+* ``shift`` (the RSS reshare, component p <- component p+k of the same session) sends
+  each component to the GPU holding its destination party and receives from the GPU
+  holding its source party: one grouped ``batch_isend_irecv``, zero-copy into the
+  component slices;
+* ``move`` of a host value from role a to role b is a ring shift by ``o(b) - o(a)``;
+* ``take``/``gather`` stay local (component p and role ``owner_p`` belong to the same
+  session on this GPU).
+
+Because all N sessions run the same program on tensors of the same shapes (data-parallel
+replicas), every receiver knows the shape and dtype of what it receives from its own
+local copy: transfers carry no header and never synchronise with the host.  Public
+(mirrored) values are assumed replica-invariant (e.g. model weights); secret inputs may
+differ per session.
+
+Correlated randomness: each component has its OWN key pair (k_p, k_{p+1}) and k_all of
+its session -- the three components of a stack belong to different sessions, so the
+stacked zero-share kernels run in "pairs" mode (``mx_rss_cross_kp``).  Key setup follows
+``replicated/setup.rs:39-58``: party p draws k_p and hands a copy to party p-1 (here: a
+48-word key slot -- raw key plus expanded AES schedule -- sent device to device); party 0
+draws k_all and passes it on.
+
+With N = 1 the layout degenerates to one stacked session (every offset is 0 mod 1), which
+is what ``bench.py`` runs on one GPU (with the fully fused single-GPU kernels).
+
+Reference parity: the reference runs each party as its own worker process exchanging
+bincode values over gRPC (``execution/asynchronous.rs:557-632``, ``networking/grpc.rs``);
+its benchmark reports the max over the three workers (``benchmarks/pymoose/
+dot_product.py:124-139``).  This layout is that deployment, replicated N times across a
+node so that all N GPUs are busy.
+"""
+from __future__ import annotations
+
+import hashlib
+from typing import Dict
+from typing import List
+from typing import Sequence
+from typing import Tuple
+
+import torch
+import torch.distributed as dist
+
+from moose_amd.ops import ring as R
+from moose_amd.runtime.session import HV
+from moose_amd.runtime.session import PV
+from moose_amd.runtime.session import StackedSession
+from moose_amd.runtime.session import _nbytes
+
+
+class RingComm:
+    """Header-free symmetric point-to-point exchange over a process group.
+
+    ``exchange(sends, recvs)``: ``sends`` = [(tensor, dst_rank)], ``recvs`` =
+    [(out_tensor, src_rank)].  Every rank calls it with mirror-image lists (the n-th send
+    from A to B pairs with the n-th receive at B from A).  On RCCL the transfers are one
+    grouped ``batch_isend_irecv`` whose completion is a stream dependency, never a host
+    wait; transfers to oneself are device copies.  On gloo with device tensors the
+    payloads are staged through host memory (CPU tests and the one-GPU rehearsal).
+    """
+
+    def __init__(self, rank: int, world: int, device, group=None):
+        self.rank = rank
+        self.world = world
+        self.device = torch.device(device)
+        self.group = group
+        backend = dist.get_backend(group) if world > 1 else "none"
+        self.stage = backend == "gloo" and self.device.type == "cuda"
+        self.bytes_sent = 0
+        self.messages = 0
+        self.rounds = 0
+
+    def exchange(self, sends: Sequence[Tuple[torch.Tensor, int]],
+                 recvs: Sequence[Tuple[torch.Tensor, int]]):
+        local_s = [t for t, r in sends if r == self.rank]
+        local_r = [t for t, r in recvs if r == self.rank]
+        if len(local_s) != len(local_r):
+            raise RuntimeError("unbalanced self-exchange")
+        for src, out in zip(local_s, local_r):
+            out.copy_(src)
+        ops = []
+        staged = []
+        for t, r in sends:
+            if r == self.rank or t.numel() == 0:
+                continue
+            t = t.contiguous()
+            if self.stage:
+                t = t.cpu()
+            ops.append(dist.P2POp(dist.isend, t, r, group=self.group))
+            self.bytes_sent += t.numel() * t.element_size()
+            self.messages += 1
+        for out, r in recvs:
+            if r == self.rank or out.numel() == 0:
+                continue
+            if self.stage:
+                buf = torch.empty(out.shape, dtype=out.dtype)
+                staged.append((out, buf))
+                ops.append(dist.P2POp(dist.irecv, buf, r, group=self.group))
+            else:
+                ops.append(dist.P2POp(dist.irecv, out, r, group=self.group))
+        if not ops:
+            return
+        self.rounds += 1
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()  # RCCL: the current stream waits; gloo: completes the transfer
+        for out, buf in staged:
+            out.copy_(buf, non_blocking=True)
+
+
+def default_offsets(roles: Sequence[str]) -> Dict[str, int]:
+    return {r: i for i, r in enumerate(roles)}
+
+
+class CyclicSession(StackedSession):
+    """Stacked party vectors whose components belong to N different sessions (module
+    doc).  Runs the generic (per-round) protocol code; every round's messages are one
+    grouped exchange."""
+
+    is_simulated = False
+    fused = False      # the single-GPU whole-protocol kernels assume all parties local
+    ks_fused = False
+    KEY_SLOTS = 9      # per placement: for each component p: k_p, k_{p+1}, k_all
+
+    def __init__(self, comm: RingComm, offsets: Dict[str, int], device="cpu", seed=None):
+        super().__init__(device, seed)
+        self.comm = comm
+        self.g = comm.rank
+        self.N = comm.world
+        self.off = dict(offsets)
+        if seed is not None:  # distinct per-rank stream for fresh seeds
+            self._rng = torch.Generator().manual_seed(seed * 7919 + self.g)
+
+    # -- layout helpers -------------------------------------------------------------
+    def offset(self, role: str) -> int:
+        try:
+            return self.off[role]
+        except KeyError:
+            raise KeyError(f"role {role!r} has no offset in the cyclic layout") from None
+
+    def session_of(self, role: str) -> int:
+        """Index of the session whose ``role`` this GPU hosts."""
+        return (self.g - self.offset(role)) % self.N
+
+    def _peer(self, d: int) -> int:
+        return (self.g + d) % self.N
+
+    def _shift_tensor(self, plc, data: torch.Tensor, k: int) -> torch.Tensor:
+        """Component q <- component (q + k) % 3 of the same session, for a stacked
+        ``[3, ...]`` tensor of placement ``plc`` (grouped exchange, zero-copy slices)."""
+        data = data.contiguous()
+        out = torch.empty_like(data)
+        o = [self.offset(r) for r in plc.owners]
+        sends, recvs = [], []
+        for q in range(3):  # iterate by DESTINATION component on both sides
+            p = (q + k) % 3
+            recvs.append((out[q], self._peer(o[p] - o[q])))
+            sends.append((data[p], self._peer(o[q] - o[p])))
+        self.comm.exchange(sends, recvs)
+        return out
+
+    # -- data movement ----------------------------------------------------------------
+    def shift(self, x, k=1):
+        self.stats.record_round(_nbytes(x.v))
+        v = x.v
+        if isinstance(v, R.RT):
+            return PV(x.plc, R.RT(self._shift_tensor(x.plc, v.data, k), v.bits))
+        if v.dtype == torch.bool:
+            return PV(x.plc, self._shift_tensor(x.plc, v.to(torch.uint8), k).to(torch.bool))
+        return PV(x.plc, self._shift_tensor(x.plc, v, k))
+
+    def move(self, x, host):
+        if x.host == host:
+            return x
+        d = self.offset(host) - self.offset(x.host)
+        self.stats.record_send(x.host, host, _nbytes(x.v))
+        if d % self.N == 0:  # both roles of that session live on this GPU
+            return HV(host, x.v)
+        return HV(host, self._move_value(x.v, d))
+
+    def _move_value(self, v, d):
+        dst, src = self._peer(d), self._peer(-d)
+        if isinstance(v, R.RT):
+            out = torch.empty_like(v.data)
+            self.comm.exchange([(v.data, dst)], [(out, src)])
+            return R.RT(out, v.bits)
+        if isinstance(v, torch.Tensor):
+            t = v.to(torch.uint8) if v.dtype == torch.bool else v
+            out = torch.empty_like(t)
+            self.comm.exchange([(t, dst)], [(out, src)])
+            return out.to(torch.bool) if v.dtype == torch.bool else out
+        if type(v).__name__ == "KeyRef":  # a fresh seed: ship its key slot (raw + schedule)
+            from moose_amd.runtime.keys import KeyRef
+
+            kt = self.keytable
+            slot = kt.alloc(1)
+            self.comm.exchange([(v.table.t[v.slot], dst)], [(kt.t[slot], src)])
+            return KeyRef(kt, slot)
+        if isinstance(v, (bytes, bytearray)):
+            t = torch.tensor(list(v), dtype=torch.uint8, device=self.device)
+            out = torch.empty_like(t)
+            self.comm.exchange([(t, dst)], [(out, src)])
+            return bytes(out.cpu().tolist())
+        # shapes, Python scalars, strings: identical in every session (same program)
+        return v
+
+    def gather(self, plc, xs):
+        xs = [x if x.host == plc.owners[i] else self.move(x, plc.owners[i])
+              for i, x in enumerate(xs)]
+        vs = [x.v for x in xs]
+        if isinstance(vs[0], R.RT):
+            return PV(plc, R.RT(torch.stack([v.data for v in vs]), vs[0].bits))
+        return PV(plc, torch.stack(vs))
+
+    # -- keys -------------------------------------------------------------------------
+    def _seeded_key(self, plc, session: int, what) -> bytes:
+        h = hashlib.blake2b(repr((self.seed, tuple(plc.owners), session, what)).encode(),
+                            digest_size=16)
+        return h.digest()
+
+    def session_keys(self, plc, session: int):
+        """(k_0, k_1, k_2, k_all) of ``session`` in seeded mode (tests)."""
+        return [self._seeded_key(plc, session, i) for i in range(3)] + [
+            self._seeded_key(plc, session, "all")]
+
+    def setup(self, plc) -> int:
+        base = self._keys.get(plc)
+        if base is not None:
+            return base
+        kt = self.keytable
+        base = kt.alloc(self.KEY_SLOTS)  # random keys everywhere
+        self._keys[plc] = base
+        o = [self.offset(r) for r in plc.owners]
+        if self.seed is not None:
+            for p in range(3):
+                s = (self.g - o[p]) % self.N
+                kt._write(base + 3 * p, [self._seeded_key(plc, s, p)])
+                if p == 0:
+                    kt._write(base + 2, [self._seeded_key(plc, s, "all")])
+        # k_{p+1}: party p+1 of the same session hands a copy of its own key to party p
+        own = kt.t[[base, base + 3, base + 6]]
+        nxt = self._shift_tensor(plc, own, 1)
+        for p in range(3):
+            kt.t[base + 3 * p + 1].copy_(nxt[p])
+        # k_all: drawn by party 0, passed 0 -> 1 -> 2
+        kall = kt.t[[base + 2, base + 5, base + 8]]
+        a = self._shift_tensor(plc, kall, 2)   # component 1 <- component 0
+        b = self._shift_tensor(plc, a, 2)      # component 2 <- component 1's copy
+        kt.t[base + 5].copy_(a[1])
+        kt.t[base + 8].copy_(b[2])
+        return base
+
+    def _slot(self, plc, p: int, which: int) -> int:
+        return self.keytable.ptr(self.setup(plc) + 3 * p + which)
+
+    def _pair_ptrs(self, plc) -> List[int]:
+        return [self._slot(plc, p, w) for p in range(3) for w in (0, 1)]
+
+    def h_prf(self, plc, host, key_id, shape: HV, bits, nonce):
+        i = plc.owners.index(host)
+        if key_id == "all":
+            w = 2
+        elif key_id == i:
+            w = 0
+        elif key_id == (i + 1) % 3:
+            w = 1
+        else:
+            raise RuntimeError(f"{host} does not hold PRF key {key_id}")
+        out = R.prf_expand_k(self._slot(plc, i, w), 1, nonce, tuple(shape.v), bits, self.device)
+        return HV(host, R.RT(out.data[0], bits))
+
+    # -- RSS kernels with per-component key pairs --------------------------------------
+    def p_cross(self, kind, plc, x0, x1, y0, y1, zero_share=True):
+        x1v = x1.v if x1 is not None else None
+        y1v = y1.v if y1 is not None else None
+        nonce = self.nonce(plc)
+        if not zero_share:
+            return PV(plc, R.rss_cross(kind, x0.v, x1v, y0.v, y1v, None, nonce, 3))
+        return PV(plc, R.rss_cross_kp(kind, x0.v, x1v, y0.v, y1v, self._pair_ptrs(plc), nonce))
+
+    def p_add_zero_share(self, plc, z, kind="arith"):
+        return PV(plc, R.rss_cross_kp(kind, z.v, None, None, None, self._pair_ptrs(plc),
+                                      self.nonce(plc)))
+
+    # the single-GPU fused variants read other parties' data in-kernel: never used here
+    p_mul_reshare = None
+    p_zero_share_reshare = None
+    p_ks_level = None
+    p_dot_zs_reshare = None

@@ -1,0 +1,136 @@
+"""Cyclic multi-GPU layout (moose_amd/parallel/cyclic.py) over gloo: N ranks, N sessions,
+each party of a session on a different rank.  Every component of every rank must be
+bitwise equal to the same party of a single-process stacked session run with that
+session's keys -- i.e. moving the parties apart changed where the data lives, not what it
+is.  (Reference strategy: the per-worker integration runs of ``moose/src/execution``
+compared against the in-process runtime.)"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from moose_amd.ir.computation import ReplicatedPlacement
+from moose_amd.ops import ring as R
+
+PLC = ReplicatedPlacement(("a", "b", "c"))
+SEED = 5
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _data(session, bits):
+    v = torch.linspace(-20, 20, 96, dtype=torch.float64) + 0.25 * session
+    return R.encode(v, 23, bits)
+
+
+def _program(sess, xb, ya):
+    """share (owners b and a), mul + trunc, dot, bit decomposition, reveal to c."""
+    from moose_amd.protocols import replicated as rep
+
+    X = rep.share(sess, PLC, xb)
+    Y = rep.share(sess, PLC, ya)
+    M = rep.trunc_pr(sess, rep.mul(sess, X, Y), 23)
+    D = rep.dot(sess, rep.local(sess, X, "Reshape", shape=(8, 12)),
+                rep.local(sess, Y, "Reshape", shape=(12, 8)))
+    B = rep.bit_decompose(sess, X)
+    out = rep.reveal(sess, M, "c")
+    tensors = [t.s0.v.data.clone() for t in (X, Y, M, D, B)] + [
+        t.s1.v.data.clone() for t in (X, Y, M, D, B)]
+    return tensors, out.v.data.clone()
+
+
+def _worker(rank, world, port, q, device="cpu"):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from moose_amd.parallel.cyclic import CyclicSession
+    from moose_amd.parallel.cyclic import RingComm
+    from moose_amd.runtime.session import HV
+
+    sess = CyclicSession(RingComm(rank, world, device), {"a": 0, "b": 1, "c": 2}, seed=SEED,
+                         device=device)
+    res = {}
+    for bits in (64, 128):
+        xb = HV("b", R.to_device(_data(sess.session_of("b"), bits), device))
+        ya = HV("a", R.to_device(_data(100 + sess.session_of("a"), bits), device))
+        ts, out = _program(sess, xb, ya)
+        res[bits] = ([t.cpu().numpy() for t in ts], out.cpu().numpy(), sess.session_of("c"))
+    keys = {s: sess.session_keys(PLC, s) for s in range(world)}
+    q.put((rank, res, keys, sess.comm.messages))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _stacked_reference(keys, session):
+    """The worker's program for both ring widths, in the same order (one nonce stream)."""
+    from moose_amd.runtime.session import HV
+    from moose_amd.runtime.session import StackedSession
+
+    s = StackedSession("cpu", seed=1)
+    s.fused = False
+    base = s.setup(PLC)
+    s.keytable._write(base, keys)
+    out = {}
+    for bits in (64, 128):
+        xb = HV("b", _data(session, bits))
+        ya = HV("a", _data(100 + session, bits))
+        out[bits] = _program(s, xb, ya)
+    return out
+
+
+def _run(world, device):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, device)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = {}
+    for _ in range(world):
+        rank, res, keys, msgs = q.get(timeout=300)
+        got[rank] = (res, keys, msgs)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    keys = got[0][1]
+    refs = {}
+    for s in range(world):
+        r = _stacked_reference(keys[s], s)
+        refs.update({(s, b): r[b] for b in (64, 128)})
+    for g in range(world):
+        res, _, msgs = got[g]
+        assert msgs > 0  # the parties really exchanged messages
+        for bits in (64, 128):
+            ts, out, s_c = res[bits]
+            for i, t in enumerate(ts):
+                for p in range(3):
+                    s = (g - p) % world  # component p of rank g = party p of session g - p
+                    ref = refs[(s, bits)][0][i][p].numpy()
+                    assert np.array_equal(t[p], ref), (world, g, bits, i, p)
+            # carole's revealed product on rank g is session g - 2's
+            assert np.array_equal(out, refs[(s_c, bits)][1].numpy())
+            x = _data(s_c, bits)
+            y = _data(100 + s_c, bits)
+            want = R.decode(x, 23) * R.decode(y, 23)
+            np.testing.assert_allclose(R.decode(R.RT(torch.from_numpy(out), bits), 23).numpy(),
+                                       want.numpy(), atol=1e-5)
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_cyclic_bitwise_equals_stacked(world):
+    _run(world, "cpu")
+
+
+@pytest.mark.gpu
+def test_cyclic_on_gpu_bitwise_equals_cpu_stacked():
+    """Three party processes sharing the one test GPU (payloads staged through gloo):
+    the per-party key-pair kernels and the layout's data movement run on the device and
+    must reproduce the CPU stacked reference bit for bit."""
+    _run(3, "cuda:0")

@@ -191,3 +191,28 @@ def test_dot_zero_share_overlap_bitwise(bits, monkeypatch):
         Z = rep.dot(s, X, Y)
         res.append((Z.s0.v.data.cpu(), Z.s1.v.data.cpu()))
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+@pytest.mark.parametrize("kind", ["arith", "bool"])
+def test_rss_cross_kp_matches_host(bits, kind):
+    """Per-party key pairs (cyclic multi-GPU layout): device kernel == host kernel, and
+    party p's zero share uses exactly keys 2p and 2p+1."""
+    from moose_amd.runtime.keys import KeyTable
+
+    keys = [bytes([7 * i + 1] * 16) for i in range(6)]
+    tabs = []
+    for dev in ("cpu", "cuda"):
+        kt = KeyTable(dev)
+        base = kt.alloc(6)
+        kt._write(base, keys)
+        tabs.append([kt.ptr(base + i) for i in range(6)])
+    x0, x1 = rand_rt((3, 1000), bits, 11), rand_rt((3, 1000), bits, 12)
+    y0, y1 = rand_rt((3, 1000), bits, 13), rand_rt((3, 1000), bits, 14)
+    host = R.rss_cross_kp(kind, x0, x1, y0, y1, tabs[0], 99)
+    dev = R.rss_cross_kp(kind, gpu(x0), gpu(x1), gpu(y0), gpu(y1), tabs[1], 99)
+    same(host, dev)
+    # party 1 alone with its own pair == the one-party generic kernel
+    one = R.rss_cross(kind, R.RT(x0.data[1], bits), R.RT(x1.data[1], bits),
+                      R.RT(y0.data[1], bits), R.RT(y1.data[1], bits), keys[2:4], 99, 1)
+    assert torch.equal(one.data, host.data[1])
