@@ -24,6 +24,13 @@ STEPS=${STEPS:-all}
 [[ $STEPS == *smoke* || $STEPS == all ]] && run smoke 300 python __graft_entry__.py smoke
 [[ $STEPS == *bench* || $STEPS == all ]] && run bench128 600 python bench.py --steps 5 --warmup 2 --check
 [[ $STEPS == *bench* || $STEPS == all ]] && run bench64 600 python bench.py --steps 5 --warmup 2 --ring 64 --check
+if [[ $STEPS == *multi* || $STEPS == all ]]; then
+  # multi-rank layouts rehearsed on the one GPU (ranks share cuda:0, payloads via gloo)
+  export MOOSEX_SHARED_GPU=1
+  run cyclic3 600 python bench.py --gpus 3 --layout cyclic --size 1024 --steps 3 --warmup 1 --check
+  run spmd3 600 python bench.py --gpus 3 --layout spmd --size 1024 --steps 3 --warmup 1 --check
+  unset MOOSEX_SHARED_GPU
+fi
 if [[ $STEPS == *logreg* ]]; then
   rm -f gpurun_out/logreg.jsonl
   for it in 10 50 100; do for bs in 128 256 512 1024 2048; do

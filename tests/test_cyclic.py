@@ -5,7 +5,9 @@ session's keys -- i.e. moving the parties apart changed where the data lives, no
 is.  (Reference strategy: the per-worker integration runs of ``moose/src/execution``
 compared against the in-process runtime.)"""
 import os
+import queue
 import socket
+import time
 
 import numpy as np
 import pytest
@@ -58,8 +60,9 @@ def _worker(rank, world, port, q, device="cpu"):
                          device=device)
     res = {}
     for bits in (64, 128):
-        xb = HV("b", R.to_device(_data(sess.session_of("b"), bits), device))
-        ya = HV("a", R.to_device(_data(100 + sess.session_of("a"), bits), device))
+        xd, yd = _data(sess.session_of("b"), bits), _data(100 + sess.session_of("a"), bits)
+        xb = HV("b", R.RT(R.to_device(xd.data, device), bits))
+        ya = HV("a", R.RT(R.to_device(yd.data, device), bits))
         ts, out = _program(sess, xb, ya)
         res[bits] = ([t.cpu().numpy() for t in ts], out.cpu().numpy(), sess.session_of("c"))
     keys = {s: sess.session_keys(PLC, s) for s in range(world)}
@@ -93,9 +96,17 @@ def _run(world, device):
     for p in ps:
         p.start()
     got = {}
-    for _ in range(world):
-        rank, res, keys, msgs = q.get(timeout=300)
-        got[rank] = (res, keys, msgs)
+    deadline = time.monotonic() + 300
+    while len(got) < world:  # fail fast if a worker died instead of waiting out a timeout
+        try:
+            rank, res, keys, msgs = q.get(timeout=2)
+            got[rank] = (res, keys, msgs)
+        except queue.Empty:
+            dead = [p.exitcode for p in ps if p.exitcode not in (None, 0)]
+            if dead or time.monotonic() > deadline:
+                for p in ps:
+                    p.kill()
+                raise AssertionError(f"cyclic workers failed: exit codes {dead}")
     for p in ps:
         p.join(60)
         assert p.exitcode == 0
