@@ -1,10 +1,14 @@
 """Time the stacked RSS cross GEMM (the Dot hot kernel) alone: 3 x (M x 2K) . (2K x N)."""
 import argparse
+import os
+import sys
 import time
 
-import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from moose_amd.ops import ring as R
+import torch  # noqa: E402
+
+from moose_amd.ops import ring as R  # noqa: E402
 
 
 def main():

@@ -201,9 +201,10 @@ def test_rss_cross_kp_matches_host(bits, kind):
     from moose_amd.runtime.keys import KeyTable
 
     keys = [bytes([7 * i + 1] * 16) for i in range(6)]
-    tabs = []
+    tabs, alive = [], []  # keep both tables alive: the kernels read through raw pointers
     for dev in ("cpu", "cuda"):
         kt = KeyTable(dev)
+        alive.append(kt)
         base = kt.alloc(6)
         kt._write(base, keys)
         tabs.append([kt.ptr(base + i) for i in range(6)])
