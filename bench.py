@@ -172,7 +172,7 @@ def main():
         from moose_amd.parallel.transport import Transport
 
         roles = {r: 3 * (rank // 3) + i for i, r in enumerate(ROLES)}
-        transport = Transport(rank, world, device)
+        transport = comm = Transport(rank, world, device)
 
         def new_session():
             return SPMDSession(ROLES[rank % 3], roles, transport, device)
@@ -190,6 +190,8 @@ def main():
         def new_session():
             return StackedSession(device)
 
+    if layout == "stacked":
+        comm = None
     n_steps = [0]
 
     def step():
@@ -220,12 +222,15 @@ def main():
         step()
     drain()
     sync()
+    comm0 = (comm.bytes_sent, comm.messages) if comm is not None else (0, 0)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         z = step()
     drain()  # every step's gather is complete inside the timed region
     sync()
     elapsed = time.perf_counter() - t0
+    p2p = ((comm.bytes_sent - comm0[0]) / args.steps, (comm.messages - comm0[1]) / args.steps) \
+        if comm is not None else (0, 0)
     per_rank = [elapsed]
     if world > 1:
         tdev = device if dist.get_backend() == "nccl" else "cpu"
@@ -277,6 +282,9 @@ def main():
             "world_size": world,
             "sessions": n_sessions,
             "per_rank_ms_per_step": [t / args.steps * 1e3 for t in per_rank],
+            # rank 0's point-to-point traffic (inter-party shares over RCCL/xGMI) per step
+            "p2p_bytes_per_step_rank0": p2p[0],
+            "p2p_messages_per_step_rank0": p2p[1],
         }
         if args.check:
             line["check"] = [c for c in checks if c is not None]

@@ -435,6 +435,331 @@ __global__ void __launch_bounds__(512, 1)
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// v2 kernels: software-pipelined across the k-step boundary.
+//
+// PMC on the kernels above (profiles/r2_v0_gemm_pmc.md): the matrix pipes idle ~26 % of
+// the time.  After each k-step barrier every wave first issues its LDS-DMA pieces, then a
+// burst of fragment reads, and waits for them before its first MFMA -- with both waves of a
+// SIMD doing the same thing at the same moment, the pipe drains at every step.
+//
+// Here each wave's share of a k-step is a static schedule of "rounds" (round i multiplies
+// A limb i into its diagonals) split in two phases around ONE barrier:
+//   phase 1 (rounds < SPLIT): fragments of the current stage are read >= 2 rounds ahead of
+//            use; every read of the stage is issued (and waited for) before the barrier;
+//   barrier: all waves have finished reading stage k and their DMA of stage k+1 landed;
+//   phase 2 (rounds >= SPLIT): operands already in registers.  Interleaved with these MFMAs
+//            the wave issues its share of the DMA of stage k+2 (into stage k's buffer) and
+//            reads the fragments that step k+1 needs first ("carried": A_0, A_1 and the B
+//            limbs used in rounds 0-1) from stage k+1.
+// So right after the barrier every wave has MFMAs ready, and the next step starts with its
+// first operands already in registers: the pipe never waits on LDS at a step boundary.
+// Two LDS stages (A + B per stage).  The k-loop is unrolled by two so the carried register
+// sets swap roles without moves.
+// ---------------------------------------------------------------------------------------
+template <int L_, int DLO_, int DHI_, int SPLIT_>
+struct TriWave {
+  static constexpr int L = L_, DLO = DLO_, DHI = DHI_, SPLIT = SPLIT_;
+  static constexpr int LAST = DHI < L - 1 ? DHI : L - 1;  // last round (= last A limb)
+  static constexpr int ND = DHI - DLO + 1;                // accumulators
+  __host__ __device__ static constexpr int jlo(int i) { return DLO - i > 0 ? DLO - i : 0; }
+  __host__ __device__ static constexpr int jhi(int i) { return DHI - i < L - 1 ? DHI - i : L - 1; }
+  __host__ __device__ static constexpr int bfirst(int j) { return DLO - j > 0 ? DLO - j : 0; }
+  // Operands used in rounds 0 and 1 are "carried" (read during the previous step); any
+  // other operand first used in round `use` is read right after the MFMAs of round
+  // rd(use) = use - 2, so a whole round of MFMAs covers its latency (the compiler waits
+  // with lgkmcnt(0) before a consumer, so a read must not be issued just before one), and
+  // never after the step's barrier.
+  __host__ __device__ static constexpr bool carried(int j) { return bfirst(j) <= 1; }
+  __host__ __device__ static constexpr int rd(int use) {
+    return use - 2 < SPLIT - 1 ? use - 2 : SPLIT - 1;
+  }
+  __host__ __device__ static constexpr int mfmas() {
+    int n = 0;
+    for (int i = 0; i <= LAST; ++i) n += jhi(i) - jlo(i) + 1;
+    return n;
+  }
+  __host__ __device__ static constexpr int phase2_mfmas() {
+    int n = 0;
+    for (int i = SPLIT; i <= LAST; ++i) n += jhi(i) - jlo(i) + 1;
+    return n;
+  }
+  static_assert(SPLIT >= 2 && SPLIT <= LAST, "phase 2 must exist and start after round 1");
+};
+
+// s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(0) in the gfx9 encoding
+constexpr int kWaitVmLgkm0 = 0x0070;
+
+__device__ __forceinline__ v4i lds_frag(const int8_t* base, int limb, int off) {
+  return *(const v4i*)(base + limb * kTileBytes + off);
+}
+
+// One k-step of one wave.  `dma(t)` issues this wave's t-th DMA piece of stage k+2 (past
+// the last stage it re-reads the last stage into a buffer nobody reads any more, so the
+// schedule has no branches); the carried fragments of stage k+1 are read unconditionally
+// (past the end they are never used).
+template <class W, int NPIECE, class Dma>
+__device__ __forceinline__ void tri_step(const int8_t* As, const int8_t* Bs,
+                                         const int8_t* Asn, const int8_t* Bsn, int aoff,
+                                         int boff, v16i (&acc)[W::ND], const v4i (&Ac)[2],
+                                         const v4i (&Bc)[W::L], v4i (&An)[2], v4i (&Bn)[W::L],
+                                         Dma&& dma) {
+  constexpr int L = W::L;
+  v4i A[L], B[L];
+  A[0] = Ac[0];
+  A[1] = Ac[1];
+#pragma unroll
+  for (int j = 0; j <= W::LAST; ++j)
+    if (W::carried(j)) B[j] = Bc[j];
+  int piece = 0;  // DMA pieces issued in phase 2 (compile-time after unrolling)
+#pragma unroll
+  for (int r = 0; r <= W::LAST; ++r) {
+    if (r == W::SPLIT) {
+      // all reads of this stage done, my DMA of the next stage landed (a builtin, so the
+      // compiler's wait-count model knows the pre-barrier reads are complete)
+      __builtin_amdgcn_s_waitcnt(kWaitVmLgkm0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int j = W::jlo(r); j <= W::jhi(r); ++j) {
+      acc[r + j - W::DLO] =
+          __builtin_amdgcn_mfma_i32_32x32x32_i8(A[r], B[j], acc[r + j - W::DLO], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (r == W::SPLIT && j == W::jlo(r)) {  // carried fragments of the next step
+        An[0] = lds_frag(Asn, 0, aoff);
+        An[1] = lds_frag(Asn, 1, aoff);
+#pragma unroll
+        for (int jj = 0; jj <= W::LAST; ++jj)
+          if (W::carried(jj)) Bn[jj] = lds_frag(Bsn, jj, boff);
+        __builtin_amdgcn_sched_barrier(0);
+      } else if (r >= W::SPLIT && piece < NPIECE) {
+        dma(piece);
+        ++piece;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // reads issued after this round's MFMAs
+#pragma unroll
+    for (int i = 2; i <= W::LAST; ++i)
+      if (W::rd(i) == r) A[i] = lds_frag(As, i, aoff);
+#pragma unroll
+    for (int j = 0; j <= W::LAST; ++j)
+      if (!W::carried(j) && W::rd(W::bfirst(j)) == r) B[j] = lds_frag(Bs, j, boff);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (; piece < NPIECE; ++piece) dma(piece);  // phase 2 shorter than the DMA share
+}
+
+// The whole k-loop of one wave: prologue (stage 0 landed, carried fragments read, DMA of
+// stage 1 in flight), then steps unrolled by two.  Ends with every DMA landed and a
+// barrier, so the caller may reuse the LDS.
+template <class W, int NPIECE, class Dma>
+__device__ __forceinline__ void tri_loop(const int8_t* smem, int stage_bytes, int a_bytes,
+                                         int aoff, int boff, int64_t nkb,
+                                         v16i (&acc)[W::ND], Dma&& dma_stage) {
+  constexpr int L = W::L;
+  v4i A0[2], B0[L], A1[2], B1[L];
+  auto As = [&](int64_t kb) { return smem + (kb & 1) * stage_bytes; };
+  auto Bs = [&](int64_t kb) { return smem + (kb & 1) * stage_bytes + a_bytes; };
+  auto clampk = [&](int64_t kb) { return kb < nkb ? kb : nkb - 1; };
+#pragma unroll
+  for (int t = 0; t < NPIECE; ++t) dma_stage(0, t, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  A0[0] = lds_frag(As(0), 0, aoff);
+  A0[1] = lds_frag(As(0), 1, aoff);
+#pragma unroll
+  for (int j = 0; j <= W::LAST; ++j)
+    if (W::carried(j)) B0[j] = lds_frag(Bs(0), j, boff);
+#pragma unroll
+  for (int t = 0; t < NPIECE; ++t) dma_stage(clampk(1), t, 1);
+  for (int64_t kb = 0; kb < nkb; kb += 2) {
+    const int64_t s2 = clampk(kb + 2), s3 = clampk(kb + 3);
+    tri_step<W, NPIECE>(As(kb), Bs(kb), As(kb + 1), Bs(kb + 1), aoff, boff, acc, A0, B0, A1,
+                        B1, [&](int t) { dma_stage(s2, t, (int)(kb & 1)); });
+    if (kb + 1 < nkb)
+      tri_step<W, NPIECE>(As(kb + 1), Bs(kb + 1), As(kb + 2), Bs(kb + 2), aoff, boff, acc,
+                          A1, B1, A0, B0, [&](int t) { dma_stage(s3, t, (int)((kb + 1) & 1)); });
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+// Z_2^128, 64x64 block tile, 8 waves: wave w owns 32x32 quarter (w & 3); waves 0-3 sum the
+// anti-diagonals 0..kLo-1, waves 4-7 the rest (register budget: 2 waves per SIMD).
+constexpr int kLo = 9;
+using Lo128 = TriWave<16, 0, kLo - 1, 5>;
+using Hi128 = TriWave<16, kLo, 15, 11>;
+
+__global__ void __launch_bounds__(512, 1)
+    k_gemm128_v2(const int8_t* __restrict__ LA, const int8_t* __restrict__ LB,
+                 u128* __restrict__ C, int64_t M, int64_t N, int64_t Mp, int64_t Np, int64_t Kp,
+                 int accumulate, int gM, int xcd) {
+  constexpr int L = 16;
+  constexpr int SA = L * kTileBytes;  // A stage bytes (32 KB); B the same
+  constexpr int STAGE = 2 * SA;
+  constexpr int NPIECE = STAGE / 1024 / 8;  // DMA pieces per wave per stage
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+
+  const int64_t tiles_n = Np / TN, tiles_m = Mp / TM;
+  const int64_t ntiles = tiles_n * tiles_m;
+  const int64_t tid_flat = xcd ? xcd_remap(blockIdx.x, ntiles) : (int64_t)blockIdx.x;
+  const int64_t group = tid_flat / (gM * tiles_n);
+  const int64_t first_m = group * gM;
+  const int64_t gm = tiles_m - first_m < gM ? tiles_m - first_m : gM;
+  const int64_t in_group = tid_flat % (gM * tiles_n);
+  const int64_t tm = first_m + in_group % gm, tn = in_group / gm;
+  const int64_t b = blockIdx.y;
+  const int64_t nkb = Kp / TK;
+  const int8_t* ga = LA + (b * tiles_m + tm) * nkb * (int64_t)SA;
+  const int8_t* gb = LB + (b * tiles_n + tn) * nkb * (int64_t)SA;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tile = wave & 3;
+  const bool high = wave >= 4;
+  const int wr = tile >> 1, wc = tile & 1;
+  const int half = lane >> 5;
+  const int aoff = swz(wr * 32 + (lane & 31), half);
+  const int boff = swz(wc * 32 + (lane & 31), half);
+
+  // piece c = wave + 8 t of a stage: A pieces 0..31, B pieces 32..63
+  auto dma_stage = [&](int64_t kb, int t, int bufi) {
+    const int c = wave + 8 * t;
+    const bool is_b = t >= 4;  // wave < 8
+    const int cc = is_b ? c - 32 : c;
+    const int8_t* src = (is_b ? gb : ga) + kb * SA + cc * 1024 + lane * 16;
+    int8_t* dst = smem + bufi * STAGE + (is_b ? SA : 0) + cc * 1024;
+    __builtin_amdgcn_global_load_lds((const void*)src,
+                                     (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+  };
+
+  v16i acc[Lo128::ND > Hi128::ND ? Lo128::ND : Hi128::ND];
+#pragma unroll
+  for (int d = 0; d < (Lo128::ND > Hi128::ND ? Lo128::ND : Hi128::ND); ++d) acc[d] = v16i{0};
+  if (high) {
+    v16i (&a)[Hi128::ND] = *reinterpret_cast<v16i(*)[Hi128::ND]>(&acc);
+    tri_loop<Hi128, NPIECE>(smem, STAGE, SA, aoff, boff, nkb, a, dma_stage);
+  } else {
+    v16i (&a)[Lo128::ND] = *reinterpret_cast<v16i(*)[Lo128::ND]>(&acc);
+    tri_loop<Lo128, NPIECE>(smem, STAGE, SA, aoff, boff, nkb, a, dma_stage);
+  }
+
+  // epilogue: high waves park their partial sums in LDS, low waves add and store
+  u128* part = (u128*)smem + tile * (16 * 64);
+  if (high) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      u128 v = 0;
+#pragma unroll
+      for (int d = 0; d < Hi128::ND; ++d) v += ((u128)(int64_t)acc[d][r]) << (8 * (d + kLo));
+      part[r * 64 + lane] = v;
+    }
+  }
+  __syncthreads();
+  if (!high) {
+    const int col = lane & 31;
+    const int64_t gcol = tn * TN + wc * 32 + col;
+    u128* cb = C + b * M * N;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int64_t grow = tm * TM + wr * 32 + row;
+      u128 v = part[r * 64 + lane];
+#pragma unroll
+      for (int d = 0; d < Lo128::ND; ++d) v += ((u128)(int64_t)acc[d][r]) << (8 * d);
+      if (grow < M && gcol < N) {
+        u128* p = cb + grow * N + gcol;
+        *p = accumulate ? (u128)(*p + v) : v;
+      }
+    }
+  }
+}
+
+// Z_2^64, 64x128 block tile (two 64-column B tiles), 8 waves = 2 x 4 quarters of 32x32,
+// every wave all 8 diagonals (128 accumulator registers; 2 waves per SIMD).  Versus the
+// 64x64 / 4-wave kernel this cuts the L2->LDS stream per MFMA by a quarter.
+using W64 = TriWave<8, 0, 7, 4>;
+
+__global__ void __launch_bounds__(512, 1)
+    k_gemm64_v2(const int8_t* __restrict__ LA, const int8_t* __restrict__ LB,
+                u64* __restrict__ C, int64_t M, int64_t N, int64_t Mp, int64_t Np, int64_t Kp,
+                int accumulate, int gM, int xcd) {
+  constexpr int L = 8;
+  constexpr int SA = L * kTileBytes;  // 16 KB: one 64-row tile of A
+  constexpr int SB = 2 * SA;          // two 64-column tiles of B
+  constexpr int STAGE = SA + SB;
+  constexpr int NPIECE = STAGE / 1024 / 8;  // 6
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+
+  const int64_t tiles_n2 = Np / (2 * TN), tiles_m = Mp / TM;  // block tiles
+  const int64_t ntiles = tiles_n2 * tiles_m;
+  const int64_t tid_flat = xcd ? xcd_remap(blockIdx.x, ntiles) : (int64_t)blockIdx.x;
+  const int64_t group = tid_flat / (gM * tiles_n2);
+  const int64_t first_m = group * gM;
+  const int64_t gm = tiles_m - first_m < gM ? tiles_m - first_m : gM;
+  const int64_t in_group = tid_flat % (gM * tiles_n2);
+  const int64_t tm = first_m + in_group % gm, tn2 = in_group / gm;
+  const int64_t b = blockIdx.y;
+  const int64_t nkb = Kp / TK;
+  const int8_t* ga = LA + (b * tiles_m + tm) * nkb * (int64_t)SA;
+  const int8_t* gb = LB + (b * (Np / TN) + 2 * tn2) * nkb * (int64_t)SA;  // first of two
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;  // 2 x 4 quarters
+  const int half = lane >> 5;
+  const int aoff = swz(wr * 32 + (lane & 31), half);
+  const int boff = (wc >> 1) * SA + swz((wc & 1) * 32 + (lane & 31), half);
+
+  // piece c = wave + 8 t: A pieces 0..15, B pieces 16..47 (16 per 64-column tile)
+  auto dma_stage = [&](int64_t kb, int t, int bufi) {
+    const int c = wave + 8 * t;
+    const int8_t* src;
+    if (t < 2) {
+      src = ga + kb * SA + c * 1024;
+    } else {
+      const int cb = c - 16, h = cb >> 4;
+      src = gb + (h * nkb + kb) * SA + (cb & 15) * 1024;
+    }
+    int8_t* dst = smem + bufi * STAGE + c * 1024;
+    __builtin_amdgcn_global_load_lds((const void*)(src + lane * 16),
+                                     (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+  };
+
+  v16i acc[W64::ND];
+#pragma unroll
+  for (int d = 0; d < W64::ND; ++d) acc[d] = v16i{0};
+  tri_loop<W64, NPIECE>(smem, STAGE, SA, aoff, boff, nkb, acc, dma_stage);
+
+  const int col = lane & 31;
+  const int64_t gcol = tn2 * 2 * TN + wc * 32 + col;
+  u64* cbase = C + b * M * N;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    const int64_t grow = tm * TM + wr * 32 + row;
+    u64 v = 0;
+#pragma unroll
+    for (int d = 0; d < W64::ND; ++d) v += ((u64)(int64_t)acc[d][r]) << (8 * d);
+    if (grow < M && gcol < N) {
+      u64* p = cbase + grow * N + gcol;
+      *p = accumulate ? (u64)(*p + v) : v;
+    }
+  }
+}
+
+// MOOSEX_GEMM_V=1 selects the round-1 kernels (A/B measurements)
+bool use_v1_kernels() {
+  static const bool on = [] {
+    const char* e = std::getenv("MOOSEX_GEMM_V");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 // MOOSEX_GEMM_SPLIT=0 selects the one-wave-per-SIMD kernel for Z_2^128 (A/B testing)
 // Tile-order knobs (tuning experiments): MOOSEX_GEMM_GROUPM row bands per L2 group
 // (default kGroupM), MOOSEX_GEMM_XCD=0 disables the XCD-contiguous block remap.
@@ -495,7 +820,7 @@ Plan make_plan(int words, int64_t batch, int64_t M, int64_t N, int64_t Kchunk, i
   Plan p;
   p.L = words == 1 ? 8 : 16;
   p.Mp = round_up(M, TM);
-  p.Np = round_up(N, TN);
+  p.Np = round_up(N, words == 1 ? 2 * TN : TN);
   p.Kp = round_up(mode ? 2 * Kchunk : Kchunk, TK);
   p.la_bytes = batch * p.Mp * p.Kp * p.L;
   p.lb_bytes = batch * p.Np * p.Kp * p.L;
@@ -548,9 +873,23 @@ int run(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T* A1
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipFuncSetAttribute((const void*)k_gemm_limb128_split,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipFuncSetAttribute((const void*)k_gemm128_v2,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 4 * 16 * kTileBytes);
+        hipFuncSetAttribute((const void*)k_gemm64_v2,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 3 * 8 * kTileBytes);
         attr_set = true;
       }
-      if (sizeof(T) == 16 && use_split_kernel()) {
+      if (!use_v1_kernels()) {
+        if constexpr (sizeof(T) == 16) {
+          hipLaunchKernelGGL(k_gemm128_v2, dim3((unsigned)ntiles, (unsigned)batch), dim3(512),
+                             4 * 16 * kTileBytes, st, la, lb, (u128*)C, M, N, p.Mp, p.Np, p.Kp,
+                             accumulate, gemm_group_m(), gemm_xcd());
+        } else {
+          hipLaunchKernelGGL(k_gemm64_v2, dim3((unsigned)(ntiles / 2), (unsigned)batch),
+                             dim3(512), 2 * 3 * 8 * kTileBytes, st, la, lb, (u64*)C, M, N, p.Mp,
+                             p.Np, p.Kp, accumulate, gemm_group_m(), gemm_xcd());
+        }
+      } else if (sizeof(T) == 16 && use_split_kernel()) {
         hipLaunchKernelGGL(k_gemm_limb128_split, dim3((unsigned)ntiles, (unsigned)batch),
                            dim3(512), lds, st, la, lb, (u128*)C, M, N, p.Mp, p.Np, p.Kp,
                            accumulate, gemm_group_m(), gemm_xcd());

@@ -130,6 +130,48 @@ def test_gemm_long_k_split():
     same(R.dot(a, b, nb=1), R.dot(gpu(a), gpu(b), nb=1))
 
 
+def _const_limbs(digit, bits):
+    """The ring element whose balanced base-256 limbs all equal ``digit``."""
+    return sum(digit * 256**l for l in range(bits // 8)) % (1 << bits)
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+@pytest.mark.parametrize("da,db", [(-128, -128), (-128, 127), (127, 127)])
+def test_gemm_worst_case_limbs_at_max_k(bits, da, db):
+    """Every limb at the extreme of [-128, 127] and K' at the largest unsplit chunk (8192
+    for Z_2^128, 16384 for Z_2^64): the i32 diagonal accumulators of the MFMA kernels must
+    stay exact (header of csrc/gemm_mfma.hip).  Every output equals K.a.b mod 2^bits."""
+    K = 8192 if bits == 128 else 16384
+    M, N = 64, 130  # N not a multiple of the 64x128 Z_2^64 block tile
+    va, vb = _const_limbs(da, bits), _const_limbs(db, bits)
+    a = R.from_ints([[va] * K] * M, bits, "cuda")
+    b = R.from_ints([[vb] * N] * K, bits, "cuda")
+    c = R.to_ints(R.dot(a, b))
+    want = (K * va * vb) % (1 << bits)
+    assert (c == want).all()
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+def test_gemm_cross_long_k_split(bits):
+    """Mode 1 (K-doubled RSS cross GEMM) with K' = 2K above the exact-chunk limit, so the
+    host splits K and the kernel accumulates into C."""
+    M, K, N = 64, 5000 if bits == 128 else 9000, 72
+    xs = [rand_rt((1, M, K), bits, 50 + i) for i in range(2)]
+    ys = [rand_rt((1, K, N), bits, 60 + i) for i in range(2)]
+    h = R.dot_cross(xs[0], xs[1], ys[0], ys[1], nb=1)
+    d = R.dot_cross(gpu(xs[0]), gpu(xs[1]), gpu(ys[0]), gpu(ys[1]), nb=1)
+    same(h, d)
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+def test_gemm_multi_tile_odd_ksteps(bits):
+    """Several block tiles per batch, ragged M/N edges and an odd number of k-steps (the
+    pipelined kernels unroll the k-loop by two)."""
+    M, K, N = 200, 330, 260
+    a, b = rand_rt((3, M, K), bits, 70), rand_rt((3, K, N), bits, 71)
+    same(R.dot(a, b, nb=1), R.dot(gpu(a), gpu(b), nb=1))
+
+
 @pytest.mark.parametrize("bits", [64, 128])
 def test_fused_protocol_kernels_match_host(bits):
     from moose_amd.ir.computation import ReplicatedPlacement
