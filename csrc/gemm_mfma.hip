@@ -108,14 +108,14 @@ __device__ inline void prep_coords(int64_t g, int64_t nkb, int64_t& t, int64_t& 
 // A' [batch, M, K'] (K' = K or 2K: mode 1 concatenates A0 | A1) -> blocked limbs.
 template <class T>
 __global__ void __launch_bounds__(256) k_prep_a(const T* __restrict__ A0, const T* __restrict__ A1,
-                                                int64_t M, int64_t K, int mode,
+                                                int64_t M, int64_t K, int64_t a_bstride, int mode,
                                                 int8_t* __restrict__ out, int64_t Mp, int64_t Kp) {
   constexpr int L = Limbs<T>::L;
   const int64_t nkb = Kp / TK;
   const int64_t total = (Mp / TM) * nkb * 128;
   const int64_t b = blockIdx.y;
-  const T* a0 = A0 + b * M * K;
-  const T* a1 = mode ? A1 + b * M * K : a0;
+  const T* a0 = A0 + b * a_bstride;
+  const T* a1 = mode ? A1 + b * a_bstride : a0;
   int8_t* ob = out + b * (Mp / TM) * nkb * (int64_t)L * kTileBytes;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total;
        g += (int64_t)gridDim.x * blockDim.x) {
@@ -834,76 +834,78 @@ int64_t max_k_chunk(int words, int mode) {
 }
 
 template <class T>
+void launch_prep_a(const Plan& p, int64_t batch, int64_t M, int64_t K, const T* A0,
+                   const T* A1, int64_t a_bstride, int mode, int8_t* la, hipStream_t st) {
+  const int threads = 256;
+  const int64_t work = p.Mp * (p.Kp / 16);
+  const int gx = (int)std::min<int64_t>((work + threads - 1) / threads, 8192);
+  hipLaunchKernelGGL(k_prep_a<T>, dim3(gx, (unsigned)batch), dim3(threads), 0, st, A0, A1, M, K,
+                     a_bstride, mode, la, p.Mp, p.Kp);
+}
+
+template <class T>
+void launch_prep_b(const Plan& p, int64_t batch, int64_t K, int64_t N, const T* B0,
+                   const T* B1, int mode, int8_t* lb, hipStream_t st) {
+  const int threads = 256;
+  const int64_t work = p.Np * (p.Kp / 16);
+  const int gx = (int)std::min<int64_t>((work + threads - 1) / threads, 8192);
+  hipLaunchKernelGGL(k_prep_b<T>, dim3(gx, (unsigned)batch), dim3(threads), 0, st, B0, B1, K, N,
+                     mode, lb, p.Np, p.Kp);
+}
+
+template <class T>
+void launch_gemm(const Plan& p, int64_t batch, int64_t M, int64_t N, const int8_t* la,
+                 const int8_t* lb, T* C, int accumulate, hipStream_t st) {
+  constexpr int L = Limbs<T>::L;
+  const int64_t ntiles = (p.Mp / TM) * (p.Np / TN);
+  const size_t lds = 4 * (size_t)L * kTileBytes;  // 2 buffers x (A + B) stages
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)k_gemm_limb<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)lds);
+    hipFuncSetAttribute((const void*)k_gemm_limb128_split,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipFuncSetAttribute((const void*)k_gemm128_v2, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        4 * 16 * kTileBytes);
+    hipFuncSetAttribute((const void*)k_gemm64_v2, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        2 * 3 * 8 * kTileBytes);
+    attr_set = true;
+  }
+  if (!use_v1_kernels()) {
+    if constexpr (sizeof(T) == 16) {
+      hipLaunchKernelGGL(k_gemm128_v2, dim3((unsigned)ntiles, (unsigned)batch), dim3(512),
+                         4 * 16 * kTileBytes, st, la, lb, (u128*)C, M, N, p.Mp, p.Np, p.Kp,
+                         accumulate, gemm_group_m(), gemm_xcd());
+    } else {
+      hipLaunchKernelGGL(k_gemm64_v2, dim3((unsigned)(ntiles / 2), (unsigned)batch), dim3(512),
+                         2 * 3 * 8 * kTileBytes, st, la, lb, (u64*)C, M, N, p.Mp, p.Np, p.Kp,
+                         accumulate, gemm_group_m(), gemm_xcd());
+    }
+  } else if (sizeof(T) == 16 && use_split_kernel()) {
+    hipLaunchKernelGGL(k_gemm_limb128_split, dim3((unsigned)ntiles, (unsigned)batch), dim3(512),
+                       lds, st, la, lb, (u128*)C, M, N, p.Mp, p.Np, p.Kp, accumulate,
+                       gemm_group_m(), gemm_xcd());
+  } else {
+    hipLaunchKernelGGL(k_gemm_limb<T>, dim3((unsigned)ntiles, (unsigned)batch), dim3(256), lds,
+                       st, la, lb, C, M, N, p.Mp, p.Np, p.Kp, accumulate, gemm_group_m(),
+                       gemm_xcd());
+  }
+}
+
+template <class T>
 int run(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T* A1, const T* B0,
         const T* B1, int mode, T* C, int accumulate, void* ws, int64_t ws_bytes,
         hipStream_t st) {
-  constexpr int L = Limbs<T>::L;
-  const int64_t kc = max_k_chunk(sizeof(T) == 8 ? 1 : 2, mode);
-  for (int64_t k0 = 0; k0 < K || (K == 0 && k0 == 0); k0 += kc) {
-    const int64_t kk = std::min(kc, K - k0);
-    Plan p = make_plan(sizeof(T) == 8 ? 1 : 2, batch, M, N, kk, mode);
-    if (p.la_bytes + p.lb_bytes > ws_bytes) return -5;
-    int8_t* la = (int8_t*)ws;
-    int8_t* lb = la + p.la_bytes;
-    // A chunk: columns [k0, k0+kk) of A0/A1 -> sub-matrix view with row stride K
-    // (handled by offsetting and passing K as the row stride through a temporary view)
-    const int threads = 256;
-    {
-      int64_t work = p.Mp * (p.Kp / 16);
-      int gx = (int)std::min<int64_t>((work + threads - 1) / threads, 8192);
-      if (kk == K) {
-        hipLaunchKernelGGL(k_prep_a<T>, dim3(gx, (unsigned)batch), dim3(threads), 0, st, A0, A1,
-                           M, K, mode, la, p.Mp, p.Kp);
-      } else {
-        return -6;  // chunked K handled by the caller (mx_gemm splits K)
-      }
-    }
-    {
-      int64_t work = p.Np * (p.Kp / 16);
-      int gx = (int)std::min<int64_t>((work + threads - 1) / threads, 8192);
-      hipLaunchKernelGGL(k_prep_b<T>, dim3(gx, (unsigned)batch), dim3(threads), 0, st, B0, B1,
-                         K, N, mode, lb, p.Np, p.Kp);
-    }
-    {
-      const int64_t ntiles = (p.Mp / TM) * (p.Np / TN);
-      const size_t lds = 4 * (size_t)L * kTileBytes;  // 2 buffers x (A + B) stages
-      static bool attr_set = false;
-      if (!attr_set) {
-        hipFuncSetAttribute((const void*)k_gemm_limb<T>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipFuncSetAttribute((const void*)k_gemm_limb128_split,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipFuncSetAttribute((const void*)k_gemm128_v2,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 4 * 16 * kTileBytes);
-        hipFuncSetAttribute((const void*)k_gemm64_v2,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 3 * 8 * kTileBytes);
-        attr_set = true;
-      }
-      if (!use_v1_kernels()) {
-        if constexpr (sizeof(T) == 16) {
-          hipLaunchKernelGGL(k_gemm128_v2, dim3((unsigned)ntiles, (unsigned)batch), dim3(512),
-                             4 * 16 * kTileBytes, st, la, lb, (u128*)C, M, N, p.Mp, p.Np, p.Kp,
-                             accumulate, gemm_group_m(), gemm_xcd());
-        } else {
-          hipLaunchKernelGGL(k_gemm64_v2, dim3((unsigned)(ntiles / 2), (unsigned)batch),
-                             dim3(512), 2 * 3 * 8 * kTileBytes, st, la, lb, (u64*)C, M, N, p.Mp,
-                             p.Np, p.Kp, accumulate, gemm_group_m(), gemm_xcd());
-        }
-      } else if (sizeof(T) == 16 && use_split_kernel()) {
-        hipLaunchKernelGGL(k_gemm_limb128_split, dim3((unsigned)ntiles, (unsigned)batch),
-                           dim3(512), lds, st, la, lb, (u128*)C, M, N, p.Mp, p.Np, p.Kp,
-                           accumulate, gemm_group_m(), gemm_xcd());
-      } else {
-        hipLaunchKernelGGL(k_gemm_limb<T>, dim3((unsigned)ntiles, (unsigned)batch), dim3(256),
-                           lds, st, la, lb, C, M, N, p.Mp, p.Np, p.Kp, accumulate,
-                           gemm_group_m(), gemm_xcd());
-      }
-    }
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return -100 - (int)e;
-    break;
-  }
-  return 0;
+  if (K > max_k_chunk(sizeof(T) == 8 ? 1 : 2, mode)) return -6;  // caller splits long K
+  Plan p = make_plan(sizeof(T) == 8 ? 1 : 2, batch, M, N, K, mode);
+  if (p.la_bytes + p.lb_bytes > ws_bytes) return -5;
+  int8_t* la = (int8_t*)ws;
+  int8_t* lb = la + p.la_bytes;
+  launch_prep_a<T>(p, batch, M, K, A0, A1, M * K, mode, la, st);
+  launch_prep_b<T>(p, batch, K, N, B0, B1, mode, lb, st);
+  launch_gemm<T>(p, batch, M, N, la, lb, C, accumulate, st);
+  hipError_t e = hipGetLastError();
+  return e != hipSuccess ? -100 - (int)e : 0;
 }
 
 }  // namespace
@@ -960,6 +962,57 @@ int mx_gemm_ws(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const 
     return run<u128>(batch, M, N, K, (const u128*)A0, (const u128*)A1, (const u128*)B0,
                      (const u128*)B1, mode, (u128*)C, accumulate, workspace, ws_bytes, st);
   return -2;
+}
+
+// Prepared-B GEMM: the B' operand's limb planes are built once (mx_gemm_prep_b into a
+// caller buffer of mx_gemm_b_bytes) and reused by several products with different A row
+// blocks (mx_gemm_with_b; A given with a batch stride, so row blocks of a stacked
+// [batch, M, K] tensor need no copy).  Used by the row-chunked dot pipeline.
+int64_t mx_gemm_b_bytes(int words, int64_t batch, int64_t N, int64_t K, int mode) {
+  if (words != 1 && words != 2) return 0;
+  if (K > max_k_chunk(words, mode)) return 0;
+  return make_plan(words, batch, 64, N, K, mode).lb_bytes;
+}
+
+int mx_gemm_prep_b(int words, int64_t batch, int64_t K, int64_t N, const void* B0,
+                   const void* B1, int mode, void* lb, void* stream) {
+  if (K > max_k_chunk(words, mode)) return -6;
+  Plan p = make_plan(words, batch, 64, N, K, mode);
+  hipStream_t st = (hipStream_t)stream;
+  if (words == 1)
+    launch_prep_b<u64>(p, batch, K, N, (const u64*)B0, (const u64*)B1, mode, (int8_t*)lb, st);
+  else if (words == 2)
+    launch_prep_b<u128>(p, batch, K, N, (const u128*)B0, (const u128*)B1, mode, (int8_t*)lb,
+                        st);
+  else
+    return -2;
+  hipError_t e = hipGetLastError();
+  return e != hipSuccess ? -100 - (int)e : 0;
+}
+
+int mx_gemm_with_b(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
+                   const void* A1, int64_t a_bstride, int mode, const void* lb, void* C,
+                   int accumulate, void* stream) {
+  if (K > max_k_chunk(words, mode)) return -6;
+  Plan p = make_plan(words, batch, M, N, K, mode);
+  void* la = get_workspace(p.la_bytes);
+  if (!la) return -4;
+  hipStream_t st = (hipStream_t)stream;
+  if (words == 1) {
+    launch_prep_a<u64>(p, batch, M, K, (const u64*)A0, (const u64*)A1, a_bstride, mode,
+                       (int8_t*)la, st);
+    launch_gemm<u64>(p, batch, M, N, (const int8_t*)la, (const int8_t*)lb, (u64*)C, accumulate,
+                     st);
+  } else if (words == 2) {
+    launch_prep_a<u128>(p, batch, M, K, (const u128*)A0, (const u128*)A1, a_bstride, mode,
+                        (int8_t*)la, st);
+    launch_gemm<u128>(p, batch, M, N, (const int8_t*)la, (const int8_t*)lb, (u128*)C,
+                      accumulate, st);
+  } else {
+    return -2;
+  }
+  hipError_t e = hipGetLastError();
+  return e != hipSuccess ? -100 - (int)e : 0;
 }
 
 int mxh_gemm_mfma(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,

@@ -103,6 +103,15 @@ int64_t mx_gemm_workspace_bytes(int words, int64_t batch, int64_t M, int64_t N,
 int mx_gemm_ws(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
                const void* A1, const void* B0, const void* B1, int mode, void* C,
                int accumulate, void* workspace, int64_t ws_bytes, void* stream);
+// Prepared-B GEMM (device only): B' limb planes built once, reused for several A row
+// blocks; A given with a batch stride (elements).  mx_gemm_b_bytes returns 0 when K is
+// above the exact single-chunk limit (then use mx_gemm).
+int64_t mx_gemm_b_bytes(int words, int64_t batch, int64_t N, int64_t K, int mode);
+int mx_gemm_prep_b(int words, int64_t batch, int64_t K, int64_t N, const void* B0,
+                   const void* B1, int mode, void* lb, void* stream);
+int mx_gemm_with_b(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
+                   const void* A1, int64_t a_bstride, int mode, const void* lb, void* C,
+                   int accumulate, void* stream);
 // select the GEMM kernel: 0 = auto, 1 = force VALU reference kernel, 2 = force MFMA
 void mx_set_gemm_impl(int impl);
 
@@ -164,6 +173,28 @@ int mx_trunc_pr3_k(int dev, int words, const void* s0, void* out0, void* out1, i
 int mx_share3_k(int dev, int kind, int words, const void* x, void* out0, void* out1, int64_t n,
                 int j, const uint32_t* slot_next, const uint32_t* slot_all, uint64_t n1,
                 uint64_t na, void* stream);
+
+// Per-party protocol rounds for layouts with the parties of a session on different GPUs
+// (rss_party.hip): ncomp stacked components [ncomp, n], component c in role roles[c]
+// (-1 = idle), key slots (own k_p, next k_{p+1}) per component.  nonces: r0, r1, t, m, z0,
+// z2 of the TruncPr.  Round 0 writes the outgoing messages (P0: mk0, P1: mk1, P2: rt1 in
+// msg; P2: rm1 in msg_rm as u64) and P2's new shares; round 1 takes the received mask
+// share (rmk) and dealer shares (rrt, rrm) and writes w (P0: y0 - z0, P1: y1 - z2) and
+// P0's s0 / P1's s1.
+int mx_trunc_party_r0(int dev, int words, int64_t n, int m, int ncomp, const int* roles,
+                      const void* s0, const void* s1, void* msg, void* msg_rm, void* out0,
+                      void* out1, const uint32_t* const* slots, const uint64_t* nonces,
+                      void* stream);
+int mx_trunc_party_r1(int dev, int words, int64_t n, int m, int ncomp, const int* roles,
+                      const void* msg, const void* rmk, const void* rrt, const void* rrm,
+                      void* w, void* out0, void* out1, const uint32_t* const* slots,
+                      const uint64_t* nonces, void* stream);
+// Share by member j, per component: rel[c] = (role - j) mod 3; key slots per component:
+// rel 0 (next, all), rel 1 (own, all), rel 2 (all, all).  The owner's out0 (its masked
+// x_j) is then sent to P_{j+2}, whose out1 it becomes.
+int mx_share_party(int dev, int kind, int words, int64_t n, int ncomp, const int* rel,
+                   const void* x, void* out0, void* out1, const uint32_t* const* slots,
+                   uint64_t n1, uint64_t na, void* stream);
 
 #ifdef __cplusplus
 }

@@ -47,3 +47,42 @@ MX_HD inline T trunc_pr_z1(T x0, T x1, T x2, T r0, T r1, T rt0, T rm0, T z0, T z
 }
 
 }  // namespace mxf
+
+// ---------------------------------------------------------------------------------------
+// Per-party TruncPr rounds (one party per stacked component, parties on different GPUs;
+// see rss_party.hip).  Same arithmetic as trunc_pr_z1, split at the two message rounds.
+// The dealer's msb-mask share only matters modulo 2^(m+1) (it is shifted left by k - m),
+// so it travels as a u64 (m <= 63).
+// ---------------------------------------------------------------------------------------
+namespace mxf {
+
+// dealer P2: r = r0 + r1 -> (rt1, rm1) for P1
+template <class T>
+MX_HD inline void trunc_dealer(T r0, T r1, T rt0, T rm0, int m, T* rt1, uint64_t* rm1) {
+  constexpr int W = 8 * sizeof(T);
+  const T r = r0 + r1;
+  *rt1 = shr<T>(shl<T>(r, 1), m + 1) - rt0;
+  *rm1 = (uint64_t)(shr<T>(r, W - 1) - rm0);
+}
+
+// P0's masked opening share: x0 + x1 + 2^(k-1) + r0
+template <class T>
+MX_HD inline T trunc_mask0(T x0, T x1, T r0) {
+  constexpr int W = 8 * sizeof(T);
+  return x0 + x1 + shl<T>((T)1, W - 2) + r0;
+}
+
+// P0's (first) / P1's truncated additive share from the opened c
+template <class T>
+MX_HD inline T trunc_y(T c, T rt, T rm, int m, bool first) {
+  constexpr int W = 8 * sizeof(T);
+  const int k = W - 1;
+  const T c_msb = shr<T>(c, W - 1);
+  T ov = rm - shl<T>(c_msb * rm, 1);
+  if (!first) return shl<T>(ov, k - m) - rt;
+  ov = ov + c_msb;
+  const T c_top = shr<T>(shl<T>(c, 1), m + 1);
+  return shl<T>(ov, k - m) - rt + c_top - shl<T>((T)1, k - 1 - m);
+}
+
+}  // namespace mxf

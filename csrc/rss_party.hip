@@ -1,0 +1,289 @@
+// Per-party protocol kernels for layouts where the three parties of a session sit on
+// DIFFERENT GPUs (moose_amd/parallel/cyclic.py): a GPU stacks one party of each of up to
+// three sessions, component c playing role roles[c].  Each kernel does every stacked
+// role's local work of one protocol round in one pass; the messages between rounds go
+// over RCCL.  Same PRF keys / nonces / counters as the generic protocol code, so the shares
+// are bitwise equal to it (and to the single-GPU fused kernels of rss_fused.hip).
+//
+// TruncPr (dealer P2, reference additive/trunc.rs:114-170), rounds:
+//   r0: P0 mk0 = x0 + x1 + 2^(k-2) + r0          -> P1
+//       P1 mk1 = x2 + r1                          -> P0
+//       P2 rt1, rm1 (dealer shares for P1)        -> P1;  P2's new shares (z2, z0)
+//   r1: P0 c = mk0 + mk1, y0, w0 = y0 - z0        -> P1;  P0's s0 = z0
+//       P1 c = mk1 + mk0, y1, w1 = y1 - z2        -> P0;  P1's s1 = z2
+//   r2: z1 = w0 + w1 (elementwise, host side)
+// Share by member j: one kernel computing every role's two slots (the owner's masked
+// x_j is then sent to P_{j+2}).
+// Key slots: component c passes (own k_p, next k_{p+1}[, k_all]) of its session.
+#include <hip/hip_runtime.h>
+
+#include "aes_dev.h"
+#include "moosex.h"
+#include "rss_fused.h"
+
+using u64 = uint64_t;
+using u128 = unsigned __int128;
+
+namespace {
+
+struct Roles {
+  int r[3];
+};
+
+template <class T>
+__global__ void __launch_bounds__(256)
+    k_trunc_party_r0(int64_t n, int m, Roles roles, const T* __restrict__ s0,
+                     const T* __restrict__ s1, T* __restrict__ msg, u64* __restrict__ msg_rm,
+                     T* __restrict__ out0, T* __restrict__ out1, mxd::KeySrc keys, uint64_t n_r0,
+                     uint64_t n_r1, uint64_t n_t, uint64_t n_m, uint64_t n_z0, uint64_t n_z2,
+                     int ncomp) {
+  __shared__ uint32_t Tt[mxd::kTTWords];
+  __shared__ uint32_t rks[mxd::kMaxKeySlots][44];
+  mxd::stage_keys(rks, keys, 2 * ncomp);
+  mxd::stage_tables_rep(Tt);
+  constexpr int P = mxd::Lane<T>::kPer;
+  const int64_t nb = (n + P - 1) / P;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < nb * ncomp;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(g / nb);
+    const int64_t b = g - c * nb;
+    const int role = roles.r[c];
+    const uint32_t* own = rks[2 * c];
+    const uint32_t* nxt = rks[2 * c + 1];
+    const int64_t base = (int64_t)c * n;
+    if (role == 0) {  // k0 = own
+      uint64_t al, ah;
+      mxd::aes_ctr_rep(own, Tt, n_r0, b, &al, &ah);
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const int64_t i = b * P + j;
+        if (i >= n) break;
+        msg[base + i] = mxf::trunc_mask0<T>(s0[base + i], s1[base + i], mxd::pick<T>(al, ah, j));
+      }
+    } else if (role == 1) {  // k2 = next
+      uint64_t al, ah;
+      mxd::aes_ctr_rep(nxt, Tt, n_r1, b, &al, &ah);
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const int64_t i = b * P + j;
+        if (i >= n) break;
+        msg[base + i] = s1[base + i] + mxd::pick<T>(al, ah, j);
+      }
+    } else if (role == 2) {  // k2 = own, k0 = next
+      uint64_t r0l, r0h, r1l, r1h, tl, th, ml, mh, z0l, z0h, z2l, z2h;
+      mxd::aes_ctr_rep(nxt, Tt, n_r0, b, &r0l, &r0h);
+      mxd::aes_ctr_rep(own, Tt, n_r1, b, &r1l, &r1h);
+      mxd::aes_ctr_rep(nxt, Tt, n_t, b, &tl, &th);
+      mxd::aes_ctr_rep(nxt, Tt, n_m, b, &ml, &mh);
+      mxd::aes_ctr_rep(nxt, Tt, n_z0, b, &z0l, &z0h);
+      mxd::aes_ctr_rep(own, Tt, n_z2, b, &z2l, &z2h);
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const int64_t i = b * P + j;
+        if (i >= n) break;
+        T rt1;
+        u64 rm1;
+        mxf::trunc_dealer<T>(mxd::pick<T>(r0l, r0h, j), mxd::pick<T>(r1l, r1h, j),
+                             mxd::pick<T>(tl, th, j), mxd::pick<T>(ml, mh, j), m, &rt1, &rm1);
+        msg[base + i] = rt1;
+        msg_rm[base + i] = rm1;
+        out0[base + i] = mxd::pick<T>(z2l, z2h, j);
+        out1[base + i] = mxd::pick<T>(z0l, z0h, j);
+      }
+    }
+  }
+}
+
+template <class T>
+__global__ void __launch_bounds__(256)
+    k_trunc_party_r1(int64_t n, int m, Roles roles, const T* __restrict__ msg,
+                     const T* __restrict__ rmk, const T* __restrict__ rrt,
+                     const u64* __restrict__ rrm, T* __restrict__ w, T* __restrict__ out0,
+                     T* __restrict__ out1, mxd::KeySrc keys, uint64_t n_t, uint64_t n_m,
+                     uint64_t n_z0, uint64_t n_z2, int ncomp) {
+  __shared__ uint32_t Tt[mxd::kTTWords];
+  __shared__ uint32_t rks[mxd::kMaxKeySlots][44];
+  mxd::stage_keys(rks, keys, 2 * ncomp);
+  mxd::stage_tables_rep(Tt);
+  constexpr int P = mxd::Lane<T>::kPer;
+  const int64_t nb = (n + P - 1) / P;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < nb * ncomp;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(g / nb);
+    const int64_t b = g - c * nb;
+    const int role = roles.r[c];
+    const int64_t base = (int64_t)c * n;
+    if (role == 0) {
+      const uint32_t* k0 = rks[2 * c];
+      uint64_t tl, th, ml, mh, zl, zh;
+      mxd::aes_ctr_rep(k0, Tt, n_t, b, &tl, &th);
+      mxd::aes_ctr_rep(k0, Tt, n_m, b, &ml, &mh);
+      mxd::aes_ctr_rep(k0, Tt, n_z0, b, &zl, &zh);
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const int64_t i = b * P + j;
+        if (i >= n) break;
+        const T cc = msg[base + i] + rmk[base + i];
+        const T z0 = mxd::pick<T>(zl, zh, j);
+        const T y0 = mxf::trunc_y<T>(cc, mxd::pick<T>(tl, th, j), mxd::pick<T>(ml, mh, j), m, true);
+        w[base + i] = y0 - z0;
+        out0[base + i] = z0;
+      }
+    } else if (role == 1) {
+      const uint32_t* k2 = rks[2 * c + 1];
+      uint64_t zl, zh;
+      mxd::aes_ctr_rep(k2, Tt, n_z2, b, &zl, &zh);
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const int64_t i = b * P + j;
+        if (i >= n) break;
+        const T cc = msg[base + i] + rmk[base + i];
+        const T z2 = mxd::pick<T>(zl, zh, j);
+        const T y1 = mxf::trunc_y<T>(cc, rrt[base + i], (T)rrm[base + i], m, false);
+        w[base + i] = y1 - z2;
+        out1[base + i] = z2;
+      }
+    }
+  }
+}
+
+template <class T>
+__global__ void __launch_bounds__(256)
+    k_share_party(int kind, int64_t n, Roles rel, const T* __restrict__ x, T* __restrict__ out0,
+                  T* __restrict__ out1, mxd::KeySrc keys, uint64_t n1, uint64_t na, int ncomp) {
+  __shared__ uint32_t Tt[mxd::kTTWords];
+  __shared__ uint32_t rks[mxd::kMaxKeySlots][44];
+  // keys: 2 per component: rel 0 -> (next, all), rel 1 -> (own, all), rel 2 -> (all, all)
+  mxd::stage_keys(rks, keys, 2 * ncomp);
+  mxd::stage_tables_rep(Tt);
+  constexpr int P = mxd::Lane<T>::kPer;
+  const int64_t nb = (n + P - 1) / P;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < nb * ncomp;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(g / nb);
+    const int64_t b = g - c * nb;
+    const int r = rel.r[c];
+    const int64_t base = (int64_t)c * n;
+    uint64_t al, ah, bl, bh;
+    if (r == 2) {
+      mxd::aes_ctr_rep(rks[2 * c + 1], Tt, na, b, &bl, &bh);
+    } else if (r == 0 || r == 1) {
+      mxd::aes_ctr_rep(rks[2 * c], Tt, n1, b, &al, &ah);
+      mxd::aes_ctr_rep(rks[2 * c + 1], Tt, na, b, &bl, &bh);
+    } else {
+      continue;
+    }
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const int64_t i = b * P + j;
+      if (i >= n) break;
+      const T ra = mxd::pick<T>(bl, bh, j);
+      if (r == 2) {
+        out0[base + i] = ra;  // s1 arrives from the owner
+      } else {
+        const T r1 = mxd::pick<T>(al, ah, j);
+        if (r == 0) {
+          out0[base + i] = kind == MX_CROSS_BOOL ? (T)(x[i] ^ r1 ^ ra) : (T)(x[i] - r1 - ra);
+          out1[base + i] = r1;
+        } else {
+          out0[base + i] = r1;
+          out1[base + i] = ra;
+        }
+      }
+    }
+  }
+}
+
+inline Roles roles_of(const int* r, int ncomp) {
+  Roles o;
+  for (int c = 0; c < 3; ++c) o.r[c] = c < ncomp ? r[c] : -1;
+  return o;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mxh_trunc_party_r0(int words, int64_t n, int m, int ncomp, const int* roles,
+                       const void* s0, const void* s1, void* msg, void* msg_rm, void* out0,
+                       void* out1, const uint32_t* const* slots, const uint64_t* nn,
+                       void* stream) {
+  if (n == 0) return 0;
+  if (ncomp < 1 || ncomp > 3) return -3;
+  const mxd::KeySrc k = mxd::keysrc_slots(slots, 2 * ncomp);
+  const Roles rr = roles_of(roles, ncomp);
+  hipStream_t st = (hipStream_t)stream;
+  if (words == 1) {
+    hipLaunchKernelGGL(k_trunc_party_r0<u64>, dim3(mxd::grid_for((n + 1) / 2 * ncomp)),
+                       dim3(256), 0, st, n, m, rr, (const u64*)s0, (const u64*)s1, (u64*)msg,
+                       (u64*)msg_rm, (u64*)out0, (u64*)out1, k, nn[0], nn[1], nn[2], nn[3],
+                       nn[4], nn[5], ncomp);
+  } else if (words == 2) {
+    hipLaunchKernelGGL(k_trunc_party_r0<u128>, dim3(mxd::grid_for(n * ncomp)), dim3(256), 0, st,
+                       n, m, rr, (const u128*)s0, (const u128*)s1, (u128*)msg, (u64*)msg_rm,
+                       (u128*)out0, (u128*)out1, k, nn[0], nn[1], nn[2], nn[3], nn[4], nn[5],
+                       ncomp);
+  } else {
+    return -2;
+  }
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : -100 - (int)e;
+}
+
+int mxh_trunc_party_r1(int words, int64_t n, int m, int ncomp, const int* roles,
+                       const void* msg, const void* rmk, const void* rrt, const void* rrm,
+                       void* w, void* out0, void* out1, const uint32_t* const* slots,
+                       const uint64_t* nn, void* stream) {
+  if (n == 0) return 0;
+  if (ncomp < 1 || ncomp > 3) return -3;
+  const mxd::KeySrc k = mxd::keysrc_slots(slots, 2 * ncomp);
+  const Roles rr = roles_of(roles, ncomp);
+  hipStream_t st = (hipStream_t)stream;
+  if (words == 1) {
+    hipLaunchKernelGGL(k_trunc_party_r1<u64>, dim3(mxd::grid_for((n + 1) / 2 * ncomp)),
+                       dim3(256), 0, st, n, m, rr, (const u64*)msg, (const u64*)rmk,
+                       (const u64*)rrt, (const u64*)rrm, (u64*)w, (u64*)out0, (u64*)out1, k,
+                       nn[2], nn[3], nn[4], nn[5], ncomp);
+  } else if (words == 2) {
+    hipLaunchKernelGGL(k_trunc_party_r1<u128>, dim3(mxd::grid_for(n * ncomp)), dim3(256), 0, st,
+                       n, m, rr, (const u128*)msg, (const u128*)rmk, (const u128*)rrt,
+                       (const u64*)rrm, (u128*)w, (u128*)out0, (u128*)out1, k, nn[2], nn[3],
+                       nn[4], nn[5], ncomp);
+  } else {
+    return -2;
+  }
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : -100 - (int)e;
+}
+
+int mxh_share_party(int kind, int words, int64_t n, int ncomp, const int* rel, const void* x,
+                    void* out0, void* out1, const uint32_t* const* slots, uint64_t n1,
+                    uint64_t na, void* stream) {
+  if (n == 0) return 0;
+  if (ncomp < 1 || ncomp > 3) return -3;
+  const mxd::KeySrc k = mxd::keysrc_slots(slots, 2 * ncomp);
+  const Roles rr = roles_of(rel, ncomp);
+  hipStream_t st = (hipStream_t)stream;
+  switch (words) {
+    case 0:
+      hipLaunchKernelGGL(k_share_party<uint8_t>, dim3(mxd::grid_for((n + 15) / 16 * ncomp)),
+                         dim3(256), 0, st, kind, n, rr, (const uint8_t*)x, (uint8_t*)out0,
+                         (uint8_t*)out1, k, n1, na, ncomp);
+      break;
+    case 1:
+      hipLaunchKernelGGL(k_share_party<u64>, dim3(mxd::grid_for((n + 1) / 2 * ncomp)), dim3(256),
+                         0, st, kind, n, rr, (const u64*)x, (u64*)out0, (u64*)out1, k, n1, na,
+                         ncomp);
+      break;
+    case 2:
+      hipLaunchKernelGGL(k_share_party<u128>, dim3(mxd::grid_for(n * ncomp)), dim3(256), 0, st,
+                         kind, n, rr, (const u128*)x, (u128*)out0, (u128*)out1, k, n1, na, ncomp);
+      break;
+    default:
+      return -2;
+  }
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : -100 - (int)e;
+}
+
+}  // extern "C"

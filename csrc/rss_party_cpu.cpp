@@ -1,0 +1,215 @@
+// Host versions of the per-party protocol kernels (rss_party.hip) and the C ABI entry
+// points that dispatch host / device.  Key slots are MX_KEY_SLOT_WORDS-word images whose
+// first four words are the raw AES key.
+#include <functional>
+#include <vector>
+
+#include "moosex.h"
+#include "rss_fused.h"
+
+void mx_cpu_prf_range(const uint8_t* key, uint64_t nonce, int words, int64_t i0, int64_t n,
+                      void* out);
+void mx_cpu_parallel_for(int64_t n, int64_t grain,
+                         const std::function<void(int64_t, int64_t)>& f);
+
+extern "C" {
+int mxh_trunc_party_r0(int words, int64_t n, int m, int ncomp, const int* roles,
+                       const void* s0, const void* s1, void* msg, void* msg_rm, void* out0,
+                       void* out1, const uint32_t* const* slots, const uint64_t* nn,
+                       void* stream);
+int mxh_trunc_party_r1(int words, int64_t n, int m, int ncomp, const int* roles,
+                       const void* msg, const void* rmk, const void* rrt, const void* rrm,
+                       void* w, void* out0, void* out1, const uint32_t* const* slots,
+                       const uint64_t* nn, void* stream);
+int mxh_share_party(int kind, int words, int64_t n, int ncomp, const int* rel, const void* x,
+                    void* out0, void* out1, const uint32_t* const* slots, uint64_t n1,
+                    uint64_t na, void* stream);
+}
+
+namespace {
+
+using u64 = uint64_t;
+using u128 = unsigned __int128;
+
+const uint8_t* key_of(const uint32_t* slot) { return (const uint8_t*)slot; }
+
+// chunked element loop with up to six PRF streams per chunk
+template <class T, class F>
+void for_chunks(int64_t n, F&& f) {
+  mx_cpu_parallel_for(n, 1 << 12, [&](int64_t s, int64_t e) {
+    const int64_t CH = 512;
+    for (int64_t c = s; c < e; c += CH) f(c, std::min(CH, e - c));
+  });
+}
+
+template <class T>
+void prf(const uint32_t* slot, uint64_t nonce, int64_t i0, int64_t len, T* out) {
+  const int words = sizeof(T) == 1 ? 0 : (int)(sizeof(T) / 8);
+  mx_cpu_prf_range(key_of(slot), nonce, words, i0, len, out);
+}
+
+template <class T>
+int trunc_r0(int64_t n, int m, int ncomp, const int* roles, const T* s0, const T* s1, T* msg,
+             u64* msg_rm, T* out0, T* out1, const uint32_t* const* slots, const uint64_t* nn) {
+  for (int c = 0; c < ncomp; ++c) {
+    const int role = roles[c];
+    const uint32_t* own = slots[2 * c];
+    const uint32_t* nxt = slots[2 * c + 1];
+    const int64_t base = (int64_t)c * n;
+    for_chunks<T>(n, [&](int64_t i0, int64_t len) {
+      std::vector<T> a(len), b(len), t(len), mm(len), z0(len), z2(len);
+      if (role == 0) {
+        prf<T>(own, nn[0], i0, len, a.data());
+        for (int64_t q = 0; q < len; ++q) {
+          const int64_t i = base + i0 + q;
+          msg[i] = mxf::trunc_mask0<T>(s0[i], s1[i], a[q]);
+        }
+      } else if (role == 1) {
+        prf<T>(nxt, nn[1], i0, len, a.data());
+        for (int64_t q = 0; q < len; ++q) {
+          const int64_t i = base + i0 + q;
+          msg[i] = s1[i] + a[q];
+        }
+      } else if (role == 2) {
+        prf<T>(nxt, nn[0], i0, len, a.data());
+        prf<T>(own, nn[1], i0, len, b.data());
+        prf<T>(nxt, nn[2], i0, len, t.data());
+        prf<T>(nxt, nn[3], i0, len, mm.data());
+        prf<T>(nxt, nn[4], i0, len, z0.data());
+        prf<T>(own, nn[5], i0, len, z2.data());
+        for (int64_t q = 0; q < len; ++q) {
+          const int64_t i = base + i0 + q;
+          mxf::trunc_dealer<T>(a[q], b[q], t[q], mm[q], m, &msg[i], &msg_rm[i]);
+          out0[i] = z2[q];
+          out1[i] = z0[q];
+        }
+      }
+    });
+  }
+  return 0;
+}
+
+template <class T>
+int trunc_r1(int64_t n, int m, int ncomp, const int* roles, const T* msg, const T* rmk,
+             const T* rrt, const u64* rrm, T* w, T* out0, T* out1,
+             const uint32_t* const* slots, const uint64_t* nn) {
+  for (int c = 0; c < ncomp; ++c) {
+    const int role = roles[c];
+    const int64_t base = (int64_t)c * n;
+    for_chunks<T>(n, [&](int64_t i0, int64_t len) {
+      std::vector<T> t(len), mm(len), z(len);
+      if (role == 0) {
+        const uint32_t* k0 = slots[2 * c];
+        prf<T>(k0, nn[2], i0, len, t.data());
+        prf<T>(k0, nn[3], i0, len, mm.data());
+        prf<T>(k0, nn[4], i0, len, z.data());
+        for (int64_t q = 0; q < len; ++q) {
+          const int64_t i = base + i0 + q;
+          const T y0 = mxf::trunc_y<T>(msg[i] + rmk[i], t[q], mm[q], m, true);
+          w[i] = y0 - z[q];
+          out0[i] = z[q];
+        }
+      } else if (role == 1) {
+        prf<T>(slots[2 * c + 1], nn[5], i0, len, z.data());
+        for (int64_t q = 0; q < len; ++q) {
+          const int64_t i = base + i0 + q;
+          const T y1 = mxf::trunc_y<T>(msg[i] + rmk[i], rrt[i], (T)rrm[i], m, false);
+          w[i] = y1 - z[q];
+          out1[i] = z[q];
+        }
+      }
+    });
+  }
+  return 0;
+}
+
+template <class T>
+int share_party(int kind, int64_t n, int ncomp, const int* rel, const T* x, T* out0, T* out1,
+                const uint32_t* const* slots, uint64_t n1, uint64_t na) {
+  for (int c = 0; c < ncomp; ++c) {
+    const int r = rel[c];
+    const int64_t base = (int64_t)c * n;
+    if (r < 0 || r > 2) continue;
+    for_chunks<T>(n, [&](int64_t i0, int64_t len) {
+      std::vector<T> a(len), b(len);
+      prf<T>(slots[2 * c + 1], na, i0, len, b.data());
+      if (r != 2) prf<T>(slots[2 * c], n1, i0, len, a.data());
+      for (int64_t q = 0; q < len; ++q) {
+        const int64_t i = base + i0 + q;
+        if (r == 2) {
+          out0[i] = b[q];
+        } else if (r == 0) {
+          const T xv = x[i0 + q];
+          out0[i] = kind == MX_CROSS_BOOL ? (T)(xv ^ a[q] ^ b[q]) : (T)(xv - a[q] - b[q]);
+          out1[i] = a[q];
+        } else {
+          out0[i] = a[q];
+          out1[i] = b[q];
+        }
+      }
+    });
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mx_trunc_party_r0(int dev, int words, int64_t n, int m, int ncomp, const int* roles,
+                      const void* s0, const void* s1, void* msg, void* msg_rm, void* out0,
+                      void* out1, const uint32_t* const* slots, const uint64_t* nn,
+                      void* stream) {
+  if (m < 1 || m > 63) return -3;
+  if (dev)
+    return mxh_trunc_party_r0(words, n, m, ncomp, roles, s0, s1, msg, msg_rm, out0, out1,
+                              slots, nn, stream);
+  if (words == 1)
+    return trunc_r0<u64>(n, m, ncomp, roles, (const u64*)s0, (const u64*)s1, (u64*)msg,
+                         (u64*)msg_rm, (u64*)out0, (u64*)out1, slots, nn);
+  if (words == 2)
+    return trunc_r0<u128>(n, m, ncomp, roles, (const u128*)s0, (const u128*)s1, (u128*)msg,
+                          (u64*)msg_rm, (u128*)out0, (u128*)out1, slots, nn);
+  return -2;
+}
+
+int mx_trunc_party_r1(int dev, int words, int64_t n, int m, int ncomp, const int* roles,
+                      const void* msg, const void* rmk, const void* rrt, const void* rrm,
+                      void* w, void* out0, void* out1, const uint32_t* const* slots,
+                      const uint64_t* nn, void* stream) {
+  if (m < 1 || m > 63) return -3;
+  if (dev)
+    return mxh_trunc_party_r1(words, n, m, ncomp, roles, msg, rmk, rrt, rrm, w, out0, out1,
+                              slots, nn, stream);
+  if (words == 1)
+    return trunc_r1<u64>(n, m, ncomp, roles, (const u64*)msg, (const u64*)rmk,
+                         (const u64*)rrt, (const u64*)rrm, (u64*)w, (u64*)out0, (u64*)out1,
+                         slots, nn);
+  if (words == 2)
+    return trunc_r1<u128>(n, m, ncomp, roles, (const u128*)msg, (const u128*)rmk,
+                          (const u128*)rrt, (const u64*)rrm, (u128*)w, (u128*)out0,
+                          (u128*)out1, slots, nn);
+  return -2;
+}
+
+int mx_share_party(int dev, int kind, int words, int64_t n, int ncomp, const int* rel,
+                   const void* x, void* out0, void* out1, const uint32_t* const* slots,
+                   uint64_t n1, uint64_t na, void* stream) {
+  if (dev)
+    return mxh_share_party(kind, words, n, ncomp, rel, x, out0, out1, slots, n1, na, stream);
+  switch (words) {
+    case 0:
+      return share_party<uint8_t>(kind, n, ncomp, rel, (const uint8_t*)x, (uint8_t*)out0,
+                                  (uint8_t*)out1, slots, n1, na);
+    case 1:
+      return share_party<u64>(kind, n, ncomp, rel, (const u64*)x, (u64*)out0, (u64*)out1,
+                              slots, n1, na);
+    case 2:
+      return share_party<u128>(kind, n, ncomp, rel, (const u128*)x, (u128*)out0, (u128*)out1,
+                               slots, n1, na);
+    default:
+      return -2;
+  }
+}
+
+}  // extern "C"

@@ -93,6 +93,26 @@ _SIGS = {
         c_int,
         [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_u64, c_u64, c_vp],
     ),
+    "mx_trunc_party_r0": (
+        c_int,
+        [c_int, c_int, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+         c_vp, c_vp],
+    ),
+    "mx_trunc_party_r1": (
+        c_int,
+        [c_int, c_int, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+         c_vp, c_vp, c_vp],
+    ),
+    "mx_share_party": (
+        c_int,
+        [c_int, c_int, c_int, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_u64, c_u64, c_vp],
+    ),
+    "mx_gemm_b_bytes": (c_i64, [c_int, c_i64, c_i64, c_i64, c_int]),
+    "mx_gemm_prep_b": (c_int, [c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_int, c_vp, c_vp]),
+    "mx_gemm_with_b": (
+        c_int,
+        [c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_int, c_vp],
+    ),
     "mx_share3": (
         c_int,
         [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_u64, c_u64, c_vp],

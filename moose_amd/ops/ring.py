@@ -647,6 +647,46 @@ def dot(x: RT, y: RT, nb=0) -> RT:
     return reshape(out, oshape, nb) if oshape != (M, N) else out
 
 
+class PreparedCross:
+    """The B' = [y0 + y1; y0] operand of a stacked RSS cross GEMM, limb-split once on the
+    device (mx_gemm_prep_b) so that several row blocks of x reuse it (dot_cross_rows).  On
+    the host, or when K is too long for one exact chunk, it just keeps y0, y1."""
+
+    def __init__(self, y0: RT, y1: RT):
+        self.y0, self.y1, self.bits = y0, y1, y0.bits
+        self.batch, self.K, self.N = y0.shape[0], y0.shape[1], y0.shape[2]
+        self.lb = None
+        if y0.data.is_cuda:
+            w = _words(self.bits)
+            nbytes = nat.lib().mx_gemm_b_bytes(w, self.batch, self.N, self.K, 1)
+            if nbytes > 0:
+                d0, d1 = y0.data.contiguous(), y1.data.contiguous()
+                self.lb = torch.empty(nbytes, dtype=torch.uint8, device=d0.device)
+                nat.check(nat.lib().mx_gemm_prep_b(
+                    w, self.batch, self.K, self.N, nat.ptr(d0), nat.ptr(d1), 1,
+                    nat.ptr(self.lb), nat.stream_of(d0)), "gemm_prep_b")
+
+
+def dot_cross_rows(x0: RT, x1: RT, r0: int, r1: int, pb: PreparedCross) -> RT:
+    """Rows [r0, r1) of the stacked cross GEMM x0.(y0+y1) + x1.y0 for x* [batch, M, K]
+    (no copy of the row block on the device)."""
+    if pb.lb is None:
+        rows = lambda t: RT(t.data[:, r0:r1], t.bits)  # noqa: E731
+        return dot_cross(rows(x0), rows(x1), pb.y0, pb.y1, nb=1)
+    batch, M, K = x0.shape
+    d0, d1 = x0.data, x1.data
+    if not (d0.is_contiguous() and d1.is_contiguous()):
+        d0, d1 = d0.contiguous(), d1.contiguous()
+    el = 2 if pb.bits == 128 else 1  # int64 words per element
+    out = empty((batch, r1 - r0, pb.N), pb.bits, d0.device)
+    off = r0 * K * el * 8
+    nat.check(nat.lib().mx_gemm_with_b(
+        _words(pb.bits), batch, r1 - r0, pb.N, K, ctypes.c_void_p(d0.data_ptr() + off),
+        ctypes.c_void_p(d1.data_ptr() + off), M * K, 1,
+        nat.ptr(pb.lb), nat.ptr(out.data), 0, nat.stream_of(d0)), "gemm_with_b")
+    return out
+
+
 def dot_cross(x0: RT, x1: RT, y0: RT, y1: RT, nb=0) -> RT:
     """RSS cross terms of a matrix product: x0.(y0+y1) + x1.y0 in one K-doubled GEMM."""
     bits = x0.bits
@@ -948,3 +988,61 @@ def zero_share(kind: str, shape, bits, keys, nonce: int, nparties: int, device) 
         "zero_share",
     )
     return out
+
+
+# ---------------------------------------------------------------------------
+# per-party protocol rounds (parties of a session on different GPUs)
+# ---------------------------------------------------------------------------
+def _roles_arr(roles):
+    return (ctypes.c_int * len(roles))(*roles)
+
+
+def _slots_arr(slots):
+    return (ctypes.c_void_p * len(slots))(*slots)
+
+
+def _nonces_arr(nonces):
+    return (ctypes.c_uint64 * len(nonces))(*[v & MASK64 for v in nonces])
+
+
+def trunc_party_r0(s0: RT, s1: RT, m: int, roles, slots, nonces):
+    """Round 0 of the per-party TruncPr (mx_trunc_party_r0) on stacked [ncomp, ...] shares.
+    Returns (msg, msg_rm, out0, out1): outgoing messages and the (partly filled) new
+    shares."""
+    ncomp = len(roles)
+    d0 = s0.data.contiguous()
+    d1 = s1.data.contiguous()
+    n = math.prod(s0.shape) // ncomp
+    msg, out0, out1 = (torch.empty_like(d0) for _ in range(3))
+    msg_rm = torch.empty((ncomp, n), dtype=torch.int64, device=d0.device)
+    nat.check(nat.lib().mx_trunc_party_r0(
+        nat.dev_of(d0), _words(s0.bits), n, m, ncomp, _roles_arr(roles), nat.ptr(d0),
+        nat.ptr(d1), nat.ptr(msg), nat.ptr(msg_rm), nat.ptr(out0), nat.ptr(out1),
+        _slots_arr(slots), _nonces_arr(nonces), nat.stream_of(d0)), "trunc_party_r0")
+    return msg, msg_rm, out0, out1
+
+
+def trunc_party_r1(msg, rmk, rrt, rrm, out0, out1, bits, m, roles, slots, nonces):
+    """Round 1 (mx_trunc_party_r1): returns w; writes P0's s0 / P1's s1 into out0/out1."""
+    ncomp = len(roles)
+    n = msg.numel() // ncomp // (2 if bits == 128 else 1)
+    w = torch.empty_like(msg)
+    nat.check(nat.lib().mx_trunc_party_r1(
+        nat.dev_of(msg), _words(bits), n, m, ncomp, _roles_arr(roles), nat.ptr(msg),
+        nat.ptr(rmk), nat.ptr(rrt), nat.ptr(rrm), nat.ptr(w), nat.ptr(out0), nat.ptr(out1),
+        _slots_arr(slots), _nonces_arr(nonces), nat.stream_of(msg)), "trunc_party_r1")
+    return w
+
+
+def share_party(kind: str, x: RT, ncomp: int, rel, slots, n1: int, na: int):
+    """Per-component slots of a sharing by member j (mx_share_party); the owner's out0
+    is the message to P_{j+2} (whose out1 it becomes)."""
+    xd = x.data.contiguous()
+    shape = (ncomp,) + tuple(xd.shape)
+    out0 = torch.empty(shape, dtype=xd.dtype, device=xd.device)
+    out1 = torch.empty_like(out0)
+    nat.check(nat.lib().mx_share_party(
+        nat.dev_of(xd), 1 if kind == "bool" else 0, _words(x.bits), x.numel(), ncomp,
+        _roles_arr(rel), nat.ptr(xd), nat.ptr(out0), nat.ptr(out1), _slots_arr(slots),
+        n1 & MASK64, na & MASK64, nat.stream_of(xd)), "share_party")
+    return out0, out1

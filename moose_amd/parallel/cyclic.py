@@ -49,6 +49,7 @@ node so that all N GPUs are busy.
 from __future__ import annotations
 
 import hashlib
+import os
 from typing import Dict
 from typing import List
 from typing import Sequence
@@ -137,9 +138,14 @@ class CyclicSession(StackedSession):
     ks_fused = False
     KEY_SLOTS = 9      # per placement: for each component p: k_p, k_{p+1}, k_all
 
-    def __init__(self, comm: RingComm, offsets: Dict[str, int], device="cpu", seed=None):
+    def __init__(self, comm: RingComm, offsets: Dict[str, int], device="cpu", seed=None,
+                 pipeline_chunks=None):
         super().__init__(device, seed)
         self.comm = comm
+        if pipeline_chunks is None:  # reshares cross GPUs: overlap them with the GEMM
+            pipeline_chunks = int(os.environ.get("MOOSEX_PIPELINE_CHUNKS",
+                                                 "8" if comm.world > 1 else "1"))
+        self.pipeline_chunks = pipeline_chunks
         self.g = comm.rank
         self.N = comm.world
         self.off = dict(offsets)
@@ -296,6 +302,50 @@ class CyclicSession(StackedSession):
     def p_add_zero_share(self, plc, z, kind="arith"):
         return PV(plc, R.rss_cross_kp(kind, z.v, None, None, None, self._pair_ptrs(plc),
                                       self.nonce(plc)))
+
+    # -- per-party protocol rounds (csrc/rss_party.hip) ----------------------------------
+    def party_trunc(self, x, m, nonces):
+        """TruncPr as two per-party kernels + two grouped exchanges (+ one add): component p
+        runs party p's local work of each round (replicated.trunc_pr, generic path), and
+        every message goes straight to the GPU of its destination party."""
+        plc, bits = x.plc, x.bits
+        roles = [0, 1, 2]
+        slots = self._pair_ptrs(plc)
+        o = [self.offset(r) for r in plc.owners]
+        p01, p10, p21 = self._peer(o[1] - o[0]), self._peer(o[0] - o[1]), self._peer(o[1] - o[2])
+        p12 = self._peer(o[2] - o[1])
+        msg, msg_rm, out0, out1 = R.trunc_party_r0(x.s0.v, x.s1.v, m, roles, slots, nonces)
+        # round A, by message type: mk0 P0->P1, mk1 P1->P0, rt1 P2->P1, rm1 P2->P1
+        rmk, rrt, rrm = torch.empty_like(msg), torch.empty_like(msg), torch.empty_like(msg_rm)
+        self.comm.exchange([(msg[0], p01), (msg[1], p10), (msg[2], p21), (msg_rm[2], p21)],
+                           [(rmk[1], p10), (rmk[0], p01), (rrt[1], p12), (rrm[1], p12)])
+        w = R.trunc_party_r1(msg, rmk, rrt, rrm, out0, out1, bits, m, roles, slots, nonces)
+        # round B: w0 P0->P1, w1 P1->P0; then z1 = w0 + w1 at both
+        rw = torch.empty_like(w)
+        self.comm.exchange([(w[0], p01), (w[1], p10)], [(rw[1], p10), (rw[0], p01)])
+        out1[0].copy_(R.binary("add", R.RT(w[0], bits), R.RT(rw[0], bits)).data)
+        out0[1].copy_(R.binary("add", R.RT(w[1], bits), R.RT(rw[1], bits)).data)
+        nb = _nbytes(x.s0.v) // 3
+        self.stats.record_round(3 * nb)
+        self.stats.record_round(2 * nb)
+        return PV(plc, R.RT(out0, bits)), PV(plc, R.RT(out1, bits))
+
+    def party_share(self, plc, x, j, kind, n1, na):
+        """Input sharing by member j: one kernel for every component's slots, then the
+        owner's masked x_j goes to P_{j+2} (received straight into its s1)."""
+        bits = x.v.bits
+        rel = [(c - j) % 3 for c in range(3)]
+        slots = []
+        for c in range(3):
+            w = {0: (1, 2), 1: (0, 2), 2: (2, 2)}[rel[c]]
+            slots += [self._slot(plc, c, w[0]), self._slot(plc, c, w[1])]
+        out0, out1 = R.share_party(kind, x.v, 3, rel, slots, n1, na)
+        o = [self.offset(r) for r in plc.owners]
+        j2 = (j + 2) % 3
+        self.comm.exchange([(out0[j], self._peer(o[j2] - o[j]))],
+                           [(out1[j2], self._peer(o[j] - o[j2]))])
+        self.stats.record_send(x.host, plc.owners[j2], _nbytes(x.v))
+        return PV(plc, R.RT(out0, bits)), PV(plc, R.RT(out1, bits))
 
     # the single-GPU fused variants read other parties' data in-kernel: never used here
     p_mul_reshare = None

@@ -113,8 +113,7 @@ def dot(sess, x, y, px=None, py=None, f=None):
         z = rep.dot_public(sess, x.t, py)
         base = x
     else:
-        z = rep.dot(sess, x.t, y.t)
-        base = x
+        return _with(x, rep.dot_trunc(sess, x.t, y.t, f if f is not None else x.frac))
     return _with(base, rep.trunc_pr(sess, z, f if f is not None else base.frac))
 
 

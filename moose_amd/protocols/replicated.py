@@ -34,6 +34,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+import torch
+
 from moose_amd.ir.computation import ReplicatedPlacement
 from moose_amd.ops import ring as R
 from moose_amd.runtime.session import HV
@@ -79,6 +81,10 @@ def share(sess, plc, x: HV, kind="arith") -> RepTensor:
         n1, na = sess.nonce(plc), sess.nonce(plc)
         if getattr(sess, "fused", False):
             s0, s1 = sess.fused_share(plc, x, j, kind, n1, na)
+            return RepTensor(plc, bits, kind, s0, s1)
+        party = getattr(sess, "party_share", None)
+        if party is not None and bits in (64, 128):
+            s0, s1 = party(plc, x, j, kind, n1, na)
             return RepTensor(plc, bits, kind, s0, s1)
         # slot_{j+1} = PRF(k_{j+1}) [P_j, P_{j+1}]; slot_{j+2} = PRF(k_all); slot_j = rest
         r1_j = sess.h_prf(plc, o[j], j1, shape, bits, n1)
@@ -275,6 +281,68 @@ def dot(sess, x: RepTensor, y: RepTensor) -> RepTensor:
         return _reshare(sess, x.plc, z, x.bits, x.kind)
 
 
+def _rows(pv: PV, r0: int, r1: int) -> PV:
+    """Rows [r0, r1) of a stacked party vector holding a 2-D tensor per party (a view)."""
+    v = pv.v
+    return PV(pv.plc, R.RT(v.data[:, r0:r1], v.bits))
+
+
+def _cat_rows(pvs) -> PV:
+    return PV(pvs[0].plc, R.RT(torch.cat([p.v.data for p in pvs], dim=1), pvs[0].v.bits))
+
+
+def dot_trunc(sess, x: RepTensor, y: RepTensor, m: int) -> RepTensor:
+    """trunc_pr(dot(x, y), m) -- the fixed-point matrix product.
+
+    Sessions whose reshares cross GPUs set ``pipeline_chunks`` > 1: the product of 2-D
+    operands then runs as a row-chunked pipeline.  The GEMM of row chunk c+1 runs on the
+    main HIP stream while chunk c's zero share, reshare and TruncPr -- row-local, with all
+    their RCCL exchanges -- run on the session's side stream, so the inter-GPU traffic of
+    the dot hides behind the MFMA work (chunked RSS pipelines).  Every chunk is
+    its own protocol instance (own nonces): a valid sharing of the same product, and two
+    sessions that chunk alike produce bitwise-equal shares.  The y operand is limb-split
+    once (p_prepare_cross) and x row blocks are read in place."""
+    chunks = getattr(sess, "pipeline_chunks", 1)
+    nchunk = 1
+    if chunks > 1:
+        xs, ys = x.s0.v.shape, y.s0.v.shape  # stacked: (3, M, K), (3, K, N)
+        if len(xs) == 3 and len(ys) == 3:
+            M = xs[1]
+            nchunk = min(chunks, M // 128)
+    if nchunk <= 1:
+        return trunc_pr(sess, dot(sess, x, y), m)
+    with span("rep.dot_trunc_pipelined"):
+        plc, bits, kind = x.plc, x.bits, x.kind
+        bounds = [M * c // nchunk for c in range(nchunk + 1)]
+        data = x.s0.v.data
+        cuda = data.is_cuda
+        main = torch.cuda.current_stream(data.device) if cuda else None
+        side = sess.side_stream() if cuda else None
+        parts = []
+        prepared = sess.p_prepare_cross(plc, y.s0, y.s1)
+        for c in range(nchunk):
+            r0, r1 = bounds[c], bounds[c + 1]
+            v = sess.p_dot_cross_rows(plc, x.s0, x.s1, r0, r1, prepared)
+            if not cuda:
+                z = sess.p_add_zero_share(plc, v, kind)
+                parts.append(trunc_pr(sess, _reshare(sess, plc, z, bits, kind), m))
+                continue
+            ev = torch.cuda.Event()
+            ev.record(main)
+            with torch.cuda.stream(side):
+                side.wait_event(ev)
+                v.v.data.record_stream(side)
+                z = sess.p_add_zero_share(plc, v, kind)
+                t = trunc_pr(sess, _reshare(sess, plc, z, bits, kind), m)
+            for pv in (t.s0, t.s1):
+                pv.v.data.record_stream(main)
+            parts.append(t)
+        if cuda:
+            main.wait_stream(side)
+        return RepTensor(plc, bits, kind, _cat_rows([t.s0 for t in parts]),
+                         _cat_rows([t.s1 for t in parts]))
+
+
 # ---------------------------------------------------------------------------
 # probabilistic truncation (dealer-assisted, P2 = dealer)
 # ---------------------------------------------------------------------------
@@ -296,6 +364,11 @@ def trunc_pr(sess, x: RepTensor, m: int) -> RepTensor:
         if getattr(sess, "fused", False):
             n0, n2 = sess.nonce(plc), sess.nonce(plc)
             s0, s1 = sess.fused_trunc_pr(x, m, (nr0, nr1, nt, nm, n0, n2))
+            return RepTensor(plc, bits, "arith", s0, s1)
+        party = getattr(sess, "party_trunc", None)
+        if party is not None and bits in (64, 128) and m <= 63:
+            n0, n2 = sess.nonce(plc), sess.nonce(plc)
+            s0, s1 = party(x, m, (nr0, nr1, nt, nm, n0, n2))
             return RepTensor(plc, bits, "arith", s0, s1)
         from moose_amd.protocols import additive
 

@@ -133,6 +133,16 @@ class StackedSession(Session):
         """Run on a caller-provided key table (graph capture: a frozen, refreshed one)."""
         self._keytable = kt
 
+    # rows per pipelined dot+TruncPr (protocols/replicated.dot_trunc); 1 = no pipelining
+    pipeline_chunks = 1
+
+    def side_stream(self):
+        """The HIP stream that pipelined protocol tails run on (created on first use)."""
+        st = getattr(self, "_side", None)
+        if st is None:
+            st = self._side = torch.cuda.Stream(self.device)
+        return st
+
     def setup(self, plc) -> int:
         base = self._keys.get(plc)
         if base is None:
@@ -311,6 +321,13 @@ class StackedSession(Session):
         s0, s1 = R.add_zs3(v, r)
         self.stats.record_round(_nbytes(s0))
         return PV(plc, s0), PV(plc, s1)
+
+    def p_prepare_cross(self, plc, y0, y1):
+        """The B' operand of p_dot_cross, limb-split once for several row blocks."""
+        return R.PreparedCross(y0.v, y1.v)
+
+    def p_dot_cross_rows(self, plc, x0, x1, r0, r1, prepared):
+        return PV(plc, R.dot_cross_rows(x0.v, x1.v, r0, r1, prepared))
 
     def p_dot_cross(self, plc, x0, x1, y0, y1):
         return PV(plc, R.dot_cross(x0.v, x1.v, y0.v, y1.v, nb=1))

@@ -33,8 +33,16 @@ def _data(session, bits):
     return R.encode(v, 23, bits)
 
 
-def _program(sess, xb, ya):
-    """share (owners b and a), mul + trunc, dot, bit decomposition, reveal to c."""
+def _mats(session, bits):
+    """(256 x 16) . (16 x 8) operands for the row-chunked dot+TruncPr pipeline."""
+    a = torch.linspace(-3, 3, 256 * 16, dtype=torch.float64).reshape(256, 16) + 0.1 * session
+    b = torch.linspace(-2, 2, 16 * 8, dtype=torch.float64).reshape(16, 8) - 0.05 * session
+    return R.encode(a, 23, bits), R.encode(b, 23, bits)
+
+
+def _program(sess, xb, ya, mb, ma):
+    """share (owners b and a), mul + trunc, dot, bit decomposition, reveal to c; a
+    pipelined fixed-point matrix product (2 row chunks) revealed to c."""
     from moose_amd.protocols import replicated as rep
 
     X = rep.share(sess, PLC, xb)
@@ -43,10 +51,12 @@ def _program(sess, xb, ya):
     D = rep.dot(sess, rep.local(sess, X, "Reshape", shape=(8, 12)),
                 rep.local(sess, Y, "Reshape", shape=(12, 8)))
     B = rep.bit_decompose(sess, X)
+    DT = rep.dot_trunc(sess, rep.share(sess, PLC, mb), rep.share(sess, PLC, ma), 23)
     out = rep.reveal(sess, M, "c")
-    tensors = [t.s0.v.data.clone() for t in (X, Y, M, D, B)] + [
-        t.s1.v.data.clone() for t in (X, Y, M, D, B)]
-    return tensors, out.v.data.clone()
+    dt = rep.reveal(sess, DT, "c")
+    tensors = [t.s0.v.data.clone() for t in (X, Y, M, D, B, DT)] + [
+        t.s1.v.data.clone() for t in (X, Y, M, D, B, DT)]
+    return tensors, (out.v.data.clone(), dt.v.data.clone())
 
 
 def _worker(rank, world, port, q, device="cpu"):
@@ -57,14 +67,19 @@ def _worker(rank, world, port, q, device="cpu"):
     from moose_amd.runtime.session import HV
 
     sess = CyclicSession(RingComm(rank, world, device), {"a": 0, "b": 1, "c": 2}, seed=SEED,
-                         device=device)
+                         device=device, pipeline_chunks=4)
     res = {}
     for bits in (64, 128):
         xd, yd = _data(sess.session_of("b"), bits), _data(100 + sess.session_of("a"), bits)
         xb = HV("b", R.RT(R.to_device(xd.data, device), bits))
         ya = HV("a", R.RT(R.to_device(yd.data, device), bits))
-        ts, out = _program(sess, xb, ya)
-        res[bits] = ([t.cpu().numpy() for t in ts], out.cpu().numpy(), sess.session_of("c"))
+        ma_, _ = _mats(sess.session_of("b"), bits)
+        _, mb_ = _mats(sess.session_of("a"), bits)
+        mb = HV("b", R.RT(R.to_device(ma_.data, device), bits))
+        ma = HV("a", R.RT(R.to_device(mb_.data, device), bits))
+        ts, outs = _program(sess, xb, ya, mb, ma)
+        res[bits] = ([t.cpu().numpy() for t in ts], [o.cpu().numpy() for o in outs],
+                     sess.session_of("c"))
     keys = {s: sess.session_keys(PLC, s) for s in range(world)}
     q.put((rank, res, keys, sess.comm.messages))
     dist.barrier()
@@ -78,13 +93,15 @@ def _stacked_reference(keys, session):
 
     s = StackedSession("cpu", seed=1)
     s.fused = False
+    s.pipeline_chunks = 4
     base = s.setup(PLC)
     s.keytable._write(base, keys)
     out = {}
     for bits in (64, 128):
         xb = HV("b", _data(session, bits))
         ya = HV("a", _data(100 + session, bits))
-        out[bits] = _program(s, xb, ya)
+        ma_, mb_ = _mats(session, bits)
+        out[bits] = _program(s, xb, ya, HV("b", ma_), HV("a", mb_))
     return out
 
 
@@ -125,13 +142,19 @@ def _run(world, device):
                     s = (g - p) % world  # component p of rank g = party p of session g - p
                     ref = refs[(s, bits)][0][i][p].numpy()
                     assert np.array_equal(t[p], ref), (world, g, bits, i, p)
-            # carole's revealed product on rank g is session g - 2's
-            assert np.array_equal(out, refs[(s_c, bits)][1].numpy())
+            # carole's revealed products on rank g are session g - 2's
+            for o, r in zip(out, refs[(s_c, bits)][1]):
+                assert np.array_equal(o, r.numpy())
             x = _data(s_c, bits)
             y = _data(100 + s_c, bits)
             want = R.decode(x, 23) * R.decode(y, 23)
-            np.testing.assert_allclose(R.decode(R.RT(torch.from_numpy(out), bits), 23).numpy(),
-                                       want.numpy(), atol=1e-5)
+            np.testing.assert_allclose(
+                R.decode(R.RT(torch.from_numpy(out[0]), bits), 23).numpy(), want.numpy(),
+                atol=1e-5)
+            ma_, mb_ = _mats(s_c, bits)
+            want = R.decode(ma_, 23).numpy() @ R.decode(mb_, 23).numpy()
+            np.testing.assert_allclose(
+                R.decode(R.RT(torch.from_numpy(out[1]), bits), 23).numpy(), want, atol=1e-4)
 
 
 @pytest.mark.parametrize("world", [2, 3, 4])

@@ -259,3 +259,67 @@ def test_rss_cross_kp_matches_host(bits, kind):
     one = R.rss_cross(kind, R.RT(x0.data[1], bits), R.RT(x1.data[1], bits),
                       R.RT(y0.data[1], bits), R.RT(y1.data[1], bits), keys[2:4], 99, 1)
     assert torch.equal(one.data, host.data[1])
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+def test_dot_cross_rows_prepared_b(bits):
+    """Row blocks through the prepared-B GEMM (pipelined dot) == rows of the full product."""
+    xs = [rand_rt((3, 300, 96), bits, 80 + i) for i in range(2)]
+    ys = [rand_rt((3, 96, 80), bits, 90 + i) for i in range(2)]
+    full = R.dot_cross(*xs, *ys, nb=1)
+    g = [gpu(t) for t in xs + ys]
+    pb = R.PreparedCross(g[2], g[3])
+    assert pb.lb is not None
+    for r0, r1 in ((0, 75), (75, 150), (150, 300)):
+        part = R.dot_cross_rows(g[0], g[1], r0, r1, pb)
+        assert torch.equal(part.data.cpu(), full.data[:, r0:r1])
+
+
+def _slot_tables(n):
+    from moose_amd.runtime.keys import KeyTable
+
+    keys = [bytes([(13 * i + 5) % 256] * 16) for i in range(n)]
+    tabs = []
+    for dev in ("cpu", "cuda"):
+        kt = KeyTable(dev)
+        base = kt.alloc(n)
+        kt._write(base, keys)
+        tabs.append(kt)
+    return tabs, [[t.ptr(base + i) for i in range(n)] for t in tabs]
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+def test_trunc_party_rounds_match_host(bits):
+    """Per-party TruncPr round kernels (cyclic layout): device == host for every output."""
+    tabs, (hs, ds) = _slot_tables(6)  # tabs keeps both tables alive
+    nonces = [11, 12, 13, 14, 15, 16]
+    s0, s1 = rand_rt((3, 777), bits, 100), rand_rt((3, 777), bits, 101)
+    h = R.trunc_party_r0(s0, s1, 23, [0, 1, 2], hs, nonces)
+    d = R.trunc_party_r0(gpu(s0), gpu(s1), 23, [0, 1, 2], ds, nonces)
+    assert torch.equal(h[0], d[0].cpu())  # every role's outgoing message
+    for a, b in zip(h[1:], d[1:]):  # msg_rm and the new shares: the dealer's component only
+        assert torch.equal(a[2], b[2].cpu())
+    rmk, rrt = rand_rt((3, 777), bits, 102), rand_rt((3, 777), bits, 103)
+    rrm = torch.randint(0, 2**62, (3, 777), dtype=torch.int64)
+    out_h = [t.clone() for t in h[2:]]
+    out_d = [t.clone() for t in d[2:]]
+    wh = R.trunc_party_r1(h[0], rmk.data, rrt.data, rrm, *out_h, bits, 23, [0, 1, 2], hs, nonces)
+    wd = R.trunc_party_r1(d[0], rmk.data.cuda(), rrt.data.cuda(), rrm.cuda(), *out_d, bits, 23,
+                          [0, 1, 2], ds, nonces)
+    assert torch.equal(wh[:2], wd.cpu()[:2])
+    assert torch.equal(out_h[0][:1], out_d[0].cpu()[:1])
+    assert torch.equal(out_h[1][1:2], out_d[1].cpu()[1:2])
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+@pytest.mark.parametrize("j", [0, 1, 2])
+def test_share_party_matches_host(bits, j):
+    tabs, (hs, ds) = _slot_tables(6)
+    x = rand_rt((500,), bits, 110 + j)
+    rel = [(c - j) % 3 for c in range(3)]
+    h = R.share_party("arith", x, 3, rel, hs, 21, 22)
+    d = R.share_party("arith", gpu(x), 3, rel, ds, 21, 22)
+    j2 = (j + 2) % 3
+    assert torch.equal(h[0], d[0].cpu())
+    keep = [c for c in range(3) if c != j2]  # the j+2 component's s1 arrives by message
+    assert torch.equal(h[1][keep], d[1].cpu()[keep])
