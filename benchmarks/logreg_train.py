@@ -37,13 +37,14 @@ LEARNING_RATE = 0.1
 MOMENTUM = 0.9
 FIXED = pm.fixed(24, 40)
 
-# reference wall times (seconds, mean of 3) from BASELINE.md, keyed (batch_size, n_iter)
+# the reference's published moose wall times (seconds), keyed (batch_size, n_iter):
+# benchmarks/README.md:44-48 of the reference, as tabulated in BASELINE.md (main table).
+# The reference published no batch-256 row.
 REFERENCE_S = {
-    (128, 10): 1.316, (128, 50): 6.424, (128, 100): 12.788,
-    (256, 10): 1.498, (256, 50): 7.367, (256, 100): 14.770,
-    (512, 10): 1.838, (512, 50): 9.101, (512, 100): 18.111,
-    (1024, 10): 2.558, (1024, 50): 12.652, (1024, 100): 25.359,
-    (2048, 10): 3.951, (2048, 50): 19.728, (2048, 100): 39.318,
+    (128, 10): 1.316, (128, 50): 7.091, (128, 100): 14.385,
+    (512, 10): 1.981, (512, 50): 10.134, (512, 100): 20.819,
+    (1024, 10): 2.963, (1024, 50): 15.033, (1024, 100): 31.017,
+    (2048, 10): 4.730, (2048, 50): 24.266, (2048, 100): 63.100,
 }
 
 

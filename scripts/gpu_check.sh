@@ -33,7 +33,7 @@ if [[ $STEPS == *multi* || $STEPS == all ]]; then
 fi
 if [[ $STEPS == *logreg* ]]; then
   rm -f gpurun_out/logreg.jsonl
-  for it in 10 50 100; do for bs in 128 256 512 1024 2048; do
+  for it in 10 50 100; do for bs in 128 512 1024 2048; do
     run logreg_${bs}_${it} 600 python benchmarks/logreg_train.py --batch_size $bs --n_iter $it --n_exp 3 --json gpurun_out/logreg.jsonl
   done; done
 fi

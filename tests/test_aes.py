@@ -29,7 +29,7 @@ def _bytes(bits):
 
 def test_circuit_matches_fips197_and_aesni():
     lc = aes.levelled_aes()
-    assert lc.depth == 40
+    assert lc.depth == 60  # 10 S-box layers of AND depth 6 (key schedule alongside)
     keys = [bytes.fromhex("000102030405060708090a0b0c0d0e0f")] + [os.urandom(16) for _ in range(3)]
     blocks = [bytes.fromhex("00112233445566778899aabbccddeeff")] + [os.urandom(16) for _ in range(3)]
     inp = torch.tensor([_bits(k) + _bits(b) for k, b in zip(keys, blocks)], dtype=torch.uint8).T
@@ -43,7 +43,49 @@ def test_bristol_text_roundtrip():
     c = aes128_circuit()
     c2 = parse_bristol(c.to_bristol())
     assert c2.num_wires == c.num_wires and c2.stats() == c.stats()
-    assert c.stats()["AND"] == 51200
+    assert c.stats()["AND"] == 6400  # as the reference's bristol_fashion/aes_128.txt
+
+
+def test_sbox_circuit_all_inputs():
+    """The 32-AND S-box sub-circuit against the FIPS-197 S-box table, all 256 bytes."""
+    from moose_amd.protocols.aes_circuit import _Builder
+    from moose_amd.protocols.bristol import Circuit
+
+    b = _Builder(8)
+    outs = b.sbox(list(range(8)))  # lsb-first byte in, lsb-first byte out
+    assert sum(g.op == "AND" for g in b.gates) == 32
+    outs = [b.copy(w) for w in outs]
+    circ = Circuit(b.n, [8], [8], b.gates)
+    inp = torch.tensor([[(v >> i) & 1 for i in range(8)] for v in range(256)],
+                       dtype=torch.uint8).T
+    from moose_amd.protocols.bristol import LevelledCircuit
+
+    got = LevelledCircuit(circ).eval_plain(inp)
+    sbox = _sbox_table()
+    for v in range(256):
+        assert sum(int(got[i, v]) << i for i in range(8)) == sbox[v], v
+
+
+def _sbox_table():
+    def mul(a, b):
+        r = 0
+        while b:
+            if b & 1:
+                r ^= a
+            a <<= 1
+            if a & 0x100:
+                a ^= 0x11B
+            b >>= 1
+        return r
+
+    inv = [0] + [next(b for b in range(1, 256) if mul(a, b) == 1) for a in range(1, 256)]
+    out = []
+    for a in range(256):
+        x, s = inv[a], inv[a]
+        for i in range(1, 5):
+            s ^= ((x << i) | (x >> (8 - i))) & 0xFF
+        out.append(s ^ 0x63)
+    return out
 
 
 def test_small_bristol_circuit_levelling():
