@@ -6,6 +6,10 @@ the stacked single-device session; lowered ones on the graph executor::
 
     dasher COMPUTATION [-i textual|msgpack] [--compile] [--arg name=file.npy ...]
            [--device cuda|cpu] [--ring 64|128]
+    dasher --session FILE.session [--arg name=file.npy ...] [--backend nccl|gloo]
+
+``--session`` runs a filesystem-choreography session file with one worker process per
+(replica, role) on this node, honouring its ``gpu``/``gpus`` pinning and ``replicas``.
 """
 from __future__ import annotations
 
@@ -20,7 +24,9 @@ from moose_amd.cli.common import read_computation
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="dasher", description=__doc__.splitlines()[0])
-    ap.add_argument("input")
+    ap.add_argument("input", nargs="?")
+    ap.add_argument("--session", default=None, help="run a .session file (multi-process)")
+    ap.add_argument("--backend", default=None)
     ap.add_argument("-i", "--input-format", default="textual", choices=FORMATS)
     ap.add_argument("--compile", action="store_true", help="lower before running")
     ap.add_argument("--arg", action="append", default=[], help="name=path.npy")
@@ -30,6 +36,20 @@ def main(argv=None) -> int:
     from moose_amd.runtime.local import LocalMooseRuntime
     from moose_amd.utils.storage import load_from_path
 
+    if a.session:
+        from moose_amd.runtime.choreography import run_session_file
+
+        extra = {}
+        for it in a.arg:
+            k, _, p = it.partition("=")
+            extra[k] = load_from_path(p, None)
+        outs, timings = run_session_file(a.session, extra, backend=a.backend)
+        for k in sorted(outs):
+            print(f"{k} = {np.array2string(np.asarray(outs[k]), threshold=20)}")
+        print(f"elapsed_us = {timings}")
+        return 0
+    if not a.input:
+        ap.error("a computation (or --session) is required")
     comp = read_computation(a.input, a.input_format)
     args = {}
     for it in a.arg:

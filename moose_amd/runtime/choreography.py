@@ -233,18 +233,84 @@ def _plain_args(d):
 # ---------------------------------------------------------------------------
 def parse_session_file(path: str) -> dict:
     """``[computation] path = ..., format = "textual"|"msgpack"`` and
-    ``[[roles]] name = ..., endpoint = ...`` (reference examples/test.session)."""
+    ``[[roles]] name = ..., endpoint = ...`` (reference examples/test.session), plus the
+    GPU topology of this engine (optional):
+
+    * ``[[roles]] gpu = g`` -- the device ordinal (on its endpoint's node) that runs the
+      role in replica 0; ``gpus = [g0, g1, ...]`` -- one per replica;
+    * ``[session] replicas = R`` -- data-parallel copies of the 3-party session on
+      disjoint GPU groups; ``shard_args = ["x", ...]`` -- arguments split along axis 0
+      across the replicas (outputs concatenated back, parallel/replicas.py);
+      ``fixedpoint_ring = 64|128``; ``[arguments] name = "file.npy"``.
+    """
     import tomli
 
     with open(path, "rb") as f:
         d = tomli.load(f)
+    base = os.path.dirname(os.path.abspath(path))
     comp = d.get("computation", {})
     cpath = comp["path"]
     if not os.path.isabs(cpath):
-        cpath = os.path.join(os.path.dirname(os.path.abspath(path)), cpath)
-    roles = {r["name"]: r.get("endpoint", r["name"]) for r in d.get("roles", [])}
+        cpath = os.path.join(base, cpath)
+    role_list = d.get("roles", [])
+    roles = {r["name"]: r.get("endpoint", r["name"]) for r in role_list}
+    sess = d.get("session", {})
+    replicas = int(sess.get("replicas", 1))
+    if replicas < 1:
+        raise ValueError(f"{path}: replicas must be >= 1")
+    gpus = {}
+    for i, r in enumerate(role_list):
+        if "gpus" in r:
+            g = [int(v) for v in r["gpus"]]
+            if len(g) != replicas:
+                raise ValueError(f"{path}: role {r['name']} lists {len(g)} gpus for "
+                                 f"{replicas} replicas")
+            gpus[r["name"]] = g
+        elif "gpu" in r:
+            gpus[r["name"]] = [int(r["gpu"]) + k * len(role_list) for k in range(replicas)]
+    args = {k: (v if os.path.isabs(v) else os.path.join(base, v))
+            for k, v in d.get("arguments", {}).items()}
     return {"session_id": os.path.splitext(os.path.basename(path))[0],
-            "computation_path": cpath, "format": comp.get("format", "textual"), "roles": roles}
+            "computation_path": cpath, "format": comp.get("format", "textual"), "roles": roles,
+            "replicas": replicas, "shard_args": list(sess.get("shard_args", [])),
+            "fixedpoint_ring": int(sess.get("fixedpoint_ring", 128)), "gpus": gpus,
+            "arguments": args}
+
+
+def session_device_map(s: dict) -> Optional[List[int]]:
+    """Global rank -> device ordinal for a parsed session (rank = replica * n + role
+    index, roles in file order), or None when the file pins no GPU."""
+    if not s["gpus"]:
+        return None
+    names = list(s["roles"])
+    n = len(names)
+    dm = []
+    for k in range(s["replicas"]):
+        for i, name in enumerate(names):
+            g = s["gpus"].get(name)
+            dm.append(g[k] if g is not None else k * n + i)
+    if len(set(dm)) != len(dm):
+        raise ValueError(f"session {s['session_id']}: two ranks pinned to one GPU: {dm}")
+    return dm
+
+
+def run_session_file(path: str, arguments: Optional[dict] = None, backend=None, **kw):
+    """Run a ``.session`` file on one node as one worker process per (replica, role),
+    honouring its GPU pinning and replicas (DistributedMooseRuntime); returns
+    (outputs, timings)."""
+    from moose_amd.cli.common import read_computation
+    from moose_amd.runtime.distributed import DistributedMooseRuntime
+    from moose_amd.utils.storage import load_from_path
+
+    s = parse_session_file(path)
+    comp = read_computation(s["computation_path"], s["format"])
+    args = {k: load_from_path(v, None) for k, v in s["arguments"].items()}
+    args.update(arguments or {})
+    rt = DistributedMooseRuntime(list(s["roles"]), backend=backend,
+                                 fixedpoint_ring=s["fixedpoint_ring"], replicas=s["replicas"],
+                                 shard_args=s["shard_args"] or None,
+                                 device_map=session_device_map(s), **kw)
+    return rt.run_computation(comp, args)
 
 
 def watch_sessions(sessions_dir: str, client: ChoreographyClient, world: int,

@@ -11,7 +11,8 @@ OUT=build/sanitize
 mkdir -p "$OUT"
 CXX=${CXX:-g++}
 SRC="csrc/tests/native_tests.cpp csrc/runtime/graph.cpp csrc/runtime/scheduler.cpp
-     csrc/runtime/textual.cpp csrc/runtime/net.cpp csrc/ring_cpu.cpp csrc/rss_fused_cpu.cpp"
+     csrc/runtime/textual.cpp csrc/runtime/net.cpp csrc/ring_cpu.cpp csrc/rss_fused_cpu.cpp
+     csrc/rss_party_cpu.cpp"
 # device entry points (mxh_*) are only reached with dev != 0, which the tests never use
 LINK="-Wl,--unresolved-symbols=ignore-all -lssl -lcrypto -pthread"
 COMMON="-std=c++17 -g -O1 -fno-omit-frame-pointer -msse4.1 -maes -pthread"

@@ -119,3 +119,41 @@ def test_rudolph_no_listen_exits_after_existing_sessions(tmp_path):
         with open(tmp_path / f"trace_{ident}.json") as f:
             evs = json.load(f)["traceEvents"]
         assert any(e["name"].startswith("op.") for e in evs)
+
+
+def test_session_file_gpu_topology_and_replicas(tmp_path):
+    """``[session] replicas`` / ``shard_args`` and per-role ``gpus``:
+    parsed into a rank -> device map and run as 2 replicas x 3 parties (gloo here)."""
+    import shutil
+
+    import numpy as np
+
+    from moose_amd.runtime.choreography import parse_session_file
+    from moose_amd.runtime.choreography import run_session_file
+    from moose_amd.runtime.choreography import session_device_map
+
+    ex = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples")
+    for f in ("dot_input.moose", "dot_replicas.session"):
+        shutil.copy(os.path.join(ex, f), tmp_path / f)
+    s = parse_session_file(str(tmp_path / "dot_replicas.session"))
+    assert s["replicas"] == 2 and s["shard_args"] == ["x"]
+    assert session_device_map(s) == [0, 1, 2, 3, 4, 5]
+    x = np.arange(15, dtype=np.float64).reshape(5, 3) / 4
+    outs, timings = run_session_file(str(tmp_path / "dot_replicas.session"), {"x": x},
+                                     backend="gloo")
+    np.testing.assert_allclose(outs["result"], x @ np.array([[2.0], [0.5], [-4.0]]), atol=1e-5)
+    assert set(timings) == {"alice", "bob", "carole"}
+
+
+def test_session_file_rejects_double_pinned_gpu(tmp_path):
+    from moose_amd.runtime.choreography import parse_session_file
+    from moose_amd.runtime.choreography import session_device_map
+
+    (tmp_path / "c.moose").write_text("")
+    (tmp_path / "s.session").write_text(
+        '[computation]\npath = "c.moose"\n[[roles]]\nname = "a"\ngpu = 0\n'
+        '[[roles]]\nname = "b"\ngpu = 0\n')
+    import pytest
+
+    with pytest.raises(ValueError):
+        session_device_map(parse_session_file(str(tmp_path / "s.session")))
