@@ -126,6 +126,7 @@ EXTENSION_OPERATORS = {
     "BitSplit": [("start", "int"), ("count", "int")],  # packed word -> bit planes
     "WeightedSum": [("weights", "ints"), ("bits", "int")],
     "StridedSlice": [("slices", "ints")],
+    "MulLeading": [],  # x[i, ...] * c[i]: rank-agnostic public scaling (polymorphic plans)
 }
 
 ALL_OPERATORS = {**OPERATORS, **EXTENSION_OPERATORS}

@@ -318,13 +318,13 @@ def poly_eval(sess, x: RepFixed, coeffs) -> RepFixed:
     ceil(log2 n) rounds), and the sum is one public weighted sum over P + one TruncPr."""
     n = len(coeffs) - 1
     f, bits = x.frac, x.bits
-    shape = tuple(shape_of(sess, x))
     P = local(sess, x, "ExpandDims", axis=[0])
     have = 1
     while have < n:
         m = min(2 * have, n) - have
         xh = local(sess, P, "Slice", slice=(have - 1, have, None))
-        left = xh if m == 1 else local(sess, xh, "Broadcast", shape=(m,) + shape)
+        # m copies of x^h on the stacking axis (a concat, so no static shape is needed)
+        left = xh if m == 1 else concat(sess, [xh] * m, 0)
         right = P if m == have else local(sess, P, "Slice", slice=(0, m, None))
         P = concat(sess, [P, mul(sess, left, right)], 0)
         have += m
@@ -453,10 +453,10 @@ def _exp2_parts(sess, a: RepFixed, negative: bool):
             c = 2.0 ** min(e, integ + 1)  # saturate: larger results overflow anyway
         cs.append(int(round((c - 1.0) * (1 << f))))
     ints = local(sess, ab, "Slice", slice=(f, f + nint, None))
-    ndim = len(shape_of(sess, ints)) - 1
-    cvec = R.from_ints(np.array(cs, dtype=object).reshape((nint,) + (1,) * ndim), bits,
-                       sess.device)
-    fac = rep.mul_public(sess, ints, cvec)
+    cvec = R.from_ints(np.array(cs, dtype=object), bits, sess.device)
+    pc = sess.public(ints.plc, cvec)
+    fac = RepTensor(ints.plc, bits, "arith", sess.p("MulLeading", ints.plc, ints.s0, pc),
+                    sess.p("MulLeading", ints.plc, ints.s1, pc))
     fac = rep.add_public(sess, fac, _encode_const(sess, 1.0, f, bits))
     # log-depth product over the leading axis: one stacked multiplication per level
     F, n = RepFixed(fac, f, integ), nint

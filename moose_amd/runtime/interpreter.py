@@ -554,10 +554,10 @@ class Interpreter:
         from moose_amd.compiler.symbolic import ring_ty
 
         spec = self.arg_specs.get(name) if getattr(self, "arg_specs", None) else None
-        if spec is None:
-            raise MooseRuntimeError(
-                f"lowering needs the shape of argument {name!r} (pass arg_specs)")
-        shape, dtype = spec
+        # no spec: shape-polymorphic lowering -- the value's shape is unknown (None) and
+        # every protocol step that needs it reads it at run time through a Shape op
+        # (reference execution/symbolic.rs:400-435); the dtype comes from the signature
+        shape, dtype = spec if spec is not None else (None, None)
         plc = op.placement
         host = plc.owner if isinstance(plc, HostPlacement) else plc.owners[0]
         hp = HostPlacement(host)

@@ -86,6 +86,17 @@ prim("Or")(_arith("or"))
 prim("Xor")(_arith("xor"))
 
 
+@prim("MulLeading")
+def _mul_leading(nb, a, c):
+    """a[..., i, ...] * c[i] along the first non-party axis of ``a`` (``c`` 1-D public):
+    a rank-agnostic scaling, so shape-polymorphic lowering can express it."""
+    if not _is_rt(a):
+        k = a.dim() - nb - 1
+        return a * c.reshape((c.shape[0],) + (1,) * k)
+    k = len(a.shape) - nb - 1
+    return R.binary("mul", a, R.reshape(c, (c.shape[0],) + (1,) * k))
+
+
 @prim("Neg")
 def _neg(nb, a):
     if _is_rt(a):  # on bit tensors Neg is NOT (reference host/ops.rs:1519-1527)

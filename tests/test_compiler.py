@@ -147,3 +147,46 @@ d = Add: (HostFloat64Tensor, HostFloat64Tensor) -> HostFloat64Tensor (a, a) @Hos
     comp = passes.networking(Computation.from_textual(src))
     assert sum(op.kind == "Send" for op in comp.operations) == 2  # a->bob once, a->carole once
     passes.well_formed(comp.toposorted())
+
+
+POLY = """\
+x = Input{arg_name = "x"}: () -> Tensor<Float64> () @Host(player0)
+cast_0 = Cast: (Tensor<Float64>) -> Tensor<Fixed128(24, 40)> (x) @Host(player0)
+y = Input{arg_name = "y"}: () -> Tensor<Float64> () @Host(player1)
+cast_1 = Cast: (Tensor<Float64>) -> Tensor<Fixed128(24, 40)> (y) @Host(player1)
+dot_0 = Dot: (Tensor<Fixed128(24, 40)>, Tensor<Fixed128(24, 40)>) -> Tensor<Fixed128(24, 40)> (cast_0, cast_1) @Replicated(player0, player1, player2)
+sig = Sigmoid: (Tensor<Fixed128(24, 40)>) -> Tensor<Fixed128(24, 40)> (dot_0) @Replicated(player0, player1, player2)
+cast_2 = Cast: (Tensor<Fixed128(24, 40)>) -> Tensor<Float64> (sig) @Host(player2)
+output_0 = Output{tag = "output_0"}: (Tensor<Float64>) -> Tensor<Float64> (cast_2) @Host(player2)
+"""
+
+
+def test_shape_polymorphic_lowering_one_plan_two_sizes():
+    """Lowering without arg_specs (reference execution/symbolic.rs:400-435,
+    tutorials/dotprod-compiled.moose): input shapes are unknown, every PRF draw / fill
+    reads its shape from a Shape op at run time, and ONE lowered plan evaluates inputs of
+    different sizes."""
+    from moose_amd.compiler import passes as P
+    from moose_amd.ir.textual import parse_computation
+    from moose_amd.runtime.local import LocalMooseRuntime
+
+    low = P.compile(parse_computation(POLY), P.DEFAULT_PASSES, cache=False)
+    kinds = [op.kind for op in low.operations]
+    assert "Shape" in kinds and "Input" in kinds
+    assert all(op.placement.__class__.__name__ == "HostPlacement" for op in low.operations)
+    rt = LocalMooseRuntime(["player0", "player1", "player2"], device="cpu")
+    for (m, k, n) in ((2, 3, 1), (5, 3, 4)):
+        rng = np.random.default_rng(m)
+        x, y = rng.uniform(-1, 1, (m, k)), rng.uniform(-1, 1, (k, n))
+        out = np.asarray(rt.evaluate_compiled(low, {"x": x, "y": y})["output_0"])
+        assert out.shape == (m, n)
+        np.testing.assert_allclose(out, 1 / (1 + np.exp(-(x @ y))), atol=1e-6)
+
+
+def test_polymorphic_plan_asks_for_shapes_where_structure_depends_on_size():
+    from moose_amd.compiler import passes as P
+    from moose_amd.ir.textual import parse_computation
+
+    src = POLY.replace("Sigmoid:", "Softmax{axis = 1, upmost_index = 4}:")
+    with pytest.raises(Exception, match="arg_specs|static shapes"):
+        P.compile(parse_computation(src), P.DEFAULT_PASSES, cache=False)
