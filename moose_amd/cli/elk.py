@@ -8,8 +8,11 @@ Parity: reference ``moose/src/bin/elk/main.rs:11-276``::
     elk stats op-count INPUT [--by-placement]
     elk stats out-degree INPUT [--by-operator]
 
-``--arg-shape`` exists because lowering here is shape-specialised (inputs of unknown
-shape cannot be lowered; constants carry their shapes).
+Without ``--arg-shape`` lowering is shape-polymorphic, as in the reference (input shapes
+are read at run time through ``Shape`` operations; one plan serves every input size).
+``--arg-shape`` specialises the plan to fixed input shapes: static shapes throughout, the
+form a hipGraph capture replays, and the only form for protocols whose structure depends
+on a size (argmax / softmax over a dynamic axis).
 """
 from __future__ import annotations
 
