@@ -19,8 +19,9 @@ Layouts (``--layout``; default ``auto`` = stacked on 1 GPU, cyclic on N > 1):
   send/recv over xGMI.  Weak scaling with the same per-GPU work as the 1-GPU stacked run.
 * ``spmd`` -- one party per GPU, N/3 sessions (latency layout).
 
-All layouts all-gather the revealed outputs of every session over RCCL inside the timed
-region (overlapped with the next step).  Inputs are synthetic (uniform [-4, 4)),
+With several sessions, the revealed outputs of every session are collected on rank 0 (the
+client, as the reference's benchmark collects them) over RCCL inside the timed region,
+overlapped with the next step (``--gather all`` all-gathers them to every rank instead).  Inputs are synthetic (uniform [-4, 4)),
 device-resident; tracing/conversion happens once before the timed region (the
 reference's client-side compile).  Every step creates a fresh session (fresh PRF keys).
 
@@ -77,7 +78,10 @@ def _parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--ring", type=int, default=128, choices=[64, 128])
-    ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--gather", default="root", choices=["root", "all", "none"],
+                    help="revealed outputs of every session: to rank 0 (the client; "
+                         "default), all-gathered to every rank, or left on their owners")
+    ap.add_argument("--no-gather", action="store_true", help="= --gather none")
     ap.add_argument("--layout", default="auto", choices=["auto", "stacked", "cyclic", "spmd"])
     ap.add_argument("--check", action="store_true", help="verify against float64 torch")
     return ap.parse_args()
@@ -158,14 +162,18 @@ def main():
     x = _inputs(n, xs, "x", device)
     y = _inputs(n, ys, "y", device)
 
+    gather_mode = "none" if args.no_gather or n_sessions == 1 else args.gather
+    owners = [3 * s + 2 for s in range(n_sessions)] if layout == "spmd" else list(range(world))
+    root = owners[0]
     gather_bufs, gather_group, pending = None, None, []
-    if n_sessions > 1 and not args.no_gather:
+    if gather_mode != "none":
         # every session's revealed output, concatenated along rows.  Double-buffered:
-        # step k's all-gather runs on the RCCL stream while step k+1 computes.
-        gather_bufs = [torch.empty((n_sessions * n, n), dtype=torch.float64, device=device)
-                       for _ in range(2)]
-        if layout == "spmd":  # the output owners (carole = party 2) of every session
-            gather_group = dist.new_group([3 * s + 2 for s in range(n_sessions)])
+        # step k's transfer runs on the RCCL stream while step k+1 computes.
+        if gather_mode == "all" or rank == root:
+            gather_bufs = [torch.empty((n_sessions * n, n), dtype=torch.float64, device=device)
+                           for _ in range(2)]
+        if gather_mode == "all" and layout == "spmd":  # the output owners of every session
+            gather_group = dist.new_group(owners)
 
     if layout == "spmd":
         from moose_amd.parallel.spmd import SPMDSession
@@ -199,12 +207,22 @@ def main():
         interp = Interpreter(sess, {}, fixedpoint_ring=args.ring)
         outs = interp.run(comp, {"x": x, "y": y})
         z = outs["output_0"].v.v if out_owner else None
-        if gather_bufs is not None and out_owner:
-            if len(pending) == 2:
+        if gather_mode != "none" and out_owner:
+            while len(pending) >= 2 * max(1, len(owners) - 1):
                 pending.pop(0).wait()
-            buf = gather_bufs[n_steps[0] % 2]
-            pending.append(dist.all_gather_into_tensor(buf, z.contiguous(), group=gather_group,
-                                                       async_op=True))
+            zc = z.contiguous()
+            if gather_mode == "all":
+                buf = gather_bufs[n_steps[0] % 2]
+                pending.append(dist.all_gather_into_tensor(buf, zc, group=gather_group,
+                                                           async_op=True))
+            elif rank == root:
+                buf = gather_bufs[n_steps[0] % 2]
+                ops = [dist.P2POp(dist.irecv, buf[i * n:(i + 1) * n], r)
+                       for i, r in enumerate(owners) if r != root]
+                buf[owners.index(root) * n:(owners.index(root) + 1) * n].copy_(zc)
+                pending.extend(dist.batch_isend_irecv(ops))
+            else:
+                pending.extend(dist.batch_isend_irecv([dist.P2POp(dist.isend, zc, root)]))
         n_steps[0] += 1
         return z
 
@@ -246,6 +264,17 @@ def main():
     if args.check and out_owner:
         ref = _inputs(n, out_session, "x", device) @ _inputs(n, out_session, "y", device)
         check = {"max_abs_err": (z - ref).abs().max().item()}
+    if args.check and gather_bufs is not None and (gather_mode == "all" or rank == root):
+        # the last step's collected outputs: rank r's revealed output is session s(r)'s
+        buf = gather_bufs[(n_steps[0] - 1) % 2]
+        sess_of = {"cyclic": lambda r: (r - 2) % world, "spmd": lambda r: r // 3,
+                   "stacked": lambda r: r}[layout]
+        gerr = 0.0
+        for i, r in enumerate(owners):
+            s_ = sess_of(r)
+            ref = _inputs(n, s_, "x", device) @ _inputs(n, s_, "y", device)
+            gerr = max(gerr, (buf[i * n:(i + 1) * n] - ref).abs().max().item())
+        check = dict(check or {}, gathered_max_abs_err=gerr)
     checks = [check]
     if world > 1 and args.check:
         checks = [None] * world
@@ -279,6 +308,7 @@ def main():
                 "parallelism": parallelism,
             },
             "layout": layout,
+            "gather": gather_mode,
             "world_size": world,
             "sessions": n_sessions,
             "per_rank_ms_per_step": [t / args.steps * 1e3 for t in per_rank],

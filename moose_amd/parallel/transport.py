@@ -61,6 +61,13 @@ class Transport:
         self.fault = fault if fault is not None else _parse_fault(os.environ.get("MOOSEX_FAULT"),
                                                                    rank)
         self._sends = 0
+        # gloo with device tensors (CPU tests, one-GPU rehearsals of multi-rank layouts):
+        # stage payloads through host memory explicitly, as parallel/cyclic.RingComm does
+        try:
+            backend = dist.get_backend(group) if world > 1 else "none"
+        except (RuntimeError, ValueError):
+            backend = "none"
+        self.stage = backend == "gloo" and self.device.type == "cuda"
 
     # -- encoding -----------------------------------------------------------------
     def _header(self, v):
@@ -152,16 +159,16 @@ class Transport:
                 return  # the receiver waits until the session deadline
             if kind == "delay":
                 time.sleep(val)
-        dist.send(t, dst, group=self.group)
+        dist.send(t.cpu() if self.stage else t, dst, group=self.group)
         self.bytes_sent += t.numel() * t.element_size()
         self.messages += 1
 
     def _recv_tensor(self, shape, dtype, src: int) -> torch.Tensor:
-        t = torch.empty(shape, dtype=dtype, device=self.device)
+        t = torch.empty(shape, dtype=dtype, device="cpu" if self.stage else self.device)
         if t.numel() == 0:
-            return t
+            return t.to(self.device)
         dist.recv(t, src, group=self.group)
-        return t
+        return t.to(self.device) if self.stage else t
 
     # -- typed values -----------------------------------------------------------------
     def send(self, v, dst: int):
@@ -199,10 +206,13 @@ class Transport:
         out = torch.empty_like(t)
         if t.numel() == 0:
             return out
-        ops = [dist.P2POp(dist.isend, t, to_rank, group=self.group),
-               dist.P2POp(dist.irecv, out, from_rank, group=self.group)]
+        st, so = (t.cpu(), torch.empty(t.shape, dtype=t.dtype)) if self.stage else (t, out)
+        ops = [dist.P2POp(dist.isend, st, to_rank, group=self.group),
+               dist.P2POp(dist.irecv, so, from_rank, group=self.group)]
         for w in dist.batch_isend_irecv(ops):
             w.wait()
+        if self.stage:
+            out.copy_(so)
         self.bytes_sent += t.numel() * t.element_size()
         self.messages += 1
         return out

@@ -31,6 +31,10 @@ if [[ $STEPS == *multi* || $STEPS == all ]]; then
   run spmd3 600 python bench.py --gpus 3 --layout spmd --size 1024 --steps 3 --warmup 1 --check
   unset MOOSEX_SHARED_GPU
 fi
+if [[ $STEPS == *aes* ]]; then
+  run aes_bp 600 python scripts/bench_aes_decrypt.py --n 64 --runs 5
+  MOOSEX_AES_SBOX=algebraic run aes_alg 600 python scripts/bench_aes_decrypt.py --n 64 --runs 3
+fi
 if [[ $STEPS == *logreg* ]]; then
   rm -f gpurun_out/logreg.jsonl
   for it in 10 50 100; do for bs in 128 512 1024 2048; do

@@ -60,3 +60,5 @@ def test_bench_self_launch(n, layout, sessions):
     assert len(d["per_rank_ms_per_step"]) == n
     assert d["ms_per_step"] == pytest.approx(max(d["per_rank_ms_per_step"]))
     assert d["check"] and all(c["max_abs_err"] < 1e-4 for c in d["check"])
+    if sessions > 1:  # rank 0 (the client) collected every session's revealed output
+        assert d["gather"] == "root" and d["check"][0]["gathered_max_abs_err"] < 1e-4
