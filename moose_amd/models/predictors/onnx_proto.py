@@ -200,3 +200,112 @@ def to_array(t: Message) -> np.ndarray:
     else:
         a = np.asarray(t.uint64_data, dtype=dt)
     return a.reshape(shape).astype(dt)
+
+
+# ---------------------------------------------------------------------------
+# encoding (the inverse of parse, for models built in Python -- e.g. the tutorial's
+# sklearn logistic regression exported the way skl2onnx does, without skl2onnx)
+# ---------------------------------------------------------------------------
+def _enc_varint(v: int) -> bytes:
+    v &= (1 << 64) - 1
+    out = bytearray()
+    while True:
+        b = v & 0x7F
+        v >>= 7
+        if v:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)
+
+
+def serialize(msg: Message) -> bytes:
+    out = bytearray()
+    for field, (name, k, rep) in sorted(_SCHEMA[msg._kind].items()):
+        val = getattr(msg, name)
+        vals = val if rep else [val]
+        if rep and not vals:
+            continue
+        if not rep and (val is None or val == "" or val == b"" or
+                        (k in ("int", "float", "double") and val == 0)):
+            continue
+        if rep and k in ("int", "float", "double"):  # packed
+            if k == "float":
+                data = np.asarray(vals, dtype="<f4").tobytes()
+            elif k == "double":
+                data = np.asarray(vals, dtype="<f8").tobytes()
+            else:
+                data = b"".join(_enc_varint(int(v)) for v in vals)
+            out += _enc_varint((field << 3) | 2) + _enc_varint(len(data)) + data
+            continue
+        for v in vals:
+            if k.startswith("msg:"):
+                data = serialize(v)
+                out += _enc_varint((field << 3) | 2) + _enc_varint(len(data)) + data
+            elif k in ("str", "bytes"):
+                data = v.encode() if isinstance(v, str) else bytes(v)
+                out += _enc_varint((field << 3) | 2) + _enc_varint(len(data)) + data
+            elif k == "float":
+                out += _enc_varint((field << 3) | 5) + struct.pack("<f", v)
+            elif k == "double":
+                out += _enc_varint((field << 3) | 1) + struct.pack("<d", v)
+            else:
+                out += _enc_varint(field << 3) + _enc_varint(int(v))
+    return bytes(out)
+
+
+def make(kind: str, **fields) -> Message:
+    m = Message(kind)
+    for k, v in fields.items():
+        setattr(m, k, v)
+    return m
+
+
+def attr(name: str, value) -> Message:
+    if isinstance(value, str):
+        return make("AttributeProto", name=name, s=value.encode(), type=STRING)
+    if isinstance(value, int):
+        return make("AttributeProto", name=name, i=value, type=INT)
+    if isinstance(value, float):
+        return make("AttributeProto", name=name, f=value, type=FLOAT)
+    value = list(value)
+    if value and isinstance(value[0], str):
+        return make("AttributeProto", name=name, strings=[v.encode() for v in value],
+                    type=STRINGS)
+    if value and isinstance(value[0], (int, np.integer)):
+        return make("AttributeProto", name=name, ints=[int(v) for v in value], type=INTS)
+    return make("AttributeProto", name=name, floats=[float(v) for v in value], type=FLOATS)
+
+
+def sklearn_logistic_regression_model(coef, intercept, n_features: int) -> bytes:
+    """The ONNX graph skl2onnx emits for a binary ``LogisticRegression``
+    (ml-inference-with-onnx tutorial): a LinearClassifier (ai.onnx.ml) with both class
+    rows ``[-w, w]``, ``post_transform = LOGISTIC``, then a Normalizer and a ZipMap."""
+    w = np.asarray(coef, dtype=np.float64).reshape(-1)
+    b = float(np.asarray(intercept).reshape(-1)[0])
+    lc = make("NodeProto", input=["float_input"], output=["label", "probability_tensor"],
+              name="LinearClassifier", op_type="LinearClassifier", domain="ai.onnx.ml",
+              attribute=[attr("classlabels_ints", [0, 1]),
+                         attr("coefficients", list(-w) + list(w)),
+                         attr("intercepts", [-b, b]),
+                         attr("multi_class", 0), attr("post_transform", "LOGISTIC")])
+    norm = make("NodeProto", input=["probability_tensor"], output=["probabilities"],
+                name="Normalizer", op_type="Normalizer", domain="ai.onnx.ml",
+                attribute=[attr("norm", "L1")])
+    zm = make("NodeProto", input=["probabilities"], output=["output_probability"],
+              name="ZipMap", op_type="ZipMap", domain="ai.onnx.ml",
+              attribute=[attr("classlabels_int64s", [0, 1])])
+    shape = make("TensorShapeProto", dim=[make("Dimension", dim_param="N"),
+                                          make("Dimension", dim_value=n_features)])
+    inp = make("ValueInfoProto", name="float_input",
+               type=make("TypeProto", tensor_type=make("TypeProtoTensor", elem_type=1,
+                                                       shape=shape)))
+    out = make("ValueInfoProto", name="label",
+               type=make("TypeProto", tensor_type=make("TypeProtoTensor", elem_type=7)))
+    graph = make("GraphProto", node=[lc, norm, zm], name="ONNX(LogisticRegression)",
+                 input=[inp], output=[out])
+    model = make("ModelProto", ir_version=8, producer_name="skl2onnx",
+                 producer_version="1.13", domain="ai.onnx", graph=graph,
+                 opset_import=[make("OperatorSetIdProto", domain="", version=15),
+                               make("OperatorSetIdProto", domain="ai.onnx.ml", version=1)])
+    return serialize(model)

@@ -40,10 +40,12 @@ def main():
     X, y = make_classification(n_samples=1000, n_features=10, n_classes=2, random_state=5)
     X_train, X_test, y_train, _ = train_test_split(X, y, test_size=0.2, random_state=5)
     lg = LogisticRegression().fit(X_train, y_train)
-    w, b = lg.coef_[0], lg.intercept_[0]
-    # the ONNX export of a binary sklearn LR: two score rows (-w, w), LOGISTIC transform
-    model = predictors.LinearClassifier(np.stack([-w, w]), np.array([-b, b]),
-                                        predictors.PostTransform.SIGMOID)
+    # the tutorial's path: sklearn model -> ONNX (the graph skl2onnx emits: LinearClassifier
+    # with rows (-w, w) and a LOGISTIC post-transform) -> predictors.from_onnx
+    from moose_amd.models.predictors import onnx_proto
+
+    onnx_bytes = onnx_proto.sklearn_logistic_regression_model(lg.coef_, lg.intercept_, 10)
+    model = predictors.from_onnx(onnx_bytes)
     # fixed(24,40) needs Z_2^128 (pymoose's mapping); Z_2^64 uses the reference's
     # canonical Fixed64 precision fixed(14,23) (replicated/input.rs:91-92)
     import moose_amd as pm
@@ -70,7 +72,9 @@ def main():
         "higher_is_better": False, "batch": int(X_test.shape[0]), "features": 10,
         "device": dev, "ring": a.ring, "graphs": a.graphs,
         "fixed": [dtype.integral_precision, dtype.fractional_precision], "max_abs_err_vs_sklearn": err,
-        "data": "make_classification(random_state=5), sklearn LogisticRegression",
+        "data": "make_classification(random_state=5), sklearn LogisticRegression -> ONNX "
+                "-> predictors.from_onnx",
+        "layout": "stacked 3-party session on one GPU",
     }))
 
 

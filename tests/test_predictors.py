@@ -123,3 +123,26 @@ def test_aes_wrapped_predictor_traces_and_runs():
             "aes_key/carole/share2": kb, "aes_key/carole/share0": s0}
     out = LocalMooseRuntime(["alice", "bob", "carole"], device="cpu").evaluate_computation(comp, args)
     np.testing.assert_allclose(list(out.values())[0], np.asarray(expected).reshape(2, -1), atol=1e-4)
+
+
+def test_tutorial_lr_via_onnx_bytes():
+    """The ml-inference-with-onnx tutorial's model (sklearn binary LogisticRegression),
+    serialized to ONNX as skl2onnx does (onnx_proto.sklearn_logistic_regression_model)
+    and loaded back through predictors.from_onnx, predicts sklearn's probabilities."""
+    import numpy as np
+    from sklearn.datasets import make_classification
+    from sklearn.linear_model import LogisticRegression
+
+    from moose_amd.models import predictors
+    from moose_amd.models.predictors import onnx_proto
+    from moose_amd.runtime.local import LocalMooseRuntime
+
+    X, y = make_classification(n_samples=200, n_features=10, n_classes=2, random_state=5)
+    lg = LogisticRegression().fit(X[:150], y[:150])
+    model = predictors.from_onnx(
+        onnx_proto.sklearn_logistic_regression_model(lg.coef_, lg.intercept_, 10))
+    comp = model.predictor_factory(predictors.DEFAULT_FIXED_DTYPE)
+    out = LocalMooseRuntime(["alice", "bob", "carole"], device="cpu").evaluate_computation(
+        comp, {"x": X[150:]})
+    pred = np.asarray(list(out.values())[0])
+    np.testing.assert_allclose(pred, lg.predict_proba(X[150:]), atol=1e-3)
