@@ -117,6 +117,21 @@ def dot(sess, x, y, px=None, py=None, f=None):
     return _with(base, rep.trunc_pr(sess, z, f if f is not None else base.frac))
 
 
+def dot_many(sess, pairs, f=None):
+    """Several independent secret x secret fixed-point products of equal shapes at once:
+    the operands are stacked on a new leading axis, so the k products share one batched
+    MFMA GEMM launch (batch = parties x k), one zero-share/reshare round and one TruncPr
+    -- instead of k of each (the interpreter batches independent Dot ops this way)."""
+    if len(pairs) == 1:
+        return [dot(sess, pairs[0][0], pairs[0][1], f=f)]
+    x0 = pairs[0][0]
+    X = concat(sess, [local(sess, x, "ExpandDims", axis=[0]) for x, _ in pairs], 0)
+    Y = concat(sess, [local(sess, y, "ExpandDims", axis=[0]) for _, y in pairs], 0)
+    Z = rep.dot(sess, X.t, Y.t, nbatch=1)
+    T = _with(x0, rep.trunc_pr(sess, Z, f if f is not None else x0.frac))
+    return [local(sess, T, "IndexAxis", axis=0, index=i) for i in range(len(pairs))]
+
+
 def mul_const(sess, x: RepFixed, c: float) -> RepFixed:
     """x * c for a public real constant (one truncation)."""
     z = rep.mul_public(sess, x.t, _encode_const(sess, c, x.frac, x.bits))

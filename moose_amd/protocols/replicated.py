@@ -263,16 +263,20 @@ def xor(sess, x: RepTensor, y: RepTensor) -> RepTensor:
     return add(sess, x, y)
 
 
-def dot(sess, x: RepTensor, y: RepTensor) -> RepTensor:
+def dot(sess, x: RepTensor, y: RepTensor, nbatch: int = 0) -> RepTensor:
     """Matrix product: z_p = x_p.(y_p + y_{p+1}) + x_{p+1}.y_p as ONE K-doubled MFMA
-    GEMM (all parties batched when stacked), + zero share, + reshare."""
+    GEMM (all parties batched when stacked), + zero share, + reshare.  ``nbatch``
+    leading axes of x and y index independent products done in the same launches."""
     with span("rep.dot"):
         over = getattr(sess, "p_dot_zs_reshare", None)
-        if over is not None and getattr(sess, "fused", False):
+        if over is not None and getattr(sess, "fused", False) and not nbatch:
             res = over(x.plc, x.s0, x.s1, y.s0, y.s1, x.kind)
             if res is not None:
                 return RepTensor(x.plc, x.bits, x.kind, res[0], res[1])
-        v = sess.p_dot_cross(x.plc, x.s0, x.s1, y.s0, y.s1)
+        if nbatch:
+            v = sess.p_dot_cross(x.plc, x.s0, x.s1, y.s0, y.s1, nbatch=nbatch)
+        else:
+            v = sess.p_dot_cross(x.plc, x.s0, x.s1, y.s0, y.s1)
         fused = getattr(sess, "p_zero_share_reshare", None)
         if fused is not None and getattr(sess, "fused", False):
             s0, s1 = fused(x.plc, v, x.kind)

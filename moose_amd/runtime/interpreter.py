@@ -17,6 +17,7 @@ symbolic session.
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict
 
 import numpy as np
@@ -113,7 +114,14 @@ class Interpreter:
         self.arguments = arguments or {}
         comp = comp.toposorted()
         me = getattr(self.sess, "me", None)  # set for one-process-per-party sessions
-        for op in comp.operations:
+        batch = getattr(self.sess, "batch_dots", False) and os.environ.get(
+            "MOOSEX_BATCH_DOTS", "1") != "0"
+        ops = comp.operations
+        for idx, op in enumerate(ops):
+            if op.name in self.env:  # computed ahead as part of a batch
+                continue
+            if batch and op.kind == "Dot" and self._batch_dots(op, ops[idx + 1:]):
+                continue
             handler = getattr(self, f"op_{op.kind}", None) or self._dialect_handler(op)
             if handler is None:
                 raise MooseRuntimeError(f"operator {op.kind} is not supported by the interpreter")
@@ -131,6 +139,57 @@ class Interpreter:
                 except Exception as e:  # annotate with the failing op
                     raise MooseRuntimeError(f"{op.name} = {op.kind} failed: {e}") from e
         return self.outputs
+
+    def _batch_dots(self, op, later, limit: int = 256) -> bool:
+        """Independent-op batching (the reference runs independent operations as
+        concurrent tasks, execution/asynchronous.rs:456-530): a secret x secret
+        fixed-point Dot on a replicated placement is executed together with every later
+        Dot whose operands are already computed (so none depends on another) and have the
+        same placement, dtype and shapes -- one batched GEMM / reshare / TruncPr for all
+        (fixedpoint.dot_many).  Returns False when there is nothing to batch."""
+        def key(o):
+            if not isinstance(o.placement, ReplicatedPlacement):
+                return None
+            if any(n not in self.env for n in o.inputs):
+                return None
+            x, y = (self.at(o, self.env[n]) for n in o.inputs)
+            if x.kind != "tensor" or y.kind != "tensor" or x.dtype is None:
+                return None
+            if not x.dtype.is_fixed or x.dtype != y.dtype or x.is_host or x.is_mir or y.is_mir:
+                return None
+            if self._public(x) is not None or self._public(y) is not None:
+                return None
+            try:
+                sx, sy = fxp.shape_of(self.sess, x.v), fxp.shape_of(self.sess, y.v)
+            except Exception:  # noqa: BLE001 - symbolic/unknown shapes: no batching
+                return None
+            if len(sx) != 2 or len(sy) != 2:
+                return None
+            return (o.placement, x.dtype, tuple(sx), tuple(sy)), x, y
+
+        k0 = key(op)
+        if k0 is None:
+            return False
+        group = [(op, k0[1], k0[2])]
+        for o in later:
+            if len(group) >= limit:
+                break
+            if o.kind != "Dot" or o.name in self.env:
+                continue
+            k = key(o)
+            if k is not None and k[0] == k0[0]:
+                group.append((o, k[1], k[2]))
+        if len(group) == 1:
+            return False
+        dtype = k0[1].dtype
+        with span("op.Dot.batched", n=len(group)):
+            outs = fxp.dot_many(self.sess, [(x.v, y.v) for _, x, y in group],
+                                dtype.fractional_precision)
+        for (o, x, _), r in zip(group, outs):
+            if self.on_op is not None:
+                self.on_op()
+            self.env[o.name] = LV(x.plc, "tensor", dtype, r)
+        return True
 
     # ------------------------------------------------------------------------
     # dialect-level operations (textual computations below the logical level)

@@ -135,6 +135,8 @@ class StackedSession(Session):
 
     # rows per pipelined dot+TruncPr (protocols/replicated.dot_trunc); 1 = no pipelining
     pipeline_chunks = 1
+    # the interpreter batches independent same-shape Dots into one launch sequence
+    batch_dots = True
 
     def side_stream(self):
         """The HIP stream that pipelined protocol tails run on (created on first use)."""
@@ -329,8 +331,10 @@ class StackedSession(Session):
     def p_dot_cross_rows(self, plc, x0, x1, r0, r1, prepared):
         return PV(plc, R.dot_cross_rows(x0.v, x1.v, r0, r1, prepared))
 
-    def p_dot_cross(self, plc, x0, x1, y0, y1):
-        return PV(plc, R.dot_cross(x0.v, x1.v, y0.v, y1.v, nb=1))
+    def p_dot_cross(self, plc, x0, x1, y0, y1, nbatch=0):
+        """``nbatch`` leading logical axes are batch axes (independent products, one
+        batched GEMM launch with the parties)."""
+        return PV(plc, R.dot_cross(x0.v, x1.v, y0.v, y1.v, nb=1 + nbatch))
 
     def p_add_zero_share(self, plc, z, kind="arith"):
         return PV(plc, R.rss_cross_k(kind, z.v, None, None, None, self.key_ptr(plc, 0), 3,
