@@ -265,15 +265,29 @@ def abs_(sess, x: RepFixed) -> RepFixed:
     return _with(x, rep.sub(sess, x.t, rep.shl(sess, rep.mul(sess, s, x.t), 1)))
 
 
+def _stack0(sess, xs):
+    """Equal-shape values stacked on a new leading axis (one concat per share)."""
+    return concat(sess, [local(sess, x, "ExpandDims", axis=[0]) for x in xs], 0)
+
+
+def _unstack0(sess, x, n):
+    return [local(sess, x, "IndexAxis", axis=0, index=i) for i in range(n)]
+
+
 def maximum(sess, xs):
-    """Elementwise maximum of a list: tree of (less, mux)."""
+    """Elementwise maximum of a list: a tree of (less, mux) whose every level is ONE
+    stacked comparison and ONE stacked mux over all its pairs (log2(n) protocol
+    instances in all, not n - 1)."""
     xs = list(xs)
     while len(xs) > 1:
-        nxt = []
-        for i in range(0, len(xs) - 1, 2):
-            a, b = xs[i], xs[i + 1]
-            lt = rep.msb(sess, rep.sub(sess, a.t, b.t))  # a < b
-            nxt.append(mux(sess, lt, b, a))
+        h = len(xs) // 2
+        if h == 1:
+            a, b = xs[0], xs[1]
+            nxt = [mux(sess, rep.msb(sess, rep.sub(sess, a.t, b.t)), b, a)]  # a < b
+        else:
+            A, B = _stack0(sess, xs[0:2 * h:2]), _stack0(sess, xs[1:2 * h:2])
+            lt = rep.msb(sess, rep.sub(sess, A.t, B.t))
+            nxt = _unstack0(sess, mux(sess, lt, B, A), h)
         if len(xs) % 2:
             nxt.append(xs[-1])
         xs = nxt
@@ -537,24 +551,30 @@ def _bcast(sess, small: RepTensor, big: RepTensor) -> RepTensor:
 
 
 def argmax(sess, x: RepFixed, axis: int, upmost_index: int) -> RepTensor:
-    """Index of the maximum along ``axis`` as an arithmetic Z_2^64 sharing: tree of
-    (value, index) pairs reduced with less + mux (reference argmax.rs:6-96)."""
+    """Index of the maximum along ``axis`` as an arithmetic Z_2^64 sharing: a tree of
+    (value, index) pairs reduced with less + mux (reference argmax.rs:6-96).  Each tree
+    level is ONE stacked comparison over all its pairs and ONE mux that selects values
+    and indices together."""
     n = min(shape_of(sess, x)[axis], upmost_index)
     vals = [local(sess, x, "IndexAxis", axis=axis, index=i) for i in range(n)]
     bits = x.bits
-    idx = [rep.from_public(sess, x.plc, R.fill(shape_of(sess, vals[0]), i, bits, sess.device),
-                           bits) for i in range(n)]
+    idx = [RepFixed(rep.from_public(sess, x.plc, R.fill(shape_of(sess, vals[0]), i, bits,
+                                                        sess.device), bits), 0, x.integ)
+           for i in range(n)]
     pairs = list(zip(vals, idx))
     while len(pairs) > 1:
-        nxt = []
-        for i in range(0, len(pairs) - 1, 2):
-            (va, ia), (vb, ib) = pairs[i], pairs[i + 1]
-            lt = rep.b2a(sess, rep.msb(sess, rep.sub(sess, va.t, vb.t)), bits)  # a < b
-            v = _with(va, rep.mux(sess, lt, vb.t, va.t))
-            ix = rep.mux(sess, lt, ib, ia)
-            nxt.append((v, ix))
+        h = len(pairs) // 2
+        va = _stack0(sess, [p[0] for p in pairs[0:2 * h:2]])
+        vb = _stack0(sess, [p[0] for p in pairs[1:2 * h:2]])
+        ia = _stack0(sess, [p[1] for p in pairs[0:2 * h:2]])
+        ib = _stack0(sess, [p[1] for p in pairs[1:2 * h:2]])
+        lt = rep.b2a(sess, rep.msb(sess, rep.sub(sess, va.t, vb.t)), bits)  # a < b
+        lt2 = concat(sess, [lt, lt], 0)
+        sel = rep.mux(sess, lt2, concat(sess, [vb, ib], 0).t, concat(sess, [va, ia], 0).t)
+        both = _unstack0(sess, _with(va, sel), 2 * h)
+        nxt = [(both[i], RepFixed(both[h + i].t, 0, x.integ)) for i in range(h)]
         if len(pairs) % 2:
             nxt.append(pairs[-1])
         pairs = nxt
-    out = pairs[0][1]
+    out = pairs[0][1].t
     return rep.ring_cast(sess, out, 64) if bits != 64 else out
