@@ -87,7 +87,8 @@ def run_one(runtime, mode, n, k, n_iter):
     ref = REFERENCE_S.get((mode, k, n))
     mean = statistics.mean(times)
     return {"bench": "dot_product", "mode": mode, "n": n, "k": k, "seconds_mean": mean,
-            "seconds_min": min(times), "max_abs_err": float(np.abs(z - expect).max()),
+            "seconds_min": min(times), "seconds_median": statistics.median(times),
+            "seconds_all": times, "max_abs_err": float(np.abs(z - expect).max()),
             "reference_s": ref, "speedup_vs_reference": (ref / mean) if ref else None}
 
 

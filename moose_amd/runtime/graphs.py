@@ -179,6 +179,7 @@ class GraphPlan:
         torch.cuda.synchronize(self.device)
         self._stager = stager  # keep the staged constants alive
         self.replays = 0
+        self._pinned = {}
 
     def _decode(self, interp, outs) -> Dict[str, np.ndarray]:
         res = {}
@@ -192,10 +193,16 @@ class GraphPlan:
         for k, v in arguments.items():
             t = self.static.get(k)
             if isinstance(t, torch.Tensor):
-                src = torch.from_numpy(np.ascontiguousarray(
-                    np.asarray(v).view(np.int64) if np.asarray(v).dtype == np.uint64
-                    else np.asarray(v)))
-                t.copy_(src)
+                a = np.asarray(v)
+                a = a.view(np.int64) if a.dtype == np.uint64 else a
+                # stage through a pinned buffer: an asynchronous DMA on the replay stream
+                # instead of a pageable (bounce-buffered, host-blocking) copy per argument
+                pin = self._pinned.get(k)
+                if pin is None or pin.shape != t.shape or pin.dtype != t.dtype:
+                    pin = self._pinned[k] = torch.empty(t.shape, dtype=t.dtype,
+                                                        pin_memory=True)
+                np.copyto(pin.numpy(), a.reshape(pin.shape), casting="same_kind")
+                t.copy_(pin, non_blocking=True)
         self.keys.refresh()  # fresh randomness for this replay
         for g in self.graphs:
             g.replay()
