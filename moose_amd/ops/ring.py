@@ -264,35 +264,22 @@ def binary(op: str, a, b) -> RT:
             return RT(x & y, 1)
         if op == "or":
             return RT(x | y, 1)
-    if bits == 64:
-        x, y = a.data, b.data
-        if op == "add":
-            return RT(x + y, 64)
-        if op == "sub":
-            return RT(x - y, 64)
-        if op == "mul":
-            return RT(x * y, 64)
-        if op == "and":
-            return RT(x & y, 64)
-        if op == "or":
-            return RT(x | y, 64)
-        if op == "xor":
-            return RT(x ^ y, 64)
-    # Z_2^128: native kernel; scalar operands broadcast natively
+    # Z_2^64 / Z_2^128: one native kernel (libmoosex, gfx950 on the device); scalar
+    # operands broadcast natively, other broadcasts are expanded first
     na, nb_ = a.numel(), b.numel()
     if na != nb_ and na != 1 and nb_ != 1:
         a, b = _broadcast(a, b)
         na = nb_ = a.numel()
     n = max(na, nb_)
     out_shape = a.shape if na >= nb_ else b.shape
-    out = empty(out_shape, 128, a.device)
+    out = empty(out_shape, bits, a.device)
     ad, bd = a.data.contiguous(), b.data.contiguous()
     nat.check(
         nat.lib().mx_ew_binary(
-            nat.dev_of(ad), _BIN[op], 2, nat.ptr(ad), na, nat.ptr(bd), nb_, nat.ptr(out.data), n,
-            nat.stream_of(ad),
+            nat.dev_of(ad), _BIN[op], _words(bits), nat.ptr(ad), na, nat.ptr(bd), nb_,
+            nat.ptr(out.data), n, nat.stream_of(ad),
         ),
-        f"ring128 {op}",
+        f"ring{bits} {op}",
     )
     return out
 
@@ -305,28 +292,12 @@ def unary(op: str, a: RT, k: int = 0) -> RT:
         if op == "not":
             return RT(a.data ^ 1, 1)
         return RT(a.data.clone() if k == 0 else torch.zeros_like(a.data), 1)
-    if bits == 64:
-        x = a.data
-        if op == "neg":
-            return RT(-x, 64)
-        if op == "not":
-            return RT(~x, 64)
-        if op == "shl":
-            return RT(torch.zeros_like(x) if k >= 64 else (x << k), 64)
-        if op == "shr":
-            if k == 0:
-                return RT(x.clone(), 64)
-            if k >= 64:
-                return RT(torch.zeros_like(x), 64)
-            return RT((x >> k) & ((1 << (64 - k)) - 1), 64)
-        if op == "sar":
-            return RT(x >> min(k, 63), 64)
-    out = empty(a.shape, 128, a.device)
+    out = empty(a.shape, bits, a.device)
     ad = a.data.contiguous()
     nat.check(
         nat.lib().mx_ew_unary(
-            nat.dev_of(ad), _UN[op], 2, nat.ptr(ad), nat.ptr(out.data), a.numel(), int(k),
-            nat.stream_of(ad),
+            nat.dev_of(ad), _UN[op], _words(bits), nat.ptr(ad), nat.ptr(out.data), a.numel(),
+            int(k), nat.stream_of(ad),
         ),
         f"ring128 {op}",
     )
