@@ -1,0 +1,685 @@
+// Exact ring GEMM over Z_2^64 / Z_2^128 by multi-modular (CRT) int8 MFMA products.
+//
+// The limb GEMM (gemm_mfma.hip) splits every ring element into L 8-bit limbs and needs the
+// L(L+1)/2 limb-pair products on or below the anti-diagonal: 136 int8 GEMMs for Z_2^128,
+// 36 for Z_2^64.  Here the exact INTEGER product is computed instead, in residues:
+//
+//   * every ring element x is read as its signed representative X in [-2^(w-1), 2^(w-1));
+//     the integer product Z = sum_k X_k Y_k then satisfies |Z| <= K' 2^(2w-2);
+//   * n pairwise-coprime moduli p_i <= 256 (256, 255, 253, 251, ...) with product
+//     M > |Z| / 0.45 are chosen -- 37 for Z_2^128 at K' = 8192, 18 for Z_2^64;
+//   * each operand is reduced to centered int8 residues (prep kernels, one udot4 per 4 bytes
+//     of the element + one fp32 rounding), and ONE int8 GEMM per modulus gives
+//     acc_i = Z mod p_i exactly in i32 (K' <= 2^15 keeps the epilogue's fp32 rounding exact);
+//   * the CRT reconstruction  Z = sum_i c_i (M/p_i) - q M,  c_i = Z (M/p_i)^-1 mod p_i,
+//     q = round(sum_i c_i / p_i), is evaluated mod 2^w:  z = sum_i c_i W_i - q (M mod 2^w)
+//     with W_i = (M/p_i) mod 2^w.  The inverse (M/p_i)^-1 is folded into A's residues, so
+//     the GEMM epilogue only reduces acc_i mod p_i (centered, stored as one byte).
+//
+// So a Z_2^128 product costs 37 int8 GEMMs instead of 136 (3.7x fewer MFMAs), Z_2^64 18
+// instead of 36, at the price of wider operand prep and one reconstruction pass.  (The same
+// idea as the Ozaki-II / multi-modular emulation of high-precision GEMM on integer matrix
+// units; here the target is modular rather than floating-point arithmetic.)
+//
+// Kernels:
+//   k_crt_prep<T, TRANS>  operand -> n residue planes in a blocked, swizzled int8 image
+//                         [g = batch*n + i][tile][k-step][256 rows][64 bytes] (one 16 KB
+//                         image per (tile, k-step), LDS-DMA ready, ds_read_b128 conflict free)
+//   k_crt_gemm            256x256 block tile, 4 waves (1 per SIMD) of 128x128, K-step 64,
+//                         3-stage LDS-DMA ring, one barrier per step; epilogue reduces the
+//                         i32 accumulators mod p_i and stores one byte per output element in
+//                         MFMA register order (16 B per lane per 32x32 block)
+//   k_crt_recon<T>        n residue bytes per element -> ring element (sum c_i W_i - q Mw),
+//                         optionally accumulated into C
+// Mode 1 (RSS cross GEMM, as in gemm_mfma.hip): A' = [A0 | A1], B' = [B0 + B1 ; B0].
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+
+#include "moosex.h"
+
+namespace {
+
+using u64 = uint64_t;
+using u128 = unsigned __int128;
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+constexpr int kMaxMod = 48;
+// pairwise coprime, descending: 2^8, 3*5*17, 11*23, 13*19, primes, 7*31, primes
+constexpr int kModuli[kMaxMod] = {256, 255, 253, 251, 247, 241, 239, 233, 229, 227, 223, 217,
+                                  211, 199, 197, 193, 191, 181, 179, 173, 167, 163, 157, 151,
+                                  149, 139, 137, 131, 127, 113, 109, 107, 103, 101, 97,  89,
+                                  83,  79,  73,  71,  67,  61,  59,  53,  47,  43,  41,  37};
+
+constexpr int BM = 256;          // block tile rows (A side) = cols (B side)
+constexpr int BK = 64;           // k bytes per stage
+constexpr int kImg = BM * BK;    // one operand image per (tile, k-step): 16 KB
+constexpr int kStages = 3;       // LDS ring depth
+constexpr int kStageBytes = 2 * kImg;
+constexpr int kCrTile = BM * BM;  // residue bytes of one output tile (64 KB)
+
+// byte offset of 16-byte chunk c (0..3) of image row r: chunks XOR-swizzled by (r >> 2) & 3
+// so that the 16 lanes of each ds_read_b128 lane group hit 16 distinct 16-byte bank slots
+__device__ __host__ inline int img_off(int r, int c) { return r * BK + 16 * (c ^ ((r >> 2) & 3)); }
+
+// --- tables ---------------------------------------------------------------------------------
+struct PrepTab {  // operand residues
+  int n;
+  int p[kMaxMod];
+  float rcp[kMaxMod];
+  uint32_t w[kMaxMod][4];  // weight of byte j of the element = byte j%4 of word j/4
+  uint32_t neg[kMaxMod];   // added when the element is negative: (p - 2^w mod p) [* inv] mod p
+  uint32_t mul0;           // p = 256: residue = (byte0 * mul0) mod 256
+};
+struct EpiTab {  // GEMM epilogue
+  int n;
+  int p[kMaxMod];
+  float pf[kMaxMod];
+  float rcp[kMaxMod];
+  int t16[kMaxMod];  // 2^16 mod p
+};
+struct RecTab {  // reconstruction
+  int n;
+  float rcp[kMaxMod];
+  uint16_t W[kMaxMod][8];  // (M / p_i) mod 2^w, 16-bit words
+  uint16_t Mw[8];          // M mod 2^w
+};
+
+struct Tables {
+  int words = 0, n = 0;
+  PrepTab pa, pb;
+  EpiTab ep;
+  RecTab rc;
+};
+
+int modinv(int a, int m) {
+  int t = 0, nt = 1, r = m, nr = ((a % m) + m) % m;
+  while (nr) {
+    int q = r / nr, x;
+    x = t - q * nt; t = nt; nt = x;
+    x = r - q * nr; r = nr; nr = x;
+  }
+  return r == 1 ? (t % m + m) % m : -1;
+}
+
+// smallest n with prod p_i >= |Z|max / 0.45, |Z| <= K' 2^(2w-2)
+int moduli_needed(int words, int64_t kprime) {
+  const double need = 2.0 * 64 * words - 2 + std::log2((double)std::max<int64_t>(kprime, 1)) +
+                      std::log2(1 / 0.45);
+  double have = 0;
+  for (int i = 0; i < kMaxMod; ++i) {
+    have += std::log2((double)kModuli[i]);
+    if (have >= need) return i + 1;
+  }
+  return -1;
+}
+
+void build_tables(int words, int n, Tables& t) {
+  t.words = words;
+  t.n = n;
+  const int wbits = 64 * words;
+  const int nbytes = 8 * words;
+  u128 Mw = 1;
+  for (int i = 0; i < n; ++i) Mw *= (u128)kModuli[i];
+  if (words == 1) Mw &= ~(u64)0;
+  std::memset(&t.pa, 0, sizeof t.pa);
+  std::memset(&t.pb, 0, sizeof t.pb);
+  std::memset(&t.ep, 0, sizeof t.ep);
+  std::memset(&t.rc, 0, sizeof t.rc);
+  t.pa.n = t.pb.n = t.ep.n = t.rc.n = n;
+  for (int i = 0; i < n; ++i) {
+    const int p = kModuli[i];
+    u128 W = 1;
+    int rest = 1;  // (M / p) mod p
+    for (int j = 0; j < n; ++j)
+      if (j != i) {
+        W *= (u128)kModuli[j];
+        rest = (int)((int64_t)rest * kModuli[j] % p);
+      }
+    const int inv = modinv(rest, p);
+    for (int k = 0; k < 8; ++k) t.rc.W[i][k] = (uint16_t)(W >> (16 * k));
+    t.rc.rcp[i] = 1.0f / (float)p;
+    t.ep.p[i] = p;
+    t.ep.pf[i] = (float)p;
+    t.ep.rcp[i] = 1.0f / (float)p;
+    t.ep.t16[i] = (int)((1 << 16) % p);
+    t.pa.p[i] = t.pb.p[i] = p;
+    t.pa.rcp[i] = t.pb.rcp[i] = 1.0f / (float)p;
+    int pw = 1 % p;  // 256^j mod p
+    for (int j = 0; j < nbytes; ++j) {
+      const int wb = pw, wa = (int)((int64_t)pw * inv % p);
+      t.pb.w[i][j / 4] |= (uint32_t)wb << (8 * (j % 4));
+      t.pa.w[i][j / 4] |= (uint32_t)wa << (8 * (j % 4));
+      pw = pw * 256 % p;
+    }
+    // pw = 2^w mod p now; element negative => subtract 2^w, i.e. add p - 2^w mod p
+    const int negb = (p - pw) % p;
+    t.pb.neg[i] = (uint32_t)negb;
+    t.pa.neg[i] = (uint32_t)((int64_t)negb * inv % p);
+    if (i == 0) {
+      t.pa.mul0 = (uint32_t)inv;
+      t.pb.mul0 = 1;
+    }
+  }
+  for (int k = 0; k < 8; ++k) t.rc.Mw[k] = (uint16_t)(Mw >> (16 * k));
+  (void)wbits;
+}
+
+const Tables& tables_for(int words, int n) {
+  static std::mutex mu;
+  static Tables cache[3][kMaxMod + 1];
+  std::lock_guard<std::mutex> lk(mu);
+  Tables& t = cache[words][n];
+  if (t.n != n || t.words != words) build_tables(words, n, t);
+  return t;
+}
+
+// --- device helpers ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t pack4(int a, int b, int c, int d) {
+  const uint32_t lo = __builtin_amdgcn_perm((uint32_t)b, (uint32_t)a, 0x0c0c0400u);
+  const uint32_t hi = __builtin_amdgcn_perm((uint32_t)d, (uint32_t)c, 0x0c0c0400u);
+  return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+}
+
+template <class T>
+struct Words;
+template <>
+struct Words<u64> {
+  static constexpr int N = 2;
+};
+template <>
+struct Words<u128> {
+  static constexpr int N = 4;
+};
+
+// centered residue of the signed element whose little-endian 32-bit words are x[0..NW-1]
+template <int NW>
+__device__ __forceinline__ int residue(const uint32_t (&x)[NW], const uint32_t (&w)[4],
+                                       uint32_t neg, float p, float rcp) {
+  uint32_t s = (x[NW - 1] >> 31) * neg;
+#pragma unroll
+  for (int q = 0; q < NW; ++q) s = __builtin_amdgcn_udot4(x[q], w[q], s, false);
+  const float fs = (float)s;  // < 2^20: exact
+  const float qt = __builtin_rintf(fs * rcp);  // p odd: s/p is never within 1/(2p) of k + 1/2
+  return (int)__builtin_fmaf(-qt, p, fs);      // in [-(p-1)/2, (p-1)/2]
+}
+
+// One thread = (tile, k-step, image row r, 16-byte chunk c) of every residue plane.
+// TRANS = false: A' rows are M rows of [A0 | A1] (row-major [R][K] per batch, batch stride
+// xs elements).  TRANS = true: B' rows are the N columns of [B0 + B1 ; B0] ([K][R]).
+template <class T, bool TRANS>
+__global__ void __launch_bounds__(256)
+    k_crt_prep(const T* __restrict__ X0, const T* __restrict__ X1, int64_t R, int64_t K,
+               int64_t xs, int mode, int8_t* __restrict__ out, int64_t tiles, int64_t nkb,
+               const PrepTab tab) {
+  constexpr int NW = Words<T>::N;
+  const int64_t total = tiles * nkb * (BM * 4);
+  const int64_t b = blockIdx.y;
+  const T* x0 = X0 + b * xs;
+  const T* x1 = mode ? X1 + b * xs : x0;
+  const int n = tab.n;
+  const int64_t plane = tiles * nkb * (int64_t)kImg;
+  int8_t* ob = out + b * n * plane;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(g & 3);
+    const int r = (int)((g >> 2) & (BM - 1));
+    const int64_t q = g >> 10;
+    const int64_t kb = q % nkb, t = q / nkb;
+    const int64_t row = t * BM + r;
+    const int64_t k0 = kb * BK + c * 16;
+    uint32_t v[16][NW];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int64_t k = k0 + j;
+      T e = 0;
+      if (row < R) {
+        if (!TRANS) {
+          if (k < K) e = x0[row * K + k];
+          else if (mode && k < 2 * K) e = x1[row * K + (k - K)];
+        } else {
+          if (k < K) e = mode ? (T)(x0[k * R + row] + x1[k * R + row]) : x0[k * R + row];
+          else if (mode && k < 2 * K) e = x0[(k - K) * R + row];
+        }
+      }
+#pragma unroll
+      for (int w = 0; w < NW; ++w) v[j][w] = (uint32_t)(e >> (32 * w));
+    }
+    int8_t* base = ob + (t * nkb + kb) * (int64_t)kImg + img_off(r, c);
+    {  // p = 256: the low byte (times the folded inverse)
+      int rr[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) rr[j] = (int)(v[j][0] * tab.mul0);
+      v4i o;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) o[u] = (int)pack4(rr[4 * u], rr[4 * u + 1], rr[4 * u + 2], rr[4 * u + 3]);
+      *(v4i*)base = o;
+    }
+    for (int i = 1; i < n; ++i) {
+      const uint32_t w[4] = {tab.w[i][0], tab.w[i][1], tab.w[i][2], tab.w[i][3]};
+      const uint32_t neg = tab.neg[i];
+      const float p = (float)tab.p[i], rcp = tab.rcp[i];
+      int rr[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) rr[j] = residue<NW>(v[j], w, neg, p, rcp);
+      v4i o;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) o[u] = (int)pack4(rr[4 * u], rr[4 * u + 1], rr[4 * u + 2], rr[4 * u + 3]);
+      *(v4i*)(base + i * plane) = o;
+    }
+  }
+}
+
+// XCD-aware remap (as gemm_mfma.hip): consecutive tile ids land on one XCD
+__device__ inline int64_t xcd_remap(int64_t bid, int64_t nwg) {
+  const int64_t q = nwg / 8, r = nwg % 8;
+  const int64_t x = bid % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
+// s_waitcnt vmcnt(N) lgkmcnt(0) expcnt(7), gfx9 encoding (vmcnt split 4 + 2 bits)
+constexpr int waitcnt_vm_lgkm0(int vm) { return (vm & 15) | ((vm >> 4) << 14) | (7 << 4); }
+
+__device__ __forceinline__ int centered_mod(int acc, float pf, float rcp, int t16) {
+  // acc = hi 2^16 + lo; s = hi (2^16 mod p) + lo is exact in fp32 (|s| < 2^24)
+  const int hi = acc >> 16, lo = acc & 0xffff;
+  const int s = __mul24(hi, t16) + lo;
+  const float fs = (float)s;
+  const float qt = __builtin_rintf(fs * rcp);
+  return (int)__builtin_fmaf(-qt, pf, fs);
+}
+
+__global__ void __launch_bounds__(256, 1)
+    k_crt_gemm(const int8_t* __restrict__ RA, const int8_t* __restrict__ RB,
+               int8_t* __restrict__ CR, int64_t tiles_m, int64_t tiles_n, int64_t nkb, int gM,
+               const EpiTab ep) {
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+  const int64_t ntiles = tiles_m * tiles_n;
+  const int64_t tid_flat = xcd_remap(blockIdx.x, ntiles);
+  const int64_t group = tid_flat / (gM * tiles_n);
+  const int64_t first_m = group * gM;
+  const int64_t gm = tiles_m - first_m < gM ? tiles_m - first_m : gM;
+  const int64_t in_group = tid_flat % (gM * tiles_n);
+  const int64_t tm = first_m + in_group % gm, tn = in_group / gm;
+  const int64_t g = blockIdx.y;  // batch * n + modulus
+  const int mi = (int)(g % ep.n);
+
+  const int8_t* ga = RA + (g * tiles_m + tm) * nkb * (int64_t)kImg;
+  const int8_t* gb = RB + (g * tiles_n + tn) * nkb * (int64_t)kImg;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int half = lane >> 5;
+  const int sw = (lane >> 2) & 3;  // row swizzle of every fragment row this lane reads
+  const int rowa = (wr * 128 + (lane & 31)) * BK;
+  const int rowb = kImg + (wc * 128 + (lane & 31)) * BK;
+  const int co0 = 16 * (half ^ sw), co1 = 16 * ((2 + half) ^ sw);
+
+  // wave w issues pieces w, w+4, .. of the 32 1-KB pieces of a stage (16 A, then 16 B)
+  auto dma = [&](int64_t kb, int t, int8_t* dst_stage) {
+    const int pc = wave + 4 * t;  // 0..31
+    const bool is_b = pc >= 16;
+    const int pp = pc & 15;
+    const int8_t* src = (is_b ? gb : ga) + kb * kImg + pp * 1024 + lane * 16;
+    int8_t* dst = dst_stage + (is_b ? kImg : 0) + pp * 1024;
+    __builtin_amdgcn_global_load_lds((const void*)src,
+                                     (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+  };
+  auto stage = [&](int64_t kb) { return smem + (int)(kb % kStages) * kStageBytes; };
+  auto clampk = [&](int64_t kb) { return kb < nkb ? kb : nkb - 1; };
+
+  v16i acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v16i{0};
+
+  v4i fa0[4], fb0[4], fa1[4], fb1[4];
+  auto frags = [&](const int8_t* st, int co, v4i(&fa)[4], v4i(&fb)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa[i] = *(const v4i*)(st + rowa + i * 32 * BK + co);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[j] = *(const v4i*)(st + rowb + j * 32 * BK + co);
+  };
+
+  // prologue: stages 0, 1, 2 in flight; wait for stage 0
+#pragma unroll
+  for (int s = 0; s < kStages; ++s)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) dma(clampk(s), t, smem + s * kStageBytes);
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(16));
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  frags(smem, co0, fa0, fb0);
+
+  for (int64_t kb = 0; kb < nkb; ++kb) {
+    int8_t* cur = stage(kb);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0[i], fb0[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (i == 0 && j == 1) {  // second-half fragments, behind the first MFMAs (the
+          frags(cur, co1, fa1, fb1);  // compiler waits for all LDS reads before an MFMA
+          __builtin_amdgcn_sched_barrier(0);  // that follows any of them)
+        }
+      }
+    // my DMA of stage kb+1 landed (only stage kb+2's 8 pieces may be outstanding) and my
+    // reads of stage kb are done; after the barrier, everyone's are
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(8));
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    frags(stage(kb + 1), co0, fa0, fb0);  // past the end: stale bytes, never used
+    __builtin_amdgcn_sched_barrier(0);
+    const int64_t nxt = clampk(kb + kStages);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1[i], fb1[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (j & 1) {  // 8 DMA pieces of stage kb+3 into the buffer just released
+          dma(nxt, i * 2 + (j >> 1), cur);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // epilogue: centered acc mod p, one byte per element, MFMA register order
+  const float pf = ep.pf[mi], rcp = ep.rcp[mi];
+  const int t16 = ep.t16[mi];
+  int8_t* cr = CR + (g * ntiles + tm * tiles_n + tn) * (int64_t)kCrTile;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      // (p = 256 takes the same path: t16 = 0, exact power-of-two rounding, r in
+      // [-128, 128] whose low byte is the residue)
+      int rr[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) rr[e] = centered_mod(acc[i][j][e], pf, rcp, t16);
+      v4i o;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) o[u] = (int)pack4(rr[4 * u], rr[4 * u + 1], rr[4 * u + 2], rr[4 * u + 3]);
+      *(v4i*)(cr + ((wave * 16 + i * 4 + j) * 64 + lane) * 16) = o;
+    }
+}
+
+// One thread = 8 residue bytes (8 output elements of one MFMA block) of every modulus.
+template <class T>
+__global__ void __launch_bounds__(256)
+    k_crt_recon(const int8_t* __restrict__ CR, T* __restrict__ C, int64_t M, int64_t N,
+                int64_t tiles_m, int64_t tiles_n, int accumulate, const RecTab rc) {
+  constexpr int NK = sizeof(T) / 2;  // 16-bit words of a ring element
+  const int64_t ntiles = tiles_m * tiles_n;
+  const int64_t total = ntiles * (kCrTile / 8);
+  const int64_t b = blockIdx.y;
+  const int n = rc.n;
+  for (int64_t gt = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; gt < total;
+       gt += (int64_t)gridDim.x * blockDim.x) {
+    const int hf = (int)(gt & 1);
+    const int lane = (int)((gt >> 1) & 63);
+    const int64_t rest = gt >> 7;
+    const int blk = (int)(rest & 15);
+    const int wave = (int)((rest >> 4) & 3);
+    const int64_t tile = rest >> 6;
+    const int64_t off = tile * kCrTile + ((wave * 16 + blk) * 64 + lane) * 16 + hf * 8;
+    int acc[8][NK];
+    float qs[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      qs[e] = 0.f;
+#pragma unroll
+      for (int k = 0; k < NK; ++k) acc[e][k] = 0;
+    }
+    const int8_t* src = CR + b * n * ntiles * (int64_t)kCrTile + off;
+    for (int i = 0; i < n; ++i) {
+      const uint2 v = *(const uint2*)(src + i * ntiles * (int64_t)kCrTile);
+      const float rcp = rc.rcp[i];
+      int wk[NK];
+#pragma unroll
+      for (int k = 0; k < NK; ++k) wk[k] = rc.W[i][k];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = (int)(int8_t)(((e < 4 ? v.x : v.y) >> (8 * (e & 3))) & 0xff);
+        qs[e] = __builtin_fmaf((float)c, rcp, qs[e]);
+#pragma unroll
+        for (int k = 0; k < NK; ++k) acc[e][k] += __mul24(c, wk[k]);
+      }
+    }
+    const int64_t tm = tile / tiles_n, tn = tile % tiles_n;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int bi = blk >> 2, bj = blk & 3;
+    const int64_t gcol = tn * BM + wc * 128 + bj * 32 + (lane & 31);
+    T mw = 0;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) mw |= (T)rc.Mw[k] << (16 * k);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int ee = hf * 8 + e;  // accumulator register index in the 32x32 block
+      const int row = (ee & 3) + 8 * (ee >> 2) + 4 * (lane >> 5);
+      const int64_t grow = tm * BM + wr * 128 + bi * 32 + row;
+      T z = 0;
+#pragma unroll
+      for (int k = 0; k < NK; ++k) z += (T)(int64_t)acc[e][k] << (16 * k);
+      const int q = (int)__builtin_rintf(qs[e]);
+      z -= (T)(int64_t)q * mw;
+      if (grow < M && gcol < N) {
+        T* pc = C + (b * M + grow) * N + gcol;
+        *pc = accumulate ? (T)(*pc + z) : z;
+      }
+    }
+  }
+}
+
+inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+struct CPlan {
+  int n;
+  int64_t tiles_m, tiles_n, nkb, ra_bytes, rb_bytes, cr_bytes;
+};
+
+CPlan make_cplan(int words, int64_t batch, int64_t M, int64_t N, int64_t K, int mode) {
+  CPlan p;
+  const int64_t kprime = mode ? 2 * K : K;
+  p.n = moduli_needed(words, kprime);
+  p.tiles_m = (M + BM - 1) / BM;
+  p.tiles_n = (N + BM - 1) / BM;
+  p.nkb = round_up(kprime, BK) / BK;
+  p.ra_bytes = batch * p.n * p.tiles_m * p.nkb * (int64_t)kImg;
+  p.rb_bytes = batch * p.n * p.tiles_n * p.nkb * (int64_t)kImg;
+  p.cr_bytes = batch * p.n * p.tiles_m * p.tiles_n * (int64_t)kCrTile;
+  return p;
+}
+
+int gemm_group_m() {
+  const char* e = std::getenv("MOOSEX_CRT_GROUPM");
+  const int v = e ? std::atoi(e) : 4;
+  return v >= 1 && v <= 64 ? v : 4;
+}
+
+template <class T>
+void launch_prep(const CPlan& p, const Tables& tb, bool is_b, int64_t batch, int64_t R,
+                 int64_t K, int64_t xs, const T* X0, const T* X1, int mode, int8_t* out,
+                 hipStream_t st) {
+  const int64_t tiles = is_b ? p.tiles_n : p.tiles_m;
+  const int64_t work = tiles * p.nkb * (BM * 4);
+  const int gx = (int)std::min<int64_t>((work + 255) / 256, 16384);
+  if (is_b)
+    hipLaunchKernelGGL((k_crt_prep<T, true>), dim3(gx, (unsigned)batch), dim3(256), 0, st, X0,
+                       X1, R, K, xs, mode, out, tiles, p.nkb, tb.pb);
+  else
+    hipLaunchKernelGGL((k_crt_prep<T, false>), dim3(gx, (unsigned)batch), dim3(256), 0, st, X0,
+                       X1, R, K, xs, mode, out, tiles, p.nkb, tb.pa);
+}
+
+void launch_crt_gemm(const CPlan& p, const Tables& tb, int64_t batch, const int8_t* ra,
+                     const int8_t* rb, int8_t* cr, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)k_crt_gemm, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        kStages * kStageBytes);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_crt_gemm, dim3((unsigned)(p.tiles_m * p.tiles_n), (unsigned)(batch * p.n)),
+                     dim3(256), kStages * kStageBytes, st, ra, rb, cr, p.tiles_m, p.tiles_n,
+                     p.nkb, gemm_group_m(), tb.ep);
+}
+
+template <class T>
+void launch_recon(const CPlan& p, const Tables& tb, int64_t batch, int64_t M, int64_t N,
+                  const int8_t* cr, T* C, int accumulate, hipStream_t st) {
+  const int64_t work = p.tiles_m * p.tiles_n * (kCrTile / 8);
+  const int gx = (int)std::min<int64_t>((work + 255) / 256, 16384);
+  hipLaunchKernelGGL(k_crt_recon<T>, dim3(gx, (unsigned)batch), dim3(256), 0, st, cr, C, M, N,
+                     p.tiles_m, p.tiles_n, accumulate, tb.rc);
+}
+
+struct Ws {
+  void* ptr = nullptr;
+  int64_t bytes = 0;
+};
+std::mutex g_mu;
+Ws g_ws[16];
+
+// grow-only per-device scratch; replaced buffers are retired (a captured graph may hold them)
+void* workspace(int64_t bytes) {
+  int dev = 0;
+  hipGetDevice(&dev);
+  if (dev < 0 || dev >= 16) return nullptr;
+  std::lock_guard<std::mutex> lk(g_mu);
+  Ws& w = g_ws[dev];
+  if (w.bytes < bytes) {
+    int64_t want = 1 << 20;
+    while (want < bytes) want <<= 1;
+    void* q = nullptr;
+    if (hipMalloc(&q, want) != hipSuccess) return nullptr;
+    w.ptr = q;
+    w.bytes = want;
+  }
+  return w.ptr;
+}
+
+template <class T>
+int run_crt(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T* A1,
+            int64_t a_bstride, const T* B0, const T* B1, const int8_t* rb_pre, int mode, T* C,
+            int accumulate, hipStream_t st) {
+  constexpr int words = sizeof(T) / 8;
+  const CPlan p = make_cplan(words, batch, M, N, K, mode);
+  if (p.n < 0) return -6;
+  if ((mode ? 2 * K : K) > (1 << 15)) return -6;  // exact epilogue rounding bound
+  const Tables& tb = tables_for(words, p.n);
+  const int64_t need = p.ra_bytes + (rb_pre ? 0 : p.rb_bytes) + p.cr_bytes;
+  int8_t* ws = (int8_t*)workspace(need);
+  if (!ws) return -4;
+  int8_t* ra = ws;
+  int8_t* cr = ra + p.ra_bytes;
+  const int8_t* rb = rb_pre;
+  if (!rb) {
+    int8_t* rbw = cr + p.cr_bytes;
+    launch_prep<T>(p, tb, true, batch, N, K, K * N, B0, B1, mode, rbw, st);
+    rb = rbw;
+  }
+  launch_prep<T>(p, tb, false, batch, M, K, a_bstride, A0, A1, mode, ra, st);
+  launch_crt_gemm(p, tb, batch, ra, rb, cr, st);
+  launch_recon<T>(p, tb, batch, M, N, cr, C, accumulate, st);
+  const hipError_t e = hipGetLastError();
+  return e != hipSuccess ? -100 - (int)e : 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Moduli count for a K' (= K, or 2K in mode 1) inner dimension; -1 if out of range.
+int mx_crt_moduli(int words, int64_t kprime) {
+  if (words != 1 && words != 2) return -2;
+  return moduli_needed(words, kprime);
+}
+
+// Host copy of the tables (tests re-run the arithmetic on the CPU): per modulus i
+// p, inv-folded A byte weights, B byte weights, A/B negative corrections, W_i words; and Mw.
+int mx_crt_tables(int words, int n, int32_t* p_out, uint8_t* wa_out, uint8_t* wb_out,
+                  int32_t* nega_out, int32_t* negb_out, uint16_t* W_out, uint16_t* Mw_out) {
+  if ((words != 1 && words != 2) || n < 1 || n > kMaxMod) return -2;
+  const Tables& t = tables_for(words, n);
+  for (int i = 0; i < n; ++i) {
+    p_out[i] = t.ep.p[i];
+    for (int j = 0; j < 16; ++j) {
+      wa_out[i * 16 + j] = (uint8_t)(t.pa.w[i][j / 4] >> (8 * (j % 4)));
+      wb_out[i * 16 + j] = (uint8_t)(t.pb.w[i][j / 4] >> (8 * (j % 4)));
+    }
+    nega_out[i] = (int32_t)t.pa.neg[i];
+    negb_out[i] = (int32_t)t.pb.neg[i];
+    if (i == 0) {
+      nega_out[0] = (int32_t)t.pa.mul0;  // p = 256 uses the multiplier instead
+      negb_out[0] = 1;
+    }
+    for (int k = 0; k < 8; ++k) W_out[i * 8 + k] = t.rc.W[i][k];
+  }
+  for (int k = 0; k < 8; ++k) Mw_out[k] = t.rc.Mw[k];
+  return 0;
+}
+
+int mxh_gemm_crt(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
+                 const void* A1, const void* B0, const void* B1, int mode, void* C,
+                 int accumulate, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (words == 1)
+    return run_crt<u64>(batch, M, N, K, (const u64*)A0, (const u64*)A1, M * K, (const u64*)B0,
+                        (const u64*)B1, nullptr, mode, (u64*)C, accumulate, st);
+  if (words == 2)
+    return run_crt<u128>(batch, M, N, K, (const u128*)A0, (const u128*)A1, M * K,
+                         (const u128*)B0, (const u128*)B1, nullptr, mode, (u128*)C, accumulate,
+                         st);
+  return -2;
+}
+
+// Prepared-B variant (row-chunked dot pipeline): B' residues built once into a caller buffer.
+int64_t mxh_crt_b_bytes(int words, int64_t batch, int64_t N, int64_t K, int mode) {
+  if (words != 1 && words != 2) return 0;
+  const CPlan p = make_cplan(words, batch, BM, N, K, mode);
+  return p.n < 0 ? 0 : p.rb_bytes;
+}
+
+int mxh_crt_prep_b(int words, int64_t batch, int64_t K, int64_t N, const void* B0,
+                   const void* B1, int mode, void* rb, void* stream) {
+  const CPlan p = make_cplan(words, batch, BM, N, K, mode);
+  if (p.n < 0) return -6;
+  const Tables& tb = tables_for(words, p.n);
+  hipStream_t st = (hipStream_t)stream;
+  if (words == 1)
+    launch_prep<u64>(p, tb, true, batch, N, K, K * N, (const u64*)B0, (const u64*)B1, mode,
+                     (int8_t*)rb, st);
+  else if (words == 2)
+    launch_prep<u128>(p, tb, true, batch, N, K, K * N, (const u128*)B0, (const u128*)B1, mode,
+                      (int8_t*)rb, st);
+  else
+    return -2;
+  const hipError_t e = hipGetLastError();
+  return e != hipSuccess ? -100 - (int)e : 0;
+}
+
+int mxh_crt_with_b(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
+                   const void* A1, int64_t a_bstride, int mode, const void* rb, void* C,
+                   int accumulate, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (words == 1)
+    return run_crt<u64>(batch, M, N, K, (const u64*)A0, (const u64*)A1, a_bstride, nullptr,
+                        nullptr, (const int8_t*)rb, mode, (u64*)C, accumulate, st);
+  if (words == 2)
+    return run_crt<u128>(batch, M, N, K, (const u128*)A0, (const u128*)A1, a_bstride, nullptr,
+                         nullptr, (const int8_t*)rb, mode, (u128*)C, accumulate, st);
+  return -2;
+}
+
+}  // extern "C"

@@ -941,7 +941,42 @@ int mx_mfma_peak(int blocks, int iters, void* sink, void* stream) {
 
 }  // extern "C"
 
+// multi-modular (CRT) GEMM, gemm_crt.hip
+extern "C" int mxh_gemm_crt(int words, int64_t batch, int64_t M, int64_t N, int64_t K,
+                            const void* A0, const void* A1, const void* B0, const void* B1,
+                            int mode, void* C, int accumulate, void* stream);
+extern "C" int64_t mxh_crt_b_bytes(int words, int64_t batch, int64_t N, int64_t K, int mode);
+extern "C" int mxh_crt_prep_b(int words, int64_t batch, int64_t K, int64_t N, const void* B0,
+                              const void* B1, int mode, void* rb, void* stream);
+extern "C" int mxh_crt_with_b(int words, int64_t batch, int64_t M, int64_t N, int64_t K,
+                              const void* A0, const void* A1, int64_t a_bstride, int mode,
+                              const void* rb, void* C, int accumulate, void* stream);
+
+namespace {
+// 0 = auto (CRT for products with at least one full 256x256 output tile and K' >= 512),
+// 1 = CRT whenever K' allows, 2 = limb GEMM only.  MOOSEX_GEMM_CRT overrides the default.
+int g_crt_mode = -1;
+
+int crt_mode() {
+  if (g_crt_mode < 0) {
+    const char* e = std::getenv("MOOSEX_GEMM_CRT");
+    g_crt_mode = !e ? 0 : (e[0] == '0' ? 2 : (e[0] == '1' ? 1 : 0));
+  }
+  return g_crt_mode;
+}
+
+bool use_crt(int64_t M, int64_t N, int64_t K, int mode) {
+  const int64_t kp = mode ? 2 * K : K;
+  const int m = crt_mode();
+  if (m == 2 || kp > 32768) return false;
+  if (m == 1) return true;
+  return M >= 256 && N >= 256 && kp >= 512;
+}
+}  // namespace
+
 extern "C" {
+
+void mx_set_gemm_crt(int mode) { g_crt_mode = mode; }
 
 int64_t mx_gemm_workspace_bytes(int words, int64_t batch, int64_t M, int64_t N, int64_t K,
                                 int mode) {
@@ -970,12 +1005,14 @@ int mx_gemm_ws(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const 
 // [batch, M, K] tensor need no copy).  Used by the row-chunked dot pipeline.
 int64_t mx_gemm_b_bytes(int words, int64_t batch, int64_t N, int64_t K, int mode) {
   if (words != 1 && words != 2) return 0;
+  if (use_crt(256, N, K, mode)) return mxh_crt_b_bytes(words, batch, N, K, mode);
   if (K > max_k_chunk(words, mode)) return 0;
   return make_plan(words, batch, 64, N, K, mode).lb_bytes;
 }
 
 int mx_gemm_prep_b(int words, int64_t batch, int64_t K, int64_t N, const void* B0,
                    const void* B1, int mode, void* lb, void* stream) {
+  if (use_crt(256, N, K, mode)) return mxh_crt_prep_b(words, batch, K, N, B0, B1, mode, lb, stream);
   if (K > max_k_chunk(words, mode)) return -6;
   Plan p = make_plan(words, batch, 64, N, K, mode);
   hipStream_t st = (hipStream_t)stream;
@@ -993,6 +1030,9 @@ int mx_gemm_prep_b(int words, int64_t batch, int64_t K, int64_t N, const void* B
 int mx_gemm_with_b(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
                    const void* A1, int64_t a_bstride, int mode, const void* lb, void* C,
                    int accumulate, void* stream) {
+  if (use_crt(256, N, K, mode))  // the prepared B' holds residues (same test as prep_b)
+    return mxh_crt_with_b(words, batch, M, N, K, A0, A1, a_bstride, mode, lb, C, accumulate,
+                          stream);
   if (K > max_k_chunk(words, mode)) return -6;
   Plan p = make_plan(words, batch, M, N, K, mode);
   void* la = get_workspace(p.la_bytes);
@@ -1018,6 +1058,8 @@ int mx_gemm_with_b(int words, int64_t batch, int64_t M, int64_t N, int64_t K, co
 int mxh_gemm_mfma(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
                   const void* A1, const void* B0, const void* B1, int mode, void* C,
                   int accumulate, void* stream) {
+  if (use_crt(M, N, K, mode))
+    return mxh_gemm_crt(words, batch, M, N, K, A0, A1, B0, B1, mode, C, accumulate, stream);
   if (K > max_k_chunk(words, mode)) return -6;  // caller splits long K
   int64_t bytes = mx_gemm_workspace_bytes(words, batch, M, N, K, mode);
   void* ws = get_workspace(bytes);

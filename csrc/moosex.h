@@ -114,6 +114,12 @@ int mx_gemm_with_b(int words, int64_t batch, int64_t M, int64_t N, int64_t K, co
                    int accumulate, void* stream);
 // select the GEMM kernel: 0 = auto, 1 = force VALU reference kernel, 2 = force MFMA
 void mx_set_gemm_impl(int impl);
+// multi-modular (CRT) int8 GEMM for large products: 0 = auto, 1 = force, 2 = off
+void mx_set_gemm_crt(int mode);
+// moduli for an inner dimension K' (K, or 2K in mode 1); host copy of the CRT tables
+int mx_crt_moduli(int words, int64_t kprime);
+int mx_crt_tables(int words, int n, int32_t* p, uint8_t* wa, uint8_t* wb, int32_t* nega,
+                  int32_t* negb, uint16_t* W, uint16_t* Mw);
 
 // Fused stacked-session protocols (rss_fused.h).  s0/out0/out1 are [3, n] slot
 // vectors (party p holds out0[p] = z_p and out1[p] = z_{p+1}).

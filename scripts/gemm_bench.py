@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--bits", type=int, default=128)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--peak", action="store_true", help="also run the MFMA peak probe")
+    ap.add_argument("--impl", default="both", choices=["crt", "limb", "both"])
     ap.add_argument("--sweep", action="store_true",
                     help="sweep the tile-order knobs (MOOSEX_GEMM_GROUPM / MOOSEX_GEMM_XCD)")
     a = ap.parse_args()
@@ -26,16 +27,23 @@ def main():
     shp = (3, n, n) + ((2,) if bits == 128 else ())
     g = torch.Generator(device="cuda").manual_seed(0)
     xs = [R.RT(torch.randint(-2**62, 2**62, shp, device="cuda", generator=g), bits) for _ in range(4)]
-    R.dot_cross(*xs, nb=1)
-    torch.cuda.synchronize()
-    t = time.perf_counter()
-    for _ in range(a.iters):
-        R.dot_cross(*xs, nb=1)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t) / a.iters
+    from moose_amd.ops import native as nat
+
     L = 16 if bits == 128 else 8
-    ops = 2 * 3 * n * n * 2 * n * L * (L + 1) / 2
-    print(f"n={n} bits={bits} {dt*1e3:.2f} ms/call  {ops/dt/1e15:.2f} int8 POPS")
+    for impl in (("crt", "limb") if a.impl == "both" else (a.impl,)):
+        nat.lib().mx_set_gemm_crt(1 if impl == "crt" else 2)
+        nmul = nat.lib().mx_crt_moduli(bits // 64, 2 * n) if impl == "crt" else L * (L + 1) // 2
+        R.dot_cross(*xs, nb=1)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(a.iters):
+            R.dot_cross(*xs, nb=1)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t) / a.iters
+        ops = 2 * 3 * n * n * 2 * n * nmul
+        print(f"n={n} bits={bits} {impl} ({nmul} int8 GEMMs per party): {dt*1e3:.2f} ms/call  "
+              f"{ops/dt/1e15:.2f} int8 POPS executed", flush=True)
+    nat.lib().mx_set_gemm_crt(0)
     if a.sweep:
         import os
 

@@ -1,0 +1,228 @@
+"""Multi-modular (CRT) ring GEMM (csrc/gemm_crt.hip).
+
+CPU: the moduli choice and the host tables are checked by re-running the kernels'
+arithmetic (byte-weighted residues, centered reductions, CRT reconstruction with the
+rounded quotient) in numpy on random and worst-case operands against exact python-int
+products.  GPU: the kernels, forced on, are bit-exact against the host ring GEMM and the
+limb GEMM, including worst-case operands at the largest inner dimension of one call."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from moose_amd.ops import native as nat
+from moose_amd.ops import ring as R
+
+
+def _tables(words, n):
+    lib = nat.lib()
+    p = np.zeros(n, np.int32)
+    wa = np.zeros((n, 16), np.uint8)
+    wb = np.zeros((n, 16), np.uint8)
+    nega = np.zeros(n, np.int32)
+    negb = np.zeros(n, np.int32)
+    W = np.zeros((n, 8), np.uint16)
+    Mw = np.zeros(8, np.uint16)
+    ptr = lambda a: a.ctypes.data_as(nat.ctypes.c_void_p)  # noqa: E731
+    assert lib.mx_crt_tables(words, n, ptr(p), ptr(wa), ptr(wb), ptr(nega), ptr(negb), ptr(W),
+                             ptr(Mw)) == 0
+    join = lambda ws: sum(int(v) << (16 * k) for k, v in enumerate(ws))  # noqa: E731
+    return dict(p=p.astype(np.int64), wa=wa.astype(np.int64), wb=wb.astype(np.int64),
+                nega=nega.astype(np.int64), negb=negb.astype(np.int64),
+                W=[join(w) for w in W], Mw=join(Mw))
+
+
+def _centered(s, p):
+    return (s + p // 2) % p - p // 2
+
+
+def _residues(vals, bits, t, side):
+    """int8 residues [len(vals), n] exactly as k_crt_prep computes them."""
+    nb = bits // 8
+    v = np.array([[(x >> (8 * j)) & 0xFF for j in range(nb)] for x in vals], dtype=np.int64)
+    negbit = np.array([x >> (bits - 1) for x in vals], dtype=np.int64)
+    w = t["wa" if side == "a" else "wb"][:, :nb]
+    neg = t["nega" if side == "a" else "negb"]
+    s = v @ w.T + negbit[:, None] * neg[None, :]
+    out = _centered(s, t["p"][None, :])
+    out[:, 0] = ((v[:, 0] * neg[0]) & 0xFF) - (((v[:, 0] * neg[0]) & 0x80) << 1)  # p = 256
+    return out
+
+
+def _crt_dot(A, B, bits):
+    """A [M][K], B [K][N] python ints mod 2^bits -> the kernels' result."""
+    words = bits // 64
+    K = len(B)
+    n = nat.lib().mx_crt_moduli(words, K)
+    t = _tables(words, n)
+    M, N = len(A), len(B[0])
+    ra = _residues([x for row in A for x in row], bits, t, "a").reshape(M, K, n)
+    rb = _residues([x for row in B for x in row], bits, t, "b").reshape(K, N, n)
+    acc = np.einsum("mki,kni->mni", ra, rb)
+    c = _centered(acc, t["p"][None, None, :])
+    out = []
+    for m in range(M):
+        row = []
+        for j in range(N):
+            ci = [int(v) for v in c[m, j]]
+            q = round(sum(ci[i] / int(t["p"][i]) for i in range(n)))
+            z = sum(ci[i] * t["W"][i] for i in range(n)) - q * t["Mw"]
+            row.append(z % (1 << bits))
+        out.append(row)
+    return out
+
+
+def _exact(A, B, bits):
+    K = len(B)
+    return [[sum(A[m][k] * B[k][j] for k in range(K)) % (1 << bits) for j in range(len(B[0]))]
+            for m in range(len(A))]
+
+
+def test_moduli_counts_and_bound():
+    lib = nat.lib()
+    assert lib.mx_crt_moduli(2, 8192) == 37  # vs 136 limb-pair GEMMs
+    assert lib.mx_crt_moduli(1, 8192) == 18  # vs 36
+    for words in (1, 2):
+        for kp in (1, 100, 8192, 32768):
+            n = lib.mx_crt_moduli(words, kp)
+            t = _tables(words, n)
+            ps = [int(p) for p in t["p"]]
+            assert all(math.gcd(a, b) == 1 for i, a in enumerate(ps) for b in ps[i + 1:])
+            M = math.prod(ps)
+            zmax = kp * (1 << (2 * 64 * words - 2))
+            assert zmax <= 0.45 * M
+            # one modulus fewer would not do
+            assert kp == 1 or zmax > 0.45 * math.prod(ps[:-1]) or n == 1
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+def test_crt_arithmetic_random(bits):
+    rng = np.random.default_rng(bits)
+    M, K, N = 3, 37, 4
+    A = [[int.from_bytes(rng.bytes(bits // 8), "little") for _ in range(K)] for _ in range(M)]
+    B = [[int.from_bytes(rng.bytes(bits // 8), "little") for _ in range(N)] for _ in range(K)]
+    assert _crt_dot(A, B, bits) == _exact(A, B, bits)
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+@pytest.mark.parametrize("a,b", [("min", "min"), ("min", "max"), ("max", "max")])
+def test_crt_arithmetic_worst_case(bits, a, b):
+    """|Z| at its bound: every product at +-2^(2w-2), K' = 8192 (one bench-size call)."""
+    K = 8192
+    val = {"min": 1 << (bits - 1), "max": (1 << (bits - 1)) - 1}
+    A = [[val[a]] * K]
+    B = [[val[b]] for _ in range(K)]
+    assert _crt_dot(A, B, bits) == _exact(A, B, bits)
+
+
+# --- GPU ------------------------------------------------------------------------------------
+def rand_rt(shape, bits, seed):
+    g = torch.Generator().manual_seed(seed)
+    lo = torch.randint(-(2**63), 2**63 - 1, shape + ((2,) if bits == 128 else ()),
+                       generator=g, dtype=torch.int64)
+    return R.RT(lo, bits)
+
+
+def gpu(x):
+    return R.RT(x.data.cuda(), x.bits)
+
+
+def same(a, b):
+    assert a.bits == b.bits
+    assert torch.equal(a.data.cpu(), b.data.cpu())
+
+
+class _crt:
+    def __init__(self, mode):
+        self.mode = mode
+
+    def __enter__(self):
+        nat.lib().mx_set_gemm_crt(self.mode)
+
+    def __exit__(self, *a):
+        nat.lib().mx_set_gemm_crt(0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [64, 128])
+@pytest.mark.parametrize("shape", [(3, 5, 4), (70, 130, 96), (300, 520, 270)])
+def test_gpu_crt_gemm_matches_host(bits, shape):
+    M, K, N = shape
+    a, b = rand_rt((2, M, K), bits, 10), rand_rt((2, K, N), bits, 11)
+    with _crt(1):
+        d = R.dot(gpu(a), gpu(b), nb=1)
+    same(R.dot(a, b, nb=1), d)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [64, 128])
+def test_gpu_crt_cross_matches_host(bits):
+    M, K, N = 273, 260, 300
+    xs = [rand_rt((3, M, K), bits, 20 + i) for i in range(2)]
+    ys = [rand_rt((3, K, N), bits, 30 + i) for i in range(2)]
+    h = R.dot_cross(xs[0], xs[1], ys[0], ys[1], nb=1)
+    with _crt(1):
+        d = R.dot_cross(gpu(xs[0]), gpu(xs[1]), gpu(ys[0]), gpu(ys[1]), nb=1)
+    same(h, d)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [64, 128])
+def test_gpu_crt_matches_limb_gemm_large(bits):
+    M, K, N = 512, 2048, 768
+    xs = [gpu(rand_rt((3, M, K), bits, 50 + i)) for i in range(2)]
+    ys = [gpu(rand_rt((3, K, N), bits, 60 + i)) for i in range(2)]
+    with _crt(1):
+        c = R.dot_cross(*xs, *ys, nb=1)
+    with _crt(2):
+        lmb = R.dot_cross(*xs, *ys, nb=1)
+    same(c, lmb)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [64, 128])
+def test_gpu_crt_long_k_accumulates(bits):
+    # K above one call's exact limit: the caller splits K and accumulates into C
+    a, b = rand_rt((1, 64, 9000), bits, 40), rand_rt((1, 9000, 80), bits, 41)
+    with _crt(1):
+        d = R.dot(gpu(a), gpu(b), nb=1)
+    same(R.dot(a, b, nb=1), d)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [64, 128])
+@pytest.mark.parametrize("va,vb", [("min", "min"), ("min", "max"), ("max", "max")])
+def test_gpu_crt_worst_case_at_max_k(bits, va, vb):
+    """Mode 1 at K' = 8192 (the bench's call) with every operand at an extreme signed value."""
+    K = 4096
+    val = {"min": 1 << (bits - 1), "max": (1 << (bits - 1)) - 1}
+    mask = (1 << bits) - 1
+
+    def full(shape, v):
+        return R.fill(shape, v, bits, torch.device("cuda"))
+
+    x0, x1 = full((3, 64, K), val[va]), full((3, 64, K), val[va])
+    y0, y1 = full((3, K, 40), val[vb]), full((3, K, 40), val[vb])
+    with _crt(1):
+        c = R.dot_cross(x0, x1, y0, y1, nb=1)
+    # x0.(y0 + y1) + x1.y0 with every entry equal: K a (2b mod 2^w) + K a b
+    a, b = val[va], val[vb]
+    want = (K * a * ((2 * b) & mask) + K * a * b) & mask
+    got = R.to_ints(c)
+    assert (got == want).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [64, 128])
+def test_gpu_crt_prepared_b_rows(bits):
+    M, K, N = 600, 300, 280
+    xs = [rand_rt((3, M, K), bits, 70 + i) for i in range(2)]
+    ys = [rand_rt((3, K, N), bits, 80 + i) for i in range(2)]
+    want = R.dot_cross(xs[0], xs[1], ys[0], ys[1], nb=1)
+    with _crt(1):
+        pb = R.PreparedCross(gpu(ys[0]), gpu(ys[1]))
+        parts = [R.dot_cross_rows(gpu(xs[0]), gpu(xs[1]), r0, min(M, r0 + 256), pb)
+                 for r0 in range(0, M, 256)]
+    got = torch.cat([p.data.cpu() for p in parts], dim=1)
+    assert torch.equal(got, want.data)
