@@ -112,6 +112,7 @@ class Interpreter:
     # ------------------------------------------------------------------------
     def run(self, comp: Computation, arguments: dict) -> dict:
         self.arguments = arguments or {}
+        self._at_memo = {}
         comp = comp.toposorted()
         me = getattr(self.sess, "me", None)  # set for one-process-per-party sessions
         batch = getattr(self.sess, "batch_dots", False) and os.environ.get(
@@ -152,7 +153,7 @@ class Interpreter:
                 return None
             if any(n not in self.env for n in o.inputs):
                 return None
-            x, y = (self.at(o, self.env[n]) for n in o.inputs)
+            x, y = (self._at_memo_put(o, self.env[n]) for n in o.inputs)
             if x.kind != "tensor" or y.kind != "tensor" or x.dtype is None:
                 return None
             if not x.dtype.is_fixed or x.dtype != y.dtype or x.is_host or x.is_mir or y.is_mir:
@@ -392,8 +393,25 @@ class Interpreter:
     def _public(self, x: LV):
         return x.v.v if isinstance(x.v, MV) else None
 
+    def _at_memo_put(self, op, x: LV) -> LV:
+        """``at`` for the batching probe: the converted value (e.g. a fresh sharing of a host
+        input) is kept so that executing ``op`` later reuses it instead of sharing again."""
+        memo = self.__dict__.setdefault("_at_memo", {})
+        hit = memo.get((id(x), op.placement))
+        if hit is not None and hit[0] is x:
+            return hit[1]
+        conv = self.at(op, x)
+        if conv is not x:
+            memo[(id(x), op.placement)] = (x, conv)
+        return conv
+
     def at(self, op, x: LV) -> LV:
         plc = op.placement
+        memo = self.__dict__.get("_at_memo")
+        if memo:
+            hit = memo.pop((id(x), plc), None)
+            if hit is not None and hit[0] is x:
+                return hit[1]
         if isinstance(plc, HostPlacement):
             return self.to_host(x, plc.owner)
         if isinstance(plc, ReplicatedPlacement):
