@@ -1,10 +1,7 @@
-// AES-128 (FIPS-197) building blocks shared by the host and the gfx950 kernels.
-//
-// The PRG of moosex is AES-128 in counter mode: keystream block c is
-// AES_k(nonce_le64 || c_le64).  Host code uses AES-NI when available; device code uses a
-// 4 x 256-entry T-table staged in LDS (see ring_hip.hip).  Both are bit-exact with the
-// portable table implementation below, which the unit tests check against the FIPS-197
-// appendix vector.
+// AES-128 (FIPS-197) building blocks: the AES dialect (AES-GCM decryption of host
+// ciphertexts, protocols/aes.py) encrypts blocks with AES-NI when available and with the
+// portable T-table implementation below otherwise; the unit tests check both against the
+// FIPS-197 appendix vector.  (The protocols' PRF is ChaCha12, prf_core.h.)
 #pragma once
 #include <stdint.h>
 

@@ -25,7 +25,7 @@
 //   k_crt_prep<T, TRANS>  operand -> n residue planes in a blocked, swizzled int8 image
 //                         [g = batch*n + i][tile][k-step][256 rows][64 bytes] (one 16 KB
 //                         image per (tile, k-step), LDS-DMA ready, ds_read_b128 conflict free)
-//   k_crt_gemm            256x256 block tile, 4 waves (1 per SIMD) of 128x128, K-step 64,
+//   k_crt_gemm            256x256 block tile, 8 waves (2 per SIMD) of 128x64, K-step 64,
 //                         3-stage LDS-DMA ring, one barrier per step; epilogue reduces the
 //                         i32 accumulators mod p_i and stores one byte per output element in
 //                         MFMA register order (16 B per lane per 32x32 block)
@@ -295,76 +295,91 @@ __device__ __forceinline__ int centered_mod(int acc, float pf, float rcp, int t1
   return (int)__builtin_fmaf(-qt, pf, fs);
 }
 
-__global__ void __launch_bounds__(256, 1)
+// WR x WC waves per 256x256 block tile; wave tile (256/WR) x (256/WC) = MI x NJ MFMA
+// blocks of 32x32.  <2,2>: 4 waves of 128x128 (256 accumulator registers, one wave per
+// SIMD); <2,4>: 8 waves of 128x64 (128 accumulators, two waves per SIMD, so one wave's
+// LDS reads, address arithmetic and barrier waits hide behind its partner's MFMAs).
+template <int WR, int WC>
+__global__ void __launch_bounds__(64 * WR * WC, WR * WC / 4)
     k_crt_gemm(const int8_t* __restrict__ RA, const int8_t* __restrict__ RB,
-               int8_t* __restrict__ CR, int64_t tiles_m, int64_t tiles_n, int64_t nkb, int gM,
-               const EpiTab ep) {
+               int8_t* __restrict__ CR, int tiles_m, int tiles_n, int nkb, int gM,
+               const EpiTab ep, int dma_mask) {
+  constexpr int NW = WR * WC;
+  constexpr int MI = BM / WR / 32, NJ = BM / WC / 32;
+  constexpr int PPW = 32 / NW;  // DMA pieces per wave per stage
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
-  const int64_t ntiles = tiles_m * tiles_n;
-  const int64_t tid_flat = xcd_remap(blockIdx.x, ntiles);
-  const int64_t group = tid_flat / (gM * tiles_n);
-  const int64_t first_m = group * gM;
-  const int64_t gm = tiles_m - first_m < gM ? tiles_m - first_m : gM;
-  const int64_t in_group = tid_flat % (gM * tiles_n);
-  const int64_t tm = first_m + in_group % gm, tn = in_group / gm;
-  const int64_t g = blockIdx.y;  // batch * n + modulus
-  const int mi = (int)(g % ep.n);
+  const int ntiles = tiles_m * tiles_n;
+  const int tid_flat = (int)xcd_remap(blockIdx.x, ntiles);
+  const int group = tid_flat / (gM * tiles_n);
+  const int first_m = group * gM;
+  const int gm = tiles_m - first_m < gM ? tiles_m - first_m : gM;
+  const int in_group = tid_flat % (gM * tiles_n);
+  const int tm = first_m + in_group % gm, tn = in_group / gm;
+  const int g = blockIdx.y;  // batch * n + modulus
+  const int mi = g % ep.n;
 
-  const int8_t* ga = RA + (g * tiles_m + tm) * nkb * (int64_t)kImg;
-  const int8_t* gb = RB + (g * tiles_n + tn) * nkb * (int64_t)kImg;
+  const int8_t* ga = RA + ((int64_t)g * tiles_m + tm) * nkb * (int64_t)kImg;
+  const int8_t* gb = RB + ((int64_t)g * tiles_n + tn) * nkb * (int64_t)kImg;
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wave >> 1, wc = wave & 1;
+  const int wr = wave / WC, wc = wave % WC;
   const int half = lane >> 5;
   const int sw = (lane >> 2) & 3;  // row swizzle of every fragment row this lane reads
-  const int rowa = (wr * 128 + (lane & 31)) * BK;
-  const int rowb = kImg + (wc * 128 + (lane & 31)) * BK;
+  const int rowa = (wr * (BM / WR) + (lane & 31)) * BK;
+  const int rowb = kImg + (wc * (BM / WC) + (lane & 31)) * BK;
   const int co0 = 16 * (half ^ sw), co1 = 16 * ((2 + half) ^ sw);
 
-  // wave w issues pieces w, w+4, .. of the 32 1-KB pieces of a stage (16 A, then 16 B)
-  auto dma = [&](int64_t kb, int t, int8_t* dst_stage) {
-    const int pc = wave + 4 * t;  // 0..31
+  // wave w issues pieces w, w + NW, .. of the 32 1-KB pieces of a stage (16 A, then 16 B);
+  // the source advances by one 16 KB image per k-step
+  const int8_t* srcs[PPW];
+  int dsts[PPW];
+#pragma unroll
+  for (int t = 0; t < PPW; ++t) {
+    const int pc = wave + NW * t;
     const bool is_b = pc >= 16;
-    const int pp = pc & 15;
-    const int8_t* src = (is_b ? gb : ga) + kb * kImg + pp * 1024 + lane * 16;
-    int8_t* dst = dst_stage + (is_b ? kImg : 0) + pp * 1024;
-    __builtin_amdgcn_global_load_lds((const void*)src,
-                                     (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    srcs[t] = (is_b ? gb : ga) + (pc & 15) * 1024 + lane * 16;
+    dsts[t] = (is_b ? kImg : 0) + (pc & 15) * 1024;
+  }
+  auto dma = [&](int kb, int t, int8_t* dst_stage) {
+    if (!((dma_mask >> ((wave + NW * t) >> 4)) & 1)) return;  // timing experiments only
+    __builtin_amdgcn_global_load_lds((const void*)(srcs[t] + (int64_t)kb * kImg),
+                                     (__attribute__((address_space(3))) void*)(dst_stage + dsts[t]),
+                                     16, 0, 0);
   };
-  auto stage = [&](int64_t kb) { return smem + (int)(kb % kStages) * kStageBytes; };
-  auto clampk = [&](int64_t kb) { return kb < nkb ? kb : nkb - 1; };
 
-  v16i acc[4][4];
+  v16i acc[MI][NJ];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = v16i{0};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = v16i{0};
 
-  v4i fa0[4], fb0[4], fa1[4], fb1[4];
-  auto frags = [&](const int8_t* st, int co, v4i(&fa)[4], v4i(&fb)[4]) {
+  v4i fa0[MI], fb0[NJ], fa1[MI], fb1[NJ];
+  auto frags = [&](const int8_t* st, int co, v4i(&fa)[MI], v4i(&fb)[NJ]) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) fa[i] = *(const v4i*)(st + rowa + i * 32 * BK + co);
+    for (int i = 0; i < MI; ++i) fa[i] = *(const v4i*)(st + rowa + i * 32 * BK + co);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) fb[j] = *(const v4i*)(st + rowb + j * 32 * BK + co);
+    for (int j = 0; j < NJ; ++j) fb[j] = *(const v4i*)(st + rowb + j * 32 * BK + co);
   };
 
   // prologue: stages 0, 1, 2 in flight; wait for stage 0
 #pragma unroll
   for (int s = 0; s < kStages; ++s)
 #pragma unroll
-    for (int t = 0; t < 8; ++t) dma(clampk(s), t, smem + s * kStageBytes);
-  __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(16));
+    for (int t = 0; t < PPW; ++t) dma(s < nkb ? s : nkb - 1, t, smem + s * kStageBytes);
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(2 * PPW));
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   frags(smem, co0, fa0, fb0);
 
-  for (int64_t kb = 0; kb < nkb; ++kb) {
-    int8_t* cur = stage(kb);
+  int8_t* cur = smem;                    // stage kb
+  int8_t* nxt = smem + kStageBytes;      // stage kb + 1
+  int8_t* nn = smem + 2 * kStageBytes;   // stage kb + 2
+  for (int kb = 0; kb < nkb; ++kb) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0[i], fb0[j], acc[i][j], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
         if (i == 0 && j == 1) {  // second-half fragments, behind the first MFMAs (the
@@ -372,36 +387,43 @@ __global__ void __launch_bounds__(256, 1)
           __builtin_amdgcn_sched_barrier(0);  // that follows any of them)
         }
       }
-    // my DMA of stage kb+1 landed (only stage kb+2's 8 pieces may be outstanding) and my
+    // my DMA of stage kb+1 landed (only stage kb+2's pieces may be outstanding) and my
     // reads of stage kb are done; after the barrier, everyone's are
-    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(8));
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(PPW));
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    frags(stage(kb + 1), co0, fa0, fb0);  // past the end: stale bytes, never used
+    frags(nxt, co0, fa0, fb0);  // past the end: stale bytes, never used
     __builtin_amdgcn_sched_barrier(0);
-    const int64_t nxt = clampk(kb + kStages);
+    const int kn = kb + kStages < nkb ? kb + kStages : nkb - 1;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1[i], fb1[j], acc[i][j], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
-        if (j & 1) {  // 8 DMA pieces of stage kb+3 into the buffer just released
-          dma(nxt, i * 2 + (j >> 1), cur);
+        constexpr int EVERY = MI * NJ / PPW;
+        const int m = i * NJ + j;
+        if (m % EVERY == EVERY - 1) {  // this wave's pieces of stage kb+3 into the freed buffer
+          dma(kn, m / EVERY, cur);
           __builtin_amdgcn_sched_barrier(0);
         }
       }
+    int8_t* t = cur;
+    cur = nxt;
+    nxt = nn;
+    nn = t;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  // epilogue: centered acc mod p, one byte per element, MFMA register order
+  // epilogue: centered acc mod p, one byte per element, MFMA register order; 32x32 block
+  // (bi, bj) of the tile at byte ((bi * 8 + bj) * 64 + lane) * 16 of the tile's 64 KB
   const float pf = ep.pf[mi], rcp = ep.rcp[mi];
   const int t16 = ep.t16[mi];
-  int8_t* cr = CR + (g * ntiles + tm * tiles_n + tn) * (int64_t)kCrTile;
+  int8_t* cr = CR + ((int64_t)g * ntiles + tm * tiles_n + tn) * (int64_t)kCrTile;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       // (p = 256 takes the same path: t16 = 0, exact power-of-two rounding, r in
       // [-128, 128] whose low byte is the residue)
       int rr[16];
@@ -410,7 +432,8 @@ __global__ void __launch_bounds__(256, 1)
       v4i o;
 #pragma unroll
       for (int u = 0; u < 4; ++u) o[u] = (int)pack4(rr[4 * u], rr[4 * u + 1], rr[4 * u + 2], rr[4 * u + 3]);
-      *(v4i*)(cr + ((wave * 16 + i * 4 + j) * 64 + lane) * 16) = o;
+      const int bi = wr * MI + i, bj = wc * NJ + j;
+      *(v4i*)(cr + ((bi * 8 + bj) * 64 + lane) * 16) = o;
     }
 }
 
@@ -429,10 +452,9 @@ __global__ void __launch_bounds__(256)
     const int hf = (int)(gt & 1);
     const int lane = (int)((gt >> 1) & 63);
     const int64_t rest = gt >> 7;
-    const int blk = (int)(rest & 15);
-    const int wave = (int)((rest >> 4) & 3);
+    const int blk = (int)(rest & 63);  // 32x32 block (bi, bj) = (blk >> 3, blk & 7)
     const int64_t tile = rest >> 6;
-    const int64_t off = tile * kCrTile + ((wave * 16 + blk) * 64 + lane) * 16 + hf * 8;
+    const int64_t off = tile * kCrTile + (blk * 64 + lane) * 16 + hf * 8;
     int acc[8][NK];
     float qs[8];
 #pragma unroll
@@ -457,9 +479,8 @@ __global__ void __launch_bounds__(256)
       }
     }
     const int64_t tm = tile / tiles_n, tn = tile % tiles_n;
-    const int wr = wave >> 1, wc = wave & 1;
-    const int bi = blk >> 2, bj = blk & 3;
-    const int64_t gcol = tn * BM + wc * 128 + bj * 32 + (lane & 31);
+    const int bi = blk >> 3, bj = blk & 7;
+    const int64_t gcol = tn * BM + bj * 32 + (lane & 31);
     T mw = 0;
 #pragma unroll
     for (int k = 0; k < NK; ++k) mw |= (T)rc.Mw[k] << (16 * k);
@@ -467,7 +488,7 @@ __global__ void __launch_bounds__(256)
     for (int e = 0; e < 8; ++e) {
       const int ee = hf * 8 + e;  // accumulator register index in the 32x32 block
       const int row = (ee & 3) + 8 * (ee >> 2) + 4 * (lane >> 5);
-      const int64_t grow = tm * BM + wr * 128 + bi * 32 + row;
+      const int64_t grow = tm * BM + bi * 32 + row;
       T z = 0;
 #pragma unroll
       for (int k = 0; k < NK; ++k) z += (T)(int64_t)acc[e][k] << (16 * k);
@@ -522,17 +543,34 @@ void launch_prep(const CPlan& p, const Tables& tb, bool is_b, int64_t batch, int
                        X1, R, K, xs, mode, out, tiles, p.nkb, tb.pa);
 }
 
+// MOOSEX_CRT_DMA_MASK (timing experiments, wrong results): bit 0 = stream A, bit 1 = B
+int dma_mask() {
+  const char* e = std::getenv("MOOSEX_CRT_DMA_MASK");
+  return e ? std::atoi(e) : 3;
+}
+
+int crt_kernel() {  // MOOSEX_CRT_KERNEL: 1 = 4 waves of 128x128, 2 = 8 waves of 128x64
+  const char* e = std::getenv("MOOSEX_CRT_KERNEL");
+  return e && e[0] == '1' ? 1 : 2;
+}
+
 void launch_crt_gemm(const CPlan& p, const Tables& tb, int64_t batch, const int8_t* ra,
                      const int8_t* rb, int8_t* cr, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)k_crt_gemm, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipFuncSetAttribute((const void*)k_crt_gemm<2, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        kStages * kStageBytes);
+    hipFuncSetAttribute((const void*)k_crt_gemm<2, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         kStages * kStageBytes);
     attr = true;
   }
-  hipLaunchKernelGGL(k_crt_gemm, dim3((unsigned)(p.tiles_m * p.tiles_n), (unsigned)(batch * p.n)),
-                     dim3(256), kStages * kStageBytes, st, ra, rb, cr, p.tiles_m, p.tiles_n,
-                     p.nkb, gemm_group_m(), tb.ep);
+  const dim3 grid((unsigned)(p.tiles_m * p.tiles_n), (unsigned)(batch * p.n));
+  if (crt_kernel() == 1)
+    hipLaunchKernelGGL((k_crt_gemm<2, 2>), grid, dim3(256), kStages * kStageBytes, st, ra, rb, cr,
+                       (int)p.tiles_m, (int)p.tiles_n, (int)p.nkb, gemm_group_m(), tb.ep, dma_mask());
+  else
+    hipLaunchKernelGGL((k_crt_gemm<2, 4>), grid, dim3(512), kStages * kStageBytes, st, ra, rb, cr,
+                       (int)p.tiles_m, (int)p.tiles_n, (int)p.nkb, gemm_group_m(), tb.ep, dma_mask());
 }
 
 template <class T>

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "aes_core.h"
+#include "prf_core.h"
 #include "moosex.h"
 #include "ring_common.h"
 
@@ -53,7 +54,7 @@ void parallel_for(int64_t n, int64_t grain, F f) {
 }
 
 // ---------------------------------------------------------------------------
-// AES-NI keystream
+// AES-NI block encryption (the AES dialect; the PRF is ChaCha, prf_core.h)
 // ---------------------------------------------------------------------------
 struct NiKey {
   __m128i rk[11];
@@ -81,14 +82,17 @@ __attribute__((target("aes,sse4.1"))) inline __m128i ni_encrypt(const NiKey& k, 
   return _mm_aesenclast_si128(b, k.rk[10]);
 }
 
+__attribute__((target("aes,sse4.1"))) void aesni_blocks(const NiKey& k, const uint8_t* in,
+                                                        uint8_t* out, int64_t nblocks) {
+  for (int64_t b = 0; b < nblocks; ++b)
+    _mm_storeu_si128((__m128i*)(out + 16 * b),
+                     ni_encrypt(k, _mm_loadu_si128((const __m128i*)(in + 16 * b))));
+}
+
 bool have_aesni() {
   static bool v = __builtin_cpu_supports("aes");
   return v;
 }
-
-struct SwKey {
-  uint32_t rk[44];
-};
 
 uint32_t g_T0[256];
 struct TInit {
@@ -97,60 +101,49 @@ struct TInit {
   }
 } g_tinit;
 
-// Fill `nblocks` keystream blocks starting at counter ctr into out (16 bytes each)
-__attribute__((target("aes,sse4.1"))) void keystream_ni(const NiKey& k, uint64_t nonce,
-                                                        uint64_t ctr, uint8_t* out,
-                                                        int64_t nblocks) {
-  for (int64_t i = 0; i < nblocks; ++i) {
-    __m128i in = _mm_set_epi64x((long long)(ctr + i), (long long)nonce);
-    _mm_storeu_si128((__m128i*)(out + 16 * i), ni_encrypt(k, in));
-  }
-}
-
-void keystream_sw(const SwKey& k, uint64_t nonce, uint64_t ctr, uint8_t* out, int64_t nblocks) {
-  for (int64_t i = 0; i < nblocks; ++i) {
-    uint32_t w[4], o[4];
-    mx::ctr_block_words(nonce, ctr + i, w);
-    mx::encrypt_block_tt(k.rk, g_T0, mx::kSbox, w[0], w[1], w[2], w[3], o);
-    uint64_t lo, hi;
-    mx::block_to_u64(o, &lo, &hi);
-    memcpy(out + 16 * i, &lo, 8);
-    memcpy(out + 16 * i + 8, &hi, 8);
-  }
-}
-
+// The PRF keystream (prf_core.h): chunk c is part (c >> 6) & 3 of ChaCha12 block
+// ((c >> 8) << 6) | (c & 63), so a 256-chunk group is exactly 64 blocks.
 struct Prf {
-  NiKey ni;
-  SwKey sw;
-  bool use_ni;
-  explicit Prf(const uint8_t* key) {
-    use_ni = have_aesni();
-    if (use_ni)
-      ni_expand(key, &ni);
-    else
-      mx::expand_key(key, sw.rk);
-  }
+  uint32_t k[4];
+  explicit Prf(const uint8_t* key) { mx::key_words(key, k); }
+  // chunks [ctr, ctr + n) into out (16 bytes each)
   void blocks(uint64_t nonce, uint64_t ctr, uint8_t* out, int64_t n) const {
-    if (use_ni)
-      keystream_ni(ni, nonce, ctr, out, n);
-    else
-      keystream_sw(sw, nonce, ctr, out, n);
+    int64_t done = 0;
+    uint32_t w[64][16];
+    while (done < n) {
+      const uint64_t c = ctr + (uint64_t)done;
+      const uint64_t grp = c >> 8;
+      const int off = (int)(c & 255);
+      const int take = (int)std::min<int64_t>(256 - off, n - done);
+      uint64_t have = 0;  // bit b: block b of the group computed
+      for (int j = 0; j < take; ++j) {
+        const int idx = off + j, b = idx & 63, part = idx >> 6;
+        if (!((have >> b) & 1)) {
+          mx::chacha_block(k, nonce, (grp << 6) | (uint64_t)b, w[b]);
+          have |= 1ull << b;
+        }
+        memcpy(out + 16 * (done + j), &w[b][4 * part], 16);
+      }
+      done += take;
+    }
   }
 };
 
 // keystream bytes [byte0, byte0 + nbytes) into out
 void keystream_range(const Prf& p, uint64_t nonce, int64_t byte0, int64_t nbytes, uint8_t* out) {
   int64_t b0 = byte0 / 16, b1 = (byte0 + nbytes + 15) / 16;
-  uint8_t tmp[16 * 64];
+  uint8_t tmp[16 * 256];
   int64_t pos = 0;
-  for (int64_t b = b0; b < b1; b += 64) {
-    int64_t nb = std::min<int64_t>(64, b1 - b);
+  for (int64_t b = b0; b < b1;) {
+    // up to the end of b's 256-chunk group (whole ChaCha blocks per call)
+    const int64_t nb = std::min<int64_t>(256 - (b & 255), b1 - b);
     p.blocks(nonce, (uint64_t)b, tmp, nb);
     int64_t start = (b == b0) ? byte0 - b0 * 16 : 0;
     int64_t avail = nb * 16 - start;
     int64_t take = std::min(avail, nbytes - pos);
     memcpy(out + pos, tmp + start, take);
     pos += take;
+    b += nb;
   }
 }
 
@@ -526,6 +519,12 @@ int mx_prg(int dev, const uint8_t* key16, uint64_t nonce, uint64_t ctr0, void* o
 
 int mx_aes_encrypt_blocks(const uint8_t* key16, const uint8_t* in, uint8_t* out,
                           int64_t nblocks) {
+  if (have_aesni()) {  // AES-NI (the AES dialect and the AES tests); table code otherwise
+    NiKey k;
+    ni_expand(key16, &k);
+    aesni_blocks(k, in, out, nblocks);
+    return 0;
+  }
   uint32_t rk[44];
   mx::expand_key(key16, rk);
   for (int64_t b = 0; b < nblocks; ++b) {

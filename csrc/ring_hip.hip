@@ -1,12 +1,13 @@
 // gfx950 kernels for the moosex ring dialect: elementwise Z_2^64 / Z_2^128 / Z_2 ops,
-// the AES-128-CTR correlated-randomness generator, the fused RSS local step
+// the ChaCha12 correlated-randomness generator (prf_core.h), the fused RSS local step
 // (cross terms + zero share in one pass), fixed-point encode/decode, reductions.
 //
 // Design notes (MI355X):
 //  * every elementwise kernel is a grid-stride loop over 16-byte elements (one u128, two
 //    u64) so each lane issues dwordx4 loads; the grid is capped at 256 CUs x 8 blocks.
-//  * AES uses a T0 table + S-box staged in LDS by each block (1.25 KB), rotations give
-//    T1..T3; one AES block yields one u128 / two u64 / sixteen bits.
+//  * the PRF is ChaCha12 (VALU add/rotate/xor, no tables): a thread computes one 64-byte
+//    block and hands its four 16-byte chunks to elements 64 chunks apart; one chunk yields
+//    one u128 / two u64 / sixteen bits.
 //  * the fused RSS kernel (mxh_rss_cross) reads the four share streams once and writes
 //    z_i + alpha_i once: the whole local half of an RSS multiplication is one launch, for
 //    all three parties at once when they are stacked on one device.
@@ -15,8 +16,7 @@
 #include <algorithm>
 #include <cstring>
 
-#include "aes_core.h"
-#include "aes_dev.h"
+#include "prf_dev.h"
 #include "moosex.h"
 #include "ring_common.h"
 
@@ -217,27 +217,27 @@ __global__ void __launch_bounds__(256) k_sum_axis_wide(const T* __restrict__ a, 
 }
 
 // ---------------------------------------------------------------------------
-// AES
+// PRF (ChaCha12 keystream, prf_core.h / prf_dev.h)
 // ---------------------------------------------------------------------------
-using mxd::aes_ctr;
 using mxd::KeySrc;
 using mxd::Lane;
 using mxd::pick;
-using mxd::RK;
 using mxd::stage_keys;
-using mxd::stage_tables;
-using mxd::stage_tables_rep;
-using mxd::aes_ctr_rep;
+using mxd::prf_chunk;
+using mxd::kKeyWords;
 
-__global__ void __launch_bounds__(256) k_prg(RK key, uint64_t nonce, uint64_t ctr0, uint8_t* __restrict__ out,
-                      int64_t nbytes) {
-  __shared__ uint32_t T[mxd::kTTWords];
-    stage_tables_rep(T);
+struct RawKey {
+  uint32_t k[kKeyWords];
+};
+
+// raw keystream bytes from chunk ctr0 on (random access per chunk; tests and tools only)
+__global__ void __launch_bounds__(256) k_prg(RawKey key, uint64_t nonce, uint64_t ctr0,
+                                             uint8_t* __restrict__ out, int64_t nbytes) {
   int64_t nblocks = (nbytes + 15) / 16;
   for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < nblocks;
        b += (int64_t)gridDim.x * blockDim.x) {
     uint64_t lo, hi;
-    aes_ctr_rep(key.rk, T, nonce, ctr0 + b, &lo, &hi);
+    prf_chunk(key.k, nonce, ctr0 + b, &lo, &hi);
     if ((b + 1) * 16 <= nbytes) {
       uint64_t* o = (uint64_t*)(out + b * 16);
       o[0] = lo;
@@ -251,9 +251,10 @@ __global__ void __launch_bounds__(256) k_prg(RK key, uint64_t nonce, uint64_t ct
   }
 }
 
-// Element e of type T lives in keystream block e / (16 / sizeof(T)); one thread per block.
-// Key schedules are staged in LDS next to the T-table (from launch parameters or from
-// key slots in device memory, see aes_dev.h).
+// Element e of type T lives in keystream chunk e / (16 / sizeof(T)).  A thread computes one
+// ChaCha block per key and finishes the block's four chunks (64 chunks apart); g walks
+// (party, block).  Keys are staged in LDS (from launch parameters or from key slots in
+// device memory, see prf_dev.h).
 template <class T>
 __global__ void __launch_bounds__(256) k_rss_cross(int kind, const T* __restrict__ x0, const T* __restrict__ x1,
                             const T* __restrict__ y0, const T* __restrict__ y1,
@@ -261,65 +262,64 @@ __global__ void __launch_bounds__(256) k_rss_cross(int kind, const T* __restrict
                             KeySrc keys, uint64_t nonce, int pairs) {
   // pairs == 0: party p uses keys p and p+1 (one session, shared ring of keys);
   // pairs == 1: party p uses keys 2p and 2p+1 (parties of independent sessions)
-  __shared__ uint32_t Tt[mxd::kTTWords];
-  __shared__ uint32_t rks[mxd::kMaxKeySlots][44];
-  if (has_keys) {
-    stage_keys(rks, keys, pairs ? 2 * nparties : nparties + 1);
-    stage_tables_rep(Tt);
-  }
+  __shared__ uint32_t rks[mxd::kMaxKeySlots][kKeyWords];
+  if (has_keys) stage_keys(rks, keys, pairs ? 2 * nparties : nparties + 1);
   constexpr int P = Lane<T>::kPer;
-  const int64_t nb = (n + P - 1) / P;  // keystream blocks per party
-  const int64_t total = nb * nparties;
-  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total;
+  const int64_t nb = (n + P - 1) / P;  // keystream chunks per party
+  const int64_t nblk = (int64_t)mx::ks_blocks_for((uint64_t)nb);
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < nblk * nparties;
        g += (int64_t)gridDim.x * blockDim.x) {
-    const int p = (int)(g / nb);
-    const int64_t b = g % nb;
-    uint64_t alo = 0, ahi = 0, blo = 0, bhi = 0;
+    const int p = (int)(g / nblk);
+    const uint64_t B = (uint64_t)(g - p * nblk);
+    uint32_t wa[16], wb[16];
     if (has_keys) {
       const int ka = pairs ? 2 * p : p;
-      aes_ctr_rep(rks[ka], Tt, nonce, (uint64_t)b, &alo, &ahi);
-      aes_ctr_rep(rks[ka + 1], Tt, nonce, (uint64_t)b, &blo, &bhi);
+      mx::chacha_block(rks[ka], nonce, B, wa);
+      mx::chacha_block(rks[ka + 1], nonce, B, wb);
     }
 #pragma unroll
-    for (int j = 0; j < P; ++j) {
-      int64_t e = b * P + j;
-      if (e >= n) break;
-      int64_t i = (int64_t)p * n + e;
-      T v = 0;
-      if (x0 != nullptr && y0 != nullptr)
-        v = mxr::cross<T>(kind, x0[i], x1 ? x1[i] : (T)0, y0[i], y1 ? y1[i] : (T)0,
-                          x1 != nullptr, y1 != nullptr);
-      else if (x0 != nullptr)
-        v = x0[i];  // add-zero-share mode
-      if (has_keys) v = mxr::zs_combine<T>(kind, v, pick<T>(alo, ahi, j), pick<T>(blo, bhi, j));
-      out[i] = v;
+    for (int part = 0; part < 4; ++part) {
+      const int64_t b = (int64_t)mx::ks_chunk(B, part);
+      if (b >= nb) break;
+      uint64_t alo = 0, ahi = 0, blo = 0, bhi = 0;
+      if (has_keys) {
+        mx::part_u64(wa, part, &alo, &ahi);
+        mx::part_u64(wb, part, &blo, &bhi);
+      }
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        int64_t e = b * P + j;
+        if (e >= n) break;
+        int64_t i = (int64_t)p * n + e;
+        T v = 0;
+        if (x0 != nullptr && y0 != nullptr)
+          v = mxr::cross<T>(kind, x0[i], x1 ? x1[i] : (T)0, y0[i], y1 ? y1[i] : (T)0,
+                            x1 != nullptr, y1 != nullptr);
+        else if (x0 != nullptr)
+          v = x0[i];  // add-zero-share mode
+        if (has_keys) v = mxr::zs_combine<T>(kind, v, pick<T>(alo, ahi, j), pick<T>(blo, bhi, j));
+        out[i] = v;
+      }
     }
   }
 }
 
 // Stacked three-party ring (keys k0, k1, k2, k3 == k0): party p needs PRF(k_p) and
 // PRF(k_{p+1}), so each of the three keystreams is used by two parties.  One thread per
-// keystream block evaluates the three AES blocks once and finishes all three parties'
-// elements: 3 AES per block instead of 6 (the shares are identical to k_rss_cross).
+// ChaCha block evaluates the three keys' blocks once and finishes all three parties'
+// elements of the block's chunks (the shares are identical to k_rss_cross).
 template <class T>
-// default launch bounds on purpose: at 128 VGPRs it spills a little but runs more waves,
-// which is faster for the large launches it serves (small ones use k_rss_cross_ring3_lat)
-__global__ void k_rss_cross_ring3(int kind, const T* __restrict__ x0, const T* __restrict__ x1,
+__global__ void __launch_bounds__(256) k_rss_cross_ring3(int kind, const T* __restrict__ x0, const T* __restrict__ x1,
                                   const T* __restrict__ y0, const T* __restrict__ y1,
                                   T* __restrict__ out, T* __restrict__ out1, int64_t n,
                                   KeySrc keys, uint64_t nonce) {
-  __shared__ uint32_t Tt[256];
-  __shared__ uint8_t Sb[256];
-    __shared__ uint32_t rks[3][44];
+  __shared__ uint32_t rks[3][kKeyWords];
   stage_keys(rks, keys, 3);
-  stage_tables(Tt, Sb);
   constexpr int P = Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;
-  for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < nb;
-       b += (int64_t)gridDim.x * blockDim.x) {
-    uint64_t lo[3], hi[3];
-#pragma unroll
-    for (int q = 0; q < 3; ++q) aes_ctr(rks[q], Tt, Sb, nonce, (uint64_t)b, &lo[q], &hi[q]);
+  const uint32_t* const key[3] = {rks[0], rks[1], rks[2]};
+  const uint64_t nn[3] = {nonce, nonce, nonce};
+  mxd::walk_chunks<3>(nb, key, nn, [&](int64_t b, const uint64_t (&lo)[3], const uint64_t (&hi)[3]) {
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
       const int q = p == 2 ? 0 : p + 1;
@@ -340,13 +340,13 @@ __global__ void k_rss_cross_ring3(int kind, const T* __restrict__ x0, const T* _
         if (out1 != nullptr) out1[(int64_t)(p == 0 ? 2 : p - 1) * n + e] = z;
       }
     }
-  }
+  });
 }
 
 // One Kogge-Stone level for the three stacked parties (see mx_ks_level3_k).  A block
 // handles EPB elements: its NS = 3 (t) or 6 (t and pk') keystream values per element are
-// computed one AES per thread into LDS (one AES on the critical path), then EPB threads
-// finish all three parties' shares and write the reshared outputs directly.
+// computed one PRF chunk per thread into LDS (one PRF on the critical path), then EPB
+// threads finish all three parties' shares and write the reshared outputs directly.
 template <class T>
 __global__ void __launch_bounds__(256) k_ks_level3(const T* __restrict__ g0, const T* __restrict__ g1,
                                                    const T* __restrict__ p0, const T* __restrict__ p1,
@@ -355,12 +355,9 @@ __global__ void __launch_bounds__(256) k_ks_level3(const T* __restrict__ g0, con
                                                    int64_t n, int d, int both, KeySrc keys,
                                                    uint64_t nonce) {
   constexpr int EPB = 256 / 6;
-  __shared__ uint32_t Tt[256];
-  __shared__ uint8_t Sb[256];
-  __shared__ uint32_t rks[3][44];
+  __shared__ uint32_t rks[3][kKeyWords];
   __shared__ T ks[6][EPB];
   stage_keys(rks, keys, 3);
-  stage_tables(Tt, Sb);
   constexpr int P = Lane<T>::kPer;
   const int NS = both ? 6 : 3;
   const int tid = threadIdx.x, s = tid / EPB, le = tid % EPB;
@@ -368,7 +365,7 @@ __global__ void __launch_bounds__(256) k_ks_level3(const T* __restrict__ g0, con
     if (s < NS && e0 + le < n) {
       const int64_t c = (s < 3 ? 0 : n) + e0 + le;  // t at e, pk' at n + e
       uint64_t lo, hi;
-      aes_ctr(rks[s % 3], Tt, Sb, nonce, (uint64_t)(c / P), &lo, &hi);
+      prf_chunk(rks[s % 3], nonce, (uint64_t)(c / P), &lo, &hi);
       ks[s][le] = pick<T>(lo, hi, (int)(c % P));
     }
     __syncthreads();
@@ -413,25 +410,22 @@ __global__ void __launch_bounds__(256) k_ks_cross1(const T* __restrict__ g0, con
                                                    const T* __restrict__ p0, const T* __restrict__ p1,
                                                    T* __restrict__ z, int64_t n, int d, int both,
                                                    KeySrc keys, uint64_t nonce) {
-  __shared__ uint32_t Tt[256];
-  __shared__ uint8_t Sb[256];
-  __shared__ uint32_t rks[2][44];
+  __shared__ uint32_t rks[2][kKeyWords];
   stage_keys(rks, keys, 2);
-  stage_tables(Tt, Sb);
   constexpr int P = Lane<T>::kPer;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
        e += (int64_t)gridDim.x * blockDim.x) {
     uint64_t l0, h0, l1, h1;
-    aes_ctr(rks[0], Tt, Sb, nonce, (uint64_t)(e / P), &l0, &h0);
-    aes_ctr(rks[1], Tt, Sb, nonce, (uint64_t)(e / P), &l1, &h1);
+    prf_chunk(rks[0], nonce, (uint64_t)(e / P), &l0, &h0);
+    prf_chunk(rks[1], nonce, (uint64_t)(e / P), &l1, &h1);
     const T a0 = p0[e], a1 = p1[e];
     const T s0 = g0[e] << d, s1 = g1[e] << d;
     z[e] = (a0 & s0) ^ (a0 & s1) ^ (a1 & s0) ^ pick<T>(l0, h0, (int)(e % P)) ^
            pick<T>(l1, h1, (int)(e % P));
     if (both) {
       const int64_t c = n + e;
-      aes_ctr(rks[0], Tt, Sb, nonce, (uint64_t)(c / P), &l0, &h0);
-      aes_ctr(rks[1], Tt, Sb, nonce, (uint64_t)(c / P), &l1, &h1);
+      prf_chunk(rks[0], nonce, (uint64_t)(c / P), &l0, &h0);
+      prf_chunk(rks[1], nonce, (uint64_t)(c / P), &l1, &h1);
       const T u0 = a0 << d, u1 = a1 << d;
       z[c] = (a0 & u0) ^ (a0 & u1) ^ (a1 & u0) ^ pick<T>(l0, h0, (int)(c % P)) ^
              pick<T>(l1, h1, (int)(c % P));
@@ -439,9 +433,9 @@ __global__ void __launch_bounds__(256) k_ks_cross1(const T* __restrict__ g0, con
   }
 }
 
-// Latency variant for small launches (few keystream blocks): the block's 3 x EPB AES
-// blocks are computed one per thread into LDS, then EPB threads finish the elements --
-// one AES on the critical path instead of three.
+// Latency variant for small launches (few keystream chunks): the block's 3 x EPB chunks are
+// computed one per thread into LDS, then EPB threads finish the elements -- one PRF on the
+// critical path instead of three.
 template <class T>
 __global__ void __launch_bounds__(256) k_rss_cross_ring3_lat(int kind, const T* __restrict__ x0,
                                                              const T* __restrict__ x1,
@@ -451,19 +445,16 @@ __global__ void __launch_bounds__(256) k_rss_cross_ring3_lat(int kind, const T* 
                                                              T* __restrict__ out1, int64_t n,
                                                              KeySrc keys, uint64_t nonce) {
   constexpr int EPB = 256 / 3;
-  __shared__ uint32_t Tt[256];
-  __shared__ uint8_t Sb[256];
-  __shared__ uint32_t rks[3][44];
+  __shared__ uint32_t rks[3][kKeyWords];
   __shared__ uint64_t kl[3][EPB], kh[3][EPB];
   stage_keys(rks, keys, 3);
-  stage_tables(Tt, Sb);
   constexpr int P = Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;
   const int tid = threadIdx.x, s = tid / EPB, lb = tid % EPB;
   for (int64_t b0 = (int64_t)blockIdx.x * EPB; b0 < nb; b0 += (int64_t)gridDim.x * EPB) {
     if (s < 3 && b0 + lb < nb) {
       uint64_t lo, hi;
-      aes_ctr(rks[s], Tt, Sb, nonce, (uint64_t)(b0 + lb), &lo, &hi);
+      prf_chunk(rks[s], nonce, (uint64_t)(b0 + lb), &lo, &hi);
       kl[s][lb] = lo;
       kh[s][lb] = hi;
     }
@@ -498,23 +489,28 @@ __global__ void __launch_bounds__(256) k_rss_cross_ring3_lat(int kind, const T* 
 template <class T>
 __global__ void __launch_bounds__(256) k_prf_expand(T* __restrict__ out, int64_t n, int nkeys, KeySrc keys,
                              uint64_t nonce) {
-  __shared__ uint32_t Tt[mxd::kTTWords];
-    __shared__ uint32_t rks[4][44];
+  __shared__ uint32_t rks[4][kKeyWords];
   stage_keys(rks, keys, nkeys);
-  stage_tables_rep(Tt);
   constexpr int P = Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;
-  const int64_t total = nb * nkeys;
-  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total;
+  const int64_t nblk = (int64_t)mx::ks_blocks_for((uint64_t)nb);
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < nblk * nkeys;
        g += (int64_t)gridDim.x * blockDim.x) {
-    const int p = (int)(g / nb);
-    const int64_t b = g % nb;
-    uint64_t lo, hi;
-    aes_ctr_rep(rks[p], Tt, nonce, (uint64_t)b, &lo, &hi);
+    const int p = (int)(g / nblk);
+    const uint64_t B = (uint64_t)(g - p * nblk);
+    uint32_t w[16];
+    mx::chacha_block(rks[p], nonce, B, w);
 #pragma unroll
-    for (int j = 0; j < P; ++j) {
-      int64_t e = b * P + j;
-      if (e < n) out[(int64_t)p * n + e] = pick<T>(lo, hi, j);
+    for (int part = 0; part < 4; ++part) {
+      const int64_t b = (int64_t)mx::ks_chunk(B, part);
+      if (b >= nb) break;
+      uint64_t lo, hi;
+      mx::part_u64(w, part, &lo, &hi);
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        int64_t e = b * P + j;
+        if (e < n) out[(int64_t)p * n + e] = pick<T>(lo, hi, j);
+      }
     }
   }
 }
@@ -759,8 +755,8 @@ int mxh_sum_axis(int words, const void* a, void* out, int64_t outer, int64_t red
 int mxh_prg(const uint8_t* key16, uint64_t nonce, uint64_t ctr0, void* out, int64_t nbytes,
             void* stream) {
   if (nbytes == 0) return 0;
-  RK k;
-  mx::expand_key(key16, k.rk);
+  RawKey k;
+  mx::key_words(key16, k.k);
   hipLaunchKernelGGL(k_prg, dim3(grid_for((nbytes + 15) / 16)), dim3(kBlock), 0, S(stream), k,
                      nonce, ctr0, (uint8_t*)out, nbytes);
   MX_LAUNCH_CHECK();
@@ -781,7 +777,7 @@ int launch_rss_cross(int kind, int words, const void* x0, const void* x1, const 
     constexpr int P = 16 / (int)sizeof(T);
     if (ring3) {
       const int64_t blocks = (n + P - 1) / P;
-      if (blocks <= 16384) {  // latency-bound launch: one AES per thread, via LDS
+      if (blocks <= 16384) {  // latency-bound launch: one PRF chunk per thread, via LDS
         const int64_t g = (blocks + 84) / 85;
         hipLaunchKernelGGL(k_rss_cross_ring3_lat<T>, dim3((unsigned)g), dim3(kBlock), 0,
                            S(stream), kind, (const T*)x0, (const T*)x1, (const T*)y0,
@@ -789,13 +785,13 @@ int launch_rss_cross(int kind, int words, const void* x0, const void* x1, const 
         MX_LAUNCH_CHECK();
         return 0;
       }
-      hipLaunchKernelGGL(k_rss_cross_ring3<T>, dim3(grid_for(blocks)), dim3(kBlock), 0,
+      hipLaunchKernelGGL(k_rss_cross_ring3<T>, dim3(mxd::grid_for_chunks(blocks)), dim3(kBlock), 0,
                          S(stream), kind, (const T*)x0, (const T*)x1, (const T*)y0,
                          (const T*)y1, (T*)out, (T*)out1, n, k, nonce);
       MX_LAUNCH_CHECK();
       return 0;
     }
-    int64_t work = ((n + P - 1) / P) * nparties;
+    const int64_t work = (int64_t)mx::ks_blocks_for((n + P - 1) / P) * nparties;
     hipLaunchKernelGGL(k_rss_cross<T>, dim3(grid_for(work)), dim3(kBlock), 0, S(stream), kind,
                        (const T*)x0, (const T*)x1, (const T*)y0, (const T*)y1, (T*)out, n,
                        nparties, has_keys ? 1 : 0, k, nonce, pairs);
@@ -810,7 +806,7 @@ int launch_prf_expand(int words, void* out, int64_t n, int nkeys, const KeySrc& 
   if (nkeys < 1 || nkeys > 4) return -3;
   DEV_DISPATCH(words, T, {
     constexpr int P = 16 / (int)sizeof(T);
-    int64_t work = ((n + P - 1) / P) * nkeys;
+    const int64_t work = (int64_t)mx::ks_blocks_for((n + P - 1) / P) * nkeys;
     hipLaunchKernelGGL(k_prf_expand<T>, dim3(grid_for(work)), dim3(kBlock), 0, S(stream),
                        (T*)out, n, nkeys, k, nonce);
     MX_LAUNCH_CHECK();

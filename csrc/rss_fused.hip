@@ -2,12 +2,12 @@
 //
 // trunc_pr3: one pass per element computes the dealer's masks, both parties' masked
 // openings, the local truncation and the additive->replicated conversion for all three
-// parties -- six AES-CTR blocks and ~40 integer ops per element, one read of the three
-// input slots, one write of the two output share vectors.
-// share3: input sharing by a member party (two AES blocks per element).
+// parties -- six keystream chunks (prf_core.h) and ~40 integer ops per element, one read of
+// the three input slots, one write of the two output share vectors.
+// share3: input sharing by a member party (two keystream chunks per element).
 #include <hip/hip_runtime.h>
 
-#include "aes_dev.h"
+#include "prf_dev.h"
 #include "moosex.h"
 #include "rss_fused.h"
 
@@ -20,32 +20,23 @@ template <class T>
 __global__ void __launch_bounds__(256) k_trunc_pr3(const T* __restrict__ s0, T* __restrict__ out0, T* __restrict__ out1,
                             int64_t n, int m, mxd::KeySrc keys, uint64_t n_r0, uint64_t n_r1,
                             uint64_t n_t, uint64_t n_m, uint64_t n_z0, uint64_t n_z2) {
-  __shared__ uint32_t Tt[mxd::kTTWords];
-    __shared__ uint32_t rks[2][44];
+  __shared__ uint32_t rks[2][mxd::kKeyWords];
   mxd::stage_keys(rks, keys, 2);
-  mxd::stage_tables_rep(Tt);
   constexpr int P = mxd::Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;
-  const uint32_t* k0 = rks[0];
-  const uint32_t* k2 = rks[1];
-  for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < nb;
-       b += (int64_t)gridDim.x * blockDim.x) {
-    uint64_t r0l, r0h, r1l, r1h, tl, th, ml, mh, z0l, z0h, z2l, z2h;
-    mxd::aes_ctr_rep(k0, Tt, n_r0, b, &r0l, &r0h);
-    mxd::aes_ctr_rep(k2, Tt, n_r1, b, &r1l, &r1h);
-    mxd::aes_ctr_rep(k0, Tt, n_t, b, &tl, &th);
-    mxd::aes_ctr_rep(k0, Tt, n_m, b, &ml, &mh);
-    mxd::aes_ctr_rep(k0, Tt, n_z0, b, &z0l, &z0h);
-    mxd::aes_ctr_rep(k2, Tt, n_z2, b, &z2l, &z2h);
+  // streams r0, r1, t, m, z0, z2 (dealer keys k0 / k2)
+  const uint32_t* const key[6] = {rks[0], rks[1], rks[0], rks[0], rks[0], rks[1]};
+  const uint64_t nonce[6] = {n_r0, n_r1, n_t, n_m, n_z0, n_z2};
+  mxd::walk_chunks<6>(nb, key, nonce, [&](int64_t b, const uint64_t (&lo)[6], const uint64_t (&hi)[6]) {
 #pragma unroll
     for (int j = 0; j < P; ++j) {
       const int64_t i = b * P + j;
       if (i >= n) break;
-      const T z0 = mxd::pick<T>(z0l, z0h, j);
-      const T z2 = mxd::pick<T>(z2l, z2h, j);
-      const T z1 = mxf::trunc_pr_z1<T>(s0[i], s0[n + i], s0[2 * n + i], mxd::pick<T>(r0l, r0h, j),
-                                       mxd::pick<T>(r1l, r1h, j), mxd::pick<T>(tl, th, j),
-                                       mxd::pick<T>(ml, mh, j), z0, z2, m);
+      const T z0 = mxd::pick<T>(lo[4], hi[4], j);
+      const T z2 = mxd::pick<T>(lo[5], hi[5], j);
+      const T z1 = mxf::trunc_pr_z1<T>(s0[i], s0[n + i], s0[2 * n + i], mxd::pick<T>(lo[0], hi[0], j),
+                                       mxd::pick<T>(lo[1], hi[1], j), mxd::pick<T>(lo[2], hi[2], j),
+                                       mxd::pick<T>(lo[3], hi[3], j), z0, z2, m);
       out0[i] = z0;
       out0[n + i] = z1;
       out0[2 * n + i] = z2;
@@ -53,11 +44,11 @@ __global__ void __launch_bounds__(256) k_trunc_pr3(const T* __restrict__ s0, T* 
       out1[n + i] = z2;
       out1[2 * n + i] = z0;
     }
-  }
+  });
 }
 
-// Latency variant (small n): the six keystream blocks of each of the block's EPB AES
-// blocks are computed one per thread into LDS; then EPB threads finish the elements.
+// Latency variant (small n): the six keystream chunks of each of the block's EPB chunk
+// positions are computed one per thread into LDS; then EPB threads finish the elements.
 template <class T>
 __global__ void __launch_bounds__(256) k_trunc_pr3_lat(const T* __restrict__ s0, T* __restrict__ out0,
                                                        T* __restrict__ out1, int64_t n, int m,
@@ -65,12 +56,9 @@ __global__ void __launch_bounds__(256) k_trunc_pr3_lat(const T* __restrict__ s0,
                                                        uint64_t n_r1, uint64_t n_t, uint64_t n_m,
                                                        uint64_t n_z0, uint64_t n_z2) {
   constexpr int EPB = 256 / 6;
-  __shared__ uint32_t Tt[256];
-  __shared__ uint8_t Sb[256];
-  __shared__ uint32_t rks[2][44];
+  __shared__ uint32_t rks[2][mxd::kKeyWords];
   __shared__ uint64_t kl[6][EPB], kh[6][EPB];
   mxd::stage_keys(rks, keys, 2);
-  mxd::stage_tables(Tt, Sb);
   constexpr int P = mxd::Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;
   const int tid = threadIdx.x, s = tid / EPB, lb = tid % EPB;
@@ -81,7 +69,7 @@ __global__ void __launch_bounds__(256) k_trunc_pr3_lat(const T* __restrict__ s0,
   for (int64_t b0 = (int64_t)blockIdx.x * EPB; b0 < nb; b0 += (int64_t)gridDim.x * EPB) {
     if (s < 6 && b0 + lb < nb) {
       uint64_t lo, hi;
-      mxd::aes_ctr(rks[key_of], Tt, Sb, nonce_of, (uint64_t)(b0 + lb), &lo, &hi);
+      mxd::prf_chunk(rks[key_of], nonce_of, (uint64_t)(b0 + lb), &lo, &hi);
       kl[s][lb] = lo;
       kh[s][lb] = hi;
     }
@@ -114,23 +102,19 @@ template <class T>
 __global__ void __launch_bounds__(256) k_share3(int kind, const T* __restrict__ x, T* __restrict__ out0,
                          T* __restrict__ out1, int64_t n, int j0, mxd::KeySrc keys, uint64_t n1,
                          uint64_t na) {
-  __shared__ uint32_t Tt[mxd::kTTWords];
-    __shared__ uint32_t rks[2][44];
+  __shared__ uint32_t rks[2][mxd::kKeyWords];
   mxd::stage_keys(rks, keys, 2);
-  mxd::stage_tables_rep(Tt);
   constexpr int P = mxd::Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;
-  for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < nb;
-       b += (int64_t)gridDim.x * blockDim.x) {
-    uint64_t al, ah, bl, bh;
-    mxd::aes_ctr_rep(rks[0], Tt, n1, b, &al, &ah);
-    mxd::aes_ctr_rep(rks[1], Tt, na, b, &bl, &bh);
+  const uint32_t* const key[2] = {rks[0], rks[1]};
+  const uint64_t nonce[2] = {n1, na};
+  mxd::walk_chunks<2>(nb, key, nonce, [&](int64_t b, const uint64_t (&lo)[2], const uint64_t (&hi)[2]) {
 #pragma unroll
     for (int j = 0; j < P; ++j) {
       const int64_t i = b * P + j;
       if (i >= n) break;
-      const T r1 = mxd::pick<T>(al, ah, j);
-      const T ra = mxd::pick<T>(bl, bh, j);
+      const T r1 = mxd::pick<T>(lo[0], hi[0], j);
+      const T ra = mxd::pick<T>(lo[1], hi[1], j);
       const T xj = kind == MX_CROSS_BOOL ? (T)(x[i] ^ r1 ^ ra) : (T)(x[i] - r1 - ra);
       T slot[3];
       slot[j0] = xj;
@@ -142,7 +126,7 @@ __global__ void __launch_bounds__(256) k_share3(int kind, const T* __restrict__ 
         out1[p * n + i] = slot[(p + 1) % 3];
       }
     }
-  }
+  });
 }
 
 int launch_trunc_pr3(int words, const void* s0, void* out0, void* out1, int64_t n, int m,
@@ -150,7 +134,7 @@ int launch_trunc_pr3(int words, const void* s0, void* out0, void* out1, int64_t 
   if (n == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   const int64_t nblk = words == 1 ? (n + 1) / 2 : n;
-  if (nblk <= 8192 && (words == 1 || words == 2)) {  // latency-bound: one AES per thread
+  if (nblk <= 8192 && (words == 1 || words == 2)) {  // latency-bound: one PRF per thread
     const unsigned g = (unsigned)((nblk + 41) / 42);
     if (words == 1)
       hipLaunchKernelGGL(k_trunc_pr3_lat<u64>, dim3(g), dim3(256), 0, st, (const u64*)s0,
@@ -165,11 +149,11 @@ int launch_trunc_pr3(int words, const void* s0, void* out0, void* out1, int64_t 
   }
   if (words == 1) {
     int64_t nb = (n + 1) / 2;
-    hipLaunchKernelGGL(k_trunc_pr3<u64>, dim3(mxd::grid_for(nb)), dim3(256), 0, st,
+    hipLaunchKernelGGL(k_trunc_pr3<u64>, dim3(mxd::grid_for_chunks(nb)), dim3(256), 0, st,
                        (const u64*)s0, (u64*)out0, (u64*)out1, n, m, keys, nn[0], nn[1], nn[2],
                        nn[3], nn[4], nn[5]);
   } else if (words == 2) {
-    hipLaunchKernelGGL(k_trunc_pr3<u128>, dim3(mxd::grid_for(n)), dim3(256), 0, st,
+    hipLaunchKernelGGL(k_trunc_pr3<u128>, dim3(mxd::grid_for_chunks(n)), dim3(256), 0, st,
                        (const u128*)s0, (u128*)out0, (u128*)out1, n, m, keys, nn[0], nn[1], nn[2],
                        nn[3], nn[4], nn[5]);
   } else {
@@ -185,16 +169,16 @@ int launch_share3(int kind, int words, const void* x, void* out0, void* out1, in
   hipStream_t st = (hipStream_t)stream;
   switch (words) {
     case 0:
-      hipLaunchKernelGGL(k_share3<uint8_t>, dim3(mxd::grid_for((n + 15) / 16)), dim3(256), 0, st,
+      hipLaunchKernelGGL(k_share3<uint8_t>, dim3(mxd::grid_for_chunks((n + 15) / 16)), dim3(256), 0, st,
                          kind, (const uint8_t*)x, (uint8_t*)out0, (uint8_t*)out1, n, j, keys, n1,
                          na);
       break;
     case 1:
-      hipLaunchKernelGGL(k_share3<u64>, dim3(mxd::grid_for((n + 1) / 2)), dim3(256), 0, st, kind,
+      hipLaunchKernelGGL(k_share3<u64>, dim3(mxd::grid_for_chunks((n + 1) / 2)), dim3(256), 0, st, kind,
                          (const u64*)x, (u64*)out0, (u64*)out1, n, j, keys, n1, na);
       break;
     case 2:
-      hipLaunchKernelGGL(k_share3<u128>, dim3(mxd::grid_for(n)), dim3(256), 0, st, kind,
+      hipLaunchKernelGGL(k_share3<u128>, dim3(mxd::grid_for_chunks(n)), dim3(256), 0, st, kind,
                          (const u128*)x, (u128*)out0, (u128*)out1, n, j, keys, n1, na);
       break;
     default:

@@ -17,7 +17,7 @@
 // Key slots: component c passes (own k_p, next k_{p+1}[, k_all]) of its session.
 #include <hip/hip_runtime.h>
 
-#include "aes_dev.h"
+#include "prf_dev.h"
 #include "moosex.h"
 #include "rss_fused.h"
 
@@ -30,6 +30,13 @@ struct Roles {
   int r[3];
 };
 
+// Each thread walks ChaCha blocks (prf_dev.h) of one component: g = c * nblk + B, and the
+// body runs for the block's chunks b = ks_chunk(B, part).
+#define MX_PARTY_WALK(NB, NCOMP)                                                    \
+  const int64_t nblk = (int64_t)mx::ks_blocks_for((uint64_t)(NB));               \
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < nblk * (NCOMP); \
+       g += (int64_t)gridDim.x * blockDim.x)
+
 template <class T>
 __global__ void __launch_bounds__(256)
     k_trunc_party_r0(int64_t n, int m, Roles roles, const T* __restrict__ s0,
@@ -37,58 +44,79 @@ __global__ void __launch_bounds__(256)
                      T* __restrict__ out0, T* __restrict__ out1, mxd::KeySrc keys, uint64_t n_r0,
                      uint64_t n_r1, uint64_t n_t, uint64_t n_m, uint64_t n_z0, uint64_t n_z2,
                      int ncomp) {
-  __shared__ uint32_t Tt[mxd::kTTWords];
-  __shared__ uint32_t rks[mxd::kMaxKeySlots][44];
+  __shared__ uint32_t rks[mxd::kMaxKeySlots][mxd::kKeyWords];
   mxd::stage_keys(rks, keys, 2 * ncomp);
-  mxd::stage_tables_rep(Tt);
   constexpr int P = mxd::Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;
-  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < nb * ncomp;
-       g += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)(g / nb);
-    const int64_t b = g - c * nb;
+  MX_PARTY_WALK(nb, ncomp) {
+    const int c = (int)(g / nblk);
+    const uint64_t B = (uint64_t)(g - c * nblk);
     const int role = roles.r[c];
     const uint32_t* own = rks[2 * c];
     const uint32_t* nxt = rks[2 * c + 1];
     const int64_t base = (int64_t)c * n;
     if (role == 0) {  // k0 = own
-      uint64_t al, ah;
-      mxd::aes_ctr_rep(own, Tt, n_r0, b, &al, &ah);
+      uint32_t wa[16];
+      mx::chacha_block(own, n_r0, B, wa);
 #pragma unroll
-      for (int j = 0; j < P; ++j) {
-        const int64_t i = b * P + j;
-        if (i >= n) break;
-        msg[base + i] = mxf::trunc_mask0<T>(s0[base + i], s1[base + i], mxd::pick<T>(al, ah, j));
+      for (int part = 0; part < 4; ++part) {
+        const int64_t b = (int64_t)mx::ks_chunk(B, part);
+        if (b >= nb) break;
+        uint64_t al, ah;
+        mx::part_u64(wa, part, &al, &ah);
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+          const int64_t i = b * P + j;
+          if (i >= n) break;
+          msg[base + i] = mxf::trunc_mask0<T>(s0[base + i], s1[base + i], mxd::pick<T>(al, ah, j));
+        }
       }
     } else if (role == 1) {  // k2 = next
-      uint64_t al, ah;
-      mxd::aes_ctr_rep(nxt, Tt, n_r1, b, &al, &ah);
+      uint32_t wa[16];
+      mx::chacha_block(nxt, n_r1, B, wa);
 #pragma unroll
-      for (int j = 0; j < P; ++j) {
-        const int64_t i = b * P + j;
-        if (i >= n) break;
-        msg[base + i] = s1[base + i] + mxd::pick<T>(al, ah, j);
+      for (int part = 0; part < 4; ++part) {
+        const int64_t b = (int64_t)mx::ks_chunk(B, part);
+        if (b >= nb) break;
+        uint64_t al, ah;
+        mx::part_u64(wa, part, &al, &ah);
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+          const int64_t i = b * P + j;
+          if (i >= n) break;
+          msg[base + i] = s1[base + i] + mxd::pick<T>(al, ah, j);
+        }
       }
     } else if (role == 2) {  // k2 = own, k0 = next
-      uint64_t r0l, r0h, r1l, r1h, tl, th, ml, mh, z0l, z0h, z2l, z2h;
-      mxd::aes_ctr_rep(nxt, Tt, n_r0, b, &r0l, &r0h);
-      mxd::aes_ctr_rep(own, Tt, n_r1, b, &r1l, &r1h);
-      mxd::aes_ctr_rep(nxt, Tt, n_t, b, &tl, &th);
-      mxd::aes_ctr_rep(nxt, Tt, n_m, b, &ml, &mh);
-      mxd::aes_ctr_rep(nxt, Tt, n_z0, b, &z0l, &z0h);
-      mxd::aes_ctr_rep(own, Tt, n_z2, b, &z2l, &z2h);
+      // streams r0, r1, t, m, z0, z2
+      uint32_t w[6][16];
+      mx::chacha_block(nxt, n_r0, B, w[0]);
+      mx::chacha_block(own, n_r1, B, w[1]);
+      mx::chacha_block(nxt, n_t, B, w[2]);
+      mx::chacha_block(nxt, n_m, B, w[3]);
+      mx::chacha_block(nxt, n_z0, B, w[4]);
+      mx::chacha_block(own, n_z2, B, w[5]);
 #pragma unroll
-      for (int j = 0; j < P; ++j) {
-        const int64_t i = b * P + j;
-        if (i >= n) break;
-        T rt1;
-        u64 rm1;
-        mxf::trunc_dealer<T>(mxd::pick<T>(r0l, r0h, j), mxd::pick<T>(r1l, r1h, j),
-                             mxd::pick<T>(tl, th, j), mxd::pick<T>(ml, mh, j), m, &rt1, &rm1);
-        msg[base + i] = rt1;
-        msg_rm[base + i] = rm1;
-        out0[base + i] = mxd::pick<T>(z2l, z2h, j);
-        out1[base + i] = mxd::pick<T>(z0l, z0h, j);
+      for (int part = 0; part < 4; ++part) {
+        const int64_t b = (int64_t)mx::ks_chunk(B, part);
+        if (b >= nb) break;
+        uint64_t lo[6], hi[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) mx::part_u64(w[q], part, &lo[q], &hi[q]);
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+          const int64_t i = b * P + j;
+          if (i >= n) break;
+          T rt1;
+          u64 rm1;
+          mxf::trunc_dealer<T>(mxd::pick<T>(lo[0], hi[0], j), mxd::pick<T>(lo[1], hi[1], j),
+                               mxd::pick<T>(lo[2], hi[2], j), mxd::pick<T>(lo[3], hi[3], j), m,
+                               &rt1, &rm1);
+          msg[base + i] = rt1;
+          msg_rm[base + i] = rm1;
+          out0[base + i] = mxd::pick<T>(lo[5], hi[5], j);
+          out1[base + i] = mxd::pick<T>(lo[4], hi[4], j);
+        }
       }
     }
   }
@@ -101,47 +129,60 @@ __global__ void __launch_bounds__(256)
                      const u64* __restrict__ rrm, T* __restrict__ w, T* __restrict__ out0,
                      T* __restrict__ out1, mxd::KeySrc keys, uint64_t n_t, uint64_t n_m,
                      uint64_t n_z0, uint64_t n_z2, int ncomp) {
-  __shared__ uint32_t Tt[mxd::kTTWords];
-  __shared__ uint32_t rks[mxd::kMaxKeySlots][44];
+  __shared__ uint32_t rks[mxd::kMaxKeySlots][mxd::kKeyWords];
   mxd::stage_keys(rks, keys, 2 * ncomp);
-  mxd::stage_tables_rep(Tt);
   constexpr int P = mxd::Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;
-  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < nb * ncomp;
-       g += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)(g / nb);
-    const int64_t b = g - c * nb;
+  MX_PARTY_WALK(nb, ncomp) {
+    const int c = (int)(g / nblk);
+    const uint64_t B = (uint64_t)(g - c * nblk);
     const int role = roles.r[c];
     const int64_t base = (int64_t)c * n;
     if (role == 0) {
       const uint32_t* k0 = rks[2 * c];
-      uint64_t tl, th, ml, mh, zl, zh;
-      mxd::aes_ctr_rep(k0, Tt, n_t, b, &tl, &th);
-      mxd::aes_ctr_rep(k0, Tt, n_m, b, &ml, &mh);
-      mxd::aes_ctr_rep(k0, Tt, n_z0, b, &zl, &zh);
+      uint32_t wt[16], wm[16], wz[16];
+      mx::chacha_block(k0, n_t, B, wt);
+      mx::chacha_block(k0, n_m, B, wm);
+      mx::chacha_block(k0, n_z0, B, wz);
 #pragma unroll
-      for (int j = 0; j < P; ++j) {
-        const int64_t i = b * P + j;
-        if (i >= n) break;
-        const T cc = msg[base + i] + rmk[base + i];
-        const T z0 = mxd::pick<T>(zl, zh, j);
-        const T y0 = mxf::trunc_y<T>(cc, mxd::pick<T>(tl, th, j), mxd::pick<T>(ml, mh, j), m, true);
-        w[base + i] = y0 - z0;
-        out0[base + i] = z0;
+      for (int part = 0; part < 4; ++part) {
+        const int64_t b = (int64_t)mx::ks_chunk(B, part);
+        if (b >= nb) break;
+        uint64_t tl, th, ml, mh, zl, zh;
+        mx::part_u64(wt, part, &tl, &th);
+        mx::part_u64(wm, part, &ml, &mh);
+        mx::part_u64(wz, part, &zl, &zh);
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+          const int64_t i = b * P + j;
+          if (i >= n) break;
+          const T cc = msg[base + i] + rmk[base + i];
+          const T z0 = mxd::pick<T>(zl, zh, j);
+          const T y0 = mxf::trunc_y<T>(cc, mxd::pick<T>(tl, th, j), mxd::pick<T>(ml, mh, j), m, true);
+          w[base + i] = y0 - z0;
+          out0[base + i] = z0;
+        }
       }
     } else if (role == 1) {
       const uint32_t* k2 = rks[2 * c + 1];
-      uint64_t zl, zh;
-      mxd::aes_ctr_rep(k2, Tt, n_z2, b, &zl, &zh);
+      uint32_t wz[16];
+      mx::chacha_block(k2, n_z2, B, wz);
 #pragma unroll
-      for (int j = 0; j < P; ++j) {
-        const int64_t i = b * P + j;
-        if (i >= n) break;
-        const T cc = msg[base + i] + rmk[base + i];
-        const T z2 = mxd::pick<T>(zl, zh, j);
-        const T y1 = mxf::trunc_y<T>(cc, rrt[base + i], (T)rrm[base + i], m, false);
-        w[base + i] = y1 - z2;
-        out1[base + i] = z2;
+      for (int part = 0; part < 4; ++part) {
+        const int64_t b = (int64_t)mx::ks_chunk(B, part);
+        if (b >= nb) break;
+        uint64_t zl, zh;
+        mx::part_u64(wz, part, &zl, &zh);
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+          const int64_t i = b * P + j;
+          if (i >= n) break;
+          const T cc = msg[base + i] + rmk[base + i];
+          const T z2 = mxd::pick<T>(zl, zh, j);
+          const T y1 = mxf::trunc_y<T>(cc, rrt[base + i], (T)rrm[base + i], m, false);
+          w[base + i] = y1 - z2;
+          out1[base + i] = z2;
+        }
       }
     }
   }
@@ -151,43 +192,43 @@ template <class T>
 __global__ void __launch_bounds__(256)
     k_share_party(int kind, int64_t n, Roles rel, const T* __restrict__ x, T* __restrict__ out0,
                   T* __restrict__ out1, mxd::KeySrc keys, uint64_t n1, uint64_t na, int ncomp) {
-  __shared__ uint32_t Tt[mxd::kTTWords];
-  __shared__ uint32_t rks[mxd::kMaxKeySlots][44];
+  __shared__ uint32_t rks[mxd::kMaxKeySlots][mxd::kKeyWords];
   // keys: 2 per component: rel 0 -> (next, all), rel 1 -> (own, all), rel 2 -> (all, all)
   mxd::stage_keys(rks, keys, 2 * ncomp);
-  mxd::stage_tables_rep(Tt);
   constexpr int P = mxd::Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;
-  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < nb * ncomp;
-       g += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)(g / nb);
-    const int64_t b = g - c * nb;
+  MX_PARTY_WALK(nb, ncomp) {
+    const int c = (int)(g / nblk);
+    const uint64_t B = (uint64_t)(g - c * nblk);
     const int r = rel.r[c];
     const int64_t base = (int64_t)c * n;
-    uint64_t al, ah, bl, bh;
-    if (r == 2) {
-      mxd::aes_ctr_rep(rks[2 * c + 1], Tt, na, b, &bl, &bh);
-    } else if (r == 0 || r == 1) {
-      mxd::aes_ctr_rep(rks[2 * c], Tt, n1, b, &al, &ah);
-      mxd::aes_ctr_rep(rks[2 * c + 1], Tt, na, b, &bl, &bh);
-    } else {
-      continue;
-    }
+    if (r < 0 || r > 2) continue;
+    uint32_t wa[16], wb[16];
+    if (r != 2) mx::chacha_block(rks[2 * c], n1, B, wa);
+    mx::chacha_block(rks[2 * c + 1], na, B, wb);
 #pragma unroll
-    for (int j = 0; j < P; ++j) {
-      const int64_t i = b * P + j;
-      if (i >= n) break;
-      const T ra = mxd::pick<T>(bl, bh, j);
-      if (r == 2) {
-        out0[base + i] = ra;  // s1 arrives from the owner
-      } else {
-        const T r1 = mxd::pick<T>(al, ah, j);
-        if (r == 0) {
-          out0[base + i] = kind == MX_CROSS_BOOL ? (T)(x[i] ^ r1 ^ ra) : (T)(x[i] - r1 - ra);
-          out1[base + i] = r1;
+    for (int part = 0; part < 4; ++part) {
+      const int64_t b = (int64_t)mx::ks_chunk(B, part);
+      if (b >= nb) break;
+      uint64_t al = 0, ah = 0, bl, bh;
+      if (r != 2) mx::part_u64(wa, part, &al, &ah);
+      mx::part_u64(wb, part, &bl, &bh);
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const int64_t i = b * P + j;
+        if (i >= n) break;
+        const T ra = mxd::pick<T>(bl, bh, j);
+        if (r == 2) {
+          out0[base + i] = ra;  // s1 arrives from the owner
         } else {
-          out0[base + i] = r1;
-          out1[base + i] = ra;
+          const T r1 = mxd::pick<T>(al, ah, j);
+          if (r == 0) {
+            out0[base + i] = kind == MX_CROSS_BOOL ? (T)(x[i] ^ r1 ^ ra) : (T)(x[i] - r1 - ra);
+            out1[base + i] = r1;
+          } else {
+            out0[base + i] = r1;
+            out1[base + i] = ra;
+          }
         }
       }
     }
@@ -214,12 +255,12 @@ int mxh_trunc_party_r0(int words, int64_t n, int m, int ncomp, const int* roles,
   const Roles rr = roles_of(roles, ncomp);
   hipStream_t st = (hipStream_t)stream;
   if (words == 1) {
-    hipLaunchKernelGGL(k_trunc_party_r0<u64>, dim3(mxd::grid_for((n + 1) / 2 * ncomp)),
+    hipLaunchKernelGGL(k_trunc_party_r0<u64>, dim3(mxd::grid_for_chunks((n + 1) / 2) * ncomp),
                        dim3(256), 0, st, n, m, rr, (const u64*)s0, (const u64*)s1, (u64*)msg,
                        (u64*)msg_rm, (u64*)out0, (u64*)out1, k, nn[0], nn[1], nn[2], nn[3],
                        nn[4], nn[5], ncomp);
   } else if (words == 2) {
-    hipLaunchKernelGGL(k_trunc_party_r0<u128>, dim3(mxd::grid_for(n * ncomp)), dim3(256), 0, st,
+    hipLaunchKernelGGL(k_trunc_party_r0<u128>, dim3(mxd::grid_for_chunks(n) * ncomp), dim3(256), 0, st,
                        n, m, rr, (const u128*)s0, (const u128*)s1, (u128*)msg, (u64*)msg_rm,
                        (u128*)out0, (u128*)out1, k, nn[0], nn[1], nn[2], nn[3], nn[4], nn[5],
                        ncomp);
@@ -240,12 +281,12 @@ int mxh_trunc_party_r1(int words, int64_t n, int m, int ncomp, const int* roles,
   const Roles rr = roles_of(roles, ncomp);
   hipStream_t st = (hipStream_t)stream;
   if (words == 1) {
-    hipLaunchKernelGGL(k_trunc_party_r1<u64>, dim3(mxd::grid_for((n + 1) / 2 * ncomp)),
+    hipLaunchKernelGGL(k_trunc_party_r1<u64>, dim3(mxd::grid_for_chunks((n + 1) / 2) * ncomp),
                        dim3(256), 0, st, n, m, rr, (const u64*)msg, (const u64*)rmk,
                        (const u64*)rrt, (const u64*)rrm, (u64*)w, (u64*)out0, (u64*)out1, k,
                        nn[2], nn[3], nn[4], nn[5], ncomp);
   } else if (words == 2) {
-    hipLaunchKernelGGL(k_trunc_party_r1<u128>, dim3(mxd::grid_for(n * ncomp)), dim3(256), 0, st,
+    hipLaunchKernelGGL(k_trunc_party_r1<u128>, dim3(mxd::grid_for_chunks(n) * ncomp), dim3(256), 0, st,
                        n, m, rr, (const u128*)msg, (const u128*)rmk, (const u128*)rrt,
                        (const u64*)rrm, (u128*)w, (u128*)out0, (u128*)out1, k, nn[2], nn[3],
                        nn[4], nn[5], ncomp);
@@ -266,17 +307,17 @@ int mxh_share_party(int kind, int words, int64_t n, int ncomp, const int* rel, c
   hipStream_t st = (hipStream_t)stream;
   switch (words) {
     case 0:
-      hipLaunchKernelGGL(k_share_party<uint8_t>, dim3(mxd::grid_for((n + 15) / 16 * ncomp)),
+      hipLaunchKernelGGL(k_share_party<uint8_t>, dim3(mxd::grid_for_chunks((n + 15) / 16) * ncomp),
                          dim3(256), 0, st, kind, n, rr, (const uint8_t*)x, (uint8_t*)out0,
                          (uint8_t*)out1, k, n1, na, ncomp);
       break;
     case 1:
-      hipLaunchKernelGGL(k_share_party<u64>, dim3(mxd::grid_for((n + 1) / 2 * ncomp)), dim3(256),
+      hipLaunchKernelGGL(k_share_party<u64>, dim3(mxd::grid_for_chunks((n + 1) / 2) * ncomp), dim3(256),
                          0, st, kind, n, rr, (const u64*)x, (u64*)out0, (u64*)out1, k, n1, na,
                          ncomp);
       break;
     case 2:
-      hipLaunchKernelGGL(k_share_party<u128>, dim3(mxd::grid_for(n * ncomp)), dim3(256), 0, st,
+      hipLaunchKernelGGL(k_share_party<u128>, dim3(mxd::grid_for_chunks(n) * ncomp), dim3(256), 0, st,
                          kind, n, rr, (const u128*)x, (u128*)out0, (u128*)out1, k, n1, na, ncomp);
       break;
     default:

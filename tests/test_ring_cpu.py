@@ -20,15 +20,66 @@ def test_aes_fips197_vector():
     assert R.aes_encrypt(key, pt).hex() == "69c4e0d86a7b0430d8cdb78070b4c55a"
 
 
-def test_prg_is_counter_mode():
+def _chacha_block(key_words, consts, ctr_words, nonce_words, rounds):
+    m = 0xFFFFFFFF
+    st = list(consts) + list(key_words) + list(ctr_words) + list(nonce_words)
+    x = list(st)
+
+    def qr(a, b, c, d):
+        for (p, q, r, k) in ((a, b, d, 16), (c, d, b, 12), (a, b, d, 8), (c, d, b, 7)):
+            x[p] = (x[p] + x[q]) & m
+            x[r] ^= x[p]
+            x[r] = ((x[r] << k) | (x[r] >> (32 - k))) & m
+
+    for _ in range(rounds // 2):
+        qr(0, 4, 8, 12), qr(1, 5, 9, 13), qr(2, 6, 10, 14), qr(3, 7, 11, 15)
+        qr(0, 5, 10, 15), qr(1, 6, 11, 12), qr(2, 7, 8, 13), qr(3, 4, 9, 14)
+    return b"".join(((x[i] + st[i]) & m).to_bytes(4, "little") for i in range(16))
+
+
+def test_chacha_core_rfc7539_vector():
+    """The quarter-round / double-round structure against RFC 7539 section 2.3.2."""
+    words = lambda b: [int.from_bytes(b[i:i + 4], "little") for i in range(0, len(b), 4)]  # noqa
+    sigma = words(b"expand 32-byte k")
+    out = _chacha_block(words(bytes(range(32))), sigma, [1],
+                        words(bytes.fromhex("000000090000004a00000000")), 20)
+    assert out[:16].hex() == "10f1e7e4d13b5915500fdd1fa32071c4"
+
+
+def _prf_stream(key, nonce, nchunks):
+    """moosex PRF (csrc/prf_core.h): ChaCha12, 128-bit key, 64-bit block counter and nonce;
+    chunk c = 16-byte part (c >> 6) & 3 of block ((c >> 8) << 6) | (c & 63)."""
+    words = lambda b: [int.from_bytes(b[i:i + 4], "little") for i in range(0, len(b), 4)]  # noqa
+    tau = words(b"expand 16-byte k")
+    kw = words(key) * 2
+    out = []
+    for c in range(nchunks):
+        blk, part = ((c >> 8) << 6) | (c & 63), (c >> 6) & 3
+        b = _chacha_block(kw, tau, [blk & 0xFFFFFFFF, blk >> 32],
+                          [nonce & 0xFFFFFFFF, nonce >> 32], 12)
+        out.append(b[16 * part:16 * part + 16])
+    return b"".join(out)
+
+
+def test_prg_is_the_chacha12_stream():
     key = bytes(range(16))
-    ks = R.prg_bytes(key, 5, 64).numpy().tobytes()
-    for c in range(4):
-        block = (5).to_bytes(8, "little") + c.to_bytes(8, "little")
-        assert ks[16 * c:16 * c + 16] == R.aes_encrypt(key, block)
+    ks = R.prg_bytes(key, 5, 300 * 16).numpy().tobytes()
+    assert ks == _prf_stream(key, 5, 300)
     # offsets are consistent
     tail = R.prg_bytes(key, 5, 32, ctr0=2).numpy().tobytes()
-    assert tail == ks[32:]
+    assert tail == ks[32:64]
+
+
+def test_prf_expand_elements_follow_the_stream():
+    key = bytes(range(3, 19))
+    ref = _prf_stream(key, 77, 600)
+    for bits, per in ((128, 1), (64, 2)):
+        got = R.to_ints(R.prf_expand([key], 77, (700,), bits, "cpu"))[0]
+        for i in (0, 1, 63, 64, 65, 255, 256, 299, 599 // per):
+            c, j = divmod(i, per)
+            chunk = ref[16 * c:16 * c + 16]
+            want = int.from_bytes(chunk[8 * j:8 * j + bits // 8] if per == 2 else chunk, "little")
+            assert int(got[i]) == want
 
 
 @settings(max_examples=40, deadline=None)
