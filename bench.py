@@ -4,7 +4,8 @@
 Metric (BASELINE.json): "replicated fixed(14,23) matmul elems/sec" -- one step is the
 reference's dot benchmark (``benchmarks/pymoose/dot_product.py``) at the BASELINE config
 3 size: x (alice) and y (bob) are cast to fixed(14,23), secret-shared onto a 3-party
-replicated placement, multiplied (RSS dot = int8-MFMA limb GEMM + zero share + reshare),
+replicated placement, multiplied (RSS dot = exact multi-modular int8-MFMA GEMM + zero share
++ reshare),
 truncated (TruncPr) and revealed to carole, who decodes to float64.  As in pymoose every
 fixed dtype runs over Z_2^128 (``--ring 64`` selects the Z_2^64 path).  Value = output
 elements per second over the whole job (all GPUs).
@@ -299,7 +300,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": value / REFERENCE_ELEMS_PER_SEC,
-            "dtype": f"fixed(14,23) over Z_2^{args.ring} (int8-MFMA limb GEMM)",
+            "dtype": f"fixed(14,23) over Z_2^{args.ring} (exact multi-modular int8-MFMA GEMM)",
             "data": "synthetic uniform[-4,4) inputs, device resident",
             "config": {
                 "model": f"replicated fixed(14,23) RingDot {n}x{n} (share+dot+trunc_pr+reveal)",

@@ -57,16 +57,17 @@ constexpr int kModuli[kMaxMod] = {256, 255, 253, 251, 247, 241, 239, 233, 229, 2
                                   149, 139, 137, 131, 127, 113, 109, 107, 103, 101, 97,  89,
                                   83,  79,  73,  71,  67,  61,  59,  53,  47,  43,  41,  37};
 
-constexpr int BM = 256;          // block tile rows (A side) = cols (B side)
+constexpr int BM = 256;          // block tile rows (A side); the cols BN are 256 or 128
 constexpr int BK = 64;           // k bytes per stage
-constexpr int kImg = BM * BK;    // one operand image per (tile, k-step): 16 KB
+constexpr int kImg = BM * BK;    // one A operand image per (tile, k-step): 16 KB
 constexpr int kStages = 3;       // LDS ring depth
-constexpr int kStageBytes = 2 * kImg;
-constexpr int kCrTile = BM * BM;  // residue bytes of one output tile (64 KB)
 
-// byte offset of 16-byte chunk c (0..3) of image row r: chunks XOR-swizzled by (r >> 2) & 3
-// so that the 16 lanes of each ds_read_b128 lane group hit 16 distinct 16-byte bank slots
-__device__ __host__ inline int img_off(int r, int c) { return r * BK + 16 * (c ^ ((r >> 2) & 3)); }
+// byte offset of 16-byte chunk c (0..3) of image row r: chunks XOR-swizzled by
+// f((r >> 2) & 3), f = [0, 2, 3, 1], so that the 16 lanes of each ds_read_b128 lane group hit
+// 16 distinct 16-byte bank slots both for the 32x32x32 fragments (lane l: row l & 31, one
+// chunk per half-wave) and for the 16x16x64 fragments (lane l: row l & 15, chunk l >> 4).
+__device__ __host__ inline int swz(int q) { return (0x78 >> (2 * (q & 3))) & 3; }
+__device__ __host__ inline int img_off(int r, int c) { return r * BK + 16 * (c ^ swz(r >> 2)); }
 
 // --- tables ---------------------------------------------------------------------------------
 struct PrepTab {  // operand residues
@@ -213,26 +214,26 @@ __device__ __forceinline__ int residue(const uint32_t (&x)[NW], const uint32_t (
 // One thread = (tile, k-step, image row r, 16-byte chunk c) of every residue plane.
 // TRANS = false: A' rows are M rows of [A0 | A1] (row-major [R][K] per batch, batch stride
 // xs elements).  TRANS = true: B' rows are the N columns of [B0 + B1 ; B0] ([K][R]).
-template <class T, bool TRANS>
+template <class T, bool TRANS, int ROWS>
 __global__ void __launch_bounds__(256)
     k_crt_prep(const T* __restrict__ X0, const T* __restrict__ X1, int64_t R, int64_t K,
                int64_t xs, int mode, int8_t* __restrict__ out, int64_t tiles, int64_t nkb,
                const PrepTab tab) {
   constexpr int NW = Words<T>::N;
-  const int64_t total = tiles * nkb * (BM * 4);
+  const int64_t total = tiles * nkb * (ROWS * 4);
   const int64_t b = blockIdx.y;
   const T* x0 = X0 + b * xs;
   const T* x1 = mode ? X1 + b * xs : x0;
   const int n = tab.n;
-  const int64_t plane = tiles * nkb * (int64_t)kImg;
+  const int64_t plane = tiles * nkb * (int64_t)(ROWS * BK);
   int8_t* ob = out + b * n * plane;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total;
        g += (int64_t)gridDim.x * blockDim.x) {
     const int c = (int)(g & 3);
-    const int r = (int)((g >> 2) & (BM - 1));
-    const int64_t q = g >> 10;
+    const int r = (int)((g >> 2) & (ROWS - 1));
+    const int64_t q = g / (ROWS * 4);
     const int64_t kb = q % nkb, t = q / nkb;
-    const int64_t row = t * BM + r;
+    const int64_t row = t * ROWS + r;
     const int64_t k0 = kb * BK + c * 16;
     uint32_t v[16][NW];
 #pragma unroll
@@ -251,7 +252,7 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
       for (int w = 0; w < NW; ++w) v[j][w] = (uint32_t)(e >> (32 * w));
     }
-    int8_t* base = ob + (t * nkb + kb) * (int64_t)kImg + img_off(r, c);
+    int8_t* base = ob + (t * nkb + kb) * (int64_t)(ROWS * BK) + img_off(r, c);
     {  // p = 256: the low byte (times the folded inverse)
       int rr[16];
 #pragma unroll
@@ -299,14 +300,18 @@ __device__ __forceinline__ int centered_mod(int acc, float pf, float rcp, int t1
 // blocks of 32x32.  <2,2>: 4 waves of 128x128 (256 accumulator registers, one wave per
 // SIMD); <2,4>: 8 waves of 128x64 (128 accumulators, two waves per SIMD, so one wave's
 // LDS reads, address arithmetic and barrier waits hide behind its partner's MFMAs).
-template <int WR, int WC>
-__global__ void __launch_bounds__(64 * WR * WC, WR * WC / 4)
+template <int WR, int WC, int BN, int MINW>
+__global__ void __launch_bounds__(64 * WR * WC, MINW)
     k_crt_gemm(const int8_t* __restrict__ RA, const int8_t* __restrict__ RB,
                int8_t* __restrict__ CR, int tiles_m, int tiles_n, int nkb, int gM,
                const EpiTab ep, int dma_mask) {
   constexpr int NW = WR * WC;
-  constexpr int MI = BM / WR / 32, NJ = BM / WC / 32;
-  constexpr int PPW = 32 / NW;  // DMA pieces per wave per stage
+  constexpr int MI = BM / WR / 32, NJ = BN / WC / 32;
+  constexpr int kImgB = BN * BK;                 // one B image per (tile, k-step)
+  constexpr int kStageBytes = kImg + kImgB;
+  constexpr int NPIECE = kStageBytes / 1024;     // 1 KB LDS-DMA pieces per stage
+  constexpr int PPW = NPIECE / NW;               // DMA pieces per wave per stage
+  static_assert(PPW * NW == NPIECE, "stage pieces must split evenly over the waves");
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
   const int ntiles = tiles_m * tiles_n;
   const int tid_flat = (int)xcd_remap(blockIdx.x, ntiles);
@@ -319,31 +324,33 @@ __global__ void __launch_bounds__(64 * WR * WC, WR * WC / 4)
   const int mi = g % ep.n;
 
   const int8_t* ga = RA + ((int64_t)g * tiles_m + tm) * nkb * (int64_t)kImg;
-  const int8_t* gb = RB + ((int64_t)g * tiles_n + tn) * nkb * (int64_t)kImg;
+  const int8_t* gb = RB + ((int64_t)g * tiles_n + tn) * nkb * (int64_t)kImgB;
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave / WC, wc = wave % WC;
   const int half = lane >> 5;
-  const int sw = (lane >> 2) & 3;  // row swizzle of every fragment row this lane reads
+  const int sw = swz(lane >> 2);  // row swizzle of every fragment row this lane reads
   const int rowa = (wr * (BM / WR) + (lane & 31)) * BK;
-  const int rowb = kImg + (wc * (BM / WC) + (lane & 31)) * BK;
+  const int rowb = kImg + (wc * (BN / WC) + (lane & 31)) * BK;
   const int co0 = 16 * (half ^ sw), co1 = 16 * ((2 + half) ^ sw);
 
-  // wave w issues pieces w, w + NW, .. of the 32 1-KB pieces of a stage (16 A, then 16 B);
-  // the source advances by one 16 KB image per k-step
+  // wave w issues pieces w, w + NW, .. of the NPIECE 1-KB pieces of a stage (16 A, then
+  // BN / 16 B); the sources advance by one image per k-step
   const int8_t* srcs[PPW];
-  int dsts[PPW];
+  int dsts[PPW], steps[PPW];
 #pragma unroll
   for (int t = 0; t < PPW; ++t) {
     const int pc = wave + NW * t;
     const bool is_b = pc >= 16;
-    srcs[t] = (is_b ? gb : ga) + (pc & 15) * 1024 + lane * 16;
-    dsts[t] = (is_b ? kImg : 0) + (pc & 15) * 1024;
+    const int pp = is_b ? pc - 16 : pc;
+    srcs[t] = (is_b ? gb : ga) + pp * 1024 + lane * 16;
+    dsts[t] = (is_b ? kImg : 0) + pp * 1024;
+    steps[t] = is_b ? kImgB : kImg;
   }
   auto dma = [&](int kb, int t, int8_t* dst_stage) {
-    if (!((dma_mask >> ((wave + NW * t) >> 4)) & 1)) return;  // timing experiments only
-    __builtin_amdgcn_global_load_lds((const void*)(srcs[t] + (int64_t)kb * kImg),
+    if (!((dma_mask >> (wave + NW * t >= 16 ? 1 : 0)) & 1)) return;  // timing experiments only
+    __builtin_amdgcn_global_load_lds((const void*)(srcs[t] + (int64_t)kb * steps[t]),
                                      (__attribute__((address_space(3))) void*)(dst_stage + dsts[t]),
                                      16, 0, 0);
   };
@@ -371,6 +378,7 @@ __global__ void __launch_bounds__(64 * WR * WC, WR * WC / 4)
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   frags(smem, co0, fa0, fb0);
+  if (dma_mask & 8) frags(smem, co1, fa1, fb1);
 
   int8_t* cur = smem;                    // stage kb
   int8_t* nxt = smem + kStageBytes;      // stage kb + 1
@@ -382,9 +390,9 @@ __global__ void __launch_bounds__(64 * WR * WC, WR * WC / 4)
       for (int j = 0; j < NJ; ++j) {
         acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0[i], fb0[j], acc[i][j], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
-        if (i == 0 && j == 1) {  // second-half fragments, behind the first MFMAs (the
-          frags(cur, co1, fa1, fb1);  // compiler waits for all LDS reads before an MFMA
-          __builtin_amdgcn_sched_barrier(0);  // that follows any of them)
+        if (i == 0 && j == 1 && !(dma_mask & 8)) {  // second-half fragments, behind the
+          frags(cur, co1, fa1, fb1);  // first MFMAs (the compiler waits for all LDS reads
+          __builtin_amdgcn_sched_barrier(0);  // before an MFMA that follows any of them)
         }
       }
     // my DMA of stage kb+1 landed (only stage kb+2's pieces may be outstanding) and my
@@ -392,7 +400,7 @@ __global__ void __launch_bounds__(64 * WR * WC, WR * WC / 4)
     __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(PPW));
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    frags(nxt, co0, fa0, fb0);  // past the end: stale bytes, never used
+    if (!(dma_mask & 8)) frags(nxt, co0, fa0, fb0);  // past the end: stale, never used
     __builtin_amdgcn_sched_barrier(0);
     const int kn = kb + kStages < nkb ? kb + kStages : nkb - 1;
 #pragma unroll
@@ -401,12 +409,15 @@ __global__ void __launch_bounds__(64 * WR * WC, WR * WC / 4)
       for (int j = 0; j < NJ; ++j) {
         acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1[i], fb1[j], acc[i][j], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
-        constexpr int EVERY = MI * NJ / PPW;
+        // this wave's PPW pieces of stage kb+3 into the freed buffer, spread over the
+        // MI * NJ MFMAs: piece t after MFMA floor((t + 1) MI NJ / PPW) - 1
         const int m = i * NJ + j;
-        if (m % EVERY == EVERY - 1) {  // this wave's pieces of stage kb+3 into the freed buffer
-          dma(kn, m / EVERY, cur);
-          __builtin_amdgcn_sched_barrier(0);
-        }
+#pragma unroll
+        for (int t = 0; t < PPW; ++t)
+          if (m == (t + 1) * MI * NJ / PPW - 1) {
+            dma(kn, t, cur);
+            __builtin_amdgcn_sched_barrier(0);
+          }
       }
     int8_t* t = cur;
     cur = nxt;
@@ -416,10 +427,10 @@ __global__ void __launch_bounds__(64 * WR * WC, WR * WC / 4)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   // epilogue: centered acc mod p, one byte per element, MFMA register order; 32x32 block
-  // (bi, bj) of the tile at byte ((bi * 8 + bj) * 64 + lane) * 16 of the tile's 64 KB
+  // (bi, bj) of the tile at byte ((bi * BN / 32 + bj) * 64 + lane) * 16 of the tile's bytes
   const float pf = ep.pf[mi], rcp = ep.rcp[mi];
   const int t16 = ep.t16[mi];
-  int8_t* cr = CR + ((int64_t)g * ntiles + tm * tiles_n + tn) * (int64_t)kCrTile;
+  int8_t* cr = CR + ((int64_t)g * ntiles + tm * tiles_n + tn) * (int64_t)(BM * BN);
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -428,22 +439,24 @@ __global__ void __launch_bounds__(64 * WR * WC, WR * WC / 4)
       // [-128, 128] whose low byte is the residue)
       int rr[16];
 #pragma unroll
-      for (int e = 0; e < 16; ++e) rr[e] = centered_mod(acc[i][j][e], pf, rcp, t16);
+      for (int e = 0; e < 16; ++e)
+        rr[e] = (dma_mask & 4) ? acc[i][j][e] : centered_mod(acc[i][j][e], pf, rcp, t16);
       v4i o;
 #pragma unroll
       for (int u = 0; u < 4; ++u) o[u] = (int)pack4(rr[4 * u], rr[4 * u + 1], rr[4 * u + 2], rr[4 * u + 3]);
       const int bi = wr * MI + i, bj = wc * NJ + j;
-      *(v4i*)(cr + ((bi * 8 + bj) * 64 + lane) * 16) = o;
+      *(v4i*)(cr + ((bi * (BN / 32) + bj) * 64 + lane) * 16) = o;
     }
 }
 
 // One thread = 8 residue bytes (8 output elements of one MFMA block) of every modulus.
-template <class T>
+template <class T, int BN>
 __global__ void __launch_bounds__(256)
     k_crt_recon(const int8_t* __restrict__ CR, T* __restrict__ C, int64_t M, int64_t N,
                 int64_t tiles_m, int64_t tiles_n, int accumulate, const RecTab rc) {
   constexpr int NK = sizeof(T) / 2;  // 16-bit words of a ring element
   const int64_t ntiles = tiles_m * tiles_n;
+  constexpr int kCrTile = BM * BN, NBJ = BN / 32, LOGB = BN == 256 ? 6 : 5;
   const int64_t total = ntiles * (kCrTile / 8);
   const int64_t b = blockIdx.y;
   const int n = rc.n;
@@ -452,8 +465,8 @@ __global__ void __launch_bounds__(256)
     const int hf = (int)(gt & 1);
     const int lane = (int)((gt >> 1) & 63);
     const int64_t rest = gt >> 7;
-    const int blk = (int)(rest & 63);  // 32x32 block (bi, bj) = (blk >> 3, blk & 7)
-    const int64_t tile = rest >> 6;
+    const int blk = (int)(rest & ((1 << LOGB) - 1));  // 32x32 block (blk / NBJ, blk % NBJ)
+    const int64_t tile = rest >> LOGB;
     const int64_t off = tile * kCrTile + (blk * 64 + lane) * 16 + hf * 8;
     int acc[8][NK];
     float qs[8];
@@ -479,8 +492,8 @@ __global__ void __launch_bounds__(256)
       }
     }
     const int64_t tm = tile / tiles_n, tn = tile % tiles_n;
-    const int bi = blk >> 3, bj = blk & 7;
-    const int64_t gcol = tn * BM + bj * 32 + (lane & 31);
+    const int bi = blk / NBJ, bj = blk % NBJ;
+    const int64_t gcol = tn * BN + bj * 32 + (lane & 31);
     T mw = 0;
 #pragma unroll
     for (int k = 0; k < NK; ++k) mw |= (T)rc.Mw[k] << (16 * k);
@@ -502,23 +515,237 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// 16x16x64 variant: one v_mfma_i32_16x16x64_i8 covers a whole 64-byte k-step, lane l reads
+// row l & 15, chunk l >> 4 of the image.  WR x WC waves, wave tile (BM/WR) x (BN/WC) =
+// MI x NJ MFMA blocks of 16x16 (4 accumulator registers each).  Fragments of stage kb+1 are
+// read right after the step's barrier into the second register set (the k-loop is unrolled
+// by two so the sets swap without moves), while the second half of stage kb's MFMAs runs.
+// Output bytes: 16x16 block (bi, bj) at ((bi * BN / 16 + bj) * 64 + lane) * 4 of the tile.
+template <int WR, int WC, int BN, int MINW>
+__global__ void __launch_bounds__(64 * WR * WC, MINW)
+    k_crt_gemm16(const int8_t* __restrict__ RA, const int8_t* __restrict__ RB,
+                 int8_t* __restrict__ CR, int tiles_m, int tiles_n, int nkb, int gM,
+                 const EpiTab ep, int dma_mask) {
+  constexpr int NW = WR * WC;
+  constexpr int MI = BM / WR / 16, NJ = BN / WC / 16;
+  constexpr int NM = MI * NJ;                    // MFMAs per wave per k-step
+  constexpr int kImgB = BN * BK;
+  constexpr int kStageBytes = kImg + kImgB;
+  constexpr int NPIECE = kStageBytes / 1024;
+  constexpr int PPW = NPIECE / NW;
+  static_assert(PPW * NW == NPIECE, "stage pieces must split evenly over the waves");
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+  const int ntiles = tiles_m * tiles_n;
+  const int tid_flat = (int)xcd_remap(blockIdx.x, ntiles);
+  const int group = tid_flat / (gM * tiles_n);
+  const int first_m = group * gM;
+  const int gm = tiles_m - first_m < gM ? tiles_m - first_m : gM;
+  const int in_group = tid_flat % (gM * tiles_n);
+  const int tm = first_m + in_group % gm, tn = in_group / gm;
+  const int g = blockIdx.y;
+  const int mi = g % ep.n;
+  const int8_t* ga = RA + ((int64_t)g * tiles_m + tm) * nkb * (int64_t)kImg;
+  const int8_t* gb = RB + ((int64_t)g * tiles_n + tn) * nkb * (int64_t)kImgB;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave / WC, wc = wave % WC;
+  const int co = 16 * ((lane >> 4) ^ swz((lane & 15) >> 2));
+  const int rowa = (wr * (BM / WR) + (lane & 15)) * BK + co;
+  const int rowb = kImg + (wc * (BN / WC) + (lane & 15)) * BK + co;
+
+  const int8_t* srcs[PPW];
+  int dsts[PPW], steps[PPW];
+#pragma unroll
+  for (int t = 0; t < PPW; ++t) {
+    const int pc = wave + NW * t;
+    const bool is_b = pc >= 16;
+    const int pp = is_b ? pc - 16 : pc;
+    srcs[t] = (is_b ? gb : ga) + pp * 1024 + lane * 16;
+    dsts[t] = (is_b ? kImg : 0) + pp * 1024;
+    steps[t] = is_b ? kImgB : kImg;
+  }
+  (void)dma_mask;
+  auto dma = [&](int kb, int t, int8_t* dst_stage) {
+    __builtin_amdgcn_global_load_lds((const void*)(srcs[t] + (int64_t)kb * steps[t]),
+                                     (__attribute__((address_space(3))) void*)(dst_stage + dsts[t]),
+                                     16, 0, 0);
+  };
+
+  v4i acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = v4i{0, 0, 0, 0};
+
+  v4i fa0[MI], fb0[NJ], fa1[MI], fb1[NJ];
+  auto frags = [&](const int8_t* st, v4i(&fa)[MI], v4i(&fb)[NJ]) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i) fa[i] = *(const v4i*)(st + rowa + i * 16 * BK);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) fb[j] = *(const v4i*)(st + rowb + j * 16 * BK);
+  };
+
+#pragma unroll
+  for (int s = 0; s < kStages; ++s)
+#pragma unroll
+    for (int t = 0; t < PPW; ++t) dma(s < nkb ? s : nkb - 1, t, smem + s * kStageBytes);
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(2 * PPW));
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  frags(smem, fa0, fb0);
+
+  // one k-step: MFMAs of the stage in registers (fa, fb); after the first half, the barrier
+  // (stage kb+1 landed everywhere, stage kb no longer read) and the reads of stage kb+1 into
+  // (na, nb); the DMA of stage kb+3 into the freed buffer runs beside the second half
+  auto step = [&](int kb, int8_t* cur, int8_t* nxt, v4i(&fa)[MI], v4i(&fb)[NJ], v4i(&na)[MI],
+                  v4i(&nbf)[NJ]) __attribute__((always_inline)) {
+    const int kn = kb + kStages < nkb ? kb + kStages : nkb - 1;
+#pragma unroll MI
+    for (int i = 0; i < MI; ++i) {
+      if (i == MI / 2) {
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(PPW));
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        frags(nxt, na, nbf);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll NJ
+      for (int j = 0; j < NJ; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        const int h = (i - MI / 2) * NJ + j;  // MFMA index in the second half
+#pragma unroll PPW
+        for (int t = 0; t < PPW; ++t)
+          if (h == (t + 1) * (NM / 2) / PPW - 1) {
+            dma(kn, t, cur);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+      }
+    }
+  };
+
+  auto buf = [&](int i) { return smem + i * kStageBytes; };
+  int r = 0;  // stage kb lives in buf(r)
+  for (int kb = 0; kb < nkb; kb += 2) {
+    step(kb, buf(r), buf(r == 2 ? 0 : r + 1), fa0, fb0, fa1, fb1);
+    r = r == 2 ? 0 : r + 1;
+    if (kb + 1 < nkb) {
+      step(kb + 1, buf(r), buf(r == 2 ? 0 : r + 1), fa1, fb1, fa0, fb0);
+      r = r == 2 ? 0 : r + 1;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  const float pf = ep.pf[mi], rcp = ep.rcp[mi];
+  const int t16 = ep.t16[mi];
+  int8_t* cr = CR + ((int64_t)g * ntiles + tm * tiles_n + tn) * (int64_t)(BM * BN);
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      int rr[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        rr[e] = centered_mod(acc[i][j][e], pf, rcp, t16);
+      const int bi = wr * MI + i, bj = wc * NJ + j;
+      *(uint32_t*)(cr + ((bi * (BN / 16) + bj) * 64 + lane) * 4) = pack4(rr[0], rr[1], rr[2], rr[3]);
+    }
+}
+
+// reconstruction for the 16x16 output layout: one thread = one lane's 4 bytes of a block
+template <class T, int BN>
+__global__ void __launch_bounds__(256)
+    k_crt_recon16(const int8_t* __restrict__ CR, T* __restrict__ C, int64_t M, int64_t N,
+                  int64_t tiles_m, int64_t tiles_n, int accumulate, const RecTab rc) {
+  constexpr int NK = sizeof(T) / 2;
+  constexpr int kCrTile = BM * BN, NBJ = BN / 16;
+  const int64_t ntiles = tiles_m * tiles_n;
+  const int64_t total = ntiles * (kCrTile / 4);
+  const int64_t b = blockIdx.y;
+  const int n = rc.n;
+  for (int64_t gt = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; gt < total;
+       gt += (int64_t)gridDim.x * blockDim.x) {
+    const int lane = (int)(gt & 63);
+    const int64_t rest = gt >> 6;
+    const int blk = (int)(rest % (16 * NBJ));
+    const int64_t tile = rest / (16 * NBJ);
+    const int64_t off = tile * kCrTile + (blk * 64 + lane) * 4;
+    int acc[4][NK];
+    float qs[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      qs[e] = 0.f;
+#pragma unroll
+      for (int k = 0; k < NK; ++k) acc[e][k] = 0;
+    }
+    const int8_t* src = CR + b * n * ntiles * (int64_t)kCrTile + off;
+    for (int i = 0; i < n; ++i) {
+      const uint32_t v = *(const uint32_t*)(src + i * ntiles * (int64_t)kCrTile);
+      const float rcp = rc.rcp[i];
+      int wk[NK];
+#pragma unroll
+      for (int k = 0; k < NK; ++k) wk[k] = rc.W[i][k];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = (int)(int8_t)((v >> (8 * e)) & 0xff);
+        qs[e] = __builtin_fmaf((float)c, rcp, qs[e]);
+#pragma unroll
+        for (int k = 0; k < NK; ++k) acc[e][k] += __mul24(c, wk[k]);
+      }
+    }
+    const int64_t tm = tile / tiles_n, tn = tile % tiles_n;
+    const int bi = blk / NBJ, bj = blk % NBJ;
+    const int64_t gcol = tn * BN + bj * 16 + (lane & 15);
+    T mw = 0;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) mw |= (T)rc.Mw[k] << (16 * k);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t grow = tm * BM + bi * 16 + 4 * (lane >> 4) + e;
+      T z = 0;
+#pragma unroll
+      for (int k = 0; k < NK; ++k) z += (T)(int64_t)acc[e][k] << (16 * k);
+      const int q = (int)__builtin_rintf(qs[e]);
+      z -= (T)(int64_t)q * mw;
+      if (grow < M && gcol < N) {
+        T* pc = C + (b * M + grow) * N + gcol;
+        *pc = accumulate ? (T)(*pc + z) : z;
+      }
+    }
+  }
+}
+
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
+int crt_kernel() {  // MOOSEX_CRT_KERNEL: 1 = 4 waves of 128x128, 2 = 8 waves of 128x64
+  // (256x256 tiles, one block per CU), 3 = 4 waves of 128x64 in 256x128 tiles (two blocks
+  // per CU, so one block's barrier waits, LDS bursts and epilogue overlap the other's MFMAs)
+  // 4 = 16x16x64 MFMAs, 4 waves of 128x128 (256x256 tiles), 5 = 16x16x64, 4 waves of
+  // 128x64 in 256x128 tiles (two blocks per CU; the default: 12 % faster than 3 -- the chip
+  // holds a higher clock on the 16x16 shape), 6 = 16x16x64, 8 waves of 128x64 (256x256)
+  const char* e = std::getenv("MOOSEX_CRT_KERNEL");
+  const int v = e ? std::atoi(e) : 5;
+  return v >= 1 && v <= 6 ? v : 5;
+}
+bool crt_mfma16() { return crt_kernel() >= 4; }
+
 struct CPlan {
-  int n;
+  int n, bn;
   int64_t tiles_m, tiles_n, nkb, ra_bytes, rb_bytes, cr_bytes;
 };
 
 CPlan make_cplan(int words, int64_t batch, int64_t M, int64_t N, int64_t K, int mode) {
   CPlan p;
+  p.bn = (crt_kernel() == 3 || crt_kernel() == 5) ? 128 : 256;  // B tile columns
   const int64_t kprime = mode ? 2 * K : K;
   p.n = moduli_needed(words, kprime);
   p.tiles_m = (M + BM - 1) / BM;
-  p.tiles_n = (N + BM - 1) / BM;
+  p.tiles_n = (N + p.bn - 1) / p.bn;
   p.nkb = round_up(kprime, BK) / BK;
   p.ra_bytes = batch * p.n * p.tiles_m * p.nkb * (int64_t)kImg;
-  p.rb_bytes = batch * p.n * p.tiles_n * p.nkb * (int64_t)kImg;
-  p.cr_bytes = batch * p.n * p.tiles_m * p.tiles_n * (int64_t)kCrTile;
+  p.rb_bytes = batch * p.n * p.tiles_n * p.nkb * (int64_t)(p.bn * BK);
+  p.cr_bytes = batch * p.n * p.tiles_m * p.tiles_n * (int64_t)(BM * p.bn);
   return p;
 }
 
@@ -533,53 +760,80 @@ void launch_prep(const CPlan& p, const Tables& tb, bool is_b, int64_t batch, int
                  int64_t K, int64_t xs, const T* X0, const T* X1, int mode, int8_t* out,
                  hipStream_t st) {
   const int64_t tiles = is_b ? p.tiles_n : p.tiles_m;
-  const int64_t work = tiles * p.nkb * (BM * 4);
-  const int gx = (int)std::min<int64_t>((work + 255) / 256, 16384);
-  if (is_b)
-    hipLaunchKernelGGL((k_crt_prep<T, true>), dim3(gx, (unsigned)batch), dim3(256), 0, st, X0,
-                       X1, R, K, xs, mode, out, tiles, p.nkb, tb.pb);
+  const int rows = is_b ? p.bn : BM;
+  const int64_t work = tiles * p.nkb * (rows * 4);
+  const dim3 grid((unsigned)std::min<int64_t>((work + 255) / 256, 16384), (unsigned)batch);
+  if (!is_b)
+    hipLaunchKernelGGL((k_crt_prep<T, false, BM>), grid, dim3(256), 0, st, X0, X1, R, K, xs, mode,
+                       out, tiles, p.nkb, tb.pa);
+  else if (rows == 256)
+    hipLaunchKernelGGL((k_crt_prep<T, true, 256>), grid, dim3(256), 0, st, X0, X1, R, K, xs, mode,
+                       out, tiles, p.nkb, tb.pb);
   else
-    hipLaunchKernelGGL((k_crt_prep<T, false>), dim3(gx, (unsigned)batch), dim3(256), 0, st, X0,
-                       X1, R, K, xs, mode, out, tiles, p.nkb, tb.pa);
+    hipLaunchKernelGGL((k_crt_prep<T, true, 128>), grid, dim3(256), 0, st, X0, X1, R, K, xs, mode,
+                       out, tiles, p.nkb, tb.pb);
 }
 
-// MOOSEX_CRT_DMA_MASK (timing experiments, wrong results): bit 0 = stream A, bit 1 = B
+// MOOSEX_CRT_DMA_MASK (timing experiments, wrong results): bit 0 = stream A, bit 1 = B,
+// bit 2 = skip the epilogue reduction, bit 3 = no LDS fragment reads in the main loop
 int dma_mask() {
   const char* e = std::getenv("MOOSEX_CRT_DMA_MASK");
   return e ? std::atoi(e) : 3;
 }
 
-int crt_kernel() {  // MOOSEX_CRT_KERNEL: 1 = 4 waves of 128x128, 2 = 8 waves of 128x64
-  const char* e = std::getenv("MOOSEX_CRT_KERNEL");
-  return e && e[0] == '1' ? 1 : 2;
+template <int WR, int WC, int BN, int MINW, bool M16>
+void launch_variant(const CPlan& p, const Tables& tb, int64_t batch, const int8_t* ra,
+                    const int8_t* rb, int8_t* cr, hipStream_t st) {
+  constexpr int lds = kStages * (kImg + BN * BK);
+  const void* fn = M16 ? (const void*)k_crt_gemm16<WR, WC, BN, MINW>
+                       : (const void*)k_crt_gemm<WR, WC, BN, MINW>;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = true;
+  }
+  const dim3 grid((unsigned)(p.tiles_m * p.tiles_n), (unsigned)(batch * p.n));
+  if constexpr (M16)
+    hipLaunchKernelGGL((k_crt_gemm16<WR, WC, BN, MINW>), grid, dim3(64 * WR * WC), lds, st, ra,
+                       rb, cr, (int)p.tiles_m, (int)p.tiles_n, (int)p.nkb, gemm_group_m(), tb.ep,
+                       dma_mask());
+  else
+    hipLaunchKernelGGL((k_crt_gemm<WR, WC, BN, MINW>), grid, dim3(64 * WR * WC), lds, st, ra, rb,
+                       cr, (int)p.tiles_m, (int)p.tiles_n, (int)p.nkb, gemm_group_m(), tb.ep,
+                       dma_mask());
 }
 
 void launch_crt_gemm(const CPlan& p, const Tables& tb, int64_t batch, const int8_t* ra,
                      const int8_t* rb, int8_t* cr, hipStream_t st) {
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)k_crt_gemm<2, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        kStages * kStageBytes);
-    hipFuncSetAttribute((const void*)k_crt_gemm<2, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        kStages * kStageBytes);
-    attr = true;
+  switch (crt_kernel()) {
+    case 1: launch_variant<2, 2, 256, 1, false>(p, tb, batch, ra, rb, cr, st); break;
+    case 2: launch_variant<2, 4, 256, 2, false>(p, tb, batch, ra, rb, cr, st); break;
+    case 4: launch_variant<2, 2, 256, 1, true>(p, tb, batch, ra, rb, cr, st); break;
+    case 3: launch_variant<2, 2, 128, 2, false>(p, tb, batch, ra, rb, cr, st); break;
+    case 6: launch_variant<2, 4, 256, 2, true>(p, tb, batch, ra, rb, cr, st); break;
+    default: launch_variant<2, 2, 128, 2, true>(p, tb, batch, ra, rb, cr, st); break;
   }
-  const dim3 grid((unsigned)(p.tiles_m * p.tiles_n), (unsigned)(batch * p.n));
-  if (crt_kernel() == 1)
-    hipLaunchKernelGGL((k_crt_gemm<2, 2>), grid, dim3(256), kStages * kStageBytes, st, ra, rb, cr,
-                       (int)p.tiles_m, (int)p.tiles_n, (int)p.nkb, gemm_group_m(), tb.ep, dma_mask());
-  else
-    hipLaunchKernelGGL((k_crt_gemm<2, 4>), grid, dim3(512), kStages * kStageBytes, st, ra, rb, cr,
-                       (int)p.tiles_m, (int)p.tiles_n, (int)p.nkb, gemm_group_m(), tb.ep, dma_mask());
 }
 
 template <class T>
 void launch_recon(const CPlan& p, const Tables& tb, int64_t batch, int64_t M, int64_t N,
                   const int8_t* cr, T* C, int accumulate, hipStream_t st) {
-  const int64_t work = p.tiles_m * p.tiles_n * (kCrTile / 8);
+  const int64_t work = p.tiles_m * p.tiles_n * (BM * p.bn / 8);
   const int gx = (int)std::min<int64_t>((work + 255) / 256, 16384);
-  hipLaunchKernelGGL(k_crt_recon<T>, dim3(gx, (unsigned)batch), dim3(256), 0, st, cr, C, M, N,
-                     p.tiles_m, p.tiles_n, accumulate, tb.rc);
+  if (crt_mfma16()) {
+    const int gx16 = (int)std::min<int64_t>((2 * work + 255) / 256, 16384);
+    if (p.bn == 256)
+      hipLaunchKernelGGL((k_crt_recon16<T, 256>), dim3(gx16, (unsigned)batch), dim3(256), 0, st,
+                         cr, C, M, N, p.tiles_m, p.tiles_n, accumulate, tb.rc);
+    else
+      hipLaunchKernelGGL((k_crt_recon16<T, 128>), dim3(gx16, (unsigned)batch), dim3(256), 0, st,
+                         cr, C, M, N, p.tiles_m, p.tiles_n, accumulate, tb.rc);
+  } else if (p.bn == 256)
+    hipLaunchKernelGGL((k_crt_recon<T, 256>), dim3(gx, (unsigned)batch), dim3(256), 0, st, cr, C,
+                       M, N, p.tiles_m, p.tiles_n, accumulate, tb.rc);
+  else
+    hipLaunchKernelGGL((k_crt_recon<T, 128>), dim3(gx, (unsigned)batch), dim3(256), 0, st, cr, C,
+                       M, N, p.tiles_m, p.tiles_n, accumulate, tb.rc);
 }
 
 struct Ws {
