@@ -74,6 +74,8 @@ int mx_sum_axis(int dev, int words, const void* a, void* out, int64_t outer, int
 int mx_prg(int dev, const uint8_t* key16, uint64_t nonce, uint64_t ctr0, void* out,
            int64_t nbytes, void* stream);
 // AES-128 encryption of single 16-byte blocks (ECB) on the host; used for seed derivation
+// DeriveSeed: 16-byte seed = first 16 bytes of PRF block(key; sync key as counter||nonce)
+int mx_derive_seed(const uint8_t* key16, const uint8_t* sync16, uint8_t* out16);
 int mx_aes_encrypt_blocks(const uint8_t* key16, const uint8_t* in, uint8_t* out,
                           int64_t nblocks);
 // RSS local step for `nparties` stacked parties of n elements each:

@@ -517,6 +517,19 @@ int mx_prg(int dev, const uint8_t* key16, uint64_t nonce, uint64_t ctr0, void* o
   return 0;
 }
 
+// HostSeed derivation (DeriveSeed): the first 16 bytes of PRF block (key; counter =
+// sync[0..8), nonce = sync[8..16)) -- a PRF of the full 128-bit sync key.
+int mx_derive_seed(const uint8_t* key16, const uint8_t* sync16, uint8_t* out16) {
+  uint32_t k[4], w[16];
+  mx::key_words(key16, k);
+  uint64_t blk, nonce;
+  memcpy(&blk, sync16, 8);
+  memcpy(&nonce, sync16 + 8, 8);
+  mx::chacha_block(k, nonce, blk, w);
+  memcpy(out16, w, 16);
+  return 0;
+}
+
 int mx_aes_encrypt_blocks(const uint8_t* key16, const uint8_t* in, uint8_t* out,
                           int64_t nblocks) {
   if (have_aesni()) {  // AES-NI (the AES dialect and the AES tests); table code otherwise

@@ -38,6 +38,7 @@ _SIGS = {
     "mx_weighted_sum": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
     "mx_prg": (c_int, [c_int, c_vp, c_u64, c_u64, c_vp, c_i64, c_vp]),
     "mx_aes_encrypt_blocks": (c_int, [c_vp, c_vp, c_vp, c_i64]),
+    "mx_derive_seed": (c_int, [c_vp, c_vp, c_vp]),
     "mx_rss_cross": (
         c_int,
         [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_u64, c_vp],

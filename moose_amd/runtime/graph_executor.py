@@ -155,6 +155,8 @@ class GraphExecutor:
             if name not in arguments:
                 raise GraphExecutionError(f"missing argument {name}")
             a = arguments[name]
+            if isinstance(a, (str, bytes)) or op.sig.ret.name in ("HostString", "HostShape"):
+                return a if not isinstance(a, list) else tuple(a)  # non-tensor arguments
             t = a.to(self.device) if isinstance(a, torch.Tensor) else numpy_to_torch(np.asarray(a), self.device)
             bits = bits_of_ty(op.sig.ret)
             if bits is not None and not isinstance(a, R.RT):
