@@ -121,9 +121,11 @@ class Interpreter:
         for idx, op in enumerate(ops):
             if op.name in self.env:  # computed ahead as part of a batch
                 continue
-            if batch and op.kind == "Dot" and self._batch_dots(op, ops[idx + 1:]):
+            table = self._table_handler(op)
+            if (table is None and batch and op.kind == "Dot"
+                    and self._batch_dots(op, ops[idx + 1:])):
                 continue
-            handler = getattr(self, f"op_{op.kind}", None) or self._dialect_handler(op)
+            handler = table or getattr(self, f"op_{op.kind}", None) or self._dialect_handler(op)
             if handler is None:
                 raise MooseRuntimeError(f"operator {op.kind} is not supported by the interpreter")
             ins = [self.env[n] for n in op.inputs]
@@ -175,7 +177,7 @@ class Interpreter:
         for o in later:
             if len(group) >= limit:
                 break
-            if o.kind != "Dot" or o.name in self.env:
+            if o.kind != "Dot" or o.name in self.env or self._table_handler(o) is not None:
                 continue
             k = key(o)
             if k is not None and k[0] == k0[0]:
@@ -195,6 +197,41 @@ class Interpreter:
     # ------------------------------------------------------------------------
     # dialect-level operations (textual computations below the logical level)
     # ------------------------------------------------------------------------
+    def _table_handler(self, op):
+        """Ring-level operations on replicated / additive placements (and their Reveal to a
+        host) through the declarative (op, placement, operand types) table of
+        runtime/dispatch.py; None when no row matches (logical types never do)."""
+        from moose_amd.ir.computation import AdditivePlacement
+        from moose_amd.runtime import dispatch
+
+        plc = op.placement
+        kind = ("rep" if isinstance(plc, ReplicatedPlacement) else
+                "adt" if isinstance(plc, AdditivePlacement) else
+                "host" if isinstance(plc, HostPlacement) and op.kind == "Reveal" else None)
+        if kind is None or op.sig is None:
+            return None
+        args = [t.name for t in op.sig.args]
+        if op.sig.variadic and args:
+            args = args[:1] * max(1, len(op.inputs))
+        k = dispatch.lookup(op.kind, kind, args)
+        if k is None:
+            return None
+        fams = [dispatch.family(t) for t in args]
+
+        def run(op, ins):
+            vals = []
+            for x, f in zip(ins, fams):
+                if f.startswith("rep_"):
+                    if not x.is_rep:
+                        x = self.to_rep(x, plc)
+                    vals.append(x.v.t if isinstance(x.v, RepFixed) else x.v)
+                else:  # additive shares, public host operands
+                    vals.append(x.v)
+            out = k.fn(dispatch.Ctx(self.sess, op), *vals)
+            return LV(plc, "tensor", None, out)
+
+        return run
+
     def _dialect_handler(self, op):
         """Handler for an operator without a logical ``op_*`` method: replicated dialect
         protocols (Share/Reveal/TruncPr/Msb/BitDecompose/...) or, on a host, the host
