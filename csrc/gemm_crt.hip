@@ -863,8 +863,8 @@ void* workspace(int64_t bytes) {
 
 template <class T>
 int run_crt(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T* A1,
-            int64_t a_bstride, const T* B0, const T* B1, const int8_t* rb_pre, int mode, T* C,
-            int accumulate, hipStream_t st) {
+            int64_t a_bstride, const T* B0, const T* B1, int64_t b_bstride,
+            const int8_t* rb_pre, int mode, T* C, int accumulate, hipStream_t st) {
   constexpr int words = sizeof(T) / 8;
   const CPlan p = make_cplan(words, batch, M, N, K, mode);
   if (p.n < 0) return -6;
@@ -878,7 +878,7 @@ int run_crt(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T
   const int8_t* rb = rb_pre;
   if (!rb) {
     int8_t* rbw = cr + p.cr_bytes;
-    launch_prep<T>(p, tb, true, batch, N, K, K * N, B0, B1, mode, rbw, st);
+    launch_prep<T>(p, tb, true, batch, N, K, b_bstride, B0, B1, mode, rbw, st);
     rb = rbw;
   }
   launch_prep<T>(p, tb, false, batch, M, K, a_bstride, A0, A1, mode, ra, st);
@@ -928,11 +928,29 @@ int mxh_gemm_crt(int words, int64_t batch, int64_t M, int64_t N, int64_t K, cons
   hipStream_t st = (hipStream_t)stream;
   if (words == 1)
     return run_crt<u64>(batch, M, N, K, (const u64*)A0, (const u64*)A1, M * K, (const u64*)B0,
-                        (const u64*)B1, nullptr, mode, (u64*)C, accumulate, st);
+                        (const u64*)B1, K * N, nullptr, mode, (u64*)C, accumulate, st);
   if (words == 2)
     return run_crt<u128>(batch, M, N, K, (const u128*)A0, (const u128*)A1, M * K,
-                         (const u128*)B0, (const u128*)B1, nullptr, mode, (u128*)C, accumulate,
-                         st);
+                         (const u128*)B0, (const u128*)B1, K * N, nullptr, mode, (u128*)C,
+                         accumulate, st);
+  return -2;
+}
+
+// Batch strides given (elements; 0 broadcasts one operand over the batch): the operands of a
+// batched product may be views such as an expanded (stride-0) stack -- no copy is made.
+int mxh_gemm_crt_strided(int words, int64_t batch, int64_t M, int64_t N, int64_t K,
+                         const void* A0, const void* A1, int64_t a_bstride, const void* B0,
+                         const void* B1, int64_t b_bstride, int mode, void* C, int accumulate,
+                         void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (words == 1)
+    return run_crt<u64>(batch, M, N, K, (const u64*)A0, (const u64*)A1, a_bstride,
+                        (const u64*)B0, (const u64*)B1, b_bstride, nullptr, mode, (u64*)C,
+                        accumulate, st);
+  if (words == 2)
+    return run_crt<u128>(batch, M, N, K, (const u128*)A0, (const u128*)A1, a_bstride,
+                         (const u128*)B0, (const u128*)B1, b_bstride, nullptr, mode, (u128*)C,
+                         accumulate, st);
   return -2;
 }
 
@@ -967,10 +985,10 @@ int mxh_crt_with_b(int words, int64_t batch, int64_t M, int64_t N, int64_t K, co
   hipStream_t st = (hipStream_t)stream;
   if (words == 1)
     return run_crt<u64>(batch, M, N, K, (const u64*)A0, (const u64*)A1, a_bstride, nullptr,
-                        nullptr, (const int8_t*)rb, mode, (u64*)C, accumulate, st);
+                        nullptr, 0, (const int8_t*)rb, mode, (u64*)C, accumulate, st);
   if (words == 2)
     return run_crt<u128>(batch, M, N, K, (const u128*)A0, (const u128*)A1, a_bstride, nullptr,
-                         nullptr, (const int8_t*)rb, mode, (u128*)C, accumulate, st);
+                         nullptr, 0, (const int8_t*)rb, mode, (u128*)C, accumulate, st);
   return -2;
 }
 

@@ -144,14 +144,14 @@ __global__ void __launch_bounds__(256) k_prep_a(const T* __restrict__ A0, const 
 // B0 + B1, rows K <= k < 2K hold B0.  Lanes of a wave read 32 consecutive columns.
 template <class T>
 __global__ void __launch_bounds__(256) k_prep_b(const T* __restrict__ B0, const T* __restrict__ B1,
-                                                int64_t K, int64_t N, int mode,
+                                                int64_t K, int64_t N, int64_t b_bstride, int mode,
                                                 int8_t* __restrict__ out, int64_t Np, int64_t Kp) {
   constexpr int L = Limbs<T>::L;
   const int64_t nkb = Kp / TK;
   const int64_t total = (Np / TN) * nkb * 128;
   const int64_t b = blockIdx.y;
-  const T* b0 = B0 + b * K * N;
-  const T* b1 = mode ? B1 + b * K * N : b0;
+  const T* b0 = B0 + b * b_bstride;
+  const T* b1 = mode ? B1 + b * b_bstride : b0;
   int8_t* ob = out + b * (Np / TN) * nkb * (int64_t)L * kTileBytes;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total;
        g += (int64_t)gridDim.x * blockDim.x) {
@@ -845,12 +845,12 @@ void launch_prep_a(const Plan& p, int64_t batch, int64_t M, int64_t K, const T* 
 
 template <class T>
 void launch_prep_b(const Plan& p, int64_t batch, int64_t K, int64_t N, const T* B0,
-                   const T* B1, int mode, int8_t* lb, hipStream_t st) {
+                   const T* B1, int mode, int8_t* lb, hipStream_t st, int64_t b_bstride = -1) {
   const int threads = 256;
   const int64_t work = p.Np * (p.Kp / 16);
   const int gx = (int)std::min<int64_t>((work + threads - 1) / threads, 8192);
   hipLaunchKernelGGL(k_prep_b<T>, dim3(gx, (unsigned)batch), dim3(threads), 0, st, B0, B1, K, N,
-                     mode, lb, p.Np, p.Kp);
+                     b_bstride < 0 ? K * N : b_bstride, mode, lb, p.Np, p.Kp);
 }
 
 template <class T>
@@ -948,6 +948,10 @@ extern "C" int mxh_gemm_crt(int words, int64_t batch, int64_t M, int64_t N, int6
 extern "C" int64_t mxh_crt_b_bytes(int words, int64_t batch, int64_t N, int64_t K, int mode);
 extern "C" int mxh_crt_prep_b(int words, int64_t batch, int64_t K, int64_t N, const void* B0,
                               const void* B1, int mode, void* rb, void* stream);
+extern "C" int mxh_gemm_crt_strided(int words, int64_t batch, int64_t M, int64_t N, int64_t K,
+                                    const void* A0, const void* A1, int64_t a_bstride,
+                                    const void* B0, const void* B1, int64_t b_bstride, int mode,
+                                    void* C, int accumulate, void* stream);
 extern "C" int mxh_crt_with_b(int words, int64_t batch, int64_t M, int64_t N, int64_t K,
                               const void* A0, const void* A1, int64_t a_bstride, int mode,
                               const void* rb, void* C, int accumulate, void* stream);
@@ -1050,6 +1054,37 @@ int mx_gemm_with_b(int words, int64_t batch, int64_t M, int64_t N, int64_t K, co
                       accumulate, st);
   } else {
     return -2;
+  }
+  hipError_t e = hipGetLastError();
+  return e != hipSuccess ? -100 - (int)e : 0;
+}
+
+// Batched product with explicit batch strides (elements) for A and B (0 broadcasts).
+int mx_gemm_strided(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
+                    const void* A1, int64_t a_bstride, const void* B0, const void* B1,
+                    int64_t b_bstride, int mode, void* C, int accumulate, void* stream) {
+  if (M == 0 || N == 0 || batch == 0) return 0;
+  if (words != 1 && words != 2) return -2;
+  if (use_crt(M, N, K, mode))
+    return mxh_gemm_crt_strided(words, batch, M, N, K, A0, A1, a_bstride, B0, B1, b_bstride,
+                                mode, C, accumulate, stream);
+  if (K > max_k_chunk(words, mode)) return -6;
+  Plan p = make_plan(words, batch, M, N, K, mode);
+  void* ws = get_workspace(p.la_bytes + p.lb_bytes);
+  if (!ws) return -4;
+  int8_t* la = (int8_t*)ws;
+  int8_t* lb = la + p.la_bytes;
+  hipStream_t st = (hipStream_t)stream;
+  if (words == 1) {
+    launch_prep_a<u64>(p, batch, M, K, (const u64*)A0, (const u64*)A1, a_bstride, mode, la, st);
+    launch_prep_b<u64>(p, batch, K, N, (const u64*)B0, (const u64*)B1, mode, lb, st, b_bstride);
+    launch_gemm<u64>(p, batch, M, N, la, lb, (u64*)C, accumulate, st);
+  } else {
+    launch_prep_a<u128>(p, batch, M, K, (const u128*)A0, (const u128*)A1, a_bstride, mode, la,
+                        st);
+    launch_prep_b<u128>(p, batch, K, N, (const u128*)B0, (const u128*)B1, mode, lb, st,
+                        b_bstride);
+    launch_gemm<u128>(p, batch, M, N, la, lb, (u128*)C, accumulate, st);
   }
   hipError_t e = hipGetLastError();
   return e != hipSuccess ? -100 - (int)e : 0;

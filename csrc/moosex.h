@@ -114,6 +114,11 @@ int mx_gemm_prep_b(int words, int64_t batch, int64_t K, int64_t N, const void* B
 int mx_gemm_with_b(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
                    const void* A1, int64_t a_bstride, int mode, const void* lb, void* C,
                    int accumulate, void* stream);
+// Device GEMM with explicit batch strides (elements) for the A and B operands; a stride of 0
+// broadcasts one operand over the batch (no copy of an expanded stack).
+int mx_gemm_strided(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
+                    const void* A1, int64_t a_bstride, const void* B0, const void* B1,
+                    int64_t b_bstride, int mode, void* C, int accumulate, void* stream);
 // select the GEMM kernel: 0 = auto, 1 = force VALU reference kernel, 2 = force MFMA
 void mx_set_gemm_impl(int impl);
 // multi-modular (CRT) int8 GEMM for large products: 0 = auto, 1 = force, 2 = off

@@ -58,6 +58,11 @@ _SIGS = {
     ),
     "mx_set_gemm_impl": (None, [c_int]),
     "mx_set_gemm_crt": (None, [c_int]),
+    "mx_gemm_strided": (
+        c_int,
+        [c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_int, c_vp,
+         c_int, c_vp],
+    ),
     "mx_crt_moduli": (c_int, [c_int, c_i64]),
     "mx_crt_tables": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mx_trunc_pr3": (

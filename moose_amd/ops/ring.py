@@ -658,12 +658,57 @@ def dot_cross_rows(x0: RT, x1: RT, r0: int, r1: int, pb: PreparedCross) -> RT:
     return out
 
 
+def _party_batch_strides(t: RT):
+    """(party stride, batch stride) in ring elements of a [P, B, *inner] device tensor whose
+    inner dims are contiguous (e.g. an expanded, stride-0 stack of one operand); None if
+    the layout is anything else."""
+    d = t.data
+    el = 2 if t.bits == 128 else 1
+    if d.dim() < 3:
+        return None
+    expect = 1
+    for size, st in zip(reversed(d.shape[2:]), reversed(d.stride()[2:])):
+        if size != 1 and st != expect:
+            return None
+        expect *= size
+    if d.stride(0) % el or d.stride(1) % el:
+        return None
+    return d.stride(0) // el, d.stride(1) // el
+
+
+def _dot_cross_strided(x0, x1, y0, y1, out, M, K, N):
+    """Per-party strided GEMMs for [3, B, M, K] x [3, B, K, N] operands that are views
+    (no copy of an expanded stack).  False when the layout does not allow it."""
+    bits = x0.bits
+    limit = (16384 if bits == 64 else 8192) // 2
+    if not out.data.is_cuda or K > limit:
+        return False
+    st = [_party_batch_strides(t) for t in (x0, x1, y0, y1)]
+    if any(s is None for s in st) or st[0][1] != st[1][1] or st[2][1] != st[3][1]:
+        return False
+    eb = 16 if bits == 128 else 8
+    B = out.shape[1]
+    lib = nat.lib()
+    for p in range(out.shape[0]):
+        def at(t, s):
+            return ctypes.c_void_p(t.data.data_ptr() + p * s[0] * eb)
+        optr = ctypes.c_void_p(out.data.data_ptr() + p * B * M * N * eb)
+        nat.check(lib.mx_gemm_strided(_words(bits), B, M, N, K, at(x0, st[0]), at(x1, st[1]),
+                                      st[0][1], at(y0, st[2]), at(y1, st[3]), st[2][1], 1, optr,
+                                      0, nat.stream_of(out.data)), "gemm_strided")
+    return True
+
+
 def dot_cross(x0: RT, x1: RT, y0: RT, y1: RT, nb=0) -> RT:
     """RSS cross terms of a matrix product: x0.(y0+y1) + x1.y0 in one K-doubled GEMM."""
     bits = x0.bits
     bshape, M, K, N, oshape = _dot_shapes(x0.shape, y0.shape, nb)
     batch = math.prod(bshape)
     out = empty(bshape + (M, N), bits, x0.device)
+    if (nb == 2 and oshape == (M, N) and not all(
+            t.data.is_contiguous() for t in (x0, x1, y0, y1))
+            and _dot_cross_strided(x0, x1, y0, y1, out, M, K, N)):
+        return out
     _gemm_call(
         bits, batch, M, N, K, x0.data.contiguous(), x1.data.contiguous(), y0.data.contiguous(),
         y1.data.contiguous(), 1, out.data,

@@ -125,11 +125,23 @@ def dot_many(sess, pairs, f=None):
     if len(pairs) == 1:
         return [dot(sess, pairs[0][0], pairs[0][1], f=f)]
     x0 = pairs[0][0]
-    X = concat(sess, [local(sess, x, "ExpandDims", axis=[0]) for x, _ in pairs], 0)
-    Y = concat(sess, [local(sess, y, "ExpandDims", axis=[0]) for _, y in pairs], 0)
+    X = _stack_operands(sess, [x for x, _ in pairs])
+    Y = _stack_operands(sess, [y for _, y in pairs])
     Z = rep.dot(sess, X.t, Y.t, nbatch=1)
     T = _with(x0, rep.trunc_pr(sess, Z, f if f is not None else x0.frac))
     return [local(sess, T, "IndexAxis", axis=0, index=i) for i in range(len(pairs))]
+
+
+def _stack_operands(sess, xs):
+    """Stack on a new leading axis; k uses of ONE operand become a zero-copy broadcast view
+    where the session supports it (the GEMM reads it with batch stride 0) -- k products are
+    still computed, only the k physical copies of the operand are avoided."""
+    rep0 = getattr(sess, "p_repeat0", None)
+    if rep0 is not None and all(x is xs[0] for x in xs):
+        t = xs[0].t if isinstance(xs[0], RepFixed) else xs[0]
+        r = RepTensor(t.plc, t.bits, t.kind, rep0(t.s0, len(xs)), rep0(t.s1, len(xs)))
+        return _with(xs[0], r) if isinstance(xs[0], RepFixed) else r
+    return concat(sess, [local(sess, x, "ExpandDims", axis=[0]) for x in xs], 0)
 
 
 def mul_const(sess, x: RepFixed, c: float) -> RepFixed:

@@ -251,6 +251,13 @@ class StackedSession(Session):
         d[which] = part.data
         return PV(plc, R.RT(d, v.bits))
 
+    def p_repeat0(self, x, k):
+        """k copies of a party vector on a new axis after the party axis, as a stride-0
+        view (consumers that need memory materialise it; the batched GEMM does not)."""
+        v = x.v
+        d = v.data.unsqueeze(1)
+        return PV(x.plc, R.RT(d.expand((d.shape[0], k) + tuple(d.shape[2:])), v.bits))
+
     def p_stack2(self, a, b):
         return PV(a.plc, R.RT(torch.stack([a.v.data, b.v.data], dim=1), a.v.bits))
 
