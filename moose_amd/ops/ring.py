@@ -330,6 +330,13 @@ def compare(op: str, a: RT, b: RT = None) -> RT:
 
 
 def bit_extract(a: RT, bit: int) -> RT:
+    if a.data.is_cuda and a.bits in (64, 128) and 0 <= bit < a.bits:  # one kernel
+        ad = a.data.contiguous()
+        out = torch.empty(a.shape, dtype=torch.uint8, device=ad.device)
+        nat.check(nat.lib().mx_bit_extract(nat.dev_of(ad), _words(a.bits), nat.ptr(ad),
+                                           nat.ptr(out), out.numel(), bit, nat.stream_of(ad)),
+                  "bit_extract")
+        return RT(out, 1)
     if a.bits == 64:
         return RT(((a.data >> bit) & 1).to(torch.uint8), 1)
     w = a.data[..., bit // 64]
@@ -338,6 +345,15 @@ def bit_extract(a: RT, bit: int) -> RT:
 
 def ring_inject(bitsrt: RT, bit: int, ring_bits: int) -> RT:
     """bit tensor -> ring tensor with the bit placed at position ``bit``."""
+    if bitsrt.data.is_cuda and ring_bits in (64, 128) and 0 <= bit < ring_bits:  # one kernel
+        bd = bitsrt.data.contiguous()
+        if bd.dtype != torch.uint8:
+            bd = bd.to(torch.uint8)
+        out = empty(tuple(bd.shape), ring_bits, bd.device)
+        nat.check(nat.lib().mx_ring_inject(nat.dev_of(bd), _words(ring_bits), nat.ptr(bd),
+                                           nat.ptr(out.data), bd.numel(), bit,
+                                           nat.stream_of(bd)), "ring_inject")
+        return out
     b = bitsrt.data.to(torch.int64) & 1
     if ring_bits == 64:
         return RT(b << bit if bit < 64 else torch.zeros_like(b), 64)
