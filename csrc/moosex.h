@@ -159,6 +159,11 @@ int mx_rss_cross_kp(int dev, int kind, int words, const void* x0, const void* x1
 // Stacked 3-party RSS product with the reshare fused in: out0[p] = z_p (cross terms +
 // zero share from slots p, p+1 mod 3) and out1[p] = z_{p+1}, i.e. both shares of every
 // party after the one-round reshare (x*/y*/out* are [3, n] slot vectors)
+// mx_rss_mul3_k (device only) with operand views: views[0..3] party strides, views[4..7]
+// periods (elements) of x0, x1, y0, y1 -- element e of party p is op[p * ps + e % per]
+int mx_rss_mul3_kv(int dev, int kind, int words, const void* x0, const void* x1, const void* y0,
+                   const void* y1, void* out0, void* out1, int64_t n, const uint32_t* slots,
+                   uint64_t nonce, const int64_t* views, void* stream);
 int mx_rss_mul3_k(int dev, int kind, int words, const void* x0, const void* x1, const void* y0,
                   const void* y1, void* out0, void* out1, int64_t n, const uint32_t* slots,
                   uint64_t nonce, void* stream);

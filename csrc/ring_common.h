@@ -187,6 +187,9 @@ int mxh_rss_cross_kp(int kind, int words, const void* x0, const void* x1, const 
 int mxh_rss_cross_k(int kind, int words, const void* x0, const void* x1, const void* y0,
                     const void* y1, void* out, int64_t n, int nparties, const uint32_t* slots,
                     int nslots, uint64_t nonce, void* stream);
+int mxh_rss_mul3_kv(int kind, int words, const void* x0, const void* x1, const void* y0,
+                    const void* y1, void* out0, void* out1, int64_t n, const uint32_t* slots,
+                    uint64_t nonce, const int64_t* views, void* stream);
 int mxh_rss_mul3_k(int kind, int words, const void* x0, const void* x1, const void* y0,
                    const void* y1, void* out0, void* out1, int64_t n, const uint32_t* slots,
                    uint64_t nonce, void* stream);

@@ -663,6 +663,13 @@ int mx_rss_mul3_k(int dev, int kind, int words, const void* x0, const void* x1, 
   return 0;
 }
 
+int mx_rss_mul3_kv(int dev, int kind, int words, const void* x0, const void* x1, const void* y0,
+                   const void* y1, void* out0, void* out1, int64_t n, const uint32_t* slots,
+                   uint64_t nonce, const int64_t* views, void* stream) {
+  if (!dev) return -2;  // device only: host callers pass contiguous operands
+  return mxh_rss_mul3_kv(kind, words, x0, x1, y0, y1, out0, out1, n, slots, nonce, views, stream);
+}
+
 int mx_ks_cross1(int dev, int words, const void* g0, const void* g1, const void* p0,
                  const void* p1, void* z, int64_t n, int d, int both, const uint8_t* keys16,
                  uint64_t nonce, void* stream) {

@@ -304,6 +304,23 @@ __global__ void __launch_bounds__(256) k_rss_cross(int kind, const T* __restrict
   }
 }
 
+// Operand layouts of the stacked multiplication kernels: operand k of party p, element e is
+// ptr_k[p * ps[k] + e % per[k]] -- a slice along the first logical axis (party stride !=
+// n) or a broadcast of one row over it (per = row size) without materialising the view.
+// strided == 0: every operand is a contiguous [3, n] vector (ps = per = n).
+struct Views {
+  int64_t ps[4];
+  int64_t per[4];
+  int strided;
+};
+
+template <class T>
+__device__ __forceinline__ T ld_view(const T* __restrict__ a, const Views& v, int k, int p,
+                                     int64_t e, int64_t n) {
+  if (!v.strided) return a[(int64_t)p * n + e];
+  return a[(int64_t)p * v.ps[k] + (v.per[k] == n ? e : e % v.per[k])];
+}
+
 // Stacked three-party ring (keys k0, k1, k2, k3 == k0): party p needs PRF(k_p) and
 // PRF(k_{p+1}), so each of the three keystreams is used by two parties.  One thread per
 // ChaCha block evaluates the three keys' blocks once and finishes all three parties'
@@ -312,7 +329,7 @@ template <class T>
 __global__ void __launch_bounds__(256) k_rss_cross_ring3(int kind, const T* __restrict__ x0, const T* __restrict__ x1,
                                   const T* __restrict__ y0, const T* __restrict__ y1,
                                   T* __restrict__ out, T* __restrict__ out1, int64_t n,
-                                  KeySrc keys, uint64_t nonce) {
+                                  KeySrc keys, uint64_t nonce, Views vw) {
   __shared__ uint32_t rks[3][kKeyWords];
   stage_keys(rks, keys, 3);
   constexpr int P = Lane<T>::kPer;
@@ -330,10 +347,11 @@ __global__ void __launch_bounds__(256) k_rss_cross_ring3(int kind, const T* __re
         const int64_t i = (int64_t)p * n + e;
         T v = 0;
         if (x0 != nullptr && y0 != nullptr)
-          v = mxr::cross<T>(kind, x0[i], x1 ? x1[i] : (T)0, y0[i], y1 ? y1[i] : (T)0,
+          v = mxr::cross<T>(kind, ld_view(x0, vw, 0, p, e, n), x1 ? ld_view(x1, vw, 1, p, e, n) : (T)0,
+                            ld_view(y0, vw, 2, p, e, n), y1 ? ld_view(y1, vw, 3, p, e, n) : (T)0,
                             x1 != nullptr, y1 != nullptr);
         else if (x0 != nullptr)
-          v = x0[i];
+          v = ld_view(x0, vw, 0, p, e, n);
         const T z = mxr::zs_combine<T>(kind, v, pick<T>(lo[p], hi[p], j), pick<T>(lo[q], hi[q], j));
         out[i] = z;
         // fused reshare: z_p is party p-1's second share
@@ -443,7 +461,7 @@ __global__ void __launch_bounds__(256) k_rss_cross_ring3_lat(int kind, const T* 
                                                              const T* __restrict__ y1,
                                                              T* __restrict__ out,
                                                              T* __restrict__ out1, int64_t n,
-                                                             KeySrc keys, uint64_t nonce) {
+                                                             KeySrc keys, uint64_t nonce, Views vw) {
   constexpr int EPB = 256 / 3;
   __shared__ uint32_t rks[3][kKeyWords];
   __shared__ uint64_t kl[3][EPB], kh[3][EPB];
@@ -471,10 +489,11 @@ __global__ void __launch_bounds__(256) k_rss_cross_ring3_lat(int kind, const T* 
           const int64_t i = (int64_t)p * n + e;
           T v = 0;
           if (x0 != nullptr && y0 != nullptr)
-            v = mxr::cross<T>(kind, x0[i], x1 ? x1[i] : (T)0, y0[i], y1 ? y1[i] : (T)0,
-                              x1 != nullptr, y1 != nullptr);
+            v = mxr::cross<T>(kind, ld_view(x0, vw, 0, p, e, n),
+                              x1 ? ld_view(x1, vw, 1, p, e, n) : (T)0, ld_view(y0, vw, 2, p, e, n),
+                              y1 ? ld_view(y1, vw, 3, p, e, n) : (T)0, x1 != nullptr, y1 != nullptr);
           else if (x0 != nullptr)
-            v = x0[i];
+            v = ld_view(x0, vw, 0, p, e, n);
           const T z = mxr::zs_combine<T>(kind, v, pick<T>(kl[p][tid], kh[p][tid], j),
                                          pick<T>(kl[q][tid], kh[q][tid], j));
           out[i] = z;
@@ -770,7 +789,9 @@ namespace {
 int launch_rss_cross(int kind, int words, const void* x0, const void* x1, const void* y0,
                      const void* y1, void* out, int64_t n, int nparties, bool has_keys,
                      bool ring3, const KeySrc& k, uint64_t nonce, void* stream,
-                     void* out1 = nullptr, int pairs = 0) {
+                     void* out1 = nullptr, int pairs = 0, const Views* views = nullptr) {
+  Views vw{};
+  if (views) vw = *views;
   if (n == 0) return 0;
   if (nparties < 1 || nparties > 3) return -3;
   DEV_DISPATCH(words, T, {
@@ -781,13 +802,13 @@ int launch_rss_cross(int kind, int words, const void* x0, const void* x1, const 
         const int64_t g = (blocks + 84) / 85;
         hipLaunchKernelGGL(k_rss_cross_ring3_lat<T>, dim3((unsigned)g), dim3(kBlock), 0,
                            S(stream), kind, (const T*)x0, (const T*)x1, (const T*)y0,
-                           (const T*)y1, (T*)out, (T*)out1, n, k, nonce);
+                           (const T*)y1, (T*)out, (T*)out1, n, k, nonce, vw);
         MX_LAUNCH_CHECK();
         return 0;
       }
       hipLaunchKernelGGL(k_rss_cross_ring3<T>, dim3(mxd::grid_for_chunks(blocks)), dim3(kBlock), 0,
                          S(stream), kind, (const T*)x0, (const T*)x1, (const T*)y0,
-                         (const T*)y1, (T*)out, (T*)out1, n, k, nonce);
+                         (const T*)y1, (T*)out, (T*)out1, n, k, nonce, vw);
       MX_LAUNCH_CHECK();
       return 0;
     }
@@ -855,6 +876,23 @@ int mxh_rss_mul3_k(int kind, int words, const void* x0, const void* x1, const vo
   for (int i = 0; i < 3; ++i) ptrs[i] = slots + MX_KEY_SLOT_WORDS * i;
   return launch_rss_cross(kind, words, x0, x1, y0, y1, out0, n, 3, true, true,
                           mxd::keysrc_slots(ptrs, 3), nonce, stream, out1);
+}
+
+// mxh_rss_mul3_k with operand views: views = {ps[4], per[4]} in elements (see Views)
+int mxh_rss_mul3_kv(int kind, int words, const void* x0, const void* x1, const void* y0,
+                    const void* y1, void* out0, void* out1, int64_t n, const uint32_t* slots,
+                    uint64_t nonce, const int64_t* views, void* stream) {
+  if (words != 1 && words != 2) return -2;
+  const uint32_t* ptrs[3];
+  for (int i = 0; i < 3; ++i) ptrs[i] = slots + MX_KEY_SLOT_WORDS * i;
+  Views vw;
+  for (int i = 0; i < 4; ++i) {
+    vw.ps[i] = views[i];
+    vw.per[i] = views[4 + i] > 0 ? views[4 + i] : n;
+  }
+  vw.strided = 1;
+  return launch_rss_cross(kind, words, x0, x1, y0, y1, out0, n, 3, true, true,
+                          mxd::keysrc_slots(ptrs, 3), nonce, stream, out1, 0, &vw);
 }
 
 int mxh_ks_cross1(int words, const void* g0, const void* g1, const void* p0, const void* p1,

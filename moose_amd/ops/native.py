@@ -91,6 +91,10 @@ _SIGS = {
         c_int,
         [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_u64, c_vp],
     ),
+    "mx_rss_mul3_kv": (
+        c_int,
+        [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_u64, c_vp, c_vp],
+    ),
     "mx_rss_mul3_k": (
         c_int,
         [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_u64, c_vp],

@@ -830,6 +830,33 @@ def aes_encrypt(key: bytes, block: bytes) -> bytes:
     return out.raw
 
 
+def _party_view(t: RT):
+    """(party stride, period) in elements of a stacked [3, *inner] operand: element e of
+    party p lives at p * ps + e % per.  Covers contiguous data, slices along the first inner
+    axis and one row broadcast over it (stride 0); None for anything else."""
+    d = t.data
+    shape, strides = list(d.shape), list(d.stride())
+    if t.bits == 128:
+        if shape[-1] != 2 or strides[-1] != 1 or any(st % 2 for st in strides[:-1]):
+            return None
+        shape, strides = shape[:-1], [st // 2 for st in strides[:-1]]
+    inner, ist = shape[1:], strides[1:]
+
+    def dense(sh, st):
+        expect = 1
+        for size, stride in zip(reversed(sh), reversed(st)):
+            if size != 1 and stride != expect:
+                return False
+            expect *= size
+        return True
+
+    if dense(inner, ist):
+        return strides[0], math.prod(inner)
+    if inner and ist[0] == 0 and dense(inner[1:], ist[1:]):
+        return strides[0], math.prod(inner[1:])
+    return None
+
+
 def rss_mul3_k(kind: str, x0: RT, x1: RT, y0: RT, y1: RT, slot_ptr: int, nonce: int):
     """Stacked 3-party product with the reshare fused in: returns (s0, s1) with
     s0[p] = z_p and s1[p] = z_{p+1} (one kernel, see mx_rss_mul3_k)."""
@@ -839,10 +866,20 @@ def rss_mul3_k(kind: str, x0: RT, x1: RT, y0: RT, y1: RT, slot_ptr: int, nonce: 
         x0, y0 = _broadcast(x0, y0)
         shp = x0.shape
     # x1/y0/y1 may be None: y0 None -> out = x0 + zero share (then reshared)
-    datas = [None if p is None else (p if p.shape == shp else expand(p, shp)).data.contiguous()
-             for p in (x0, x1, y0, y1)]
+    ops = [None if p is None else (p if p.shape == shp else expand(p, shp)) for p in (x0, x1, y0, y1)]
     n = math.prod(shp) // 3
     out0, out1 = empty(shp, bits, x0.device), empty(shp, bits, x0.device)
+    if x0.data.is_cuda and any(o is not None and not o.data.is_contiguous() for o in ops):
+        views = [(n, n) if o is None else _party_view(o) for o in ops]
+        if all(v is not None for v in views):  # slices / row broadcasts read in place
+            desc = (ctypes.c_int64 * 8)(*[v[0] for v in views], *[v[1] for v in views])
+            nat.check(nat.lib().mx_rss_mul3_kv(
+                nat.dev_of(out0.data), 1 if kind == "bool" else 0, _words(bits),
+                *[nat.ptr(None if o is None else o.data) for o in ops], nat.ptr(out0.data),
+                nat.ptr(out1.data), n, ctypes.c_void_p(slot_ptr), nonce & MASK64, desc,
+                nat.stream_of(out0.data)), "rss_mul3_kv")
+            return out0, out1
+    datas = [None if o is None else o.data.contiguous() for o in ops]
     nat.check(
         nat.lib().mx_rss_mul3_k(
             nat.dev_of(out0.data), 1 if kind == "bool" else 0, _words(bits),

@@ -359,6 +359,8 @@ def poly_eval(sess, x: RepFixed, coeffs) -> RepFixed:
     ceil(log2 n) rounds), and the sum is one public weighted sum over P + one TruncPr."""
     n = len(coeffs) - 1
     f, bits = x.frac, x.bits
+    if n > 1 and _rows_ok(sess, x):
+        return _poly_eval_rows(sess, x, coeffs)
     P = local(sess, x, "ExpandDims", axis=[0])
     have = 1
     while have < n:
@@ -370,6 +372,37 @@ def poly_eval(sess, x: RepFixed, coeffs) -> RepFixed:
         P = concat(sess, [P, mul(sess, left, right)], 0)
         have += m
     acc = _weighted(sess, P.t, [int(round(c * (1 << f))) for c in coeffs[1:]], bits)
+    acc = rep.trunc_pr(sess, acc, f)
+    return add_const(sess, RepFixed(acc, f, x.integ), coeffs[0])
+
+
+def _rows_ok(sess, x) -> bool:
+    """The session builds stacks in place and the mul kernel reads row views (device)."""
+    return (getattr(sess, "p_rows_alloc", None) is not None and x.t.bits in (64, 128)
+            and getattr(sess, "device", None) is not None and sess.device.type == "cuda")
+
+
+def _poly_eval_rows(sess, x: RepFixed, coeffs) -> RepFixed:
+    """poly_eval with the powers stack P preallocated: each level's multiplication reads
+    x^h (a broadcast row) and P[0:m] (a slice) in place and its truncated product is
+    written into rows h..h+m-1 -- the same protocol calls (and shares) as the generic
+    path, without the per-level slice/concat copies."""
+    n = len(coeffs) - 1
+    f, bits, t = x.frac, x.bits, x.t
+    P0, P1 = sess.p_rows_alloc(t.s0, n), sess.p_rows_alloc(t.s1, n)
+    have = 1
+    while have < n:
+        m = min(2 * have, n) - have
+        left = RepTensor(t.plc, bits, t.kind, sess.p_rows_bcast(P0, have - 1, m),
+                         sess.p_rows_bcast(P1, have - 1, m))
+        right = RepTensor(t.plc, bits, t.kind, sess.p_rows_view(P0, 0, m),
+                          sess.p_rows_view(P1, 0, m))
+        z = rep.trunc_pr(sess, rep.mul(sess, left, right), f)
+        sess.p_rows_write(P0, have, z.s0)
+        sess.p_rows_write(P1, have, z.s1)
+        have += m
+    P = RepTensor(t.plc, bits, t.kind, P0, P1)
+    acc = _weighted(sess, P, [int(round(c * (1 << f))) for c in coeffs[1:]], bits)
     acc = rep.trunc_pr(sess, acc, f)
     return add_const(sess, RepFixed(acc, f, x.integ), coeffs[0])
 
@@ -501,10 +534,18 @@ def _exp2_parts(sess, a: RepFixed, negative: bool):
     fac = rep.add_public(sess, fac, _encode_const(sess, 1.0, f, bits))
     # log-depth product over the leading axis: one stacked multiplication per level
     F, n = RepFixed(fac, f, integ), nint
+    views = _rows_ok(sess, F)
     while n > 1:
         h = n // 2
-        prod = mul(sess, local(sess, F, "Slice", slice=(0, h, None)),
-                   local(sess, F, "Slice", slice=(h, 2 * h, None)))
+        if views:  # both halves read in place by the mul kernel
+            lo = _with(F, RepTensor(F.t.plc, bits, "arith", sess.p_rows_view(F.t.s0, 0, h),
+                                    sess.p_rows_view(F.t.s1, 0, h)))
+            hi = _with(F, RepTensor(F.t.plc, bits, "arith", sess.p_rows_view(F.t.s0, h, 2 * h),
+                                    sess.p_rows_view(F.t.s1, h, 2 * h)))
+            prod = mul(sess, lo, hi)
+        else:
+            prod = mul(sess, local(sess, F, "Slice", slice=(0, h, None)),
+                       local(sess, F, "Slice", slice=(h, 2 * h, None)))
         F = prod if n % 2 == 0 else concat(
             sess, [prod, local(sess, F, "Slice", slice=(2 * h, n, None))], 0)
         n = (n + 1) // 2

@@ -251,6 +251,26 @@ class StackedSession(Session):
         d[which] = part.data
         return PV(plc, R.RT(d, v.bits))
 
+    # -- stacked rows (device): build [3, n, ...] stacks in place instead of concat/slice --
+    def p_rows_alloc(self, x, n):
+        """A [3, n, *shape] stack whose row 0 is x (rows 1.. written later)."""
+        v = x.v
+        d = torch.empty((v.data.shape[0], n) + tuple(v.data.shape[1:]), dtype=v.data.dtype,
+                        device=v.data.device)
+        d[:, 0].copy_(v.data)
+        return PV(x.plc, R.RT(d, v.bits))
+
+    def p_rows_view(self, x, r0, r1):
+        return PV(x.plc, R.RT(x.v.data[:, r0:r1], x.v.bits))
+
+    def p_rows_bcast(self, x, r, m):
+        d = x.v.data[:, r:r + 1]
+        return PV(x.plc, R.RT(d.expand((d.shape[0], m) + tuple(d.shape[2:])), x.v.bits))
+
+    def p_rows_write(self, x, r0, src):
+        s = src.v.data
+        x.v.data[:, r0:r0 + s.shape[1]].copy_(s)
+
     def p_repeat0(self, x, k):
         """k copies of a party vector on a new axis after the party axis, as a stride-0
         view (consumers that need memory materialise it; the batched GEMM does not)."""
