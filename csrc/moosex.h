@@ -43,6 +43,17 @@ int mx_add_zs3(int dev, int words, const void* v, const void* r, void* out0, voi
 // out[i] = op(a[i], param)
 int mx_ew_unary(int dev, int op, int words, const void* a, void* out, int64_t n,
                 int64_t param, void* stream);
+// Share-pair forms (both replicated share vectors of a share-wise op, one launch):
+// out0 = a0 op b0, out1 = a1 op b1 (same na / nb / n for both)
+int mx_ew_binary2(int dev, int op, int words, const void* a0, const void* b0, void* out0,
+                  const void* a1, const void* b1, void* out1, int64_t na, int64_t nb, int64_t n,
+                  void* stream);
+int mx_ew_unary2(int dev, int op, int words, const void* a0, void* out0, const void* a1,
+                 void* out1, int64_t n, int64_t param, void* stream);
+// mx_ew_binary_slot on a0 (slot which0) and a1 (slot which1) with one public b
+int mx_ew_binary_slot2(int dev, int op, int words, const void* a0, const void* a1,
+                       const void* b, int64_t nb, void* out0, void* out1, int64_t m,
+                       int nparties, int which0, int which1, void* stream);
 // out[i] = (a[i] cmp b[i]) as 0/1 bytes, signed two's-complement comparison
 int mx_ew_compare(int dev, int op, int words, const void* a, int64_t na, const void* b,
                   int64_t nb, uint8_t* out, int64_t n, void* stream);
@@ -188,6 +199,9 @@ int mx_prf_expand_k(int dev, int words, void* out, int64_t n, int nkeys, const u
 int mx_trunc_pr3_k(int dev, int words, const void* s0, void* out0, void* out1, int64_t n, int m,
                    const uint32_t* slot_k0, const uint32_t* slot_k2, const uint64_t* nonces,
                    void* stream);
+int mx_trunc_pr3_ko(int dev, int words, const void* s0, void* out0, void* out1, int64_t n,
+                    int m, const uint32_t* slot_k0, const uint32_t* slot_k2,
+                    const uint64_t* nonces, int64_t ostride, void* stream);
 int mx_share3_k(int dev, int kind, int words, const void* x, void* out0, void* out1, int64_t n,
                 int j, const uint32_t* slot_next, const uint32_t* slot_all, uint64_t n1,
                 uint64_t na, void* stream);

@@ -374,6 +374,32 @@ int mx_ew_unary(int dev, int op, int words, const void* a, void* out, int64_t n,
   DISPATCH_WORDS(words, T, return unary_t<T>(op, (const T*)a, (T*)out, n, param));
 }
 
+int mx_ew_binary2(int dev, int op, int words, const void* a0, const void* b0, void* out0,
+                  const void* a1, const void* b1, void* out1, int64_t na, int64_t nb, int64_t n,
+                  void* stream) {
+  if (dev) return mxh_ew_binary2(op, words, a0, b0, out0, a1, b1, out1, na, nb, n, stream);
+  int rc = mx_ew_binary(0, op, words, a0, na, b0, nb, out0, n, stream);
+  return rc ? rc : mx_ew_binary(0, op, words, a1, na, b1, nb, out1, n, stream);
+}
+
+int mx_ew_unary2(int dev, int op, int words, const void* a0, void* out0, const void* a1,
+                 void* out1, int64_t n, int64_t param, void* stream) {
+  if (dev) return mxh_ew_unary2(op, words, a0, out0, a1, out1, n, param, stream);
+  int rc = mx_ew_unary(0, op, words, a0, out0, n, param, stream);
+  return rc ? rc : mx_ew_unary(0, op, words, a1, out1, n, param, stream);
+}
+
+int mx_ew_binary_slot2(int dev, int op, int words, const void* a0, const void* a1,
+                       const void* b, int64_t nb, void* out0, void* out1, int64_t m,
+                       int nparties, int which0, int which1, void* stream) {
+  if (dev)
+    return mxh_ew_binary_slot2(op, words, a0, a1, b, nb, out0, out1, m, nparties, which0,
+                               which1, stream);
+  int rc = mx_ew_binary_slot(0, op, words, a0, b, nb, out0, m, nparties, which0, stream);
+  return rc ? rc
+            : mx_ew_binary_slot(0, op, words, a1, b, nb, out1, m, nparties, which1, stream);
+}
+
 int mx_ew_compare(int dev, int op, int words, const void* a, int64_t na, const void* b,
                   int64_t nb, uint8_t* out, int64_t n, void* stream) {
   if (dev) return mxh_ew_compare(op, words, a, na, b, nb, out, n, stream);

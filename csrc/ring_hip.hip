@@ -62,6 +62,55 @@ __global__ void __launch_bounds__(256) k_binary_slot(int op, const T* __restrict
   }
 }
 
+// Share-pair forms: both replicated share vectors (s0, s1) of a share-wise op in ONE launch,
+// blockIdx.y picks the pair member.
+template <class T>
+struct Pair {
+  const T* a[2];
+  const T* b[2];
+  T* o[2];
+  int which[2];
+};
+
+template <class T>
+__global__ void __launch_bounds__(256) k_binary2(int op, Pair<T> p, int64_t na, int64_t nb,
+                                                 int64_t n) {
+  const int y = blockIdx.y;
+  const T* __restrict__ a = p.a[y];
+  const T* __restrict__ b = p.b[y];
+  T* __restrict__ out = p.o[y];
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = mxr::binop<T>(op, a[na == 1 ? 0 : i], b[nb == 1 ? 0 : i]);
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) k_unary2(int op, Pair<T> p, int64_t n, int k) {
+  const int y = blockIdx.y;
+  const T* __restrict__ a = p.a[y];
+  T* __restrict__ out = p.o[y];
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = mxr::unop<T>(op, a[i], k);
+}
+
+// public b applied to party slot which[y] of stacked a[y] ([np, m]), other slots copied
+template <class T>
+__global__ void __launch_bounds__(256) k_binary_slot2(int op, Pair<T> p, int64_t nb, int64_t m,
+                                                      int np) {
+  const int y = blockIdx.y;
+  const T* __restrict__ a = p.a[y];
+  const T* __restrict__ b = p.b[0];
+  T* __restrict__ out = p.o[y];
+  const int which = p.which[y];
+  const int64_t n = m * np;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < n;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t q = g / m, i = g - q * m;
+    out[g] = q == which ? mxr::binop<T>(op, a[g], b[nb == 1 ? 0 : i]) : a[g];
+  }
+}
+
 template <class T>
 __global__ void __launch_bounds__(256) k_add_zs3(const T* __restrict__ v, const T* __restrict__ r,
                                                  T* __restrict__ out0, T* __restrict__ out1,
@@ -621,6 +670,46 @@ int mxh_ew_binary(int op, int words, const void* a, int64_t na, const void* b, i
   DEV_DISPATCH(words, T, {
     hipLaunchKernelGGL(k_binary<T>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream), op,
                        (const T*)a, na, (const T*)b, nb, (T*)out, n);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mxh_ew_binary2(int op, int words, const void* a0, const void* b0, void* out0,
+                   const void* a1, const void* b1, void* out1, int64_t na, int64_t nb, int64_t n,
+                   void* stream) {
+  if (n == 0) return 0;
+  DEV_DISPATCH(words, T, {
+    Pair<T> p{{(const T*)a0, (const T*)a1}, {(const T*)b0, (const T*)b1}, {(T*)out0, (T*)out1},
+              {0, 0}};
+    hipLaunchKernelGGL(k_binary2<T>, dim3(grid_for(n), 2), dim3(kBlock), 0, S(stream), op, p,
+                       na, nb, n);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mxh_ew_unary2(int op, int words, const void* a0, void* out0, const void* a1, void* out1,
+                  int64_t n, int64_t param, void* stream) {
+  if (n == 0) return 0;
+  DEV_DISPATCH(words, T, {
+    Pair<T> p{{(const T*)a0, (const T*)a1}, {nullptr, nullptr}, {(T*)out0, (T*)out1}, {0, 0}};
+    hipLaunchKernelGGL(k_unary2<T>, dim3(grid_for(n), 2), dim3(kBlock), 0, S(stream), op, p, n,
+                       (int)param);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mxh_ew_binary_slot2(int op, int words, const void* a0, const void* a1, const void* b,
+                        int64_t nb, void* out0, void* out1, int64_t m, int nparties, int which0,
+                        int which1, void* stream) {
+  if (m == 0) return 0;
+  DEV_DISPATCH(words, T, {
+    Pair<T> p{{(const T*)a0, (const T*)a1}, {(const T*)b, (const T*)b}, {(T*)out0, (T*)out1},
+              {which0, which1}};
+    hipLaunchKernelGGL(k_binary_slot2<T>, dim3(grid_for(m * nparties), 2), dim3(kBlock), 0,
+                       S(stream), op, p, nb, m, nparties);
     MX_LAUNCH_CHECK();
     return 0;
   });

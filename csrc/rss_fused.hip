@@ -18,7 +18,7 @@ namespace {
 
 template <class T>
 __global__ void __launch_bounds__(256) k_trunc_pr3(const T* __restrict__ s0, T* __restrict__ out0, T* __restrict__ out1,
-                            int64_t n, int m, mxd::KeySrc keys, uint64_t n_r0, uint64_t n_r1,
+                            int64_t n, int64_t os, int m, mxd::KeySrc keys, uint64_t n_r0, uint64_t n_r1,
                             uint64_t n_t, uint64_t n_m, uint64_t n_z0, uint64_t n_z2) {
   __shared__ uint32_t rks[2][mxd::kKeyWords];
   mxd::stage_keys(rks, keys, 2);
@@ -38,11 +38,11 @@ __global__ void __launch_bounds__(256) k_trunc_pr3(const T* __restrict__ s0, T* 
                                        mxd::pick<T>(lo[1], hi[1], j), mxd::pick<T>(lo[2], hi[2], j),
                                        mxd::pick<T>(lo[3], hi[3], j), z0, z2, m);
       out0[i] = z0;
-      out0[n + i] = z1;
-      out0[2 * n + i] = z2;
+      out0[os + i] = z1;
+      out0[2 * os + i] = z2;
       out1[i] = z1;
-      out1[n + i] = z2;
-      out1[2 * n + i] = z0;
+      out1[os + i] = z2;
+      out1[2 * os + i] = z0;
     }
   });
 }
@@ -51,8 +51,8 @@ __global__ void __launch_bounds__(256) k_trunc_pr3(const T* __restrict__ s0, T* 
 // positions are computed one per thread into LDS; then EPB threads finish the elements.
 template <class T>
 __global__ void __launch_bounds__(256) k_trunc_pr3_lat(const T* __restrict__ s0, T* __restrict__ out0,
-                                                       T* __restrict__ out1, int64_t n, int m,
-                                                       mxd::KeySrc keys, uint64_t n_r0,
+                                                       T* __restrict__ out1, int64_t n,
+                                                       int64_t os, int m, mxd::KeySrc keys, uint64_t n_r0,
                                                        uint64_t n_r1, uint64_t n_t, uint64_t n_m,
                                                        uint64_t n_z0, uint64_t n_z2) {
   constexpr int EPB = 256 / 6;
@@ -87,11 +87,11 @@ __global__ void __launch_bounds__(256) k_trunc_pr3_lat(const T* __restrict__ s0,
             mxd::pick<T>(kl[1][tid], kh[1][tid], j), mxd::pick<T>(kl[2][tid], kh[2][tid], j),
             mxd::pick<T>(kl[3][tid], kh[3][tid], j), z0, z2, m);
         out0[i] = z0;
-        out0[n + i] = z1;
-        out0[2 * n + i] = z2;
+        out0[os + i] = z1;
+        out0[2 * os + i] = z2;
         out1[i] = z1;
-        out1[n + i] = z2;
-        out1[2 * n + i] = z0;
+        out1[os + i] = z2;
+        out1[2 * os + i] = z0;
       }
     }
     __syncthreads();
@@ -129,8 +129,9 @@ __global__ void __launch_bounds__(256) k_share3(int kind, const T* __restrict__ 
   });
 }
 
-int launch_trunc_pr3(int words, const void* s0, void* out0, void* out1, int64_t n, int m,
-                     const mxd::KeySrc& keys, const uint64_t* nn, void* stream) {
+// out0 / out1: party p's slot at out + p * os (os = n: dense stacks; larger: row views)
+int launch_trunc_pr3(int words, const void* s0, void* out0, void* out1, int64_t n, int64_t os,
+                     int m, const mxd::KeySrc& keys, const uint64_t* nn, void* stream) {
   if (n == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   const int64_t nblk = words == 1 ? (n + 1) / 2 : n;
@@ -138,11 +139,11 @@ int launch_trunc_pr3(int words, const void* s0, void* out0, void* out1, int64_t 
     const unsigned g = (unsigned)((nblk + 41) / 42);
     if (words == 1)
       hipLaunchKernelGGL(k_trunc_pr3_lat<u64>, dim3(g), dim3(256), 0, st, (const u64*)s0,
-                         (u64*)out0, (u64*)out1, n, m, keys, nn[0], nn[1], nn[2], nn[3], nn[4],
+                         (u64*)out0, (u64*)out1, n, os, m, keys, nn[0], nn[1], nn[2], nn[3], nn[4],
                          nn[5]);
     else
       hipLaunchKernelGGL(k_trunc_pr3_lat<u128>, dim3(g), dim3(256), 0, st, (const u128*)s0,
-                         (u128*)out0, (u128*)out1, n, m, keys, nn[0], nn[1], nn[2], nn[3],
+                         (u128*)out0, (u128*)out1, n, os, m, keys, nn[0], nn[1], nn[2], nn[3],
                          nn[4], nn[5]);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : -100 - (int)e;
@@ -150,11 +151,11 @@ int launch_trunc_pr3(int words, const void* s0, void* out0, void* out1, int64_t 
   if (words == 1) {
     int64_t nb = (n + 1) / 2;
     hipLaunchKernelGGL(k_trunc_pr3<u64>, dim3(mxd::grid_for_chunks(nb)), dim3(256), 0, st,
-                       (const u64*)s0, (u64*)out0, (u64*)out1, n, m, keys, nn[0], nn[1], nn[2],
+                       (const u64*)s0, (u64*)out0, (u64*)out1, n, os, m, keys, nn[0], nn[1], nn[2],
                        nn[3], nn[4], nn[5]);
   } else if (words == 2) {
     hipLaunchKernelGGL(k_trunc_pr3<u128>, dim3(mxd::grid_for_chunks(n)), dim3(256), 0, st,
-                       (const u128*)s0, (u128*)out0, (u128*)out1, n, m, keys, nn[0], nn[1], nn[2],
+                       (const u128*)s0, (u128*)out0, (u128*)out1, n, os, m, keys, nn[0], nn[1], nn[2],
                        nn[3], nn[4], nn[5]);
   } else {
     return -2;
@@ -197,14 +198,22 @@ int mxh_trunc_pr3(int words, const void* s0, void* out0, void* out1, int64_t n, 
   uint8_t kk[32];
   memcpy(kk, k0, 16);
   memcpy(kk + 16, k2, 16);
-  return launch_trunc_pr3(words, s0, out0, out1, n, m, mxd::keysrc_host(kk, 2), nn, stream);
+  return launch_trunc_pr3(words, s0, out0, out1, n, n, m, mxd::keysrc_host(kk, 2), nn, stream);
 }
 
 int mxh_trunc_pr3_k(int words, const void* s0, void* out0, void* out1, int64_t n, int m,
                     const uint32_t* slot_k0, const uint32_t* slot_k2, const uint64_t* nn,
                     void* stream) {
   const uint32_t* ptrs[2] = {slot_k0, slot_k2};
-  return launch_trunc_pr3(words, s0, out0, out1, n, m, mxd::keysrc_slots(ptrs, 2), nn, stream);
+  return launch_trunc_pr3(words, s0, out0, out1, n, n, m, mxd::keysrc_slots(ptrs, 2), nn, stream);
+}
+
+int mxh_trunc_pr3_ko(int words, const void* s0, void* out0, void* out1, int64_t n, int m,
+                     const uint32_t* slot_k0, const uint32_t* slot_k2, const uint64_t* nn,
+                     int64_t ostride, void* stream) {
+  const uint32_t* ptrs[2] = {slot_k0, slot_k2};
+  return launch_trunc_pr3(words, s0, out0, out1, n, ostride, m, mxd::keysrc_slots(ptrs, 2), nn,
+                          stream);
 }
 
 int mxh_share3(int kind, int words, const void* x, void* out0, void* out1, int64_t n, int j,

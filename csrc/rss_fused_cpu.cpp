@@ -1,5 +1,6 @@
 // Host versions of the fused stacked-session kernels (see rss_fused.h) and the C ABI
 // entry points that dispatch host / device.
+#include <cstring>
 #include <functional>
 #include <vector>
 
@@ -20,6 +21,9 @@ extern "C" int mxh_share3(int kind, int words, const void* x, void* out0, void* 
 extern "C" int mxh_trunc_pr3_k(int words, const void* s0, void* out0, void* out1, int64_t n,
                                int m, const uint32_t* slot_k0, const uint32_t* slot_k2,
                                const uint64_t* nonces, void* stream);
+extern "C" int mxh_trunc_pr3_ko(int words, const void* s0, void* out0, void* out1, int64_t n,
+                                int m, const uint32_t* slot_k0, const uint32_t* slot_k2,
+                                const uint64_t* nonces, int64_t ostride, void* stream);
 extern "C" int mxh_share3_k(int kind, int words, const void* x, void* out0, void* out1,
                             int64_t n, int j, const uint32_t* slot_next,
                             const uint32_t* slot_all, uint64_t n1, uint64_t na, void* stream);
@@ -128,6 +132,27 @@ int mx_trunc_pr3_k(int dev, int words, const void* s0, void* out0, void* out1, i
     return mxh_trunc_pr3_k(words, s0, out0, out1, n, m, slot_k0, slot_k2, nonces, stream);
   return mx_trunc_pr3(0, words, s0, out0, out1, n, m, (const uint8_t*)slot_k0,
                       (const uint8_t*)slot_k2, nonces, stream);
+}
+
+// mx_trunc_pr3_k writing party p's output slot at out + p * ostride (row views of a
+// larger stack); the host path computes dense slots and copies them out
+int mx_trunc_pr3_ko(int dev, int words, const void* s0, void* out0, void* out1, int64_t n,
+                    int m, const uint32_t* slot_k0, const uint32_t* slot_k2,
+                    const uint64_t* nonces, int64_t ostride, void* stream) {
+  if (dev)
+    return mxh_trunc_pr3_ko(words, s0, out0, out1, n, m, slot_k0, slot_k2, nonces, ostride,
+                            stream);
+  if (words != 1 && words != 2) return -2;
+  const size_t es = 8 * (size_t)words;
+  std::vector<uint8_t> t0(3 * n * es), t1(3 * n * es);
+  int rc = mx_trunc_pr3_k(0, words, s0, t0.data(), t1.data(), n, m, slot_k0, slot_k2, nonces,
+                          stream);
+  if (rc) return rc;
+  for (int p = 0; p < 3; ++p) {
+    std::memcpy((uint8_t*)out0 + p * ostride * es, t0.data() + p * n * es, n * es);
+    std::memcpy((uint8_t*)out1 + p * ostride * es, t1.data() + p * n * es, n * es);
+  }
+  return 0;
 }
 
 int mx_share3_k(int dev, int kind, int words, const void* x, void* out0, void* out1, int64_t n,

@@ -27,6 +27,11 @@ _SIGS = {
     "mx_device_count": (c_int, []),
     "mx_ew_binary": (c_int, [c_int, c_int, c_int, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "mx_ew_unary": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_i64, c_i64, c_vp]),
+    "mx_ew_binary2": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
+                              c_i64, c_i64, c_vp]),
+    "mx_ew_unary2": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp]),
+    "mx_ew_binary_slot2": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
+                                   c_i64, c_int, c_int, c_int, c_vp]),
     "mx_ew_compare": (c_int, [c_int, c_int, c_int, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "mx_bit_extract": (c_int, [c_int, c_int, c_vp, c_vp, c_i64, c_int, c_vp]),
     "mx_ring_inject": (c_int, [c_int, c_int, c_vp, c_vp, c_i64, c_int, c_vp]),
@@ -101,6 +106,9 @@ _SIGS = {
     ),
     "mx_trunc_pr3_k": (
         c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_vp],
+    ),
+    "mx_trunc_pr3_ko": (
+        c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_i64, c_vp],
     ),
     "mx_share3_k": (
         c_int,

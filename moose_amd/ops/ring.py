@@ -304,6 +304,39 @@ def unary(op: str, a: RT, k: int = 0) -> RT:
     return out
 
 
+def binary2(op: str, a0: RT, b0: RT, a1: RT, b1: RT):
+    """(a0 op b0, a1 op b1) -- both share vectors of a share-wise replicated op -- in one
+    launch (mx_ew_binary2).  Operands of each pair have the same shapes as the other pair's;
+    anything else (bit tensors, general broadcasts) takes two binary() calls."""
+    bits = a0.bits
+    na, nb_ = a0.numel(), b0.numel()
+    if (bits == 1 or not all(isinstance(t, RT) and t.bits == bits for t in (b0, a1, b1))
+            or a1.shape != a0.shape or b1.shape != b0.shape
+            or (na != nb_ and na != 1 and nb_ != 1)):
+        return binary(op, a0, b0), binary(op, a1, b1)
+    n = max(na, nb_)
+    shp = a0.shape if na >= nb_ else b0.shape
+    o0, o1 = empty(shp, bits, a0.device), empty(shp, bits, a0.device)
+    d = [t.data.contiguous() for t in (a0, b0, a1, b1)]
+    nat.check(nat.lib().mx_ew_binary2(
+        nat.dev_of(d[0]), _BIN[op], _words(bits), nat.ptr(d[0]), nat.ptr(d[1]),
+        nat.ptr(o0.data), nat.ptr(d[2]), nat.ptr(d[3]), nat.ptr(o1.data), na, nb_, n,
+        nat.stream_of(d[0])), f"ring{bits} {op} (pair)")
+    return o0, o1
+
+
+def unary2(op: str, a0: RT, a1: RT, k: int = 0):
+    """(op a0, op a1) in one launch (mx_ew_unary2)."""
+    if a0.bits == 1 or a1.bits != a0.bits or a1.shape != a0.shape:
+        return unary(op, a0, k), unary(op, a1, k)
+    o0, o1 = empty(a0.shape, a0.bits, a0.device), empty(a0.shape, a0.bits, a0.device)
+    d0, d1 = a0.data.contiguous(), a1.data.contiguous()
+    nat.check(nat.lib().mx_ew_unary2(
+        nat.dev_of(d0), _UN[op], _words(a0.bits), nat.ptr(d0), nat.ptr(o0.data), nat.ptr(d1),
+        nat.ptr(o1.data), a0.numel(), int(k), nat.stream_of(d0)), f"ring{a0.bits} {op} (pair)")
+    return o0, o1
+
+
 def compare(op: str, a: RT, b: RT = None) -> RT:
     """Signed comparison -> bit tensor (op: lt, gt, eq, msb)."""
     if a.bits == 64 and op != "msb":
@@ -923,6 +956,25 @@ def binary_slot(op: str, a: RT, b: RT, which: int):
         "binary_slot",
     )
     return out
+
+
+def binary_slot2(op: str, a0: RT, a1: RT, b: RT, which0: int, which1: int):
+    """binary_slot on both share vectors (slots which0 / which1) in one launch."""
+    if a0.bits == 1 or a1.shape != a0.shape:
+        return binary_slot(op, a0, b, which0), binary_slot(op, a1, b, which1)
+    np_, m = a0.shape[0], math.prod(a0.shape[1:])
+    nb = b.numel()
+    if nb not in (1, m):
+        raise ValueError("binary_slot2: operand must be a scalar or one slot's shape")
+    d0, d1, bd = a0.data.contiguous(), a1.data.contiguous(), b.data.contiguous()
+    if bd.device != d0.device:
+        bd = bd.to(d0.device)
+    o0, o1 = empty(a0.shape, a0.bits, a0.device), empty(a0.shape, a0.bits, a0.device)
+    nat.check(nat.lib().mx_ew_binary_slot2(
+        nat.dev_of(d0), _BIN[op], _words(a0.bits), nat.ptr(d0), nat.ptr(d1), nat.ptr(bd), nb,
+        nat.ptr(o0.data), nat.ptr(o1.data), m, np_, int(which0), int(which1),
+        nat.stream_of(d0)), "binary_slot (pair)")
+    return o0, o1
 
 
 def ks_cross1(g0: RT, g1: RT, p0: RT, p1: RT, d: int, both: bool, keys, nonce: int) -> RT:

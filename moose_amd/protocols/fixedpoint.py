@@ -397,9 +397,14 @@ def _poly_eval_rows(sess, x: RepFixed, coeffs) -> RepFixed:
                          sess.p_rows_bcast(P1, have - 1, m))
         right = RepTensor(t.plc, bits, t.kind, sess.p_rows_view(P0, 0, m),
                           sess.p_rows_view(P1, 0, m))
-        z = rep.trunc_pr(sess, rep.mul(sess, left, right), f)
-        sess.p_rows_write(P0, have, z.s0)
-        sess.p_rows_write(P1, have, z.s1)
+        prod = rep.mul(sess, left, right)
+        if getattr(sess, "fused", False):  # the trunc kernel writes rows have.. in place
+            rep.trunc_pr(sess, prod, f, out=(sess.p_rows_view(P0, have, have + m),
+                                             sess.p_rows_view(P1, have, have + m)))
+        else:
+            z = rep.trunc_pr(sess, prod, f)
+            sess.p_rows_write(P0, have, z.s0)
+            sess.p_rows_write(P1, have, z.s1)
         have += m
     P = RepTensor(t.plc, bits, t.kind, P0, P1)
     acc = _weighted(sess, P, [int(round(c * (1 << f))) for c in coeffs[1:]], bits)

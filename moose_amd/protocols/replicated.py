@@ -166,22 +166,34 @@ def from_slot_holders(sess, plc, slot: int, x_h0: HV, x_h1: HV, like: PV,
 # ---------------------------------------------------------------------------
 # local (communication-free) operations
 # ---------------------------------------------------------------------------
+def _sharewise(sess, prim, plc, a, b=None, **attrs):
+    """prim on both share vectors: (prim(a[0], b[0]), prim(a[1], b[1])).  A stacked session
+    does the pair in one kernel where it can (p_pair); otherwise two ops."""
+    pair = getattr(sess, "p_pair", None)
+    if pair is not None:
+        r = pair(prim, plc, a, b, **attrs)
+        if r is not None:
+            return r
+    if b is None:
+        return sess.p(prim, plc, a[0], **attrs), sess.p(prim, plc, a[1], **attrs)
+    return sess.p(prim, plc, a[0], b[0], **attrs), sess.p(prim, plc, a[1], b[1], **attrs)
+
+
 def local(sess, x: RepTensor, prim, **attrs) -> RepTensor:
     """Apply a linear / shape primitive share-wise."""
-    return RepTensor(x.plc, x.bits, x.kind, sess.p(prim, x.plc, x.s0, **attrs),
-                     sess.p(prim, x.plc, x.s1, **attrs))
+    s0, s1 = _sharewise(sess, prim, x.plc, (x.s0, x.s1), **attrs)
+    return RepTensor(x.plc, x.bits, x.kind, s0, s1)
 
 
 def add(sess, x: RepTensor, y: RepTensor) -> RepTensor:
-    a = x.add_prim
-    return RepTensor(x.plc, x.bits, x.kind, sess.p(a, x.plc, x.s0, y.s0),
-                     sess.p(a, x.plc, x.s1, y.s1))
+    s0, s1 = _sharewise(sess, x.add_prim, x.plc, (x.s0, x.s1), (y.s0, y.s1))
+    return RepTensor(x.plc, x.bits, x.kind, s0, s1)
 
 
 def sub(sess, x: RepTensor, y: RepTensor) -> RepTensor:
     a = "Sub" if x.kind == "arith" else "Xor"
-    return RepTensor(x.plc, x.bits, x.kind, sess.p(a, x.plc, x.s0, y.s0),
-                     sess.p(a, x.plc, x.s1, y.s1))
+    s0, s1 = _sharewise(sess, a, x.plc, (x.s0, x.s1), (y.s0, y.s1))
+    return RepTensor(x.plc, x.bits, x.kind, s0, s1)
 
 
 def neg(sess, x: RepTensor) -> RepTensor:
@@ -192,16 +204,22 @@ def neg(sess, x: RepTensor) -> RepTensor:
 
 def add_public(sess, x: RepTensor, c) -> RepTensor:
     """x + c for a public c (added to slot 0 only)."""
-    a = x.add_prim
-    s0 = sess.p_apply_at(a, x.plc, x.s0, 0, c)
-    s1 = sess.p_apply_at(a, x.plc, x.s1, 2, c)
-    return RepTensor(x.plc, x.bits, x.kind, s0, s1)
+    return _apply_public(sess, x, x.add_prim, c)
 
 
 def sub_public(sess, x: RepTensor, c) -> RepTensor:
-    a = "Sub" if x.kind == "arith" else "Xor"
-    s0 = sess.p_apply_at(a, x.plc, x.s0, 0, c)
-    s1 = sess.p_apply_at(a, x.plc, x.s1, 2, c)
+    return _apply_public(sess, x, "Sub" if x.kind == "arith" else "Xor", c)
+
+
+def _apply_public(sess, x: RepTensor, prim, c) -> RepTensor:
+    """prim(share of party 0, c): slot 0 of s0 and slot 2 of s1 hold x_0."""
+    both = getattr(sess, "p_apply_at2", None)
+    if both is not None:
+        r = both(prim, x.plc, x.s0, x.s1, 0, 2, c)
+        if r is not None:
+            return RepTensor(x.plc, x.bits, x.kind, r[0], r[1])
+    s0 = sess.p_apply_at(prim, x.plc, x.s0, 0, c)
+    s1 = sess.p_apply_at(prim, x.plc, x.s1, 2, c)
     return RepTensor(x.plc, x.bits, x.kind, s0, s1)
 
 
@@ -212,8 +230,8 @@ def public_sub(sess, c, x: RepTensor) -> RepTensor:
 def mul_public(sess, x: RepTensor, c) -> RepTensor:
     m = "Mul" if x.kind == "arith" else "And"
     pc = sess.public(x.plc, c)
-    return RepTensor(x.plc, x.bits, x.kind, sess.p(m, x.plc, x.s0, pc),
-                     sess.p(m, x.plc, x.s1, pc))
+    s0, s1 = _sharewise(sess, m, x.plc, (x.s0, x.s1), (pc, pc))
+    return RepTensor(x.plc, x.bits, x.kind, s0, s1)
 
 
 def dot_public(sess, x: RepTensor, c, public_left=False) -> RepTensor:
@@ -350,7 +368,7 @@ def dot_trunc(sess, x: RepTensor, y: RepTensor, m: int) -> RepTensor:
 # ---------------------------------------------------------------------------
 # probabilistic truncation (dealer-assisted, P2 = dealer)
 # ---------------------------------------------------------------------------
-def trunc_pr(sess, x: RepTensor, m: int) -> RepTensor:
+def trunc_pr(sess, x: RepTensor, m: int, out=None) -> RepTensor:
     """y ~= x / 2^m (probabilistic rounding, error <= 1 ulp), for |x| < 2^(k-2).
 
     Escudero et al. (as in reference additive/trunc.rs:114-170) with dealer P2 and all
@@ -359,6 +377,8 @@ def trunc_pr(sess, x: RepTensor, m: int) -> RepTensor:
       * shares of r_top, r_msb for P1 are the only dealer messages (input independent);
       * round 1: P0 and P1 exchange their masked shares -> both know c = x + r + 2^(k-2);
       * round 2: additive -> replicated exchange (w_0, w_1).
+
+    ``out`` (fused stacked sessions only): (s0, s1) party-vector views written in place.
     """
     if m == 0:
         return x
@@ -367,8 +387,13 @@ def trunc_pr(sess, x: RepTensor, m: int) -> RepTensor:
         nr0, nr1, nt, nm = (sess.nonce(plc) for _ in range(4))
         if getattr(sess, "fused", False):
             n0, n2 = sess.nonce(plc), sess.nonce(plc)
-            s0, s1 = sess.fused_trunc_pr(x, m, (nr0, nr1, nt, nm, n0, n2))
+            if out is not None:
+                s0, s1 = sess.fused_trunc_pr(x, m, (nr0, nr1, nt, nm, n0, n2), out=out)
+            else:
+                s0, s1 = sess.fused_trunc_pr(x, m, (nr0, nr1, nt, nm, n0, n2))
             return RepTensor(plc, bits, "arith", s0, s1)
+        if out is not None:
+            raise ValueError("trunc_pr(out=...) needs a fused stacked session")
         party = getattr(sess, "party_trunc", None)
         if party is not None and bits in (64, 128) and m <= 63:
             n0, n2 = sess.nonce(plc), sess.nonce(plc)

@@ -251,6 +251,45 @@ class StackedSession(Session):
         d[which] = part.data
         return PV(plc, R.RT(d, v.bits))
 
+    # -- share pairs: both share vectors of a share-wise op in one launch ----------------
+    _PAIR_BIN = {"Add": "add", "Sub": "sub", "Xor": "xor", "And": "and", "Mul": "mul"}
+
+    def p_pair(self, prim, plc, a, b=None, **attrs):
+        """(prim(a[0], b[0]), prim(a[1], b[1])) as one kernel when both are ring tensors of
+        64/128 bits (Neg / Shl / the binary ring ops); None -> caller issues two ops."""
+        v0, v1 = a[0].v, a[1].v
+        if not (isinstance(v0, R.RT) and isinstance(v1, R.RT)) or v0.bits not in (64, 128):
+            return None
+        if b is None:
+            if prim == "Neg":
+                o0, o1 = R.unary2("neg", v0, v1)
+            elif prim == "Shl":
+                o0, o1 = R.unary2("shl", v0, v1, attrs["amount"])
+            else:
+                return None
+            return PV(plc, o0), PV(plc, o1)
+        op = self._PAIR_BIN.get(prim)
+        if op is None:
+            return None
+        w = [x.v for x in b]
+        if not all(isinstance(t, R.RT) and t.bits == v0.bits for t in w):
+            return None
+        o0, o1 = R.binary2(op, v0, w[0], v1, w[1])
+        return PV(plc, o0), PV(plc, o1)
+
+    def p_apply_at2(self, prim, plc, x0, x1, which0, which1, c):
+        """p_apply_at on both share vectors in one kernel (None if not applicable)."""
+        op = self._PAIR_BIN.get(prim)
+        v0, v1 = x0.v, x1.v
+        if (op is None or not isinstance(c, R.RT) or c.bits != v0.bits
+                or v0.bits not in (64, 128) or v1.shape != v0.shape):
+            return None
+        m = math.prod(v0.shape[1:])
+        if not (c.numel() == 1 or tuple(c.shape) == tuple(v0.shape[1:])) or c.numel() not in (1, m):
+            return None
+        o0, o1 = R.binary_slot2(op, v0, v1, c, which0, which1)
+        return PV(plc, o0), PV(plc, o1)
+
     # -- stacked rows (device): build [3, n, ...] stacks in place instead of concat/slice --
     def p_rows_alloc(self, x, n):
         """A [3, n, *shape] stack whose row 0 is x (rows 1.. written later)."""
@@ -373,25 +412,44 @@ class StackedSession(Session):
     # -- fused whole-protocol kernels (same shares as the generic protocol code) ------
     fused = os.environ.get("MOOSEX_FUSED", "1") != "0"
 
-    def fused_trunc_pr(self, x, m, nonces):
-        """All three parties' TruncPr in one kernel (see replicated.trunc_pr)."""
+    def fused_trunc_pr(self, x, m, nonces, out=None):
+        """All three parties' TruncPr in one kernel (see replicated.trunc_pr).  ``out``:
+        optional (s0, s1) party-vector views (each party's slot dense, e.g. rows of a larger
+        stack) that the kernel writes in place."""
         import ctypes
 
         from moose_amd.ops import native as nat
 
         s0 = x.s0.v.data.contiguous()
-        out0, out1 = torch.empty_like(s0), torch.empty_like(s0)
         n = x.s0.v.numel() // 3
         nn = (ctypes.c_uint64 * 6)(*[v & ((1 << 64) - 1) for v in nonces])
+        keys = (ctypes.c_void_p(self.key_ptr(x.plc, 0)), ctypes.c_void_p(self.key_ptr(x.plc, 2)))
+        if out is not None:
+            out0, out1 = out[0].v.data, out[1].v.data
+            w = 2 if x.bits == 128 else 1  # int64 words per element
+            os_ = out0.stride(0)
+            if not (out0.shape == s0.shape and out1.shape == s0.shape
+                    and out1.stride(0) == os_ and out0[0].is_contiguous()
+                    and out1[0].is_contiguous() and os_ % w == 0 and os_ // w >= n):
+                raise ValueError("fused_trunc_pr: out views must hold dense party slots")
+            os_ //= w
+            nat.check(nat.lib().mx_trunc_pr3_ko(
+                nat.dev_of(s0), R._words(x.bits), nat.ptr(s0), nat.ptr(out0), nat.ptr(out1), n, m,
+                *keys, nn, os_, nat.stream_of(s0)), "trunc_pr3 (views)")
+            self._trunc_traffic(x, out0[0].numel() * out0.element_size())
+            return out[0], out[1]
+        out0, out1 = torch.empty_like(s0), torch.empty_like(s0)
         nat.check(
             nat.lib().mx_trunc_pr3_k(
                 nat.dev_of(s0), R._words(x.bits), nat.ptr(s0), nat.ptr(out0), nat.ptr(out1), n, m,
-                ctypes.c_void_p(self.key_ptr(x.plc, 0)), ctypes.c_void_p(self.key_ptr(x.plc, 2)),
-                nn, nat.stream_of(s0),
+                *keys, nn, nat.stream_of(s0),
             ),
             "trunc_pr3",
         )
-        nbytes = out0.numel() * out0.element_size() // 3
+        self._trunc_traffic(x, out0.numel() * out0.element_size() // 3)
+        return PV(x.plc, R.RT(out0, x.bits)), PV(x.plc, R.RT(out1, x.bits))
+
+    def _trunc_traffic(self, x, nbytes):
         o = x.plc.owners
         # messages of the protocol: dealer -> P1 (2 tensors), P0 <-> P1 (two rounds)
         for src, dst, k in ((o[2], o[1], 2), (o[0], o[1], 2), (o[1], o[0], 2)):
@@ -399,7 +457,6 @@ class StackedSession(Session):
                 self.stats.record_send(src, dst, nbytes)
         self.stats.record_round(2 * nbytes)
         self.stats.record_round(2 * nbytes)
-        return PV(x.plc, R.RT(out0, x.bits)), PV(x.plc, R.RT(out1, x.bits))
 
     def fused_share(self, plc, x: HV, j, kind, n1, na):
         import ctypes

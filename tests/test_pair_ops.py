@@ -1,0 +1,74 @@
+"""Share-pair elementwise kernels (mx_ew_binary2 / mx_ew_unary2 / mx_ew_binary_slot2: both
+replicated share vectors of a share-wise op in one launch) and the TruncPr kernel writing
+into row views (mx_trunc_pr3_ko) agree exactly with the one-operand forms."""
+import numpy as np
+import pytest
+import torch
+
+from moose_amd.ir.computation import ReplicatedPlacement
+from moose_amd.ops import ring as R
+from moose_amd.protocols import replicated as rep
+from moose_amd.runtime.session import PV
+from moose_amd.runtime.session import StackedSession
+
+DEVICES = ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)]
+
+
+def _rand(shape, bits, dev, seed):
+    rng = np.random.default_rng(seed)
+    vals = rng.integers(0, 2**62, size=int(np.prod(shape)), dtype=np.int64).astype(object)
+    vals = vals * (1 << (bits - 62)) + rng.integers(0, 2**40, size=vals.shape[0]).astype(object)
+    return R.reshape(R.from_ints(vals % (1 << bits), bits, dev), shape)
+
+
+def _eq(a, b):
+    np.testing.assert_array_equal(R.to_ints(a), R.to_ints(b))
+
+
+@pytest.mark.parametrize("dev", DEVICES)
+@pytest.mark.parametrize("bits", [64, 128])
+@pytest.mark.parametrize("op", ["add", "sub", "mul", "xor", "and"])
+def test_binary2_matches_binary(dev, bits, op):
+    a0, b0, a1, b1 = (_rand((3, 37), bits, dev, s) for s in range(4))
+    o0, o1 = R.binary2(op, a0, b0, a1, b1)
+    _eq(o0, R.binary(op, a0, b0))
+    _eq(o1, R.binary(op, a1, b1))
+    c = _rand((1,), bits, dev, 9)  # scalar broadcast
+    o0, o1 = R.binary2(op, a0, c, a1, c)
+    _eq(o0, R.binary(op, a0, c))
+    _eq(o1, R.binary(op, a1, c))
+
+
+@pytest.mark.parametrize("dev", DEVICES)
+@pytest.mark.parametrize("bits", [64, 128])
+def test_unary2_and_slot2(dev, bits):
+    a0, a1 = _rand((3, 5, 7), bits, dev, 1), _rand((3, 5, 7), bits, dev, 2)
+    for op, k in (("neg", 0), ("shl", 5)):
+        o0, o1 = R.unary2(op, a0, a1, k)
+        _eq(o0, R.unary(op, a0, k))
+        _eq(o1, R.unary(op, a1, k))
+    c = _rand((5, 7), bits, dev, 3)
+    o0, o1 = R.binary_slot2("add", a0, a1, c, 0, 2)
+    _eq(o0, R.binary_slot("add", a0, c, 0))
+    _eq(o1, R.binary_slot("add", a1, c, 2))
+
+
+@pytest.mark.parametrize("dev", DEVICES)
+@pytest.mark.parametrize("bits", [64, 128])
+def test_trunc_into_row_views(dev, bits):
+    """fused_trunc_pr(out=row views) writes the same shares as the dense form."""
+    plc = ReplicatedPlacement(("alice", "bob", "carole"))
+    shp = (3, 2, 11)
+    x0, x1 = _rand(shp, bits, dev, 4), _rand(shp, bits, dev, 5)
+    x = rep.RepTensor(plc, bits, "arith", PV(plc, x0), PV(plc, x1))
+    nonces = (11, 12, 13, 14, 15, 16)
+    s = StackedSession(dev, seed=7)
+    d0, d1 = s.fused_trunc_pr(x, 20, nonces)
+    big0 = R.zeros((3, 5, 11), bits, dev).data
+    big1 = torch.zeros_like(big0)
+    v0, v1 = PV(plc, R.RT(big0[:, 2:4], bits)), PV(plc, R.RT(big1[:, 2:4], bits))
+    s.fused_trunc_pr(x, 20, nonces, out=(v0, v1))
+    _eq(R.RT(big0[:, 2:4].contiguous(), bits), d0.v)
+    _eq(R.RT(big1[:, 2:4].contiguous(), bits), d1.v)
+    # rows outside the view are untouched
+    assert not big0[:, :2].any() and not big0[:, 4:].any()
