@@ -175,8 +175,69 @@ def toposort(comp: Computation, **_) -> Computation:
     return comp.toposorted()
 
 
+_NO_KERNEL_CHECK = {"Load", "Save", "Send", "Receive"}  # as well_formed.rs:31
+# host operations the graph executor runs itself (runtime/graph_executor.py _exec)
+_HOST_EXECUTOR_OPS = {"Constant", "Input", "Output", "PrfKeyGen", "RingMulCross",
+                      "BitAndCross", "RingDotCross"}
+_PLAIN_TYPES = {"Unknown", "HostUnit", "HostString", "HostSeed", "HostPrfKey", "HostShape",
+                "Shape", "Tensor", "Bit", "Float32", "Float64", "Ring64", "Ring128", "Fixed"}
+
+
+def _types_compatible(expected: T.Ty, found: T.Ty) -> bool:
+    if expected == found or "Unknown" in (expected.name, found.name):
+        return True
+    if expected.name == found.name == "Tensor":
+        return T.UNKNOWN_DTYPE in (expected.inner, found.inner) or expected.inner is None \
+            or found.inner is None
+    shapes = {("HostShape", None), ("Shape", "Host"), ("Shape", "Unknown"), ("Shape", None)}
+    return (expected.name, expected.inner) in shapes and (found.name, found.inner) in shapes
+
+
+def _kernel_error(op) -> Optional[str]:
+    """Why no kernel of this executor runs ``op`` at its placement and signature, or None:
+    the static counterpart of the interpreter's routing (declarative table for ring-level
+    replicated / additive ops, replicated dialect protocols, logical op_* handlers, host
+    primitives) -- the role of DispatchKernel::compile in well_formed.rs:28-116."""
+    from moose_amd.ir.computation import AdditivePlacement
+    from moose_amd.ir.computation import ReplicatedPlacement
+    from moose_amd.runtime import dispatch
+    from moose_amd.runtime import interpreter as I
+    from moose_amd.runtime.prims import PRIMS
+
+    if op.kind in _NO_KERNEL_CHECK or op.sig is None:
+        return None
+    plc = op.placement
+    args = [t.name for t in op.sig.args]
+    if op.sig.variadic and args:
+        args = args[:1] * max(1, len(op.inputs))
+    concrete = any(a not in _PLAIN_TYPES for a in args) or op.sig.ret.name not in _PLAIN_TYPES
+    logical = getattr(I.Interpreter, f"op_{op.kind}", None) is not None
+    if isinstance(plc, AdditivePlacement):
+        if dispatch.lookup(op.kind, "adt", args) is not None:
+            return None
+        return f"no additive kernel for {op.kind} on ({', '.join(args)})"
+    if isinstance(plc, ReplicatedPlacement):
+        if dispatch.lookup(op.kind, "rep", args) is not None or op.kind in I._REP_DIALECT:
+            return None
+        if logical and not any(a.startswith(("Additive", "Host")) for a in args):
+            return None
+        return f"no replicated kernel for {op.kind} on ({', '.join(args)})"
+    if isinstance(plc, HostPlacement):
+        if op.kind == "Reveal" and dispatch.lookup("Reveal", "host", args) is not None:
+            return None
+        if logical or op.kind in PRIMS or op.kind in _HOST_EXECUTOR_OPS:
+            return None
+        return f"no host kernel for {op.kind}"
+    # mirrored placements run the logical handlers
+    if logical or (not concrete and op.kind in PRIMS):
+        return None
+    return f"no kernel for {op.kind} on {type(plc).__name__}"
+
+
 def well_formed(comp: Computation, **_) -> Computation:
-    """Topological order + every operator known + every input defined earlier."""
+    """Topological order, every operator known, every input defined earlier, argument
+    counts and producer types consistent with each signature, and a kernel for every
+    (operator, placement, signature) instantiation (reference well_formed.rs:13-123)."""
     from moose_amd.ir.operators import ALL_OPERATORS
     from moose_amd.runtime import native_rt
 
@@ -189,7 +250,7 @@ def well_formed(comp: Computation, **_) -> Computation:
             op = comp.operations[bad]
             raise CompilationError(f"{op.name}: an input is not defined before use")
 
-    seen = set()
+    seen = {}
     sends = {bytes(op.attrs["rendezvous_key"]) for op in comp.operations if op.kind == "Send"}
     for op in comp.operations:
         if op.kind not in ALL_OPERATORS:
@@ -201,7 +262,22 @@ def well_formed(comp: Computation, **_) -> Computation:
             raise CompilationError(f"{op.name}: no Send for its rendezvous key")
         if op.name in seen:
             raise CompilationError(f"duplicate operation name {op.name}")
-        seen.add(op.name)
+        sig = op.sig
+        if sig is not None and sig.args:
+            if not sig.variadic and len(sig.args) != len(op.inputs):
+                raise CompilationError(f"{op.name}: {op.kind} takes {len(sig.args)} "
+                                       f"argument(s), {len(op.inputs)} given")
+            for k, i in enumerate(op.inputs):
+                want = sig.args[0] if sig.variadic else sig.args[k]
+                got = seen[i].sig.ret if seen[i].sig is not None else T.UNKNOWN
+                if not _types_compatible(want, got):
+                    raise CompilationError(
+                        f"{op.name}: argument {k} ({i}): "
+                        f"{errors.TypeMismatch(want.to_textual(), got.to_textual())}")
+        why = _kernel_error(op)
+        if why is not None:
+            raise CompilationError(f"{op.name}: {why}")
+        seen[op.name] = op
     return comp
 
 

@@ -136,7 +136,8 @@ kernel("TruncPr", "rep", "rep_ring")(
     lambda c, x: rep.trunc_pr(c.sess, x, int(c.attr("amount", "precision", default=0))))
 kernel("Abs", "rep", "rep_ring")(lambda c, x: rep.abs_(c.sess, x))
 kernel("Relu", "rep", "rep_ring")(lambda c, x: rep.relu(c.sess, x))
-kernel("Mux", "rep", "*", "rep_ring", "rep_ring")(lambda c, s, x, y: rep.mux(c.sess, s, x, y))
+for _sel in ("rep_ring", "rep_bit"):  # ring-form or bit-form selector
+    kernel("Mux", "rep", _sel, "rep_ring", "rep_ring")(lambda c, s, x, y: rep.mux(c.sess, s, x, y))
 
 
 def _add_n(c, xs):

@@ -137,6 +137,32 @@ a = Constant{value = HostFloat64Tensor([1.0])}: () -> HostFloat64Tensor () @Host
         passes.compile(Computation.from_textual(src), ["nope"])
 
 
+def test_well_formed_checks_signatures_and_kernels():
+    """Argument counts, producer types and a kernel per (op, placement, signature) are
+    checked like the reference's symbolic kernel compilation (well_formed.rs:28-116)."""
+    head = """a = Constant{value = HostRing64Tensor([1])}: () -> HostRing64Tensor () @Host(alice)
+f = Constant{value = HostFloat64Tensor([1.0])}: () -> HostFloat64Tensor () @Host(alice)
+"""
+    ok = head + "z = Add: (HostRing64Tensor, HostRing64Tensor) -> HostRing64Tensor (a, a) @Host(alice)\n"
+    passes.well_formed(Computation.from_textual(ok))
+    bad_type = head + "z = Add: (HostRing64Tensor, HostRing64Tensor) -> HostRing64Tensor (a, f) @Host(alice)\n"
+    with pytest.raises(passes.CompilationError, match="Type mismatch"):
+        passes.well_formed(Computation.from_textual(bad_type))
+    bad_arity = head + "z = Add: (HostRing64Tensor, HostRing64Tensor) -> HostRing64Tensor (a) @Host(alice)\n"
+    with pytest.raises(passes.CompilationError, match="argument"):
+        passes.well_formed(Computation.from_textual(bad_arity))
+    adt = head + """s = Share: (HostRing64Tensor) -> ReplicatedRing64Tensor (a) @Replicated(alice, bob, carole)
+d = RepToAdt: (ReplicatedRing64Tensor) -> AdditiveRing64Tensor (s) @Additive(alice, bob)
+"""
+    passes.well_formed(Computation.from_textual(adt))
+    no_kernel = adt + "z = Dot: (AdditiveRing64Tensor, AdditiveRing64Tensor) -> AdditiveRing64Tensor (d, d) @Additive(alice, bob)\n"
+    with pytest.raises(passes.CompilationError, match="no additive kernel"):
+        passes.well_formed(Computation.from_textual(no_kernel))
+    no_rep = adt + "z = Mux: (AdditiveRing64Tensor, ReplicatedRing64Tensor, ReplicatedRing64Tensor) -> ReplicatedRing64Tensor (d, s, s) @Replicated(alice, bob, carole)\n"
+    with pytest.raises(passes.CompilationError, match="no replicated kernel"):
+        passes.well_formed(Computation.from_textual(no_rep))
+
+
 def test_networking_dedups_per_destination():
     src = """
 a = Constant{value = HostFloat64Tensor([1.0])}: () -> HostFloat64Tensor () @Host(alice)
