@@ -54,6 +54,10 @@ int mx_ew_unary2(int dev, int op, int words, const void* a0, void* out0, const v
 int mx_ew_binary_slot2(int dev, int op, int words, const void* a0, const void* a1,
                        const void* b, int64_t nb, void* out0, void* out1, int64_t m,
                        int nparties, int which0, int which1, void* stream);
+// Two trivial sharings in the stacked layout [nparties, m], one launch:
+// out0[q, i] = q == which0 ? x0[i] : 0 ; out1[q, i] = q == which1 ? x1[i] : 0
+int mx_slot_place2(int dev, int words, const void* x0, const void* x1, void* out0, void* out1,
+                   int64_t m, int nparties, int which0, int which1, void* stream);
 // out[i] = (a[i] cmp b[i]) as 0/1 bytes, signed two's-complement comparison
 int mx_ew_compare(int dev, int op, int words, const void* a, int64_t na, const void* b,
                   int64_t nb, uint8_t* out, int64_t n, void* stream);

@@ -400,6 +400,25 @@ int mx_ew_binary_slot2(int dev, int op, int words, const void* a0, const void* a
             : mx_ew_binary_slot(0, op, words, a1, b, nb, out1, m, nparties, which1, stream);
 }
 
+int mx_slot_place2(int dev, int words, const void* x0, const void* x1, void* out0, void* out1,
+                   int64_t m, int nparties, int which0, int which1, void* stream) {
+  if (dev)
+    return mxh_slot_place2(words, x0, x1, out0, out1, m, nparties, which0, which1, stream);
+  DISPATCH_WORDS(words, T, {
+    const T* X[2] = {(const T*)x0, (const T*)x1};
+    T* O[2] = {(T*)out0, (T*)out1};
+    const int W[2] = {which0, which1};
+    for (int y = 0; y < 2; ++y)
+      for (int q = 0; q < nparties; ++q) {
+        if (q == W[y])
+          std::memcpy(O[y] + q * m, X[y], sizeof(T) * m);
+        else
+          std::memset((void*)(O[y] + q * m), 0, sizeof(T) * m);
+      }
+    return 0;
+  });
+}
+
 int mx_ew_compare(int dev, int op, int words, const void* a, int64_t na, const void* b,
                   int64_t nb, uint8_t* out, int64_t n, void* stream) {
   if (dev) return mxh_ew_compare(op, words, a, na, b, nb, out, n, stream);

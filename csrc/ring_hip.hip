@@ -111,6 +111,21 @@ __global__ void __launch_bounds__(256) k_binary_slot2(int op, Pair<T> p, int64_t
   }
 }
 
+// trivial sharings in the stacked layout: out_y[q, i] = q == which[y] ? a[y][i] : 0
+template <class T>
+__global__ void __launch_bounds__(256) k_slot_place2(Pair<T> p, int64_t m, int np) {
+  const int y = blockIdx.y;
+  const T* __restrict__ a = p.a[y];
+  T* __restrict__ out = p.o[y];
+  const int which = p.which[y];
+  const int64_t n = m * np;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < n;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t q = g / m, i = g - q * m;
+    out[g] = q == which ? a[i] : (T)0;
+  }
+}
+
 template <class T>
 __global__ void __launch_bounds__(256) k_add_zs3(const T* __restrict__ v, const T* __restrict__ r,
                                                  T* __restrict__ out0, T* __restrict__ out1,
@@ -710,6 +725,19 @@ int mxh_ew_binary_slot2(int op, int words, const void* a0, const void* a1, const
               {which0, which1}};
     hipLaunchKernelGGL(k_binary_slot2<T>, dim3(grid_for(m * nparties), 2), dim3(kBlock), 0,
                        S(stream), op, p, nb, m, nparties);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mxh_slot_place2(int words, const void* x0, const void* x1, void* out0, void* out1,
+                    int64_t m, int nparties, int which0, int which1, void* stream) {
+  if (m == 0) return 0;
+  DEV_DISPATCH(words, T, {
+    Pair<T> p{{(const T*)x0, (const T*)x1}, {nullptr, nullptr}, {(T*)out0, (T*)out1},
+              {which0, which1}};
+    hipLaunchKernelGGL(k_slot_place2<T>, dim3(grid_for(m * nparties), 2), dim3(kBlock), 0,
+                       S(stream), p, m, nparties);
     MX_LAUNCH_CHECK();
     return 0;
   });

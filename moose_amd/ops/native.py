@@ -32,6 +32,8 @@ _SIGS = {
     "mx_ew_unary2": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp]),
     "mx_ew_binary_slot2": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
                                    c_i64, c_int, c_int, c_int, c_vp]),
+    "mx_slot_place2": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int,
+                               c_vp]),
     "mx_ew_compare": (c_int, [c_int, c_int, c_int, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "mx_bit_extract": (c_int, [c_int, c_int, c_vp, c_vp, c_i64, c_int, c_vp]),
     "mx_ring_inject": (c_int, [c_int, c_int, c_vp, c_vp, c_i64, c_int, c_vp]),
@@ -180,14 +182,22 @@ def dev_of(t: torch.Tensor) -> int:
     return 1 if t.is_cuda else 0
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_of(t: torch.Tensor):
+    """The current HIP stream of t's device as a raw handle (None on the host).  This is
+    on every launch's path, so it skips torch.cuda.current_stream's Stream object."""
     if t.is_cuda:
-        return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+        if _raw_stream is not None:
+            return _raw_stream(t.get_device())
+        return torch.cuda.current_stream(t.device).cuda_stream
     return None
 
 
 def ptr(t):
-    return None if t is None else ctypes.c_void_p(t.data_ptr())
+    # plain ints: the c_void_p argtypes convert them (no ctypes object per operand)
+    return None if t is None else t.data_ptr()
 
 
 def key_buffer(keys) -> ctypes.Array:

@@ -57,17 +57,21 @@ def _words(bits):
 class RT:
     """A ring tensor (see module docstring)."""
 
-    __slots__ = ("data", "bits")
+    __slots__ = ("data", "bits", "_shape")
 
     def __init__(self, data: torch.Tensor, bits: int):
         self.data = data
         self.bits = bits
+        self._shape = None
 
     # -- shape -------------------------------------------------------------
     @property
     def shape(self):
-        s = tuple(self.data.shape)
-        return s[:-1] if self.bits == 128 else s
+        s = self._shape
+        if s is None:  # computed once: shapes are read several times per launch
+            s = tuple(self.data.shape)
+            s = self._shape = s[:-1] if self.bits == 128 else s
+        return s
 
     @property
     def ndim(self):
@@ -134,6 +138,13 @@ def empty(shape, bits, device) -> RT:
     if bits == 64:
         return RT(torch.empty(shape, dtype=torch.int64, device=device), 64)
     return RT(torch.empty(shape, dtype=torch.uint8, device=device), 1)
+
+
+def empty2(shape, bits, device):
+    """Two ring tensors of one shape from ONE allocation (the paired outputs of the share-
+    pair / stacked-protocol kernels)."""
+    both = empty((2,) + tuple(shape), bits, device).data
+    return RT(both[0], bits), RT(both[1], bits)
 
 
 def zeros(shape, bits, device) -> RT:
@@ -316,7 +327,7 @@ def binary2(op: str, a0: RT, b0: RT, a1: RT, b1: RT):
         return binary(op, a0, b0), binary(op, a1, b1)
     n = max(na, nb_)
     shp = a0.shape if na >= nb_ else b0.shape
-    o0, o1 = empty(shp, bits, a0.device), empty(shp, bits, a0.device)
+    o0, o1 = empty2(shp, bits, a0.device)
     d = [t.data.contiguous() for t in (a0, b0, a1, b1)]
     nat.check(nat.lib().mx_ew_binary2(
         nat.dev_of(d[0]), _BIN[op], _words(bits), nat.ptr(d[0]), nat.ptr(d[1]),
@@ -329,7 +340,7 @@ def unary2(op: str, a0: RT, a1: RT, k: int = 0):
     """(op a0, op a1) in one launch (mx_ew_unary2)."""
     if a0.bits == 1 or a1.bits != a0.bits or a1.shape != a0.shape:
         return unary(op, a0, k), unary(op, a1, k)
-    o0, o1 = empty(a0.shape, a0.bits, a0.device), empty(a0.shape, a0.bits, a0.device)
+    o0, o1 = empty2(a0.shape, a0.bits, a0.device)
     d0, d1 = a0.data.contiguous(), a1.data.contiguous()
     nat.check(nat.lib().mx_ew_unary2(
         nat.dev_of(d0), _UN[op], _words(a0.bits), nat.ptr(d0), nat.ptr(o0.data), nat.ptr(d1),
@@ -901,7 +912,7 @@ def rss_mul3_k(kind: str, x0: RT, x1: RT, y0: RT, y1: RT, slot_ptr: int, nonce: 
     # x1/y0/y1 may be None: y0 None -> out = x0 + zero share (then reshared)
     ops = [None if p is None else (p if p.shape == shp else expand(p, shp)) for p in (x0, x1, y0, y1)]
     n = math.prod(shp) // 3
-    out0, out1 = empty(shp, bits, x0.device), empty(shp, bits, x0.device)
+    out0, out1 = empty2(shp, bits, x0.device)
     if x0.data.is_cuda and any(o is not None and not o.data.is_contiguous() for o in ops):
         views = [(n, n) if o is None else _party_view(o) for o in ops]
         if all(v is not None for v in views):  # slices / row broadcasts read in place
@@ -969,11 +980,25 @@ def binary_slot2(op: str, a0: RT, a1: RT, b: RT, which0: int, which1: int):
     d0, d1, bd = a0.data.contiguous(), a1.data.contiguous(), b.data.contiguous()
     if bd.device != d0.device:
         bd = bd.to(d0.device)
-    o0, o1 = empty(a0.shape, a0.bits, a0.device), empty(a0.shape, a0.bits, a0.device)
+    o0, o1 = empty2(a0.shape, a0.bits, a0.device)
     nat.check(nat.lib().mx_ew_binary_slot2(
         nat.dev_of(d0), _BIN[op], _words(a0.bits), nat.ptr(d0), nat.ptr(d1), nat.ptr(bd), nb,
         nat.ptr(o0.data), nat.ptr(o1.data), m, np_, int(which0), int(which1),
         nat.stream_of(d0)), "binary_slot (pair)")
+    return o0, o1
+
+
+def slot_place2(x0: RT, x1: RT, which0: int, which1: int, nparties: int = 3):
+    """Two trivial stacked sharings [nparties, *x.shape] in one launch: slot which0 of the
+    first = x0, slot which1 of the second = x1, zeros elsewhere (mx_slot_place2)."""
+    bits = x0.bits
+    shp = (nparties,) + tuple(x0.shape)
+    o0, o1 = empty2(shp, bits, x0.device)
+    d0, d1 = x0.data.contiguous(), x1.data.contiguous()
+    nat.check(nat.lib().mx_slot_place2(
+        nat.dev_of(d0), _words(bits), nat.ptr(d0), nat.ptr(d1), nat.ptr(o0.data),
+        nat.ptr(o1.data), x0.numel(), nparties, int(which0), int(which1), nat.stream_of(d0)),
+        "slot_place2")
     return o0, o1
 
 
@@ -1004,7 +1029,9 @@ def ks_level3_k(g0: RT, g1: RT, p0: RT, p1: RT, d: int, both: bool, slot_ptr: in
     shp = g0.shape
     datas = [x.data.contiguous() for x in (g0, g1, p0, p1)]
     n = math.prod(shp) // 3
-    outs = [empty(shp, bits, g0.device) for _ in range(4 if both else 2)]
+    nout = 4 if both else 2
+    blk = empty((nout,) + tuple(shp), bits, g0.device).data
+    outs = [RT(blk[i], bits) for i in range(nout)]
     dummy = outs[0].data
     nat.check(
         nat.lib().mx_ks_level3_k(

@@ -150,6 +150,11 @@ def from_slot_holders(sess, plc, slot: int, x_h0: HV, x_h1: HV, like: PV,
     No communication (e.g. x_2 of an arithmetic sharing in bit decomposition).  ``like``
     is any party vector of the same shape (each party takes its zeros' shape from it)."""
     bits = x_h0.v.bits if hasattr(x_h0.v, "bits") else None
+    fused = getattr(sess, "p_from_slot_holders", None)
+    if fused is not None:
+        r = fused(plc, slot, x_h0, x_h1, like)
+        if r is not None:
+            return RepTensor(plc, bits, kind, r[0], r[1])
     o = plc.owners
     h0, h1 = slot, (slot - 1) % 3
     comps0, comps1 = [], []

@@ -277,6 +277,19 @@ class StackedSession(Session):
         o0, o1 = R.binary2(op, v0, w[0], v1, w[1])
         return PV(plc, o0), PV(plc, o1)
 
+    def p_from_slot_holders(self, plc, slot, x_h0, x_h1, like):
+        """rep.from_slot_holders in one kernel (None -> generic path)."""
+        v0, v1 = x_h0.v, x_h1.v
+        if not (isinstance(v0, R.RT) and isinstance(v1, R.RT)) or v0.bits not in (64, 128) \
+                or v1.shape != v0.shape or tuple(v0.shape) != tuple(like.v.shape[1:]):
+            return None
+        o = plc.owners
+        h0, h1 = slot, (slot - 1) % 3
+        if x_h0.host != o[h0] or x_h1.host != o[h1]:
+            return None
+        a, b = R.slot_place2(v0, v1, h0, h1)
+        return PV(plc, a), PV(plc, b)
+
     def p_apply_at2(self, prim, plc, x0, x1, which0, which1, c):
         """p_apply_at on both share vectors in one kernel (None if not applicable)."""
         op = self._PAIR_BIN.get(prim)
@@ -423,7 +436,7 @@ class StackedSession(Session):
         s0 = x.s0.v.data.contiguous()
         n = x.s0.v.numel() // 3
         nn = (ctypes.c_uint64 * 6)(*[v & ((1 << 64) - 1) for v in nonces])
-        keys = (ctypes.c_void_p(self.key_ptr(x.plc, 0)), ctypes.c_void_p(self.key_ptr(x.plc, 2)))
+        keys = (self.key_ptr(x.plc, 0), self.key_ptr(x.plc, 2))
         if out is not None:
             out0, out1 = out[0].v.data, out[1].v.data
             w = 2 if x.bits == 128 else 1  # int64 words per element
@@ -438,7 +451,8 @@ class StackedSession(Session):
                 *keys, nn, os_, nat.stream_of(s0)), "trunc_pr3 (views)")
             self._trunc_traffic(x, out0[0].numel() * out0.element_size())
             return out[0], out[1]
-        out0, out1 = torch.empty_like(s0), torch.empty_like(s0)
+        both = torch.empty((2,) + tuple(s0.shape), dtype=s0.dtype, device=s0.device)
+        out0, out1 = both[0], both[1]
         nat.check(
             nat.lib().mx_trunc_pr3_k(
                 nat.dev_of(s0), R._words(x.bits), nat.ptr(s0), nat.ptr(out0), nat.ptr(out1), n, m,
@@ -452,11 +466,10 @@ class StackedSession(Session):
     def _trunc_traffic(self, x, nbytes):
         o = x.plc.owners
         # messages of the protocol: dealer -> P1 (2 tensors), P0 <-> P1 (two rounds)
-        for src, dst, k in ((o[2], o[1], 2), (o[0], o[1], 2), (o[1], o[0], 2)):
-            for _ in range(k):
-                self.stats.record_send(src, dst, nbytes)
-        self.stats.record_round(2 * nbytes)
-        self.stats.record_round(2 * nbytes)
+        st = self.stats
+        for src, dst in ((o[2], o[1]), (o[0], o[1]), (o[1], o[0])):
+            st.record_send(src, dst, nbytes, count=2)
+        st.record_round(2 * nbytes, count=2)
 
     def fused_share(self, plc, x: HV, j, kind, n1, na):
         import ctypes

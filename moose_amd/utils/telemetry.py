@@ -18,6 +18,7 @@ import threading
 import time
 from collections import defaultdict
 from contextlib import contextmanager
+from contextlib import nullcontext
 
 _LOG = logging.getLogger("moose_amd")
 if os.environ.get("MOOSEX_LOG"):
@@ -36,13 +37,13 @@ class SessionStats:
         self.round_bytes = 0
         self.elapsed = {}
 
-    def record_send(self, src, dst, nbytes):
-        self.bytes[(src, dst)] += int(nbytes)
-        self.messages[(src, dst)] += 1
+    def record_send(self, src, dst, nbytes, count=1):
+        self.bytes[(src, dst)] += int(nbytes) * count
+        self.messages[(src, dst)] += count
 
-    def record_round(self, nbytes):
-        self.rounds += 1
-        self.round_bytes += int(nbytes)
+    def record_round(self, nbytes, count=1):
+        self.rounds += count
+        self.round_bytes += int(nbytes) * count
 
     def as_dict(self):
         return {
@@ -70,10 +71,22 @@ def _nvtx():
     return None
 
 
-@contextmanager
+_ROCTX = os.environ.get("MOOSEX_ROCTX")
+_NULL_SPAN = nullcontext()
+
+
 def span(name, **args):
-    """Record a named interval (Chrome trace + roctx range when on GPU)."""
-    nv = _nvtx() if _TRACE_PATH or os.environ.get("MOOSEX_ROCTX") else None
+    """Record a named interval (Chrome trace + roctx range when on GPU).  A shared no-op
+    context when neither tracing nor roctx ranges are on (spans sit on every protocol
+    call)."""
+    if not _TRACE_PATH and not _ROCTX:
+        return _NULL_SPAN
+    return _span(name, **args)
+
+
+@contextmanager
+def _span(name, **args):
+    nv = _nvtx()
     if nv is not None:
         nv.range_push(name)
     t0 = time.perf_counter_ns()

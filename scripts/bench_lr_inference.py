@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--device", default=None)
     ap.add_argument("--ring", type=int, default=128, choices=(64, 128))
     ap.add_argument("--graphs", action="store_true", help="replay captured hipGraphs")
+    ap.add_argument("--cprofile", default=None, help="write a host-side cProfile summary")
     a = ap.parse_args()
     import torch
     from sklearn.datasets import make_classification
@@ -59,10 +60,27 @@ def main():
     for _ in range(a.warmup):
         out = rt.evaluate_computation(comp, args)
     lat = []
+    prof = None
+    if a.cprofile:
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
     for _ in range(a.runs):
         t0 = time.perf_counter()
         out = rt.evaluate_computation(comp, args)
         lat.append(time.perf_counter() - t0)
+    if prof is not None:
+        import io
+        import pstats
+
+        prof.disable()
+        buf = io.StringIO()
+        st = pstats.Stats(prof, stream=buf)
+        st.sort_stats("tottime").print_stats(45)
+        st.sort_stats("cumulative").print_stats(60)
+        with open(a.cprofile, "w") as f:
+            f.write(buf.getvalue())
     pred = np.asarray(list(out.values())[0])
     err = float(np.abs(pred - lg.predict_proba(X_test)).max())
     lat = np.sort(np.asarray(lat)) * 1e3

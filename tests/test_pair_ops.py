@@ -72,3 +72,13 @@ def test_trunc_into_row_views(dev, bits):
     _eq(R.RT(big1[:, 2:4].contiguous(), bits), d1.v)
     # rows outside the view are untouched
     assert not big0[:, :2].any() and not big0[:, 4:].any()
+
+
+@pytest.mark.parametrize("dev", DEVICES)
+@pytest.mark.parametrize("bits", [64, 128])
+def test_slot_place2(dev, bits):
+    x0, x1 = _rand((4, 3), bits, dev, 6), _rand((4, 3), bits, dev, 7)
+    o0, o1 = R.slot_place2(x0, x1, 2, 1)
+    z = np.zeros((4, 3), dtype=object)
+    np.testing.assert_array_equal(R.to_ints(o0), np.stack([z, z, R.to_ints(x0)]))
+    np.testing.assert_array_equal(R.to_ints(o1), np.stack([z, R.to_ints(x1), z]))
