@@ -156,6 +156,19 @@ def zeros(shape, bits, device) -> RT:
 _SCALARS = {}
 
 
+def _cache_put(cache, key, t, limit):
+    """Insert a freshly made device constant into a shared cache.  While dataflow lanes
+    run (runtime/lanes.py) other streams may read it next, so the producing stream is
+    drained first (once per constant)."""
+    if len(cache) >= limit:
+        return
+    from moose_amd.runtime import lanes
+
+    if lanes.ACTIVE and t.data.is_cuda:
+        torch.cuda.current_stream(t.data.device).synchronize()
+    cache[key] = t
+
+
 def fill(shape, value: int, bits, device) -> RT:
     """Constant ring tensor (``value`` taken mod 2^bits).
 
@@ -171,8 +184,7 @@ def fill(shape, value: int, bits, device) -> RT:
             return hit
         t = _fill(shape, value, bits, device)
         if torch.device(device).type == "cpu" or not torch.cuda.is_current_stream_capturing():
-            if len(_SCALARS) < 65536:
-                _SCALARS[key] = t
+            _cache_put(_SCALARS, key, t, 65536)
         return t
     return _fill(shape, value, bits, device)
 
@@ -824,8 +836,7 @@ def weighted_sum(a: RT, weights, nb=0) -> RT:
     if w is None:
         w = from_ints(np.array([int(v) for v in weights], dtype=object), bits, a.device)
         if a.device.type == "cpu" or not torch.cuda.is_current_stream_capturing():
-            if len(_WEIGHTS) < 4096:
-                _WEIGHTS[key] = w
+            _cache_put(_WEIGHTS, key, w, 4096)
     shp = a.shape
     k = shp[nb]
     outer = math.prod(shp[:nb])

@@ -110,7 +110,8 @@ def capturable(comp) -> bool:
 class GraphPlan:
     """One captured evaluation (see module docstring)."""
 
-    def __init__(self, comp, arguments: dict, device, storage, fixedpoint_ring, seed=None):
+    def __init__(self, comp, arguments: dict, device, storage, fixedpoint_ring, seed=None,
+                 lanes=None):
         self.comp = comp
         self.device = torch.device(device)
         self.ring = fixedpoint_ring
@@ -128,7 +129,7 @@ class GraphPlan:
         # 1. warm-up (eager): first result + recorded uploads
         rec = _Recorder()
         sess = StackedSession(self.device, seed=seed)
-        interp = Interpreter(sess, storage, fixedpoint_ring)
+        interp = Interpreter(sess, storage, fixedpoint_ring, lanes=lanes)
         with _upload_hook(rec):
             outs = interp.run(comp, self.static)
             self.first = self._decode(interp, outs)
@@ -140,7 +141,7 @@ class GraphPlan:
         self.keys.frozen = True
         self.sess = StackedSession(self.device, seed=seed)
         self.sess.use_keytable(self.keys)
-        self.interp = Interpreter(self.sess, storage, fixedpoint_ring)
+        self.interp = Interpreter(self.sess, storage, fixedpoint_ring, lanes=lanes)
         stager = _Stager(rec.items, self.device)
         torch.cuda.synchronize(self.device)
         # The evaluation is captured as a chain of graphs of SEGMENT_OPS logical ops each
@@ -151,12 +152,18 @@ class GraphPlan:
         stream = torch.cuda.Stream(self.device)
         state = {"g": None, "n": 0}
 
+        lanes = self.interp.lanes
+
         def begin():
             g = torch.cuda.CUDAGraph()
             g.capture_begin(pool=pool)
             state["g"], state["n"] = g, 0
+            if lanes is not None:  # the lanes join this segment's capture
+                lanes.fork()
 
         def end():
+            if lanes is not None:  # ... and are joined back before it ends
+                lanes.join()
             state["g"].capture_end()
             self.graphs.append(state["g"])
 
@@ -172,6 +179,14 @@ class GraphPlan:
         with _upload_hook(stager), torch.cuda.stream(stream):
             try:
                 self.outs = self.interp.run(comp, self.static)
+            except BaseException:
+                if os.environ.get("MOOSEX_GRAPHS_DEBUG") == "1":
+                    import sys
+                    import traceback
+
+                    traceback.print_exc(file=sys.stderr)
+                    sys.stderr.flush()
+                raise
             finally:
                 if state["g"] is not None:
                     end()
@@ -217,7 +232,7 @@ class GraphCache:
         self.plans = {}
         self.failed = set()
 
-    def evaluate(self, comp, arguments, device, storage, ring, seed=None):
+    def evaluate(self, comp, arguments, device, storage, ring, seed=None, lanes=None):
         key = (id(comp), signature(arguments))
         plan = self.plans.get(key)
         if plan is not None and plan.comp is comp:
@@ -225,7 +240,7 @@ class GraphCache:
         if key in self.failed or not capturable(comp):
             return None
         try:
-            plan = GraphPlan(comp, arguments, device, storage, ring, seed)
+            plan = GraphPlan(comp, arguments, device, storage, ring, seed, lanes=lanes)
         except Exception as e:  # noqa: BLE001 - any capture failure means "run eagerly"
             import traceback
 

@@ -35,6 +35,7 @@ from moose_amd.ops import ring as R
 from moose_amd.protocols import fixedpoint as fxp
 from moose_amd.protocols import replicated as rep
 from moose_amd.protocols.fixedpoint import RepFixed
+from moose_amd.runtime import lanes as _lanes
 from moose_amd.runtime import shares
 from moose_amd.runtime.session import HV
 from moose_amd.runtime.values import LV
@@ -99,13 +100,19 @@ def numpy_to_torch(a, device):
 
 
 class Interpreter:
-    def __init__(self, sess, storage=None, fixedpoint_ring: int = None):
+    def __init__(self, sess, storage=None, fixedpoint_ring: int = None, lanes: int = None):
         self.sess = sess
         self.storage = storage if storage is not None else {}
         self.env: Dict[str, LV] = {}
         self.fixed_ring = fixedpoint_ring  # override Fixed128 -> Fixed64 if 64
         self.outputs = {}
         self.on_op = None
+        # independent operations on separate HIP streams (runtime/lanes.py)
+        self.lanes = None
+        dev = getattr(sess, "device", None)
+        n = lanes if lanes is not None else _lanes.default_lanes()
+        if n > 1 and dev is not None and dev.type == "cuda" and getattr(sess, "me", None) is None:
+            self.lanes = _lanes.LaneRunner(dev, n)
 
     # ------------------------------------------------------------------------
     # driver
@@ -118,30 +125,47 @@ class Interpreter:
         batch = getattr(self.sess, "batch_dots", False) and os.environ.get(
             "MOOSEX_BATCH_DOTS", "1") != "0"
         ops = comp.operations
-        for idx, op in enumerate(ops):
-            if op.name in self.env:  # computed ahead as part of a batch
-                continue
-            table = self._table_handler(op)
-            if (table is None and batch and op.kind == "Dot"
-                    and self._batch_dots(op, ops[idx + 1:])):
-                continue
-            handler = table or getattr(self, f"op_{op.kind}", None) or self._dialect_handler(op)
-            if handler is None:
-                raise MooseRuntimeError(f"operator {op.kind} is not supported by the interpreter")
-            ins = [self.env[n] for n in op.inputs]
-            if self.on_op is not None:  # e.g. graph capture segmentation (graphs.py)
-                self.on_op()
-            with span(f"op.{op.kind}", op=op.name):
+        lanes = self.lanes
+        if lanes is not None:
+            lanes.start(ops)
+        try:
+            for idx, op in enumerate(ops):
+                if op.name in self.env:  # computed ahead as part of a batch
+                    continue
+                if self.on_op is not None:  # e.g. graph capture segmentation (graphs.py)
+                    self.on_op()
+                if lanes is not None:
+                    lanes.enter(op, self.env)
+                    before = len(self.env)
                 try:
-                    if me is not None and me not in _owners(op.placement):
-                        self.env[op.name] = self._foreign_op(op, ins, me)
-                    else:
-                        self.env[op.name] = handler(op, ins)
-                except MooseRuntimeError:
-                    raise
-                except Exception as e:  # annotate with the failing op
-                    raise MooseRuntimeError(f"{op.name} = {op.kind} failed: {e}") from e
+                    self._run_op(op, ops, idx, batch, me)
+                finally:
+                    if lanes is not None:
+                        lanes.leave([n for n in list(self.env)[before:]])
+        finally:
+            if lanes is not None:
+                lanes.finish()
         return self.outputs
+
+    def _run_op(self, op, ops, idx, batch, me):
+        table = self._table_handler(op)
+        if (table is None and batch and op.kind == "Dot"
+                and self._batch_dots(op, ops[idx + 1:])):
+            return
+        handler = table or getattr(self, f"op_{op.kind}", None) or self._dialect_handler(op)
+        if handler is None:
+            raise MooseRuntimeError(f"operator {op.kind} is not supported by the interpreter")
+        ins = [self.env[n] for n in op.inputs]
+        with span(f"op.{op.kind}", op=op.name):
+            try:
+                if me is not None and me not in _owners(op.placement):
+                    self.env[op.name] = self._foreign_op(op, ins, me)
+                else:
+                    self.env[op.name] = handler(op, ins)
+            except MooseRuntimeError:
+                raise
+            except Exception as e:  # annotate with the failing op
+                raise MooseRuntimeError(f"{op.name} = {op.kind} failed: {e}") from e
 
     def _batch_dots(self, op, later, limit: int = 256) -> bool:
         """Independent-op batching (the reference runs independent operations as
@@ -189,7 +213,7 @@ class Interpreter:
             outs = fxp.dot_many(self.sess, [(x.v, y.v) for _, x, y in group],
                                 dtype.fractional_precision)
         for (o, x, _), r in zip(group, outs):
-            if self.on_op is not None:
+            if self.on_op is not None and self.lanes is None:
                 self.on_op()
             self.env[o.name] = LV(x.plc, "tensor", dtype, r)
         return True
@@ -439,7 +463,9 @@ class Interpreter:
             return hit[1]
         conv = self.at(op, x)
         if conv is not x:
-            memo[(id(x), op.placement)] = (x, conv)
+            # with lanes, the op that reuses it may run on another stream: it waits on this
+            ev = self.lanes.mark() if self.lanes is not None else None
+            memo[(id(x), op.placement)] = (x, conv, ev)
         return conv
 
     def at(self, op, x: LV) -> LV:
@@ -448,6 +474,8 @@ class Interpreter:
         if memo:
             hit = memo.pop((id(x), plc), None)
             if hit is not None and hit[0] is x:
+                if hit[2] is not None and self.lanes is not None:
+                    self.lanes.wait_mark(hit[2], hit[1])
                 return hit[1]
         if isinstance(plc, HostPlacement):
             return self.to_host(x, plc.owner)

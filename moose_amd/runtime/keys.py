@@ -56,6 +56,12 @@ def slot_words(keys) -> np.ndarray:
     return out
 
 
+def _lanes_active(device) -> bool:
+    from moose_amd.runtime import lanes
+
+    return lanes.ACTIVE and device.type == "cuda"
+
+
 class KeyTable:
     """Fixed-capacity table of key slots on ``device``.
 
@@ -78,6 +84,8 @@ class KeyTable:
         if base + n > self.capacity:
             if self.frozen:
                 raise RuntimeError("key table exhausted during graph capture")
+            if _lanes_active(self.device):  # kernels on other lanes may still read self.t
+                torch.cuda.synchronize(self.device)
             grown = torch.zeros((max(2 * self.capacity, base + n), SLOT_WORDS),
                                 dtype=torch.int32, device=self.device)
             grown[:self.capacity].copy_(self.t)
@@ -90,6 +98,8 @@ class KeyTable:
     def _write(self, base: int, keys):
         img = torch.from_numpy(slot_words(keys).view(np.int32))
         self.t[base:base + len(keys)].copy_(img)
+        if _lanes_active(self.device):  # readers on other streams see complete keys
+            torch.cuda.current_stream(self.device).synchronize()
 
     def refresh(self, upto: int = None):
         """Fresh random keys for slots ``[0, upto)`` (default: every slot)."""

@@ -68,6 +68,7 @@ class LocalMooseRuntime:
         fixedpoint_ring: int = 128,
         seed: Optional[int] = None,
         use_graphs: Optional[bool] = None,
+        lanes: Optional[int] = None,
     ):
         identities = [getattr(i, "name", i) for i in identities]
         storage_mapping = dict(storage_mapping or {})
@@ -88,6 +89,8 @@ class LocalMooseRuntime:
         if use_graphs is None:
             use_graphs = os.environ.get("MOOSEX_GRAPHS", "0") == "1"
         self.use_graphs = use_graphs
+        # HIP streams for independent operations (runtime/lanes.py); MOOSEX_LANES=n
+        self.lanes = lanes
         from moose_amd.runtime.graphs import GraphCache
 
         self._graphs = GraphCache()
@@ -141,7 +144,7 @@ class LocalMooseRuntime:
         if self.use_graphs and self.device.type == "cuda":
             t0 = time.perf_counter()
             r = self._graphs.evaluate(comp, arguments, self.device, self.storage,
-                                      self.fixedpoint_ring, self.seed)
+                                      self.fixedpoint_ring, self.seed, lanes=self.lanes)
             if r is not None:
                 result, self.last_stats = r
                 torch.cuda.synchronize(self.device)
@@ -149,7 +152,7 @@ class LocalMooseRuntime:
                 self.last_timings = {i: elapsed for i in self.identities}
                 return result
         sess = StackedSession(self.device, seed=self.seed)
-        interp = Interpreter(sess, self.storage, self.fixedpoint_ring)
+        interp = Interpreter(sess, self.storage, self.fixedpoint_ring, lanes=self.lanes)
         t0 = time.perf_counter()
         outs = interp.run(comp, arguments)
         result = {}

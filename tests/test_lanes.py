@@ -1,0 +1,77 @@
+"""Intra-party dataflow lanes (runtime/lanes.py): the static chain plan on the host, and on
+the GPU bitwise-identical results with 1 and 4 lanes -- eagerly and under hipGraph capture
+-- for a computation with independent branches (reference: independent operations run as
+concurrent tasks, execution/asynchronous.rs:456-530)."""
+import numpy as np
+import pytest
+
+import moose_amd as pm
+from moose_amd.ir.computation import Computation
+from moose_amd.runtime.lanes import LanePlan
+
+
+def test_plan_chains_follow_dependencies():
+    src = """a = Constant{value = HostFloat64Tensor([1.0])}: () -> HostFloat64Tensor () @Host(alice)
+b = Constant{value = HostFloat64Tensor([2.0])}: () -> HostFloat64Tensor () @Host(alice)
+c = Add: (HostFloat64Tensor, HostFloat64Tensor) -> HostFloat64Tensor (a, a) @Host(alice)
+d = Add: (HostFloat64Tensor, HostFloat64Tensor) -> HostFloat64Tensor (b, b) @Host(alice)
+e = Add: (HostFloat64Tensor, HostFloat64Tensor) -> HostFloat64Tensor (c, d) @Host(alice)
+"""
+    ops = Computation.from_textual(src).toposorted().operations
+    plan = LanePlan(ops, 4)
+    ln = plan.lane
+    assert ln["a"] != ln["b"]  # independent roots start separate chains
+    assert ln["c"] == ln["a"] and ln["d"] == ln["b"]  # each chain extends its tail
+    assert ln["e"] in (ln["c"], ln["d"])  # the join continues one of them
+    # exactly the value coming from the other chain needs an event
+    other = "d" if ln["e"] == ln["c"] else "c"
+    assert plan.crosses(other, ln[other]) and not plan.crosses("a", ln["a"])
+    assert plan.width() == 2
+    assert set(LanePlan(ops, 1).lane.values()) == {0}
+
+
+def _wide_comp(branches=4, n=64, k=10):
+    alice, bob, carole = (pm.host_placement(x) for x in ("alice", "bob", "carole"))
+    rep = pm.replicated_placement("rep", players=[alice, bob, carole])
+    fx = pm.fixed(24, 40)
+    rng = np.random.default_rng(3)
+    ws = [rng.normal(size=(k, 1)) * 0.3 for _ in range(branches)]
+
+    @pm.computation
+    def f(x: pm.Argument(placement=alice, vtype=pm.TensorType(pm.float64))):
+        with alice:
+            xf = pm.cast(x, dtype=fx)
+        wf = []
+        with bob:
+            for w in ws:
+                wf.append(pm.cast(pm.constant(w, dtype=pm.float64), dtype=fx))
+        with rep:
+            ys = [pm.sigmoid(pm.dot(xf, w)) for w in wf]
+            acc = ys[0]
+            for y in ys[1:]:
+                acc = pm.add(acc, y)
+        with carole:
+            out = pm.cast(acc, dtype=pm.float64)
+        return out
+
+    x = rng.normal(size=(n, k))
+    ref = sum(1 / (1 + np.exp(-(x @ w))) for w in ws)
+    return f, x, ref
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graphs", [False, True])
+def test_lanes_match_single_stream_bitwise(graphs):
+    f, x, ref = _wide_comp()
+    outs = {}
+    for lanes in (1, 4):
+        rt = pm.LocalMooseRuntime(["alice", "bob", "carole"], device="cuda", seed=11,
+                                  use_graphs=graphs, lanes=lanes)
+        for _ in range(3 if graphs else 1):  # graphs: warm-up, capture, replays
+            r = rt.evaluate_computation(f, {"x": x})
+        if graphs:
+            assert rt._graphs.plans, getattr(rt._graphs, "last_error", "capture failed")
+        outs[lanes] = np.asarray(list(r.values())[0])
+        np.testing.assert_allclose(outs[lanes], ref, atol=1e-4)
+    if not graphs:  # same seed, same program order of PRF draws -> identical shares
+        np.testing.assert_array_equal(outs[1], outs[4])
