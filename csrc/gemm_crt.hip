@@ -6,8 +6,8 @@
 //
 //   * every ring element x is read as its signed representative X in [-2^(w-1), 2^(w-1));
 //     the integer product Z = sum_k X_k Y_k then satisfies |Z| <= K' 2^(2w-2);
-//   * n pairwise-coprime moduli p_i <= 256 (256, 255, 253, 251, ...) with product
-//     M > |Z| / 0.45 are chosen -- 37 for Z_2^128 at K' = 8192, 18 for Z_2^64;
+//   * n pairwise-coprime moduli p_i <= 256 (256, 253, 251, 249, ...) with product
+//     M > |Z| / 0.45 are chosen -- 36 for Z_2^128 at K' = 8192, 18 for Z_2^64;
 //   * each operand is reduced to centered int8 residues (prep kernels, one udot4 per 4 bytes
 //     of the element + one fp32 rounding), and ONE int8 GEMM per modulus gives
 //     acc_i = Z mod p_i exactly in i32 (K' <= 2^15 keeps the epilogue's fp32 rounding exact);
@@ -16,7 +16,7 @@
 //     with W_i = (M/p_i) mod 2^w.  The inverse (M/p_i)^-1 is folded into A's residues, so
 //     the GEMM epilogue only reduces acc_i mod p_i (centered, stored as one byte).
 //
-// So a Z_2^128 product costs 37 int8 GEMMs instead of 136 (3.7x fewer MFMAs), Z_2^64 18
+// So a Z_2^128 product costs 36 int8 GEMMs instead of 136 (3.8x fewer MFMAs), Z_2^64 18
 // instead of 36, at the price of wider operand prep and one reconstruction pass.  (The same
 // idea as the Ozaki-II / multi-modular emulation of high-precision GEMM on integer matrix
 // units; here the target is modular rather than floating-point arithmetic.)
@@ -52,10 +52,15 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 
 constexpr int kMaxMod = 48;
 // pairwise coprime, descending: 2^8, 3*5*17, 11*23, 13*19, primes, 7*31, primes
-constexpr int kModuli[kMaxMod] = {256, 255, 253, 251, 247, 241, 239, 233, 229, 227, 223, 217,
-                                  211, 199, 197, 193, 191, 181, 179, 173, 167, 163, 157, 151,
-                                  149, 139, 137, 131, 127, 113, 109, 107, 103, 101, 97,  89,
-                                  83,  79,  73,  71,  67,  61,  59,  53,  47,  43,  41,  37};
+// Pairwise coprime, in the order they are used (a call takes the shortest prefix whose
+// product is large enough).  The first 36 are the product-maximising set of 36 coprime
+// integers <= 256 (exhaustive branch-and-bound over 61..256): 268.2 bits, just enough for an
+// exact Z_2^128 product at K' = 8192 (268.15 bits), where the greedy descending set
+// (256, 255, 253, ...) needs 37.  Their first 18 also cover Z_2^64 at K' = 8192.
+constexpr int kModuli[kMaxMod] = {256, 253, 251, 249, 247, 241, 239, 235, 233, 229, 227, 223,
+                                  217, 211, 199, 197, 193, 191, 181, 179, 173, 167, 163, 157,
+                                  151, 149, 139, 137, 131, 127, 113, 109, 107, 103, 101, 97,
+                                  89,  79,  73,  71,  67,  61,  59,  53,  43,  41,  37,  17};
 
 constexpr int BM = 256;          // block tile rows (A side); the cols BN are 256 or 128
 constexpr int BK = 64;           // k bytes per stage
