@@ -217,6 +217,32 @@ class Transport:
         self.messages += 1
         return out
 
+    def exchange(self, sends, recvs):
+        """One grouped round of header-free point-to-point messages: ``sends`` is a list of
+        (tensor, dst), ``recvs`` a list of (preallocated tensor, src) whose shapes both
+        sides know (protocol messages of a known element count)."""
+        ops, staged = [], []
+        for t, dst in sends:
+            t = t.contiguous()
+            if t.numel() == 0:
+                continue
+            ops.append(dist.P2POp(dist.isend, t.cpu() if self.stage else t, dst,
+                                  group=self.group))
+            self.bytes_sent += t.numel() * t.element_size()
+            self.messages += 1
+        for out, src in recvs:
+            if out.numel() == 0:
+                continue
+            buf = torch.empty(out.shape, dtype=out.dtype) if self.stage else out
+            if self.stage or not out.is_contiguous():
+                staged.append((out, buf))
+            ops.append(dist.P2POp(dist.irecv, buf, src, group=self.group))
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        for out, buf in staged:
+            out.copy_(buf)
+
     def broadcast_from(self, v, src: int, dsts: List[int], me: int):
         """``src`` sends ``v`` to every rank in ``dsts``; returns the value at ``me``."""
         if me == src:

@@ -83,7 +83,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _shares_worker(rank, port, q):
+def _shares_worker(rank, port, q, device="cpu"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=3)
     from moose_amd.parallel.spmd import SPMDSession
@@ -92,19 +92,20 @@ def _shares_worker(rank, port, q):
     from moose_amd.runtime.session import HV
 
     plc = ReplicatedPlacement(("a", "b", "c"))
-    s = SPMDSession(plc.owners[rank], {"a": 0, "b": 1, "c": 2}, Transport(rank, 3, "cpu"),
-                    seed=9)
+    s = SPMDSession(plc.owners[rank], {"a": 0, "b": 1, "c": 2}, Transport(rank, 3, device),
+                    device=device, seed=9)
     out = {}
     for bits in (64, 128):
         enc = R.encode(torch.linspace(-20, 20, 257, dtype=torch.float64), 23, bits)
+        enc = R.RT(enc.data.to(device), bits)
         x = HV("b", enc if rank == 1 else _remote(bits))
         X = rep.share(s, plc, x)
         Y = rep.trunc_pr(s, rep.mul(s, X, X), 23)
         D = rep.dot(s, rep.local(s, X, "Reshape", shape=(1, 257)),
                     rep.local(s, X, "Reshape", shape=(257, 1)))
         B = rep.bit_decompose(s, X)  # per-party fused Kogge-Stone levels (SPMD p_ks_level)
-        out[bits] = ([t.s0.v.data.clone() for t in (X, Y, D, B)]
-                     + [t.s1.v.data.clone() for t in (X, Y, D, B)])
+        out[bits] = ([t.s0.v.data.cpu().clone() for t in (X, Y, D, B)]
+                     + [t.s1.v.data.cpu().clone() for t in (X, Y, D, B)])
     q.put((rank, {b: [t.numpy() for t in v] for b, v in out.items()}))
     dist.barrier()
     dist.destroy_process_group()
@@ -116,7 +117,11 @@ def _remote(bits):
     return Remote(bits)
 
 
-def test_spmd_shares_bitwise_equal_stacked():
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_spmd_shares_bitwise_equal_stacked(device):
+    """One process per party (gloo; on the GPU all three share the test device and stage
+    messages through the host): shares after Share / TruncPr (per-party kernels) / Dot /
+    BitDecompose equal the stacked generic protocol bit for bit."""
     from moose_amd.protocols import replicated as rep
     from moose_amd.runtime.session import HV
     from moose_amd.runtime.session import StackedSession
@@ -124,7 +129,7 @@ def test_spmd_shares_bitwise_equal_stacked():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_shares_worker, args=(r, port, q)) for r in range(3)]
+    ps = [ctx.Process(target=_shares_worker, args=(r, port, q, device)) for r in range(3)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=240) for _ in range(3))
