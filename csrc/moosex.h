@@ -33,7 +33,8 @@ int mx_device_count(void);
 int mx_ew_binary(int dev, int op, int words, const void* a, int64_t na, const void* b,
                  int64_t nb, void* out, int64_t n, void* stream);
 // Stacked party vectors a[nparties, m]: out[p, i] = p == which ? a[p, i] op b[i % nb]
-// : a[p, i] (a public operand applied to one party's share slot, in one pass); nb in {m, 1}
+// : a[p, i] (a public operand applied to one party's share slot, in one pass); nb divides m
+// (b repeats with period nb: scalars, full slots, trailing-axis vectors)
 int mx_ew_binary_slot(int dev, int op, int words, const void* a, const void* b, int64_t nb,
                       void* out, int64_t m, int nparties, int which, void* stream);
 // Zero share from precomputed keystreams + reshare, three stacked parties (arith):

@@ -359,7 +359,11 @@ int mx_ew_binary_slot(int dev, int op, int words, const void* a, const void* b, 
     T* O = (T*)out;
     for (int p = 0; p < nparties; ++p) {
       if (p == which) {
-        binary_t<T>(op, A + p * m, m, B, nb, O + p * m, m);
+        if (nb == 1 || nb == m) {
+          binary_t<T>(op, A + p * m, m, B, nb, O + p * m, m);
+        } else {  // b repeats with period nb (a trailing-axis public operand)
+          for (int64_t r = 0; r < m; r += nb) binary_t<T>(op, A + p * m + r, nb, B, nb, O + p * m + r, nb);
+        }
       } else if (O != A) {
         std::memcpy(O + p * m, A + p * m, sizeof(T) * m);
       }

@@ -58,7 +58,7 @@ __global__ void __launch_bounds__(256) k_binary_slot(int op, const T* __restrict
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < n;
        g += (int64_t)gridDim.x * blockDim.x) {
     const int64_t p = g / m, i = g - p * m;
-    out[g] = p == which ? mxr::binop<T>(op, a[g], b[nb == 1 ? 0 : i]) : a[g];
+    out[g] = p == which ? mxr::binop<T>(op, a[g], b[nb == 1 ? 0 : i % nb]) : a[g];
   }
 }
 
@@ -107,7 +107,7 @@ __global__ void __launch_bounds__(256) k_binary_slot2(int op, Pair<T> p, int64_t
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < n;
        g += (int64_t)gridDim.x * blockDim.x) {
     const int64_t q = g / m, i = g - q * m;
-    out[g] = q == which ? mxr::binop<T>(op, a[g], b[nb == 1 ? 0 : i]) : a[g];
+    out[g] = q == which ? mxr::binop<T>(op, a[g], b[nb == 1 ? 0 : i % nb]) : a[g];
   }
 }
 

@@ -958,13 +958,26 @@ def add_zs3(v: RT, r: RT):
     return o0, o1
 
 
+def _slot_operand_ok(a: RT, b: RT) -> bool:
+    """b broadcasts over one slot of stacked a as a period: a scalar, or b's shape (leading
+    1s dropped) is a suffix of the slot's shape."""
+    if b.numel() == 1:
+        return True
+    bs = list(b.shape)
+    while bs and bs[0] == 1:
+        bs.pop(0)
+    ss = list(a.shape[1:])
+    return len(bs) <= len(ss) and ss[len(ss) - len(bs):] == bs
+
+
 def binary_slot(op: str, a: RT, b: RT, which: int):
     """Stacked [nparties, *shape] ``a``: ``op`` with public ``b`` (same shape as one slot,
     or a scalar) applied to slot ``which`` only, one kernel (mx_ew_binary_slot)."""
     np_, m = a.shape[0], math.prod(a.shape[1:])
     nb = b.numel()
-    if nb not in (1, m):
-        raise ValueError("binary_slot: operand must be a scalar or one slot's shape")
+    if not _slot_operand_ok(a, b):
+        raise ValueError("binary_slot: operand must be a scalar, one slot's shape or a "
+                         "trailing-axes suffix of it")
     ad = a.data.contiguous()
     bd = b.data.contiguous()
     if bd.device != ad.device:
@@ -986,8 +999,9 @@ def binary_slot2(op: str, a0: RT, a1: RT, b: RT, which0: int, which1: int):
         return binary_slot(op, a0, b, which0), binary_slot(op, a1, b, which1)
     np_, m = a0.shape[0], math.prod(a0.shape[1:])
     nb = b.numel()
-    if nb not in (1, m):
-        raise ValueError("binary_slot2: operand must be a scalar or one slot's shape")
+    if not _slot_operand_ok(a0, b):
+        raise ValueError("binary_slot2: operand must be a scalar, one slot's shape or a "
+                         "trailing-axes suffix of it")
     d0, d1, bd = a0.data.contiguous(), a1.data.contiguous(), b.data.contiguous()
     if bd.device != d0.device:
         bd = bd.to(d0.device)

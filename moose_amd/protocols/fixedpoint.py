@@ -509,11 +509,17 @@ def _exp2_parts(sess, a: RepFixed, negative: bool):
     f, bits, integ = a.frac, a.bits, a.integ
     # every integer bit of a must be inspected (a < 2^(integ+1) after the log2(e) scale)
     nint = max(1, min(bits - 2 - f, integ + 1))
+    # the product tree below runs over a power-of-two number of factors: extra factors are
+    # exactly 1 (bit planes above the integer range with weight 0), so no level has an odd
+    # factor to carry over (a slice + concat per party vector per odd level otherwise)
+    npad = 1 << (nint - 1).bit_length()
+    if f + npad > bits:
+        npad = nint
     bd = rep.bit_decompose(sess, a.t)
-    planes = RepTensor(a.plc, 1, "bool", sess.p("BitSplit", a.plc, bd.s0, start=0, count=f + nint),
-                       sess.p("BitSplit", a.plc, bd.s1, start=0, count=f + nint))
+    planes = RepTensor(a.plc, 1, "bool", sess.p("BitSplit", a.plc, bd.s0, start=0, count=f + npad),
+                       sess.p("BitSplit", a.plc, bd.s1, start=0, count=f + npad))
     ab = rep.b2a(sess, planes, bits)  # arithmetic bits, leading axis
-    frac_w = [(1 << j) for j in range(f)] + [0] * nint
+    frac_w = [(1 << j) for j in range(f)] + [0] * npad
     r = RepFixed(_weighted(sess, ab, frac_w, bits), f, integ)
     if negative:
         # 2^-r for r in [0,1) = 2^(1-r) / 2 -> fit exp2 on [0, 1] of (1 - r)
@@ -531,14 +537,15 @@ def _exp2_parts(sess, a: RepFixed, negative: bool):
         else:
             c = 2.0 ** min(e, integ + 1)  # saturate: larger results overflow anyway
         cs.append(int(round((c - 1.0) * (1 << f))))
-    ints = local(sess, ab, "Slice", slice=(f, f + nint, None))
+    cs += [0] * (npad - nint)
+    ints = local(sess, ab, "Slice", slice=(f, f + npad, None))
     cvec = R.from_ints(np.array(cs, dtype=object), bits, sess.device)
     pc = sess.public(ints.plc, cvec)
     fac = RepTensor(ints.plc, bits, "arith", sess.p("MulLeading", ints.plc, ints.s0, pc),
                     sess.p("MulLeading", ints.plc, ints.s1, pc))
     fac = rep.add_public(sess, fac, _encode_const(sess, 1.0, f, bits))
     # log-depth product over the leading axis: one stacked multiplication per level
-    F, n = RepFixed(fac, f, integ), nint
+    F, n = RepFixed(fac, f, integ), npad
     views = _rows_ok(sess, F)
     while n > 1:
         h = n // 2

@@ -240,8 +240,7 @@ class StackedSession(Session):
         v = x.v
         op = {"Add": "add", "Sub": "sub", "Xor": "xor", "And": "and", "Mul": "mul"}.get(prim)
         if op is not None and isinstance(c, R.RT) and c.bits == v.bits and v.bits in (1, 64, 128):
-            m = math.prod(v.shape[1:])
-            if c.numel() in (1, m) and (c.numel() == 1 or tuple(c.shape) == tuple(v.shape[1:])):
+            if R._slot_operand_ok(v, c):  # scalar, slot-shaped or trailing-axes vector
                 return PV(plc, R.binary_slot(op, v, c, which))  # one kernel
         part = PRIMS[prim].impl(0, R.RT(v.data[which], v.bits), c)
         d = v.data.clone() if part.data.shape == v.data.shape[1:] else None
@@ -295,10 +294,8 @@ class StackedSession(Session):
         op = self._PAIR_BIN.get(prim)
         v0, v1 = x0.v, x1.v
         if (op is None or not isinstance(c, R.RT) or c.bits != v0.bits
-                or v0.bits not in (64, 128) or v1.shape != v0.shape):
-            return None
-        m = math.prod(v0.shape[1:])
-        if not (c.numel() == 1 or tuple(c.shape) == tuple(v0.shape[1:])) or c.numel() not in (1, m):
+                or v0.bits not in (64, 128) or v1.shape != v0.shape
+                or not R._slot_operand_ok(v0, c)):
             return None
         o0, o1 = R.binary_slot2(op, v0, v1, c, which0, which1)
         return PV(plc, o0), PV(plc, o1)

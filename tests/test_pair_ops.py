@@ -82,3 +82,16 @@ def test_slot_place2(dev, bits):
     z = np.zeros((4, 3), dtype=object)
     np.testing.assert_array_equal(R.to_ints(o0), np.stack([z, z, R.to_ints(x0)]))
     np.testing.assert_array_equal(R.to_ints(o1), np.stack([z, R.to_ints(x1), z]))
+
+
+@pytest.mark.parametrize("dev", DEVICES)
+@pytest.mark.parametrize("bits", [64, 128])
+def test_slot_ops_broadcast_trailing_vector(dev, bits):
+    """A public operand shaped like the slot's trailing axes repeats with that period."""
+    a0, a1 = _rand((3, 5, 4), bits, dev, 8), _rand((3, 5, 4), bits, dev, 9)
+    c = _rand((4,), bits, dev, 10)
+    full = R.RT(c.data.unsqueeze(0).expand((5,) + tuple(c.data.shape)).contiguous(), bits)
+    _eq(R.binary_slot("add", a0, c, 1), R.binary_slot("add", a0, full, 1))
+    o0, o1 = R.binary_slot2("sub", a0, a1, c, 0, 2)
+    _eq(o0, R.binary_slot("sub", a0, full, 0))
+    _eq(o1, R.binary_slot("sub", a1, full, 2))
