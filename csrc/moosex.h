@@ -55,6 +55,15 @@ int mx_ew_unary2(int dev, int op, int words, const void* a0, void* out0, const v
 int mx_ew_binary_slot2(int dev, int op, int words, const void* a0, const void* a1,
                        const void* b, int64_t nb, void* out0, void* out1, int64_t m,
                        int nparties, int which0, int which1, void* stream);
+// Fixed-point product of three stacked parties in one launch (device, latency-bound sizes):
+// rss_mul3 (zero share from slots k0, k1, k2 at nmul) followed by trunc_pr3 (slots k0 / k2,
+// nonces r0 r1 t m z0 z2) on the product, outputs at party stride ostride.  views: operand
+// {party stride[4], period[4]} or null.  Returns 1 when the size is not latency-bound (the
+// caller then runs the two kernels), 0 on success.
+int mx_mul_trunc3_kv(int dev, int words, const void* x0, const void* x1, const void* y0,
+                     const void* y1, void* out0, void* out1, int64_t n, int64_t ostride,
+                     const uint32_t* slots, uint64_t nmul, int m, const uint64_t* nonces,
+                     const int64_t* views, void* stream);
 // Two trivial sharings in the stacked layout [nparties, m], one launch:
 // out0[q, i] = q == which0 ? x0[i] : 0 ; out1[q, i] = q == which1 ? x1[i] : 0
 int mx_slot_place2(int dev, int words, const void* x0, const void* x1, void* out0, void* out1,

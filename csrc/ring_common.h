@@ -202,6 +202,10 @@ int mxh_ew_binary2(int op, int words, const void* a0, const void* b0, void* out0
                    void* stream);
 int mxh_slot_place2(int words, const void* x0, const void* x1, void* out0, void* out1,
                     int64_t m, int nparties, int which0, int which1, void* stream);
+int mxh_mul_trunc3_kv(int words, const void* x0, const void* x1, const void* y0, const void* y1,
+                      void* out0, void* out1, int64_t n, int64_t ostride, const uint32_t* slots,
+                      uint64_t nmul, int m, const uint64_t* nn, const int64_t* views,
+                      void* stream);
 int mxh_ew_unary2(int op, int words, const void* a0, void* out0, const void* a1, void* out1,
                   int64_t n, int64_t param, void* stream);
 int mxh_ew_binary_slot2(int op, int words, const void* a0, const void* a1, const void* b,

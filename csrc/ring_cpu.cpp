@@ -404,6 +404,16 @@ int mx_ew_binary_slot2(int dev, int op, int words, const void* a0, const void* a
             : mx_ew_binary_slot(0, op, words, a1, b, nb, out1, m, nparties, which1, stream);
 }
 
+int mx_mul_trunc3_kv(int dev, int words, const void* x0, const void* x1, const void* y0,
+                     const void* y1, void* out0, void* out1, int64_t n, int64_t ostride,
+                     const uint32_t* slots, uint64_t nmul, int m, const uint64_t* nonces,
+                     const int64_t* views, void* stream) {
+  if (dev)
+    return mxh_mul_trunc3_kv(words, x0, x1, y0, y1, out0, out1, n, ostride, slots, nmul, m,
+                             nonces, views, stream);
+  return 1;  // host: the caller composes mx_rss_mul3 and mx_trunc_pr3
+}
+
 int mx_slot_place2(int dev, int words, const void* x0, const void* x1, void* out0, void* out1,
                    int64_t m, int nparties, int which0, int which1, void* stream) {
   if (dev)

@@ -19,6 +19,7 @@
 #include "prf_dev.h"
 #include "moosex.h"
 #include "ring_common.h"
+#include "rss_fused.h"
 
 using mxr::u128;
 using u64 = uint64_t;
@@ -569,6 +570,71 @@ __global__ void __launch_bounds__(256) k_rss_cross_ring3_lat(int kind, const T* 
   }
 }
 
+// Fixed-point product of a latency-bound launch in ONE kernel: the stacked RSS product
+// with its zero share (as k_rss_cross_ring3_lat) and the TruncPr of the reshared product
+// (as k_trunc_pr3_lat) -- the product never leaves registers.  Nine keystream chunks per
+// chunk position: the product's zero share (k0, k1, k2 at nmul) and the TruncPr's r0, r1,
+// t, m, z0, z2 (keys k0 / k2, as in k_trunc_pr3).  Bitwise equal to the two kernels.
+template <class T>
+__global__ void __launch_bounds__(256) k_mul_trunc3_lat(
+    const T* __restrict__ x0, const T* __restrict__ x1, const T* __restrict__ y0,
+    const T* __restrict__ y1, T* __restrict__ out0, T* __restrict__ out1, int64_t n, int64_t os,
+    KeySrc keys, uint64_t nmul, int m, uint64_t nr0, uint64_t nr1, uint64_t nt, uint64_t nm,
+    uint64_t nz0, uint64_t nz2, Views vw) {
+  constexpr int NS = 9, EPB = 256 / NS;
+  __shared__ uint32_t rks[3][kKeyWords];
+  __shared__ uint64_t kl[NS][EPB], kh[NS][EPB];
+  stage_keys(rks, keys, 3);
+  constexpr int P = Lane<T>::kPer;
+  const int64_t nb = (n + P - 1) / P;
+  const int tid = threadIdx.x, s = tid / EPB, lb = tid % EPB;
+  // stream s: 0..2 product zero share (k_s), 3 r0 (k0), 4 r1 (k2), 5 t (k0), 6 m (k0),
+  // 7 z0 (k0), 8 z2 (k2)
+  const int key_of = s < 3 ? s : (s == 4 || s == 8) ? 2 : 0;
+  const uint64_t nonce_of = s < 3 ? nmul : s == 3 ? nr0 : s == 4 ? nr1 : s == 5 ? nt
+                            : s == 6 ? nm : s == 7 ? nz0 : nz2;
+  for (int64_t b0 = (int64_t)blockIdx.x * EPB; b0 < nb; b0 += (int64_t)gridDim.x * EPB) {
+    if (s < NS && b0 + lb < nb) {
+      uint64_t lo, hi;
+      prf_chunk(rks[key_of], nonce_of, (uint64_t)(b0 + lb), &lo, &hi);
+      kl[s][lb] = lo;
+      kh[s][lb] = hi;
+    }
+    __syncthreads();
+    if (tid < EPB && b0 + tid < nb) {
+      const int64_t b = b0 + tid;
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const int64_t e = b * P + j;
+        if (e >= n) break;
+        T z[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const int q = p == 2 ? 0 : p + 1;
+          const T v = mxr::cross<T>(MX_CROSS_ARITH, ld_view(x0, vw, 0, p, e, n),
+                                    ld_view(x1, vw, 1, p, e, n), ld_view(y0, vw, 2, p, e, n),
+                                    ld_view(y1, vw, 3, p, e, n), true, true);
+          z[p] = mxr::zs_combine<T>(MX_CROSS_ARITH, v, pick<T>(kl[p][tid], kh[p][tid], j),
+                                    pick<T>(kl[q][tid], kh[q][tid], j));
+        }
+        const T Z0 = pick<T>(kl[7][tid], kh[7][tid], j);
+        const T Z2 = pick<T>(kl[8][tid], kh[8][tid], j);
+        const T Z1 = mxf::trunc_pr_z1<T>(
+            z[0], z[1], z[2], pick<T>(kl[3][tid], kh[3][tid], j),
+            pick<T>(kl[4][tid], kh[4][tid], j), pick<T>(kl[5][tid], kh[5][tid], j),
+            pick<T>(kl[6][tid], kh[6][tid], j), Z0, Z2, m);
+        out0[e] = Z0;
+        out0[os + e] = Z1;
+        out0[2 * os + e] = Z2;
+        out1[e] = Z1;
+        out1[os + e] = Z2;
+        out1[2 * os + e] = Z0;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 template <class T>
 __global__ void __launch_bounds__(256) k_prf_expand(T* __restrict__ out, int64_t n, int nkeys, KeySrc keys,
                              uint64_t nonce) {
@@ -1010,6 +1076,38 @@ int mxh_rss_mul3_kv(int kind, int words, const void* x0, const void* x1, const v
   vw.strided = 1;
   return launch_rss_cross(kind, words, x0, x1, y0, y1, out0, n, 3, true, true,
                           mxd::keysrc_slots(ptrs, 3), nonce, stream, out1, 0, &vw);
+}
+
+// k_mul_trunc3_lat: latency-bound launches only (returns 1 -- "not handled" -- above the
+// size where the separate throughput kernels win).  views: {ps[4], per[4]} or null.
+int mxh_mul_trunc3_kv(int words, const void* x0, const void* x1, const void* y0, const void* y1,
+                      void* out0, void* out1, int64_t n, int64_t ostride, const uint32_t* slots,
+                      uint64_t nmul, int m, const uint64_t* nn, const int64_t* views,
+                      void* stream) {
+  if (n == 0) return 0;
+  const uint32_t* ptrs[3];
+  for (int i = 0; i < 3; ++i) ptrs[i] = slots + MX_KEY_SLOT_WORDS * i;
+  Views vw{};
+  if (views) {
+    for (int i = 0; i < 4; ++i) {
+      vw.ps[i] = views[i];
+      vw.per[i] = views[4 + i] > 0 ? views[4 + i] : n;
+    }
+    vw.strided = 1;
+  }
+  DEV_DISPATCH(words, T, {
+    constexpr int P = 16 / (int)sizeof(T);
+    const int64_t blocks = (n + P - 1) / P;
+    if (blocks > 8192) return 1;
+    constexpr int EPB = 256 / 9;
+    const int64_t g = (blocks + EPB - 1) / EPB;
+    hipLaunchKernelGGL(k_mul_trunc3_lat<T>, dim3((unsigned)g), dim3(kBlock), 0, S(stream),
+                       (const T*)x0, (const T*)x1, (const T*)y0, (const T*)y1, (T*)out0,
+                       (T*)out1, n, ostride, mxd::keysrc_slots(ptrs, 3), nmul, m, nn[0], nn[1],
+                       nn[2], nn[3], nn[4], nn[5], vw);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
 }
 
 int mxh_ks_cross1(int words, const void* g0, const void* g1, const void* p0, const void* p1,

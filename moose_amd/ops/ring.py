@@ -946,6 +946,49 @@ def rss_mul3_k(kind: str, x0: RT, x1: RT, y0: RT, y1: RT, slot_ptr: int, nonce: 
     return out0, out1
 
 
+def mul_trunc3_k(x0: RT, x1: RT, y0: RT, y1: RT, slot_ptr: int, nmul: int, m: int, nonces,
+                 out=None):
+    """Fixed-point product of three stacked parties in one kernel on the device
+    (mx_mul_trunc3_kv): ``rss_mul3_k(arith)`` + the stacked TruncPr of its result, bitwise
+    the same.  ``out``: optional (s0, s1) views with dense party slots to write into.
+    Returns (s0, s1), or None when not applicable (host, large or mixed-shape operands)."""
+    bits = x0.bits
+    if not x0.data.is_cuda or bits not in (64, 128):
+        return None
+    shp = x0.shape
+    ops = (x0, x1, y0, y1)
+    if any(o.shape != shp or o.bits != bits for o in ops):
+        return None
+    n = math.prod(shp) // 3
+    if n == 0:
+        return None
+    views = None
+    if any(not o.data.is_contiguous() for o in ops):
+        vs = [_party_view(o) for o in ops]
+        if any(v is None for v in vs):
+            return None
+        views = (ctypes.c_int64 * 8)(*[v[0] for v in vs], *[v[1] for v in vs])
+    w = 2 if bits == 128 else 1
+    if out is None:
+        o0, o1 = empty2(shp, bits, x0.device)
+        os_ = n
+    else:
+        o0, o1 = out
+        os_ = o0.data.stride(0) // w
+        if not (o0.shape == shp and o1.shape == shp and o1.data.stride(0) == o0.data.stride(0)
+                and o0.data[0].is_contiguous() and o1.data[0].is_contiguous()):
+            return None
+    nn = (ctypes.c_uint64 * 6)(*[v & MASK64 for v in nonces])
+    rc = nat.lib().mx_mul_trunc3_kv(
+        nat.dev_of(o0.data), _words(bits), *[nat.ptr(o.data) for o in ops], nat.ptr(o0.data),
+        nat.ptr(o1.data), n, os_, ctypes.c_void_p(slot_ptr), nmul & MASK64, int(m), nn, views,
+        nat.stream_of(o0.data))
+    if rc == 1:
+        return None
+    nat.check(rc, "mul_trunc3")
+    return o0, o1
+
+
 def add_zs3(v: RT, r: RT):
     """Stacked arith zero share from precomputed keystreams ``r`` (= PRF(k_p) per party)
     plus the reshare: returns (s0, s1) exactly like ``rss_mul3_k(arith, v)``."""

@@ -101,7 +101,7 @@ def mul(sess, x, y, px=None, py=None, f=None):
     if py is not None:
         z = rep.mul_public(sess, x.t, _pub(py))
     else:
-        z = rep.mul(sess, x.t, y.t)
+        return _with(x, rep.mul_trunc(sess, x.t, y.t, f if f is not None else x.frac))
     return _with(x, rep.trunc_pr(sess, z, f if f is not None else x.frac))
 
 
@@ -397,12 +397,11 @@ def _poly_eval_rows(sess, x: RepFixed, coeffs) -> RepFixed:
                          sess.p_rows_bcast(P1, have - 1, m))
         right = RepTensor(t.plc, bits, t.kind, sess.p_rows_view(P0, 0, m),
                           sess.p_rows_view(P1, 0, m))
-        prod = rep.mul(sess, left, right)
         if getattr(sess, "fused", False):  # the trunc kernel writes rows have.. in place
-            rep.trunc_pr(sess, prod, f, out=(sess.p_rows_view(P0, have, have + m),
-                                             sess.p_rows_view(P1, have, have + m)))
+            rep.mul_trunc(sess, left, right, f, out=(sess.p_rows_view(P0, have, have + m),
+                                                     sess.p_rows_view(P1, have, have + m)))
         else:
-            z = rep.trunc_pr(sess, prod, f)
+            z = rep.trunc_pr(sess, rep.mul(sess, left, right), f)
             sess.p_rows_write(P0, have, z.s0)
             sess.p_rows_write(P1, have, z.s1)
         have += m

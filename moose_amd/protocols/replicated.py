@@ -276,6 +276,17 @@ def mul(sess, x: RepTensor, y: RepTensor) -> RepTensor:
         return _reshare(sess, x.plc, z, x.bits, kind)
 
 
+def mul_trunc(sess, x: RepTensor, y: RepTensor, m: int, out=None) -> RepTensor:
+    """trunc_pr(mul(x, y), m): one fused kernel on a stacked device session for small
+    operands (same shares as the two steps), the two protocol steps otherwise."""
+    f = getattr(sess, "p_mul_trunc", None)
+    if f is not None and m and x.kind == "arith" and getattr(sess, "fused", False):
+        r = f(x.plc, x.s0, x.s1, y.s0, y.s1, m, out=out)
+        if r is not None:
+            return RepTensor(x.plc, x.bits, "arith", r[0], r[1])
+    return trunc_pr(sess, mul(sess, x, y), m, out=out)
+
+
 def and_(sess, x: RepTensor, y: RepTensor) -> RepTensor:
     assert x.kind == "bool"
     return mul(sess, x, y)

@@ -353,6 +353,37 @@ class StackedSession(Session):
         self.stats.record_round(_nbytes(s0))
         return PV(plc, s0), PV(plc, s1)
 
+    def p_mul_trunc(self, plc, x0, x1, y0, y1, m, out=None):
+        """rep.mul + rep.trunc_pr (arith) in one latency kernel when the launch is small
+        (device); None -> the caller runs the two protocol steps.  Draws the same nonces
+        in the same order as the two steps."""
+        if self.device.type != "cuda":
+            return None
+        v = [t.v for t in (x0, x1, y0, y1)]
+        if not all(isinstance(t, R.RT) for t in v) or v[0].bits not in (64, 128):
+            return None
+        if any(t.shape != v[0].shape for t in v) or math.prod(v[0].shape) // 3 > 8192 * (
+                1 if v[0].bits == 128 else 2):
+            return None
+        if any(not t.data.is_contiguous() and R._party_view(t) is None for t in v):
+            return None
+        if out is not None:
+            o = [t.v.data for t in out]
+            if not (tuple(out[0].v.shape) == tuple(v[0].shape) == tuple(out[1].v.shape)
+                    and o[0].stride(0) == o[1].stride(0) and o[0][0].is_contiguous()
+                    and o[1][0].is_contiguous()):
+                return None
+        nmul = self.nonce(plc)
+        nonces = tuple(self.nonce(plc) for _ in range(6))
+        outs = None if out is None else (out[0].v, out[1].v)
+        r = R.mul_trunc3_k(*v, self.key_ptr(plc, 0), nmul, m, nonces, out=outs)
+        if r is None:  # cannot happen after the checks above; keep the protocol honest
+            raise RuntimeError("mul_trunc3 declined after its checks")
+        nbytes = _nbytes(r[0])
+        self.stats.record_round(nbytes)
+        self._trunc_traffic(x0, nbytes // 3)
+        return PV(plc, r[0]), PV(plc, r[1])
+
     def p_ks_level(self, plc, g0, g1, p0, p1, d, both):
         """One Kogge-Stone level of rep.binary_adder (AND(s) + reshare + xor) in one
         kernel; consumes the one nonce of the generic level's AND round."""

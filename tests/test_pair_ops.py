@@ -95,3 +95,27 @@ def test_slot_ops_broadcast_trailing_vector(dev, bits):
     o0, o1 = R.binary_slot2("sub", a0, a1, c, 0, 2)
     _eq(o0, R.binary_slot("sub", a0, full, 0))
     _eq(o1, R.binary_slot("sub", a1, full, 2))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [64, 128])
+@pytest.mark.parametrize("layout", ["dense", "views"])
+def test_mul_trunc_fused_matches_two_steps(bits, layout):
+    """rep.mul_trunc's single kernel (mx_mul_trunc3_kv) produces exactly the shares of
+    rep.mul followed by rep.trunc_pr (same keys, same nonce order)."""
+    plc = ReplicatedPlacement(("alice", "bob", "carole"))
+    shp = (3, 6, 50)
+    xs = [_rand(shp, bits, "cuda", s) for s in (21, 22)]
+    ys = [_rand(shp, bits, "cuda", s) for s in (23, 24)]
+    if layout == "views":  # row slices of larger stacks, read in place
+        xs = [R.RT(R.zeros((3, 9, 50), bits, "cuda").data, bits) for _ in range(2)]
+        for i, s in enumerate((21, 22)):
+            xs[i].data[:, 2:8] = _rand(shp, bits, "cuda", s).data
+        xs = [R.RT(x.data[:, 2:8], bits) for x in xs]
+    X = rep.RepTensor(plc, bits, "arith", PV(plc, xs[0]), PV(plc, xs[1]))
+    Y = rep.RepTensor(plc, bits, "arith", PV(plc, ys[0]), PV(plc, ys[1]))
+    s1, s2 = StackedSession("cuda", seed=3), StackedSession("cuda", seed=3)
+    a = rep.mul_trunc(s1, X, Y, 20)
+    b = rep.trunc_pr(s2, rep.mul(s2, X, Y), 20)
+    _eq(a.s0.v, b.s0.v)
+    _eq(a.s1.v, b.s1.v)
