@@ -181,3 +181,64 @@ def test_fused_kogge_stone_level_bitwise_equals_generic(bits):
         assert (opened == want).all()
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+# --- property tests (reference replicated/mod.rs:630-696 test_fuzzy_rep_mul/dot) -------------
+from hypothesis import given  # noqa: E402
+from hypothesis import settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+
+def _ring_vals(bits):
+    return st.lists(st.integers(min_value=0, max_value=(1 << bits) - 1), min_size=1, max_size=24)
+
+
+def _share_ints(sess, vals, bits, owner="alice"):
+    return rep.share(sess, PLC, HV(owner, R.from_ints(np.array(vals, dtype=object), bits, "cpu")))
+
+
+def _reveal_ints(sess, t):
+    return [int(v) for v in R.to_ints(rep.reveal(sess, t, "carole").v).reshape(-1)]
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+@settings(max_examples=25, deadline=None)
+@given(data=st.data())
+def test_fuzzy_rep_mul_add_sub(bits, data):
+    xs = data.draw(_ring_vals(bits))
+    ys = data.draw(st.lists(st.integers(0, (1 << bits) - 1), min_size=len(xs),
+                            max_size=len(xs)))
+    s = StackedSession("cpu", seed=data.draw(st.integers(0, 2**31)))
+    X, Y = _share_ints(s, xs, bits), _share_ints(s, ys, bits, "bob")
+    mod = 1 << bits
+    assert _reveal_ints(s, rep.mul(s, X, Y)) == [(a * b) % mod for a, b in zip(xs, ys)]
+    assert _reveal_ints(s, rep.add(s, X, Y)) == [(a + b) % mod for a, b in zip(xs, ys)]
+    assert _reveal_ints(s, rep.sub(s, X, Y)) == [(a - b) % mod for a, b in zip(xs, ys)]
+    assert _reveal_ints(s, rep.neg(s, X)) == [(-a) % mod for a in xs]
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+@settings(max_examples=25, deadline=None)
+@given(data=st.data())
+def test_fuzzy_rep_dot(bits, data):
+    xs = data.draw(_ring_vals(bits))
+    ys = data.draw(st.lists(st.integers(0, (1 << bits) - 1), min_size=len(xs),
+                            max_size=len(xs)))
+    s = StackedSession("cpu", seed=data.draw(st.integers(0, 2**31)))
+    X = rep.local(s, _share_ints(s, xs, bits), "Reshape", shape=(1, len(xs)))
+    Y = rep.local(s, _share_ints(s, ys, bits, "carole"), "Reshape", shape=(len(ys), 1))
+    want = sum(a * b for a, b in zip(xs, ys)) % (1 << bits)
+    assert _reveal_ints(s, rep.dot(s, X, Y)) == [want]
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+@settings(max_examples=20, deadline=None)
+@given(data=st.data())
+def test_fuzzy_rep_msb_and_bit_decompose(bits, data):
+    xs = data.draw(_ring_vals(bits))
+    s = StackedSession("cpu", seed=data.draw(st.integers(0, 2**31)))
+    X = _share_ints(s, xs, bits)
+    assert _reveal_ints(s, rep.msb(s, X)) == [a >> (bits - 1) for a in xs]
+    from moose_amd.runtime.dispatch import bit_compose
+
+    assert _reveal_ints(s, bit_compose(s, rep.bit_decompose(s, X))) == xs
