@@ -64,6 +64,12 @@ int mx_mul_trunc3_kv(int dev, int words, const void* x0, const void* x1, const v
                      const void* y1, void* out0, void* out1, int64_t n, int64_t ostride,
                      const uint32_t* slots, uint64_t nmul, int m, const uint64_t* nonces,
                      const int64_t* views, void* stream);
+// Share-wise linear combination of nin <= 3 stacked replicated values [nparties, m], both
+// share vectors in one launch: out_y = sum_t coef[t] * ins[2t + y] (mod 2^w), plus the public
+// b (period nb, null = none) at party slot which_y.
+int mx_lincomb2(int dev, int words, int nin, const void* const* ins, const int64_t* coef,
+                const void* b, int64_t nb, void* out0, void* out1, int64_t m, int nparties,
+                int which0, int which1, void* stream);
 // Two trivial sharings in the stacked layout [nparties, m], one launch:
 // out0[q, i] = q == which0 ? x0[i] : 0 ; out1[q, i] = q == which1 ? x1[i] : 0
 int mx_slot_place2(int dev, int words, const void* x0, const void* x1, void* out0, void* out1,

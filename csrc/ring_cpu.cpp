@@ -414,6 +414,32 @@ int mx_mul_trunc3_kv(int dev, int words, const void* x0, const void* x1, const v
   return 1;  // host: the caller composes mx_rss_mul3 and mx_trunc_pr3
 }
 
+int mx_lincomb2(int dev, int words, int nin, const void* const* ins, const int64_t* coef,
+                const void* b, int64_t nb, void* out0, void* out1, int64_t m, int nparties,
+                int which0, int which1, void* stream) {
+  if (dev)
+    return mxh_lincomb2(words, nin, ins, coef, b, nb, out0, out1, m, nparties, which0, which1,
+                        stream);
+  if (nin < 1 || nin > 3) return -3;
+  DISPATCH_WORDS(words, T, {
+    T* O[2] = {(T*)out0, (T*)out1};
+    const int W[2] = {which0, which1};
+    const T* B = (const T*)b;
+    const int64_t n = m * nparties;
+    for (int y = 0; y < 2; ++y) {
+      parallel_for(n, 1 << 14, [&](int64_t lo, int64_t hi) {
+        for (int64_t g = lo; g < hi; ++g) {
+          T v = 0;
+          for (int t = 0; t < nin; ++t) v += (T)(int64_t)coef[t] * ((const T*)ins[2 * t + y])[g];
+          if (B != nullptr && g / m == W[y]) v += B[nb == 1 ? 0 : (g % m) % nb];
+          O[y][g] = v;
+        }
+      });
+    }
+    return 0;
+  });
+}
+
 int mx_slot_place2(int dev, int words, const void* x0, const void* x1, void* out0, void* out1,
                    int64_t m, int nparties, int which0, int which1, void* stream) {
   if (dev)

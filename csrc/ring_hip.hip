@@ -112,6 +112,36 @@ __global__ void __launch_bounds__(256) k_binary_slot2(int op, Pair<T> p, int64_t
   }
 }
 
+// Share-wise linear combination of up to three replicated values, both share vectors in one
+// launch: out_y = sum_t coef[t] * in_t[y] (+ public b at party slot which[y], period nb).
+template <class T>
+struct Lin3 {
+  const T* a[3][2];
+  T* o[2];
+  int64_t coef[3];
+  int which[2];
+};
+
+template <class T>
+__global__ void __launch_bounds__(256) k_lincomb2(Lin3<T> p, int nin, const T* __restrict__ b,
+                                                  int64_t nb, int64_t m, int np) {
+  const int y = blockIdx.y;
+  T* __restrict__ out = p.o[y];
+  const int which = p.which[y];
+  const int64_t n = m * np;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < n;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    T v = (T)(int64_t)p.coef[0] * p.a[0][y][g];
+    if (nin > 1) v += (T)(int64_t)p.coef[1] * p.a[1][y][g];
+    if (nin > 2) v += (T)(int64_t)p.coef[2] * p.a[2][y][g];
+    if (b != nullptr) {
+      const int64_t q = g / m, i = g - q * m;
+      if (q == which) v += b[nb == 1 ? 0 : i % nb];
+    }
+    out[g] = v;
+  }
+}
+
 // trivial sharings in the stacked layout: out_y[q, i] = q == which[y] ? a[y][i] : 0
 template <class T>
 __global__ void __launch_bounds__(256) k_slot_place2(Pair<T> p, int64_t m, int np) {
@@ -791,6 +821,29 @@ int mxh_ew_binary_slot2(int op, int words, const void* a0, const void* a1, const
               {which0, which1}};
     hipLaunchKernelGGL(k_binary_slot2<T>, dim3(grid_for(m * nparties), 2), dim3(kBlock), 0,
                        S(stream), op, p, nb, m, nparties);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mxh_lincomb2(int words, int nin, const void* const* ins, const int64_t* coef, const void* b,
+                 int64_t nb, void* out0, void* out1, int64_t m, int nparties, int which0,
+                 int which1, void* stream) {
+  if (m == 0) return 0;
+  if (nin < 1 || nin > 3) return -3;
+  DEV_DISPATCH(words, T, {
+    Lin3<T> p{};
+    for (int t = 0; t < nin; ++t) {
+      p.a[t][0] = (const T*)ins[2 * t];
+      p.a[t][1] = (const T*)ins[2 * t + 1];
+      p.coef[t] = coef[t];
+    }
+    p.o[0] = (T*)out0;
+    p.o[1] = (T*)out1;
+    p.which[0] = which0;
+    p.which[1] = which1;
+    hipLaunchKernelGGL(k_lincomb2<T>, dim3(grid_for(m * nparties), 2), dim3(kBlock), 0,
+                       S(stream), p, nin, (const T*)b, nb, m, nparties);
     MX_LAUNCH_CHECK();
     return 0;
   });

@@ -34,6 +34,8 @@ _SIGS = {
                                    c_i64, c_int, c_int, c_int, c_vp]),
     "mx_mul_trunc3_kv": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
                                  c_vp, c_u64, c_int, c_vp, c_vp, c_vp]),
+    "mx_lincomb2": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64,
+                            c_int, c_int, c_int, c_vp]),
     "mx_slot_place2": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int,
                                c_vp]),
     "mx_ew_compare": (c_int, [c_int, c_int, c_int, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),

@@ -1056,6 +1056,31 @@ def binary_slot2(op: str, a0: RT, a1: RT, b: RT, which0: int, which1: int):
     return o0, o1
 
 
+def lincomb2(terms, b=None, which0: int = 0, which1: int = 2):
+    """Share-wise sum_t coef_t * (s0_t, s1_t) of stacked [nparties, ...] share vectors (+ the
+    public ``b`` at slots which0 / which1) in one launch (mx_lincomb2).  ``terms``: up to 3
+    (int coef, RT s0, RT s1) of one shape.  Returns (out0, out1)."""
+    c0, a0, _ = terms[0]
+    bits, shp = a0.bits, a0.shape
+    np_, m = shp[0], math.prod(shp[1:])
+    datas = []
+    for _, x0, x1 in terms:
+        datas += [x0.data.contiguous(), x1.data.contiguous()]
+    bd = None
+    if b is not None:
+        bd = b.data.contiguous()
+        if bd.device != a0.device:
+            bd = bd.to(a0.device)
+    o0, o1 = empty2(shp, bits, a0.device)
+    ins = (ctypes.c_void_p * len(datas))(*[d.data_ptr() for d in datas])
+    coef = (ctypes.c_int64 * len(terms))(*[int(t[0]) for t in terms])
+    nat.check(nat.lib().mx_lincomb2(
+        nat.dev_of(o0.data), _words(bits), len(terms), ins, coef, nat.ptr(bd),
+        b.numel() if b is not None else 0, nat.ptr(o0.data), nat.ptr(o1.data), m, np_,
+        int(which0), int(which1), nat.stream_of(o0.data)), "lincomb2")
+    return o0, o1
+
+
 def slot_place2(x0: RT, x1: RT, which0: int, which1: int, nparties: int = 3):
     """Two trivial stacked sharings [nparties, *x.shape] in one launch: slot which0 of the
     first = x0, slot which1 of the second = x1, zeros elsewhere (mx_slot_place2)."""

@@ -154,6 +154,11 @@ def add_const(sess, x: RepFixed, c: float) -> RepFixed:
     return _with(x, rep.add_public(sess, x.t, _encode_const(sess, c, x.frac, x.bits)))
 
 
+def const_sub(sess, c: float, x: RepFixed) -> RepFixed:
+    """c - x for a public real constant (one share-wise kernel)."""
+    return _with(x, rep.lincomb(sess, [(-1, x.t)], const=_encode_const(sess, c, x.frac, x.bits)))
+
+
 def ring_binary(sess, kind, x, y, px=None, py=None):
     if kind == "Add":
         if px is not None:
@@ -274,7 +279,7 @@ def relu(sess, x: RepFixed) -> RepFixed:
 
 def abs_(sess, x: RepFixed) -> RepFixed:
     s = sign_bit(sess, x)
-    return _with(x, rep.sub(sess, x.t, rep.shl(sess, rep.mul(sess, s, x.t), 1)))
+    return _with(x, rep.lincomb(sess, [(1, x.t), (-2, rep.mul(sess, s, x.t))]))
 
 
 def _stack0(sess, xs):
@@ -441,7 +446,7 @@ def _fit(fn_name: str, lo: float, hi: float, degree: int):
 # ---------------------------------------------------------------------------
 def _newton_recip(sess, m: RepFixed, w: RepFixed, iters: int) -> RepFixed:
     for _ in range(iters):
-        e = add_const(sess, neg(sess, mul(sess, m, w)), 2.0)  # 2 - m w
+        e = const_sub(sess, 2.0, mul(sess, m, w))  # 2 - m w
         w = mul(sess, w, e)
     return w
 
@@ -458,9 +463,9 @@ def reciprocal_positive(sess, x: RepFixed) -> RepFixed:
 
 def reciprocal(sess, x: RepFixed) -> RepFixed:
     s = sign_bit(sess, x)
-    ax = _with(x, rep.sub(sess, x.t, rep.shl(sess, rep.mul(sess, s, x.t), 1)))
+    ax = _with(x, rep.lincomb(sess, [(1, x.t), (-2, rep.mul(sess, s, x.t))]))
     r = reciprocal_positive(sess, ax)
-    return _with(r, rep.sub(sess, r.t, rep.shl(sess, rep.mul(sess, s, r.t), 1)))
+    return _with(r, rep.lincomb(sess, [(1, r.t), (-2, rep.mul(sess, s, r.t))]))
 
 
 def div(sess, x, y, px=None, py=None):
@@ -522,7 +527,7 @@ def _exp2_parts(sess, a: RepFixed, negative: bool):
     r = RepFixed(_weighted(sess, ab, frac_w, bits), f, integ)
     if negative:
         # 2^-r for r in [0,1) = 2^(1-r) / 2 -> fit exp2 on [0, 1] of (1 - r)
-        one_minus = add_const(sess, neg(sess, r), 1.0)
+        one_minus = const_sub(sess, 1.0, r)
         p = mul_const(sess, poly_eval(sess, one_minus, _fit("exp2", 0.0, 1.0, 7)), 0.5)
     else:
         p = poly_eval(sess, r, _fit("exp2", 0.0, 1.0, 7))
@@ -565,7 +570,7 @@ def _exp2_parts(sess, a: RepFixed, negative: bool):
 
 def exp2(sess, x: RepFixed) -> RepFixed:
     s = sign_bit(sess, x)
-    ax = _with(x, rep.sub(sess, x.t, rep.shl(sess, rep.mul(sess, s, x.t), 1)))
+    ax = _with(x, rep.lincomb(sess, [(1, x.t), (-2, rep.mul(sess, s, x.t))]))
     pos = _exp2_parts(sess, ax, negative=False)
     negv = _exp2_parts(sess, ax, negative=True)
     return _with(pos, rep.mux(sess, s, negv.t, pos.t))
@@ -585,14 +590,14 @@ def sigmoid(sess, x: RepFixed) -> RepFixed:
     """sigma(x) = 1 / (1 + e^-|x|) mirrored for x < 0; 1 + e^-|x| is in [1, 2] so the
     reciprocal needs no normalisation."""
     s = sign_bit(sess, x)
-    ax = _with(x, rep.sub(sess, x.t, rep.shl(sess, rep.mul(sess, s, x.t), 1)))
+    ax = _with(x, rep.lincomb(sess, [(1, x.t), (-2, rep.mul(sess, s, x.t))]))
     e = exp_nonpositive(sess, neg(sess, ax))
     d = add_const(sess, e, 1.0)  # in [1, 2]
     half = mul_const(sess, d, 0.5)  # in [0.5, 1]
     w = poly_eval(sess, half, _fit("recip", 0.5, 1.0, 4))
     w = _newton_recip(sess, half, w, 1)
     pos = mul_const(sess, w, 0.5)  # 1/d
-    one_minus = add_const(sess, neg(sess, pos), 1.0)
+    one_minus = const_sub(sess, 1.0, pos)
     return _with(pos, rep.mux(sess, s, one_minus.t, pos.t))
 
 

@@ -252,6 +252,33 @@ def shl(sess, x: RepTensor, k: int) -> RepTensor:
     return local(sess, x, "Shl", amount=k)
 
 
+def lincomb(sess, terms, const=None) -> RepTensor:
+    """sum_t k_t * x_t (+ public const) for arithmetic sharings of one shape and small integer
+    k_t: one share-wise kernel on a stacked device session, else composed from neg / shl /
+    mul_public / add (exactly the same ring values either way)."""
+    x = terms[0][1]
+    f = getattr(sess, "p_lincomb", None)
+    if f is not None and x.kind == "arith":
+        r = f(x.plc, [(k, t.s0, t.s1) for k, t in terms], const)
+        if r is not None:
+            return RepTensor(x.plc, x.bits, x.kind, r[0], r[1])
+
+    def scaled(k, t):
+        if k == 1:
+            return t
+        if k == -1:
+            return neg(sess, t)
+        if k in (2, -2):
+            d = shl(sess, t, 1)
+            return d if k == 2 else neg(sess, d)
+        return mul_public(sess, t, R.fill((), int(k), t.bits, getattr(sess, "device", "cpu")))
+
+    acc = scaled(*terms[0])
+    for k, t in terms[1:]:
+        acc = add(sess, acc, scaled(k, t))
+    return acc if const is None else add_public(sess, acc, const)
+
+
 def sum(sess, x: RepTensor, axis=None) -> RepTensor:  # noqa: A001
     return local(sess, x, "Sum", axis=axis)
 
@@ -511,7 +538,7 @@ def b2a(sess, b: RepTensor, ring_bits: int) -> RepTensor:
         b2_h1 = sess.h("RingInject", o[1], sess.take(b.s1, 1), bit_idx=0, bits=ring_bits)
         B = from_slot_holders(sess, plc, 2, b2_h0, b2_h1, b.s0, kind="arith")
         AB = mul(sess, A, B)
-        return sub(sess, add(sess, A, B), shl(sess, AB, 1))
+        return lincomb(sess, [(1, A), (1, B), (-2, AB)])
 
 
 def msb(sess, x: RepTensor) -> RepTensor:
@@ -558,7 +585,7 @@ def mux(sess, s: RepTensor, x: RepTensor, y: RepTensor) -> RepTensor:
 def abs_(sess, x: RepTensor) -> RepTensor:
     s = less_than_zero_arith(sess, x)
     # |x| = x - 2 s x
-    return sub(sess, x, shl(sess, mul(sess, s, x), 1))
+    return lincomb(sess, [(1, x), (-2, mul(sess, s, x))])
 
 
 def relu(sess, x: RepTensor) -> RepTensor:

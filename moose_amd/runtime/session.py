@@ -289,6 +289,26 @@ class StackedSession(Session):
         a, b = R.slot_place2(v0, v1, h0, h1)
         return PV(plc, a), PV(plc, b)
 
+    def p_lincomb(self, plc, terms, const=None):
+        """sum_t k_t * x_t (+ public const on party 0's share) for 64/128-bit replicated
+        values of one shape, one kernel; ``terms`` = [(k, PV s0, PV s1)].  None -> the
+        caller composes the share-wise ops."""
+        if not 1 <= len(terms) <= 3:
+            return None
+        vs = [(k, a.v, b.v) for k, a, b in terms]
+        v0 = vs[0][1]
+        if not all(isinstance(a, R.RT) and isinstance(b, R.RT) for _, a, b in vs):
+            return None
+        if v0.bits not in (64, 128) or any(
+                a.bits != v0.bits or b.bits != v0.bits or a.shape != v0.shape or b.shape != v0.shape
+                for _, a, b in vs):
+            return None
+        if const is not None and not (isinstance(const, R.RT) and const.bits == v0.bits
+                                      and R._slot_operand_ok(v0, const)):
+            return None
+        o0, o1 = R.lincomb2(vs, const, 0, 2)
+        return PV(plc, o0), PV(plc, o1)
+
     def p_apply_at2(self, prim, plc, x0, x1, which0, which1, c):
         """p_apply_at on both share vectors in one kernel (None if not applicable)."""
         op = self._PAIR_BIN.get(prim)

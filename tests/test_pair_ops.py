@@ -119,3 +119,17 @@ def test_mul_trunc_fused_matches_two_steps(bits, layout):
     b = rep.trunc_pr(s2, rep.mul(s2, X, Y), 20)
     _eq(a.s0.v, b.s0.v)
     _eq(a.s1.v, b.s1.v)
+
+
+@pytest.mark.parametrize("dev", DEVICES)
+@pytest.mark.parametrize("bits", [64, 128])
+def test_lincomb2_matches_composition(dev, bits):
+    a = [_rand((3, 4, 5), bits, dev, s) for s in range(31, 37)]
+    c = _rand((5,), bits, dev, 40)
+    o0, o1 = R.lincomb2([(1, a[0], a[1]), (1, a[2], a[3]), (-2, a[4], a[5])], c, 0, 2)
+    for o, (x, y, z), w in ((o0, (a[0], a[2], a[4]), 0), (o1, (a[1], a[3], a[5]), 2)):
+        want = R.binary("sub", R.binary("add", x, y), R.unary("shl", z, 1))
+        _eq(o, R.binary_slot("add", want, c, w))
+    o0, o1 = R.lincomb2([(-1, a[0], a[1])])
+    _eq(o0, R.unary("neg", a[0]))
+    _eq(o1, R.unary("neg", a[1]))
