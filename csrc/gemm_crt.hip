@@ -309,7 +309,7 @@ template <int WR, int WC, int BN, int MINW>
 __global__ void __launch_bounds__(64 * WR * WC, MINW)
     k_crt_gemm(const int8_t* __restrict__ RA, const int8_t* __restrict__ RB,
                int8_t* __restrict__ CR, int tiles_m, int tiles_n, int nkb, int gM,
-               const EpiTab ep, int dma_mask) {
+               const EpiTab ep, int dma_mask, int bcast) {
   constexpr int NW = WR * WC;
   constexpr int MI = BM / WR / 32, NJ = BN / WC / 32;
   constexpr int kImgB = BN * BK;                 // one B image per (tile, k-step)
@@ -327,9 +327,9 @@ __global__ void __launch_bounds__(64 * WR * WC, MINW)
   const int tm = first_m + in_group % gm, tn = in_group / gm;
   const int g = blockIdx.y;  // batch * n + modulus
   const int mi = g % ep.n;
-
-  const int8_t* ga = RA + ((int64_t)g * tiles_m + tm) * nkb * (int64_t)kImg;
-  const int8_t* gb = RB + ((int64_t)g * tiles_n + tn) * nkb * (int64_t)kImgB;
+  // bcast bit 0 / 1: A / B residues were prepared once for every batch entry
+  const int8_t* ga = RA + ((int64_t)((bcast & 1) ? mi : g) * tiles_m + tm) * nkb * (int64_t)kImg;
+  const int8_t* gb = RB + ((int64_t)((bcast & 2) ? mi : g) * tiles_n + tn) * nkb * (int64_t)kImgB;
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -530,7 +530,7 @@ template <int WR, int WC, int BN, int MINW>
 __global__ void __launch_bounds__(64 * WR * WC, MINW)
     k_crt_gemm16(const int8_t* __restrict__ RA, const int8_t* __restrict__ RB,
                  int8_t* __restrict__ CR, int tiles_m, int tiles_n, int nkb, int gM,
-                 const EpiTab ep, int dma_mask) {
+                 const EpiTab ep, int dma_mask, int bcast) {
   constexpr int NW = WR * WC;
   constexpr int MI = BM / WR / 16, NJ = BN / WC / 16;
   constexpr int NM = MI * NJ;                    // MFMAs per wave per k-step
@@ -549,8 +549,8 @@ __global__ void __launch_bounds__(64 * WR * WC, MINW)
   const int tm = first_m + in_group % gm, tn = in_group / gm;
   const int g = blockIdx.y;
   const int mi = g % ep.n;
-  const int8_t* ga = RA + ((int64_t)g * tiles_m + tm) * nkb * (int64_t)kImg;
-  const int8_t* gb = RB + ((int64_t)g * tiles_n + tn) * nkb * (int64_t)kImgB;
+  const int8_t* ga = RA + ((int64_t)((bcast & 1) ? mi : g) * tiles_m + tm) * nkb * (int64_t)kImg;
+  const int8_t* gb = RB + ((int64_t)((bcast & 2) ? mi : g) * tiles_n + tn) * nkb * (int64_t)kImgB;
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -788,7 +788,7 @@ int dma_mask() {
 
 template <int WR, int WC, int BN, int MINW, bool M16>
 void launch_variant(const CPlan& p, const Tables& tb, int64_t batch, const int8_t* ra,
-                    const int8_t* rb, int8_t* cr, hipStream_t st) {
+                    const int8_t* rb, int8_t* cr, int bcast, hipStream_t st) {
   constexpr int lds = kStages * (kImg + BN * BK);
   const void* fn = M16 ? (const void*)k_crt_gemm16<WR, WC, BN, MINW>
                        : (const void*)k_crt_gemm<WR, WC, BN, MINW>;
@@ -801,22 +801,22 @@ void launch_variant(const CPlan& p, const Tables& tb, int64_t batch, const int8_
   if constexpr (M16)
     hipLaunchKernelGGL((k_crt_gemm16<WR, WC, BN, MINW>), grid, dim3(64 * WR * WC), lds, st, ra,
                        rb, cr, (int)p.tiles_m, (int)p.tiles_n, (int)p.nkb, gemm_group_m(), tb.ep,
-                       dma_mask());
+                       dma_mask(), bcast);
   else
     hipLaunchKernelGGL((k_crt_gemm<WR, WC, BN, MINW>), grid, dim3(64 * WR * WC), lds, st, ra, rb,
                        cr, (int)p.tiles_m, (int)p.tiles_n, (int)p.nkb, gemm_group_m(), tb.ep,
-                       dma_mask());
+                       dma_mask(), bcast);
 }
 
 void launch_crt_gemm(const CPlan& p, const Tables& tb, int64_t batch, const int8_t* ra,
-                     const int8_t* rb, int8_t* cr, hipStream_t st) {
+                     const int8_t* rb, int8_t* cr, int bcast, hipStream_t st) {
   switch (crt_kernel()) {
-    case 1: launch_variant<2, 2, 256, 1, false>(p, tb, batch, ra, rb, cr, st); break;
-    case 2: launch_variant<2, 4, 256, 2, false>(p, tb, batch, ra, rb, cr, st); break;
-    case 4: launch_variant<2, 2, 256, 1, true>(p, tb, batch, ra, rb, cr, st); break;
-    case 3: launch_variant<2, 2, 128, 2, false>(p, tb, batch, ra, rb, cr, st); break;
-    case 6: launch_variant<2, 4, 256, 2, true>(p, tb, batch, ra, rb, cr, st); break;
-    default: launch_variant<2, 2, 128, 2, true>(p, tb, batch, ra, rb, cr, st); break;
+    case 1: launch_variant<2, 2, 256, 1, false>(p, tb, batch, ra, rb, cr, bcast, st); break;
+    case 2: launch_variant<2, 4, 256, 2, false>(p, tb, batch, ra, rb, cr, bcast, st); break;
+    case 4: launch_variant<2, 2, 256, 1, true>(p, tb, batch, ra, rb, cr, bcast, st); break;
+    case 3: launch_variant<2, 2, 128, 2, false>(p, tb, batch, ra, rb, cr, bcast, st); break;
+    case 6: launch_variant<2, 4, 256, 2, true>(p, tb, batch, ra, rb, cr, bcast, st); break;
+    default: launch_variant<2, 2, 128, 2, true>(p, tb, batch, ra, rb, cr, bcast, st); break;
   }
 }
 
@@ -881,13 +881,17 @@ int run_crt(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T
   int8_t* ra = ws;
   int8_t* cr = ra + p.ra_bytes;
   const int8_t* rb = rb_pre;
+  // an operand broadcast over the batch (stride 0) has its residues prepared once and read
+  // by every batch entry's GEMM (every product is still computed)
+  const bool a_bc = batch > 1 && a_bstride == 0;
+  const bool b_bc = batch > 1 && b_bstride == 0 && !rb_pre;
   if (!rb) {
     int8_t* rbw = cr + p.cr_bytes;
-    launch_prep<T>(p, tb, true, batch, N, K, b_bstride, B0, B1, mode, rbw, st);
+    launch_prep<T>(p, tb, true, b_bc ? 1 : batch, N, K, b_bstride, B0, B1, mode, rbw, st);
     rb = rbw;
   }
-  launch_prep<T>(p, tb, false, batch, M, K, a_bstride, A0, A1, mode, ra, st);
-  launch_crt_gemm(p, tb, batch, ra, rb, cr, st);
+  launch_prep<T>(p, tb, false, a_bc ? 1 : batch, M, K, a_bstride, A0, A1, mode, ra, st);
+  launch_crt_gemm(p, tb, batch, ra, rb, cr, (a_bc ? 1 : 0) | (b_bc ? 2 : 0), st);
   launch_recon<T>(p, tb, batch, M, N, cr, C, accumulate, st);
   const hipError_t e = hipGetLastError();
   return e != hipSuccess ? -100 - (int)e : 0;

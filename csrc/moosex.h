@@ -70,6 +70,12 @@ int mx_mul_trunc3_kv(int dev, int words, const void* x0, const void* x1, const v
 int mx_lincomb2(int dev, int words, int nin, const void* const* ins, const int64_t* coef,
                 const void* b, int64_t nb, void* out0, void* out1, int64_t m, int nparties,
                 int which0, int which1, void* stream);
+// Sum of k stacked share vectors that are views of one buffer at a constant element step
+// is_y (party stride ps_y, each party's slot dense, m elements): out_y[p, e] =
+// sum_t base_y[t * is_y + p * ps_y + e], both share vectors (y = 0, 1) in one launch.
+int mx_sum_views2(int dev, int words, const void* base0, const void* base1, int64_t is0,
+                  int64_t is1, int64_t ps0, int64_t ps1, int k, void* out0, void* out1, int64_t m,
+                  int nparties, void* stream);
 // Two trivial sharings in the stacked layout [nparties, m], one launch:
 // out0[q, i] = q == which0 ? x0[i] : 0 ; out1[q, i] = q == which1 ? x1[i] : 0
 int mx_slot_place2(int dev, int words, const void* x0, const void* x1, void* out0, void* out1,

@@ -203,6 +203,9 @@ int mxh_ew_binary2(int op, int words, const void* a0, const void* b0, void* out0
 int mxh_lincomb2(int words, int nin, const void* const* ins, const int64_t* coef, const void* b,
                  int64_t nb, void* out0, void* out1, int64_t m, int nparties, int which0,
                  int which1, void* stream);
+int mxh_sum_views2(int words, const void* base0, const void* base1, int64_t is0, int64_t is1,
+                   int64_t ps0, int64_t ps1, int k, void* out0, void* out1, int64_t m,
+                   int nparties, void* stream);
 int mxh_slot_place2(int words, const void* x0, const void* x1, void* out0, void* out1,
                     int64_t m, int nparties, int which0, int which1, void* stream);
 int mxh_mul_trunc3_kv(int words, const void* x0, const void* x1, const void* y0, const void* y1,

@@ -440,6 +440,27 @@ int mx_lincomb2(int dev, int words, int nin, const void* const* ins, const int64
   });
 }
 
+int mx_sum_views2(int dev, int words, const void* base0, const void* base1, int64_t is0,
+                  int64_t is1, int64_t ps0, int64_t ps1, int k, void* out0, void* out1, int64_t m,
+                  int nparties, void* stream) {
+  if (dev)
+    return mxh_sum_views2(words, base0, base1, is0, is1, ps0, ps1, k, out0, out1, m, nparties,
+                          stream);
+  DISPATCH_WORDS(words, T, {
+    const T* B[2] = {(const T*)base0, (const T*)base1};
+    T* O[2] = {(T*)out0, (T*)out1};
+    const int64_t IS[2] = {is0, is1}, PS[2] = {ps0, ps1};
+    for (int y = 0; y < 2; ++y)
+      for (int q = 0; q < nparties; ++q)
+        for (int64_t e = 0; e < m; ++e) {
+          T acc = 0;
+          for (int t = 0; t < k; ++t) acc += B[y][t * IS[y] + q * PS[y] + e];
+          O[y][q * m + e] = acc;
+        }
+    return 0;
+  });
+}
+
 int mx_slot_place2(int dev, int words, const void* x0, const void* x1, void* out0, void* out1,
                    int64_t m, int nparties, int which0, int which1, void* stream) {
   if (dev)

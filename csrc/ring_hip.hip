@@ -142,6 +142,34 @@ __global__ void __launch_bounds__(256) k_lincomb2(Lin3<T> p, int nin, const T* _
   }
 }
 
+// AddN of k replicated values that are evenly spaced views of one stack (the products of a
+// batched Dot): out_y[p, e] = sum_t base_y[t * is_y + p * ps_y + e], both share vectors in
+// one launch.
+template <class T>
+struct SumViews {
+  const T* base[2];
+  T* o[2];
+  int64_t is[2];
+  int64_t ps[2];
+};
+
+template <class T>
+__global__ void __launch_bounds__(256) k_sum_views2(SumViews<T> p, int k, int64_t m, int np) {
+  const int y = blockIdx.y;
+  const T* __restrict__ base = p.base[y];
+  T* __restrict__ out = p.o[y];
+  const int64_t is = p.is[y], ps = p.ps[y];
+  const int64_t n = m * np;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < n;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t q = g / m, e = g - q * m;
+    const T* src = base + q * ps + e;
+    T acc = 0;
+    for (int t = 0; t < k; ++t) acc += src[(int64_t)t * is];
+    out[g] = acc;
+  }
+}
+
 // trivial sharings in the stacked layout: out_y[q, i] = q == which[y] ? a[y][i] : 0
 template <class T>
 __global__ void __launch_bounds__(256) k_slot_place2(Pair<T> p, int64_t m, int np) {
@@ -844,6 +872,20 @@ int mxh_lincomb2(int words, int nin, const void* const* ins, const int64_t* coef
     p.which[1] = which1;
     hipLaunchKernelGGL(k_lincomb2<T>, dim3(grid_for(m * nparties), 2), dim3(kBlock), 0,
                        S(stream), p, nin, (const T*)b, nb, m, nparties);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mxh_sum_views2(int words, const void* base0, const void* base1, int64_t is0, int64_t is1,
+                   int64_t ps0, int64_t ps1, int k, void* out0, void* out1, int64_t m,
+                   int nparties, void* stream) {
+  if (m == 0) return 0;
+  DEV_DISPATCH(words, T, {
+    SumViews<T> p{{(const T*)base0, (const T*)base1}, {(T*)out0, (T*)out1}, {is0, is1},
+                  {ps0, ps1}};
+    hipLaunchKernelGGL(k_sum_views2<T>, dim3(grid_for(m * nparties), 2), dim3(kBlock), 0,
+                       S(stream), p, k, m, nparties);
     MX_LAUNCH_CHECK();
     return 0;
   });

@@ -36,6 +36,8 @@ _SIGS = {
                                  c_vp, c_u64, c_int, c_vp, c_vp, c_vp]),
     "mx_lincomb2": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64,
                             c_int, c_int, c_int, c_vp]),
+    "mx_sum_views2": (c_int, [c_int, c_int, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_vp,
+                              c_vp, c_i64, c_int, c_vp]),
     "mx_slot_place2": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int,
                                c_vp]),
     "mx_ew_compare": (c_int, [c_int, c_int, c_int, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),

@@ -531,7 +531,12 @@ def concat(xs: Sequence[RT], axis=0, nb=0) -> RT:
 
 def index_axis(a: RT, axis: int, index: int, nb=0) -> RT:
     ax = _ax(a, axis, nb)
-    return RT(a.data.select(ax, index).contiguous(), a.bits)
+    v = a.data.select(ax, index)
+    if nb == 1 and ax == 1 and v.dim() >= 1 and v[0].is_contiguous():
+        # one entry of a party-stacked batch ([P, k, ...] -> [P, ...]): a view whose party
+        # slots stay dense -- consumers read it in place or copy on demand
+        return RT(v, a.bits)
+    return RT(v.contiguous(), a.bits)
 
 
 def slice_axis(a: RT, axis: int, start, end, step=None, nb=0) -> RT:
@@ -1078,6 +1083,46 @@ def lincomb2(terms, b=None, which0: int = 0, which1: int = 2):
         nat.dev_of(o0.data), _words(bits), len(terms), ins, coef, nat.ptr(bd),
         b.numel() if b is not None else 0, nat.ptr(o0.data), nat.ptr(o1.data), m, np_,
         int(which0), int(which1), nat.stream_of(o0.data)), "lincomb2")
+    return o0, o1
+
+
+def _even_views(ts):
+    """(base tensor, element step, party stride) when the stacked RTs ``ts`` are views of one
+    buffer at a constant step with dense party slots; None otherwise."""
+    d0 = ts[0].data
+    w = 2 if ts[0].bits == 128 else 1
+    if d0.dim() < 1 or not d0[0].is_contiguous() or d0.stride(0) % w:
+        return None
+    es = d0.element_size() * w
+    ptrs = [t.data.data_ptr() for t in ts]
+    for t in ts:
+        d = t.data
+        if (d.shape != d0.shape or d.stride() != d0.stride() or d.dtype != d0.dtype
+                or d.device != d0.device or t.bits != ts[0].bits):
+            return None
+    if len(ts) > 1:
+        step = ptrs[1] - ptrs[0]
+        if step <= 0 or step % es or any(ptrs[i + 1] - ptrs[i] != step for i in range(len(ts) - 1)):
+            return None
+        step //= es
+    else:
+        step = 0
+    return d0, step, d0.stride(0) // w
+
+
+def sum_views2(ts0, ts1):
+    """(sum of ts0, sum of ts1) -- k stacked share vectors each -- in one launch when both
+    lists are evenly spaced views of one buffer (mx_sum_views2); None otherwise."""
+    v0, v1 = _even_views(ts0), _even_views(ts1)
+    if v0 is None or v1 is None or ts0[0].shape != ts1[0].shape:
+        return None
+    bits, shp = ts0[0].bits, ts0[0].shape
+    o0, o1 = empty2(shp, bits, ts0[0].device)
+    np_, m = shp[0], math.prod(shp[1:])
+    nat.check(nat.lib().mx_sum_views2(
+        nat.dev_of(o0.data), _words(bits), v0[0].data_ptr(), v1[0].data_ptr(), v0[1], v1[1],
+        v0[2], v1[2], len(ts0), nat.ptr(o0.data), nat.ptr(o1.data), m, np_,
+        nat.stream_of(o0.data)), "sum_views2")
     return o0, o1
 
 

@@ -257,6 +257,21 @@ def shl(sess, x: RepTensor, k: int) -> RepTensor:
     return local(sess, x, "Shl", amount=k)
 
 
+def add_n(sess, xs) -> RepTensor:
+    """sum of replicated values (one kernel for views of one stack on a stacked device
+    session, else a chain of share-wise adds -- the same ring values)."""
+    x = xs[0]
+    f = getattr(sess, "p_add_n", None)
+    if f is not None and x.kind == "arith" and len(xs) > 1:
+        r = f(x.plc, [(t.s0, t.s1) for t in xs])
+        if r is not None:
+            return RepTensor(x.plc, x.bits, x.kind, r[0], r[1])
+    acc = x
+    for t in xs[1:]:
+        acc = add(sess, acc, t)
+    return acc
+
+
 def lincomb(sess, terms, const=None) -> RepTensor:
     """sum_t k_t * x_t (+ public const) for arithmetic sharings of one shape and small integer
     k_t: one share-wise kernel on a stacked device session, else composed from neg / shl /

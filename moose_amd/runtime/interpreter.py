@@ -967,6 +967,11 @@ class Interpreter:
         return self._binary(op, ins, "Or")
 
     def op_AddN(self, op, ins):
+        if (len(ins) > 2 and all(x.is_rep and isinstance(x.v, RepFixed) for x in ins)
+                and len({(x.v.frac, x.dtype) for x in ins}) == 1):
+            t = rep.add_n(self.sess, [x.v.t for x in ins])
+            v = ins[0].v
+            return LV(ins[0].plc, "tensor", ins[0].dtype, RepFixed(t, v.frac, v.integ))
         acc = ins[0]
         for x in ins[1:]:
             acc = self._binary(op, [acc, x], "Add")

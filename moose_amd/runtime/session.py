@@ -289,6 +289,19 @@ class StackedSession(Session):
         a, b = R.slot_place2(v0, v1, h0, h1)
         return PV(plc, a), PV(plc, b)
 
+    def p_add_n(self, plc, xs):
+        """Sum of replicated values ``xs`` [(PV s0, PV s1)] in one kernel when they are evenly
+        spaced views of one stack (e.g. the products of a batched Dot); None otherwise."""
+        v0, v1 = [a.v for a, _ in xs], [b.v for _, b in xs]
+        if len(xs) < 2 or not all(isinstance(t, R.RT) for t in v0 + v1):
+            return None
+        if v0[0].bits not in (64, 128):
+            return None
+        r = R.sum_views2(v0, v1)
+        if r is None:
+            return None
+        return PV(plc, r[0]), PV(plc, r[1])
+
     def p_lincomb(self, plc, terms, const=None):
         """sum_t k_t * x_t (+ public const on party 0's share) for 64/128-bit replicated
         values of one shape, one kernel; ``terms`` = [(k, PV s0, PV s1)].  None -> the

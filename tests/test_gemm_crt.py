@@ -231,20 +231,26 @@ def test_gpu_crt_prepared_b_rows(bits):
 @pytest.mark.gpu
 @pytest.mark.parametrize("bits", [64, 128])
 @pytest.mark.parametrize("crt", [1, 2])
-def test_gpu_dot_cross_broadcast_views(bits, crt):
+@pytest.mark.parametrize("both", [False, True])
+def test_gpu_dot_cross_broadcast_views(bits, crt, both):
     """[3, k, M, K] stride-0 stacks of one operand (fixedpoint.dot_many on k uses of the same
-    values) go to the strided GEMM without a copy; equal to the materialised product."""
+    values) go to the strided GEMM without a copy -- the CRT path prepares a broadcast
+    operand's residues once; equal to the materialised product."""
     k, M, K, N = 5, 300, 270, 260
     xs = [gpu(rand_rt((3, M, K), bits, 90 + i)) for i in range(2)]
-    ys = [gpu(rand_rt((3, 1, K, N), bits, 95 + i)) for i in range(2)]
-    ys = [R.RT(torch.cat([y.data] * k, dim=1), bits) for y in ys]  # a real stack for y
 
     def view(t):
         d = t.data.unsqueeze(1)
         return R.RT(d.expand((3, k) + tuple(d.shape[2:])), bits)
 
+    if both:
+        ys = [view(gpu(rand_rt((3, K, N), bits, 95 + i))) for i in range(2)]
+    else:
+        ys = [gpu(rand_rt((3, 1, K, N), bits, 95 + i)) for i in range(2)]
+        ys = [R.RT(torch.cat([y.data] * k, dim=1), bits) for y in ys]  # a real stack for y
+    dense = [R.RT(y.data.contiguous(), bits) for y in ys]
     with _crt(crt):
         got = R.dot_cross(view(xs[0]), view(xs[1]), ys[0], ys[1], nb=2)
         want = R.dot_cross(R.RT(view(xs[0]).data.contiguous(), bits),
-                           R.RT(view(xs[1]).data.contiguous(), bits), ys[0], ys[1], nb=2)
+                           R.RT(view(xs[1]).data.contiguous(), bits), *dense, nb=2)
     same(got, want)

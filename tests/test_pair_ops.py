@@ -133,3 +133,21 @@ def test_lincomb2_matches_composition(dev, bits):
     o0, o1 = R.lincomb2([(-1, a[0], a[1])])
     _eq(o0, R.unary("neg", a[0]))
     _eq(o1, R.unary("neg", a[1]))
+
+
+@pytest.mark.parametrize("dev", DEVICES)
+@pytest.mark.parametrize("bits", [64, 128])
+def test_sum_views2_of_one_stack(dev, bits):
+    """AddN over the entries of a party-stacked batch reads them in place (mx_sum_views2)."""
+    b0, b1 = _rand((3, 7, 4, 5), bits, dev, 50), _rand((3, 7, 4, 5), bits, dev, 51)
+    v0 = [R.index_axis(b0, 0, i, nb=1) for i in range(7)]
+    v1 = [R.index_axis(b1, 0, i, nb=1) for i in range(7)]
+    assert not v0[1].data.is_contiguous()  # views, not copies
+    o0, o1 = R.sum_views2(v0, v1)
+    w0, w1 = v0[0], v1[0]
+    for i in range(1, 7):
+        w0, w1 = R.binary("add", w0, v0[i]), R.binary("add", w1, v1[i])
+    _eq(o0, w0)
+    _eq(o1, w1)
+    assert R.sum_views2([v0[0], v0[2]], [v1[0], v1[1]]) is not None  # any even spacing
+    assert R.sum_views2([v0[0], v0[1], v0[3]], v1[:3]) is None  # uneven: declined
