@@ -55,6 +55,11 @@ _REP_DIALECT = {
 }
 
 
+# argument types of logical-level operations: the dispatch table only holds ring-level rows
+_LOGICAL_TY = frozenset({"Tensor", "Shape", "Unknown", "HostShape", "HostUnit", "HostString",
+                         "HostSeed", "HostPrfKey", "Float32", "Float64"})
+
+
 class MooseRuntimeError(errors.KernelError):
     pass
 
@@ -201,7 +206,9 @@ class Interpreter:
         for o in later:
             if len(group) >= limit:
                 break
-            if o.kind != "Dot" or o.name in self.env or self._table_handler(o) is not None:
+            if o.kind != "Dot" or o.name in self.env or any(n not in self.env for n in o.inputs):
+                continue
+            if self._table_handler(o) is not None:
                 continue
             k = key(o)
             if k is not None and k[0] == k0[0]:
@@ -225,6 +232,8 @@ class Interpreter:
         """Ring-level operations on replicated / additive placements (and their Reveal to a
         host) through the declarative (op, placement, operand types) table of
         runtime/dispatch.py; None when no row matches (logical types never do)."""
+        if op.sig is None or not any(t.name not in _LOGICAL_TY for t in op.sig.args):
+            return None  # logical signatures: no table row (fast path, checked per op)
         from moose_amd.ir.computation import AdditivePlacement
         from moose_amd.runtime import dispatch
 

@@ -473,7 +473,26 @@ class StackedSession(Session):
 
     def p_dot_cross(self, plc, x0, x1, y0, y1, nbatch=0):
         """``nbatch`` leading logical axes are batch axes (independent products, one
-        batched GEMM launch with the parties)."""
+        batched GEMM launch with the parties).  A right operand used by several products of
+        one evaluation (e.g. a chain z = z.y) has its GEMM operand image prepared once, from
+        its second use on; every product is still computed."""
+        yv0, yv1 = y0.v, y1.v
+        if (nbatch == 0 and self.device.type == "cuda" and len(yv0.shape) == 3
+                and len(x0.v.shape) == 3 and min(x0.v.shape[1], yv0.shape[1], yv0.shape[2]) >= 256):
+            # (large products only: small ones run the VALU GEMM, which has no prepared form)
+            cache = self.__dict__.setdefault("_prepared_b", {})
+            key = (id(yv0.data), id(yv1.data))
+            hit = cache.get(key)
+            if hit is not None and hit[0] is yv0.data and hit[1] is yv1.data:
+                pb = hit[2]
+                if pb is None:  # second use: prepare once for this and every later product
+                    pb = R.PreparedCross(yv0, yv1)
+                    cache[key] = (yv0.data, yv1.data, pb)
+                if pb.lb is not None:
+                    M = x0.v.shape[1]
+                    return PV(plc, R.dot_cross_rows(x0.v, x1.v, 0, M, pb))
+            elif len(cache) < 64:
+                cache[key] = (yv0.data, yv1.data, None)  # holds the tensors: ids stay unique
         return PV(plc, R.dot_cross(x0.v, x1.v, y0.v, y1.v, nb=1 + nbatch))
 
     def p_add_zero_share(self, plc, z, kind="arith"):
