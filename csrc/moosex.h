@@ -228,6 +228,9 @@ int mx_trunc_pr3_k(int dev, int words, const void* s0, void* out0, void* out1, i
 int mx_trunc_pr3_ko(int dev, int words, const void* s0, void* out0, void* out1, int64_t n,
                     int m, const uint32_t* slot_k0, const uint32_t* slot_k2,
                     const uint64_t* nonces, int64_t ostride, void* stream);
+int mx_trunc_pr3_kmo(int dev, int words, const void* s0, void* out0, void* out1, int64_t n,
+                     int m, const uint32_t* slot_k0, const uint32_t* slot_k2,
+                     const uint64_t* nonces, int64_t ostride, const uint64_t* cm, void* stream);
 int mx_share3_k(int dev, int kind, int words, const void* x, void* out0, void* out1, int64_t n,
                 int j, const uint32_t* slot_next, const uint32_t* slot_all, uint64_t n1,
                 uint64_t na, void* stream);

@@ -18,7 +18,7 @@ namespace {
 
 template <class T>
 __global__ void __launch_bounds__(256) k_trunc_pr3(const T* __restrict__ s0, T* __restrict__ out0, T* __restrict__ out1,
-                            int64_t n, int64_t os, int m, mxd::KeySrc keys, uint64_t n_r0, uint64_t n_r1,
+                            int64_t n, int64_t os, T cm, int m, mxd::KeySrc keys, uint64_t n_r0, uint64_t n_r1,
                             uint64_t n_t, uint64_t n_m, uint64_t n_z0, uint64_t n_z2) {
   __shared__ uint32_t rks[2][mxd::kKeyWords];
   mxd::stage_keys(rks, keys, 2);
@@ -34,7 +34,7 @@ __global__ void __launch_bounds__(256) k_trunc_pr3(const T* __restrict__ s0, T* 
       if (i >= n) break;
       const T z0 = mxd::pick<T>(lo[4], hi[4], j);
       const T z2 = mxd::pick<T>(lo[5], hi[5], j);
-      const T z1 = mxf::trunc_pr_z1<T>(s0[i], s0[n + i], s0[2 * n + i], mxd::pick<T>(lo[0], hi[0], j),
+      const T z1 = mxf::trunc_pr_z1<T>(cm * s0[i], cm * s0[n + i], cm * s0[2 * n + i], mxd::pick<T>(lo[0], hi[0], j),
                                        mxd::pick<T>(lo[1], hi[1], j), mxd::pick<T>(lo[2], hi[2], j),
                                        mxd::pick<T>(lo[3], hi[3], j), z0, z2, m);
       out0[i] = z0;
@@ -52,7 +52,7 @@ __global__ void __launch_bounds__(256) k_trunc_pr3(const T* __restrict__ s0, T* 
 template <class T>
 __global__ void __launch_bounds__(256) k_trunc_pr3_lat(const T* __restrict__ s0, T* __restrict__ out0,
                                                        T* __restrict__ out1, int64_t n,
-                                                       int64_t os, int m, mxd::KeySrc keys, uint64_t n_r0,
+                                                       int64_t os, T cm, int m, mxd::KeySrc keys, uint64_t n_r0,
                                                        uint64_t n_r1, uint64_t n_t, uint64_t n_m,
                                                        uint64_t n_z0, uint64_t n_z2) {
   constexpr int EPB = 256 / 6;
@@ -83,7 +83,7 @@ __global__ void __launch_bounds__(256) k_trunc_pr3_lat(const T* __restrict__ s0,
         const T z0 = mxd::pick<T>(kl[4][tid], kh[4][tid], j);
         const T z2 = mxd::pick<T>(kl[5][tid], kh[5][tid], j);
         const T z1 = mxf::trunc_pr_z1<T>(
-            s0[i], s0[n + i], s0[2 * n + i], mxd::pick<T>(kl[0][tid], kh[0][tid], j),
+            cm * s0[i], cm * s0[n + i], cm * s0[2 * n + i], mxd::pick<T>(kl[0][tid], kh[0][tid], j),
             mxd::pick<T>(kl[1][tid], kh[1][tid], j), mxd::pick<T>(kl[2][tid], kh[2][tid], j),
             mxd::pick<T>(kl[3][tid], kh[3][tid], j), z0, z2, m);
         out0[i] = z0;
@@ -129,9 +129,13 @@ __global__ void __launch_bounds__(256) k_share3(int kind, const T* __restrict__ 
   });
 }
 
-// out0 / out1: party p's slot at out + p * os (os = n: dense stacks; larger: row views)
+// out0 / out1: party p's slot at out + p * os (os = n: dense stacks; larger: row views);
+// cm: public premultiplier of the input shares (words little-endian; null = 1)
 int launch_trunc_pr3(int words, const void* s0, void* out0, void* out1, int64_t n, int64_t os,
-                     int m, const mxd::KeySrc& keys, const uint64_t* nn, void* stream) {
+                     int m, const mxd::KeySrc& keys, const uint64_t* nn, void* stream,
+                     const uint64_t* cm = nullptr) {
+  const u64 c64 = cm ? cm[0] : 1;
+  const u128 c128 = cm ? (((u128)cm[1] << 64) | cm[0]) : (u128)1;
   if (n == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   const int64_t nblk = words == 1 ? (n + 1) / 2 : n;
@@ -139,11 +143,11 @@ int launch_trunc_pr3(int words, const void* s0, void* out0, void* out1, int64_t 
     const unsigned g = (unsigned)((nblk + 41) / 42);
     if (words == 1)
       hipLaunchKernelGGL(k_trunc_pr3_lat<u64>, dim3(g), dim3(256), 0, st, (const u64*)s0,
-                         (u64*)out0, (u64*)out1, n, os, m, keys, nn[0], nn[1], nn[2], nn[3], nn[4],
+                         (u64*)out0, (u64*)out1, n, os, c64, m, keys, nn[0], nn[1], nn[2], nn[3], nn[4],
                          nn[5]);
     else
       hipLaunchKernelGGL(k_trunc_pr3_lat<u128>, dim3(g), dim3(256), 0, st, (const u128*)s0,
-                         (u128*)out0, (u128*)out1, n, os, m, keys, nn[0], nn[1], nn[2], nn[3],
+                         (u128*)out0, (u128*)out1, n, os, c128, m, keys, nn[0], nn[1], nn[2], nn[3],
                          nn[4], nn[5]);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : -100 - (int)e;
@@ -151,11 +155,11 @@ int launch_trunc_pr3(int words, const void* s0, void* out0, void* out1, int64_t 
   if (words == 1) {
     int64_t nb = (n + 1) / 2;
     hipLaunchKernelGGL(k_trunc_pr3<u64>, dim3(mxd::grid_for_chunks(nb)), dim3(256), 0, st,
-                       (const u64*)s0, (u64*)out0, (u64*)out1, n, os, m, keys, nn[0], nn[1], nn[2],
+                       (const u64*)s0, (u64*)out0, (u64*)out1, n, os, c64, m, keys, nn[0], nn[1], nn[2],
                        nn[3], nn[4], nn[5]);
   } else if (words == 2) {
     hipLaunchKernelGGL(k_trunc_pr3<u128>, dim3(mxd::grid_for_chunks(n)), dim3(256), 0, st,
-                       (const u128*)s0, (u128*)out0, (u128*)out1, n, os, m, keys, nn[0], nn[1], nn[2],
+                       (const u128*)s0, (u128*)out0, (u128*)out1, n, os, c128, m, keys, nn[0], nn[1], nn[2],
                        nn[3], nn[4], nn[5]);
   } else {
     return -2;
@@ -214,6 +218,14 @@ int mxh_trunc_pr3_ko(int words, const void* s0, void* out0, void* out1, int64_t 
   const uint32_t* ptrs[2] = {slot_k0, slot_k2};
   return launch_trunc_pr3(words, s0, out0, out1, n, ostride, m, mxd::keysrc_slots(ptrs, 2), nn,
                           stream);
+}
+
+int mxh_trunc_pr3_kmo(int words, const void* s0, void* out0, void* out1, int64_t n, int m,
+                      const uint32_t* slot_k0, const uint32_t* slot_k2, const uint64_t* nn,
+                      int64_t ostride, const uint64_t* cm, void* stream) {
+  const uint32_t* ptrs[2] = {slot_k0, slot_k2};
+  return launch_trunc_pr3(words, s0, out0, out1, n, ostride, m, mxd::keysrc_slots(ptrs, 2), nn,
+                          stream, cm);
 }
 
 int mxh_share3(int kind, int words, const void* x, void* out0, void* out1, int64_t n, int j,

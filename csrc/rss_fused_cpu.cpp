@@ -21,6 +21,10 @@ extern "C" int mxh_share3(int kind, int words, const void* x, void* out0, void* 
 extern "C" int mxh_trunc_pr3_k(int words, const void* s0, void* out0, void* out1, int64_t n,
                                int m, const uint32_t* slot_k0, const uint32_t* slot_k2,
                                const uint64_t* nonces, void* stream);
+extern "C" int mxh_trunc_pr3_kmo(int words, const void* s0, void* out0, void* out1, int64_t n,
+                                 int m, const uint32_t* slot_k0, const uint32_t* slot_k2,
+                                 const uint64_t* nonces, int64_t ostride, const uint64_t* cm,
+                                 void* stream);
 extern "C" int mxh_trunc_pr3_ko(int words, const void* s0, void* out0, void* out1, int64_t n,
                                 int m, const uint32_t* slot_k0, const uint32_t* slot_k2,
                                 const uint64_t* nonces, int64_t ostride, void* stream);
@@ -153,6 +157,30 @@ int mx_trunc_pr3_ko(int dev, int words, const void* s0, void* out0, void* out1, 
     std::memcpy((uint8_t*)out1 + p * ostride * es, t1.data() + p * n * es, n * es);
   }
   return 0;
+}
+
+// mx_trunc_pr3_ko of cm * s0 (cm: public multiplier, words little-endian)
+int mx_trunc_pr3_kmo(int dev, int words, const void* s0, void* out0, void* out1, int64_t n,
+                     int m, const uint32_t* slot_k0, const uint32_t* slot_k2,
+                     const uint64_t* nonces, int64_t ostride, const uint64_t* cm, void* stream) {
+  if (dev)
+    return mxh_trunc_pr3_kmo(words, s0, out0, out1, n, m, slot_k0, slot_k2, nonces, ostride, cm,
+                             stream);
+  if (words == 1) {
+    std::vector<uint64_t> t(3 * n);
+    for (int64_t i = 0; i < 3 * n; ++i) t[i] = ((const uint64_t*)s0)[i] * cm[0];
+    return mx_trunc_pr3_ko(0, words, t.data(), out0, out1, n, m, slot_k0, slot_k2, nonces,
+                           ostride, stream);
+  }
+  if (words == 2) {
+    using u128 = unsigned __int128;
+    const u128 c = ((u128)cm[1] << 64) | cm[0];
+    std::vector<u128> t(3 * n);
+    for (int64_t i = 0; i < 3 * n; ++i) t[i] = ((const u128*)s0)[i] * c;
+    return mx_trunc_pr3_ko(0, words, t.data(), out0, out1, n, m, slot_k0, slot_k2, nonces,
+                           ostride, stream);
+  }
+  return -2;
 }
 
 int mx_share3_k(int dev, int kind, int words, const void* x, void* out0, void* out1, int64_t n,

@@ -118,6 +118,10 @@ _SIGS = {
     "mx_trunc_pr3_ko": (
         c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_i64, c_vp],
     ),
+    "mx_trunc_pr3_kmo": (
+        c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_i64, c_vp,
+                c_vp],
+    ),
     "mx_share3_k": (
         c_int,
         [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_u64, c_u64, c_vp],

@@ -146,8 +146,8 @@ def _stack_operands(sess, xs):
 
 def mul_const(sess, x: RepFixed, c: float) -> RepFixed:
     """x * c for a public real constant (one truncation)."""
-    z = rep.mul_public(sess, x.t, _encode_const(sess, c, x.frac, x.bits))
-    return _with(x, rep.trunc_pr(sess, z, x.frac))
+    return _with(x, rep.mul_public_trunc(sess, x.t, _encode_const(sess, c, x.frac, x.bits),
+                                         x.frac))
 
 
 def add_const(sess, x: RepFixed, c: float) -> RepFixed:

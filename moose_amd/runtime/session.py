@@ -32,6 +32,7 @@ from typing import Any
 from typing import List
 from typing import Optional
 
+import numpy as np
 import torch
 
 from moose_amd.ir.computation import ReplicatedPlacement
@@ -504,6 +505,27 @@ class StackedSession(Session):
 
     # -- fused whole-protocol kernels (same shares as the generic protocol code) ------
     fused = os.environ.get("MOOSEX_FUSED", "1") != "0"
+
+    def fused_trunc_pr_premul(self, x, m, nonces, c):
+        """fused_trunc_pr of c * x for a public scalar ring constant c (mul_public folded
+        into the TruncPr kernel)."""
+        import ctypes
+
+        from moose_amd.ops import native as nat
+
+        s0 = x.s0.v.data.contiguous()
+        n = x.s0.v.numel() // 3
+        nn = (ctypes.c_uint64 * 6)(*[v & ((1 << 64) - 1) for v in nonces])
+        cv = int(np.asarray(R.to_ints(c), dtype=object).reshape(-1)[0]) % (1 << x.bits)
+        cm = (ctypes.c_uint64 * 2)(cv & ((1 << 64) - 1), cv >> 64)
+        both = torch.empty((2,) + tuple(s0.shape), dtype=s0.dtype, device=s0.device)
+        out0, out1 = both[0], both[1]
+        nat.check(nat.lib().mx_trunc_pr3_kmo(
+            nat.dev_of(s0), R._words(x.bits), nat.ptr(s0), nat.ptr(out0), nat.ptr(out1), n, m,
+            self.key_ptr(x.plc, 0), self.key_ptr(x.plc, 2), nn, n, cm, nat.stream_of(s0)),
+            "trunc_pr3 (premultiplied)")
+        self._trunc_traffic(x, out0.numel() * out0.element_size() // 3)
+        return PV(x.plc, R.RT(out0, x.bits)), PV(x.plc, R.RT(out1, x.bits))
 
     def fused_trunc_pr(self, x, m, nonces, out=None):
         """All three parties' TruncPr in one kernel (see replicated.trunc_pr).  ``out``:

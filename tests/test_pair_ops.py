@@ -151,3 +151,18 @@ def test_sum_views2_of_one_stack(dev, bits):
     _eq(o1, w1)
     assert R.sum_views2([v0[0], v0[2]], [v1[0], v1[1]]) is not None  # any even spacing
     assert R.sum_views2([v0[0], v0[1], v0[3]], v1[:3]) is None  # uneven: declined
+
+
+@pytest.mark.parametrize("dev", DEVICES)
+@pytest.mark.parametrize("bits", [64, 128])
+def test_mul_public_trunc_matches_two_steps(dev, bits):
+    """TruncPr with the public scalar folded in equals mul_public then trunc_pr."""
+    plc = ReplicatedPlacement(("alice", "bob", "carole"))
+    x0, x1 = _rand((3, 9, 7), bits, dev, 60), _rand((3, 9, 7), bits, dev, 61)
+    X = rep.RepTensor(plc, bits, "arith", PV(plc, x0), PV(plc, x1))
+    c = R.fill((), (1 << (bits - 3)) + 12345, bits, dev)
+    s1, s2 = StackedSession(dev, seed=5), StackedSession(dev, seed=5)
+    a = rep.mul_public_trunc(s1, X, c, 20)
+    b = rep.trunc_pr(s2, rep.mul_public(s2, X, c), 20)
+    _eq(a.s0.v, b.s0.v)
+    _eq(a.s1.v, b.s1.v)
