@@ -146,8 +146,9 @@ def _stack_operands(sess, xs):
 
 def mul_const(sess, x: RepFixed, c: float) -> RepFixed:
     """x * c for a public real constant (one truncation)."""
+    cv = int(round(c * (1 << x.frac)))
     return _with(x, rep.mul_public_trunc(sess, x.t, _encode_const(sess, c, x.frac, x.bits),
-                                         x.frac))
+                                         x.frac, value=cv))
 
 
 def add_const(sess, x: RepFixed, c: float) -> RepFixed:

@@ -323,16 +323,16 @@ def mul(sess, x: RepTensor, y: RepTensor) -> RepTensor:
         return _reshare(sess, x.plc, z, x.bits, kind)
 
 
-def mul_public_trunc(sess, x: RepTensor, c, m: int) -> RepTensor:
-    """trunc_pr(mul_public(x, c), m); for a public scalar ring constant on a fused stacked
-    session the multiplication runs inside the TruncPr kernel (same shares)."""
-    if (m and x.kind == "arith" and getattr(sess, "fused", False)
-            and isinstance(c, R.RT) and c.numel() == 1 and c.bits == x.bits
+def mul_public_trunc(sess, x: RepTensor, c, m: int, value: int = None) -> RepTensor:
+    """trunc_pr(mul_public(x, c), m); for a public scalar ring constant whose integer
+    ``value`` the caller knows, on a fused stacked session, the multiplication runs inside the
+    TruncPr kernel (same shares)."""
+    if (m and value is not None and x.kind == "arith" and getattr(sess, "fused", False)
             and x.bits in (64, 128) and hasattr(sess, "fused_trunc_pr_premul")):
         with span("rep.trunc_pr"):
             plc = x.plc
             nonces = tuple(sess.nonce(plc) for _ in range(6))  # as trunc_pr draws them
-            s0, s1 = sess.fused_trunc_pr_premul(x, m, nonces, c)
+            s0, s1 = sess.fused_trunc_pr_premul(x, m, nonces, value)
             return RepTensor(plc, x.bits, "arith", s0, s1)
     return trunc_pr(sess, mul_public(sess, x, c), m)
 

@@ -506,9 +506,9 @@ class StackedSession(Session):
     # -- fused whole-protocol kernels (same shares as the generic protocol code) ------
     fused = os.environ.get("MOOSEX_FUSED", "1") != "0"
 
-    def fused_trunc_pr_premul(self, x, m, nonces, c):
-        """fused_trunc_pr of c * x for a public scalar ring constant c (mul_public folded
-        into the TruncPr kernel)."""
+    def fused_trunc_pr_premul(self, x, m, nonces, c: int):
+        """fused_trunc_pr of c * x for a public integer c (mul_public folded into the
+        TruncPr kernel; c is a host value, so nothing is read back from the device)."""
         import ctypes
 
         from moose_amd.ops import native as nat
@@ -516,7 +516,7 @@ class StackedSession(Session):
         s0 = x.s0.v.data.contiguous()
         n = x.s0.v.numel() // 3
         nn = (ctypes.c_uint64 * 6)(*[v & ((1 << 64) - 1) for v in nonces])
-        cv = int(np.asarray(R.to_ints(c), dtype=object).reshape(-1)[0]) % (1 << x.bits)
+        cv = int(c) % (1 << x.bits)
         cm = (ctypes.c_uint64 * 2)(cv & ((1 << 64) - 1), cv >> 64)
         both = torch.empty((2,) + tuple(s0.shape), dtype=s0.dtype, device=s0.device)
         out0, out1 = both[0], both[1]

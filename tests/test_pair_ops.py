@@ -160,9 +160,10 @@ def test_mul_public_trunc_matches_two_steps(dev, bits):
     plc = ReplicatedPlacement(("alice", "bob", "carole"))
     x0, x1 = _rand((3, 9, 7), bits, dev, 60), _rand((3, 9, 7), bits, dev, 61)
     X = rep.RepTensor(plc, bits, "arith", PV(plc, x0), PV(plc, x1))
-    c = R.fill((), (1 << (bits - 3)) + 12345, bits, dev)
+    cv = (1 << (bits - 3)) + 12345
+    c = R.fill((), cv, bits, dev)
     s1, s2 = StackedSession(dev, seed=5), StackedSession(dev, seed=5)
-    a = rep.mul_public_trunc(s1, X, c, 20)
+    a = rep.mul_public_trunc(s1, X, c, 20, value=cv)
     b = rep.trunc_pr(s2, rep.mul_public(s2, X, c), 20)
     _eq(a.s0.v, b.s0.v)
     _eq(a.s1.v, b.s1.v)
