@@ -64,6 +64,9 @@ int mx_mul_trunc3_kv(int dev, int words, const void* x0, const void* x1, const v
                      const void* y1, void* out0, void* out1, int64_t n, int64_t ostride,
                      const uint32_t* slots, uint64_t nmul, int m, const uint64_t* nonces,
                      const int64_t* views, void* stream);
+// out = a + b + c elementwise (mod 2^w)
+int mx_ew_add3(int dev, int words, const void* a, const void* b, const void* c, void* out,
+               int64_t n, void* stream);
 // Share-wise linear combination of nin <= 3 stacked replicated values [nparties, m], both
 // share vectors in one launch: out_y = sum_t coef[t] * ins[2t + y] (mod 2^w), plus the public
 // b (period nb, null = none) at party slot which_y.

@@ -414,6 +414,19 @@ int mx_mul_trunc3_kv(int dev, int words, const void* x0, const void* x1, const v
   return 1;  // host: the caller composes mx_rss_mul3 and mx_trunc_pr3
 }
 
+int mx_ew_add3(int dev, int words, const void* a, const void* b, const void* c, void* out,
+               int64_t n, void* stream) {
+  if (dev) return mxh_ew_add3(words, a, b, c, out, n, stream);
+  DISPATCH_WORDS(words, T, {
+    const T *A = (const T*)a, *B = (const T*)b, *C = (const T*)c;
+    T* O = (T*)out;
+    parallel_for(n, 1 << 16, [&](int64_t s, int64_t e) {
+      for (int64_t i = s; i < e; ++i) O[i] = A[i] + B[i] + C[i];
+    });
+    return 0;
+  });
+}
+
 int mx_lincomb2(int dev, int words, int nin, const void* const* ins, const int64_t* coef,
                 const void* b, int64_t nb, void* out0, void* out1, int64_t m, int nparties,
                 int which0, int which1, void* stream) {

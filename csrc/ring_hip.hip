@@ -112,6 +112,16 @@ __global__ void __launch_bounds__(256) k_binary_slot2(int op, Pair<T> p, int64_t
   }
 }
 
+// out = a + b + c (a reveal: the holder's two shares plus the received third)
+template <class T>
+__global__ void __launch_bounds__(256) k_add3(const T* __restrict__ a, const T* __restrict__ b,
+                                              const T* __restrict__ c, T* __restrict__ out,
+                                              int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = a[i] + b[i] + c[i];
+}
+
 // Share-wise linear combination of up to three replicated values, both share vectors in one
 // launch: out_y = sum_t coef[t] * in_t[y] (+ public b at party slot which[y], period nb).
 template <class T>
@@ -849,6 +859,17 @@ int mxh_ew_binary_slot2(int op, int words, const void* a0, const void* a1, const
               {which0, which1}};
     hipLaunchKernelGGL(k_binary_slot2<T>, dim3(grid_for(m * nparties), 2), dim3(kBlock), 0,
                        S(stream), op, p, nb, m, nparties);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mxh_ew_add3(int words, const void* a, const void* b, const void* c, void* out, int64_t n,
+                void* stream) {
+  if (n == 0) return 0;
+  DEV_DISPATCH(words, T, {
+    hipLaunchKernelGGL(k_add3<T>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream), (const T*)a,
+                       (const T*)b, (const T*)c, (T*)out, n);
     MX_LAUNCH_CHECK();
     return 0;
   });

@@ -34,6 +34,7 @@ _SIGS = {
                                    c_i64, c_int, c_int, c_int, c_vp]),
     "mx_mul_trunc3_kv": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
                                  c_vp, c_u64, c_int, c_vp, c_vp, c_vp]),
+    "mx_ew_add3": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "mx_lincomb2": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64,
                             c_int, c_int, c_int, c_vp]),
     "mx_sum_views2": (c_int, [c_int, c_int, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_vp,

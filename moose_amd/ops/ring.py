@@ -1061,6 +1061,17 @@ def binary_slot2(op: str, a0: RT, a1: RT, b: RT, which0: int, which1: int):
     return o0, o1
 
 
+def add3(a: RT, b: RT, c: RT) -> RT:
+    """a + b + c of one shape in one pass (mx_ew_add3)."""
+    if not (a.shape == b.shape == c.shape and a.bits == b.bits == c.bits) or a.bits == 1:
+        return binary("add", binary("add", a, b), c)
+    d = [t.data.contiguous() for t in (a, b, c)]
+    out = empty(a.shape, a.bits, a.device)
+    nat.check(nat.lib().mx_ew_add3(nat.dev_of(d[0]), _words(a.bits), *[nat.ptr(x) for x in d],
+                                   nat.ptr(out.data), a.numel(), nat.stream_of(d[0])), "add3")
+    return out
+
+
 def lincomb2(terms, b=None, which0: int = 0, which1: int = 2):
     """Share-wise sum_t coef_t * (s0_t, s1_t) of stacked [nparties, ...] share vectors (+ the
     public ``b`` at slots which0 / which1) in one launch (mx_lincomb2).  ``terms``: up to 3

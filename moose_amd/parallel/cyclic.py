@@ -350,5 +350,6 @@ class CyclicSession(StackedSession):
     # the single-GPU fused variants read other parties' data in-kernel: never used here
     p_mul_reshare = None
     p_zero_share_reshare = None
+    p_reveal = None  # the third share of a session lives on another GPU: generic move
     p_ks_level = None
     p_dot_zs_reshare = None

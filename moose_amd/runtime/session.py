@@ -290,6 +290,20 @@ class StackedSession(Session):
         a, b = R.slot_place2(v0, v1, h0, h1)
         return PV(plc, a), PV(plc, b)
 
+    def p_reveal(self, x, host):
+        """Reveal to a member P_j: its two shares plus the third (from P_{j+1}) summed in one
+        kernel; None for outsiders (generic)."""
+        if host not in x.plc.owners:
+            return None
+        v0, v1 = x.s0.v, x.s1.v
+        if not (isinstance(v0, R.RT) and isinstance(v1, R.RT)):
+            return None
+        j = x.plc.owners.index(host)
+        j1 = (j + 1) % 3
+        self.stats.record_send(x.plc.owners[j1], host, _nbytes(v1) // 3)
+        return HV(host, R.add3(R.RT(v0.data[j], v0.bits), R.RT(v1.data[j], v1.bits),
+                               R.RT(v1.data[j1], v1.bits)))
+
     def p_add_n(self, plc, xs):
         """Sum of replicated values ``xs`` [(PV s0, PV s1)] in one kernel when they are evenly
         spaced views of one stack (e.g. the products of a batched Dot); None otherwise."""
