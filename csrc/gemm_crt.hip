@@ -844,17 +844,34 @@ void launch_recon(const CPlan& p, const Tables& tb, int64_t batch, int64_t M, in
 struct Ws {
   void* ptr = nullptr;
   int64_t bytes = 0;
+  hipStream_t stream = nullptr;
+  bool used = false;
 };
 std::mutex g_mu;
-Ws g_ws[16];
+constexpr int kWsPerDev = 8;
+Ws g_ws[16][kWsPerDev];
 
-// grow-only per-device scratch; replaced buffers are retired (a captured graph may hold them)
-void* workspace(int64_t bytes) {
+// Grow-only scratch per (device, stream): GEMMs issued on different streams (dataflow lanes,
+// pipelined steps) may run concurrently and must not share residue buffers.  Up to
+// kWsPerDev streams per device get their own; further streams share the last slot (their
+// work is then ordered only by the caller).  Replaced buffers are retired, never freed (a
+// captured graph may hold them).
+void* workspace(int64_t bytes, hipStream_t st) {
   int dev = 0;
   hipGetDevice(&dev);
   if (dev < 0 || dev >= 16) return nullptr;
   std::lock_guard<std::mutex> lk(g_mu);
-  Ws& w = g_ws[dev];
+  Ws* slot = nullptr;
+  for (int i = 0; i < kWsPerDev && !slot; ++i)
+    if (g_ws[dev][i].used && g_ws[dev][i].stream == st) slot = &g_ws[dev][i];
+  for (int i = 0; i < kWsPerDev && !slot; ++i)
+    if (!g_ws[dev][i].used) {
+      slot = &g_ws[dev][i];
+      slot->used = true;
+      slot->stream = st;
+    }
+  if (!slot) slot = &g_ws[dev][kWsPerDev - 1];
+  Ws& w = *slot;
   if (w.bytes < bytes) {
     int64_t want = 1 << 20;
     while (want < bytes) want <<= 1;
@@ -876,7 +893,7 @@ int run_crt(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T
   if ((mode ? 2 * K : K) > (1 << 15)) return -6;  // exact epilogue rounding bound
   const Tables& tb = tables_for(words, p.n);
   const int64_t need = p.ra_bytes + (rb_pre ? 0 : p.rb_bytes) + p.cr_bytes;
-  int8_t* ws = (int8_t*)workspace(need);
+  int8_t* ws = (int8_t*)workspace(need, st);
   if (!ws) return -4;
   int8_t* ra = ws;
   int8_t* cr = ra + p.ra_bytes;

@@ -785,19 +785,32 @@ bool use_split_kernel() {
 struct Workspace {
   void* ptr = nullptr;
   int64_t bytes = 0;
-  int device = -1;
+  hipStream_t stream = nullptr;
+  bool used = false;
 };
 std::mutex g_ws_mu;
-Workspace g_ws[16];
+constexpr int kWsPerDev = 8;
+Workspace g_ws[16][kWsPerDev];
 
-// Grow-only per-device scratch.  A replaced buffer is retired, never freed: a captured
-// hipGraph may still reference it, and freeing would need a device-wide sync.
-void* get_workspace(int64_t bytes) {
+// Grow-only scratch per (device, stream) -- see gemm_crt.hip workspace(): concurrent GEMMs
+// on different streams get different buffers.  A replaced buffer is retired, never freed: a
+// captured hipGraph may still reference it, and freeing would need a device-wide sync.
+void* get_workspace(int64_t bytes, hipStream_t st) {
   int dev = 0;
   hipGetDevice(&dev);
   if (dev < 0 || dev >= 16) return nullptr;
   std::lock_guard<std::mutex> lk(g_ws_mu);
-  Workspace& w = g_ws[dev];
+  Workspace* slot = nullptr;
+  for (int i = 0; i < kWsPerDev && !slot; ++i)
+    if (g_ws[dev][i].used && g_ws[dev][i].stream == st) slot = &g_ws[dev][i];
+  for (int i = 0; i < kWsPerDev && !slot; ++i)
+    if (!g_ws[dev][i].used) {
+      slot = &g_ws[dev][i];
+      slot->used = true;
+      slot->stream = st;
+    }
+  if (!slot) slot = &g_ws[dev][kWsPerDev - 1];
+  Workspace& w = *slot;
   if (w.bytes < bytes) {
     int64_t want = 1 << 20;
     while (want < bytes) want <<= 1;
@@ -1039,7 +1052,7 @@ int mx_gemm_with_b(int words, int64_t batch, int64_t M, int64_t N, int64_t K, co
                           stream);
   if (K > max_k_chunk(words, mode)) return -6;
   Plan p = make_plan(words, batch, M, N, K, mode);
-  void* la = get_workspace(p.la_bytes);
+  void* la = get_workspace(p.la_bytes, (hipStream_t)stream);
   if (!la) return -4;
   hipStream_t st = (hipStream_t)stream;
   if (words == 1) {
@@ -1070,7 +1083,7 @@ int mx_gemm_strided(int words, int64_t batch, int64_t M, int64_t N, int64_t K, c
                                 mode, C, accumulate, stream);
   if (K > max_k_chunk(words, mode)) return -6;
   Plan p = make_plan(words, batch, M, N, K, mode);
-  void* ws = get_workspace(p.la_bytes + p.lb_bytes);
+  void* ws = get_workspace(p.la_bytes + p.lb_bytes, (hipStream_t)stream);
   if (!ws) return -4;
   int8_t* la = (int8_t*)ws;
   int8_t* lb = la + p.la_bytes;
@@ -1097,7 +1110,7 @@ int mxh_gemm_mfma(int words, int64_t batch, int64_t M, int64_t N, int64_t K, con
     return mxh_gemm_crt(words, batch, M, N, K, A0, A1, B0, B1, mode, C, accumulate, stream);
   if (K > max_k_chunk(words, mode)) return -6;  // caller splits long K
   int64_t bytes = mx_gemm_workspace_bytes(words, batch, M, N, K, mode);
-  void* ws = get_workspace(bytes);
+  void* ws = get_workspace(bytes, (hipStream_t)stream);
   if (!ws) return -4;
   return mx_gemm_ws(words, batch, M, N, K, A0, A1, B0, B1, mode, C, accumulate, ws, bytes,
                     stream);

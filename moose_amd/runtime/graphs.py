@@ -126,11 +126,14 @@ class GraphPlan:
                 self.static[k] = t
             else:
                 self.static[k] = v
-        # 1. warm-up (eager): first result + recorded uploads
+        # 1. warm-up (eager): first result + recorded uploads.  It runs on the stream (and
+        # the dataflow lanes) the capture will use, so per-stream GEMM workspaces are sized
+        # before the capture (no allocation while capturing)
+        stream = torch.cuda.Stream(self.device)
         rec = _Recorder()
         sess = StackedSession(self.device, seed=seed)
         interp = Interpreter(sess, storage, fixedpoint_ring, lanes=lanes)
-        with _upload_hook(rec):
+        with _upload_hook(rec), torch.cuda.stream(stream):
             outs = interp.run(comp, self.static)
             self.first = self._decode(interp, outs)
         self.stats = sess.stats
@@ -142,6 +145,7 @@ class GraphPlan:
         self.sess = StackedSession(self.device, seed=seed)
         self.sess.use_keytable(self.keys)
         self.interp = Interpreter(self.sess, storage, fixedpoint_ring, lanes=lanes)
+        self.interp.lanes = interp.lanes  # the warm-up's streams
         stager = _Stager(rec.items, self.device)
         torch.cuda.synchronize(self.device)
         # The evaluation is captured as a chain of graphs of SEGMENT_OPS logical ops each
@@ -149,7 +153,6 @@ class GraphPlan:
         # kernel nodes is slow to instantiate and has crashed the HIP runtime.
         self.graphs = []
         pool = torch.cuda.graph_pool_handle()
-        stream = torch.cuda.Stream(self.device)
         state = {"g": None, "n": 0}
 
         lanes = self.interp.lanes
