@@ -530,7 +530,7 @@ template <int WR, int WC, int BN, int MINW>
 __global__ void __launch_bounds__(64 * WR * WC, MINW)
     k_crt_gemm16(const int8_t* __restrict__ RA, const int8_t* __restrict__ RB,
                  int8_t* __restrict__ CR, int tiles_m, int tiles_n, int nkb, int gM,
-                 const EpiTab ep, int dma_mask, int bcast) {
+                 const EpiTab ep, int dma_mask, int bcast, int a_nkb, int roll) {
   constexpr int NW = WR * WC;
   constexpr int MI = BM / WR / 16, NJ = BN / WC / 16;
   constexpr int NM = MI * NJ;                    // MFMAs per wave per k-step
@@ -549,8 +549,20 @@ __global__ void __launch_bounds__(64 * WR * WC, MINW)
   const int tm = first_m + in_group % gm, tn = in_group / gm;
   const int g = blockIdx.y;
   const int mi = g % ep.n;
-  const int8_t* ga = RA + ((int64_t)((bcast & 1) ? mi : g) * tiles_m + tm) * nkb * (int64_t)kImg;
+  const int8_t* ga = RA + ((int64_t)((bcast & 1) ? mi : g) * tiles_m + tm) * a_nkb * (int64_t)kImg;
   const int8_t* gb = RB + ((int64_t)((bcast & 2) ? mi : g) * tiles_n + tn) * nkb * (int64_t)kImgB;
+  // roll != 0: A' = [x_b | x_{b+roll}] (an RSS pair whose second share is the next party's
+  // first) -- the image holds each batch entry's K residues once; k-blocks from a_nkb on
+  // read entry b + roll's image (ga2 is biased so that ga2 + kb * kImg addresses it)
+  const int8_t* ga2 = ga;
+  int khalf = 1 << 30;
+  if (roll) {
+    const int nbt = (int)gridDim.y / ep.n;
+    const int b2 = (g / ep.n + roll) % nbt;
+    ga2 = RA + ((int64_t)(b2 * ep.n + mi) * tiles_m + tm) * a_nkb * (int64_t)kImg -
+          (int64_t)a_nkb * kImg;
+    khalf = a_nkb;
+  }
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -560,6 +572,7 @@ __global__ void __launch_bounds__(64 * WR * WC, MINW)
   const int rowb = kImg + (wc * (BN / WC) + (lane & 15)) * BK + co;
 
   const int8_t* srcs[PPW];
+  const int8_t* srcs2[PPW];
   int dsts[PPW], steps[PPW];
 #pragma unroll
   for (int t = 0; t < PPW; ++t) {
@@ -567,12 +580,14 @@ __global__ void __launch_bounds__(64 * WR * WC, MINW)
     const bool is_b = pc >= 16;
     const int pp = is_b ? pc - 16 : pc;
     srcs[t] = (is_b ? gb : ga) + pp * 1024 + lane * 16;
+    srcs2[t] = (is_b ? gb : ga2) + pp * 1024 + lane * 16;
     dsts[t] = (is_b ? kImg : 0) + pp * 1024;
     steps[t] = is_b ? kImgB : kImg;
   }
   (void)dma_mask;
   auto dma = [&](int kb, int t, int8_t* dst_stage) {
-    __builtin_amdgcn_global_load_lds((const void*)(srcs[t] + (int64_t)kb * steps[t]),
+    const int8_t* src = kb >= khalf ? srcs2[t] : srcs[t];
+    __builtin_amdgcn_global_load_lds((const void*)(src + (int64_t)kb * steps[t]),
                                      (__attribute__((address_space(3))) void*)(dst_stage + dsts[t]),
                                      16, 0, 0);
   };
@@ -737,10 +752,12 @@ bool crt_mfma16() { return crt_kernel() >= 4; }
 
 struct CPlan {
   int n, bn;
-  int64_t tiles_m, tiles_n, nkb, ra_bytes, rb_bytes, cr_bytes;
+  int64_t tiles_m, tiles_n, nkb, a_nkb, ra_bytes, rb_bytes, cr_bytes;
 };
 
-CPlan make_cplan(int words, int64_t batch, int64_t M, int64_t N, int64_t K, int mode) {
+// roll: the A' image holds each batch entry's K residues once (k_crt_gemm16's roll)
+CPlan make_cplan(int words, int64_t batch, int64_t M, int64_t N, int64_t K, int mode,
+                 bool roll = false) {
   CPlan p;
   p.bn = (crt_kernel() == 3 || crt_kernel() == 5) ? 128 : 256;  // B tile columns
   const int64_t kprime = mode ? 2 * K : K;
@@ -748,7 +765,8 @@ CPlan make_cplan(int words, int64_t batch, int64_t M, int64_t N, int64_t K, int 
   p.tiles_m = (M + BM - 1) / BM;
   p.tiles_n = (N + p.bn - 1) / p.bn;
   p.nkb = round_up(kprime, BK) / BK;
-  p.ra_bytes = batch * p.n * p.tiles_m * p.nkb * (int64_t)kImg;
+  p.a_nkb = roll ? p.nkb / 2 : p.nkb;
+  p.ra_bytes = batch * p.n * p.tiles_m * p.a_nkb * (int64_t)kImg;
   p.rb_bytes = batch * p.n * p.tiles_n * p.nkb * (int64_t)(p.bn * BK);
   p.cr_bytes = batch * p.n * p.tiles_m * p.tiles_n * (int64_t)(BM * p.bn);
   return p;
@@ -763,20 +781,21 @@ int gemm_group_m() {
 template <class T>
 void launch_prep(const CPlan& p, const Tables& tb, bool is_b, int64_t batch, int64_t R,
                  int64_t K, int64_t xs, const T* X0, const T* X1, int mode, int8_t* out,
-                 hipStream_t st) {
+                 hipStream_t st, int64_t nkb = -1) {
+  if (nkb < 0) nkb = p.nkb;
   const int64_t tiles = is_b ? p.tiles_n : p.tiles_m;
   const int rows = is_b ? p.bn : BM;
-  const int64_t work = tiles * p.nkb * (rows * 4);
+  const int64_t work = tiles * nkb * (rows * 4);
   const dim3 grid((unsigned)std::min<int64_t>((work + 255) / 256, 16384), (unsigned)batch);
   if (!is_b)
     hipLaunchKernelGGL((k_crt_prep<T, false, BM>), grid, dim3(256), 0, st, X0, X1, R, K, xs, mode,
-                       out, tiles, p.nkb, tb.pa);
+                       out, tiles, nkb, tb.pa);
   else if (rows == 256)
     hipLaunchKernelGGL((k_crt_prep<T, true, 256>), grid, dim3(256), 0, st, X0, X1, R, K, xs, mode,
-                       out, tiles, p.nkb, tb.pb);
+                       out, tiles, nkb, tb.pb);
   else
     hipLaunchKernelGGL((k_crt_prep<T, true, 128>), grid, dim3(256), 0, st, X0, X1, R, K, xs, mode,
-                       out, tiles, p.nkb, tb.pb);
+                       out, tiles, nkb, tb.pb);
 }
 
 // MOOSEX_CRT_DMA_MASK (timing experiments, wrong results): bit 0 = stream A, bit 1 = B,
@@ -788,7 +807,7 @@ int dma_mask() {
 
 template <int WR, int WC, int BN, int MINW, bool M16>
 void launch_variant(const CPlan& p, const Tables& tb, int64_t batch, const int8_t* ra,
-                    const int8_t* rb, int8_t* cr, int bcast, hipStream_t st) {
+                    const int8_t* rb, int8_t* cr, int bcast, int roll, hipStream_t st) {
   constexpr int lds = kStages * (kImg + BN * BK);
   const void* fn = M16 ? (const void*)k_crt_gemm16<WR, WC, BN, MINW>
                        : (const void*)k_crt_gemm<WR, WC, BN, MINW>;
@@ -801,7 +820,7 @@ void launch_variant(const CPlan& p, const Tables& tb, int64_t batch, const int8_
   if constexpr (M16)
     hipLaunchKernelGGL((k_crt_gemm16<WR, WC, BN, MINW>), grid, dim3(64 * WR * WC), lds, st, ra,
                        rb, cr, (int)p.tiles_m, (int)p.tiles_n, (int)p.nkb, gemm_group_m(), tb.ep,
-                       dma_mask(), bcast);
+                       dma_mask(), bcast, (int)p.a_nkb, roll);
   else
     hipLaunchKernelGGL((k_crt_gemm<WR, WC, BN, MINW>), grid, dim3(64 * WR * WC), lds, st, ra, rb,
                        cr, (int)p.tiles_m, (int)p.tiles_n, (int)p.nkb, gemm_group_m(), tb.ep,
@@ -809,14 +828,14 @@ void launch_variant(const CPlan& p, const Tables& tb, int64_t batch, const int8_
 }
 
 void launch_crt_gemm(const CPlan& p, const Tables& tb, int64_t batch, const int8_t* ra,
-                     const int8_t* rb, int8_t* cr, int bcast, hipStream_t st) {
-  switch (crt_kernel()) {
-    case 1: launch_variant<2, 2, 256, 1, false>(p, tb, batch, ra, rb, cr, bcast, st); break;
-    case 2: launch_variant<2, 4, 256, 2, false>(p, tb, batch, ra, rb, cr, bcast, st); break;
-    case 4: launch_variant<2, 2, 256, 1, true>(p, tb, batch, ra, rb, cr, bcast, st); break;
-    case 3: launch_variant<2, 2, 128, 2, false>(p, tb, batch, ra, rb, cr, bcast, st); break;
-    case 6: launch_variant<2, 4, 256, 2, true>(p, tb, batch, ra, rb, cr, bcast, st); break;
-    default: launch_variant<2, 2, 128, 2, true>(p, tb, batch, ra, rb, cr, bcast, st); break;
+                     const int8_t* rb, int8_t* cr, int bcast, int roll, hipStream_t st) {
+  switch (crt_kernel()) {  // roll: 16x16x64 kernels only (run_crt checks)
+    case 1: launch_variant<2, 2, 256, 1, false>(p, tb, batch, ra, rb, cr, bcast, 0, st); break;
+    case 2: launch_variant<2, 4, 256, 2, false>(p, tb, batch, ra, rb, cr, bcast, 0, st); break;
+    case 4: launch_variant<2, 2, 256, 1, true>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
+    case 3: launch_variant<2, 2, 128, 2, false>(p, tb, batch, ra, rb, cr, bcast, 0, st); break;
+    case 6: launch_variant<2, 4, 256, 2, true>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
+    default: launch_variant<2, 2, 128, 2, true>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
   }
 }
 
@@ -886,9 +905,13 @@ void* workspace(int64_t bytes, hipStream_t st) {
 template <class T>
 int run_crt(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T* A1,
             int64_t a_bstride, const T* B0, const T* B1, int64_t b_bstride,
-            const int8_t* rb_pre, int mode, T* C, int accumulate, hipStream_t st) {
+            const int8_t* rb_pre, int mode, T* C, int accumulate, hipStream_t st,
+            int64_t roll = 0) {
   constexpr int words = sizeof(T) / 8;
-  const CPlan p = make_cplan(words, batch, M, N, K, mode);
+  if (roll && (mode != 1 || K % BK || !crt_mfma16() || a_bstride == 0 || batch < 2 ||
+               roll % batch == 0))
+    return -7;  // not applicable: the caller runs the two-operand form
+  const CPlan p = make_cplan(words, batch, M, N, K, mode, roll != 0);
   if (p.n < 0) return -6;
   if ((mode ? 2 * K : K) > (1 << 15)) return -6;  // exact epilogue rounding bound
   const Tables& tb = tables_for(words, p.n);
@@ -907,8 +930,12 @@ int run_crt(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T
     launch_prep<T>(p, tb, true, b_bc ? 1 : batch, N, K, b_bstride, B0, B1, mode, rbw, st);
     rb = rbw;
   }
-  launch_prep<T>(p, tb, false, a_bc ? 1 : batch, M, K, a_bstride, A0, A1, mode, ra, st);
-  launch_crt_gemm(p, tb, batch, ra, rb, cr, (a_bc ? 1 : 0) | (b_bc ? 2 : 0), st);
+  if (roll)  // each entry's own K residues; the GEMM reads entry b + roll's for the 2nd half
+    launch_prep<T>(p, tb, false, batch, M, K, a_bstride, A0, A0, 0, ra, st, p.a_nkb);
+  else
+    launch_prep<T>(p, tb, false, a_bc ? 1 : batch, M, K, a_bstride, A0, A1, mode, ra, st);
+  launch_crt_gemm(p, tb, batch, ra, rb, cr, (a_bc ? 1 : 0) | (b_bc ? 2 : 0),
+                  (int)(((roll % batch) + batch) % batch), st);
   launch_recon<T>(p, tb, batch, M, N, cr, C, accumulate, st);
   const hipError_t e = hipGetLastError();
   return e != hipSuccess ? -100 - (int)e : 0;
@@ -977,6 +1004,25 @@ int mxh_gemm_crt_strided(int words, int64_t batch, int64_t M, int64_t N, int64_t
     return run_crt<u128>(batch, M, N, K, (const u128*)A0, (const u128*)A1, a_bstride,
                          (const u128*)B0, (const u128*)B1, b_bstride, nullptr, mode, (u128*)C,
                          accumulate, st);
+  return -2;
+}
+
+// RSS pair form of the mode-1 product: A1 is A0 rolled by ``roll`` batch entries
+// (A1[b] = A0[(b + roll) % batch], as the second shares of a stacked replicated sharing are
+// the next party's first), so A' residues are prepared once per share instead of twice.
+// rb: prepared B' (mxh_crt_prep_b) or null (then B0, B1).  -7: not applicable.
+int mxh_crt_roll(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
+                 int64_t a_bstride, int64_t roll, const void* B0, const void* B1, const void* rb,
+                 void* C, int accumulate, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t bs = K * N;
+  if (words == 1)
+    return run_crt<u64>(batch, M, N, K, (const u64*)A0, nullptr, a_bstride, (const u64*)B0,
+                        (const u64*)B1, bs, (const int8_t*)rb, 1, (u64*)C, accumulate, st, roll);
+  if (words == 2)
+    return run_crt<u128>(batch, M, N, K, (const u128*)A0, nullptr, a_bstride, (const u128*)B0,
+                         (const u128*)B1, bs, (const int8_t*)rb, 1, (u128*)C, accumulate, st,
+                         roll);
   return -2;
 }
 

@@ -968,6 +968,10 @@ extern "C" int mxh_gemm_crt_strided(int words, int64_t batch, int64_t M, int64_t
 extern "C" int mxh_crt_with_b(int words, int64_t batch, int64_t M, int64_t N, int64_t K,
                               const void* A0, const void* A1, int64_t a_bstride, int mode,
                               const void* rb, void* C, int accumulate, void* stream);
+extern "C" int mxh_crt_roll(int words, int64_t batch, int64_t M, int64_t N, int64_t K,
+                            const void* A0, int64_t a_bstride, int64_t roll, const void* B0,
+                            const void* B1, const void* rb, void* C, int accumulate,
+                            void* stream);
 
 namespace {
 // 0 = auto (CRT for products with at least one full 256x256 output tile and K' >= 512),
@@ -1070,6 +1074,18 @@ int mx_gemm_with_b(int words, int64_t batch, int64_t M, int64_t N, int64_t K, co
   }
   hipError_t e = hipGetLastError();
   return e != hipSuccess ? -100 - (int)e : 0;
+}
+
+// Mode-1 product whose second A operand is the first rolled over the batch (a stacked RSS
+// pair: A1[b] = A0[(b + roll) % batch]); lb: prepared B' (mx_gemm_prep_b) or null.  Runs
+// on the CRT GEMM only; -7 (the caller falls back to the two-operand form) otherwise.
+int mx_gemm_roll(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
+                 int64_t a_bstride, int64_t roll, const void* B0, const void* B1, const void* lb,
+                 void* C, int accumulate, void* stream) {
+  if (M == 0 || N == 0 || batch == 0) return 0;
+  if ((words != 1 && words != 2) || !use_crt(lb ? 256 : M, N, K, 1)) return -7;
+  return mxh_crt_roll(words, batch, M, N, K, A0, a_bstride, roll, B0, B1, lb, C, accumulate,
+                      stream);
 }
 
 // Batched product with explicit batch strides (elements) for A and B (0 broadcasts).

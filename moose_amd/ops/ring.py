@@ -735,6 +735,40 @@ def dot_cross_rows(x0: RT, x1: RT, r0: int, r1: int, pb: PreparedCross) -> RT:
     return out
 
 
+def dot_cross_pair(x0: RT, y0: RT, y1: RT, roll: int, pb: PreparedCross = None, r0=0,
+                   r1=None):
+    """dot_cross(x0, x1, y0, y1) for a stacked RSS pair whose second share is the first
+    rolled over the flattened batch (x1[b] = x0[(b + roll) % batch]): the CRT GEMM prepares
+    each share's residues once and reads them for both K halves.  Rows [r0, r1) of x0 only
+    when given.  None when the device path does not apply (the caller runs dot_cross)."""
+    d0 = x0.data
+    if not d0.is_cuda or len(x0.shape) != 3:
+        return None
+    if not d0.is_contiguous():
+        d0 = d0.contiguous()
+    batch, M, K = x0.shape
+    r1 = M if r1 is None else r1
+    bits = x0.bits
+    el = 2 if bits == 128 else 1
+    if pb is not None:
+        if pb.lb is None:
+            return None
+        N, lb, b0, b1 = pb.N, nat.ptr(pb.lb), None, None
+    else:
+        N = y0.shape[2]
+        b0, b1 = y0.data.contiguous(), y1.data.contiguous()
+        lb = None
+    out = empty((batch, r1 - r0, N), bits, d0.device)
+    rc = nat.lib().mx_gemm_roll(
+        _words(bits), batch, r1 - r0, N, K, ctypes.c_void_p(d0.data_ptr() + r0 * K * el * 8),
+        M * K, roll, None if b0 is None else nat.ptr(b0), None if b1 is None else nat.ptr(b1),
+        lb, nat.ptr(out.data), 0, nat.stream_of(d0))
+    if rc == -7:
+        return None
+    nat.check(rc, "gemm_roll")
+    return out
+
+
 def _party_batch_strides(t: RT):
     """(party stride, batch stride) in ring elements of a [P, B, *inner] device tensor whose
     inner dims are contiguous (e.g. an expanded, stride-0 stack of one operand); None if

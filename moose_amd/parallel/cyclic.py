@@ -136,6 +136,7 @@ class CyclicSession(StackedSession):
     is_simulated = False
     fused = False      # the single-GPU whole-protocol kernels assume all parties local
     ks_fused = False
+    pair_rolled = False  # component p + 1 of a stack is another session's party
     KEY_SLOTS = 9      # per placement: for each component p: k_p, k_{p+1}, k_all
 
     def __init__(self, comm: RingComm, offsets: Dict[str, int], device="cpu", seed=None,

@@ -483,7 +483,15 @@ class StackedSession(Session):
         """The B' operand of p_dot_cross, limb-split once for several row blocks."""
         return R.PreparedCross(y0.v, y1.v)
 
+    # every party of a session on this device: a pair's second share vector is its first
+    # rolled by one party (s1[p] = s0[p + 1]), so the CRT GEMM needs the residues of s0 only
+    pair_rolled = os.environ.get("MOOSEX_PAIR_ROLL", "1") != "0"
+
     def p_dot_cross_rows(self, plc, x0, x1, r0, r1, prepared):
+        if self.pair_rolled:
+            v = R.dot_cross_pair(x0.v, None, None, 1, pb=prepared, r0=r0, r1=r1)
+            if v is not None:
+                return PV(plc, v)
         return PV(plc, R.dot_cross_rows(x0.v, x1.v, r0, r1, prepared))
 
     def p_dot_cross(self, plc, x0, x1, y0, y1, nbatch=0):
@@ -504,10 +512,13 @@ class StackedSession(Session):
                     pb = R.PreparedCross(yv0, yv1)
                     cache[key] = (yv0.data, yv1.data, pb)
                 if pb.lb is not None:
-                    M = x0.v.shape[1]
-                    return PV(plc, R.dot_cross_rows(x0.v, x1.v, 0, M, pb))
+                    return self.p_dot_cross_rows(plc, x0, x1, 0, x0.v.shape[1], pb)
             elif len(cache) < 64:
                 cache[key] = (yv0.data, yv1.data, None)  # holds the tensors: ids stay unique
+        if nbatch == 0 and self.pair_rolled and self.device.type == "cuda":
+            v = R.dot_cross_pair(x0.v, yv0, yv1, 1)
+            if v is not None:
+                return PV(plc, v)
         return PV(plc, R.dot_cross(x0.v, x1.v, y0.v, y1.v, nb=1 + nbatch))
 
     def p_add_zero_share(self, plc, z, kind="arith"):

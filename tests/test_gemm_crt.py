@@ -254,3 +254,27 @@ def test_gpu_dot_cross_broadcast_views(bits, crt, both):
         want = R.dot_cross(R.RT(view(xs[0]).data.contiguous(), bits),
                            R.RT(view(xs[1]).data.contiguous(), bits), *dense, nb=2)
     same(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [64, 128])
+@pytest.mark.parametrize("K", [320, 300])
+def test_gpu_dot_cross_pair_rolled(bits, K):
+    """An RSS pair (x1 = x0 rolled by one party) through the rolled CRT GEMM (each share's
+    residues prepared once) equals the two-operand product; K not a multiple of the k-block
+    falls back (None).  Also with a prepared B' and row blocks."""
+    M, N = 300, 280
+    x0 = gpu(rand_rt((3, M, K), bits, 110))
+    x1 = R.RT(torch.roll(x0.data, -1, dims=0).contiguous(), bits)
+    ys = [gpu(rand_rt((3, K, N), bits, 111 + i)) for i in range(2)]
+    with _crt(1):
+        want = R.dot_cross(x0, x1, *ys, nb=1)
+        got = R.dot_cross_pair(x0, ys[0], ys[1], 1)
+        pb = R.PreparedCross(*ys)
+        rows = [R.dot_cross_pair(x0, None, None, 1, pb=pb, r0=r0, r1=min(M, r0 + 128))
+                for r0 in range(0, M, 128)]
+    if K % 64:
+        assert got is None and all(r is None for r in rows)
+        return
+    same(want, got)
+    assert torch.equal(torch.cat([r.data for r in rows], dim=1).cpu(), want.data.cpu())
