@@ -679,9 +679,10 @@ __global__ void __launch_bounds__(256) k_mul_trunc3_lat(
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
           const int q = p == 2 ? 0 : p + 1;
-          const T v = mxr::cross<T>(MX_CROSS_ARITH, ld_view(x0, vw, 0, p, e, n),
-                                    ld_view(x1, vw, 1, p, e, n), ld_view(y0, vw, 2, p, e, n),
-                                    ld_view(y1, vw, 3, p, e, n), true, true);
+          const T v = y0 == nullptr ? ld_view(x0, vw, 0, p, e, n)
+                      : mxr::cross<T>(MX_CROSS_ARITH, ld_view(x0, vw, 0, p, e, n),
+                                      ld_view(x1, vw, 1, p, e, n), ld_view(y0, vw, 2, p, e, n),
+                                      ld_view(y1, vw, 3, p, e, n), true, true);
           z[p] = mxr::zs_combine<T>(MX_CROSS_ARITH, v, pick<T>(kl[p][tid], kh[p][tid], j),
                                     pick<T>(kl[q][tid], kh[q][tid], j));
         }
@@ -701,6 +702,57 @@ __global__ void __launch_bounds__(256) k_mul_trunc3_lat(
     }
     __syncthreads();
   }
+}
+
+// Throughput form of k_mul_trunc3_lat: one ChaCha block of each of the nine streams per
+// thread (walk_chunks), same shares.  y0 == nullptr: x0 already holds the three parties'
+// local products (a GEMM's) -- the zero share + reshare + TruncPr tail of a fixed-point dot
+// in one pass, the reshared product never written.
+template <class T>
+__global__ void __launch_bounds__(256) k_mul_trunc3(
+    const T* __restrict__ x0, const T* __restrict__ x1, const T* __restrict__ y0,
+    const T* __restrict__ y1, T* __restrict__ out0, T* __restrict__ out1, int64_t n, int64_t os,
+    KeySrc keys, uint64_t nmul, int m, uint64_t nr0, uint64_t nr1, uint64_t nt, uint64_t nm,
+    uint64_t nz0, uint64_t nz2, Views vw) {
+  __shared__ uint32_t rks[3][kKeyWords];
+  stage_keys(rks, keys, 3);
+  constexpr int P = Lane<T>::kPer;
+  const int64_t nb = (n + P - 1) / P;
+  // streams as k_mul_trunc3_lat: product zero share (k0, k1, k2), r0 (k0), r1 (k2), t (k0),
+  // m (k0), z0 (k0), z2 (k2)
+  const uint32_t* const key[9] = {rks[0], rks[1], rks[2], rks[0], rks[2],
+                                  rks[0], rks[0], rks[0], rks[2]};
+  const uint64_t nonce[9] = {nmul, nmul, nmul, nr0, nr1, nt, nm, nz0, nz2};
+  mxd::walk_chunks<9>(nb, key, nonce, [&](int64_t b, const uint64_t (&lo)[9],
+                                          const uint64_t (&hi)[9]) {
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const int64_t e = b * P + j;
+      if (e >= n) break;
+      T z[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const int q = p == 2 ? 0 : p + 1;
+        const T v = y0 == nullptr ? ld_view(x0, vw, 0, p, e, n)
+                    : mxr::cross<T>(MX_CROSS_ARITH, ld_view(x0, vw, 0, p, e, n),
+                                    ld_view(x1, vw, 1, p, e, n), ld_view(y0, vw, 2, p, e, n),
+                                    ld_view(y1, vw, 3, p, e, n), true, true);
+        z[p] = mxr::zs_combine<T>(MX_CROSS_ARITH, v, pick<T>(lo[p], hi[p], j),
+                                  pick<T>(lo[q], hi[q], j));
+      }
+      const T Z0 = pick<T>(lo[7], hi[7], j);
+      const T Z2 = pick<T>(lo[8], hi[8], j);
+      const T Z1 = mxf::trunc_pr_z1<T>(z[0], z[1], z[2], pick<T>(lo[3], hi[3], j),
+                                       pick<T>(lo[4], hi[4], j), pick<T>(lo[5], hi[5], j),
+                                       pick<T>(lo[6], hi[6], j), Z0, Z2, m);
+      out0[e] = Z0;
+      out0[os + e] = Z1;
+      out0[2 * os + e] = Z2;
+      out1[e] = Z1;
+      out1[os + e] = Z2;
+      out1[2 * os + e] = Z0;
+    }
+  });
 }
 
 template <class T>
@@ -1194,8 +1246,8 @@ int mxh_rss_mul3_kv(int kind, int words, const void* x0, const void* x1, const v
                           mxd::keysrc_slots(ptrs, 3), nonce, stream, out1, 0, &vw);
 }
 
-// k_mul_trunc3_lat: latency-bound launches only (returns 1 -- "not handled" -- above the
-// size where the separate throughput kernels win).  views: {ps[4], per[4]} or null.
+// k_mul_trunc3_lat for latency-bound launches, k_mul_trunc3 above.  x1 == y0 == y1 == null:
+// x0 holds the parties' local products (the dot's tail).  views: {ps[4], per[4]} or null.
 int mxh_mul_trunc3_kv(int words, const void* x0, const void* x1, const void* y0, const void* y1,
                       void* out0, void* out1, int64_t n, int64_t ostride, const uint32_t* slots,
                       uint64_t nmul, int m, const uint64_t* nn, const int64_t* views,
@@ -1214,7 +1266,14 @@ int mxh_mul_trunc3_kv(int words, const void* x0, const void* x1, const void* y0,
   DEV_DISPATCH(words, T, {
     constexpr int P = 16 / (int)sizeof(T);
     const int64_t blocks = (n + P - 1) / P;
-    if (blocks > 8192) return 1;
+    if (blocks > 8192) {
+      hipLaunchKernelGGL(k_mul_trunc3<T>, dim3(mxd::grid_for_chunks(blocks)), dim3(kBlock), 0,
+                         S(stream), (const T*)x0, (const T*)x1, (const T*)y0, (const T*)y1,
+                         (T*)out0, (T*)out1, n, ostride, mxd::keysrc_slots(ptrs, 3), nmul, m,
+                         nn[0], nn[1], nn[2], nn[3], nn[4], nn[5], vw);
+      MX_LAUNCH_CHECK();
+      return 0;
+    }
     constexpr int EPB = 256 / 9;
     const int64_t g = (blocks + EPB - 1) / EPB;
     hipLaunchKernelGGL(k_mul_trunc3_lat<T>, dim3((unsigned)g), dim3(kBlock), 0, S(stream),

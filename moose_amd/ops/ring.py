@@ -1028,6 +1028,31 @@ def mul_trunc3_k(x0: RT, x1: RT, y0: RT, y1: RT, slot_ptr: int, nmul: int, m: in
     return o0, o1
 
 
+def zs_trunc3_k(z: RT, slot_ptr: int, nmul: int, m: int, nonces):
+    """Zero share + reshare + TruncPr of three stacked parties' local products ``z``
+    ([3, ...], e.g. a dot's GEMM output) in one kernel (mx_mul_trunc3_kv with the product
+    given): bitwise ``trunc_pr3(rss_mul3_k(arith, z))`` -- the reshared product is never
+    written.  Returns (s0, s1), or None on the host."""
+    bits = z.bits
+    if not z.data.is_cuda or bits not in (64, 128):
+        return None
+    d = z.data.contiguous()
+    shp = z.shape
+    n = math.prod(shp) // 3
+    if n == 0:
+        return None
+    o0, o1 = empty2(shp, bits, d.device)
+    nn = (ctypes.c_uint64 * 6)(*[v & MASK64 for v in nonces])
+    rc = nat.lib().mx_mul_trunc3_kv(
+        nat.dev_of(d), _words(bits), nat.ptr(d), None, None, None, nat.ptr(o0.data),
+        nat.ptr(o1.data), n, n, ctypes.c_void_p(slot_ptr), nmul & MASK64, int(m), nn, None,
+        nat.stream_of(d))
+    if rc == 1:
+        return None
+    nat.check(rc, "zs_trunc3")
+    return o0, o1
+
+
 def add_zs3(v: RT, r: RT):
     """Stacked arith zero share from precomputed keystreams ``r`` (= PRF(k_p) per party)
     plus the reshare: returns (s0, s1) exactly like ``rss_mul3_k(arith, v)``."""

@@ -33,6 +33,7 @@ instead of k bit tensors (reference bits.rs stacks a [k, ...] bit array).
 from __future__ import annotations
 
 from dataclasses import dataclass
+import os
 
 import torch
 
@@ -409,6 +410,14 @@ def dot_trunc(sess, x: RepTensor, y: RepTensor, m: int) -> RepTensor:
             M = xs[1]
             nchunk = min(chunks, M // 128)
     if nchunk <= 1:
+        tail = getattr(sess, "p_zs_trunc", None)
+        if (tail is not None and m and x.kind == "arith" and getattr(sess, "fused", False)
+                and getattr(sess, "device", None) is not None and sess.device.type == "cuda"
+                and os.environ.get("MOOSEX_DOT_TAIL", "1") != "0"):
+            with span("rep.dot_trunc_fused"):
+                v = sess.p_dot_cross(x.plc, x.s0, x.s1, y.s0, y.s1)
+                s0, s1 = tail(x.plc, v, m)  # zero share + reshare + TruncPr: one kernel
+                return RepTensor(x.plc, x.bits, "arith", s0, s1)
         return trunc_pr(sess, dot(sess, x, y), m)
     with span("rep.dot_trunc_pipelined"):
         plc, bits, kind = x.plc, x.bits, x.kind

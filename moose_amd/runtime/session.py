@@ -432,6 +432,22 @@ class StackedSession(Session):
         self._trunc_traffic(x0, nbytes // 3)
         return PV(plc, r[0]), PV(plc, r[1])
 
+    def p_zs_trunc(self, plc, z, m):
+        """The tail of a fixed-point dot in one kernel (device): rep.dot's zero share and
+        reshare of the local products ``z`` and rep.trunc_pr of the result -- the same
+        nonces in the same order as the two steps, so the same shares.  None on the host."""
+        if self.device.type != "cuda" or z.v.bits not in (64, 128) or not m:
+            return None
+        nmul = self.nonce(plc)
+        nonces = tuple(self.nonce(plc) for _ in range(6))
+        r = R.zs_trunc3_k(z.v, self.key_ptr(plc, 0), nmul, m, nonces)
+        if r is None:  # nonces are drawn: never fall back silently
+            raise RuntimeError("zs_trunc3 declined on a device session")
+        nbytes = _nbytes(r[0])
+        self.stats.record_round(nbytes)
+        self._trunc_traffic(z, nbytes // 3)
+        return PV(plc, r[0]), PV(plc, r[1])
+
     def p_ks_level(self, plc, g0, g1, p0, p1, d, both):
         """One Kogge-Stone level of rep.binary_adder (AND(s) + reshare + xor) in one
         kernel; consumes the one nonce of the generic level's AND round."""

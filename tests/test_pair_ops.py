@@ -167,3 +167,27 @@ def test_mul_public_trunc_matches_two_steps(dev, bits):
     b = rep.trunc_pr(s2, rep.mul_public(s2, X, c), 20)
     _eq(a.s0.v, b.s0.v)
     _eq(a.s1.v, b.s1.v)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [64, 128])
+@pytest.mark.parametrize("mnk", [(6, 9, 5), (150, 40, 160)])
+def test_dot_tail_fused_matches_two_steps(bits, mnk, monkeypatch):
+    """rep.dot_trunc's one-kernel tail (zero share + reshare + TruncPr of the GEMM output,
+    mx_mul_trunc3_kv with the product given; latency and throughput kernels) gives exactly
+    the shares of rep.dot followed by rep.trunc_pr."""
+    plc = ReplicatedPlacement(("alice", "bob", "carole"))
+    M, K, N = mnk
+    x0 = _rand((3, M, K), bits, "cuda", 61)
+    y0 = _rand((3, K, N), bits, "cuda", 62)
+    roll = lambda t: R.RT(torch.roll(t.data, -1, dims=0).contiguous(), bits)  # noqa: E731
+    X = rep.RepTensor(plc, bits, "arith", PV(plc, x0), PV(plc, roll(x0)))
+    Y = rep.RepTensor(plc, bits, "arith", PV(plc, y0), PV(plc, roll(y0)))
+    s1, s2 = StackedSession("cuda", seed=5), StackedSession("cuda", seed=5)
+    a = rep.dot_trunc(s1, X, Y, 20)
+    monkeypatch.setenv("MOOSEX_DOT_TAIL", "0")
+    b = rep.dot_trunc(s2, X, Y, 20)
+    _eq(a.s0.v, b.s0.v)
+    _eq(a.s1.v, b.s1.v)
+    # the unfused pair is a valid sharing: s1 is s0 rolled by one party
+    _eq(roll(a.s0.v), a.s1.v)
