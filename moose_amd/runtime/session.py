@@ -25,7 +25,6 @@ and k_{p+1}, so PRF(k_s) is computable by exactly the two holders of slot s) and
 """
 from __future__ import annotations
 
-import math
 import os
 from dataclasses import dataclass
 from typing import Any
@@ -402,16 +401,15 @@ class StackedSession(Session):
         return PV(plc, s0), PV(plc, s1)
 
     def p_mul_trunc(self, plc, x0, x1, y0, y1, m, out=None):
-        """rep.mul + rep.trunc_pr (arith) in one latency kernel when the launch is small
-        (device); None -> the caller runs the two protocol steps.  Draws the same nonces
-        in the same order as the two steps."""
+        """rep.mul + rep.trunc_pr (arith) in one kernel (device: the latency form for small
+        launches, the throughput form above); None -> the caller runs the two protocol
+        steps.  Draws the same nonces in the same order as the two steps."""
         if self.device.type != "cuda":
             return None
         v = [t.v for t in (x0, x1, y0, y1)]
         if not all(isinstance(t, R.RT) for t in v) or v[0].bits not in (64, 128):
             return None
-        if any(t.shape != v[0].shape for t in v) or math.prod(v[0].shape) // 3 > 8192 * (
-                1 if v[0].bits == 128 else 2):
+        if any(t.shape != v[0].shape for t in v):
             return None
         if any(not t.data.is_contiguous() and R._party_view(t) is None for t in v):
             return None

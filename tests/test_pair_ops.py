@@ -100,15 +100,17 @@ def test_slot_ops_broadcast_trailing_vector(dev, bits):
 @pytest.mark.gpu
 @pytest.mark.parametrize("bits", [64, 128])
 @pytest.mark.parametrize("layout", ["dense", "views"])
-def test_mul_trunc_fused_matches_two_steps(bits, layout):
-    """rep.mul_trunc's single kernel (mx_mul_trunc3_kv) produces exactly the shares of
-    rep.mul followed by rep.trunc_pr (same keys, same nonce order)."""
+@pytest.mark.parametrize("cols", [50, 3000])
+def test_mul_trunc_fused_matches_two_steps(bits, layout, cols):
+    """rep.mul_trunc's single kernel (mx_mul_trunc3_kv; latency form, and the throughput
+    form at 18000 elements per party) produces exactly the shares of rep.mul followed by
+    rep.trunc_pr (same keys, same nonce order)."""
     plc = ReplicatedPlacement(("alice", "bob", "carole"))
-    shp = (3, 6, 50)
+    shp = (3, 6, cols)
     xs = [_rand(shp, bits, "cuda", s) for s in (21, 22)]
     ys = [_rand(shp, bits, "cuda", s) for s in (23, 24)]
     if layout == "views":  # row slices of larger stacks, read in place
-        xs = [R.RT(R.zeros((3, 9, 50), bits, "cuda").data, bits) for _ in range(2)]
+        xs = [R.RT(R.zeros((3, 9, cols), bits, "cuda").data, bits) for _ in range(2)]
         for i, s in enumerate((21, 22)):
             xs[i].data[:, 2:8] = _rand(shp, bits, "cuda", s).data
         xs = [R.RT(x.data[:, 2:8], bits) for x in xs]
