@@ -97,11 +97,21 @@ struct RecTab {  // reconstruction
   uint16_t Mw[8];          // M mod 2^w
 };
 
+// Reconstruction by v_dot4_i32_i8 over groups of 4 moduli: W_i and R_i = round(2^24 / p_i)
+// as signed base-256 digits, packed per (group, digit) with modulus 4g + u in byte u, so one
+// dot4 of an element's 4 residues with one (uniform, SGPR) word adds that digit's 4 terms.
+struct RecTab4 {
+  int groups;
+  uint32_t wd[kMaxMod / 4][16];
+  uint32_t rd[kMaxMod / 4][3];
+};
+
 struct Tables {
   int words = 0, n = 0;
   PrepTab pa, pb;
   EpiTab ep;
   RecTab rc;
+  RecTab4 r4;
 };
 
 int modinv(int a, int m) {
@@ -174,6 +184,29 @@ void build_tables(int words, int n, Tables& t) {
     }
   }
   for (int k = 0; k < 8; ++k) t.rc.Mw[k] = (uint16_t)(Mw >> (16 * k));
+  std::memset(&t.r4, 0, sizeof t.r4);
+  t.r4.groups = (n + 3) / 4;
+  for (int i = 0; i < n; ++i) {
+    u128 W = 0;
+    for (int k = 0; k < 8; ++k) W |= (u128)t.rc.W[i][k] << (16 * k);
+    int carry = 0;
+    for (int d = 0; d < nbytes; ++d) {  // W mod 2^w in signed digits (carry out dropped)
+      int b = (int)((W >> (8 * d)) & 0xff) + carry;
+      carry = b >= 128;
+      b -= 256 * carry;
+      t.r4.wd[i / 4][d] |= (uint32_t)(uint8_t)(int8_t)b << (8 * (i % 4));
+    }
+    int R = (int)std::lround(16777216.0 / kModuli[i]);
+    for (int d = 0; d < 3; ++d) {  // R < 2^24: exact in three signed digits
+      int b = (R & 0xff);
+      R >>= 8;
+      if (b >= 128) {
+        b -= 256;
+        R += 1;
+      }
+      t.r4.rd[i / 4][d] |= (uint32_t)(uint8_t)(int8_t)b << (8 * (i % 4));
+    }
+  }
   (void)wbits;
 }
 
@@ -736,6 +769,90 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// k_crt_recon16 with the per-modulus multiply-adds done as v_dot4_i32_i8: a thread's 4
+// elements x 4 moduli of residues (4 dwords, one per modulus plane) are transposed with 8
+// v_perm_b32 into one dword of 4 moduli per element, then one dot4 per (element, W digit)
+// and per (element, R digit) -- 19 dot4 for 4 moduli instead of 4 x (8 multiply-adds + a
+// float convert and fma).  q = round(sum_i c_i R_i / 2^24) (error <= 36 * 128 / 2^25, far
+// inside the 0.05 rounding margin of |Z| <= 0.45 M).  Same output as k_crt_recon16.
+template <class T, int BN>
+__global__ void __launch_bounds__(256)
+    k_crt_recon16d(const int8_t* __restrict__ CR, T* __restrict__ C, int64_t M, int64_t N,
+                   int64_t tiles_m, int64_t tiles_n, int accumulate, const RecTab4 r4, int n,
+                   const RecTab rc) {
+  constexpr int ND = (int)sizeof(T);  // W digits
+  constexpr int NK = ND / 2;
+  constexpr int kCrTile = BM * BN, NBJ = BN / 16;
+  const int64_t ntiles = tiles_m * tiles_n;
+  const int64_t total = ntiles * (kCrTile / 4);
+  const int64_t b = blockIdx.y;
+  for (int64_t gt = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; gt < total;
+       gt += (int64_t)gridDim.x * blockDim.x) {
+    const int lane = (int)(gt & 63);
+    const int64_t rest = gt >> 6;
+    const int blk = (int)(rest % (16 * NBJ));
+    const int64_t tile = rest / (16 * NBJ);
+    const int64_t off = tile * kCrTile + (blk * 64 + lane) * 4;
+    int acc[4][ND], aq[4][3];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+#pragma unroll
+      for (int d = 0; d < ND; ++d) acc[e][d] = 0;
+#pragma unroll
+      for (int d = 0; d < 3; ++d) aq[e][d] = 0;
+    }
+    const int8_t* src = CR + b * n * ntiles * (int64_t)kCrTile + off;
+    const int64_t pstride = ntiles * (int64_t)kCrTile;
+    for (int g = 0; g < r4.groups; ++g) {
+      uint32_t v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        v[u] = 4 * g + u < n ? *(const uint32_t*)(src + (4 * g + u) * pstride) : 0u;
+      const uint32_t a0 = __builtin_amdgcn_perm(v[1], v[0], 0x05010400u);
+      const uint32_t a1 = __builtin_amdgcn_perm(v[1], v[0], 0x07030602u);
+      const uint32_t c0 = __builtin_amdgcn_perm(v[3], v[2], 0x05010400u);
+      const uint32_t c1 = __builtin_amdgcn_perm(v[3], v[2], 0x07030602u);
+      const int t[4] = {(int)__builtin_amdgcn_perm(c0, a0, 0x05040100u),
+                        (int)__builtin_amdgcn_perm(c0, a0, 0x07060302u),
+                        (int)__builtin_amdgcn_perm(c1, a1, 0x05040100u),
+                        (int)__builtin_amdgcn_perm(c1, a1, 0x07060302u)};
+#pragma unroll
+      for (int d = 0; d < ND; ++d) {
+        const int w = (int)r4.wd[g][d];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e][d] = __builtin_amdgcn_sdot4(t[e], w, acc[e][d], false);
+      }
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        const int w = (int)r4.rd[g][d];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) aq[e][d] = __builtin_amdgcn_sdot4(t[e], w, aq[e][d], false);
+      }
+    }
+    const int64_t tm = tile / tiles_n, tn = tile % tiles_n;
+    const int bi = blk / NBJ, bj = blk % NBJ;
+    const int64_t gcol = tn * BN + bj * 16 + (lane & 15);
+    T mw = 0;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) mw |= (T)rc.Mw[k] << (16 * k);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t grow = tm * BM + bi * 16 + 4 * (lane >> 4) + e;
+      T z = 0;
+#pragma unroll
+      for (int k = 0; k < NK; ++k)
+        z += (T)(int64_t)(acc[e][2 * k] + acc[e][2 * k + 1] * 256) << (16 * k);
+      const int64_t F = (int64_t)aq[e][0] + (int64_t)aq[e][1] * 256 + (int64_t)aq[e][2] * 65536;
+      const int64_t q = (F + (1 << 23)) >> 24;
+      z -= (T)q * mw;
+      if (grow < M && gcol < N) {
+        T* pc = C + (b * M + grow) * N + gcol;
+        *pc = accumulate ? (T)(*pc + z) : z;
+      }
+    }
+  }
+}
+
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 int crt_kernel() {  // MOOSEX_CRT_KERNEL: 1 = 4 waves of 128x128, 2 = 8 waves of 128x64
@@ -749,6 +866,13 @@ int crt_kernel() {  // MOOSEX_CRT_KERNEL: 1 = 4 waves of 128x128, 2 = 8 waves of
   return v >= 1 && v <= 6 ? v : 5;
 }
 bool crt_mfma16() { return crt_kernel() >= 4; }
+int recon_dot4() {  // MOOSEX_CRT_RECON=0: the multiply-add reconstruction
+  static const int v = [] {
+    const char* e = std::getenv("MOOSEX_CRT_RECON");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return v;
+}
 
 struct CPlan {
   int n, bn;
@@ -844,7 +968,15 @@ void launch_recon(const CPlan& p, const Tables& tb, int64_t batch, int64_t M, in
                   const int8_t* cr, T* C, int accumulate, hipStream_t st) {
   const int64_t work = p.tiles_m * p.tiles_n * (BM * p.bn / 8);
   const int gx = (int)std::min<int64_t>((work + 255) / 256, 16384);
-  if (crt_mfma16()) {
+  if (crt_mfma16() && recon_dot4()) {
+    const int gx16 = (int)std::min<int64_t>((2 * work + 255) / 256, 16384);
+    if (p.bn == 256)
+      hipLaunchKernelGGL((k_crt_recon16d<T, 256>), dim3(gx16, (unsigned)batch), dim3(256), 0, st,
+                         cr, C, M, N, p.tiles_m, p.tiles_n, accumulate, tb.r4, p.n, tb.rc);
+    else
+      hipLaunchKernelGGL((k_crt_recon16d<T, 128>), dim3(gx16, (unsigned)batch), dim3(256), 0, st,
+                         cr, C, M, N, p.tiles_m, p.tiles_n, accumulate, tb.r4, p.n, tb.rc);
+  } else if (crt_mfma16()) {
     const int gx16 = (int)std::min<int64_t>((2 * work + 255) / 256, 16384);
     if (p.bn == 256)
       hipLaunchKernelGGL((k_crt_recon16<T, 256>), dim3(gx16, (unsigned)batch), dim3(256), 0, st,
