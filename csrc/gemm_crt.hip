@@ -1107,6 +1107,18 @@ int mx_crt_tables(int words, int n, int32_t* p_out, uint8_t* wa_out, uint8_t* wb
   return 0;
 }
 
+// Host copy of the dot4 reconstruction tables (tests recompose the digits): wd
+// [groups][16], rd [groups][3] words, modulus 4g + u in byte u.  Returns the group count.
+int mx_crt_tables4(int words, int n, uint32_t* wd_out, uint32_t* rd_out) {
+  if ((words != 1 && words != 2) || n < 1 || n > kMaxMod) return -2;
+  const Tables& t = tables_for(words, n);
+  for (int g = 0; g < t.r4.groups; ++g) {
+    for (int d = 0; d < 16; ++d) wd_out[g * 16 + d] = t.r4.wd[g][d];
+    for (int d = 0; d < 3; ++d) rd_out[g * 3 + d] = t.r4.rd[g][d];
+  }
+  return t.r4.groups;
+}
+
 int mxh_gemm_crt(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
                  const void* A1, const void* B0, const void* B1, int mode, void* C,
                  int accumulate, void* stream) {

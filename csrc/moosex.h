@@ -156,6 +156,7 @@ int mx_gemm_with_b(int words, int64_t batch, int64_t M, int64_t N, int64_t K, co
                    int accumulate, void* stream);
 // Device GEMM with explicit batch strides (elements) for the A and B operands; a stride of 0
 // broadcasts one operand over the batch (no copy of an expanded stack).
+int mx_crt_tables4(int words, int n, uint32_t* wd_out, uint32_t* rd_out);
 int mx_gemm_roll(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
                  int64_t a_bstride, int64_t roll, const void* B0, const void* B1, const void* lb,
                  void* C, int accumulate, void* stream);

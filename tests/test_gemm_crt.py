@@ -116,6 +116,43 @@ def test_crt_arithmetic_worst_case(bits, a, b):
     assert _crt_dot(A, B, bits) == _exact(A, B, bits)
 
 
+@pytest.mark.parametrize("bits", [64, 128])
+def test_dot4_reconstruction_tables(bits):
+    """k_crt_recon16d's digit tables: W_i mod 2^w and round(2^24 / p_i) recompose from their
+    signed base-256 digits, and the integer quotient estimate round(sum c_i R_i / 2^24)
+    reconstructs random products Z at the |Z| <= 0.45 M bound exactly."""
+    lib = nat.lib()
+    words = bits // 64
+    n = lib.mx_crt_moduli(words, 8192)
+    t = _tables(words, n)
+    wd = np.zeros(12 * 16, np.uint32)
+    rd = np.zeros(12 * 3, np.uint32)
+    ptr = lambda a: a.ctypes.data_as(nat.ctypes.c_void_p)  # noqa: E731
+    assert lib.mx_crt_tables4(words, n, ptr(wd), ptr(rd)) == (n + 3) // 4
+
+    def digit(word, u):
+        b = (int(word) >> (8 * u)) & 0xFF
+        return b - 256 if b >= 128 else b
+
+    ps = [int(p) for p in t["p"]]
+    R = []
+    for i in range(n):
+        W = sum(digit(wd[(i // 4) * 16 + d], i % 4) * 256**d for d in range(bits // 8))
+        assert W % (1 << bits) == t["W"][i] % (1 << bits)
+        R.append(sum(digit(rd[(i // 4) * 3 + d], i % 4) * 256**d for d in range(3)))
+        assert R[-1] == round((1 << 24) / ps[i])
+    M = math.prod(ps)
+    inv = [pow(M // p, -1, p) for p in ps]
+    rng = np.random.default_rng(bits)
+    for trial in range(200):
+        frac = (rng.random() * 2 - 1) * 0.45 if trial > 1 else (0.45, -0.45)[trial]
+        Z = int(frac * M)
+        c = [_centered(Z * inv[i], ps[i]) for i in range(n)]
+        q = ((sum(ci * ri for ci, ri in zip(c, R))) + (1 << 23)) >> 24
+        z = (sum(ci * wi for ci, wi in zip(c, t["W"])) - q * t["Mw"]) % (1 << bits)
+        assert z == Z % (1 << bits)
+
+
 # --- GPU ------------------------------------------------------------------------------------
 def rand_rt(shape, bits, seed):
     g = torch.Generator().manual_seed(seed)
