@@ -695,8 +695,10 @@ __global__ void __launch_bounds__(256) k_mul_trunc3_lat(
         out0[e] = Z0;
         out0[os + e] = Z1;
         out0[2 * os + e] = Z2;
-        out1[e] = Z1;
-        out1[os + e] = Z2;
+        if (out1 != out0 + os) {  // else a 4-slot ring: out1's slots 0, 1 are out0's 1, 2
+          out1[e] = Z1;
+          out1[os + e] = Z2;
+        }
         out1[2 * os + e] = Z0;
       }
     }
@@ -748,8 +750,10 @@ __global__ void __launch_bounds__(256) k_mul_trunc3(
       out0[e] = Z0;
       out0[os + e] = Z1;
       out0[2 * os + e] = Z2;
-      out1[e] = Z1;
-      out1[os + e] = Z2;
+      if (out1 != out0 + os) {
+        out1[e] = Z1;
+        out1[os + e] = Z2;
+      }
       out1[2 * os + e] = Z0;
     }
   });

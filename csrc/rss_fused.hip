@@ -40,8 +40,10 @@ __global__ void __launch_bounds__(256) k_trunc_pr3(const T* __restrict__ s0, T* 
       out0[i] = z0;
       out0[os + i] = z1;
       out0[2 * os + i] = z2;
-      out1[i] = z1;
-      out1[os + i] = z2;
+      if (out1 != out0 + os) {  // else out1 = out0 + os: a 4-slot ring, slots 1, 2 shared
+        out1[i] = z1;
+        out1[os + i] = z2;
+      }
       out1[2 * os + i] = z0;
     }
   });
@@ -89,8 +91,10 @@ __global__ void __launch_bounds__(256) k_trunc_pr3_lat(const T* __restrict__ s0,
         out0[i] = z0;
         out0[os + i] = z1;
         out0[2 * os + i] = z2;
-        out1[i] = z1;
-        out1[os + i] = z2;
+        if (out1 != out0 + os) {
+          out1[i] = z1;
+          out1[os + i] = z2;
+        }
         out1[2 * os + i] = z0;
       }
     }
@@ -120,10 +124,11 @@ __global__ void __launch_bounds__(256) k_share3(int kind, const T* __restrict__ 
       slot[j0] = xj;
       slot[(j0 + 1) % 3] = r1;
       slot[(j0 + 2) % 3] = ra;
+      const bool ring4 = out1 == out0 + n;  // 4-slot ring: out1's slots 0, 1 are out0's 1, 2
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
         out0[p * n + i] = slot[p];
-        out1[p * n + i] = slot[(p + 1) % 3];
+        if (!ring4 || p == 2) out1[p * n + i] = slot[(p + 1) % 3];
       }
     }
   });

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from typing import List
 from typing import Sequence
 
@@ -145,6 +146,21 @@ def empty2(shape, bits, device):
     pair / stacked-protocol kernels)."""
     both = empty((2,) + tuple(shape), bits, device).data
     return RT(both[0], bits), RT(both[1], bits)
+
+
+_RING4 = os.environ.get("MOOSEX_RING4", "1") != "0"
+
+
+def ring4(shape, bits, device):
+    """The two share vectors of a stacked replicated value ([3, ...]) as views of ONE
+    [4, ...] buffer holding slots x0, x1, x2, x0: s0 = buf[0:3], s1 = buf[1:4] = s0 rolled
+    by one party.  Pair-producing kernels detect out1 == out0 + slot and write 4 slots, not
+    6; every consumer sees two ordinary contiguous [3, ...] tensors."""
+    shape = tuple(shape)
+    if not shape or shape[0] != 3 or not _RING4:
+        return empty2(shape, bits, device)
+    buf = empty((4,) + shape[1:], bits, device).data
+    return RT(buf[0:3], bits), RT(buf[1:4], bits)
 
 
 def zeros(shape, bits, device) -> RT:
@@ -1009,7 +1025,7 @@ def mul_trunc3_k(x0: RT, x1: RT, y0: RT, y1: RT, slot_ptr: int, nmul: int, m: in
         views = (ctypes.c_int64 * 8)(*[v[0] for v in vs], *[v[1] for v in vs])
     w = 2 if bits == 128 else 1
     if out is None:
-        o0, o1 = empty2(shp, bits, x0.device)
+        o0, o1 = ring4(shp, bits, x0.device)
         os_ = n
     else:
         o0, o1 = out
@@ -1041,7 +1057,7 @@ def zs_trunc3_k(z: RT, slot_ptr: int, nmul: int, m: int, nonces):
     n = math.prod(shp) // 3
     if n == 0:
         return None
-    o0, o1 = empty2(shp, bits, d.device)
+    o0, o1 = ring4(shp, bits, d.device)
     nn = (ctypes.c_uint64 * 6)(*[v & MASK64 for v in nonces])
     rc = nat.lib().mx_mul_trunc3_kv(
         nat.dev_of(d), _words(bits), nat.ptr(d), None, None, None, nat.ptr(o0.data),

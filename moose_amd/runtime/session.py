@@ -557,8 +557,7 @@ class StackedSession(Session):
         nn = (ctypes.c_uint64 * 6)(*[v & ((1 << 64) - 1) for v in nonces])
         cv = int(c) % (1 << x.bits)
         cm = (ctypes.c_uint64 * 2)(cv & ((1 << 64) - 1), cv >> 64)
-        both = torch.empty((2,) + tuple(s0.shape), dtype=s0.dtype, device=s0.device)
-        out0, out1 = both[0], both[1]
+        out0, out1 = (t.data for t in R.ring4(x.s0.v.shape, x.bits, s0.device))
         nat.check(nat.lib().mx_trunc_pr3_kmo(
             nat.dev_of(s0), R._words(x.bits), nat.ptr(s0), nat.ptr(out0), nat.ptr(out1), n, m,
             self.key_ptr(x.plc, 0), self.key_ptr(x.plc, 2), nn, n, cm, nat.stream_of(s0)),
@@ -592,8 +591,7 @@ class StackedSession(Session):
                 *keys, nn, os_, nat.stream_of(s0)), "trunc_pr3 (views)")
             self._trunc_traffic(x, out0[0].numel() * out0.element_size())
             return out[0], out[1]
-        both = torch.empty((2,) + tuple(s0.shape), dtype=s0.dtype, device=s0.device)
-        out0, out1 = both[0], both[1]
+        out0, out1 = (t.data for t in R.ring4(x.s0.v.shape, x.bits, s0.device))
         nat.check(
             nat.lib().mx_trunc_pr3_k(
                 nat.dev_of(s0), R._words(x.bits), nat.ptr(s0), nat.ptr(out0), nat.ptr(out1), n, m,
@@ -618,9 +616,7 @@ class StackedSession(Session):
         from moose_amd.ops import native as nat
 
         xd = x.v.data.contiguous()
-        shape = (3,) + tuple(xd.shape)
-        out0 = torch.empty(shape, dtype=xd.dtype, device=xd.device)
-        out1 = torch.empty_like(out0)
+        out0, out1 = (t.data for t in R.ring4((3,) + tuple(x.v.shape), x.v.bits, xd.device))
         nat.check(
             nat.lib().mx_share3_k(
                 nat.dev_of(xd), 1 if kind == "bool" else 0, R._words(x.v.bits), nat.ptr(xd),
