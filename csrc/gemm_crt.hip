@@ -859,11 +859,13 @@ int crt_kernel() {  // MOOSEX_CRT_KERNEL: 1 = 4 waves of 128x128, 2 = 8 waves of
   // (256x256 tiles, one block per CU), 3 = 4 waves of 128x64 in 256x128 tiles (two blocks
   // per CU, so one block's barrier waits, LDS bursts and epilogue overlap the other's MFMAs)
   // 4 = 16x16x64 MFMAs, 4 waves of 128x128 (256x256 tiles), 5 = 16x16x64, 4 waves of
-  // 128x64 in 256x128 tiles (two blocks per CU; the default: 12 % faster than 3 -- the chip
-  // holds a higher clock on the 16x16 shape), 6 = 16x16x64, 8 waves of 128x64 (256x256)
+  // 128x64 in 256x128 tiles (two blocks per CU; 12 % faster than 3 -- the chip holds a
+  // higher clock on the 16x16 shape), 6 = 16x16x64, 8 waves of 128x64 in 256x256 tiles, two
+  // blocks per CU (the default: 11.95 vs 12.12 ms for 5 on the 4096^2 Z_2^128 RSS product,
+  // profiles/r2_crt_variant_ab.md)
   const char* e = std::getenv("MOOSEX_CRT_KERNEL");
-  const int v = e ? std::atoi(e) : 5;
-  return v >= 1 && v <= 6 ? v : 5;
+  const int v = e ? std::atoi(e) : 6;
+  return v >= 1 && v <= 6 ? v : 6;
 }
 bool crt_mfma16() { return crt_kernel() >= 4; }
 int recon_dot4() {  // MOOSEX_CRT_RECON=0: the multiply-add reconstruction
