@@ -193,3 +193,29 @@ def test_dot_tail_fused_matches_two_steps(bits, mnk, monkeypatch):
     _eq(a.s1.v, b.s1.v)
     # the unfused pair is a valid sharing: s1 is s0 rolled by one party
     _eq(roll(a.s0.v), a.s1.v)
+
+
+@pytest.mark.parametrize("dev", DEVICES)
+@pytest.mark.parametrize("bits", [64, 128])
+def test_share_pair_ring_buffer(dev, bits):
+    """Share and TruncPr outputs of a stacked session are views of one 4-slot ring buffer
+    (s1 = s0 rolled by one party, no second copy), and hold the same shares as two separate
+    buffers (MOOSEX_RING4=0 path: R.empty2)."""
+    plc = ReplicatedPlacement(("alice", "bob", "carole"))
+    x0 = _rand((3, 4, 9), bits, dev, 70)
+    roll = lambda t: R.RT(torch.roll(t.data, -1, dims=0).contiguous(), bits)  # noqa: E731
+    X = rep.RepTensor(plc, bits, "arith", PV(plc, x0), PV(plc, roll(x0)))
+    s = StackedSession(dev, seed=9)
+    t0, t1 = s.fused_trunc_pr(X, 20, (1, 2, 3, 4, 5, 6))
+    el = t0.v.data.element_size() * t0.v.data[0].numel()
+    assert t1.v.data.data_ptr() - t0.v.data.data_ptr() == el  # one buffer, offset one slot
+    _eq(roll(t0.v), t1.v)
+    a, b = R.ring4((3, 5), bits, dev)
+    assert b.data.data_ptr() - a.data.data_ptr() == a.data[0].numel() * a.data.element_size()
+    R._RING4 = False
+    try:
+        u0, u1 = s.fused_trunc_pr(X, 20, (1, 2, 3, 4, 5, 6))
+    finally:
+        R._RING4 = True
+    _eq(u0.v, t0.v)
+    _eq(u1.v, t1.v)
