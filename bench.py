@@ -105,6 +105,41 @@ def _self_launch(args):
     return subprocess.call(cmd, env=env)
 
 
+def _device_info(device):
+    """Identity of the GPU the numbers were taken on (and the torch/HIP/RCCL versions)."""
+    import torch
+
+    info = {"torch": torch.__version__, "hip": torch.version.hip}
+    if device.type != "cuda":
+        return dict(info, name="cpu")
+    p = torch.cuda.get_device_properties(device)
+    info.update(name=p.name, arch=getattr(p, "gcnArchName", ""),
+                cus=p.multi_processor_count, mem_gib=round(p.total_memory / 2**30, 1),
+                clock_mhz=getattr(p, "clock_rate", 0) // 1000 or None)
+    try:
+        v = torch.cuda.nccl.version()
+        info["rccl"] = ".".join(map(str, v)) if isinstance(v, tuple) else v
+    except Exception:  # noqa: BLE001 - informational only
+        pass
+    return info
+
+
+def _revision():
+    """git head of the tree (the GPU box gets a snapshot without .git: fall back to the
+    REVISION file written by __graft_entry__.build())."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    try:
+        return subprocess.run(["git", "-C", here, "rev-parse", "--short=12", "HEAD"],
+                              capture_output=True, text=True, timeout=5,
+                              check=True).stdout.strip()
+    except Exception:  # noqa: BLE001
+        try:
+            with open(os.path.join(here, "moose_amd", "_native", "REVISION")) as f:
+                return f.read().strip()
+        except OSError:
+            return None
+
+
 def _inputs(n, session, which, device):
     import torch
 
@@ -258,12 +293,21 @@ def main():
     drain()
     sync()
     comm0 = (comm.bytes_sent, comm.messages) if comm is not None else (0, 0)
+    # per-step device time: one event pair per step on the issuing stream (no host sync
+    # inside the timed loop; read after the final synchronize)
+    evs = ([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            for _ in range(args.steps)] if device.type == "cuda" else None)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        if evs is not None:
+            evs[i][0].record()
         z = step()
+        if evs is not None:
+            evs[i][1].record()
     drain()  # every step's gather is complete inside the timed region
     sync()
     elapsed = time.perf_counter() - t0
+    step_ms = sorted(a.elapsed_time(b) for a, b in evs) if evs is not None else []
     p2p = ((comm.bytes_sent - comm0[0]) / args.steps, (comm.messages - comm0[1]) / args.steps) \
         if comm is not None else (0, 0)
     per_rank = [elapsed]
@@ -334,6 +378,11 @@ def main():
             "p2p_bytes_per_step_rank0": p2p[0],
             "p2p_messages_per_step_rank0": p2p[1],
         }
+        if step_ms:
+            line["step_ms_rank0"] = {"min": step_ms[0], "median": step_ms[len(step_ms) // 2],
+                                     "max": step_ms[-1]}
+        line["device"] = _device_info(device)
+        line["revision"] = _revision()
         if args.check:
             line["check"] = [c for c in checks if c is not None]
         print(json.dumps(line), flush=True)

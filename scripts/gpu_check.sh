@@ -20,6 +20,16 @@ run() {  # run <name> <timeout> <cmd...>
 }
 
 STEPS=${STEPS:-all}
+if [[ $STEPS == *driver* ]]; then
+  # the driver's exact bench command, twice, then under rocprofv3 (kernel trace only)
+  (rocm-smi --showclocks --showpower --showperflevel > gpurun_out/smi_before.txt 2>&1 || true)
+  run driver1 300 python3 bench.py --gpus 1 --steps 20 --warmup 5
+  run driver2 300 python3 bench.py --gpus 1 --steps 20 --warmup 5
+  run default 300 python3 bench.py
+  (rocm-smi --showclocks --showpower --showperflevel > gpurun_out/smi_after.txt 2>&1 || true)
+  export TMPDIR=/tmp
+  run driver_prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/driver_prof -o run --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5
+fi
 [[ $STEPS == *test* || $STEPS == all ]] && run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
 [[ $STEPS == *smoke* || $STEPS == all ]] && run smoke 300 python __graft_entry__.py smoke
 [[ $STEPS == *bench* || $STEPS == all ]] && run bench128 600 python bench.py --steps 5 --warmup 2 --check
