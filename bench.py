@@ -1,14 +1,21 @@
 #!/usr/bin/env python
-"""Headline benchmark: replicated fixed-point matrix product throughput.
+"""Headline benchmark: replicated fixed-point matrix product throughput, plus private
+logistic-regression inference latency (the two halves of BASELINE.json's metric).
 
-Metric (BASELINE.json): "replicated fixed(14,23) matmul elems/sec" -- one step is the
-reference's dot benchmark (``benchmarks/pymoose/dot_product.py``) at the BASELINE config
-3 size: x (alice) and y (bob) are cast to fixed(14,23), secret-shared onto a 3-party
-replicated placement, multiplied (RSS dot = exact multi-modular int8-MFMA GEMM + zero share
-+ reshare),
-truncated (TruncPr) and revealed to carole, who decodes to float64.  As in pymoose every
-fixed dtype runs over Z_2^128 (``--ring 64`` selects the Z_2^64 path).  Value = output
-elements per second over the whole job (all GPUs).
+Matmul (the JSON line's ``value``) -- one step is the reference's dot benchmark
+(``benchmarks/pymoose/dot_product.py``) at the BASELINE config 3 size: x (alice) and y (bob)
+are cast to fixed(14,23), secret-shared onto a 3-party replicated placement, multiplied
+(RSS dot = exact multi-modular int8-MFMA GEMM + zero share + reshare), truncated (TruncPr)
+and revealed to carole, who decodes to float64.  As in pymoose every fixed dtype runs over
+Z_2^128 (``--ring 64`` selects the Z_2^64 path).  Value = output elements per second over
+the whole job (all GPUs).
+
+LR inference (``lr_inference`` in the line) -- the reference's ml-inference-with-onnx
+tutorial model (``moose_amd/models/predictors/tutorial.py``: 200 x 10 rows, fixed(24,40),
+Z_2^128, secure sigmoid) through ``predictors.from_onnx``: p50 latency of whole
+evaluations (share -> predict -> reveal) on rank 0's GPU, eager and hipGraph replay, and
+with >= 3 GPUs also one party per GPU (SPMD over RCCL).  Measured after the timed matmul
+steps, outside their timed region.
 
 Layouts (``--layout``; default ``auto`` = stacked on 1 GPU, cyclic on N > 1):
 
@@ -20,15 +27,27 @@ Layouts (``--layout``; default ``auto`` = stacked on 1 GPU, cyclic on N > 1):
   send/recv over xGMI.  Weak scaling with the same per-GPU work as the 1-GPU stacked run.
 * ``spmd`` -- one party per GPU, N/3 sessions (latency layout).
 
+``--step-streams S``: consecutive steps (independent sessions) alternate between S HIP
+streams, each with its own RCCL communicator, so one step's exchanges overlap the next
+step's GEMM (the reference runs independent operations as concurrent tasks).  Default 2 for
+the cyclic layout at N > 1, else 1.
+
 With several sessions, the revealed outputs of every session are collected on rank 0 (the
 client, as the reference's benchmark collects them) over RCCL inside the timed region,
-overlapped with the next step (``--gather all`` all-gathers them to every rank instead).  Inputs are synthetic (uniform [-4, 4)),
-device-resident; tracing/conversion happens once before the timed region (the
-reference's client-side compile).  Every step creates a fresh session (fresh PRF keys).
+overlapped with the next step (``--gather all`` all-gathers them to every rank instead).
+Inputs are synthetic (uniform [-4, 4)), device-resident; tracing/conversion happens once
+before the timed region (the reference's client-side compile).  Every step creates a fresh
+session (fresh PRF keys).  After the timed steps the last step's outputs are checked
+against float64 torch on every rank (``--no-check`` skips it).
+
+Failing loudly (``moose_amd/utils/benchwatch.py``): every phase (init, preflight, warmup,
+timed, check, lr) runs under a watchdog budget; a stall ends the run with a JSON line naming
+the stalled ranks.  Before the warmup every rank does one grouped round trip with each of
+its peers on every communicator it will use and verifies who answered.
 
 Launch: ``python bench.py --gpus N`` spawns N ranks itself (torch.distributed.run on
-127.0.0.1, before anything touches the GPU); under an external launcher (WORLD_SIZE set)
-it runs as one rank.
+127.0.0.1, before anything touches the GPU) under a wall-clock supervisor; under an
+external launcher (WORLD_SIZE set) it runs as one rank.
 """
 from __future__ import annotations
 
@@ -38,12 +57,14 @@ import os
 import socket
 import subprocess
 import sys
+import tempfile
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 REFERENCE_ELEMS_PER_SEC = 1.0e6 / 5.910  # benchmarks/README.md:21, 1000x1000 Fixed128
 ROLES = ("alice", "bob", "carole")
+METRIC = "replicated fixed(14,23) matmul elems/sec"
 
 
 def build_computation(ring):
@@ -84,7 +105,16 @@ def _parse():
                          "default), all-gathered to every rank, or left on their owners")
     ap.add_argument("--no-gather", action="store_true", help="= --gather none")
     ap.add_argument("--layout", default="auto", choices=["auto", "stacked", "cyclic", "spmd"])
-    ap.add_argument("--check", action="store_true", help="verify against float64 torch")
+    ap.add_argument("--step-streams", type=int, default=None,
+                    help="HIP streams (and RCCL communicators) consecutive steps alternate "
+                         "between (default: 2 for cyclic at N > 1, else 1)")
+    ap.add_argument("--check", dest="check", action="store_true", default=True,
+                    help="verify the last step's outputs against float64 torch (default)")
+    ap.add_argument("--no-check", dest="check", action="store_false")
+    ap.add_argument("--lr-runs", type=int, default=30,
+                    help="LR-inference evaluations per mode (0 = skip)")
+    ap.add_argument("--watchdog", type=float, default=float(os.environ.get(
+        "MOOSEX_BENCH_WATCHDOG", "600")), help="seconds any one phase may take")
     return ap.parse_args()
 
 
@@ -94,15 +124,48 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def _base_line(args, world):
+    """The fields of the JSON line that do not depend on the measurement."""
+    return {"metric": METRIC, "value": None, "unit": "output elems/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "higher_is_better": True,
+            "scaling": "weak", "dtype": f"fixed(14,23) over Z_2^{args.ring}",
+            "data": "synthetic uniform[-4,4) inputs, device resident",
+            "config": {"model": f"replicated fixed(14,23) RingDot {args.size}x{args.size} "
+                                "(share+dot+trunc_pr+reveal)",
+                       "seq_len": args.size}}
+
+
 def _self_launch(args):
-    """N > 1 without a launcher: run N fresh ranks as child processes.  This process has
-    not touched the GPU (only argparse ran), and exits with the launcher's status."""
+    """N > 1 without a launcher: run N fresh ranks as child processes under a wall-clock
+    supervisor.  This process never touches the GPU (only argparse ran), and exits with
+    the launcher's status (or 3 with an error line if the rank group hangs)."""
+    import importlib.util
+
+    # load the watchdog module by path: importing the moose_amd package would pull in torch
+    # and the native libraries, and this process must stay away from the GPU
+    spec = importlib.util.spec_from_file_location(
+        "moosex_benchwatch", os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                          "moose_amd", "utils", "benchwatch.py"))
+    benchwatch = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(benchwatch)
+    rdir = tempfile.mkdtemp(prefix="moosex_bench_")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
            "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    return subprocess.call(cmd, env=env)
+    env["MOOSEX_BENCH_RUN_DIR"] = rdir
+    # the ranks' own watchdogs fire per phase; this limit only catches a launcher or a
+    # rank that cannot even run its watchdog (7 phases + start-up)
+    limit = 8 * args.watchdog + 120
+    return benchwatch.supervise(cmd, env, args.gpus, limit, _base_line(args, args.gpus), rdir)
+
+
+def _inputs(n, session, which, device):
+    import torch
+
+    g = torch.Generator(device="cpu").manual_seed(1234 + 2 * session + (which == "y"))
+    return (torch.rand(n, n, generator=g, dtype=torch.float64) * 8 - 4).to(device)
 
 
 def _device_info(device):
@@ -140,26 +203,181 @@ def _revision():
             return None
 
 
-def _inputs(n, session, which, device):
+# ---------------------------------------------------------------------------------------
+# preflight: one grouped round trip with every peer on every communicator
+# ---------------------------------------------------------------------------------------
+def _preflight(layout, comms, world, rank, device, prog):
+    """Each rank sends its rank id to every peer it will exchange with and checks what it
+    receives (catches a wrong peer map, a dead link or an RCCL set-up hang before the
+    measured work starts).  Returns a short record for the JSON line."""
+    import torch
+    import torch.distributed as dist
+
+    t0 = time.perf_counter()
+    tdev = device if world > 1 and dist.get_backend() == "nccl" else torch.device("cpu")
+    if world > 1:
+        prog.tick(0)
+        one = torch.ones(1, dtype=torch.float64, device=tdev)
+        dist.all_reduce(one)
+        if int(one.item()) != world:
+            raise RuntimeError(f"preflight all_reduce gave {one.item()} on {world} ranks")
+    peers = []
+    if layout == "cyclic" and world > 1:
+        from moose_amd.parallel.cyclic import default_offsets
+
+        off = list(default_offsets(ROLES).values())
+        dists = sorted({(b - a) % world for a in off for b in off} - {0})
+        for k, comm in enumerate(comms):
+            prog.tick(1 + k)
+            sends, recvs, expect = [], [], []
+            for d in dists:
+                src = (rank - d) % world
+                buf = torch.full((4,), -1, dtype=torch.int64, device=device)
+                sends.append((torch.full((4,), rank, dtype=torch.int64, device=device),
+                              (rank + d) % world))
+                recvs.append((buf, src))
+                expect.append(src)
+            comm.exchange(sends, recvs)
+            got = [int(b[0].item()) for b, _ in recvs]
+            if got != expect:
+                raise RuntimeError(f"preflight: rank {rank} expected peers {expect}, got {got}")
+            peers = sorted(set(expect) | {(rank + d) % world for d in dists})
+    elif layout == "spmd" and world >= 3:
+        base = 3 * (rank // 3)
+        others = [base + i for i in range(3) if base + i != rank]
+        tr = comms[0]
+        prog.tick(1)
+        bufs = [torch.full((4,), -1, dtype=torch.int64, device=device) for _ in others]
+        tr.exchange([(torch.full((4,), rank, dtype=torch.int64, device=device), o)
+                     for o in others], list(zip(bufs, others)))
+        got = [int(b[0].item()) for b in bufs]
+        if got != others:
+            raise RuntimeError(f"preflight: rank {rank} expected {others}, got {got}")
+        peers = others
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    return {"ok": True, "peers_rank0": peers, "ms": round((time.perf_counter() - t0) * 1e3, 2)}
+
+
+# ---------------------------------------------------------------------------------------
+# LR inference (BASELINE config 4)
+# ---------------------------------------------------------------------------------------
+def _lr_stacked(runs, device):
+    """p50 latency of the tutorial model on one GPU: eager, then hipGraph replay."""
+    import numpy as np
     import torch
 
-    g = torch.Generator(device="cpu").manual_seed(1234 + 2 * session + (which == "y"))
-    return (torch.rand(n, n, generator=g, dtype=torch.float64) * 8 - 4).to(device)
+    from moose_amd.models.predictors.tutorial import logistic_regression_tutorial
+    from moose_amd.runtime.local import LocalMooseRuntime
+
+    tm = logistic_regression_tutorial(128)
+    out = {}
+    for mode in ("eager", "graphs"):
+        rt = LocalMooseRuntime(list(ROLES), device=device, fixedpoint_ring=128,
+                               use_graphs=mode == "graphs")
+        args = {"x": tm.x_test}
+        for _ in range(3):
+            r = rt.evaluate_computation(tm.computation, args)
+        lat = []
+        for _ in range(runs):
+            t0 = time.perf_counter()
+            r = rt.evaluate_computation(tm.computation, args)  # synchronises the device
+            lat.append((time.perf_counter() - t0) * 1e3)
+        err = float(np.abs(np.asarray(list(r.values())[0]) - tm.proba).max())
+        lat.sort()
+        rec = {"p50_ms": lat[len(lat) // 2], "p90_ms": lat[int(0.9 * (len(lat) - 1))],
+               "max_abs_err_vs_sklearn": err}
+        if mode == "graphs":
+            rec["captured"] = bool(rt._graphs.plans)
+        out[mode] = rec
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+    return out
 
 
+def _lr_spmd(runs, world, rank, device, prog):
+    """The tutorial model with one party per GPU (ranks 3s, 3s+1, 3s+2 = alice, bob,
+    carole of session s): every reshare, dealer message and reveal an RCCL send/recv.
+    Latency of an evaluation = max over its three ranks; p50 over ``runs``."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from moose_amd.models.predictors.tutorial import logistic_regression_tutorial
+    from moose_amd.parallel.spmd import SPMDSession
+    from moose_amd.parallel.transport import Transport
+    from moose_amd.runtime.interpreter import Interpreter
+    from moose_amd.runtime.local import to_native
+
+    triples = [list(range(3 * s, 3 * s + 3)) for s in range(world // 3)]
+    groups = [dist.new_group(t) for t in triples]  # every rank creates every group
+    mine = rank // 3 if rank < 3 * len(triples) else None
+    rec = None
+    if mine is not None:
+        g = groups[mine]
+        tm = logistic_regression_tutorial(128)
+        comp = to_native(tm.computation, 128)
+        tr = Transport(rank, world, device)
+        roles = {r: 3 * mine + i for i, r in enumerate(ROLES)}
+        bdev = [device.index] if device.type == "cuda" and dist.get_backend() == "nccl" else None
+        lat = []
+        for i in range(runs + 3):
+            prog.tick(i)
+            dist.barrier(group=g, device_ids=bdev)
+            t0 = time.perf_counter()
+            sess = SPMDSession(ROLES[rank % 3], roles, tr, device)
+            interp = Interpreter(sess, {}, fixedpoint_ring=128)
+            outs = interp.run(comp, {"x": tm.x_test})
+            if device.type == "cuda":
+                torch.cuda.synchronize(device)
+            if i >= 3:
+                lat.append((time.perf_counter() - t0) * 1e3)
+        tdev = device if dist.get_backend() == "nccl" else torch.device("cpu")
+        mine_t = torch.tensor(lat, dtype=torch.float64, device=tdev)
+        allt = torch.empty(3 * runs, dtype=torch.float64, device=tdev)
+        dist.all_gather_into_tensor(allt, mine_t, group=g)
+        per_run = allt.reshape(3, runs).max(dim=0).values.cpu().numpy()
+        per_run.sort()
+        rec = {"p50_ms": float(per_run[len(per_run) // 2]),
+               "p90_ms": float(per_run[int(0.9 * (runs - 1))]), "ranks": triples[mine]}
+        if rank % 3 == 1:  # bob holds the opened probabilities
+            got = interp.to_numpy(list(outs.values())[0])
+            rec["max_abs_err_vs_sklearn"] = float(np.abs(np.asarray(got) - tm.proba).max())
+    return rec
+
+
+# ---------------------------------------------------------------------------------------
 def main():
     args = _parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_self_launch(args))
+    prog = []
+    try:
+        _main(args, prog)
+    except SystemExit:
+        raise
+    except BaseException as e:  # noqa: BLE001 - report, then fail
+        if prog:
+            prog[0].fail(f"{type(e).__name__}: {e}")
+        raise
+
+
+def _main(args, prog_out):
+
+    import datetime
 
     import torch
     import torch.distributed as dist
+
+    from moose_amd.utils.benchwatch import Progress
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but the launcher started {world} ranks")
+    prog = Progress(rank, world, args.watchdog, lambda: _base_line(args, world))
+    prog_out.append(prog)
     # MOOSEX_SHARED_GPU=1: every rank on cuda:0 with gloo (rehearsing the multi-GPU
     # layouts on a one-GPU box; RCCL refuses two ranks on one device)
     shared = os.environ.get("MOOSEX_SHARED_GPU") == "1"
@@ -172,7 +390,10 @@ def main():
     if world > 1:
         backend = "nccl" if device.type == "cuda" and not shared else "gloo"
         dist.init_process_group(backend=backend,
-                                device_id=device if backend == "nccl" else None)
+                                device_id=device if backend == "nccl" else None,
+                                # longer than a phase budget: the watchdog reports first
+                                timeout=datetime.timedelta(seconds=args.watchdog + 120))
+        prog.phase("rendezvous", args.watchdog)
         dist.barrier()
 
     from moose_amd.runtime.interpreter import Interpreter
@@ -183,6 +404,11 @@ def main():
         layout = "stacked" if world == 1 else "cyclic"
     if layout == "spmd" and (world < 3 or world % 3):
         raise SystemExit("--layout spmd needs a multiple of 3 GPUs (one per party)")
+    nstreams = args.step_streams
+    if nstreams is None:
+        nstreams = int(os.environ.get("MOOSEX_BENCH_STREAMS",
+                                      "2" if layout == "cyclic" and world > 1 else "1"))
+    nstreams = max(1, nstreams)
 
     comp = build_computation(args.ring)
     n = args.size
@@ -211,49 +437,50 @@ def main():
         if gather_mode == "all" and layout == "spmd":  # the output owners of every session
             gather_group = dist.new_group(owners)
 
+    streams = ([torch.cuda.Stream(device) for _ in range(nstreams)]
+               if device.type == "cuda" and nstreams > 1 else None)
     if layout == "spmd":
         from moose_amd.parallel.spmd import SPMDSession
         from moose_amd.parallel.transport import Transport
 
         roles = {r: 3 * (rank // 3) + i for i, r in enumerate(ROLES)}
-        transport = comm = Transport(rank, world, device)
+        comms = [Transport(rank, world, device)]
 
-        def new_session():
-            return SPMDSession(ROLES[rank % 3], roles, transport, device)
+        def new_session(k):
+            return SPMDSession(ROLES[rank % 3], roles, comms[0], device)
     elif layout == "cyclic":
         from moose_amd.parallel.cyclic import CyclicSession
         from moose_amd.parallel.cyclic import RingComm
         from moose_amd.parallel.cyclic import default_offsets
 
-        comm = RingComm(rank, world, device)
+        # one communicator per step stream: RCCL runs the operations of a communicator in
+        # issue order, so step k+1's exchanges must not queue behind step k's
+        groups = [None] + ([dist.new_group(list(range(world))) for _ in range(nstreams - 1)]
+                           if world > 1 else [None] * (nstreams - 1))
+        comms = [RingComm(rank, world, device, group=g) for g in groups]
         offsets = default_offsets(ROLES)
 
-        def new_session():
-            return CyclicSession(comm, offsets, device)
+        def new_session(k):
+            return CyclicSession(comms[k % len(comms)], offsets, device)
     else:
-        def new_session():
+        comms = []
+
+        def new_session(k):
             return StackedSession(device)
 
-    if layout == "stacked":
-        comm = None
     n_steps = [0]
-    # MOOSEX_BENCH_STREAMS=n (stacked layout): consecutive steps alternate between n HIP
-    # streams so one step's VALU-bound kernels could overlap the previous step's GEMM (the
-    # GEMM scratch is per stream).  Measured: 16.6 ms/step with 1 stream, 17.1 with 2, 19.1
-    # with 3 -- the GEMM keeps the MFMA pipes ~80 % busy and loses clock and CU slots to the
-    # overlapping kernels -- so the default is 1.
-    nstreams = int(os.environ.get("MOOSEX_BENCH_STREAMS", "1"))
-    streams = ([torch.cuda.Stream(device) for _ in range(nstreams)]
-               if layout == "stacked" and device.type == "cuda" and nstreams > 1 else None)
 
     def step():
         if streams is None:
             return _step()
-        with torch.cuda.stream(streams[n_steps[0] % len(streams)]):
+        st = streams[n_steps[0] % len(streams)]
+        st.wait_stream(torch.cuda.current_stream(device))  # inputs / previous host work
+        with torch.cuda.stream(st):
             return _step()
 
     def _step():
-        sess = new_session()
+        k = n_steps[0]
+        sess = new_session(k)
         interp = Interpreter(sess, {}, fixedpoint_ring=args.ring)
         outs = interp.run(comp, {"x": x, "y": y})
         z = outs["output_0"].v.v if out_owner else None
@@ -262,11 +489,11 @@ def main():
                 pending.pop(0).wait()
             zc = z.contiguous()
             if gather_mode == "all":
-                buf = gather_bufs[n_steps[0] % 2]
+                buf = gather_bufs[k % 2]
                 pending.append(dist.all_gather_into_tensor(buf, zc, group=gather_group,
                                                            async_op=True))
             elif rank == root:
-                buf = gather_bufs[n_steps[0] % 2]
+                buf = gather_bufs[k % 2]
                 ops = [dist.P2POp(dist.irecv, buf[i * n:(i + 1) * n], r)
                        for i, r in enumerate(owners) if r != root]
                 buf[owners.index(root) * n:(owners.index(root) + 1) * n].copy_(zc)
@@ -281,24 +508,35 @@ def main():
             pending.pop(0).wait()
 
     def sync():
+        if streams is not None:
+            cur = torch.cuda.current_stream(device)
+            for st in streams:
+                cur.wait_stream(st)
         if device.type == "cuda":
             torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
 
+    prog.phase("preflight", min(args.watchdog, 180))
+    preflight = _preflight(layout, comms, world, rank, device, prog)
+
+    prog.phase("warmup", args.watchdog)
     for i in range(args.warmup):
+        prog.tick(i)
         step()
         if i == 0:  # the first step fills the shared constant caches: let it finish alone
             sync()
     drain()
     sync()
-    comm0 = (comm.bytes_sent, comm.messages) if comm is not None else (0, 0)
+    comm0 = [(c.bytes_sent, c.messages) for c in comms]
     # per-step device time: one event pair per step on the issuing stream (no host sync
     # inside the timed loop; read after the final synchronize)
     evs = ([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            for _ in range(args.steps)] if device.type == "cuda" else None)
+            for _ in range(args.steps)] if device.type == "cuda" and streams is None else None)
+    prog.phase("timed", args.watchdog)
     t0 = time.perf_counter()
     for i in range(args.steps):
+        prog.tick(i)
         if evs is not None:
             evs[i][0].record()
         z = step()
@@ -308,86 +546,118 @@ def main():
     sync()
     elapsed = time.perf_counter() - t0
     step_ms = sorted(a.elapsed_time(b) for a, b in evs) if evs is not None else []
-    p2p = ((comm.bytes_sent - comm0[0]) / args.steps, (comm.messages - comm0[1]) / args.steps) \
-        if comm is not None else (0, 0)
-    per_rank = [elapsed]
+
+    prog.phase("report", min(args.watchdog, 180))
+    p2p = [sum(c.bytes_sent for c in comms) - sum(b for b, _ in comm0),
+           sum(c.messages for c in comms) - sum(m for _, m in comm0)]
+    per_rank = [[elapsed] + p2p]
     if world > 1:
         tdev = device if dist.get_backend() == "nccl" else "cpu"
-        t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
-        allt = torch.empty(world, dtype=torch.float64, device=tdev)
+        t = torch.tensor([elapsed] + p2p, dtype=torch.float64, device=tdev)
+        allt = torch.empty(3 * world, dtype=torch.float64, device=tdev)
         dist.all_gather_into_tensor(allt, t)
-        per_rank = allt.cpu().tolist()
-    elapsed = max(per_rank)
+        per_rank = allt.reshape(world, 3).cpu().tolist()
+    elapsed = max(r[0] for r in per_rank)
     ms_per_step = elapsed / args.steps * 1e3
     value = n_sessions * n * n * args.steps / elapsed
 
-    check = None
-    if args.check and out_owner:
-        ref = _inputs(n, out_session, "x", device) @ _inputs(n, out_session, "y", device)
-        check = {"max_abs_err": (z - ref).abs().max().item()}
-    if args.check and gather_bufs is not None and (gather_mode == "all" or rank == root):
-        # the last step's collected outputs: rank r's revealed output is session s(r)'s
-        buf = gather_bufs[(n_steps[0] - 1) % 2]
-        sess_of = {"cyclic": lambda r: (r - 2) % world, "spmd": lambda r: r // 3,
-                   "stacked": lambda r: r}[layout]
-        gerr = 0.0
-        for i, r in enumerate(owners):
-            s_ = sess_of(r)
-            ref = _inputs(n, s_, "x", device) @ _inputs(n, s_, "y", device)
-            gerr = max(gerr, (buf[i * n:(i + 1) * n] - ref).abs().max().item())
-        check = dict(check or {}, gathered_max_abs_err=gerr)
-    checks = [check]
-    if world > 1 and args.check:
-        checks = [None] * world
-        dist.all_gather_object(checks, check)
+    parallelism = {
+        "stacked": f"dp{world} (one stacked 3-party session per GPU, no inter-GPU reshare)",
+        "cyclic": (f"{n_sessions} 3-party sessions on {world} GPUs, each party on its own "
+                   "GPU (cyclic layout): every reshare an RCCL send/recv" if world > 1 else
+                   "1 stacked 3-party session"),
+        "spmd": f"dp{n_sessions} x 3-party sessions, one party per GPU (RCCL reshare)",
+    }[layout]
+    line = _base_line(args, world)
+    line.update({
+        "value": value,
+        "ms_per_step": ms_per_step,
+        "vs_baseline": value / REFERENCE_ELEMS_PER_SEC,
+        "dtype": f"fixed(14,23) over Z_2^{args.ring} (exact multi-modular int8-MFMA GEMM)",
+        "layout": layout,
+        "step_streams": nstreams,
+        "gather": gather_mode,
+        "world_size": world,
+        "sessions": n_sessions,
+        "per_rank_ms_per_step": [r[0] / args.steps * 1e3 for r in per_rank],
+        # point-to-point traffic (inter-party shares over RCCL/xGMI) per step and rank
+        "p2p_bytes_per_step": [r[1] / args.steps for r in per_rank],
+        "p2p_messages_per_step": [r[2] / args.steps for r in per_rank],
+        "preflight": preflight,
+    })
+    line["config"].update(global_batch=n_sessions, parallelism=parallelism)
+    if step_ms:
+        line["step_ms_rank0"] = {"min": step_ms[0], "median": step_ms[len(step_ms) // 2],
+                                 "max": step_ms[-1]}
+    line["device"] = _device_info(device)
+    line["revision"] = _revision()
+    prog.headline_done(line)
 
+    exit_code = 0
+    if args.check:
+        prog.phase("check", min(args.watchdog, 300))
+        check = None
+        if out_owner:
+            ref = _inputs(n, out_session, "x", device) @ _inputs(n, out_session, "y", device)
+            check = {"rank": rank, "max_abs_err": (z - ref).abs().max().item()}
+        if gather_bufs is not None and (gather_mode == "all" or rank == root):
+            # the last step's collected outputs: rank r's revealed output is session s(r)'s
+            buf = gather_bufs[(n_steps[0] - 1) % 2]
+            sess_of = {"cyclic": lambda r: (r - 2) % world, "spmd": lambda r: r // 3,
+                       "stacked": lambda r: r}[layout]
+            gerr = 0.0
+            for i, r in enumerate(owners):
+                s_ = sess_of(r)
+                ref = _inputs(n, s_, "x", device) @ _inputs(n, s_, "y", device)
+                gerr = max(gerr, (buf[i * n:(i + 1) * n] - ref).abs().max().item())
+            check = dict(check or {"rank": rank}, gathered_max_abs_err=gerr)
+        checks = [check]
+        if world > 1:
+            checks = [None] * world
+            dist.all_gather_object(checks, check)
+        checks = [c for c in checks if c is not None]
+        worst = max([c.get("max_abs_err", 0.0) for c in checks]
+                    + [c.get("gathered_max_abs_err", 0.0) for c in checks] + [0.0])
+        line["check"] = {"ranks": len(checks), "max_abs_err": worst, "ok": worst < 1e-2}
+        if worst >= 1e-2:
+            line["error"] = f"wrong results: max abs error {worst} vs float64 torch"
+            exit_code = 4
+
+    if args.lr_runs > 0:
+        prog.phase("lr", min(args.watchdog, 300))
+        lr = {"model": "ml-inference-with-onnx tutorial LogisticRegression (200x10, "
+                       "fixed(24,40), Z_2^128, from_onnx)"}
+        if rank == 0:
+            lr["one_gpu"] = _lr_stacked(args.lr_runs, device)
+        if world > 1:
+            dist.barrier()
+        if world >= 3:
+            prog.phase("lr_spmd", min(args.watchdog, 300))
+            rec = _lr_spmd(args.lr_runs, world, rank, device, prog)
+            recs = [None] * world
+            dist.all_gather_object(recs, rec)
+            mine = [r for r in recs if r is not None and 0 in r.get("ranks", [])]
+            if mine:
+                r0 = dict(mine[0])
+                errs = [r.get("max_abs_err_vs_sklearn") for r in recs
+                        if r is not None and r.get("ranks") == r0["ranks"]
+                        and r.get("max_abs_err_vs_sklearn") is not None]
+                r0["max_abs_err_vs_sklearn"] = errs[0] if errs else None
+                lr["spmd_one_party_per_gpu"] = r0
+        if rank == 0:
+            line["lr_inference_p50_ms"] = {k: v["p50_ms"] for k, v in lr["one_gpu"].items()}
+            if "spmd_one_party_per_gpu" in lr:
+                line["lr_inference_p50_ms"]["spmd"] = lr["spmd_one_party_per_gpu"]["p50_ms"]
+            line["lr_inference"] = lr
+
+    prog.phase("done", 120)
     if rank == 0:
-        parallelism = {
-            "stacked": f"dp{world} (one stacked 3-party session per GPU, no inter-GPU reshare)",
-            "cyclic": (f"{n_sessions} 3-party sessions on {world} GPUs, each party on its own "
-                       "GPU (cyclic layout): every reshare an RCCL send/recv" if world > 1 else
-                       "1 stacked 3-party session"),
-            "spmd": f"dp{n_sessions} x 3-party sessions, one party per GPU (RCCL reshare)",
-        }[layout]
-        line = {
-            "metric": "replicated fixed(14,23) matmul elems/sec",
-            "value": value,
-            "unit": "output elems/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": value / REFERENCE_ELEMS_PER_SEC,
-            "dtype": f"fixed(14,23) over Z_2^{args.ring} (exact multi-modular int8-MFMA GEMM)",
-            "data": "synthetic uniform[-4,4) inputs, device resident",
-            "config": {
-                "model": f"replicated fixed(14,23) RingDot {n}x{n} (share+dot+trunc_pr+reveal)",
-                "global_batch": n_sessions,
-                "seq_len": n,
-                "parallelism": parallelism,
-            },
-            "layout": layout,
-            "step_streams": len(streams) if streams is not None else 1,
-            "gather": gather_mode,
-            "world_size": world,
-            "sessions": n_sessions,
-            "per_rank_ms_per_step": [t / args.steps * 1e3 for t in per_rank],
-            # rank 0's point-to-point traffic (inter-party shares over RCCL/xGMI) per step
-            "p2p_bytes_per_step_rank0": p2p[0],
-            "p2p_messages_per_step_rank0": p2p[1],
-        }
-        if step_ms:
-            line["step_ms_rank0"] = {"min": step_ms[0], "median": step_ms[len(step_ms) // 2],
-                                     "max": step_ms[-1]}
-        line["device"] = _device_info(device)
-        line["revision"] = _revision()
-        if args.check:
-            line["check"] = [c for c in checks if c is not None]
         print(json.dumps(line), flush=True)
+    prog.disarm()
     if world > 1:
         dist.destroy_process_group()
+    if exit_code:
+        sys.exit(exit_code)
 
 
 if __name__ == "__main__":

@@ -41,6 +41,7 @@
 #include <cstring>
 #include <mutex>
 
+#include "hip_attr.h"
 #include "moosex.h"
 
 namespace {
@@ -937,11 +938,7 @@ void launch_variant(const CPlan& p, const Tables& tb, int64_t batch, const int8_
   constexpr int lds = kStages * (kImg + BN * BK);
   const void* fn = M16 ? (const void*)k_crt_gemm16<WR, WC, BN, MINW>
                        : (const void*)k_crt_gemm<WR, WC, BN, MINW>;
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    attr = true;
-  }
+  ensure_lds_attr(fn, lds, st);
   const dim3 grid((unsigned)(p.tiles_m * p.tiles_n), (unsigned)(batch * p.n));
   if constexpr (M16)
     hipLaunchKernelGGL((k_crt_gemm16<WR, WC, BN, MINW>), grid, dim3(64 * WR * WC), lds, st, ra,

@@ -33,6 +33,7 @@
 #include <cstdlib>
 #include <mutex>
 
+#include "hip_attr.h"
 #include "moosex.h"
 
 using u64 = uint64_t;
@@ -872,18 +873,10 @@ void launch_gemm(const Plan& p, int64_t batch, int64_t M, int64_t N, const int8_
   constexpr int L = Limbs<T>::L;
   const int64_t ntiles = (p.Mp / TM) * (p.Np / TN);
   const size_t lds = 4 * (size_t)L * kTileBytes;  // 2 buffers x (A + B) stages
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute((const void*)k_gemm_limb<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)lds);
-    hipFuncSetAttribute((const void*)k_gemm_limb128_split,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipFuncSetAttribute((const void*)k_gemm128_v2, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        4 * 16 * kTileBytes);
-    hipFuncSetAttribute((const void*)k_gemm64_v2, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        2 * 3 * 8 * kTileBytes);
-    attr_set = true;
-  }
+  ensure_lds_attr((const void*)k_gemm_limb<T>, (int)lds, st);
+  ensure_lds_attr((const void*)k_gemm_limb128_split, (int)lds, st);
+  ensure_lds_attr((const void*)k_gemm128_v2, 4 * 16 * kTileBytes, st);
+  ensure_lds_attr((const void*)k_gemm64_v2, 2 * 3 * 8 * kTileBytes, st);
   if (!use_v1_kernels()) {
     if constexpr (sizeof(T) == 16) {
       hipLaunchKernelGGL(k_gemm128_v2, dim3((unsigned)ntiles, (unsigned)batch), dim3(512),

@@ -771,6 +771,11 @@ def dot_cross_pair(x0: RT, y0: RT, y1: RT, roll: int, pb: PreparedCross = None, 
             return None
         N, lb, b0, b1 = pb.N, nat.ptr(pb.lb), None, None
     else:
+        # [batch, K, N] right operands only (a stacked secret vector [batch, K] takes the
+        # generic dot_cross path, which handles rank-1 operands)
+        if (len(y0.shape) != 3 or tuple(y1.shape) != tuple(y0.shape)
+                or y0.shape[0] != batch or y0.shape[1] != K):
+            return None
         N = y0.shape[2]
         b0, b1 = y0.data.contiguous(), y1.data.contiguous()
         lb = None

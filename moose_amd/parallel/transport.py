@@ -233,9 +233,13 @@ class Transport:
         for out, src in recvs:
             if out.numel() == 0:
                 continue
-            buf = torch.empty(out.shape, dtype=out.dtype) if self.stage else out
             if self.stage or not out.is_contiguous():
+                # a contiguous landing buffer (host memory when staging), copied into out
+                buf = torch.empty(out.shape, dtype=out.dtype,
+                                  device="cpu" if self.stage else out.device)
                 staged.append((out, buf))
+            else:
+                buf = out
             ops.append(dist.P2POp(dist.irecv, buf, src, group=self.group))
         if ops:
             for w in dist.batch_isend_irecv(ops):

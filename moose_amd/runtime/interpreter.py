@@ -150,6 +150,9 @@ class Interpreter:
         finally:
             if lanes is not None:
                 lanes.finish()
+            release = getattr(self.sess, "end_evaluation", None)
+            if release is not None:
+                release()
         return self.outputs
 
     def _run_op(self, op, ops, idx, batch, me):
@@ -208,6 +211,8 @@ class Interpreter:
                 break
             if o.kind != "Dot" or o.name in self.env or any(n not in self.env for n in o.inputs):
                 continue
+            if self.lanes is not None and not self.lanes.ordered_here(o.inputs):
+                continue  # an operand from another lane this lane has not waited on
             if self._table_handler(o) is not None:
                 continue
             k = key(o)

@@ -205,6 +205,14 @@ class LaneRunner:
         _trace("enter", op.name, op.kind, "lane", ln)
         torch.cuda.set_stream(s)
 
+    def ordered_here(self, names) -> bool:
+        """Every value in ``names`` is safe to read on the current lane without a new wait:
+        produced on it, produced before the lanes forked, or already waited on (its tensors
+        then carry a record_stream for this lane).  Ops executed ahead of their own turn
+        (batched Dots) are restricted to such operands."""
+        ln = self.cur
+        return all(self.where.get(n, ln) == ln or n in self.waited[ln] for n in names)
+
     def leave(self, names):
         """Values ``names`` were just produced on the current lane."""
         ln = self.cur

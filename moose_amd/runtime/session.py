@@ -36,6 +36,7 @@ import torch
 
 from moose_amd.ir.computation import ReplicatedPlacement
 from moose_amd.ops import ring as R
+from moose_amd.runtime import lanes as _lanes
 from moose_amd.runtime.prims import PRIMS
 from moose_amd.utils import telemetry
 
@@ -514,7 +515,10 @@ class StackedSession(Session):
         one evaluation (e.g. a chain z = z.y) has its GEMM operand image prepared once, from
         its second use on; every product is still computed."""
         yv0, yv1 = y0.v, y1.v
+        # (not while dataflow lanes run: a prepared image produced on one lane would be
+        # read by products on other lanes without an event)
         if (nbatch == 0 and self.device.type == "cuda" and len(yv0.shape) == 3
+                and not _lanes.ACTIVE
                 and len(x0.v.shape) == 3 and min(x0.v.shape[1], yv0.shape[1], yv0.shape[2]) >= 256):
             # (large products only: small ones run the VALU GEMM, which has no prepared form)
             cache = self.__dict__.setdefault("_prepared_b", {})
@@ -529,11 +533,17 @@ class StackedSession(Session):
                     return self.p_dot_cross_rows(plc, x0, x1, 0, x0.v.shape[1], pb)
             elif len(cache) < 64:
                 cache[key] = (yv0.data, yv1.data, None)  # holds the tensors: ids stay unique
-        if nbatch == 0 and self.pair_rolled and self.device.type == "cuda":
+        if (nbatch == 0 and self.pair_rolled and self.device.type == "cuda"
+                and len(yv0.shape) == 3):
             v = R.dot_cross_pair(x0.v, yv0, yv1, 1)
             if v is not None:
                 return PV(plc, v)
         return PV(plc, R.dot_cross(x0.v, x1.v, y0.v, y1.v, nb=1 + nbatch))
+
+    def end_evaluation(self):
+        """Drop per-evaluation caches (prepared GEMM operands hold device memory and must
+        not outlive the evaluation whose values they were prepared from)."""
+        self.__dict__.pop("_prepared_b", None)
 
     def p_add_zero_share(self, plc, z, kind="arith"):
         return PV(plc, R.rss_cross_k(kind, z.v, None, None, None, self.key_ptr(plc, 0), 3,

@@ -22,7 +22,8 @@ def _port():
 def _run(n, *extra):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py",
-           "--gpus", str(n), "--steps", "2", "--warmup", "1", "--size", "64", *extra]
+           "--gpus", str(n), "--steps", "2", "--warmup", "1", "--size", "64", "--lr-runs", "0",
+           *extra]
     out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
@@ -42,7 +43,7 @@ def test_bench_json_line(n, layout):
 def _run_self(n, *extra):
     """No launcher: bench.py --gpus N spawns its N ranks itself."""
     cmd = [sys.executable, "bench.py", "--gpus", str(n), "--steps", "2", "--warmup", "1",
-           "--size", "48", "--check", *extra]
+           "--size", "48", "--lr-runs", "0", *extra]
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
     assert out.returncode == 0, out.stderr[-3000:]
@@ -59,6 +60,66 @@ def test_bench_self_launch(n, layout, sessions):
     assert d["layout"] == ("cyclic" if layout == "auto" else layout)
     assert len(d["per_rank_ms_per_step"]) == n
     assert d["ms_per_step"] == pytest.approx(max(d["per_rank_ms_per_step"]))
-    assert d["check"] and all(c["max_abs_err"] < 1e-4 for c in d["check"])
+    # every output owner checked its last output (and rank 0 the collected outputs)
+    assert d["check"]["ok"] and d["check"]["max_abs_err"] < 1e-4
+    assert d["check"]["ranks"] == (1 if layout == "spmd" else n)
+    assert d["preflight"]["ok"]
+    assert len(d["p2p_bytes_per_step"]) == n
     if sessions > 1:  # rank 0 (the client) collected every session's revealed output
-        assert d["gather"] == "root" and d["check"][0]["gathered_max_abs_err"] < 1e-4
+        assert d["gather"] == "root"
+    if d["layout"] == "cyclic":  # every reshare crossed ranks
+        assert min(d["p2p_bytes_per_step"]) > 0 and d["step_streams"] == 2
+
+
+def test_bench_lr_inference_in_line():
+    """The second half of the headline metric: LR-inference p50 in the same JSON line
+    (one GPU eager/graphs, and with >= 3 ranks one party per rank)."""
+    cmd = [sys.executable, "bench.py", "--gpus", "3", "--steps", "1", "--warmup", "1",
+           "--size", "32", "--lr-runs", "2"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    p50 = d["lr_inference_p50_ms"]
+    assert {"eager", "graphs", "spmd"} <= set(p50) and all(v > 0 for v in p50.values())
+    lr = d["lr_inference"]
+    assert lr["one_gpu"]["eager"]["max_abs_err_vs_sklearn"] < 1e-3
+    assert lr["spmd_one_party_per_gpu"]["max_abs_err_vs_sklearn"] < 1e-3
+
+
+@pytest.mark.parametrize("phase,rank", [("timed", 2), ("preflight", 1)])
+def test_bench_stalled_rank_fails_loudly(phase, rank):
+    """A rank that hangs makes bench.py --gpus 3 exit non-zero within its watchdog budget
+    with an error line naming the stalled rank."""
+    cmd = [sys.executable, "bench.py", "--gpus", "3", "--steps", "2", "--warmup", "1",
+           "--size", "32", "--lr-runs", "0", "--watchdog", "15"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["MOOSEX_BENCH_STALL"] = f"{rank}:{phase}"
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode != 0
+    d = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["value"] is None and "error" in d
+    assert d["stalled_ranks"] == [rank]
+    assert d["phases"][str(rank)]["phase"] == phase
+
+
+def test_supervisor_kills_a_hung_rank_group(tmp_path):
+    """The self-launch parent's wall-clock limit: a child group that never finishes is
+    killed and an error line is printed from the phase files."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location(
+        "bw", os.path.join(ROOT, "moose_amd", "utils", "benchwatch.py"))
+    bw = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bw)
+    (tmp_path / "rank0.json").write_text(json.dumps({"phase": "timed", "seq": 4, "step": 3}))
+    (tmp_path / "rank1.json").write_text(json.dumps({"phase": "timed", "seq": 4, "step": 0}))
+    import contextlib
+    import io
+
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        rc = bw.supervise([sys.executable, "-c", "import time; time.sleep(600)"], dict(os.environ),
+                          2, 2.0, {"metric": "m"}, str(tmp_path))
+    d = json.loads(buf.getvalue().strip().splitlines()[-1])
+    assert rc == 3 and d["stalled_ranks"] == [1] and "error" in d

@@ -71,3 +71,30 @@ def test_lowered_graph_on_gpu(args):
     for k in ref:
         np.testing.assert_allclose(np.asarray(got[k], dtype=float), np.asarray(ref[k], dtype=float),
                                    atol=5e-3)
+
+
+@pytest.mark.parametrize("shapes", [((300, 260), (260,)), ((260,), (260, 300)), ((64, 96), (96,))])
+def test_secret_matrix_vector_dot(shapes):
+    """Secret matrix . secret vector (and vector . matrix) at fixed(24, 40): the stacked
+    right operand is [3, K], which the rolled-pair CRT GEMM must decline."""
+    fp = pm.fixed(24, 40)
+    alice, bob, carole = (pm.host_placement(n) for n in ("alice", "bob", "carole"))
+    rep = pm.replicated_placement("rep", players=[alice, bob, carole])
+
+    @pm.computation
+    def f(x: pm.Argument(placement=alice, vtype=pm.TensorType(pm.float64)),
+          y: pm.Argument(placement=bob, vtype=pm.TensorType(pm.float64))):
+        with alice:
+            xf = pm.cast(x, dtype=fp)
+        with bob:
+            yf = pm.cast(y, dtype=fp)
+        with rep:
+            z = pm.dot(xf, yf)
+        with carole:
+            return pm.cast(z, dtype=pm.float64)
+
+    rng = np.random.default_rng(11)
+    x, y = rng.uniform(-1, 1, shapes[0]), rng.uniform(-1, 1, shapes[1])
+    rt = LocalMooseRuntime(["alice", "bob", "carole"], device="cuda")
+    got = rt.evaluate_computation(f, {"x": x, "y": y})["output_0"]
+    np.testing.assert_allclose(got, x @ y, atol=1e-6)

@@ -75,3 +75,60 @@ def test_lanes_match_single_stream_bitwise(graphs):
         np.testing.assert_allclose(outs[lanes], ref, atol=1e-4)
     if not graphs:  # same seed, same program order of PRF draws -> identical shares
         np.testing.assert_array_equal(outs[1], outs[4])
+
+
+def test_batched_ops_only_read_values_ordered_on_their_lane():
+    """A Dot executed ahead of its turn (batched into an earlier Dot's launch) runs on the
+    earlier Dot's lane: its operands must be produced there, before the fork, or already
+    waited on (no event existed for a same-lane producer of a later Dot)."""
+    from moose_amd.runtime.lanes import LaneRunner
+
+    r = LaneRunner("cpu", 2)
+    r.cur = 0
+    r.where = {"w0": 0, "w1": 1, "x": 0}
+    r.waited = [set(), set()]
+    assert r.ordered_here(["x", "w0"])
+    assert r.ordered_here(["arg"])          # produced before the lanes forked
+    assert not r.ordered_here(["x", "w1"])  # lane 1's value, never waited on by lane 0
+    r.waited[0].add("w1")
+    assert r.ordered_here(["x", "w1"])
+
+
+@pytest.mark.gpu
+def test_lanes_slow_producer_on_other_lane():
+    """Weights of later Dots come from long chains on other lanes; the result must match
+    the single-stream run however the lanes interleave."""
+    alice, bob, carole = (pm.host_placement(x) for x in ("alice", "bob", "carole"))
+    rep = pm.replicated_placement("rep", players=[alice, bob, carole])
+    fx = pm.fixed(24, 40)
+    rng = np.random.default_rng(4)
+    ws = [rng.normal(size=(512, 256)) * 0.05 for _ in range(4)]
+
+    @pm.computation
+    def f(x: pm.Argument(placement=alice, vtype=pm.TensorType(pm.float64))):
+        with alice:
+            xf = pm.cast(x, dtype=fx)
+        wf = []
+        with bob:
+            for i, w in enumerate(ws):
+                c = pm.constant(w, dtype=pm.float64)
+                for _ in range(8 * i):  # slower producers for later branches
+                    c = pm.add(c, pm.constant(np.zeros_like(w), dtype=pm.float64))
+                wf.append(pm.cast(c, dtype=fx))
+        with rep:
+            ys = [pm.dot(xf, w) for w in wf]
+            acc = ys[0]
+            for y in ys[1:]:
+                acc = pm.add(acc, y)
+        with carole:
+            return pm.cast(acc, dtype=pm.float64)
+
+    x = rng.normal(size=(256, 512)) * 0.05
+    outs = {}
+    for lanes in (1, 4):
+        rt = pm.LocalMooseRuntime(["alice", "bob", "carole"], device="cuda", seed=5,
+                                  lanes=lanes)
+        outs[lanes] = np.asarray(list(rt.evaluate_computation(f, {"x": x}).values())[0])
+    np.testing.assert_allclose(outs[1], sum(x @ w for w in ws), atol=1e-6)
+    # (batching may differ between the runs, and with it the TruncPr rounding: 1 ulp)
+    np.testing.assert_allclose(outs[1], outs[4], atol=1e-9)
