@@ -263,6 +263,24 @@ int mx_trunc_party_r1(int dev, int words, int64_t n, int m, int ncomp, const int
 int mx_share_party(int dev, int kind, int words, int64_t n, int ncomp, const int* rel,
                    const void* x, void* out0, void* out1, const uint32_t* const* slots,
                    uint64_t n1, uint64_t na, void* stream);
+// Fixed-point dot tail (rep.dot_trunc) with the parties on different GPUs: the reshare of
+// the dot is folded into TruncPr's first round (rss_party.hip).  Every array argument is
+// an array of ncomp per-component pointers (entries a role does not use may be null).
+// nonces: zero share, r0, r1, t, m, z0, z2.  r0: messages (P0 m0, P1 m1, P2 z2) in msg, the
+// dealer's rt1 / rm1 (u64) in msg_rt / msg_rm, P2's new shares; r1: rmk = the other
+// party's message, rz = z2, rrt / rrm = dealer shares (P1) -> w, P0's s0 / P1's s1;
+// r2: out = a + b (P0's s1, P1's s0).
+int mx_dot_tail_r0(int dev, int words, int64_t n, int m, int ncomp, const int* roles,
+                   const void* const* cross, void* const* msg, void* const* msg_rt,
+                   void* const* msg_rm, void* const* out0, void* const* out1,
+                   const uint32_t* const* slots, const uint64_t* nonces, void* stream);
+int mx_dot_tail_r1(int dev, int words, int64_t n, int m, int ncomp, const int* roles,
+                   const void* const* msg, const void* const* rmk, const void* const* rz,
+                   const void* const* rrt, const void* const* rrm, void* const* w,
+                   void* const* out0, void* const* out1, const uint32_t* const* slots,
+                   const uint64_t* nonces, void* stream);
+int mx_dot_tail_r2(int dev, int words, int64_t n, int ncomp, const int* roles,
+                   const void* const* a, const void* const* b, void* const* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -241,6 +241,211 @@ inline Roles roles_of(const int* r, int ncomp) {
   return o;
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Fixed-point dot tail (rep.dot_trunc) for parties on different GPUs.  Input: each party's
+// local cross products (the RSS dot's GEMM output).  The reshare of rep.dot is folded into
+// TruncPr's first round: P_p's product masked by the zero share is z_p (3-out-of-3
+// additive), and the opening c = x + r + 2^(k-2) of TruncPr is assembled from
+//   P0: m0 = z0 + 2^(k-2) + r0   -> P1
+//   P1: m1 = z1 + r1              -> P0
+//   P2: z2                        -> P0 and P1        (+ the dealer's rt1, rm1 -> P1)
+// so both P0 and P1 get c = m0 + m1 + z2 in ONE round (the generic path needs the
+// reshare round plus the P0 <-> P1 round).  c is the same value, and every output share
+// depends on the input only through c, so the shares are bitwise equal to reshare +
+// TruncPr (and to the stacked fused kernel).  Round 1 is k_trunc_party_r1's with the
+// three-term c; round 2 adds the exchanged w's.  Every array argument is a per-component
+// pointer triple (component slots need not be adjacent: rows of a larger stack, buffers
+// received from other GPUs, or -- one party per process at N = 1 -- the sender's buffer).
+// ---------------------------------------------------------------------------------------
+struct CP3 {
+  const void* p[3];
+};
+struct WP3 {
+  void* p[3];
+};
+
+template <class T>
+__device__ __forceinline__ const T* cp(const CP3& a, int c) {
+  return (const T*)a.p[c];
+}
+template <class T>
+__device__ __forceinline__ T* wp(const WP3& a, int c) {
+  return (T*)a.p[c];
+}
+
+template <class T>
+__global__ void __launch_bounds__(256)
+    k_dot_tail_r0(int64_t n, int m, Roles roles, CP3 cross, WP3 msg, WP3 msg_rt, WP3 msg_rm,
+                  WP3 out0, WP3 out1, mxd::KeySrc keys, uint64_t n_a, uint64_t n_r0,
+                  uint64_t n_r1, uint64_t n_t, uint64_t n_m, uint64_t n_z0, uint64_t n_z2,
+                  int ncomp) {
+  __shared__ uint32_t rks[mxd::kMaxKeySlots][mxd::kKeyWords];
+  mxd::stage_keys(rks, keys, 2 * ncomp);
+  constexpr int P = mxd::Lane<T>::kPer;
+  const int64_t nb = (n + P - 1) / P;
+  MX_PARTY_WALK(nb, ncomp) {
+    const int c = (int)(g / nblk);
+    const uint64_t B = (uint64_t)(g - c * nblk);
+    const int role = roles.r[c];
+    if (role < 0 || role > 2) continue;
+    const uint32_t* own = rks[2 * c];
+    const uint32_t* nxt = rks[2 * c + 1];
+    const T* x = cp<T>(cross, c);
+    T* mo = wp<T>(msg, c);
+    // zero share alpha_p = PRF(k_p) - PRF(k_{p+1}) and this role's opening mask
+    uint32_t wa[16], wb[16], wr[16];
+    mx::chacha_block(own, n_a, B, wa);
+    mx::chacha_block(nxt, n_a, B, wb);
+    if (role == 0) mx::chacha_block(own, n_r0, B, wr);
+    if (role == 1) mx::chacha_block(nxt, n_r1, B, wr);
+#pragma unroll
+    for (int part = 0; part < 4; ++part) {
+      const int64_t b = (int64_t)mx::ks_chunk(B, part);
+      if (b >= nb) break;
+      uint64_t al, ah, bl, bh, rl = 0, rh = 0;
+      mx::part_u64(wa, part, &al, &ah);
+      mx::part_u64(wb, part, &bl, &bh);
+      if (role != 2) mx::part_u64(wr, part, &rl, &rh);
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const int64_t i = b * P + j;
+        if (i >= n) break;
+        const T z = x[i] + mxd::pick<T>(al, ah, j) - mxd::pick<T>(bl, bh, j);
+        if (role == 0)
+          mo[i] = mxf::trunc_mask0<T>(z, (T)0, mxd::pick<T>(rl, rh, j));
+        else if (role == 1)
+          mo[i] = z + mxd::pick<T>(rl, rh, j);
+        else
+          mo[i] = z;
+      }
+    }
+    if (role == 2) {  // dealer (as k_trunc_party_r0): streams r0, r1, t, m, z0, z2
+      uint32_t w[6][16];
+      mx::chacha_block(nxt, n_r0, B, w[0]);
+      mx::chacha_block(own, n_r1, B, w[1]);
+      mx::chacha_block(nxt, n_t, B, w[2]);
+      mx::chacha_block(nxt, n_m, B, w[3]);
+      mx::chacha_block(nxt, n_z0, B, w[4]);
+      mx::chacha_block(own, n_z2, B, w[5]);
+      T* rt = wp<T>(msg_rt, c);
+      u64* rm = wp<u64>(msg_rm, c);
+      T* o0 = wp<T>(out0, c);
+      T* o1 = wp<T>(out1, c);
+#pragma unroll
+      for (int part = 0; part < 4; ++part) {
+        const int64_t b = (int64_t)mx::ks_chunk(B, part);
+        if (b >= nb) break;
+        uint64_t lo[6], hi[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) mx::part_u64(w[q], part, &lo[q], &hi[q]);
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+          const int64_t i = b * P + j;
+          if (i >= n) break;
+          T rt1;
+          u64 rm1;
+          mxf::trunc_dealer<T>(mxd::pick<T>(lo[0], hi[0], j), mxd::pick<T>(lo[1], hi[1], j),
+                               mxd::pick<T>(lo[2], hi[2], j), mxd::pick<T>(lo[3], hi[3], j), m,
+                               &rt1, &rm1);
+          rt[i] = rt1;
+          rm[i] = rm1;
+          o0[i] = mxd::pick<T>(lo[5], hi[5], j);
+          o1[i] = mxd::pick<T>(lo[4], hi[4], j);
+        }
+      }
+    }
+  }
+}
+
+// P0 / P1: c = own message + the other's + z2 (rz may be null: the two-term opening of
+// k_trunc_party_r0's protocol), then y, w = y - z and the PRF share of the new sharing.
+template <class T>
+__global__ void __launch_bounds__(256)
+    k_dot_tail_r1(int64_t n, int m, Roles roles, CP3 msg, CP3 rmk, CP3 rz, CP3 rrt, CP3 rrm,
+                  WP3 w, WP3 out0, WP3 out1, mxd::KeySrc keys, uint64_t n_t, uint64_t n_m,
+                  uint64_t n_z0, uint64_t n_z2, int ncomp) {
+  __shared__ uint32_t rks[mxd::kMaxKeySlots][mxd::kKeyWords];
+  mxd::stage_keys(rks, keys, 2 * ncomp);
+  constexpr int P = mxd::Lane<T>::kPer;
+  const int64_t nb = (n + P - 1) / P;
+  MX_PARTY_WALK(nb, ncomp) {
+    const int c = (int)(g / nblk);
+    const uint64_t B = (uint64_t)(g - c * nblk);
+    const int role = roles.r[c];
+    if (role != 0 && role != 1) continue;
+    const T* mine = cp<T>(msg, c);
+    const T* other = cp<T>(rmk, c);
+    const T* z2m = cp<T>(rz, c);
+    T* wo = wp<T>(w, c);
+    uint32_t wt[16], wm[16], wz[16];
+    if (role == 0) {
+      const uint32_t* k0 = rks[2 * c];
+      mx::chacha_block(k0, n_t, B, wt);
+      mx::chacha_block(k0, n_m, B, wm);
+      mx::chacha_block(k0, n_z0, B, wz);
+    } else {
+      mx::chacha_block(rks[2 * c + 1], n_z2, B, wz);
+    }
+    const T* rt = cp<T>(rrt, c);
+    const u64* rm = cp<u64>(rrm, c);
+    T* o = role == 0 ? wp<T>(out0, c) : wp<T>(out1, c);
+#pragma unroll
+    for (int part = 0; part < 4; ++part) {
+      const int64_t b = (int64_t)mx::ks_chunk(B, part);
+      if (b >= nb) break;
+      uint64_t tl = 0, th = 0, ml = 0, mh = 0, zl, zh;
+      if (role == 0) {
+        mx::part_u64(wt, part, &tl, &th);
+        mx::part_u64(wm, part, &ml, &mh);
+      }
+      mx::part_u64(wz, part, &zl, &zh);
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const int64_t i = b * P + j;
+        if (i >= n) break;
+        T cc = mine[i] + other[i];
+        if (z2m != nullptr) cc += z2m[i];
+        const T z = mxd::pick<T>(zl, zh, j);
+        const T y = role == 0
+                        ? mxf::trunc_y<T>(cc, mxd::pick<T>(tl, th, j), mxd::pick<T>(ml, mh, j), m,
+                                          true)
+                        : mxf::trunc_y<T>(cc, rt[i], (T)rm[i], m, false);
+        wo[i] = y - z;
+        o[i] = z;
+      }
+    }
+  }
+}
+
+// out[c] = a[c] + b[c] for the components in role 0 or 1 (P0's s1, P1's s0 = w0 + w1)
+template <class T>
+__global__ void __launch_bounds__(256)
+    k_dot_tail_r2(int64_t n, Roles roles, CP3 a, CP3 b, WP3 out, int ncomp) {
+  const int64_t total = n * ncomp;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(g / n);
+    const int64_t i = g - (int64_t)c * n;
+    const int role = roles.r[c];
+    if (role != 0 && role != 1) continue;
+    wp<T>(out, c)[i] = cp<T>(a, c)[i] + cp<T>(b, c)[i];
+  }
+}
+
+inline CP3 cp3(const void* const* a, int ncomp) {
+  CP3 o{{nullptr, nullptr, nullptr}};
+  if (a)
+    for (int c = 0; c < ncomp; ++c) o.p[c] = a[c];
+  return o;
+}
+inline WP3 wp3(void* const* a, int ncomp) {
+  WP3 o{{nullptr, nullptr, nullptr}};
+  if (a)
+    for (int c = 0; c < ncomp; ++c) o.p[c] = a[c];
+  return o;
+}
+
 }  // namespace
 
 extern "C" {
@@ -323,6 +528,81 @@ int mxh_share_party(int kind, int words, int64_t n, int ncomp, const int* rel, c
     default:
       return -2;
   }
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : -100 - (int)e;
+}
+
+
+int mxh_dot_tail_r0(int words, int64_t n, int m, int ncomp, const int* roles,
+                    const void* const* cross, void* const* msg, void* const* msg_rt,
+                    void* const* msg_rm, void* const* out0, void* const* out1,
+                    const uint32_t* const* slots, const uint64_t* nn, void* stream) {
+  if (n == 0) return 0;
+  if (ncomp < 1 || ncomp > 3) return -3;
+  const mxd::KeySrc k = mxd::keysrc_slots(slots, 2 * ncomp);
+  const Roles rr = roles_of(roles, ncomp);
+  hipStream_t st = (hipStream_t)stream;
+  const CP3 x = cp3(cross, ncomp);
+  const WP3 mo = wp3(msg, ncomp), rt = wp3(msg_rt, ncomp), rm = wp3(msg_rm, ncomp),
+            o0 = wp3(out0, ncomp), o1 = wp3(out1, ncomp);
+  if (words == 1) {
+    hipLaunchKernelGGL(k_dot_tail_r0<u64>, dim3(mxd::grid_for_chunks((n + 1) / 2) * ncomp),
+                       dim3(256), 0, st, n, m, rr, x, mo, rt, rm, o0, o1, k, nn[0], nn[1],
+                       nn[2], nn[3], nn[4], nn[5], nn[6], ncomp);
+  } else if (words == 2) {
+    hipLaunchKernelGGL(k_dot_tail_r0<u128>, dim3(mxd::grid_for_chunks(n) * ncomp), dim3(256), 0,
+                       st, n, m, rr, x, mo, rt, rm, o0, o1, k, nn[0], nn[1], nn[2], nn[3], nn[4],
+                       nn[5], nn[6], ncomp);
+  } else {
+    return -2;
+  }
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : -100 - (int)e;
+}
+
+int mxh_dot_tail_r1(int words, int64_t n, int m, int ncomp, const int* roles,
+                    const void* const* msg, const void* const* rmk, const void* const* rz,
+                    const void* const* rrt, const void* const* rrm, void* const* w,
+                    void* const* out0, void* const* out1, const uint32_t* const* slots,
+                    const uint64_t* nn, void* stream) {
+  if (n == 0) return 0;
+  if (ncomp < 1 || ncomp > 3) return -3;
+  const mxd::KeySrc k = mxd::keysrc_slots(slots, 2 * ncomp);
+  const Roles rr = roles_of(roles, ncomp);
+  hipStream_t st = (hipStream_t)stream;
+  const CP3 a = cp3(msg, ncomp), b = cp3(rmk, ncomp), z = cp3(rz, ncomp), t = cp3(rrt, ncomp),
+            r = cp3(rrm, ncomp);
+  const WP3 wo = wp3(w, ncomp), o0 = wp3(out0, ncomp), o1 = wp3(out1, ncomp);
+  if (words == 1) {
+    hipLaunchKernelGGL(k_dot_tail_r1<u64>, dim3(mxd::grid_for_chunks((n + 1) / 2) * ncomp),
+                       dim3(256), 0, st, n, m, rr, a, b, z, t, r, wo, o0, o1, k, nn[3], nn[4],
+                       nn[5], nn[6], ncomp);
+  } else if (words == 2) {
+    hipLaunchKernelGGL(k_dot_tail_r1<u128>, dim3(mxd::grid_for_chunks(n) * ncomp), dim3(256), 0,
+                       st, n, m, rr, a, b, z, t, r, wo, o0, o1, k, nn[3], nn[4], nn[5], nn[6],
+                       ncomp);
+  } else {
+    return -2;
+  }
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : -100 - (int)e;
+}
+
+int mxh_dot_tail_r2(int words, int64_t n, int ncomp, const int* roles, const void* const* a,
+                    const void* const* b, void* const* out, void* stream) {
+  if (n == 0) return 0;
+  if (ncomp < 1 || ncomp > 3) return -3;
+  const Roles rr = roles_of(roles, ncomp);
+  hipStream_t st = (hipStream_t)stream;
+  const CP3 x = cp3(a, ncomp), y = cp3(b, ncomp);
+  const WP3 o = wp3(out, ncomp);
+  const int grid = mxd::grid_for(n * ncomp);
+  if (words == 1)
+    hipLaunchKernelGGL(k_dot_tail_r2<u64>, dim3(grid), dim3(256), 0, st, n, rr, x, y, o, ncomp);
+  else if (words == 2)
+    hipLaunchKernelGGL(k_dot_tail_r2<u128>, dim3(grid), dim3(256), 0, st, n, rr, x, y, o, ncomp);
+  else
+    return -2;
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : -100 - (int)e;
 }

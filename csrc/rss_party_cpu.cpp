@@ -24,6 +24,17 @@ int mxh_trunc_party_r1(int words, int64_t n, int m, int ncomp, const int* roles,
 int mxh_share_party(int kind, int words, int64_t n, int ncomp, const int* rel, const void* x,
                     void* out0, void* out1, const uint32_t* const* slots, uint64_t n1,
                     uint64_t na, void* stream);
+int mxh_dot_tail_r0(int words, int64_t n, int m, int ncomp, const int* roles,
+                    const void* const* cross, void* const* msg, void* const* msg_rt,
+                    void* const* msg_rm, void* const* out0, void* const* out1,
+                    const uint32_t* const* slots, const uint64_t* nn, void* stream);
+int mxh_dot_tail_r1(int words, int64_t n, int m, int ncomp, const int* roles,
+                    const void* const* msg, const void* const* rmk, const void* const* rz,
+                    const void* const* rrt, const void* const* rrm, void* const* w,
+                    void* const* out0, void* const* out1, const uint32_t* const* slots,
+                    const uint64_t* nn, void* stream);
+int mxh_dot_tail_r2(int words, int64_t n, int ncomp, const int* roles, const void* const* a,
+                    const void* const* b, void* const* out, void* stream);
 }
 
 namespace {
@@ -152,6 +163,104 @@ int share_party(int kind, int64_t n, int ncomp, const int* rel, const T* x, T* o
   return 0;
 }
 
+
+// ---- fixed-point dot tail (see rss_party.hip: reshare folded into TruncPr round A) ----
+template <class T>
+int dot_tail_r0(int64_t n, int m, int ncomp, const int* roles, const void* const* cross,
+                void* const* msg, void* const* msg_rt, void* const* msg_rm, void* const* out0,
+                void* const* out1, const uint32_t* const* slots, const uint64_t* nn) {
+  for (int c = 0; c < ncomp; ++c) {
+    const int role = roles[c];
+    if (role < 0 || role > 2) continue;
+    const uint32_t* own = slots[2 * c];
+    const uint32_t* nxt = slots[2 * c + 1];
+    const T* x = (const T*)cross[c];
+    T* mo = (T*)msg[c];
+    for_chunks<T>(n, [&](int64_t i0, int64_t len) {
+      std::vector<T> a(len), b(len), r(len);
+      prf<T>(own, nn[0], i0, len, a.data());
+      prf<T>(nxt, nn[0], i0, len, b.data());
+      if (role == 0) prf<T>(own, nn[1], i0, len, r.data());
+      if (role == 1) prf<T>(nxt, nn[2], i0, len, r.data());
+      for (int64_t q = 0; q < len; ++q) {
+        const int64_t i = i0 + q;
+        const T z = x[i] + a[q] - b[q];
+        mo[i] = role == 0 ? mxf::trunc_mask0<T>(z, (T)0, r[q]) : role == 1 ? (T)(z + r[q]) : z;
+      }
+      if (role == 2) {
+        std::vector<T> r0(len), r1(len), t(len), mm(len), z0(len), z2(len);
+        prf<T>(nxt, nn[1], i0, len, r0.data());
+        prf<T>(own, nn[2], i0, len, r1.data());
+        prf<T>(nxt, nn[3], i0, len, t.data());
+        prf<T>(nxt, nn[4], i0, len, mm.data());
+        prf<T>(nxt, nn[5], i0, len, z0.data());
+        prf<T>(own, nn[6], i0, len, z2.data());
+        T* rt = (T*)msg_rt[c];
+        u64* rm = (u64*)msg_rm[c];
+        for (int64_t q = 0; q < len; ++q) {
+          const int64_t i = i0 + q;
+          mxf::trunc_dealer<T>(r0[q], r1[q], t[q], mm[q], m, &rt[i], &rm[i]);
+          ((T*)out0[c])[i] = z2[q];
+          ((T*)out1[c])[i] = z0[q];
+        }
+      }
+    });
+  }
+  return 0;
+}
+
+template <class T>
+int dot_tail_r1(int64_t n, int m, int ncomp, const int* roles, const void* const* msg,
+                const void* const* rmk, const void* const* rz, const void* const* rrt,
+                const void* const* rrm, void* const* w, void* const* out0, void* const* out1,
+                const uint32_t* const* slots, const uint64_t* nn) {
+  for (int c = 0; c < ncomp; ++c) {
+    const int role = roles[c];
+    if (role != 0 && role != 1) continue;
+    const T* mine = (const T*)msg[c];
+    const T* other = (const T*)rmk[c];
+    const T* z2m = rz ? (const T*)rz[c] : nullptr;
+    T* wo = (T*)w[c];
+    T* o = role == 0 ? (T*)out0[c] : (T*)out1[c];
+    for_chunks<T>(n, [&](int64_t i0, int64_t len) {
+      std::vector<T> t(len), mm(len), z(len);
+      if (role == 0) {
+        prf<T>(slots[2 * c], nn[3], i0, len, t.data());
+        prf<T>(slots[2 * c], nn[4], i0, len, mm.data());
+        prf<T>(slots[2 * c], nn[5], i0, len, z.data());
+      } else {
+        prf<T>(slots[2 * c + 1], nn[6], i0, len, z.data());
+      }
+      for (int64_t q = 0; q < len; ++q) {
+        const int64_t i = i0 + q;
+        T cc = mine[i] + other[i];
+        if (z2m) cc += z2m[i];
+        const T y = role == 0 ? mxf::trunc_y<T>(cc, t[q], mm[q], m, true)
+                              : mxf::trunc_y<T>(cc, ((const T*)rrt[c])[i],
+                                                (T)((const u64*)rrm[c])[i], m, false);
+        wo[i] = y - z[q];
+        o[i] = z[q];
+      }
+    });
+  }
+  return 0;
+}
+
+template <class T>
+int dot_tail_r2(int64_t n, int ncomp, const int* roles, const void* const* a,
+                const void* const* b, void* const* out) {
+  for (int c = 0; c < ncomp; ++c) {
+    if (roles[c] != 0 && roles[c] != 1) continue;
+    const T* x = (const T*)a[c];
+    const T* y = (const T*)b[c];
+    T* o = (T*)out[c];
+    mx_cpu_parallel_for(n, 1 << 14, [&](int64_t s, int64_t e) {
+      for (int64_t i = s; i < e; ++i) o[i] = x[i] + y[i];
+    });
+  }
+  return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -210,6 +319,53 @@ int mx_share_party(int dev, int kind, int words, int64_t n, int ncomp, const int
     default:
       return -2;
   }
+}
+
+
+int mx_dot_tail_r0(int dev, int words, int64_t n, int m, int ncomp, const int* roles,
+                   const void* const* cross, void* const* msg, void* const* msg_rt,
+                   void* const* msg_rm, void* const* out0, void* const* out1,
+                   const uint32_t* const* slots, const uint64_t* nn, void* stream) {
+  if (m < 1 || m > 63) return -3;
+  if (ncomp < 1 || ncomp > 3) return -3;
+  if (dev)
+    return mxh_dot_tail_r0(words, n, m, ncomp, roles, cross, msg, msg_rt, msg_rm, out0, out1,
+                           slots, nn, stream);
+  if (words == 1)
+    return dot_tail_r0<u64>(n, m, ncomp, roles, cross, msg, msg_rt, msg_rm, out0, out1, slots,
+                            nn);
+  if (words == 2)
+    return dot_tail_r0<u128>(n, m, ncomp, roles, cross, msg, msg_rt, msg_rm, out0, out1, slots,
+                             nn);
+  return -2;
+}
+
+int mx_dot_tail_r1(int dev, int words, int64_t n, int m, int ncomp, const int* roles,
+                   const void* const* msg, const void* const* rmk, const void* const* rz,
+                   const void* const* rrt, const void* const* rrm, void* const* w,
+                   void* const* out0, void* const* out1, const uint32_t* const* slots,
+                   const uint64_t* nn, void* stream) {
+  if (m < 1 || m > 63) return -3;
+  if (ncomp < 1 || ncomp > 3) return -3;
+  if (dev)
+    return mxh_dot_tail_r1(words, n, m, ncomp, roles, msg, rmk, rz, rrt, rrm, w, out0, out1,
+                           slots, nn, stream);
+  if (words == 1)
+    return dot_tail_r1<u64>(n, m, ncomp, roles, msg, rmk, rz, rrt, rrm, w, out0, out1, slots,
+                            nn);
+  if (words == 2)
+    return dot_tail_r1<u128>(n, m, ncomp, roles, msg, rmk, rz, rrt, rrm, w, out0, out1, slots,
+                             nn);
+  return -2;
+}
+
+int mx_dot_tail_r2(int dev, int words, int64_t n, int ncomp, const int* roles,
+                   const void* const* a, const void* const* b, void* const* out, void* stream) {
+  if (ncomp < 1 || ncomp > 3) return -3;
+  if (dev) return mxh_dot_tail_r2(words, n, ncomp, roles, a, b, out, stream);
+  if (words == 1) return dot_tail_r2<u64>(n, ncomp, roles, a, b, out);
+  if (words == 2) return dot_tail_r2<u128>(n, ncomp, roles, a, b, out);
+  return -2;
 }
 
 }  // extern "C"

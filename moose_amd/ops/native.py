@@ -137,6 +137,17 @@ _SIGS = {
         [c_int, c_int, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
          c_vp, c_vp, c_vp],
     ),
+    "mx_dot_tail_r0": (
+        c_int,
+        [c_int, c_int, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+         c_vp, c_vp],
+    ),
+    "mx_dot_tail_r1": (
+        c_int,
+        [c_int, c_int, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+         c_vp, c_vp, c_vp, c_vp],
+    ),
+    "mx_dot_tail_r2": (c_int, [c_int, c_int, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mx_share_party": (
         c_int,
         [c_int, c_int, c_int, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_u64, c_u64, c_vp],

@@ -1423,3 +1423,56 @@ def share_party(kind: str, x: RT, ncomp: int, rel, slots, n1: int, na: int):
         _roles_arr(rel), nat.ptr(xd), nat.ptr(out0), nat.ptr(out1), _slots_arr(slots),
         n1 & MASK64, na & MASK64, nat.stream_of(xd)), "share_party")
     return out0, out1
+
+
+# ---------------------------------------------------------------------------
+# fixed-point dot tail, per party (csrc/rss_party.hip; moose_amd/parallel/party.py)
+# ---------------------------------------------------------------------------
+def _vp(ts):
+    """Per-component pointer array (None -> null) of dense tensors."""
+    for t in ts:
+        if t is not None and not t.is_contiguous():
+            raise ValueError("per-component buffers must be dense")
+    return (ctypes.c_void_p * len(ts))(*[None if t is None else t.data_ptr() for t in ts])
+
+
+def _dev_stream(ts):
+    t = next(t for t in ts if t is not None)
+    return nat.dev_of(t), nat.stream_of(t)
+
+
+def dot_tail_r0(cross, bits, m, roles, slots, nonces, out0, out1, n):
+    """Round 0 of the per-party dot tail (mx_dot_tail_r0): returns the per-component
+    outgoing messages (P0 m0, P1 m1, P2 z2), the dealer's rt1 and rm1 (P2 only); writes
+    P2's new shares into out0 / out1."""
+    msg = [torch.empty_like(x) for x in cross]
+    rt = [torch.empty_like(x) if r == 2 else None for x, r in zip(cross, roles)]
+    rm = [torch.empty((n,), dtype=torch.int64, device=x.device) if r == 2 else None
+          for x, r in zip(cross, roles)]
+    dev, st = _dev_stream(cross)
+    nat.check(nat.lib().mx_dot_tail_r0(
+        dev, _words(bits), n, m, len(roles), _roles_arr(roles), _vp(cross), _vp(msg), _vp(rt),
+        _vp(rm), _vp(out0), _vp(out1), _slots_arr(slots), _nonces_arr(nonces), st),
+        "dot_tail_r0")
+    return msg, rt, rm
+
+
+def dot_tail_r1(msg, rmk, rz, rrt, rrm, bits, m, roles, slots, nonces, out0, out1, n):
+    """Round 1 (mx_dot_tail_r1): returns w per component (P0, P1); writes P0's s0 and
+    P1's s1 into out0 / out1."""
+    w = [torch.empty_like(x) if r in (0, 1) else None for x, r in zip(msg, roles)]
+    dev, st = _dev_stream(msg)
+    nat.check(nat.lib().mx_dot_tail_r1(
+        dev, _words(bits), n, m, len(roles), _roles_arr(roles), _vp(msg), _vp(rmk), _vp(rz),
+        _vp(rrt), _vp(rrm), _vp(w), _vp(out0), _vp(out1), _slots_arr(slots),
+        _nonces_arr(nonces), st), "dot_tail_r1")
+    return w
+
+
+def dot_tail_r2(a, b, out, bits, roles, n):
+    """out[c] = a[c] + b[c] for the components of P0 and P1 (mx_dot_tail_r2)."""
+    if not any(t is not None for t in out):
+        return
+    dev, st = _dev_stream([t for t in out if t is not None])
+    nat.check(nat.lib().mx_dot_tail_r2(dev, _words(bits), n, len(roles), _roles_arr(roles),
+                                       _vp(a), _vp(b), _vp(out), st), "dot_tail_r2")

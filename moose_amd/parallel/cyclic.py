@@ -33,9 +33,9 @@ differ per session.
 Correlated randomness: each component has its OWN key pair (k_p, k_{p+1}) and k_all of
 its session -- the three components of a stack belong to different sessions, so the
 stacked zero-share kernels run in "pairs" mode (``mx_rss_cross_kp``).  Key setup follows
-``replicated/setup.rs:39-58``: party p draws k_p and hands a copy to party p-1 (here: a
-48-word key slot -- raw key plus expanded AES schedule -- sent device to device); party 0
-draws k_all and passes it on.
+``replicated/setup.rs:39-58``: party p draws k_p and hands a copy to party p-1 (here: its
+device key slot -- the raw 128-bit ChaCha12 key -- sent device to device); party 0 draws
+k_all and passes it on.
 
 With N = 1 the layout degenerates to one stacked session (every offset is 0 mod 1), which
 is what ``bench.py`` runs on one GPU (with the fully fused single-GPU kernels).
@@ -143,9 +143,12 @@ class CyclicSession(StackedSession):
                  pipeline_chunks=None):
         super().__init__(device, seed)
         self.comm = comm
-        if pipeline_chunks is None:  # reshares cross GPUs: overlap them with the GEMM
-            pipeline_chunks = int(os.environ.get("MOOSEX_PIPELINE_CHUNKS",
-                                                 "8" if comm.world > 1 else "1"))
+        if pipeline_chunks is None:
+            # row-chunked dot pipeline (rep.dot_trunc): off by default -- chunking re-reads
+            # the prepared B operand per chunk (GEMM 12.0 -> 15.4 ms at 8 chunks); bench.py
+            # hides the exchanges behind the NEXT step's GEMM instead (two step streams with
+            # one RCCL communicator each)
+            pipeline_chunks = int(os.environ.get("MOOSEX_PIPELINE_CHUNKS", "1"))
         self.pipeline_chunks = pipeline_chunks
         self.g = comm.rank
         self.N = comm.world
@@ -348,9 +351,59 @@ class CyclicSession(StackedSession):
         self.stats.record_send(x.host, plc.owners[j2], _nbytes(x.v))
         return PV(plc, R.RT(out0, bits)), PV(plc, R.RT(out1, bits))
 
+    def party_exchange(self, plc, specs):
+        """Route per-party messages (parallel/party.py): party a's payload on this GPU goes
+        to the GPU hosting party b of the same session; a message between two parties on
+        the same GPU (offsets equal mod N) is the payload itself, no copy."""
+        o = [self.offset(r) for r in plc.owners]
+        got, sends, recvs = {}, [], []
+        for name, a, b, t, like in specs:
+            if (o[b] - o[a]) % self.N == 0:
+                got[name] = t
+                continue
+            buf = torch.empty(like[0], dtype=like[1], device=self.device)
+            sends.append((t, self._peer(o[b] - o[a])))
+            recvs.append((buf, self._peer(o[a] - o[b])))
+            got[name] = buf
+        if sends:
+            self.comm.exchange(sends, recvs)
+        return got
+
+    def party_dot_trunc(self, plc, v, m, nonces, out=None):
+        """rep.dot_trunc's zero share + reshare + TruncPr of the local products ``v`` with
+        the reshare folded into TruncPr's first round (parallel/party.py); ``out``: optional
+        (s0, s1) [3, ...] views (dense per component) written in place."""
+        from moose_amd.parallel import party
+
+        bits = v.v.bits
+        data = v.v.data.contiguous()
+        s0, s1 = out if out is not None else (torch.empty_like(data), torch.empty_like(data))
+        party.dot_trunc_tail(self, plc, [0, 1, 2], [data[c] for c in range(3)], bits, m,
+                             nonces, [s0[c] for c in range(3)], [s1[c] for c in range(3)],
+                             self._pair_ptrs(plc))
+        return PV(plc, R.RT(s0, bits)), PV(plc, R.RT(s1, bits))
+
     # the single-GPU fused variants read other parties' data in-kernel: never used here
     p_mul_reshare = None
     p_zero_share_reshare = None
-    p_reveal = None  # the third share of a session lives on another GPU: generic move
+
+    def p_reveal(self, x, host):
+        """Reveal to a member P_j: P_{j+1}'s second share (x_{j+2}) is the one message
+        (party_exchange: a device buffer on another GPU, the share itself on this one),
+        then one add3 kernel.  None for outsiders (generic path)."""
+        plc = x.plc
+        if host not in plc.owners:
+            return None
+        v0, v1 = x.s0.v, x.s1.v
+        if not (isinstance(v0, R.RT) and isinstance(v1, R.RT)) or v0.bits not in (64, 128):
+            return None
+        j = plc.owners.index(host)
+        j1 = (j + 1) % 3
+        d1 = v1.data
+        src = d1[j1] if d1[j1].is_contiguous() else d1[j1].contiguous()
+        got = self.party_exchange(plc, [("reveal", j1, j, src, (tuple(src.shape), src.dtype))])
+        self.stats.record_send(plc.owners[j1], host, _nbytes(v1) // 3)
+        return HV(host, R.add3(R.RT(v0.data[j], v0.bits), R.RT(d1[j], v1.bits),
+                               R.RT(got["reveal"], v1.bits)))
     p_ks_level = None
     p_dot_zs_reshare = None

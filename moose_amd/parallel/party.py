@@ -1,0 +1,86 @@
+"""Per-party protocol steps shared by the layouts whose parties sit on different GPUs.
+
+:class:`~moose_amd.parallel.cyclic.CyclicSession` (every GPU stacks one party of each of
+three sessions) and :class:`~moose_amd.parallel.spmd.SPMDSession` (one party per process)
+run the same per-party kernels (``csrc/rss_party.hip``); they differ only in which parties a
+process hosts and how a message from party a to party b is routed.  A session provides
+
+    party_exchange(plc, specs) -> {name: received tensor}
+
+where ``specs`` is an ordered list of ``(name, a, b, tensor, like)``: message ``name`` goes
+from party a to party b (``tensor`` = the payload on a process hosting a, ``like`` = a
+tensor of the payload's shape and dtype for the receiver).  Every process walks the same
+list in the same order, so the n-th message between two processes in one direction always
+pairs with the n-th receive -- the role of the reference's rendezvous keys
+(``moose/src/compilation/networking.rs``); no shape header travels.
+
+Fixed-point dot tail (``rep.dot_trunc``): reference ``replicated/arith.rs:436-492`` (dot:
+cross terms, zero share, reshare) followed by ``replicated/fixedpoint.rs:80-103`` ->
+``additive/trunc.rs:114-170`` (TruncPr with dealer P2).  Here the reshare is folded into
+TruncPr's first round (``rss_party.hip``): 2 rounds and 8 messages instead of 3 rounds and
+9, with bitwise the same output shares.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from moose_amd.ops import ring as R
+
+
+def alias_exchange(specs):
+    """party_exchange of a process hosting every party (stacked sessions): every
+    message is the sender's buffer itself."""
+    return {name: t for name, _a, _b, t, _like in specs}
+
+# round A: (name, from party, to party); round B likewise
+TAIL_A = (("m0", 0, 1), ("m1", 1, 0), ("z2_0", 2, 0), ("z2_1", 2, 1), ("rt1", 2, 1),
+          ("rm1", 2, 1))
+TAIL_B = (("w0", 0, 1), ("w1", 1, 0))
+
+
+def dot_trunc_tail(sess, plc, roles, cross, bits, m, nonces, out0, out1, slots):
+    """Zero share + reshare + TruncPr of the local cross products ``cross`` (one dense
+    ring-``bits`` tensor per hosted component; component c plays party ``roles[c]``).
+    Writes the new shares into ``out0`` / ``out1`` (dense per-component tensors, e.g. rows
+    of a stack).  ``nonces`` = (zero share, r0, r1, t, m, z0, z2); ``slots`` = the key-slot
+    pointers (own k_p, next k_{p+1}) of every component."""
+    comp = {r: c for c, r in enumerate(roles)}
+    n_el = math.prod(cross[0].shape) // (2 if bits == 128 else 1)
+    msg, rt, rm = R.dot_tail_r0(cross, bits, m, roles, slots, nonces, out0, out1, n_el)
+
+    def mine(party, arrs):
+        c = comp.get(party)
+        return None if c is None else arrs[c]
+
+    like_rm = ((n_el,), torch.int64)
+    like = (tuple(cross[0].shape), cross[0].dtype)
+    payload = {"m0": mine(0, msg), "m1": mine(1, msg), "z2_0": mine(2, msg),
+               "z2_1": mine(2, msg), "rt1": mine(2, rt), "rm1": mine(2, rm)}
+    got = sess.party_exchange(plc, [(nm, a, b, payload[nm], like_rm if nm == "rm1" else like)
+                                    for nm, a, b in TAIL_A])
+    rmk = [got.get("m1") if r == 0 else got.get("m0") if r == 1 else None for r in roles]
+    rz = [got.get("z2_0") if r == 0 else got.get("z2_1") if r == 1 else None for r in roles]
+    rrt = [got.get("rt1") if r == 1 else None for r in roles]
+    rrm = [got.get("rm1") if r == 1 else None for r in roles]
+    w = R.dot_tail_r1(msg, rmk, rz, rrt, rrm, bits, m, roles, slots, nonces, out0, out1, n_el)
+    got = sess.party_exchange(plc, [("w0", 0, 1, mine(0, w), like), ("w1", 1, 0, mine(1, w), like)])
+    other = [got.get("w1") if r == 0 else got.get("w0") if r == 1 else None for r in roles]
+    dst = [out1[c] if r == 0 else out0[c] if r == 1 else None for c, r in enumerate(roles)]
+    R.dot_tail_r2(w, other, dst, bits, roles, n_el)
+    nb = cross[0].numel() * cross[0].element_size()
+    record_tail_traffic(sess.stats, plc, nb)
+
+
+def record_tail_traffic(stats, plc, nb):
+    """Messages of the folded dot tail (``nb`` bytes per share tensor): round A carries
+    m0, m1, z2 (twice), rt1 and rm1 (a u64, half of a Z_2^128 element); round B w0, w1."""
+    o = plc.owners
+    for a, b, k in ((0, 1, 1), (1, 0, 1), (2, 0, 1), (2, 1, 2)):
+        stats.record_send(o[a], o[b], nb, count=k)
+    stats.record_send(o[2], o[1], nb // 2)
+    stats.record_round(5 * nb + nb // 2)
+    for a, b in ((0, 1), (1, 0)):
+        stats.record_send(o[a], o[b], nb)
+    stats.record_round(2 * nb)

@@ -387,10 +387,6 @@ def _rows(pv: PV, r0: int, r1: int) -> PV:
     return PV(pv.plc, R.RT(v.data[:, r0:r1], v.bits))
 
 
-def _cat_rows(pvs) -> PV:
-    return PV(pvs[0].plc, R.RT(torch.cat([p.v.data for p in pvs], dim=1), pvs[0].v.bits))
-
-
 def dot_trunc(sess, x: RepTensor, y: RepTensor, m: int) -> RepTensor:
     """trunc_pr(dot(x, y), m) -- the fixed-point matrix product.
 
@@ -409,6 +405,9 @@ def dot_trunc(sess, x: RepTensor, y: RepTensor, m: int) -> RepTensor:
         if len(xs) == 3 and len(ys) == 3:
             M = xs[1]
             nchunk = min(chunks, M // 128)
+    party = getattr(sess, "party_dot_trunc", None)
+    use_party = (party is not None and m and 0 < m <= 63 and x.kind == "arith"
+                 and x.bits in (64, 128) and os.environ.get("MOOSEX_DOT_TAIL", "1") != "0")
     if nchunk <= 1:
         tail = getattr(sess, "p_zs_trunc", None)
         if (tail is not None and m and x.kind == "arith" and getattr(sess, "fused", False)
@@ -418,6 +417,12 @@ def dot_trunc(sess, x: RepTensor, y: RepTensor, m: int) -> RepTensor:
                 v = sess.p_dot_cross(x.plc, x.s0, x.s1, y.s0, y.s1)
                 s0, s1 = tail(x.plc, v, m)  # zero share + reshare + TruncPr: one kernel
                 return RepTensor(x.plc, x.bits, "arith", s0, s1)
+        if use_party:  # the per-party tail: reshare folded into TruncPr (2 rounds)
+            with span("rep.dot_trunc_party"):
+                v = sess.p_dot_cross(x.plc, x.s0, x.s1, y.s0, y.s1)
+                nonces = tuple(sess.nonce(x.plc) for _ in range(7))  # as dot + trunc_pr
+                s0, s1 = party(x.plc, v, m, nonces)
+                return RepTensor(x.plc, x.bits, "arith", s0, s1)
         return trunc_pr(sess, dot(sess, x, y), m)
     with span("rep.dot_trunc_pipelined"):
         plc, bits, kind = x.plc, x.bits, x.kind
@@ -426,29 +431,38 @@ def dot_trunc(sess, x: RepTensor, y: RepTensor, m: int) -> RepTensor:
         cuda = data.is_cuda
         main = torch.cuda.current_stream(data.device) if cuda else None
         side = sess.side_stream() if cuda else None
-        parts = []
         prepared = sess.p_prepare_cross(plc, y.s0, y.s1)
+        # every chunk's shares land in rows of the result (no concatenation afterwards)
+        N = y.s0.v.shape[2]
+        shp = (3, M, N) + ((2,) if bits == 128 else ())
+        out0 = torch.empty(shp, dtype=data.dtype, device=data.device)
+        out1 = torch.empty_like(out0)
+
+        def tail(v, r0, r1):
+            if use_party:
+                nonces = tuple(sess.nonce(plc) for _ in range(7))
+                party(plc, v, m, nonces, out=(out0[:, r0:r1], out1[:, r0:r1]))
+                return
+            z = sess.p_add_zero_share(plc, v, kind)
+            t = trunc_pr(sess, _reshare(sess, plc, z, bits, kind), m)
+            out0[:, r0:r1].copy_(t.s0.v.data)
+            out1[:, r0:r1].copy_(t.s1.v.data)
+
         for c in range(nchunk):
             r0, r1 = bounds[c], bounds[c + 1]
             v = sess.p_dot_cross_rows(plc, x.s0, x.s1, r0, r1, prepared)
             if not cuda:
-                z = sess.p_add_zero_share(plc, v, kind)
-                parts.append(trunc_pr(sess, _reshare(sess, plc, z, bits, kind), m))
+                tail(v, r0, r1)
                 continue
             ev = torch.cuda.Event()
             ev.record(main)
             with torch.cuda.stream(side):
                 side.wait_event(ev)
                 v.v.data.record_stream(side)
-                z = sess.p_add_zero_share(plc, v, kind)
-                t = trunc_pr(sess, _reshare(sess, plc, z, bits, kind), m)
-            for pv in (t.s0, t.s1):
-                pv.v.data.record_stream(main)
-            parts.append(t)
+                tail(v, r0, r1)
         if cuda:
             main.wait_stream(side)
-        return RepTensor(plc, bits, kind, _cat_rows([t.s0 for t in parts]),
-                         _cat_rows([t.s1 for t in parts]))
+        return RepTensor(plc, bits, kind, PV(plc, R.RT(out0, bits)), PV(plc, R.RT(out1, bits)))
 
 
 # ---------------------------------------------------------------------------

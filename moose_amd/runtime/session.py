@@ -442,10 +442,29 @@ class StackedSession(Session):
         r = R.zs_trunc3_k(z.v, self.key_ptr(plc, 0), nmul, m, nonces)
         if r is None:  # nonces are drawn: never fall back silently
             raise RuntimeError("zs_trunc3 declined on a device session")
-        nbytes = _nbytes(r[0])
-        self.stats.record_round(nbytes)
-        self._trunc_traffic(z, nbytes // 3)
+        from moose_amd.parallel.party import record_tail_traffic
+
+        # the messages of the per-party protocol (reshare folded into TruncPr, 2 rounds)
+        record_tail_traffic(self.stats, plc, _nbytes(r[0]) // 3)
         return PV(plc, r[0]), PV(plc, r[1])
+
+    def party_exchange(self, plc, specs):
+        """Every party is local: a per-party message is the sender's buffer."""
+        return {name: t for name, _a, _b, t, _like in specs}
+
+    def party_dot_trunc(self, plc, v, m, nonces, out=None):
+        """rep.dot_trunc's tail with the per-party kernels (reshare folded into TruncPr's
+        first round, parallel/party.py): the host path; a device session runs the whole tail
+        as one kernel (p_zs_trunc), which gives the same shares."""
+        from moose_amd.parallel import party
+
+        bits = v.v.bits
+        data = v.v.data.contiguous()
+        s0, s1 = out if out is not None else (torch.empty_like(data), torch.empty_like(data))
+        slots = [self.key_ptr(plc, q) for p in range(3) for q in (p, (p + 1) % 3)]
+        party.dot_trunc_tail(self, plc, [0, 1, 2], [data[c] for c in range(3)], bits, m,
+                             nonces, [s0[c] for c in range(3)], [s1[c] for c in range(3)], slots)
+        return PV(plc, R.RT(s0, bits)), PV(plc, R.RT(s1, bits))
 
     def p_ks_level(self, plc, g0, g1, p0, p1, d, both):
         """One Kogge-Stone level of rep.binary_adder (AND(s) + reshare + xor) in one
