@@ -560,7 +560,7 @@ __global__ void __launch_bounds__(256)
 // read right after the step's barrier into the second register set (the k-loop is unrolled
 // by two so the sets swap without moves), while the second half of stage kb's MFMAs runs.
 // Output bytes: 16x16 block (bi, bj) at ((bi * BN / 16 + bj) * 64 + lane) * 4 of the tile.
-template <int WR, int WC, int BN, int MINW>
+template <int WR, int WC, int BN, int MINW, int STG = kStages, bool IL = false>
 __global__ void __launch_bounds__(64 * WR * WC, MINW)
     k_crt_gemm16(const int8_t* __restrict__ RA, const int8_t* __restrict__ RB,
                  int8_t* __restrict__ CR, int tiles_m, int tiles_n, int nkb, int gM,
@@ -618,8 +618,11 @@ __global__ void __launch_bounds__(64 * WR * WC, MINW)
     dsts[t] = (is_b ? kImg : 0) + pp * 1024;
     steps[t] = is_b ? kImgB : kImg;
   }
-  (void)dma_mask;
+  bool dma_on[PPW];
+#pragma unroll
+  for (int t = 0; t < PPW; ++t) dma_on[t] = (dma_mask >> ((wave + NW * t) >= 16 ? 1 : 0)) & 1;
   auto dma = [&](int kb, int t, int8_t* dst_stage) {
+    if (!dma_on[t]) return;  // MOOSEX_CRT_DMA_MASK timing experiments only
     const int8_t* src = kb >= khalf ? srcs2[t] : srcs[t];
     __builtin_amdgcn_global_load_lds((const void*)(src + (int64_t)kb * steps[t]),
                                      (__attribute__((address_space(3))) void*)(dst_stage + dsts[t]),
@@ -633,7 +636,9 @@ __global__ void __launch_bounds__(64 * WR * WC, MINW)
     for (int j = 0; j < NJ; ++j) acc[i][j] = v4i{0, 0, 0, 0};
 
   v4i fa0[MI], fb0[NJ], fa1[MI], fb1[NJ];
+  const bool no_frags = (dma_mask & 8) != 0;  // timing experiments only
   auto frags = [&](const int8_t* st, v4i(&fa)[MI], v4i(&fb)[NJ]) {
+    if (no_frags) return;
 #pragma unroll
     for (int i = 0; i < MI; ++i) fa[i] = *(const v4i*)(st + rowa + i * 16 * BK);
 #pragma unroll
@@ -641,10 +646,10 @@ __global__ void __launch_bounds__(64 * WR * WC, MINW)
   };
 
 #pragma unroll
-  for (int s = 0; s < kStages; ++s)
+  for (int s = 0; s < STG; ++s)
 #pragma unroll
     for (int t = 0; t < PPW; ++t) dma(s < nkb ? s : nkb - 1, t, smem + s * kStageBytes);
-  __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(2 * PPW));
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0((STG - 1) * PPW));
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   frags(smem, fa0, fb0);
@@ -654,11 +659,11 @@ __global__ void __launch_bounds__(64 * WR * WC, MINW)
   // (na, nb); the DMA of stage kb+3 into the freed buffer runs beside the second half
   auto step = [&](int kb, int8_t* cur, int8_t* nxt, v4i(&fa)[MI], v4i(&fb)[NJ], v4i(&na)[MI],
                   v4i(&nbf)[NJ]) __attribute__((always_inline)) {
-    const int kn = kb + kStages < nkb ? kb + kStages : nkb - 1;
+    const int kn = kb + STG < nkb ? kb + STG : nkb - 1;
 #pragma unroll MI
     for (int i = 0; i < MI; ++i) {
       if (i == MI / 2) {
-        __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(PPW));
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0((STG - 2) * PPW));
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
         frags(nxt, na, nbf);
@@ -679,14 +684,58 @@ __global__ void __launch_bounds__(64 * WR * WC, MINW)
     }
   };
 
+  // IL: one barrier at the START of each k-step (stage kb+1 landed everywhere, stage kb's
+  // buffer no longer read), then the step's MFMAs with the next stage's fragment reads
+  // spread one per GAP MFMAs and the DMAs of stage kb+STG in the last gaps -- instead of
+  // every wave bursting its 12 fragment reads into the LDS right after a mid-step barrier
+  auto rd_frag = [&](const int8_t* st, int q, v4i(&fa)[MI], v4i(&fb)[NJ])
+                     __attribute__((always_inline)) {
+    if (no_frags) return;
+    if (q < MI)
+      fa[q] = *(const v4i*)(st + rowa + q * 16 * BK);
+    else
+      fb[q - MI] = *(const v4i*)(st + rowb + (q - MI) * 16 * BK);
+  };
+  auto step_il = [&](int kb, int8_t* cur, int8_t* nxt, v4i(&fa)[MI], v4i(&fb)[NJ],
+                     v4i(&na)[MI], v4i(&nbf)[NJ]) __attribute__((always_inline)) {
+    const int kn = kb + STG < nkb ? kb + STG : nkb - 1;
+    constexpr int NR = MI + NJ;
+    constexpr int GAP = (NM - 2 * PPW) / NR > 0 ? (NM - 2 * PPW) / NR : 1;
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0((STG - 2) * PPW));
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int h = 0; h < NM; ++h) {
+      const int i = h / NJ, j = h % NJ;
+      acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (h % GAP == GAP - 1 && h / GAP < NR) {
+        rd_frag(nxt, h / GAP, na, nbf);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll PPW
+      for (int t = 0; t < PPW; ++t)
+        if (h == NM - 2 * PPW + 2 * t + 1) {
+          dma(kn, t, cur);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+  };
+
   auto buf = [&](int i) { return smem + i * kStageBytes; };
   int r = 0;  // stage kb lives in buf(r)
   for (int kb = 0; kb < nkb; kb += 2) {
-    step(kb, buf(r), buf(r == 2 ? 0 : r + 1), fa0, fb0, fa1, fb1);
-    r = r == 2 ? 0 : r + 1;
+    if constexpr (IL)
+      step_il(kb, buf(r), buf(r == STG - 1 ? 0 : r + 1), fa0, fb0, fa1, fb1);
+    else
+      step(kb, buf(r), buf(r == STG - 1 ? 0 : r + 1), fa0, fb0, fa1, fb1);
+    r = r == STG - 1 ? 0 : r + 1;
     if (kb + 1 < nkb) {
-      step(kb + 1, buf(r), buf(r == 2 ? 0 : r + 1), fa1, fb1, fa0, fb0);
-      r = r == 2 ? 0 : r + 1;
+      if constexpr (IL)
+        step_il(kb + 1, buf(r), buf(r == STG - 1 ? 0 : r + 1), fa1, fb1, fa0, fb0);
+      else
+        step(kb + 1, buf(r), buf(r == STG - 1 ? 0 : r + 1), fa1, fb1, fa0, fb0);
+      r = r == STG - 1 ? 0 : r + 1;
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -864,9 +913,12 @@ int crt_kernel() {  // MOOSEX_CRT_KERNEL: 1 = 4 waves of 128x128, 2 = 8 waves of
   // higher clock on the 16x16 shape), 6 = 16x16x64, 8 waves of 128x64 in 256x256 tiles, two
   // blocks per CU (the default: 11.95 vs 12.12 ms for 5 on the 4096^2 Z_2^128 RSS product,
   // profiles/r2_crt_variant_ab.md)
+  // 7 = 6 with a 4-stage ring (no gain), 8 = 6 with one barrier at the start of each k-step
+  // and the next stage's fragment reads spread over the step's MFMAs (the default: ~6 %
+  // faster than 6 on the same box, profiles/r3_crt_gemm.md), 9 = 8 with 4 stages
   const char* e = std::getenv("MOOSEX_CRT_KERNEL");
-  const int v = e ? std::atoi(e) : 6;
-  return v >= 1 && v <= 6 ? v : 6;
+  const int v = e ? std::atoi(e) : 8;
+  return v >= 1 && v <= 9 ? v : 8;
 }
 bool crt_mfma16() { return crt_kernel() >= 4; }
 int recon_dot4() {  // MOOSEX_CRT_RECON=0: the multiply-add reconstruction
@@ -932,16 +984,16 @@ int dma_mask() {
   return e ? std::atoi(e) : 3;
 }
 
-template <int WR, int WC, int BN, int MINW, bool M16>
+template <int WR, int WC, int BN, int MINW, bool M16, int STG = kStages, bool IL = false>
 void launch_variant(const CPlan& p, const Tables& tb, int64_t batch, const int8_t* ra,
                     const int8_t* rb, int8_t* cr, int bcast, int roll, hipStream_t st) {
-  constexpr int lds = kStages * (kImg + BN * BK);
-  const void* fn = M16 ? (const void*)k_crt_gemm16<WR, WC, BN, MINW>
+  constexpr int lds = STG * (kImg + BN * BK);
+  const void* fn = M16 ? (const void*)k_crt_gemm16<WR, WC, BN, MINW, STG, IL>
                        : (const void*)k_crt_gemm<WR, WC, BN, MINW>;
   ensure_lds_attr(fn, lds, st);
   const dim3 grid((unsigned)(p.tiles_m * p.tiles_n), (unsigned)(batch * p.n));
   if constexpr (M16)
-    hipLaunchKernelGGL((k_crt_gemm16<WR, WC, BN, MINW>), grid, dim3(64 * WR * WC), lds, st, ra,
+    hipLaunchKernelGGL((k_crt_gemm16<WR, WC, BN, MINW, STG, IL>), grid, dim3(64 * WR * WC), lds, st, ra,
                        rb, cr, (int)p.tiles_m, (int)p.tiles_n, (int)p.nkb, gemm_group_m(), tb.ep,
                        dma_mask(), bcast, (int)p.a_nkb, roll);
   else
@@ -958,6 +1010,9 @@ void launch_crt_gemm(const CPlan& p, const Tables& tb, int64_t batch, const int8
     case 4: launch_variant<2, 2, 256, 1, true>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
     case 3: launch_variant<2, 2, 128, 2, false>(p, tb, batch, ra, rb, cr, bcast, 0, st); break;
     case 6: launch_variant<2, 4, 256, 2, true>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
+    case 7: launch_variant<2, 4, 256, 2, true, 4>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
+    case 8: launch_variant<2, 4, 256, 2, true, 3, true>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
+    case 9: launch_variant<2, 4, 256, 2, true, 4, true>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
     default: launch_variant<2, 2, 128, 2, true>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
   }
 }

@@ -18,8 +18,24 @@ def load(paths):
     return per, dispatches
 
 
+def durations(paths):
+    """Mean dispatch duration (ns) per kernel from the kernel_trace.csv next to each
+    counter CSV (same rocprofv3 run)."""
+    import os
+
+    d = collections.defaultdict(list)
+    for p in paths:
+        kt = os.path.join(os.path.dirname(p), "run_kernel_trace.csv")
+        if not os.path.exists(kt):
+            continue
+        for r in csv.DictReader(open(kt)):
+            d[r["Kernel_Name"][:80]].append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
+    return {k: sum(v) / len(v) for k, v in d.items() if v}
+
+
 def main(paths):
     per, disp = load(paths)
+    dur = durations(paths[:1])
     print("| kernel | counter | value |")
     print("|---|---|---|")
     for k, c in per.items():
@@ -37,6 +53,15 @@ def main(paths):
             simds = 256 * 4
             util = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (c["GRBM_GUI_ACTIVE"] / 8 * simds)
             print(f"| `{k}` | MFMA busy / (GUI_ACTIVE/8 x 1024 SIMDs) | {util:.3f} |")
+        nd = len({d for p_, d in disp[k] if p_ == paths[0]}) or 1
+        if c.get("GRBM_GUI_ACTIVE") and k in dur:
+            clk = c["GRBM_GUI_ACTIVE"] / nd / 8 / (dur[k] * 1e-9)
+            print(f"| `{k}` | mean dispatch ms (profiled) | {dur[k] / 1e6:.3f} |")
+            print(f"| `{k}` | effective clock GHz (GUI_ACTIVE/8/duration) | {clk / 1e9:.3f} |")
+            if c.get("SQ_INSTS_MFMA"):
+                # 16x16x64 i8 MFMA: 16 cycles on one SIMD
+                busy = c["SQ_INSTS_MFMA"] / nd * 16 / (1024 * clk * dur[k] * 1e-9)
+                print(f"| `{k}` | MFMA pipe occupancy (INSTS_MFMA x 16 cyc / SIMD-cycles) | {busy:.3f} |")
         if c.get("SQ_LDS_IDX_ACTIVE"):
             print(f"| `{k}` | LDS bank conflict / LDS active | "
                   f"{c.get('SQ_LDS_BANK_CONFLICT', 0) / c['SQ_LDS_IDX_ACTIVE']:.3f} |")

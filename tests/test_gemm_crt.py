@@ -315,3 +315,24 @@ def test_gpu_dot_cross_pair_rolled(bits, K):
         return
     same(want, got)
     assert torch.equal(torch.cat([r.data for r in rows], dim=1).cpu(), want.data.cpu())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["6", "8"])
+def test_gpu_crt_bench_tiling_matches_limb_gemm(variant, monkeypatch):
+    """The bench's tile grid: many 256x256 tiles in both directions (GROUPM remap over 8 x 8
+    tiles per party and modulus), K' = 8192 (mode 1), Z_2^128 -- bit-exact against the limb
+    GEMM, for the plain cross GEMM and the rolled-pair form the stacked session runs."""
+    monkeypatch.setenv("MOOSEX_CRT_KERNEL", variant)
+    bits, M, K, N = 128, 2048, 4096, 2048
+    x0 = gpu(rand_rt((3, M, K), bits, 90))
+    ys = [gpu(rand_rt((3, K, N), bits, 91 + i)) for i in range(2)]
+    x1 = R.RT(torch.roll(x0.data, -1, dims=0), bits)  # s1[p] = s0[p + 1]
+    with _crt(2):
+        want = R.dot_cross(x0, x1, *ys, nb=1)
+    with _crt(1):
+        got = R.dot_cross(x0, x1, *ys, nb=1)
+        rolled = R.dot_cross_pair(x0, ys[0], ys[1], 1)
+    same(want, got)
+    assert rolled is not None
+    same(want, rolled)
