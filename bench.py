@@ -317,7 +317,7 @@ def _lr_spmd(runs, world, rank, device, prog):
         g = groups[mine]
         tm = logistic_regression_tutorial(128)
         comp = to_native(tm.computation, 128)
-        tr = Transport(rank, world, device)
+        tr = Transport(rank, world, device, plans=True)  # every rank holds every argument
         roles = {r: 3 * mine + i for i, r in enumerate(ROLES)}
         bdev = [device.index] if device.type == "cuda" and dist.get_backend() == "nccl" else None
         lat = []

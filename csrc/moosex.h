@@ -226,6 +226,10 @@ int mx_ks_level3_k(int dev, int words, const void* g0, const void* g1, const voi
 int mx_ks_cross1(int dev, int words, const void* g0, const void* g1, const void* p0,
                  const void* p1, void* z, int64_t n, int d, int both, const uint8_t* keys16,
                  uint64_t nonce, void* stream);
+// mx_ks_cross1 with the two keys read from key slots (slots[0] = k_p, slots[1] = k_{p+1})
+int mx_ks_cross1_s(int dev, int words, const void* g0, const void* g1, const void* p0,
+                   const void* p1, void* z, int64_t n, int d, int both,
+                   const uint32_t* const* slots, uint64_t nonce, void* stream);
 // mx_prf_expand with nkeys consecutive key slots
 int mx_prf_expand_k(int dev, int words, void* out, int64_t n, int nkeys, const uint32_t* slots,
                     uint64_t nonce, void* stream);

@@ -222,6 +222,9 @@ int mxh_ew_binary_slot2(int op, int words, const void* a0, const void* a1, const
 int mxh_ks_cross1(int words, const void* g0, const void* g1, const void* p0, const void* p1,
                   void* z, int64_t n, int d, int both, const uint8_t* keys16, uint64_t nonce,
                   void* stream);
+int mxh_ks_cross1_s(int words, const void* g0, const void* g1, const void* p0, const void* p1,
+                    void* z, int64_t n, int d, int both, const uint32_t* const* slots,
+                    uint64_t nonce, void* stream);
 int mxh_ks_level3_k(int words, const void* g0, const void* g1, const void* p0, const void* p1,
                     void* og0, void* og1, void* op0, void* op1, int64_t n, int d, int both,
                     const uint32_t* slots, uint64_t nonce, void* stream);

@@ -815,6 +815,16 @@ int mx_ks_cross1(int dev, int words, const void* g0, const void* g1, const void*
   });
 }
 
+int mx_ks_cross1_s(int dev, int words, const void* g0, const void* g1, const void* p0,
+                   const void* p1, void* z, int64_t n, int d, int both,
+                   const uint32_t* const* slots, uint64_t nonce, void* stream) {
+  if (dev) return mxh_ks_cross1_s(words, g0, g1, p0, p1, z, n, d, both, slots, nonce, stream);
+  uint8_t keys16[32];  // host slots: the raw key is the slot's first 16 bytes
+  memcpy(keys16, slots[0], 16);
+  memcpy(keys16 + 16, slots[1], 16);
+  return mx_ks_cross1(0, words, g0, g1, p0, p1, z, n, d, both, keys16, nonce, stream);
+}
+
 int mx_ks_level3_k(int dev, int words, const void* g0, const void* g1, const void* p0,
                    const void* p1, void* og0, void* og1, void* op0, void* op1, int64_t n,
                    int d, int both, const uint32_t* slots, uint64_t nonce, void* stream) {

@@ -1309,6 +1309,26 @@ int mxh_ks_cross1(int words, const void* g0, const void* g1, const void* p0, con
   return 0;
 }
 
+int mxh_ks_cross1_s(int words, const void* g0, const void* g1, const void* p0, const void* p1,
+                    void* z, int64_t n, int d, int both, const uint32_t* const* slots,
+                    uint64_t nonce, void* stream) {
+  if (n == 0) return 0;
+  KeySrc k = mxd::keysrc_slots(slots, 2);
+  if (words == 1) {
+    hipLaunchKernelGGL(k_ks_cross1<u64>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
+                       (const u64*)g0, (const u64*)g1, (const u64*)p0, (const u64*)p1, (u64*)z,
+                       n, d, both, k, nonce);
+  } else if (words == 2) {
+    hipLaunchKernelGGL(k_ks_cross1<u128>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
+                       (const u128*)g0, (const u128*)g1, (const u128*)p0, (const u128*)p1,
+                       (u128*)z, n, d, both, k, nonce);
+  } else {
+    return -2;
+  }
+  MX_LAUNCH_CHECK();
+  return 0;
+}
+
 inline int ks_grid(int64_t items, int per_block = 256 / 6) {
   int64_t b = (items + per_block - 1) / per_block;
   return (int)std::max<int64_t>(1, std::min<int64_t>(b, 8192));

@@ -1250,6 +1250,25 @@ def ks_cross1(g0: RT, g1: RT, p0: RT, p1: RT, d: int, both: bool, keys, nonce: i
     return z
 
 
+def ks_cross1_s(g0: RT, g1: RT, p0: RT, p1: RT, d: int, both: bool, slot_ptrs,
+                nonce: int) -> RT:
+    """ks_cross1 with the keys (k_p, k_{p+1}) read from two device key slots."""
+    bits = g0.bits
+    shp = g0.shape
+    datas = [x.data.contiguous() for x in (g0, g1, p0, p1)]
+    n = math.prod(shp)
+    z = empty(((2,) + tuple(shp)) if both else tuple(shp), bits, g0.device)
+    nat.check(
+        nat.lib().mx_ks_cross1_s(
+            nat.dev_of(z.data), _words(bits), *[nat.ptr(x) for x in datas], nat.ptr(z.data),
+            n, int(d), 1 if both else 0, _slots_arr(slot_ptrs), nonce & MASK64,
+            nat.stream_of(z.data),
+        ),
+        "ks_cross1_s",
+    )
+    return z
+
+
 def ks_level3_k(g0: RT, g1: RT, p0: RT, p1: RT, d: int, both: bool, slot_ptr: int,
                 nonce: int):
     """One fused Kogge-Stone level for three stacked parties (mx_ks_level3_k): returns

@@ -361,7 +361,8 @@ class CyclicSession(StackedSession):
             if (o[b] - o[a]) % self.N == 0:
                 got[name] = t
                 continue
-            buf = torch.empty(like[0], dtype=like[1], device=self.device)
+            buf = like if isinstance(like, torch.Tensor) else torch.empty(
+                like[0], dtype=like[1], device=self.device)
             sends.append((t, self._peer(o[b] - o[a])))
             recvs.append((buf, self._peer(o[a] - o[b])))
             got[name] = buf

@@ -8,8 +8,9 @@ process hosts and how a message from party a to party b is routed.  A session pr
     party_exchange(plc, specs) -> {name: received tensor}
 
 where ``specs`` is an ordered list of ``(name, a, b, tensor, like)``: message ``name`` goes
-from party a to party b (``tensor`` = the payload on a process hosting a, ``like`` = a
-tensor of the payload's shape and dtype for the receiver).  Every process walks the same
+from party a to party b (``tensor`` = the payload on a process hosting a; ``like`` = the
+payload's (shape, dtype) for the receiver to allocate, or the receiver's destination
+tensor itself).  Every process walks the same
 list in the same order, so the n-th message between two processes in one direction always
 pairs with the n-th receive -- the role of the reference's rendezvous keys
 (``moose/src/compilation/networking.rs``); no shape header travels.

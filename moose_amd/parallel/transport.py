@@ -43,14 +43,37 @@ class TransportError(errors.Networking):
     pass
 
 
+# Message plans (header replay).  Every party process runs the same program, so for a given
+# computation and argument shapes the sequence of typed messages between two processes --
+# kinds, dtypes, ring widths, shapes -- is the same in every evaluation.  The first
+# evaluation under a plan key sends headers and records them on both sides; later ones
+# send payloads only and take the headers from the plan, so no message makes the receiver
+# read a header back to the host (the reference ships HostShape metadata with every Share,
+# replicated/convert.rs:49-160).  A sender whose header differs from the plan raises
+# instead of desynchronising its peer.
+_PLANS = {}
+
+
+class _Plan:
+    __slots__ = ("inb", "outb")
+
+    def __init__(self):
+        self.inb = {}   # src rank -> [header, ...] received in order
+        self.outb = {}  # dst rank -> [header, ...] sent in order
+
+
 class Transport:
     """Typed send/recv between the ranks of a process group.
 
     ``device`` is where payload tensors travel (a CUDA device for RCCL, CPU for gloo).
     """
 
-    def __init__(self, rank: int, world: int, device, group=None, fault=None):
+    def __init__(self, rank: int, world: int, device, group=None, fault=None,
+                 plans: bool = False):
         self.rank = rank
+        # message plans (module doc of _PLANS): only for runtimes that hand every process
+        # every argument, so that all processes derive the same plan key
+        self.plans = plans
         self.world = world
         self.device = torch.device(device)
         self.group = group
@@ -61,6 +84,9 @@ class Transport:
         self.fault = fault if fault is not None else _parse_fault(os.environ.get("MOOSEX_FAULT"),
                                                                    rank)
         self._sends = 0
+        self._mode = None  # message plan: None, "record" or "replay"
+        self._plan = None
+        self.header_recvs = 0  # headers read back from the device (record / no plan)
         # gloo with device tensors (CPU tests, one-GPU rehearsals of multi-rank layouts):
         # stage payloads through host memory explicitly, as parallel/cyclic.RingComm does
         try:
@@ -170,15 +196,57 @@ class Transport:
         dist.recv(t, src, group=self.group)
         return t.to(self.device) if self.stage else t
 
+    # -- message plans ----------------------------------------------------------------
+    def begin_plan(self, key):
+        """Start an evaluation under plan ``key`` (identical on every process): replay the
+        recorded headers if the plan exists, else record them."""
+        p = _PLANS.get((self.rank, self.world, key))
+        self._plan_key = key
+        self._cursor_in, self._cursor_out = {}, {}
+        if p is not None:
+            self._mode, self._plan = "replay", p
+        else:
+            self._mode, self._plan = "record", _Plan()
+
+    def end_plan(self, ok: bool = True):
+        if self._mode == "record" and ok:
+            _PLANS[(self.rank, self.world, self._plan_key)] = self._plan
+        self._mode = self._plan = None
+
+    def _next(self, cursors, peer):
+        k = cursors.get(peer, 0)
+        cursors[peer] = k + 1
+        return k
+
     # -- typed values -----------------------------------------------------------------
     def send(self, v, dst: int):
         h, payload = self._header(v)
-        self._send_tensor(torch.tensor(h, dtype=torch.int64), dst)
+        if self._mode == "replay":
+            rec = self._plan.outb.get(dst, [])
+            k = self._next(self._cursor_out, dst)
+            if k >= len(rec) or rec[k] != h:
+                raise TransportError(
+                    f"message {k} to rank {dst} does not match the evaluation's message plan "
+                    "(data-dependent shapes?)")
+        else:
+            self._send_tensor(torch.tensor(h, dtype=torch.int64), dst)
+            if self._mode == "record":
+                self._plan.outb.setdefault(dst, []).append(h)
         if payload is not None:
             self._send_tensor(payload, dst)
 
     def recv(self, src: int, device=None):
-        h = self._recv_tensor((HEADER_WORDS,), torch.int64, src).cpu().tolist()
+        if self._mode == "replay":
+            rec = self._plan.inb.get(src, [])
+            k = self._next(self._cursor_in, src)
+            if k >= len(rec):
+                raise TransportError(f"message {k} from rank {src} is not in the message plan")
+            h = rec[k]
+        else:
+            h = self._recv_tensor((HEADER_WORDS,), torch.int64, src).cpu().tolist()
+            self.header_recvs += 1
+            if self._mode == "record":
+                self._plan.inb.setdefault(src, []).append(h)
         kind, shape, scalar = self._decode_header(h)
         if shape is None:
             return scalar

@@ -76,7 +76,9 @@ def run_spmd(comp: Computation, arguments: dict, identities: List[str], *, rank:
     identity = identities[rank]
     role_ranks = {r: rank_offset + i for i, r in enumerate(identities)}
     device = torch.device(device) if device is not None else torch.device("cpu")
-    tr = Transport(rank_offset + rank, len(identities), device, group=group)
+    # every worker gets every argument (the client sends them all, as the reference's
+    # GrpcMooseRuntime does), so the processes agree on message plans
+    tr = Transport(rank_offset + rank, len(identities), device, group=group, plans=True)
     store = storage if storage is not None else {}
     if is_lowered(comp):
         # a compiled host graph: run this identity's operations, Send/Receive over RCCL

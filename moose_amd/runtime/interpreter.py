@@ -131,6 +131,10 @@ class Interpreter:
             "MOOSEX_BATCH_DOTS", "1") != "0"
         ops = comp.operations
         lanes = self.lanes
+        begin = getattr(self.sess, "begin_evaluation", None)
+        if begin is not None:
+            begin(comp, self.arguments)
+        ok = False
         if lanes is not None:
             lanes.start(ops)
         try:
@@ -147,12 +151,13 @@ class Interpreter:
                 finally:
                     if lanes is not None:
                         lanes.leave([n for n in list(self.env)[before:]])
+            ok = True
         finally:
             if lanes is not None:
                 lanes.finish()
             release = getattr(self.sess, "end_evaluation", None)
             if release is not None:
-                release()
+                release(ok)
         return self.outputs
 
     def _run_op(self, op, ops, idx, batch, me):

@@ -559,7 +559,7 @@ class StackedSession(Session):
                 return PV(plc, v)
         return PV(plc, R.dot_cross(x0.v, x1.v, y0.v, y1.v, nb=1 + nbatch))
 
-    def end_evaluation(self):
+    def end_evaluation(self, ok=True):
         """Drop per-evaluation caches (prepared GEMM operands hold device memory and must
         not outlive the evaluation whose values they were prepared from)."""
         self.__dict__.pop("_prepared_b", None)

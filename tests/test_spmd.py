@@ -167,3 +167,71 @@ def test_distributed_runtime_runs_lowered_graph():
     for k in local:
         np.testing.assert_allclose(np.asarray(got[k], dtype=np.float64),
                                    np.asarray(local[k], dtype=np.float64), atol=1e-5)
+
+
+def _lr_worker(rank, port, q):
+    import collections
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=3)
+    from moose_amd.models.predictors.tutorial import logistic_regression_tutorial
+    from moose_amd.parallel.spmd import SPMDSession
+    from moose_amd.parallel.transport import Transport
+    from moose_amd.runtime.interpreter import Interpreter
+    from moose_amd.runtime.local import to_native
+
+    tm = logistic_regression_tutorial(128)
+    comp = to_native(tm.computation, 128)
+    tr = Transport(rank, 3, "cpu", plans=True)
+    res = []
+    for _ in range(2):
+        reads = collections.Counter()
+        saved = {n: getattr(torch.Tensor, n) for n in ("cpu", "item", "tolist")}
+        for n, f in saved.items():
+            def wrap(self, *a, _f=f, _n=n, **k):
+                reads[_n] += 1
+                return _f(self, *a, **k)
+            setattr(torch.Tensor, n, wrap)
+        h0 = tr.header_recvs
+        try:
+            sess = SPMDSession(("alice", "bob", "carole")[rank], {"alice": 0, "bob": 1, "carole": 2},
+                               tr, "cpu")
+            interp = Interpreter(sess, {}, fixedpoint_ring=128)
+            outs = interp.run(comp, {"x": tm.x_test})
+        finally:
+            for n, f in saved.items():
+                setattr(torch.Tensor, n, f)
+        got = interp.to_numpy(list(outs.values())[0]) if rank == 1 else None
+        res.append((tr.header_recvs - h0, sum(reads.values()), sess.stats.rounds,
+                    None if got is None else float(np.abs(got - tm.proba).max())))
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_spmd_lr_inference_steady_state_is_header_free():
+    """SPMD private LR inference (the tutorial model, one process per party): after the
+    first evaluation under a message plan, no protocol step reads a header or any tensor
+    back to the host, and the round count equals the stacked session's (VERDICT r2 item 5;
+    reference replicated/convert.rs:49-160 ships HostShape metadata with every Share)."""
+    import torch.multiprocessing as mp
+
+    from moose_amd.models.predictors.tutorial import logistic_regression_tutorial
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_lr_worker, args=(r, port, q)) for r in range(3)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(3))
+    for p in ps:
+        p.join(60)
+    tm = logistic_regression_tutorial(128)
+    rt = LocalMooseRuntime(["alice", "bob", "carole"], device="cpu")
+    rt.evaluate_computation(tm.computation, {"x": tm.x_test})
+    for rank, evals in got.items():
+        (h0, _, r0, _), (h1, reads1, r1, _) = evals
+        assert h1 == 0 and reads1 == 0, (rank, evals)
+        assert r0 == r1 == rt.last_stats.rounds
+    assert got[1][1][3] < 1e-3  # bob's opened probabilities
