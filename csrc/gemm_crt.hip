@@ -560,7 +560,7 @@ __global__ void __launch_bounds__(256)
 // read right after the step's barrier into the second register set (the k-loop is unrolled
 // by two so the sets swap without moves), while the second half of stage kb's MFMAs runs.
 // Output bytes: 16x16 block (bi, bj) at ((bi * BN / 16 + bj) * 64 + lane) * 4 of the tile.
-template <int WR, int WC, int BN, int MINW, int STG = kStages, bool IL = false>
+template <int WR, int WC, int BN, int MINW, int STG = kStages, int IL = 0>
 __global__ void __launch_bounds__(64 * WR * WC, MINW)
     k_crt_gemm16(const int8_t* __restrict__ RA, const int8_t* __restrict__ RB,
                  int8_t* __restrict__ CR, int tiles_m, int tiles_n, int nkb, int gM,
@@ -704,21 +704,37 @@ __global__ void __launch_bounds__(64 * WR * WC, MINW)
     __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0((STG - 2) * PPW));
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    // IL == 2: the NR reads and PPW DMAs share the NM/2 odd gaps, a DMA in every
+    // (NR + PPW)/PPW-th of them (so the DMAs spread over the whole step)
+    constexpr int NMEM = NR + PPW, DEV = NMEM / PPW;
 #pragma unroll
     for (int h = 0; h < NM; ++h) {
       const int i = h / NJ, j = h % NJ;
       acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
-      if (h % GAP == GAP - 1 && h / GAP < NR) {
-        rd_frag(nxt, h / GAP, na, nbf);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#pragma unroll PPW
-      for (int t = 0; t < PPW; ++t)
-        if (h == NM - 2 * PPW + 2 * t + 1) {
-          dma(kn, t, cur);
+      if constexpr (IL == 2) {
+        if (h % 2 == 1 && h / 2 < NMEM) {
+          const int u = h / 2;
+          if (u % DEV == DEV - 1 && u / DEV < PPW) {
+            dma(kn, u / DEV, cur);
+          } else {
+            const int q = u - (u / DEV < PPW ? u / DEV : PPW);
+            if (q < NR) rd_frag(nxt, q, na, nbf);
+          }
           __builtin_amdgcn_sched_barrier(0);
         }
+      } else {
+        if (h % GAP == GAP - 1 && h / GAP < NR) {
+          rd_frag(nxt, h / GAP, na, nbf);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll PPW
+        for (int t = 0; t < PPW; ++t)
+          if (h == NM - 2 * PPW + 2 * t + 1) {
+            dma(kn, t, cur);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+      }
     }
   };
 
@@ -918,7 +934,7 @@ int crt_kernel() {  // MOOSEX_CRT_KERNEL: 1 = 4 waves of 128x128, 2 = 8 waves of
   // faster than 6 on the same box, profiles/r3_crt_gemm.md), 9 = 8 with 4 stages
   const char* e = std::getenv("MOOSEX_CRT_KERNEL");
   const int v = e ? std::atoi(e) : 8;
-  return v >= 1 && v <= 9 ? v : 8;
+  return v >= 1 && v <= 11 ? v : 8;
 }
 bool crt_mfma16() { return crt_kernel() >= 4; }
 int recon_dot4() {  // MOOSEX_CRT_RECON=0: the multiply-add reconstruction
@@ -984,7 +1000,7 @@ int dma_mask() {
   return e ? std::atoi(e) : 3;
 }
 
-template <int WR, int WC, int BN, int MINW, bool M16, int STG = kStages, bool IL = false>
+template <int WR, int WC, int BN, int MINW, bool M16, int STG = kStages, int IL = 0>
 void launch_variant(const CPlan& p, const Tables& tb, int64_t batch, const int8_t* ra,
                     const int8_t* rb, int8_t* cr, int bcast, int roll, hipStream_t st) {
   constexpr int lds = STG * (kImg + BN * BK);
@@ -1011,8 +1027,10 @@ void launch_crt_gemm(const CPlan& p, const Tables& tb, int64_t batch, const int8
     case 3: launch_variant<2, 2, 128, 2, false>(p, tb, batch, ra, rb, cr, bcast, 0, st); break;
     case 6: launch_variant<2, 4, 256, 2, true>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
     case 7: launch_variant<2, 4, 256, 2, true, 4>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
-    case 8: launch_variant<2, 4, 256, 2, true, 3, true>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
-    case 9: launch_variant<2, 4, 256, 2, true, 4, true>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
+    case 8: launch_variant<2, 4, 256, 2, true, 3, 1>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
+    case 9: launch_variant<2, 4, 256, 2, true, 4, 1>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
+    case 10: launch_variant<2, 4, 256, 2, true, 3, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
+    case 11: launch_variant<2, 4, 256, 2, true, 4, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
     default: launch_variant<2, 2, 128, 2, true>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
   }
 }

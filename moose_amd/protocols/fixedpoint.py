@@ -234,6 +234,26 @@ def shape_of(sess, x):
     return sess.p_shape(t.s0)
 
 
+def static_shape(sess, x):
+    """shape_of, or None where the shape is only known at run time (shape-polymorphic
+    lowering without arg_specs)."""
+    try:
+        return shape_of(sess, x)
+    except ValueError:
+        return None
+
+
+def broadcast_like(sess, small: RepTensor, big: RepTensor) -> RepTensor:
+    """``small`` broadcast to ``big``'s shape: a static Broadcast when the shape is known,
+    else BroadcastLike, which reads the shape from ``big`` when the lowered graph runs."""
+    shape = static_shape(sess, big)
+    if shape is not None:
+        return rep.local(sess, small, "Broadcast", shape=tuple(shape))
+    s0, s1 = rep._sharewise(sess, "BroadcastLike", small.plc, (small.s0, small.s1),
+                            (big.s0, big.s1))
+    return RepTensor(small.plc, small.bits, small.kind, s0, s1)
+
+
 # ---------------------------------------------------------------------------
 # comparisons and selection
 # ---------------------------------------------------------------------------
@@ -603,8 +623,12 @@ def sigmoid(sess, x: RepFixed) -> RepFixed:
 
 
 def softmax(sess, x: RepFixed, axis: int, upmost_index: int) -> RepFixed:
-    n = shape_of(sess, x)[axis]
-    cols = [local(sess, x, "IndexAxis", axis=axis, index=i) for i in range(min(n, upmost_index))]
+    """Reference softmax.rs:55-70: the comparison tree is unrolled over ``upmost_index``
+    slices of ``axis`` (the axis length when the shape is static), so it lowers without
+    concrete shapes."""
+    shape = static_shape(sess, x)
+    n = upmost_index if shape is None else min(shape[axis], upmost_index)
+    cols = [local(sess, x, "IndexAxis", axis=axis, index=i) for i in range(n)]
     mx = maximum(sess, cols)
     mxe = local(sess, mx, "ExpandDims", axis=[axis])
     shifted = _with(x, rep.sub(sess, x.t, _bcast(sess, mxe.t, x.t)))
@@ -616,8 +640,7 @@ def softmax(sess, x: RepFixed, axis: int, upmost_index: int) -> RepFixed:
 
 
 def _bcast(sess, small: RepTensor, big: RepTensor) -> RepTensor:
-    shape = sess.p_shape(big.s0)
-    return rep.local(sess, small, "Broadcast", shape=shape)
+    return broadcast_like(sess, small, big)
 
 
 def argmax(sess, x: RepFixed, axis: int, upmost_index: int) -> RepTensor:
@@ -625,12 +648,20 @@ def argmax(sess, x: RepFixed, axis: int, upmost_index: int) -> RepTensor:
     (value, index) pairs reduced with less + mux (reference argmax.rs:6-96).  Each tree
     level is ONE stacked comparison over all its pairs and ONE mux that selects values
     and indices together."""
-    n = min(shape_of(sess, x)[axis], upmost_index)
+    shape = static_shape(sess, x)
+    n = upmost_index if shape is None else min(shape[axis], upmost_index)
     vals = [local(sess, x, "IndexAxis", axis=axis, index=i) for i in range(n)]
     bits = x.bits
-    idx = [RepFixed(rep.from_public(sess, x.plc, R.fill(shape_of(sess, vals[0]), i, bits,
-                                                        sess.device), bits), 0, x.integ)
-           for i in range(n)]
+    vshape = static_shape(sess, vals[0])
+
+    def index_const(i):
+        if vshape is not None:
+            return rep.from_public(sess, x.plc, R.fill(vshape, i, bits, sess.device), bits)
+        # shape-polymorphic: a public scalar broadcast to the slices' run-time shape
+        c = rep.from_public(sess, x.plc, R.fill((), i, bits, sess.device), bits)
+        return broadcast_like(sess, c, vals[0].t)
+
+    idx = [RepFixed(index_const(i), 0, x.integ) for i in range(n)]
     pairs = list(zip(vals, idx))
     while len(pairs) > 1:
         h = len(pairs) // 2

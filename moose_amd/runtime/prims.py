@@ -287,6 +287,13 @@ def _broadcast(nb, a, shape):
     return a.expand(tuple(a.shape[:nb]) + tuple(shape)).contiguous()
 
 
+@prim("BroadcastLike")
+def _broadcast_like(nb, a, like):
+    """Broadcast ``a`` to the (run-time) shape of ``like`` -- the shape-polymorphic form of
+    Broadcast, for lowered graphs whose shapes are only known when they run."""
+    return _broadcast(nb, a, tuple(like.shape[nb:]))
+
+
 @prim("AtLeast2D")
 def _atleast_2d(nb, a, to_column_vector=False):
     if _is_rt(a):

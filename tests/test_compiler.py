@@ -209,10 +209,36 @@ def test_shape_polymorphic_lowering_one_plan_two_sizes():
         np.testing.assert_allclose(out, 1 / (1 + np.exp(-(x @ y))), atol=1e-6)
 
 
-def test_polymorphic_plan_asks_for_shapes_where_structure_depends_on_size():
+@pytest.mark.parametrize("op", ["Softmax", "Argmax"])
+def test_shape_polymorphic_softmax_argmax_one_plan_two_sizes(op):
+    """Size-structured ops lower from their ``upmost_index`` attribute, as the reference
+    does (replicated/softmax.rs:55-70, argmax.rs:6-96): no arg_specs, one plan, two row
+    counts (broadcasts read their shape at run time)."""
     from moose_amd.compiler import passes as P
     from moose_amd.ir.textual import parse_computation
+    from moose_amd.runtime.local import LocalMooseRuntime
 
-    src = POLY.replace("Sigmoid:", "Softmax{axis = 1, upmost_index = 4}:")
-    with pytest.raises(Exception, match="arg_specs|static shapes"):
-        P.compile(parse_computation(src), P.DEFAULT_PASSES, cache=False)
+    if op == "Softmax":
+        src = POLY.replace("Sigmoid:", "Softmax{axis = 1, upmost_index = 4}:")
+    else:
+        src = POLY.replace(
+            "sig = Sigmoid: (Tensor<Fixed128(24, 40)>) -> Tensor<Fixed128(24, 40)> (dot_0)",
+            "sig = Argmax{axis = 1, upmost_index = 4}: (Tensor<Fixed128(24, 40)>) -> "
+            "Tensor<Uint64> (dot_0)").replace(
+            "cast_2 = Cast: (Tensor<Fixed128(24, 40)>) -> Tensor<Float64> (sig) @Host(player2)",
+            "cast_2 = Identity: (Tensor<Uint64>) -> Tensor<Uint64> (sig) @Host(player2)").replace(
+            "output_0 = Output{tag = \"output_0\"}: (Tensor<Float64>) -> Tensor<Float64>",
+            "output_0 = Output{tag = \"output_0\"}: (Tensor<Uint64>) -> Tensor<Uint64>")
+    low = P.compile(parse_computation(src), P.DEFAULT_PASSES, cache=False)
+    assert "BroadcastLike" in {o.kind for o in low.operations}
+    rt = LocalMooseRuntime(["player0", "player1", "player2"], device="cpu")
+    for m in (2, 5):
+        rng = np.random.default_rng(m)
+        x, y = rng.uniform(-1, 1, (m, 3)), rng.uniform(-1, 1, (3, 4))
+        z = x @ y
+        out = np.asarray(rt.evaluate_compiled(low, {"x": x, "y": y})["output_0"])
+        if op == "Softmax":
+            e = np.exp(z - z.max(axis=1, keepdims=True))
+            np.testing.assert_allclose(out, e / e.sum(axis=1, keepdims=True), atol=1e-4)
+        else:
+            assert out.shape == (m,) and (out.astype(np.int64) == z.argmax(axis=1)).all()
