@@ -77,6 +77,13 @@ def run_one(runtime, mode, n, k, n_iter):
     y = np.identity(n)
     args = {"x_arg": x, "y_arg": y}
     runtime.evaluate_computation(native, args)  # warm-up
+    if getattr(runtime, "use_graphs", False):
+        # hipGraph plans: capture, then the adaptive probes (runtime/graphs.py) decide
+        # between replay and eager before the timed evaluations
+        from moose_amd.runtime.graphs import PROBES
+
+        for _ in range(2 * PROBES + 1):
+            runtime.evaluate_computation(native, args)
     times = []
     out = None
     for _ in range(n_iter):

@@ -198,6 +198,21 @@ class GraphPlan:
         self._stager = stager  # keep the staged constants alive
         self.replays = 0
         self._pinned = {}
+        self.t_graph, self.t_eager = [], []
+        self.decision = "graph" if PROBES <= 0 else None
+
+    def next_mode(self) -> str:
+        """"graph" / "eager" once decided; "probe" (a timed replay) or "eager" (a timed
+        eager evaluation) while measuring."""
+        if self.decision is not None:
+            return self.decision
+        if len(self.t_graph) < PROBES:
+            return "probe"
+        if len(self.t_eager) < PROBES:
+            return "eager"
+        med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
+        self.decision = "graph" if med(self.t_graph) <= med(self.t_eager) else "eager"
+        return self.decision
 
     def _decode(self, interp, outs) -> Dict[str, np.ndarray]:
         res = {}
@@ -228,18 +243,40 @@ class GraphPlan:
         return self._decode(self.interp, self.outs)
 
 
+PROBES = int(os.environ.get("MOOSEX_GRAPHS_PROBES", "3"))
+
+
 class GraphCache:
-    """Per-runtime cache of captured plans keyed by (computation, argument signature)."""
+    """Per-runtime cache of captured plans keyed by (computation, argument signature).
+
+    Adaptive replay: a replay only pays where an evaluation is bound by host dispatch; at
+    sizes where the GPU work dominates, HIP's graph dispatch can be slower than the eager
+    stream (profiles/r3_graphs_vs_eager.md).  So after the capture each plan times
+    ``PROBES`` replays and ``PROBES`` eager evaluations (the caller runs those and reports
+    them through :meth:`note_eager`) and then keeps the faster mode by median
+    (``MOOSEX_GRAPHS_PROBES=0``: always replay)."""
 
     def __init__(self):
         self.plans = {}
         self.failed = set()
+        self._eager_key = None
 
     def evaluate(self, comp, arguments, device, storage, ring, seed=None, lanes=None):
         key = (id(comp), signature(arguments))
+        self._eager_key = None
         plan = self.plans.get(key)
         if plan is not None and plan.comp is comp:
-            return plan.run(arguments), plan.stats
+            mode = plan.next_mode()
+            if mode == "eager":
+                self._eager_key = key  # the caller evaluates eagerly and reports the time
+                return None
+            import time
+
+            t0 = time.perf_counter()
+            res = plan.run(arguments)
+            if mode == "probe":
+                plan.t_graph.append(time.perf_counter() - t0)
+            return res, plan.stats
         if key in self.failed or not capturable(comp):
             return None
         try:
@@ -259,3 +296,10 @@ class GraphCache:
             return None
         self.plans[key] = plan
         return plan.first, plan.stats
+
+    def note_eager(self, seconds: float):
+        """Time of the eager evaluation that evaluate() just handed to the caller."""
+        key, self._eager_key = self._eager_key, None
+        plan = self.plans.get(key) if key is not None else None
+        if plan is not None and plan.decision is None:
+            plan.t_eager.append(seconds)

@@ -162,7 +162,10 @@ class LocalMooseRuntime:
             result[tag] = interp.to_numpy(lv)
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
-        elapsed = int((time.perf_counter() - t0) * 1e6)
+        dt = time.perf_counter() - t0
+        if self.use_graphs and self.device.type == "cuda":
+            self._graphs.note_eager(dt)  # adaptive replay: the plan's eager probe
+        elapsed = int(dt * 1e6)
         self.last_timings = {i: elapsed for i in self.identities}
         self.last_stats = sess.stats
         return result

@@ -42,6 +42,22 @@ def test_stager_rejects_data_dependent_uploads():
         st(torch.arange(4) + 1, "cpu")
 
 
+@pytest.mark.parametrize("t_graph,t_eager,want", [(1.0, 2.0, "graph"), (3.0, 2.0, "eager")])
+def test_adaptive_replay_keeps_the_faster_mode(t_graph, t_eager, want):
+    """After the capture a plan times PROBES replays and PROBES eager evaluations, then
+    keeps the faster mode (graphs never lose to eager on a plan)."""
+    plan = graphs.GraphPlan.__new__(graphs.GraphPlan)
+    plan.t_graph, plan.t_eager, plan.decision = [], [], None
+    seen = []
+    for _ in range(2 * graphs.PROBES):
+        mode = plan.next_mode()
+        seen.append(mode)
+        (plan.t_graph if mode == "probe" else plan.t_eager).append(
+            t_graph if mode == "probe" else t_eager)
+    assert seen == ["probe"] * graphs.PROBES + ["eager"] * graphs.PROBES
+    assert plan.next_mode() == want and plan.decision == want
+
+
 @pytest.mark.gpu
 def test_logreg_training_replays_from_graph():
     L = _load("logreg_train")
