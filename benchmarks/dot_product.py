@@ -82,7 +82,7 @@ def run_one(runtime, mode, n, k, n_iter):
         # between replay and eager before the timed evaluations
         from moose_amd.runtime.graphs import PROBES
 
-        for _ in range(2 * PROBES + 1):
+        for _ in range(2 * PROBES + 2):
             runtime.evaluate_computation(native, args)
     times = []
     out = None

@@ -199,17 +199,20 @@ class GraphPlan:
         self.replays = 0
         self._pinned = {}
         self.t_graph, self.t_eager = [], []
+        self._warm = False
         self.decision = "graph" if PROBES <= 0 else None
 
     def next_mode(self) -> str:
-        """"graph" / "eager" once decided; "probe" (a timed replay) or "eager" (a timed
-        eager evaluation) while measuring."""
+        """"graph" / "eager" once decided; while measuring, "probe" (a timed replay) and
+        "eager" (a timed eager evaluation) alternate, after one untimed replay (a graph's
+        first launch uploads it)."""
         if self.decision is not None:
             return self.decision
-        if len(self.t_graph) < PROBES:
-            return "probe"
-        if len(self.t_eager) < PROBES:
-            return "eager"
+        if not self._warm:
+            self._warm = True
+            return "graph"
+        if len(self.t_graph) < PROBES or len(self.t_eager) < PROBES:
+            return "probe" if len(self.t_graph) <= len(self.t_eager) else "eager"
         med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
         self.decision = "graph" if med(self.t_graph) <= med(self.t_eager) else "eager"
         return self.decision

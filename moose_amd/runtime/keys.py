@@ -97,7 +97,14 @@ class KeyTable:
 
     def _write(self, base: int, keys):
         img = torch.from_numpy(slot_words(keys).view(np.int32))
-        self.t[base:base + len(keys)].copy_(img)
+        if self.device.type == "cuda":
+            # a pinned staging copy + asynchronous DMA in stream order: a pageable copy
+            # would block the host until the stream drained (a host sync per session
+            # setup / per graph replay).  The caching host allocator keeps the staging
+            # buffer alive until the copy has run.
+            self.t[base:base + len(keys)].copy_(img.pin_memory(), non_blocking=True)
+        else:
+            self.t[base:base + len(keys)].copy_(img)
         if _lanes_active(self.device):  # readers on other streams see complete keys
             torch.cuda.current_stream(self.device).synchronize()
 
