@@ -1,11 +1,11 @@
 """Session PRF keys held in device memory ("key slots").
 
-Every PRF evaluation of a stacked session -- zero shares, input sharing, the dealer masks
-of TruncPr, seeded sampling -- is an AES-128-CTR keystream under one of the session's
-keys.  Instead of expanding the key on the host and passing the schedule as a launch
-parameter, the session keeps its keys in a :class:`KeyTable`: one device tensor of
-``MX_KEY_SLOT_WORDS``-word slots (raw key + expanded schedule, ``csrc/moosex.h``) that the
-kernels read at run time.  Two things follow:
+Every PRF evaluation of a session -- zero shares, input sharing, the dealer masks of
+TruncPr, seeded sampling -- is a ChaCha12 keystream (``csrc/prf_core.h``) under one of the
+session's keys.  Instead of passing keys as launch parameters, the session keeps them in a
+:class:`KeyTable`: one device tensor of ``MX_KEY_SLOT_WORDS``-word slots (the raw 128-bit key
+in words 0..3, followed by its AES-128 schedule for the AES dialect, ``csrc/moosex.h``) that
+the kernels read at run time.  Two things follow:
 
 * a hipGraph captured from an evaluation does not bake the keys in: refreshing the table
   before each replay gives every replay fresh, independent randomness
