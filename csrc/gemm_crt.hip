@@ -560,7 +560,7 @@ __global__ void __launch_bounds__(256)
 // read right after the step's barrier into the second register set (the k-loop is unrolled
 // by two so the sets swap without moves), while the second half of stage kb's MFMAs runs.
 // Output bytes: 16x16 block (bi, bj) at ((bi * BN / 16 + bj) * 64 + lane) * 4 of the tile.
-template <int WR, int WC, int BN, int MINW, int STG = kStages, int IL = 0>
+template <int WR, int WC, int BN, int MINW, int STG = kStages, int IL = 0, bool BUF = false>
 __global__ void __launch_bounds__(64 * WR * WC, MINW)
     k_crt_gemm16(const int8_t* __restrict__ RA, const int8_t* __restrict__ RB,
                  int8_t* __restrict__ CR, int tiles_m, int tiles_n, int nkb, int gM,
@@ -621,12 +621,40 @@ __global__ void __launch_bounds__(64 * WR * WC, MINW)
   bool dma_on[PPW];
 #pragma unroll
   for (int t = 0; t < PPW; ++t) dma_on[t] = (dma_mask >> ((wave + NW * t) >= 16 ? 1 : 0)) & 1;
+  // BUF: buffer_load ... lds through wave-uniform buffer descriptors -- the per-lane part
+  // of every DMA address is the lane's 16-byte slot (one VGPR), the piece and k-step
+  // offsets are scalar -- instead of 64-bit per-lane pointers per piece (VGPRs + VALU)
+  auto rsrc_of = [](const int8_t* base, int64_t bytes) __attribute__((always_inline)) {
+    const uint64_t a = (uint64_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0,
+                                             (int)bytes, 0x00020000);
+  };
+  const int64_t a_bytes = (int64_t)a_nkb * kImg, b_bytes = (int64_t)nkb * kImgB;
+  __amdgpu_buffer_rsrc_t rs_a = rsrc_of(ga, a_bytes), rs_b = rsrc_of(gb, b_bytes);
+  __amdgpu_buffer_rsrc_t rs_a2 = roll ? rsrc_of(ga2 + a_bytes, a_bytes) : rs_a;
+  const int lane16 = lane * 16;
   auto dma = [&](int kb, int t, int8_t* dst_stage) {
     if (!dma_on[t]) return;  // MOOSEX_CRT_DMA_MASK timing experiments only
-    const int8_t* src = kb >= khalf ? srcs2[t] : srcs[t];
-    __builtin_amdgcn_global_load_lds((const void*)(src + (int64_t)kb * steps[t]),
-                                     (__attribute__((address_space(3))) void*)(dst_stage + dsts[t]),
-                                     16, 0, 0);
+    if constexpr (BUF) {
+      const int pc = wave + NW * t;
+      auto* dst = (__attribute__((address_space(3))) void*)(dst_stage + dsts[t]);
+      if (pc >= 16)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_b, dst, 16, lane16,
+                                                 (pc - 16) * 1024 + kb * kImgB, 0, 0);
+      else if (kb >= khalf)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_a2, dst, 16, lane16,
+                                                 pc * 1024 + (kb - khalf) * kImg, 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_a, dst, 16, lane16, pc * 1024 + kb * kImg,
+                                                 0, 0);
+    } else {
+      const int8_t* src = kb >= khalf ? srcs2[t] : srcs[t];
+      __builtin_amdgcn_global_load_lds((const void*)(src + (int64_t)kb * steps[t]),
+                                       (__attribute__((address_space(3))) void*)(dst_stage + dsts[t]),
+                                       16, 0, 0);
+    }
   };
 
   v4i acc[MI][NJ];
@@ -934,7 +962,7 @@ int crt_kernel() {  // MOOSEX_CRT_KERNEL: 1 = 4 waves of 128x128, 2 = 8 waves of
   // faster than 6 on the same box, profiles/r3_crt_gemm.md), 9 = 8 with 4 stages
   const char* e = std::getenv("MOOSEX_CRT_KERNEL");
   const int v = e ? std::atoi(e) : 8;
-  return v >= 1 && v <= 11 ? v : 8;
+  return v >= 1 && v <= 14 ? v : 8;
 }
 bool crt_mfma16() { return crt_kernel() >= 4; }
 int recon_dot4() {  // MOOSEX_CRT_RECON=0: the multiply-add reconstruction
@@ -1000,16 +1028,17 @@ int dma_mask() {
   return e ? std::atoi(e) : 3;
 }
 
-template <int WR, int WC, int BN, int MINW, bool M16, int STG = kStages, int IL = 0>
+template <int WR, int WC, int BN, int MINW, bool M16, int STG = kStages, int IL = 0,
+          bool BUF = false>
 void launch_variant(const CPlan& p, const Tables& tb, int64_t batch, const int8_t* ra,
                     const int8_t* rb, int8_t* cr, int bcast, int roll, hipStream_t st) {
   constexpr int lds = STG * (kImg + BN * BK);
-  const void* fn = M16 ? (const void*)k_crt_gemm16<WR, WC, BN, MINW, STG, IL>
+  const void* fn = M16 ? (const void*)k_crt_gemm16<WR, WC, BN, MINW, STG, IL, BUF>
                        : (const void*)k_crt_gemm<WR, WC, BN, MINW>;
   ensure_lds_attr(fn, lds, st);
   const dim3 grid((unsigned)(p.tiles_m * p.tiles_n), (unsigned)(batch * p.n));
   if constexpr (M16)
-    hipLaunchKernelGGL((k_crt_gemm16<WR, WC, BN, MINW, STG, IL>), grid, dim3(64 * WR * WC), lds, st, ra,
+    hipLaunchKernelGGL((k_crt_gemm16<WR, WC, BN, MINW, STG, IL, BUF>), grid, dim3(64 * WR * WC), lds, st, ra,
                        rb, cr, (int)p.tiles_m, (int)p.tiles_n, (int)p.nkb, gemm_group_m(), tb.ep,
                        dma_mask(), bcast, (int)p.a_nkb, roll);
   else
@@ -1031,6 +1060,9 @@ void launch_crt_gemm(const CPlan& p, const Tables& tb, int64_t batch, const int8
     case 9: launch_variant<2, 4, 256, 2, true, 4, 1>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
     case 10: launch_variant<2, 4, 256, 2, true, 3, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
     case 11: launch_variant<2, 4, 256, 2, true, 4, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
+    case 12: launch_variant<2, 2, 256, 1, true, 3, 1>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
+    case 13: launch_variant<2, 4, 256, 2, true, 3, 1, true>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
+    case 14: launch_variant<2, 2, 256, 1, true, 3, 1, true>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
     default: launch_variant<2, 2, 128, 2, true>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
   }
 }

@@ -28,6 +28,7 @@ import torch
 from moose_amd.ops import native as nat
 
 SLOT_WORDS = 48  # MX_KEY_SLOT_WORDS
+_PINNED = os.environ.get("MOOSEX_KEYS_PINNED", "1") != "0"
 
 
 class KeyRef:
@@ -97,7 +98,7 @@ class KeyTable:
 
     def _write(self, base: int, keys):
         img = torch.from_numpy(slot_words(keys).view(np.int32))
-        if self.device.type == "cuda":
+        if self.device.type == "cuda" and _PINNED:
             # a pinned staging copy + asynchronous DMA in stream order: a pageable copy
             # would block the host until the stream drained (a host sync per session
             # setup / per graph replay).  The caching host allocator keeps the staging

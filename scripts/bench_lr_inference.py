@@ -31,28 +31,12 @@ def main():
     ap.add_argument("--cprofile", default=None, help="write a host-side cProfile summary")
     a = ap.parse_args()
     import torch
-    from sklearn.datasets import make_classification
-    from sklearn.linear_model import LogisticRegression
-    from sklearn.model_selection import train_test_split
-
-    from moose_amd.models import predictors
+    from moose_amd.models.predictors.tutorial import logistic_regression_tutorial
     from moose_amd.runtime.local import LocalMooseRuntime
 
-    X, y = make_classification(n_samples=1000, n_features=10, n_classes=2, random_state=5)
-    X_train, X_test, y_train, _ = train_test_split(X, y, test_size=0.2, random_state=5)
-    lg = LogisticRegression().fit(X_train, y_train)
-    # the tutorial's path: sklearn model -> ONNX (the graph skl2onnx emits: LinearClassifier
-    # with rows (-w, w) and a LOGISTIC post-transform) -> predictors.from_onnx
-    from moose_amd.models.predictors import onnx_proto
-
-    onnx_bytes = onnx_proto.sklearn_logistic_regression_model(lg.coef_, lg.intercept_, 10)
-    model = predictors.from_onnx(onnx_bytes)
-    # fixed(24,40) needs Z_2^128 (pymoose's mapping); Z_2^64 uses the reference's
-    # canonical Fixed64 precision fixed(14,23) (replicated/input.rs:91-92)
-    import moose_amd as pm
-
-    dtype = predictors.DEFAULT_FIXED_DTYPE if a.ring == 128 else pm.fixed(14, 23)
-    comp = model.predictor_factory(dtype)
+    # the tutorial's path: sklearn model -> ONNX -> predictors.from_onnx (tutorial.py)
+    tm = logistic_regression_tutorial(a.ring)
+    dtype, comp, X_test = tm.dtype, tm.computation, tm.x_test
     dev = a.device or ("cuda" if torch.cuda.is_available() else "cpu")
     rt = LocalMooseRuntime(["alice", "bob", "carole"], device=dev, fixedpoint_ring=a.ring,
                            use_graphs=a.graphs)
@@ -82,7 +66,7 @@ def main():
         with open(a.cprofile, "w") as f:
             f.write(buf.getvalue())
     pred = np.asarray(list(out.values())[0])
-    err = float(np.abs(pred - lg.predict_proba(X_test)).max())
+    err = float(np.abs(pred - tm.proba).max())
     lat = np.sort(np.asarray(lat)) * 1e3
     print(json.dumps({
         "metric": "private LR inference p50 latency", "value": float(np.median(lat)),
