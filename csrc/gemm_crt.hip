@@ -952,14 +952,16 @@ inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 int crt_kernel() {  // MOOSEX_CRT_KERNEL: 1 = 4 waves of 128x128, 2 = 8 waves of 128x64
   // (256x256 tiles, one block per CU), 3 = 4 waves of 128x64 in 256x128 tiles (two blocks
   // per CU, so one block's barrier waits, LDS bursts and epilogue overlap the other's MFMAs)
-  // 4 = 16x16x64 MFMAs, 4 waves of 128x128 (256x256 tiles), 5 = 16x16x64, 4 waves of
-  // 128x64 in 256x128 tiles (two blocks per CU; 12 % faster than 3 -- the chip holds a
-  // higher clock on the 16x16 shape), 6 = 16x16x64, 8 waves of 128x64 in 256x256 tiles, two
-  // blocks per CU (the default: 11.95 vs 12.12 ms for 5 on the 4096^2 Z_2^128 RSS product,
-  // profiles/r2_crt_variant_ab.md)
-  // 7 = 6 with a 4-stage ring (no gain), 8 = 6 with one barrier at the start of each k-step
-  // and the next stage's fragment reads spread over the step's MFMAs (the default: ~6 %
-  // faster than 6 on the same box, profiles/r3_crt_gemm.md), 9 = 8 with 4 stages
+  // 4 = 16x16x64 MFMAs, 4 waves of 128x128 (256x256 tiles; the compiler spills: 71 ms),
+  // 5 = 16x16x64, 4 waves of 128x64 in 256x128 tiles (72 KB LDS: two blocks per CU; 12 %
+  // faster than 3 -- the chip holds a higher clock on the 16x16 shape), 6 = 16x16x64, 8
+  // waves of 128x64 in 256x256 tiles (96 KB LDS and 242 VGPRs: ONE block per CU, two waves
+  // per SIMD; 11.95 vs 12.12 ms for 5 on the 4096^2 Z_2^128 RSS product,
+  // profiles/r2_crt_variant_ab.md), 7 = 6 with a 4-stage ring (no gain), 8 = 6 with one
+  // barrier at the start of each k-step and the next stage's fragment reads spread over the
+  // step's MFMAs (the default: 4-6 % faster than 6 on the same box, profiles/r3_crt_gemm.md),
+  // 9 = 8 with 4 stages, 10 / 11 = 8 / 9 with the DMAs spread over the step too, 12 = 4
+  // with 8's schedule (spills), 13 / 14 = 8 / 12 with buffer-descriptor DMAs (13: slower)
   const char* e = std::getenv("MOOSEX_CRT_KERNEL");
   const int v = e ? std::atoi(e) : 8;
   return v >= 1 && v <= 14 ? v : 8;
