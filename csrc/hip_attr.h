@@ -16,13 +16,13 @@ inline void ensure_lds_attr(const void* fn, int bytes, hipStream_t st) {
   static std::mutex mu;
   static std::set<std::pair<int, const void*>> done;
   int dev = 0;
-  if (hipStreamGetDevice(st, &dev) != hipSuccess) hipGetDevice(&dev);
+  if (hipStreamGetDevice(st, &dev) != hipSuccess) (void)hipGetDevice(&dev);
   std::lock_guard<std::mutex> lock(mu);
   if (done.insert({dev, fn}).second) {
     int cur = 0;
-    hipGetDevice(&cur);
-    if (cur != dev) hipSetDevice(dev);
-    hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-    if (cur != dev) hipSetDevice(cur);
+    (void)hipGetDevice(&cur);
+    if (cur != dev) (void)hipSetDevice(dev);
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (cur != dev) (void)hipSetDevice(cur);
   }
 }
