@@ -200,9 +200,13 @@ __global__ void __launch_bounds__(256)
   MX_PARTY_WALK(nb, ncomp) {
     const int c = (int)(g / nblk);
     const uint64_t B = (uint64_t)(g - c * nblk);
-    const int r = rel.r[c];
+    // rel code: the role relative to the owner (0..2) + 4 * (1 + the component of P_{j+2})
+    // when the owner's masked share stays on this device (written straight into its s1)
+    const int code = rel.r[c];
+    if (code < 0) continue;
+    const int r = code & 3, fwd = (code >> 2) - 1;
     const int64_t base = (int64_t)c * n;
-    if (r < 0 || r > 2) continue;
+    if (r > 2) continue;
     uint32_t wa[16], wb[16];
     if (r != 2) mx::chacha_block(rks[2 * c], n1, B, wa);
     mx::chacha_block(rks[2 * c + 1], na, B, wb);
@@ -223,8 +227,10 @@ __global__ void __launch_bounds__(256)
         } else {
           const T r1 = mxd::pick<T>(al, ah, j);
           if (r == 0) {
-            out0[base + i] = kind == MX_CROSS_BOOL ? (T)(x[i] ^ r1 ^ ra) : (T)(x[i] - r1 - ra);
+            const T v = kind == MX_CROSS_BOOL ? (T)(x[i] ^ r1 ^ ra) : (T)(x[i] - r1 - ra);
+            out0[base + i] = v;
             out1[base + i] = r1;
+            if (fwd >= 0) out1[(int64_t)fwd * n + i] = v;
           } else {
             out0[base + i] = r1;
             out1[base + i] = ra;

@@ -138,9 +138,11 @@ template <class T>
 int share_party(int kind, int64_t n, int ncomp, const int* rel, const T* x, T* out0, T* out1,
                 const uint32_t* const* slots, uint64_t n1, uint64_t na) {
   for (int c = 0; c < ncomp; ++c) {
-    const int r = rel[c];
+    const int code = rel[c];  // as k_share_party: role + 4 * (1 + local P_{j+2} component)
+    if (code < 0) continue;
+    const int r = code & 3, fwd = (code >> 2) - 1;
     const int64_t base = (int64_t)c * n;
-    if (r < 0 || r > 2) continue;
+    if (r > 2) continue;
     for_chunks<T>(n, [&](int64_t i0, int64_t len) {
       std::vector<T> a(len), b(len);
       prf<T>(slots[2 * c + 1], na, i0, len, b.data());
@@ -153,6 +155,7 @@ int share_party(int kind, int64_t n, int ncomp, const int* rel, const T* x, T* o
           const T xv = x[i0 + q];
           out0[i] = kind == MX_CROSS_BOOL ? (T)(xv ^ a[q] ^ b[q]) : (T)(xv - a[q] - b[q]);
           out1[i] = a[q];
+          if (fwd >= 0) out1[(int64_t)fwd * n + i0 + q] = out0[i];
         } else {
           out0[i] = a[q];
           out1[i] = b[q];

@@ -343,11 +343,15 @@ class CyclicSession(StackedSession):
         for c in range(3):
             w = {0: (1, 2), 1: (0, 2), 2: (2, 2)}[rel[c]]
             slots += [self._slot(plc, c, w[0]), self._slot(plc, c, w[1])]
-        out0, out1 = R.share_party(kind, x.v, 3, rel, slots, n1, na)
         o = [self.offset(r) for r in plc.owners]
         j2 = (j + 2) % 3
-        self.comm.exchange([(out0[j], self._peer(o[j2] - o[j]))],
-                           [(out1[j2], self._peer(o[j] - o[j2]))])
+        local = (o[j2] - o[j]) % self.N == 0  # P_{j+2} of the owner's session is here
+        if local:  # the kernel writes the owner's masked share into P_{j+2}'s s1 too
+            rel[j] += 4 * (1 + j2)
+        out0, out1 = R.share_party(kind, x.v, 3, rel, slots, n1, na)
+        if not local:
+            self.comm.exchange([(out0[j], self._peer(o[j2] - o[j]))],
+                               [(out1[j2], self._peer(o[j] - o[j2]))])
         self.stats.record_send(x.host, plc.owners[j2], _nbytes(x.v))
         return PV(plc, R.RT(out0, bits)), PV(plc, R.RT(out1, bits))
 
