@@ -560,7 +560,7 @@ __global__ void __launch_bounds__(256)
 // read right after the step's barrier into the second register set (the k-loop is unrolled
 // by two so the sets swap without moves), while the second half of stage kb's MFMAs runs.
 // Output bytes: 16x16 block (bi, bj) at ((bi * BN / 16 + bj) * 64 + lane) * 4 of the tile.
-template <int WR, int WC, int BN, int MINW, int STG = kStages, int IL = 0, bool BUF = false>
+template <int WR, int WC, int BN, int MINW, int STG = kStages, int IL = 0>
 __global__ void __launch_bounds__(64 * WR * WC, MINW)
     k_crt_gemm16(const int8_t* __restrict__ RA, const int8_t* __restrict__ RB,
                  int8_t* __restrict__ CR, int tiles_m, int tiles_n, int nkb, int gM,
@@ -621,40 +621,12 @@ __global__ void __launch_bounds__(64 * WR * WC, MINW)
   bool dma_on[PPW];
 #pragma unroll
   for (int t = 0; t < PPW; ++t) dma_on[t] = (dma_mask >> ((wave + NW * t) >= 16 ? 1 : 0)) & 1;
-  // BUF: buffer_load ... lds through wave-uniform buffer descriptors -- the per-lane part
-  // of every DMA address is the lane's 16-byte slot (one VGPR), the piece and k-step
-  // offsets are scalar -- instead of 64-bit per-lane pointers per piece (VGPRs + VALU)
-  auto rsrc_of = [](const int8_t* base, int64_t bytes) __attribute__((always_inline)) {
-    const uint64_t a = (uint64_t)base;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0,
-                                             (int)bytes, 0x00020000);
-  };
-  const int64_t a_bytes = (int64_t)a_nkb * kImg, b_bytes = (int64_t)nkb * kImgB;
-  __amdgpu_buffer_rsrc_t rs_a = rsrc_of(ga, a_bytes), rs_b = rsrc_of(gb, b_bytes);
-  __amdgpu_buffer_rsrc_t rs_a2 = roll ? rsrc_of(ga2 + a_bytes, a_bytes) : rs_a;
-  const int lane16 = lane * 16;
   auto dma = [&](int kb, int t, int8_t* dst_stage) {
     if (!dma_on[t]) return;  // MOOSEX_CRT_DMA_MASK timing experiments only
-    if constexpr (BUF) {
-      const int pc = wave + NW * t;
-      auto* dst = (__attribute__((address_space(3))) void*)(dst_stage + dsts[t]);
-      if (pc >= 16)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_b, dst, 16, lane16,
-                                                 (pc - 16) * 1024 + kb * kImgB, 0, 0);
-      else if (kb >= khalf)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_a2, dst, 16, lane16,
-                                                 pc * 1024 + (kb - khalf) * kImg, 0, 0);
-      else
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_a, dst, 16, lane16, pc * 1024 + kb * kImg,
-                                                 0, 0);
-    } else {
-      const int8_t* src = kb >= khalf ? srcs2[t] : srcs[t];
-      __builtin_amdgcn_global_load_lds((const void*)(src + (int64_t)kb * steps[t]),
-                                       (__attribute__((address_space(3))) void*)(dst_stage + dsts[t]),
-                                       16, 0, 0);
-    }
+    const int8_t* src = kb >= khalf ? srcs2[t] : srcs[t];
+    __builtin_amdgcn_global_load_lds((const void*)(src + (int64_t)kb * steps[t]),
+                                     (__attribute__((address_space(3))) void*)(dst_stage + dsts[t]),
+                                     16, 0, 0);
   };
 
   v4i acc[MI][NJ];
@@ -798,346 +770,6 @@ __global__ void __launch_bounds__(64 * WR * WC, MINW)
       const int bi = wr * MI + i, bj = wc * NJ + j;
       *(uint32_t*)(cr + ((bi * (BN / 16) + bj) * 64 + lane) * 4) = pack4(rr[0], rr[1], rr[2], rr[3]);
     }
-}
-
-// Variant 16: the interleaved kernel with the B operand read straight from global memory
-// into registers (the prepared image is already in fragment order): only A goes through the
-// LDS ring (16 KB stages: half the LDS-DMA and a third fewer LDS fragment reads).  The two
-// waves that share a B column block read it through the CU's L1.  Per k-step a wave issues
-// its NJ B loads for the NEXT step first, then the A DMAs, so the step-start wait
-// vmcnt((STG-2) * PPW) covers both (B loads are older than the youngest DMAs).
-template <int WR, int WC, int BN, int MINW, int STG>
-__global__ void __launch_bounds__(64 * WR * WC, MINW)
-    k_crt_gemm16g(const int8_t* __restrict__ RA, const int8_t* __restrict__ RB,
-                  int8_t* __restrict__ CR, int tiles_m, int tiles_n, int nkb, int gM,
-                  const EpiTab ep, int bcast, int a_nkb, int roll) {
-  constexpr int NW = WR * WC;
-  constexpr int MI = BM / WR / 16, NJ = BN / WC / 16;
-  constexpr int NM = MI * NJ;
-  constexpr int kImgB = BN * BK;
-  constexpr int kStageBytes = kImg;  // A only
-  constexpr int NPIECE = kStageBytes / 1024;
-  constexpr int PPW = NPIECE / NW;
-  constexpr int GAP = (NM - 2 * PPW - NJ) / MI > 0 ? (NM - 2 * PPW - NJ) / MI : 1;
-  static_assert(PPW * NW == NPIECE, "stage pieces must split evenly over the waves");
-  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
-  const int ntiles = tiles_m * tiles_n;
-  const int tid_flat = (int)xcd_remap(blockIdx.x, ntiles);
-  const int group = tid_flat / (gM * tiles_n);
-  const int first_m = group * gM;
-  const int gm = tiles_m - first_m < gM ? tiles_m - first_m : gM;
-  const int in_group = tid_flat % (gM * tiles_n);
-  const int tm = first_m + in_group % gm, tn = in_group / gm;
-  const int g = blockIdx.y;
-  const int mi = g % ep.n;
-  const int8_t* ga = RA + ((int64_t)((bcast & 1) ? mi : g) * tiles_m + tm) * a_nkb * (int64_t)kImg;
-  const int8_t* gb = RB + ((int64_t)((bcast & 2) ? mi : g) * tiles_n + tn) * nkb * (int64_t)kImgB;
-  const int8_t* ga2 = ga;
-  int khalf = 1 << 30;
-  if (roll) {
-    const int nbt = (int)gridDim.y / ep.n;
-    const int b2 = (g / ep.n + roll) % nbt;
-    ga2 = RA + ((int64_t)(b2 * ep.n + mi) * tiles_m + tm) * a_nkb * (int64_t)kImg -
-          (int64_t)a_nkb * kImg;
-    khalf = a_nkb;
-  }
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wave / WC, wc = wave % WC;
-  const int co = 16 * ((lane >> 4) ^ swz((lane & 15) >> 2));
-  const int rowa = (wr * (BM / WR) + (lane & 15)) * BK + co;
-  const int8_t* gbl = gb + (wc * (BN / WC) + (lane & 15)) * BK + co;  // this lane's B rows
-
-  const int8_t* srcs[PPW];
-  const int8_t* srcs2[PPW];
-  int dsts[PPW];
-#pragma unroll
-  for (int t = 0; t < PPW; ++t) {
-    const int pp = wave + NW * t;
-    srcs[t] = ga + pp * 1024 + lane * 16;
-    srcs2[t] = ga2 + pp * 1024 + lane * 16;
-    dsts[t] = pp * 1024;
-  }
-  auto dma = [&](int kb, int t, int8_t* dst_stage) __attribute__((always_inline)) {
-    const int8_t* src = kb >= khalf ? srcs2[t] : srcs[t];
-    __builtin_amdgcn_global_load_lds((const void*)(src + (int64_t)kb * kImg),
-                                     (__attribute__((address_space(3))) void*)(dst_stage + dsts[t]),
-                                     16, 0, 0);
-  };
-  auto ldb = [&](int kb, v4i(&fb)[NJ]) __attribute__((always_inline)) {
-    // global address space: a generic (flat) load would count in lgkmcnt too and make
-    // the compiler drain every counter before its first use
-    typedef const __attribute__((address_space(1))) v4i* gv4p;
-    const int8_t* p = gbl + (int64_t)(kb < nkb ? kb : nkb - 1) * kImgB;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) fb[j] = *(gv4p)(p + j * 16 * BK);
-  };
-
-  v4i acc[MI][NJ];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = v4i{0, 0, 0, 0};
-  v4i fa0[MI], fb0[NJ], fa1[MI], fb1[NJ];
-
-  ldb(0, fb0);
-#pragma unroll
-  for (int s = 0; s < STG; ++s)
-#pragma unroll
-    for (int t = 0; t < PPW; ++t) dma(s < nkb ? s : nkb - 1, t, smem + s * kStageBytes);
-  __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0((STG - 1) * PPW));
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int i = 0; i < MI; ++i) fa0[i] = *(const v4i*)(smem + rowa + i * 16 * BK);
-
-  auto step = [&](int kb, int8_t* cur, int8_t* nxt, v4i(&fa)[MI], v4i(&fb)[NJ], v4i(&na)[MI],
-                  v4i(&nbf)[NJ]) __attribute__((always_inline)) {
-    const int kn = kb + STG < nkb ? kb + STG : nkb - 1;
-    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0((STG - 2) * PPW));
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    ldb(kb + 1, nbf);  // next step's B fragments, straight from global memory
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int h = 0; h < NM; ++h) {
-      const int i = h / NJ, j = h % NJ;
-      acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (h % GAP == GAP - 1 && h / GAP < MI) {
-        na[h / GAP] = *(const v4i*)(nxt + rowa + (h / GAP) * 16 * BK);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#pragma unroll PPW
-      for (int t = 0; t < PPW; ++t)
-        if (h == NM - 2 * PPW + 2 * t + 1) {
-          dma(kn, t, cur);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-  };
-  auto buf = [&](int i) { return smem + i * kStageBytes; };
-  int r = 0;
-  for (int kb = 0; kb < nkb; kb += 2) {
-    step(kb, buf(r), buf(r == STG - 1 ? 0 : r + 1), fa0, fb0, fa1, fb1);
-    r = r == STG - 1 ? 0 : r + 1;
-    if (kb + 1 < nkb) {
-      step(kb + 1, buf(r), buf(r == STG - 1 ? 0 : r + 1), fa1, fb1, fa0, fb0);
-      r = r == STG - 1 ? 0 : r + 1;
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-  const float pf = ep.pf[mi], rcp = ep.rcp[mi];
-  const int t16 = ep.t16[mi];
-  int8_t* cr = CR + ((int64_t)g * ntiles + tm * tiles_n + tn) * (int64_t)(BM * BN);
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      int rr[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) rr[e] = centered_mod(acc[i][j][e], pf, rcp, t16);
-      const int bi = wr * MI + i, bj = wc * NJ + j;
-      *(uint32_t*)(cr + ((bi * (BN / 16) + bj) * 64 + lane) * 4) = pack4(rr[0], rr[1], rr[2], rr[3]);
-    }
-}
-
-// Persistent form of the interleaved 16x16x64 kernel (variant 15): a grid of one block per
-// CU walks the (tile, k-step) pairs of ALL its tiles as one stream of k-steps, so the DMAs
-// the last k-steps of a tile issue are the first stages of its NEXT tile (landing while the
-// epilogue of the finished tile runs) instead of redundant reloads, and a tile costs no
-// block launch.  Block b takes items w = j * gridDim.x + xcd_remap(b) (item = (batch
-// entry, tile)): the blocks on one XCD work on neighbouring tiles of one plane at a time.
-// The epilogue's 32 byte-stores per wave sit between two k-steps' DMAs in the vmcnt
-// order, so the first wait after an epilogue allows them to stay in flight.
-template <int WR, int WC, int BN, int MINW, int STG>
-__global__ void __launch_bounds__(64 * WR * WC, MINW)
-    k_crt_gemm16p(const int8_t* __restrict__ RA, const int8_t* __restrict__ RB,
-                  int8_t* __restrict__ CR, int tiles_m, int tiles_n, int nkb, int gM,
-                  const EpiTab ep, int bcast, int a_nkb, int roll, int nbatch) {
-  constexpr int NW = WR * WC;
-  constexpr int MI = BM / WR / 16, NJ = BN / WC / 16;
-  constexpr int NM = MI * NJ;
-  constexpr int kImgB = BN * BK;
-  constexpr int kStageBytes = kImg + kImgB;
-  constexpr int NPIECE = kStageBytes / 1024;
-  constexpr int PPW = NPIECE / NW;
-  constexpr int NR = MI + NJ;
-  constexpr int GAP = (NM - 2 * PPW) / NR > 0 ? (NM - 2 * PPW) / NR : 1;
-  static_assert(PPW * NW == NPIECE, "stage pieces must split evenly over the waves");
-  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
-  const int ntiles = tiles_m * tiles_n;
-  const int nitems = ntiles * nbatch;
-  const int G = (int)gridDim.x;
-  const int slot = (int)xcd_remap(blockIdx.x, G);
-  const int nmine = slot < nitems ? (nitems - slot + G - 1) / G : 0;
-  const int64_t total = (int64_t)nmine * nkb;  // k-steps of this block
-  if (total == 0) return;
-  const int nbt = nbatch / ep.n;
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wave / WC, wc = wave % WC;
-  const int co = 16 * ((lane >> 4) ^ swz((lane & 15) >> 2));
-  const int rowa = (wr * (BM / WR) + (lane & 15)) * BK + co;
-  const int rowb = kImg + (wc * (BN / WC) + (lane & 15)) * BK + co;
-
-  // item j of this block -> batch entry g, tile (tm, tn), operand image bases
-  struct Item {
-    int g, tm, tn;
-    const int8_t *a, *a2, *b;
-  };
-  auto item_of = [&](int j) __attribute__((always_inline)) {
-    Item it;
-    const int w = j * G + slot;
-    it.g = w / ntiles;
-    const int tid_flat = w - it.g * ntiles;
-    const int group = tid_flat / (gM * tiles_n);
-    const int first_m = group * gM;
-    const int gm = tiles_m - first_m < gM ? tiles_m - first_m : gM;
-    const int in_group = tid_flat % (gM * tiles_n);
-    it.tm = first_m + in_group % gm;
-    it.tn = in_group / gm;
-    const int mi = it.g % ep.n;
-    it.a = RA + ((int64_t)((bcast & 1) ? mi : it.g) * tiles_m + it.tm) * a_nkb * (int64_t)kImg;
-    it.b = RB + ((int64_t)((bcast & 2) ? mi : it.g) * tiles_n + it.tn) * nkb * (int64_t)kImgB;
-    it.a2 = it.a;
-    if (roll) {
-      const int b2 = (it.g / ep.n + roll) % nbt;
-      it.a2 = RA + ((int64_t)(b2 * ep.n + mi) * tiles_m + it.tm) * a_nkb * (int64_t)kImg -
-              (int64_t)a_nkb * kImg;
-    }
-    return it;
-  };
-  const int khalf = roll ? a_nkb : (1 << 30);
-  int pcs[PPW], dsts[PPW];
-#pragma unroll
-  for (int t = 0; t < PPW; ++t) {
-    pcs[t] = wave + NW * t;
-    dsts[t] = (pcs[t] >= 16 ? kImg : 0) + (pcs[t] >= 16 ? pcs[t] - 16 : pcs[t]) * 1024;
-  }
-  // the DMA stream: k-step ds of item dj (runs STG k-steps ahead of the MFMAs); past the
-  // block's last k-step it reloads that step (kept for uniform vmcnt counts)
-  int dj = 0, dkb = 0;
-  int64_t ds = 0;
-  Item di = item_of(0);
-  auto dma_step = [&](int8_t* dst_stage) __attribute__((always_inline)) {
-#pragma unroll
-    for (int t = 0; t < PPW; ++t) {
-      const int pc = pcs[t];
-      const int8_t* src;
-      if (pc >= 16)
-        src = di.b + (pc - 16) * 1024 + (int64_t)dkb * kImgB;
-      else
-        src = (dkb >= khalf ? di.a2 : di.a) + pc * 1024 + (int64_t)dkb * kImg;
-      __builtin_amdgcn_global_load_lds((const void*)(src + lane * 16),
-                                       (__attribute__((address_space(3))) void*)(dst_stage + dsts[t]),
-                                       16, 0, 0);
-      if (t + 1 < PPW) __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  auto dma_advance = [&]() __attribute__((always_inline)) {
-    if (ds + 1 < total) {
-      ++ds;
-      if (++dkb == nkb) {
-        dkb = 0;
-        di = item_of(++dj);
-      }
-    }
-  };
-
-  v4i acc[MI][NJ];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = v4i{0, 0, 0, 0};
-  v4i fa0[MI], fb0[NJ], fa1[MI], fb1[NJ];
-  auto rd_frag = [&](const int8_t* st, int q, v4i(&fa)[MI], v4i(&fb)[NJ])
-                     __attribute__((always_inline)) {
-    if (q < MI)
-      fa[q] = *(const v4i*)(st + rowa + q * 16 * BK);
-    else
-      fb[q - MI] = *(const v4i*)(st + rowb + (q - MI) * 16 * BK);
-  };
-
-#pragma unroll
-  for (int s = 0; s < STG; ++s) {
-    dma_step(smem + s * kStageBytes);
-    dma_advance();
-  }
-  __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0((STG - 1) * PPW));
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int q = 0; q < NR; ++q) rd_frag(smem, q, fa0, fb0);
-
-  // the MFMA stream: item mj, k-step mkb
-  int mj = 0, mkb = 0;
-  Item mi_item = item_of(0);
-  bool after_epi = false;
-  auto epilogue = [&]() __attribute__((always_inline)) {
-    const int mi = mi_item.g % ep.n;
-    const float pf = ep.pf[mi], rcp = ep.rcp[mi];
-    const int t16 = ep.t16[mi];
-    int8_t* cr = CR + ((int64_t)mi_item.g * ntiles + mi_item.tm * tiles_n + mi_item.tn) *
-                          (int64_t)(BM * BN);
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        int rr[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) rr[e] = centered_mod(acc[i][j][e], pf, rcp, t16);
-        const int bi = wr * MI + i, bj = wc * NJ + j;
-        *(uint32_t*)(cr + ((bi * (BN / 16) + bj) * 64 + lane) * 4) =
-            pack4(rr[0], rr[1], rr[2], rr[3]);
-        acc[i][j] = v4i{0, 0, 0, 0};
-      }
-  };
-  auto step = [&](int8_t* cur, int8_t* nxt, v4i(&fa)[MI], v4i(&fb)[NJ], v4i(&na)[MI],
-                  v4i(&nbf)[NJ]) __attribute__((always_inline)) {
-    if (after_epi)  // the epilogue's stores are younger than the DMAs this wait is for
-      __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0((STG - 2) * PPW + NM));
-    else
-      __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0((STG - 2) * PPW));
-    after_epi = false;
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int h = 0; h < NM; ++h) {
-      const int i = h / NJ, j = h % NJ;
-      acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (h % GAP == GAP - 1 && h / GAP < NR) {
-        rd_frag(nxt, h / GAP, na, nbf);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (h == NM - 2 * PPW + 1) {  // this step's DMAs (stage + STG) into the freed buffer
-        dma_step(cur);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    dma_advance();
-    if (++mkb == nkb) {
-      epilogue();
-      after_epi = true;
-      mkb = 0;
-      if (mj + 1 < nmine) mi_item = item_of(++mj);
-    }
-  };
-
-  auto buf = [&](int i) { return smem + i * kStageBytes; };
-  int r = 0;
-  for (int64_t S = 0; S < total; S += 2) {
-    step(buf(r), buf(r == STG - 1 ? 0 : r + 1), fa0, fb0, fa1, fb1);
-    r = r == STG - 1 ? 0 : r + 1;
-    if (S + 1 < total) {
-      step(buf(r), buf(r == STG - 1 ? 0 : r + 1), fa1, fb1, fa0, fb0);
-      r = r == STG - 1 ? 0 : r + 1;
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // reconstruction for the 16x16 output layout: one thread = one lane's 4 bytes of a block
@@ -1301,12 +933,13 @@ int crt_kernel() {  // MOOSEX_CRT_KERNEL: 1 = 4 waves of 128x128, 2 = 8 waves of
   // barrier at the start of each k-step and the next stage's fragment reads spread over the
   // step's MFMAs (the default: 4-6 % faster than 6 on the same box, profiles/r3_crt_gemm.md),
   // 9 = 8 with 4 stages, 10 / 11 = 8 / 9 with the DMAs spread over the step too, 12 = 4
-  // with 8's schedule (spills), 13 / 14 = 8 / 12 with buffer-descriptor DMAs (13: slower),
-  // 15 = 8 as a persistent kernel (k_crt_gemm16p, slower), 16 / 17 = 8 with B fragments
-  // read from global memory (k_crt_gemm16g; 3 / 4 A stages)
+  // with 8's schedule (spills).  Tried and removed (profiles/r3_crt_gemm.md): DMAs through
+  // buffer descriptors (16.2 vs 15.5 ms per step), a persistent one-block-per-CU kernel
+  // streaming all its tiles' k-steps (16.2 vs 15.5 ms), B fragments loaded from global
+  // memory straight into registers (hipcc drains every counter before their first use)
   const char* e = std::getenv("MOOSEX_CRT_KERNEL");
   const int v = e ? std::atoi(e) : 8;
-  return v >= 1 && v <= 17 ? v : 8;
+  return v >= 1 && v <= 12 ? v : 8;
 }
 bool crt_mfma16() { return crt_kernel() >= 4; }
 int recon_dot4() {  // MOOSEX_CRT_RECON=0: the multiply-add reconstruction
@@ -1372,17 +1005,16 @@ int dma_mask() {
   return e ? std::atoi(e) : 3;
 }
 
-template <int WR, int WC, int BN, int MINW, bool M16, int STG = kStages, int IL = 0,
-          bool BUF = false>
+template <int WR, int WC, int BN, int MINW, bool M16, int STG = kStages, int IL = 0>
 void launch_variant(const CPlan& p, const Tables& tb, int64_t batch, const int8_t* ra,
                     const int8_t* rb, int8_t* cr, int bcast, int roll, hipStream_t st) {
   constexpr int lds = STG * (kImg + BN * BK);
-  const void* fn = M16 ? (const void*)k_crt_gemm16<WR, WC, BN, MINW, STG, IL, BUF>
+  const void* fn = M16 ? (const void*)k_crt_gemm16<WR, WC, BN, MINW, STG, IL>
                        : (const void*)k_crt_gemm<WR, WC, BN, MINW>;
   ensure_lds_attr(fn, lds, st);
   const dim3 grid((unsigned)(p.tiles_m * p.tiles_n), (unsigned)(batch * p.n));
   if constexpr (M16)
-    hipLaunchKernelGGL((k_crt_gemm16<WR, WC, BN, MINW, STG, IL, BUF>), grid, dim3(64 * WR * WC), lds, st, ra,
+    hipLaunchKernelGGL((k_crt_gemm16<WR, WC, BN, MINW, STG, IL>), grid, dim3(64 * WR * WC), lds, st, ra,
                        rb, cr, (int)p.tiles_m, (int)p.tiles_n, (int)p.nkb, gemm_group_m(), tb.ep,
                        dma_mask(), bcast, (int)p.a_nkb, roll);
   else
@@ -1391,40 +1023,9 @@ void launch_variant(const CPlan& p, const Tables& tb, int64_t batch, const int8_
                        dma_mask(), bcast);
 }
 
-template <int WR, int WC, int BN, int MINW, int STG>
-void launch_persistent(const CPlan& p, const Tables& tb, int64_t batch, const int8_t* ra,
-                       const int8_t* rb, int8_t* cr, int bcast, int roll, hipStream_t st) {
-  constexpr int lds = STG * (kImg + BN * BK);
-  const void* fn = (const void*)k_crt_gemm16p<WR, WC, BN, MINW, STG>;
-  ensure_lds_attr(fn, lds, st);
-  int dev = 0, cus = 256;
-  if (hipStreamGetDevice(st, &dev) != hipSuccess) (void)hipGetDevice(&dev);
-  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const int64_t items = p.tiles_m * p.tiles_n * batch * p.n;
-  const int grid = (int)std::min<int64_t>(items, cus);  // one block per CU (96 KB LDS)
-  hipLaunchKernelGGL((k_crt_gemm16p<WR, WC, BN, MINW, STG>), dim3(grid), dim3(64 * WR * WC), lds,
-                     st, ra, rb, cr, (int)p.tiles_m, (int)p.tiles_n, (int)p.nkb, gemm_group_m(),
-                     tb.ep, bcast, (int)p.a_nkb, roll, (int)(batch * p.n));
-}
-
-template <int WR, int WC, int BN, int MINW, int STG>
-void launch_bglobal(const CPlan& p, const Tables& tb, int64_t batch, const int8_t* ra,
-                    const int8_t* rb, int8_t* cr, int bcast, int roll, hipStream_t st) {
-  constexpr int lds = STG * kImg;
-  const void* fn = (const void*)k_crt_gemm16g<WR, WC, BN, MINW, STG>;
-  ensure_lds_attr(fn, lds, st);
-  const dim3 grid((unsigned)(p.tiles_m * p.tiles_n), (unsigned)(batch * p.n));
-  hipLaunchKernelGGL((k_crt_gemm16g<WR, WC, BN, MINW, STG>), grid, dim3(64 * WR * WC), lds, st,
-                     ra, rb, cr, (int)p.tiles_m, (int)p.tiles_n, (int)p.nkb, gemm_group_m(), tb.ep,
-                     bcast, (int)p.a_nkb, roll);
-}
-
 void launch_crt_gemm(const CPlan& p, const Tables& tb, int64_t batch, const int8_t* ra,
                      const int8_t* rb, int8_t* cr, int bcast, int roll, hipStream_t st) {
   switch (crt_kernel()) {  // roll: 16x16x64 kernels only (run_crt checks)
-    case 16: launch_bglobal<2, 4, 256, 2, 3>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
-    case 17: launch_bglobal<2, 4, 256, 2, 4>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
-    case 15: launch_persistent<2, 4, 256, 2, 3>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
     case 1: launch_variant<2, 2, 256, 1, false>(p, tb, batch, ra, rb, cr, bcast, 0, st); break;
     case 2: launch_variant<2, 4, 256, 2, false>(p, tb, batch, ra, rb, cr, bcast, 0, st); break;
     case 4: launch_variant<2, 2, 256, 1, true>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
@@ -1436,8 +1037,6 @@ void launch_crt_gemm(const CPlan& p, const Tables& tb, int64_t batch, const int8
     case 10: launch_variant<2, 4, 256, 2, true, 3, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
     case 11: launch_variant<2, 4, 256, 2, true, 4, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
     case 12: launch_variant<2, 2, 256, 1, true, 3, 1>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
-    case 13: launch_variant<2, 4, 256, 2, true, 3, 1, true>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
-    case 14: launch_variant<2, 2, 256, 1, true, 3, 1, true>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
     default: launch_variant<2, 2, 128, 2, true>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
   }
 }

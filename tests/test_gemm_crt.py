@@ -318,7 +318,7 @@ def test_gpu_dot_cross_pair_rolled(bits, K):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", ["6", "8", "15"])
+@pytest.mark.parametrize("variant", ["6", "8"])
 def test_gpu_crt_bench_tiling_matches_limb_gemm(variant, monkeypatch):
     """The bench's tile grid: many 256x256 tiles in both directions (GROUPM remap over 8 x 8
     tiles per party and modulus), K' = 8192 (mode 1), Z_2^128 -- bit-exact against the limb
@@ -336,22 +336,3 @@ def test_gpu_crt_bench_tiling_matches_limb_gemm(variant, monkeypatch):
     same(want, got)
     assert rolled is not None
     same(want, rolled)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("bits", [64, 128])
-@pytest.mark.parametrize("shape", [(3, 5, 4), (300, 520, 270), (513, 64, 700)])
-def test_gpu_crt_persistent_kernel_matches_host(bits, shape, monkeypatch):
-    """Variant 15 (persistent: one k-step stream over all of a block's tiles) on partial
-    tiles and on K shorter than the LDS ring (k-step streams that cross tiles in the
-    prologue)."""
-    monkeypatch.setenv("MOOSEX_CRT_KERNEL", "15")
-    M, K, N = shape
-    a, b = rand_rt((2, M, K), bits, 12), rand_rt((2, K, N), bits, 13)
-    xs = [rand_rt((3, M, K), bits, 22 + i) for i in range(2)]
-    ys = [rand_rt((3, K, N), bits, 32 + i) for i in range(2)]
-    with _crt(1):
-        d = R.dot(gpu(a), gpu(b), nb=1)
-        c = R.dot_cross(*[gpu(t) for t in xs + ys], nb=1)
-    same(R.dot(a, b, nb=1), d)
-    same(R.dot_cross(*xs, *ys, nb=1), c)
