@@ -225,7 +225,7 @@ def _preflight(layout, comms, world, rank, device, prog):
     if layout == "cyclic" and world > 1:
         from moose_amd.parallel.cyclic import default_offsets
 
-        off = list(default_offsets(ROLES).values())
+        off = list(default_offsets(ROLES, world).values())
         dists = sorted({(b - a) % world for a in off for b in off} - {0})
         for k, comm in enumerate(comms):
             prog.tick(1 + k)
@@ -415,9 +415,12 @@ def _main(args, prog_out):
     if layout == "spmd":
         n_sessions, out_owner = world // 3, rank % 3 == 2
         xs, ys, out_session = rank // 3, rank // 3, rank // 3
-    elif layout == "cyclic":  # rank g hosts alice of session g, bob of g-1, carole of g-2
+    elif layout == "cyclic":  # rank g hosts role r of session g - o(r) (cyclic.py)
+        from moose_amd.parallel.cyclic import default_offsets
+
+        offsets = default_offsets(ROLES, world)
         n_sessions, out_owner = world, True
-        xs, ys, out_session = rank, (rank - 1) % world, (rank - 2) % world
+        xs, ys, out_session = [(rank - offsets[r]) % world for r in ROLES]
     else:
         n_sessions, out_owner = world, True
         xs, ys, out_session = rank, rank, rank
@@ -451,14 +454,12 @@ def _main(args, prog_out):
     elif layout == "cyclic":
         from moose_amd.parallel.cyclic import CyclicSession
         from moose_amd.parallel.cyclic import RingComm
-        from moose_amd.parallel.cyclic import default_offsets
 
         # one communicator per step stream: RCCL runs the operations of a communicator in
         # issue order, so step k+1's exchanges must not queue behind step k's
         groups = [None] + ([dist.new_group(list(range(world))) for _ in range(nstreams - 1)]
                            if world > 1 else [None] * (nstreams - 1))
         comms = [RingComm(rank, world, device, group=g) for g in groups]
-        offsets = default_offsets(ROLES)
 
         def new_session(k):
             return CyclicSession(comms[k % len(comms)], offsets, device)
@@ -603,7 +604,8 @@ def _main(args, prog_out):
         if gather_bufs is not None and (gather_mode == "all" or rank == root):
             # the last step's collected outputs: rank r's revealed output is session s(r)'s
             buf = gather_bufs[(n_steps[0] - 1) % 2]
-            sess_of = {"cyclic": lambda r: (r - 2) % world, "spmd": lambda r: r // 3,
+            sess_of = {"cyclic": lambda r: (r - offsets[ROLES[2]]) % world,
+                       "spmd": lambda r: r // 3,
                        "stacked": lambda r: r}[layout]
             gerr = 0.0
             for i, r in enumerate(owners):

@@ -2,7 +2,8 @@
 session on its own GPU, every reshare an RCCL send/recv over xGMI.
 
 Placement rule: role ``r`` (offset ``o(r)``: 0, 1, 2 for the three parties of the
-replicated placement, further roles after them) of session ``s`` lives on GPU
+replicated placement -- 0, 1, 3 on >= 4 GPUs, so that every inter-party flow gets its own
+xGMI link (:func:`default_offsets`) -- further roles after them) of session ``s`` lives on GPU
 ``(s + o(r)) mod N``.  So GPU ``g`` hosts role ``r`` of session ``(g - o(r)) mod N`` --
 one instance of EVERY role, each from a different session (for N >= 3):
 
@@ -124,8 +125,44 @@ class RingComm:
             out.copy_(buf, non_blocking=True)
 
 
-def default_offsets(roles: Sequence[str]) -> Dict[str, int]:
-    return {r: i for i, r in enumerate(roles)}
+# Per-step traffic between the three parties of one session of the dot-product program
+# (x owned by party 0, y by party 1, output revealed to party 2), in units of one share
+# tensor of the output: input shares (owner -> its P_{j+2}), the folded dot tail
+# (parallel/party.py: m0, w0 0->1; m1, w1 1->0; z2 2->0 and 2->1; rt1, rm1 2->1) and the
+# reveal (P0 -> P2).
+TRAFFIC = {(0, 1): 2.0, (1, 0): 3.0, (2, 0): 1.0, (2, 1): 2.5, (0, 2): 2.0}
+
+
+def link_loads(offsets: Sequence[int], world: int, traffic=None) -> Dict[int, float]:
+    """Per-GPU traffic on each outgoing link ``g -> g + d`` (key ``d``), for party offsets
+    ``offsets``.  Every GPU runs the same pattern, so link ``d`` of every GPU carries the sum
+    of the flows whose offset difference is ``d`` mod ``world``; ``d = 0`` is a local copy."""
+    load: Dict[int, float] = {}
+    for (a, b), w in (traffic or TRAFFIC).items():
+        d = (offsets[b] - offsets[a]) % world
+        load[d] = load.get(d, 0.0) + w
+    return load
+
+
+def default_offsets(roles: Sequence[str], world: int = None) -> Dict[str, int]:
+    """Offsets of the roles (module doc): 0, 1, 2, ... unless ``world`` GPUs allow a
+    link-balanced choice.
+
+    xGMI is point to point -- every GPU pair has its own link (≈50-64 GB/s per direction
+    under RCCL) -- so the step time of a communication-heavy program is set by the busiest
+    link, not the total volume.  With offsets (0, 1, 2) the flows 1->0 and 2->1 share
+    distance -1 (5.5 of the 10.5 units above on one link); for ``world >= 4`` the offsets
+    of the three parties are chosen to minimise the busiest link, e.g. (0, 1, 3) on 8 GPUs
+    puts every flow on its own link (max 3 units: 1.8x less time on the wire per step).
+    Further roles take the smallest unused offsets."""
+    n = len(roles)
+    off = list(range(n))
+    if world is not None and world >= 4 and n >= 3:
+        cands = [(0, o1, o2) for o1 in range(1, world) for o2 in range(1, world) if o1 != o2]
+        best = min(cands, key=lambda o: (max(link_loads(o, world).values()), o))
+        rest = [k for k in range(max(world, n)) if k not in best]
+        off = list(best) + rest[:n - 3]
+    return {r: o for r, o in zip(roles, off)}
 
 
 class CyclicSession(StackedSession):

@@ -59,14 +59,15 @@ def _program(sess, xb, ya, mb, ma):
     return tensors, (out.v.data.clone(), dt.v.data.clone())
 
 
-def _worker(rank, world, port, q, device="cpu"):
+def _worker(rank, world, port, q, device="cpu", offsets=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from moose_amd.parallel.cyclic import CyclicSession
     from moose_amd.parallel.cyclic import RingComm
     from moose_amd.runtime.session import HV
 
-    sess = CyclicSession(RingComm(rank, world, device), {"a": 0, "b": 1, "c": 2}, seed=SEED,
+    sess = CyclicSession(RingComm(rank, world, device), offsets or {"a": 0, "b": 1, "c": 2},
+                         seed=SEED,
                          device=device, pipeline_chunks=4)
     res = {}
     for bits in (64, 128):
@@ -105,11 +106,11 @@ def _stacked_reference(keys, session):
     return out
 
 
-def _run(world, device):
+def _run(world, device, offsets=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q, device)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, device, offsets)) for r in range(world)]
     for p in ps:
         p.start()
     got = {}
@@ -139,10 +140,11 @@ def _run(world, device):
             ts, out, s_c = res[bits]
             for i, t in enumerate(ts):
                 for p in range(3):
-                    s = (g - p) % world  # component p of rank g = party p of session g - p
+                    # component p of rank g = party p of session g - o(p)
+                    s = (g - (offsets or {}).get("abc"[p], p)) % world
                     ref = refs[(s, bits)][0][i][p].numpy()
                     assert np.array_equal(t[p], ref), (world, g, bits, i, p)
-            # carole's revealed products on rank g are session g - 2's
+            # carole's revealed products on rank g are session g - o(c)'s
             for o, r in zip(out, refs[(s_c, bits)][1]):
                 assert np.array_equal(o, r.numpy())
             x = _data(s_c, bits)
@@ -160,6 +162,19 @@ def _run(world, device):
 @pytest.mark.parametrize("world", [2, 3, 4])
 def test_cyclic_bitwise_equals_stacked(world):
     _run(world, "cpu")
+
+
+def test_cyclic_link_balanced_offsets():
+    """The link-balanced placement bench.py uses on >= 4 GPUs (carole at offset 3, so
+    every inter-party flow of the dot program has its own xGMI link on 8 GPUs)."""
+    from moose_amd.parallel.cyclic import default_offsets
+    from moose_amd.parallel.cyclic import link_loads
+
+    off = default_offsets(("a", "b", "c"), 4)
+    assert off == {"a": 0, "b": 1, "c": 3}
+    assert max(link_loads((0, 1, 3), 8).values()) == 3.0 < max(link_loads((0, 1, 2), 8).values())
+    assert default_offsets(("a", "b", "c"), 2) == {"a": 0, "b": 1, "c": 2}
+    _run(4, "cpu", off)
 
 
 @pytest.mark.gpu
