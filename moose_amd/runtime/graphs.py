@@ -197,7 +197,6 @@ class GraphPlan:
         torch.cuda.synchronize(self.device)
         self._stager = stager  # keep the staged constants alive
         self.replays = 0
-        self._pinned = {}
         self.t_graph, self.t_eager = [], []
         self._warm = False
         self.decision = "graph" if PROBES <= 0 else None
@@ -231,14 +230,11 @@ class GraphPlan:
             if isinstance(t, torch.Tensor):
                 a = np.asarray(v)
                 a = a.view(np.int64) if a.dtype == np.uint64 else a
-                # stage through a pinned buffer: an asynchronous DMA on the replay stream
-                # instead of a pageable (bounce-buffered, host-blocking) copy per argument
-                pin = self._pinned.get(k)
-                if pin is None or pin.shape != t.shape or pin.dtype != t.dtype:
-                    pin = self._pinned[k] = torch.empty(t.shape, dtype=t.dtype,
-                                                        pin_memory=True)
-                np.copyto(pin.numpy(), a.reshape(pin.shape), casting="same_kind")
-                t.copy_(pin, non_blocking=True)
+                # a pageable copy straight from the caller's array, as the eager path does:
+                # HIP's staged DMA (0.155 ms for 8 MB on MI355X) beats a host memcpy into a
+                # pinned buffer followed by a blit (0.321 ms; profiles/r3_graphs_vs_eager.md)
+                src = torch.from_numpy(np.ascontiguousarray(a).reshape(t.shape))
+                t.copy_(src if src.dtype == t.dtype else src.to(t.dtype))
         self.keys.refresh()  # fresh randomness for this replay
         for g in self.graphs:
             g.replay()
@@ -246,18 +242,19 @@ class GraphPlan:
         return self._decode(self.interp, self.outs)
 
 
-PROBES = int(os.environ.get("MOOSEX_GRAPHS_PROBES", "3"))
+PROBES = int(os.environ.get("MOOSEX_GRAPHS_PROBES", "0"))
 
 
 class GraphCache:
     """Per-runtime cache of captured plans keyed by (computation, argument signature).
 
-    Adaptive replay: a replay only pays where an evaluation is bound by host dispatch; at
-    sizes where the GPU work dominates, HIP's graph dispatch can be slower than the eager
-    stream (profiles/r3_graphs_vs_eager.md).  So after the capture each plan times
-    ``PROBES`` replays and ``PROBES`` eager evaluations (the caller runs those and reports
-    them through :meth:`note_eager`) and then keeps the faster mode by median
-    (``MOOSEX_GRAPHS_PROBES=0``: always replay)."""
+    Replay is the default on every shape (``MOOSEX_GRAPHS_PROBES=0``): with arguments
+    uploaded the way the eager path uploads them, a replay is never slower than the eager
+    evaluation on the reference dot sweep (profiles/r3_graphs_vs_eager.md).  Adaptive mode
+    (``MOOSEX_GRAPHS_PROBES=k > 0``): after the capture a plan times ``k`` replays and ``k``
+    eager evaluations, alternating (the caller runs the eager ones and reports them through
+    :meth:`note_eager`), and keeps the faster mode by median -- a guard for programs whose
+    device work dwarfs dispatch, at the price of decisions made on a few noisy samples."""
 
     def __init__(self):
         self.plans = {}

@@ -7,9 +7,9 @@ mkdir -p gpurun_out
 rm -f gpurun_out/g_*.jsonl
 for c in "seq 1 1000" "parallel 1 1000" "seq 10 1000" "parallel 10 100" "seq 1 1"; do
   set -- $c
-  timeout -k 10 300 python benchmarks/dot_product.py --c $1 --c_arg $2 --s $3 --n 5 --json gpurun_out/g_eager.jsonl > /dev/null 2>&1 || exit 1
-  MOOSEX_GRAPHS_PROBES=0 timeout -k 10 300 python benchmarks/dot_product.py --graphs --c $1 --c_arg $2 --s $3 --n 5 --json gpurun_out/g_forced.jsonl > /dev/null 2>&1 || exit 1
-  timeout -k 10 300 python benchmarks/dot_product.py --graphs --c $1 --c_arg $2 --s $3 --n 5 --json gpurun_out/g_adaptive.jsonl > /dev/null 2>&1 || exit 1
+  timeout -k 10 300 python benchmarks/dot_product.py --c $1 --c_arg $2 --s $3 --n 20 --json gpurun_out/g_eager.jsonl > /dev/null 2>&1 || exit 1
+  MOOSEX_GRAPHS_PROBES=0 timeout -k 10 300 python benchmarks/dot_product.py --graphs --c $1 --c_arg $2 --s $3 --n 20 --json gpurun_out/g_forced.jsonl > /dev/null 2>&1 || exit 1
+  timeout -k 10 300 python benchmarks/dot_product.py --graphs --c $1 --c_arg $2 --s $3 --n 20 --json gpurun_out/g_adaptive.jsonl > /dev/null 2>&1 || exit 1
 done
 python - <<'PY'
 import json

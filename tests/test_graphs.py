@@ -43,9 +43,10 @@ def test_stager_rejects_data_dependent_uploads():
 
 
 @pytest.mark.parametrize("t_graph,t_eager,want", [(1.0, 2.0, "graph"), (3.0, 2.0, "eager")])
-def test_adaptive_replay_keeps_the_faster_mode(t_graph, t_eager, want):
-    """After the capture a plan times PROBES replays and PROBES eager evaluations, then
-    keeps the faster mode (graphs never lose to eager on a plan)."""
+def test_adaptive_replay_keeps_the_faster_mode(monkeypatch, t_graph, t_eager, want):
+    """Adaptive mode (MOOSEX_GRAPHS_PROBES=k): after the capture a plan times k replays and
+    k eager evaluations, then keeps the faster mode."""
+    monkeypatch.setattr(graphs, "PROBES", 3)
     plan = graphs.GraphPlan.__new__(graphs.GraphPlan)
     plan.t_graph, plan.t_eager, plan.decision, plan._warm = [], [], None, False
     seen = []
