@@ -94,6 +94,7 @@ class Progress:
         self.deadline = time.monotonic() + budget_s
         self.t0 = time.monotonic()
         self._lock = threading.Lock()
+        self._wlock = threading.Lock()
         self._fired = False
         self._write()
         t = threading.Thread(target=self._watch, name="bench-watchdog", daemon=True)
@@ -121,22 +122,26 @@ class Progress:
             self.deadline = float("inf")
 
     def _write(self):
-        rec = {"phase": self.phase_name, "seq": self.seq, "step": self.step,
-               "pid": os.getpid(), "t": round(time.monotonic() - self.t0, 3)}
-        self._written = (self.seq, self.step)
-        tmp = os.path.join(self.dir, f".rank{self.rank}.tmp")
-        with open(tmp, "w") as f:
-            json.dump(rec, f)
-        os.replace(tmp, os.path.join(self.dir, f"rank{self.rank}.json"))
+        # the main thread (phase entry) and the watchdog thread (tick publication) both
+        # write: one at a time, or one's rename finds the other's temp file gone
+        with self._wlock:
+            rec = {"phase": self.phase_name, "seq": self.seq, "step": self.step,
+                   "pid": os.getpid(), "t": round(time.monotonic() - self.t0, 3)}
+            self._written = (self.seq, self.step)
+            tmp = os.path.join(self.dir, f".rank{self.rank}.tmp")
+            try:
+                with open(tmp, "w") as f:
+                    json.dump(rec, f)
+                os.replace(tmp, os.path.join(self.dir, f"rank{self.rank}.json"))
+            except OSError as e:  # a phase record is diagnostics: never fail the run on it
+                print(f"[bench] rank {self.rank}: phase record not written: {e}",
+                      file=sys.stderr, flush=True)
 
     def _watch(self):
         while True:
             time.sleep(0.5)
             if (self.seq, self.step) != getattr(self, "_written", None):
-                try:
-                    self._write()
-                except OSError:
-                    pass
+                self._write()
             with self._lock:
                 late = time.monotonic() > self.deadline and not self._fired
                 if late:
