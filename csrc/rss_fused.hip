@@ -106,24 +106,23 @@ template <class T>
 __global__ void __launch_bounds__(256) k_share3(int kind, const T* __restrict__ x, T* __restrict__ out0,
                          T* __restrict__ out1, int64_t n, int j0, mxd::KeySrc keys, uint64_t n1,
                          uint64_t na) {
-  __shared__ uint32_t rks[2][mxd::kKeyWords];
-  mxd::stage_keys(rks, keys, 2);
+  __shared__ uint32_t rks[1][mxd::kKeyWords];
+  mxd::stage_keys(rks, keys, 1);
   constexpr int P = mxd::Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;
-  const uint32_t* const key[2] = {rks[0], rks[1]};
-  const uint64_t nonce[2] = {n1, na};
-  mxd::walk_chunks<2>(nb, key, nonce, [&](int64_t b, const uint64_t (&lo)[2], const uint64_t (&hi)[2]) {
+  const uint32_t* const key[1] = {rks[0]};
+  const uint64_t nonce[1] = {n1};
+  mxd::walk_chunks<1>(nb, key, nonce, [&](int64_t b, const uint64_t (&lo)[1], const uint64_t (&hi)[1]) {
 #pragma unroll
     for (int j = 0; j < P; ++j) {
       const int64_t i = b * P + j;
       if (i >= n) break;
       const T r1 = mxd::pick<T>(lo[0], hi[0], j);
-      const T ra = mxd::pick<T>(lo[1], hi[1], j);
-      const T xj = kind == MX_CROSS_BOOL ? (T)(x[i] ^ r1 ^ ra) : (T)(x[i] - r1 - ra);
+      const T xj = kind == MX_CROSS_BOOL ? (T)(x[i] ^ r1) : (T)(x[i] - r1);
       T slot[3];
       slot[j0] = xj;
       slot[(j0 + 1) % 3] = r1;
-      slot[(j0 + 2) % 3] = ra;
+      slot[(j0 + 2) % 3] = 0;
       const bool ring4 = out1 == out0 + n;  // 4-slot ring: out1's slots 0, 1 are out0's 1, 2
 #pragma unroll
       for (int p = 0; p < 3; ++p) {

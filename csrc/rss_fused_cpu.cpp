@@ -67,22 +67,21 @@ int trunc3_host(const T* s0, T* out0, T* out1, int64_t n, int m, const uint8_t* 
 
 template <class T>
 int share3_host(int kind, const T* x, T* out0, T* out1, int64_t n, int j, const uint8_t* kn,
-                const uint8_t* ka, uint64_t n1, uint64_t na) {
+                const uint8_t* /*ka: unused*/, uint64_t n1, uint64_t /*na: unused*/) {
   const int words = sizeof(T) == 1 ? 0 : (int)(sizeof(T) / 8);
   mx_cpu_parallel_for(n, 1 << 12, [&](int64_t s, int64_t e) {
     const int64_t CH = 512;
-    std::vector<T> r1(CH), ra(CH);
+    std::vector<T> r1(CH);
     for (int64_t c = s; c < e; c += CH) {
       int64_t len = std::min(CH, e - c);
       mx_cpu_prf_range(kn, n1, words, c, len, r1.data());
-      mx_cpu_prf_range(ka, na, words, c, len, ra.data());
       for (int64_t t = 0; t < len; ++t) {
         int64_t i = c + t;
-        T xj = kind == MX_CROSS_BOOL ? (T)(x[i] ^ r1[t] ^ ra[t]) : (T)(x[i] - r1[t] - ra[t]);
+        T xj = kind == MX_CROSS_BOOL ? (T)(x[i] ^ r1[t]) : (T)(x[i] - r1[t]);
         T slot[3];
         slot[j] = xj;
         slot[(j + 1) % 3] = r1[t];
-        slot[(j + 2) % 3] = ra[t];
+        slot[(j + 2) % 3] = 0;
         for (int p = 0; p < 3; ++p) {
           out0[p * n + i] = slot[p];
           out1[p * n + i] = slot[(p + 1) % 3];

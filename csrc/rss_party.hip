@@ -193,7 +193,9 @@ __global__ void __launch_bounds__(256)
     k_share_party(int kind, int64_t n, Roles rel, const T* __restrict__ x, T* __restrict__ out0,
                   T* __restrict__ out1, mxd::KeySrc keys, uint64_t n1, uint64_t na, int ncomp) {
   __shared__ uint32_t rks[mxd::kMaxKeySlots][mxd::kKeyWords];
-  // keys: 2 per component: rel 0 -> (next, all), rel 1 -> (own, all), rel 2 -> (all, all)
+  // keys: 2 per component, the first used: rel 0 -> next, rel 1 -> own (k_{j+1} of the owner
+  // j); slot j+2 of the sharing is zero (reference replicated/convert.rs:74-90), so rel 2
+  // draws nothing
   mxd::stage_keys(rks, keys, 2 * ncomp);
   constexpr int P = mxd::Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;
@@ -207,33 +209,30 @@ __global__ void __launch_bounds__(256)
     const int r = code & 3, fwd = (code >> 2) - 1;
     const int64_t base = (int64_t)c * n;
     if (r > 2) continue;
-    uint32_t wa[16], wb[16];
+    uint32_t wa[16];
     if (r != 2) mx::chacha_block(rks[2 * c], n1, B, wa);
-    mx::chacha_block(rks[2 * c + 1], na, B, wb);
 #pragma unroll
     for (int part = 0; part < 4; ++part) {
       const int64_t b = (int64_t)mx::ks_chunk(B, part);
       if (b >= nb) break;
-      uint64_t al = 0, ah = 0, bl, bh;
+      uint64_t al = 0, ah = 0;
       if (r != 2) mx::part_u64(wa, part, &al, &ah);
-      mx::part_u64(wb, part, &bl, &bh);
 #pragma unroll
       for (int j = 0; j < P; ++j) {
         const int64_t i = b * P + j;
         if (i >= n) break;
-        const T ra = mxd::pick<T>(bl, bh, j);
         if (r == 2) {
-          out0[base + i] = ra;  // s1 arrives from the owner
+          out0[base + i] = 0;  // slot j+2 is zero; s1 arrives from the owner
         } else {
           const T r1 = mxd::pick<T>(al, ah, j);
           if (r == 0) {
-            const T v = kind == MX_CROSS_BOOL ? (T)(x[i] ^ r1 ^ ra) : (T)(x[i] - r1 - ra);
+            const T v = kind == MX_CROSS_BOOL ? (T)(x[i] ^ r1) : (T)(x[i] - r1);
             out0[base + i] = v;
             out1[base + i] = r1;
             if (fwd >= 0) out1[(int64_t)fwd * n + i] = v;
           } else {
             out0[base + i] = r1;
-            out1[base + i] = ra;
+            out1[base + i] = 0;
           }
         }
       }

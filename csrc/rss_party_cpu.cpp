@@ -136,7 +136,7 @@ int trunc_r1(int64_t n, int m, int ncomp, const int* roles, const T* msg, const 
 
 template <class T>
 int share_party(int kind, int64_t n, int ncomp, const int* rel, const T* x, T* out0, T* out1,
-                const uint32_t* const* slots, uint64_t n1, uint64_t na) {
+                const uint32_t* const* slots, uint64_t n1, uint64_t /*na: unused*/) {
   for (int c = 0; c < ncomp; ++c) {
     const int code = rel[c];  // as k_share_party: role + 4 * (1 + local P_{j+2} component)
     if (code < 0) continue;
@@ -144,21 +144,20 @@ int share_party(int kind, int64_t n, int ncomp, const int* rel, const T* x, T* o
     const int64_t base = (int64_t)c * n;
     if (r > 2) continue;
     for_chunks<T>(n, [&](int64_t i0, int64_t len) {
-      std::vector<T> a(len), b(len);
-      prf<T>(slots[2 * c + 1], na, i0, len, b.data());
+      std::vector<T> a(len);
       if (r != 2) prf<T>(slots[2 * c], n1, i0, len, a.data());
       for (int64_t q = 0; q < len; ++q) {
         const int64_t i = base + i0 + q;
         if (r == 2) {
-          out0[i] = b[q];
+          out0[i] = 0;  // slot j+2 is zero; s1 arrives from the owner
         } else if (r == 0) {
           const T xv = x[i0 + q];
-          out0[i] = kind == MX_CROSS_BOOL ? (T)(xv ^ a[q] ^ b[q]) : (T)(xv - a[q] - b[q]);
+          out0[i] = kind == MX_CROSS_BOOL ? (T)(xv ^ a[q]) : (T)(xv - a[q]);
           out1[i] = a[q];
           if (fwd >= 0) out1[(int64_t)fwd * n + i0 + q] = out0[i];
         } else {
           out0[i] = a[q];
-          out1[i] = b[q];
+          out1[i] = 0;
         }
       }
     });

@@ -5,7 +5,9 @@ holds (x_p, x_{p+1}).  A :class:`RepTensor` keeps the two party vectors ``s0`` (
 party p) and ``s1`` (x_{p+1} at party p); ``s1`` is ``s0`` shifted by one party.
 
 Correlated randomness: party p holds PRF keys k_p and k_{p+1} (so slot s can be sampled
-by exactly the two parties holding slot s) and one key k_all common to all three.
+by exactly the two parties holding slot s) and one key k_all common to all three (kept in
+the setup; input sharing no longer draws from it: its third slot is zero, as the
+reference's).
 
 Parity with the reference (``moose/src/replicated``):
 
@@ -87,15 +89,15 @@ def share(sess, plc, x: HV, kind="arith") -> RepTensor:
         if party is not None and bits in (64, 128):
             s0, s1 = party(plc, x, j, kind, n1, na)
             return RepTensor(plc, bits, kind, s0, s1)
-        # slot_{j+1} = PRF(k_{j+1}) [P_j, P_{j+1}]; slot_{j+2} = PRF(k_all); slot_j = rest
+        # slot_{j+1} = PRF(k_{j+1}) [P_j, P_{j+1}]; slot_{j+2} = 0; slot_j = x - slot_{j+1}
+        # [P_j, sent to P_{j+2}].  As the reference (replicated/convert.rs:74-90), one slot
+        # of an input sharing is zero: each single party still misses one random slot
         r1_j = sess.h_prf(plc, o[j], j1, shape, bits, n1)
         r1_j1 = sess.h_prf(plc, o[j1], j1, shape, bits, n1)
-        ra_j = sess.h_prf(plc, o[j], "all", shape, bits, na)
-        ra_j1 = sess.h_prf(plc, o[j1], "all", shape, bits, na)
-        ra_j2 = sess.h_prf(plc, o[j2], "all", shape, bits, na)
-        xj = sess.h(sub, o[j], sess.h(sub, o[j], x, r1_j), ra_j)
-        comp0 = {j: xj, j1: r1_j1, j2: ra_j2}
-        comp1 = {j: r1_j, j1: ra_j1, j2: sess.move(xj, o[j2])}
+        xj = sess.h(sub, o[j], x, r1_j)
+        comp0 = {j: xj, j1: r1_j1, j2: sess.h("Fill", o[j2], shape, value=0, bits=bits)}
+        comp1 = {j: r1_j, j1: sess.h("Fill", o[j1], shape, value=0, bits=bits),
+                 j2: sess.move(xj, o[j2])}
         s0 = sess.gather(plc, [comp0[i] for i in range(3)])
         s1 = sess.gather(plc, [comp1[i] for i in range(3)])
         return RepTensor(plc, bits, kind, s0, s1)
