@@ -179,9 +179,10 @@ int dot_tail_r0(int64_t n, int m, int ncomp, const int* roles, const void* const
     const T* x = (const T*)cross[c];
     T* mo = (T*)msg[c];
     for_chunks<T>(n, [&](int64_t i0, int64_t len) {
-      std::vector<T> a(len), b(len), r(len);
-      prf<T>(own, nn[0], i0, len, a.data());
-      prf<T>(nxt, nn[0], i0, len, b.data());
+      // zero share: P0 f(k0), P1 -f(k2), P2 f(k2) - f(k0) (rss_party.hip)
+      std::vector<T> a(len, (T)0), b(len, (T)0), r(len);
+      if (role != 1) prf<T>(own, nn[0], i0, len, a.data());
+      if (role != 0) prf<T>(nxt, nn[0], i0, len, b.data());
       if (role == 0) prf<T>(own, nn[1], i0, len, r.data());
       if (role == 1) prf<T>(nxt, nn[2], i0, len, r.data());
       for (int64_t q = 0; q < len; ++q) {
