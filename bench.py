@@ -17,7 +17,10 @@ evaluations (share -> predict -> reveal) on rank 0's GPU, eager and hipGraph rep
 with >= 3 GPUs also one party per GPU (SPMD over RCCL).  Measured after the timed matmul
 steps, outside their timed region.
 
-Layouts (``--layout``; default ``auto`` = stacked on 1 GPU, cyclic on N > 1):
+Layouts (``--layout``; default ``auto`` = stacked on 1 and 2 GPUs, cyclic on N >= 3: with
+two GPUs the three parties of a session cannot sit on three different GPUs, so the cyclic
+layout would only add xGMI traffic -- 7.5 share-tensor units per GPU and step on its one
+link -- without separating the parties):
 
 * ``stacked`` -- one 3-party session per GPU, all three parties' local work batched into
   one kernel per protocol step; N GPUs = N data-parallel session replicas.
@@ -401,7 +404,7 @@ def _main(args, prog_out):
 
     layout = args.layout
     if layout == "auto":
-        layout = "stacked" if world == 1 else "cyclic"
+        layout = "stacked" if world < 3 else "cyclic"
     if layout == "spmd" and (world < 3 or world % 3):
         raise SystemExit("--layout spmd needs a multiple of 3 GPUs (one per party)")
     nstreams = args.step_streams
@@ -563,7 +566,8 @@ def _main(args, prog_out):
     value = n_sessions * n * n * args.steps / elapsed
 
     parallelism = {
-        "stacked": f"dp{world} (one stacked 3-party session per GPU, no inter-GPU reshare)",
+        "stacked": f"dp{world} (one stacked 3-party session per GPU, no inter-GPU reshare"
+                   + ("; 3 parties cannot sit on 3 distinct GPUs with 2)" if world == 2 else ")"),
         "cyclic": (f"{n_sessions} 3-party sessions on {world} GPUs, each party on its own "
                    "GPU (cyclic layout): every reshare an RCCL send/recv" if world > 1 else
                    "1 stacked 3-party session"),

@@ -52,12 +52,13 @@ def _run_self(n, *extra):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("n,layout,sessions", [(2, "auto", 2), (3, "spmd", 1), (4, "cyclic", 4)])
+@pytest.mark.parametrize("n,layout,sessions", [(2, "auto", 2), (3, "spmd", 1), (4, "cyclic", 4),
+                                               (3, "auto", 3)])
 def test_bench_self_launch(n, layout, sessions):
     d = _run_self(n, "--layout", layout)
     assert FIELDS <= set(d)
     assert d["n_gpus"] == n and d["world_size"] == n and d["sessions"] == sessions
-    assert d["layout"] == ("cyclic" if layout == "auto" else layout)
+    assert d["layout"] == ({2: "stacked"}.get(n, "cyclic") if layout == "auto" else layout)
     assert len(d["per_rank_ms_per_step"]) == n
     assert d["ms_per_step"] == pytest.approx(max(d["per_rank_ms_per_step"]))
     # every output owner checked its last output (and rank 0 the collected outputs)
