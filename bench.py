@@ -19,7 +19,7 @@ steps, outside their timed region.
 
 Layouts (``--layout``; default ``auto`` = stacked on 1 and 2 GPUs, cyclic on N >= 3: with
 two GPUs the three parties of a session cannot sit on three different GPUs, so the cyclic
-layout would only add xGMI traffic -- 7.5 share-tensor units per GPU and step on its one
+layout would only add xGMI traffic -- 8.5 share-tensor units per GPU and step on its one
 link -- without separating the parties):
 
 * ``stacked`` -- one 3-party session per GPU, all three parties' local work batched into

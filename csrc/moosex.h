@@ -177,8 +177,9 @@ int mx_crt_tables(int words, int n, int32_t* p, uint8_t* wa, uint8_t* wb, int32_
 // trunc_pr3 nonces: r0, r1, r_top, r_msb, z0, z2 (dealer keys k0, k2).
 int mx_trunc_pr3(int dev, int words, const void* s0, void* out0, void* out1, int64_t n, int m,
                  const uint8_t* k0, const uint8_t* k2, const uint64_t* nonces, void* stream);
-// share3: owner party j; slot_{j+1} = PRF(k_next, n1), slot_{j+2} = 0, slot_j = x - slot_{j+1}
-// (reference replicated/convert.rs:74-90); k_all / na are not read (kept for the ABI).
+// share3: owner party j; slot_j = PRF(k_j, n1) (k_j: held by P_j and P_{j+2}), slot_{j+1} =
+// x - slot_j (sent to P_{j+1}), slot_{j+2} = 0 (reference replicated/convert.rs:74-90).
+// The key argument is k_j; k_all / na are not read (kept for the ABI).
 int mx_share3(int dev, int kind, int words, const void* x, void* out0, void* out1, int64_t n,
               int j, const uint8_t* k_next, const uint8_t* k_all, uint64_t n1, uint64_t na,
               void* stream);

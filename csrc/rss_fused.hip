@@ -117,11 +117,10 @@ __global__ void __launch_bounds__(256) k_share3(int kind, const T* __restrict__ 
     for (int j = 0; j < P; ++j) {
       const int64_t i = b * P + j;
       if (i >= n) break;
-      const T r1 = mxd::pick<T>(lo[0], hi[0], j);
-      const T xj = kind == MX_CROSS_BOOL ? (T)(x[i] ^ r1) : (T)(x[i] - r1);
+      const T r = mxd::pick<T>(lo[0], hi[0], j);
       T slot[3];
-      slot[j0] = xj;
-      slot[(j0 + 1) % 3] = r1;
+      slot[j0] = r;
+      slot[(j0 + 1) % 3] = kind == MX_CROSS_BOOL ? (T)(x[i] ^ r) : (T)(x[i] - r);
       slot[(j0 + 2) % 3] = 0;
       const bool ring4 = out1 == out0 + n;  // 4-slot ring: out1's slots 0, 1 are out0's 1, 2
 #pragma unroll

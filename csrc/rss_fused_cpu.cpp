@@ -77,10 +77,9 @@ int share3_host(int kind, const T* x, T* out0, T* out1, int64_t n, int j, const 
       mx_cpu_prf_range(kn, n1, words, c, len, r1.data());
       for (int64_t t = 0; t < len; ++t) {
         int64_t i = c + t;
-        T xj = kind == MX_CROSS_BOOL ? (T)(x[i] ^ r1[t]) : (T)(x[i] - r1[t]);
         T slot[3];
-        slot[j] = xj;
-        slot[(j + 1) % 3] = r1[t];
+        slot[j] = r1[t];
+        slot[(j + 1) % 3] = kind == MX_CROSS_BOOL ? (T)(x[i] ^ r1[t]) : (T)(x[i] - r1[t]);
         slot[(j + 2) % 3] = 0;
         for (int p = 0; p < 3; ++p) {
           out0[p * n + i] = slot[p];

@@ -193,47 +193,45 @@ __global__ void __launch_bounds__(256)
     k_share_party(int kind, int64_t n, Roles rel, const T* __restrict__ x, T* __restrict__ out0,
                   T* __restrict__ out1, mxd::KeySrc keys, uint64_t n1, uint64_t na, int ncomp) {
   __shared__ uint32_t rks[mxd::kMaxKeySlots][mxd::kKeyWords];
-  // keys: 2 per component, the first used: rel 0 -> next, rel 1 -> own (k_{j+1} of the owner
-  // j); slot j+2 of the sharing is zero (reference replicated/convert.rs:74-90), so rel 2
-  // draws nothing
+  // keys: 2 per component, the first used: k_j of the owner j (rel 0: own, rel 2: next).
+  // As the reference (replicated/convert.rs:74-90): slot j = PRF(k_j), slot j+1 = x - slot j
+  // (sent to P_{j+1}), slot j+2 = 0, so rel 1 draws nothing
   mxd::stage_keys(rks, keys, 2 * ncomp);
   constexpr int P = mxd::Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;
   MX_PARTY_WALK(nb, ncomp) {
     const int c = (int)(g / nblk);
     const uint64_t B = (uint64_t)(g - c * nblk);
-    // rel code: the role relative to the owner (0..2) + 4 * (1 + the component of P_{j+2})
-    // when the owner's masked share stays on this device (written straight into its s1)
+    // rel code: the role relative to the owner (0..2) + 4 * (1 + the component of P_{j+1})
+    // when the owner's masked share stays on this device (written straight into its s0)
     const int code = rel.r[c];
     if (code < 0) continue;
     const int r = code & 3, fwd = (code >> 2) - 1;
     const int64_t base = (int64_t)c * n;
     if (r > 2) continue;
     uint32_t wa[16];
-    if (r != 2) mx::chacha_block(rks[2 * c], n1, B, wa);
+    if (r != 1) mx::chacha_block(rks[2 * c], n1, B, wa);
 #pragma unroll
     for (int part = 0; part < 4; ++part) {
       const int64_t b = (int64_t)mx::ks_chunk(B, part);
       if (b >= nb) break;
       uint64_t al = 0, ah = 0;
-      if (r != 2) mx::part_u64(wa, part, &al, &ah);
+      if (r != 1) mx::part_u64(wa, part, &al, &ah);
 #pragma unroll
       for (int j = 0; j < P; ++j) {
         const int64_t i = b * P + j;
         if (i >= n) break;
-        if (r == 2) {
-          out0[base + i] = 0;  // slot j+2 is zero; s1 arrives from the owner
-        } else {
-          const T r1 = mxd::pick<T>(al, ah, j);
-          if (r == 0) {
-            const T v = kind == MX_CROSS_BOOL ? (T)(x[i] ^ r1) : (T)(x[i] - r1);
-            out0[base + i] = v;
-            out1[base + i] = r1;
-            if (fwd >= 0) out1[(int64_t)fwd * n + i] = v;
-          } else {
-            out0[base + i] = r1;
-            out1[base + i] = 0;
-          }
+        const T rr = mxd::pick<T>(al, ah, j);
+        if (r == 0) {  // owner: (slot j, slot j+1) = (PRF(k_j), x - PRF(k_j))
+          const T v = kind == MX_CROSS_BOOL ? (T)(x[i] ^ rr) : (T)(x[i] - rr);
+          out0[base + i] = rr;
+          out1[base + i] = v;
+          if (fwd >= 0) out0[(int64_t)fwd * n + i] = v;
+        } else if (r == 1) {  // P_{j+1}: s0 arrives from the owner, slot j+2 is zero
+          out1[base + i] = 0;
+        } else {  // P_{j+2}: (0, PRF(k_j))
+          out0[base + i] = 0;
+          out1[base + i] = rr;
         }
       }
     }

@@ -138,26 +138,26 @@ template <class T>
 int share_party(int kind, int64_t n, int ncomp, const int* rel, const T* x, T* out0, T* out1,
                 const uint32_t* const* slots, uint64_t n1, uint64_t /*na: unused*/) {
   for (int c = 0; c < ncomp; ++c) {
-    const int code = rel[c];  // as k_share_party: role + 4 * (1 + local P_{j+2} component)
+    const int code = rel[c];  // as k_share_party: role + 4 * (1 + local P_{j+1} component)
     if (code < 0) continue;
     const int r = code & 3, fwd = (code >> 2) - 1;
     const int64_t base = (int64_t)c * n;
     if (r > 2) continue;
     for_chunks<T>(n, [&](int64_t i0, int64_t len) {
       std::vector<T> a(len);
-      if (r != 2) prf<T>(slots[2 * c], n1, i0, len, a.data());
+      if (r != 1) prf<T>(slots[2 * c], n1, i0, len, a.data());
       for (int64_t q = 0; q < len; ++q) {
         const int64_t i = base + i0 + q;
-        if (r == 2) {
-          out0[i] = 0;  // slot j+2 is zero; s1 arrives from the owner
-        } else if (r == 0) {
+        if (r == 0) {
           const T xv = x[i0 + q];
-          out0[i] = kind == MX_CROSS_BOOL ? (T)(xv ^ a[q]) : (T)(xv - a[q]);
-          out1[i] = a[q];
-          if (fwd >= 0) out1[(int64_t)fwd * n + i0 + q] = out0[i];
-        } else {
           out0[i] = a[q];
-          out1[i] = 0;
+          out1[i] = kind == MX_CROSS_BOOL ? (T)(xv ^ a[q]) : (T)(xv - a[q]);
+          if (fwd >= 0) out0[(int64_t)fwd * n + i0 + q] = out1[i];
+        } else if (r == 1) {
+          out1[i] = 0;  // s0 arrives from the owner
+        } else {
+          out0[i] = 0;
+          out1[i] = a[q];
         }
       }
     });

@@ -1431,8 +1431,8 @@ def trunc_party_r1(msg, rmk, rrt, rrm, out0, out1, bits, m, roles, slots, nonces
 
 
 def share_party(kind: str, x: RT, ncomp: int, rel, slots, n1: int, na: int):
-    """Per-component slots of a sharing by member j (mx_share_party); the owner's out0
-    is the message to P_{j+2} (whose out1 it becomes)."""
+    """Per-component slots of a sharing by member j (mx_share_party); the owner's out1
+    (slot x_{j+1}) is the message to P_{j+1} (whose out0 it becomes)."""
     xd = x.data.contiguous()
     shape = (ncomp,) + tuple(xd.shape)
     out0 = torch.empty(shape, dtype=xd.dtype, device=xd.device)

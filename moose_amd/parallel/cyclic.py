@@ -127,10 +127,10 @@ class RingComm:
 
 # Per-step traffic between the three parties of one session of the dot-product program
 # (x owned by party 0, y by party 1, output revealed to party 2), in units of one share
-# tensor of the output: input shares (owner -> its P_{j+2}), the folded dot tail
+# tensor of the output: input shares (owner j -> P_{j+1}), the folded dot tail
 # (parallel/party.py: m0, w0 0->1; m1, w1 1->0; z2 2->0 and 2->1; rt1, rm1 2->1) and the
 # reveal (P0 -> P2).
-TRAFFIC = {(0, 1): 2.0, (1, 0): 3.0, (2, 0): 1.0, (2, 1): 2.5, (0, 2): 2.0}
+TRAFFIC = {(0, 1): 3.0, (1, 0): 2.0, (2, 0): 1.0, (2, 1): 2.5, (0, 2): 1.0, (1, 2): 1.0}
 
 
 def link_loads(offsets: Sequence[int], world: int, traffic=None) -> Dict[int, float]:
@@ -150,10 +150,11 @@ def default_offsets(roles: Sequence[str], world: int = None) -> Dict[str, int]:
 
     xGMI is point to point -- every GPU pair has its own link (≈50-64 GB/s per direction
     under RCCL) -- so the step time of a communication-heavy program is set by the busiest
-    link, not the total volume.  With offsets (0, 1, 2) the flows 1->0 and 2->1 share
-    distance -1 (5.5 of the 10.5 units above on one link); for ``world >= 4`` the offsets
-    of the three parties are chosen to minimise the busiest link, e.g. (0, 1, 3) on 8 GPUs
-    puts every flow on its own link (max 3 units: 1.8x less time on the wire per step).
+    link, not the total volume.  With offsets (0, 1, 2) the flows 0->1 and 1->2 share
+    distance +1 and 1->0 and 2->1 distance -1 (4.5 of the 10.5 units above on one link);
+    for ``world >= 4`` the offsets of the three parties are chosen to minimise the busiest
+    link, e.g. (0, 1, 3) on 8 GPUs puts every flow on its own link (max 3 units: 1.5x less
+    time on the wire per step), on 4 GPUs 4 units instead of 4.5.
     Further roles take the smallest unused offsets."""
     n = len(roles)
     off = list(range(n))
@@ -373,23 +374,23 @@ class CyclicSession(StackedSession):
 
     def party_share(self, plc, x, j, kind, n1, na):
         """Input sharing by member j: one kernel for every component's slots, then the
-        owner's masked x_j goes to P_{j+2} (received straight into its s1)."""
+        owner's masked slot x_{j+1} goes to P_{j+1} (received straight into its s0)."""
         bits = x.v.bits
         rel = [(c - j) % 3 for c in range(3)]
         slots = []
-        for c in range(3):
-            w = {0: (1, 2), 1: (0, 2), 2: (2, 2)}[rel[c]]
+        for c in range(3):  # the kernels read k_j: the owner's own key, P_{j+2}'s next key
+            w = {0: (0, 2), 1: (0, 2), 2: (1, 2)}[rel[c]]
             slots += [self._slot(plc, c, w[0]), self._slot(plc, c, w[1])]
         o = [self.offset(r) for r in plc.owners]
-        j2 = (j + 2) % 3
-        local = (o[j2] - o[j]) % self.N == 0  # P_{j+2} of the owner's session is here
-        if local:  # the kernel writes the owner's masked share into P_{j+2}'s s1 too
-            rel[j] += 4 * (1 + j2)
+        j1 = (j + 1) % 3
+        local = (o[j1] - o[j]) % self.N == 0  # P_{j+1} of the owner's session is here
+        if local:  # the kernel writes the owner's masked slot into P_{j+1}'s s0 too
+            rel[j] += 4 * (1 + j1)
         out0, out1 = R.share_party(kind, x.v, 3, rel, slots, n1, na)
         if not local:
-            self.comm.exchange([(out0[j], self._peer(o[j2] - o[j]))],
-                               [(out1[j2], self._peer(o[j] - o[j2]))])
-        self.stats.record_send(x.host, plc.owners[j2], _nbytes(x.v))
+            self.comm.exchange([(out1[j], self._peer(o[j1] - o[j]))],
+                               [(out0[j1], self._peer(o[j] - o[j1]))])
+        self.stats.record_send(x.host, plc.owners[j1], _nbytes(x.v))
         return PV(plc, R.RT(out0, bits)), PV(plc, R.RT(out1, bits))
 
     def party_exchange(self, plc, specs):

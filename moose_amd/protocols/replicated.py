@@ -14,7 +14,7 @@ Parity with the reference (``moose/src/replicated``):
 =====================  =====================================  =========================
 protocol               reference                              rounds here
 =====================  =====================================  =========================
-share (owner member)   convert.rs:74-125                      1 msg (x_j -> P_{j+2})
+share (owner member)   convert.rs:74-125                      1 msg (x_{j+1} -> P_{j+1})
 share (outsider)       convert.rs:126-156                     1 (x sent + seeds)
 reveal                 convert.rs:280-313                     1
 add/sub/neg/sum/shape  arith.rs:7-314, ops.rs                 0
@@ -89,15 +89,15 @@ def share(sess, plc, x: HV, kind="arith") -> RepTensor:
         if party is not None and bits in (64, 128):
             s0, s1 = party(plc, x, j, kind, n1, na)
             return RepTensor(plc, bits, kind, s0, s1)
-        # slot_{j+1} = PRF(k_{j+1}) [P_j, P_{j+1}]; slot_{j+2} = 0; slot_j = x - slot_{j+1}
-        # [P_j, sent to P_{j+2}].  As the reference (replicated/convert.rs:74-90), one slot
-        # of an input sharing is zero: each single party still misses one random slot
-        r1_j = sess.h_prf(plc, o[j], j1, shape, bits, n1)
-        r1_j1 = sess.h_prf(plc, o[j1], j1, shape, bits, n1)
-        xj = sess.h(sub, o[j], x, r1_j)
-        comp0 = {j: xj, j1: r1_j1, j2: sess.h("Fill", o[j2], shape, value=0, bits=bits)}
-        comp1 = {j: r1_j, j1: sess.h("Fill", o[j1], shape, value=0, bits=bits),
-                 j2: sess.move(xj, o[j2])}
+        # as the reference (replicated/convert.rs:74-90): slot_j = PRF(k_j) [P_j, P_{j+2}],
+        # slot_{j+1} = x - slot_j [P_j, sent to P_{j+1}], slot_{j+2} = 0.  Each single
+        # party other than the owner still misses one random slot
+        r_j = sess.h_prf(plc, o[j], j, shape, bits, n1)
+        r_j2 = sess.h_prf(plc, o[j2], j, shape, bits, n1)
+        xj1 = sess.h(sub, o[j], x, r_j)
+        comp0 = {j: r_j, j1: sess.move(xj1, o[j1]),
+                 j2: sess.h("Fill", o[j2], shape, value=0, bits=bits)}
+        comp1 = {j: xj1, j1: sess.h("Fill", o[j1], shape, value=0, bits=bits), j2: r_j2}
         s0 = sess.gather(plc, [comp0[i] for i in range(3)])
         s1 = sess.gather(plc, [comp1[i] for i in range(3)])
         return RepTensor(plc, bits, kind, s0, s1)

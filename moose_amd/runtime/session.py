@@ -650,12 +650,12 @@ class StackedSession(Session):
             nat.lib().mx_share3_k(
                 nat.dev_of(xd), 1 if kind == "bool" else 0, R._words(x.v.bits), nat.ptr(xd),
                 nat.ptr(out0), nat.ptr(out1), x.v.numel(), j,
-                ctypes.c_void_p(self.key_ptr(plc, (j + 1) % 3)),
+                ctypes.c_void_p(self.key_ptr(plc, j)),
                 ctypes.c_void_p(self.key_ptr(plc, 3)), n1, na, nat.stream_of(xd),
             ),
             "share3",
         )
-        self.stats.record_send(x.host, plc.owners[(j + 2) % 3], _nbytes(x.v))
+        self.stats.record_send(x.host, plc.owners[(j + 1) % 3], _nbytes(x.v))
         return PV(plc, R.RT(out0, x.v.bits)), PV(plc, R.RT(out1, x.v.bits))
 
     def mirror(self, x: HV, plc):
