@@ -311,6 +311,22 @@ __global__ void __launch_bounds__(256) k_decode(const T* __restrict__ x, double*
   }
 }
 
+// decode(a + b + c): the reveal's add and the decode in one pass (no ring-valued sum in HBM)
+template <class T>
+__global__ void __launch_bounds__(256) k_add3_decode(const T* __restrict__ a, const T* __restrict__ b,
+                                                     const T* __restrict__ c,
+                                                     double* __restrict__ out, int64_t n,
+                                                     double scale) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const T v = a[i] + b[i] + c[i];
+    if constexpr (sizeof(T) == 8)
+      out[i] = (double)(int64_t)v * scale;
+    else
+      out[i] = mxr::i128_to_f64(v) * scale;
+  }
+}
+
 // one thread per output when the reduced axis is short; a block per output otherwise
 template <class T>
 __global__ void __launch_bounds__(256) k_sum_axis(const T* __restrict__ a, T* __restrict__ out, int64_t outer,
@@ -1056,6 +1072,22 @@ int mxh_encode(int words, const double* x, void* out, int64_t n, int frac, void*
   else if (words == 2)
     hipLaunchKernelGGL(k_encode<u128>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream), x,
                        (u128*)out, n, scale);
+  else
+    return -2;
+  MX_LAUNCH_CHECK();
+  return 0;
+}
+
+int mxh_add3_decode(int words, const void* a, const void* b, const void* c, double* out,
+                    int64_t n, int frac, void* stream) {
+  if (n == 0) return 0;
+  const double scale = ldexp(1.0, -frac);
+  if (words == 1)
+    hipLaunchKernelGGL(k_add3_decode<u64>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
+                       (const u64*)a, (const u64*)b, (const u64*)c, out, n, scale);
+  else if (words == 2)
+    hipLaunchKernelGGL(k_add3_decode<u128>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
+                       (const u128*)a, (const u128*)b, (const u128*)c, out, n, scale);
   else
     return -2;
   MX_LAUNCH_CHECK();

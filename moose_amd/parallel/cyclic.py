@@ -446,7 +446,7 @@ class CyclicSession(StackedSession):
         src = d1[j1] if d1[j1].is_contiguous() else d1[j1].contiguous()
         got = self.party_exchange(plc, [("reveal", j1, j, src, (tuple(src.shape), src.dtype))])
         self.stats.record_send(plc.owners[j1], host, _nbytes(v1) // 3)
-        return HV(host, R.add3(R.RT(v0.data[j], v0.bits), R.RT(d1[j], v1.bits),
-                               R.RT(got["reveal"], v1.bits)))
+        return HV(host, R.opened(R.RT(v0.data[j], v0.bits), R.RT(d1[j], v1.bits),
+                                 R.RT(got["reveal"], v1.bits)))
     p_ks_level = None
     p_dot_zs_reshare = None

@@ -301,8 +301,8 @@ class StackedSession(Session):
         j = x.plc.owners.index(host)
         j1 = (j + 1) % 3
         self.stats.record_send(x.plc.owners[j1], host, _nbytes(v1) // 3)
-        return HV(host, R.add3(R.RT(v0.data[j], v0.bits), R.RT(v1.data[j], v1.bits),
-                               R.RT(v1.data[j1], v1.bits)))
+        return HV(host, R.opened(R.RT(v0.data[j], v0.bits), R.RT(v1.data[j], v1.bits),
+                                 R.RT(v1.data[j1], v1.bits)))
 
     def p_add_n(self, plc, xs):
         """Sum of replicated values ``xs`` [(PV s0, PV s1)] in one kernel when they are evenly
