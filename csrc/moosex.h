@@ -20,6 +20,10 @@ enum mx_unop { MX_NEG = 0, MX_NOT = 1, MX_SHL = 2, MX_SHR = 3, MX_SAR = 4 };
 enum mx_cmpop { MX_LT = 0, MX_GT = 1, MX_EQ = 2, MX_MSB = 3 };
 // RSS cross-term kinds: arithmetic (x0*y0 + x0*y1 + x1*y0 + a - b) or boolean (& and ^)
 enum mx_cross { MX_CROSS_ARITH = 0, MX_CROSS_BOOL = 1 };
+// share kernels (mx_share3*, mx_share_party): kind MX_SHARE_F64 = an arithmetic sharing of a
+// float64 input, fixed-point encoded in the kernel (x * 2^na, truncated as RingFixedpointEncode);
+// the nonce argument na carries the fractional bits (the zero slot draws no randomness)
+enum mx_share_src { MX_SHARE_F64 = 2 };
 
 // AES-128 key schedule: 11 round keys of 4 big-endian-packed words (FIPS-197 layout)
 typedef struct {

@@ -9,6 +9,7 @@
 
 #include "prf_dev.h"
 #include "moosex.h"
+#include "ring_common.h"
 #include "rss_fused.h"
 
 using u64 = uint64_t;
@@ -103,9 +104,12 @@ __global__ void __launch_bounds__(256) k_trunc_pr3_lat(const T* __restrict__ s0,
 }
 
 template <class T>
-__global__ void __launch_bounds__(256) k_share3(int kind, const T* __restrict__ x, T* __restrict__ out0,
+__global__ void __launch_bounds__(256) k_share3(int kind, const void* __restrict__ xv, T* __restrict__ out0,
                          T* __restrict__ out1, int64_t n, int j0, mxd::KeySrc keys, uint64_t n1,
                          uint64_t na) {
+  const T* x = (const T*)xv;
+  const double* xf = (const double*)xv;  // kind MX_SHARE_F64: encode in the kernel
+  const double scale = kind == MX_SHARE_F64 ? ldexp(1.0, (int)na) : 0.0;
   __shared__ uint32_t rks[1][mxd::kKeyWords];
   mxd::stage_keys(rks, keys, 1);
   constexpr int P = mxd::Lane<T>::kPer;
@@ -118,9 +122,10 @@ __global__ void __launch_bounds__(256) k_share3(int kind, const T* __restrict__ 
       const int64_t i = b * P + j;
       if (i >= n) break;
       const T r = mxd::pick<T>(lo[0], hi[0], j);
+      const T xi = kind == MX_SHARE_F64 ? (T)mxr::f64_to_i128(xf[i] * scale) : x[i];
       T slot[3];
       slot[j0] = r;
-      slot[(j0 + 1) % 3] = kind == MX_CROSS_BOOL ? (T)(x[i] ^ r) : (T)(x[i] - r);
+      slot[(j0 + 1) % 3] = kind == MX_CROSS_BOOL ? (T)(xi ^ r) : (T)(xi - r);
       slot[(j0 + 2) % 3] = 0;
       const bool ring4 = out1 == out0 + n;  // 4-slot ring: out1's slots 0, 1 are out0's 1, 2
 #pragma unroll
@@ -178,16 +183,16 @@ int launch_share3(int kind, int words, const void* x, void* out0, void* out1, in
   switch (words) {
     case 0:
       hipLaunchKernelGGL(k_share3<uint8_t>, dim3(mxd::grid_for_chunks((n + 15) / 16)), dim3(256), 0, st,
-                         kind, (const uint8_t*)x, (uint8_t*)out0, (uint8_t*)out1, n, j, keys, n1,
+                         kind, x, (uint8_t*)out0, (uint8_t*)out1, n, j, keys, n1,
                          na);
       break;
     case 1:
       hipLaunchKernelGGL(k_share3<u64>, dim3(mxd::grid_for_chunks((n + 1) / 2)), dim3(256), 0, st, kind,
-                         (const u64*)x, (u64*)out0, (u64*)out1, n, j, keys, n1, na);
+                         x, (u64*)out0, (u64*)out1, n, j, keys, n1, na);
       break;
     case 2:
       hipLaunchKernelGGL(k_share3<u128>, dim3(mxd::grid_for_chunks(n)), dim3(256), 0, st, kind,
-                         (const u128*)x, (u128*)out0, (u128*)out1, n, j, keys, n1, na);
+                         x, (u128*)out0, (u128*)out1, n, j, keys, n1, na);
       break;
     default:
       return -2;

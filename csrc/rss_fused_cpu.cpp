@@ -1,10 +1,12 @@
 // Host versions of the fused stacked-session kernels (see rss_fused.h) and the C ABI
 // entry points that dispatch host / device.
+#include <cmath>
 #include <cstring>
 #include <functional>
 #include <vector>
 
 #include "moosex.h"
+#include "ring_common.h"
 #include "rss_fused.h"
 
 void mx_cpu_prf_range(const uint8_t* key, uint64_t nonce, int words, int64_t i0, int64_t n,
@@ -66,9 +68,12 @@ int trunc3_host(const T* s0, T* out0, T* out1, int64_t n, int m, const uint8_t* 
 }
 
 template <class T>
-int share3_host(int kind, const T* x, T* out0, T* out1, int64_t n, int j, const uint8_t* kn,
-                const uint8_t* /*ka: unused*/, uint64_t n1, uint64_t /*na: unused*/) {
+int share3_host(int kind, const void* xv, T* out0, T* out1, int64_t n, int j, const uint8_t* kn,
+                const uint8_t* /*ka: unused*/, uint64_t n1, uint64_t na) {
   const int words = sizeof(T) == 1 ? 0 : (int)(sizeof(T) / 8);
+  const T* x = (const T*)xv;
+  const double* xf = (const double*)xv;  // kind MX_SHARE_F64 (moosex.h)
+  const double scale = kind == MX_SHARE_F64 ? std::ldexp(1.0, (int)na) : 0.0;
   mx_cpu_parallel_for(n, 1 << 12, [&](int64_t s, int64_t e) {
     const int64_t CH = 512;
     std::vector<T> r1(CH);
@@ -77,9 +82,10 @@ int share3_host(int kind, const T* x, T* out0, T* out1, int64_t n, int j, const 
       mx_cpu_prf_range(kn, n1, words, c, len, r1.data());
       for (int64_t t = 0; t < len; ++t) {
         int64_t i = c + t;
+        const T xi = kind == MX_SHARE_F64 ? (T)mxr::f64_to_i128(xf[i] * scale) : x[i];
         T slot[3];
         slot[j] = r1[t];
-        slot[(j + 1) % 3] = kind == MX_CROSS_BOOL ? (T)(x[i] ^ r1[t]) : (T)(x[i] - r1[t]);
+        slot[(j + 1) % 3] = kind == MX_CROSS_BOOL ? (T)(xi ^ r1[t]) : (T)(xi - r1[t]);
         slot[(j + 2) % 3] = 0;
         for (int p = 0; p < 3; ++p) {
           out0[p * n + i] = slot[p];

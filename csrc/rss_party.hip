@@ -19,6 +19,7 @@
 
 #include "prf_dev.h"
 #include "moosex.h"
+#include "ring_common.h"
 #include "rss_fused.h"
 
 using u64 = uint64_t;
@@ -190,8 +191,11 @@ __global__ void __launch_bounds__(256)
 
 template <class T>
 __global__ void __launch_bounds__(256)
-    k_share_party(int kind, int64_t n, Roles rel, const T* __restrict__ x, T* __restrict__ out0,
+    k_share_party(int kind, int64_t n, Roles rel, const void* __restrict__ xv, T* __restrict__ out0,
                   T* __restrict__ out1, mxd::KeySrc keys, uint64_t n1, uint64_t na, int ncomp) {
+  const T* x = (const T*)xv;
+  const double* xf = (const double*)xv;  // kind MX_SHARE_F64: encode in the kernel
+  const double scale = kind == MX_SHARE_F64 ? ldexp(1.0, (int)na) : 0.0;
   __shared__ uint32_t rks[mxd::kMaxKeySlots][mxd::kKeyWords];
   // keys: 2 per component, the first used: k_j of the owner j (rel 0: own, rel 2: next).
   // As the reference (replicated/convert.rs:74-90): slot j = PRF(k_j), slot j+1 = x - slot j
@@ -223,7 +227,8 @@ __global__ void __launch_bounds__(256)
         if (i >= n) break;
         const T rr = mxd::pick<T>(al, ah, j);
         if (r == 0) {  // owner: (slot j, slot j+1) = (PRF(k_j), x - PRF(k_j))
-          const T v = kind == MX_CROSS_BOOL ? (T)(x[i] ^ rr) : (T)(x[i] - rr);
+          const T xi = kind == MX_SHARE_F64 ? (T)mxr::f64_to_i128(xf[i] * scale) : x[i];
+          const T v = kind == MX_CROSS_BOOL ? (T)(xi ^ rr) : (T)(xi - rr);
           out0[base + i] = rr;
           out1[base + i] = v;
           if (fwd >= 0) out0[(int64_t)fwd * n + i] = v;

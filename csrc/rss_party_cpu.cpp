@@ -1,10 +1,12 @@
 // Host versions of the per-party protocol kernels (rss_party.hip) and the C ABI entry
 // points that dispatch host / device.  Key slots are MX_KEY_SLOT_WORDS-word images whose
 // first four words are the raw AES key.
+#include <cmath>
 #include <functional>
 #include <vector>
 
 #include "moosex.h"
+#include "ring_common.h"
 #include "rss_fused.h"
 
 void mx_cpu_prf_range(const uint8_t* key, uint64_t nonce, int words, int64_t i0, int64_t n,
@@ -135,8 +137,11 @@ int trunc_r1(int64_t n, int m, int ncomp, const int* roles, const T* msg, const 
 }
 
 template <class T>
-int share_party(int kind, int64_t n, int ncomp, const int* rel, const T* x, T* out0, T* out1,
-                const uint32_t* const* slots, uint64_t n1, uint64_t /*na: unused*/) {
+int share_party(int kind, int64_t n, int ncomp, const int* rel, const void* xp, T* out0, T* out1,
+                const uint32_t* const* slots, uint64_t n1, uint64_t na) {
+  const T* x = (const T*)xp;
+  const double* xf = (const double*)xp;  // kind MX_SHARE_F64 (moosex.h)
+  const double scale = kind == MX_SHARE_F64 ? std::ldexp(1.0, (int)na) : 0.0;
   for (int c = 0; c < ncomp; ++c) {
     const int code = rel[c];  // as k_share_party: role + 4 * (1 + local P_{j+1} component)
     if (code < 0) continue;
@@ -149,7 +154,8 @@ int share_party(int kind, int64_t n, int ncomp, const int* rel, const T* x, T* o
       for (int64_t q = 0; q < len; ++q) {
         const int64_t i = base + i0 + q;
         if (r == 0) {
-          const T xv = x[i0 + q];
+          const T xv =
+              kind == MX_SHARE_F64 ? (T)mxr::f64_to_i128(xf[i0 + q] * scale) : x[i0 + q];
           out0[i] = a[q];
           out1[i] = kind == MX_CROSS_BOOL ? (T)(xv ^ a[q]) : (T)(xv - a[q]);
           if (fwd >= 0) out0[(int64_t)fwd * n + i0 + q] = out1[i];

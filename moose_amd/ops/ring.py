@@ -479,6 +479,56 @@ def encode(x: torch.Tensor, frac: int, bits: int) -> RT:
     return out
 
 
+class Encoded(RT):
+    """A float64 tensor's fixed-point encoding (x * 2^frac), formed on first use of
+    ``data``.  Input sharing of it encodes inside the share kernel (kind MX_SHARE_F64): the
+    ring-valued encoding never goes to memory."""
+
+    __slots__ = ("src", "frac")
+
+    def __init__(self, x: torch.Tensor, frac: int, bits: int):
+        _RT_DATA.__set__(self, None)
+        self.bits = bits
+        self._shape = tuple(x.shape)
+        self.src = x
+        self.frac = int(frac)
+
+    def pending(self) -> bool:
+        return _RT_DATA.__get__(self) is None
+
+    @property
+    def data(self):
+        d = _RT_DATA.__get__(self)
+        if d is None:
+            d = encode(self.src, self.frac, self.bits).data
+            _RT_DATA.__set__(self, d)
+            self.src = None
+        return d
+
+    @data.setter
+    def data(self, v):
+        _RT_DATA.__set__(self, v)
+
+    @property
+    def device(self):
+        return self.src.device if self.pending() else self.data.device
+
+
+def encode_lazy(x: torch.Tensor, frac: int, bits: int) -> RT:
+    """encode(), deferred to the first use (:class:`Encoded`) for 64/128-bit rings."""
+    if bits not in (64, 128):
+        return encode(x, frac, bits)
+    return Encoded(x.to(torch.float64).contiguous(), frac, bits)
+
+
+def share_source(x: RT, kind: str):
+    """(kind code, device tensor, aux) for the share kernels: an unencoded float64 input is
+    passed as is (MX_SHARE_F64 = 2, aux = its fractional bits), else the ring data."""
+    if kind == "arith" and isinstance(x, Encoded) and x.pending():
+        return 2, x.src, x.frac
+    return (1 if kind == "bool" else 0), x.data.contiguous(), None
+
+
 def decode(a: RT, frac: int) -> torch.Tensor:
     if isinstance(a, Opened) and a.pending():  # the reveal's add fused into the decode
         d = [t.data.contiguous() for t in a.parts]
@@ -1483,13 +1533,14 @@ def trunc_party_r1(msg, rmk, rrt, rrm, out0, out1, bits, m, roles, slots, nonces
 
 def share_party(kind: str, x: RT, ncomp: int, rel, slots, n1: int, na: int):
     """Per-component slots of a sharing by member j (mx_share_party); the owner's out1
-    (slot x_{j+1}) is the message to P_{j+1} (whose out0 it becomes)."""
-    xd = x.data.contiguous()
-    shape = (ncomp,) + tuple(xd.shape)
-    out0 = torch.empty(shape, dtype=xd.dtype, device=xd.device)
-    out1 = torch.empty_like(out0)
+    (slot x_{j+1}) is the message to P_{j+1} (whose out0 it becomes).  A pending
+    :class:`Encoded` input is encoded inside the kernel."""
+    code, xd, aux = share_source(x, kind)
+    na = na if aux is None else aux
+    out0, out1 = empty2((ncomp,) + tuple(x.shape), x.bits, xd.device)
+    out0, out1 = out0.data, out1.data
     nat.check(nat.lib().mx_share_party(
-        nat.dev_of(xd), 1 if kind == "bool" else 0, _words(x.bits), x.numel(), ncomp,
+        nat.dev_of(xd), code, _words(x.bits), x.numel(), ncomp,
         _roles_arr(rel), nat.ptr(xd), nat.ptr(out0), nat.ptr(out1), _slots_arr(slots),
         n1 & MASK64, na & MASK64, nat.stream_of(xd)), "share_party")
     return out0, out1

@@ -347,6 +347,8 @@ def _s64(u: int) -> int:
 
 def payload_bytes(v) -> int:
     if isinstance(v, R.RT):
+        if v.bits in (64, 128):  # without touching data (lazy Encoded / Opened)
+            return v.numel() * (v.bits // 8)
         return v.data.numel() * v.data.element_size()
     if isinstance(v, torch.Tensor):
         return v.numel() * v.element_size()

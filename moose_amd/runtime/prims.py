@@ -380,7 +380,8 @@ def _ones(nb, shape, dtype, device):
 # ---------------------------------------------------------------------------
 @prim("RingFixedpointEncode")
 def _encode(nb, x, scaling_exp, bits):
-    return R.encode(x, scaling_exp, bits)
+    # deferred: an input sharing of the result encodes inside the share kernel
+    return R.encode_lazy(x, scaling_exp, bits)
 
 
 @prim("RingFixedpointDecode")

@@ -68,6 +68,8 @@ _DEVICE_PRIMS = {"Fill", "Zeros", "Ones", "SampleSeeded", "Sample"}
 
 def _nbytes(v):
     if isinstance(v, R.RT):
+        if v.bits in (64, 128):  # without touching data (a lazy Encoded / Opened stays so)
+            return v.numel() * (v.bits // 8)
         return v.data.numel() * v.data.element_size()
     if isinstance(v, torch.Tensor):
         return v.numel() * v.element_size()
@@ -644,14 +646,15 @@ class StackedSession(Session):
 
         from moose_amd.ops import native as nat
 
-        xd = x.v.data.contiguous()
+        code, xd, aux = R.share_source(x.v, kind)  # a pending encoding: encoded in-kernel
         out0, out1 = (t.data for t in R.ring4((3,) + tuple(x.v.shape), x.v.bits, xd.device))
         nat.check(
             nat.lib().mx_share3_k(
-                nat.dev_of(xd), 1 if kind == "bool" else 0, R._words(x.v.bits), nat.ptr(xd),
+                nat.dev_of(xd), code, R._words(x.v.bits), nat.ptr(xd),
                 nat.ptr(out0), nat.ptr(out1), x.v.numel(), j,
                 ctypes.c_void_p(self.key_ptr(plc, j)),
-                ctypes.c_void_p(self.key_ptr(plc, 3)), n1, na, nat.stream_of(xd),
+                ctypes.c_void_p(self.key_ptr(plc, 3)), n1, na if aux is None else aux,
+                nat.stream_of(xd),
             ),
             "share3",
         )
