@@ -319,7 +319,7 @@ def test_share_party_matches_host(bits, j):
     rel = [(c - j) % 3 for c in range(3)]
     h = R.share_party("arith", x, 3, rel, hs, 21, 22)
     d = R.share_party("arith", gpu(x), 3, rel, ds, 21, 22)
-    j2 = (j + 2) % 3
-    assert torch.equal(h[0], d[0].cpu())
-    keep = [c for c in range(3) if c != j2]  # the j+2 component's s1 arrives by message
-    assert torch.equal(h[1][keep], d[1].cpu()[keep])
+    j1 = (j + 1) % 3
+    assert torch.equal(h[1], d[1].cpu())
+    keep = [c for c in range(3) if c != j1]  # the j+1 component's s0 arrives by message
+    assert torch.equal(h[0][keep], d[0].cpu()[keep])
