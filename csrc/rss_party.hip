@@ -301,37 +301,41 @@ __global__ void __launch_bounds__(256)
     const uint32_t* nxt = rks[2 * c + 1];
     const T* x = cp<T>(cross, c);
     T* mo = wp<T>(msg, c);
-    // zero share alpha: P0 f(k0), P1 -f(k2), P2 f(k2) - f(k0) (f = PRF at nonce n_a; sums
-    // to zero).  z2 (sent to P0 and P1) is masked by f(k2) against P0 and f(k0) against
-    // P1, m0 / m1 by the opening masks r0 / r1: every view is as with the textbook
-    // alpha_p = f(k_p) - f(k_{p+1}), with one PRF stream less at P0 and at P1
-    uint32_t wa[16], wb[16], wr[16];
-    if (role != 1) mx::chacha_block(own, n_a, B, wa);
-    if (role != 0) mx::chacha_block(nxt, n_a, B, wb);
-    if (role == 0) mx::chacha_block(own, n_r0, B, wr);
-    if (role == 1) mx::chacha_block(nxt, n_r1, B, wr);
+    // no cross (null): the dealer part only, launched before the product exists, so P2's
+    // rt1 / rm1 travel while the GEMM runs; no msg_rt (null): no dealer part
+    if (x != nullptr) {
+      // zero share alpha: P0 f(k0), P1 -f(k2), P2 f(k2) - f(k0) (f = PRF at nonce n_a; sums
+      // to zero).  z2 (sent to P0 and P1) is masked by f(k2) against P0 and f(k0) against
+      // P1, m0 / m1 by the opening masks r0 / r1: every view is as with the textbook
+      // alpha_p = f(k_p) - f(k_{p+1}), with one PRF stream less at P0 and at P1
+      uint32_t wa[16], wb[16], wr[16];
+      if (role != 1) mx::chacha_block(own, n_a, B, wa);
+      if (role != 0) mx::chacha_block(nxt, n_a, B, wb);
+      if (role == 0) mx::chacha_block(own, n_r0, B, wr);
+      if (role == 1) mx::chacha_block(nxt, n_r1, B, wr);
 #pragma unroll
-    for (int part = 0; part < 4; ++part) {
-      const int64_t b = (int64_t)mx::ks_chunk(B, part);
-      if (b >= nb) break;
-      uint64_t al = 0, ah = 0, bl = 0, bh = 0, rl = 0, rh = 0;
-      if (role != 1) mx::part_u64(wa, part, &al, &ah);
-      if (role != 0) mx::part_u64(wb, part, &bl, &bh);
-      if (role != 2) mx::part_u64(wr, part, &rl, &rh);
+      for (int part = 0; part < 4; ++part) {
+        const int64_t b = (int64_t)mx::ks_chunk(B, part);
+        if (b >= nb) break;
+        uint64_t al = 0, ah = 0, bl = 0, bh = 0, rl = 0, rh = 0;
+        if (role != 1) mx::part_u64(wa, part, &al, &ah);
+        if (role != 0) mx::part_u64(wb, part, &bl, &bh);
+        if (role != 2) mx::part_u64(wr, part, &rl, &rh);
 #pragma unroll
-      for (int j = 0; j < P; ++j) {
-        const int64_t i = b * P + j;
-        if (i >= n) break;
-        const T z = x[i] + mxd::pick<T>(al, ah, j) - mxd::pick<T>(bl, bh, j);
-        if (role == 0)
-          mo[i] = mxf::trunc_mask0<T>(z, (T)0, mxd::pick<T>(rl, rh, j));
-        else if (role == 1)
-          mo[i] = z + mxd::pick<T>(rl, rh, j);
-        else
-          mo[i] = z;
+        for (int j = 0; j < P; ++j) {
+          const int64_t i = b * P + j;
+          if (i >= n) break;
+          const T z = x[i] + mxd::pick<T>(al, ah, j) - mxd::pick<T>(bl, bh, j);
+          if (role == 0)
+            mo[i] = mxf::trunc_mask0<T>(z, (T)0, mxd::pick<T>(rl, rh, j));
+          else if (role == 1)
+            mo[i] = z + mxd::pick<T>(rl, rh, j);
+          else
+            mo[i] = z;
+        }
       }
     }
-    if (role == 2) {  // dealer (as k_trunc_party_r0): streams r0, r1, t, m, z0, z2
+    if (role == 2 && msg_rt.p[c] != nullptr) {  // dealer (as k_trunc_party_r0): r0, r1, t, m, z0, z2
       uint32_t w[6][16];
       mx::chacha_block(nxt, n_r0, B, w[0]);
       mx::chacha_block(own, n_r1, B, w[1]);

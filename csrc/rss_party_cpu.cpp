@@ -184,19 +184,24 @@ int dot_tail_r0(int64_t n, int m, int ncomp, const int* roles, const void* const
     const uint32_t* nxt = slots[2 * c + 1];
     const T* x = (const T*)cross[c];
     T* mo = (T*)msg[c];
+    // as k_dot_tail_r0: no cross -> the dealer part only; no msg_rt -> no dealer part
+    const bool main_part = x != nullptr;
+    const bool dealer = role == 2 && msg_rt[c] != nullptr;
     for_chunks<T>(n, [&](int64_t i0, int64_t len) {
-      // zero share: P0 f(k0), P1 -f(k2), P2 f(k2) - f(k0) (rss_party.hip)
-      std::vector<T> a(len, (T)0), b(len, (T)0), r(len);
-      if (role != 1) prf<T>(own, nn[0], i0, len, a.data());
-      if (role != 0) prf<T>(nxt, nn[0], i0, len, b.data());
-      if (role == 0) prf<T>(own, nn[1], i0, len, r.data());
-      if (role == 1) prf<T>(nxt, nn[2], i0, len, r.data());
-      for (int64_t q = 0; q < len; ++q) {
-        const int64_t i = i0 + q;
-        const T z = x[i] + a[q] - b[q];
-        mo[i] = role == 0 ? mxf::trunc_mask0<T>(z, (T)0, r[q]) : role == 1 ? (T)(z + r[q]) : z;
+      if (main_part) {
+        // zero share: P0 f(k0), P1 -f(k2), P2 f(k2) - f(k0) (rss_party.hip)
+        std::vector<T> a(len, (T)0), b(len, (T)0), r(len);
+        if (role != 1) prf<T>(own, nn[0], i0, len, a.data());
+        if (role != 0) prf<T>(nxt, nn[0], i0, len, b.data());
+        if (role == 0) prf<T>(own, nn[1], i0, len, r.data());
+        if (role == 1) prf<T>(nxt, nn[2], i0, len, r.data());
+        for (int64_t q = 0; q < len; ++q) {
+          const int64_t i = i0 + q;
+          const T z = x[i] + a[q] - b[q];
+          mo[i] = role == 0 ? mxf::trunc_mask0<T>(z, (T)0, r[q]) : role == 1 ? (T)(z + r[q]) : z;
+        }
       }
-      if (role == 2) {
+      if (dealer) {
         std::vector<T> r0(len), r1(len), t(len), mm(len), z0(len), z2(len);
         prf<T>(nxt, nn[1], i0, len, r0.data());
         prf<T>(own, nn[2], i0, len, r1.data());

@@ -1562,13 +1562,14 @@ def _dev_stream(ts):
     return nat.dev_of(t), nat.stream_of(t)
 
 
-def dot_tail_r0(cross, bits, m, roles, slots, nonces, out0, out1, n):
+def dot_tail_r0(cross, bits, m, roles, slots, nonces, out0, out1, n, dealer=True):
     """Round 0 of the per-party dot tail (mx_dot_tail_r0): returns the per-component
     outgoing messages (P0 m0, P1 m1, P2 z2), the dealer's rt1 and rm1 (P2 only); writes
-    P2's new shares into out0 / out1."""
+    P2's new shares into out0 / out1.  ``dealer=False``: the dealer's part already ran
+    (:func:`dot_tail_dealer`), rt / rm are None."""
     msg = [torch.empty_like(x) for x in cross]
-    rt = [torch.empty_like(x) if r == 2 else None for x, r in zip(cross, roles)]
-    rm = [torch.empty((n,), dtype=torch.int64, device=x.device) if r == 2 else None
+    rt = [torch.empty_like(x) if r == 2 and dealer else None for x, r in zip(cross, roles)]
+    rm = [torch.empty((n,), dtype=torch.int64, device=x.device) if r == 2 and dealer else None
           for x, r in zip(cross, roles)]
     dev, st = _dev_stream(cross)
     nat.check(nat.lib().mx_dot_tail_r0(
@@ -1576,6 +1577,27 @@ def dot_tail_r0(cross, bits, m, roles, slots, nonces, out0, out1, n):
         _vp(rm), _vp(out0), _vp(out1), _slots_arr(slots), _nonces_arr(nonces), st),
         "dot_tail_r0")
     return msg, rt, rm
+
+
+def dot_tail_dealer(bits, m, roles, slots, nonces, out0, out1, n):
+    """The dealer P2's part of round 0 on its own (mx_dot_tail_r0 without the products):
+    it depends on PRF keys and nonces only, so it runs before the product exists and its
+    messages rt1 / rm1 travel while the GEMM runs.  Returns (rt, rm) per component (P2's
+    components only); writes P2's new shares into out0 / out1."""
+    like = [o if r == 2 else None for o, r in zip(out0, roles)]
+    rt = [torch.empty_like(o) if o is not None else None for o in like]
+    rm = [torch.empty((n,), dtype=torch.int64, device=o.device) if o is not None else None
+          for o in like]
+    if not any(o is not None for o in like):
+        return rt, rm
+    only = [r if r == 2 else -1 for r in roles]
+    none = [None] * len(roles)
+    dev, st = _dev_stream(like)
+    nat.check(nat.lib().mx_dot_tail_r0(
+        dev, _words(bits), n, m, len(roles), _roles_arr(only), _vp(none), _vp(none), _vp(rt),
+        _vp(rm), _vp(out0), _vp(out1), _slots_arr(slots), _nonces_arr(nonces), st),
+        "dot_tail_dealer")
+    return rt, rm
 
 
 def dot_tail_r1(msg, rmk, rz, rrt, rrm, bits, m, roles, slots, nonces, out0, out1, n):

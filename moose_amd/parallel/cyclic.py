@@ -412,18 +412,41 @@ class CyclicSession(StackedSession):
             self.comm.exchange(sends, recvs)
         return got
 
-    def party_dot_trunc(self, plc, v, m, nonces, out=None):
+    def party_dot_trunc_pre(self, plc, x, y, m, nonces):
+        """The dealer's part of rep.dot_trunc's tail, issued before the GEMM of x . y
+        (party.dealer_early); None for shapes other than a plain 2-D product."""
+        from moose_amd.parallel import party
+
+        xs, ys = x.s0.v.shape, y.s0.v.shape
+        if len(xs) != 3 or len(ys) != 3:
+            return None
+        bits = x.bits
+        shp = (3, xs[1], ys[2]) + ((2,) if bits == 128 else ())
+        s0 = torch.empty(shp, dtype=torch.int64, device=self.device)
+        s1 = torch.empty_like(s0)
+        pre = party.dealer_early(self, plc, [0, 1, 2], (shp[1:], torch.int64), bits, m, nonces,
+                                 [s0[c] for c in range(3)], [s1[c] for c in range(3)],
+                                 self._pair_ptrs(plc))
+        pre.stack = (s0, s1)
+        return pre
+
+    def party_dot_trunc(self, plc, v, m, nonces, out=None, pre=None):
         """rep.dot_trunc's zero share + reshare + TruncPr of the local products ``v`` with
         the reshare folded into TruncPr's first round (parallel/party.py); ``out``: optional
-        (s0, s1) [3, ...] views (dense per component) written in place."""
+        (s0, s1) [3, ...] views (dense per component) written in place; ``pre``: the
+        dealer's part from party_dot_trunc_pre (its buffers are the output)."""
         from moose_amd.parallel import party
 
         bits = v.v.bits
         data = v.v.data.contiguous()
-        s0, s1 = out if out is not None else (torch.empty_like(data), torch.empty_like(data))
+        if pre is not None:
+            s0, s1 = pre.stack
+        else:
+            s0, s1 = out if out is not None else (torch.empty_like(data),
+                                                  torch.empty_like(data))
         party.dot_trunc_tail(self, plc, [0, 1, 2], [data[c] for c in range(3)], bits, m,
                              nonces, [s0[c] for c in range(3)], [s1[c] for c in range(3)],
-                             self._pair_ptrs(plc))
+                             self._pair_ptrs(plc), pre=pre)
         return PV(plc, R.RT(s0, bits)), PV(plc, R.RT(s1, bits))
 
     # the single-GPU fused variants read other parties' data in-kernel: never used here

@@ -41,15 +41,44 @@ TAIL_A = (("m0", 0, 1), ("m1", 1, 0), ("z2_0", 2, 0), ("z2_1", 2, 1), ("rt1", 2,
 TAIL_B = (("w0", 0, 1), ("w1", 1, 0))
 
 
-def dot_trunc_tail(sess, plc, roles, cross, bits, m, nonces, out0, out1, slots):
+class DealerEarly:
+    """The dealer's half of round A, done before the product exists (:func:`dealer_early`):
+    P2's new shares already written into ``out0`` / ``out1``, P1's received rt1 / rm1."""
+
+    __slots__ = ("out0", "out1", "rrt", "rrm", "stack")
+
+    def __init__(self, out0, out1, rrt, rrm):
+        self.out0, self.out1, self.rrt, self.rrm = out0, out1, rrt, rrm
+        self.stack = None  # the session's (s0, s1) tensors that out0 / out1 are views of
+
+
+def dealer_early(sess, plc, roles, like, bits, m, nonces, out0, out1, slots):
+    """P2's TruncPr dealer messages of the dot tail (rt1, rm1 -> P1) depend on PRF keys and
+    nonces only: computed and sent BEFORE the GEMM, they travel while it runs, and round A
+    after the product carries only m0, m1 and z2 -- on the 2 -> 1 link 1 share tensor
+    instead of 2.5.  ``like`` = (shape, dtype) of one component's product."""
+    comp = {r: c for c, r in enumerate(roles)}
+    n_el = math.prod(like[0]) // (2 if bits == 128 else 1)
+    rt, rm = R.dot_tail_dealer(bits, m, roles, slots, nonces, out0, out1, n_el)
+    c2 = comp.get(2)
+    got = sess.party_exchange(plc, [
+        ("rt1", 2, 1, None if c2 is None else rt[c2], like),
+        ("rm1", 2, 1, None if c2 is None else rm[c2], ((n_el,), torch.int64))])
+    return DealerEarly(out0, out1, [got.get("rt1") if r == 1 else None for r in roles],
+                       [got.get("rm1") if r == 1 else None for r in roles])
+
+
+def dot_trunc_tail(sess, plc, roles, cross, bits, m, nonces, out0, out1, slots, pre=None):
     """Zero share + reshare + TruncPr of the local cross products ``cross`` (one dense
     ring-``bits`` tensor per hosted component; component c plays party ``roles[c]``).
     Writes the new shares into ``out0`` / ``out1`` (dense per-component tensors, e.g. rows
     of a stack).  ``nonces`` = (zero share, r0, r1, t, m, z0, z2); ``slots`` = the key-slot
-    pointers (own k_p, next k_{p+1}) of every component."""
+    pointers (own k_p, next k_{p+1}) of every component.  ``pre``: the dealer's part, done
+    by :func:`dealer_early` (same out0 / out1)."""
     comp = {r: c for c, r in enumerate(roles)}
     n_el = math.prod(cross[0].shape) // (2 if bits == 128 else 1)
-    msg, rt, rm = R.dot_tail_r0(cross, bits, m, roles, slots, nonces, out0, out1, n_el)
+    msg, rt, rm = R.dot_tail_r0(cross, bits, m, roles, slots, nonces, out0, out1, n_el,
+                                dealer=pre is None)
 
     def mine(party, arrs):
         c = comp.get(party)
@@ -59,12 +88,16 @@ def dot_trunc_tail(sess, plc, roles, cross, bits, m, nonces, out0, out1, slots):
     like = (tuple(cross[0].shape), cross[0].dtype)
     payload = {"m0": mine(0, msg), "m1": mine(1, msg), "z2_0": mine(2, msg),
                "z2_1": mine(2, msg), "rt1": mine(2, rt), "rm1": mine(2, rm)}
+    names = TAIL_A if pre is None else TAIL_A[:4]
     got = sess.party_exchange(plc, [(nm, a, b, payload[nm], like_rm if nm == "rm1" else like)
-                                    for nm, a, b in TAIL_A])
+                                    for nm, a, b in names])
     rmk = [got.get("m1") if r == 0 else got.get("m0") if r == 1 else None for r in roles]
     rz = [got.get("z2_0") if r == 0 else got.get("z2_1") if r == 1 else None for r in roles]
-    rrt = [got.get("rt1") if r == 1 else None for r in roles]
-    rrm = [got.get("rm1") if r == 1 else None for r in roles]
+    if pre is None:
+        rrt = [got.get("rt1") if r == 1 else None for r in roles]
+        rrm = [got.get("rm1") if r == 1 else None for r in roles]
+    else:
+        rrt, rrm = pre.rrt, pre.rrm
     w = R.dot_tail_r1(msg, rmk, rz, rrt, rrm, bits, m, roles, slots, nonces, out0, out1, n_el)
     got = sess.party_exchange(plc, [("w0", 0, 1, mine(0, w), like), ("w1", 1, 0, mine(1, w), like)])
     other = [got.get("w1") if r == 0 else got.get("w0") if r == 1 else None for r in roles]

@@ -421,9 +421,13 @@ def dot_trunc(sess, x: RepTensor, y: RepTensor, m: int) -> RepTensor:
                 return RepTensor(x.plc, x.bits, "arith", s0, s1)
         if use_party:  # the per-party tail: reshare folded into TruncPr (2 rounds)
             with span("rep.dot_trunc_party"):
-                v = sess.p_dot_cross(x.plc, x.s0, x.s1, y.s0, y.s1)
                 nonces = tuple(sess.nonce(x.plc) for _ in range(7))  # as dot + trunc_pr
-                s0, s1 = party(x.plc, v, m, nonces)
+                # the dealer's messages first: they travel while the GEMM runs
+                pre_fn = getattr(sess, "party_dot_trunc_pre", None)
+                pre = pre_fn(x.plc, x, y, m, nonces) if pre_fn is not None else None
+                v = sess.p_dot_cross(x.plc, x.s0, x.s1, y.s0, y.s1)
+                s0, s1 = (party(x.plc, v, m, nonces) if pre is None
+                          else party(x.plc, v, m, nonces, pre=pre))
                 return RepTensor(x.plc, x.bits, "arith", s0, s1)
         return trunc_pr(sess, dot(sess, x, y), m)
     with span("rep.dot_trunc_pipelined"):

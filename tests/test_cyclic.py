@@ -59,7 +59,7 @@ def _program(sess, xb, ya, mb, ma):
     return tensors, (out.v.data.clone(), dt.v.data.clone())
 
 
-def _worker(rank, world, port, q, device="cpu", offsets=None):
+def _worker(rank, world, port, q, device="cpu", offsets=None, chunks=4):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from moose_amd.parallel.cyclic import CyclicSession
@@ -68,7 +68,7 @@ def _worker(rank, world, port, q, device="cpu", offsets=None):
 
     sess = CyclicSession(RingComm(rank, world, device), offsets or {"a": 0, "b": 1, "c": 2},
                          seed=SEED,
-                         device=device, pipeline_chunks=4)
+                         device=device, pipeline_chunks=chunks)
     res = {}
     for bits in (64, 128):
         xd, yd = _data(sess.session_of("b"), bits), _data(100 + sess.session_of("a"), bits)
@@ -87,14 +87,14 @@ def _worker(rank, world, port, q, device="cpu", offsets=None):
     dist.destroy_process_group()
 
 
-def _stacked_reference(keys, session):
+def _stacked_reference(keys, session, chunks=4):
     """The worker's program for both ring widths, in the same order (one nonce stream)."""
     from moose_amd.runtime.session import HV
     from moose_amd.runtime.session import StackedSession
 
     s = StackedSession("cpu", seed=1)
     s.fused = False
-    s.pipeline_chunks = 4
+    s.pipeline_chunks = chunks
     base = s.setup(PLC)
     s.keytable._write(base, keys)
     out = {}
@@ -106,11 +106,11 @@ def _stacked_reference(keys, session):
     return out
 
 
-def _run(world, device, offsets=None):
+def _run(world, device, offsets=None, chunks=4):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q, device, offsets)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, device, offsets, chunks)) for r in range(world)]
     for p in ps:
         p.start()
     got = {}
@@ -131,7 +131,7 @@ def _run(world, device, offsets=None):
     keys = got[0][1]
     refs = {}
     for s in range(world):
-        r = _stacked_reference(keys[s], s)
+        r = _stacked_reference(keys[s], s, chunks)
         refs.update({(s, b): r[b] for b in (64, 128)})
     for g in range(world):
         res, _, msgs = got[g]
@@ -162,6 +162,12 @@ def _run(world, device, offsets=None):
 @pytest.mark.parametrize("world", [2, 3, 4])
 def test_cyclic_bitwise_equals_stacked(world):
     _run(world, "cpu")
+
+
+def test_cyclic_unchunked_dealer_early():
+    """Unchunked dot_trunc: the dealer's rt1 / rm1 go out before the GEMM
+    (party.dealer_early) -- still bitwise the stacked session's shares."""
+    _run(3, "cpu", chunks=1)
 
 
 def test_cyclic_link_balanced_offsets():
