@@ -32,7 +32,7 @@ link -- without separating the parties):
 
 ``--step-streams S``: consecutive steps (independent sessions) alternate between S HIP
 streams, each with its own RCCL communicator, so one step's exchanges overlap the next
-step's GEMM (the reference runs independent operations as concurrent tasks).  Default 2 for
+step's GEMM (the reference runs independent operations as concurrent tasks).  Default 3 for
 the cyclic layout at N > 1, else 1.
 
 With several sessions, the revealed outputs of every session are collected on rank 0 (the
@@ -379,6 +379,13 @@ def _main(args, prog_out):
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but the launcher started {world} ranks")
+    if world > 1:
+        # enough HIP hardware queues for the step streams and their RCCL communicators'
+        # streams: two streams on one queue serialise (a step's exchange would wait behind
+        # the next step's whole GEMM; profiles/r3_stream_concurrency.md).  Read by the HIP
+        # runtime when it initialises, i.e. below.
+        q = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(16, max(q, 8)))
     prog = Progress(rank, world, args.watchdog, lambda: _base_line(args, world))
     prog_out.append(prog)
     # MOOSEX_SHARED_GPU=1: every rank on cuda:0 with gloo (rehearsing the multi-GPU
@@ -409,8 +416,12 @@ def _main(args, prog_out):
         raise SystemExit("--layout spmd needs a multiple of 3 GPUs (one per party)")
     nstreams = args.step_streams
     if nstreams is None:
+        # cyclic at N > 1: three steps in flight.  A step's dependency chain is its compute
+        # plus four message rounds (share, tail A, tail B, reveal: ~4-5 ms each for a
+        # 268 MB share tensor on one xGMI link), about twice its compute, so two streams
+        # would leave the GPU idle part of the time
         nstreams = int(os.environ.get("MOOSEX_BENCH_STREAMS",
-                                      "2" if layout == "cyclic" and world > 1 else "1"))
+                                      "3" if layout == "cyclic" and world > 1 else "1"))
     nstreams = max(1, nstreams)
 
     comp = build_computation(args.ring)
@@ -439,7 +450,7 @@ def _main(args, prog_out):
         # step k's transfer runs on the RCCL stream while step k+1 computes.
         if gather_mode == "all" or rank == root:
             gather_bufs = [torch.empty((n_sessions * n, n), dtype=torch.float64, device=device)
-                           for _ in range(2)]
+                           for _ in range(max(2, nstreams))]
         if gather_mode == "all" and layout == "spmd":  # the output owners of every session
             gather_group = dist.new_group(owners)
 
@@ -493,11 +504,11 @@ def _main(args, prog_out):
                 pending.pop(0).wait()
             zc = z.contiguous()
             if gather_mode == "all":
-                buf = gather_bufs[k % 2]
+                buf = gather_bufs[k % len(gather_bufs)]
                 pending.append(dist.all_gather_into_tensor(buf, zc, group=gather_group,
                                                            async_op=True))
             elif rank == root:
-                buf = gather_bufs[k % 2]
+                buf = gather_bufs[k % len(gather_bufs)]
                 ops = [dist.P2POp(dist.irecv, buf[i * n:(i + 1) * n], r)
                        for i, r in enumerate(owners) if r != root]
                 buf[owners.index(root) * n:(owners.index(root) + 1) * n].copy_(zc)
@@ -607,7 +618,7 @@ def _main(args, prog_out):
             check = {"rank": rank, "max_abs_err": (z - ref).abs().max().item()}
         if gather_bufs is not None and (gather_mode == "all" or rank == root):
             # the last step's collected outputs: rank r's revealed output is session s(r)'s
-            buf = gather_bufs[(n_steps[0] - 1) % 2]
+            buf = gather_bufs[(n_steps[0] - 1) % len(gather_bufs)]
             sess_of = {"cyclic": lambda r: (r - offsets[ROLES[2]]) % world,
                        "spmd": lambda r: r // 3,
                        "stacked": lambda r: r}[layout]
