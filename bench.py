@@ -32,7 +32,7 @@ link -- without separating the parties):
 
 ``--step-streams S``: consecutive steps (independent sessions) alternate between S HIP
 streams, each with its own RCCL communicator, so one step's exchanges overlap the next
-step's GEMM (the reference runs independent operations as concurrent tasks).  Default 3 for
+step's GEMM (the reference runs independent operations as concurrent tasks).  Default 2 for
 the cyclic layout at N > 1, else 1.
 
 With several sessions, the revealed outputs of every session are collected on rank 0 (the
@@ -416,12 +416,13 @@ def _main(args, prog_out):
         raise SystemExit("--layout spmd needs a multiple of 3 GPUs (one per party)")
     nstreams = args.step_streams
     if nstreams is None:
-        # cyclic at N > 1: three steps in flight.  A step's dependency chain is its compute
+        # cyclic at N > 1: two steps in flight.  A step's dependency chain is its compute
         # plus four message rounds (share, tail A, tail B, reveal: ~4-5 ms each for a
-        # 268 MB share tensor on one xGMI link), about twice its compute, so two streams
-        # would leave the GPU idle part of the time
+        # 268 MB share tensor on one xGMI link), about twice its compute.  A third stream
+        # would cover a slower link, but three steps computing at once cost 4.5 % on the
+        # GPU (one GPU, no messages: 16.33 ms with 2 streams, 17.08 ms with 3)
         nstreams = int(os.environ.get("MOOSEX_BENCH_STREAMS",
-                                      "3" if layout == "cyclic" and world > 1 else "1"))
+                                      "2" if layout == "cyclic" and world > 1 else "1"))
     nstreams = max(1, nstreams)
 
     comp = build_computation(args.ring)
