@@ -454,6 +454,10 @@ def _main(args, prog_out):
                            for _ in range(max(2, nstreams))]
         if gather_mode == "all" and layout == "spmd":  # the output owners of every session
             gather_group = dist.new_group(owners)
+        elif world > 1 and layout != "spmd":
+            # a communicator of its own: on the step streams' communicator the collection of
+            # step k would sit in front of step k+2's exchanges (one RCCL stream each)
+            gather_group = dist.new_group(list(range(world)))
 
     streams = ([torch.cuda.Stream(device) for _ in range(nstreams)]
                if device.type == "cuda" and nstreams > 1 else None)
@@ -510,12 +514,13 @@ def _main(args, prog_out):
                                                            async_op=True))
             elif rank == root:
                 buf = gather_bufs[k % len(gather_bufs)]
-                ops = [dist.P2POp(dist.irecv, buf[i * n:(i + 1) * n], r)
+                ops = [dist.P2POp(dist.irecv, buf[i * n:(i + 1) * n], r, group=gather_group)
                        for i, r in enumerate(owners) if r != root]
                 buf[owners.index(root) * n:(owners.index(root) + 1) * n].copy_(zc)
                 pending.extend(dist.batch_isend_irecv(ops))
             else:
-                pending.extend(dist.batch_isend_irecv([dist.P2POp(dist.isend, zc, root)]))
+                pending.extend(dist.batch_isend_irecv(
+                    [dist.P2POp(dist.isend, zc, root, group=gather_group)]))
         n_steps[0] += 1
         return z
 
