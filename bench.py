@@ -431,9 +431,10 @@ def _main(args, prog_out):
         n_sessions, out_owner = world // 3, rank % 3 == 2
         xs, ys, out_session = rank // 3, rank // 3, rank // 3
     elif layout == "cyclic":  # rank g hosts role r of session g - o(r) (cyclic.py)
-        from moose_amd.parallel.cyclic import default_offsets
+        from moose_amd.parallel.cyclic import default_layout
 
-        offsets = default_offsets(ROLES, world)
+        # link-balanced party offsets and input-share directions for this program
+        offsets, share_dirs = default_layout(ROLES, world)
         n_sessions, out_owner = world, True
         xs, ys, out_session = [(rank - offsets[r]) % world for r in ROLES]
     else:
@@ -481,7 +482,7 @@ def _main(args, prog_out):
         comms = [RingComm(rank, world, device, group=g) for g in groups]
 
         def new_session(k):
-            return CyclicSession(comms[k % len(comms)], offsets, device)
+            return CyclicSession(comms[k % len(comms)], offsets, device, share_dirs=share_dirs)
     else:
         comms = []
 

@@ -23,7 +23,9 @@ enum mx_cross { MX_CROSS_ARITH = 0, MX_CROSS_BOOL = 1 };
 // share kernels (mx_share3*, mx_share_party): kind MX_SHARE_F64 = an arithmetic sharing of a
 // float64 input, fixed-point encoded in the kernel (x * 2^na, truncated as RingFixedpointEncode);
 // the nonce argument na carries the fractional bits (the zero slot draws no randomness)
-enum mx_share_src { MX_SHARE_F64 = 2 };
+// kind | MX_SHARE_MIRROR: the masked slot goes to P_{j+2} instead of P_{j+1} (slot j =
+// x - PRF(k_{j+1}), slot j+1 = PRF(k_{j+1}), slot j+2 = 0; the key argument is k_{j+1})
+enum mx_share_src { MX_SHARE_F64 = 2, MX_SHARE_MIRROR = 8 };
 
 // AES-128 key schedule: 11 round keys of 4 big-endian-packed words (FIPS-197 layout)
 typedef struct {

@@ -107,6 +107,8 @@ template <class T>
 __global__ void __launch_bounds__(256) k_share3(int kind, const void* __restrict__ xv, T* __restrict__ out0,
                          T* __restrict__ out1, int64_t n, int j0, mxd::KeySrc keys, uint64_t n1,
                          uint64_t na) {
+  const bool mir = kind & MX_SHARE_MIRROR;
+  kind &= ~MX_SHARE_MIRROR;
   const T* x = (const T*)xv;
   const double* xf = (const double*)xv;  // kind MX_SHARE_F64: encode in the kernel
   const double scale = kind == MX_SHARE_F64 ? ldexp(1.0, (int)na) : 0.0;
@@ -123,9 +125,10 @@ __global__ void __launch_bounds__(256) k_share3(int kind, const void* __restrict
       if (i >= n) break;
       const T r = mxd::pick<T>(lo[0], hi[0], j);
       const T xi = kind == MX_SHARE_F64 ? (T)mxr::f64_to_i128(xf[i] * scale) : x[i];
+      const T v = kind == MX_CROSS_BOOL ? (T)(xi ^ r) : (T)(xi - r);
       T slot[3];
-      slot[j0] = r;
-      slot[(j0 + 1) % 3] = kind == MX_CROSS_BOOL ? (T)(xi ^ r) : (T)(xi - r);
+      slot[j0] = mir ? v : r;
+      slot[(j0 + 1) % 3] = mir ? r : v;
       slot[(j0 + 2) % 3] = 0;
       const bool ring4 = out1 == out0 + n;  // 4-slot ring: out1's slots 0, 1 are out0's 1, 2
 #pragma unroll

@@ -70,6 +70,8 @@ int trunc3_host(const T* s0, T* out0, T* out1, int64_t n, int m, const uint8_t* 
 template <class T>
 int share3_host(int kind, const void* xv, T* out0, T* out1, int64_t n, int j, const uint8_t* kn,
                 const uint8_t* /*ka: unused*/, uint64_t n1, uint64_t na) {
+  const bool mir = kind & MX_SHARE_MIRROR;
+  kind &= ~MX_SHARE_MIRROR;
   const int words = sizeof(T) == 1 ? 0 : (int)(sizeof(T) / 8);
   const T* x = (const T*)xv;
   const double* xf = (const double*)xv;  // kind MX_SHARE_F64 (moosex.h)
@@ -83,9 +85,10 @@ int share3_host(int kind, const void* xv, T* out0, T* out1, int64_t n, int j, co
       for (int64_t t = 0; t < len; ++t) {
         int64_t i = c + t;
         const T xi = kind == MX_SHARE_F64 ? (T)mxr::f64_to_i128(xf[i] * scale) : x[i];
+        const T v = kind == MX_CROSS_BOOL ? (T)(xi ^ r1[t]) : (T)(xi - r1[t]);
         T slot[3];
-        slot[j] = r1[t];
-        slot[(j + 1) % 3] = kind == MX_CROSS_BOOL ? (T)(xi ^ r1[t]) : (T)(xi - r1[t]);
+        slot[j] = mir ? v : r1[t];
+        slot[(j + 1) % 3] = mir ? r1[t] : v;
         slot[(j + 2) % 3] = 0;
         for (int p = 0; p < 3; ++p) {
           out0[p * n + i] = slot[p];

@@ -193,50 +193,57 @@ template <class T>
 __global__ void __launch_bounds__(256)
     k_share_party(int kind, int64_t n, Roles rel, const void* __restrict__ xv, T* __restrict__ out0,
                   T* __restrict__ out1, mxd::KeySrc keys, uint64_t n1, uint64_t na, int ncomp) {
+  const bool mir = kind & MX_SHARE_MIRROR;
+  kind &= ~MX_SHARE_MIRROR;
   const T* x = (const T*)xv;
   const double* xf = (const double*)xv;  // kind MX_SHARE_F64: encode in the kernel
   const double scale = kind == MX_SHARE_F64 ? ldexp(1.0, (int)na) : 0.0;
   __shared__ uint32_t rks[mxd::kMaxKeySlots][mxd::kKeyWords];
   // keys: 2 per component, the first used: k_j of the owner j (rel 0: own, rel 2: next).
   // As the reference (replicated/convert.rs:74-90): slot j = PRF(k_j), slot j+1 = x - slot j
-  // (sent to P_{j+1}), slot j+2 = 0, so rel 1 draws nothing
+  // (sent to P_{j+1}), slot j+2 = 0, so rel 1 draws nothing.  Mirrored (MX_SHARE_MIRROR):
+  // slot j+1 = PRF(k_{j+1}) (rel 0: next, rel 1: own), slot j = x - slot j+1 (sent to
+  // P_{j+2}), slot j+2 = 0, so rel 2 draws nothing
   mxd::stage_keys(rks, keys, 2 * ncomp);
   constexpr int P = mxd::Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;
   MX_PARTY_WALK(nb, ncomp) {
     const int c = (int)(g / nblk);
     const uint64_t B = (uint64_t)(g - c * nblk);
-    // rel code: the role relative to the owner (0..2) + 4 * (1 + the component of P_{j+1})
-    // when the owner's masked share stays on this device (written straight into its s0)
+    // rel code: the role relative to the owner (0..2) + 4 * (1 + the component of the
+    // recipient P_{j+1}, mirrored P_{j+2}) when the owner's masked share stays on this device
+    // (written straight into its s0, mirrored its s1)
     const int code = rel.r[c];
     if (code < 0) continue;
     const int r = code & 3, fwd = (code >> 2) - 1;
     const int64_t base = (int64_t)c * n;
     if (r > 2) continue;
+    const bool draws = mir ? r != 2 : r != 1;
     uint32_t wa[16];
-    if (r != 1) mx::chacha_block(rks[2 * c], n1, B, wa);
+    if (draws) mx::chacha_block(rks[2 * c], n1, B, wa);
 #pragma unroll
     for (int part = 0; part < 4; ++part) {
       const int64_t b = (int64_t)mx::ks_chunk(B, part);
       if (b >= nb) break;
       uint64_t al = 0, ah = 0;
-      if (r != 1) mx::part_u64(wa, part, &al, &ah);
+      if (draws) mx::part_u64(wa, part, &al, &ah);
 #pragma unroll
       for (int j = 0; j < P; ++j) {
         const int64_t i = b * P + j;
         if (i >= n) break;
         const T rr = mxd::pick<T>(al, ah, j);
-        if (r == 0) {  // owner: (slot j, slot j+1) = (PRF(k_j), x - PRF(k_j))
+        if (r == 0) {  // owner: (PRF(k_j), x - PRF(k_j)); mirrored (x - PRF(k_{j+1}), PRF)
           const T xi = kind == MX_SHARE_F64 ? (T)mxr::f64_to_i128(xf[i] * scale) : x[i];
           const T v = kind == MX_CROSS_BOOL ? (T)(xi ^ rr) : (T)(xi - rr);
-          out0[base + i] = rr;
-          out1[base + i] = v;
-          if (fwd >= 0) out0[(int64_t)fwd * n + i] = v;
-        } else if (r == 1) {  // P_{j+1}: s0 arrives from the owner, slot j+2 is zero
+          out0[base + i] = mir ? v : rr;
+          out1[base + i] = mir ? rr : v;
+          if (fwd >= 0) (mir ? out1 : out0)[(int64_t)fwd * n + i] = v;
+        } else if (r == 1) {  // P_{j+1}: (received, 0); mirrored (PRF(k_{j+1}), 0)
+          if (mir) out0[base + i] = rr;
           out1[base + i] = 0;
-        } else {  // P_{j+2}: (0, PRF(k_j))
+        } else {  // P_{j+2}: (0, PRF(k_j)); mirrored (0, received)
           out0[base + i] = 0;
-          out1[base + i] = rr;
+          if (!mir) out1[base + i] = rr;
         }
       }
     }

@@ -139,6 +139,8 @@ int trunc_r1(int64_t n, int m, int ncomp, const int* roles, const T* msg, const 
 template <class T>
 int share_party(int kind, int64_t n, int ncomp, const int* rel, const void* xp, T* out0, T* out1,
                 const uint32_t* const* slots, uint64_t n1, uint64_t na) {
+  const bool mir = kind & MX_SHARE_MIRROR;
+  kind &= ~MX_SHARE_MIRROR;
   const T* x = (const T*)xp;
   const double* xf = (const double*)xp;  // kind MX_SHARE_F64 (moosex.h)
   const double scale = kind == MX_SHARE_F64 ? std::ldexp(1.0, (int)na) : 0.0;
@@ -150,20 +152,22 @@ int share_party(int kind, int64_t n, int ncomp, const int* rel, const void* xp, 
     if (r > 2) continue;
     for_chunks<T>(n, [&](int64_t i0, int64_t len) {
       std::vector<T> a(len);
-      if (r != 1) prf<T>(slots[2 * c], n1, i0, len, a.data());
+      if (mir ? r != 2 : r != 1) prf<T>(slots[2 * c], n1, i0, len, a.data());
       for (int64_t q = 0; q < len; ++q) {
         const int64_t i = base + i0 + q;
         if (r == 0) {
           const T xv =
               kind == MX_SHARE_F64 ? (T)mxr::f64_to_i128(xf[i0 + q] * scale) : x[i0 + q];
-          out0[i] = a[q];
-          out1[i] = kind == MX_CROSS_BOOL ? (T)(xv ^ a[q]) : (T)(xv - a[q]);
-          if (fwd >= 0) out0[(int64_t)fwd * n + i0 + q] = out1[i];
+          const T v = kind == MX_CROSS_BOOL ? (T)(xv ^ a[q]) : (T)(xv - a[q]);
+          out0[i] = mir ? v : a[q];
+          out1[i] = mir ? a[q] : v;
+          if (fwd >= 0) (mir ? out1 : out0)[(int64_t)fwd * n + i0 + q] = v;
         } else if (r == 1) {
-          out1[i] = 0;  // s0 arrives from the owner
+          if (mir) out0[i] = a[q];
+          out1[i] = 0;  // s0 arrives from the owner (mirrored: zero slot j+2)
         } else {
           out0[i] = 0;
-          out1[i] = a[q];
+          if (!mir) out1[i] = a[q];  // mirrored: s1 arrives from the owner
         }
       }
     });

@@ -1531,7 +1531,10 @@ def trunc_party_r1(msg, rmk, rrt, rrm, out0, out1, bits, m, roles, slots, nonces
     return w
 
 
-def share_party(kind: str, x: RT, ncomp: int, rel, slots, n1: int, na: int):
+SHARE_MIRROR = 8  # MX_SHARE_MIRROR (moosex.h): the masked slot goes to P_{j+2}
+
+
+def share_party(kind: str, x: RT, ncomp: int, rel, slots, n1: int, na: int, mirror=False):
     """Per-component slots of a sharing by member j (mx_share_party); the owner's out1
     (slot x_{j+1}) is the message to P_{j+1} (whose out0 it becomes).  A pending
     :class:`Encoded` input is encoded inside the kernel."""
@@ -1540,7 +1543,7 @@ def share_party(kind: str, x: RT, ncomp: int, rel, slots, n1: int, na: int):
     out0, out1 = empty2((ncomp,) + tuple(x.shape), x.bits, xd.device)
     out0, out1 = out0.data, out1.data
     nat.check(nat.lib().mx_share_party(
-        nat.dev_of(xd), code, _words(x.bits), x.numel(), ncomp,
+        nat.dev_of(xd), code | (SHARE_MIRROR if mirror else 0), _words(x.bits), x.numel(), ncomp,
         _roles_arr(rel), nat.ptr(xd), nat.ptr(out0), nat.ptr(out1), _slots_arr(slots),
         n1 & MASK64, na & MASK64, nat.stream_of(xd)), "share_party")
     return out0, out1

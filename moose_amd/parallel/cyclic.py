@@ -125,12 +125,20 @@ class RingComm:
             out.copy_(buf, non_blocking=True)
 
 
-# Per-step traffic between the three parties of one session of the dot-product program
-# (x owned by party 0, y by party 1, output revealed to party 2), in units of one share
-# tensor of the output: input shares (owner j -> P_{j+1}), the folded dot tail
-# (parallel/party.py: m0, w0 0->1; m1, w1 1->0; z2 2->0 and 2->1; rt1, rm1 2->1) and the
-# reveal (P0 -> P2).
-TRAFFIC = {(0, 1): 3.0, (1, 0): 2.0, (2, 0): 1.0, (2, 1): 2.5, (0, 2): 1.0, (1, 2): 1.0}
+def dot_traffic(dirs=(1, 1)):
+    """Per-step traffic between the three parties of one session of the dot-product program
+    (x owned by party 0, y by party 1, output revealed to party 2), in units of one share
+    tensor of the output: the input shares (owner j -> P_{j+d}, d = its share direction),
+    the folded dot tail (parallel/party.py: m0, w0 0->1; m1, w1 1->0; z2 2->0 and 2->1;
+    rt1, rm1 2->1) and the reveal (P0 -> P2)."""
+    f = {(0, 1): 2.0, (1, 0): 2.0, (2, 0): 1.0, (2, 1): 2.5, (0, 2): 1.0}
+    for owner, d in ((0, dirs[0]), (1, dirs[1])):
+        key = (owner, (owner + d) % 3)
+        f[key] = f.get(key, 0.0) + 1.0
+    return f
+
+
+TRAFFIC = dot_traffic()
 
 
 def link_loads(offsets: Sequence[int], world: int, traffic=None) -> Dict[int, float]:
@@ -144,9 +152,38 @@ def link_loads(offsets: Sequence[int], world: int, traffic=None) -> Dict[int, fl
     return load
 
 
+def default_layout(roles: Sequence[str], world: int = None):
+    """(offsets, share directions) of the roles for the dot-product program on ``world``
+    GPUs: the pair minimising the busiest link (:func:`dot_traffic`, :func:`link_loads`);
+    ties keep the reference's share direction.  E.g. 8 GPUs: offsets (0, 1, 3) and x shared
+    towards P_{j+2}: every flow on its own link, the busiest one 2.5 units instead of 3."""
+    n = len(roles)
+    off = default_offsets(roles, world)
+    if world is None or world < 4 or n < 3:
+        return off, {}
+    best = None
+    for dx in (1, 2):
+        for dy in (1, 2):
+            fl = dot_traffic((dx, dy))
+            for o1 in range(1, world):
+                for o2 in range(1, world):
+                    if o1 == o2:
+                        continue
+                    o = (0, o1, o2)
+                    key = (max(link_loads(o, world, fl).values()), (dx, dy) != (1, 1), dx, dy, o)
+                    if best is None or key < best[0]:
+                        best = (key, o, dx, dy)
+    _, o, dx, dy = best
+    rest = [k for k in range(max(world, n)) if k not in o]
+    offsets = {r: v for r, v in zip(roles, list(o) + rest[:n - 3])}
+    dirs = {r: d for r, d in ((roles[0], dx), (roles[1], dy)) if d != 1}
+    return offsets, dirs
+
+
 def default_offsets(roles: Sequence[str], world: int = None) -> Dict[str, int]:
     """Offsets of the roles (module doc): 0, 1, 2, ... unless ``world`` GPUs allow a
-    link-balanced choice.
+    link-balanced choice (for the reference's share direction; :func:`default_layout`
+    chooses the share directions too).
 
     xGMI is point to point -- every GPU pair has its own link (≈50-64 GB/s per direction
     under RCCL) -- so the step time of a communication-heavy program is set by the busiest
@@ -178,8 +215,10 @@ class CyclicSession(StackedSession):
     KEY_SLOTS = 9      # per placement: for each component p: k_p, k_{p+1}, k_all
 
     def __init__(self, comm: RingComm, offsets: Dict[str, int], device="cpu", seed=None,
-                 pipeline_chunks=None):
+                 pipeline_chunks=None, share_dirs=None):
         super().__init__(device, seed)
+        if share_dirs:
+            self.share_dirs = dict(share_dirs)
         self.comm = comm
         if pipeline_chunks is None:
             # row-chunked dot pipeline (rep.dot_trunc): off by default -- chunking re-reads
@@ -374,23 +413,27 @@ class CyclicSession(StackedSession):
 
     def party_share(self, plc, x, j, kind, n1, na):
         """Input sharing by member j: one kernel for every component's slots, then the
-        owner's masked slot x_{j+1} goes to P_{j+1} (received straight into its s0)."""
+        owner's masked slot goes to its recipient -- x_{j+1} to P_{j+1} (its s0), or,
+        mirrored (share_dir 2), x_j to P_{j+2} (its s1)."""
         bits = x.v.bits
+        d = self.share_dir(plc, j)
         rel = [(c - j) % 3 for c in range(3)]
         slots = []
-        for c in range(3):  # the kernels read k_j: the owner's own key, P_{j+2}'s next key
-            w = {0: (0, 2), 1: (0, 2), 2: (1, 2)}[rel[c]]
+        for c in range(3):  # the PRF key: k_j (owner: own, P_{j+2}: next), mirrored k_{j+1}
+            w = ({0: (0, 2), 1: (0, 2), 2: (1, 2)} if d == 1 else
+                 {0: (1, 2), 1: (0, 2), 2: (0, 2)})[rel[c]]
             slots += [self._slot(plc, c, w[0]), self._slot(plc, c, w[1])]
         o = [self.offset(r) for r in plc.owners]
-        j1 = (j + 1) % 3
-        local = (o[j1] - o[j]) % self.N == 0  # P_{j+1} of the owner's session is here
-        if local:  # the kernel writes the owner's masked slot into P_{j+1}'s s0 too
-            rel[j] += 4 * (1 + j1)
-        out0, out1 = R.share_party(kind, x.v, 3, rel, slots, n1, na)
+        jr = (j + d) % 3
+        local = (o[jr] - o[j]) % self.N == 0  # the recipient of the owner's session is here
+        if local:  # the kernel writes the owner's masked slot into the recipient's share too
+            rel[j] += 4 * (1 + jr)
+        out0, out1 = R.share_party(kind, x.v, 3, rel, slots, n1, na, mirror=d == 2)
         if not local:
-            self.comm.exchange([(out1[j], self._peer(o[j1] - o[j]))],
-                               [(out0[j1], self._peer(o[j] - o[j1]))])
-        self.stats.record_send(x.host, plc.owners[j1], _nbytes(x.v))
+            src, dst = (out1[j], out0[jr]) if d == 1 else (out0[j], out1[jr])
+            self.comm.exchange([(src, self._peer(o[jr] - o[j]))],
+                               [(dst, self._peer(o[j] - o[jr]))])
+        self.stats.record_send(x.host, plc.owners[jr], _nbytes(x.v))
         return PV(plc, R.RT(out0, bits)), PV(plc, R.RT(out1, bits))
 
     def party_exchange(self, plc, specs):

@@ -89,15 +89,23 @@ def share(sess, plc, x: HV, kind="arith") -> RepTensor:
         if party is not None and bits in (64, 128):
             s0, s1 = party(plc, x, j, kind, n1, na)
             return RepTensor(plc, bits, kind, s0, s1)
-        # as the reference (replicated/convert.rs:74-90): slot_j = PRF(k_j) [P_j, P_{j+2}],
-        # slot_{j+1} = x - slot_j [P_j, sent to P_{j+1}], slot_{j+2} = 0.  Each single
-        # party other than the owner still misses one random slot
-        r_j = sess.h_prf(plc, o[j], j, shape, bits, n1)
-        r_j2 = sess.h_prf(plc, o[j2], j, shape, bits, n1)
-        xj1 = sess.h(sub, o[j], x, r_j)
-        comp0 = {j: r_j, j1: sess.move(xj1, o[j1]),
-                 j2: sess.h("Fill", o[j2], shape, value=0, bits=bits)}
-        comp1 = {j: xj1, j1: sess.h("Fill", o[j1], shape, value=0, bits=bits), j2: r_j2}
+        d = sess.share_dir(plc, j) if hasattr(sess, "share_dir") else 1
+        zero = lambda h: sess.h("Fill", o[h], shape, value=0, bits=bits)  # noqa: E731
+        if d == 1:
+            # as the reference (replicated/convert.rs:74-90): slot_j = PRF(k_j) [P_j,
+            # P_{j+2}], slot_{j+1} = x - slot_j [P_j, sent to P_{j+1}], slot_{j+2} = 0.
+            # Each single party other than the owner still misses one random slot
+            r_j = sess.h_prf(plc, o[j], j, shape, bits, n1)
+            r_j2 = sess.h_prf(plc, o[j2], j, shape, bits, n1)
+            xj1 = sess.h(sub, o[j], x, r_j)
+            comp0 = {j: r_j, j1: sess.move(xj1, o[j1]), j2: zero(j2)}
+            comp1 = {j: xj1, j1: zero(j1), j2: r_j2}
+        else:  # mirrored: slot_{j+1} = PRF(k_{j+1}) [P_j, P_{j+1}], slot_j -> P_{j+2}
+            r_j = sess.h_prf(plc, o[j], j1, shape, bits, n1)
+            r_j1 = sess.h_prf(plc, o[j1], j1, shape, bits, n1)
+            xj = sess.h(sub, o[j], x, r_j)
+            comp0 = {j: xj, j1: r_j1, j2: zero(j2)}
+            comp1 = {j: r_j, j1: zero(j1), j2: sess.move(xj, o[j2])}
         s0 = sess.gather(plc, [comp0[i] for i in range(3)])
         s1 = sess.gather(plc, [comp1[i] for i in range(3)])
         return RepTensor(plc, bits, kind, s0, s1)

@@ -83,6 +83,14 @@ def _nbytes(v):
 class Session:
     """Common bookkeeping; see subclasses."""
 
+    # input sharing: the owner's masked slot goes to P_{j+1} (1, the reference's direction,
+    # replicated/convert.rs:74-90) or to P_{j+2} (2, mirrored); per owner role, set by a
+    # layout that balances its links (parallel/cyclic.py default_layout)
+    share_dirs: dict = {}
+
+    def share_dir(self, plc, j) -> int:
+        return self.share_dirs.get(plc.owners[j], 1)
+
     nb_party = 0
 
     def __init__(self, device="cpu", seed: Optional[int] = None):
@@ -647,18 +655,19 @@ class StackedSession(Session):
         from moose_amd.ops import native as nat
 
         code, xd, aux = R.share_source(x.v, kind)  # a pending encoding: encoded in-kernel
+        d = self.share_dir(plc, j)
         out0, out1 = (t.data for t in R.ring4((3,) + tuple(x.v.shape), x.v.bits, xd.device))
         nat.check(
             nat.lib().mx_share3_k(
-                nat.dev_of(xd), code, R._words(x.v.bits), nat.ptr(xd),
-                nat.ptr(out0), nat.ptr(out1), x.v.numel(), j,
-                ctypes.c_void_p(self.key_ptr(plc, j)),
+                nat.dev_of(xd), code | (R.SHARE_MIRROR if d == 2 else 0), R._words(x.v.bits),
+                nat.ptr(xd), nat.ptr(out0), nat.ptr(out1), x.v.numel(), j,
+                ctypes.c_void_p(self.key_ptr(plc, (j + d - 1) % 3)),
                 ctypes.c_void_p(self.key_ptr(plc, 3)), n1, na if aux is None else aux,
                 nat.stream_of(xd),
             ),
             "share3",
         )
-        self.stats.record_send(x.host, plc.owners[(j + 1) % 3], _nbytes(x.v))
+        self.stats.record_send(x.host, plc.owners[(j + d) % 3], _nbytes(x.v))
         return PV(plc, R.RT(out0, x.v.bits)), PV(plc, R.RT(out1, x.v.bits))
 
     def mirror(self, x: HV, plc):

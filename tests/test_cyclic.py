@@ -59,7 +59,7 @@ def _program(sess, xb, ya, mb, ma):
     return tensors, (out.v.data.clone(), dt.v.data.clone())
 
 
-def _worker(rank, world, port, q, device="cpu", offsets=None, chunks=4):
+def _worker(rank, world, port, q, device="cpu", offsets=None, chunks=4, dirs=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from moose_amd.parallel.cyclic import CyclicSession
@@ -68,7 +68,7 @@ def _worker(rank, world, port, q, device="cpu", offsets=None, chunks=4):
 
     sess = CyclicSession(RingComm(rank, world, device), offsets or {"a": 0, "b": 1, "c": 2},
                          seed=SEED,
-                         device=device, pipeline_chunks=chunks)
+                         device=device, pipeline_chunks=chunks, share_dirs=dirs)
     res = {}
     for bits in (64, 128):
         xd, yd = _data(sess.session_of("b"), bits), _data(100 + sess.session_of("a"), bits)
@@ -87,7 +87,7 @@ def _worker(rank, world, port, q, device="cpu", offsets=None, chunks=4):
     dist.destroy_process_group()
 
 
-def _stacked_reference(keys, session, chunks=4):
+def _stacked_reference(keys, session, chunks=4, dirs=None):
     """The worker's program for both ring widths, in the same order (one nonce stream)."""
     from moose_amd.runtime.session import HV
     from moose_amd.runtime.session import StackedSession
@@ -95,6 +95,8 @@ def _stacked_reference(keys, session, chunks=4):
     s = StackedSession("cpu", seed=1)
     s.fused = False
     s.pipeline_chunks = chunks
+    if dirs:
+        s.share_dirs = dirs
     base = s.setup(PLC)
     s.keytable._write(base, keys)
     out = {}
@@ -106,11 +108,11 @@ def _stacked_reference(keys, session, chunks=4):
     return out
 
 
-def _run(world, device, offsets=None, chunks=4):
+def _run(world, device, offsets=None, chunks=4, dirs=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q, device, offsets, chunks)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, device, offsets, chunks, dirs)) for r in range(world)]
     for p in ps:
         p.start()
     got = {}
@@ -131,7 +133,7 @@ def _run(world, device, offsets=None, chunks=4):
     keys = got[0][1]
     refs = {}
     for s in range(world):
-        r = _stacked_reference(keys[s], s, chunks)
+        r = _stacked_reference(keys[s], s, chunks, dirs)
         refs.update({(s, b): r[b] for b in (64, 128)})
     for g in range(world):
         res, _, msgs = got[g]
@@ -168,6 +170,12 @@ def test_cyclic_unchunked_dealer_early():
     """Unchunked dot_trunc: the dealer's rt1 / rm1 go out before the GEMM
     (party.dealer_early) -- still bitwise the stacked session's shares."""
     _run(3, "cpu", chunks=1)
+
+
+def test_cyclic_mirrored_share_direction():
+    """Input sharing towards P_{j+2} (share_dir 2, as default_layout picks on 8 GPUs) for
+    owner b, unchunked tail: bitwise the stacked session's shares under the same choice."""
+    _run(4, "cpu", {"a": 0, "b": 1, "c": 3}, chunks=1, dirs={"b": 2})
 
 
 def test_cyclic_link_balanced_offsets():
