@@ -235,7 +235,7 @@ class GraphPlan:
                 # pinned buffer followed by a blit (0.321 ms; profiles/r3_graphs_vs_eager.md)
                 src = torch.from_numpy(np.ascontiguousarray(a).reshape(t.shape))
                 t.copy_(src if src.dtype == t.dtype else src.to(t.dtype))
-        self.keys.refresh()  # fresh randomness for this replay
+        self.keys.refresh(self.keys.n)  # fresh randomness for this replay (the used slots)
         for g in self.graphs:
             g.replay()
         self.replays += 1
