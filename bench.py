@@ -209,7 +209,7 @@ def _revision():
 # ---------------------------------------------------------------------------------------
 # preflight: one grouped round trip with every peer on every communicator
 # ---------------------------------------------------------------------------------------
-def _preflight(layout, comms, world, rank, device, prog):
+def _preflight(layout, comms, world, rank, device, prog, offsets=None):
     """Each rank sends its rank id to every peer it will exchange with and checks what it
     receives (catches a wrong peer map, a dead link or an RCCL set-up hang before the
     measured work starts).  Returns a short record for the JSON line."""
@@ -226,9 +226,7 @@ def _preflight(layout, comms, world, rank, device, prog):
             raise RuntimeError(f"preflight all_reduce gave {one.item()} on {world} ranks")
     peers = []
     if layout == "cyclic" and world > 1:
-        from moose_amd.parallel.cyclic import default_offsets
-
-        off = list(default_offsets(ROLES, world).values())
+        off = list(offsets.values())
         dists = sorted({(b - a) % world for a in off for b in off} - {0})
         for k, comm in enumerate(comms):
             prog.tick(1 + k)
@@ -540,7 +538,8 @@ def _main(args, prog_out):
             dist.barrier()
 
     prog.phase("preflight", min(args.watchdog, 180))
-    preflight = _preflight(layout, comms, world, rank, device, prog)
+    preflight = _preflight(layout, comms, world, rank, device, prog,
+                           offsets if layout == "cyclic" else None)
 
     prog.phase("warmup", args.watchdog)
     for i in range(args.warmup):

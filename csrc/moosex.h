@@ -102,9 +102,9 @@ int mx_ring_inject(int dev, int words, const uint8_t* bits, void* out, int64_t n
 int mx_encode(int dev, int words, const double* x, void* out, int64_t n, int frac,
               void* stream);
 // out[i] = signed(x[i]) / 2^frac
-// decode(a + b + c): a reveal's three shares summed and decoded in one pass
-int mx_add3_decode(int dev, int words, const void* a, const void* b, const void* c, double* out,
-                   int64_t n, int frac, void* stream);
+// decode(a + b + c [+ d]): a reveal's shares summed and decoded in one pass (d may be null)
+int mx_addn_decode(int dev, int words, const void* a, const void* b, const void* c,
+                   const void* d, double* out, int64_t n, int frac, void* stream);
 int mx_decode(int dev, int words, const void* x, double* out, int64_t n, int frac,
               void* stream);
 // out[i] = value (lo word, hi word for Z_2^128; low byte for bits)

@@ -167,8 +167,8 @@ int mxh_ring_inject(int words, const uint8_t* bits, void* out, int64_t n, int bi
                     void* stream);
 int mxh_encode(int words, const double* x, void* out, int64_t n, int frac, void* stream);
 int mxh_decode(int words, const void* x, double* out, int64_t n, int frac, void* stream);
-int mxh_add3_decode(int words, const void* a, const void* b, const void* c, double* out,
-                    int64_t n, int frac, void* stream);
+int mxh_addn_decode(int words, const void* a, const void* b, const void* c, const void* d,
+                    double* out, int64_t n, int frac, void* stream);
 int mxh_fill(int words, void* out, int64_t n, uint64_t lo, uint64_t hi, void* stream);
 int mxh_bit_planes(int words, const void* a, uint8_t* out, int64_t outer, int64_t inner,
                    int start, int count, void* stream);

@@ -544,21 +544,24 @@ int mx_encode(int dev, int words, const double* x, void* out, int64_t n, int fra
   return -2;
 }
 
-int mx_add3_decode(int dev, int words, const void* a, const void* b, const void* c, double* out,
-                   int64_t n, int frac, void* stream) {
-  if (dev) return mxh_add3_decode(words, a, b, c, out, n, frac, stream);
+int mx_addn_decode(int dev, int words, const void* a, const void* b, const void* c,
+                   const void* d, double* out, int64_t n, int frac, void* stream) {
+  if (dev) return mxh_addn_decode(words, a, b, c, d, out, n, frac, stream);
   const double scale = std::ldexp(1.0, -frac);
   if (words == 1) {
-    const u64 *x = (const u64*)a, *y = (const u64*)b, *z = (const u64*)c;
+    const u64 *x = (const u64*)a, *y = (const u64*)b, *z = (const u64*)c, *w = (const u64*)d;
     parallel_for(n, 1 << 16, [&](int64_t s, int64_t e) {
-      for (int64_t i = s; i < e; ++i) out[i] = (double)(int64_t)(x[i] + y[i] + z[i]) * scale;
+      for (int64_t i = s; i < e; ++i)
+        out[i] = (double)(int64_t)(x[i] + y[i] + z[i] + (w ? w[i] : 0)) * scale;
     });
     return 0;
   }
   if (words == 2) {
-    const u128 *x = (const u128*)a, *y = (const u128*)b, *z = (const u128*)c;
+    const u128 *x = (const u128*)a, *y = (const u128*)b, *z = (const u128*)c,
+               *w = (const u128*)d;
     parallel_for(n, 1 << 16, [&](int64_t s, int64_t e) {
-      for (int64_t i = s; i < e; ++i) out[i] = mxr::i128_to_f64(x[i] + y[i] + z[i]) * scale;
+      for (int64_t i = s; i < e; ++i)
+        out[i] = mxr::i128_to_f64(x[i] + y[i] + z[i] + (w ? w[i] : (u128)0)) * scale;
     });
     return 0;
   }

@@ -311,15 +311,17 @@ __global__ void __launch_bounds__(256) k_decode(const T* __restrict__ x, double*
   }
 }
 
-// decode(a + b + c): the reveal's add and the decode in one pass (no ring-valued sum in HBM)
+// decode(a + b + c [+ d]): the reveal's add and the decode in one pass (no ring-valued sum in
+// HBM); d may be null
 template <class T>
-__global__ void __launch_bounds__(256) k_add3_decode(const T* __restrict__ a, const T* __restrict__ b,
-                                                     const T* __restrict__ c,
+__global__ void __launch_bounds__(256) k_addn_decode(const T* __restrict__ a, const T* __restrict__ b,
+                                                     const T* __restrict__ c, const T* __restrict__ d,
                                                      double* __restrict__ out, int64_t n,
                                                      double scale) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const T v = a[i] + b[i] + c[i];
+    T v = a[i] + b[i] + c[i];
+    if (d != nullptr) v += d[i];
     if constexpr (sizeof(T) == 8)
       out[i] = (double)(int64_t)v * scale;
     else
@@ -1078,16 +1080,17 @@ int mxh_encode(int words, const double* x, void* out, int64_t n, int frac, void*
   return 0;
 }
 
-int mxh_add3_decode(int words, const void* a, const void* b, const void* c, double* out,
-                    int64_t n, int frac, void* stream) {
+int mxh_addn_decode(int words, const void* a, const void* b, const void* c, const void* d,
+                    double* out, int64_t n, int frac, void* stream) {
   if (n == 0) return 0;
   const double scale = ldexp(1.0, -frac);
   if (words == 1)
-    hipLaunchKernelGGL(k_add3_decode<u64>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
-                       (const u64*)a, (const u64*)b, (const u64*)c, out, n, scale);
+    hipLaunchKernelGGL(k_addn_decode<u64>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
+                       (const u64*)a, (const u64*)b, (const u64*)c, (const u64*)d, out, n, scale);
   else if (words == 2)
-    hipLaunchKernelGGL(k_add3_decode<u128>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
-                       (const u128*)a, (const u128*)b, (const u128*)c, out, n, scale);
+    hipLaunchKernelGGL(k_addn_decode<u128>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
+                       (const u128*)a, (const u128*)b, (const u128*)c, (const u128*)d, out, n,
+                       scale);
   else
     return -2;
   MX_LAUNCH_CHECK();

@@ -46,7 +46,7 @@ _SIGS = {
     "mx_ring_inject": (c_int, [c_int, c_int, c_vp, c_vp, c_i64, c_int, c_vp]),
     "mx_encode": (c_int, [c_int, c_int, c_vp, c_vp, c_i64, c_int, c_vp]),
     "mx_decode": (c_int, [c_int, c_int, c_vp, c_vp, c_i64, c_int, c_vp]),
-    "mx_add3_decode": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp]),
+    "mx_addn_decode": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp]),
     "mx_sum_axis": (c_int, [c_int, c_int, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
     "mx_fill": (c_int, [c_int, c_int, c_vp, c_i64, c_u64, c_u64, c_vp]),
     "mx_bit_planes": (c_int, [c_int, c_int, c_vp, c_vp, c_i64, c_i64, c_int, c_int, c_vp]),

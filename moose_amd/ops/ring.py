@@ -533,9 +533,10 @@ def decode(a: RT, frac: int) -> torch.Tensor:
     if isinstance(a, Opened) and a.pending():  # the reveal's add fused into the decode
         d = [t.data.contiguous() for t in a.parts]
         out = torch.empty(a.shape, dtype=torch.float64, device=a.device)
-        nat.check(nat.lib().mx_add3_decode(
-            nat.dev_of(d[0]), _words(a.bits), *[nat.ptr(x) for x in d], nat.ptr(out),
-            a.numel(), int(frac), nat.stream_of(d[0])), "add3_decode")
+        ptrs = [nat.ptr(x) for x in d] + [None] * (4 - len(d))
+        nat.check(nat.lib().mx_addn_decode(
+            nat.dev_of(d[0]), _words(a.bits), *ptrs, nat.ptr(out), a.numel(), int(frac),
+            nat.stream_of(d[0])), "addn_decode")
         return out
     ad = a.data.contiguous()
     out = torch.empty(a.shape, dtype=torch.float64, device=a.device)
@@ -1202,17 +1203,17 @@ _RT_DATA = RT.__dict__["data"]  # the base class's slot descriptor
 
 
 class Opened(RT):
-    """An opened (revealed) value a + b + c whose sum is formed on first use of ``data``.
-    A decode of it runs one fused pass (mx_add3_decode) instead of add3 + decode: the
-    ring-valued sum never goes to memory."""
+    """An opened (revealed) value a + b + c [+ d] whose sum is formed on first use of
+    ``data``.  A decode of it runs one fused pass (mx_addn_decode) instead of add + decode:
+    the ring-valued sum never goes to memory."""
 
     __slots__ = ("parts",)
 
-    def __init__(self, a: RT, b: RT, c: RT):
+    def __init__(self, a: RT, b: RT, c: RT, d: RT = None):
         _RT_DATA.__set__(self, None)
         self.bits = a.bits
         self._shape = a.shape
-        self.parts = (a, b, c)
+        self.parts = (a, b, c) if d is None else (a, b, c, d)
 
     def pending(self) -> bool:
         return _RT_DATA.__get__(self) is None
@@ -1221,7 +1222,10 @@ class Opened(RT):
     def data(self):
         d = _RT_DATA.__get__(self)
         if d is None:
-            d = add3(*self.parts).data
+            s = add3(*self.parts[:3])
+            if len(self.parts) == 4:
+                s = binary("add", s, self.parts[3])
+            d = s.data
             _RT_DATA.__set__(self, d)
             self.parts = None
         return d
@@ -1235,11 +1239,13 @@ class Opened(RT):
         return self.parts[0].device if self.pending() else self.data.device
 
 
-def opened(a: RT, b: RT, c: RT) -> RT:
-    """a + b + c as an :class:`Opened` (lazy) when the fused decode applies, else add3."""
-    if a.bits in (64, 128) and a.shape == b.shape == c.shape and a.bits == b.bits == c.bits:
-        return Opened(a, b, c)
-    return add3(a, b, c)
+def opened(a: RT, b: RT, c: RT, d: RT = None) -> RT:
+    """a + b + c [+ d] as an :class:`Opened` (lazy) when the fused decode applies."""
+    parts = (a, b, c) if d is None else (a, b, c, d)
+    if a.bits in (64, 128) and all(t.shape == a.shape and t.bits == a.bits for t in parts):
+        return Opened(*parts)
+    s = add3(a, b, c)
+    return s if d is None else binary("add", s, d)
 
 
 def add3(a: RT, b: RT, c: RT) -> RT:

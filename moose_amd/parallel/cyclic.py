@@ -128,10 +128,10 @@ class RingComm:
 def dot_traffic(dirs=(1, 1)):
     """Per-step traffic between the three parties of one session of the dot-product program
     (x owned by party 0, y by party 1, output revealed to party 2), in units of one share
-    tensor of the output: the input shares (owner j -> P_{j+d}, d = its share direction),
-    the folded dot tail (parallel/party.py: m0, w0 0->1; m1, w1 1->0; z2 2->0 and 2->1;
-    rt1, rm1 2->1) and the reveal (P0 -> P2)."""
-    f = {(0, 1): 2.0, (1, 0): 2.0, (2, 0): 1.0, (2, 1): 2.5, (0, 2): 1.0}
+    tensor of the output: the input shares (owner j -> P_{j+d}, d = its share direction)
+    and the folded dot tail with the reveal merged into its last round (parallel/party.py:
+    m0 0->1; m1 1->0; z2 2->0 and 2->1; rt1, rm1 2->1; w0 0->2, w1 1->2)."""
+    f = {(0, 1): 1.0, (1, 0): 1.0, (2, 0): 1.0, (2, 1): 2.5, (0, 2): 1.0, (1, 2): 1.0}
     for owner, d in ((0, dirs[0]), (1, dirs[1])):
         key = (owner, (owner + d) % 3)
         f[key] = f.get(key, 0.0) + 1.0
@@ -155,8 +155,10 @@ def link_loads(offsets: Sequence[int], world: int, traffic=None) -> Dict[int, fl
 def default_layout(roles: Sequence[str], world: int = None):
     """(offsets, share directions) of the roles for the dot-product program on ``world``
     GPUs: the pair minimising the busiest link (:func:`dot_traffic`, :func:`link_loads`);
-    ties keep the reference's share direction.  E.g. 8 GPUs: offsets (0, 1, 3) and x shared
-    towards P_{j+2}: every flow on its own link, the busiest one 2.5 units instead of 3."""
+    ties keep the reference's share direction.  E.g. 8 GPUs: offsets (0, 1, 3), every flow
+    on its own link, the busiest one 2.5 units (4.5 with offsets 0, 1, 2); 4 GPUs: offsets
+    (0, 2, 1), 3.5 units.  The mirrored share direction wins for other traffic patterns
+    (before the reveal was merged into the tail, it took 8 GPUs from 3 units to 2.5)."""
     n = len(roles)
     off = default_offsets(roles, world)
     if world is None or world < 4 or n < 3:
@@ -187,11 +189,10 @@ def default_offsets(roles: Sequence[str], world: int = None) -> Dict[str, int]:
 
     xGMI is point to point -- every GPU pair has its own link (≈50-64 GB/s per direction
     under RCCL) -- so the step time of a communication-heavy program is set by the busiest
-    link, not the total volume.  With offsets (0, 1, 2) the flows 0->1 and 1->2 share
-    distance +1 and 1->0 and 2->1 distance -1 (4.5 of the 10.5 units above on one link);
-    for ``world >= 4`` the offsets of the three parties are chosen to minimise the busiest
-    link, e.g. (0, 1, 3) on 8 GPUs puts every flow on its own link (max 3 units: 1.5x less
-    time on the wire per step), on 4 GPUs 4 units instead of 4.5.
+    link, not the total volume.  With offsets (0, 1, 2) several flows of the dot program
+    share a distance (4.5 of its 9.5 units on one link on 8 GPUs); for ``world >= 4`` the
+    offsets of the three parties are chosen to minimise the busiest link, e.g. (0, 1, 3) on
+    8 GPUs puts every flow on its own link (2.5 units).
     Further roles take the smallest unused offsets."""
     n = len(roles)
     off = list(range(n))
@@ -473,7 +474,20 @@ class CyclicSession(StackedSession):
         pre.stack = (s0, s1)
         return pre
 
-    def party_dot_trunc(self, plc, v, m, nonces, out=None, pre=None):
+    # rep.dot_trunc returns its product with the last reshare round pending (DeferredRep)
+    defer_reshare = True
+
+    def p_reveal_deferred(self, x, tail, host):
+        """Reveal to the dealer P2 of a product whose round B is pending: w0, w1 go to P2
+        (one round) and P2 sums z2 + z0 + w0 + w1 (fused into the decode).  None for other
+        hosts (the generic reveal completes the shares first)."""
+        plc = x.plc
+        if host not in plc.owners or plc.owners.index(host) != 2:
+            return None
+        parts = tail.reveal_to_dealer()[2]
+        return HV(host, R.opened(*[R.RT(t, x.bits) for t in parts]))
+
+    def party_dot_trunc(self, plc, v, m, nonces, out=None, pre=None, defer=False):
         """rep.dot_trunc's zero share + reshare + TruncPr of the local products ``v`` with
         the reshare folded into TruncPr's first round (parallel/party.py); ``out``: optional
         (s0, s1) [3, ...] views (dense per component) written in place; ``pre``: the
@@ -487,9 +501,11 @@ class CyclicSession(StackedSession):
         else:
             s0, s1 = out if out is not None else (torch.empty_like(data),
                                                   torch.empty_like(data))
-        party.dot_trunc_tail(self, plc, [0, 1, 2], [data[c] for c in range(3)], bits, m,
-                             nonces, [s0[c] for c in range(3)], [s1[c] for c in range(3)],
-                             self._pair_ptrs(plc), pre=pre)
+        rb = party.dot_trunc_tail(self, plc, [0, 1, 2], [data[c] for c in range(3)], bits, m,
+                                  nonces, [s0[c] for c in range(3)], [s1[c] for c in range(3)],
+                                  self._pair_ptrs(plc), pre=pre, defer=defer)
+        if defer:
+            return PV(plc, R.RT(s0, bits)), PV(plc, R.RT(s1, bits)), rb
         return PV(plc, R.RT(s0, bits)), PV(plc, R.RT(s1, bits))
 
     # the single-GPU fused variants read other parties' data in-kernel: never used here

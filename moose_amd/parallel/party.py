@@ -68,13 +68,64 @@ def dealer_early(sess, plc, roles, like, bits, m, nonces, out0, out1, slots):
                        [got.get("rm1") if r == 1 else None for r in roles])
 
 
-def dot_trunc_tail(sess, plc, roles, cross, bits, m, nonces, out0, out1, slots, pre=None):
+class RoundB:
+    """Round B of the dot tail, not yet run (``dot_trunc_tail(..., defer=True)``): P0 and
+    P1 hold w0 / w1, every other share is in place.  :meth:`finish` runs it (w0 <-> w1, then
+    s1 of P0 and s0 of P1 = w0 + w1).  A reveal to the dealer P2 instead sends w0 and w1 to
+    P2 (:meth:`reveal_to_dealer`): P2 holds z2, z0 and gets the third slot as w0 + w1, so
+    the reshare round and the reveal round become ONE round of the same two messages (a
+    product that is only revealed -- the benchmark's dot -- saves a round and a share
+    tensor on the wire)."""
+
+    def __init__(self, sess, plc, roles, w, out0, out1, bits, n_el, like):
+        self.sess, self.plc, self.roles, self.w = sess, plc, roles, w
+        self.out0, self.out1, self.bits, self.n_el, self.like = out0, out1, bits, n_el, like
+        self.done = False
+
+    def _mine(self, party):
+        c = {r: c for c, r in enumerate(self.roles)}.get(party)
+        return None if c is None else self.w[c]
+
+    def finish(self):
+        if self.done:
+            return
+        self.done = True
+        sess, roles, like = self.sess, self.roles, self.like
+        got = sess.party_exchange(self.plc, [("w0", 0, 1, self._mine(0), like),
+                                             ("w1", 1, 0, self._mine(1), like)])
+        other = [got.get("w1") if r == 0 else got.get("w0") if r == 1 else None for r in roles]
+        dst = [self.out1[c] if r == 0 else self.out0[c] if r == 1 else None
+               for c, r in enumerate(roles)]
+        R.dot_tail_r2(self.w, other, dst, self.bits, roles, self.n_el)
+        nb = math.prod(like[0]) * 8
+        for a, b in ((0, 1), (1, 0)):
+            sess.stats.record_send(self.plc.owners[a], self.plc.owners[b], nb)
+        sess.stats.record_round(2 * nb)
+
+    def reveal_to_dealer(self):
+        """Open the product to P2: returns, for each hosted component playing P2, the four
+        addends (z2, z0, w0, w1) of the value; None for other components.  The shares of
+        P0 and P1 stay incomplete until something reads them (:meth:`finish`)."""
+        sess, roles, like = self.sess, self.roles, self.like
+        got = sess.party_exchange(self.plc, [("w0", 0, 2, self._mine(0), like),
+                                             ("w1", 1, 2, self._mine(1), like)])
+        nb = math.prod(like[0]) * 8
+        for a in (0, 1):
+            sess.stats.record_send(self.plc.owners[a], self.plc.owners[2], nb)
+        sess.stats.record_round(2 * nb)
+        return [(self.out0[c], self.out1[c], got["w0"], got["w1"]) if r == 2 else None
+                for c, r in enumerate(roles)]
+
+
+def dot_trunc_tail(sess, plc, roles, cross, bits, m, nonces, out0, out1, slots, pre=None,
+                   defer=False):
     """Zero share + reshare + TruncPr of the local cross products ``cross`` (one dense
     ring-``bits`` tensor per hosted component; component c plays party ``roles[c]``).
     Writes the new shares into ``out0`` / ``out1`` (dense per-component tensors, e.g. rows
     of a stack).  ``nonces`` = (zero share, r0, r1, t, m, z0, z2); ``slots`` = the key-slot
     pointers (own k_p, next k_{p+1}) of every component.  ``pre``: the dealer's part, done
-    by :func:`dealer_early` (same out0 / out1)."""
+    by :func:`dealer_early` (same out0 / out1).  ``defer``: return round B as a
+    :class:`RoundB` instead of running it."""
     comp = {r: c for c, r in enumerate(roles)}
     n_el = math.prod(cross[0].shape) // (2 if bits == 128 else 1)
     msg, rt, rm = R.dot_tail_r0(cross, bits, m, roles, slots, nonces, out0, out1, n_el,
@@ -99,15 +150,16 @@ def dot_trunc_tail(sess, plc, roles, cross, bits, m, nonces, out0, out1, slots, 
     else:
         rrt, rrm = pre.rrt, pre.rrm
     w = R.dot_tail_r1(msg, rmk, rz, rrt, rrm, bits, m, roles, slots, nonces, out0, out1, n_el)
-    got = sess.party_exchange(plc, [("w0", 0, 1, mine(0, w), like), ("w1", 1, 0, mine(1, w), like)])
-    other = [got.get("w1") if r == 0 else got.get("w0") if r == 1 else None for r in roles]
-    dst = [out1[c] if r == 0 else out0[c] if r == 1 else None for c, r in enumerate(roles)]
-    R.dot_tail_r2(w, other, dst, bits, roles, n_el)
     nb = cross[0].numel() * cross[0].element_size()
-    record_tail_traffic(sess.stats, plc, nb)
+    record_tail_traffic(sess.stats, plc, nb, round_b=False)
+    rb = RoundB(sess, plc, roles, w, out0, out1, bits, n_el, like)
+    if defer:
+        return rb
+    rb.finish()
+    return None
 
 
-def record_tail_traffic(stats, plc, nb):
+def record_tail_traffic(stats, plc, nb, round_b=True):
     """Messages of the folded dot tail (``nb`` bytes per share tensor): round A carries
     m0, m1, z2 (twice), rt1 and rm1 (a u64, half of a Z_2^128 element); round B w0, w1."""
     o = plc.owners
@@ -115,6 +167,8 @@ def record_tail_traffic(stats, plc, nb):
         stats.record_send(o[a], o[b], nb, count=k)
     stats.record_send(o[2], o[1], nb // 2)
     stats.record_round(5 * nb + nb // 2)
+    if not round_b:
+        return
     for a, b in ((0, 1), (1, 0)):
         stats.record_send(o[a], o[b], nb)
     stats.record_round(2 * nb)

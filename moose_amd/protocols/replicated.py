@@ -59,6 +59,34 @@ class RepTensor:
         return "Add" if self.kind == "arith" else "Xor"
 
 
+class DeferredRep(RepTensor):
+    """A product whose last reshare round has not run (parallel/party.py ``RoundB``): the
+    shares are completed when first read, and a reveal to the dealer P2 merges that round
+    with the reveal (session ``p_reveal_deferred``)."""
+
+    def __init__(self, plc, bits, kind, s0, s1, tail):
+        self._tail = tail
+        super().__init__(plc, bits, kind, s0, s1)
+
+    @property
+    def s0(self):
+        self._tail.finish()
+        return self._s0
+
+    @s0.setter
+    def s0(self, v):
+        self._s0 = v
+
+    @property
+    def s1(self):
+        self._tail.finish()
+        return self._s1
+
+    @s1.setter
+    def s1(self, v):
+        self._s1 = v
+
+
 def _owner_index(plc, host):
     try:
         return plc.owners.index(host)
@@ -134,6 +162,12 @@ def _share_outsider(sess, plc, x, kind, bits, shape):
 def reveal(sess, x: RepTensor, host: str) -> HV:
     """Open x to ``host`` (a party of x.plc or an outsider)."""
     with span("rep.reveal"):
+        tail = getattr(x, "_tail", None)
+        if tail is not None and not tail.done:
+            fast = getattr(sess, "p_reveal_deferred", None)
+            r = fast(x, tail, host) if fast is not None else None
+            if r is not None:
+                return r
         add = x.add_prim
         fast = getattr(sess, "p_reveal", None)
         if fast is not None and x.kind == "arith" and x.bits in (64, 128):
@@ -434,6 +468,11 @@ def dot_trunc(sess, x: RepTensor, y: RepTensor, m: int) -> RepTensor:
                 pre_fn = getattr(sess, "party_dot_trunc_pre", None)
                 pre = pre_fn(x.plc, x, y, m, nonces) if pre_fn is not None else None
                 v = sess.p_dot_cross(x.plc, x.s0, x.s1, y.s0, y.s1)
+                if getattr(sess, "defer_reshare", False) and pre is not None:
+                    # the last reshare round waits for the first reader (a reveal to the
+                    # dealer merges it with the reveal)
+                    s0, s1, rb = party(x.plc, v, m, nonces, pre=pre, defer=True)
+                    return DeferredRep(x.plc, x.bits, "arith", s0, s1, rb)
                 s0, s1 = (party(x.plc, v, m, nonces) if pre is None
                           else party(x.plc, v, m, nonces, pre=pre))
                 return RepTensor(x.plc, x.bits, "arith", s0, s1)

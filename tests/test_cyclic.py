@@ -179,16 +179,19 @@ def test_cyclic_mirrored_share_direction():
 
 
 def test_cyclic_link_balanced_offsets():
-    """The link-balanced placement bench.py uses on >= 4 GPUs (carole at offset 3, so
-    every inter-party flow of the dot program has its own xGMI link on 8 GPUs)."""
-    from moose_amd.parallel.cyclic import default_offsets
+    """The link-balanced placement bench.py uses on >= 4 GPUs: on 8 GPUs carole at offset
+    3, so every inter-party flow of the dot program has its own xGMI link (busiest link 2.5
+    share tensors per step instead of 4.5 with offsets 0, 1, 2)."""
+    from moose_amd.parallel.cyclic import default_layout
     from moose_amd.parallel.cyclic import link_loads
 
-    off = default_offsets(("a", "b", "c"), 4)
-    assert off == {"a": 0, "b": 1, "c": 3}
-    assert max(link_loads((0, 1, 3), 8).values()) == 3.0 < max(link_loads((0, 1, 2), 8).values())
-    assert default_offsets(("a", "b", "c"), 2) == {"a": 0, "b": 1, "c": 2}
-    _run(4, "cpu", off)
+    off8, dirs8 = default_layout(("a", "b", "c"), 8)
+    assert off8 == {"a": 0, "b": 1, "c": 3} and dirs8 == {}
+    assert max(link_loads((0, 1, 3), 8).values()) == 2.5 < max(link_loads((0, 1, 2), 8).values())
+    off4, dirs4 = default_layout(("a", "b", "c"), 4)
+    assert max(link_loads(list(off4.values()), 4).values()) == 3.5
+    assert default_layout(("a", "b", "c"), 2) == ({"a": 0, "b": 1, "c": 2}, {})
+    _run(4, "cpu", off4, dirs=dirs4)
 
 
 @pytest.mark.gpu

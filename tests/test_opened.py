@@ -1,5 +1,5 @@
 """The reveal's lazy sum (ops/ring.py ``Opened``): decoding a revealed value runs one fused
-add3 + decode pass (mx_add3_decode) and must equal add3 followed by decode; any other use
+add + decode pass (mx_addn_decode) and must equal add3 followed by decode; any other use
 materialises the ring-valued sum (reference reveal: replicated/convert.rs:280-313, decode:
 host/fixedpoint.rs)."""
 import pytest
