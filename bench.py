@@ -102,6 +102,9 @@ def _parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--size", type=int, default=4096)
+    ap.add_argument("--zero-slot-steps", type=int, default=10,
+                    help="one GPU, stacked: also time this many steps with the opt-in "
+                         "zero-slot-aware product (reported apart from the headline)")
     ap.add_argument("--ring", type=int, default=128, choices=[64, 128])
     ap.add_argument("--gather", default="root", choices=["root", "all", "none"],
                     help="revealed outputs of every session: to rank 0 (the client; "
@@ -567,6 +570,37 @@ def _main(args, prog_out):
     sync()
     elapsed = time.perf_counter() - t0
     step_ms = sorted(a.elapsed_time(b) for a, b in evs) if evs is not None else []
+    z_last = z
+
+    zero_slot = None
+    if world == 1 and layout == "stacked" and args.zero_slot_steps > 0:
+        # secondary figure, NOT the headline: the same steps with the zero-slot-aware RSS
+        # product (protocols/replicated.py _zero_slot_cross, opt-in MOOSEX_ZERO_SLOTS=1):
+        # both operands are fresh input sharings with a public zero slot, so each party's
+        # cross product is one K-long GEMM instead of the K-doubled one
+        from moose_amd.protocols import replicated as rep_mod
+
+        prog.phase("zero_slot", args.watchdog)
+        prev, rep_mod.ZERO_SLOTS = rep_mod.ZERO_SLOTS, True
+        try:
+            for _ in range(2):
+                step()
+            sync()
+            tz = time.perf_counter()
+            for _ in range(args.zero_slot_steps):
+                zz = step()
+            sync()
+            zms = (time.perf_counter() - tz) / args.zero_slot_steps * 1e3
+            zero_slot = {"ms_per_step": zms, "value": n * n / zms * 1e3,
+                         "steps": args.zero_slot_steps,
+                         # TruncPr rounds probabilistically: ~1 ulp (2^-23) apart
+                         "max_abs_diff_vs_headline_output":
+                             (zz - z_last).abs().max().item() if zz is not None else None,
+                         "note": "opt-in MOOSEX_ZERO_SLOTS=1, not the headline: skips the "
+                                 "cross terms that multiply a fresh input sharing's public "
+                                 "zero slot (half the GEMM)"}
+        finally:
+            rep_mod.ZERO_SLOTS = prev
 
     prog.phase("report", min(args.watchdog, 180))
     p2p = [sum(c.bytes_sent for c in comms) - sum(b for b, _ in comm0),
@@ -611,6 +645,8 @@ def _main(args, prog_out):
     if step_ms:
         line["step_ms_rank0"] = {"min": step_ms[0], "median": step_ms[len(step_ms) // 2],
                                  "max": step_ms[-1]}
+    if zero_slot is not None:
+        line["zero_slot_aware"] = zero_slot
     line["device"] = _device_info(device)
     line["revision"] = _revision()
     prog.headline_done(line)

@@ -34,8 +34,9 @@ instead of k bit tensors (reference bits.rs stacks a [k, ...] bit array).
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
 import os
+from dataclasses import dataclass
+from typing import Optional
 
 import torch
 
@@ -53,6 +54,9 @@ class RepTensor:
     kind: str  # "arith" (additive) or "bool" (xor)
     s0: PV
     s1: PV
+    # slot known to be zero by construction (a fresh input sharing sets slot j+2 = 0, as
+    # the reference's; public knowledge of every party), else None
+    zero_slot: Optional[int] = None
 
     @property
     def add_prim(self):
@@ -112,11 +116,11 @@ def share(sess, plc, x: HV, kind="arith") -> RepTensor:
         n1, na = sess.nonce(plc), sess.nonce(plc)
         if getattr(sess, "fused", False):
             s0, s1 = sess.fused_share(plc, x, j, kind, n1, na)
-            return RepTensor(plc, bits, kind, s0, s1)
+            return RepTensor(plc, bits, kind, s0, s1, zero_slot=j2)
         party = getattr(sess, "party_share", None)
         if party is not None and bits in (64, 128):
             s0, s1 = party(plc, x, j, kind, n1, na)
-            return RepTensor(plc, bits, kind, s0, s1)
+            return RepTensor(plc, bits, kind, s0, s1, zero_slot=j2)
         d = sess.share_dir(plc, j) if hasattr(sess, "share_dir") else 1
         zero = lambda h: sess.h("Fill", o[h], shape, value=0, bits=bits)  # noqa: E731
         if d == 1:
@@ -136,7 +140,7 @@ def share(sess, plc, x: HV, kind="arith") -> RepTensor:
             comp1 = {j: r_j, j1: zero(j1), j2: sess.move(xj, o[j2])}
         s0 = sess.gather(plc, [comp0[i] for i in range(3)])
         s1 = sess.gather(plc, [comp1[i] for i in range(3)])
-        return RepTensor(plc, bits, kind, s0, s1)
+        return RepTensor(plc, bits, kind, s0, s1, zero_slot=j2)
 
 
 def _share_outsider(sess, plc, x, kind, bits, shape):
@@ -403,6 +407,58 @@ def xor(sess, x: RepTensor, y: RepTensor) -> RepTensor:
     return add(sess, x, y)
 
 
+ZERO_SLOTS = os.environ.get("MOOSEX_ZERO_SLOTS", "0") == "1"
+
+
+def _cross_terms(p, zx, zy):
+    """The nonzero terms of party p's cross product x_p y_p + x_p y_{p+1} + x_{p+1} y_p
+    given the operands' known-zero slots, as ONE product (a, b) of share expressions --
+    a, b in {"x0", "x1", "x01", "y0", "y1", "y01"} (x0 = x_p, x1 = x_{p+1}, x01 = their
+    sum) -- or None when all three terms are nonzero (two products needed)."""
+    xp, xq = p != zx, (p + 1) % 3 != zx
+    yp, yq = p != zy, (p + 1) % 3 != zy
+    t1, t2, t3 = xp and yp, xp and yq, xq and yp
+    if t1 and t2 and t3:
+        return None
+    if t1 and t2:
+        return "x0", "y01"
+    if t1 and t3:
+        return "x01", "y0"
+    if t1:
+        return "x0", "y0"
+    if t2:
+        return "x0", "y1"
+    if t3:
+        return "x1", "y0"
+    return "zero", "zero"
+
+
+def _zero_slot_cross(sess, x: RepTensor, y: RepTensor):
+    """The local cross products of a stacked-layout session ([3, M, K] party vectors) when
+    the operands have known-zero slots (fresh input sharings): every party's product is a
+    single K-long GEMM instead of the K-doubled one -- half the MFMA work, bitwise the same
+    values.  Opt-in (MOOSEX_ZERO_SLOTS=1); None when it does not apply."""
+    if not ZERO_SLOTS or x.zero_slot is None and y.zero_slot is None:
+        return None
+    xs0, xs1, ys0, ys1 = x.s0.v, x.s1.v, y.s0.v, y.s1.v
+    if not all(isinstance(t, R.RT) for t in (xs0, xs1, ys0, ys1)):
+        return None
+    if len(xs0.shape) != 3 or len(ys0.shape) != 3 or x.bits not in (64, 128):
+        return None
+    terms = [_cross_terms(p, x.zero_slot, y.zero_slot) for p in range(3)]
+    if any(t is None or t[0] == "zero" for t in terms):
+        return None
+    bits = x.bits
+
+    def pick(name, s0, s1, p):
+        a, b = R.RT(s0.data[p], bits), R.RT(s1.data[p], bits)
+        return a if name[1:] == "0" else b if name[1:] == "1" else R.binary("add", a, b)
+
+    A = torch.stack([pick(a, xs0, xs1, p).data for p, (a, _) in enumerate(terms)])
+    B = torch.stack([pick(b, ys0, ys1, p).data for p, (_, b) in enumerate(terms)])
+    return PV(x.plc, R.dot(R.RT(A, bits), R.RT(B, bits), nb=1))
+
+
 def dot(sess, x: RepTensor, y: RepTensor, nbatch: int = 0) -> RepTensor:
     """Matrix product: z_p = x_p.(y_p + y_{p+1}) + x_{p+1}.y_p as ONE K-doubled MFMA
     GEMM (all parties batched when stacked), + zero share, + reshare.  ``nbatch``
@@ -416,7 +472,8 @@ def dot(sess, x: RepTensor, y: RepTensor, nbatch: int = 0) -> RepTensor:
         if nbatch:
             v = sess.p_dot_cross(x.plc, x.s0, x.s1, y.s0, y.s1, nbatch=nbatch)
         else:
-            v = sess.p_dot_cross(x.plc, x.s0, x.s1, y.s0, y.s1)
+            v = _zero_slot_cross(sess, x, y) or sess.p_dot_cross(x.plc, x.s0, x.s1, y.s0,
+                                                                    y.s1)
         fused = getattr(sess, "p_zero_share_reshare", None)
         if fused is not None and getattr(sess, "fused", False):
             s0, s1 = fused(x.plc, v, x.kind)
@@ -458,7 +515,8 @@ def dot_trunc(sess, x: RepTensor, y: RepTensor, m: int) -> RepTensor:
                 and getattr(sess, "device", None) is not None and sess.device.type == "cuda"
                 and os.environ.get("MOOSEX_DOT_TAIL", "1") != "0"):
             with span("rep.dot_trunc_fused"):
-                v = sess.p_dot_cross(x.plc, x.s0, x.s1, y.s0, y.s1)
+                v = _zero_slot_cross(sess, x, y) or sess.p_dot_cross(x.plc, x.s0, x.s1, y.s0,
+                                                                        y.s1)
                 s0, s1 = tail(x.plc, v, m)  # zero share + reshare + TruncPr: one kernel
                 return RepTensor(x.plc, x.bits, "arith", s0, s1)
         if use_party:  # the per-party tail: reshare folded into TruncPr (2 rounds)
@@ -467,7 +525,8 @@ def dot_trunc(sess, x: RepTensor, y: RepTensor, m: int) -> RepTensor:
                 # the dealer's messages first: they travel while the GEMM runs
                 pre_fn = getattr(sess, "party_dot_trunc_pre", None)
                 pre = pre_fn(x.plc, x, y, m, nonces) if pre_fn is not None else None
-                v = sess.p_dot_cross(x.plc, x.s0, x.s1, y.s0, y.s1)
+                v = _zero_slot_cross(sess, x, y) or sess.p_dot_cross(x.plc, x.s0, x.s1, y.s0,
+                                                                        y.s1)
                 if getattr(sess, "defer_reshare", False) and pre is not None:
                     # the last reshare round waits for the first reader (a reveal to the
                     # dealer merges it with the reveal)
