@@ -479,12 +479,27 @@ def encode(x: torch.Tensor, frac: int, bits: int) -> RT:
     return out
 
 
+def _stream_of(t: torch.Tensor):
+    """The current stream of ``t``'s device (None on the host): where a lazy value's inputs
+    were issued."""
+    return torch.cuda.current_stream(t.device) if t.is_cuda else None
+
+
+def _join(stream):
+    """Order the current stream after the work issued so far on ``stream`` -- a lazy value
+    created on one stream and consumed on another (dataflow lanes, step streams)."""
+    if stream is not None:
+        cur = torch.cuda.current_stream(stream.device)
+        if cur != stream:
+            cur.wait_stream(stream)
+
+
 class Encoded(RT):
     """A float64 tensor's fixed-point encoding (x * 2^frac), formed on first use of
     ``data``.  Input sharing of it encodes inside the share kernel (kind MX_SHARE_F64): the
     ring-valued encoding never goes to memory."""
 
-    __slots__ = ("src", "frac")
+    __slots__ = ("src", "frac", "stream")
 
     def __init__(self, x: torch.Tensor, frac: int, bits: int):
         _RT_DATA.__set__(self, None)
@@ -492,6 +507,7 @@ class Encoded(RT):
         self._shape = tuple(x.shape)
         self.src = x
         self.frac = int(frac)
+        self.stream = _stream_of(x)
 
     def pending(self) -> bool:
         return _RT_DATA.__get__(self) is None
@@ -500,6 +516,7 @@ class Encoded(RT):
     def data(self):
         d = _RT_DATA.__get__(self)
         if d is None:
+            _join(self.stream)
             d = encode(self.src, self.frac, self.bits).data
             _RT_DATA.__set__(self, d)
             self.src = None
@@ -525,12 +542,14 @@ def share_source(x: RT, kind: str):
     """(kind code, device tensor, aux) for the share kernels: an unencoded float64 input is
     passed as is (MX_SHARE_F64 = 2, aux = its fractional bits), else the ring data."""
     if kind == "arith" and isinstance(x, Encoded) and x.pending():
+        _join(x.stream)
         return 2, x.src, x.frac
     return (1 if kind == "bool" else 0), x.data.contiguous(), None
 
 
 def decode(a: RT, frac: int) -> torch.Tensor:
     if isinstance(a, Opened) and a.pending():  # the reveal's add fused into the decode
+        _join(a.stream)
         d = [t.data.contiguous() for t in a.parts]
         out = torch.empty(a.shape, dtype=torch.float64, device=a.device)
         ptrs = [nat.ptr(x) for x in d] + [None] * (4 - len(d))
@@ -1207,13 +1226,14 @@ class Opened(RT):
     ``data``.  A decode of it runs one fused pass (mx_addn_decode) instead of add + decode:
     the ring-valued sum never goes to memory."""
 
-    __slots__ = ("parts",)
+    __slots__ = ("parts", "stream")
 
     def __init__(self, a: RT, b: RT, c: RT, d: RT = None):
         _RT_DATA.__set__(self, None)
         self.bits = a.bits
         self._shape = a.shape
         self.parts = (a, b, c) if d is None else (a, b, c, d)
+        self.stream = _stream_of(a.data)
 
     def pending(self) -> bool:
         return _RT_DATA.__get__(self) is None
@@ -1222,6 +1242,7 @@ class Opened(RT):
     def data(self):
         d = _RT_DATA.__get__(self)
         if d is None:
+            _join(self.stream)
             s = add3(*self.parts[:3])
             if len(self.parts) == 4:
                 s = binary("add", s, self.parts[3])

@@ -81,6 +81,8 @@ class RoundB:
         self.sess, self.plc, self.roles, self.w = sess, plc, roles, w
         self.out0, self.out1, self.bits, self.n_el, self.like = out0, out1, bits, n_el, like
         self.done = False
+        t = next(x for x in out0 if x is not None)
+        self.stream = R._stream_of(t)  # round A was issued here
 
     def _mine(self, party):
         c = {r: c for c, r in enumerate(self.roles)}.get(party)
@@ -90,6 +92,7 @@ class RoundB:
         if self.done:
             return
         self.done = True
+        R._join(self.stream)
         sess, roles, like = self.sess, self.roles, self.like
         got = sess.party_exchange(self.plc, [("w0", 0, 1, self._mine(0), like),
                                              ("w1", 1, 0, self._mine(1), like)])
@@ -107,6 +110,7 @@ class RoundB:
         addends (z2, z0, w0, w1) of the value; None for other components.  The shares of
         P0 and P1 stay incomplete until something reads them (:meth:`finish`)."""
         sess, roles, like = self.sess, self.roles, self.like
+        R._join(self.stream)
         got = sess.party_exchange(self.plc, [("w0", 0, 2, self._mine(0), like),
                                              ("w1", 1, 2, self._mine(1), like)])
         nb = math.prod(like[0]) * 8

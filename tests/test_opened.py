@@ -41,3 +41,23 @@ def test_opened_decode_equals_add3_then_decode(bits):
 @pytest.mark.parametrize("bits", [64, 128])
 def test_opened_decode_gpu(bits):
     _check(bits, "cuda")
+
+
+@pytest.mark.gpu
+def test_lazy_values_cross_streams():
+    """A lazy value made on one stream and consumed on another: the consumer orders itself
+    after the producer stream (ring._join), for Opened (fused decode) and Encoded (fused
+    share source and materialisation)."""
+    x, a, b, c = _parts(128, "cuda")
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        big = torch.full((1 << 24,), 3.0, device="cuda")
+        for _ in range(20):  # keep the side stream busy before the parts are written
+            big = big * 1.0000001
+        c2 = R.RT(c.data.clone(), 128)
+        o = R.opened(a, b, c2)
+        e = R.encode_lazy(x.cuda(), 23, 128)
+    got = R.decode(o, 23)  # on the default stream
+    assert (got.cpu() - x).abs().max() < 1e-6
+    assert torch.equal(e.data.cpu(), R.encode(x, 23, 128).data)
