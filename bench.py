@@ -102,6 +102,9 @@ def _parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--size", type=int, default=4096)
+    ap.add_argument("--spmd-configs", action=argparse.BooleanOptionalAction, default=True,
+                    help="with >= 3 GPUs also time BASELINE configs 2 (tutorials/"
+                         "dotprod.moose) and 3 (RingDot, one party per GPU) on ranks 0-2")
     ap.add_argument("--zero-slot-steps", type=int, default=10,
                     help="one GPU, stacked: also time this many steps with the opt-in "
                          "zero-slot-aware product (reported apart from the headline)")
@@ -347,6 +350,79 @@ def _lr_spmd(runs, world, rank, device, prog):
         if rank % 3 == 1:  # bob holds the opened probabilities
             got = interp.to_numpy(list(outs.values())[0])
             rec["max_abs_err_vs_sklearn"] = float(np.abs(np.asarray(got) - tm.proba).max())
+    return rec
+
+
+# The reference's tutorials/dotprod.moose (BASELINE config 2), verbatim: a fixed(24,40)
+# 1x3 . 3x1 dot product of two players' constants, revealed to the third.
+DOTPROD_MOOSE = """\
+constant_0 = Constant{value = HostFloat64Tensor([[1.0, 2.0, 3.0]])}: () -> Tensor<Float64> () @Host(player0)
+cast_0 = Cast: (Tensor<Float64>) -> Tensor<Fixed128(24, 40)> (constant_0) @Host(player0)
+constant_1 = Constant{value = HostFloat64Tensor([[4.0], [5.0], [6.0]])}: () -> Tensor<Float64> () @Host(player1)
+cast_1 = Cast: (Tensor<Float64>) -> Tensor<Fixed128(24, 40)> (constant_1) @Host(player1)
+dot_0 = Dot: (Tensor<Fixed128(24, 40)>, Tensor<Fixed128(24, 40)>) -> Tensor<Fixed128(24, 40)> (cast_0, cast_1) @Replicated(player0, player1, player2)
+cast_2 = Cast: (Tensor<Fixed128(24, 40)>) -> Tensor<Float64> (dot_0) @Host(player2)
+output_0 = Output{tag = "output_0"}: (Tensor<Float64>) -> Tensor<Float64> (cast_2) @Host(player2)
+"""
+
+
+def _spmd_configs(args, world, rank, device, prog):
+    """BASELINE configs 2 and 3 on three GPUs (ranks 0, 1, 2, one party each, every
+    reshare an RCCL send/recv over xGMI): the reference's tutorials/dotprod.moose latency
+    (p50 over ``args.lr_runs`` evaluations) and the headline RingDot at ``args.size`` (ms
+    per step over 5 steps).  A step's time is the max over the three ranks."""
+    import torch
+    import torch.distributed as dist
+
+    from moose_amd.ir import textual
+    from moose_amd.parallel.spmd import SPMDSession
+    from moose_amd.parallel.transport import Transport
+    from moose_amd.runtime.interpreter import Interpreter
+
+    g = dist.new_group([0, 1, 2])  # every rank creates the group
+    if rank >= 3:
+        return None
+    bdev = [device.index] if device.type == "cuda" and dist.get_backend() == "nccl" else None
+    tdev = device if dist.get_backend() == "nccl" else torch.device("cpu")
+    tr = Transport(rank, world, device, plans=True)
+
+    def timed(comp, roles, args_of, runs, warm):
+        lat, outs = [], None
+        for i in range(runs + warm):
+            prog.tick(i)
+            dist.barrier(group=g, device_ids=bdev)
+            t0 = time.perf_counter()
+            sess = SPMDSession(list(roles)[rank], roles, tr, device)
+            outs = Interpreter(sess, {}, fixedpoint_ring=128).run(comp, args_of())
+            if device.type == "cuda":
+                torch.cuda.synchronize(device)
+            if i >= warm:
+                lat.append((time.perf_counter() - t0) * 1e3)
+        mine = torch.tensor(lat, dtype=torch.float64, device=tdev)
+        allt = torch.empty(3 * runs, dtype=torch.float64, device=tdev)
+        dist.all_gather_into_tensor(allt, mine, group=g)
+        per_run = sorted(allt.reshape(3, runs).max(dim=0).values.cpu().tolist())
+        return per_run, outs
+
+    rec = {}
+    comp2 = textual.parse_computation(DOTPROD_MOOSE, parallel=False)
+    roles2 = {"player0": 0, "player1": 1, "player2": 2}
+    runs = max(5, args.lr_runs)
+    per, outs = timed(comp2, roles2, dict, runs, 3)
+    rec["config2_dotprod_moose"] = {"p50_ms": per[len(per) // 2], "runs": runs}
+    if rank == 2:
+        got = float(outs["output_0"].v.v.reshape(-1)[0])
+        rec["config2_dotprod_moose"]["output"] = got  # 1*4 + 2*5 + 3*6 = 32
+    n = args.size
+    comp3 = build_computation(args.ring)
+    roles3 = {r: i for i, r in enumerate(ROLES)}
+    x = _inputs(n, 0, "x", device) if rank == 0 else None
+    y = _inputs(n, 0, "y", device) if rank == 1 else None
+    feed = lambda: {k: v for k, v in (("x", x), ("y", y)) if v is not None}  # noqa: E731
+    per, _ = timed(comp3, roles3, feed, 5, 2)
+    ms = sum(per) / len(per)
+    rec["config3_ringdot_3gpu"] = {"ms_per_step": ms, "elems_per_sec": n * n / ms * 1e3,
+                                   "size": n, "steps": 5}
     return rec
 
 
@@ -708,6 +784,18 @@ def _main(args, prog_out):
             if "spmd_one_party_per_gpu" in lr:
                 line["lr_inference_p50_ms"]["spmd"] = lr["spmd_one_party_per_gpu"]["p50_ms"]
             line["lr_inference"] = lr
+
+    if world >= 3 and args.spmd_configs:
+        prog.phase("spmd_configs", min(args.watchdog, 600))
+        rec = _spmd_configs(args, world, rank, device, prog)
+        recs = [None] * world
+        dist.all_gather_object(recs, rec)
+        if rank == 0:
+            merged = dict(recs[0] or {})
+            out2 = (recs[2] or {}).get("config2_dotprod_moose", {}).get("output")
+            if "config2_dotprod_moose" in merged:
+                merged["config2_dotprod_moose"]["output"] = out2
+            line["spmd_three_gpus"] = merged
 
     prog.phase("done", 120)
     if rank == 0:

@@ -86,6 +86,11 @@ def test_bench_lr_inference_in_line():
     lr = d["lr_inference"]
     assert lr["one_gpu"]["eager"]["max_abs_err_vs_sklearn"] < 1e-3
     assert lr["spmd_one_party_per_gpu"]["max_abs_err_vs_sklearn"] < 1e-3
+    # BASELINE configs 2 and 3 with one party per rank (the reference's dotprod.moose: 32)
+    sp = d["spmd_three_gpus"]
+    assert sp["config2_dotprod_moose"]["output"] == pytest.approx(32.0, abs=1e-6)
+    assert sp["config2_dotprod_moose"]["p50_ms"] > 0
+    assert sp["config3_ringdot_3gpu"]["ms_per_step"] > 0
 
 
 @pytest.mark.parametrize("phase,rank", [("timed", 2), ("preflight", 1)])
