@@ -228,6 +228,11 @@ int mx_rss_mul3_k(int dev, int kind, int words, const void* x0, const void* x1, 
 //   g' = g ^ t ;  pk' = pk AND (pk << d) if both
 // zero shares: party p xors PRF(k_p) ^ PRF(k_{p+1}) at element e (t) and n + e (pk') of
 // ONE nonce -- the same values as the generic path's stacked [2, n] AND.
+// rep.binary_adder's whole carry chain (nlev Kogge-Stone levels, level l at nonces[l]) for
+// three stacked parties in one launch; returns the final g shares (device only)
+int mx_ks_adder3_k(int dev, int words, const void* g0, const void* g1, const void* p0,
+                   const void* p1, void* og0, void* og1, int64_t n, int nlev,
+                   const uint32_t* slots, const uint64_t* nonces, void* stream);
 int mx_ks_level3_k(int dev, int words, const void* g0, const void* g1, const void* p0,
                    const void* p1, void* og0, void* og1, void* op0, void* op1, int64_t n,
                    int d, int both, const uint32_t* slots, uint64_t nonce, void* stream);

@@ -849,6 +849,38 @@ int mx_ks_cross1_s(int dev, int words, const void* g0, const void* g1, const voi
   return mx_ks_cross1(0, words, g0, g1, p0, p1, z, n, d, both, keys16, nonce, stream);
 }
 
+int mx_ks_adder3_k(int dev, int words, const void* g0, const void* g1, const void* p0,
+                   const void* p1, void* og0, void* og1, int64_t n, int nlev,
+                   const uint32_t* slots, const uint64_t* nonces, void* stream) {
+  if (dev)
+    return mxh_ks_adder3_k(words, g0, g1, p0, p1, og0, og1, n, nlev, slots, nonces, stream);
+  // host: the per-level chain (mx_ks_level3_k), ping-ponging through temporaries
+  if (words != 1 && words != 2) return -2;
+  const size_t es = 8 * (size_t)words, sz = 3 * (size_t)n * es;
+  std::vector<uint8_t> G0(sz), G1(sz), A0(sz), A1(sz), NG0(sz), NG1(sz), NA0(sz), NA1(sz);
+  memcpy(G0.data(), g0, sz);
+  memcpy(G1.data(), g1, sz);
+  memcpy(A0.data(), p0, sz);
+  memcpy(A1.data(), p1, sz);
+  int d = 1;
+  for (int l = 0; l < nlev; ++l, d *= 2) {
+    const int both = 2 * d < 64 * words;
+    const int rc = mx_ks_level3_k(0, words, G0.data(), G1.data(), A0.data(), A1.data(),
+                                  NG0.data(), NG1.data(), NA0.data(), NA1.data(), n, d, both,
+                                  slots, nonces[l], stream);
+    if (rc) return rc;
+    G0.swap(NG0);
+    G1.swap(NG1);
+    if (both) {
+      A0.swap(NA0);
+      A1.swap(NA1);
+    }
+  }
+  memcpy(og0, G0.data(), sz);
+  memcpy(og1, G1.data(), sz);
+  return 0;
+}
+
 int mx_ks_level3_k(int dev, int words, const void* g0, const void* g1, const void* p0,
                    const void* p1, void* og0, void* og1, void* op0, void* op1, int64_t n,
                    int d, int both, const uint32_t* slots, uint64_t nonce, void* stream) {

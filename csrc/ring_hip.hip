@@ -573,6 +573,94 @@ __global__ void __launch_bounds__(256) k_ks_level3(const T* __restrict__ g0, con
   }
 }
 
+// The whole Kogge-Stone carry chain of rep.binary_adder for three stacked parties: the
+// levels d = 1, 2, 4, ... of k_ks_level3 in ONE launch (a level is element-local: its
+// shifts stay inside an element's packed bits, its reshare inside the stack), g and p held
+// in registers between levels; level l draws its masks at nonce nn[l] exactly as
+// k_ks_level3 does, so the result is bitwise the per-level chain's.  Returns the final g.
+struct Nonces8 {
+  uint64_t v[8];
+};
+
+template <class T>
+__global__ void __launch_bounds__(256) k_ks_adder3(const T* __restrict__ g0, const T* __restrict__ g1,
+                                                   const T* __restrict__ p0, const T* __restrict__ p1,
+                                                   T* __restrict__ og0, T* __restrict__ og1,
+                                                   int64_t n, int nlev, KeySrc keys, Nonces8 nn) {
+  constexpr int EPB = 256 / 6;
+  constexpr int W = 8 * (int)sizeof(T);
+  __shared__ uint32_t rks[3][kKeyWords];
+  __shared__ T ks[6][EPB];
+  stage_keys(rks, keys, 3);
+  constexpr int P = Lane<T>::kPer;
+  const int tid = threadIdx.x, s = tid / EPB, le = tid % EPB;
+  for (int64_t e0 = (int64_t)blockIdx.x * EPB; e0 < n; e0 += (int64_t)gridDim.x * EPB) {
+    const int64_t e = e0 + tid;
+    const bool act = tid < EPB && e < n;
+    T G0[3], G1[3], A0[3], A1[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      const int64_t i = (int64_t)p * n + e;
+      G0[p] = act ? g0[i] : (T)0;
+      G1[p] = act ? g1[i] : (T)0;
+      A0[p] = act ? p0[i] : (T)0;
+      A1[p] = act ? p1[i] : (T)0;
+    }
+    int d = 1;
+    for (int lev = 0; lev < nlev; ++lev, d *= 2) {
+      const bool both = 2 * d < W;
+      const int NS = both ? 6 : 3;
+      if (s < NS && e0 + le < n) {
+        const int64_t c = (s < 3 ? 0 : n) + e0 + le;  // t at e, pk' at n + e
+        uint64_t lo, hi;
+        prf_chunk(rks[s % 3], nn.v[lev], (uint64_t)(c / P), &lo, &hi);
+        ks[s][le] = pick<T>(lo, hi, (int)(c % P));
+      }
+      __syncthreads();
+      if (act) {
+        T t[3], q[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const int pn = p == 2 ? 0 : p + 1;
+          const T s0 = G0[p] << d, s1 = G1[p] << d;
+          t[p] = (A0[p] & s0) ^ (A0[p] & s1) ^ (A1[p] & s0) ^ ks[p][tid] ^ ks[pn][tid];
+          if (both) {
+            const T u0 = A0[p] << d, u1 = A1[p] << d;
+            q[p] = (A0[p] & u0) ^ (A0[p] & u1) ^ (A1[p] & u0) ^ ks[3 + p][tid] ^ ks[3 + pn][tid];
+          } else {
+            q[p] = 0;
+          }
+        }
+        T nG1[3], nA1[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const int pn = p == 2 ? 0 : p + 1;
+          nG1[p] = G1[p] ^ t[pn];
+          nA1[p] = q[pn];
+        }
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          G0[p] ^= t[p];
+          G1[p] = nG1[p];
+          if (both) {
+            A0[p] = q[p];
+            A1[p] = nA1[p];
+          }
+        }
+      }
+      __syncthreads();
+    }
+    if (act) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const int64_t i = (int64_t)p * n + e;
+        og0[i] = G0[p];
+        og1[i] = G1[p];
+      }
+    }
+  }
+}
+
 // One party's cross terms of a Kogge-Stone level (mx_ks_cross1): thread per element.
 template <class T>
 __global__ void __launch_bounds__(256) k_ks_cross1(const T* __restrict__ g0, const T* __restrict__ g1,
@@ -1384,6 +1472,31 @@ int mxh_ks_level3_k(int words, const void* g0, const void* g1, const void* p0, c
     hipLaunchKernelGGL(k_ks_level3<u128>, dim3(ks_grid(n)), dim3(kBlock), 0, S(stream),
                        (const u128*)g0, (const u128*)g1, (const u128*)p0, (const u128*)p1,
                        (u128*)og0, (u128*)og1, (u128*)op0, (u128*)op1, n, d, both, k, nonce);
+  } else {
+    return -2;
+  }
+  MX_LAUNCH_CHECK();
+  return 0;
+}
+
+int mxh_ks_adder3_k(int words, const void* g0, const void* g1, const void* p0, const void* p1,
+                    void* og0, void* og1, int64_t n, int nlev, const uint32_t* slots,
+                    const uint64_t* nonces, void* stream) {
+  if (n == 0) return 0;
+  if (nlev < 1 || nlev > 8) return -3;
+  const uint32_t* ptrs[3];
+  for (int i = 0; i < 3; ++i) ptrs[i] = slots + MX_KEY_SLOT_WORDS * i;
+  KeySrc k = mxd::keysrc_slots(ptrs, 3);
+  Nonces8 nn{};
+  for (int l = 0; l < nlev; ++l) nn.v[l] = nonces[l];
+  if (words == 1) {
+    hipLaunchKernelGGL(k_ks_adder3<u64>, dim3(ks_grid(n)), dim3(kBlock), 0, S(stream),
+                       (const u64*)g0, (const u64*)g1, (const u64*)p0, (const u64*)p1,
+                       (u64*)og0, (u64*)og1, n, nlev, k, nn);
+  } else if (words == 2) {
+    hipLaunchKernelGGL(k_ks_adder3<u128>, dim3(ks_grid(n)), dim3(kBlock), 0, S(stream),
+                       (const u128*)g0, (const u128*)g1, (const u128*)p0, (const u128*)p1,
+                       (u128*)og0, (u128*)og1, n, nlev, k, nn);
   } else {
     return -2;
   }

@@ -1397,6 +1397,22 @@ def ks_cross1_s(g0: RT, g1: RT, p0: RT, p1: RT, d: int, both: bool, slot_ptrs,
     return z
 
 
+def ks_adder3_k(g0: RT, g1: RT, p0: RT, p1: RT, slot_ptr: int, nonces) -> tuple:
+    """The whole Kogge-Stone carry chain (len(nonces) levels d = 1, 2, 4, ...) for three
+    stacked parties in one launch (mx_ks_adder3_k): bitwise the chain of ks_level3_k calls
+    with those nonces; returns the final (g0, g1)."""
+    bits = g0.bits
+    datas = [x.data.contiguous() for x in (g0, g1, p0, p1)]
+    n = math.prod(g0.shape) // 3
+    o0, o1 = empty2(g0.shape, bits, g0.device)
+    arr = (ctypes.c_uint64 * len(nonces))(*[int(v) & MASK64 for v in nonces])
+    nat.check(nat.lib().mx_ks_adder3_k(
+        nat.dev_of(o0.data), _words(bits), *[nat.ptr(x) for x in datas], nat.ptr(o0.data),
+        nat.ptr(o1.data), n, len(nonces), ctypes.c_void_p(slot_ptr), arr,
+        nat.stream_of(o0.data)), "ks_adder3_k")
+    return o0, o1
+
+
 def ks_level3_k(g0: RT, g1: RT, p0: RT, p1: RT, d: int, both: bool, slot_ptr: int,
                 nonce: int):
     """One fused Kogge-Stone level for three stacked parties (mx_ks_level3_k): returns

@@ -1,0 +1,44 @@
+"""rep.binary_adder's Kogge-Stone carry chain in one launch (mx_ks_adder3_k): bitwise the
+chain of per-level kernels (mx_ks_level3_k) with the same nonces, on the host and on the
+device (reference: replicated/misc.rs binary adder; the level structure is bits.rs)."""
+import pytest
+import torch
+
+from moose_amd.ops import ring as R
+from moose_amd.runtime.keys import KeyTable
+
+
+def _chain(bits, device):
+    kt = KeyTable(device, capacity=8)
+    base = kt.alloc(3)
+    g = torch.Generator().manual_seed(bits)
+    n = 301
+    mk = lambda: R.RT(torch.randint(-2**62, 2**62, (3, n) + ((2,) if bits == 128 else ()),  # noqa: E731
+                                    dtype=torch.int64, generator=g).to(device), bits)
+    g0, g1, p0, p1 = mk(), mk(), mk(), mk()
+    nl = bits.bit_length() - 1
+    nonces = [1000 + 3 * i for i in range(nl)]
+    fused = R.ks_adder3_k(g0, g1, p0, p1, kt.ptr(base), nonces)
+    G0, G1, A0, A1 = g0, g1, p0, p1
+    d = 1
+    for lev in range(nl):
+        both = 2 * d < bits
+        o = R.ks_level3_k(G0, G1, A0, A1, d, both, kt.ptr(base), nonces[lev])
+        G0, G1 = o[0], o[1]
+        if both:
+            A0, A1 = o[2], o[3]
+        d *= 2
+    return fused, (G0, G1), kt.t.cpu()
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+def test_ks_adder_chain_host(bits):
+    fused, chain, _ = _chain(bits, "cpu")
+    assert torch.equal(fused[0].data, chain[0].data) and torch.equal(fused[1].data, chain[1].data)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [64, 128])
+def test_ks_adder_chain_gpu(bits):
+    fused, chain, _ = _chain(bits, "cuda")
+    assert torch.equal(fused[0].data, chain[0].data) and torch.equal(fused[1].data, chain[1].data)
