@@ -121,6 +121,16 @@ class RoundB:
                 for c, r in enumerate(roles)]
 
 
+class NoRoundB:
+    """The deferred round of a process that hosts no party of the placement (SPMD
+    outsiders): nothing to send, nothing to complete."""
+
+    done = True
+
+    def finish(self):
+        pass
+
+
 def dot_trunc_tail(sess, plc, roles, cross, bits, m, nonces, out0, out1, slots, pre=None,
                    defer=False):
     """Zero share + reshare + TruncPr of the local cross products ``cross`` (one dense
