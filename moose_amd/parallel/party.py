@@ -19,7 +19,13 @@ Fixed-point dot tail (``rep.dot_trunc``): reference ``replicated/arith.rs:436-49
 cross terms, zero share, reshare) followed by ``replicated/fixedpoint.rs:80-103`` ->
 ``additive/trunc.rs:114-170`` (TruncPr with dealer P2).  Here the reshare is folded into
 TruncPr's first round (``rss_party.hip``): 2 rounds and 8 messages instead of 3 rounds and
-9, with bitwise the same output shares.
+9, with bitwise the same output shares.  Two schedule refinements on top:
+
+* the dealer's messages (rt1, rm1) depend on keys and nonces only and go out before the
+  GEMM (:func:`dealer_early`);
+* round B can be left pending (:class:`RoundB`): a product that is revealed to the dealer
+  next merges it with the reveal -- w0 and w1 go straight to P2 -- and otherwise it runs
+  when the shares are first read (``protocols/replicated.py`` DeferredRep).
 """
 from __future__ import annotations
 
