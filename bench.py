@@ -724,6 +724,8 @@ def _main(args, prog_out):
     if zero_slot is not None:
         line["zero_slot_aware"] = zero_slot
     line["device"] = _device_info(device)
+    if device.type == "cuda":  # device memory high-water mark of this rank (of 288 GB)
+        line["peak_mem_gib_rank0"] = round(torch.cuda.max_memory_allocated(device) / 2**30, 2)
     line["revision"] = _revision()
     prog.headline_done(line)
 
