@@ -724,8 +724,15 @@ def _main(args, prog_out):
     if zero_slot is not None:
         line["zero_slot_aware"] = zero_slot
     line["device"] = _device_info(device)
-    if device.type == "cuda":  # device memory high-water mark of this rank (of 288 GB)
-        line["peak_mem_gib_rank0"] = round(torch.cuda.max_memory_allocated(device) / 2**30, 2)
+    if device.type == "cuda":
+        # rank 0's device memory: the torch allocator's high-water mark, and what the device
+        # reports in use after the steps (this also counts the native GEMM workspaces and
+        # the caching allocator's reserve)
+        free, total = torch.cuda.mem_get_info(device)
+        line["mem_gib_rank0"] = {
+            "torch_peak_allocated": round(torch.cuda.max_memory_allocated(device) / 2**30, 2),
+            "device_in_use": round((total - free) / 2**30, 2),
+            "device_total": round(total / 2**30, 1)}
     line["revision"] = _revision()
     prog.headline_done(line)
 
