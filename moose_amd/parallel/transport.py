@@ -94,6 +94,9 @@ class Transport:
         except (RuntimeError, ValueError):
             backend = "none"
         self.stage = backend == "gloo" and self.device.type == "cuda"
+        # RCCL: a send-only round does not hold the compute stream (exchange)
+        self.async_sends = backend == "nccl"
+        self._unwaited = []
 
     # -- encoding -----------------------------------------------------------------
     def _header(self, v):
@@ -310,8 +313,18 @@ class Transport:
                 buf = out
             ops.append(dist.P2POp(dist.irecv, buf, src, group=self.group))
         if ops:
-            for w in dist.batch_isend_irecv(ops):
-                w.wait()
+            works = dist.batch_isend_irecv(ops)
+            if recvs or not self.async_sends:
+                for w in works:
+                    w.wait()
+            else:
+                # a send-only round (a share's owner, the dealer, the revealing party): the
+                # compute stream goes on while the bytes travel -- nothing here reads what
+                # a send delivers, and the process group keeps the payload alive until the
+                # transfer is done (its RCCL stream runs the round's messages in order)
+                self._unwaited.extend(works)
+                if len(self._unwaited) > 64:  # bound the bookkeeping
+                    self._unwaited = self._unwaited[-32:]
         for out, buf in staged:
             out.copy_(buf)
 
