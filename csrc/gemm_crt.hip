@@ -933,13 +933,14 @@ int crt_kernel() {  // MOOSEX_CRT_KERNEL: 1 = 4 waves of 128x128, 2 = 8 waves of
   // barrier at the start of each k-step and the next stage's fragment reads spread over the
   // step's MFMAs (the default: 4-6 % faster than 6 on the same box, profiles/r3_crt_gemm.md),
   // 9 = 8 with 4 stages, 10 / 11 = 8 / 9 with the DMAs spread over the step too, 12 = 4
-  // with 8's schedule (spills).  Tried and removed (profiles/r3_crt_gemm.md): DMAs through
+  // with 8's schedule, 13 = 12 with 4 stages, 14 / 15 = 12 / 13 with the DMAs spread (4 and
+  // 12-15 need the VGPR-form MFMA flag of _native/build.py, else they spill).  Tried and removed (profiles/r3_crt_gemm.md): DMAs through
   // buffer descriptors (16.2 vs 15.5 ms per step), a persistent one-block-per-CU kernel
   // streaming all its tiles' k-steps (16.2 vs 15.5 ms), B fragments loaded from global
   // memory straight into registers (hipcc drains every counter before their first use)
   const char* e = std::getenv("MOOSEX_CRT_KERNEL");
   const int v = e ? std::atoi(e) : 8;
-  return v >= 1 && v <= 12 ? v : 8;
+  return v >= 1 && v <= 15 ? v : 8;
 }
 bool crt_mfma16() { return crt_kernel() >= 4; }
 int recon_dot4() {  // MOOSEX_CRT_RECON=0: the multiply-add reconstruction
@@ -1037,6 +1038,9 @@ void launch_crt_gemm(const CPlan& p, const Tables& tb, int64_t batch, const int8
     case 10: launch_variant<2, 4, 256, 2, true, 3, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
     case 11: launch_variant<2, 4, 256, 2, true, 4, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
     case 12: launch_variant<2, 2, 256, 1, true, 3, 1>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
+    case 13: launch_variant<2, 2, 256, 1, true, 4, 1>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
+    case 14: launch_variant<2, 2, 256, 1, true, 3, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
+    case 15: launch_variant<2, 2, 256, 1, true, 4, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
     default: launch_variant<2, 2, 128, 2, true>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
   }
 }

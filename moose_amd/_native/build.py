@@ -34,6 +34,13 @@ def _headers_mtime():
     return max((h.stat().st_mtime for h in hs), default=0.0)
 
 
+# Per-source extra flags.  gemm_crt.hip: let the MFMA accumulators live in VGPRs and the
+# allocator use the AGPR half of the unified register file for the rest, so the 4-wave
+# 128x128 wave-tile variants (256 accumulators per lane, one wave per SIMD) compile without
+# scratch spills (default form: 275 spilled VGPRs).  The 8-wave variants' code is unchanged.
+_HIP_EXTRA = {"gemm_crt.hip": ("-mllvm", "-amdgpu-mfma-vgpr-form=1")}
+
+
 def _compile(src: Path, obj: Path, verbose: bool):
     if src.suffix == ".hip":
         cmd = [
@@ -43,6 +50,7 @@ def _compile(src: Path, obj: Path, verbose: bool):
             "-fPIC",
             "-std=c++17",
             "-Wno-unused-result",
+            *_HIP_EXTRA.get(src.name, ()),
             "-c",
             str(src),
             "-o",
