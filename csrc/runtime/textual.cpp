@@ -254,8 +254,12 @@ void parse_constant_literal(Cursor& c, std::string_view kind, Value& v) {
     v.nums.push_back(c.number());
     c.expect(",");
     v.nums.push_back(c.number());
-    c.expect(",");
-    v.nums.push_back(c.number());
+    if (c.peek(",")) {
+      c.expect(",");
+      v.nums.push_back(c.number());
+    } else {  // the reference's Fixed(value, precision): integral precision 0
+      v.nums.insert(v.nums.begin() + 1, Num{std::string_view("0"), false});
+    }
   } else {
     c.fail("unknown constant kind " + std::string(kind));
   }

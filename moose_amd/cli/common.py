@@ -3,7 +3,17 @@ from __future__ import annotations
 
 from moose_amd.ir.computation import Computation
 
-FORMATS = ("textual", "msgpack", "bincode")
+# msgpack / bincode: this framework's compact binary forms; msgpack-rs / bincode-rs: the
+# reference's own NamedComputation bytes (moose_amd/ir/rust_serde.py)
+FORMATS = ("textual", "msgpack", "bincode", "msgpack-rs", "bincode-rs")
+
+
+def _rust(fmt):
+    from moose_amd.ir import rust_serde
+
+    if fmt == "msgpack-rs":
+        return rust_serde.to_rust_msgpack, rust_serde.from_rust_msgpack
+    return rust_serde.to_rust_bincode, rust_serde.from_rust_bincode
 
 
 def read_computation(path, fmt="textual") -> Computation:
@@ -16,6 +26,9 @@ def read_computation(path, fmt="textual") -> Computation:
     if fmt == "bincode":
         with open(path, "rb") as f:
             return Computation.from_bincode(f.read())
+    if fmt in ("msgpack-rs", "bincode-rs"):
+        with open(path, "rb") as f:
+            return _rust(fmt)[1](f.read())
     raise ValueError(f"unsupported computation format {fmt!r}")
 
 
@@ -39,6 +52,12 @@ def write_computation(comp: Computation, path, fmt="textual"):
             raise ValueError("bincode output needs --output")
         with open(path, "wb") as f:
             f.write(comp.to_bincode())
+        return
+    if fmt in ("msgpack-rs", "bincode-rs"):
+        if path is None:
+            raise ValueError(f"{fmt} output needs --output")
+        with open(path, "wb") as f:
+            f.write(_rust(fmt)[0](comp))
         return
     raise ValueError(f"unsupported computation format {fmt!r}")
 

@@ -2,7 +2,8 @@
 
 Parity: reference ``moose/src/bin/elk/main.rs:11-276``::
 
-    elk compile INPUT [-o OUT] [-i textual|msgpack] [-f textual|msgpack] [-p pass,pass]
+    elk compile INPUT [-o OUT] [-i FORMAT] [-f FORMAT] [-p pass,pass]
+        (FORMAT: textual, msgpack, bincode, or the reference's own msgpack-rs / bincode-rs)
                       [--arg-shape name=3,4 ...]
     elk stats op-hist  INPUT [--by-placement]
     elk stats op-count INPUT [--by-placement]

@@ -148,8 +148,10 @@ def _parse_constant_literal(c: _Cursor, kind: str) -> Constant:
         v = float(_num(c))
         c.expect(",")
         i = int(_num(c))
-        c.expect(",")
-        f = int(_num(c))
+        if c.eat(","):
+            f = int(_num(c))
+        else:  # the reference's Fixed(value, precision) (textual/parsing.rs:1556)
+            i, f = 0, i
         val = Constant("Fixed", (v, i, f))
     else:
         c.fail(f"unknown constant kind {kind}")
