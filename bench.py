@@ -439,6 +439,10 @@ def main():
     except BaseException as e:  # noqa: BLE001 - report, then fail
         if prog:
             prog[0].fail(f"{type(e).__name__}: {e}")
+            if prog[0].result is not None:
+                # the headline was measured and rank 0 printed it with this error noted: an
+                # optional extra (LR inference, configs 2/3) failed -- keep the measurement
+                os._exit(0)
         raise
 
 

@@ -68,15 +68,26 @@ def stalled_ranks(phases: Dict[int, dict]):
 
 
 def stall_if_requested(rank: int, phase: str):
-    spec = os.environ.get("MOOSEX_BENCH_STALL", "")
-    if not spec:
-        return
-    r, _, ph = spec.partition(":")
-    if int(r) == rank and ph == phase:
+    """Test hooks: ``MOOSEX_BENCH_STALL=rank:phase`` hangs that rank at the phase's entry,
+    ``MOOSEX_BENCH_FAIL=rank:phase`` raises there."""
+    for var in ("MOOSEX_BENCH_STALL", "MOOSEX_BENCH_FAIL"):
+        spec = os.environ.get(var, "")
+        if not spec:
+            continue
+        r, _, ph = spec.partition(":")
+        if int(r) != rank or ph != phase:
+            continue
+        if var == "MOOSEX_BENCH_FAIL":
+            raise RuntimeError(f"MOOSEX_BENCH_FAIL in {phase}")
         print(f"[bench] rank {rank}: MOOSEX_BENCH_STALL -> hanging in {phase}", file=sys.stderr,
               flush=True)
         while True:
             time.sleep(3600)
+
+
+def failed_ranks(phases: Dict[int, dict]):
+    """Ranks whose phase record says they raised (``Progress.fail``)."""
+    return sorted(r for r, p in phases.items() if p.get("failed"))
 
 
 class Progress:
@@ -96,6 +107,7 @@ class Progress:
         self._lock = threading.Lock()
         self._wlock = threading.Lock()
         self._fired = False
+        self.failed: Optional[str] = None
         self._write()
         t = threading.Thread(target=self._watch, name="bench-watchdog", daemon=True)
         t.start()
@@ -127,6 +139,8 @@ class Progress:
         with self._wlock:
             rec = {"phase": self.phase_name, "seq": self.seq, "step": self.step,
                    "pid": os.getpid(), "t": round(time.monotonic() - self.t0, 3)}
+            if self.failed:
+                rec["failed"] = self.failed
             self._written = (self.seq, self.step)
             tmp = os.path.join(self.dir, f".rank{self.rank}.tmp")
             try:
@@ -138,16 +152,22 @@ class Progress:
                       file=sys.stderr, flush=True)
 
     def _watch(self):
+        n = 0
         while True:
             time.sleep(0.5)
+            n += 1
             if (self.seq, self.step) != getattr(self, "_written", None):
                 self._write()
+            # a rank that raised ends the run now, not when this rank's phase budget runs
+            # out (its peers would otherwise wait in a collective until then)
+            bad = failed_ranks(read_phases(self.dir, self.world)) if n % 2 == 0 else []
+            bad = [r for r in bad if r != self.rank]
             with self._lock:
-                late = time.monotonic() > self.deadline and not self._fired
+                late = (time.monotonic() > self.deadline or bad) and not self._fired
                 if late:
                     self._fired = True
             if late:
-                self.fire()
+                self.fire(f"rank {bad[0]} failed" if bad else None)
 
     def fail(self, what: str):
         """An exception on this rank: report it like a stall (rank 0 prints the line),
@@ -156,7 +176,9 @@ class Progress:
             if self._fired:
                 return
             self._fired = True
-        self.fire(f"rank {self.rank}: {what} in phase {self.phase_name!r}", exit=False)
+        self.failed = f"{what} in phase {self.phase_name!r}"
+        self._write()
+        self.fire(f"rank {self.rank}: {self.failed}", exit=False)
 
     def fire(self, msg: Optional[str] = None, exit: bool = True):
         phases = read_phases(self.dir, self.world)

@@ -129,3 +129,28 @@ def test_supervisor_kills_a_hung_rank_group(tmp_path):
                           2, 2.0, {"metric": "m"}, str(tmp_path))
     d = json.loads(buf.getvalue().strip().splitlines()[-1])
     assert rc == 3 and d["stalled_ranks"] == [1] and "error" in d
+
+
+@pytest.mark.parametrize("phase,rank,headline", [("lr_spmd", 1, True), ("warmup", 2, False)])
+def test_bench_rank_exception_ends_the_run_promptly(phase, rank, headline):
+    """A rank that raises ends the whole group at once (its peers' watchdogs read its
+    failure record instead of waiting out their phase budget).  After the headline was
+    measured (an optional extra failed) the line keeps the measurement, notes the error
+    and the run exits 0; before it, the run fails with an error line."""
+    import time
+
+    cmd = [sys.executable, "bench.py", "--gpus", "3", "--steps", "1", "--warmup", "1",
+           "--size", "32", "--lr-runs", "2", "--watchdog", "200"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["MOOSEX_BENCH_FAIL"] = f"{rank}:{phase}"
+    t0 = time.monotonic()
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=400, env=env)
+    assert time.monotonic() - t0 < 150  # far inside the 200 s phase budget
+    d = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    if headline:
+        assert out.returncode == 0, out.stderr[-2000:]
+        assert d["value"] > 0 and d["check"]["ok"]
+        assert d["errors"][0]["phase"] == phase
+    else:
+        assert out.returncode != 0
+        assert d["value"] is None and f"rank {rank}" in d["error"]
