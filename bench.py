@@ -157,7 +157,8 @@ def _self_launch(args):
                                           "moose_amd", "utils", "benchwatch.py"))
     benchwatch = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(benchwatch)
-    rdir = tempfile.mkdtemp(prefix="moosex_bench_")
+    rdir = os.environ.get("MOOSEX_BENCH_RUN_DIR") or tempfile.mkdtemp(prefix="moosex_bench_")
+    os.makedirs(rdir, exist_ok=True)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
            "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
@@ -379,8 +380,12 @@ def _spmd_configs(args, world, rank, device, prog):
     from moose_amd.parallel.transport import Transport
     from moose_amd.runtime.interpreter import Interpreter
 
-    g = dist.new_group([0, 1, 2])  # every rank creates the group
+    g = dist.new_group([0, 1, 2])  # every rank creates every group
+    g6 = dist.new_group(list(range(6))) if world >= 6 else None
+    gout = dist.new_group([2, 5]) if world >= 6 else None
     if rank >= 3:
+        if world >= 6 and rank < 6:
+            return {"config5_dp2_replicas": _config5(args, world, rank, device, prog, g6, gout)}
         return None
     bdev = [device.index] if device.type == "cuda" and dist.get_backend() == "nccl" else None
     tdev = device if dist.get_backend() == "nccl" else torch.device("cpu")
@@ -423,7 +428,71 @@ def _spmd_configs(args, world, rank, device, prog):
     ms = sum(per) / len(per)
     rec["config3_ringdot_3gpu"] = {"ms_per_step": ms, "elems_per_sec": n * n / ms * 1e3,
                                    "size": n, "steps": 5}
+    if world >= 6:
+        rec["config5_dp2_replicas"] = _config5(args, world, rank, device, prog, g6, gout)
     return rec
+
+
+MPSPDZ_DOT_1000_S = 5.910  # benchmarks/README.md: moose, one 1000x1000 dot, sequential table
+
+
+def _config5(args, world, rank, device, prog, g6, gout):
+    """BASELINE config 5 (benchmarks/mp-spdz parity): two data-parallel replicas of the
+    3-party session on six GPUs (ranks 3r, 3r+1, 3r+2 = alice, bob, carole of replica r),
+    each step one replicated fixed(14,23) 1000 x 1000 dot per replica -- every reshare an
+    RCCL send/recv inside the replica -- and an all-gather of the two revealed outputs
+    between the replicas' output owners (ranks 2 and 5).  ms per step = max over the six
+    ranks, mean of 5 steps after 2 warmup steps."""
+    import torch
+    import torch.distributed as dist
+
+    from moose_amd.parallel.spmd import SPMDSession
+    from moose_amd.parallel.transport import Transport
+    from moose_amd.runtime.interpreter import Interpreter
+
+    rep = rank // 3
+    n = min(1000, args.size)  # the reference's table size (smaller only in CPU tests)
+    comp = build_computation(args.ring)
+    roles = {r: 3 * rep + i for i, r in enumerate(ROLES)}
+    tr = Transport(rank, world, device, plans=True)
+    x = _inputs(n, rep, "x", device) if rank % 3 == 0 else None
+    y = _inputs(n, rep, "y", device) if rank % 3 == 1 else None
+    feed = {k: v for k, v in (("x", x), ("y", y)) if v is not None}
+    nccl = dist.get_backend() == "nccl"
+    bdev = [device.index] if device.type == "cuda" and nccl else None
+    gdev = device if nccl else torch.device("cpu")
+    both = torch.empty(2 * n * n, dtype=torch.float64, device=gdev)
+    lat, steps, warm = [], 5, 2
+    for i in range(steps + warm):
+        prog.tick(i)
+        dist.barrier(group=g6, device_ids=bdev)
+        t0 = time.perf_counter()
+        outs = Interpreter(SPMDSession(ROLES[rank % 3], roles, tr, device), {},
+                           fixedpoint_ring=128).run(comp, feed)
+        if rank % 3 == 2:  # the replica's client: collect both replicas' outputs
+            z = outs["output_0"].v.v.reshape(-1).to(device=gdev, dtype=torch.float64)
+            dist.all_gather_into_tensor(both, z.contiguous(), group=gout)
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        if i >= warm:
+            lat.append((time.perf_counter() - t0) * 1e3)
+    err = None
+    if rank % 3 == 2:
+        err = 0.0
+        for r in range(2):
+            ref = _inputs(n, r, "x", device) @ _inputs(n, r, "y", device)
+            got = both[r * n * n:(r + 1) * n * n].to(device).reshape(n, n)
+            err = max(err, (got - ref).abs().max().item())
+    t = torch.tensor(lat + [err if err is not None else -1.0], dtype=torch.float64, device=gdev)
+    allt = torch.empty(6 * (steps + 1), dtype=torch.float64, device=gdev)
+    dist.all_gather_into_tensor(allt, t, group=g6)
+    allt = allt.reshape(6, steps + 1).cpu()
+    ms = allt[:, :steps].max(dim=0).values.mean().item()
+    errs = [e for e in allt[:, steps].tolist() if e >= 0]
+    return {"ms_per_step": ms, "replicas": 2, "size": n, "dots_per_step": 2,
+            "steps": steps, "dots_per_sec": 2e3 / ms,
+            "vs_reference_dots_per_sec": 2e3 / ms * MPSPDZ_DOT_1000_S,
+            "gathered_max_abs_err": max(errs) if errs else None}
 
 
 # ---------------------------------------------------------------------------------------
@@ -808,6 +877,8 @@ def _main(args, prog_out):
             out2 = (recs[2] or {}).get("config2_dotprod_moose", {}).get("output")
             if "config2_dotprod_moose" in merged:
                 merged["config2_dotprod_moose"]["output"] = out2
+            if "config5_dp2_replicas" in merged:
+                line["config5_dp2_replicas"] = merged.pop("config5_dp2_replicas")
             line["spmd_three_gpus"] = merged
 
     prog.phase("done", 120)

@@ -154,3 +154,14 @@ def test_bench_rank_exception_ends_the_run_promptly(phase, rank, headline):
     else:
         assert out.returncode != 0
         assert d["value"] is None and f"rank {rank}" in d["error"]
+
+
+def test_bench_config5_two_replicas_on_six_ranks():
+    """BASELINE config 5: two data-parallel replicas of the 3-party session on six ranks,
+    RingDot per replica with every reshare cross-rank, both revealed outputs all-gathered
+    between the replicas' clients and checked."""
+    d = _run_self(6, "--layout", "cyclic")
+    c5 = d["config5_dp2_replicas"]
+    assert c5["replicas"] == 2 and c5["dots_per_step"] == 2 and c5["ms_per_step"] > 0
+    assert c5["gathered_max_abs_err"] < 1e-3
+    assert d["spmd_three_gpus"]["config2_dotprod_moose"]["output"] == pytest.approx(32.0)
