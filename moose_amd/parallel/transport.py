@@ -69,11 +69,15 @@ class Transport:
     """
 
     def __init__(self, rank: int, world: int, device, group=None, fault=None,
-                 plans: bool = False):
+                 plans: bool = False, plan_scope=None):
         self.rank = rank
         # message plans (module doc of _PLANS): only for runtimes that hand every process
         # every argument, so that all processes derive the same plan key
         self.plans = plans
+        # plans are shared by the transports of one scope: a process that runs the same
+        # computation under another argument layout (e.g. a party that holds no argument,
+        # so its key cannot see the others' shapes) uses a scope of its own for it
+        self.plan_scope = plan_scope
         self.world = world
         self.device = torch.device(device)
         self.group = group
@@ -203,7 +207,7 @@ class Transport:
     def begin_plan(self, key):
         """Start an evaluation under plan ``key`` (identical on every process): replay the
         recorded headers if the plan exists, else record them."""
-        p = _PLANS.get((self.rank, self.world, key))
+        p = _PLANS.get((self.plan_scope, self.rank, self.world, key))
         self._plan_key = key
         self._cursor_in, self._cursor_out = {}, {}
         if p is not None:
@@ -213,7 +217,7 @@ class Transport:
 
     def end_plan(self, ok: bool = True):
         if self._mode == "record" and ok:
-            _PLANS[(self.rank, self.world, self._plan_key)] = self._plan
+            _PLANS[(self.plan_scope, self.rank, self.world, self._plan_key)] = self._plan
         self._mode = self._plan = None
 
     def _next(self, cursors, peer):
