@@ -59,9 +59,14 @@ def _program(sess, xb, ya, mb, ma):
     return tensors, (out.v.data.clone(), dt.v.data.clone())
 
 
-def _worker(rank, world, port, q, device="cpu", offsets=None, chunks=4, dirs=None):
+def _worker(rank, world, port, q, device="cpu", offsets=None, chunks=4, dirs=None,
+            backend="gloo"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":  # one GPU per rank, every exchange an RCCL send/recv
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(rank)
+        device = f"cuda:{rank}"
+    dist.init_process_group(backend, rank=rank, world_size=world)
     from moose_amd.parallel.cyclic import CyclicSession
     from moose_amd.parallel.cyclic import RingComm
     from moose_amd.runtime.session import HV
@@ -108,11 +113,12 @@ def _stacked_reference(keys, session, chunks=4, dirs=None):
     return out
 
 
-def _run(world, device, offsets=None, chunks=4, dirs=None):
+def _run(world, device, offsets=None, chunks=4, dirs=None, backend="gloo"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q, device, offsets, chunks, dirs)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, device, offsets, chunks, dirs,
+                                            backend)) for r in range(world)]
     for p in ps:
         p.start()
     got = {}
@@ -200,3 +206,15 @@ def test_cyclic_on_gpu_bitwise_equals_cpu_stacked():
     the per-party key-pair kernels and the layout's data movement run on the device and
     must reproduce the CPU stacked reference bit for bit."""
     _run(3, "cuda:0")
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(torch.cuda.device_count() < 3, reason="RCCL across GPUs: needs >= 3 GPUs")
+@pytest.mark.parametrize("world", [3, 4])
+def test_cyclic_rccl_multi_gpu_bitwise_equals_cpu_stacked(world):
+    """One rank per GPU over RCCL (backend "nccl"): every reshare, dealer message and
+    reveal crosses xGMI, and the shares are bit for bit the CPU stacked session's
+    (multi-GPU RCCL tests gated on the device count)."""
+    if torch.cuda.device_count() < world:
+        pytest.skip(f"needs {world} GPUs")
+    _run(world, "cuda", backend="nccl")
