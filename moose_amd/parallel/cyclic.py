@@ -111,7 +111,10 @@ class RingComm:
             if r == self.rank or out.numel() == 0:
                 continue
             if self.stage:
-                buf = torch.empty(out.shape, dtype=out.dtype)
+                # pinned: the copy into ``out`` below is asynchronous, and the host caching
+                # allocator keeps a pinned buffer alive until that copy has run (a pageable
+                # buffer could be freed and reused while the DMA still reads it)
+                buf = torch.empty(out.shape, dtype=out.dtype, pin_memory=True)
                 staged.append((out, buf))
                 ops.append(dist.P2POp(dist.irecv, buf, r, group=self.group))
             else:
