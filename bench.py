@@ -642,6 +642,27 @@ def _main(args, prog_out):
             return StackedSession(device)
 
     n_steps = [0]
+    gloo_staged = (gather_mode != "none" and device.type == "cuda" and world > 1
+                   and dist.get_backend() == "gloo")
+
+    def _gather_staged(zc, k):
+        zh = zc.cpu()  # waits for the step's stream
+        if gather_mode == "all":
+            hb = torch.empty((len(owners) * n, n), dtype=torch.float64)
+            dist.all_gather_into_tensor(hb, zh, group=gather_group)
+        elif rank == root:
+            hb = torch.empty((len(owners) * n, n), dtype=torch.float64)
+            ops = [dist.P2POp(dist.irecv, hb[i * n:(i + 1) * n], r, group=gather_group)
+                   for i, r in enumerate(owners) if r != root]
+            hb[owners.index(root) * n:(owners.index(root) + 1) * n].copy_(zh)
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        else:
+            for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, zh, root,
+                                                        group=gather_group)]):
+                w.wait()
+            return
+        gather_bufs[k % len(gather_bufs)].copy_(hb)
 
     def step():
         if streams is None:
@@ -661,7 +682,11 @@ def _main(args, prog_out):
             while len(pending) >= 2 * max(1, len(owners) - 1):
                 pending.pop(0).wait()
             zc = z.contiguous()
-            if gather_mode == "all":
+            if gloo_staged:
+                # gloo moves host memory: stage the device output through the host, in
+                # stream order (one-GPU rehearsals only; RCCL takes the device tensors)
+                _gather_staged(zc, k)
+            elif gather_mode == "all":
                 buf = gather_bufs[k % len(gather_bufs)]
                 pending.append(dist.all_gather_into_tensor(buf, zc, group=gather_group,
                                                            async_op=True))
