@@ -102,6 +102,9 @@ def _parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--size", type=int, default=4096)
+    ap.add_argument("--link-probe-mib", type=int, default=256,
+                    help="after the headline (cyclic, N > 1): point-to-point GB/s of the "
+                         "layout's exchange pattern with this many MiB per message (0: off)")
     ap.add_argument("--spmd-configs", action=argparse.BooleanOptionalAction, default=True,
                     help="with >= 3 GPUs also time BASELINE configs 2 (tutorials/"
                          "dotprod.moose) and 3 (RingDot, one party per GPU) on ranks 0-2")
@@ -216,6 +219,51 @@ def _revision():
 # ---------------------------------------------------------------------------------------
 # preflight: one grouped round trip with every peer on every communicator
 # ---------------------------------------------------------------------------------------
+def _link_probe(comm, world, rank, device, prog, dists, mib, reps=3):
+    """Point-to-point bandwidth of the layout's exchange pattern, after the headline: every
+    rank sends ``mib`` MiB to rank + d and receives as much from rank - d (one grouped
+    exchange), for each distance d the cyclic layout uses, then for all of them at once
+    (the step's pattern).  GB/s per rank and direction = bytes / the slowest rank's best
+    time of ``reps``.  Gives the xGMI/RCCL numbers the step's link model needs."""
+    import torch
+    import torch.distributed as dist
+
+    nccl = dist.get_backend() == "nccl"
+    tdev = device if nccl else torch.device("cpu")
+    bdev = [device.index] if device.type == "cuda" and nccl else None
+    nbytes = mib << 20
+    src = torch.full((nbytes // 8,), rank, dtype=torch.int64, device=device)
+
+    def timed(ds, tick):
+        bufs = [torch.empty_like(src) for _ in ds]
+        best = float("inf")
+        for r in range(reps + 1):
+            prog.tick(tick)
+            dist.barrier(device_ids=bdev)
+            if device.type == "cuda":
+                torch.cuda.synchronize(device)
+            t0 = time.perf_counter()
+            comm.exchange([(src, (rank + d) % world) for d in ds],
+                          [(b, (rank - d) % world) for b, d in zip(bufs, ds)])
+            if device.type == "cuda":
+                torch.cuda.synchronize(device)
+            if r:  # the first round warms the connections up
+                best = min(best, time.perf_counter() - t0)
+        for b, d in zip(bufs, ds):
+            if int(b[0].item()) != (rank - d) % world:
+                raise RuntimeError(f"link probe: wrong payload from rank {(rank - d) % world}")
+        t = torch.tensor([best], dtype=torch.float64, device=tdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return round(len(ds) * nbytes / t.item() / 1e9, 2)
+
+    rec = {"mib": mib, "reps": reps, "backend": dist.get_backend(),
+           "gbs_per_rank_and_direction": {}}
+    for i, d in enumerate(dists):
+        rec["gbs_per_rank_and_direction"][f"d{d}"] = timed([d], i)
+    rec["gbs_per_rank_and_direction"]["all"] = timed(list(dists), len(dists))
+    return rec
+
+
 def _preflight(layout, comms, world, rank, device, prog, offsets=None):
     """Each rank sends its rank id to every peer it will exchange with and checks what it
     receives (catches a wrong peer map, a dead link or an RCCL set-up hang before the
@@ -866,6 +914,15 @@ def _main(args, prog_out):
         if worst >= 1e-2:
             line["error"] = f"wrong results: max abs error {worst} vs float64 torch"
             exit_code = 4
+
+    if layout == "cyclic" and world > 1 and args.link_probe_mib > 0:
+        prog.phase("link_probe", min(args.watchdog, 180))
+        off = list(offsets.values())
+        dists = sorted({(b - a) % world for a in off for b in off} - {0})
+        mib = args.link_probe_mib if dist.get_backend() == "nccl" else 1  # gloo: path only
+        probe = _link_probe(comms[0], world, rank, device, prog, dists, mib)
+        if rank == 0:
+            line["link_probe"] = probe
 
     if args.lr_runs > 0:
         prog.phase("lr", min(args.watchdog, 300))

@@ -70,6 +70,8 @@ def test_bench_self_launch(n, layout, sessions):
         assert d["gather"] == "root"
     if d["layout"] == "cyclic":  # every reshare crossed ranks
         assert min(d["p2p_bytes_per_step"]) > 0 and d["step_streams"] == 2
+        # after the headline: point-to-point GB/s of the layout's exchange pattern
+        assert all(v > 0 for v in d["link_probe"]["gbs_per_rank_and_direction"].values())
 
 
 def test_bench_lr_inference_in_line():
