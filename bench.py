@@ -192,6 +192,9 @@ def _device_info(device):
     info.update(name=p.name, arch=getattr(p, "gcnArchName", ""),
                 cus=p.multi_processor_count, mem_gib=round(p.total_memory / 2**30, 1),
                 clock_mhz=getattr(p, "clock_rate", 0) // 1000 or None)
+    # communication/runtime knobs in effect (RCCL reads the NCCL_* names)
+    info["env"] = {k: v for k, v in sorted(os.environ.items())
+                   if k.startswith(("NCCL_", "RCCL_", "HSA_", "GPU_MAX_HW_QUEUES", "HIP_"))}
     try:
         v = torch.cuda.nccl.version()
         info["rccl"] = ".".join(map(str, v)) if isinstance(v, tuple) else v
