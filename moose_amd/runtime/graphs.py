@@ -159,7 +159,9 @@ class GraphPlan:
 
         def begin():
             g = torch.cuda.CUDAGraph()
-            g.capture_begin(pool=pool)
+            # thread-local: only this thread's calls can invalidate the capture -- a
+            # process-group watchdog thread polling its events (multi-rank runs) cannot
+            g.capture_begin(pool=pool, capture_error_mode="thread_local")
             state["g"], state["n"] = g, 0
             if lanes is not None:  # the lanes join this segment's capture
                 lanes.fork()
