@@ -889,7 +889,7 @@ def _main(args, prog_out):
 
     exit_code = 0
     if args.check:
-        prog.phase("check", min(args.watchdog, 300))
+        prog.phase("check", min(args.watchdog, 150))
         check = None
         if out_owner:
             ref = _inputs(n, out_session, "x", device) @ _inputs(n, out_session, "y", device)
@@ -918,8 +918,11 @@ def _main(args, prog_out):
             line["error"] = f"wrong results: max abs error {worst} vs float64 torch"
             exit_code = 4
 
+    # the optional extras after the headline get short budgets: a hang in one of them
+    # fires the watchdog (which prints the measured line) well inside a driver's
+    # per-run limit, instead of the run being killed with no line at all
     if layout == "cyclic" and world > 1 and args.link_probe_mib > 0:
-        prog.phase("link_probe", min(args.watchdog, 180))
+        prog.phase("link_probe", min(args.watchdog, 60))
         off = list(offsets.values())
         dists = sorted({(b - a) % world for a in off for b in off} - {0})
         mib = args.link_probe_mib if dist.get_backend() == "nccl" else 1  # gloo: path only
@@ -928,7 +931,7 @@ def _main(args, prog_out):
             line["link_probe"] = probe
 
     if args.lr_runs > 0:
-        prog.phase("lr", min(args.watchdog, 300))
+        prog.phase("lr", min(args.watchdog, 120))
         lr = {"model": "ml-inference-with-onnx tutorial LogisticRegression (200x10, "
                        "fixed(24,40), Z_2^128, from_onnx)"}
         if rank == 0:
@@ -936,7 +939,7 @@ def _main(args, prog_out):
         if world > 1:
             dist.barrier()
         if world >= 3:
-            prog.phase("lr_spmd", min(args.watchdog, 300))
+            prog.phase("lr_spmd", min(args.watchdog, 120))
             rec = _lr_spmd(args.lr_runs, world, rank, device, prog)
             recs = [None] * world
             dist.all_gather_object(recs, rec)
@@ -955,7 +958,7 @@ def _main(args, prog_out):
             line["lr_inference"] = lr
 
     if world >= 3 and args.spmd_configs:
-        prog.phase("spmd_configs", min(args.watchdog, 600))
+        prog.phase("spmd_configs", min(args.watchdog, 180))
         rec = _spmd_configs(args, world, rank, device, prog)
         recs = [None] * world
         dist.all_gather_object(recs, rec)
