@@ -645,11 +645,14 @@ __global__ void __launch_bounds__(64 * WR * WC, MINW)
     for (int j = 0; j < NJ; ++j) fb[j] = *(const v4i*)(st + rowb + j * 16 * BK);
   };
 
+  // IL == 3 (STG == 5): one barrier per TWO k-steps; the prologue issues stages 0..3 and
+  // waits for 0..2 (stage 3 may still be in flight)
+  constexpr int PRO = IL == 3 ? 4 : STG;
 #pragma unroll
-  for (int s = 0; s < STG; ++s)
+  for (int s = 0; s < PRO; ++s)
 #pragma unroll
     for (int t = 0; t < PPW; ++t) dma(s < nkb ? s : nkb - 1, t, smem + s * kStageBytes);
-  __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0((STG - 1) * PPW));
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0((PRO - 1) * PPW));
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   frags(smem, fa0, fb0);
@@ -738,8 +741,61 @@ __global__ void __launch_bounds__(64 * WR * WC, MINW)
     }
   };
 
+  // IL == 3: five 32 KB stage buffers (160 KB), stage s in buffer s % 5, a barrier only at
+  // even k-steps.  Barrier B_k (even k) follows each wave's wait for its DMAs of stages
+  // k+1 and k+2 (only stage k+3's may still be in flight), so step k reads stage k+1 and
+  // step k+1 reads stage k+2 without a barrier of its own; and every wave has finished
+  // step k-1, so the buffers of stages k-1 and k (fragments already in registers) are free
+  // and take stages k+4 and k+5 -- issued in that order, the k+4 pieces first, so that
+  // "all but the last PPW" is exactly "all but stage k+5".
+  auto step_pair = [&](int kb, bool even, v4i(&fa)[MI], v4i(&fb)[NJ], v4i(&na)[MI],
+                       v4i(&nbf)[NJ]) __attribute__((always_inline)) {
+    constexpr int NR = MI + NJ;
+    constexpr int GAP = (NM - 2 * PPW) / NR > 0 ? (NM - 2 * PPW) / NR : 1;
+    const int8_t* nxt = smem + ((kb + 1) % STG) * kStageBytes;
+    int8_t* d4 = smem + ((kb + 4) % STG) * kStageBytes;
+    int8_t* d5 = smem + ((kb + 5) % STG) * kStageBytes;
+    const int k4 = kb + 4 < nkb ? kb + 4 : nkb - 1;
+    const int k5 = kb + 5 < nkb ? kb + 5 : nkb - 1;
+    if (even) {
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(PPW));
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int h = 0; h < NM; ++h) {
+      const int i = h / NJ, j = h % NJ;
+      acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (h % GAP == GAP - 1 && h / GAP < NR) {
+        rd_frag(nxt, h / GAP, na, nbf);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (even) {
+#pragma unroll PPW
+        for (int t = 0; t < PPW; ++t) {
+          if (h == NM - 2 * PPW + t) {
+            dma(k4, t, d4);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          if (h == NM - PPW + t) {
+            dma(k5, t, d5);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+    }
+  };
+
   auto buf = [&](int i) { return smem + i * kStageBytes; };
   int r = 0;  // stage kb lives in buf(r)
+  if constexpr (IL == 3) {
+    static_assert(STG == 5, "the paired schedule needs five stage buffers");
+    for (int kb = 0; kb < nkb; kb += 2) {
+      step_pair(kb, true, fa0, fb0, fa1, fb1);
+      if (kb + 1 < nkb) step_pair(kb + 1, false, fa1, fb1, fa0, fb0);
+    }
+  } else
   for (int kb = 0; kb < nkb; kb += 2) {
     if constexpr (IL)
       step_il(kb, buf(r), buf(r == STG - 1 ? 0 : r + 1), fa0, fb0, fa1, fb1);
@@ -934,13 +990,14 @@ int crt_kernel() {  // MOOSEX_CRT_KERNEL: 1 = 4 waves of 128x128, 2 = 8 waves of
   // step's MFMAs (the default: 4-6 % faster than 6 on the same box, profiles/r3_crt_gemm.md),
   // 9 = 8 with 4 stages, 10 / 11 = 8 / 9 with the DMAs spread over the step too, 12 = 4
   // with 8's schedule, 13 = 12 with 4 stages, 14 / 15 = 12 / 13 with the DMAs spread (4 and
-  // 12-15 need the VGPR-form MFMA flag of _native/build.py, else they spill).  Tried and removed (profiles/r3_crt_gemm.md): DMAs through
+  // 12-15 need the VGPR-form MFMA flag of _native/build.py, else they spill), 16 = 8 with
+  // one barrier per two k-steps over five stage buffers (160 KB LDS).  Tried and removed (profiles/r3_crt_gemm.md): DMAs through
   // buffer descriptors (16.2 vs 15.5 ms per step), a persistent one-block-per-CU kernel
   // streaming all its tiles' k-steps (16.2 vs 15.5 ms), B fragments loaded from global
   // memory straight into registers (hipcc drains every counter before their first use)
   const char* e = std::getenv("MOOSEX_CRT_KERNEL");
   const int v = e ? std::atoi(e) : 8;
-  return v >= 1 && v <= 15 ? v : 8;
+  return v >= 1 && v <= 16 ? v : 8;
 }
 bool crt_mfma16() { return crt_kernel() >= 4; }
 int recon_dot4() {  // MOOSEX_CRT_RECON=0: the multiply-add reconstruction
@@ -1041,6 +1098,7 @@ void launch_crt_gemm(const CPlan& p, const Tables& tb, int64_t batch, const int8
     case 13: launch_variant<2, 2, 256, 1, true, 4, 1>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
     case 14: launch_variant<2, 2, 256, 1, true, 3, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
     case 15: launch_variant<2, 2, 256, 1, true, 4, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
+    case 16: launch_variant<2, 4, 256, 2, true, 5, 3>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
     default: launch_variant<2, 2, 128, 2, true>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
   }
 }

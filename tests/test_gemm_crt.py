@@ -318,7 +318,7 @@ def test_gpu_dot_cross_pair_rolled(bits, K):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", ["6", "8", "12", "14"])
+@pytest.mark.parametrize("variant", ["6", "8", "12", "14", "16"])
 def test_gpu_crt_bench_tiling_matches_limb_gemm(variant, monkeypatch):
     """The bench's tile grid: many 256x256 tiles in both directions (GROUPM remap over 8 x 8
     tiles per party and modulus), K' = 8192 (mode 1), Z_2^128 -- bit-exact against the limb
