@@ -202,3 +202,28 @@ def test_reference_fixed_constant_form(monkeypatch):
         data = RS.to_rust_bincode(c)
         assert data.endswith(struct.pack("<d", 1.5) + _u64(40) + _u64(0) + _u32(0) + _s("a"))
         assert RS.from_rust_bincode(data).to_textual() == c.to_textual()
+
+
+@pytest.mark.parametrize("fmt", sorted(ENC))
+def test_every_type_and_placement_round_trips(fmt):
+    """All 66 Ty variants (with the TensorShape / TensorDType inners) in signatures, on all
+    four placement kinds."""
+    from moose_amd.ir.computation import Operation
+    from moose_amd.ir.computation import Signature
+    from moose_amd.ir.computation import placement_from
+    from moose_amd.ir.types import SHAPE_KINDS
+    from moose_amd.ir.types import TensorDType
+    from moose_amd.ir.types import Ty
+
+    tys = [Ty(n) for n in RS.TY_VARIANTS if n not in ("Shape", "Tensor")]
+    tys += [Ty("Shape", k) for k in SHAPE_KINDS]
+    tys += [Ty("Tensor", TensorDType(k, 3, 5) if k.startswith("Fixed") else TensorDType(k))
+            for k in RS.DTYPE_VARIANTS]
+    plcs = [placement_from("Host", ["a"]), placement_from("Replicated", ["a", "b", "c"]),
+            placement_from("Additive", ["a", "b"]), placement_from("Mirrored3", ["a", "b", "c"])]
+    ops = [Operation(f"op{i}", "Identity", [], plcs[i % 4], Signature((t,), t), {})
+           for i, t in enumerate(tys)]
+    comp = Computation(ops)
+    enc, dec = ENC[fmt]
+    back = dec(enc(comp))
+    assert [(o.sig, o.placement) for o in back.operations] == [(o.sig, o.placement) for o in ops]
