@@ -43,14 +43,20 @@ before the timed region (the reference's client-side compile).  Every step creat
 session (fresh PRF keys).  After the timed steps the last step's outputs are checked
 against float64 torch on every rank (``--no-check`` skips it).
 
-Failing loudly (``moose_amd/utils/benchwatch.py``): every phase (init, preflight, warmup,
-timed, check, lr) runs under a watchdog budget; a stall ends the run with a JSON line naming
-the stalled ranks.  Before the warmup every rank does one grouped round trip with each of
-its peers on every communicator it will use and verifies who answered.
+Failing loudly (``moose_amd/utils/benchwatch.py``): the whole run has one wall-clock
+deadline (``--deadline``, default 540 s, under the driver's 600 s).  Every phase (init +
+rendezvous, preflight, warmup, timed, then the optional extras) runs under a watchdog budget
+clipped to it; an extra is skipped (and listed) when too little time is left; ``phase_s``
+in the line records what each phase took.  Before the warmup every rank does one grouped
+round trip with each of its peers on every communicator it will use and verifies who
+answered.
 
-Launch: ``python bench.py --gpus N`` spawns N ranks itself (torch.distributed.run on
-127.0.0.1, before anything touches the GPU) under a wall-clock supervisor; under an
-external launcher (WORLD_SIZE set) it runs as one rank.
+Launch: ``python bench.py --gpus N`` starts torch.distributed.run on 127.0.0.1 itself.
+Under a launcher (WORLD_SIZE set) each rank process is a supervisor that never touches the
+GPU: it runs the rank's worker as a child process, and the supervisors walk a fallback
+ladder together -- an attempt that fails or stalls before its headline is killed on every
+rank and a fresh one starts (cyclic with 2 step streams -> 1 step stream -> stacked over
+gloo); ``attempts`` in the line says which configuration produced the number.
 """
 from __future__ import annotations
 
@@ -62,6 +68,8 @@ import subprocess
 import sys
 import tempfile
 import time
+
+_T_START = time.monotonic()  # "init" in phase_s counts the imports too
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
@@ -125,8 +133,13 @@ def _parse():
     ap.add_argument("--no-check", dest="check", action="store_false")
     ap.add_argument("--lr-runs", type=int, default=30,
                     help="LR-inference evaluations per mode (0 = skip)")
-    ap.add_argument("--watchdog", type=float, default=float(os.environ.get(
-        "MOOSEX_BENCH_WATCHDOG", "600")), help="seconds any one phase may take")
+    ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
+                    help="process-group backend (auto: RCCL on GPUs, gloo on the CPU and "
+                         "with MOOSEX_SHARED_GPU=1)")
+    ap.add_argument("--deadline", type=float, default=float(os.environ.get(
+        "MOOSEX_BENCH_DEADLINE", "540")),
+        help="wall-clock seconds for the whole run (every phase budget is carved out of "
+             "it; the driver's own limit is 600 s)")
     return ap.parse_args()
 
 
@@ -147,19 +160,26 @@ def _base_line(args, world):
                        "seq_len": args.size}}
 
 
-def _self_launch(args):
-    """N > 1 without a launcher: run N fresh ranks as child processes under a wall-clock
-    supervisor.  This process never touches the GPU (only argparse ran), and exits with
-    the launcher's status (or 3 with an error line if the rank group hangs)."""
+def _benchwatch():
+    """The watchdog/supervisor module, loaded by path: importing the moose_amd package would
+    pull in torch and the native libraries, and the supervising processes must stay away
+    from the GPU."""
     import importlib.util
 
-    # load the watchdog module by path: importing the moose_amd package would pull in torch
-    # and the native libraries, and this process must stay away from the GPU
     spec = importlib.util.spec_from_file_location(
         "moosex_benchwatch", os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                           "moose_amd", "utils", "benchwatch.py"))
-    benchwatch = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(benchwatch)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _self_launch(args):
+    """N > 1 without a launcher: start the launcher (N rank supervisors, each of which runs
+    its rank's worker as a child) under a wall-clock limit of the deadline plus a grace.
+    This process never touches the GPU (only argparse ran), and exits with the launcher's
+    status (or 3 with an error line if the rank group hangs)."""
+    benchwatch = _benchwatch()
     rdir = os.environ.get("MOOSEX_BENCH_RUN_DIR") or tempfile.mkdtemp(prefix="moosex_bench_")
     os.makedirs(rdir, exist_ok=True)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
@@ -168,10 +188,57 @@ def _self_launch(args):
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env["MOOSEX_BENCH_RUN_DIR"] = rdir
-    # the ranks' own watchdogs fire per phase; this limit only catches a launcher or a
-    # rank that cannot even run its watchdog (7 phases + start-up)
-    limit = 8 * args.watchdog + 120
-    return benchwatch.supervise(cmd, env, args.gpus, limit, _base_line(args, args.gpus), rdir)
+    return benchwatch.supervise(cmd, env, args.gpus, args.deadline + 45,
+                                _base_line(args, args.gpus), rdir)
+
+
+def _resolve(args, world):
+    """(layout, step streams, backend) the run will use."""
+    layout = args.layout
+    if layout == "auto":
+        layout = "stacked" if world < 3 else "cyclic"
+    nstreams = args.step_streams
+    if nstreams is None:
+        # cyclic at N > 1: two steps in flight.  A step's dependency chain is its compute
+        # plus four message rounds (share, tail A, tail B, reveal: ~4-5 ms each for a
+        # 268 MB share tensor on one xGMI link), about twice its compute.  A third stream
+        # would cover a slower link, but three steps computing at once cost 4.5 % on the
+        # GPU (one GPU, no messages: 16.33 ms with 2 streams, 17.08 ms with 3)
+        nstreams = int(os.environ.get("MOOSEX_BENCH_STREAMS",
+                                      "2" if layout == "cyclic" and world > 1 else "1"))
+    backend = args.backend
+    if backend == "auto":
+        gpu = os.environ.get("MOOSEX_SHARED_GPU") != "1" and _has_gpus()
+        backend = "nccl" if gpu else "gloo"
+    return layout, max(1, nstreams), backend
+
+
+def _has_gpus():
+    """Whether a GPU is present, asked without torch (a supervisor never imports it): the
+    ROCm kernel driver's device node.  Only labels the supervisor's rungs; the worker
+    decides with ``torch.cuda.is_available()``."""
+    return os.path.exists("/dev/kfd") and os.environ.get("HIP_VISIBLE_DEVICES", "x") != ""
+
+
+def _ladder(args, world):
+    """The fallback rungs under a launcher: the requested configuration, then (cyclic with
+    several step streams) one step stream, then the stacked layout over gloo with no
+    inter-GPU traffic at all.  ``reserve_s``: what a rung needs at least (at the default
+    deadline); earlier rungs must measure their headline before the later ones' reserve."""
+    layout, nstreams, backend = _resolve(args, world)
+    base = list(sys.argv[1:])
+    rungs = [{"argv": base, "reserve_s": 120,
+              "label": {"layout": layout, "streams": nstreams, "backend": backend}}]
+    if layout == "cyclic" and nstreams > 1:
+        rungs.append({"argv": base + ["--step-streams", "1"], "reserve_s": 150,
+                      "label": {"layout": layout, "streams": 1, "backend": backend}})
+    if not (layout == "stacked" and backend == "gloo"):
+        rungs.append({"argv": base + ["--layout", "stacked", "--gather", "none",
+                                      "--backend", "gloo", "--step-streams", "1",
+                                      "--no-spmd-configs", "--link-probe-mib", "0"],
+                      "reserve_s": 75,
+                      "label": {"layout": "stacked", "streams": 1, "backend": "gloo"}})
+    return rungs
 
 
 def _inputs(n, session, which, device):
@@ -551,8 +618,16 @@ def _config5(args, world, rank, device, prog, g6, gout):
 # ---------------------------------------------------------------------------------------
 def main():
     args = _parse()
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    world = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    if args.gpus > 1 and not world:
         sys.exit(_self_launch(args))
+    if world > 1 and os.environ.get("MOOSEX_BENCH_CHILD") != "1":
+        # under a launcher: this rank process supervises its worker (a child process) and
+        # walks the fallback ladder with the other ranks; it never touches the GPU
+        bw = _benchwatch()
+        sys.exit(bw.rank_supervisor(os.path.abspath(__file__), int(os.environ["RANK"]), world,
+                                    _ladder(args, world), args.deadline,
+                                    _base_line(args, world)))
     prog = []
     try:
         _main(args, prog)
@@ -562,8 +637,8 @@ def main():
         if prog:
             prog[0].fail(f"{type(e).__name__}: {e}")
             if prog[0].result is not None:
-                # the headline was measured and rank 0 printed it with this error noted: an
-                # optional extra (LR inference, configs 2/3) failed -- keep the measurement
+                # the headline was measured and rank 0 reported it with this error noted:
+                # an optional extra (LR inference, configs 2/3) failed -- keep it
                 os._exit(0)
         raise
 
@@ -575,6 +650,7 @@ def _main(args, prog_out):
     import torch
     import torch.distributed as dist
 
+    from moose_amd.utils.benchwatch import Clock
     from moose_amd.utils.benchwatch import Progress
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -589,8 +665,11 @@ def _main(args, prog_out):
         # runtime when it initialises, i.e. below.
         q = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(16, max(q, 8)))
-    prog = Progress(rank, world, args.watchdog, lambda: _base_line(args, world))
+    clock = Clock.from_env(args.deadline)
+    prog = Progress(rank, world, clock, lambda: _base_line(args, world),
+                    result_path=os.environ.get("MOOSEX_BENCH_RESULT"), t0=_T_START)
     prog_out.append(prog)
+    layout, nstreams, backend = _resolve(args, world)
     # MOOSEX_SHARED_GPU=1: every rank on cuda:0 with gloo (rehearsing the multi-GPU
     # layouts on a one-GPU box; RCCL refuses two ranks on one device)
     shared = os.environ.get("MOOSEX_SHARED_GPU") == "1"
@@ -600,33 +679,37 @@ def _main(args, prog_out):
         device = torch.device("cuda", idx)
     else:
         device = torch.device("cpu")
+    if device.type != "cuda" or shared:
+        backend = "gloo"
+    elif args.backend == "auto":
+        backend = "nccl"
     if world > 1:
-        backend = "nccl" if device.type == "cuda" and not shared else "gloo"
         dist.init_process_group(backend=backend,
                                 device_id=device if backend == "nccl" else None,
-                                # longer than a phase budget: the watchdog reports first
-                                timeout=datetime.timedelta(seconds=args.watchdog + 120))
-        prog.phase("rendezvous", args.watchdog)
+                                # past the deadline: the watchdog reports first
+                                timeout=datetime.timedelta(
+                                    seconds=max(60.0, prog.remaining() + 60)))
+        prog.phase("rendezvous")
         dist.barrier()
 
     from moose_amd.runtime.interpreter import Interpreter
     from moose_amd.runtime.session import StackedSession
 
-    layout = args.layout
-    if layout == "auto":
-        layout = "stacked" if world < 3 else "cyclic"
     if layout == "spmd" and (world < 3 or world % 3):
         raise SystemExit("--layout spmd needs a multiple of 3 GPUs (one per party)")
-    nstreams = args.step_streams
-    if nstreams is None:
-        # cyclic at N > 1: two steps in flight.  A step's dependency chain is its compute
-        # plus four message rounds (share, tail A, tail B, reveal: ~4-5 ms each for a
-        # 268 MB share tensor on one xGMI link), about twice its compute.  A third stream
-        # would cover a slower link, but three steps computing at once cost 4.5 % on the
-        # GPU (one GPU, no messages: 16.33 ms with 2 streams, 17.08 ms with 3)
-        nstreams = int(os.environ.get("MOOSEX_BENCH_STREAMS",
-                                      "2" if layout == "cyclic" and world > 1 else "1"))
-    nstreams = max(1, nstreams)
+    nccl = world > 1 and backend == "nccl"
+    tdev = device if nccl else torch.device("cpu")
+
+    def fits(name):
+        """Every rank agrees whether the optional phase ``name`` still fits the deadline."""
+        ok = prog.extra_fits(name)
+        if world > 1:
+            t = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=tdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            ok = t.item() > 0
+        if not ok:
+            prog.skip(name)
+        return ok
 
     comp = build_computation(args.ring)
     n = args.size
@@ -767,11 +850,11 @@ def _main(args, prog_out):
         if world > 1:
             dist.barrier()
 
-    prog.phase("preflight", min(args.watchdog, 180))
+    prog.phase("preflight")
     preflight = _preflight(layout, comms, world, rank, device, prog,
                            offsets if layout == "cyclic" else None)
 
-    prog.phase("warmup", args.watchdog)
+    prog.phase("warmup")
     for i in range(args.warmup):
         prog.tick(i)
         step()
@@ -784,7 +867,7 @@ def _main(args, prog_out):
     # inside the timed loop; read after the final synchronize)
     evs = ([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             for _ in range(args.steps)] if device.type == "cuda" and streams is None else None)
-    prog.phase("timed", args.watchdog)
+    prog.phase("timed")
     t0 = time.perf_counter()
     for i in range(args.steps):
         prog.tick(i)
@@ -797,44 +880,12 @@ def _main(args, prog_out):
     sync()
     elapsed = time.perf_counter() - t0
     step_ms = sorted(a.elapsed_time(b) for a, b in evs) if evs is not None else []
-    z_last = z
 
-    zero_slot = None
-    if world == 1 and layout == "stacked" and args.zero_slot_steps > 0:
-        # secondary figure, NOT the headline: the same steps with the zero-slot-aware RSS
-        # product (protocols/replicated.py _zero_slot_cross, opt-in MOOSEX_ZERO_SLOTS=1):
-        # both operands are fresh input sharings with a public zero slot, so each party's
-        # cross product is one K-long GEMM instead of the K-doubled one
-        from moose_amd.protocols import replicated as rep_mod
-
-        prog.phase("zero_slot", args.watchdog)
-        prev, rep_mod.ZERO_SLOTS = rep_mod.ZERO_SLOTS, True
-        try:
-            for _ in range(2):
-                step()
-            sync()
-            tz = time.perf_counter()
-            for _ in range(args.zero_slot_steps):
-                zz = step()
-            sync()
-            zms = (time.perf_counter() - tz) / args.zero_slot_steps * 1e3
-            zero_slot = {"ms_per_step": zms, "value": n * n / zms * 1e3,
-                         "steps": args.zero_slot_steps,
-                         # TruncPr rounds probabilistically: ~1 ulp (2^-23) apart
-                         "max_abs_diff_vs_headline_output":
-                             (zz - z_last).abs().max().item() if zz is not None else None,
-                         "note": "opt-in MOOSEX_ZERO_SLOTS=1, not the headline: skips the "
-                                 "cross terms that multiply a fresh input sharing's public "
-                                 "zero slot (half the GEMM)"}
-        finally:
-            rep_mod.ZERO_SLOTS = prev
-
-    prog.phase("report", min(args.watchdog, 180))
+    prog.phase("report")
     p2p = [sum(c.bytes_sent for c in comms) - sum(b for b, _ in comm0),
            sum(c.messages for c in comms) - sum(m for _, m in comm0)]
     per_rank = [[elapsed] + p2p]
     if world > 1:
-        tdev = device if dist.get_backend() == "nccl" else "cpu"
         t = torch.tensor([elapsed] + p2p, dtype=torch.float64, device=tdev)
         allt = torch.empty(3 * world, dtype=torch.float64, device=tdev)
         dist.all_gather_into_tensor(allt, t)
@@ -867,13 +918,12 @@ def _main(args, prog_out):
         "p2p_bytes_per_step": [r[1] / args.steps for r in per_rank],
         "p2p_messages_per_step": [r[2] / args.steps for r in per_rank],
         "preflight": preflight,
+        "deadline_s": args.deadline,
     })
     line["config"].update(global_batch=n_sessions, parallelism=parallelism)
     if step_ms:
         line["step_ms_rank0"] = {"min": step_ms[0], "median": step_ms[len(step_ms) // 2],
                                  "max": step_ms[-1]}
-    if zero_slot is not None:
-        line["zero_slot_aware"] = zero_slot
     line["device"] = _device_info(device)
     if device.type == "cuda":
         # rank 0's device memory: the torch allocator's high-water mark, and what the device
@@ -888,8 +938,8 @@ def _main(args, prog_out):
     prog.headline_done(line)
 
     exit_code = 0
-    if args.check:
-        prog.phase("check", min(args.watchdog, 150))
+    if args.check and fits("check"):
+        prog.phase("check")
         check = None
         if out_owner:
             ref = _inputs(n, out_session, "x", device) @ _inputs(n, out_session, "y", device)
@@ -918,11 +968,11 @@ def _main(args, prog_out):
             line["error"] = f"wrong results: max abs error {worst} vs float64 torch"
             exit_code = 4
 
-    # the optional extras after the headline get short budgets: a hang in one of them
-    # fires the watchdog (which prints the measured line) well inside a driver's
-    # per-run limit, instead of the run being killed with no line at all
-    if layout == "cyclic" and world > 1 and args.link_probe_mib > 0:
-        prog.phase("link_probe", min(args.watchdog, 60))
+    # the optional extras after the headline: each runs only when its expected need is
+    # left before the deadline (all ranks agree), under a budget clipped to the deadline;
+    # a hang in one fires the watchdog, which reports the measured line with the error
+    if layout == "cyclic" and world > 1 and args.link_probe_mib > 0 and fits("link_probe"):
+        prog.phase("link_probe")
         off = list(offsets.values())
         dists = sorted({(b - a) % world for a in off for b in off} - {0})
         mib = args.link_probe_mib if dist.get_backend() == "nccl" else 1  # gloo: path only
@@ -930,16 +980,16 @@ def _main(args, prog_out):
         if rank == 0:
             line["link_probe"] = probe
 
-    if args.lr_runs > 0:
-        prog.phase("lr", min(args.watchdog, 120))
+    if args.lr_runs > 0 and fits("lr"):
+        prog.phase("lr")
         lr = {"model": "ml-inference-with-onnx tutorial LogisticRegression (200x10, "
                        "fixed(24,40), Z_2^128, from_onnx)"}
         if rank == 0:
             lr["one_gpu"] = _lr_stacked(args.lr_runs, device)
         if world > 1:
             dist.barrier()
-        if world >= 3:
-            prog.phase("lr_spmd", min(args.watchdog, 120))
+        if world >= 3 and args.spmd_configs and fits("lr_spmd"):
+            prog.phase("lr_spmd")
             rec = _lr_spmd(args.lr_runs, world, rank, device, prog)
             recs = [None] * world
             dist.all_gather_object(recs, rec)
@@ -957,8 +1007,8 @@ def _main(args, prog_out):
                 line["lr_inference_p50_ms"]["spmd"] = lr["spmd_one_party_per_gpu"]["p50_ms"]
             line["lr_inference"] = lr
 
-    if world >= 3 and args.spmd_configs:
-        prog.phase("spmd_configs", min(args.watchdog, 180))
+    if world >= 3 and args.spmd_configs and fits("spmd_configs"):
+        prog.phase("spmd_configs")
         rec = _spmd_configs(args, world, rank, device, prog)
         recs = [None] * world
         dist.all_gather_object(recs, rec)
@@ -971,10 +1021,38 @@ def _main(args, prog_out):
                 line["config5_dp2_replicas"] = merged.pop("config5_dp2_replicas")
             line["spmd_three_gpus"] = merged
 
-    prog.phase("done", 120)
-    if rank == 0:
-        print(json.dumps(line), flush=True)
+    if (world == 1 and layout == "stacked" and args.zero_slot_steps > 0
+            and fits("zero_slot")):
+        # secondary figure, NOT the headline: the same steps with the zero-slot-aware RSS
+        # product (protocols/replicated.py _zero_slot_cross, opt-in MOOSEX_ZERO_SLOTS=1):
+        # both operands are fresh input sharings with a public zero slot, so each party's
+        # cross product is one K-long GEMM instead of the K-doubled one
+        from moose_amd.protocols import replicated as rep_mod
+
+        prog.phase("zero_slot")
+        prev, rep_mod.ZERO_SLOTS = rep_mod.ZERO_SLOTS, True
+        try:
+            for _ in range(2):
+                step()
+            sync()
+            tz = time.perf_counter()
+            for _ in range(args.zero_slot_steps):
+                zz = step()
+            sync()
+            zms = (time.perf_counter() - tz) / args.zero_slot_steps * 1e3
+            line["zero_slot_aware"] = {
+                "ms_per_step": zms, "value": n * n / zms * 1e3, "steps": args.zero_slot_steps,
+                # TruncPr rounds probabilistically: ~1 ulp (2^-23) apart
+                "max_abs_diff_vs_headline_output": (zz - z).abs().max().item(),
+                "note": "opt-in MOOSEX_ZERO_SLOTS=1, not the headline: skips the cross terms "
+                        "that multiply a fresh input sharing's public zero slot (half the "
+                        "GEMM)"}
+        finally:
+            rep_mod.ZERO_SLOTS = prev
+
+    prog.phase("done")
     prog.disarm()
+    prog.emit(line)
     if world > 1:
         dist.destroy_process_group()
     if exit_code:

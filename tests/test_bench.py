@@ -5,6 +5,7 @@ import os
 import socket
 import subprocess
 import sys
+import time
 
 import pytest
 
@@ -95,31 +96,86 @@ def test_bench_lr_inference_in_line():
     assert sp["config3_ringdot_3gpu"]["ms_per_step"] > 0
 
 
+def _run_env(n, env_extra, *extra, timeout=300):
+    cmd = [sys.executable, "bench.py", "--gpus", str(n), "--steps", "2", "--warmup", "1",
+           "--size", "32", "--lr-runs", "0", *extra]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra)
+    t0 = time.monotonic()
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout,
+                         env=env)
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, (out.stdout[-2000:], out.stderr[-3000:])
+    return out.returncode, json.loads(lines[0]), time.monotonic() - t0
+
+
 @pytest.mark.parametrize("phase,rank", [("timed", 2), ("preflight", 1)])
 def test_bench_stalled_rank_fails_loudly(phase, rank):
-    """A rank that hangs makes bench.py --gpus 3 exit non-zero within its watchdog budget
-    with an error line naming the stalled rank."""
-    cmd = [sys.executable, "bench.py", "--gpus", "3", "--steps", "2", "--warmup", "1",
-           "--size", "32", "--lr-runs", "0", "--watchdog", "15"]
-    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    env["MOOSEX_BENCH_STALL"] = f"{rank}:{phase}"
-    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
-    assert out.returncode != 0
-    d = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    """A rank that hangs in every attempt of the fallback ladder: bench.py --gpus 3 exits
+    non-zero inside its deadline with an error line naming the stalled rank and listing
+    every attempt."""
+    rc, d, secs = _run_env(3, {"MOOSEX_BENCH_STALL": f"{rank}:{phase}:*"}, "--deadline", "90")
+    assert rc != 0 and secs < 90 + 45
     assert d["value"] is None and "error" in d
     assert d["stalled_ranks"] == [rank]
-    assert d["phases"][str(rank)]["phase"] == phase
+    assert [a["outcome"] for a in d["attempts"]] == ["failed"] * 3
+    assert all(a["phase"] == phase for a in d["attempts"])
+    assert [(a["layout"], a["streams"]) for a in d["attempts"]] == [
+        ("cyclic", 2), ("cyclic", 1), ("stacked", 1)]
 
 
-def test_supervisor_kills_a_hung_rank_group(tmp_path):
-    """The self-launch parent's wall-clock limit: a child group that never finishes is
-    killed and an error line is printed from the phase files."""
+def test_bench_fallback_ladder_recovers_a_stalled_attempt():
+    """A rank that hangs in the warmup of the first attempt (cyclic, two step streams): the
+    supervisors kill that attempt on every rank and the next rung (one step stream)
+    measures the headline, well inside the deadline; the line carries both attempts."""
+    rc, d, secs = _run_env(3, {"MOOSEX_BENCH_STALL": "1:warmup"}, "--step-streams", "2",
+                           "--deadline", "150")
+    assert rc == 0 and secs < 150
+    assert d["value"] > 0 and d["check"]["ok"] and d["fallback"] is True
+    a0, a1 = d["attempts"]
+    assert (a0["layout"], a0["streams"], a0["outcome"], a0["phase"]) == (
+        "cyclic", 2, "failed", "warmup")
+    assert a0["stalled_ranks"] == [1]
+    assert (a1["layout"], a1["streams"], a1["outcome"]) == ("cyclic", 1, "ok")
+    assert d["step_streams"] == 1
+    # per-phase wall times of the attempt that measured
+    assert {"init", "rendezvous", "preflight", "warmup", "timed"} <= set(d["phase_s"])
+
+
+def _benchwatch():
     import importlib.util
 
     spec = importlib.util.spec_from_file_location(
         "bw", os.path.join(ROOT, "moose_amd", "utils", "benchwatch.py"))
     bw = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bw)
+    return bw
+
+
+def test_phase_budgets_are_clipped_to_the_deadline(tmp_path):
+    """Budgets come out of one deadline: a phase's watchdog budget is its cap clipped to
+    the time left (before the headline: to the attempt's headline deadline), and an extra
+    whose expected need no longer fits is reported as not fitting (then skipped)."""
+    bw = _benchwatch()
+    now = time.time()
+    clock = bw.Clock(now + 40, now + 20, 1.0)
+    p = bw.Progress(0, 1, clock, lambda: {}, directory=str(tmp_path))
+    p.phase("warmup")  # cap 120 s, clipped to the headline deadline (20 s - margin)
+    assert p.deadline - time.monotonic() < 20
+    p.headline_done({"value": 1.0})
+    p.phase("check")  # after the headline: clipped to the run's deadline instead
+    assert 20 < p.deadline - time.monotonic() < 40
+    assert p.extra_fits("check") and not p.extra_fits("spmd_configs")  # need 10 s vs 45 s
+    p.skip("spmd_configs")
+    line = p.final_line()
+    assert line["skipped"] == ["spmd_configs"] and {"init", "warmup"} <= set(line["phase_s"])
+    p.disarm()
+
+
+def test_supervisor_kills_a_hung_rank_group(tmp_path):
+    """The self-launch parent's wall-clock limit: a child group that never finishes is
+    killed and an error line is printed from the phase files."""
+    bw = _benchwatch()
     (tmp_path / "rank0.json").write_text(json.dumps({"phase": "timed", "seq": 4, "step": 3}))
     (tmp_path / "rank1.json").write_text(json.dumps({"phase": "timed", "seq": 4, "step": 0}))
     import contextlib
@@ -135,27 +191,27 @@ def test_supervisor_kills_a_hung_rank_group(tmp_path):
 
 @pytest.mark.parametrize("phase,rank,headline", [("lr_spmd", 1, True), ("warmup", 2, False)])
 def test_bench_rank_exception_ends_the_run_promptly(phase, rank, headline):
-    """A rank that raises ends the whole group at once (its peers' watchdogs read its
-    failure record instead of waiting out their phase budget).  After the headline was
-    measured (an optional extra failed) the line keeps the measurement, notes the error
-    and the run exits 0; before it, the run fails with an error line."""
-    import time
-
+    """A rank that raises ends its attempt on every rank at once (its peers' watchdogs read
+    its failure record instead of waiting out their phase budget).  After the headline was
+    measured (an optional extra failed) the line keeps the measurement and notes the error;
+    before it, the next rung of the ladder measures instead."""
     cmd = [sys.executable, "bench.py", "--gpus", "3", "--steps", "1", "--warmup", "1",
-           "--size", "32", "--lr-runs", "2", "--watchdog", "200"]
+           "--size", "32", "--lr-runs", "2", "--deadline", "200"]
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env["MOOSEX_BENCH_FAIL"] = f"{rank}:{phase}"
     t0 = time.monotonic()
     out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=400, env=env)
-    assert time.monotonic() - t0 < 150  # far inside the 200 s phase budget
+    assert time.monotonic() - t0 < 120  # far inside the 200 s phase budget
     d = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert d["value"] > 0 and d["check"]["ok"]
     if headline:
-        assert out.returncode == 0, out.stderr[-2000:]
-        assert d["value"] > 0 and d["check"]["ok"]
         assert d["errors"][0]["phase"] == phase
+        assert len(d["attempts"]) == 1
     else:
-        assert out.returncode != 0
-        assert d["value"] is None and f"rank {rank}" in d["error"]
+        a0 = d["attempts"][0]
+        assert a0["outcome"] == "failed" and f"rank {rank}" in a0["error"]
+        assert d["attempts"][1]["outcome"] == "ok"
 
 
 def test_bench_config5_two_replicas_on_six_ranks():
@@ -188,7 +244,7 @@ def test_bench_rccl_multi_gpu(n):
     if _gpus() < n:
         pytest.skip(f"needs {n} GPUs")
     cmd = [sys.executable, "bench.py", "--gpus", str(n), "--steps", "2", "--warmup", "1",
-           "--size", "1024", "--lr-runs", "3", "--watchdog", "240"]
+           "--size", "1024", "--lr-runs", "3", "--deadline", "400"]
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MOOSEX_SHARED_GPU")}
     out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=900, env=env)
