@@ -16,6 +16,7 @@ everything else is preceded by a fixed-size int64 header describing the payload
 """
 from __future__ import annotations
 
+import collections
 import math
 import os
 import struct
@@ -50,8 +51,12 @@ class TransportError(errors.Networking):
 # send payloads only and take the headers from the plan, so no message makes the receiver
 # read a header back to the host (the reference ships HostShape metadata with every Share,
 # replicated/convert.rs:49-160).  A sender whose header differs from the plan raises
-# instead of desynchronising its peer.
-_PLANS = {}
+# instead of desynchronising its peer.  Least-recently-used first out, so a long-lived
+# worker that sees many argument shapes keeps a bounded table.
+_PLANS: "collections.OrderedDict" = collections.OrderedDict()
+PLAN_CACHE = int(os.environ.get("MOOSEX_PLAN_CACHE", "256"))
+# send-only rounds in flight per transport before the oldest is waited for
+MAX_UNWAITED = 64
 
 
 class _Plan:
@@ -84,7 +89,8 @@ class Transport:
         self.bytes_sent = 0
         self.messages = 0
         # test-only fault injection: MOOSEX_FAULT="drop:<k>@<rank>" drops this rank's
-        # k-th outgoing message, "delay:<seconds>@<rank>" delays every send
+        # k-th outgoing message, "delay:<seconds>@<rank>" delays every send,
+        # "exit:<k>@<rank>" kills the process at its k-th grouped exchange
         self.fault = fault if fault is not None else _parse_fault(os.environ.get("MOOSEX_FAULT"),
                                                                    rank)
         self._sends = 0
@@ -98,9 +104,11 @@ class Transport:
         except (RuntimeError, ValueError):
             backend = "none"
         self.stage = backend == "gloo" and self.device.type == "cuda"
-        # RCCL: a send-only round does not hold the compute stream (exchange)
-        self.async_sends = backend == "nccl"
-        self._unwaited = []
+        # RCCL: a send-only round does not hold the compute stream (exchange); gloo only on
+        # request (MOOSEX_ASYNC_SENDS=1: CPU tests of the completion checks)
+        self.async_sends = backend == "nccl" or (
+            backend == "gloo" and os.environ.get("MOOSEX_ASYNC_SENDS") == "1")
+        self._unwaited = []  # [(work, dst)] of send-only rounds not yet known complete
 
     # -- encoding -----------------------------------------------------------------
     def _header(self, v):
@@ -208,6 +216,8 @@ class Transport:
         """Start an evaluation under plan ``key`` (identical on every process): replay the
         recorded headers if the plan exists, else record them."""
         p = _PLANS.get((self.plan_scope, self.rank, self.world, key))
+        if p is not None:
+            _PLANS.move_to_end((self.plan_scope, self.rank, self.world, key))
         self._plan_key = key
         self._cursor_in, self._cursor_out = {}, {}
         if p is not None:
@@ -218,7 +228,35 @@ class Transport:
     def end_plan(self, ok: bool = True):
         if self._mode == "record" and ok:
             _PLANS[(self.plan_scope, self.rank, self.world, self._plan_key)] = self._plan
+            while len(_PLANS) > PLAN_CACHE:
+                _PLANS.popitem(last=False)
         self._mode = self._plan = None
+
+    # -- completion of send-only rounds ------------------------------------------------
+    def _failed(self, w, dst, err):
+        self._unwaited = []
+        raise TransportError(f"rank {self.rank}: send to rank {dst} failed: {err}")
+
+    def reap(self, block: bool = False):
+        """Observe the send-only rounds still in flight: a completed one that failed raises
+        :class:`TransportError` here, on the SENDER (not only as a timeout on its peer);
+        ``block`` waits for all of them (end of an evaluation)."""
+        keep = []
+        for w, dst in self._unwaited:
+            # a completed work's wait() returns at once or raises its error (gloo reports a
+            # dead peer only through wait(); Work.exception() is not usable from Python)
+            if block or w.is_completed():
+                try:
+                    w.wait()
+                except Exception as e:  # noqa: BLE001 - any backend error
+                    self._failed(w, dst, e)
+            else:
+                keep.append((w, dst))
+        self._unwaited = keep
+
+    def end_evaluation(self):
+        """Every send of the evaluation confirmed (or its failure raised)."""
+        self.reap(block=True)
 
     def _next(self, cursors, peer):
         k = cursors.get(peer, 0)
@@ -316,6 +354,12 @@ class Transport:
             else:
                 buf = out
             ops.append(dist.P2POp(dist.irecv, buf, src, group=self.group))
+        if self._unwaited:
+            self.reap()  # a failed earlier send surfaces at the sender's next round
+        if self.fault is not None and self.fault[0] == "exit":
+            self._sends += 1
+            if self._sends == self.fault[1]:
+                os._exit(17)  # test-only: this rank dies before its k-th round (a lost peer)
         if ops:
             works = dist.batch_isend_irecv(ops)
             if recvs or not self.async_sends:
@@ -325,10 +369,16 @@ class Transport:
                 # a send-only round (a share's owner, the dealer, the revealing party): the
                 # compute stream goes on while the bytes travel -- nothing here reads what
                 # a send delivers, and the process group keeps the payload alive until the
-                # transfer is done (its RCCL stream runs the round's messages in order)
-                self._unwaited.extend(works)
-                if len(self._unwaited) > 64:  # bound the bookkeeping
-                    self._unwaited = self._unwaited[-32:]
+                # transfer is done (its RCCL stream runs the round's messages in order).
+                # Completion is observed at the next rounds and at the evaluation's end.
+                dst = sends[0][1] if sends else -1
+                self._unwaited.extend((w, dst) for w in works)
+                while len(self._unwaited) > MAX_UNWAITED:  # bound: wait for the oldest
+                    w, d = self._unwaited.pop(0)
+                    try:
+                        w.wait()
+                    except Exception as e:  # noqa: BLE001
+                        self._failed(w, d, e)
         for out, buf in staged:
             out.copy_(buf)
 
@@ -355,6 +405,8 @@ def _parse_fault(spec, rank):
         return ("drop", int(val))
     if kind == "delay":
         return ("delay", float(val))
+    if kind == "exit":  # the process dies at its k-th grouped exchange (a lost peer)
+        return ("exit", int(val))
     raise ValueError(f"bad MOOSEX_FAULT spec {spec!r}")
 
 

@@ -81,19 +81,27 @@ class Worker:
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
         if not dist.is_initialized():
+            # per-session deadline: a party that never receives (dead peer, dropped
+            # message) fails after MOOSEX_SESSION_TIMEOUT seconds instead of hanging
+            tmo = timedelta(seconds=float(os.environ.get("MOOSEX_SESSION_TIMEOUT", "1800")))
             dist.init_process_group(backend, store=dist.PrefixStore("pg", self.store),
-                                    rank=rank, world_size=world)
+                                    rank=rank, world_size=world, timeout=tmo)
         self.identities = [_get(self.store, f"{PREFIX}/worker/{r}").decode() for r in range(world)]
         self.storage_dir = storage_dir
         self.storage: Dict[str, object] = {}
         self.seen = set()
+        self._groups = {}  # (parties, replicas) -> replica / owner process groups
 
     def serve(self, max_sessions: Optional[int] = None, poll_s: float = 0.05) -> int:
         n = 0
         while max_sessions is None or n < max_sessions:
             key = f"{PREFIX}/session/{n}"
-            while not _has(self.store, key):
-                time.sleep(poll_s)
+            while True:  # block on the store (no polling latency per session)
+                try:
+                    self.store.wait([key], timedelta(seconds=max(poll_s, 30.0)))
+                    break
+                except Exception:  # noqa: BLE001 - wait timed out: keep serving
+                    continue
             job = valuecodec.loads(_get(self.store, key))
             n += 1
             if job.get("shutdown"):
@@ -102,21 +110,26 @@ class Worker:
         return 0
 
     def _run(self, job):
+        """One session.  Besides the reference's launch fields a job may carry (the
+        :class:`~moose_amd.runtime.distributed.DistributedMooseRuntime` client):
+        ``identities`` (party order), ``replicas`` + ``replica_arguments`` (data-parallel
+        copies of the session, global rank = replica * parties + party), ``seed``,
+        ``storage_update`` (values the client wrote to this identity's storage) and
+        ``by_rank`` (results keyed by rank: replicas share identities)."""
+        import torch
         import torch.distributed as dist
 
         from moose_amd.ir.computation import Computation
         from moose_amd.runtime.distributed import run_spmd
 
         sid = job["session_id"]
-        rkey = f"{PREFIX}/result/{sid}/{self.identity}"
+        rkey = f"{PREFIX}/result/{sid}/{self.rank if job.get('by_rank') else self.identity}"
         if sid in self.seen:  # choreography/grpc.rs:114-118
             self.store.set(rkey, valuecodec.dumps({"error": f"session {sid} already exists"}))
             return
         self.seen.add(sid)
         # rank 0 decides whether an abort request arrived before the start, so every
         # worker takes the same branch
-        import torch
-
         flag = torch.tensor([1 if (self.rank == 0 and _has(self.store, f"{PREFIX}/abort/{sid}"))
                              else 0], device=self.device)
         dist.broadcast(flag, 0)
@@ -125,18 +138,51 @@ class Worker:
             return
         try:
             comp = Computation.from_msgpack(job["computation"])
-            roles = job.get("role_assignment") or {}
-            # identities in rank order, renamed to the computation's roles
-            inv = {ident: role for role, ident in roles.items()}
-            idents = [inv.get(i, i) for i in self.identities]
-            storage = {idents[self.rank]: self._load_storage()}
-            outs, stats, elapsed = run_spmd(comp, job.get("arguments", {}), idents,
-                                            rank=self.rank, device=self.device,
+            replicas = int(job.get("replicas", 1))
+            if job.get("identities"):
+                idents = list(job["identities"])
+            else:
+                roles = job.get("role_assignment") or {}
+                # identities in rank order, renamed to the computation's roles
+                inv = {ident: role for role, ident in roles.items()}
+                idents = [inv.get(i, i) for i in self.identities]
+            n = len(idents)
+            if n * replicas != self.world:
+                raise RuntimeError(f"{n} identities x {replicas} replicas != {self.world} workers")
+            replica, party = divmod(self.rank, n)
+            me = idents[party]
+            upd = (job.get("storage_update") or {}).get(me)
+            if upd:
+                self._save_storage(upd)
+            mine = self._load_storage()
+            before = dict(mine)
+            storage = {me: mine}
+            arguments = dict(job.get("arguments", {}))
+            group = owner_groups = None
+            if replicas > 1:
+                from moose_amd.parallel import replicas as REP
+
+                if (n, replicas) not in self._groups:  # every worker, same order
+                    self._groups[(n, replicas)] = REP.make_groups(n, replicas)
+                replica_groups, owner_groups = self._groups[(n, replicas)]
+                group = replica_groups[replica]
+                arguments.update((job.get("replica_arguments") or [{}] * replicas)[replica])
+            outs, stats, elapsed = run_spmd(comp, arguments, idents, rank=party,
+                                            device=self.device, seed=job.get("seed"),
                                             fixedpoint_ring=job.get("fixedpoint_ring", 128),
-                                            storage=storage)
-            self._save_storage(storage.get(idents[self.rank], {}))
-            res = {"outputs": {k: np.asarray(v) for k, v in outs.items()},
-                   "elapsed_us": elapsed, "rounds": stats.rounds}
+                                            storage=storage, group=group,
+                                            rank_offset=replica * n)
+            if replicas > 1:
+                comm_dev = self.device if self.backend == "nccl" else torch.device("cpu")
+                outs = REP.gather_outputs(outs, owner_groups[party], replicas, comm_dev)
+                if replica > 0:
+                    outs = {}
+            saved = {k: v for k, v in storage.get(me, {}).items()
+                     if before.get(k) is not v and isinstance(v, (np.ndarray, str))}
+            self._save_storage(saved)
+            res = {"outputs": {k: np.asarray(v) if not isinstance(v, (str, bytes)) else v
+                               for k, v in outs.items()},
+                   "elapsed_us": elapsed, "rounds": stats.rounds, "storage": saved}
         except Exception as e:  # report, keep serving
             res = {"error": f"{type(e).__name__}: {e}", "trace": traceback.format_exc()[-4000:]}
         self.store.set(rkey, valuecodec.dumps(res))
@@ -171,6 +217,28 @@ class ChoreographyClient:
 
     def worker_identities(self, world: int) -> List[str]:
         return [_get(self.store, f"{PREFIX}/worker/{r}").decode() for r in range(world)]
+
+    def post_job(self, job: dict) -> int:
+        """Queue a prepared job (``Worker._run`` fields) for every worker; returns its
+        index.  Duplicate session ids are rejected (choreography/grpc.rs:114-118)."""
+        if self.store.add(f"{PREFIX}/sid/{job['session_id']}", 1) > 1:
+            raise errors.SessionAlreadyExists(f"session {job['session_id']} already exists")
+        n = self.store.add(f"{PREFIX}/launch_count", 1) - 1
+        self.store.set(f"{PREFIX}/session/{n}", valuecodec.dumps(job))
+        return n
+
+    def result(self, session_id: str, who, wait_s: float = 0.0) -> Optional[dict]:
+        """One worker's result record (keyed by identity, or by rank for ``by_rank``
+        jobs), or None if it is not there within ``wait_s`` seconds."""
+        key = f"{PREFIX}/result/{session_id}/{who}"
+        if not _has(self.store, key):
+            if wait_s <= 0:
+                return None
+            try:
+                self.store.wait([key], timedelta(seconds=wait_s))
+            except Exception:  # noqa: BLE001 - not yet
+                return None
+        return valuecodec.loads(_get(self.store, key))
 
     def launch_computation(self, session_id: str, computation, arguments=None,
                            role_assignment=None, fixedpoint_ring: int = 128):

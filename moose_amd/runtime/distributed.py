@@ -16,17 +16,25 @@ message is a point-to-point RCCL transfer.  There is no host-op graph to schedul
 Two ways to run:
 
 * :func:`run_spmd` inside an existing process group (e.g. under ``torchrun``);
-* :class:`DistributedMooseRuntime` from a client process: it starts one worker per
-  identity on this node (``python -m moose_amd.runtime.worker``) and gathers results.
+* :class:`DistributedMooseRuntime` from a client process: it starts one long-running
+  worker per identity on this node (``python -m moose_amd.runtime.worker --serve``, the
+  ``comet`` analogue) ONCE, then every evaluation is a session posted to their control
+  store (:class:`~moose_amd.runtime.choreography.ChoreographyClient`) -- no process start,
+  torch import or process-group set-up per evaluation, as the reference's client talks to
+  running comet workers (``execution/grpc.rs:46-146``).  ``close()`` shuts them down.
+  ``persistent=False`` keeps the one-shot form (fresh workers per evaluation).
 """
 from __future__ import annotations
 
+import atexit
 import os
 import socket
 import subprocess
 import sys
 import tempfile
 import time
+import uuid
+import weakref
 from typing import Dict
 from typing import List
 from typing import Optional
@@ -123,7 +131,8 @@ class DistributedMooseRuntime:
                  seed: Optional[int] = None, timeout: float = 900.0,
                  master_addr: str = "127.0.0.1", session_timeout: Optional[float] = None,
                  retries: int = 0, worker_env: Optional[Dict[str, str]] = None,
-                 replicas: int = 1, shard_args=None, device_map: Optional[List[int]] = None):
+                 replicas: int = 1, shard_args=None, device_map: Optional[List[int]] = None,
+                 persistent: bool = True):
         if isinstance(identities, dict):  # GrpcMooseRuntime-style {role: endpoint}
             identities = list(identities.keys())
         self.identities = [getattr(i, "name", i) for i in identities]
@@ -152,6 +161,15 @@ class DistributedMooseRuntime:
             raise ValueError("replicas must be >= 1")
         self.last_timings = None
         self.last_stats = None
+        self.last_rounds = None
+        # long-running workers (module doc): spawned on first use, reused while their
+        # configuration is unchanged, replaced after a failed session
+        self.persistent = persistent
+        self.worker_spawns = 0
+        self._pool = None
+        self._sessions = 0
+        self._dirty = {i: dict(v) for i, v in self.storage.items() if v}
+        _LIVE.add(self)
 
     def set_default(self):
         from moose_amd.edsl.base import set_current_runtime
@@ -169,9 +187,10 @@ class DistributedMooseRuntime:
 
             comp = passes.compile(comp, compiler_passes, arg_specs=arg_specs_of(arguments),
                                   fixedpoint_ring=self.fixedpoint_ring)
+        launch = self._launch_persistent if self.persistent else self._launch
         for attempt in range(self.retries + 1):
             try:
-                return self._launch(comp, dict(arguments or {}))
+                return launch(comp, dict(arguments or {}))
             except DistributedRuntimeError:
                 if attempt == self.retries:
                     raise
@@ -180,6 +199,175 @@ class DistributedMooseRuntime:
     def run_computation(self, computation, arguments=None):
         outs = self.evaluate_computation(computation, arguments)
         return outs, dict(self.last_timings or {})
+
+    # -- persistent workers ---------------------------------------------------------------
+    def _pool_key(self):
+        return (self.backend, tuple(sorted(self.worker_env.items())), self.session_timeout,
+                self.replicas, tuple(self.device_map or ()), self.master_addr)
+
+    def _ensure_pool(self):
+        from moose_amd.runtime.choreography import ChoreographyClient
+
+        pool = self._pool
+        if pool is not None and pool["key"] == self._pool_key() and all(
+                p.poll() is None for p in pool["procs"]):
+            return pool
+        self.close()
+        n = len(self.identities) * self.replicas
+        port = free_port()
+        env = dict(os.environ)
+        for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT", "TORCHELASTIC_USE_AGENT_STORE"):
+            env.pop(k, None)
+        env.update(WORLD_SIZE=str(n), MOOSEX_STORE=f"{self.master_addr}:{port}",
+                   HSA_ENABLE_IPC_MODE_LEGACY="0")
+        if self.session_timeout is not None:
+            env["MOOSEX_SESSION_TIMEOUT"] = str(self.session_timeout)
+        env.update(self.worker_env)
+        pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        env["PYTHONPATH"] = pkg_root + os.pathsep + env.get("PYTHONPATH", "")
+        logdir = tempfile.mkdtemp(prefix="moosex_workers_")
+        procs, logs = [], []
+        for r in range(n):
+            dev = self.device_map[r] if self.device_map is not None else r
+            log = open(os.path.join(logdir, f"worker{r}.log"), "wb")
+            logs.append(log)
+            procs.append(subprocess.Popen(
+                [sys.executable, "-m", "moose_amd.runtime.worker", "--serve",
+                 "--identity", self.identities[r % len(self.identities)],
+                 "--backend", self.backend],
+                env=dict(env, RANK=str(r), LOCAL_RANK=str(dev)), stdout=log,
+                stderr=subprocess.STDOUT))
+        self.worker_spawns += 1
+        pool = {"key": self._pool_key(), "procs": procs, "logs": logs, "logdir": logdir,
+                "client": None}
+        self._pool = pool
+        deadline = time.time() + min(self.timeout, 600)
+        while True:  # rank 0 hosts the store; the client connects once it is up
+            if any(p.poll() is not None for p in procs):
+                raise DistributedRuntimeError(f"a worker exited during start-up:\n"
+                                              f"{self._worker_logs()}")
+            try:
+                pool["client"] = ChoreographyClient(f"{self.master_addr}:{port}", timeout=30)
+                break
+            except Exception:  # noqa: BLE001 - not listening yet
+                if time.time() > deadline:
+                    raise DistributedRuntimeError("workers did not start") from None
+                time.sleep(0.2)
+        client = pool["client"]
+        from moose_amd.runtime.choreography import PREFIX
+        from moose_amd.runtime.choreography import _has
+
+        for r in range(n):  # every worker registered: the process group is up
+            while not _has(client.store, f"{PREFIX}/worker/{r}"):
+                if any(p.poll() is not None for p in procs) or time.time() > deadline:
+                    raise DistributedRuntimeError(f"worker {r} did not register:\n"
+                                                  f"{self._worker_logs()}")
+                time.sleep(0.05)
+        # fresh workers hold no storage: everything the client knows goes with the next job
+        self._dirty = {i: dict(v) for i, v in self.storage.items() if v}
+        return pool
+
+    def _worker_logs(self, tail=3000):
+        pool = self._pool
+        if pool is None:
+            return ""
+        out = []
+        for r, lg in enumerate(pool["logs"]):
+            try:
+                lg.flush()
+                with open(lg.name, "rb") as f:
+                    out.append(f"--- worker {r}\n" + f.read().decode(errors="replace")[-tail:])
+            except OSError:
+                pass
+        return "\n".join(out)
+
+    def _launch_persistent(self, comp: Computation, arguments: dict):
+        R = self.replicas
+        n = len(self.identities) * R
+        replica_args = None
+        if R > 1:
+            from moose_amd.parallel.replicas import shard_arguments
+
+            shards = shard_arguments(arguments, self.shard_args, R)
+            arguments = {k: v for k, v in arguments.items() if k not in self.shard_args}
+            replica_args = [{k: v for k, v in sh.items() if k in self.shard_args}
+                            for sh in shards]
+        pool = self._ensure_pool()
+        client = pool["client"]
+        self._sessions += 1
+        sid = f"{os.getpid()}-{self._sessions}-{uuid.uuid4().hex[:8]}"
+        job = {"session_id": sid, "computation": comp.to_msgpack(),
+               "arguments": _encodable(arguments), "identities": self.identities,
+               "fixedpoint_ring": self.fixedpoint_ring, "seed": self.seed, "replicas": R,
+               "replica_arguments": [_encodable(a) for a in replica_args or []],
+               "storage_update": {k: _encodable(v) for k, v in self._dirty.items() if v},
+               "by_rank": True}
+        client.post_job(job)
+        self._dirty = {}
+        deadline = time.time() + self.timeout
+        results, pending = {}, set(range(n))
+        try:
+            while pending:
+                for r in sorted(pending):
+                    res = client.result(sid, r, wait_s=0.5)  # blocks on the store
+                    if res is None:
+                        break
+                    results[r] = res
+                    pending.discard(r)
+                if not pending:
+                    break
+                dead = [r for r, p in enumerate(pool["procs"]) if p.poll() is not None]
+                if dead:
+                    raise DistributedRuntimeError(
+                        f"worker(s) {dead} exited during session {sid}:\n{self._worker_logs()}")
+                if time.time() > deadline:
+                    raise DistributedRuntimeError(f"session {sid} timed out after "
+                                                  f"{self.timeout:.0f} s (workers {sorted(pending)})")
+            failed = {r: res for r, res in results.items() if "error" in res}
+            if failed:
+                msg = "\n".join(f"--- {self.identities[r % len(self.identities)]} rank {r}: "
+                                f"{res['error']}\n{res.get('trace', '')[-2000:]}"
+                                for r, res in sorted(failed.items()))
+                raise DistributedRuntimeError(f"worker(s) failed:\n{msg}")
+        except DistributedRuntimeError:
+            self.close()  # a failed session may leave the process group unusable
+            raise
+        outputs, timings = {}, {}
+        for r in range(n):
+            ident = self.identities[r % len(self.identities)]
+            res = results[r]
+            outputs.update(res["outputs"])  # replica 0 holds the gathered outputs
+            timings[ident] = max(timings.get(ident, 0), res["elapsed_us"])
+            if r < len(self.identities):
+                self.storage[ident].update(res.get("storage", {}))
+        self.last_timings = timings
+        self.last_rounds = max(res.get("rounds", 0) for res in results.values())
+        return outputs
+
+    def close(self):
+        """Shut the long-running workers down (they finish the session they run)."""
+        pool, self._pool = self._pool, None
+        if pool is None:
+            return
+        try:
+            if pool["client"] is not None and all(p.poll() is None for p in pool["procs"]):
+                pool["client"].shutdown()
+        except Exception:  # noqa: BLE001 - the store may be gone with a dead rank 0
+            pass
+        for p in pool["procs"]:
+            try:
+                p.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        for lg in pool["logs"]:
+            lg.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
     def _launch(self, comp: Computation, arguments: dict):
         R = self.replicas
@@ -256,7 +444,21 @@ class DistributedMooseRuntime:
         return self.storage[identity][key]
 
     def write_value_to_storage(self, identity, key, value):
-        self.storage[identity][key] = np.asarray(value) if not isinstance(value, str) else value
+        v = np.asarray(value) if not isinstance(value, str) else value
+        self.storage[identity][key] = v
+        self._dirty.setdefault(identity, {})[key] = v  # reaches the worker with the next job
+
+
+_LIVE: "weakref.WeakSet" = weakref.WeakSet()
+
+
+@atexit.register
+def _close_all():
+    for rt in list(_LIVE):
+        try:
+            rt.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
 
 
 def _host_numpy(v):
