@@ -1,0 +1,156 @@
+"""Transport bookkeeping and the persistent client runtime (VERDICT r3 items 6 and 7,
+ADVICE r3):
+
+* a send-only round whose peer dies makes the SENDER raise ``TransportError`` (at its next
+  round or at the end of the evaluation), instead of the failure being dropped;
+* the message-plan table is least-recently-used bounded;
+* ``DistributedMooseRuntime`` runs many evaluations on one set of long-running workers
+  (reference ``execution/grpc.rs:46-146``: the client talks to running comet workers);
+* an SPMD computation that Loads a stored value whose shape changes between sessions still
+  runs (no header replay for it).
+"""
+import os
+import socket
+import time
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import moose_amd as pm
+from moose_amd.runtime.distributed import DistributedMooseRuntime
+
+IDS = ["alice", "bob", "carole"]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _sender_worker(rank, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MOOSEX_ASYNC_SENDS="1")
+    # the receiver (rank 0) dies at its first grouped exchange, before posting its receive
+    os.environ["MOOSEX_FAULT"] = "exit:1@0"
+    import datetime
+
+    dist.init_process_group("gloo", rank=rank, world_size=2,
+                            timeout=datetime.timedelta(seconds=30))
+    from moose_amd.parallel.transport import Transport
+    from moose_amd.parallel.transport import TransportError
+
+    tr = Transport(rank, 2, "cpu")
+    if rank == 0:
+        tr.exchange([], [(torch.empty(1000), 1)])  # exits inside
+        q.put((0, "not reached"))
+        return
+    tr.exchange([(torch.ones(1000), 0)], [])  # send-only round: returns at once
+    assert len(tr._unwaited) == 1
+    time.sleep(2.0)
+    try:
+        tr.end_evaluation()
+        q.put((1, "no error"))
+    except TransportError as e:
+        q.put((1, f"TransportError: {e}"))
+    os._exit(0)
+
+
+def test_sender_raises_on_a_failed_async_send():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_sender_worker, args=(r, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    rank, msg = q.get(timeout=120)
+    for p in ps:
+        p.join(60)
+    assert rank == 1 and msg.startswith("TransportError"), msg
+    assert "send to rank 0 failed" in msg
+    assert ps[0].exitcode == 17  # the injected death
+
+
+def test_message_plan_table_is_lru_bounded(monkeypatch):
+    from moose_amd.parallel import transport as T
+
+    monkeypatch.setattr(T, "PLAN_CACHE", 4)
+    monkeypatch.setattr(T, "_PLANS", T.collections.OrderedDict())
+    tr = T.Transport(0, 1, "cpu", plans=True)
+    for k in range(6):
+        tr.begin_plan(("comp", k))
+        tr.end_plan(True)
+    assert len(T._PLANS) == 4
+    keys = [k[3] for k in T._PLANS]
+    assert keys == [("comp", k) for k in range(2, 6)]
+    tr.begin_plan(("comp", 2))  # a replayed plan becomes the most recent
+    assert tr._mode == "replay"
+    tr.end_plan(True)
+    assert [k[3] for k in T._PLANS][-1] == ("comp", 2)
+
+
+def _mul_comp():
+    alice, bob, carole = (pm.host_placement(n) for n in IDS)
+    rep = pm.replicated_placement("rep", players=[alice, bob, carole])
+
+    @pm.computation
+    def f(x: pm.Argument(alice, vtype=pm.TensorType(pm.float64))):
+        with alice:
+            xf = pm.cast(x, dtype=pm.fixed(14, 23))
+        with rep:
+            y = pm.mul(xf, xf)
+        with bob:
+            return pm.cast(y, dtype=pm.float64)
+
+    return f
+
+
+def test_persistent_workers_serve_many_evaluations():
+    """Ten evaluations through one runtime object: one worker spawn, results correct,
+    per-role timings in the reference's (outputs, timings) shape; the p50 latency of the
+    warm evaluations is printed."""
+    f = _mul_comp()
+    with DistributedMooseRuntime(IDS, backend="gloo", timeout=180) as rt:
+        lat = []
+        for i in range(10):
+            x = np.array([1.5, -2.0 + i])
+            t0 = time.perf_counter()
+            out, timings = rt.run_computation(f, {"x": x})
+            lat.append(time.perf_counter() - t0)
+            np.testing.assert_allclose(list(out.values())[0], x * x, atol=1e-5)
+            assert set(timings) == set(IDS)
+        assert rt.worker_spawns == 1
+        warm = sorted(lat[1:])
+        print(f"persistent DistributedMooseRuntime: first {lat[0] * 1e3:.0f} ms, "
+              f"p50 {warm[len(warm) // 2] * 1e3:.1f} ms over 9 warm evaluations")
+        assert warm[len(warm) // 2] < lat[0]  # no process start per evaluation
+
+
+def test_spmd_load_with_changing_stored_shape():
+    """A computation that Loads from worker storage runs twice on the same workers with a
+    stored value of a different shape the second time (message plans would replay the
+    first shape's headers)."""
+    alice, bob, carole = (pm.host_placement(n) for n in IDS)
+    rep = pm.replicated_placement("rep", players=[alice, bob, carole])
+
+    @pm.computation
+    def g():
+        with alice:
+            x = pm.load("x", dtype=pm.float64)
+            xf = pm.cast(x, dtype=pm.fixed(14, 23))
+        with rep:
+            y = pm.mul(xf, xf)
+        with bob:
+            return pm.cast(y, dtype=pm.float64)
+
+    with DistributedMooseRuntime(IDS, backend="gloo", timeout=180) as rt:
+        for shape in ((3,), (2, 5)):
+            x = np.arange(np.prod(shape), dtype=np.float64).reshape(shape) / 4
+            rt.write_value_to_storage("alice", "x", x)
+            out = rt.evaluate_computation(g, {})
+            got = np.asarray(list(out.values())[0])
+            assert got.shape == shape
+            np.testing.assert_allclose(got, x * x, atol=1e-4)
+        assert rt.worker_spawns == 1
