@@ -398,9 +398,12 @@ def _lr_stacked(runs, device):
 
     tm = logistic_regression_tutorial(128)
     out = {}
-    for mode in ("eager", "graphs"):
-        rt = LocalMooseRuntime(list(ROLES), device=device, fixedpoint_ring=128,
-                               use_graphs=mode == "graphs")
+    # eager (use_graphs=False), replay from the first evaluation (True), and the runtime's
+    # default with no flags (auto: captured at the second evaluation, replayed after)
+    for mode in ("eager", "graphs", "default"):
+        flags = {"eager": {"use_graphs": False}, "graphs": {"use_graphs": True},
+                 "default": {}}[mode]
+        rt = LocalMooseRuntime(list(ROLES), device=device, fixedpoint_ring=128, **flags)
         args = {"x": tm.x_test}
         for _ in range(3):
             r = rt.evaluate_computation(tm.computation, args)
@@ -413,7 +416,7 @@ def _lr_stacked(runs, device):
         lat.sort()
         rec = {"p50_ms": lat[len(lat) // 2], "p90_ms": lat[int(0.9 * (len(lat) - 1))],
                "max_abs_err_vs_sklearn": err}
-        if mode == "graphs":
+        if mode != "eager":
             rec["captured"] = bool(rt._graphs.plans)
         out[mode] = rec
         if device.type == "cuda":

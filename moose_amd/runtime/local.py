@@ -85,10 +85,16 @@ class LocalMooseRuntime:
         self.seed = seed
         self.last_stats = None
         self.last_timings = None
-        # replay whole evaluations as hipGraphs (runtime/graphs.py); MOOSEX_GRAPHS=1
+        # replay whole evaluations as hipGraphs (runtime/graphs.py).  Default (None): on a
+        # GPU, "auto" -- a computation evaluated a second time with the same argument
+        # signature, whose eager evaluation was dispatch-bound (under AUTO_GRAPH_MS), is
+        # captured then and replayed from the third evaluation on; True captures at the
+        # first evaluation; False (or MOOSEX_GRAPHS=0) never captures.
         if use_graphs is None:
-            use_graphs = os.environ.get("MOOSEX_GRAPHS", "0") == "1"
+            env = os.environ.get("MOOSEX_GRAPHS", "auto")
+            use_graphs = {"1": True, "0": False}.get(env, "auto")
         self.use_graphs = use_graphs
+        self._seen = {}  # auto mode: (id(comp), signature) -> (comp, last eager seconds)
         # HIP streams for independent operations (runtime/lanes.py); MOOSEX_LANES=n
         self.lanes = lanes
         from moose_amd.runtime.graphs import GraphCache
@@ -141,7 +147,15 @@ class LocalMooseRuntime:
             from moose_amd.runtime.distributed import _host_numpy
 
             return {k: _host_numpy(v) for k, v in outs.items()}
-        if self.use_graphs and self.device.type == "cuda":
+        graphs = self.use_graphs and self.device.type == "cuda"
+        akey = None
+        if graphs and self.use_graphs == "auto":
+            from moose_amd.runtime.graphs import signature
+
+            akey = (id(comp), signature(arguments))
+            seen = self._seen.get(akey)
+            graphs = (seen is not None and seen[0] is comp and seen[1] < AUTO_GRAPH_MS / 1e3)
+        if graphs:
             t0 = time.perf_counter()
             r = self._graphs.evaluate(comp, arguments, self.device, self.storage,
                                       self.fixedpoint_ring, self.seed, lanes=self.lanes)
@@ -163,8 +177,12 @@ class LocalMooseRuntime:
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
         dt = time.perf_counter() - t0
-        if self.use_graphs and self.device.type == "cuda":
+        if graphs:
             self._graphs.note_eager(dt)  # adaptive replay: the plan's eager probe
+        if akey is not None:
+            if len(self._seen) >= 256:
+                self._seen.pop(next(iter(self._seen)))
+            self._seen[akey] = (comp, dt)
         elapsed = int(dt * 1e6)
         self.last_timings = {i: elapsed for i in self.identities}
         self.last_stats = sess.stats
@@ -179,6 +197,11 @@ class LocalMooseRuntime:
         if identity not in self.storage:
             raise RuntimeError(f"unknown identity {identity}")
         self.storage[identity][key] = np.asarray(value) if not isinstance(value, str) else value
+
+
+# auto hipGraph mode: only evaluations whose eager run took less than this are captured
+# (dispatch-bound; a GEMM-bound evaluation gains nothing and its capture pins memory)
+AUTO_GRAPH_MS = float(os.environ.get("MOOSEX_GRAPHS_AUTO_MS", "50"))
 
 
 def _is_lowered(comp: Computation) -> bool:

@@ -99,3 +99,29 @@ def test_graph_replay_refreshes_keys():
     out = rt.evaluate_computation(native, args)
     assert not torch.equal(k0, plan.keys.t)
     np.testing.assert_allclose(next(iter(out.values())), np.ones((8, 8)), atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_default_runtime_replays_dispatch_bound_evaluations():
+    """LocalMooseRuntime with no flags on a GPU (auto mode): the first evaluation runs
+    eagerly, the second (same signature, dispatch-bound) is captured, later ones replay --
+    with fresh inputs and correct results."""
+    import time
+
+    from moose_amd.models.predictors.tutorial import logistic_regression_tutorial
+
+    tm = logistic_regression_tutorial(128)
+    rt = pm.LocalMooseRuntime(["alice", "bob", "carole"], device="cuda")
+    assert rt.use_graphs == "auto"
+    lat = []
+    for i in range(12):
+        t0 = time.perf_counter()
+        out = rt.evaluate_computation(tm.computation, {"x": tm.x_test})
+        lat.append((time.perf_counter() - t0) * 1e3)
+        got = np.asarray(list(out.values())[0])
+        assert np.abs(got - tm.proba).max() < 1e-3
+        assert bool(rt._graphs.plans) == (i >= 1)
+    plan = next(iter(rt._graphs.plans.values()))
+    assert plan.replays == 10
+    warm = sorted(lat[3:])
+    print(f"default LocalMooseRuntime LR p50 {warm[len(warm) // 2]:.3f} ms")
