@@ -43,6 +43,8 @@
 
 #include "hip_attr.h"
 #include "moosex.h"
+#include "prf_dev.h"
+#include "rss_fused.h"
 
 namespace {
 
@@ -975,6 +977,149 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// --- fused reconstruction + dot tail (stacked 3-party session) -----------------------------
+// The RSS product of a stacked session is z_p = cross product of party p (batch entry p of
+// the mode-1 GEMM); its tail -- zero share, reshare and TruncPr -- is k_mul_trunc3 over the
+// three parties' z of each element.  k_crt_recon_tail3 does both in one pass: a workgroup
+// takes a 4-row x 256-column strip of one 256x256 output tile, reconstructs the three
+// parties' z of its 1024 elements from the residue planes (k_crt_recon16d's arithmetic, one
+// thread = one column's 4 rows) into LDS, then re-maps to keystream order (one thread = one
+// ChaCha block of each of the nine streams = four elements 64 columns apart in one row,
+// exactly k_mul_trunc3's chunk<->element mapping, so the shares are bitwise the same) and
+// writes the output slots.  The 805 MB product tensor of a 4096^2 Z_2^128 step is never
+// written or read back.  Needs N % 256 == 0 (a 256-column strip is one keystream group)
+// and M % 4 == 0.
+template <class T>
+__device__ __forceinline__ void recon4(const int8_t* __restrict__ src, int64_t pstride, int n,
+                                       const RecTab4& r4, const RecTab& rc, T (&z)[4]) {
+  constexpr int ND = (int)sizeof(T);
+  constexpr int NK = ND / 2;
+  int acc[4][ND], aq[4][3];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+#pragma unroll
+    for (int d = 0; d < ND; ++d) acc[e][d] = 0;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) aq[e][d] = 0;
+  }
+  for (int g = 0; g < r4.groups; ++g) {
+    uint32_t v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      v[u] = 4 * g + u < n ? *(const uint32_t*)(src + (4 * g + u) * pstride) : 0u;
+    const uint32_t a0 = __builtin_amdgcn_perm(v[1], v[0], 0x05010400u);
+    const uint32_t a1 = __builtin_amdgcn_perm(v[1], v[0], 0x07030602u);
+    const uint32_t c0 = __builtin_amdgcn_perm(v[3], v[2], 0x05010400u);
+    const uint32_t c1 = __builtin_amdgcn_perm(v[3], v[2], 0x07030602u);
+    const int t[4] = {(int)__builtin_amdgcn_perm(c0, a0, 0x05040100u),
+                      (int)__builtin_amdgcn_perm(c0, a0, 0x07060302u),
+                      (int)__builtin_amdgcn_perm(c1, a1, 0x05040100u),
+                      (int)__builtin_amdgcn_perm(c1, a1, 0x07060302u)};
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+      const int w = (int)r4.wd[g][d];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e][d] = __builtin_amdgcn_sdot4(t[e], w, acc[e][d], false);
+    }
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      const int w = (int)r4.rd[g][d];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) aq[e][d] = __builtin_amdgcn_sdot4(t[e], w, aq[e][d], false);
+    }
+  }
+  T mw = 0;
+#pragma unroll
+  for (int k = 0; k < NK; ++k) mw |= (T)rc.Mw[k] << (16 * k);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    T s = 0;
+#pragma unroll
+    for (int k = 0; k < NK; ++k)
+      s += (T)(int64_t)(acc[e][2 * k] + acc[e][2 * k + 1] * 256) << (16 * k);
+    const int64_t F = (int64_t)aq[e][0] + (int64_t)aq[e][1] * 256 + (int64_t)aq[e][2] * 65536;
+    const int64_t q = (F + (1 << 23)) >> 24;
+    z[e] = s - (T)q * mw;
+  }
+}
+
+template <class T>
+__global__ void __launch_bounds__(256)
+    k_crt_recon_tail3(const int8_t* __restrict__ CR, T* __restrict__ out0, T* __restrict__ out1,
+                      int64_t M, int64_t N, int64_t tiles_n, int64_t ntiles, int64_t os,
+                      const RecTab4 r4, int n, const RecTab rc, mxd::KeySrc keys,
+                      uint64_t nmul, int m, uint64_t nr0, uint64_t nr1, uint64_t nt,
+                      uint64_t nm, uint64_t nz0, uint64_t nz2) {
+  static_assert(sizeof(T) == 16, "one 16-byte keystream chunk per element");
+  constexpr int BN = 256, kCrTile = BM * BN;
+  __shared__ uint32_t rks[3][mxd::kKeyWords];
+  __shared__ T zl[3][4][BN];  // the strip's products: 48 KB
+  mxd::stage_keys(rks, keys, 3);
+  const int64_t pstride = ntiles * (int64_t)kCrTile;
+  const int tid = (int)threadIdx.x;
+  const uint32_t* const key[9] = {rks[0], rks[1], rks[2], rks[0], rks[2],
+                                  rks[0], rks[0], rks[0], rks[2]};
+  const uint64_t nonce[9] = {nmul, nmul, nmul, nr0, nr1, nt, nm, nz0, nz2};
+  for (int64_t wg = blockIdx.x; wg < ntiles * 64; wg += gridDim.x) {
+    const int64_t tile = wg >> 6;
+    const int s = (int)(wg & 63);  // 4-row strip of the tile
+    const int64_t tm = tile / tiles_n, tn = tile % tiles_n;
+    const int64_t row0 = tm * BM + 4 * s;
+    if (row0 >= M) continue;  // whole strips only (M % 4 == 0): uniform per workgroup
+    {  // phase 1: thread = column tid of the strip; its 4 rows of every party's product
+      const int c = tid, bj = c >> 4;
+      const int lane = (s & 3) * 16 + (c & 15);
+      const int64_t off = tile * kCrTile + (((s >> 2) * (BN / 16) + bj) * 64 + lane) * 4;
+#pragma unroll 1
+      for (int b = 0; b < 3; ++b) {
+        T z[4];
+        recon4<T>(CR + (int64_t)b * n * pstride + off, pstride, n, r4, rc, z);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) zl[b][e][c] = z[e];
+      }
+    }
+    __syncthreads();
+    {  // phase 2: thread = ChaCha block j of row r's keystream group: columns j + 64 part
+      const int r = tid >> 6, j = tid & 63;
+      const int64_t cbase = (row0 + r) * N + tn * BN;  // a multiple of 256 (N % 256 == 0)
+      const uint64_t B = ((uint64_t)(cbase >> 8) << 6) | (uint64_t)j;  // ks_block_of(cbase+j)
+      uint32_t w[9][16];
+#pragma unroll
+      for (int q = 0; q < 9; ++q) mx::chacha_block(key[q], nonce[q], B, w[q]);
+#pragma unroll
+      for (int part = 0; part < 4; ++part) {
+        const int col = j + 64 * part;
+        const int64_t e = cbase + col;  // == ks_chunk(B, part): k_mul_trunc3's element
+        uint64_t lo[9], hi[9];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) mx::part_u64(w[q], part, &lo[q], &hi[q]);
+        T z[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const int q = p == 2 ? 0 : p + 1;
+          z[p] = mxr::zs_combine<T>(MX_CROSS_ARITH, zl[p][r][col], mxd::pick<T>(lo[p], hi[p], 0),
+                                    mxd::pick<T>(lo[q], hi[q], 0));
+        }
+        const T Z0 = mxd::pick<T>(lo[7], hi[7], 0);
+        const T Z2 = mxd::pick<T>(lo[8], hi[8], 0);
+        const T Z1 = mxf::trunc_pr_z1<T>(z[0], z[1], z[2], mxd::pick<T>(lo[3], hi[3], 0),
+                                         mxd::pick<T>(lo[4], hi[4], 0),
+                                         mxd::pick<T>(lo[5], hi[5], 0),
+                                         mxd::pick<T>(lo[6], hi[6], 0), Z0, Z2, m);
+        out0[e] = Z0;
+        out0[os + e] = Z1;
+        out0[2 * os + e] = Z2;
+        if (out1 != out0 + os) {  // else a 4-slot ring: out1's slots 0, 1 are out0's 1, 2
+          out1[e] = Z1;
+          out1[os + e] = Z2;
+        }
+        out1[2 * os + e] = Z0;
+      }
+    }
+    __syncthreads();  // the next strip reuses the LDS
+  }
+}
+
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 int crt_kernel() {  // MOOSEX_CRT_KERNEL: 1 = 4 waves of 128x128, 2 = 8 waves of 128x64
@@ -1174,17 +1319,33 @@ void* workspace(int64_t bytes, hipStream_t st) {
   return w.ptr;
 }
 
+// The dot tail fused into the reconstruction (k_crt_recon_tail3): output slots, keys and
+// nonces of the stacked zero share + reshare + TruncPr.
+template <class T>
+struct TailArgs {
+  T* out0;
+  T* out1;
+  int64_t os;
+  mxd::KeySrc keys;
+  uint64_t nmul;
+  int m;
+  uint64_t nn[6];
+};
+
 template <class T>
 int run_crt(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T* A1,
             int64_t a_bstride, const T* B0, const T* B1, int64_t b_bstride,
             const int8_t* rb_pre, int mode, T* C, int accumulate, hipStream_t st,
-            int64_t roll = 0) {
+            int64_t roll = 0, const TailArgs<T>* tail = nullptr) {
   constexpr int words = sizeof(T) / 8;
   if (roll && (mode != 1 || K % BK || !crt_mfma16() || a_bstride == 0 || batch < 2 ||
                roll % batch == 0))
     return -7;  // not applicable: the caller runs the two-operand form
   const CPlan p = make_cplan(words, batch, M, N, K, mode, roll != 0);
   if (p.n < 0) return -6;
+  if (tail && (batch != 3 || p.bn != 256 || N % 256 || M % 4 || !crt_mfma16() ||
+               !recon_dot4()))
+    return -7;  // the caller runs the product and the tail kernel
   if ((mode ? 2 * K : K) > (1 << 15)) return -6;  // exact epilogue rounding bound
   const Tables& tb = tables_for(words, p.n);
   const int64_t need = p.ra_bytes + (rb_pre ? 0 : p.rb_bytes) + p.cr_bytes;
@@ -1208,6 +1369,19 @@ int run_crt(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T
     launch_prep<T>(p, tb, false, a_bc ? 1 : batch, M, K, a_bstride, A0, A1, mode, ra, st);
   launch_crt_gemm(p, tb, batch, ra, rb, cr, (a_bc ? 1 : 0) | (b_bc ? 2 : 0),
                   (int)(((roll % batch) + batch) % batch), st);
+  if constexpr (sizeof(T) == 16) {
+    if (tail) {
+      const int64_t ntiles = p.tiles_m * p.tiles_n;
+      const int64_t wgs = ntiles * 64;
+      hipLaunchKernelGGL(k_crt_recon_tail3<T>, dim3((unsigned)std::min<int64_t>(wgs, 1 << 20)),
+                         dim3(256), 0, st, cr, tail->out0, tail->out1, M, N, p.tiles_n, ntiles,
+                         tail->os, tb.r4, p.n, tb.rc, tail->keys, tail->nmul, tail->m,
+                         tail->nn[0], tail->nn[1], tail->nn[2], tail->nn[3], tail->nn[4],
+                         tail->nn[5]);
+      const hipError_t e = hipGetLastError();
+      return e != hipSuccess ? -100 - (int)e : 0;
+    }
+  }
   launch_recon<T>(p, tb, batch, M, N, cr, C, accumulate, st);
   const hipError_t e = hipGetLastError();
   return e != hipSuccess ? -100 - (int)e : 0;
@@ -1308,6 +1482,31 @@ int mxh_crt_roll(int words, int64_t batch, int64_t M, int64_t N, int64_t K, cons
                          (const u128*)B1, bs, (const int8_t*)rb, 1, (u128*)C, accumulate, st,
                          roll);
   return -2;
+}
+
+// mxh_crt_roll for the three parties of a stacked session (batch 3, roll 1) with the dot's
+// tail fused into the reconstruction: out0 / out1 receive the shares of
+// trunc_pr(reshare(z + zero share), m) exactly as mx_mul_trunc3_kv(z) would write them
+// (slots: the three key slots k0, k1, k2; nn: nonces r0, r1, t, m, z0, z2).  Z_2^128 only;
+// -7 when not applicable (the caller runs mxh_crt_roll and the tail kernel).  out0 == null:
+// only the applicability check (nothing launched).
+int mxh_crt_roll_tail(int words, int64_t M, int64_t N, int64_t K, const void* A0,
+                      int64_t a_bstride, const void* B0, const void* B1, const void* rb,
+                      void* out0, void* out1, int64_t os, const uint32_t* slots, uint64_t nmul,
+                      int m, const uint64_t* nn, void* stream) {
+  if (words != 2) return -7;
+  if (out0 == nullptr) {  // query: would this product run fused?
+    if (!crt_mfma16() || !recon_dot4() || N % 256 || M % 4 || K % BK) return -7;
+    const CPlan p = make_cplan(2, 3, M, N, K, 1, true);
+    return p.n < 0 || p.bn != 256 || 2 * K > (1 << 15) ? -7 : 0;
+  }
+  const uint32_t* ptrs[3];
+  for (int i = 0; i < 3; ++i) ptrs[i] = slots + MX_KEY_SLOT_WORDS * i;
+  TailArgs<u128> t{(u128*)out0, (u128*)out1, os, mxd::keysrc_slots(ptrs, 3), nmul, m,
+                   {nn[0], nn[1], nn[2], nn[3], nn[4], nn[5]}};
+  return run_crt<u128>(3, M, N, K, (const u128*)A0, nullptr, a_bstride, (const u128*)B0,
+                       (const u128*)B1, K * N, (const int8_t*)rb, 1, nullptr, 0,
+                       (hipStream_t)stream, 1, &t);
 }
 
 // Prepared-B variant (row-chunked dot pipeline): B' residues built once into a caller buffer.
