@@ -85,6 +85,8 @@ struct PrepTab {  // operand residues
   uint32_t w[kMaxMod][4];  // weight of byte j of the element = byte j%4 of word j/4
   uint32_t neg[kMaxMod];   // added when the element is negative: (p - 2^w mod p) [* inv] mod p
   uint32_t mul0;           // p = 256: residue = (byte0 * mul0) mod 256
+  uint32_t magic[kMaxMod];  // ceil(2^32 / p): floor(t / p) = mulhi(t, magic) for t < 2^21
+  uint32_t half[kMaxMod];   // (p - 1) / 2 (p odd)
 };
 struct EpiTab {  // GEMM epilogue
   int n;
@@ -170,6 +172,8 @@ void build_tables(int words, int n, Tables& t) {
     t.ep.t16[i] = (int)((1 << 16) % p);
     t.pa.p[i] = t.pb.p[i] = p;
     t.pa.rcp[i] = t.pb.rcp[i] = 1.0f / (float)p;
+    t.pa.magic[i] = t.pb.magic[i] = (uint32_t)(((uint64_t)1 << 32) / (uint64_t)p + 1);
+    t.pa.half[i] = t.pb.half[i] = (uint32_t)((p - 1) / 2);
     int pw = 1 % p;  // 256^j mod p
     for (int j = 0; j < nbytes; ++j) {
       const int wb = pw, wa = (int)((int64_t)pw * inv % p);
@@ -252,16 +256,34 @@ __device__ __forceinline__ int residue(const uint32_t (&x)[NW], const uint32_t (
   return (int)__builtin_fmaf(-qt, p, fs);      // in [-(p-1)/2, (p-1)/2]
 }
 
+// The same residue with integer arithmetic only: the accumulation starts at (p - 1) / 2
+// (plus the negative correction), so floor(s / p) -- one multiply-high by ceil(2^32 / p),
+// exact for s < 2^21 and p < 2^11 -- is the rounded quotient of the centered residue.
+// 8 VALU ops per residue instead of 11 (the prep kernels are VALU-bound).
+template <int NW>
+__device__ __forceinline__ int residue_i(const uint32_t (&x)[NW], const uint32_t (&w)[4],
+                                         uint32_t h, uint32_t nh, uint32_t magic, int p) {
+  uint32_t s = (x[NW - 1] >> 31) ? nh : h;
+#pragma unroll
+  for (int q = 0; q < NW; ++q) s = __builtin_amdgcn_udot4(x[q], w[q], s, false);
+  const uint32_t qt = __umulhi(s, magic);
+  return (int)(s - qt * (uint32_t)p) - (int)h;  // in [-(p-1)/2, (p-1)/2]
+}
+
 // One thread = (tile, k-step, image row r, 16-byte chunk c) of every residue plane.
 // TRANS = false: A' rows are M rows of [A0 | A1] (row-major [R][K] per batch, batch stride
 // xs elements).  TRANS = true: B' rows are the N columns of [B0 + B1 ; B0] ([K][R]).
-template <class T, bool TRANS, int ROWS>
+// dual (TRANS, mode 1, K % BK == 0): a thread does k-step kb of the first half AND kb + nkb/2
+// of the second, so B0's element is read twice back to back (the second read a cache hit)
+// instead of by two threads far apart (2.4 -> 1.6 GB of HBM reads for a 4096^2 Z_2^128 B').
+template <class T, bool TRANS, int ROWS, bool IP>
 __global__ void __launch_bounds__(256)
     k_crt_prep(const T* __restrict__ X0, const T* __restrict__ X1, int64_t R, int64_t K,
                int64_t xs, int mode, int8_t* __restrict__ out, int64_t tiles, int64_t nkb,
-               const PrepTab tab) {
+               const PrepTab tab, int dual) {
   constexpr int NW = Words<T>::N;
-  const int64_t total = tiles * nkb * (ROWS * 4);
+  const int64_t kbs = dual ? nkb / 2 : nkb;  // k-steps walked by the index space
+  const int64_t total = tiles * kbs * (ROWS * 4);
   const int64_t b = blockIdx.y;
   const T* x0 = X0 + b * xs;
   const T* x1 = mode ? X1 + b * xs : x0;
@@ -269,11 +291,13 @@ __global__ void __launch_bounds__(256)
   const int64_t plane = tiles * nkb * (int64_t)(ROWS * BK);
   int8_t* ob = out + b * n * plane;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total;
-       g += (int64_t)gridDim.x * blockDim.x) {
+       g += (int64_t)gridDim.x * blockDim.x)
+#pragma unroll 1
+  for (int pass = 0; pass < 1 + dual; ++pass) {
     const int c = (int)(g & 3);
     const int r = (int)((g >> 2) & (ROWS - 1));
     const int64_t q = g / (ROWS * 4);
-    const int64_t kb = q % nkb, t = q / nkb;
+    const int64_t kb = q % kbs + pass * kbs, t = q / kbs;
     const int64_t row = t * ROWS + r;
     const int64_t k0 = kb * BK + c * 16;
     uint32_t v[16][NW];
@@ -306,10 +330,17 @@ __global__ void __launch_bounds__(256)
     for (int i = 1; i < n; ++i) {
       const uint32_t w[4] = {tab.w[i][0], tab.w[i][1], tab.w[i][2], tab.w[i][3]};
       const uint32_t neg = tab.neg[i];
-      const float p = (float)tab.p[i], rcp = tab.rcp[i];
       int rr[16];
+      if constexpr (IP) {
+        const uint32_t h = tab.half[i], magic = tab.magic[i];
+        const int p = tab.p[i];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) rr[j] = residue<NW>(v[j], w, neg, p, rcp);
+        for (int j = 0; j < 16; ++j) rr[j] = residue_i<NW>(v[j], w, h, h + neg, magic, p);
+      } else {
+        const float p = (float)tab.p[i], rcp = tab.rcp[i];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) rr[j] = residue<NW>(v[j], w, neg, p, rcp);
+      }
       v4i o;
 #pragma unroll
       for (int u = 0; u < 4; ++u) o[u] = (int)pack4(rr[4 * u], rr[4 * u + 1], rr[4 * u + 2], rr[4 * u + 3]);
@@ -1043,7 +1074,7 @@ __device__ __forceinline__ void recon4(const int8_t* __restrict__ src, int64_t p
   }
 }
 
-template <class T>
+template <class T, int REMAP>
 __global__ void __launch_bounds__(256)
     k_crt_recon_tail3(const int8_t* __restrict__ CR, T* __restrict__ out0, T* __restrict__ out1,
                       int64_t M, int64_t N, int64_t tiles_n, int64_t ntiles, int64_t os,
@@ -1060,7 +1091,9 @@ __global__ void __launch_bounds__(256)
   const uint32_t* const key[9] = {rks[0], rks[1], rks[2], rks[0], rks[2],
                                   rks[0], rks[0], rks[0], rks[2]};
   const uint64_t nonce[9] = {nmul, nmul, nmul, nr0, nr1, nt, nm, nz0, nz2};
-  for (int64_t wg = blockIdx.x; wg < ntiles * 64; wg += gridDim.x) {
+  for (int64_t wg0 = blockIdx.x; wg0 < ntiles * 64; wg0 += gridDim.x) {
+    // REMAP: consecutive strips on one XCD (strips 2s, 2s+1 share the residue cache lines)
+    const int64_t wg = REMAP && gridDim.x == ntiles * 64 ? xcd_remap(wg0, gridDim.x) : wg0;
     const int64_t tile = wg >> 6;
     const int s = (int)(wg & 63);  // 4-row strip of the tile
     const int64_t tm = tile / tiles_n, tn = tile % tiles_n;
@@ -1153,6 +1186,16 @@ int recon_dot4() {  // MOOSEX_CRT_RECON=0: the multiply-add reconstruction
   return v;
 }
 
+// MOOSEX_CRT_TAIL: 1 = the fused reconstruction + dot tail with XCD-aware strip order
+// (default), 2 = the same in launch order, 0 = not fused (reconstruction, then the tail kernel)
+int tail_variant() {
+  static const int v = [] {
+    const char* e = std::getenv("MOOSEX_CRT_TAIL");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+
 struct CPlan {
   int n, bn;
   int64_t tiles_m, tiles_n, nkb, a_nkb, ra_bytes, rb_bytes, cr_bytes;
@@ -1181,6 +1224,15 @@ int gemm_group_m() {
   return v >= 1 && v <= 64 ? v : 4;
 }
 
+// MOOSEX_CRT_PREP bits: 1 = integer residues (residue_i), 2 = dual-pass B' prep (default 3)
+int prep_flags() {
+  static const int v = [] {
+    const char* e = std::getenv("MOOSEX_CRT_PREP");
+    return e ? std::atoi(e) : 3;
+  }();
+  return v;
+}
+
 template <class T>
 void launch_prep(const CPlan& p, const Tables& tb, bool is_b, int64_t batch, int64_t R,
                  int64_t K, int64_t xs, const T* X0, const T* X1, int mode, int8_t* out,
@@ -1188,17 +1240,25 @@ void launch_prep(const CPlan& p, const Tables& tb, bool is_b, int64_t batch, int
   if (nkb < 0) nkb = p.nkb;
   const int64_t tiles = is_b ? p.tiles_n : p.tiles_m;
   const int rows = is_b ? p.bn : BM;
-  const int64_t work = tiles * nkb * (rows * 4);
+  const int dual = is_b && mode == 1 && K % BK == 0 && nkb % 2 == 0 && prep_flags() & 2 ? 1 : 0;
+  const int64_t work = tiles * (dual ? nkb / 2 : nkb) * (rows * 4);
   const dim3 grid((unsigned)std::min<int64_t>((work + 255) / 256, 16384), (unsigned)batch);
+#define MX_PREP(TR, ROWS, TAB)                                                               \
+  do {                                                                                      \
+    if (prep_flags() & 1)                                                                   \
+      hipLaunchKernelGGL((k_crt_prep<T, TR, ROWS, true>), grid, dim3(256), 0, st, X0, X1, R, K, \
+                         xs, mode, out, tiles, nkb, TAB, dual);                              \
+    else                                                                                    \
+      hipLaunchKernelGGL((k_crt_prep<T, TR, ROWS, false>), grid, dim3(256), 0, st, X0, X1, R,   \
+                         K, xs, mode, out, tiles, nkb, TAB, dual);                           \
+  } while (0)
   if (!is_b)
-    hipLaunchKernelGGL((k_crt_prep<T, false, BM>), grid, dim3(256), 0, st, X0, X1, R, K, xs, mode,
-                       out, tiles, nkb, tb.pa);
+    MX_PREP(false, BM, tb.pa);
   else if (rows == 256)
-    hipLaunchKernelGGL((k_crt_prep<T, true, 256>), grid, dim3(256), 0, st, X0, X1, R, K, xs, mode,
-                       out, tiles, nkb, tb.pb);
+    MX_PREP(true, 256, tb.pb);
   else
-    hipLaunchKernelGGL((k_crt_prep<T, true, 128>), grid, dim3(256), 0, st, X0, X1, R, K, xs, mode,
-                       out, tiles, nkb, tb.pb);
+    MX_PREP(true, 128, tb.pb);
+#undef MX_PREP
 }
 
 // MOOSEX_CRT_DMA_MASK (timing experiments, wrong results): bit 0 = stream A, bit 1 = B,
@@ -1373,11 +1433,18 @@ int run_crt(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T
     if (tail) {
       const int64_t ntiles = p.tiles_m * p.tiles_n;
       const int64_t wgs = ntiles * 64;
-      hipLaunchKernelGGL(k_crt_recon_tail3<T>, dim3((unsigned)std::min<int64_t>(wgs, 1 << 20)),
-                         dim3(256), 0, st, cr, tail->out0, tail->out1, M, N, p.tiles_n, ntiles,
-                         tail->os, tb.r4, p.n, tb.rc, tail->keys, tail->nmul, tail->m,
-                         tail->nn[0], tail->nn[1], tail->nn[2], tail->nn[3], tail->nn[4],
-                         tail->nn[5]);
+      if (tail_variant() == 2)
+        hipLaunchKernelGGL((k_crt_recon_tail3<T, 0>),
+                           dim3((unsigned)std::min<int64_t>(wgs, 1 << 20)), dim3(256), 0, st, cr,
+                           tail->out0, tail->out1, M, N, p.tiles_n, ntiles, tail->os, tb.r4, p.n,
+                           tb.rc, tail->keys, tail->nmul, tail->m, tail->nn[0], tail->nn[1],
+                           tail->nn[2], tail->nn[3], tail->nn[4], tail->nn[5]);
+      else
+        hipLaunchKernelGGL((k_crt_recon_tail3<T, 1>),
+                           dim3((unsigned)std::min<int64_t>(wgs, 1 << 20)), dim3(256), 0, st, cr,
+                           tail->out0, tail->out1, M, N, p.tiles_n, ntiles, tail->os, tb.r4, p.n,
+                           tb.rc, tail->keys, tail->nmul, tail->m, tail->nn[0], tail->nn[1],
+                           tail->nn[2], tail->nn[3], tail->nn[4], tail->nn[5]);
       const hipError_t e = hipGetLastError();
       return e != hipSuccess ? -100 - (int)e : 0;
     }
@@ -1496,7 +1563,8 @@ int mxh_crt_roll_tail(int words, int64_t M, int64_t N, int64_t K, const void* A0
                       int m, const uint64_t* nn, void* stream) {
   if (words != 2) return -7;
   if (out0 == nullptr) {  // query: would this product run fused?
-    if (!crt_mfma16() || !recon_dot4() || N % 256 || M % 4 || K % BK) return -7;
+    if (!tail_variant() || !crt_mfma16() || !recon_dot4() || N % 256 || M % 4 || K % BK)
+      return -7;
     const CPlan p = make_cplan(2, 3, M, N, K, 1, true);
     return p.n < 0 || p.bn != 256 || 2 * K > (1 << 15) ? -7 : 0;
   }

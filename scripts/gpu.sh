@@ -12,6 +12,8 @@
 #   logreg    logistic-regression training sweep            aes  AES-in-MPC decrypt
 #   coresid   GEMM + concurrent copy kernel co-residency trace
 #   ladder    the bench fallback ladder with a rank stalled in attempt 0 (one GPU, 3 ranks)
+#   ab        driver command under env configurations ABCFG="name=VAR=v,VAR2=w ..." (ABPROF=1:
+#             plus a rocprofv3 kernel-stats pass each)      gemmtest  the CRT GEMM GPU tests
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export PYTHONPATH=$PWD TMPDIR=/tmp
@@ -78,6 +80,28 @@ if has ladder; then
   # rank 1, the supervisors kill it on every rank and attempt 1 (1 stream) measures
   run ladder3 400 env MOOSEX_SHARED_GPU=1 MOOSEX_BENCH_STALL=1:warmup python bench.py --gpus 3 \
     --steps 3 --warmup 1 --size 1024 --lr-runs 3 --deadline 300 && summary gpurun_out/ladder3.log
+fi
+if has ab; then
+  # A/B of env configurations on the driver command (ABCFG="NAME=VAR=v,VAR2=w ...")
+  for cfg in ${ABCFG:-base=MOOSEX_CRT_TAIL=0}; do
+    name=${cfg%%=*}; vars=${cfg#*=}
+    for kv in ${vars//,/ }; do export "$kv"; done
+    run ab_$name 300 python3 bench.py --steps 20 --warmup 5 --lr-runs 0 --zero-slot-steps 0 \
+      && summary gpurun_out/ab_$name.log
+    if [ -n "$ABPROF" ]; then
+      run abprof_$name 300 rocprofv3 --kernel-trace --stats -d gpurun_out/abprof_$name -o run \
+        --output-format csv -- python3 bench.py --steps 10 --warmup 3 --lr-runs 0 \
+        --zero-slot-steps 0 --no-check
+      python3 scripts/prof_summary.py gpurun_out/abprof_$name/run_kernel_stats.csv "$name" \
+        | head -12 > gpurun_out/abprof_$name.md || true
+      cat gpurun_out/abprof_$name.md
+    fi
+    for kv in ${vars//,/ }; do unset "${kv%%=*}"; done
+  done
+fi
+if has gemmtest; then
+  run gemmtest 600 python -u -m pytest tests/test_gemm_crt.py -m gpu -x -v --timeout 300 \
+    --timeout-method thread
 fi
 if has variants; then
   for v in ${VARS:-8 16}; do
