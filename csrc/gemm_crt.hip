@@ -43,8 +43,6 @@
 
 #include "hip_attr.h"
 #include "moosex.h"
-#include "prf_dev.h"
-#include "rss_fused.h"
 
 namespace {
 
@@ -85,8 +83,6 @@ struct PrepTab {  // operand residues
   uint32_t w[kMaxMod][4];  // weight of byte j of the element = byte j%4 of word j/4
   uint32_t neg[kMaxMod];   // added when the element is negative: (p - 2^w mod p) [* inv] mod p
   uint32_t mul0;           // p = 256: residue = (byte0 * mul0) mod 256
-  uint32_t magic[kMaxMod];  // ceil(2^32 / p): floor(t / p) = mulhi(t, magic) for t < 2^21
-  uint32_t half[kMaxMod];   // (p - 1) / 2 (p odd)
 };
 struct EpiTab {  // GEMM epilogue
   int n;
@@ -172,8 +168,6 @@ void build_tables(int words, int n, Tables& t) {
     t.ep.t16[i] = (int)((1 << 16) % p);
     t.pa.p[i] = t.pb.p[i] = p;
     t.pa.rcp[i] = t.pb.rcp[i] = 1.0f / (float)p;
-    t.pa.magic[i] = t.pb.magic[i] = (uint32_t)(((uint64_t)1 << 32) / (uint64_t)p + 1);
-    t.pa.half[i] = t.pb.half[i] = (uint32_t)((p - 1) / 2);
     int pw = 1 % p;  // 256^j mod p
     for (int j = 0; j < nbytes; ++j) {
       const int wb = pw, wa = (int)((int64_t)pw * inv % p);
@@ -256,34 +250,16 @@ __device__ __forceinline__ int residue(const uint32_t (&x)[NW], const uint32_t (
   return (int)__builtin_fmaf(-qt, p, fs);      // in [-(p-1)/2, (p-1)/2]
 }
 
-// The same residue with integer arithmetic only: the accumulation starts at (p - 1) / 2
-// (plus the negative correction), so floor(s / p) -- one multiply-high by ceil(2^32 / p),
-// exact for s < 2^21 and p < 2^11 -- is the rounded quotient of the centered residue.
-// 8 VALU ops per residue instead of 11 (the prep kernels are VALU-bound).
-template <int NW>
-__device__ __forceinline__ int residue_i(const uint32_t (&x)[NW], const uint32_t (&w)[4],
-                                         uint32_t h, uint32_t nh, uint32_t magic, int p) {
-  uint32_t s = (x[NW - 1] >> 31) ? nh : h;
-#pragma unroll
-  for (int q = 0; q < NW; ++q) s = __builtin_amdgcn_udot4(x[q], w[q], s, false);
-  const uint32_t qt = __umulhi(s, magic);
-  return (int)(s - qt * (uint32_t)p) - (int)h;  // in [-(p-1)/2, (p-1)/2]
-}
-
 // One thread = (tile, k-step, image row r, 16-byte chunk c) of every residue plane.
 // TRANS = false: A' rows are M rows of [A0 | A1] (row-major [R][K] per batch, batch stride
 // xs elements).  TRANS = true: B' rows are the N columns of [B0 + B1 ; B0] ([K][R]).
-// dual (TRANS, mode 1, K % BK == 0): a thread does k-step kb of the first half AND kb + nkb/2
-// of the second, so B0's element is read twice back to back (the second read a cache hit)
-// instead of by two threads far apart (2.4 -> 1.6 GB of HBM reads for a 4096^2 Z_2^128 B').
-template <class T, bool TRANS, int ROWS, bool IP>
+template <class T, bool TRANS, int ROWS>
 __global__ void __launch_bounds__(256)
     k_crt_prep(const T* __restrict__ X0, const T* __restrict__ X1, int64_t R, int64_t K,
                int64_t xs, int mode, int8_t* __restrict__ out, int64_t tiles, int64_t nkb,
-               const PrepTab tab, int dual) {
+               const PrepTab tab) {
   constexpr int NW = Words<T>::N;
-  const int64_t kbs = dual ? nkb / 2 : nkb;  // k-steps walked by the index space
-  const int64_t total = tiles * kbs * (ROWS * 4);
+  const int64_t total = tiles * nkb * (ROWS * 4);
   const int64_t b = blockIdx.y;
   const T* x0 = X0 + b * xs;
   const T* x1 = mode ? X1 + b * xs : x0;
@@ -291,13 +267,11 @@ __global__ void __launch_bounds__(256)
   const int64_t plane = tiles * nkb * (int64_t)(ROWS * BK);
   int8_t* ob = out + b * n * plane;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total;
-       g += (int64_t)gridDim.x * blockDim.x)
-#pragma unroll 1
-  for (int pass = 0; pass < 1 + dual; ++pass) {
+       g += (int64_t)gridDim.x * blockDim.x) {
     const int c = (int)(g & 3);
     const int r = (int)((g >> 2) & (ROWS - 1));
     const int64_t q = g / (ROWS * 4);
-    const int64_t kb = q % kbs + pass * kbs, t = q / kbs;
+    const int64_t kb = q % nkb, t = q / nkb;
     const int64_t row = t * ROWS + r;
     const int64_t k0 = kb * BK + c * 16;
     uint32_t v[16][NW];
@@ -330,17 +304,10 @@ __global__ void __launch_bounds__(256)
     for (int i = 1; i < n; ++i) {
       const uint32_t w[4] = {tab.w[i][0], tab.w[i][1], tab.w[i][2], tab.w[i][3]};
       const uint32_t neg = tab.neg[i];
+      const float p = (float)tab.p[i], rcp = tab.rcp[i];
       int rr[16];
-      if constexpr (IP) {
-        const uint32_t h = tab.half[i], magic = tab.magic[i];
-        const int p = tab.p[i];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) rr[j] = residue_i<NW>(v[j], w, h, h + neg, magic, p);
-      } else {
-        const float p = (float)tab.p[i], rcp = tab.rcp[i];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) rr[j] = residue<NW>(v[j], w, neg, p, rcp);
-      }
+      for (int j = 0; j < 16; ++j) rr[j] = residue<NW>(v[j], w, neg, p, rcp);
       v4i o;
 #pragma unroll
       for (int u = 0; u < 4; ++u) o[u] = (int)pack4(rr[4 * u], rr[4 * u + 1], rr[4 * u + 2], rr[4 * u + 3]);
@@ -1008,151 +975,6 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// --- fused reconstruction + dot tail (stacked 3-party session) -----------------------------
-// The RSS product of a stacked session is z_p = cross product of party p (batch entry p of
-// the mode-1 GEMM); its tail -- zero share, reshare and TruncPr -- is k_mul_trunc3 over the
-// three parties' z of each element.  k_crt_recon_tail3 does both in one pass: a workgroup
-// takes a 4-row x 256-column strip of one 256x256 output tile, reconstructs the three
-// parties' z of its 1024 elements from the residue planes (k_crt_recon16d's arithmetic, one
-// thread = one column's 4 rows) into LDS, then re-maps to keystream order (one thread = one
-// ChaCha block of each of the nine streams = four elements 64 columns apart in one row,
-// exactly k_mul_trunc3's chunk<->element mapping, so the shares are bitwise the same) and
-// writes the output slots.  The 805 MB product tensor of a 4096^2 Z_2^128 step is never
-// written or read back.  Needs N % 256 == 0 (a 256-column strip is one keystream group)
-// and M % 4 == 0.
-template <class T>
-__device__ __forceinline__ void recon4(const int8_t* __restrict__ src, int64_t pstride, int n,
-                                       const RecTab4& r4, const RecTab& rc, T (&z)[4]) {
-  constexpr int ND = (int)sizeof(T);
-  constexpr int NK = ND / 2;
-  int acc[4][ND], aq[4][3];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-#pragma unroll
-    for (int d = 0; d < ND; ++d) acc[e][d] = 0;
-#pragma unroll
-    for (int d = 0; d < 3; ++d) aq[e][d] = 0;
-  }
-  for (int g = 0; g < r4.groups; ++g) {
-    uint32_t v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      v[u] = 4 * g + u < n ? *(const uint32_t*)(src + (4 * g + u) * pstride) : 0u;
-    const uint32_t a0 = __builtin_amdgcn_perm(v[1], v[0], 0x05010400u);
-    const uint32_t a1 = __builtin_amdgcn_perm(v[1], v[0], 0x07030602u);
-    const uint32_t c0 = __builtin_amdgcn_perm(v[3], v[2], 0x05010400u);
-    const uint32_t c1 = __builtin_amdgcn_perm(v[3], v[2], 0x07030602u);
-    const int t[4] = {(int)__builtin_amdgcn_perm(c0, a0, 0x05040100u),
-                      (int)__builtin_amdgcn_perm(c0, a0, 0x07060302u),
-                      (int)__builtin_amdgcn_perm(c1, a1, 0x05040100u),
-                      (int)__builtin_amdgcn_perm(c1, a1, 0x07060302u)};
-#pragma unroll
-    for (int d = 0; d < ND; ++d) {
-      const int w = (int)r4.wd[g][d];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) acc[e][d] = __builtin_amdgcn_sdot4(t[e], w, acc[e][d], false);
-    }
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      const int w = (int)r4.rd[g][d];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) aq[e][d] = __builtin_amdgcn_sdot4(t[e], w, aq[e][d], false);
-    }
-  }
-  T mw = 0;
-#pragma unroll
-  for (int k = 0; k < NK; ++k) mw |= (T)rc.Mw[k] << (16 * k);
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    T s = 0;
-#pragma unroll
-    for (int k = 0; k < NK; ++k)
-      s += (T)(int64_t)(acc[e][2 * k] + acc[e][2 * k + 1] * 256) << (16 * k);
-    const int64_t F = (int64_t)aq[e][0] + (int64_t)aq[e][1] * 256 + (int64_t)aq[e][2] * 65536;
-    const int64_t q = (F + (1 << 23)) >> 24;
-    z[e] = s - (T)q * mw;
-  }
-}
-
-template <class T, int REMAP>
-__global__ void __launch_bounds__(256)
-    k_crt_recon_tail3(const int8_t* __restrict__ CR, T* __restrict__ out0, T* __restrict__ out1,
-                      int64_t M, int64_t N, int64_t tiles_n, int64_t ntiles, int64_t os,
-                      const RecTab4 r4, int n, const RecTab rc, mxd::KeySrc keys,
-                      uint64_t nmul, int m, uint64_t nr0, uint64_t nr1, uint64_t nt,
-                      uint64_t nm, uint64_t nz0, uint64_t nz2) {
-  static_assert(sizeof(T) == 16, "one 16-byte keystream chunk per element");
-  constexpr int BN = 256, kCrTile = BM * BN;
-  __shared__ uint32_t rks[3][mxd::kKeyWords];
-  __shared__ T zl[3][4][BN];  // the strip's products: 48 KB
-  mxd::stage_keys(rks, keys, 3);
-  const int64_t pstride = ntiles * (int64_t)kCrTile;
-  const int tid = (int)threadIdx.x;
-  const uint32_t* const key[9] = {rks[0], rks[1], rks[2], rks[0], rks[2],
-                                  rks[0], rks[0], rks[0], rks[2]};
-  const uint64_t nonce[9] = {nmul, nmul, nmul, nr0, nr1, nt, nm, nz0, nz2};
-  for (int64_t wg0 = blockIdx.x; wg0 < ntiles * 64; wg0 += gridDim.x) {
-    // REMAP: consecutive strips on one XCD (strips 2s, 2s+1 share the residue cache lines)
-    const int64_t wg = REMAP && gridDim.x == ntiles * 64 ? xcd_remap(wg0, gridDim.x) : wg0;
-    const int64_t tile = wg >> 6;
-    const int s = (int)(wg & 63);  // 4-row strip of the tile
-    const int64_t tm = tile / tiles_n, tn = tile % tiles_n;
-    const int64_t row0 = tm * BM + 4 * s;
-    if (row0 >= M) continue;  // whole strips only (M % 4 == 0): uniform per workgroup
-    {  // phase 1: thread = column tid of the strip; its 4 rows of every party's product
-      const int c = tid, bj = c >> 4;
-      const int lane = (s & 3) * 16 + (c & 15);
-      const int64_t off = tile * kCrTile + (((s >> 2) * (BN / 16) + bj) * 64 + lane) * 4;
-#pragma unroll 1
-      for (int b = 0; b < 3; ++b) {
-        T z[4];
-        recon4<T>(CR + (int64_t)b * n * pstride + off, pstride, n, r4, rc, z);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) zl[b][e][c] = z[e];
-      }
-    }
-    __syncthreads();
-    {  // phase 2: thread = ChaCha block j of row r's keystream group: columns j + 64 part
-      const int r = tid >> 6, j = tid & 63;
-      const int64_t cbase = (row0 + r) * N + tn * BN;  // a multiple of 256 (N % 256 == 0)
-      const uint64_t B = ((uint64_t)(cbase >> 8) << 6) | (uint64_t)j;  // ks_block_of(cbase+j)
-      uint32_t w[9][16];
-#pragma unroll
-      for (int q = 0; q < 9; ++q) mx::chacha_block(key[q], nonce[q], B, w[q]);
-#pragma unroll
-      for (int part = 0; part < 4; ++part) {
-        const int col = j + 64 * part;
-        const int64_t e = cbase + col;  // == ks_chunk(B, part): k_mul_trunc3's element
-        uint64_t lo[9], hi[9];
-#pragma unroll
-        for (int q = 0; q < 9; ++q) mx::part_u64(w[q], part, &lo[q], &hi[q]);
-        T z[3];
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          const int q = p == 2 ? 0 : p + 1;
-          z[p] = mxr::zs_combine<T>(MX_CROSS_ARITH, zl[p][r][col], mxd::pick<T>(lo[p], hi[p], 0),
-                                    mxd::pick<T>(lo[q], hi[q], 0));
-        }
-        const T Z0 = mxd::pick<T>(lo[7], hi[7], 0);
-        const T Z2 = mxd::pick<T>(lo[8], hi[8], 0);
-        const T Z1 = mxf::trunc_pr_z1<T>(z[0], z[1], z[2], mxd::pick<T>(lo[3], hi[3], 0),
-                                         mxd::pick<T>(lo[4], hi[4], 0),
-                                         mxd::pick<T>(lo[5], hi[5], 0),
-                                         mxd::pick<T>(lo[6], hi[6], 0), Z0, Z2, m);
-        out0[e] = Z0;
-        out0[os + e] = Z1;
-        out0[2 * os + e] = Z2;
-        if (out1 != out0 + os) {  // else a 4-slot ring: out1's slots 0, 1 are out0's 1, 2
-          out1[e] = Z1;
-          out1[os + e] = Z2;
-        }
-        out1[2 * os + e] = Z0;
-      }
-    }
-    __syncthreads();  // the next strip reuses the LDS
-  }
-}
-
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 int crt_kernel() {  // MOOSEX_CRT_KERNEL: 1 = 4 waves of 128x128, 2 = 8 waves of 128x64
@@ -1186,16 +1008,6 @@ int recon_dot4() {  // MOOSEX_CRT_RECON=0: the multiply-add reconstruction
   return v;
 }
 
-// MOOSEX_CRT_TAIL: 1 = the fused reconstruction + dot tail with XCD-aware strip order
-// (default), 2 = the same in launch order, 0 = not fused (reconstruction, then the tail kernel)
-int tail_variant() {
-  static const int v = [] {
-    const char* e = std::getenv("MOOSEX_CRT_TAIL");
-    return e ? std::atoi(e) : 1;
-  }();
-  return v;
-}
-
 struct CPlan {
   int n, bn;
   int64_t tiles_m, tiles_n, nkb, a_nkb, ra_bytes, rb_bytes, cr_bytes;
@@ -1224,15 +1036,6 @@ int gemm_group_m() {
   return v >= 1 && v <= 64 ? v : 4;
 }
 
-// MOOSEX_CRT_PREP bits: 1 = integer residues (residue_i), 2 = dual-pass B' prep (default 3)
-int prep_flags() {
-  static const int v = [] {
-    const char* e = std::getenv("MOOSEX_CRT_PREP");
-    return e ? std::atoi(e) : 3;
-  }();
-  return v;
-}
-
 template <class T>
 void launch_prep(const CPlan& p, const Tables& tb, bool is_b, int64_t batch, int64_t R,
                  int64_t K, int64_t xs, const T* X0, const T* X1, int mode, int8_t* out,
@@ -1240,25 +1043,17 @@ void launch_prep(const CPlan& p, const Tables& tb, bool is_b, int64_t batch, int
   if (nkb < 0) nkb = p.nkb;
   const int64_t tiles = is_b ? p.tiles_n : p.tiles_m;
   const int rows = is_b ? p.bn : BM;
-  const int dual = is_b && mode == 1 && K % BK == 0 && nkb % 2 == 0 && prep_flags() & 2 ? 1 : 0;
-  const int64_t work = tiles * (dual ? nkb / 2 : nkb) * (rows * 4);
+  const int64_t work = tiles * nkb * (rows * 4);
   const dim3 grid((unsigned)std::min<int64_t>((work + 255) / 256, 16384), (unsigned)batch);
-#define MX_PREP(TR, ROWS, TAB)                                                               \
-  do {                                                                                      \
-    if (prep_flags() & 1)                                                                   \
-      hipLaunchKernelGGL((k_crt_prep<T, TR, ROWS, true>), grid, dim3(256), 0, st, X0, X1, R, K, \
-                         xs, mode, out, tiles, nkb, TAB, dual);                              \
-    else                                                                                    \
-      hipLaunchKernelGGL((k_crt_prep<T, TR, ROWS, false>), grid, dim3(256), 0, st, X0, X1, R,   \
-                         K, xs, mode, out, tiles, nkb, TAB, dual);                           \
-  } while (0)
   if (!is_b)
-    MX_PREP(false, BM, tb.pa);
+    hipLaunchKernelGGL((k_crt_prep<T, false, BM>), grid, dim3(256), 0, st, X0, X1, R, K, xs, mode,
+                       out, tiles, nkb, tb.pa);
   else if (rows == 256)
-    MX_PREP(true, 256, tb.pb);
+    hipLaunchKernelGGL((k_crt_prep<T, true, 256>), grid, dim3(256), 0, st, X0, X1, R, K, xs, mode,
+                       out, tiles, nkb, tb.pb);
   else
-    MX_PREP(true, 128, tb.pb);
-#undef MX_PREP
+    hipLaunchKernelGGL((k_crt_prep<T, true, 128>), grid, dim3(256), 0, st, X0, X1, R, K, xs, mode,
+                       out, tiles, nkb, tb.pb);
 }
 
 // MOOSEX_CRT_DMA_MASK (timing experiments, wrong results): bit 0 = stream A, bit 1 = B,
@@ -1379,33 +1174,17 @@ void* workspace(int64_t bytes, hipStream_t st) {
   return w.ptr;
 }
 
-// The dot tail fused into the reconstruction (k_crt_recon_tail3): output slots, keys and
-// nonces of the stacked zero share + reshare + TruncPr.
-template <class T>
-struct TailArgs {
-  T* out0;
-  T* out1;
-  int64_t os;
-  mxd::KeySrc keys;
-  uint64_t nmul;
-  int m;
-  uint64_t nn[6];
-};
-
 template <class T>
 int run_crt(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T* A1,
             int64_t a_bstride, const T* B0, const T* B1, int64_t b_bstride,
             const int8_t* rb_pre, int mode, T* C, int accumulate, hipStream_t st,
-            int64_t roll = 0, const TailArgs<T>* tail = nullptr) {
+            int64_t roll = 0) {
   constexpr int words = sizeof(T) / 8;
   if (roll && (mode != 1 || K % BK || !crt_mfma16() || a_bstride == 0 || batch < 2 ||
                roll % batch == 0))
     return -7;  // not applicable: the caller runs the two-operand form
   const CPlan p = make_cplan(words, batch, M, N, K, mode, roll != 0);
   if (p.n < 0) return -6;
-  if (tail && (batch != 3 || p.bn != 256 || N % 256 || M % 4 || !crt_mfma16() ||
-               !recon_dot4()))
-    return -7;  // the caller runs the product and the tail kernel
   if ((mode ? 2 * K : K) > (1 << 15)) return -6;  // exact epilogue rounding bound
   const Tables& tb = tables_for(words, p.n);
   const int64_t need = p.ra_bytes + (rb_pre ? 0 : p.rb_bytes) + p.cr_bytes;
@@ -1429,26 +1208,6 @@ int run_crt(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T
     launch_prep<T>(p, tb, false, a_bc ? 1 : batch, M, K, a_bstride, A0, A1, mode, ra, st);
   launch_crt_gemm(p, tb, batch, ra, rb, cr, (a_bc ? 1 : 0) | (b_bc ? 2 : 0),
                   (int)(((roll % batch) + batch) % batch), st);
-  if constexpr (sizeof(T) == 16) {
-    if (tail) {
-      const int64_t ntiles = p.tiles_m * p.tiles_n;
-      const int64_t wgs = ntiles * 64;
-      if (tail_variant() == 2)
-        hipLaunchKernelGGL((k_crt_recon_tail3<T, 0>),
-                           dim3((unsigned)std::min<int64_t>(wgs, 1 << 20)), dim3(256), 0, st, cr,
-                           tail->out0, tail->out1, M, N, p.tiles_n, ntiles, tail->os, tb.r4, p.n,
-                           tb.rc, tail->keys, tail->nmul, tail->m, tail->nn[0], tail->nn[1],
-                           tail->nn[2], tail->nn[3], tail->nn[4], tail->nn[5]);
-      else
-        hipLaunchKernelGGL((k_crt_recon_tail3<T, 1>),
-                           dim3((unsigned)std::min<int64_t>(wgs, 1 << 20)), dim3(256), 0, st, cr,
-                           tail->out0, tail->out1, M, N, p.tiles_n, ntiles, tail->os, tb.r4, p.n,
-                           tb.rc, tail->keys, tail->nmul, tail->m, tail->nn[0], tail->nn[1],
-                           tail->nn[2], tail->nn[3], tail->nn[4], tail->nn[5]);
-      const hipError_t e = hipGetLastError();
-      return e != hipSuccess ? -100 - (int)e : 0;
-    }
-  }
   launch_recon<T>(p, tb, batch, M, N, cr, C, accumulate, st);
   const hipError_t e = hipGetLastError();
   return e != hipSuccess ? -100 - (int)e : 0;
@@ -1549,32 +1308,6 @@ int mxh_crt_roll(int words, int64_t batch, int64_t M, int64_t N, int64_t K, cons
                          (const u128*)B1, bs, (const int8_t*)rb, 1, (u128*)C, accumulate, st,
                          roll);
   return -2;
-}
-
-// mxh_crt_roll for the three parties of a stacked session (batch 3, roll 1) with the dot's
-// tail fused into the reconstruction: out0 / out1 receive the shares of
-// trunc_pr(reshare(z + zero share), m) exactly as mx_mul_trunc3_kv(z) would write them
-// (slots: the three key slots k0, k1, k2; nn: nonces r0, r1, t, m, z0, z2).  Z_2^128 only;
-// -7 when not applicable (the caller runs mxh_crt_roll and the tail kernel).  out0 == null:
-// only the applicability check (nothing launched).
-int mxh_crt_roll_tail(int words, int64_t M, int64_t N, int64_t K, const void* A0,
-                      int64_t a_bstride, const void* B0, const void* B1, const void* rb,
-                      void* out0, void* out1, int64_t os, const uint32_t* slots, uint64_t nmul,
-                      int m, const uint64_t* nn, void* stream) {
-  if (words != 2) return -7;
-  if (out0 == nullptr) {  // query: would this product run fused?
-    if (!tail_variant() || !crt_mfma16() || !recon_dot4() || N % 256 || M % 4 || K % BK)
-      return -7;
-    const CPlan p = make_cplan(2, 3, M, N, K, 1, true);
-    return p.n < 0 || p.bn != 256 || 2 * K > (1 << 15) ? -7 : 0;
-  }
-  const uint32_t* ptrs[3];
-  for (int i = 0; i < 3; ++i) ptrs[i] = slots + MX_KEY_SLOT_WORDS * i;
-  TailArgs<u128> t{(u128*)out0, (u128*)out1, os, mxd::keysrc_slots(ptrs, 3), nmul, m,
-                   {nn[0], nn[1], nn[2], nn[3], nn[4], nn[5]}};
-  return run_crt<u128>(3, M, N, K, (const u128*)A0, nullptr, a_bstride, (const u128*)B0,
-                       (const u128*)B1, K * N, (const int8_t*)rb, 1, nullptr, 0,
-                       (hipStream_t)stream, 1, &t);
 }
 
 // Prepared-B variant (row-chunked dot pipeline): B' residues built once into a caller buffer.

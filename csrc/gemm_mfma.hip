@@ -965,11 +965,6 @@ extern "C" int mxh_crt_roll(int words, int64_t batch, int64_t M, int64_t N, int6
                             const void* A0, int64_t a_bstride, int64_t roll, const void* B0,
                             const void* B1, const void* rb, void* C, int accumulate,
                             void* stream);
-extern "C" int mxh_crt_roll_tail(int words, int64_t M, int64_t N, int64_t K, const void* A0,
-                                 int64_t a_bstride, const void* B0, const void* B1,
-                                 const void* rb, void* out0, void* out1, int64_t os,
-                                 const uint32_t* slots, uint64_t nmul, int m, const uint64_t* nn,
-                                 void* stream);
 
 namespace {
 // 0 = auto (CRT for products with at least one full 256x256 output tile and K' >= 512),
@@ -1084,19 +1079,6 @@ int mx_gemm_roll(int words, int64_t batch, int64_t M, int64_t N, int64_t K, cons
   if ((words != 1 && words != 2) || !use_crt(lb ? 256 : M, N, K, 1)) return -7;
   return mxh_crt_roll(words, batch, M, N, K, A0, a_bstride, roll, B0, B1, lb, C, accumulate,
                       stream);
-}
-
-// mx_gemm_roll for a stacked session's three parties (batch 3, roll 1) with the dot's zero
-// share + reshare + TruncPr fused into the CRT reconstruction (mxh_crt_roll_tail); -7 when
-// not applicable.
-int mx_gemm_roll_tail(int words, int64_t M, int64_t N, int64_t K, const void* A0,
-                      int64_t a_bstride, const void* B0, const void* B1, const void* lb,
-                      void* out0, void* out1, int64_t os, const uint32_t* slots, uint64_t nmul,
-                      int m, const uint64_t* nn, void* stream) {
-  if (M == 0 || N == 0) return -7;
-  if (words != 2 || !use_crt(lb ? 256 : M, N, K, 1)) return -7;  // (out0 null: a query)
-  return mxh_crt_roll_tail(words, M, N, K, A0, a_bstride, B0, B1, lb, out0, out1, os, slots,
-                           nmul, m, nn, stream);
 }
 
 // Batched product with explicit batch strides (elements) for A and B (0 broadcasts).

@@ -169,13 +169,6 @@ int mx_crt_tables4(int words, int n, uint32_t* wd_out, uint32_t* rd_out);
 int mx_gemm_roll(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
                  int64_t a_bstride, int64_t roll, const void* B0, const void* B1, const void* lb,
                  void* C, int accumulate, void* stream);
-// mx_gemm_roll of a stacked session (batch 3, roll 1) with the dot's zero share + reshare +
-// TruncPr fused into the CRT reconstruction: out0 / out1 as mx_mul_trunc3_kv of the product
-// (slots: key slots k0..k2; nn: nonces r0, r1, t, m, z0, z2).  -7: not applicable.
-int mx_gemm_roll_tail(int words, int64_t M, int64_t N, int64_t K, const void* A0,
-                      int64_t a_bstride, const void* B0, const void* B1, const void* lb,
-                      void* out0, void* out1, int64_t os, const uint32_t* slots, uint64_t nmul,
-                      int m, const uint64_t* nn, void* stream);
 int mx_gemm_strided(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
                     const void* A1, int64_t a_bstride, const void* B0, const void* B1,
                     int64_t b_bstride, int mode, void* C, int accumulate, void* stream);

@@ -177,11 +177,6 @@ _SIGS = {
         [c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_int,
          c_vp],
     ),
-    "mx_gemm_roll_tail": (
-        c_int,
-        [c_int, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp,
-         c_u64, c_int, c_vp, c_vp],
-    ),
 }
 
 

@@ -867,36 +867,6 @@ def dot_cross_pair(x0: RT, y0: RT, y1: RT, roll: int, pb: PreparedCross = None, 
     return out
 
 
-def dot_pair_tail_ok(x0: RT, y0: RT) -> bool:
-    """Whether dot_pair_tail runs for these operands (nothing is launched)."""
-    d0 = x0.data
-    if (not d0.is_cuda or x0.bits != 128 or len(x0.shape) != 3 or len(y0.shape) != 3
-            or x0.shape[0] != 3 or y0.shape[0] != 3 or y0.shape[1] != x0.shape[2]):
-        return False
-    _, M, K = x0.shape
-    N = y0.shape[2]
-    return nat.lib().mx_gemm_roll_tail(_words(128), M, N, K, None, M * K, None, None, None,
-                                       None, None, 0, None, 0, 0, None, None) == 0
-
-
-def dot_pair_tail(x0: RT, y0: RT, y1: RT, slot_ptr: int, nmul: int, m: int, nonces):
-    """The fixed-point product of a stacked 3-party session in one native call: the RSS
-    cross product of the rolled pair (dot_cross_pair, roll 1) on the CRT GEMM with the
-    zero share + reshare + TruncPr (zs_trunc3_k) fused into its reconstruction -- the same
-    shares, the [3, M, N] product never written.  Call only when dot_pair_tail_ok."""
-    d0 = x0.data.contiguous()
-    b0, b1 = y0.data.contiguous(), y1.data.contiguous()
-    _, M, K = x0.shape
-    N = y0.shape[2]
-    o0, o1 = ring4((3, M, N), 128, d0.device)
-    nn = (ctypes.c_uint64 * 6)(*[v & MASK64 for v in nonces])
-    nat.check(nat.lib().mx_gemm_roll_tail(
-        _words(128), M, N, K, nat.ptr(d0), M * K, nat.ptr(b0), nat.ptr(b1), None,
-        nat.ptr(o0.data), nat.ptr(o1.data), M * N, ctypes.c_void_p(slot_ptr), nmul & MASK64,
-        int(m), nn, nat.stream_of(d0)), "gemm_roll_tail")
-    return o0, o1
-
-
 def _party_batch_strides(t: RT):
     """(party stride, batch stride) in ring elements of a [P, B, *inner] device tensor whose
     inner dims are contiguous (e.g. an expanded, stride-0 stack of one operand); None if

@@ -515,12 +515,6 @@ def dot_trunc(sess, x: RepTensor, y: RepTensor, m: int) -> RepTensor:
                 and getattr(sess, "device", None) is not None and sess.device.type == "cuda"
                 and os.environ.get("MOOSEX_DOT_TAIL", "1") != "0"):
             with span("rep.dot_trunc_fused"):
-                whole = getattr(sess, "p_dot_zs_trunc", None)
-                if whole is not None and not (ZERO_SLOTS and (x.zero_slot is not None
-                                                              or y.zero_slot is not None)):
-                    r = whole(x.plc, x, y, m)  # GEMM + tail in one native call
-                    if r is not None:
-                        return RepTensor(x.plc, x.bits, "arith", r[0], r[1])
                 v = _zero_slot_cross(sess, x, y) or sess.p_dot_cross(x.plc, x.s0, x.s1, y.s0,
                                                                         y.s1)
                 s0, s1 = tail(x.plc, v, m)  # zero share + reshare + TruncPr: one kernel

@@ -458,33 +458,6 @@ class StackedSession(Session):
         record_tail_traffic(self.stats, plc, _nbytes(r[0]) // 3)
         return PV(plc, r[0]), PV(plc, r[1])
 
-    def p_dot_zs_trunc(self, plc, x, y, m):
-        """The whole fixed-point product of the three parties in one native call on the
-        device: the rolled-pair CRT GEMM with p_zs_trunc's tail fused into its
-        reconstruction (ring.dot_pair_tail) -- the same nonces in the same order, so the
-        same shares, and the [3, M, N] product is never written.  None when it does not
-        apply (host, Z_2^64, shapes the fused kernel does not take, a right operand whose
-        prepared GEMM image is cached); nothing is drawn then."""
-        if not (self.pair_rolled and self.device.type == "cuda" and m and x.bits == 128):
-            return None
-        from moose_amd.runtime import lanes as _lanes
-
-        x0, y0, y1 = x.s0.v, y.s0.v, y.s1.v
-        if _lanes.ACTIVE or not isinstance(x0, R.RT) or not isinstance(y0, R.RT):
-            return None
-        cache = self.__dict__.get("_prepared_b") or {}
-        if (id(y0.data), id(y1.data)) in cache:  # p_dot_cross reuses its prepared image
-            return None
-        if not R.dot_pair_tail_ok(x0, y0):
-            return None
-        nmul = self.nonce(plc)
-        nonces = tuple(self.nonce(plc) for _ in range(6))
-        o0, o1 = R.dot_pair_tail(x0, y0, y1, self.key_ptr(plc, 0), nmul, m, nonces)
-        from moose_amd.parallel.party import record_tail_traffic
-
-        record_tail_traffic(self.stats, plc, _nbytes(o0) // 3)
-        return PV(plc, o0), PV(plc, o1)
-
     def party_exchange(self, plc, specs):
         """Every party is local: a per-party message is the sender's buffer."""
         return {name: t for name, _a, _b, t, _like in specs}

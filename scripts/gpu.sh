@@ -83,7 +83,7 @@ if has ladder; then
 fi
 if has ab; then
   # A/B of env configurations on the driver command (ABCFG="NAME=VAR=v,VAR2=w ...")
-  for cfg in ${ABCFG:-base=MOOSEX_CRT_TAIL=0}; do
+  for cfg in ${ABCFG:-base=MOOSEX_CRT_KERNEL=8}; do
     name=${cfg%%=*}; vars=${cfg#*=}
     for kv in ${vars//,/ }; do export "$kv"; done
     run ab_$name 300 python3 bench.py --steps 20 --warmup 5 --lr-runs 0 --zero-slot-steps 0 \

@@ -336,47 +336,3 @@ def test_gpu_crt_bench_tiling_matches_limb_gemm(variant, monkeypatch):
     same(want, got)
     assert rolled is not None
     same(want, rolled)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("M,K,N", [(512, 512, 512), (300, 320, 512), (2048, 4096, 1024),
-                                   (256, 256, 300)])
-def test_gpu_dot_trunc_fused_tail_bitwise(M, K, N):
-    """The stacked session's fixed-point product with the dot tail (zero share, reshare,
-    TruncPr) fused into the CRT reconstruction (k_crt_recon_tail3) gives bitwise the shares
-    of the unfused path (GEMM, then k_mul_trunc3 over the product) under the same seed;
-    shapes the fused kernel does not take (N % 256, K % 64) run the unfused path."""
-    from moose_amd.protocols import replicated as rep
-    from moose_amd.runtime.session import HV
-    from moose_amd.runtime.session import StackedSession
-    from moose_amd.ir.computation import ReplicatedPlacement
-
-    plc = ReplicatedPlacement(("a", "b", "c"))
-    g = torch.Generator().manual_seed(7)
-    xf = (torch.rand(M, K, generator=g, dtype=torch.float64) * 8 - 4).cuda()
-    yf = (torch.rand(K, N, generator=g, dtype=torch.float64) * 8 - 4).cuda()
-    res = {}
-    for fused in (True, False):
-        s = StackedSession("cuda:0", seed=11)
-        if not fused:
-            s.p_dot_zs_trunc = lambda *a, **k: None
-        X = rep.share(s, plc, HV("a", R.encode(xf, 23, 128)))
-        Y = rep.share(s, plc, HV("b", R.encode(yf, 23, 128)))
-        Z = rep.dot_trunc(s, X, Y, 23)
-        res[fused] = (Z.s0.v.data.cpu(), Z.s1.v.data.cpu())
-        if fused:
-            took = R.dot_pair_tail_ok(X.s0.v, Y.s0.v)
-    assert took == (N % 256 == 0 and K % 64 == 0 and M % 4 == 0)
-    assert torch.equal(res[True][0], res[False][0])
-    assert torch.equal(res[True][1], res[False][1])
-    # and the opened product is right
-    s = StackedSession("cuda:0", seed=3)
-    X = rep.share(s, plc, HV("a", R.encode(xf, 23, 128)))
-    Y = rep.share(s, plc, HV("b", R.encode(yf, 23, 128)))
-    Z = rep.dot_trunc(s, X, Y, 23)
-    d = Z.s0.v.data
-    opened = R.RT(d[0], 128)
-    for p in (1, 2):
-        opened = R.binary("add", opened, R.RT(d[p], 128))
-    got = R.decode(opened, 23).double()
-    assert (got - xf @ yf).abs().max().item() < 1e-3
