@@ -172,6 +172,9 @@ _SIGS = {
         [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_u64, c_u64, c_vp],
     ),
     "mx_crt_tables4": (c_int, [c_int, c_int, c_vp, c_vp]),
+    "mx_copy_channels": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp]),
+    "mx_stream_cumask": (c_int, [c_vp, c_int, c_vp]),
+    "mx_stream_destroy": (c_int, [c_vp]),
     "mx_gemm_roll": (
         c_int,
         [c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_int,

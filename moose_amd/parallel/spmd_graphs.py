@@ -1,0 +1,263 @@
+"""Replayed one-party-per-GPU evaluations: the SPMD tape.
+
+An SPMD evaluation (``parallel/spmd.py``: one process per party, every reshare a
+point-to-point message) of a latency-bound program -- the tutorial LR inference is 73
+message rounds of a few small kernels each -- costs per-op Python dispatch in every
+process on top of the message latency.  The reference pre-wires every operation as a
+task of a compiled host graph once per session (``execution/asynchronous.rs:456-530``);
+here an evaluation is recorded once and replayed:
+
+1. **warm-up** (eager, message plans recording): the first result; sizes every
+   workspace; records the host->device uploads (public constants) and, through the
+   transport's message plan, the header of every message;
+2. **capture** on a fresh session over a *frozen* key table: the interpreter runs the
+   program again with its kernels captured as hipGraph segments (``torch.cuda.CUDAGraph``
+   is hipGraph on ROCm) and the transport in tape mode, so every message round ends the
+   current segment and is recorded as a :class:`~moose_amd.parallel.transport.CommStep`
+   (its device buffers, peers and order) instead of being sent;
+3. **replay**: copy the new arguments into the static buffers, refresh the key table
+   (fresh keys per evaluation; the key exchange of the setup is one of the taped rounds),
+   then walk the tape -- replay a segment, issue a round (one grouped exchange, no header,
+   no Python op dispatch), replay the next segment ... -- and decode the outputs.
+
+Every process runs the same program, so every process's tape has the same rounds in the
+same order and replays pair up exactly as the eager evaluations did.  Whether to tape is
+decided collectively (an all-reduce of every rank's capture outcome): a program that one
+process cannot capture runs eagerly everywhere.
+
+Deterministic (seeded) sessions replay bitwise like a fresh eager seeded session: the
+replay re-draws the seeded keys in the order the eager setup would.
+"""
+from __future__ import annotations
+
+import os
+import time
+from typing import Dict
+from typing import Optional
+
+import numpy as np
+import torch
+
+from moose_amd.parallel.transport import CommStep
+from moose_amd.runtime import graphs as G
+from moose_amd.runtime.interpreter import Interpreter
+from moose_amd.runtime.interpreter import dtype_of_numpy
+from moose_amd.runtime.interpreter import numpy_to_torch
+from moose_amd.runtime.keys import KeyTable
+
+SEGMENT_OPS = G.SEGMENT_OPS
+
+
+class SPMDTape:
+    """One recorded SPMD evaluation of this process (module doc)."""
+
+    def __init__(self, comp, arguments: dict, identity: str, role_ranks: Dict[str, int],
+                 tr, device, storage, ring: int, seed: Optional[int] = None):
+        from moose_amd.parallel.spmd import SPMDSession
+
+        self.comp, self.device, self.tr = comp, torch.device(device), tr
+        self.identity, self.role_ranks, self.seed = identity, dict(role_ranks), seed
+        self.static = {}
+        for k, v in arguments.items():
+            if isinstance(v, (np.ndarray, np.generic)) or (
+                    isinstance(v, (list, tuple)) and v and not isinstance(v[0], (str, bytes))):
+                a = np.asarray(v)
+                t = numpy_to_torch(a, self.device)
+                t._moose_dtype = dtype_of_numpy(a)
+                self.static[k] = t
+            else:
+                self.static[k] = v
+        stream = torch.cuda.Stream(self.device)
+        # 1. warm-up: the first result, the message plan, the uploads
+        rec = G._Recorder()
+        sess = SPMDSession(identity, role_ranks, tr, device=self.device, seed=seed)
+        interp = Interpreter(sess, storage, ring)
+        with G._upload_hook(rec), torch.cuda.stream(stream):
+            outs = interp.run(comp, self.static)
+            self.first = self._decode(interp, sess, outs)
+        self.stats = sess.stats
+        torch.cuda.synchronize(self.device)
+        # 2. capture: frozen keys, transport in tape mode
+        self.keys = KeyTable(self.device, capacity=max(64, sess.keytable.n + 16))
+        self.keys.frozen = True
+        self.sess = SPMDSession(identity, role_ranks, tr, device=self.device, seed=seed)
+        self.sess.use_keytable(self.keys)
+        self.sess.key_setups = []
+        self.interp = Interpreter(self.sess, storage, ring)
+        stager = G._Stager(rec.items, self.device)
+        self.steps = []  # CUDAGraph segments and CommSteps, in program order
+        pool = torch.cuda.graph_pool_handle()
+        state = {"g": None, "n": 0}
+
+        def begin():
+            g = torch.cuda.CUDAGraph()
+            g.capture_begin(pool=pool, capture_error_mode="thread_local")
+            state["g"], state["n"] = g, 0
+
+        def end():
+            if state["g"] is not None:
+                state["g"].capture_end()
+                self.steps.append(state["g"])
+                state["g"] = None
+
+        def rotate():  # before each op: bounded segments
+            if state["g"] is None:
+                begin()
+            elif state["n"] >= SEGMENT_OPS:
+                end()
+                begin()
+            state["n"] += 1
+
+        def on_comm(step: CommStep):
+            end()
+            self.steps.append(step)
+            begin()
+
+        torch.cuda.synchronize(self.device)
+        self.interp.on_op = rotate
+        tr.tape = on_comm
+        try:
+            with G._upload_hook(stager), torch.cuda.stream(stream):
+                try:
+                    begin()
+                    self.outs = self.interp.run(comp, self.static)
+                finally:
+                    end()
+        finally:
+            tr.tape = None
+            self.interp.on_op = None
+        torch.cuda.synchronize(self.device)
+        self._stager = stager  # the staged constants stay alive with the graphs
+        self.stream = stream
+        self.rounds = sum(isinstance(s, CommStep) for s in self.steps)
+        self.segments = len(self.steps) - self.rounds
+        self.replays = 0
+        self.issue_s = []  # host time per replay spent issuing (graphs + message calls)
+
+    # ------------------------------------------------------------------------------
+    def _decode(self, interp, sess, outs) -> Dict[str, np.ndarray]:
+        res = {}
+        for tag, lv in outs.items():
+            if lv.kind == "unit" or not sess.materialized(lv.v):
+                continue
+            res[tag] = interp.to_numpy(lv)
+        return res
+
+    def _fill_keys(self):
+        """Fresh keys for this replay.  Unseeded: random slots; the taped setup rounds
+        overwrite the peers' slots with their keys.  Seeded: the draws a fresh seeded
+        session makes in its setups (SPMDSession.setup), in the same order."""
+        if self.seed is None:
+            self.keys.refresh(self.keys.n)
+            return
+        rng = torch.Generator().manual_seed(self.seed)
+        draw = lambda: bytes(torch.randint(0, 256, (16,), generator=rng,  # noqa: E731
+                                           dtype=torch.uint8).tolist())
+        for base, idx in self.sess.key_setups:
+            allk = [draw() for _ in range(4)]
+            if idx is None:
+                continue
+            allk[(idx + 2) % 3] = bytes(16)
+            self.keys._write(base, allk)
+
+    def replay(self, arguments: dict) -> Dict[str, np.ndarray]:
+        with torch.cuda.stream(self.stream):
+            for k, v in arguments.items():
+                t = self.static.get(k)
+                if isinstance(t, torch.Tensor):
+                    a = np.asarray(v)
+                    a = a.view(np.int64) if a.dtype == np.uint64 else a
+                    src = torch.from_numpy(np.ascontiguousarray(a).reshape(t.shape))
+                    t.copy_(src if src.dtype == t.dtype else src.to(t.dtype))
+            self._fill_keys()
+            issue = 0.0
+            tr = self.tr
+            staged = tr.stage
+            for s in self.steps:
+                t0 = time.perf_counter()
+                if isinstance(s, CommStep):
+                    s.run(tr)
+                    if not staged:  # a staged (gloo) round's time is host copies, not issue
+                        issue += time.perf_counter() - t0
+                else:
+                    s.replay()
+                    issue += time.perf_counter() - t0
+            self.issue_s.append(issue)
+            self.replays += 1
+            out = self._decode(self.interp, self.sess, self.outs)
+        end = getattr(tr, "end_evaluation", None)
+        if end is not None:
+            end()
+        return out
+
+
+# ------------------------------------------------------------------------------------------
+# per-process cache with a collective decision
+# ------------------------------------------------------------------------------------------
+_TAPES: Dict[tuple, object] = {}
+_SEEN: Dict[tuple, int] = {}
+MAX_TAPES = 32
+
+
+def enabled(device) -> bool:
+    return torch.device(device).type == "cuda" and os.environ.get("MOOSEX_SPMD_GRAPHS",
+                                                                   "1") != "0"
+
+
+def _agree(tr, ok: bool) -> bool:
+    """Every rank of the transport's group learns whether all of them succeeded."""
+    import torch.distributed as dist
+
+    if tr.world <= 1:
+        return ok
+    nccl = dist.get_backend(tr.group) == "nccl"
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                     device=tr.device if nccl else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=tr.group)
+    return bool(t.item())
+
+
+def evaluate(comp, arguments: dict, identity: str, role_ranks: Dict[str, int], tr, device,
+             storage, ring: int, seed: Optional[int] = None):
+    """Evaluate ``comp`` as ``identity`` through the tape cache: the first evaluation of a
+    (program, argument signature) runs eagerly, the second is captured (every rank, then a
+    collective decision) and replayed, later ones replay.  Returns ``(outputs, stats,
+    tape-or-None)``; None when the caller must run eagerly (first sight, not capturable,
+    or a failed capture on any rank)."""
+    from moose_amd.parallel.spmd import _argument_key
+    from moose_amd.parallel.spmd import _loads
+    from moose_amd.parallel.spmd import _structure_key
+
+    if not enabled(device) or not getattr(tr, "plans", False) or _loads(comp) \
+            or not G.capturable(comp):
+        return None
+    key = (tr.plan_scope, tr.rank, tr.world, id(tr.group), identity,
+           tuple(sorted(role_ranks.items())), _structure_key(comp), _argument_key(arguments),
+           G.signature(arguments), seed)
+    tape = _TAPES.get(key)
+    if tape is not None:
+        if tape is False:
+            return None
+        return tape.replay(arguments), tape.stats, tape
+    n = _SEEN.get(key, 0) + 1
+    _SEEN[key] = n
+    if n < 2:  # the eager evaluation records the message plan first
+        return None
+    tape, err = None, None
+    try:
+        tape = SPMDTape(comp, arguments, identity, role_ranks, tr, device, storage, ring, seed)
+    except Exception as e:  # noqa: BLE001 - any capture failure: eager, on every rank
+        err = e
+        try:
+            torch.cuda.synchronize(device)
+        except Exception:  # noqa: BLE001
+            pass
+    if not _agree(tr, tape is not None):
+        if os.environ.get("MOOSEX_GRAPHS_DEBUG") == "1" and err is not None:
+            raise err
+        _TAPES[key] = False
+        return None
+    if len(_TAPES) >= MAX_TAPES:
+        _TAPES.pop(next(iter(_TAPES)))
+    _TAPES[key] = tape
+    return tape.first, tape.stats, tape

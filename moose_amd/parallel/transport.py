@@ -109,6 +109,10 @@ class Transport:
         self.async_sends = backend == "nccl" or (
             backend == "gloo" and os.environ.get("MOOSEX_ASYNC_SENDS") == "1")
         self._unwaited = []  # [(work, dst)] of send-only rounds not yet known complete
+        # tape mode (parallel/spmd_graphs.py): every message round is handed to this
+        # callback as a CommStep instead of being sent -- the capture of a replayable
+        # evaluation, where no data exists yet
+        self.tape = None
 
     # -- encoding -----------------------------------------------------------------
     def _header(self, v):
@@ -256,12 +260,33 @@ class Transport:
 
     def end_evaluation(self):
         """Every send of the evaluation confirmed (or its failure raised)."""
-        self.reap(block=True)
+        if self.tape is None:
+            self.reap(block=True)
 
     def _next(self, cursors, peer):
         k = cursors.get(peer, 0)
         cursors[peer] = k + 1
         return k
+
+    # -- tape mode ----------------------------------------------------------------------
+    def _taped(self, sends, recvs):
+        """Tape mode: hand the round to the tape (parallel/spmd_graphs.py).  Sends are
+        made contiguous first (inside the capture, so the copy is replayed); receives land
+        in contiguous buffers whose copy into ``out`` is captured after the round."""
+        sends = [(t.contiguous(), dst) for t, dst in sends if t.numel()]
+        land, after = [], []
+        for out, src in recvs:
+            if out.numel() == 0:
+                continue
+            if out.is_contiguous():
+                land.append((out, src))
+            else:
+                buf = torch.empty(out.shape, dtype=out.dtype, device=out.device)
+                land.append((buf, src))
+                after.append((out, buf))
+        self.tape(CommStep(sends, land))
+        for out, buf in after:  # captured in the segment after the round
+            out.copy_(buf)
 
     # -- typed values -----------------------------------------------------------------
     def send(self, v, dst: int):
@@ -278,6 +303,11 @@ class Transport:
             if self._mode == "record":
                 self._plan.outb.setdefault(dst, []).append(h)
         if payload is not None:
+            if self.tape is not None:
+                if self._mode != "replay":
+                    raise TransportError("tape mode needs a recorded message plan")
+                self._taped([(payload.to(self.device), dst)], [])
+                return
             self._send_tensor(payload, dst)
 
     def recv(self, src: int, device=None):
@@ -296,7 +326,13 @@ class Transport:
         if shape is None:
             return scalar
         dtype = _DTYPES[h[1]]
-        data = self._recv_tensor(shape, dtype, src)
+        if self.tape is not None:
+            if kind in (K_BYTES, K_STR):
+                raise TransportError("tape mode: a host value (bytes) in the message flow")
+            data = torch.empty(shape, dtype=dtype, device=self.device)
+            self._taped([], [(data, src)])
+        else:
+            data = self._recv_tensor(shape, dtype, src)
         if device is not None:
             data = data.to(device)
         if kind == K_RT:
@@ -319,6 +355,9 @@ class Transport:
         out = torch.empty_like(t)
         if t.numel() == 0:
             return out
+        if self.tape is not None:
+            self._taped([(t, to_rank)], [(out, from_rank)])
+            return out
         st, so = (t.cpu(), torch.empty(t.shape, dtype=t.dtype)) if self.stage else (t, out)
         ops = [dist.P2POp(dist.isend, st, to_rank, group=self.group),
                dist.P2POp(dist.irecv, so, from_rank, group=self.group)]
@@ -334,6 +373,9 @@ class Transport:
         """One grouped round of header-free point-to-point messages: ``sends`` is a list of
         (tensor, dst), ``recvs`` a list of (preallocated tensor, src) whose shapes both
         sides know (protocol messages of a known element count)."""
+        if self.tape is not None:
+            self._taped(sends, recvs)
+            return
         ops, staged = [], []
         for t, dst in sends:
             t = t.contiguous()
@@ -394,6 +436,21 @@ class Transport:
         return None
 
 
+class CommStep:
+    """One message round of a taped evaluation (parallel/spmd_graphs.py): the round's
+    sends and receives with the device buffers they were recorded with, re-issued as one
+    grouped, header-free exchange at every replay."""
+
+    __slots__ = ("sends", "recvs")
+
+    def __init__(self, sends, recvs):
+        self.sends = sends
+        self.recvs = recvs
+
+    def run(self, tr: "Transport"):
+        tr.exchange(self.sends, self.recvs)
+
+
 def _parse_fault(spec, rank):
     if not spec:
         return None
@@ -430,4 +487,4 @@ def numel(shape) -> int:
     return int(math.prod(shape)) if shape else 1
 
 
-__all__ = ["Transport", "TransportError", "payload_bytes", "numel"]
+__all__ = ["Transport", "TransportError", "CommStep", "payload_bytes", "numel"]

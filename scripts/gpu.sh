@@ -150,7 +150,10 @@ if has aes; then
   run aes 600 python scripts/bench_aes_decrypt.py --n 64 --runs 5
 fi
 if has coresid; then
+  run coresid_plain 300 python3 scripts/coresidency.py --out gpurun_out/coresid_plain.json
   run coresid 300 rocprofv3 --kernel-trace --output-format csv -o run -d gpurun_out/coresid \
-    -- python3 scripts/coresidency.py
+    -- python3 scripts/coresidency.py --out gpurun_out/coresid_traced.json
+  python3 scripts/coresidency.py --summarize gpurun_out/coresid > gpurun_out/coresid_trace.json \
+    2>&1 || true
 fi
 exit 0

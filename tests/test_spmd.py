@@ -235,3 +235,74 @@ def test_spmd_lr_inference_steady_state_is_header_free():
         assert h1 == 0 and reads1 == 0, (rank, evals)
         assert r0 == r1 == rt.last_stats.rounds
     assert got[1][1][3] < 1e-3  # bob's opened probabilities
+
+
+def _tape_worker(rank, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=3)
+    from moose_amd.models.predictors.tutorial import logistic_regression_tutorial
+    from moose_amd.parallel import spmd_graphs
+    from moose_amd.parallel.spmd import SPMDSession
+    from moose_amd.parallel.transport import Transport
+    from moose_amd.runtime.interpreter import Interpreter
+    from moose_amd.runtime.local import to_native
+
+    dev = torch.device("cuda:0")
+    tm = logistic_regression_tutorial(128)
+    comp = to_native(tm.computation, 128)
+    roles = {"alice": 0, "bob": 1, "carole": 2}
+    me = ("alice", "bob", "carole")[rank]
+    tr = Transport(rank, 3, dev, plans=True)
+    rng = np.random.default_rng(0)
+    xs = [tm.x_test + rng.normal(0, 0.1, tm.x_test.shape) for _ in range(4)]
+
+    def eager(x):
+        sess = SPMDSession(me, roles, tr, dev, seed=5)
+        interp = Interpreter(sess, {}, fixedpoint_ring=128)
+        outs = interp.run(comp, {"x": x})
+        return {k: interp.to_numpy(v) for k, v in outs.items() if sess.materialized(v.v)}, sess
+
+    res = []
+    for i, x in enumerate(xs):
+        r = spmd_graphs.evaluate(comp, {"x": x}, me, roles, tr, dev, {}, 128, seed=5)
+        mode = "eager" if r is None else ("capture" if i == 1 else "replay")
+        got = eager(x)[0] if r is None else r[0]
+        want, sess = eager(x)  # a fresh seeded eager evaluation of the same input
+        same = all(np.array_equal(np.asarray(got[k]), np.asarray(want[k])) for k in want)
+        tape = r[2] if r is not None else None
+        res.append((mode, same, {k: np.asarray(v) for k, v in got.items()},
+                    None if tape is None else (tape.rounds, sess.stats.rounds,
+                                               tape.issue_s[-1] if tape.issue_s else None)))
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_spmd_tape_replay_bitwise_equal_eager():
+    """SPMD tape (parallel/spmd_graphs.py): three party processes on one GPU (gloo, staged
+    messages) evaluate the tutorial LR model four times with new inputs: eager, capture,
+    replay, replay.  Every replay's opened output equals a fresh seeded eager SPMD
+    evaluation of the same input bit for bit, and the tape holds exactly the evaluation's
+    message rounds."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_tape_worker, args=(r, port, q)) for r in range(3)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(3))
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, evals in got.items():
+        assert [m for m, *_ in evals] == ["eager", "capture", "replay", "replay"]
+        assert all(same for _, same, _, _ in evals), (rank, [s for _, s, _, _ in evals])
+        for mode, _, _, info in evals[1:]:
+            taped, eager_rounds, issue = info
+            assert taped >= eager_rounds  # every round on the tape (+ the key exchange)
+    outs = got[1][3][2]  # bob holds the opened probabilities
+    assert outs and all(np.isfinite(v).all() for v in outs.values())
+    issue = [e[3][2] for e in got[0][2:]]
+    print(f"tape rounds {got[0][3][3][0]}, host issue per replay (rank 0) "
+          f"{[round(i * 1e3, 3) for i in issue]} ms")
