@@ -32,6 +32,7 @@ from __future__ import annotations
 
 import os
 import time
+import warnings
 from typing import Dict
 from typing import Optional
 
@@ -96,8 +97,11 @@ class SPMDTape:
 
         def end():
             if state["g"] is not None:
-                state["g"].capture_end()
-                self.steps.append(state["g"])
+                with warnings.catch_warnings():  # a segment between two rounds may be empty
+                    warnings.filterwarnings("ignore", message="The CUDA Graph is empty")
+                    state["g"].capture_end()
+                if state["n"]:
+                    self.steps.append(state["g"])
                 state["g"] = None
 
         def rotate():  # before each op: bounded segments
@@ -109,6 +113,7 @@ class SPMDTape:
             state["n"] += 1
 
         def on_comm(step: CommStep):
+            state["n"] += 1  # the segment holds the round's send copies, if any
             end()
             self.steps.append(step)
             begin()

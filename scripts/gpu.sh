@@ -11,6 +11,7 @@
 #   lrinf     LR-inference p50 + kernel profile dots/graphs  the dot-product sweeps
 #   logreg    logistic-regression training sweep            aes  AES-in-MPC decrypt
 #   coresid   GEMM + concurrent copy kernel co-residency trace
+#   cycprof   rocprofv3 kernel stats of the cyclic layout's per-GPU path (one GPU)
 #   ladder    the bench fallback ladder with a rank stalled in attempt 0 (one GPU, 3 ranks)
 #   ab        driver command under env configurations ABCFG="name=VAR=v,VAR2=w ..." (ABPROF=1:
 #             plus a rocprofv3 kernel-stats pass each)      gemmtest  the CRT GEMM GPU tests
@@ -68,6 +69,12 @@ if has cyclic; then
     run cyc_s$s 300 python bench.py --layout cyclic --steps 10 --warmup 3 --step-streams $s \
       --lr-runs 0 && summary gpurun_out/cyc_s$s.log
   done
+fi
+if has cycprof; then
+  run cycprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/cycprof -o run \
+    --output-format csv -- python3 bench.py --layout cyclic --steps 10 --warmup 3 --lr-runs 0
+  python3 scripts/prof_summary.py gpurun_out/cycprof/run_kernel_stats.csv \
+    "cyclic layout per-GPU path (1 GPU)" > gpurun_out/cycprof_summary.md 2>&1 || true
 fi
 if has shared; then
   for N in ${NS:-3 8}; do
