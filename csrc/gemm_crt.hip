@@ -316,85 +316,6 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// A' prep through LDS (the A side of k_crt_prep, same image): a workgroup stages one
-// k-step of 16 image rows -- 16 rows x 64 elements -- with fully coalesced loads (every wave
-// instruction reads 64 consecutive elements of one row, where k_crt_prep's lanes each read
-// a 16-byte element 256 bytes from their neighbour's), then thread (row r, 16-byte chunk c,
-// moduli quarter mg) turns its 16 elements into residues.  Elements sit in LDS at
-// lds_a(r, k): row-major with the 16-element groups rotated by 4 (r & 3) + (k >> 4), so the
-// staging stores and the residue loads (lanes = 4 rows x 4 chunks per 16-lane group) both
-// hit 16 distinct 16-byte bank slots.
-__device__ __forceinline__ int lds_a(int r, int k) {
-  return r * BK + (k & 48) + ((k + 4 * (r & 3) + (k >> 4)) & 15);
-}
-
-template <class T>
-__global__ void __launch_bounds__(256)
-    k_crt_prep_a(const T* __restrict__ X0, const T* __restrict__ X1, int64_t R, int64_t K,
-                 int64_t xs, int mode, int8_t* __restrict__ out, int64_t tiles, int64_t nkb,
-                 const PrepTab tab) {
-  constexpr int NW = Words<T>::N;
-  __shared__ T st[16 * BK];
-  const int64_t b = blockIdx.y;
-  const T* x0 = X0 + b * xs;
-  const T* x1 = mode ? X1 + b * xs : x0;
-  const int n = tab.n;
-  const int64_t plane = tiles * nkb * (int64_t)(BM * BK);
-  int8_t* ob = out + b * n * plane;
-  const int64_t units = tiles * nkb * (BM / 16);
-  const int tid = (int)threadIdx.x;
-  const int task = tid & 63, mg = tid >> 6;  // mg: uniform per wave
-  const int r = task >> 2, c = task & 3;
-  const int per = (n + 3) / 4;
-  const int i0 = mg * per, i1 = min(n, i0 + per);
-  for (int64_t u = blockIdx.x; u < units; u += gridDim.x) {
-    const int rb = (int)(u % (BM / 16));
-    const int64_t q = u / (BM / 16);
-    const int64_t kb = q % nkb, t = q / nkb;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = i * 256 + tid;
-      const int rr = e >> 6, kk = e & (BK - 1);
-      const int64_t row = t * BM + rb * 16 + rr;
-      const int64_t k = kb * BK + kk;
-      T v = 0;
-      if (row < R) {
-        if (k < K) v = x0[row * K + k];
-        else if (mode && k < 2 * K) v = x1[row * K + (k - K)];
-      }
-      st[lds_a(rr, kk)] = v;
-    }
-    __syncthreads();
-    uint32_t v[16][NW];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const T e = st[lds_a(r, c * 16 + j)];
-#pragma unroll
-      for (int w = 0; w < NW; ++w) v[j][w] = (uint32_t)(e >> (32 * w));
-    }
-    int8_t* base = ob + (t * nkb + kb) * (int64_t)(BM * BK) + img_off(rb * 16 + r, c);
-    for (int i = i0; i < i1; ++i) {
-      int rr[16];
-      if (i == 0) {  // p = 256: the low byte (times the folded inverse)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) rr[j] = (int)(v[j][0] * tab.mul0);
-      } else {
-        const uint32_t w[4] = {tab.w[i][0], tab.w[i][1], tab.w[i][2], tab.w[i][3]};
-        const uint32_t neg = tab.neg[i];
-        const float p = (float)tab.p[i], rcp = tab.rcp[i];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) rr[j] = residue<NW>(v[j], w, neg, p, rcp);
-      }
-      v4i o;
-#pragma unroll
-      for (int u4 = 0; u4 < 4; ++u4)
-        o[u4] = (int)pack4(rr[4 * u4], rr[4 * u4 + 1], rr[4 * u4 + 2], rr[4 * u4 + 3]);
-      *(v4i*)(base + i * plane) = o;
-    }
-    __syncthreads();  // the next unit reuses the LDS
-  }
-}
-
 // XCD-aware remap (as gemm_mfma.hip): consecutive tile ids land on one XCD
 __device__ inline int64_t xcd_remap(int64_t bid, int64_t nwg) {
   const int64_t q = nwg / 8, r = nwg % 8;
@@ -1115,14 +1036,6 @@ int gemm_group_m() {
   return v >= 1 && v <= 64 ? v : 4;
 }
 
-int prep_a_lds() {  // MOOSEX_CRT_PREP_A=0: the one-pass A' prep (k_crt_prep)
-  static const int v = [] {
-    const char* e = std::getenv("MOOSEX_CRT_PREP_A");
-    return e && e[0] == '0' ? 0 : 1;
-  }();
-  return v;
-}
-
 template <class T>
 void launch_prep(const CPlan& p, const Tables& tb, bool is_b, int64_t batch, int64_t R,
                  int64_t K, int64_t xs, const T* X0, const T* X1, int mode, int8_t* out,
@@ -1132,12 +1045,7 @@ void launch_prep(const CPlan& p, const Tables& tb, bool is_b, int64_t batch, int
   const int rows = is_b ? p.bn : BM;
   const int64_t work = tiles * nkb * (rows * 4);
   const dim3 grid((unsigned)std::min<int64_t>((work + 255) / 256, 16384), (unsigned)batch);
-  if (!is_b && prep_a_lds()) {
-    const int64_t units = tiles * nkb * (BM / 16);
-    hipLaunchKernelGGL(k_crt_prep_a<T>, dim3((unsigned)std::min<int64_t>(units, 16384),
-                                             (unsigned)batch),
-                       dim3(256), 0, st, X0, X1, R, K, xs, mode, out, tiles, nkb, tb.pa);
-  } else if (!is_b)
+  if (!is_b)
     hipLaunchKernelGGL((k_crt_prep<T, false, BM>), grid, dim3(256), 0, st, X0, X1, R, K, xs, mode,
                        out, tiles, nkb, tb.pa);
   else if (rows == 256)
