@@ -384,6 +384,11 @@ class CyclicSession(StackedSession):
             return PV(plc, R.rss_cross(kind, x0.v, x1v, y0.v, y1v, None, nonce, 3))
         return PV(plc, R.rss_cross_kp(kind, x0.v, x1v, y0.v, y1v, self._pair_ptrs(plc), nonce))
 
+    def p_cross_plain(self, kind, plc, x0, x1, y0, y1):
+        """The components' cross terms with no zero share and no nonce drawn (the per-party
+        tail adds the zero share)."""
+        return PV(plc, R.rss_cross(kind, x0.v, x1.v, y0.v, y1.v, None, 0, 3))
+
     def p_add_zero_share(self, plc, z, kind="arith"):
         return PV(plc, R.rss_cross_kp(kind, z.v, None, None, None, self._pair_ptrs(plc),
                                       self.nonce(plc)))

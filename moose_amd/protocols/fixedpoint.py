@@ -379,14 +379,16 @@ def _normalize(sess, x: RepFixed):
 # ---------------------------------------------------------------------------
 # polynomials (log-depth power tree, public coefficients)
 # ---------------------------------------------------------------------------
-def poly_eval(sess, x: RepFixed, coeffs) -> RepFixed:
-    """sum_k c_k x^k.  The powers stay stacked on a leading axis P = [x, x^2, ...]: level
-    by level x^(h+1..h+m) = x^h * P[0:m] is ONE stacked multiplication (depth
-    ceil(log2 n) rounds), and the sum is one public weighted sum over P + one TruncPr."""
+def poly_eval(sess, x: RepFixed, coeffs, shift: int = 0) -> RepFixed:
+    """sum_k c_k x^k (divided by 2^shift: the final TruncPr drops ``shift`` more bits, so
+    a halving of the result costs no extra round).  The powers stay stacked on a leading
+    axis P = [x, x^2, ...]: level by level x^(h+1..h+m) = x^h * P[0:m] is ONE stacked
+    multiplication (depth ceil(log2 n) rounds), and the sum is one public weighted sum over
+    P + one TruncPr."""
     n = len(coeffs) - 1
     f, bits = x.frac, x.bits
     if n > 1 and _rows_ok(sess, x):
-        return _poly_eval_rows(sess, x, coeffs)
+        return _poly_eval_rows(sess, x, coeffs, shift)
     P = local(sess, x, "ExpandDims", axis=[0])
     have = 1
     while have < n:
@@ -398,8 +400,8 @@ def poly_eval(sess, x: RepFixed, coeffs) -> RepFixed:
         P = concat(sess, [P, mul(sess, left, right)], 0)
         have += m
     acc = _weighted(sess, P.t, [int(round(c * (1 << f))) for c in coeffs[1:]], bits)
-    acc = rep.trunc_pr(sess, acc, f)
-    return add_const(sess, RepFixed(acc, f, x.integ), coeffs[0])
+    acc = rep.trunc_pr(sess, acc, f + shift)
+    return add_const(sess, RepFixed(acc, f, x.integ), coeffs[0] / (1 << shift))
 
 
 def _rows_ok(sess, x) -> bool:
@@ -408,7 +410,7 @@ def _rows_ok(sess, x) -> bool:
             and getattr(sess, "device", None) is not None and sess.device.type == "cuda")
 
 
-def _poly_eval_rows(sess, x: RepFixed, coeffs) -> RepFixed:
+def _poly_eval_rows(sess, x: RepFixed, coeffs, shift: int = 0) -> RepFixed:
     """poly_eval with the powers stack P preallocated: each level's multiplication reads
     x^h (a broadcast row) and P[0:m] (a slice) in place and its truncated product is
     written into rows h..h+m-1 -- the same protocol calls (and shares) as the generic
@@ -433,8 +435,8 @@ def _poly_eval_rows(sess, x: RepFixed, coeffs) -> RepFixed:
         have += m
     P = RepTensor(t.plc, bits, t.kind, P0, P1)
     acc = _weighted(sess, P, [int(round(c * (1 << f))) for c in coeffs[1:]], bits)
-    acc = rep.trunc_pr(sess, acc, f)
-    return add_const(sess, RepFixed(acc, f, x.integ), coeffs[0])
+    acc = rep.trunc_pr(sess, acc, f + shift)
+    return add_const(sess, RepFixed(acc, f, x.integ), coeffs[0] / (1 << shift))
 
 
 def _batched_mul(sess, xs, ys):
@@ -540,6 +542,11 @@ def _exp2_parts(sess, a: RepFixed, negative: bool):
     npad = 1 << (nint - 1).bit_length()
     if f + npad > bits:
         npad = nint
+    # parties on different processes (rounds cost messages): the polynomial and the
+    # product tree advance together (_merged_exp_tail)
+    merged = (negative and not getattr(sess, "is_simulated", True)
+              and getattr(sess, "party_dot_trunc", None) is not None
+              and hasattr(sess, "p_cross_plain") and npad >= 2 and npad & (npad - 1) == 0)
     bd = rep.bit_decompose(sess, a.t)
     planes = RepTensor(a.plc, 1, "bool", sess.p("BitSplit", a.plc, bd.s0, start=0, count=f + npad),
                        sess.p("BitSplit", a.plc, bd.s1, start=0, count=f + npad))
@@ -549,7 +556,8 @@ def _exp2_parts(sess, a: RepFixed, negative: bool):
     if negative:
         # 2^-r for r in [0,1) = 2^(1-r) / 2 -> fit exp2 on [0, 1] of (1 - r)
         one_minus = const_sub(sess, 1.0, r)
-        p = mul_const(sess, poly_eval(sess, one_minus, _fit("exp2", 0.0, 1.0, 7)), 0.5)
+        p = None if merged else poly_eval(sess, one_minus, _fit("exp2", 0.0, 1.0, 7),
+                                          shift=1)
     else:
         p = poly_eval(sess, r, _fit("exp2", 0.0, 1.0, 7))
     # integer part factors 1 + b_j (c_j - 1), c_j = 2^(+-2^j), for all j at once: the
@@ -569,6 +577,10 @@ def _exp2_parts(sess, a: RepFixed, negative: bool):
     fac = RepTensor(ints.plc, bits, "arith", sess.p("MulLeading", ints.plc, ints.s0, pc),
                     sess.p("MulLeading", ints.plc, ints.s1, pc))
     fac = rep.add_public(sess, fac, _encode_const(sess, 1.0, f, bits))
+    if merged:
+        # parties on different processes: the polynomial's levels and the product tree's
+        # levels are independent -- each round carries both (module doc: _merged_exp_tail)
+        return _merged_exp_tail(sess, one_minus, fac, npad)
     # log-depth product over the leading axis: one stacked multiplication per level
     F, n = RepFixed(fac, f, integ), npad
     views = _rows_ok(sess, F)
@@ -587,6 +599,82 @@ def _exp2_parts(sess, a: RepFixed, negative: bool):
             sess, [prod, local(sess, F, "Slice", slice=(2 * h, n, None))], 0)
         n = (n + 1) // 2
     return mul(sess, p, local(sess, F, "IndexAxis", axis=0, index=0))
+
+
+def _tail_trunc(sess, plc, v, bits, m) -> RepTensor:
+    """Zero share + reshare + TruncPr(m) of local 3-out-of-3 additive products ``v`` (a
+    party vector): the dot's tail (parallel/party.py); 2 rounds."""
+    nonces = tuple(sess.nonce(plc) for _ in range(7))
+    s0, s1 = sess.party_dot_trunc(plc, v, m, nonces)
+    return RepTensor(plc, bits, "arith", s0, s1)
+
+
+def _merged_exp_tail(sess, x: RepFixed, fac: RepTensor, npad: int) -> RepFixed:
+    """2^-a = p(1 - r) / 2 * prod(factors) with the polynomial p (degree 7) and the
+    product tree over the ``npad`` integer-bit factors evaluated TOGETHER: every round's
+    messages carry one level of each -- the level's products are ONE batched tail (local
+    cross terms concatenated on the stacking axis, one zero share + reshare + TruncPr) --
+    and the polynomial's final TruncPr (its terms' additive shares) rides with a tree level
+    too.  For the tutorial LR (fixed(24,40): 32 factors) 20 rounds become 12; the values
+    are those of poly_eval + the tree up to TruncPr's probabilistic rounding."""
+    coeffs = _fit("exp2", 0.0, 1.0, 7)
+    f, bits, t = x.frac, x.bits, x.t
+    plc = t.plc
+    n = len(coeffs) - 1
+    ex = lambda v: local(sess, v, "ExpandDims", axis=[0])  # noqa: E731
+
+    def sl(v, a, b):
+        return local(sess, v, "Slice", slice=(a, b, None))
+
+    def run(pairs, truncs=()):
+        """One round: the products of ``pairs`` (stacked operands) and the TruncPr of the
+        first-share vectors ``truncs``, as one tail; returns the pieces in order."""
+        parts, sizes = [], []
+        for a, b in pairs:
+            parts.append(sess.p_cross_plain("arith", plc, a.s0, a.s1, b.s0, b.s1))
+            sizes.append(sess.p_shape(a.s0)[0])
+        for v in truncs:
+            parts.append(v)
+            sizes.append(sess.p_shape(v)[0])
+        v = parts[0] if len(parts) == 1 else sess.p("Concat", plc, *parts, axis=0)
+        out = _tail_trunc(sess, plc, v, bits, f)
+        res, at = [], 0
+        for k in sizes:
+            res.append(out if len(sizes) == 1 else sl(out, at, at + k))
+            at += k
+        return res
+
+    P = ex(t)          # powers of x, stacked: [x, x^2, ...]
+    F = fac            # tree factors, stacked
+    have, nf = 1, npad
+    while have < n:  # one polynomial level + one tree level per round
+        m = min(2 * have, n) - have
+        xh = sl(P, have - 1, have)
+        left = xh if m == 1 else concat(sess, [xh] * m, 0)
+        right = P if m == have else sl(P, 0, m)
+        pairs = [(left, right)]
+        if nf > 1:
+            pairs.append((sl(F, 0, nf // 2), sl(F, nf // 2, nf)))
+        got = run(pairs)
+        P = concat(sess, [P, got[0]], 0)
+        if nf > 1:
+            F, nf = got[1], nf // 2
+        have += m
+    # the polynomial's weighted sum (local) and its TruncPr ride with the next tree level
+    acc = _weighted(sess, P, [int(round(c * (1 << f))) for c in coeffs[1:]], bits)
+    acc_v = ex(acc).s0  # party p's first share: a 3-out-of-3 additive sharing of acc
+    if nf > 1:
+        F, acc_t = run([(sl(F, 0, nf // 2), sl(F, nf // 2, nf))], [acc_v])
+        nf //= 2
+    else:
+        acc_t = run([], [acc_v])[0]
+    p = add_const(sess, RepFixed(local(sess, acc_t, "IndexAxis", axis=0, index=0), f, x.integ),
+                  coeffs[0])
+    while nf > 1:
+        F, nf = run([(sl(F, 0, nf // 2), sl(F, nf // 2, nf))])[0], nf // 2
+    # 2^-a = p(1 - r) / 2 * prod: the halving is one more bit of the last TruncPr
+    return mul(sess, p, RepFixed(local(sess, F, "IndexAxis", axis=0, index=0), f, x.integ),
+               f=f + 1)
 
 
 def exp2(sess, x: RepFixed) -> RepFixed:
@@ -614,10 +702,13 @@ def sigmoid(sess, x: RepFixed) -> RepFixed:
     ax = _with(x, rep.lincomb(sess, [(1, x.t), (-2, rep.mul(sess, s, x.t))]))
     e = exp_nonpositive(sess, neg(sess, ax))
     d = add_const(sess, e, 1.0)  # in [1, 2]
-    half = mul_const(sess, d, 0.5)  # in [0.5, 1]
-    w = poly_eval(sess, half, _fit("recip", 0.5, 1.0, 4))
-    w = _newton_recip(sess, half, w, 1)
-    pos = mul_const(sess, w, 0.5)  # 1/d
+    # 1/d = (1/h) / 2 with h = d / 2 in [0.5, 1]: the fit of 1/h evaluated at d directly
+    # (coefficients c_k / 2^k), and both halvings folded into TruncPrs of one more bit --
+    # no round spent on multiplying by 0.5
+    w = poly_eval(sess, d, tuple(c / (1 << k)
+                                 for k, c in enumerate(_fit("recip", 0.5, 1.0, 4))))  # ~ 1/h
+    hw = mul(sess, d, w, f=d.frac + 1)  # h w
+    pos = mul(sess, w, const_sub(sess, 2.0, hw), f=w.frac + 1)  # one Newton step, halved
     one_minus = const_sub(sess, 1.0, pos)
     return _with(pos, rep.mux(sess, s, one_minus.t, pos.t))
 

@@ -394,6 +394,18 @@ def mul_trunc(sess, x: RepTensor, y: RepTensor, m: int, out=None) -> RepTensor:
         r = f(x.plc, x.s0, x.s1, y.s0, y.s1, m, out=out)
         if r is not None:
             return RepTensor(x.plc, x.bits, "arith", r[0], r[1])
+    party = getattr(sess, "party_dot_trunc", None)
+    plain = getattr(sess, "p_cross_plain", None)
+    if (party is not None and plain is not None and 0 < m <= 63 and x.kind == "arith"
+            and x.bits in (64, 128) and os.environ.get("MOOSEX_DOT_TAIL", "1") != "0"):
+        # the dot's per-party tail (parallel/party.py) on the elementwise cross products:
+        # the reshare folded into TruncPr's first round -- 2 rounds instead of 3, the same
+        # nonces in the same order as the fused stacked kernel (same shares)
+        with span("rep.mul_trunc_party"):
+            nonces = tuple(sess.nonce(x.plc) for _ in range(7))
+            v = plain("arith", x.plc, x.s0, x.s1, y.s0, y.s1)
+            s0, s1 = party(x.plc, v, m, nonces, out=(out[0], out[1]) if out else None)
+            return RepTensor(x.plc, x.bits, "arith", s0, s1)
     return trunc_pr(sess, mul(sess, x, y), m, out=out)
 
 

@@ -436,10 +436,16 @@ class StackedSession(Session):
         r = R.mul_trunc3_k(*v, self.key_ptr(plc, 0), nmul, m, nonces, out=outs)
         if r is None:  # cannot happen after the checks above; keep the protocol honest
             raise RuntimeError("mul_trunc3 declined after its checks")
-        nbytes = _nbytes(r[0])
-        self.stats.record_round(nbytes)
-        self._trunc_traffic(x0, nbytes // 3)
+        from moose_amd.parallel.party import record_tail_traffic
+
+        # the messages of the per-party protocol (reshare folded into TruncPr, 2 rounds)
+        record_tail_traffic(self.stats, plc, _nbytes(r[0]) // 3)
         return PV(plc, r[0]), PV(plc, r[1])
+
+    def p_cross_plain(self, kind, plc, x0, x1, y0, y1):
+        """The parties' cross terms with no zero share and no nonce drawn (the per-party
+        tail, rep.mul_trunc on the host, adds the zero share)."""
+        return PV(plc, R.rss_cross(kind, x0.v, x1.v, y0.v, y1.v, None, 0, 3))
 
     def p_zs_trunc(self, plc, z, m):
         """The tail of a fixed-point dot in one kernel (device): rep.dot's zero share and

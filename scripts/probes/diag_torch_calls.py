@@ -9,7 +9,7 @@ import numpy as np
 import torch
 from torch.overrides import TorchFunctionMode
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 WATCH = {"roll", "stack", "clone", "contiguous", "cat", "zeros", "zeros_like", "empty_like",
          "copy_", "to", "__setitem__", "expand", "where", "full", "__and__", "__xor__",
@@ -49,7 +49,7 @@ def main():
                                         np.array([-lg.intercept_[0], lg.intercept_[0]]),
                                         predictors.PostTransform.SIGMOID)
     comp = model.predictor_factory(predictors.DEFAULT_FIXED_DTYPE)
-    rt = LocalMooseRuntime(["alice", "bob", "carole"], device=dev)
+    rt = LocalMooseRuntime(["alice", "bob", "carole"], device=dev, use_graphs=False)
     for _ in range(2):
         rt.evaluate_computation(comp, {"x": X[800:]})
     c = Count()

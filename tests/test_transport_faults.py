@@ -33,8 +33,8 @@ def _free_port():
 
 def _sender_worker(rank, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MOOSEX_ASYNC_SENDS="1")
-    # the receiver (rank 0) dies at its first grouped exchange, before posting its receive
-    os.environ["MOOSEX_FAULT"] = "exit:1@0"
+    # the receiver (rank 0) dies at its second grouped exchange, before posting its receive
+    os.environ["MOOSEX_FAULT"] = "exit:2@0"
     import datetime
 
     dist.init_process_group("gloo", rank=rank, world_size=2,
@@ -44,17 +44,22 @@ def _sender_worker(rank, port, q):
 
     tr = Transport(rank, 2, "cpu")
     if rank == 0:
-        tr.exchange([], [(torch.empty(1000), 1)])  # exits inside
+        tr.exchange([], [])  # round 1: nothing
+        dist.barrier()  # rank 1's send is in flight now
+        tr.exchange([], [(torch.empty(1000), 1)])  # round 2: dies before receiving
         q.put((0, "not reached"))
         return
     tr.exchange([(torch.ones(1000), 0)], [])  # send-only round: returns at once
     assert len(tr._unwaited) == 1
+    dist.barrier()
     time.sleep(2.0)
     try:
         tr.end_evaluation()
         q.put((1, "no error"))
     except TransportError as e:
         q.put((1, f"TransportError: {e}"))
+    q.close()
+    q.join_thread()  # the queue's feeder thread delivers before the hard exit
     os._exit(0)
 
 
