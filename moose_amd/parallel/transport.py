@@ -54,7 +54,7 @@ class TransportError(errors.Networking):
 # instead of desynchronising its peer.  Least-recently-used first out, so a long-lived
 # worker that sees many argument shapes keeps a bounded table.
 _PLANS: "collections.OrderedDict" = collections.OrderedDict()
-PLAN_CACHE = int(os.environ.get("MOOSEX_PLAN_CACHE", "256"))
+PLAN_CACHE = int(os.environ.get("MOOSEX_MSG_PLANS", "256"))
 # send-only rounds in flight per transport before the oldest is waited for
 MAX_UNWAITED = 64
 

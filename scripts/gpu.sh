@@ -9,6 +9,7 @@
 #   shared    multi-rank rehearsal on one GPU (NS="3 8", SIZE=4096: every rank on cuda:0, gloo)
 #   variants  CRT GEMM variants (VARS="8 16")    pmc       CRT GEMM PMC passes (VARS)
 #   lrinf     LR-inference p50 + kernel profile dots/graphs  the dot-product sweeps
+#   calls     torch calls by moose_amd call site in one eager LR inference
 #   logreg    logistic-regression training sweep            aes  AES-in-MPC decrypt
 #   coresid   GEMM + concurrent copy kernel co-residency trace
 #   cycprof   rocprofv3 kernel stats of the cyclic layout's per-GPU path (one GPU)
@@ -136,6 +137,9 @@ if has lrinf; then
   run lrinf_g 600 python scripts/bench_lr_inference.py --runs 50 --graphs
   run lrinf_prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/lrinf_prof -o run \
     --output-format csv -- python scripts/bench_lr_inference.py --runs 5 --warmup 1
+fi
+if has calls; then  # torch calls by call site in one eager LR inference (the ATen copies)
+  run calls 300 python scripts/probes/diag_torch_calls.py
 fi
 if has dots; then
   rm -f gpurun_out/dots.jsonl

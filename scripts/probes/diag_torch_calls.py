@@ -27,11 +27,13 @@ class Count(TorchFunctionMode):
         if name == "contiguous" and args and args[0].is_contiguous():
             name = None  # no copy
         if name in WATCH:
-            st = [f for f in traceback.extract_stack(limit=14) if "moose_amd" in f.filename]
+            st = [f for f in traceback.extract_stack(limit=30) if "moose_amd" in f.filename]
             if st:
-                f = st[-1]
-                self.where[(name, f.filename.split("moose_amd/")[-1] + ":" + str(f.lineno)
-                            + " " + f.name)] += 1
+                # the kernel's site plus the protocol frames that asked for it
+                outer = [f for f in st[:-1] if "protocols/" in f.filename][-2:]
+                self.where[(name,) + tuple(
+                    f.filename.split("moose_amd/")[-1] + ":" + str(f.lineno) + " " + f.name
+                    for f in outer + [st[-1]])] += 1
         return func(*args, **(kwargs or {}))
 
 
