@@ -1,4 +1,6 @@
-"""``LocalMooseRuntime``: all identities simulated in one process on one device.
+"""``LocalMooseRuntime``: all identities simulated in one process on one device -- or,
+with ``device_map={identity: device}``, every identity a thread of this process on its
+own GPU, exchanging device-to-device copies (parallel/threads.py).
 
 With ``use_graphs=True`` (or ``MOOSEX_GRAPHS=1``) repeated evaluations of the same
 computation and argument signature replay a captured hipGraph (runtime/graphs.py).
@@ -69,6 +71,8 @@ class LocalMooseRuntime:
         seed: Optional[int] = None,
         use_graphs: Optional[bool] = None,
         lanes: Optional[int] = None,
+        device_map: Optional[Dict[str, str]] = None,
+        timeout: Optional[float] = None,
     ):
         identities = [getattr(i, "name", i) for i in identities]
         storage_mapping = dict(storage_mapping or {})
@@ -101,6 +105,17 @@ class LocalMooseRuntime:
 
         self._graphs = GraphCache()
         self._native_cache = {}
+        # parties as threads, each on its own device (parallel/threads.py): {identity:
+        # device}; identities not named run on ``device``
+        self.device_map = None
+        if device_map:
+            unknown = set(device_map) - set(identities)
+            if unknown:
+                raise ValueError(f"`device_map` names unknown identities {sorted(unknown)}")
+            self.device_map = {i: torch.device(device_map.get(i, self.device))
+                               for i in identities}
+        self.timeout = timeout
+        self.last_stats_by_identity = None
 
     def set_default(self):
         from moose_amd.edsl.base import set_current_runtime
@@ -135,6 +150,15 @@ class LocalMooseRuntime:
     def evaluate_compiled(self, comp, arguments=None):
         comp = to_native(comp, self.fixedpoint_ring)
         arguments = dict(arguments or {})
+        if self.device_map is not None:
+            from moose_amd.parallel.threads import run_parties
+
+            result, stats, self.last_timings = run_parties(
+                comp, arguments, self.identities, [self.device_map[i] for i in self.identities],
+                self.storage, self.fixedpoint_ring, self.seed, timeout=self.timeout)
+            self.last_stats_by_identity = stats
+            self.last_stats = stats.get(self.identities[0])
+            return result
         if _is_lowered(comp):
             from moose_amd.runtime.graph_executor import GraphExecutor
 

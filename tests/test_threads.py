@@ -1,0 +1,128 @@
+"""Parties as threads of one process, each on its own device (``LocalMooseRuntime(...,
+device_map=...)``, parallel/threads.py; VERDICT r3 "what's missing" 5: single-process
+multi-GPU LocalMooseRuntime).  CPU: every party on the host; GPU: every party on its own
+HIP stream of cuda:0, and on three GPUs when the box has them."""
+import numpy as np
+import pytest
+import torch
+
+import moose_amd as pm
+from moose_amd.runtime.local import LocalMooseRuntime
+
+from test_spmd import _args
+from test_spmd import _comp
+
+IDS = ["alice", "bob", "carole"]
+
+
+def _check_against_stacked(dev_map, outsider=False):
+    comp = _comp(outsider)
+    idents = IDS + (["dave"] if outsider else [])
+    args = _args()
+    want = LocalMooseRuntime(idents, device="cpu").evaluate_computation(comp, args)
+    rt = LocalMooseRuntime(idents, device_map={i: dev_map(k) for k, i in enumerate(idents)},
+                           timeout=300)
+    got = rt.evaluate_computation(comp, args)
+    assert set(got) == set(want)
+    for k in want:
+        np.testing.assert_allclose(np.asarray(got[k], dtype=np.float64),
+                                   np.asarray(want[k], dtype=np.float64), atol=2e-4)
+    assert set(rt.last_timings) == set(idents)
+    assert rt.last_stats.rounds > 0
+    return rt
+
+
+@pytest.mark.parametrize("outsider", [False, True])
+def test_thread_parties_match_stacked_cpu(outsider):
+    _check_against_stacked(lambda k: "cpu", outsider)
+
+
+def test_thread_parties_lr_inference_rounds_cpu():
+    """The tutorial LR inference with the parties as threads: the per-party protocol's
+    round count (scripts/lr_rounds.py --layout party) and the model's probabilities."""
+    from moose_amd.models.predictors.tutorial import logistic_regression_tutorial
+
+    tm = logistic_regression_tutorial(128)
+    rt = LocalMooseRuntime(IDS, device_map={i: "cpu" for i in IDS}, timeout=300)
+    for _ in range(2):
+        got = list(rt.evaluate_computation(tm.computation, {"x": tm.x_test}).values())[0]
+        assert np.abs(got - tm.proba).max() < 1e-3
+    rounds = {i: s.rounds for i, s in rt.last_stats_by_identity.items()}
+    assert len(set(rounds.values())) == 1 and rounds["alice"] <= 46, rounds
+
+
+def test_thread_parties_lowered_graph_cpu():
+    from moose_amd.compiler import passes
+
+    comp = _comp(False)
+    args = _args()
+    want = LocalMooseRuntime(IDS, device="cpu").evaluate_computation(comp, args)
+    rt = LocalMooseRuntime(IDS, device_map={i: "cpu" for i in IDS}, timeout=300)
+    got = rt.evaluate_computation(comp, args, compiler_passes=passes.DEFAULT_PASSES)
+    assert set(got) == set(want)
+    for k in want:
+        np.testing.assert_allclose(np.asarray(got[k], dtype=np.float64),
+                                   np.asarray(want[k], dtype=np.float64), atol=1e-5)
+
+
+def test_thread_party_failure_raises_instead_of_hanging():
+    """One party fails (a Load of a key only its storage lacks); the others are blocked on
+    its messages and must raise too, so the evaluation ends with the cause."""
+    alice, bob, carole = (pm.host_placement(n) for n in IDS)
+    rep = pm.replicated_placement("rep", players=[alice, bob, carole])
+
+    @pm.computation
+    def g():
+        with bob:
+            x = pm.load("x", dtype=pm.float64)
+            xf = pm.cast(x, dtype=pm.fixed(14, 23))
+        with rep:
+            y = pm.mul(xf, xf)
+        with carole:
+            return pm.cast(y, dtype=pm.float64)
+
+    rt = LocalMooseRuntime(IDS, device_map={i: "cpu" for i in IDS}, timeout=60)
+    with pytest.raises(Exception) as ei:
+        rt.evaluate_computation(g, {})
+    assert "x" in str(ei.value) and "TransportError" not in type(ei.value).__name__
+    rt.write_value_to_storage("bob", "x", np.array([1.5, -2.0]))
+    out = list(rt.evaluate_computation(g, {}).values())[0]
+    np.testing.assert_allclose(out, [2.25, 4.0], atol=1e-5)
+
+
+def test_device_map_rejects_unknown_identity():
+    with pytest.raises(ValueError):
+        LocalMooseRuntime(IDS, device_map={"mallory": "cpu"})
+
+
+@pytest.mark.gpu
+def test_thread_parties_on_gpu_streams():
+    """Every party on its own HIP stream of cuda:0 (the one-GPU box), then one party per GPU
+    when three are visible: results equal the stacked session's within TruncPr rounding."""
+    _check_against_stacked(lambda k: "cuda:0")
+    n = torch.cuda.device_count()
+    if n >= 3:
+        _check_against_stacked(lambda k: f"cuda:{k % n}")
+
+
+@pytest.mark.gpu
+def test_thread_parties_lr_inference_gpu():
+    """The tutorial LR inference with each party a thread on its own stream (and GPU when
+    three are visible); prints the p50 latency of 5 warm evaluations."""
+    import time
+
+    from moose_amd.models.predictors.tutorial import logistic_regression_tutorial
+
+    tm = logistic_regression_tutorial(128)
+    n = torch.cuda.device_count()
+    rt = LocalMooseRuntime(IDS, device_map={i: f"cuda:{k % n if n >= 3 else 0}"
+                                            for k, i in enumerate(IDS)}, timeout=120)
+    lat = []
+    for _ in range(6):
+        t0 = time.perf_counter()
+        got = list(rt.evaluate_computation(tm.computation, {"x": tm.x_test}).values())[0]
+        lat.append(time.perf_counter() - t0)
+        assert np.abs(got - tm.proba).max() < 1e-3
+    warm = sorted(lat[1:])
+    print(f"thread parties LR inference ({min(n, 3)} GPU): p50 {warm[2] * 1e3:.2f} ms, "
+          f"rounds {rt.last_stats.rounds}")
