@@ -53,7 +53,11 @@ class SPMDTape:
     """One recorded SPMD evaluation of this process (module doc)."""
 
     def __init__(self, comp, arguments: dict, identity: str, role_ranks: Dict[str, int],
-                 tr, device, storage, ring: int, seed: Optional[int] = None):
+                 tr, device, storage, ring: int, seed: Optional[int] = None, warm=None):
+        """``warm``: the warm-up already ran elsewhere (the in-process parties of
+        parallel/threads.py run it together, on threads) -- a dict with the recorded
+        ``uploads``, the ``first`` outputs, the session ``stats`` and the number of key
+        slots ``keys_n`` it used."""
         from moose_amd.parallel.spmd import SPMDSession
 
         self.comp, self.device, self.tr = comp, torch.device(device), tr
@@ -69,23 +73,28 @@ class SPMDTape:
             else:
                 self.static[k] = v
         stream = torch.cuda.Stream(self.device)
-        # 1. warm-up: the first result, the message plan, the uploads
-        rec = G._Recorder()
-        sess = SPMDSession(identity, role_ranks, tr, device=self.device, seed=seed)
-        interp = Interpreter(sess, storage, ring)
-        with G._upload_hook(rec), torch.cuda.stream(stream):
-            outs = interp.run(comp, self.static)
-            self.first = self._decode(interp, sess, outs)
-        self.stats = sess.stats
+        if warm is None:
+            # 1. warm-up: the first result, the message plan, the uploads
+            rec = G._Recorder()
+            sess = SPMDSession(identity, role_ranks, tr, device=self.device, seed=seed)
+            interp = Interpreter(sess, storage, ring)
+            with G._upload_hook(rec), torch.cuda.stream(stream):
+                outs = interp.run(comp, self.static)
+                self.first = self._decode(interp, sess, outs)
+            self.stats = sess.stats
+            uploads, keys_n = rec.items, sess.keytable.n
+        else:
+            uploads, keys_n = warm["uploads"], warm["keys_n"]
+            self.first, self.stats = warm["first"], warm["stats"]
         torch.cuda.synchronize(self.device)
         # 2. capture: frozen keys, transport in tape mode
-        self.keys = KeyTable(self.device, capacity=max(64, sess.keytable.n + 16))
+        self.keys = KeyTable(self.device, capacity=max(64, keys_n + 16))
         self.keys.frozen = True
         self.sess = SPMDSession(identity, role_ranks, tr, device=self.device, seed=seed)
         self.sess.use_keytable(self.keys)
         self.sess.key_setups = []
         self.interp = Interpreter(self.sess, storage, ring)
-        stager = G._Stager(rec.items, self.device)
+        stager = G._Stager(uploads, self.device)
         self.steps = []  # CUDAGraph segments and CommSteps, in program order
         pool = torch.cuda.graph_pool_handle()
         state = {"g": None, "n": 0}

@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import queue
 import threading
+from typing import Dict
 from typing import List
 from typing import Optional
 
@@ -56,15 +57,20 @@ class ThreadTransport:
     shift / exchange) between the threads of a :class:`Hub`."""
 
     plans = False  # no headers: the values themselves travel
-    tape = None
     stage = False
 
-    def __init__(self, rank: int, hub: Hub):
+    def __init__(self, rank: int, hub: Optional[Hub], device=None, world: Optional[int] = None):
         self.rank, self.hub = rank, hub
-        self.world = len(hub.devices)
-        self.device = hub.devices[rank]
+        self.world = len(hub.devices) if hub is not None else world
+        self.device = hub.devices[rank] if hub is not None else torch.device(device)
         self.bytes_sent = 0
         self.messages = 0
+        # what arrived from each peer, in order (kind, shape, dtype, bits): the landing
+        # buffers of a taped evaluation are allocated from it (PartyTapes)
+        self.log = {}
+        # tape mode: every message round goes to this callback as a CommStep
+        self.tape = None
+        self._cursor = {}
 
     # -- payload movement --------------------------------------------------------------
     def _ship(self, t: torch.Tensor, dst: int):
@@ -112,8 +118,56 @@ class ThreadTransport:
                     raise TransportError(f"rank {self.rank}: no message from rank {src} "
                                          f"within {self.hub.timeout} s") from None
 
+    # -- tape mode ------------------------------------------------------------------------
+    def _taped(self, sends, recvs):
+        from moose_amd.parallel.transport import CommStep
+
+        sends = [(t.contiguous(), dst) for t, dst in sends if t.numel()]
+        land, after = [], []
+        for out, src in recvs:
+            if out.numel() == 0:
+                continue
+            if out.is_contiguous():
+                land.append((out, src))
+            else:
+                buf = torch.empty(out.shape, dtype=out.dtype, device=out.device)
+                land.append((buf, src))
+                after.append((out, buf))
+        self.tape(CommStep(sends, land))
+        for out, buf in after:  # captured in the segment after the round
+            out.copy_(buf)
+
+    def _next_logged(self, src: int):
+        k = self._cursor.get(src, 0)
+        self._cursor[src] = k + 1
+        got = self.log.get(src, [])
+        if k >= len(got):
+            from moose_amd.runtime.graphs import CaptureError
+
+            raise CaptureError(f"message {k} from rank {src} was not seen in the warm-up")
+        return got[k]
+
+    def _logged(self, src: int, item):
+        kind, val, _ = item
+        if kind == "rt":
+            self.log.setdefault(src, []).append(("rt", tuple(val[0].shape), val[0].dtype,
+                                                 val[1]))
+        elif kind == "t":
+            self.log.setdefault(src, []).append(("t", tuple(val.shape), val.dtype, None))
+        else:
+            self.log.setdefault(src, []).append(("v", None, None, None))
+
     # -- typed values ------------------------------------------------------------------
     def send(self, v, dst: int):
+        if self.tape is not None:
+            if isinstance(v, R.RT):
+                v = v.data
+            if not isinstance(v, torch.Tensor):
+                from moose_amd.runtime.graphs import CaptureError
+
+                raise CaptureError(f"a host value ({type(v).__name__}) in the message flow")
+            self._taped([(v, dst)], [])
+            return
         if isinstance(v, R.RT):
             y, ev = self._ship(v.data, dst)
             self._put(dst, ("rt", (y, v.bits), ev))
@@ -124,7 +178,19 @@ class ThreadTransport:
             self._put(dst, ("v", v, None))
 
     def recv(self, src: int, device=None):
-        kind, val, ev = self._get(src)
+        if self.tape is not None:
+            kind, shape, dtype, bits = self._next_logged(src)
+            if kind == "v":
+                from moose_amd.runtime.graphs import CaptureError
+
+                raise CaptureError("a host value in the message flow")
+            buf = torch.empty(shape, dtype=dtype, device=self.device)
+            self._taped([], [(buf, src)])
+            data = buf if device is None else buf.to(device)
+            return R.RT(data, bits) if kind == "rt" else data
+        item = self._get(src)
+        self._logged(src, item)
+        kind, val, ev = item
         if kind == "v":
             return val
         if kind == "rt":
@@ -138,11 +204,23 @@ class ThreadTransport:
     def shift(self, t: torch.Tensor, to_rank: int, from_rank: int) -> torch.Tensor:
         if t.numel() == 0:
             return torch.empty_like(t)
+        if self.tape is not None:
+            t = t.contiguous()
+            out = torch.empty_like(t)
+            self._next_logged(from_rank)
+            self._taped([(t, to_rank)], [(out, from_rank)])
+            return out
         self.send(t, to_rank)
         return self.recv(from_rank)
 
     def exchange(self, sends, recvs):
         """Sends first (they never block), then each receive lands in its buffer."""
+        if self.tape is not None:
+            for out, src in recvs:
+                if out.numel():
+                    self._next_logged(src)
+            self._taped(sends, recvs)
+            return
         for t, dst in sends:
             if t.numel():
                 self.send(t, dst)
@@ -164,27 +242,45 @@ class ThreadTransport:
         return None
 
 
+class _ThreadUploads:
+    """The ring module's upload hook while the party threads run a warm-up: each thread's
+    host->device copies go to that thread's recorder (runtime/graphs._Recorder)."""
+
+    def __init__(self):
+        self.by_thread = {}
+
+    def __call__(self, t, device):
+        rec = self.by_thread.get(threading.get_ident())
+        return rec(t, device) if rec is not None else t.to(device)
+
+
 def run_parties(comp, arguments: dict, identities: List[str], devices: List, storage: dict,
                 fixedpoint_ring: int = 128, seed: Optional[int] = None,
-                timeout: Optional[float] = None):
+                timeout: Optional[float] = None, record: bool = False):
     """Evaluate ``comp`` with party ``identities[i]`` as a thread on ``devices[i]``.
-    Returns ``(outputs, stats_by_identity, elapsed_us_by_identity)``; the outputs of every
-    party merged (each output tag is materialised by the party that owns it)."""
+    Returns ``(outputs, stats_by_identity, elapsed_us_by_identity, warm)``: the outputs of
+    every party merged (each output tag is materialised by the party that owns it);
+    ``warm`` (with ``record``) holds per party what a :class:`PartyTapes` capture needs
+    -- the uploads, the first outputs, the stats, the key slots used and the message log."""
     import time
 
     from moose_amd.compiler.passes import is_lowered
     from moose_amd.parallel.spmd import SPMDSession
+    from moose_amd.runtime import graphs as G
     from moose_amd.runtime.interpreter import Interpreter
 
     hub = Hub(devices, timeout=timeout)
     role_ranks = {r: i for i, r in enumerate(identities)}
-    results, stats, elapsed, errors = {}, {}, {}, {}
+    results, stats, elapsed, errors, warm = {}, {}, {}, {}, {}
     lowered = is_lowered(comp)
+    hooks = _ThreadUploads() if record else None
 
     def party(i):
         ident, dev = identities[i], hub.devices[i]
         tr = ThreadTransport(i, hub)
         try:
+            if hooks is not None:
+                hooks.by_thread[threading.get_ident()] = rec = G._Recorder()
             if dev.type == "cuda":
                 torch.cuda.set_device(dev)
                 stream = torch.cuda.Stream(dev)
@@ -211,6 +307,9 @@ def run_parties(comp, arguments: dict, identities: List[str], devices: List, sto
                     out = {tag: interp.to_numpy(lv) for tag, lv in outs.items()
                            if lv.kind != "unit" and sess.materialized(lv.v)}
                     st = sess.stats
+                    if hooks is not None:
+                        warm[ident] = {"uploads": rec.items, "first": out, "stats": st,
+                                       "keys_n": sess.keytable.n, "log": tr.log}
             if dev.type == "cuda":
                 torch.cuda.synchronize(dev)
             elapsed[ident] = int((time.perf_counter() - t0) * 1e6)
@@ -221,10 +320,16 @@ def run_parties(comp, arguments: dict, identities: List[str], devices: List, sto
 
     threads = [threading.Thread(target=party, args=(i,), name=f"moose-party-{identities[i]}",
                                 daemon=True) for i in range(len(identities))]
-    for t in threads:
-        t.start()
-    for t in threads:
-        t.join()
+    prev = R._UPLOAD_HOOK
+    if hooks is not None:
+        R._UPLOAD_HOOK = hooks
+    try:
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+    finally:
+        R._UPLOAD_HOOK = prev
     if errors:
         # the first party to fail is the cause; the others saw TransportError because of it
         first = next((e for e in errors.values() if not isinstance(e, TransportError)),
@@ -233,4 +338,167 @@ def run_parties(comp, arguments: dict, identities: List[str], devices: List, sto
     merged = {}
     for ident in identities:
         merged.update(results[ident])
-    return merged, stats, elapsed
+    return merged, stats, elapsed, (warm if record and not lowered else None)
+
+
+class PartyTapes:
+    """Replayed evaluations of the in-process parties: one recorded tape per party
+    (parallel/spmd_graphs.SPMDTape: hipGraph segments between message rounds, captured on
+    the party's own device), replayed by ONE host thread that interleaves the parties.
+
+    At capture the rounds of all tapes are matched (the k-th message from party a to b is
+    the k-th receive at b from a) and turned into a fixed issue order: a party's segments
+    run until a round that receives something whose sender has not been issued yet, then
+    another party goes on.  A send records an event on the sender's stream; the receiver's
+    stream waits for it and copies into its landing buffer (a peer copy over xGMI from a
+    copy stream of the source GPU when the parties are on different devices), so every
+    dependency is a stream/event edge and the host never waits inside a replay."""
+
+    def __init__(self, comp, arguments: dict, identities: List[str], devices: List,
+                 storage: dict, ring: int, seed: Optional[int], warm: dict):
+        from moose_amd.parallel.spmd_graphs import SPMDTape
+
+        self.identities = list(identities)
+        self.devices = [torch.device(d) for d in devices]
+        n = len(identities)
+        role_ranks = {r: i for i, r in enumerate(identities)}
+        self.tapes = []
+        for i, ident in enumerate(identities):
+            tr = ThreadTransport(i, None, device=self.devices[i], world=n)
+            tr.log = warm[ident]["log"]
+            with torch.cuda.device(self.devices[i]):
+                self.tapes.append(SPMDTape(comp, arguments, ident, role_ranks, tr,
+                                           self.devices[i], storage, ring, seed,
+                                           warm=warm[ident]))
+        self.streams = [t.stream for t in self.tapes]
+        self._copy_streams = {}
+        self.actions = self._schedule()
+        self.rounds = max(t.rounds for t in self.tapes)
+        self.segments = sum(t.segments for t in self.tapes)
+        self._ends = None
+        self.issue_s = []
+
+    def _copy_stream(self, dev):
+        s = self._copy_streams.get(dev)
+        if s is None:
+            s = self._copy_streams[dev] = torch.cuda.Stream(dev)
+        return s
+
+    def _schedule(self):
+        from moose_amd.parallel.transport import CommStep
+        from moose_amd.runtime.graphs import CaptureError
+
+        n = len(self.tapes)
+        steps = [t.steps for t in self.tapes]
+        ptr, sent_done = [0] * n, [False] * n
+        sent, recvd, pending = {}, {}, {}
+        actions = []
+        while any(ptr[p] < len(steps[p]) for p in range(n)):
+            progress = False
+            for p in range(n):
+                while ptr[p] < len(steps[p]):
+                    s = steps[p][ptr[p]]
+                    if not isinstance(s, CommStep):
+                        actions.append(("g", p, s))
+                        ptr[p] += 1
+                        progress = True
+                        continue
+                    if not sent_done[p]:
+                        for t, dst in s.sends:
+                            k = sent.get((p, dst), 0)
+                            sent[(p, dst)] = k + 1
+                            ev = torch.cuda.Event()
+                            pending[(p, dst, k)] = (t, ev)
+                            actions.append(("rec", p, ev))
+                        sent_done[p] = True
+                        progress = True
+                    ready = {}
+                    for _, src in s.recvs:
+                        ready[src] = ready.get(src, 0) + 1
+                    if any(sent.get((src, p), 0) < recvd.get((src, p), 0) + c
+                           for src, c in ready.items()):
+                        break  # a sender has not reached this message yet
+                    for buf, src in s.recvs:
+                        k = recvd.get((src, p), 0)
+                        recvd[(src, p)] = k + 1
+                        t, ev = pending.pop((src, p, k))
+                        if t.numel() != buf.numel() or t.dtype != buf.dtype:
+                            raise CaptureError(f"message {k} from party {src} to {p}: "
+                                               f"{tuple(t.shape)} {t.dtype} sent, "
+                                               f"{tuple(buf.shape)} {buf.dtype} expected")
+                        actions.append(("cp", p, src, t.reshape(buf.shape), buf, ev))
+                    ptr[p] += 1
+                    sent_done[p] = False
+                    progress = True
+            if not progress:
+                raise CaptureError("the parties' tapes do not pair up (a receive no party "
+                                   "sends)")
+        if pending:
+            raise CaptureError(f"{len(pending)} messages sent but never received")
+        return actions
+
+    def replay(self, arguments: dict) -> Dict[str, dict]:
+        import time
+
+        import numpy as np
+
+        n = len(self.tapes)
+        prev_dev = torch.cuda.current_device()
+        prev = [torch.cuda.current_stream(d) for d in set(self.devices)]
+        t0 = time.perf_counter()
+        try:
+            for p, tape in enumerate(self.tapes):
+                s = self.streams[p]
+                torch.cuda.set_stream(s)
+                if self._ends is not None:  # the landing buffers are free again
+                    for q in range(n):
+                        if q != p:
+                            s.wait_event(self._ends[q])
+                for k, v in arguments.items():
+                    t = tape.static.get(k)
+                    if isinstance(t, torch.Tensor):
+                        a = np.asarray(v)
+                        a = a.view(np.int64) if a.dtype == np.uint64 else a
+                        src = torch.from_numpy(np.ascontiguousarray(a).reshape(t.shape))
+                        t.copy_(src if src.dtype == t.dtype else src.to(t.dtype))
+                tape._fill_keys()
+            cur = -1
+            for a in self.actions:
+                p = a[1]
+                if a[0] == "g":
+                    if p != cur:
+                        torch.cuda.set_stream(self.streams[p])
+                        cur = p
+                    a[2].replay()
+                elif a[0] == "rec":
+                    a[2].record(self.streams[p])
+                else:
+                    _, p, src, t, buf, ev = a
+                    if self.devices[src] != self.devices[p]:
+                        c = self._copy_stream(self.devices[src])
+                        c.wait_event(ev)
+                        torch.cuda.set_stream(c)  # the peer copy runs on the source GPU
+                        torch.cuda.set_stream(self.streams[p])
+                    else:
+                        if p != cur:
+                            torch.cuda.set_stream(self.streams[p])
+                        self.streams[p].wait_event(ev)
+                    cur = p
+                    buf.copy_(t)
+            ends = []
+            for p in range(n):
+                e = torch.cuda.Event()
+                e.record(self.streams[p])
+                ends.append(e)
+            self._ends = ends
+            self.issue_s.append(time.perf_counter() - t0)
+            out = {}
+            for p, tape in enumerate(self.tapes):
+                torch.cuda.set_stream(self.streams[p])
+                out[self.identities[p]] = tape._decode(tape.interp, tape.sess, tape.outs)
+                tape.replays += 1
+        finally:
+            for s in prev:
+                torch.cuda.set_stream(s)
+            torch.cuda.set_device(prev_dev)
+        return out

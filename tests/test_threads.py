@@ -106,23 +106,51 @@ def test_thread_parties_on_gpu_streams():
 
 
 @pytest.mark.gpu
-def test_thread_parties_lr_inference_gpu():
+def test_thread_parties_lr_inference_gpu(monkeypatch):
     """The tutorial LR inference with each party a thread on its own stream (and GPU when
-    three are visible); prints the p50 latency of 5 warm evaluations."""
+    three are visible): the second evaluation records per-party tapes, later ones replay
+    them from one host thread (PartyTapes).  Prints eager and replay p50."""
     import time
 
     from moose_amd.models.predictors.tutorial import logistic_regression_tutorial
 
+    monkeypatch.setenv("MOOSEX_GRAPHS_DEBUG", "1")  # a capture failure fails the test
     tm = logistic_regression_tutorial(128)
     n = torch.cuda.device_count()
-    rt = LocalMooseRuntime(IDS, device_map={i: f"cuda:{k % n if n >= 3 else 0}"
-                                            for k, i in enumerate(IDS)}, timeout=120)
-    lat = []
-    for _ in range(6):
-        t0 = time.perf_counter()
-        got = list(rt.evaluate_computation(tm.computation, {"x": tm.x_test}).values())[0]
-        lat.append(time.perf_counter() - t0)
-        assert np.abs(got - tm.proba).max() < 1e-3
-    warm = sorted(lat[1:])
-    print(f"thread parties LR inference ({min(n, 3)} GPU): p50 {warm[2] * 1e3:.2f} ms, "
+    devs = {i: f"cuda:{k % n if n >= 3 else 0}" for k, i in enumerate(IDS)}
+    lat = {}
+    for mode in (False, True):
+        rt = LocalMooseRuntime(IDS, device_map=devs, timeout=120, use_graphs=mode)
+        ts = []
+        for _ in range(8):
+            t0 = time.perf_counter()
+            got = list(rt.evaluate_computation(tm.computation, {"x": tm.x_test}).values())[0]
+            ts.append(time.perf_counter() - t0)
+            assert np.abs(got - tm.proba).max() < 1e-3
+        lat[mode] = sorted(ts[3:])[2] * 1e3
+        if mode:
+            (comp, tapes), = rt._party_tapes.values()
+            assert tapes is not False and tapes.tapes[0].replays >= 5
+            issue = sorted(tapes.issue_s)[len(tapes.issue_s) // 2] * 1e3
+    print(f"thread parties LR inference ({min(n, 3)} GPU): eager p50 {lat[False]:.2f} ms, "
+          f"replay p50 {lat[True]:.3f} ms (host issue {issue:.3f} ms), "
           f"rounds {rt.last_stats.rounds}")
+
+
+@pytest.mark.gpu
+def test_thread_party_tapes_replay_bitwise_equal_eager():
+    """Seeded sessions: a replay re-draws the seeded keys as a fresh eager evaluation does,
+    so every replay's outputs equal the eager ones bitwise (parties on streams of cuda:0)."""
+    comp = _comp(False)
+    args = _args()
+    devs = {i: "cuda:0" for i in IDS}
+    eager = LocalMooseRuntime(IDS, device_map=devs, seed=11, use_graphs=False)
+    want = eager.evaluate_computation(comp, args)
+    rt = LocalMooseRuntime(IDS, device_map=devs, seed=11, use_graphs=True)
+    for _ in range(4):
+        got = rt.evaluate_computation(comp, args)
+        assert set(got) == set(want)
+        for k in want:
+            assert np.array_equal(np.asarray(got[k]), np.asarray(want[k])), k
+    (c, tapes), = rt._party_tapes.values()
+    assert tapes is not False and tapes.tapes[0].replays == 2
