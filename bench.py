@@ -398,25 +398,41 @@ def _lr_stacked(runs, device):
 
     tm = logistic_regression_tutorial(128)
     out = {}
-    # eager (use_graphs=False), replay from the first evaluation (True), and the runtime's
-    # default with no flags (auto: captured at the second evaluation, replayed after)
-    for mode in ("eager", "graphs", "default"):
+    # eager (use_graphs=False), replay from the first evaluation (True), the runtime's
+    # default with no flags (auto: captured at the second evaluation, replayed after), and
+    # the three parties as threads of this process, each on its own HIP stream
+    # (parallel/threads.py; per-party tapes replayed by one host thread)
+    for mode in ("eager", "graphs", "default", "parties"):
         flags = {"eager": {"use_graphs": False}, "graphs": {"use_graphs": True},
-                 "default": {}}[mode]
-        rt = LocalMooseRuntime(list(ROLES), device=device, fixedpoint_ring=128, **flags)
-        args = {"x": tm.x_test}
-        for _ in range(3):
-            r = rt.evaluate_computation(tm.computation, args)
-        lat = []
-        for _ in range(runs):
-            t0 = time.perf_counter()
-            r = rt.evaluate_computation(tm.computation, args)  # synchronises the device
-            lat.append((time.perf_counter() - t0) * 1e3)
+                 "default": {}, "parties": {"device_map": {r: str(device) for r in ROLES}}
+                 }[mode]
+        try:
+            rt = LocalMooseRuntime(list(ROLES), device=device, fixedpoint_ring=128, **flags)
+            args = {"x": tm.x_test}
+            for _ in range(3):
+                r = rt.evaluate_computation(tm.computation, args)
+            lat = []
+            for _ in range(runs):
+                t0 = time.perf_counter()
+                r = rt.evaluate_computation(tm.computation, args)  # synchronises the device
+                lat.append((time.perf_counter() - t0) * 1e3)
+        except Exception as e:  # noqa: BLE001 - an extra mode: record, keep the others
+            if mode != "parties":
+                raise
+            out[mode] = {"error": f"{type(e).__name__}: {e}"[:300]}
+            continue
         err = float(np.abs(np.asarray(list(r.values())[0]) - tm.proba).max())
         lat.sort()
         rec = {"p50_ms": lat[len(lat) // 2], "p90_ms": lat[int(0.9 * (len(lat) - 1))],
                "max_abs_err_vs_sklearn": err}
-        if mode != "eager":
+        if mode == "parties":
+            tapes = [t for _, t in rt._party_tapes.values() if t]
+            rec["replayed"] = bool(tapes)
+            rec["rounds"] = rt.last_stats.rounds
+            if tapes:
+                iss = sorted(tapes[0].issue_s)
+                rec["host_issue_ms_p50"] = iss[len(iss) // 2] * 1e3
+        elif mode != "eager":
             rec["captured"] = bool(rt._graphs.plans)
         out[mode] = rec
         if device.type == "cuda":
@@ -1037,7 +1053,8 @@ def _main(args, prog_out):
                     r0[mode] = dict(r0[mode], max_abs_err_vs_sklearn=errs[0] if errs else None)
                 lr["spmd_one_party_per_gpu"] = r0
         if rank == 0:
-            line["lr_inference_p50_ms"] = {k: v["p50_ms"] for k, v in lr["one_gpu"].items()}
+            line["lr_inference_p50_ms"] = {k: v["p50_ms"] for k, v in lr["one_gpu"].items()
+                                           if "p50_ms" in v}
             sp = lr.get("spmd_one_party_per_gpu")
             if sp:
                 best = sp.get("tape") if sp.get("tape", {}).get("replayed") else sp["eager"]
