@@ -476,7 +476,10 @@ class StackedSession(Session):
 
         bits = v.v.bits
         data = v.v.data.contiguous()
-        s0, s1 = out if out is not None else (torch.empty_like(data), torch.empty_like(data))
+        if out is not None:  # party vectors (row views of a stack) or raw tensors
+            s0, s1 = (o.v.data if isinstance(o, PV) else o for o in out)
+        else:
+            s0, s1 = torch.empty_like(data), torch.empty_like(data)
         slots = [self.key_ptr(plc, q) for p in range(3) for q in (p, (p + 1) % 3)]
         party.dot_trunc_tail(self, plc, [0, 1, 2], [data[c] for c in range(3)], bits, m,
                              nonces, [s0[c] for c in range(3)], [s1[c] for c in range(3)], slots)
