@@ -154,3 +154,41 @@ def test_thread_party_tapes_replay_bitwise_equal_eager():
             assert np.array_equal(np.asarray(got[k]), np.asarray(want[k])), k
     (c, tapes), = rt._party_tapes.values()
     assert tapes is not False and tapes.tapes[0].replays == 2
+
+
+def test_party_tapes_schedule_pairs_rounds():
+    """The replay order of PartyTapes (CPU, mock tapes): a ring shift, then a dealer's
+    send-only round to two receive-only parties.  Every receive is issued after its
+    matched send's event, every party's steps stay in order, and an unmatched receive is
+    a capture error (the evaluation then stays eager)."""
+    from moose_amd.parallel.threads import PartyTapes
+    from moose_amd.parallel.transport import CommStep
+    from moose_amd.runtime.graphs import CaptureError
+
+    class _T:
+        def __init__(self, steps):
+            self.steps = steps
+
+    def e(n):
+        return torch.zeros(n)
+
+    tapes = [
+        ["a0", CommStep([(e(2), 1)], [(e(2), 2)]), "a1", CommStep([], [(e(3), 2)]), "a2"],
+        ["b0", CommStep([(e(2), 2)], [(e(2), 0)]), CommStep([], [(e(3), 2)]), "b1"],
+        ["c0", CommStep([(e(2), 0)], [(e(2), 1)]), "c1", CommStep([(e(3), 0), (e(3), 1)], [])],
+    ]
+    pt = PartyTapes.__new__(PartyTapes)
+    pt.tapes = [_T(s) for s in tapes]
+    acts = pt._schedule()
+    order = {p: [a[2] for a in acts if a[0] == "g" and a[1] == p] for p in range(3)}
+    assert order == {0: ["a0", "a1", "a2"], 1: ["b0", "b1"], 2: ["c0", "c1"]}
+    recorded = set()
+    for a in acts:
+        if a[0] == "rec":
+            recorded.add(id(a[2]))
+        elif a[0] == "cp":
+            assert id(a[5]) in recorded  # the send's event was recorded before
+    assert sum(a[0] == "cp" for a in acts) == 5
+    pt.tapes = [_T([CommStep([], [(e(1), 1)])]), _T(["x"])]
+    with pytest.raises(CaptureError):
+        pt._schedule()
