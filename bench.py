@@ -388,8 +388,11 @@ def _preflight(layout, comms, world, rank, device, prog, offsets=None):
 # ---------------------------------------------------------------------------------------
 # LR inference (BASELINE config 4)
 # ---------------------------------------------------------------------------------------
-def _lr_stacked(runs, device):
-    """p50 latency of the tutorial model on one GPU: eager, then hipGraph replay."""
+def _lr_stacked(runs, device, world=1):
+    """p50 latency of the tutorial model on one GPU: eager, then hipGraph replay; then the
+    three parties as threads of this process on three streams of this GPU ("parties") and,
+    in a run with >= 3 GPUs, on three GPUs ("parties_3gpu": every message a peer copy over
+    xGMI)."""
     import numpy as np
     import torch
 
@@ -402,9 +405,17 @@ def _lr_stacked(runs, device):
     # default with no flags (auto: captured at the second evaluation, replayed after), and
     # the three parties as threads of this process, each on its own HIP stream
     # (parallel/threads.py; per-party tapes replayed by one host thread)
-    for mode in ("eager", "graphs", "default", "parties"):
+    modes = ["eager", "graphs", "default", "parties"]
+    gpus3 = None
+    if (device.type == "cuda" and world >= 3 and torch.cuda.device_count() >= 3
+            and os.environ.get("MOOSEX_SHARED_GPU") != "1"):
+        gpus3 = [device] + [torch.device("cuda", (device.index + k) % torch.cuda.device_count())
+                            for k in (1, 2)]
+        modes.append("parties_3gpu")
+    for mode in modes:
         flags = {"eager": {"use_graphs": False}, "graphs": {"use_graphs": True},
-                 "default": {}, "parties": {"device_map": {r: str(device) for r in ROLES}}
+                 "default": {}, "parties": {"device_map": {r: str(device) for r in ROLES}},
+                 "parties_3gpu": {"device_map": {r: str(d) for r, d in zip(ROLES, gpus3 or [])}},
                  }[mode]
         try:
             rt = LocalMooseRuntime(list(ROLES), device=device, fixedpoint_ring=128, **flags)
@@ -417,7 +428,7 @@ def _lr_stacked(runs, device):
                 r = rt.evaluate_computation(tm.computation, args)  # synchronises the device
                 lat.append((time.perf_counter() - t0) * 1e3)
         except Exception as e:  # noqa: BLE001 - an extra mode: record, keep the others
-            if mode != "parties":
+            if not mode.startswith("parties"):
                 raise
             out[mode] = {"error": f"{type(e).__name__}: {e}"[:300]}
             continue
@@ -425,7 +436,7 @@ def _lr_stacked(runs, device):
         lat.sort()
         rec = {"p50_ms": lat[len(lat) // 2], "p90_ms": lat[int(0.9 * (len(lat) - 1))],
                "max_abs_err_vs_sklearn": err}
-        if mode == "parties":
+        if mode.startswith("parties"):
             tapes = [t for _, t in rt._party_tapes.values() if t]
             rec["replayed"] = bool(tapes)
             rec["rounds"] = rt.last_stats.rounds
@@ -1033,7 +1044,7 @@ def _main(args, prog_out):
         lr = {"model": "ml-inference-with-onnx tutorial LogisticRegression (200x10, "
                        "fixed(24,40), Z_2^128, from_onnx)"}
         if rank == 0:
-            lr["one_gpu"] = _lr_stacked(args.lr_runs, device)
+            lr["one_gpu"] = _lr_stacked(args.lr_runs, device, world)
         if world > 1:
             dist.barrier()
         if world >= 3 and args.spmd_configs and fits("lr_spmd"):
