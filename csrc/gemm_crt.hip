@@ -1320,7 +1320,7 @@ int run_crt(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T
   const bool b_bc = batch > 1 && b_bstride == 0 && !rb_pre;
   if (!rb) {
     int8_t* rbw = cr + p.cr_bytes;
-    if (!B1) {  // B1 is B0 rolled like A1: each share's residues computed once
+    if (mode == 1 && !B1) {  // B1 is B0 rolled like A1: each share's residues computed once
       const int r3 = (int)(((roll % 3) + 3) % 3);
       if (!(r3 && batch == 3 && mode == 1 && K % BK == 0 && b_bstride > 0)) return -7;
       launch_prep_b3<T>(p, tb, N, K, b_bstride, B0, (int)(((roll % 3) + 3) % 3), rbw, st);
