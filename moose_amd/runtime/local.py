@@ -238,7 +238,7 @@ class LocalMooseRuntime:
                 return result
         seen = self._seen.get(key) if key is not None else None
         record = (tapeable and seen is not None and seen[0] is comp
-                  and (self.use_graphs is True or seen[1] < AUTO_GRAPH_MS / 1e3)
+                  and (self.use_graphs is True or seen[1] < PARTIES_AUTO_GRAPH_MS / 1e3)
                   and key not in self._party_tapes)
         t0 = time.perf_counter()
         result, stats, self.last_timings, warm = T.run_parties(
@@ -280,6 +280,9 @@ class LocalMooseRuntime:
 # auto hipGraph mode: only evaluations whose eager run took less than this are captured
 # (dispatch-bound; a GEMM-bound evaluation gains nothing and its capture pins memory)
 AUTO_GRAPH_MS = float(os.environ.get("MOOSEX_GRAPHS_AUTO_MS", "50"))
+# the same for parties as threads: their eager evaluation is three Python dispatch loops
+# sharing one interpreter lock, so a dispatch-bound program takes a few times longer
+PARTIES_AUTO_GRAPH_MS = 4 * AUTO_GRAPH_MS
 
 
 def _is_lowered(comp: Computation) -> bool:
