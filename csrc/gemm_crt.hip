@@ -316,111 +316,6 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// B' image of a stacked RSS pair (mode 1, three parties, B1[b] = B0[(b + roll) % 3]): one
-// thread = 8 consecutive k of one column for ALL THREE parties, so each share's residues are
-// computed once instead of once per half and per neighbour.  Party b's bottom half (B0) is
-// R_b = res(y_b); its top half (B0 + B1, the ring sum y_b + y_b') is R_b + R_b' - w (2^w mod p)
-// re-centered, where w in {-1, 0, 1} is the signed overflow of the 2^w-bit ring sum -- the
-// same residue k_crt_prep<T, true> computes from the sum itself, so the image is bitwise the
-// same.  Work per element: 3 residues + 3 cheap re-centerings instead of 6 residues, and
-// 3 element reads instead of 9.  Needs K % BK == 0 (the halves split at a k-step).
-template <class T, int ROWS, int ROLL>
-__global__ void __launch_bounds__(256)
-    k_crt_prep_b3(const T* __restrict__ X, int64_t R, int64_t K, int64_t xs,
-                  int8_t* __restrict__ out, int64_t tiles, const PrepTab tab) {
-  constexpr int NW = Words<T>::N;
-  const int64_t khalf = K / BK, nkb = 2 * khalf;
-  const int64_t total = tiles * khalf * (ROWS * 8);
-  const int n = tab.n;
-  const int64_t plane = tiles * nkb * (int64_t)(ROWS * BK);
-  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total;
-       g += (int64_t)gridDim.x * blockDim.x) {
-    const int h = (int)(g & 1);
-    const int c = (int)((g >> 1) & 3);
-    const int r = (int)((g >> 3) & (ROWS - 1));
-    const int64_t q = g / (ROWS * 8);
-    const int64_t kb = q % khalf, t = q / khalf;
-    const int64_t row = t * ROWS + r;
-    const int64_t k0 = kb * BK + c * 16 + h * 8;
-    uint32_t v[3][8][NW];
-#pragma unroll
-    for (int b = 0; b < 3; ++b)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const T e = row < R ? X[b * xs + (k0 + j) * R + row] : (T)0;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) v[b][j][w] = (uint32_t)(e >> (32 * w));
-      }
-    // signed overflow of each pair's ring sum, and the sum's low word (the p = 256 residue)
-    int wv[3][8];
-    uint32_t lo[3][8];
-#pragma unroll
-    for (int b = 0; b < 3; ++b) {
-      const int b2 = (b + ROLL) % 3;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        uint32_t carry = 0, top = 0;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-          const uint64_t s = (uint64_t)v[b][j][w] + v[b2][j][w] + carry;
-          carry = (uint32_t)(s >> 32);
-          if (w == 0) lo[b][j] = (uint32_t)s;
-          if (w == NW - 1) top = (uint32_t)s;
-        }
-        const uint32_t sa = v[b][j][NW - 1] >> 31, sb = v[b2][j][NW - 1] >> 31, ss = top >> 31;
-        wv[b][j] = (sa == sb && ss != sa) ? (sa ? -1 : 1) : 0;
-      }
-    }
-    const int64_t off_top = (t * nkb + kb) * (int64_t)(ROWS * BK) + img_off(r, c) + 8 * h;
-    const int64_t off_bot = off_top + khalf * (int64_t)(ROWS * BK);
-    {  // p = 256: low bytes (B's multiplier is 1)
-#pragma unroll
-      for (int b = 0; b < 3; ++b) {
-        int8_t* ob = out + (int64_t)b * n * plane;
-        int2 bo, to;
-        bo.x = (int)pack4(v[b][0][0], v[b][1][0], v[b][2][0], v[b][3][0]);
-        bo.y = (int)pack4(v[b][4][0], v[b][5][0], v[b][6][0], v[b][7][0]);
-        to.x = (int)pack4(lo[b][0], lo[b][1], lo[b][2], lo[b][3]);
-        to.y = (int)pack4(lo[b][4], lo[b][5], lo[b][6], lo[b][7]);
-        *(int2*)(ob + off_bot) = bo;
-        *(int2*)(ob + off_top) = to;
-      }
-    }
-    for (int i = 1; i < n; ++i) {
-      const uint32_t w4[4] = {tab.w[i][0], tab.w[i][1], tab.w[i][2], tab.w[i][3]};
-      const uint32_t neg = tab.neg[i];
-      const int pi = tab.p[i];
-      const float p = (float)pi, rcp = tab.rcp[i];
-      int pw = (pi - (int)neg) % pi;  // 2^w mod p, centered
-      if (2 * pw > pi) pw -= pi;
-      int rr[3][8];
-#pragma unroll
-      for (int b = 0; b < 3; ++b)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) rr[b][j] = residue<NW>(v[b][j], w4, neg, p, rcp);
-#pragma unroll
-      for (int b = 0; b < 3; ++b) {
-        const int b2 = (b + ROLL) % 3;
-        int tt[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float fs = (float)(rr[b][j] + rr[b2][j] - wv[b][j] * pw);  // |.| < 3p/2
-          const float qt = __builtin_rintf(fs * rcp);
-          tt[j] = (int)__builtin_fmaf(-qt, p, fs);
-        }
-        int8_t* ob = out + ((int64_t)b * n + i) * plane;
-        int2 bo, to;
-        bo.x = (int)pack4(rr[b][0], rr[b][1], rr[b][2], rr[b][3]);
-        bo.y = (int)pack4(rr[b][4], rr[b][5], rr[b][6], rr[b][7]);
-        to.x = (int)pack4(tt[0], tt[1], tt[2], tt[3]);
-        to.y = (int)pack4(tt[4], tt[5], tt[6], tt[7]);
-        *(int2*)(ob + off_bot) = bo;
-        *(int2*)(ob + off_top) = to;
-      }
-    }
-  }
-}
-
 // XCD-aware remap (as gemm_mfma.hip): consecutive tile ids land on one XCD
 __device__ inline int64_t xcd_remap(int64_t bid, int64_t nwg) {
   const int64_t q = nwg / 8, r = nwg % 8;
@@ -1161,22 +1056,6 @@ void launch_prep(const CPlan& p, const Tables& tb, bool is_b, int64_t batch, int
                        out, tiles, nkb, tb.pb);
 }
 
-template <class T>
-void launch_prep_b3(const CPlan& p, const Tables& tb, int64_t N, int64_t K, int64_t xs,
-                    const T* B0, int roll, int8_t* out, hipStream_t st) {
-  const int64_t work = p.tiles_n * (K / BK) * (p.bn * 8);
-  const dim3 grid((unsigned)std::min<int64_t>((work + 255) / 256, 16384));
-#define MX_B3(BN, RL)                                                                   \
-  hipLaunchKernelGGL((k_crt_prep_b3<T, BN, RL>), grid, dim3(256), 0, st, B0, N, K, xs, out, \
-                     p.tiles_n, tb.pb)
-  if (p.bn == 256) {
-    if (roll == 1) MX_B3(256, 1); else MX_B3(256, 2);
-  } else {
-    if (roll == 1) MX_B3(128, 1); else MX_B3(128, 2);
-  }
-#undef MX_B3
-}
-
 // MOOSEX_CRT_DMA_MASK (timing experiments, wrong results): bit 0 = stream A, bit 1 = B,
 // bit 2 = skip the epilogue reduction, bit 3 = no LDS fragment reads in the main loop
 int dma_mask() {
@@ -1320,13 +1199,7 @@ int run_crt(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T
   const bool b_bc = batch > 1 && b_bstride == 0 && !rb_pre;
   if (!rb) {
     int8_t* rbw = cr + p.cr_bytes;
-    if (mode == 1 && !B1) {  // B1 is B0 rolled like A1: each share's residues computed once
-      const int r3 = (int)(((roll % 3) + 3) % 3);
-      if (!(r3 && batch == 3 && mode == 1 && K % BK == 0 && b_bstride > 0)) return -7;
-      launch_prep_b3<T>(p, tb, N, K, b_bstride, B0, (int)(((roll % 3) + 3) % 3), rbw, st);
-    } else {
-      launch_prep<T>(p, tb, true, b_bc ? 1 : batch, N, K, b_bstride, B0, B1, mode, rbw, st);
-    }
+    launch_prep<T>(p, tb, true, b_bc ? 1 : batch, N, K, b_bstride, B0, B1, mode, rbw, st);
     rb = rbw;
   }
   if (roll)  // each entry's own K residues; the GEMM reads entry b + roll's for the 2nd half
@@ -1421,8 +1294,7 @@ int mxh_gemm_crt_strided(int words, int64_t batch, int64_t M, int64_t N, int64_t
 // RSS pair form of the mode-1 product: A1 is A0 rolled by ``roll`` batch entries
 // (A1[b] = A0[(b + roll) % batch], as the second shares of a stacked replicated sharing are
 // the next party's first), so A' residues are prepared once per share instead of twice.
-// rb: prepared B' (mxh_crt_prep_b) or null (then B0, B1; B1 null: B1 is B0 rolled by ``roll``
-// too, the B' image built by k_crt_prep_b3).  -7: not applicable.
+// rb: prepared B' (mxh_crt_prep_b) or null (then B0, B1).  -7: not applicable.
 int mxh_crt_roll(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
                  int64_t a_bstride, int64_t roll, const void* B0, const void* B1, const void* rb,
                  void* C, int accumulate, void* stream) {

@@ -829,14 +829,11 @@ def dot_cross_rows(x0: RT, x1: RT, r0: int, r1: int, pb: PreparedCross) -> RT:
 
 
 def dot_cross_pair(x0: RT, y0: RT, y1: RT, roll: int, pb: PreparedCross = None, r0=0,
-                   r1=None, y_rolled: bool = False):
+                   r1=None):
     """dot_cross(x0, x1, y0, y1) for a stacked RSS pair whose second share is the first
     rolled over the flattened batch (x1[b] = x0[(b + roll) % batch]): the CRT GEMM prepares
-    each share's residues once and reads them for both K halves.  ``y_rolled``: y1 is y0
-    rolled the same way (a stacked RSS sharing too), so B' is built from each y share's
-    residues once (k_crt_prep_b3; MOOSEX_CRT_B3=0 builds it from both shares).  Rows
-    [r0, r1) of x0 only when given.  None when the device path does not apply (the caller
-    runs dot_cross)."""
+    each share's residues once and reads them for both K halves.  Rows [r0, r1) of x0 only
+    when given.  None when the device path does not apply (the caller runs dot_cross)."""
     d0 = x0.data
     if not d0.is_cuda or len(x0.shape) != 3:
         return None
@@ -860,24 +857,14 @@ def dot_cross_pair(x0: RT, y0: RT, y1: RT, roll: int, pb: PreparedCross = None, 
         b0, b1 = y0.data.contiguous(), y1.data.contiguous()
         lb = None
     out = empty((batch, r1 - r0, N), bits, d0.device)
-    b3 = y_rolled and b1 is not None and _B3
     rc = nat.lib().mx_gemm_roll(
         _words(bits), batch, r1 - r0, N, K, ctypes.c_void_p(d0.data_ptr() + r0 * K * el * 8),
-        M * K, roll, None if b0 is None else nat.ptr(b0),
-        None if (b1 is None or b3) else nat.ptr(b1), lb, nat.ptr(out.data), 0,
-        nat.stream_of(d0))
-    if rc == -7 and b3:  # the one-share B' does not apply here: both shares
-        rc = nat.lib().mx_gemm_roll(
-            _words(bits), batch, r1 - r0, N, K,
-            ctypes.c_void_p(d0.data_ptr() + r0 * K * el * 8), M * K, roll, nat.ptr(b0),
-            nat.ptr(b1), lb, nat.ptr(out.data), 0, nat.stream_of(d0))
+        M * K, roll, None if b0 is None else nat.ptr(b0), None if b1 is None else nat.ptr(b1),
+        lb, nat.ptr(out.data), 0, nat.stream_of(d0))
     if rc == -7:
         return None
     nat.check(rc, "gemm_roll")
     return out
-
-
-_B3 = os.environ.get("MOOSEX_CRT_B3", "1") != "0"
 
 
 def _party_batch_strides(t: RT):

@@ -587,7 +587,7 @@ class StackedSession(Session):
                 cache[key] = (yv0.data, yv1.data, None)  # holds the tensors: ids stay unique
         if (nbatch == 0 and self.pair_rolled and self.device.type == "cuda"
                 and len(yv0.shape) == 3):
-            v = R.dot_cross_pair(x0.v, yv0, yv1, 1, y_rolled=True)
+            v = R.dot_cross_pair(x0.v, yv0, yv1, 1)
             if v is not None:
                 return PV(plc, v)
         return PV(plc, R.dot_cross(x0.v, x1.v, y0.v, y1.v, nb=1 + nbatch))

@@ -336,28 +336,3 @@ def test_gpu_crt_bench_tiling_matches_limb_gemm(variant, monkeypatch):
     same(want, got)
     assert rolled is not None
     same(want, rolled)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("bits", [64, 128])
-@pytest.mark.parametrize("fill", [None, "max", "min"])
-def test_gpu_dot_cross_pair_one_share_b(bits, fill):
-    """Both operands stacked RSS pairs (x1, y1 = x0, y0 rolled by one party): the B' image
-    built from each y share's residues once (k_crt_prep_b3: the top half re-centres
-    R_b + R_b+1 with the ring sum's signed overflow) gives bitwise the product of the
-    two-operand form.  Random shares overflow the ring sum about a quarter of the time;
-    all-max / all-min shares overflow it everywhere.  N not a multiple of the tile."""
-    M, K, N = 300, 320, 280
-    x0 = gpu(rand_rt((3, M, K), bits, 120))
-    x1 = R.RT(torch.roll(x0.data, -1, dims=0).contiguous(), bits)
-    if fill is None:
-        y0 = gpu(rand_rt((3, K, N), bits, 121))
-    else:
-        v = (1 << (bits - 1)) - 1 if fill == "max" else 1 << (bits - 1)
-        y0 = R.fill((3, K, N), v, bits, torch.device("cuda"))
-    y1 = R.RT(torch.roll(y0.data, -1, dims=0).contiguous(), bits)
-    with _crt(1):
-        want = R.dot_cross(x0, x1, y0, y1, nb=1)
-        got = R.dot_cross_pair(x0, y0, y1, 1, y_rolled=True)
-    assert got is not None
-    same(want, got)
