@@ -250,10 +250,36 @@ __device__ __forceinline__ int residue(const uint32_t (&x)[NW], const uint32_t (
   return (int)__builtin_fmaf(-qt, p, fs);      // in [-(p-1)/2, (p-1)/2]
 }
 
+// Two residues at once: the fp32 scaling and the multiply-subtract as packed instructions
+// (v_pk_mul_f32, v_pk_fma_f32: one issue for both elements); the same values as residue().
+typedef float f2 __attribute__((ext_vector_type(2)));
+template <int NW>
+__device__ __forceinline__ void residue2(const uint32_t (&xa)[NW], const uint32_t (&xb)[NW],
+                                         const uint32_t (&w)[4], uint32_t neg, float p,
+                                         float rcp, int& ra, int& rb) {
+  uint32_t sa = 0, sb = 0;
+#pragma unroll
+  for (int q = 0; q < NW; ++q) {
+    sa = __builtin_amdgcn_udot4(xa[q], w[q], sa, false);
+    sb = __builtin_amdgcn_udot4(xb[q], w[q], sb, false);
+  }
+  // the negative-element correction as one packed fma (the signs are per element, hoisted
+  // out of the modulus loop): exact, the sum stays below 2^21
+  const f2 sg = {(float)(xa[NW - 1] >> 31), (float)(xb[NW - 1] >> 31)};
+  const float nf = (float)neg;
+  const f2 fs = __builtin_elementwise_fma(sg, (f2){nf, nf}, (f2){(float)sa, (float)sb});
+  f2 qt = fs * (f2){rcp, rcp};
+  qt.x = __builtin_rintf(qt.x);
+  qt.y = __builtin_rintf(qt.y);
+  const f2 r = __builtin_elementwise_fma(-qt, (f2){p, p}, fs);
+  ra = (int)r.x;
+  rb = (int)r.y;
+}
+
 // One thread = (tile, k-step, image row r, 16-byte chunk c) of every residue plane.
 // TRANS = false: A' rows are M rows of [A0 | A1] (row-major [R][K] per batch, batch stride
 // xs elements).  TRANS = true: B' rows are the N columns of [B0 + B1 ; B0] ([K][R]).
-template <class T, bool TRANS, int ROWS>
+template <class T, bool TRANS, int ROWS, bool PK = true>
 __global__ void __launch_bounds__(256)
     k_crt_prep(const T* __restrict__ X0, const T* __restrict__ X1, int64_t R, int64_t K,
                int64_t xs, int mode, int8_t* __restrict__ out, int64_t tiles, int64_t nkb,
@@ -307,7 +333,12 @@ __global__ void __launch_bounds__(256)
       const float p = (float)tab.p[i], rcp = tab.rcp[i];
       int rr[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) rr[j] = residue<NW>(v[j], w, neg, p, rcp);
+      if constexpr (PK) {
+        for (int j = 0; j < 16; j += 2)
+          residue2<NW>(v[j], v[j + 1], w, neg, p, rcp, rr[j], rr[j + 1]);
+      } else {
+        for (int j = 0; j < 16; ++j) rr[j] = residue<NW>(v[j], w, neg, p, rcp);
+      }
       v4i o;
 #pragma unroll
       for (int u = 0; u < 4; ++u) o[u] = (int)pack4(rr[4 * u], rr[4 * u + 1], rr[4 * u + 2], rr[4 * u + 3]);
@@ -1036,6 +1067,14 @@ int gemm_group_m() {
   return v >= 1 && v <= 64 ? v : 4;
 }
 
+bool prep_packed() {
+  static const bool v = [] {
+    const char* e = std::getenv("MOOSEX_CRT_PACKED");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 template <class T>
 void launch_prep(const CPlan& p, const Tables& tb, bool is_b, int64_t batch, int64_t R,
                  int64_t K, int64_t xs, const T* X0, const T* X1, int mode, int8_t* out,
@@ -1045,6 +1084,18 @@ void launch_prep(const CPlan& p, const Tables& tb, bool is_b, int64_t batch, int
   const int rows = is_b ? p.bn : BM;
   const int64_t work = tiles * nkb * (rows * 4);
   const dim3 grid((unsigned)std::min<int64_t>((work + 255) / 256, 16384), (unsigned)batch);
+  if (!prep_packed()) {  // MOOSEX_CRT_PACKED=0: one residue at a time (A/B reference)
+    if (!is_b)
+      hipLaunchKernelGGL((k_crt_prep<T, false, BM, false>), grid, dim3(256), 0, st, X0, X1, R, K,
+                         xs, mode, out, tiles, nkb, tb.pa);
+    else if (rows == 256)
+      hipLaunchKernelGGL((k_crt_prep<T, true, 256, false>), grid, dim3(256), 0, st, X0, X1, R, K,
+                         xs, mode, out, tiles, nkb, tb.pb);
+    else
+      hipLaunchKernelGGL((k_crt_prep<T, true, 128, false>), grid, dim3(256), 0, st, X0, X1, R, K,
+                         xs, mode, out, tiles, nkb, tb.pb);
+    return;
+  }
   if (!is_b)
     hipLaunchKernelGGL((k_crt_prep<T, false, BM>), grid, dim3(256), 0, st, X0, X1, R, K, xs, mode,
                        out, tiles, nkb, tb.pa);
