@@ -332,11 +332,12 @@ __global__ void __launch_bounds__(256)
       const uint32_t neg = tab.neg[i];
       const float p = (float)tab.p[i], rcp = tab.rcp[i];
       int rr[16];
-#pragma unroll
       if constexpr (PK) {
+#pragma unroll
         for (int j = 0; j < 16; j += 2)
           residue2<NW>(v[j], v[j + 1], w, neg, p, rcp, rr[j], rr[j + 1]);
       } else {
+#pragma unroll
         for (int j = 0; j < 16; ++j) rr[j] = residue<NW>(v[j], w, neg, p, rcp);
       }
       v4i o;
