@@ -1085,7 +1085,9 @@ void launch_prep(const CPlan& p, const Tables& tb, bool is_b, int64_t batch, int
   const int rows = is_b ? p.bn : BM;
   const int64_t work = tiles * nkb * (rows * 4);
   const dim3 grid((unsigned)std::min<int64_t>((work + 255) / 256, 16384), (unsigned)batch);
-  if (!prep_packed()) {  // MOOSEX_CRT_PACKED=0: one residue at a time (A/B reference)
+  // packed residues pay on A' (0.626 -> 0.592 ms at 4096^2) but not on the B' image, which
+  // streams 1.5x the bytes and loses more to the extra VGPRs (1.128 -> 1.163 ms)
+  if (!prep_packed() || is_b) {  // MOOSEX_CRT_PACKED=0: one residue at a time everywhere
     if (!is_b)
       hipLaunchKernelGGL((k_crt_prep<T, false, BM, false>), grid, dim3(256), 0, st, X0, X1, R, K,
                          xs, mode, out, tiles, nkb, tb.pa);

@@ -154,19 +154,18 @@ class ThreadTransport:
                                                  val[1]))
         elif kind == "t":
             self.log.setdefault(src, []).append(("t", tuple(val.shape), val.dtype, None))
-        else:
-            self.log.setdefault(src, []).append(("v", None, None, None))
+        else:  # a host value (a shape, a scalar): replayed as recorded, like a plan header
+            self.log.setdefault(src, []).append(("v", val, None, None))
 
     # -- typed values ------------------------------------------------------------------
     def send(self, v, dst: int):
         if self.tape is not None:
             if isinstance(v, R.RT):
                 v = v.data
-            if not isinstance(v, torch.Tensor):
-                from moose_amd.runtime.graphs import CaptureError
-
-                raise CaptureError(f"a host value ({type(v).__name__}) in the message flow")
-            self._taped([(v, dst)], [])
+            if isinstance(v, torch.Tensor):
+                self._taped([(v, dst)], [])
+            # a host value (shape, scalar) is not sent: the receiver replays the value it
+            # recorded in the warm-up, as Transport replays a message plan's header
             return
         if isinstance(v, R.RT):
             y, ev = self._ship(v.data, dst)
@@ -181,9 +180,7 @@ class ThreadTransport:
         if self.tape is not None:
             kind, shape, dtype, bits = self._next_logged(src)
             if kind == "v":
-                from moose_amd.runtime.graphs import CaptureError
-
-                raise CaptureError("a host value in the message flow")
+                return shape  # the recorded host value
             buf = torch.empty(shape, dtype=dtype, device=self.device)
             self._taped([], [(buf, src)])
             data = buf if device is None else buf.to(device)
