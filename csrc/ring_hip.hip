@@ -895,20 +895,21 @@ __global__ void __launch_bounds__(256) k_prf_expand(T* __restrict__ out, int64_t
 }
 
 // Reference (VALU) ring GEMM: 16x16 output tile per block, K staged through LDS.
+// a_bs / b_bs: batch strides in elements (0: one operand broadcast over the batch).
 template <class T, int TS>
 __global__ void __launch_bounds__(256) k_gemm_valu(int64_t M, int64_t N, int64_t K, const T* __restrict__ A0,
                             const T* __restrict__ A1, const T* __restrict__ B0,
                             const T* __restrict__ B1, int mode, T* __restrict__ C,
-                            int accumulate) {
+                            int accumulate, int64_t a_bs, int64_t b_bs) {
   __shared__ T As[TS][TS + 1];
   __shared__ T Bs[TS][TS + 1];
   const int64_t b = blockIdx.z;
   const int64_t row = blockIdx.y * TS + threadIdx.y;
   const int64_t col = blockIdx.x * TS + threadIdx.x;
-  const T* a0 = A0 + b * M * K;
-  const T* b0 = B0 + b * K * N;
-  const T* a1 = mode ? A1 + b * M * K : nullptr;
-  const T* b1 = mode ? B1 + b * K * N : nullptr;
+  const T* a0 = A0 + b * a_bs;
+  const T* b0 = B0 + b * b_bs;
+  const T* a1 = mode ? A1 + b * a_bs : nullptr;
+  const T* b1 = mode ? B1 + b * b_bs : nullptr;
   T acc = 0;
   const int passes = mode ? 2 : 1;
   for (int pass = 0; pass < passes; ++pass) {
@@ -937,12 +938,13 @@ __global__ void __launch_bounds__(256) k_gemm_valu(int64_t M, int64_t N, int64_t
 template <class T>
 int launch_gemm_valu(int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
                      const void* A1, const void* B0, const void* B1, int mode, void* C,
-                     int accumulate, hipStream_t st) {
+                     int accumulate, hipStream_t st, int64_t a_bs = -1, int64_t b_bs = -1) {
   constexpr int TS = 16;
   dim3 grid((unsigned)((N + TS - 1) / TS), (unsigned)((M + TS - 1) / TS), (unsigned)batch);
   dim3 block(TS, TS);
   hipLaunchKernelGGL((k_gemm_valu<T, TS>), grid, block, 0, st, M, N, K, (const T*)A0,
-                     (const T*)A1, (const T*)B0, (const T*)B1, mode, (T*)C, accumulate);
+                     (const T*)A1, (const T*)B0, (const T*)B1, mode, (T*)C, accumulate,
+                     a_bs < 0 ? M * K : a_bs, b_bs < 0 ? K * N : b_bs);
   MX_LAUNCH_CHECK();
   return 0;
 }
@@ -1530,6 +1532,29 @@ int mxh_gemm(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const vo
   if (words == 2)
     return launch_gemm_valu<u128>(batch, M, N, K, A0, A1, B0, B1, mode, C, accumulate,
                                   S(stream));
+  return -2;
+}
+
+// Plain batched product with explicit batch strides (elements; 0 broadcasts an operand):
+// the small-product (VALU) kernel, or the strided MFMA/CRT GEMM for large ones.
+extern "C" int mx_gemm_strided(int words, int64_t batch, int64_t M, int64_t N, int64_t K,
+                               const void* A0, const void* A1, int64_t a_bstride, const void* B0,
+                               const void* B1, int64_t b_bstride, int mode, void* C,
+                               int accumulate, void* stream);
+
+int mxh_gemm_bs(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
+                int64_t a_bs, const void* B0, int64_t b_bs, void* C, void* stream) {
+  if (M == 0 || N == 0 || batch == 0) return 0;
+  const bool big = M >= 64 && N >= 64 && K >= 32;
+  if (big && g_gemm_impl != 1)
+    return mx_gemm_strided(words, batch, M, N, K, A0, nullptr, a_bs, B0, nullptr, b_bs, 0, C, 0,
+                           stream);
+  if (words == 1)
+    return launch_gemm_valu<u64>(batch, M, N, K, A0, nullptr, B0, nullptr, 0, C, 0, S(stream),
+                                 a_bs, b_bs);
+  if (words == 2)
+    return launch_gemm_valu<u128>(batch, M, N, K, A0, nullptr, B0, nullptr, 0, C, 0, S(stream),
+                                  a_bs, b_bs);
   return -2;
 }
 

@@ -78,6 +78,9 @@ _SIGS = {
         [c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_int, c_vp,
          c_int, c_vp],
     ),
+    "mxh_gemm_bs": (
+        c_int, [c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp],
+    ),
     "mx_crt_moduli": (c_int, [c_int, c_i64]),
     "mx_crt_tables": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mx_trunc_pr3": (

@@ -742,6 +742,38 @@ def _gemm_call(bits, batch, M, N, K, a0, a1, b0, b1, mode, out, accumulate=0):
     )
 
 
+def dot_slots(x: RT, c: RT):
+    """x[b] . c for every slot b of a device ring tensor x [B, M, K] (or [B, K]) whose slots
+    may be any evenly strided views (e.g. the four slots of a share-pair ring buffer) and a
+    public operand c [K, N] (or [K]) read by every slot in place -- one launch, no copy of
+    c per slot.  None when the layout does not fit (the caller runs R.dot)."""
+    d, cd = x.data, c.data
+    if (not d.is_cuda or cd.device != d.device or x.bits not in (64, 128)
+            or c.bits != x.bits):
+        return None
+    el = 2 if x.bits == 128 else 1
+    xl, cl = tuple(x.shape[1:]), tuple(c.shape)
+    if len(xl) == 2 and len(cl) == 2:
+        M, K, N, oshape = xl[0], xl[1], cl[1], (xl[0], cl[1])
+    elif len(xl) == 2 and len(cl) == 1:
+        M, K, N, oshape = xl[0], xl[1], 1, (xl[0],)
+    elif len(xl) == 1 and len(cl) == 2:
+        M, K, N, oshape = 1, xl[0], cl[1], (cl[1],)
+    else:
+        return None
+    if cl[0] != K or d.stride(0) % el:
+        return None
+    inner = d[0]
+    if not inner.is_contiguous() or not cd.is_contiguous():
+        return None
+    B = d.shape[0]
+    out = empty((B,) + oshape, x.bits, d.device)
+    nat.check(nat.lib().mxh_gemm_bs(_words(x.bits), B, M, N, K, nat.ptr(d), d.stride(0) // el,
+                                    nat.ptr(cd), 0, nat.ptr(out.data), nat.stream_of(d)),
+              "ring gemm (slots)")
+    return out
+
+
 def _kslice_rows(t, batch, M, K, k0, k1, bits):
     v = t.reshape(batch, M, K, -1) if bits == 128 else t.reshape(batch, M, K)
     return v[:, :, k0:k1].contiguous()

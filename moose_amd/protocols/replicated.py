@@ -295,6 +295,11 @@ def mul_public(sess, x: RepTensor, c) -> RepTensor:
 
 def dot_public(sess, x: RepTensor, c, public_left=False) -> RepTensor:
     pc = sess.public(x.plc, c)
+    pair = getattr(sess, "p_dot_public_pair", None)
+    if pair is not None and not public_left:
+        r = pair(x.plc, x.s0, x.s1, pc)
+        if r is not None:
+            return RepTensor(x.plc, x.bits, x.kind, r[0], r[1])
     if public_left:
         return RepTensor(x.plc, x.bits, x.kind, sess.p("Dot", x.plc, pc, x.s0),
                          sess.p("Dot", x.plc, pc, x.s1))

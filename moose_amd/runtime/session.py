@@ -287,6 +287,32 @@ class StackedSession(Session):
         o0, o1 = R.binary2(op, v0, w[0], v1, w[1])
         return PV(plc, o0), PV(plc, o1)
 
+    def p_dot_public_pair(self, plc, x0, x1, c):
+        """rep.dot_public (x . c, c public) for both share vectors: when they are the two
+        views of one share-pair ring buffer (s0 = buf[0:3], s1 = buf[1:4]), ONE product of
+        the buffer's four slots with c, read in place by every slot, whose result is again
+        a ring buffer; otherwise one launch per share vector, still without copying c per
+        party.  None -> the generic path."""
+        v0, v1, cv = x0.v, x1.v, c.v
+        if not (isinstance(v0, R.RT) and isinstance(v1, R.RT) and isinstance(cv, R.RT)):
+            return None
+        if self.device.type != "cuda" or v0.bits not in (64, 128) or cv.bits != v0.bits:
+            return None
+        d0, d1 = v0.data, v1.data
+        el = 2 if v0.bits == 128 else 1
+        if (d0.dim() >= 2 and d0.shape == d1.shape and d0.stride() == d1.stride()
+                and d0.shape[0] == 3
+                and d1.data_ptr() - d0.data_ptr() == d0.stride(0) * d0.element_size()
+                and d0.stride(0) % el == 0):
+            buf = R.RT(d0.as_strided((4,) + tuple(d0.shape[1:]), d0.stride()), v0.bits)
+            o = R.dot_slots(buf, cv)
+            if o is not None:
+                return PV(plc, R.RT(o.data[0:3], o.bits)), PV(plc, R.RT(o.data[1:4], o.bits))
+        o0, o1 = R.dot_slots(v0, cv), R.dot_slots(v1, cv)
+        if o0 is None or o1 is None:
+            return None
+        return PV(plc, o0), PV(plc, o1)
+
     def p_from_slot_holders(self, plc, slot, x_h0, x_h1, like):
         """rep.from_slot_holders in one kernel (None -> generic path)."""
         v0, v1 = x_h0.v, x_h1.v

@@ -219,3 +219,29 @@ def test_share_pair_ring_buffer(dev, bits):
         R._RING4 = True
     _eq(u0.v, t0.v)
     _eq(u1.v, t1.v)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [64, 128])
+@pytest.mark.parametrize("shapes", [((200, 10), (10, 2)), ((200, 10), (10,)), ((10,), (10, 3)),
+                                    ((300, 96), (96, 80))])
+def test_dot_public_pair_one_launch(bits, shapes):
+    """rep.dot_public on a share-pair ring buffer: one product of the buffer's four slots
+    with the public operand read in place (small: the VALU kernel, large: the strided
+    GEMM); bitwise the per-share products, and the result is again a ring buffer."""
+    xs, cs = shapes
+    buf = _rand((4,) + xs, bits, "cuda", 1)
+    buf.data[3].copy_(buf.data[0])  # ring buffer: slot 3 = slot 0
+    s0, s1 = R.RT(buf.data[0:3], bits), R.RT(buf.data[1:4], bits)
+    c = _rand(cs, bits, "cuda", 2)
+    sess = StackedSession("cuda", seed=1)
+    r = sess.p_dot_public_pair(None, PV(None, s0), PV(None, s1), type("P", (), {"v": c})())
+    assert r is not None
+    want0 = R.dot(s0, R.RT(c.data.unsqueeze(0).expand((3,) + tuple(c.data.shape)).contiguous(),
+                           bits), nb=1)
+    want1 = R.dot(s1, R.RT(c.data.unsqueeze(0).expand((3,) + tuple(c.data.shape)).contiguous(),
+                           bits), nb=1)
+    _eq(r[0].v, want0)
+    _eq(r[1].v, want1)
+    assert r[1].v.data.data_ptr() - r[0].v.data.data_ptr() == \
+        r[0].v.data.stride(0) * r[0].v.data.element_size()
