@@ -1,0 +1,79 @@
+// One hipGraph for a whole multi-party evaluation (moose_amd/parallel/threads.py PartyTapes).
+//
+// Each party's evaluation was captured as hipGraph segments between its message rounds;
+// the rounds of all parties were matched into sends and receives.  Here the segments become
+// child-graph nodes and every message a device-to-device memcpy node, with the edges the
+// protocol implies:
+//   * a party's nodes in program order (segment -> its round's receive copies -> the next
+//     segment), so a landing buffer is overwritten only after the receiver's earlier work;
+//   * a receive copy after the sender's segment that produced the message.
+// The composed graph is instantiated once; a replay is ONE hipGraphLaunch for all parties,
+// and independent branches (different parties' segments between their rounds) may run
+// concurrently inside it -- the dataflow the host-side interleaving only approximated.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+extern "C" {
+
+// n nodes in a topological order.  kind[i] = 0: a child graph (child[i], a hipGraph_t);
+// kind[i] = 1: a device-to-device copy of bytes[i] from src[i] to dst[i].  The
+// dependencies of node i are deps[dep_off[i] .. dep_off[i + 1]) (indices < i).
+// Returns 0 and the graph / its executable, or a negative code (nothing is leaked).
+int mx_graph_compose(int n, const int* kind, void* const* child, void* const* dst,
+                     void* const* src, const int64_t* bytes, const int* dep_off,
+                     const int* deps, void** graph_out, void** exec_out) {
+  if (n < 1) return -2;
+  hipGraph_t g = nullptr;
+  if (hipGraphCreate(&g, 0) != hipSuccess) return -3;
+  std::vector<hipGraphNode_t> nodes((size_t)n, nullptr);
+  std::vector<hipGraphNode_t> d;
+  for (int i = 0; i < n; ++i) {
+    d.clear();
+    for (int e = dep_off[i]; e < dep_off[i + 1]; ++e) {
+      const int j = deps[e];
+      if (j < 0 || j >= i) {
+        hipGraphDestroy(g);
+        return -4;
+      }
+      d.push_back(nodes[(size_t)j]);
+    }
+    hipError_t rc;
+    size_t count = 0;
+    if (kind[i] == 0 && hipGraphGetNodes((hipGraph_t)child[i], nullptr, &count) == hipSuccess &&
+        count == 0)  // a segment that launched nothing: keep its place in the order
+      rc = hipGraphAddEmptyNode(&nodes[(size_t)i], g, d.data(), d.size());
+    else if (kind[i] == 0)
+      rc = hipGraphAddChildGraphNode(&nodes[(size_t)i], g, d.data(), d.size(),
+                                     (hipGraph_t)child[i]);
+    else
+      rc = hipGraphAddMemcpyNode1D(&nodes[(size_t)i], g, d.data(), d.size(), dst[i], src[i],
+                                   (size_t)bytes[i], hipMemcpyDeviceToDevice);
+    if (rc != hipSuccess) {
+      hipGraphDestroy(g);
+      return -10 - i;
+    }
+  }
+  hipGraphExec_t ex = nullptr;
+  if (hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) != hipSuccess) {
+    hipGraphDestroy(g);
+    return -5;
+  }
+  *graph_out = (void*)g;
+  *exec_out = (void*)ex;
+  return 0;
+}
+
+int mx_graph_launch(void* exec, void* stream) {
+  return hipGraphLaunch((hipGraphExec_t)exec, (hipStream_t)stream) == hipSuccess ? 0 : -1;
+}
+
+int mx_graph_free(void* graph, void* exec) {
+  int rc = 0;
+  if (exec && hipGraphExecDestroy((hipGraphExec_t)exec) != hipSuccess) rc = -1;
+  if (graph && hipGraphDestroy((hipGraph_t)graph) != hipSuccess) rc = -1;
+  return rc;
+}
+
+}  // extern "C"

@@ -178,6 +178,9 @@ _SIGS = {
     "mx_copy_channels": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp]),
     "mx_stream_cumask": (c_int, [c_vp, c_int, c_vp]),
     "mx_stream_destroy": (c_int, [c_vp]),
+    "mx_graph_compose": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mx_graph_launch": (c_int, [c_vp, c_vp]),
+    "mx_graph_free": (c_int, [c_vp, c_vp]),
     "mx_gemm_roll": (
         c_int,
         [c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_int,

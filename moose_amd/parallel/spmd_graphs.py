@@ -53,11 +53,13 @@ class SPMDTape:
     """One recorded SPMD evaluation of this process (module doc)."""
 
     def __init__(self, comp, arguments: dict, identity: str, role_ranks: Dict[str, int],
-                 tr, device, storage, ring: int, seed: Optional[int] = None, warm=None):
+                 tr, device, storage, ring: int, seed: Optional[int] = None, warm=None,
+                 keep_graph: bool = False):
         """``warm``: the warm-up already ran elsewhere (the in-process parties of
         parallel/threads.py run it together, on threads) -- a dict with the recorded
         ``uploads``, the ``first`` outputs, the session ``stats`` and the number of key
-        slots ``keys_n`` it used."""
+        slots ``keys_n`` it used.  ``keep_graph``: the segments keep their hipGraph (not
+        instantiated until a replay) so a caller can compose them into a larger graph."""
         from moose_amd.parallel.spmd import SPMDSession
 
         self.comp, self.device, self.tr = comp, torch.device(device), tr
@@ -100,7 +102,7 @@ class SPMDTape:
         state = {"g": None, "n": 0}
 
         def begin():
-            g = torch.cuda.CUDAGraph()
+            g = torch.cuda.CUDAGraph(keep_graph=keep_graph)
             g.capture_begin(pool=pool, capture_error_mode="thread_local")
             state["g"], state["n"] = g, 0
 

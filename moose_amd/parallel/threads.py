@@ -23,6 +23,7 @@ additionally be pinned to different MI355Xs (SURVEY §7.1 "3 parties on 1 or 3 G
 """
 from __future__ import annotations
 
+import os
 import queue
 import threading
 from typing import Dict
@@ -359,6 +360,9 @@ class PartyTapes:
         self.devices = [torch.device(d) for d in devices]
         n = len(identities)
         role_ranks = {r: i for i, r in enumerate(identities)}
+        # every party on one device: the tapes are composed into ONE graph (below)
+        single = (len(set(self.devices)) == 1
+                  and os.environ.get("MOOSEX_PARTY_GRAPH", "1") != "0")
         self.tapes = []
         for i, ident in enumerate(identities):
             tr = ThreadTransport(i, None, device=self.devices[i], world=n)
@@ -366,7 +370,7 @@ class PartyTapes:
             with torch.cuda.device(self.devices[i]):
                 self.tapes.append(SPMDTape(comp, arguments, ident, role_ranks, tr,
                                            self.devices[i], storage, ring, seed,
-                                           warm=warm[ident]))
+                                           warm=warm[ident], keep_graph=single))
         self.streams = [t.stream for t in self.tapes]
         self._copy_streams = {}
         self.actions = self._schedule()
@@ -374,6 +378,69 @@ class PartyTapes:
         self.segments = sum(t.segments for t in self.tapes)
         self._ends = None
         self.issue_s = []
+        self._composed = self._compose() if single else None
+
+    def _compose(self):
+        """The schedule as ONE hipGraph (csrc/graph_compose.hip): each segment a child
+        graph, each message a device-to-device memcpy node, edges for program order and for
+        send -> receive.  None when the runtime declines (the per-action replay is used)."""
+        import ctypes
+
+        from moose_amd.ops import native as nat
+
+        n = len(self.tapes)
+        kinds, child, dst, src, nbytes, deps = [], [], [], [], [], []
+        last = [None] * n
+        sent_at = {}
+        for a in self.actions:
+            p = a[1]
+            if a[0] == "g":
+                kinds.append(0)
+                child.append(a[2].raw_cuda_graph())
+                dst.append(0)
+                src.append(0)
+                nbytes.append(0)
+                deps.append([last[p]] if last[p] is not None else [])
+                last[p] = len(kinds) - 1
+            elif a[0] == "rec":
+                sent_at[id(a[2])] = last[p]
+            else:
+                _, p, s, t, buf, ev = a
+                d = [x for x in (last[p], sent_at.get(id(ev))) if x is not None]
+                kinds.append(1)
+                child.append(0)
+                dst.append(buf.data_ptr())
+                src.append(t.data_ptr())
+                nbytes.append(t.numel() * t.element_size())
+                deps.append(sorted(set(d)))
+                last[p] = len(kinds) - 1
+        m = len(kinds)
+        off = [0]
+        flat = []
+        for d in deps:
+            flat += d
+            off.append(len(flat))
+        arr = lambda ty, xs: (ty * max(1, len(xs)))(*xs)  # noqa: E731
+        g, ex = ctypes.c_void_p(), ctypes.c_void_p()
+        rc = nat.lib().mx_graph_compose(
+            m, arr(ctypes.c_int, kinds), arr(ctypes.c_void_p, child),
+            arr(ctypes.c_void_p, dst), arr(ctypes.c_void_p, src),
+            arr(ctypes.c_int64, nbytes), arr(ctypes.c_int, off), arr(ctypes.c_int, flat),
+            ctypes.byref(g), ctypes.byref(ex))
+        if rc != 0:
+            return None
+        self._graph_handles = (g, ex)
+        return ex
+
+    def __del__(self):
+        h = getattr(self, "_graph_handles", None)
+        if h is not None:
+            try:
+                from moose_amd.ops import native as nat
+
+                nat.lib().mx_graph_free(h[0], h[1])
+            except Exception:  # noqa: BLE001 - interpreter shutdown
+                pass
 
     def _copy_stream(self, dev):
         s = self._copy_streams.get(dev)
@@ -439,6 +506,8 @@ class PartyTapes:
 
         import numpy as np
 
+        if self._composed is not None:
+            return self._replay_composed(arguments)
         n = len(self.tapes)
         prev_dev = torch.cuda.current_device()
         prev = [torch.cuda.current_stream(d) for d in set(self.devices)]
@@ -499,3 +568,36 @@ class PartyTapes:
                 torch.cuda.set_stream(s)
             torch.cuda.set_device(prev_dev)
         return out
+
+    def _replay_composed(self, arguments: dict) -> Dict[str, dict]:
+        """One launch of the composed graph on the first party's stream, after every
+        party's arguments and fresh keys were written on that same stream."""
+        import time
+
+        from moose_amd.ops import native as nat
+
+        s = self.streams[0]
+        t0 = time.perf_counter()
+        with torch.cuda.stream(s):
+            for tape in self.tapes:
+                _copy_arguments(tape, arguments)
+                tape._fill_keys()
+            nat.check(nat.lib().mx_graph_launch(self._composed, s.cuda_stream), "graph launch")
+            self.issue_s.append(time.perf_counter() - t0)
+            out = {}
+            for p, tape in enumerate(self.tapes):
+                out[self.identities[p]] = tape._decode(tape.interp, tape.sess, tape.outs)
+                tape.replays += 1
+        return out
+
+
+def _copy_arguments(tape, arguments):
+    import numpy as np
+
+    for k, v in arguments.items():
+        t = tape.static.get(k)
+        if isinstance(t, torch.Tensor):
+            a = np.asarray(v)
+            a = a.view(np.int64) if a.dtype == np.uint64 else a
+            src = torch.from_numpy(np.ascontiguousarray(a).reshape(t.shape))
+            t.copy_(src if src.dtype == t.dtype else src.to(t.dtype))
