@@ -138,9 +138,12 @@ def test_thread_parties_lr_inference_gpu(monkeypatch):
 
 
 @pytest.mark.gpu
-def test_thread_party_tapes_replay_bitwise_equal_eager():
+@pytest.mark.parametrize("composed", [True, False])
+def test_thread_party_tapes_replay_bitwise_equal_eager(composed, monkeypatch):
     """Seeded sessions: a replay re-draws the seeded keys as a fresh eager evaluation does,
-    so every replay's outputs equal the eager ones bitwise (parties on streams of cuda:0)."""
+    so every replay's outputs equal the eager ones bitwise (parties on cuda:0): the tapes
+    composed into one hipGraph (default on one device), and the per-action replay."""
+    monkeypatch.setenv("MOOSEX_PARTY_GRAPH", "1" if composed else "0")
     comp = _comp(False)
     args = _args()
     devs = {i: "cuda:0" for i in IDS}
@@ -154,6 +157,7 @@ def test_thread_party_tapes_replay_bitwise_equal_eager():
             assert np.array_equal(np.asarray(got[k]), np.asarray(want[k])), k
     (c, tapes), = rt._party_tapes.values()
     assert tapes is not False and tapes.tapes[0].replays == 2
+    assert (tapes._composed is not None) == composed
 
 
 def test_party_tapes_schedule_pairs_rounds():
