@@ -415,6 +415,8 @@ class PartyTapes:
                 deps.append(sorted(set(d)))
                 last[p] = len(kinds) - 1
         m = len(kinds)
+        if os.environ.get("MOOSEX_PARTY_GRAPH_SERIAL") == "1":  # debugging: a total order
+            deps = [sorted(set(d) | ({i - 1} if i else set())) for i, d in enumerate(deps)]
         off = [0]
         flat = []
         for d in deps:
