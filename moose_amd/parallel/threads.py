@@ -382,8 +382,9 @@ class PartyTapes:
 
     def _compose(self):
         """The schedule as ONE hipGraph (csrc/graph_compose.hip): each segment a child
-        graph, each message a device-to-device memcpy node, edges for program order and for
-        send -> receive.  None when the runtime declines (the per-action replay is used)."""
+        graph, each message a device-to-device memcpy node, in the issue order of the
+        per-action replay (MOOSEX_PARTY_GRAPH_DAG=1: only program-order and send -> receive
+        edges).  None when the runtime declines (the per-action replay is used)."""
         import ctypes
 
         from moose_amd.ops import native as nat
@@ -415,7 +416,10 @@ class PartyTapes:
                 deps.append(sorted(set(d)))
                 last[p] = len(kinds) - 1
         m = len(kinds)
-        if os.environ.get("MOOSEX_PARTY_GRAPH_SERIAL") == "1":  # debugging: a total order
+        if os.environ.get("MOOSEX_PARTY_GRAPH_DAG") != "1":
+            # the issue order as a total order (profiles/r4_party_graph.md: on one device
+            # the branchy DAG ran slower -- 5.0 vs 3.2 ms per LR inference -- and its
+            # replays did not reproduce the eager values, so it stays a debugging option)
             deps = [sorted(set(d) | ({i - 1} if i else set())) for i, d in enumerate(deps)]
         off = [0]
         flat = []
