@@ -170,6 +170,9 @@ def zeros(shape, bits, device) -> RT:
 
 
 _SCALARS = {}
+# set while several threads issue work on their own streams of one device (the in-process
+# parties, parallel/threads.py): a cached constant is then read by other streams too
+SHARED_STREAMS = False
 
 
 def _cache_put(cache, key, t, limit):
@@ -180,7 +183,7 @@ def _cache_put(cache, key, t, limit):
         return
     from moose_amd.runtime import lanes
 
-    if lanes.ACTIVE and t.data.is_cuda:
+    if (lanes.ACTIVE or SHARED_STREAMS) and t.data.is_cuda:
         torch.cuda.current_stream(t.data.device).synchronize()
     cache[key] = t
 

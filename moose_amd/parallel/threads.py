@@ -318,16 +318,17 @@ def run_parties(comp, arguments: dict, identities: List[str], devices: List, sto
 
     threads = [threading.Thread(target=party, args=(i,), name=f"moose-party-{identities[i]}",
                                 daemon=True) for i in range(len(identities))]
-    prev = R._UPLOAD_HOOK
+    prev, prev_shared = R._UPLOAD_HOOK, R.SHARED_STREAMS
     if hooks is not None:
         R._UPLOAD_HOOK = hooks
+    R.SHARED_STREAMS = True  # shared device constants: their producer drains first
     try:
         for t in threads:
             t.start()
         for t in threads:
             t.join()
     finally:
-        R._UPLOAD_HOOK = prev
+        R._UPLOAD_HOOK, R.SHARED_STREAMS = prev, prev_shared
     if errors:
         # the first party to fail is the cause; the others saw TransportError because of it
         first = next((e for e in errors.values() if not isinstance(e, TransportError)),
