@@ -478,7 +478,10 @@ def _lr_spmd(runs, world, rank, device, prog):
         g = groups[mine]
         tm = logistic_regression_tutorial(128)
         comp = to_native(tm.computation, 128)
-        tr = Transport(rank, world, device, plans=True)  # every rank holds every argument
+        # the session's own group: the tape's collective capture decision (spmd_graphs
+        # ._agree) must involve these three ranks only (ranks outside every triple, and
+        # the other triples, are not in this evaluation)
+        tr = Transport(rank, world, device, group=g, plans=True)  # every rank: every argument
         roles = {r: 3 * mine + i for i, r in enumerate(ROLES)}
         me = ROLES[rank % 3]
         bdev = [device.index] if device.type == "cuda" and dist.get_backend() == "nccl" else None

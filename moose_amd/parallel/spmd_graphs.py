@@ -221,7 +221,9 @@ def enabled(device) -> bool:
 
 
 def _agree(tr, ok: bool) -> bool:
-    """Every rank of the transport's group learns whether all of them succeeded."""
+    """Every rank of the transport's group learns whether all of them succeeded.  The
+    transport's group must be exactly the session's ranks (a transport on the default group
+    of a larger job would wait for ranks that are not in this evaluation)."""
     import torch.distributed as dist
 
     if tr.world <= 1:
