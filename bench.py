@@ -1071,9 +1071,17 @@ def _main(args, prog_out):
                                            if "p50_ms" in v}
             sp = lr.get("spmd_one_party_per_gpu")
             if sp:
-                best = sp.get("tape") if sp.get("tape", {}).get("replayed") else sp["eager"]
+                # the faster of the replayed tape and eager dispatch (both are in
+                # lr_inference.spmd_one_party_per_gpu; "spmd_mode" says which one this is)
+                cands = [("eager", sp["eager"])]
+                if sp.get("tape", {}).get("replayed"):
+                    cands.append(("tape", sp["tape"]))
+                mode, best = min(cands, key=lambda kv: kv[1]["p50_ms"])
                 line["lr_inference_p50_ms"]["spmd"] = best["p50_ms"]
                 line["lr_inference_p50_ms"]["spmd_eager"] = sp["eager"]["p50_ms"]
+                if "tape" in sp:
+                    line["lr_inference_p50_ms"]["spmd_tape"] = sp["tape"]["p50_ms"]
+                line["lr_inference_spmd_mode"] = mode
                 line["lr_inference_rounds"] = best["rounds"]
             line["lr_inference"] = lr
 
