@@ -414,8 +414,10 @@ def _lr_stacked(runs, device, world=1):
         modes.append("parties_3gpu")
     for mode in modes:
         flags = {"eager": {"use_graphs": False}, "graphs": {"use_graphs": True},
-                 "default": {}, "parties": {"device_map": {r: str(device) for r in ROLES}},
-                 "parties_3gpu": {"device_map": {r: str(d) for r, d in zip(ROLES, gpus3 or [])}},
+                 "default": {},
+                 "parties": {"device_map": {r: str(device) for r in ROLES}, "timeout": 30},
+                 "parties_3gpu": {"device_map": {r: str(d) for r, d in zip(ROLES, gpus3 or [])},
+                                  "timeout": 30},
                  }[mode]
         try:
             rt = LocalMooseRuntime(list(ROLES), device=device, fixedpoint_ring=128, **flags)
