@@ -417,7 +417,11 @@ def _poly_eval_rows(sess, x: RepFixed, coeffs, shift: int = 0) -> RepFixed:
     path, without the per-level slice/concat copies."""
     n = len(coeffs) - 1
     f, bits, t = x.frac, x.bits, x.t
-    P0, P1 = sess.p_rows_alloc(t.s0, n), sess.p_rows_alloc(t.s1, n)
+    pair = getattr(sess, "p_rows_alloc_pair", None)
+    if pair is not None:
+        P0, P1 = pair(t.s0, t.s1, n)
+    else:
+        P0, P1 = sess.p_rows_alloc(t.s0, n), sess.p_rows_alloc(t.s1, n)
     have = 1
     while have < n:
         m = min(2 * have, n) - have

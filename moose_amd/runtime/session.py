@@ -393,6 +393,24 @@ class StackedSession(Session):
         d[:, 0].copy_(v.data)
         return PV(x.plc, R.RT(d, v.bits))
 
+    def p_rows_alloc_pair(self, x0, x1, n):
+        """p_rows_alloc for both share vectors of a replicated value: when they are the two
+        views of one share-pair ring buffer, ONE [4, n, ...] ring stack whose row 0 is
+        filled by one copy of the buffer's four slots (P0 = stack[0:3], P1 = stack[1:4];
+        the kernels that write later rows see a ring pair and write four slots)."""
+        v0, v1 = x0.v, x1.v
+        d0, d1 = v0.data, v1.data
+        if (isinstance(v0, R.RT) and isinstance(v1, R.RT) and d0.dim() >= 1
+                and d0.shape == d1.shape and d0.stride() == d1.stride() and d0.shape[0] == 3
+                and d1.data_ptr() - d0.data_ptr() == d0.stride(0) * d0.element_size()
+                and d0[0].is_contiguous()
+                and d0.stride(0) == d0[0].numel()):
+            buf = d0.as_strided((4,) + tuple(d0.shape[1:]), d0.stride())
+            st = torch.empty((4, n) + tuple(d0.shape[1:]), dtype=d0.dtype, device=d0.device)
+            st[:, 0].copy_(buf)
+            return PV(x0.plc, R.RT(st[0:3], v0.bits)), PV(x1.plc, R.RT(st[1:4], v1.bits))
+        return self.p_rows_alloc(x0, n), self.p_rows_alloc(x1, n)
+
     def p_rows_view(self, x, r0, r1):
         return PV(x.plc, R.RT(x.v.data[:, r0:r1], x.v.bits))
 
