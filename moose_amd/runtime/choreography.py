@@ -93,14 +93,28 @@ class Worker:
         self._groups = {}  # (parties, replicas) -> replica / owner process groups
 
     def serve(self, max_sessions: Optional[int] = None, poll_s: float = 0.05) -> int:
+        """Run jobs until a shutdown job.  A pool started for one client
+        (``MOOSEX_CLIENT_PID``, DistributedMooseRuntime) also ends when that client is gone
+        -- it may exit without closing the pool -- and any worker ends when the store it
+        waits on is unreachable (rank 0, which hosts it, died)."""
+        client = int(os.environ.get("MOOSEX_CLIENT_PID", "0") or 0)
+        if client:
+            _die_with(client)
         n = 0
         while max_sessions is None or n < max_sessions:
             key = f"{PREFIX}/session/{n}"
             while True:  # block on the store (no polling latency per session)
+                t0 = time.monotonic()
                 try:
-                    self.store.wait([key], timedelta(seconds=max(poll_s, 30.0)))
+                    self.store.wait([key], timedelta(seconds=5.0 if client else 30.0))
                     break
-                except Exception:  # noqa: BLE001 - wait timed out: keep serving
+                except Exception:  # noqa: BLE001 - a timeout, or a dead store
+                    if client and not _alive(client):
+                        return 0
+                    if time.monotonic() - t0 < 1.0:  # failed at once: the store is gone
+                        if not _store_alive(self.store):
+                            return 0
+                        time.sleep(0.5)
                     continue
             job = valuecodec.loads(_get(self.store, key))
             n += 1
@@ -281,6 +295,32 @@ class ChoreographyClient:
     def shutdown(self):
         n = self.store.add(f"{PREFIX}/launch_count", 1) - 1
         self.store.set(f"{PREFIX}/session/{n}", valuecodec.dumps({"shutdown": True}))
+
+
+def _die_with(pid: int):
+    """Exit at once if the client ``pid`` (this process's parent) is already gone; the serve
+    loop checks again at every 5 s wait.  (No PR_SET_PDEATHSIG: it fires when the parent
+    THREAD that spawned the pool exits, which may be long before the client does.)"""
+    if not _alive(pid):
+        os._exit(0)
+
+
+def _alive(pid: int) -> bool:
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return True
+    return os.getppid() == pid
+
+
+def _store_alive(store) -> bool:
+    try:
+        store.check([f"{PREFIX}/alive"])
+        return True
+    except Exception:  # noqa: BLE001
+        return False
 
 
 def _plain_args(d):

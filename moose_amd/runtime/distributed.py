@@ -228,8 +228,9 @@ class DistributedMooseRuntime:
         env = dict(os.environ)
         for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT", "TORCHELASTIC_USE_AGENT_STORE"):
             env.pop(k, None)
+        # MOOSEX_CLIENT_PID: the pool ends with this process even if it never closes it
         env.update(WORLD_SIZE=str(n), MOOSEX_STORE=f"{self.master_addr}:{port}",
-                   HSA_ENABLE_IPC_MODE_LEGACY="0")
+                   HSA_ENABLE_IPC_MODE_LEGACY="0", MOOSEX_CLIENT_PID=str(os.getpid()))
         if self.session_timeout is not None:
             env["MOOSEX_SESSION_TIMEOUT"] = str(self.session_timeout)
         env.update(self.worker_env)

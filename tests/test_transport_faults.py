@@ -159,3 +159,45 @@ def test_spmd_load_with_changing_stored_shape():
             assert got.shape == shape
             np.testing.assert_allclose(got, x * x, atol=1e-4)
         assert rt.worker_spawns == 1
+
+
+_CLIENT = r"""
+import os, sys
+import numpy as np
+sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.join(os.getcwd(), "tests"))
+from moose_amd.runtime.distributed import DistributedMooseRuntime
+from test_transport_faults import _mul_comp, IDS
+rt = DistributedMooseRuntime(IDS, backend="gloo", timeout=180)
+rt.run_computation(_mul_comp(), {"x": np.array([1.0, 2.0])})
+print("PIDS", " ".join(str(p.pid) for p in rt._pool["procs"]), flush=True)
+os._exit(0)  # the client goes away without closing its pool
+"""
+
+
+def test_persistent_workers_end_with_their_client():
+    """A client that exits without close() leaves no workers behind: they notice their
+    parent is gone at their next wait (MOOSEX_CLIENT_PID) and exit."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", _CLIENT], cwd=root, capture_output=True,
+                         text=True, timeout=300)
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith("PIDS")]
+    assert line, out.stderr[-2000:]
+    pids = [int(p) for p in line[0].split()[1:]]
+    deadline = time.time() + 30
+    alive = pids
+    while alive and time.time() < deadline:
+        time.sleep(0.5)
+        alive = []
+        for p in pids:
+            try:
+                os.kill(p, 0)
+                with open(f"/proc/{p}/stat") as f:  # a zombie has exited
+                    if f.read().split(")")[-1].split()[0] != "Z":
+                        alive.append(p)
+            except (ProcessLookupError, FileNotFoundError):
+                pass
+    assert not alive, f"workers {alive} outlived their client"
