@@ -380,6 +380,14 @@ class DistributedMooseRuntime:
     def __exit__(self, *exc):
         self.close()
 
+    def __del__(self):
+        # a runtime dropped without close(): its pool must not outlive it (the workers also
+        # watch MOOSEX_CLIENT_PID, but only for the client process's exit)
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
     def _launch(self, comp: Computation, arguments: dict):
         R = self.replicas
         n = len(self.identities) * R

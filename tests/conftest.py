@@ -29,3 +29,19 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _close_distributed_runtimes():
+    """Every DistributedMooseRuntime a test made is closed after it (their worker pools
+    would otherwise run until the test process exits)."""
+    yield
+    try:
+        from moose_amd.runtime import distributed
+    except Exception:  # noqa: BLE001
+        return
+    for rt in list(distributed._LIVE):
+        try:
+            rt.close()
+        except Exception:  # noqa: BLE001
+            pass
