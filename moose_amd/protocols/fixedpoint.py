@@ -350,16 +350,17 @@ def _top_bit_onehot(sess, x: RepTensor, lo: int, hi: int) -> RepTensor:
         p = _or(sess, p, rep.local(sess, p, "Shr", amount=d))
         d *= 2
     onehot = rep.xor(sess, p, rep.local(sess, p, "Shr", amount=1))
-    planes = RepTensor(x.plc, 1, "bool", sess.p("BitSplit", x.plc, onehot.s0, start=lo, count=hi - lo),
-                       sess.p("BitSplit", x.plc, onehot.s1, start=lo, count=hi - lo))
+    planes = RepTensor(x.plc, 1, "bool", *rep._sharewise(sess, "BitSplit", x.plc,
+                                                         (onehot.s0, onehot.s1), start=lo,
+                                                         count=hi - lo))
     return rep.b2a(sess, planes, bits)
 
 
 def _weighted(sess, t: RepTensor, weights, bits) -> RepTensor:
     """sum_j w_j t_j over the leading axis (public integer weights, mod 2^bits)."""
     w = [int(v) % (1 << bits) for v in weights]
-    return RepTensor(t.plc, bits, "arith", sess.p("WeightedSum", t.plc, t.s0, weights=w, bits=bits),
-                     sess.p("WeightedSum", t.plc, t.s1, weights=w, bits=bits))
+    s0, s1 = rep._sharewise(sess, "WeightedSum", t.plc, (t.s0, t.s1), weights=w, bits=bits)
+    return RepTensor(t.plc, bits, "arith", s0, s1)
 
 
 def _normalize(sess, x: RepFixed):
@@ -552,8 +553,8 @@ def _exp2_parts(sess, a: RepFixed, negative: bool):
               and getattr(sess, "party_dot_trunc", None) is not None
               and hasattr(sess, "p_cross_plain") and npad >= 2 and npad & (npad - 1) == 0)
     bd = rep.bit_decompose(sess, a.t)
-    planes = RepTensor(a.plc, 1, "bool", sess.p("BitSplit", a.plc, bd.s0, start=0, count=f + npad),
-                       sess.p("BitSplit", a.plc, bd.s1, start=0, count=f + npad))
+    planes = RepTensor(a.plc, 1, "bool", *rep._sharewise(sess, "BitSplit", a.plc, (bd.s0, bd.s1),
+                                                         start=0, count=f + npad))
     ab = rep.b2a(sess, planes, bits)  # arithmetic bits, leading axis
     frac_w = [(1 << j) for j in range(f)] + [0] * npad
     r = RepFixed(_weighted(sess, ab, frac_w, bits), f, integ)

@@ -710,8 +710,8 @@ def _unstack2(sess, x: RepTensor):
 def bit_extract(sess, x: RepTensor, i: int) -> RepTensor:
     """Bit i of a packed boolean sharing -> boolean bit sharing (Z_2)."""
     assert x.kind == "bool"
-    return RepTensor(x.plc, 1, "bool", sess.p("BitExtract", x.plc, x.s0, bit_idx=i),
-                     sess.p("BitExtract", x.plc, x.s1, bit_idx=i))
+    s0, s1 = _sharewise(sess, "BitExtract", x.plc, (x.s0, x.s1), bit_idx=i)
+    return RepTensor(x.plc, 1, "bool", s0, s1)
 
 
 def b2a(sess, b: RepTensor, ring_bits: int) -> RepTensor:

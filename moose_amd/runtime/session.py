@@ -264,9 +264,48 @@ class StackedSession(Session):
     # -- share pairs: both share vectors of a share-wise op in one launch ----------------
     _PAIR_BIN = {"Add": "add", "Sub": "sub", "Xor": "xor", "And": "and", "Mul": "mul"}
 
+    # per-party primitives that run over a pair-stacked base (every slot independent)
+    _PAIR_SLOTWISE = ("WeightedSum", "BitExtract", "BitSplit")
+
+    @staticmethod
+    def _pair_base(v0, v1):
+        """(base, n, off): when the two share vectors are views of ONE buffer -- a share-pair
+        ring (s1 = s0 + 1 slot: 4 slots) or adjacent halves of a pair allocation (s1 = s0 +
+        3 slots: 6 slots) -- the buffer's slots as one [n, ...] tensor and s1's offset in
+        slots; None otherwise."""
+        if not (isinstance(v0, R.RT) and isinstance(v1, R.RT)):
+            return None
+        d0, d1 = v0.data, v1.data
+        if (d0.dim() < 1 or d0.shape != d1.shape or d0.stride() != d1.stride()
+                or d0.shape[0] != 3 or d0.dtype != d1.dtype or d0.stride(0) <= 0
+                or d0.untyped_storage().data_ptr() != d1.untyped_storage().data_ptr()):
+            return None
+        step = d0.stride(0) * d0.element_size()
+        off = d1.data_ptr() - d0.data_ptr()
+        if off == step:
+            n, o = 4, 1
+        elif off == 3 * step:
+            n, o = 6, 3
+        else:
+            return None
+        try:
+            base = d0.as_strided((n,) + tuple(d0.shape[1:]), d0.stride())
+        except RuntimeError:  # not inside one storage
+            return None
+        return R.RT(base, v0.bits), n, o
+
     def p_pair(self, prim, plc, a, b=None, **attrs):
         """(prim(a[0], b[0]), prim(a[1], b[1])) as one kernel when both are ring tensors of
-        64/128 bits (Neg / Shl / the binary ring ops); None -> caller issues two ops."""
+        64/128 bits (Neg / Shl / the binary ring ops), or for a slot-wise primitive when the
+        pair is one buffer (``_pair_base``); None -> caller issues two ops."""
+        if b is None and prim in self._PAIR_SLOTWISE:
+            pb = self._pair_base(a[0].v, a[1].v)
+            if pb is None:
+                return None
+            base, n, o = pb
+            out = PRIMS[prim].impl(1, base, **self._attrs(prim, attrs))
+            return (PV(plc, R.RT(out.data[0:3], out.bits)),
+                    PV(plc, R.RT(out.data[o:o + 3], out.bits)))
         v0, v1 = a[0].v, a[1].v
         if not (isinstance(v0, R.RT) and isinstance(v1, R.RT)) or v0.bits not in (64, 128):
             return None
@@ -399,16 +438,13 @@ class StackedSession(Session):
         filled by one copy of the buffer's four slots (P0 = stack[0:3], P1 = stack[1:4];
         the kernels that write later rows see a ring pair and write four slots)."""
         v0, v1 = x0.v, x1.v
-        d0, d1 = v0.data, v1.data
-        if (isinstance(v0, R.RT) and isinstance(v1, R.RT) and d0.dim() >= 1
-                and d0.shape == d1.shape and d0.stride() == d1.stride() and d0.shape[0] == 3
-                and d1.data_ptr() - d0.data_ptr() == d0.stride(0) * d0.element_size()
-                and d0[0].is_contiguous()
-                and d0.stride(0) == d0[0].numel()):
-            buf = d0.as_strided((4,) + tuple(d0.shape[1:]), d0.stride())
-            st = torch.empty((4, n) + tuple(d0.shape[1:]), dtype=d0.dtype, device=d0.device)
-            st[:, 0].copy_(buf)
-            return PV(x0.plc, R.RT(st[0:3], v0.bits)), PV(x1.plc, R.RT(st[1:4], v1.bits))
+        pb = self._pair_base(v0, v1)
+        if pb is not None and v0.data[0].is_contiguous():
+            base, k, o = pb
+            d0 = v0.data
+            st = torch.empty((k, n) + tuple(d0.shape[1:]), dtype=d0.dtype, device=d0.device)
+            st[:, 0].copy_(base.data)  # one copy for both share vectors
+            return PV(x0.plc, R.RT(st[0:3], v0.bits)), PV(x1.plc, R.RT(st[o:o + 3], v1.bits))
         return self.p_rows_alloc(x0, n), self.p_rows_alloc(x1, n)
 
     def p_rows_view(self, x, r0, r1):
