@@ -291,6 +291,28 @@ __global__ void __launch_bounds__(256) k_ring_inject(const uint8_t* __restrict__
     out[i] = ((T)(bits[i] & 1)) << bit;
 }
 
+// The local half of rep.b2a for three stacked parties, one launch: from the bit sharing
+// (s0, s1 party vectors [3][n], P_p holding (b_p, b_{p+1})) P0's a = b_0 ^ b_1 as a ring
+// value (to be shared by P0) and the trivial sharing B of b_2 (slot 2: P2's s0 and P1's s1)
+// -- the values of the Xor + RingInject x 3 + slot placement it replaces.
+template <class T>
+__global__ void __launch_bounds__(256) k_b2a_prep3(const uint8_t* __restrict__ s0,
+                                                   const uint8_t* __restrict__ s1, int64_t n,
+                                                   T* __restrict__ a, T* __restrict__ b0,
+                                                   T* __restrict__ b1) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    a[e] = (T)((s0[e] ^ s1[e]) & 1);
+    const T x2 = (T)(s0[2 * n + e] & 1), x2b = (T)(s1[n + e] & 1);
+    b0[e] = 0;
+    b0[n + e] = 0;
+    b0[2 * n + e] = x2;
+    b1[e] = 0;
+    b1[n + e] = x2b;
+    b1[2 * n + e] = 0;
+  }
+}
+
 template <class T>
 __global__ void __launch_bounds__(256) k_encode(const double* __restrict__ x, T* __restrict__ out, int64_t n,
                          double scale) {
@@ -1139,6 +1161,17 @@ int mxh_bit_extract(int words, const void* a, uint8_t* out, int64_t n, int bit, 
   DEV_DISPATCH(words, T, {
     hipLaunchKernelGGL(k_bit_extract<T>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
                        (const T*)a, out, n, bit);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mxh_b2a_prep3(int words, const uint8_t* s0, const uint8_t* s1, int64_t n, void* a,
+                  void* b0, void* b1, void* stream) {
+  if (n == 0) return 0;
+  DEV_DISPATCH(words, T, {
+    hipLaunchKernelGGL(k_b2a_prep3<T>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream), s0, s1,
+                       n, (T*)a, (T*)b0, (T*)b1);
     MX_LAUNCH_CHECK();
     return 0;
   });

@@ -1380,6 +1380,24 @@ def sum_views2(ts0, ts1):
     return o0, o1
 
 
+def b2a_prep3(b0: RT, b1: RT, ring_bits: int):
+    """rep.b2a's local values for three stacked parties in one launch (k_b2a_prep3): P0's
+    a = b_0 ^ b_1 as a ring tensor [...] and the trivial sharing of b_2 (slot 2) as a
+    pair of [3, ...] party vectors.  None when not on the device."""
+    d0, d1 = b0.data, b1.data
+    if not d0.is_cuda or ring_bits not in (64, 128) or d0.dtype != torch.uint8 \
+            or d1.dtype != torch.uint8 or d0.shape != d1.shape or d0.shape[0] != 3:
+        return None
+    d0, d1 = d0.contiguous(), d1.contiguous()
+    shp = tuple(d0.shape[1:])
+    a = empty(shp, ring_bits, d0.device)
+    o0, o1 = empty2((3,) + shp, ring_bits, d0.device)
+    nat.check(nat.lib().mxh_b2a_prep3(_words(ring_bits), nat.ptr(d0), nat.ptr(d1),
+                                      math.prod(shp), nat.ptr(a.data), nat.ptr(o0.data),
+                                      nat.ptr(o1.data), nat.stream_of(d0)), "b2a_prep3")
+    return a, o0, o1
+
+
 def slot_place2(x0: RT, x1: RT, which0: int, which1: int, nparties: int = 3):
     """Two trivial stacked sharings [nparties, *x.shape] in one launch: slot which0 of the
     first = x0, slot which1 of the second = x1, zeros elsewhere (mx_slot_place2)."""

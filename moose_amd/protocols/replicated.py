@@ -723,12 +723,19 @@ def b2a(sess, b: RepTensor, ring_bits: int) -> RepTensor:
         o = plc.owners
         if b.bits != 1:
             raise TypeError("b2a expects a bit sharing")
-        a_bit = sess.h("Xor", o[0], sess.take(b.s0, 0), sess.take(b.s1, 0))
-        a_ring = sess.h("RingInject", o[0], a_bit, bit_idx=0, bits=ring_bits)
-        A = share(sess, plc, a_ring, kind="arith")
-        b2_h0 = sess.h("RingInject", o[2], sess.take(b.s0, 2), bit_idx=0, bits=ring_bits)
-        b2_h1 = sess.h("RingInject", o[1], sess.take(b.s1, 1), bit_idx=0, bits=ring_bits)
-        B = from_slot_holders(sess, plc, 2, b2_h0, b2_h1, b.s0, kind="arith")
+        prep = getattr(sess, "p_b2a_prep", None)
+        r = prep(plc, b, ring_bits) if prep is not None else None
+        if r is not None:  # the local steps below in one kernel (same values)
+            a_ring, B0, B1 = r
+            A = share(sess, plc, a_ring, kind="arith")
+            B = RepTensor(plc, ring_bits, "arith", B0, B1)
+        else:
+            a_bit = sess.h("Xor", o[0], sess.take(b.s0, 0), sess.take(b.s1, 0))
+            a_ring = sess.h("RingInject", o[0], a_bit, bit_idx=0, bits=ring_bits)
+            A = share(sess, plc, a_ring, kind="arith")
+            b2_h0 = sess.h("RingInject", o[2], sess.take(b.s0, 2), bit_idx=0, bits=ring_bits)
+            b2_h1 = sess.h("RingInject", o[1], sess.take(b.s1, 1), bit_idx=0, bits=ring_bits)
+            B = from_slot_holders(sess, plc, 2, b2_h0, b2_h1, b.s0, kind="arith")
         AB = mul(sess, A, B)
         return lincomb(sess, [(1, A), (1, B), (-2, AB)])
 

@@ -352,6 +352,20 @@ class StackedSession(Session):
             return None
         return PV(plc, o0), PV(plc, o1)
 
+    def p_b2a_prep(self, plc, b, ring_bits):
+        """rep.b2a's local steps in one kernel (device): (P0's a = b_0 ^ b_1 as a ring
+        value, the trivial sharing of b_2 as a (s0, s1) pair); None -> the generic steps."""
+        if self.device.type != "cuda":
+            return None
+        v0, v1 = b.s0.v, b.s1.v
+        if not (isinstance(v0, R.RT) and isinstance(v1, R.RT)) or v0.bits != 1:
+            return None
+        r = R.b2a_prep3(v0, v1, ring_bits)
+        if r is None:
+            return None
+        a, o0, o1 = r
+        return HV(plc.owners[0], a), PV(plc, o0), PV(plc, o1)
+
     def p_from_slot_holders(self, plc, slot, x_h0, x_h1, like):
         """rep.from_slot_holders in one kernel (None -> generic path)."""
         v0, v1 = x_h0.v, x_h1.v

@@ -245,3 +245,24 @@ def test_dot_public_pair_one_launch(bits, shapes):
     _eq(r[1].v, want1)
     assert r[1].v.data.data_ptr() - r[0].v.data.data_ptr() == \
         r[0].v.data.stride(0) * r[0].v.data.element_size()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [64, 128])
+def test_b2a_prep_kernel_matches_generic(bits):
+    """rep.b2a with its local steps in one kernel (StackedSession.p_b2a_prep) gives bitwise
+    the shares of the generic Xor / RingInject / slot-placement steps (same seed)."""
+    from moose_amd.runtime.session import HV
+
+    plc = ReplicatedPlacement(owners=("a", "b", "c"))
+    outs = []
+    for fused in (True, False):
+        sess = StackedSession("cuda", seed=7)
+        if not fused:
+            sess.p_b2a_prep = lambda *a, **k: None
+        x = rep.share(sess, plc, HV("a", _rand((300,), bits, "cuda", 3)))
+        b = rep.msb(sess, x)
+        y = rep.b2a(sess, b, bits)
+        outs.append((y.s0.v, y.s1.v))
+    _eq(outs[0][0], outs[1][0])
+    _eq(outs[0][1], outs[1][1])
