@@ -579,8 +579,8 @@ def _exp2_parts(sess, a: RepFixed, negative: bool):
     ints = local(sess, ab, "Slice", slice=(f, f + npad, None))
     cvec = R.from_ints(np.array(cs, dtype=object), bits, sess.device)
     pc = sess.public(ints.plc, cvec)
-    fac = RepTensor(ints.plc, bits, "arith", sess.p("MulLeading", ints.plc, ints.s0, pc),
-                    sess.p("MulLeading", ints.plc, ints.s1, pc))
+    fac = RepTensor(ints.plc, bits, "arith",
+                    *rep._sharewise(sess, "MulLeading", ints.plc, (ints.s0, ints.s1), (pc, pc)))
     fac = rep.add_public(sess, fac, _encode_const(sess, 1.0, f, bits))
     if merged:
         # parties on different processes: the polynomial's levels and the product tree's

@@ -265,7 +265,9 @@ class StackedSession(Session):
     _PAIR_BIN = {"Add": "add", "Sub": "sub", "Xor": "xor", "And": "and", "Mul": "mul"}
 
     # per-party primitives that run over a pair-stacked base (every slot independent)
-    _PAIR_SLOTWISE = ("WeightedSum", "BitExtract", "BitSplit")
+    _PAIR_SLOTWISE = ("WeightedSum", "BitExtract", "BitSplit", "Slice")
+    # slot-wise with one public operand, the same for both share vectors
+    _PAIR_SLOTWISE_PUB = ("MulLeading",)
 
     @staticmethod
     def _pair_base(v0, v1):
@@ -298,12 +300,15 @@ class StackedSession(Session):
         """(prim(a[0], b[0]), prim(a[1], b[1])) as one kernel when both are ring tensors of
         64/128 bits (Neg / Shl / the binary ring ops), or for a slot-wise primitive when the
         pair is one buffer (``_pair_base``); None -> caller issues two ops."""
-        if b is None and prim in self._PAIR_SLOTWISE:
+        pub = (b is not None and prim in self._PAIR_SLOTWISE_PUB and b[0] is b[1]
+               and isinstance(b[0], Public))
+        if (b is None and prim in self._PAIR_SLOTWISE) or pub:
             pb = self._pair_base(a[0].v, a[1].v)
             if pb is None:
                 return None
             base, n, o = pb
-            out = PRIMS[prim].impl(1, base, **self._attrs(prim, attrs))
+            extra = (b[0].v,) if pub else ()
+            out = PRIMS[prim].impl(1, base, *extra, **self._attrs(prim, attrs))
             return (PV(plc, R.RT(out.data[0:3], out.bits)),
                     PV(plc, R.RT(out.data[o:o + 3], out.bits)))
         v0, v1 = a[0].v, a[1].v
