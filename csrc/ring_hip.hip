@@ -771,16 +771,14 @@ __global__ void __launch_bounds__(256) k_rss_cross_ring3_lat(int kind, const T* 
 // (as k_trunc_pr3_lat) -- the product never leaves registers.  Nine keystream chunks per
 // chunk position: the product's zero share (k0, k1, k2 at nmul) and the TruncPr's r0, r1,
 // t, m, z0, z2 (keys k0 / k2, as in k_trunc_pr3).  Bitwise equal to the two kernels.
-template <class T>
-__global__ void __launch_bounds__(256) k_mul_trunc3_lat(
+template <class T, int EPB>
+__device__ __forceinline__ void mul_trunc3_lat_body(
     const T* __restrict__ x0, const T* __restrict__ x1, const T* __restrict__ y0,
     const T* __restrict__ y1, T* __restrict__ out0, T* __restrict__ out1, int64_t n, int64_t os,
-    KeySrc keys, uint64_t nmul, int m, uint64_t nr0, uint64_t nr1, uint64_t nt, uint64_t nm,
-    uint64_t nz0, uint64_t nz2, Views vw) {
-  constexpr int NS = 9, EPB = 256 / NS;
-  __shared__ uint32_t rks[3][kKeyWords];
-  __shared__ uint64_t kl[NS][EPB], kh[NS][EPB];
-  stage_keys(rks, keys, 3);
+    const uint32_t (&rks)[3][kKeyWords], uint64_t (&kl)[9][EPB], uint64_t (&kh)[9][EPB],
+    uint64_t nmul, int m, uint64_t nr0, uint64_t nr1, uint64_t nt, uint64_t nm, uint64_t nz0,
+    uint64_t nz2, const Views& vw) {
+  constexpr int NS = 9;
   constexpr int P = Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;
   const int tid = threadIdx.x, s = tid / EPB, lb = tid % EPB;
@@ -832,6 +830,54 @@ __global__ void __launch_bounds__(256) k_mul_trunc3_lat(
     }
     __syncthreads();
   }
+}
+
+// Fixed-point product of a latency-bound launch in ONE kernel: the stacked RSS product
+// with its zero share (as k_rss_cross_ring3_lat) and the TruncPr of the reshared product
+// (as k_trunc_pr3_lat) -- the product never leaves registers.  Nine keystream chunks per
+// chunk position: the product's zero share (k0, k1, k2 at nmul) and the TruncPr's r0, r1,
+// t, m, z0, z2 (keys k0 / k2, as in k_trunc_pr3).  Bitwise equal to the two kernels.
+template <class T>
+__global__ void __launch_bounds__(256) k_mul_trunc3_lat(
+    const T* __restrict__ x0, const T* __restrict__ x1, const T* __restrict__ y0,
+    const T* __restrict__ y1, T* __restrict__ out0, T* __restrict__ out1, int64_t n, int64_t os,
+    KeySrc keys, uint64_t nmul, int m, uint64_t nr0, uint64_t nr1, uint64_t nt, uint64_t nm,
+    uint64_t nz0, uint64_t nz2, Views vw) {
+  constexpr int EPB = 256 / 9;
+  __shared__ uint32_t rks[3][kKeyWords];
+  __shared__ uint64_t kl[9][EPB], kh[9][EPB];
+  stage_keys(rks, keys, 3);
+  mul_trunc3_lat_body<T, EPB>(x0, x1, y0, y1, out0, out1, n, os, rks, kl, kh, nmul, m, nr0,
+                              nr1, nt, nm, nz0, nz2, vw);
+}
+
+// Two independent products of one placement (same keys) in one launch: blockIdx.y picks the
+// problem (the rounds of two computations that run side by side, e.g. a polynomial level
+// and a product-tree level).  Each is exactly k_mul_trunc3_lat's.
+template <class T>
+struct MT2 {
+  const T* x0[2];
+  const T* x1[2];
+  const T* y0[2];
+  const T* y1[2];
+  T* out0[2];
+  T* out1[2];
+  int64_t n[2], os[2];
+  uint64_t nmul[2], nn[2][6];
+  int m[2];
+  Views vw[2];
+};
+
+template <class T>
+__global__ void __launch_bounds__(256) k_mul_trunc3_lat2(MT2<T> a, KeySrc keys) {
+  constexpr int EPB = 256 / 9;
+  __shared__ uint32_t rks[3][kKeyWords];
+  __shared__ uint64_t kl[9][EPB], kh[9][EPB];
+  stage_keys(rks, keys, 3);
+  const int y = blockIdx.y;
+  mul_trunc3_lat_body<T, EPB>(a.x0[y], a.x1[y], a.y0[y], a.y1[y], a.out0[y], a.out1[y], a.n[y],
+                              a.os[y], rks, kl, kh, a.nmul[y], a.m[y], a.nn[y][0], a.nn[y][1],
+                              a.nn[y][2], a.nn[y][3], a.nn[y][4], a.nn[y][5], a.vw[y]);
 }
 
 // Throughput form of k_mul_trunc3_lat: one ChaCha block of each of the nine streams per
@@ -1442,6 +1488,53 @@ int mxh_mul_trunc3_kv(int words, const void* x0, const void* x1, const void* y0,
                        (const T*)x0, (const T*)x1, (const T*)y0, (const T*)y1, (T*)out0,
                        (T*)out1, n, ostride, mxd::keysrc_slots(ptrs, 3), nmul, m, nn[0], nn[1],
                        nn[2], nn[3], nn[4], nn[5], vw);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+// Two k_mul_trunc3_lat problems of one placement in one launch (k_mul_trunc3_lat2): per
+// problem i the arguments of mxh_mul_trunc3_kv at index i of each array; nn: 6 nonces per
+// problem; views: 8 int64 per problem or a null pointer per problem.  Only for latency-bound
+// sizes (the throughput kernel has no two-problem form): -1 otherwise.
+int mxh_mul_trunc3_kv2(int words, const void* const* x0, const void* const* x1,
+                       const void* const* y0, const void* const* y1, void* const* out0,
+                       void* const* out1, const int64_t* n, const int64_t* ostride,
+                       const uint32_t* slots, const uint64_t* nmul, const int* m,
+                       const uint64_t* nn, const int64_t* const* views, void* stream) {
+  const uint32_t* ptrs[3];
+  for (int i = 0; i < 3; ++i) ptrs[i] = slots + MX_KEY_SLOT_WORDS * i;
+  DEV_DISPATCH(words, T, {
+    constexpr int P = 16 / (int)sizeof(T);
+    constexpr int EPB = 256 / 9;
+    MT2<T> a{};
+    int64_t g = 1;
+    for (int i = 0; i < 2; ++i) {
+      const int64_t blocks = (n[i] + P - 1) / P;
+      if (n[i] <= 0 || blocks > 8192) return -1;
+      g = std::max<int64_t>(g, (blocks + EPB - 1) / EPB);
+      a.x0[i] = (const T*)x0[i];
+      a.x1[i] = (const T*)x1[i];
+      a.y0[i] = (const T*)y0[i];
+      a.y1[i] = (const T*)y1[i];
+      a.out0[i] = (T*)out0[i];
+      a.out1[i] = (T*)out1[i];
+      a.n[i] = n[i];
+      a.os[i] = ostride[i];
+      a.nmul[i] = nmul[i];
+      a.m[i] = m[i];
+      for (int k = 0; k < 6; ++k) a.nn[i][k] = nn[6 * i + k];
+      a.vw[i] = Views{};
+      if (views[i]) {
+        for (int k = 0; k < 4; ++k) {
+          a.vw[i].ps[k] = views[i][k];
+          a.vw[i].per[k] = views[i][4 + k] > 0 ? views[i][4 + k] : n[i];
+        }
+        a.vw[i].strided = 1;
+      }
+    }
+    hipLaunchKernelGGL(k_mul_trunc3_lat2<T>, dim3((unsigned)g, 2), dim3(kBlock), 0, S(stream), a,
+                       mxd::keysrc_slots(ptrs, 3));
     MX_LAUNCH_CHECK();
     return 0;
   });

@@ -1161,6 +1161,70 @@ def mul_trunc3_k(x0: RT, x1: RT, y0: RT, y1: RT, slot_ptr: int, nmul: int, m: in
     return o0, o1
 
 
+def _mt3_args(x0: RT, x1: RT, y0: RT, y1: RT, out=None):
+    """mul_trunc3_k's argument checks and layout: (ops, (o0, o1), n, out stride, views) or
+    None when the device kernel does not apply."""
+    bits = x0.bits
+    if not x0.data.is_cuda or bits not in (64, 128):
+        return None
+    shp = x0.shape
+    ops = (x0, x1, y0, y1)
+    if any(o.shape != shp or o.bits != bits for o in ops):
+        return None
+    n = math.prod(shp) // 3
+    if n == 0:
+        return None
+    views = None
+    if any(not o.data.is_contiguous() for o in ops):
+        vs = [_party_view(o) for o in ops]
+        if any(v is None for v in vs):
+            return None
+        views = [v[0] for v in vs] + [v[1] for v in vs]
+    w = 2 if bits == 128 else 1
+    if out is None:
+        o0, o1 = ring4(shp, bits, x0.device)
+        os_ = n
+    else:
+        o0, o1 = out
+        os_ = o0.data.stride(0) // w
+        if not (o0.shape == shp and o1.shape == shp and o1.data.stride(0) == o0.data.stride(0)
+                and o0.data[0].is_contiguous() and o1.data[0].is_contiguous()):
+            return None
+    return ops, (o0, o1), n, os_, views
+
+
+def mul_trunc3_k2(jobs, slot_ptr: int):
+    """Two independent fixed-point products of one placement in ONE launch
+    (mx_mul_trunc3_kv2): ``jobs`` = [(x0, x1, y0, y1, nmul, m, nonces, out), ...] (two),
+    each exactly mul_trunc3_k's.  Returns [(s0, s1), (s0, s1)], or None when the batched
+    kernel does not apply (the caller runs them one by one)."""
+    if len(jobs) != 2:
+        return None
+    prep = [_mt3_args(*j[:4], out=j[7]) for j in jobs]
+    if any(p is None for p in prep) or jobs[0][0].bits != jobs[1][0].bits:
+        return None
+    bits = jobs[0][0].bits
+    if any(p[2] > 8192 * (16 // (16 if bits == 128 else 8)) for p in prep):
+        return None  # throughput sizes: one by one
+    P2 = ctypes.c_void_p * 2
+    ptr = lambda t: t.data.data_ptr()  # noqa: E731
+    vws = [None if p[4] is None else (ctypes.c_int64 * 8)(*p[4]) for p in prep]
+    views = (ctypes.c_void_p * 2)(*[None if v is None else ctypes.addressof(v) for v in vws])
+    nn = (ctypes.c_uint64 * 12)(*[v & MASK64 for j in jobs for v in j[6]])
+    rc = nat.lib().mxh_mul_trunc3_kv2(
+        _words(bits), P2(*[ptr(p[0][0]) for p in prep]), P2(*[ptr(p[0][1]) for p in prep]),
+        P2(*[ptr(p[0][2]) for p in prep]), P2(*[ptr(p[0][3]) for p in prep]),
+        P2(*[ptr(p[1][0]) for p in prep]), P2(*[ptr(p[1][1]) for p in prep]),
+        (ctypes.c_int64 * 2)(*[p[2] for p in prep]), (ctypes.c_int64 * 2)(*[p[3] for p in prep]),
+        ctypes.c_void_p(slot_ptr), (ctypes.c_uint64 * 2)(*[j[4] & MASK64 for j in jobs]),
+        (ctypes.c_int * 2)(*[int(j[5]) for j in jobs]), nn, views,
+        nat.stream_of(jobs[0][0].data))
+    if rc == -1:
+        return None
+    nat.check(rc, "mul_trunc3 x2")
+    return [p[1] for p in prep]
+
+
 def zs_trunc3_k(z: RT, slot_ptr: int, nmul: int, m: int, nonces):
     """Zero share + reshare + TruncPr of three stacked parties' local products ``z``
     ([3, ...], e.g. a dot's GEMM output) in one kernel (mx_mul_trunc3_kv with the product

@@ -560,11 +560,10 @@ def _exp2_parts(sess, a: RepFixed, negative: bool):
     r = RepFixed(_weighted(sess, ab, frac_w, bits), f, integ)
     if negative:
         # 2^-r for r in [0,1) = 2^(1-r) / 2 -> fit exp2 on [0, 1] of (1 - r)
-        one_minus = const_sub(sess, 1.0, r)
-        p = None if merged else poly_eval(sess, one_minus, _fit("exp2", 0.0, 1.0, 7),
-                                          shift=1)
+        px, shift = const_sub(sess, 1.0, r), 1
     else:
-        p = poly_eval(sess, r, _fit("exp2", 0.0, 1.0, 7))
+        px, shift = r, 0
+    one_minus = px
     # integer part factors 1 + b_j (c_j - 1), c_j = 2^(+-2^j), for all j at once: the
     # integer bit planes stay stacked on the leading axis, scaled by a public vector
     cs = []
@@ -586,24 +585,83 @@ def _exp2_parts(sess, a: RepFixed, negative: bool):
         # parties on different processes: the polynomial's levels and the product tree's
         # levels are independent -- each round carries both (module doc: _merged_exp_tail)
         return _merged_exp_tail(sess, one_minus, fac, npad)
-    # log-depth product over the leading axis: one stacked multiplication per level
-    F, n = RepFixed(fac, f, integ), npad
-    views = _rows_ok(sess, F)
-    while n > 1:
-        h = n // 2
-        if views:  # both halves read in place by the mul kernel
-            lo = _with(F, RepTensor(F.t.plc, bits, "arith", sess.p_rows_view(F.t.s0, 0, h),
-                                    sess.p_rows_view(F.t.s1, 0, h)))
-            hi = _with(F, RepTensor(F.t.plc, bits, "arith", sess.p_rows_view(F.t.s0, h, 2 * h),
-                                    sess.p_rows_view(F.t.s1, h, 2 * h)))
-            prod = mul(sess, lo, hi)
-        else:
-            prod = mul(sess, local(sess, F, "Slice", slice=(0, h, None)),
-                       local(sess, F, "Slice", slice=(h, 2 * h, None)))
-        F = prod if n % 2 == 0 else concat(
-            sess, [prod, local(sess, F, "Slice", slice=(2 * h, n, None))], 0)
-        n = (n + 1) // 2
+    # the polynomial's power levels and the product tree's levels (a log-depth product over
+    # the leading axis) advance together: each round's two products run as one launch on a
+    # stacked device session (rep.mul_trunc_many)
+    p, F = _poly_and_tree(sess, px, _fit("exp2", 0.0, 1.0, 7), shift,
+                          RepFixed(fac, f, integ), npad)
     return mul(sess, p, local(sess, F, "IndexAxis", axis=0, index=0))
+
+
+def _poly_and_tree(sess, x: RepFixed, coeffs, shift: int, F: RepFixed, nf: int):
+    """(poly_eval(x, coeffs, shift), the product of F's ``nf`` leading entries as a
+    1-entry stack) with one level of each per round: the polynomial's powers x^(h+1..h+m)
+    = x^h * P[0:m] (in place in a row stack on a stacked device session, else by slice /
+    concat) and the tree's F[0:h] * F[h:2h].  Same values as the two computed one after
+    the other."""
+    n = len(coeffs) - 1
+    f, bits, t = x.frac, x.bits, x.t
+    rows = n > 1 and _rows_ok(sess, x)
+    views = _rows_ok(sess, F)
+    if rows:
+        pair = getattr(sess, "p_rows_alloc_pair", None)
+        P0, P1 = pair(t.s0, t.s1, n) if pair is not None else (
+            sess.p_rows_alloc(t.s0, n), sess.p_rows_alloc(t.s1, n))
+    else:
+        P = local(sess, x, "ExpandDims", axis=[0])
+    have = 1
+    while have < n or nf > 1:
+        jobs = []
+        m = min(2 * have, n) - have if have < n else 0
+        if m:
+            if rows:
+                left = RepTensor(t.plc, bits, t.kind, sess.p_rows_bcast(P0, have - 1, m),
+                                 sess.p_rows_bcast(P1, have - 1, m))
+                right = RepTensor(t.plc, bits, t.kind, sess.p_rows_view(P0, 0, m),
+                                  sess.p_rows_view(P1, 0, m))
+                out = (sess.p_rows_view(P0, have, have + m), sess.p_rows_view(P1, have, have + m))
+                jobs.append((left, right, f, out))
+            else:
+                xh = local(sess, P, "Slice", slice=(have - 1, have, None))
+                left = xh if m == 1 else concat(sess, [xh] * m, 0)
+                right = P if m == have else local(sess, P, "Slice", slice=(0, m, None))
+                jobs.append((left.t, right.t, f, None))
+        h = nf // 2
+        if h:
+            if views:  # both halves read in place by the mul kernel
+                lo = RepTensor(F.t.plc, bits, "arith", sess.p_rows_view(F.t.s0, 0, h),
+                               sess.p_rows_view(F.t.s1, 0, h))
+                hi = RepTensor(F.t.plc, bits, "arith", sess.p_rows_view(F.t.s0, h, 2 * h),
+                               sess.p_rows_view(F.t.s1, h, 2 * h))
+            else:
+                lo = local(sess, F.t, "Slice", slice=(0, h, None))
+                hi = local(sess, F.t, "Slice", slice=(h, 2 * h, None))
+            jobs.append((lo, hi, F.frac, None))
+        if rows and m and not getattr(sess, "fused", False):
+            # the unfused rows path writes the level's rows itself (as _poly_eval_rows)
+            z = rep.trunc_pr(sess, rep.mul(sess, jobs[0][0], jobs[0][1]), f)
+            sess.p_rows_write(P0, have, z.s0)
+            sess.p_rows_write(P1, have, z.s1)
+            res = [None] + rep.mul_trunc_many(sess, jobs[1:])
+        else:
+            res = rep.mul_trunc_many(sess, jobs)
+        k = 0
+        if m:
+            if not rows:
+                P = concat(sess, [P, _with(x, res[0])], 0)
+            have += m
+            k = 1
+        if h:
+            prod = _with(F, res[k])
+            F = prod if nf % 2 == 0 else concat(
+                sess, [prod, local(sess, F, "Slice", slice=(2 * h, nf, None))], 0)
+            nf = (nf + 1) // 2
+    Pt = RepTensor(t.plc, bits, t.kind, P0, P1) if rows else P.t
+    if n <= 1:
+        Pt = local(sess, x, "ExpandDims", axis=[0]).t
+    acc = _weighted(sess, Pt, [int(round(c * (1 << f))) for c in coeffs[1:]], bits)
+    acc = rep.trunc_pr(sess, acc, f + shift)
+    return add_const(sess, RepFixed(acc, f, x.integ), coeffs[0] / (1 << shift)), F
 
 
 def _tail_trunc(sess, plc, v, bits, m) -> RepTensor:

@@ -414,6 +414,20 @@ def mul_trunc(sess, x: RepTensor, y: RepTensor, m: int, out=None) -> RepTensor:
     return trunc_pr(sess, mul(sess, x, y), m, out=out)
 
 
+def mul_trunc_many(sess, jobs):
+    """Independent fixed-point products [(x, y, m, out)] of one placement: two of them in ONE
+    launch on a stacked device session (p_mul_trunc2), else one by one -- the same nonces in
+    the same order either way, so the same shares."""
+    f = getattr(sess, "p_mul_trunc2", None)
+    if (f is not None and len(jobs) == 2 and getattr(sess, "fused", False)
+            and all(x.kind == "arith" and y.kind == "arith" and m for x, y, m, _ in jobs)):
+        r = f(jobs[0][0].plc, [(x.s0, x.s1, y.s0, y.s1, m, out) for x, y, m, out in jobs])
+        if r is not None:
+            return [RepTensor(x.plc, x.bits, "arith", a, b)
+                    for (x, _, _, _), (a, b) in zip(jobs, r)]
+    return [mul_trunc(sess, x, y, m, out=out) for x, y, m, out in jobs]
+
+
 def and_(sess, x: RepTensor, y: RepTensor) -> RepTensor:
     assert x.kind == "bool"
     return mul(sess, x, y)

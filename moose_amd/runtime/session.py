@@ -25,6 +25,7 @@ and k_{p+1}, so PRF(k_s) is computable by exactly the two holders of slot s) and
 """
 from __future__ import annotations
 
+import math
 import os
 from dataclasses import dataclass
 from typing import Any
@@ -540,6 +541,41 @@ class StackedSession(Session):
         # the messages of the per-party protocol (reshare folded into TruncPr, 2 rounds)
         record_tail_traffic(self.stats, plc, _nbytes(r[0]) // 3)
         return PV(plc, r[0]), PV(plc, r[1])
+
+    def p_mul_trunc2(self, plc, jobs):
+        """Two independent p_mul_trunc products [(x0, x1, y0, y1, m, out)] in ONE launch
+        (k_mul_trunc3_lat2), the nonces drawn in the order two p_mul_trunc calls draw them
+        (so the shares are the same).  None -> the caller runs them one by one."""
+        if self.device.type != "cuda" or len(jobs) != 2:
+            return None
+        args = []
+        for x0, x1, y0, y1, m, out in jobs:
+            v = [t.v for t in (x0, x1, y0, y1)]
+            if not all(isinstance(t, R.RT) for t in v) or not m:
+                return None
+            o = None if out is None else (out[0].v, out[1].v)
+            if R._mt3_args(*v, out=o) is None:
+                return None
+            args.append((v, m, o))
+        bits = args[0][0][0].bits
+        n_max = 8192 * (1 if bits == 128 else 2)
+        if any(math.prod(a[0][0].shape) // 3 > n_max for a in args):
+            return None
+        batched = []
+        for v, m, o in args:
+            nmul = self.nonce(plc)
+            nonces = tuple(self.nonce(plc) for _ in range(6))
+            batched.append((*v, nmul, m, nonces, o))
+        r = R.mul_trunc3_k2(batched, self.key_ptr(plc, 0))
+        if r is None:  # nonces are drawn: never fall back silently
+            raise RuntimeError("mul_trunc3 x2 declined after its checks")
+        from moose_amd.parallel.party import record_tail_traffic
+
+        out = []
+        for o0, o1 in r:
+            record_tail_traffic(self.stats, plc, _nbytes(o0) // 3)
+            out.append((PV(plc, o0), PV(plc, o1)))
+        return out
 
     def p_cross_plain(self, kind, plc, x0, x1, y0, y1):
         """The parties' cross terms with no zero share and no nonce drawn (the per-party

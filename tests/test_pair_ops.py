@@ -266,3 +266,25 @@ def test_b2a_prep_kernel_matches_generic(bits):
         outs.append((y.s0.v, y.s1.v))
     _eq(outs[0][0], outs[1][0])
     _eq(outs[0][1], outs[1][1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [64, 128])
+def test_mul_trunc_many_one_launch_matches_one_by_one(bits):
+    """Two independent fixed-point products in one launch (k_mul_trunc3_lat2) give bitwise
+    the shares of two k_mul_trunc3_lat launches with the same seed (same nonce order)."""
+    from moose_amd.runtime.session import HV
+
+    plc = ReplicatedPlacement(owners=("a", "b", "c"))
+    outs = []
+    for batched in (True, False):
+        sess = StackedSession("cuda", seed=5)
+        if not batched:
+            sess.p_mul_trunc2 = lambda *a, **k: None
+        xs = [rep.share(sess, plc, HV("a", _rand(shp, bits, "cuda", i)))
+              for i, shp in enumerate([(200,), (200,), (5, 40), (5, 40)])]
+        r = rep.mul_trunc_many(sess, [(xs[0], xs[1], 23, None), (xs[2], xs[3], 20, None)])
+        outs.append([(t.s0.v, t.s1.v) for t in r])
+    for (a0, a1), (b0, b1) in zip(*outs):
+        _eq(a0, b0)
+        _eq(a1, b1)
