@@ -999,6 +999,48 @@ def bit_planes(a: RT, start: int, count: int, nb=0) -> RT:
 _WEIGHTS = {}
 
 
+_CONSTS = {}
+
+
+def const_ints(values, bits, device) -> RT:
+    """A public constant vector of python ints on ``device``, made once per (values, bits,
+    device) and shared -- callers never write into it (no upload per evaluation; not
+    cached while a hipGraph is being captured: it would live in the graph's pool)."""
+    key = (tuple(int(v) for v in values), bits, str(device))
+    hit = _CONSTS.get(key)
+    if hit is not None:
+        return hit
+    t = from_ints(np.array(list(key[0]), dtype=object), bits, device)
+    if torch.device(device).type == "cpu" or not torch.cuda.is_current_stream_capturing():
+        _cache_put(_CONSTS, key, t, 4096)
+        _const_key[id(t)] = key
+    return t
+
+
+_const_key = {}  # id of a cached constant -> its _CONSTS key (constants are never freed)
+
+
+_LEADING = {}
+
+
+def mul_leading(a: RT, c: RT, nb: int) -> RT:
+    """a[.., i, ..] * c[i] along the first non-batch axis of ``a``: the public vector
+    broadcast to a's shape is made once per (constant, shape) when ``c`` is a shared
+    constant (const_ints), so an evaluation runs one multiply kernel and no copy."""
+    k = len(a.shape) - nb - 1
+    cb = reshape(c, (c.shape[0],) + (1,) * k)
+    shared = c.data.is_cuda and _CONSTS.get(_const_key.get(id(c))) is c
+    if not shared:
+        return binary("mul", a, cb)
+    key = (id(c), tuple(a.shape))
+    full = _LEADING.get(key)
+    if full is None:
+        full = RT(expand(cb, tuple(a.shape)).data.contiguous(), a.bits)
+        if not torch.cuda.is_current_stream_capturing():
+            _cache_put(_LEADING, key, full, 1024)
+    return binary("mul", a, full)
+
+
 def weighted_sum(a: RT, weights, nb=0) -> RT:
     """sum_j weights[j] * a[.., j, ..] over the leading logical axis (public integer
     weights, e.g. bit composition).  One kernel."""

@@ -576,7 +576,7 @@ def _exp2_parts(sess, a: RepFixed, negative: bool):
         cs.append(int(round((c - 1.0) * (1 << f))))
     cs += [0] * (npad - nint)
     ints = local(sess, ab, "Slice", slice=(f, f + npad, None))
-    cvec = R.from_ints(np.array(cs, dtype=object), bits, sess.device)
+    cvec = R.const_ints(cs, bits, sess.device)
     pc = sess.public(ints.plc, cvec)
     fac = RepTensor(ints.plc, bits, "arith",
                     *rep._sharewise(sess, "MulLeading", ints.plc, (ints.s0, ints.s1), (pc, pc)))

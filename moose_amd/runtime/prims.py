@@ -93,8 +93,7 @@ def _mul_leading(nb, a, c):
     if not _is_rt(a):
         k = a.dim() - nb - 1
         return a * c.reshape((c.shape[0],) + (1,) * k)
-    k = len(a.shape) - nb - 1
-    return R.binary("mul", a, R.reshape(c, (c.shape[0],) + (1,) * k))
+    return R.mul_leading(a, c, nb)
 
 
 @prim("Neg")
