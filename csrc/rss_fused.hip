@@ -103,6 +103,69 @@ __global__ void __launch_bounds__(256) k_trunc_pr3_lat(const T* __restrict__ s0,
   }
 }
 
+// A polynomial's tail in one launch: the public weighted sum of the powers stack S
+// ([3 parties][R rows][n], party stride ps, row stride rs, weights w[R] on the device), the
+// TruncPr of that sum (as k_trunc_pr3_lat: same streams, same nonces) and the public
+// constant c added to party 0's share (slot 0 of out0, slot 2 of out1) -- the values of
+// weighted_sum + trunc_pr + add_public.
+template <class T>
+__global__ void __launch_bounds__(256) k_wsum_trunc3_lat(
+    const T* __restrict__ S, int64_t ps, int64_t rs, int R, const T* __restrict__ w,
+    T* __restrict__ out0, T* __restrict__ out1, int64_t n, int64_t os, T cadd, int m,
+    mxd::KeySrc keys, uint64_t n_r0, uint64_t n_r1, uint64_t n_t, uint64_t n_m, uint64_t n_z0,
+    uint64_t n_z2) {
+  constexpr int EPB = 256 / 6;
+  __shared__ uint32_t rks[2][mxd::kKeyWords];
+  __shared__ uint64_t kl[6][EPB], kh[6][EPB];
+  mxd::stage_keys(rks, keys, 2);
+  constexpr int P = mxd::Lane<T>::kPer;
+  const int64_t nb = (n + P - 1) / P;
+  const int tid = threadIdx.x, s = tid / EPB, lb = tid % EPB;
+  const int key_of = (s == 1 || s == 5) ? 1 : 0;
+  const uint64_t nonce_of = s == 0 ? n_r0 : s == 1 ? n_r1 : s == 2 ? n_t : s == 3 ? n_m
+                            : s == 4 ? n_z0 : n_z2;
+  for (int64_t b0 = (int64_t)blockIdx.x * EPB; b0 < nb; b0 += (int64_t)gridDim.x * EPB) {
+    if (s < 6 && b0 + lb < nb) {
+      uint64_t lo, hi;
+      mxd::prf_chunk(rks[key_of], nonce_of, (uint64_t)(b0 + lb), &lo, &hi);
+      kl[s][lb] = lo;
+      kh[s][lb] = hi;
+    }
+    __syncthreads();
+    if (tid < EPB && b0 + tid < nb) {
+      const int64_t b = b0 + tid;
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const int64_t i = b * P + j;
+        if (i >= n) break;
+        T x[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          T acc = 0;
+          for (int r = 0; r < R; ++r) acc += w[r] * S[p * ps + r * rs + i];
+          x[p] = acc;
+        }
+        const T z0 = mxd::pick<T>(kl[4][tid], kh[4][tid], j);
+        const T z2 = mxd::pick<T>(kl[5][tid], kh[5][tid], j);
+        const T z1 = mxf::trunc_pr_z1<T>(
+            x[0], x[1], x[2], mxd::pick<T>(kl[0][tid], kh[0][tid], j),
+            mxd::pick<T>(kl[1][tid], kh[1][tid], j), mxd::pick<T>(kl[2][tid], kh[2][tid], j),
+            mxd::pick<T>(kl[3][tid], kh[3][tid], j), z0, z2, m);
+        const T a0 = z0 + cadd;
+        out0[i] = a0;
+        out0[os + i] = z1;
+        out0[2 * os + i] = z2;
+        if (out1 != out0 + os) {
+          out1[i] = z1;
+          out1[os + i] = z2;
+        }
+        out1[2 * os + i] = a0;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 template <class T>
 __global__ void __launch_bounds__(256) k_share3(int kind, const void* __restrict__ xv, T* __restrict__ out0,
                          T* __restrict__ out1, int64_t n, int j0, mxd::KeySrc keys, uint64_t n1,
@@ -207,6 +270,32 @@ int launch_share3(int kind, int words, const void* x, void* out0, void* out1, in
 }  // namespace
 
 extern "C" {
+
+// k_wsum_trunc3_lat (latency-bound sizes only; -1 otherwise).  Strides in elements; cadd
+// little-endian words.
+int mxh_wsum_trunc3(int words, const void* S, int64_t ps, int64_t rs, int R,
+                               const void* w, void* out0, void* out1, int64_t n, int m,
+                               const uint32_t* k0, const uint32_t* k2, const uint64_t* nn,
+                               const uint64_t* cadd, void* stream) {
+  const int64_t nblk = words == 1 ? (n + 1) / 2 : n;
+  if (n <= 0 || R < 1 || nblk > 8192 || (words != 1 && words != 2)) return -1;
+  const uint32_t* ptrs[2] = {k0, k2};
+  const mxd::KeySrc keys = mxd::keysrc_slots(ptrs, 2);
+  const unsigned g = (unsigned)((nblk + 41) / 42);
+  hipStream_t st = (hipStream_t)stream;
+  if (words == 1)
+    hipLaunchKernelGGL(k_wsum_trunc3_lat<u64>, dim3(g), dim3(256), 0, st, (const u64*)S, ps, rs,
+                       R, (const u64*)w, (u64*)out0, (u64*)out1, n, n, (u64)cadd[0], m, keys,
+                       nn[0], nn[1], nn[2], nn[3], nn[4], nn[5]);
+  else
+    hipLaunchKernelGGL(k_wsum_trunc3_lat<u128>, dim3(g), dim3(256), 0, st, (const u128*)S, ps,
+                       rs, R, (const u128*)w, (u128*)out0, (u128*)out1, n, n,
+                       (((u128)cadd[1]) << 64) | cadd[0], m, keys, nn[0], nn[1], nn[2], nn[3],
+                       nn[4], nn[5]);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : -100 - (int)e;
+}
+
 
 int mxh_trunc_pr3(int words, const void* s0, void* out0, void* out1, int64_t n, int m,
                   const uint8_t* k0, const uint8_t* k2, const uint64_t* nn, void* stream) {

@@ -78,6 +78,10 @@ _SIGS = {
         [c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_int, c_vp,
          c_int, c_vp],
     ),
+    "mxh_wsum_trunc3": (
+        c_int, [c_int, c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp,
+                c_vp, c_vp, c_vp],
+    ),
     "mxh_mul_trunc3_kv2": (
         c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                 c_vp, c_vp],

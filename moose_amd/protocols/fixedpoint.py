@@ -439,9 +439,7 @@ def _poly_eval_rows(sess, x: RepFixed, coeffs, shift: int = 0) -> RepFixed:
             sess.p_rows_write(P1, have, z.s1)
         have += m
     P = RepTensor(t.plc, bits, t.kind, P0, P1)
-    acc = _weighted(sess, P, [int(round(c * (1 << f))) for c in coeffs[1:]], bits)
-    acc = rep.trunc_pr(sess, acc, f + shift)
-    return add_const(sess, RepFixed(acc, f, x.integ), coeffs[0] / (1 << shift))
+    return _poly_tail(sess, P, coeffs, f, shift, x.integ)
 
 
 def _batched_mul(sess, xs, ys):
@@ -659,9 +657,23 @@ def _poly_and_tree(sess, x: RepFixed, coeffs, shift: int, F: RepFixed, nf: int):
     Pt = RepTensor(t.plc, bits, t.kind, P0, P1) if rows else P.t
     if n <= 1:
         Pt = local(sess, x, "ExpandDims", axis=[0]).t
-    acc = _weighted(sess, Pt, [int(round(c * (1 << f))) for c in coeffs[1:]], bits)
+    return _poly_tail(sess, Pt, coeffs, f, shift, x.integ), F
+
+
+def _poly_tail(sess, Pt: RepTensor, coeffs, f: int, shift: int, integ: int) -> RepFixed:
+    """sum_k c_k P[k-1] truncated by f + shift, plus c_0 / 2^shift: one launch on a stacked
+    device session (p_wsum_trunc_add), else weighted sum + TruncPr + add (same shares)."""
+    bits = Pt.bits
+    weights = [int(round(c * (1 << f))) for c in coeffs[1:]]
+    c0 = coeffs[0] / (1 << shift)
+    fused = getattr(sess, "p_wsum_trunc_add", None)
+    if fused is not None and getattr(sess, "fused", False):
+        r = fused(Pt.plc, Pt.s0, weights, f + shift, int(round(c0 * (1 << f))))
+        if r is not None:
+            return RepFixed(RepTensor(Pt.plc, bits, "arith", r[0], r[1]), f, integ)
+    acc = _weighted(sess, Pt, weights, bits)
     acc = rep.trunc_pr(sess, acc, f + shift)
-    return add_const(sess, RepFixed(acc, f, x.integ), coeffs[0] / (1 << shift)), F
+    return add_const(sess, RepFixed(acc, f, integ), c0)
 
 
 def _tail_trunc(sess, plc, v, bits, m) -> RepTensor:

@@ -799,6 +799,44 @@ class StackedSession(Session):
         self._trunc_traffic(x, out0.numel() * out0.element_size() // 3)
         return PV(x.plc, R.RT(out0, x.bits)), PV(x.plc, R.RT(out1, x.bits))
 
+    def p_wsum_trunc_add(self, plc, S, weights, m, cadd: int):
+        """rep.trunc_pr(weighted sum of the powers stack ``S`` (a party vector [3, R, ...]),
+        m) + the public constant ``cadd`` on party 0's share, in one launch
+        (k_wsum_trunc3_lat); the nonces drawn as trunc_pr draws them.  None -> the three
+        steps."""
+        import ctypes
+
+        from moose_amd.ops import native as nat
+
+        v = S.v
+        if (self.device.type != "cuda" or not isinstance(v, R.RT) or v.bits not in (64, 128)
+                or not m or len(v.shape) < 2):
+            return None
+        d = v.data
+        w = 2 if v.bits == 128 else 1
+        Rr, inner = v.shape[1], math.prod(v.shape[2:])
+        if (d.stride(0) % w or d.stride(1) % w or not d[0, 0].is_contiguous()
+                or d[0, 0].numel() != inner * w or Rr != len(weights)):
+            return None
+        nblk = inner if w == 2 else (inner + 1) // 2
+        if inner == 0 or nblk > 8192:
+            return None
+        wt = R.const_ints([int(x) % (1 << v.bits) for x in weights], v.bits, self.device)
+        nr0, nr1, nt, nm, n0, n2 = (self.nonce(plc) for _ in range(6))
+        nn = (ctypes.c_uint64 * 6)(*[x & ((1 << 64) - 1) for x in (nr0, nr1, nt, nm, n0, n2)])
+        c = cadd % (1 << v.bits)
+        ca = (ctypes.c_uint64 * 2)(c & ((1 << 64) - 1), c >> 64)
+        out0, out1 = (t.data for t in R.ring4((3,) + tuple(v.shape[2:]), v.bits, d.device))
+        nat.check(nat.lib().mxh_wsum_trunc3(
+            R._words(v.bits), nat.ptr(d), d.stride(0) // w, d.stride(1) // w, Rr,
+            nat.ptr(wt.data), nat.ptr(out0), nat.ptr(out1), inner, int(m),
+            ctypes.c_void_p(self.key_ptr(plc, 0)), ctypes.c_void_p(self.key_ptr(plc, 2)), nn, ca,
+            nat.stream_of(d)), "wsum_trunc3")
+        x = type("X", (), {})()
+        x.plc = plc
+        self._trunc_traffic(x, out0.numel() * out0.element_size() // 3)
+        return PV(plc, R.RT(out0, v.bits)), PV(plc, R.RT(out1, v.bits))
+
     def _trunc_traffic(self, x, nbytes):
         o = x.plc.owners
         # messages of the protocol: dealer -> P1 (2 tensors), P0 <-> P1 (two rounds)

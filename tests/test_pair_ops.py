@@ -288,3 +288,31 @@ def test_mul_trunc_many_one_launch_matches_one_by_one(bits):
     for (a0, a1), (b0, b1) in zip(*outs):
         _eq(a0, b0)
         _eq(a1, b1)
+
+
+@pytest.mark.gpu
+def test_poly_tail_one_launch_matches_three_steps(monkeypatch):
+    """A polynomial's tail (weighted sum of the powers + TruncPr + constant) in one launch
+    gives bitwise the values of the three steps (seeded sigmoid: two polynomials)."""
+    import moose_amd as pm
+
+    alice, bob, carole = (pm.host_placement(n) for n in ("alice", "bob", "carole"))
+    r = pm.replicated_placement("rep", players=[alice, bob, carole])
+
+    @pm.computation
+    def f(x: pm.Argument(placement=alice, vtype=pm.TensorType(pm.float64))):
+        with alice:
+            xf = pm.cast(x, dtype=pm.fixed(24, 40))
+        with r:
+            y = pm.sigmoid(xf)
+        with carole:
+            return pm.cast(y, dtype=pm.float64)
+
+    x = np.linspace(-5, 5, 61)
+    got = pm.LocalMooseRuntime(["alice", "bob", "carole"], device="cuda", seed=3,
+                               use_graphs=False).evaluate_computation(f, {"x": x})
+    monkeypatch.setattr(StackedSession, "p_wsum_trunc_add", lambda *a, **k: None)
+    want = pm.LocalMooseRuntime(["alice", "bob", "carole"], device="cuda", seed=3,
+                                use_graphs=False).evaluate_computation(f, {"x": x})
+    np.testing.assert_array_equal(list(got.values())[0], list(want.values())[0])
+    np.testing.assert_allclose(list(got.values())[0], 1 / (1 + np.exp(-x)), atol=1e-4)
