@@ -124,12 +124,25 @@ __global__ void __launch_bounds__(256) k_wsum_trunc3_lat(
   const int key_of = (s == 1 || s == 5) ? 1 : 0;
   const uint64_t nonce_of = s == 0 ? n_r0 : s == 1 ? n_r1 : s == 2 ? n_t : s == 3 ? n_m
                             : s == 4 ? n_z0 : n_z2;
+  __shared__ T xs[3][EPB][P];
   for (int64_t b0 = (int64_t)blockIdx.x * EPB; b0 < nb; b0 += (int64_t)gridDim.x * EPB) {
     if (s < 6 && b0 + lb < nb) {
       uint64_t lo, hi;
       mxd::prf_chunk(rks[key_of], nonce_of, (uint64_t)(b0 + lb), &lo, &hi);
       kl[s][lb] = lo;
       kh[s][lb] = hi;
+    }
+    // the weighted sums, one (party, chunk) per thread (3 x EPB of the 256), into LDS
+    if (tid < 3 * EPB && b0 + (tid % EPB) < nb) {
+      const int p = tid / EPB, c = tid % EPB;
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const int64_t i = (b0 + c) * P + j;
+        T acc = 0;
+        if (i < n)
+          for (int r = 0; r < R; ++r) acc += w[r] * S[p * ps + r * rs + i];
+        xs[p][c][j] = acc;
+      }
     }
     __syncthreads();
     if (tid < EPB && b0 + tid < nb) {
@@ -138,13 +151,7 @@ __global__ void __launch_bounds__(256) k_wsum_trunc3_lat(
       for (int j = 0; j < P; ++j) {
         const int64_t i = b * P + j;
         if (i >= n) break;
-        T x[3];
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          T acc = 0;
-          for (int r = 0; r < R; ++r) acc += w[r] * S[p * ps + r * rs + i];
-          x[p] = acc;
-        }
+        const T x[3] = {xs[0][tid][j], xs[1][tid][j], xs[2][tid][j]};
         const T z0 = mxd::pick<T>(kl[4][tid], kh[4][tid], j);
         const T z2 = mxd::pick<T>(kl[5][tid], kh[5][tid], j);
         const T z1 = mxf::trunc_pr_z1<T>(
