@@ -683,6 +683,90 @@ __global__ void __launch_bounds__(256) k_ks_adder3(const T* __restrict__ g0, con
   }
 }
 
+// k_ks_adder3 for latency-bound launches: a block takes E = 6 elements and first computes
+// EVERY level's mask chunks in parallel (up to 8 levels x 6 streams x 6 elements, one
+// ChaCha block per thread), then one thread per element runs the whole carry chain from
+// LDS -- one keystream latency instead of one per level.  Same masks, same logic: bitwise
+// k_ks_adder3's result.
+template <class T>
+__global__ void __launch_bounds__(256) k_ks_adder3p(const T* __restrict__ g0, const T* __restrict__ g1,
+                                                    const T* __restrict__ p0, const T* __restrict__ p1,
+                                                    T* __restrict__ og0, T* __restrict__ og1,
+                                                    int64_t n, int nlev, KeySrc keys, Nonces8 nn) {
+  constexpr int E = 6;
+  constexpr int W = 8 * (int)sizeof(T);
+  __shared__ uint32_t rks[3][kKeyWords];
+  __shared__ T ks[8][6][E];
+  stage_keys(rks, keys, 3);
+  constexpr int P = Lane<T>::kPer;
+  const int tid = threadIdx.x;
+  for (int64_t e0 = (int64_t)blockIdx.x * E; e0 < n; e0 += (int64_t)gridDim.x * E) {
+    for (int q = tid; q < nlev * 6 * E; q += blockDim.x) {
+      const int lev = q / (6 * E), s = (q / E) % 6, le = q % E;
+      const bool both = 2 * (1 << lev) < W;
+      if (s >= (both ? 6 : 3) || e0 + le >= n) continue;
+      const int64_t c = (s < 3 ? 0 : n) + e0 + le;  // t at e, pk' at n + e
+      uint64_t lo, hi;
+      prf_chunk(rks[s % 3], nn.v[lev], (uint64_t)(c / P), &lo, &hi);
+      ks[lev][s][le] = pick<T>(lo, hi, (int)(c % P));
+    }
+    __syncthreads();
+    const int64_t e = e0 + tid;
+    if (tid < E && e < n) {
+      T G0[3], G1[3], A0[3], A1[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const int64_t i = (int64_t)p * n + e;
+        G0[p] = g0[i];
+        G1[p] = g1[i];
+        A0[p] = p0[i];
+        A1[p] = p1[i];
+      }
+      int d = 1;
+      for (int lev = 0; lev < nlev; ++lev, d *= 2) {
+        const bool both = 2 * d < W;
+        T t[3], q[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const int pn = p == 2 ? 0 : p + 1;
+          const T s0 = G0[p] << d, s1 = G1[p] << d;
+          t[p] = (A0[p] & s0) ^ (A0[p] & s1) ^ (A1[p] & s0) ^ ks[lev][p][tid] ^ ks[lev][pn][tid];
+          if (both) {
+            const T u0 = A0[p] << d, u1 = A1[p] << d;
+            q[p] = (A0[p] & u0) ^ (A0[p] & u1) ^ (A1[p] & u0) ^ ks[lev][3 + p][tid] ^
+                   ks[lev][3 + pn][tid];
+          } else {
+            q[p] = 0;
+          }
+        }
+        T nG1[3], nA1[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const int pn = p == 2 ? 0 : p + 1;
+          nG1[p] = G1[p] ^ t[pn];
+          nA1[p] = q[pn];
+        }
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          G0[p] ^= t[p];
+          G1[p] = nG1[p];
+          if (both) {
+            A0[p] = q[p];
+            A1[p] = nA1[p];
+          }
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const int64_t i = (int64_t)p * n + e;
+        og0[i] = G0[p];
+        og1[i] = G1[p];
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // One party's cross terms of a Kogge-Stone level (mx_ks_cross1): thread per element.
 template <class T>
 __global__ void __launch_bounds__(256) k_ks_cross1(const T* __restrict__ g0, const T* __restrict__ g1,
@@ -1617,7 +1701,16 @@ int mxh_ks_adder3_k(int words, const void* g0, const void* g1, const void* p0, c
   KeySrc k = mxd::keysrc_slots(ptrs, 3);
   Nonces8 nn{};
   for (int l = 0; l < nlev; ++l) nn.v[l] = nonces[l];
-  if (words == 1) {
+  if (n <= 65536 && (words == 1 || words == 2)) {  // latency-bound: masks first
+    if (words == 1)
+      hipLaunchKernelGGL(k_ks_adder3p<u64>, dim3(ks_grid(n, 6)), dim3(kBlock), 0, S(stream),
+                         (const u64*)g0, (const u64*)g1, (const u64*)p0, (const u64*)p1,
+                         (u64*)og0, (u64*)og1, n, nlev, k, nn);
+    else
+      hipLaunchKernelGGL(k_ks_adder3p<u128>, dim3(ks_grid(n, 6)), dim3(kBlock), 0, S(stream),
+                         (const u128*)g0, (const u128*)g1, (const u128*)p0, (const u128*)p1,
+                         (u128*)og0, (u128*)og1, n, nlev, k, nn);
+  } else if (words == 1) {
     hipLaunchKernelGGL(k_ks_adder3<u64>, dim3(ks_grid(n)), dim3(kBlock), 0, S(stream),
                        (const u64*)g0, (const u64*)g1, (const u64*)p0, (const u64*)p1,
                        (u64*)og0, (u64*)og1, n, nlev, k, nn);
