@@ -1441,7 +1441,7 @@ int launch_rss_cross(int kind, int words, const void* x0, const void* x1, const 
     constexpr int P = 16 / (int)sizeof(T);
     if (ring3) {
       const int64_t blocks = (n + P - 1) / P;
-      if (blocks <= 16384) {  // latency-bound launch: one PRF chunk per thread, via LDS
+      if (blocks <= 65536) {  // latency-bound launch: one PRF chunk per thread, via LDS
         const int64_t g = (blocks + 84) / 85;
         hipLaunchKernelGGL(k_rss_cross_ring3_lat<T>, dim3((unsigned)g), dim3(kBlock), 0,
                            S(stream), kind, (const T*)x0, (const T*)x1, (const T*)y0,
