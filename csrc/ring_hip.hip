@@ -608,7 +608,8 @@ template <class T>
 __global__ void __launch_bounds__(256) k_ks_adder3(const T* __restrict__ g0, const T* __restrict__ g1,
                                                    const T* __restrict__ p0, const T* __restrict__ p1,
                                                    T* __restrict__ og0, T* __restrict__ og1,
-                                                   int64_t n, int nlev, KeySrc keys, Nonces8 nn) {
+                                                   int64_t n, int nlev, KeySrc keys, Nonces8 nn,
+                                                   int sum_out) {
   constexpr int EPB = 256 / 6;
   constexpr int W = 8 * (int)sizeof(T);
   __shared__ uint32_t rks[3][kKeyWords];
@@ -676,8 +677,9 @@ __global__ void __launch_bounds__(256) k_ks_adder3(const T* __restrict__ g0, con
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
         const int64_t i = (int64_t)p * n + e;
-        og0[i] = G0[p];
-        og1[i] = G1[p];
+        // sum_out: the adder's result p ^ (g << 1) (share-wise) instead of the carries
+        og0[i] = sum_out ? (T)(p0[i] ^ (G0[p] << 1)) : G0[p];
+        og1[i] = sum_out ? (T)(p1[i] ^ (G1[p] << 1)) : G1[p];
       }
     }
   }
@@ -692,7 +694,8 @@ template <class T>
 __global__ void __launch_bounds__(256) k_ks_adder3p(const T* __restrict__ g0, const T* __restrict__ g1,
                                                     const T* __restrict__ p0, const T* __restrict__ p1,
                                                     T* __restrict__ og0, T* __restrict__ og1,
-                                                    int64_t n, int nlev, KeySrc keys, Nonces8 nn) {
+                                                    int64_t n, int nlev, KeySrc keys, Nonces8 nn,
+                                                   int sum_out) {
   constexpr int E = 6;
   constexpr int W = 8 * (int)sizeof(T);
   __shared__ uint32_t rks[3][kKeyWords];
@@ -759,8 +762,9 @@ __global__ void __launch_bounds__(256) k_ks_adder3p(const T* __restrict__ g0, co
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
         const int64_t i = (int64_t)p * n + e;
-        og0[i] = G0[p];
-        og1[i] = G1[p];
+        // sum_out: the adder's result p ^ (g << 1) (share-wise) instead of the carries
+        og0[i] = sum_out ? (T)(p0[i] ^ (G0[p] << 1)) : G0[p];
+        og1[i] = sum_out ? (T)(p1[i] ^ (G1[p] << 1)) : G1[p];
       }
     }
     __syncthreads();
@@ -1691,9 +1695,20 @@ int mxh_ks_level3_k(int words, const void* g0, const void* g1, const void* p0, c
   return 0;
 }
 
+int mxh_ks_adder3_sum(int words, const void* g0, const void* g1, const void* p0, const void* p1,
+                      void* og0, void* og1, int64_t n, int nlev, const uint32_t* slots,
+                      const uint64_t* nonces, void* stream, int sum_out);
+
 int mxh_ks_adder3_k(int words, const void* g0, const void* g1, const void* p0, const void* p1,
                     void* og0, void* og1, int64_t n, int nlev, const uint32_t* slots,
                     const uint64_t* nonces, void* stream) {
+  return mxh_ks_adder3_sum(words, g0, g1, p0, p1, og0, og1, n, nlev, slots, nonces, stream, 0);
+}
+
+// The chain, returning the adder's sum p ^ (g << 1) when ``sum_out`` (the carries otherwise).
+int mxh_ks_adder3_sum(int words, const void* g0, const void* g1, const void* p0, const void* p1,
+                      void* og0, void* og1, int64_t n, int nlev, const uint32_t* slots,
+                      const uint64_t* nonces, void* stream, int sum_out) {
   if (n == 0) return 0;
   if (nlev < 1 || nlev > 8) return -3;
   const uint32_t* ptrs[3];
@@ -1705,19 +1720,19 @@ int mxh_ks_adder3_k(int words, const void* g0, const void* g1, const void* p0, c
     if (words == 1)
       hipLaunchKernelGGL(k_ks_adder3p<u64>, dim3(ks_grid(n, 6)), dim3(kBlock), 0, S(stream),
                          (const u64*)g0, (const u64*)g1, (const u64*)p0, (const u64*)p1,
-                         (u64*)og0, (u64*)og1, n, nlev, k, nn);
+                         (u64*)og0, (u64*)og1, n, nlev, k, nn, sum_out);
     else
       hipLaunchKernelGGL(k_ks_adder3p<u128>, dim3(ks_grid(n, 6)), dim3(kBlock), 0, S(stream),
                          (const u128*)g0, (const u128*)g1, (const u128*)p0, (const u128*)p1,
-                         (u128*)og0, (u128*)og1, n, nlev, k, nn);
+                         (u128*)og0, (u128*)og1, n, nlev, k, nn, sum_out);
   } else if (words == 1) {
     hipLaunchKernelGGL(k_ks_adder3<u64>, dim3(ks_grid(n)), dim3(kBlock), 0, S(stream),
                        (const u64*)g0, (const u64*)g1, (const u64*)p0, (const u64*)p1,
-                       (u64*)og0, (u64*)og1, n, nlev, k, nn);
+                       (u64*)og0, (u64*)og1, n, nlev, k, nn, sum_out);
   } else if (words == 2) {
     hipLaunchKernelGGL(k_ks_adder3<u128>, dim3(ks_grid(n)), dim3(kBlock), 0, S(stream),
                        (const u128*)g0, (const u128*)g1, (const u128*)p0, (const u128*)p1,
-                       (u128*)og0, (u128*)og1, n, nlev, k, nn);
+                       (u128*)og0, (u128*)og1, n, nlev, k, nn, sum_out);
   } else {
     return -2;
   }

@@ -117,6 +117,10 @@ _SIGS = {
         c_int,
         [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp],
     ),
+    "mxh_ks_adder3_sum": (
+        c_int,
+        [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_int],
+    ),
     "mx_ks_level3_k": (
         c_int,
         [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int,

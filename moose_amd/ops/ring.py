@@ -1556,15 +1556,23 @@ def ks_cross1_s(g0: RT, g1: RT, p0: RT, p1: RT, d: int, both: bool, slot_ptrs,
     return z
 
 
-def ks_adder3_k(g0: RT, g1: RT, p0: RT, p1: RT, slot_ptr: int, nonces) -> tuple:
+def ks_adder3_k(g0: RT, g1: RT, p0: RT, p1: RT, slot_ptr: int, nonces,
+                sum_out: bool = False) -> tuple:
     """The whole Kogge-Stone carry chain (len(nonces) levels d = 1, 2, 4, ...) for three
     stacked parties in one launch (mx_ks_adder3_k): bitwise the chain of ks_level3_k calls
-    with those nonces; returns the final (g0, g1)."""
+    with those nonces; returns the final (g0, g1) -- or, with ``sum_out`` (device only),
+    the adder's sum p ^ (g << 1) (p = the initial p0, p1)."""
     bits = g0.bits
     datas = [x.data.contiguous() for x in (g0, g1, p0, p1)]
     n = math.prod(g0.shape) // 3
     o0, o1 = empty2(g0.shape, bits, g0.device)
     arr = (ctypes.c_uint64 * len(nonces))(*[int(v) & MASK64 for v in nonces])
+    if sum_out:
+        nat.check(nat.lib().mxh_ks_adder3_sum(
+            _words(bits), *[nat.ptr(x) for x in datas], nat.ptr(o0.data), nat.ptr(o1.data), n,
+            len(nonces), ctypes.c_void_p(slot_ptr), arr, nat.stream_of(o0.data), 1),
+            "ks_adder3 (sum)")
+        return o0, o1
     nat.check(nat.lib().mx_ks_adder3_k(
         nat.dev_of(o0.data), _words(bits), *[nat.ptr(x) for x in datas], nat.ptr(o0.data),
         nat.ptr(o1.data), n, len(nonces), ctypes.c_void_p(slot_ptr), arr,

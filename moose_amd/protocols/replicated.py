@@ -679,10 +679,10 @@ def binary_adder(sess, a: RepTensor, b: RepTensor) -> RepTensor:
     level = getattr(sess, "p_ks_level", None) if fused else None
     chain = getattr(sess, "p_ks_adder", None) if fused else None
     if chain is not None and bits in (64, 128):
-        r = chain(a.plc, g.s0, g.s1, pk.s0, pk.s1, bits)
-        if r is not None:  # stacked device session: the whole chain in one kernel
-            g = RepTensor(a.plc, bits, "bool", r[0], r[1])
-            return xor(sess, p, shl(sess, g, 1))
+        # stacked device session: the whole chain and the final p ^ (g << 1) in one kernel
+        r = chain(a.plc, g.s0, g.s1, pk.s0, pk.s1, bits, sum_out=True)
+        if r is not None:
+            return RepTensor(a.plc, bits, "bool", r[0], r[1])
     if level is not None and bits in (64, 128):
         # stacked session: each level (shifts, both ANDs, reshare, xor) is one kernel
         while d < bits:

@@ -620,14 +620,16 @@ class StackedSession(Session):
                              nonces, [s0[c] for c in range(3)], [s1[c] for c in range(3)], slots)
         return PV(plc, R.RT(s0, bits)), PV(plc, R.RT(s1, bits))
 
-    def p_ks_adder(self, plc, g0, g1, p0, p1, bits):
+    def p_ks_adder(self, plc, g0, g1, p0, p1, bits, sum_out=False):
         """rep.binary_adder's carry chain, all log2(bits) levels in one kernel (device
-        sessions); the nonces of the per-level chain, in its order.  None on the host."""
+        sessions); the nonces of the per-level chain, in its order.  ``sum_out``: the
+        adder's sum p ^ (g << 1) instead of the carries.  None on the host."""
         if self.device.type != "cuda":
             return None
         nlev = bits.bit_length() - 1
         nonces = [self.nonce(plc) for _ in range(nlev)]
-        o0, o1 = R.ks_adder3_k(g0.v, g1.v, p0.v, p1.v, self.key_ptr(plc, 0), nonces)
+        o0, o1 = R.ks_adder3_k(g0.v, g1.v, p0.v, p1.v, self.key_ptr(plc, 0), nonces,
+                               sum_out=sum_out)
         d = 1
         for _ in range(nlev):  # the rounds of the chain it replaces
             self.stats.record_round(_nbytes(o0) * (2 if 2 * d < bits else 1))

@@ -42,3 +42,22 @@ def test_ks_adder_chain_host(bits):
 def test_ks_adder_chain_gpu(bits):
     fused, chain, _ = _chain(bits, "cuda")
     assert torch.equal(fused[0].data, chain[0].data) and torch.equal(fused[1].data, chain[1].data)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [64, 128])
+def test_ks_adder_sum_out_gpu(bits):
+    """The adder kernel's sum output equals p ^ (g << 1) of its carry output, share-wise."""
+    kt = KeyTable("cuda", capacity=8)
+    base = kt.alloc(3)
+    g = torch.Generator().manual_seed(bits + 1)
+    n = 257
+    mk = lambda: R.RT(torch.randint(-2**62, 2**62, (3, n) + ((2,) if bits == 128 else ()),  # noqa: E731
+                                    dtype=torch.int64, generator=g).to("cuda"), bits)
+    g0, g1, p0, p1 = mk(), mk(), mk(), mk()
+    nonces = [77 + i for i in range(bits.bit_length() - 1)]
+    G0, G1 = R.ks_adder3_k(g0, g1, p0, p1, kt.ptr(base), nonces)
+    S0, S1 = R.ks_adder3_k(g0, g1, p0, p1, kt.ptr(base), nonces, sum_out=True)
+    for p, G, S in ((p0, G0, S0), (p1, G1, S1)):
+        want = R.binary("xor", p, R.shl(G, 1))
+        assert torch.equal(want.data.cpu(), S.data.cpu())
