@@ -313,6 +313,64 @@ __global__ void __launch_bounds__(256) k_b2a_prep3(const uint8_t* __restrict__ s
   }
 }
 
+// The whole of rep.b2a for three stacked parties in ONE launch: P0 shares a = b_0 ^ b_1
+// (the sharing mask r = PRF(k_mir, n1); slots (r, a - r, 0), mirrored (a - r, r, 0)), the
+// product of that sharing with the trivial sharing of b_2 (slot 2) and its zero share
+// PRF(k_p, nmul) - PRF(k_{p+1}, nmul), and the lincomb A + B - 2 AB.  With A_2 = B_0 = B_1 =
+// 0 the cross terms are c_0 = 0, c_1 = A_1 b_2, c_2 = A_0 b_2.  Four keystream chunks per
+// chunk position, one per thread into LDS (as k_rss_cross_ring3_lat), then EPB threads
+// finish the elements: bitwise the shares of b2a_prep3 + share3 + rss_mul3 + lincomb2.
+template <class T>
+__global__ void __launch_bounds__(256) k_b2a3(const uint8_t* __restrict__ s0,
+                                              const uint8_t* __restrict__ s1,
+                                              T* __restrict__ out0, T* __restrict__ out1,
+                                              int64_t n, mxd::KeySrc keys, int mir, uint64_t n1,
+                                              uint64_t nmul) {
+  constexpr int EPB = 64;
+  __shared__ uint32_t rks[3][mxd::kKeyWords];
+  __shared__ uint64_t kl[4][EPB], kh[4][EPB];
+  mxd::stage_keys(rks, keys, 3);
+  constexpr int P = mxd::Lane<T>::kPer;
+  const int64_t nb = (n + P - 1) / P;
+  const int tid = threadIdx.x, s = tid / EPB, lb = tid % EPB;
+  const int key_of = s < 3 ? s : mir;  // s < 3: the product's zero share; 3: the mask
+  const uint64_t nonce_of = s < 3 ? nmul : n1;
+  const bool r4 = out1 == out0 + n;  // 4-slot ring: out1's slots 0, 1 are out0's 1, 2
+  for (int64_t b0 = (int64_t)blockIdx.x * EPB; b0 < nb; b0 += (int64_t)gridDim.x * EPB) {
+    if (b0 + lb < nb) {
+      uint64_t lo, hi;
+      mxd::prf_chunk(rks[key_of], nonce_of, (uint64_t)(b0 + lb), &lo, &hi);
+      kl[s][lb] = lo;
+      kh[s][lb] = hi;
+    }
+    __syncthreads();
+    if (tid < EPB && b0 + tid < nb) {
+      const int64_t b = b0 + tid;
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const int64_t e = b * P + j;
+        if (e >= n) break;
+        const T a = (T)((s0[e] ^ s1[e]) & 1);
+        const T x2 = (T)(s0[2 * n + e] & 1), x2b = (T)(s1[n + e] & 1);  // P2's, P1's b_2
+        const T r = mxd::pick<T>(kl[3][tid], kh[3][tid], j);
+        const T v = a - r;
+        const T A0 = mir ? v : r, A1 = mir ? r : v;
+        const T k0 = mxd::pick<T>(kl[0][tid], kh[0][tid], j);
+        const T k1 = mxd::pick<T>(kl[1][tid], kh[1][tid], j);
+        const T k2 = mxd::pick<T>(kl[2][tid], kh[2][tid], j);
+        const T z0 = k0 - k1, z1 = A1 * x2b + k1 - k2, z2 = A0 * x2 + k2 - k0;
+        const T o[3] = {(T)(A0 - (z0 << 1)), (T)(A1 - (z1 << 1)), (T)(x2 - (z2 << 1))};
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          out0[p * n + e] = o[p];
+          if (!r4 || p == 2) out1[p * n + e] = o[p == 2 ? 0 : p + 1];
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 template <class T>
 __global__ void __launch_bounds__(256) k_encode(const double* __restrict__ x, T* __restrict__ out, int64_t n,
                          double scale) {
@@ -1306,6 +1364,23 @@ int mxh_b2a_prep3(int words, const uint8_t* s0, const uint8_t* s1, int64_t n, vo
   DEV_DISPATCH(words, T, {
     hipLaunchKernelGGL(k_b2a_prep3<T>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream), s0, s1,
                        n, (T*)a, (T*)b0, (T*)b1);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+// slots: three consecutive key slots (k0, k1, k2 of the placement)
+int mxh_b2a3(int words, const uint8_t* s0, const uint8_t* s1, int64_t n, void* out0,
+             void* out1, const uint32_t* slots, int mir, uint64_t n1, uint64_t nmul,
+             void* stream) {
+  if (n == 0) return 0;
+  const uint32_t* ptrs[3];
+  for (int i = 0; i < 3; ++i) ptrs[i] = slots + MX_KEY_SLOT_WORDS * i;
+  DEV_DISPATCH(words, T, {
+    constexpr int P = 16 / (int)sizeof(T);
+    const int64_t g = std::min<int64_t>(((n + P - 1) / P + 63) / 64, 16384);
+    hipLaunchKernelGGL(k_b2a3<T>, dim3((unsigned)g), dim3(256), 0, S(stream), s0, s1,
+                       (T*)out0, (T*)out1, n, mxd::keysrc_slots(ptrs, 3), mir ? 1 : 0, n1, nmul);
     MX_LAUNCH_CHECK();
     return 0;
   });

@@ -1504,6 +1504,24 @@ def b2a_prep3(b0: RT, b1: RT, ring_bits: int):
     return a, o0, o1
 
 
+def b2a3(b0: RT, b1: RT, ring_bits: int, slot_ptr: int, mir: bool, n1: int, nmul: int):
+    """The whole of rep.b2a for three stacked parties in one launch (k_b2a3): P0's sharing
+    of a = b_0 ^ b_1 (mask nonce n1, key k_0, or k_1 mirrored), its product with the trivial
+    sharing of b_2 (zero-share nonce nmul) and A + B - 2 AB.  Returns the (s0, s1) pair of
+    [3, ...] arithmetic share vectors, or None when not on the device."""
+    d0, d1 = b0.data, b1.data
+    if not d0.is_cuda or ring_bits not in (64, 128) or d0.dtype != torch.uint8 \
+            or d1.dtype != torch.uint8 or d0.shape != d1.shape or d0.shape[0] != 3:
+        return None
+    d0, d1 = d0.contiguous(), d1.contiguous()
+    o0, o1 = ring4(tuple(d0.shape), ring_bits, d0.device)
+    nat.check(nat.lib().mxh_b2a3(_words(ring_bits), nat.ptr(d0), nat.ptr(d1),
+                                 math.prod(d0.shape[1:]), nat.ptr(o0.data), nat.ptr(o1.data),
+                                 ctypes.c_void_p(slot_ptr), int(bool(mir)), n1 & MASK64,
+                                 nmul & MASK64, nat.stream_of(d0)), "b2a3")
+    return o0, o1
+
+
 def slot_place2(x0: RT, x1: RT, which0: int, which1: int, nparties: int = 3):
     """Two trivial stacked sharings [nparties, *x.shape] in one launch: slot which0 of the
     first = x0, slot which1 of the second = x1, zeros elsewhere (mx_slot_place2)."""

@@ -372,6 +372,25 @@ class StackedSession(Session):
         a, o0, o1 = r
         return HV(plc.owners[0], a), PV(plc, o0), PV(plc, o1)
 
+    def p_b2a(self, plc, b, ring_bits):
+        """The whole of rep.b2a in one kernel (device, fused session): the same nonces in
+        the same order (share: n1, na; mul: nmul) and the same traffic records as the
+        share + mul + lincomb steps, so the same shares.  None -> those steps."""
+        if self.device.type != "cuda" or not getattr(self, "fused", False) \
+                or os.environ.get("MOOSEX_B2A_FUSED", "1") == "0":
+            return None
+        v0, v1 = b.s0.v, b.s1.v
+        if not (isinstance(v0, R.RT) and isinstance(v1, R.RT)) or v0.bits != 1 \
+                or ring_bits not in (64, 128) or not v0.data.is_cuda:
+            return None
+        d = self.share_dir(plc, 0)
+        n1, _na, nmul = self.nonce(plc), self.nonce(plc), self.nonce(plc)
+        o0, o1 = R.b2a3(v0, v1, ring_bits, self.key_ptr(plc, 0), d == 2, n1, nmul)
+        nb = math.prod(v0.shape[1:]) * (ring_bits // 8)
+        self.stats.record_send(plc.owners[0], plc.owners[d % 3], nb)
+        self.stats.record_round(3 * nb)
+        return PV(plc, o0), PV(plc, o1)
+
     def p_from_slot_holders(self, plc, slot, x_h0, x_h1, like):
         """rep.from_slot_holders in one kernel (None -> generic path)."""
         v0, v1 = x_h0.v, x_h1.v

@@ -258,6 +258,7 @@ def test_b2a_prep_kernel_matches_generic(bits):
     outs = []
     for fused in (True, False):
         sess = StackedSession("cuda", seed=7)
+        sess.p_b2a = lambda *a, **k: None
         if not fused:
             sess.p_b2a_prep = lambda *a, **k: None
         x = rep.share(sess, plc, HV("a", _rand((300,), bits, "cuda", 3)))
@@ -266,6 +267,39 @@ def test_b2a_prep_kernel_matches_generic(bits):
         outs.append((y.s0.v, y.s1.v))
     _eq(outs[0][0], outs[1][0])
     _eq(outs[0][1], outs[1][1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits,n,mirror", [(64, 301, False), (128, 300, False),
+                                           (128, 300, True), (64, 70001, False),
+                                           (128, 70001, True)])
+def test_b2a_one_kernel_matches_generic(bits, n, mirror):
+    """The whole of rep.b2a in one kernel (StackedSession.p_b2a, k_b2a3) gives bitwise the
+    shares, the nonce position and the traffic records of the share + mul + lincomb steps
+    (same seed; both share directions; latency and grid-stride sizes)."""
+    from moose_amd.runtime.session import HV
+
+    plc = ReplicatedPlacement(owners=("a", "b", "c"))
+    outs = []
+    for whole in (True, False):
+        sess = StackedSession("cuda", seed=11)
+        if mirror:
+            sess.share_dirs = {"a": 2}
+        if not whole:
+            sess.p_b2a = lambda *a, **k: None
+        xv = _rand((n,), bits, "cuda", 4)
+        x = rep.share(sess, plc, HV("a", xv))
+        y = rep.b2a(sess, rep.msb(sess, x), bits)
+        nxt = rep.share(sess, plc, HV("b", _rand((7,), bits, "cuda", 5)))  # next nonce
+        opened = rep.reveal(sess, y, "a").v
+        outs.append((y.s0.v, y.s1.v, nxt.s0.v, sess.stats.as_dict(), opened))
+    for i in (0, 1, 2, 4):
+        _eq(outs[0][i], outs[1][i])
+    st0, st1 = outs[0][3], outs[1][3]
+    for k in ("rounds", "reshare_bytes", "bytes", "messages"):
+        assert st0[k] == st1[k], k
+    sign = [v >> (bits - 1) for v in R.to_ints(xv).tolist()]
+    assert R.to_ints(outs[0][4]).tolist() == sign
 
 
 @pytest.mark.gpu
