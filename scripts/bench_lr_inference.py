@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--ring", type=int, default=128, choices=(64, 128))
     ap.add_argument("--graphs", action="store_true", help="replay captured hipGraphs")
     ap.add_argument("--cprofile", default=None, help="write a host-side cProfile summary")
+    ap.add_argument("--parties", action="store_true",
+                    help="the three parties as threads of this process, one stream each "
+                         "(LocalMooseRuntime device_map; replayed per-party tapes)")
     a = ap.parse_args()
     import torch
     from moose_amd.models.predictors.tutorial import logistic_regression_tutorial
@@ -38,8 +41,12 @@ def main():
     tm = logistic_regression_tutorial(a.ring)
     dtype, comp, X_test = tm.dtype, tm.computation, tm.x_test
     dev = a.device or ("cuda" if torch.cuda.is_available() else "cpu")
+    extra = {}
+    if a.parties:
+        extra = {"device_map": {r: "cuda:0" if dev == "cuda" else dev
+                                for r in ("alice", "bob", "carole")}, "timeout": 30}
     rt = LocalMooseRuntime(["alice", "bob", "carole"], device=dev, fixedpoint_ring=a.ring,
-                           use_graphs=a.graphs)
+                           use_graphs=a.graphs, **extra)
     args = {"x": X_test}
     for _ in range(a.warmup):
         out = rt.evaluate_computation(comp, args)
@@ -76,7 +83,8 @@ def main():
         "fixed": [dtype.integral_precision, dtype.fractional_precision], "max_abs_err_vs_sklearn": err,
         "data": "make_classification(random_state=5), sklearn LogisticRegression -> ONNX "
                 "-> predictors.from_onnx",
-        "layout": "stacked 3-party session on one GPU",
+        "layout": ("three party threads, one stream each, on one GPU" if a.parties
+                   else "stacked 3-party session on one GPU"),
     }))
 
 
