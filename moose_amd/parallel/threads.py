@@ -394,6 +394,10 @@ class PartyTapes:
         kinds, child, dst, src, nbytes, deps = [], [], [], [], [], []
         last = [None] * n
         sent_at = {}
+        # copies still reading a party's send buffers: that party's next segment waits for
+        # them (its graph pool may reuse a sent tensor's memory once the send is issued --
+        # write-after-read edges the send -> receive order alone does not give)
+        reading = [[] for _ in range(n)]
         for a in self.actions:
             p = a[1]
             if a[0] == "g":
@@ -402,13 +406,15 @@ class PartyTapes:
                 dst.append(0)
                 src.append(0)
                 nbytes.append(0)
-                deps.append([last[p]] if last[p] is not None else [])
+                deps.append(sorted(set(([last[p]] if last[p] is not None else []) + reading[p])))
+                reading[p] = []
                 last[p] = len(kinds) - 1
             elif a[0] == "rec":
-                sent_at[id(a[2])] = last[p]
+                sent_at[id(a[2])] = (last[p], p)
             else:
                 _, p, s, t, buf, ev = a
-                d = [x for x in (last[p], sent_at.get(id(ev))) if x is not None]
+                at, sender = sent_at.get(id(ev), (None, None))
+                d = [x for x in (last[p], at) if x is not None]
                 kinds.append(1)
                 child.append(0)
                 dst.append(buf.data_ptr())
@@ -416,6 +422,8 @@ class PartyTapes:
                 nbytes.append(t.numel() * t.element_size())
                 deps.append(sorted(set(d)))
                 last[p] = len(kinds) - 1
+                if sender is not None and sender != p:
+                    reading[sender].append(last[p])
         m = len(kinds)
         if os.environ.get("MOOSEX_PARTY_GRAPH_DAG") != "1":
             # the issue order as a total order (profiles/r4_party_graph.md: on one device

@@ -138,12 +138,16 @@ def test_thread_parties_lr_inference_gpu(monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("composed", [True, False])
-def test_thread_party_tapes_replay_bitwise_equal_eager(composed, monkeypatch):
+@pytest.mark.parametrize("mode", ["serial", "dag", "per-action"])
+def test_thread_party_tapes_replay_bitwise_equal_eager(mode, monkeypatch):
     """Seeded sessions: a replay re-draws the seeded keys as a fresh eager evaluation does,
     so every replay's outputs equal the eager ones bitwise (parties on cuda:0): the tapes
-    composed into one hipGraph (default on one device), and the per-action replay."""
+    composed into one hipGraph in issue order (default on one device) or as a DAG of
+    program-order, send -> receive and copy -> sender's-next-segment edges, and the
+    per-action replay."""
+    composed = mode != "per-action"
     monkeypatch.setenv("MOOSEX_PARTY_GRAPH", "1" if composed else "0")
+    monkeypatch.setenv("MOOSEX_PARTY_GRAPH_DAG", "1" if mode == "dag" else "0")
     comp = _comp(False)
     args = _args()
     devs = {i: "cuda:0" for i in IDS}
