@@ -246,6 +246,17 @@ int mx_ks_cross1(int dev, int words, const void* g0, const void* g1, const void*
 int mx_ks_cross1_s(int dev, int words, const void* g0, const void* g1, const void* p0,
                    const void* p1, void* z, int64_t n, int d, int both,
                    const uint32_t* const* slots, uint64_t nonce, void* stream);
+// mx_ks_cross1_s with the previous level's xor folded in: the level's g is g ^ t (t = the
+// previous level's reshared AND, both share components), written to go0 / go1 and used for
+// the cross terms (t0 == null: plain mx_ks_cross1_s, go unused)
+int mx_ks_cross1x_s(int dev, int words, const void* g0, const void* g1, const void* t0,
+                    const void* t1, void* go0, void* go1, const void* p0, const void* p1,
+                    void* z, int64_t n, int d, int both, const uint32_t* const* slots,
+                    uint64_t nonce, void* stream);
+// The adder's sum after the last level, both share components: o = p ^ ((g ^ t) << 1)
+int mx_ks_sum2(int dev, int words, const void* p0, const void* p1, const void* g0,
+               const void* g1, const void* t0, const void* t1, void* o0, void* o1, int64_t n,
+               void* stream);
 // mx_prf_expand with nkeys consecutive key slots
 int mx_prf_expand_k(int dev, int words, void* out, int64_t n, int nkeys, const uint32_t* slots,
                     uint64_t nonce, void* stream);

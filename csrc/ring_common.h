@@ -227,6 +227,12 @@ int mxh_ks_cross1(int words, const void* g0, const void* g1, const void* p0, con
 int mxh_ks_cross1_s(int words, const void* g0, const void* g1, const void* p0, const void* p1,
                     void* z, int64_t n, int d, int both, const uint32_t* const* slots,
                     uint64_t nonce, void* stream);
+int mxh_ks_cross1x_s(int words, const void* g0, const void* g1, const void* t0, const void* t1,
+                     void* go0, void* go1, const void* p0, const void* p1, void* z, int64_t n,
+                     int d, int both, const uint32_t* const* slots, uint64_t nonce,
+                     void* stream);
+int mxh_ks_sum2(int words, const void* p0, const void* p1, const void* g0, const void* g1,
+                const void* t0, const void* t1, void* o0, void* o1, int64_t n, void* stream);
 int mxh_ks_adder3_k(int words, const void* g0, const void* g1, const void* p0, const void* p1,
                     void* og0, void* og1, int64_t n, int nlev, const uint32_t* slots,
                     const uint64_t* nonces, void* stream);

@@ -849,6 +849,44 @@ int mx_ks_cross1_s(int dev, int words, const void* g0, const void* g1, const voi
   return mx_ks_cross1(0, words, g0, g1, p0, p1, z, n, d, both, keys16, nonce, stream);
 }
 
+int mx_ks_cross1x_s(int dev, int words, const void* g0, const void* g1, const void* t0,
+                    const void* t1, void* go0, void* go1, const void* p0, const void* p1,
+                    void* z, int64_t n, int d, int both, const uint32_t* const* slots,
+                    uint64_t nonce, void* stream) {
+  if (dev)
+    return mxh_ks_cross1x_s(words, g0, g1, t0, t1, go0, go1, p0, p1, z, n, d, both, slots,
+                            nonce, stream);
+  if (t0 != nullptr) {  // g ^ t first, then the plain level on it
+    if (words != 1 && words != 2) return -2;
+    DISPATCH_WORDS(words, T, {
+      const T *G0 = (const T*)g0, *G1 = (const T*)g1, *A = (const T*)t0, *B = (const T*)t1;
+      T *O0 = (T*)go0, *O1 = (T*)go1;
+      for (int64_t e = 0; e < n; ++e) {
+        O0[e] = G0[e] ^ A[e];
+        O1[e] = G1[e] ^ B[e];
+      }
+      return mx_ks_cross1_s(0, words, go0, go1, p0, p1, z, n, d, both, slots, nonce, stream);
+    });
+  }
+  return mx_ks_cross1_s(0, words, g0, g1, p0, p1, z, n, d, both, slots, nonce, stream);
+}
+
+int mx_ks_sum2(int dev, int words, const void* p0, const void* p1, const void* g0,
+               const void* g1, const void* t0, const void* t1, void* o0, void* o1, int64_t n,
+               void* stream) {
+  if (dev) return mxh_ks_sum2(words, p0, p1, g0, g1, t0, t1, o0, o1, n, stream);
+  if (words != 1 && words != 2) return -2;
+  DISPATCH_WORDS(words, T, {
+    const T* P[2] = {(const T*)p0, (const T*)p1};
+    const T* G[2] = {(const T*)g0, (const T*)g1};
+    const T* X[2] = {(const T*)t0, (const T*)t1};
+    T* O[2] = {(T*)o0, (T*)o1};
+    for (int s = 0; s < 2; ++s)
+      for (int64_t e = 0; e < n; ++e) O[s][e] = P[s][e] ^ (T)((G[s][e] ^ X[s][e]) << 1);
+    return 0;
+  });
+}
+
 int mx_ks_adder3_k(int dev, int words, const void* g0, const void* g1, const void* p0,
                    const void* p1, void* og0, void* og1, int64_t n, int nlev,
                    const uint32_t* slots, const uint64_t* nonces, void* stream) {

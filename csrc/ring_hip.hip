@@ -829,12 +829,32 @@ __global__ void __launch_bounds__(256) k_ks_adder3p(const T* __restrict__ g0, co
   }
 }
 
-// One party's cross terms of a Kogge-Stone level (mx_ks_cross1): thread per element.
+// The adder's sum after the last level, both share components: p ^ ((g ^ t) << 1).
+template <class T>
+__global__ void __launch_bounds__(256) k_ks_sum2(const T* __restrict__ p0, const T* __restrict__ p1,
+                                                 const T* __restrict__ g0, const T* __restrict__ g1,
+                                                 const T* __restrict__ t0, const T* __restrict__ t1,
+                                                 T* __restrict__ o0, T* __restrict__ o1,
+                                                 int64_t n) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    o0[e] = p0[e] ^ (T)((g0[e] ^ t0[e]) << 1);
+    o1[e] = p1[e] ^ (T)((g1[e] ^ t1[e]) << 1);
+  }
+}
+
+// One party's cross terms of a Kogge-Stone level (mx_ks_cross1): thread per element.  With
+// t0 (mx_ks_cross1x_s) the level's g is g ^ t -- the previous level's xor, folded in --
+// and is written to go0 / go1 for the next level.
 template <class T>
 __global__ void __launch_bounds__(256) k_ks_cross1(const T* __restrict__ g0, const T* __restrict__ g1,
                                                    const T* __restrict__ p0, const T* __restrict__ p1,
                                                    T* __restrict__ z, int64_t n, int d, int both,
-                                                   KeySrc keys, uint64_t nonce) {
+                                                   KeySrc keys, uint64_t nonce,
+                                                   const T* __restrict__ t0 = nullptr,
+                                                   const T* __restrict__ t1 = nullptr,
+                                                   T* __restrict__ go0 = nullptr,
+                                                   T* __restrict__ go1 = nullptr) {
   __shared__ uint32_t rks[2][kKeyWords];
   stage_keys(rks, keys, 2);
   constexpr int P = Lane<T>::kPer;
@@ -844,7 +864,14 @@ __global__ void __launch_bounds__(256) k_ks_cross1(const T* __restrict__ g0, con
     prf_chunk(rks[0], nonce, (uint64_t)(e / P), &l0, &h0);
     prf_chunk(rks[1], nonce, (uint64_t)(e / P), &l1, &h1);
     const T a0 = p0[e], a1 = p1[e];
-    const T s0 = g0[e] << d, s1 = g1[e] << d;
+    T G0 = g0[e], G1 = g1[e];
+    if (t0 != nullptr) {
+      G0 ^= t0[e];
+      G1 ^= t1[e];
+      go0[e] = G0;
+      go1[e] = G1;
+    }
+    const T s0 = G0 << d, s1 = G1 << d;
     z[e] = (a0 & s0) ^ (a0 & s1) ^ (a1 & s0) ^ pick<T>(l0, h0, (int)(e % P)) ^
            pick<T>(l1, h1, (int)(e % P));
     if (both) {
@@ -1716,6 +1743,47 @@ int mxh_ks_cross1(int words, const void* g0, const void* g1, const void* p0, con
     hipLaunchKernelGGL(k_ks_cross1<u128>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
                        (const u128*)g0, (const u128*)g1, (const u128*)p0, (const u128*)p1,
                        (u128*)z, n, d, both, k, nonce);
+  } else {
+    return -2;
+  }
+  MX_LAUNCH_CHECK();
+  return 0;
+}
+
+int mxh_ks_cross1x_s(int words, const void* g0, const void* g1, const void* t0, const void* t1,
+                     void* go0, void* go1, const void* p0, const void* p1, void* z, int64_t n,
+                     int d, int both, const uint32_t* const* slots, uint64_t nonce,
+                     void* stream) {
+  if (n == 0) return 0;
+  KeySrc k = mxd::keysrc_slots(slots, 2);
+  if (words == 1) {
+    hipLaunchKernelGGL(k_ks_cross1<u64>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
+                       (const u64*)g0, (const u64*)g1, (const u64*)p0, (const u64*)p1, (u64*)z,
+                       n, d, both, k, nonce, (const u64*)t0, (const u64*)t1, (u64*)go0,
+                       (u64*)go1);
+  } else if (words == 2) {
+    hipLaunchKernelGGL(k_ks_cross1<u128>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
+                       (const u128*)g0, (const u128*)g1, (const u128*)p0, (const u128*)p1,
+                       (u128*)z, n, d, both, k, nonce, (const u128*)t0, (const u128*)t1,
+                       (u128*)go0, (u128*)go1);
+  } else {
+    return -2;
+  }
+  MX_LAUNCH_CHECK();
+  return 0;
+}
+
+int mxh_ks_sum2(int words, const void* p0, const void* p1, const void* g0, const void* g1,
+                const void* t0, const void* t1, void* o0, void* o1, int64_t n, void* stream) {
+  if (n == 0) return 0;
+  if (words == 1) {
+    hipLaunchKernelGGL(k_ks_sum2<u64>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
+                       (const u64*)p0, (const u64*)p1, (const u64*)g0, (const u64*)g1,
+                       (const u64*)t0, (const u64*)t1, (u64*)o0, (u64*)o1, n);
+  } else if (words == 2) {
+    hipLaunchKernelGGL(k_ks_sum2<u128>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
+                       (const u128*)p0, (const u128*)p1, (const u128*)g0, (const u128*)g1,
+                       (const u128*)t0, (const u128*)t1, (u128*)o0, (u128*)o1, n);
   } else {
     return -2;
   }

@@ -116,6 +116,14 @@ _SIGS = {
         c_int,
         [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_u64, c_vp],
     ),
+    "mx_ks_cross1x_s": (
+        c_int,
+        [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int,
+         c_vp, c_u64, c_vp],
+    ),
+    "mx_ks_sum2": (
+        c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp],
+    ),
     "mx_ks_adder3_k": (
         c_int,
         [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp],

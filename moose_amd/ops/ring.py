@@ -1574,6 +1574,42 @@ def ks_cross1_s(g0: RT, g1: RT, p0: RT, p1: RT, d: int, both: bool, slot_ptrs,
     return z
 
 
+def ks_cross1x_s(g0: RT, g1: RT, t0, t1, p0: RT, p1: RT, d: int, both: bool, slot_ptrs,
+                 nonce: int):
+    """ks_cross1_s on g ^ t (the previous level's xor folded into this level's launch;
+    t0 = t1 = None: plain ks_cross1_s).  Returns (z, (g0 ^ t0, g1 ^ t1) or None)."""
+    if t0 is None:
+        return ks_cross1_s(g0, g1, p0, p1, d, both, slot_ptrs, nonce), None
+    bits = g0.bits
+    shp = g0.shape
+    datas = [x.data.contiguous() for x in (g0, g1, t0, t1, p0, p1)]
+    n = math.prod(shp)
+    z = empty(((2,) + tuple(shp)) if both else tuple(shp), bits, g0.device)
+    go0, go1 = empty2(shp, bits, g0.device)
+    nat.check(
+        nat.lib().mx_ks_cross1x_s(
+            nat.dev_of(z.data), _words(bits), *[nat.ptr(x) for x in datas[:4]],
+            nat.ptr(go0.data), nat.ptr(go1.data), nat.ptr(datas[4]), nat.ptr(datas[5]),
+            nat.ptr(z.data), n, int(d), 1 if both else 0, _slots_arr(slot_ptrs),
+            nonce & MASK64, nat.stream_of(z.data),
+        ),
+        "ks_cross1x_s",
+    )
+    return z, (go0, go1)
+
+
+def ks_sum2(p0: RT, p1: RT, g0: RT, g1: RT, t0: RT, t1: RT):
+    """The adder's sum after its last level for both share components, one launch:
+    p ^ ((g ^ t) << 1) (mx_ks_sum2)."""
+    bits = p0.bits
+    datas = [x.data.contiguous() for x in (p0, p1, g0, g1, t0, t1)]
+    o0, o1 = empty2(p0.shape, bits, p0.device)
+    nat.check(nat.lib().mx_ks_sum2(
+        nat.dev_of(o0.data), _words(bits), *[nat.ptr(x) for x in datas], nat.ptr(o0.data),
+        nat.ptr(o1.data), math.prod(p0.shape), nat.stream_of(o0.data)), "ks_sum2")
+    return o0, o1
+
+
 def ks_adder3_k(g0: RT, g1: RT, p0: RT, p1: RT, slot_ptr: int, nonces,
                 sum_out: bool = False) -> tuple:
     """The whole Kogge-Stone carry chain (len(nonces) levels d = 1, 2, 4, ...) for three

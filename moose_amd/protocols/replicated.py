@@ -683,6 +683,12 @@ def binary_adder(sess, a: RepTensor, b: RepTensor) -> RepTensor:
         r = chain(a.plc, g.s0, g.s1, pk.s0, pk.s1, bits, sum_out=True)
         if r is not None:
             return RepTensor(a.plc, bits, "bool", r[0], r[1])
+    party_chain = getattr(sess, "p_ks_chain", None) if fused else None
+    if party_chain is not None and bits in (64, 128):
+        # per-party session: each level's xor rides in the next level's kernel
+        r = party_chain(a.plc, g.s0, g.s1, pk.s0, pk.s1, bits)
+        if r is not None:
+            return RepTensor(a.plc, bits, "bool", r[0], r[1])
     if level is not None and bits in (64, 128):
         # stacked session: each level (shifts, both ANDs, reshare, xor) is one kernel
         while d < bits:

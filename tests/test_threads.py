@@ -206,3 +206,22 @@ def test_party_tapes_schedule_pairs_rounds():
     pt.tapes = [_T([CommStep([], [(e(1), 1)])]), _T(["x"])]
     with pytest.raises(CaptureError):
         pt._schedule()
+
+
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_party_ks_chain_matches_per_level(dev, monkeypatch):
+    """SPMDSession.p_ks_chain (each level's xor folded into the next level's cross-term
+    kernel, the last xor into the sum kernel) gives bitwise the outputs of the per-level
+    path (p_ks_level + share-wise sum), seeded, with the same round count."""
+    comp = _comp(False)
+    args = _args()
+    outs = {}
+    for chain in ("1", "0"):
+        monkeypatch.setenv("MOOSEX_KS_CHAIN", chain)
+        rt = LocalMooseRuntime(IDS, device_map={i: dev for i in IDS}, seed=5, timeout=300,
+                               use_graphs=False)
+        outs[chain] = (rt.evaluate_computation(comp, args), rt.last_stats.rounds)
+    (a, ra), (b, rb) = outs["1"], outs["0"]
+    assert ra == rb
+    for k in b:
+        assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
