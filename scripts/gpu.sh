@@ -10,7 +10,8 @@
 #   variants  CRT GEMM variants (VARS="8 16")    pmc       CRT GEMM PMC passes (VARS)
 #   lrinf     LR-inference p50 + kernel profile dots/graphs  the dot-product sweeps
 #   calls     torch calls by moose_amd call site in one eager LR inference
-#   logreg    logistic-regression training sweep            aes  AES-in-MPC decrypt
+#   logreg    logistic-regression training sweep (LRGRAPHS=1: hipGraph replay)
+#   aes       AES-in-MPC decrypt
 #   coresid   GEMM + concurrent copy kernel co-residency trace
 #   cycprof   rocprofv3 kernel stats of the cyclic layout's per-GPU path (one GPU)
 #   ladder    the bench fallback ladder with a rank stalled in attempt 0 (one GPU, 3 ranks)
@@ -154,7 +155,7 @@ if has logreg; then
   rm -f gpurun_out/logreg.jsonl
   for it in 10 50 100; do for bs in 128 512 1024 2048; do
     run logreg_${bs}_${it} 600 python benchmarks/logreg_train.py --batch_size $bs --n_iter $it \
-      --n_exp 3 --json gpurun_out/logreg.jsonl
+      --n_exp 3 --json gpurun_out/logreg.jsonl ${LRGRAPHS:+--graphs}
   done; done
 fi
 if has aes; then
