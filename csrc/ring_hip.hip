@@ -745,9 +745,9 @@ __global__ void __launch_bounds__(256) k_ks_adder3(const T* __restrict__ g0, con
 
 // k_ks_adder3 for latency-bound launches: a block takes E = 6 elements and first computes
 // EVERY level's mask chunks in parallel (up to 8 levels x 6 streams x 6 elements, one
-// ChaCha block per thread), then one thread per element runs the whole carry chain from
-// LDS -- one keystream latency instead of one per level.  Same masks, same logic: bitwise
-// k_ks_adder3's result.
+// ChaCha block per thread), then three threads per element (one per party, exchanging t
+// and pk' through LDS) run the whole carry chain from LDS -- one keystream latency instead
+// of one per level.  Same masks, same logic: bitwise k_ks_adder3's result.
 template <class T>
 __global__ void __launch_bounds__(256) k_ks_adder3p(const T* __restrict__ g0, const T* __restrict__ g1,
                                                     const T* __restrict__ p0, const T* __restrict__ p1,
@@ -758,6 +758,7 @@ __global__ void __launch_bounds__(256) k_ks_adder3p(const T* __restrict__ g0, co
   constexpr int W = 8 * (int)sizeof(T);
   __shared__ uint32_t rks[3][kKeyWords];
   __shared__ T ks[8][6][E];
+  __shared__ T xt[2][3 * E], xq[2][3 * E];
   stage_keys(rks, keys, 3);
   constexpr int P = Lane<T>::kPer;
   const int tid = threadIdx.x;
@@ -772,58 +773,46 @@ __global__ void __launch_bounds__(256) k_ks_adder3p(const T* __restrict__ g0, co
       ks[lev][s][le] = pick<T>(lo, hi, (int)(c % P));
     }
     __syncthreads();
-    const int64_t e = e0 + tid;
-    if (tid < E && e < n) {
-      T G0[3], G1[3], A0[3], A1[3];
+    // the chain: one thread per (element, party), E x 3 threads; each level's t and pk'
+    // of party p + 1 come through LDS (double-buffered by level parity: one barrier per
+    // level); levels unrolled, so every shift is by a constant
+    const int le = tid / 3, p = tid - 3 * (tid / 3), pn = p == 2 ? 0 : p + 1;
+    const int64_t e = e0 + le;
+    const bool act = tid < 3 * E && e < n;
+    const int64_t i = (int64_t)p * n + e;
+    T G0 = act ? g0[i] : (T)0, G1 = act ? g1[i] : (T)0;
+    T A0 = act ? p0[i] : (T)0, A1 = act ? p1[i] : (T)0;
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        const int64_t i = (int64_t)p * n + e;
-        G0[p] = g0[i];
-        G1[p] = g1[i];
-        A0[p] = p0[i];
-        A1[p] = p1[i];
+    for (int lev = 0; lev < 8; ++lev) {
+      if (lev >= nlev) break;  // uniform over the block
+      const int d = 1 << lev;
+      const bool both = 2 * d < W;
+      T t = 0, q = 0;
+      if (act) {
+        const T s0 = G0 << d, s1 = G1 << d;
+        t = (A0 & s0) ^ (A0 & s1) ^ (A1 & s0) ^ ks[lev][p][le] ^ ks[lev][pn][le];
+        if (both) {
+          const T u0 = A0 << d, u1 = A1 << d;
+          q = (A0 & u0) ^ (A0 & u1) ^ (A1 & u0) ^ ks[lev][3 + p][le] ^ ks[lev][3 + pn][le];
+        }
+        xt[lev & 1][tid] = t;
+        xq[lev & 1][tid] = q;
       }
-      int d = 1;
-      for (int lev = 0; lev < nlev; ++lev, d *= 2) {
-        const bool both = 2 * d < W;
-        T t[3], q[3];
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          const int pn = p == 2 ? 0 : p + 1;
-          const T s0 = G0[p] << d, s1 = G1[p] << d;
-          t[p] = (A0[p] & s0) ^ (A0[p] & s1) ^ (A1[p] & s0) ^ ks[lev][p][tid] ^ ks[lev][pn][tid];
-          if (both) {
-            const T u0 = A0[p] << d, u1 = A1[p] << d;
-            q[p] = (A0[p] & u0) ^ (A0[p] & u1) ^ (A1[p] & u0) ^ ks[lev][3 + p][tid] ^
-                   ks[lev][3 + pn][tid];
-          } else {
-            q[p] = 0;
-          }
-        }
-        T nG1[3], nA1[3];
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          const int pn = p == 2 ? 0 : p + 1;
-          nG1[p] = G1[p] ^ t[pn];
-          nA1[p] = q[pn];
-        }
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          G0[p] ^= t[p];
-          G1[p] = nG1[p];
-          if (both) {
-            A0[p] = q[p];
-            A1[p] = nA1[p];
-          }
+      __syncthreads();
+      if (act) {
+        const int src = 3 * le + pn;
+        G1 ^= xt[lev & 1][src];
+        G0 ^= t;
+        if (both) {
+          A1 = xq[lev & 1][src];
+          A0 = q;
         }
       }
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        const int64_t i = (int64_t)p * n + e;
-        // sum_out: the adder's result p ^ (g << 1) (share-wise) instead of the carries
-        og0[i] = sum_out ? (T)(p0[i] ^ (G0[p] << 1)) : G0[p];
-        og1[i] = sum_out ? (T)(p1[i] ^ (G1[p] << 1)) : G1[p];
-      }
+    }
+    if (act) {
+      // sum_out: the adder's result p ^ (g << 1) (share-wise) instead of the carries
+      og0[i] = sum_out ? (T)(p0[i] ^ (G0 << 1)) : G0;
+      og1[i] = sum_out ? (T)(p1[i] ^ (G1 << 1)) : G1;
     }
     __syncthreads();
   }
