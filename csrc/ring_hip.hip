@@ -337,6 +337,17 @@ __global__ void __launch_bounds__(256) k_b2a3(const uint8_t* __restrict__ s0,
   const uint64_t nonce_of = s < 3 ? nmul : n1;
   const bool r4 = out1 == out0 + n;  // 4-slot ring: out1's slots 0, 1 are out0's 1, 2
   for (int64_t b0 = (int64_t)blockIdx.x * EPB; b0 < nb; b0 += (int64_t)gridDim.x * EPB) {
+    // the finishing threads' bits first: their loads overlap the keystream work
+    const bool fin = tid < EPB && b0 + tid < nb;
+    uint8_t ba[P], bx[P], by[P];
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const int64_t e = (b0 + tid) * P + j;
+      const bool ok = fin && e < n;
+      ba[j] = ok ? (uint8_t)(s0[e] ^ s1[e]) : 0;
+      bx[j] = ok ? s0[2 * n + e] : 0;
+      by[j] = ok ? s1[n + e] : 0;
+    }
     if (b0 + lb < nb) {
       uint64_t lo, hi;
       mxd::prf_chunk(rks[key_of], nonce_of, (uint64_t)(b0 + lb), &lo, &hi);
@@ -344,14 +355,14 @@ __global__ void __launch_bounds__(256) k_b2a3(const uint8_t* __restrict__ s0,
       kh[s][lb] = hi;
     }
     __syncthreads();
-    if (tid < EPB && b0 + tid < nb) {
+    if (fin) {
       const int64_t b = b0 + tid;
 #pragma unroll
       for (int j = 0; j < P; ++j) {
         const int64_t e = b * P + j;
         if (e >= n) break;
-        const T a = (T)((s0[e] ^ s1[e]) & 1);
-        const T x2 = (T)(s0[2 * n + e] & 1), x2b = (T)(s1[n + e] & 1);  // P2's, P1's b_2
+        const T a = (T)(ba[j] & 1);
+        const T x2 = (T)(bx[j] & 1), x2b = (T)(by[j] & 1);  // P2's, P1's b_2
         const T r = mxd::pick<T>(kl[3][tid], kh[3][tid], j);
         const T v = a - r;
         const T A0 = mir ? v : r, A1 = mir ? r : v;
@@ -763,17 +774,8 @@ __global__ void __launch_bounds__(256) k_ks_adder3p(const T* __restrict__ g0, co
   constexpr int P = Lane<T>::kPer;
   const int tid = threadIdx.x;
   for (int64_t e0 = (int64_t)blockIdx.x * E; e0 < n; e0 += (int64_t)gridDim.x * E) {
-    for (int q = tid; q < nlev * 6 * E; q += blockDim.x) {
-      const int lev = q / (6 * E), s = (q / E) % 6, le = q % E;
-      const bool both = 2 * (1 << lev) < W;
-      if (s >= (both ? 6 : 3) || e0 + le >= n) continue;
-      const int64_t c = (s < 3 ? 0 : n) + e0 + le;  // t at e, pk' at n + e
-      uint64_t lo, hi;
-      prf_chunk(rks[s % 3], nn.v[lev], (uint64_t)(c / P), &lo, &hi);
-      ks[lev][s][le] = pick<T>(lo, hi, (int)(c % P));
-    }
-    __syncthreads();
-    // the chain: one thread per (element, party), E x 3 threads; each level's t and pk'
+    // the chain: one thread per (element, party), E x 3 threads (its operands are loaded
+    // first, so their latency hides behind the keystream work); each level's t and pk'
     // of party p + 1 come through LDS (double-buffered by level parity: one barrier per
     // level); levels unrolled, so every shift is by a constant
     const int le = tid / 3, p = tid - 3 * (tid / 3), pn = p == 2 ? 0 : p + 1;
@@ -782,6 +784,16 @@ __global__ void __launch_bounds__(256) k_ks_adder3p(const T* __restrict__ g0, co
     const int64_t i = (int64_t)p * n + e;
     T G0 = act ? g0[i] : (T)0, G1 = act ? g1[i] : (T)0;
     T A0 = act ? p0[i] : (T)0, A1 = act ? p1[i] : (T)0;
+    for (int q = tid; q < nlev * 6 * E; q += blockDim.x) {
+      const int lev = q / (6 * E), s = (q / E) % 6, lq = q % E;
+      const bool both = 2 * (1 << lev) < W;
+      if (s >= (both ? 6 : 3) || e0 + lq >= n) continue;
+      const int64_t c = (s < 3 ? 0 : n) + e0 + lq;  // t at e, pk' at n + e
+      uint64_t lo, hi;
+      prf_chunk(rks[s % 3], nn.v[lev], (uint64_t)(c / P), &lo, &hi);
+      ks[lev][s][lq] = pick<T>(lo, hi, (int)(c % P));
+    }
+    __syncthreads();
 #pragma unroll
     for (int lev = 0; lev < 8; ++lev) {
       if (lev >= nlev) break;  // uniform over the block
@@ -893,6 +905,26 @@ __global__ void __launch_bounds__(256) k_rss_cross_ring3_lat(int kind, const T* 
   const int64_t nb = (n + P - 1) / P;
   const int tid = threadIdx.x, s = tid / EPB, lb = tid % EPB;
   for (int64_t b0 = (int64_t)blockIdx.x * EPB; b0 < nb; b0 += (int64_t)gridDim.x * EPB) {
+    // the finishing threads' cross terms first: their loads overlap the keystream work
+    const bool fin = tid < EPB && b0 + tid < nb;
+    T vv[3][P];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const int64_t e = (b0 + tid) * P + j;
+        T v = 0;
+        if (fin && e < n) {
+          if (x0 != nullptr && y0 != nullptr)
+            v = mxr::cross<T>(kind, ld_view(x0, vw, 0, p, e, n),
+                              x1 ? ld_view(x1, vw, 1, p, e, n) : (T)0, ld_view(y0, vw, 2, p, e, n),
+                              y1 ? ld_view(y1, vw, 3, p, e, n) : (T)0, x1 != nullptr, y1 != nullptr);
+          else if (x0 != nullptr)
+            v = ld_view(x0, vw, 0, p, e, n);
+        }
+        vv[p][j] = v;
+      }
+    }
     if (s < 3 && b0 + lb < nb) {
       uint64_t lo, hi;
       prf_chunk(rks[s], nonce, (uint64_t)(b0 + lb), &lo, &hi);
@@ -900,7 +932,7 @@ __global__ void __launch_bounds__(256) k_rss_cross_ring3_lat(int kind, const T* 
       kh[s][lb] = hi;
     }
     __syncthreads();
-    if (tid < EPB && b0 + tid < nb) {
+    if (fin) {
       const int64_t b = b0 + tid;
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
@@ -910,13 +942,7 @@ __global__ void __launch_bounds__(256) k_rss_cross_ring3_lat(int kind, const T* 
           const int64_t e = b * P + j;
           if (e >= n) break;
           const int64_t i = (int64_t)p * n + e;
-          T v = 0;
-          if (x0 != nullptr && y0 != nullptr)
-            v = mxr::cross<T>(kind, ld_view(x0, vw, 0, p, e, n),
-                              x1 ? ld_view(x1, vw, 1, p, e, n) : (T)0, ld_view(y0, vw, 2, p, e, n),
-                              y1 ? ld_view(y1, vw, 3, p, e, n) : (T)0, x1 != nullptr, y1 != nullptr);
-          else if (x0 != nullptr)
-            v = ld_view(x0, vw, 0, p, e, n);
+          const T v = vv[p][j];
           const T z = mxr::zs_combine<T>(kind, v, pick<T>(kl[p][tid], kh[p][tid], j),
                                          pick<T>(kl[q][tid], kh[q][tid], j));
           out[i] = z;
@@ -950,6 +976,20 @@ __device__ __forceinline__ void mul_trunc3_lat_body(
   const uint64_t nonce_of = s < 3 ? nmul : s == 3 ? nr0 : s == 4 ? nr1 : s == 5 ? nt
                             : s == 6 ? nm : s == 7 ? nz0 : nz2;
   for (int64_t b0 = (int64_t)blockIdx.x * EPB; b0 < nb; b0 += (int64_t)gridDim.x * EPB) {
+    // the finishing threads' cross products first: their loads overlap the keystream work
+    const bool fin = tid < EPB && b0 + tid < nb;
+    T vv[P][3];
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const int64_t e = (b0 + tid) * P + j;
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        vv[j][p] = !fin || e >= n ? (T)0
+                   : y0 == nullptr ? ld_view(x0, vw, 0, p, e, n)
+                   : mxr::cross<T>(MX_CROSS_ARITH, ld_view(x0, vw, 0, p, e, n),
+                                   ld_view(x1, vw, 1, p, e, n), ld_view(y0, vw, 2, p, e, n),
+                                   ld_view(y1, vw, 3, p, e, n), true, true);
+    }
     if (s < NS && b0 + lb < nb) {
       uint64_t lo, hi;
       prf_chunk(rks[key_of], nonce_of, (uint64_t)(b0 + lb), &lo, &hi);
@@ -957,7 +997,7 @@ __device__ __forceinline__ void mul_trunc3_lat_body(
       kh[s][lb] = hi;
     }
     __syncthreads();
-    if (tid < EPB && b0 + tid < nb) {
+    if (fin) {
       const int64_t b = b0 + tid;
 #pragma unroll
       for (int j = 0; j < P; ++j) {
@@ -967,11 +1007,7 @@ __device__ __forceinline__ void mul_trunc3_lat_body(
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
           const int q = p == 2 ? 0 : p + 1;
-          const T v = y0 == nullptr ? ld_view(x0, vw, 0, p, e, n)
-                      : mxr::cross<T>(MX_CROSS_ARITH, ld_view(x0, vw, 0, p, e, n),
-                                      ld_view(x1, vw, 1, p, e, n), ld_view(y0, vw, 2, p, e, n),
-                                      ld_view(y1, vw, 3, p, e, n), true, true);
-          z[p] = mxr::zs_combine<T>(MX_CROSS_ARITH, v, pick<T>(kl[p][tid], kh[p][tid], j),
+          z[p] = mxr::zs_combine<T>(MX_CROSS_ARITH, vv[j][p], pick<T>(kl[p][tid], kh[p][tid], j),
                                     pick<T>(kl[q][tid], kh[q][tid], j));
         }
         const T Z0 = pick<T>(kl[7][tid], kh[7][tid], j);
