@@ -70,6 +70,15 @@ __global__ void __launch_bounds__(256) k_trunc_pr3_lat(const T* __restrict__ s0,
   const uint64_t nonce_of = s == 0 ? n_r0 : s == 1 ? n_r1 : s == 2 ? n_t : s == 3 ? n_m
                             : s == 4 ? n_z0 : n_z2;
   for (int64_t b0 = (int64_t)blockIdx.x * EPB; b0 < nb; b0 += (int64_t)gridDim.x * EPB) {
+    // the finishing threads' operands first: their loads overlap the keystream work
+    const bool fin = tid < EPB && b0 + tid < nb;
+    T xv[P][3];
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const int64_t i = (b0 + tid) * P + j;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) xv[j][p] = fin && i < n ? cm * s0[p * n + i] : (T)0;
+    }
     if (s < 6 && b0 + lb < nb) {
       uint64_t lo, hi;
       mxd::prf_chunk(rks[key_of], nonce_of, (uint64_t)(b0 + lb), &lo, &hi);
@@ -77,7 +86,7 @@ __global__ void __launch_bounds__(256) k_trunc_pr3_lat(const T* __restrict__ s0,
       kh[s][lb] = hi;
     }
     __syncthreads();
-    if (tid < EPB && b0 + tid < nb) {
+    if (fin) {
       const int64_t b = b0 + tid;
 #pragma unroll
       for (int j = 0; j < P; ++j) {
@@ -86,7 +95,7 @@ __global__ void __launch_bounds__(256) k_trunc_pr3_lat(const T* __restrict__ s0,
         const T z0 = mxd::pick<T>(kl[4][tid], kh[4][tid], j);
         const T z2 = mxd::pick<T>(kl[5][tid], kh[5][tid], j);
         const T z1 = mxf::trunc_pr_z1<T>(
-            cm * s0[i], cm * s0[n + i], cm * s0[2 * n + i], mxd::pick<T>(kl[0][tid], kh[0][tid], j),
+            xv[j][0], xv[j][1], xv[j][2], mxd::pick<T>(kl[0][tid], kh[0][tid], j),
             mxd::pick<T>(kl[1][tid], kh[1][tid], j), mxd::pick<T>(kl[2][tid], kh[2][tid], j),
             mxd::pick<T>(kl[3][tid], kh[3][tid], j), z0, z2, m);
         out0[i] = z0;
