@@ -267,6 +267,37 @@ __global__ void __launch_bounds__(256) k_weighted_sum(const T* __restrict__ a, c
   }
 }
 
+// k_weighted_sum for latency-bound launches with a long reduction: G threads per output,
+// each summing every G-th term (all k loads of an output in flight at once), then a
+// tree over the G partials in LDS.  Ring sums: any order gives the same value.
+template <class T, int G = 8>
+__global__ void __launch_bounds__(256) k_weighted_sum_wide(const T* __restrict__ a,
+                                                           const T* __restrict__ w,
+                                                           T* __restrict__ out, int64_t outer,
+                                                           int64_t k, int64_t inner) {
+  __shared__ T part[256];
+  const int64_t n = outer * inner;
+  const int lane = threadIdx.x % G;
+  for (int64_t g0 = (int64_t)blockIdx.x * (256 / G); g0 < n; g0 += (int64_t)gridDim.x * (256 / G)) {
+    const int64_t g = g0 + threadIdx.x / G;
+    T acc = 0;
+    if (g < n) {
+      const int64_t o = g / inner, i = g - o * inner;
+      const T* src = a + o * k * inner + i;
+      for (int64_t j = lane; j < k; j += G) acc += w[j] * src[j * inner];
+    }
+    part[threadIdx.x] = acc;
+    __syncthreads();
+#pragma unroll
+    for (int h = G / 2; h > 0; h /= 2) {
+      if (lane < h) part[threadIdx.x] += part[threadIdx.x + h];
+      __syncthreads();
+    }
+    if (lane == 0 && g < n) out[g] = part[threadIdx.x];
+    __syncthreads();
+  }
+}
+
 template <class T>
 __global__ void __launch_bounds__(256) k_compare(int op, const T* __restrict__ a, int64_t na, const T* __restrict__ b,
                           int64_t nb, uint8_t* __restrict__ out, int64_t n) {
@@ -1521,8 +1552,14 @@ int mxh_weighted_sum(int words, const void* a, const void* w, void* out, int64_t
                      int64_t k, int64_t inner, void* stream) {
   if (outer * inner == 0) return 0;
   DEV_DISPATCH(words, T, {
-    hipLaunchKernelGGL(k_weighted_sum<T>, dim3(grid_for(outer * inner)), dim3(kBlock), 0,
-                       S(stream), (const T*)a, (const T*)w, (T*)out, outer, k, inner);
+    if (k >= 16 && outer * inner <= 65536) {  // latency-bound: 8 threads per output
+      const int64_t blocks = (outer * inner + 31) / 32;
+      hipLaunchKernelGGL(k_weighted_sum_wide<T>, dim3((unsigned)blocks), dim3(kBlock), 0,
+                         S(stream), (const T*)a, (const T*)w, (T*)out, outer, k, inner);
+    } else {
+      hipLaunchKernelGGL(k_weighted_sum<T>, dim3(grid_for(outer * inner)), dim3(kBlock), 0,
+                         S(stream), (const T*)a, (const T*)w, (T*)out, outer, k, inner);
+    }
     MX_LAUNCH_CHECK();
     return 0;
   });

@@ -350,3 +350,17 @@ def test_poly_tail_one_launch_matches_three_steps(monkeypatch):
                                 use_graphs=False).evaluate_computation(f, {"x": x})
     np.testing.assert_array_equal(list(got.values())[0], list(want.values())[0])
     np.testing.assert_allclose(list(got.values())[0], 1 / (1 + np.exp(-x)), atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [64, 128])
+@pytest.mark.parametrize("shape,nb", [((36, 200), 0), ((3, 40, 77), 1), ((5, 300), 0)])
+def test_weighted_sum_device_matches_host(bits, shape, nb):
+    """weighted_sum on the device (k_weighted_sum_wide for long reductions of latency-sized
+    launches, k_weighted_sum otherwise) equals the host kernel."""
+    k = shape[nb]
+    w = [(1 << (i % 60)) + 3 * i for i in range(k)]
+    a = _rand(shape, bits, "cpu", 70)
+    want = R.weighted_sum(a, w, nb=nb)
+    got = R.weighted_sum(R.RT(a.data.to("cuda"), bits), w, nb=nb)
+    _eq(R.RT(got.data.cpu(), bits), want)
