@@ -534,8 +534,24 @@ class Encoded(RT):
         return self.src.device if self.pending() else self.data.device
 
 
+# ids of cached computation constants (runtime/interpreter.py _CONST_LV keeps them alive)
+CONST_IDS = set()
+_ENCODED_CONSTS = {}
+
+
 def encode_lazy(x: torch.Tensor, frac: int, bits: int) -> RT:
-    """encode(), deferred to the first use (:class:`Encoded`) for 64/128-bit rings."""
+    """encode(), deferred to the first use (:class:`Encoded`) for 64/128-bit rings; a
+    cached computation constant is encoded once (not while a hipGraph is being captured:
+    the result would live in the graph's pool)."""
+    if id(x) in CONST_IDS and x.is_cuda:
+        key = (id(x), int(frac), bits)
+        hit = _ENCODED_CONSTS.get(key)
+        if hit is not None:
+            return hit
+        if not torch.cuda.is_current_stream_capturing():
+            e = encode(x, frac, bits)
+            _cache_put(_ENCODED_CONSTS, key, e, 4096)
+            return e
     if bits not in (64, 128):
         return encode(x, frac, bits)
     return Encoded(x.to(torch.float64).contiguous(), frac, bits)

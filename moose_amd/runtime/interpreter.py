@@ -43,6 +43,8 @@ from moose_amd.runtime.values import MV
 from moose_amd.utils.telemetry import span
 
 _FLOAT = {"Float32": torch.float32, "Float64": torch.float64}
+# small numeric tensor constants of computations, uploaded once per (value, device)
+_CONST_LV = {}
 
 
 # replicated dialect operators handled by Interpreter._rep_dialect (reference
@@ -667,13 +669,34 @@ class Interpreter:
         t = shares.rep_from_components(self.sess, plc, bits, kind, lookup)
         return self._rep_lv(plc, t, dtype)
 
+    def _const_key(self, c, host, want):
+        """Cache key of a small numeric tensor constant on a device session: its bytes,
+        dtype, shape, kind, the wanted type, host and device (the value itself, so a key
+        never outlives what it names).  None: not cached."""
+        dev = getattr(self.sess, "device", None)
+        if self.symbolic or dev is None or dev.type != "cuda" or c.kind in (
+                "HostShape", "HostString", "HostRing64Tensor", "HostRing128Tensor"):
+            return None
+        try:
+            arr = np.asarray(c.value)
+        except Exception:  # noqa: BLE001 - anything unusual stays uncached
+            return None
+        if arr.dtype == object or arr.nbytes > (1 << 16) or (
+                c.kind in ("Float32", "Float64") and want.name != "Tensor"):
+            return None
+        return (c.kind, arr.dtype.str, arr.shape, arr.tobytes(), repr(want), host, str(dev))
+
     def op_Constant(self, op, ins):
         c: Constant = op.attrs["value"]
         plc = op.placement
         host = plc.owner if isinstance(plc, HostPlacement) else plc.owners[0]
         want = op.sig.ret
         hp = HostPlacement(host)
-        if c.kind == "HostShape":
+        key = self._const_key(c, host, want)
+        hit = _CONST_LV.get(key) if key is not None else None
+        if hit is not None:  # uploaded once: no host->device copy per evaluation
+            lv = hit
+        elif c.kind == "HostShape":
             lv = LV(hp, "shape", None, HV(host, tuple(c.value)))
         elif c.kind == "HostString":
             lv = LV(hp, "string", None, HV(host, c.value))
@@ -686,6 +709,14 @@ class Interpreter:
         else:
             arr = np.asarray(c.value)
             lv = self._host_value_from_python(host, arr, want)
+        if (key is not None and hit is None and isinstance(lv.v, HV)
+                and isinstance(lv.v.v, torch.Tensor) and lv.v.v.is_cuda
+                and not torch.cuda.is_current_stream_capturing()):
+            if len(_CONST_LV) < 1024:  # public constants are never written
+                if _lanes.ACTIVE or R.SHARED_STREAMS:  # other streams read it next
+                    torch.cuda.current_stream(lv.v.v.device).synchronize()
+                _CONST_LV[key] = lv
+                R.CONST_IDS.add(id(lv.v.v))  # kept alive by the cache: the id stays its own
         if isinstance(plc, HostPlacement):
             return lv
         # constants on replicated / mirrored placements are public

@@ -125,3 +125,28 @@ def test_default_runtime_replays_dispatch_bound_evaluations():
     assert plan.replays == 10
     warm = sorted(lat[3:])
     print(f"default LocalMooseRuntime LR p50 {warm[len(warm) // 2]:.3f} ms")
+
+
+@pytest.mark.gpu
+def test_small_constants_uploaded_and_encoded_once():
+    """A computation's small tensor constants (the tutorial model's weights and intercept)
+    are uploaded and fixed-point encoded once per device and reused by later evaluations,
+    eager and replayed; the predictions stay right."""
+    import numpy as np
+
+    from moose_amd.models.predictors.tutorial import logistic_regression_tutorial
+    from moose_amd.ops import ring as R
+    from moose_amd.runtime import interpreter as I
+    from moose_amd.runtime.local import LocalMooseRuntime
+
+    tm = logistic_regression_tutorial(128)
+    for graphs in (False, True):
+        rt = LocalMooseRuntime(["alice", "bob", "carole"], device="cuda", use_graphs=graphs)
+        outs = [list(rt.evaluate_computation(tm.computation, {"x": tm.x_test}).values())[0]
+                for _ in range(4)]
+        assert I._CONST_LV and R._ENCODED_CONSTS
+        n = (len(I._CONST_LV), len(R._ENCODED_CONSTS))
+        outs.append(list(rt.evaluate_computation(tm.computation, {"x": tm.x_test}).values())[0])
+        assert (len(I._CONST_LV), len(R._ENCODED_CONSTS)) == n
+        for o in outs:
+            assert np.abs(np.asarray(o) - tm.proba).max() < 1e-4
