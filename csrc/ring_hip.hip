@@ -861,6 +861,111 @@ __global__ void __launch_bounds__(256) k_ks_adder3p(const T* __restrict__ g0, co
   }
 }
 
+// The whole of rep.bit_decompose for three stacked parties in ONE launch (latency form):
+// P0's y = x_0 + x_1 boolean-shared (mask PRF(k_mir, n1): slots (r, y ^ r, 0), mirrored
+// (y ^ r, r, 0)), the trivial sharing of x_2 (slot 2: P2's s0, P1's s1), the adder's
+// p = a ^ b and g = a AND b (zero share PRF(k_q, nmul) ^ PRF(k_{q+1}, nmul); with
+// A_2 = B_0 = B_1 = 0 the cross terms are c_0 = 0, c_1 = A_1 & b_2, c_2 = A_0 & b_2), then
+// the Kogge-Stone chain as k_ks_adder3p and the sum p ^ (g << 1).  Every keystream chunk is
+// computed in parallel first (4 + 6 per level per element), then three threads per
+// element (one per party) run the chain.  Bitwise the shares of the share + slot placement
+// + xor + AND + adder kernels it replaces.
+template <class T>
+__global__ void __launch_bounds__(256) k_bitdec3(const T* __restrict__ x0, const T* __restrict__ x1,
+                                                 T* __restrict__ o0, T* __restrict__ o1,
+                                                 int64_t n, int nlev, KeySrc keys, int mir,
+                                                 uint64_t n1, uint64_t nmul, Nonces8 nn) {
+  constexpr int E = 5;
+  constexpr int W = 8 * (int)sizeof(T);
+  constexpr int P = Lane<T>::kPer;
+  __shared__ uint32_t rks[3][kKeyWords];
+  __shared__ T ks[8][6][E];
+  __shared__ T kr[E], kz[3][E];
+  __shared__ T xt[2][3 * E], xq[2][3 * E];
+  stage_keys(rks, keys, 3);
+  const int tid = threadIdx.x;
+  for (int64_t e0 = (int64_t)blockIdx.x * E; e0 < n; e0 += (int64_t)gridDim.x * E) {
+    const int le = tid / 3, p = tid - 3 * (tid / 3), pn = p == 2 ? 0 : p + 1;
+    const int64_t e = e0 + le;
+    const bool act = tid < 3 * E && e < n;
+    // operands first: their loads overlap the keystream work
+    T y = 0, b2 = 0, b2b = 0;
+    if (act) {
+      y = x0[e] + x1[e];  // P0's x_0 + x_1
+      b2 = x0[2 * n + e];  // x_2 as P2 holds it (s0)
+      b2b = x1[n + e];     // x_2 as P1 holds it (s1)
+    }
+    for (int q = tid; q < 4 * E + nlev * 6 * E; q += blockDim.x) {
+      uint64_t lo, hi;
+      if (q < 4 * E) {  // 0: the sharing mask; 1..3: the AND's zero share (k0, k1, k2)
+        const int s = q / E, lq = q % E;
+        if (e0 + lq >= n) continue;
+        const int64_t c = e0 + lq;
+        prf_chunk(rks[s == 0 ? mir : s - 1], s == 0 ? n1 : nmul, (uint64_t)(c / P), &lo, &hi);
+        const T v = pick<T>(lo, hi, (int)(c % P));
+        if (s == 0)
+          kr[lq] = v;
+        else
+          kz[s - 1][lq] = v;
+      } else {
+        const int r = q - 4 * E;
+        const int lev = r / (6 * E), s = (r / E) % 6, lq = r % E;
+        const bool both = 2 * (1 << lev) < W;
+        if (s >= (both ? 6 : 3) || e0 + lq >= n) continue;
+        const int64_t c = (s < 3 ? 0 : n) + e0 + lq;  // t at e, pk' at n + e
+        prf_chunk(rks[s % 3], nn.v[lev], (uint64_t)(c / P), &lo, &hi);
+        ks[lev][s][lq] = pick<T>(lo, hi, (int)(c % P));
+      }
+    }
+    __syncthreads();
+    T G0 = 0, G1 = 0, A0 = 0, A1 = 0, S0 = 0, S1 = 0;
+    if (act) {
+      const T r = kr[le], v = y ^ r;
+      const T As[3] = {mir ? v : r, mir ? r : v, (T)0};
+      S0 = As[p] ^ (p == 2 ? b2 : (T)0);    // p's s0 = slot p of a ^ b
+      S1 = As[pn] ^ (p == 1 ? b2b : (T)0);  // p's s1 = slot p + 1
+      const T c[3] = {(T)0, (T)(As[1] & b2b), (T)(As[0] & b2)};
+      const int pnn = pn == 2 ? 0 : pn + 1;
+      G0 = c[p] ^ kz[p][le] ^ kz[pn][le];     // z_p
+      G1 = c[pn] ^ kz[pn][le] ^ kz[pnn][le];  // z_{p+1}, reshared to p
+      A0 = S0;
+      A1 = S1;
+    }
+#pragma unroll
+    for (int lev = 0; lev < 8; ++lev) {
+      if (lev >= nlev) break;  // uniform over the block
+      const int d = 1 << lev;
+      const bool both = 2 * d < W;
+      T t = 0, q = 0;
+      if (act) {
+        const T s0 = G0 << d, s1 = G1 << d;
+        t = (A0 & s0) ^ (A0 & s1) ^ (A1 & s0) ^ ks[lev][p][le] ^ ks[lev][pn][le];
+        if (both) {
+          const T u0 = A0 << d, u1 = A1 << d;
+          q = (A0 & u0) ^ (A0 & u1) ^ (A1 & u0) ^ ks[lev][3 + p][le] ^ ks[lev][3 + pn][le];
+        }
+        xt[lev & 1][tid] = t;
+        xq[lev & 1][tid] = q;
+      }
+      __syncthreads();
+      if (act) {
+        const int src = 3 * le + pn;
+        G1 ^= xt[lev & 1][src];
+        G0 ^= t;
+        if (both) {
+          A1 = xq[lev & 1][src];
+          A0 = q;
+        }
+      }
+    }
+    if (act) {
+      o0[(int64_t)p * n + e] = S0 ^ (T)(G0 << 1);
+      o1[(int64_t)p * n + e] = S1 ^ (T)(G1 << 1);
+    }
+    __syncthreads();
+  }
+}
+
 // The adder's sum after the last level, both share components: p ^ ((g ^ t) << 1).
 template <class T>
 __global__ void __launch_bounds__(256) k_ks_sum2(const T* __restrict__ p0, const T* __restrict__ p1,
@@ -1808,6 +1913,31 @@ int mxh_ks_cross1(int words, const void* g0, const void* g1, const void* p0, con
   } else {
     return -2;
   }
+  MX_LAUNCH_CHECK();
+  return 0;
+}
+
+// slots: k0, k1, k2 of the placement; nonces: one per adder level (nlev <= 8)
+int mxh_bitdec3(int words, const void* x0, const void* x1, void* o0, void* o1, int64_t n,
+                int nlev, const uint32_t* slots, int mir, uint64_t n1, uint64_t nmul,
+                const uint64_t* nonces, void* stream) {
+  if (n == 0) return 0;
+  if (n > 65536 || nlev < 1 || nlev > 8) return -1;  // latency sizes only
+  const uint32_t* ptrs[3];
+  for (int i = 0; i < 3; ++i) ptrs[i] = slots + MX_KEY_SLOT_WORDS * i;
+  Nonces8 nn{};
+  for (int i = 0; i < nlev; ++i) nn.v[i] = nonces[i];
+  const unsigned g = (unsigned)((n + 4) / 5);
+  if (words == 1)
+    hipLaunchKernelGGL(k_bitdec3<u64>, dim3(g), dim3(256), 0, S(stream), (const u64*)x0,
+                       (const u64*)x1, (u64*)o0, (u64*)o1, n, nlev, mxd::keysrc_slots(ptrs, 3),
+                       mir ? 1 : 0, n1, nmul, nn);
+  else if (words == 2)
+    hipLaunchKernelGGL(k_bitdec3<u128>, dim3(g), dim3(256), 0, S(stream), (const u128*)x0,
+                       (const u128*)x1, (u128*)o0, (u128*)o1, n, nlev,
+                       mxd::keysrc_slots(ptrs, 3), mir ? 1 : 0, n1, nmul, nn);
+  else
+    return -2;
   MX_LAUNCH_CHECK();
   return 0;
 }

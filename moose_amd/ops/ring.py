@@ -1538,6 +1538,31 @@ def b2a3(b0: RT, b1: RT, ring_bits: int, slot_ptr: int, mir: bool, n1: int, nmul
     return o0, o1
 
 
+def bitdec3(x0: RT, x1: RT, slot_ptr: int, mir: bool, n1: int, nmul: int, nonces):
+    """The whole of rep.bit_decompose for three stacked parties in one launch (k_bitdec3):
+    P0's boolean sharing of y = x_0 + x_1 (mask nonce n1, key k_0 or mirrored k_1), the
+    trivial sharing of x_2, the adder's xor and AND (zero-share nonce nmul) and its
+    Kogge-Stone chain (``nonces``, one per level) with the sum.  Returns the (s0, s1) pair of
+    packed boolean share vectors [3, ...], or None (host, or above the latency sizes)."""
+    d0, d1 = x0.data, x1.data
+    bits = x0.bits
+    if not d0.is_cuda or bits not in (64, 128) or x1.bits != bits or x0.shape != x1.shape \
+            or x0.shape[0] != 3:
+        return None
+    n = math.prod(x0.shape[1:])
+    if n > 65536 or len(nonces) != bits.bit_length() - 1:
+        return None
+    d0, d1 = d0.contiguous(), d1.contiguous()
+    o0, o1 = empty2(x0.shape, bits, d0.device)
+    arr = (ctypes.c_uint64 * len(nonces))(*[int(v) & MASK64 for v in nonces])
+    rc = nat.lib().mxh_bitdec3(_words(bits), nat.ptr(d0), nat.ptr(d1), nat.ptr(o0.data),
+                               nat.ptr(o1.data), n, len(nonces), ctypes.c_void_p(slot_ptr),
+                               int(bool(mir)), n1 & MASK64, nmul & MASK64, arr,
+                               nat.stream_of(d0))
+    nat.check(rc, "bitdec3")
+    return o0, o1
+
+
 def slot_place2(x0: RT, x1: RT, which0: int, which1: int, nparties: int = 3):
     """Two trivial stacked sharings [nparties, *x.shape] in one launch: slot which0 of the
     first = x0, slot which1 of the second = x1, zeros elsewhere (mx_slot_place2)."""

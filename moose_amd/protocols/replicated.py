@@ -660,6 +660,10 @@ def bit_decompose(sess, x: RepTensor) -> RepTensor:
     (slot 2), and a packed Kogge-Stone adder computes y + x_2 (log2 k AND rounds)."""
     with span("rep.bit_decompose"):
         plc, bits = x.plc, x.bits
+        whole = getattr(sess, "p_bit_decompose", None)
+        r = whole(plc, x) if whole is not None and x.kind == "arith" else None
+        if r is not None:  # every step below in one kernel (same nonces, same shares)
+            return RepTensor(plc, bits, "bool", r[0], r[1])
         o = plc.owners
         y = sess.h("Add", o[0], sess.take(x.s0, 0), sess.take(x.s1, 0))
         yb = share(sess, plc, y, kind="bool")

@@ -391,6 +391,35 @@ class StackedSession(Session):
         self.stats.record_round(3 * nb)
         return PV(plc, o0), PV(plc, o1)
 
+    def p_bit_decompose(self, plc, x):
+        """The whole of rep.bit_decompose in one kernel (device, fused session, latency
+        sizes): the nonces in the generic order (share: n1, na; the adder's AND: nmul; one
+        per level) and the same traffic records, so the same shares.  None -> the steps."""
+        if self.device.type != "cuda" or not getattr(self, "fused", False) \
+                or os.environ.get("MOOSEX_BITDEC_FUSED", "1") == "0":
+            return None
+        v0, v1 = x.s0.v, x.s1.v
+        if not (isinstance(v0, R.RT) and isinstance(v1, R.RT)) or v0.bits not in (64, 128) \
+                or v1.bits != v0.bits or v0.shape != v1.shape or not v0.data.is_cuda \
+                or len(v0.shape) < 1 or v0.shape[0] != 3:
+            return None
+        bits = v0.bits
+        n = math.prod(v0.shape[1:])
+        if n > 65536:
+            return None
+        d = self.share_dir(plc, 0)
+        n1, _na, nmul = self.nonce(plc), self.nonce(plc), self.nonce(plc)
+        nonces = [self.nonce(plc) for _ in range(bits.bit_length() - 1)]
+        o0, o1 = R.bitdec3(v0, v1, self.key_ptr(plc, 0), d == 2, n1, nmul, nonces)
+        nb = n * (bits // 8)
+        self.stats.record_send(plc.owners[0], plc.owners[d % 3], nb)  # the sharing of y
+        self.stats.record_round(3 * nb)  # the adder's AND
+        dd = 1
+        for _ in nonces:  # the chain's rounds
+            self.stats.record_round(3 * nb * (2 if 2 * dd < bits else 1))
+            dd *= 2
+        return PV(plc, o0), PV(plc, o1)
+
     def p_from_slot_holders(self, plc, slot, x_h0, x_h1, like):
         """rep.from_slot_holders in one kernel (None -> generic path)."""
         v0, v1 = x_h0.v, x_h1.v

@@ -364,3 +364,34 @@ def test_weighted_sum_device_matches_host(bits, shape, nb):
     want = R.weighted_sum(a, w, nb=nb)
     got = R.weighted_sum(R.RT(a.data.to("cuda"), bits), w, nb=nb)
     _eq(R.RT(got.data.cpu(), bits), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits,n,mirror", [(64, 301, False), (128, 300, False),
+                                           (128, 37, True), (64, 4099, True)])
+def test_bit_decompose_one_kernel_matches_generic(bits, n, mirror):
+    """The whole of rep.bit_decompose in one kernel (StackedSession.p_bit_decompose,
+    k_bitdec3) gives bitwise the shares, the nonce position and the traffic records of the
+    share + slot placement + xor + AND + adder kernels (same seed, both share directions);
+    the opened packed word is x itself."""
+    from moose_amd.runtime.session import HV
+
+    plc = ReplicatedPlacement(owners=("a", "b", "c"))
+    outs = []
+    for whole in (True, False):
+        sess = StackedSession("cuda", seed=13)
+        if mirror:
+            sess.share_dirs = {"a": 2}
+        if not whole:
+            sess.p_bit_decompose = lambda *a, **k: None
+        xv = _rand((n,), bits, "cuda", 9)
+        x = rep.share(sess, plc, HV("b", xv))
+        y = rep.bit_decompose(sess, x)
+        nxt = rep.share(sess, plc, HV("b", _rand((7,), bits, "cuda", 5)))  # next nonce
+        opened = rep.reveal(sess, y, "a").v
+        outs.append((y.s0.v, y.s1.v, nxt.s0.v, sess.stats.as_dict(), opened, xv))
+    for i in (0, 1, 2, 4):
+        _eq(outs[0][i], outs[1][i])
+    for k in ("rounds", "reshare_bytes", "bytes", "messages"):
+        assert outs[0][3][k] == outs[1][3][k], k
+    _eq(outs[0][4], outs[0][5])
