@@ -870,17 +870,20 @@ __global__ void __launch_bounds__(256) k_ks_adder3p(const T* __restrict__ g0, co
 // computed in parallel first (4 + 6 per level per element), then three threads per
 // element (one per party) run the chain.  Bitwise the shares of the share + slot placement
 // + xor + AND + adder kernels it replaces.
-template <class T>
+template <class T, bool SIGN>
 __global__ void __launch_bounds__(256) k_bitdec3(const T* __restrict__ x0, const T* __restrict__ x1,
                                                  T* __restrict__ o0, T* __restrict__ o1,
                                                  int64_t n, int nlev, KeySrc keys, int mir,
-                                                 uint64_t n1, uint64_t nmul, Nonces8 nn) {
+                                                 uint64_t n1, uint64_t nmul, Nonces8 nn,
+                                                 uint64_t n1b, uint64_t nmulb) {
   constexpr int E = 5;
   constexpr int W = 8 * (int)sizeof(T);
   constexpr int P = Lane<T>::kPer;
   __shared__ uint32_t rks[3][kKeyWords];
   __shared__ T ks[8][6][E];
-  __shared__ T kr[E], kz[3][E];
+  __shared__ T kr[E], kz[3][E], kr2[E], kz2[3][E];
+  __shared__ uint8_t bs0[3 * E], bs1[3 * E];
+  constexpr int NB = SIGN ? 8 : 4;  // per element: sharing mask + AND zero share (+ b2a's)
   __shared__ T xt[2][3 * E], xq[2][3 * E];
   stage_keys(rks, keys, 3);
   const int tid = threadIdx.x;
@@ -895,20 +898,27 @@ __global__ void __launch_bounds__(256) k_bitdec3(const T* __restrict__ x0, const
       b2 = x0[2 * n + e];  // x_2 as P2 holds it (s0)
       b2b = x1[n + e];     // x_2 as P1 holds it (s1)
     }
-    for (int q = tid; q < 4 * E + nlev * 6 * E; q += blockDim.x) {
+    for (int q = tid; q < NB * E + nlev * 6 * E; q += blockDim.x) {
       uint64_t lo, hi;
-      if (q < 4 * E) {  // 0: the sharing mask; 1..3: the AND's zero share (k0, k1, k2)
+      if (q < NB * E) {  // 0: the sharing mask; 1..3: the AND's zero share (k0, k1, k2);
+                         // 4..7 (SIGN): the same two for the b2a of the sign bit
         const int s = q / E, lq = q % E;
         if (e0 + lq >= n) continue;
         const int64_t c = e0 + lq;
-        prf_chunk(rks[s == 0 ? mir : s - 1], s == 0 ? n1 : nmul, (uint64_t)(c / P), &lo, &hi);
+        const int sl = s & 3;
+        const uint64_t non = s < 4 ? (sl == 0 ? n1 : nmul) : (sl == 0 ? n1b : nmulb);
+        prf_chunk(rks[sl == 0 ? mir : sl - 1], non, (uint64_t)(c / P), &lo, &hi);
         const T v = pick<T>(lo, hi, (int)(c % P));
         if (s == 0)
           kr[lq] = v;
-        else
+        else if (s < 4)
           kz[s - 1][lq] = v;
+        else if (s == 4)
+          kr2[lq] = v;
+        else
+          kz2[s - 5][lq] = v;
       } else {
-        const int r = q - 4 * E;
+        const int r = q - NB * E;
         const int lev = r / (6 * E), s = (r / E) % 6, lq = r % E;
         const bool both = 2 * (1 << lev) < W;
         if (s >= (both ? 6 : 3) || e0 + lq >= n) continue;
@@ -958,9 +968,35 @@ __global__ void __launch_bounds__(256) k_bitdec3(const T* __restrict__ x0, const
         }
       }
     }
-    if (act) {
-      o0[(int64_t)p * n + e] = S0 ^ (T)(G0 << 1);
-      o1[(int64_t)p * n + e] = S1 ^ (T)(G1 << 1);
+    if constexpr (!SIGN) {
+      if (act) {
+        o0[(int64_t)p * n + e] = S0 ^ (T)(G0 << 1);
+        o1[(int64_t)p * n + e] = S1 ^ (T)(G1 << 1);
+      }
+    } else {
+      // the sign bit of every component (msb), then its b2a as k_b2a3 (one thread per
+      // element): P0's a = b_0 ^ b_1 shared, times the trivial sharing of b_2, lincomb
+      if (act) {
+        bs0[tid] = (uint8_t)((S0 ^ (T)(G0 << 1)) >> (W - 1)) & 1;
+        bs1[tid] = (uint8_t)((S1 ^ (T)(G1 << 1)) >> (W - 1)) & 1;
+      }
+      __syncthreads();
+      if (act && p == 0) {
+        const T a = (T)((bs0[tid] ^ bs1[tid]) & 1);
+        const T x2 = (T)bs0[tid + 2], x2b = (T)bs1[tid + 1];  // P2's, P1's b_2
+        const T r = kr2[le];
+        const T v = a - r;
+        const T B0 = mir ? v : r, B1 = mir ? r : v;
+        const T k0 = kz2[0][le], k1 = kz2[1][le], k2 = kz2[2][le];
+        const T z0 = k0 - k1, z1 = B1 * x2b + k1 - k2, z2 = B0 * x2 + k2 - k0;
+        const T o[3] = {(T)(B0 - (z0 << 1)), (T)(B1 - (z1 << 1)), (T)(x2 - (z2 << 1))};
+        const bool r4 = o1 == o0 + n;  // 4-slot ring: out1's slots 0, 1 are out0's 1, 2
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          o0[(int64_t)q * n + e] = o[q];
+          if (!r4 || q == 2) o1[(int64_t)q * n + e] = o[q == 2 ? 0 : q + 1];
+        }
+      }
     }
     __syncthreads();
   }
@@ -1920,7 +1956,7 @@ int mxh_ks_cross1(int words, const void* g0, const void* g1, const void* p0, con
 // slots: k0, k1, k2 of the placement; nonces: one per adder level (nlev <= 8)
 int mxh_bitdec3(int words, const void* x0, const void* x1, void* o0, void* o1, int64_t n,
                 int nlev, const uint32_t* slots, int mir, uint64_t n1, uint64_t nmul,
-                const uint64_t* nonces, void* stream) {
+                const uint64_t* nonces, int sign, uint64_t n1b, uint64_t nmulb, void* stream) {
   if (n == 0) return 0;
   if (n > 65536 || nlev < 1 || nlev > 8) return -1;  // latency sizes only
   const uint32_t* ptrs[3];
@@ -1928,14 +1964,24 @@ int mxh_bitdec3(int words, const void* x0, const void* x1, void* o0, void* o1, i
   Nonces8 nn{};
   for (int i = 0; i < nlev; ++i) nn.v[i] = nonces[i];
   const unsigned g = (unsigned)((n + 4) / 5);
-  if (words == 1)
-    hipLaunchKernelGGL(k_bitdec3<u64>, dim3(g), dim3(256), 0, S(stream), (const u64*)x0,
-                       (const u64*)x1, (u64*)o0, (u64*)o1, n, nlev, mxd::keysrc_slots(ptrs, 3),
-                       mir ? 1 : 0, n1, nmul, nn);
+  const KeySrc ks = mxd::keysrc_slots(ptrs, 3);
+  const int m = mir ? 1 : 0;
+  if (words == 1 && !sign)
+    hipLaunchKernelGGL((k_bitdec3<u64, false>), dim3(g), dim3(256), 0, S(stream), (const u64*)x0,
+                       (const u64*)x1, (u64*)o0, (u64*)o1, n, nlev, ks, m, n1, nmul, nn, n1b,
+                       nmulb);
+  else if (words == 1)
+    hipLaunchKernelGGL((k_bitdec3<u64, true>), dim3(g), dim3(256), 0, S(stream), (const u64*)x0,
+                       (const u64*)x1, (u64*)o0, (u64*)o1, n, nlev, ks, m, n1, nmul, nn, n1b,
+                       nmulb);
+  else if (words == 2 && !sign)
+    hipLaunchKernelGGL((k_bitdec3<u128, false>), dim3(g), dim3(256), 0, S(stream),
+                       (const u128*)x0, (const u128*)x1, (u128*)o0, (u128*)o1, n, nlev, ks, m,
+                       n1, nmul, nn, n1b, nmulb);
   else if (words == 2)
-    hipLaunchKernelGGL(k_bitdec3<u128>, dim3(g), dim3(256), 0, S(stream), (const u128*)x0,
-                       (const u128*)x1, (u128*)o0, (u128*)o1, n, nlev,
-                       mxd::keysrc_slots(ptrs, 3), mir ? 1 : 0, n1, nmul, nn);
+    hipLaunchKernelGGL((k_bitdec3<u128, true>), dim3(g), dim3(256), 0, S(stream),
+                       (const u128*)x0, (const u128*)x1, (u128*)o0, (u128*)o1, n, nlev, ks, m,
+                       n1, nmul, nn, n1b, nmulb);
   else
     return -2;
   MX_LAUNCH_CHECK();

@@ -89,7 +89,7 @@ _SIGS = {
     "mxh_b2a_prep3": (c_int, [c_int, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "mxh_bitdec3": (
         c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_u64, c_u64, c_vp,
-                c_vp],
+                c_int, c_u64, c_u64, c_vp],
     ),
     "mxh_b2a3": (
         c_int, [c_int, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_int, c_u64, c_u64, c_vp],

@@ -1538,12 +1538,15 @@ def b2a3(b0: RT, b1: RT, ring_bits: int, slot_ptr: int, mir: bool, n1: int, nmul
     return o0, o1
 
 
-def bitdec3(x0: RT, x1: RT, slot_ptr: int, mir: bool, n1: int, nmul: int, nonces):
+def bitdec3(x0: RT, x1: RT, slot_ptr: int, mir: bool, n1: int, nmul: int, nonces,
+            sign_nonces=None):
     """The whole of rep.bit_decompose for three stacked parties in one launch (k_bitdec3):
     P0's boolean sharing of y = x_0 + x_1 (mask nonce n1, key k_0 or mirrored k_1), the
     trivial sharing of x_2, the adder's xor and AND (zero-share nonce nmul) and its
     Kogge-Stone chain (``nonces``, one per level) with the sum.  Returns the (s0, s1) pair of
-    packed boolean share vectors [3, ...], or None (host, or above the latency sizes)."""
+    packed boolean share vectors [3, ...], or None (host, or above the latency sizes).
+    ``sign_nonces`` = (n1', nmul'): instead, the b2a of the sum's top bit (rep.b2a of
+    rep.msb: its sharing and product nonces) as an arithmetic share pair."""
     d0, d1 = x0.data, x1.data
     bits = x0.bits
     if not d0.is_cuda or bits not in (64, 128) or x1.bits != bits or x0.shape != x1.shape \
@@ -1553,12 +1556,14 @@ def bitdec3(x0: RT, x1: RT, slot_ptr: int, mir: bool, n1: int, nmul: int, nonces
     if n > 65536 or len(nonces) != bits.bit_length() - 1:
         return None
     d0, d1 = d0.contiguous(), d1.contiguous()
-    o0, o1 = empty2(x0.shape, bits, d0.device)
+    sign = sign_nonces is not None
+    o0, o1 = (ring4 if sign else empty2)(x0.shape, bits, d0.device)
     arr = (ctypes.c_uint64 * len(nonces))(*[int(v) & MASK64 for v in nonces])
+    sb = sign_nonces or (0, 0)
     rc = nat.lib().mxh_bitdec3(_words(bits), nat.ptr(d0), nat.ptr(d1), nat.ptr(o0.data),
                                nat.ptr(o1.data), n, len(nonces), ctypes.c_void_p(slot_ptr),
-                               int(bool(mir)), n1 & MASK64, nmul & MASK64, arr,
-                               nat.stream_of(d0))
+                               int(bool(mir)), n1 & MASK64, nmul & MASK64, arr, int(sign),
+                               sb[0] & MASK64, sb[1] & MASK64, nat.stream_of(d0))
     nat.check(rc, "bitdec3")
     return o0, o1
 

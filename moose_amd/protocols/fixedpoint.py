@@ -290,7 +290,7 @@ def mux(sess, s, x, y):
 
 def sign_bit(sess, x: RepFixed) -> RepTensor:
     """Arithmetic 0/1 sharing of [x < 0]."""
-    return rep.b2a(sess, rep.msb(sess, x.t), x.bits)
+    return rep.less_than_zero_arith(sess, x.t)
 
 
 def relu(sess, x: RepFixed) -> RepFixed:
@@ -835,7 +835,7 @@ def argmax(sess, x: RepFixed, axis: int, upmost_index: int) -> RepTensor:
         vb = _stack0(sess, [p[0] for p in pairs[1:2 * h:2]])
         ia = _stack0(sess, [p[1] for p in pairs[0:2 * h:2]])
         ib = _stack0(sess, [p[1] for p in pairs[1:2 * h:2]])
-        lt = rep.b2a(sess, rep.msb(sess, rep.sub(sess, va.t, vb.t)), bits)  # a < b
+        lt = rep.less_than_zero_arith(sess, rep.sub(sess, va.t, vb.t))  # a < b
         lt2 = concat(sess, [lt, lt], 0)
         sel = rep.mux(sess, lt2, concat(sess, [vb, ib], 0).t, concat(sess, [va, ia], 0).t)
         both = _unstack0(sess, _with(va, sel), 2 * h)

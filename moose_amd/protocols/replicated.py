@@ -775,6 +775,12 @@ def msb(sess, x: RepTensor) -> RepTensor:
 
 
 def less_than_zero_arith(sess, x: RepTensor) -> RepTensor:
+    """Arithmetic 0/1 sharing of [x < 0]: b2a of the sign bit (one kernel for the whole of
+    it on a stacked device session, same shares)."""
+    f = getattr(sess, "p_sign_arith", None)
+    r = f(x.plc, x) if f is not None and x.kind == "arith" else None
+    if r is not None:
+        return RepTensor(x.plc, x.bits, "arith", r[0], r[1])
     return b2a(sess, msb(sess, x), x.bits)
 
 
@@ -816,7 +822,7 @@ def abs_(sess, x: RepTensor) -> RepTensor:
 
 
 def relu(sess, x: RepTensor) -> RepTensor:
-    s = b2a(sess, msb(sess, x), x.bits)  # 1 if negative
+    s = less_than_zero_arith(sess, x)  # 1 if negative
     return sub(sess, x, mul(sess, s, x))
 
 

@@ -391,7 +391,13 @@ class StackedSession(Session):
         self.stats.record_round(3 * nb)
         return PV(plc, o0), PV(plc, o1)
 
-    def p_bit_decompose(self, plc, x):
+    def p_sign_arith(self, plc, x):
+        """rep.b2a(rep.msb(x)) in one kernel: p_bit_decompose's work, then the top bit's
+        b2a (its sharing nonces n1', na' and product nonce nmul' after the decomposition's,
+        as the two protocol steps draw them).  None -> the steps."""
+        return self.p_bit_decompose(plc, x, sign=True)
+
+    def p_bit_decompose(self, plc, x, sign=False):
         """The whole of rep.bit_decompose in one kernel (device, fused session, latency
         sizes): the nonces in the generic order (share: n1, na; the adder's AND: nmul; one
         per level) and the same traffic records, so the same shares.  None -> the steps."""
@@ -410,7 +416,11 @@ class StackedSession(Session):
         d = self.share_dir(plc, 0)
         n1, _na, nmul = self.nonce(plc), self.nonce(plc), self.nonce(plc)
         nonces = [self.nonce(plc) for _ in range(bits.bit_length() - 1)]
-        o0, o1 = R.bitdec3(v0, v1, self.key_ptr(plc, 0), d == 2, n1, nmul, nonces)
+        sn = None
+        if sign:
+            n1b, _nab, nmulb = self.nonce(plc), self.nonce(plc), self.nonce(plc)
+            sn = (n1b, nmulb)
+        o0, o1 = R.bitdec3(v0, v1, self.key_ptr(plc, 0), d == 2, n1, nmul, nonces, sn)
         nb = n * (bits // 8)
         self.stats.record_send(plc.owners[0], plc.owners[d % 3], nb)  # the sharing of y
         self.stats.record_round(3 * nb)  # the adder's AND
@@ -418,6 +428,9 @@ class StackedSession(Session):
         for _ in nonces:  # the chain's rounds
             self.stats.record_round(3 * nb * (2 if 2 * dd < bits else 1))
             dd *= 2
+        if sign:  # the b2a of the top bit: its sharing and its product round
+            self.stats.record_send(plc.owners[0], plc.owners[d % 3], nb)
+            self.stats.record_round(3 * nb)
         return PV(plc, o0), PV(plc, o1)
 
     def p_from_slot_holders(self, plc, slot, x_h0, x_h1, like):

@@ -395,3 +395,34 @@ def test_bit_decompose_one_kernel_matches_generic(bits, n, mirror):
     for k in ("rounds", "reshare_bytes", "bytes", "messages"):
         assert outs[0][3][k] == outs[1][3][k], k
     _eq(outs[0][4], outs[0][5])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits,n,mirror", [(64, 301, False), (128, 300, True), (128, 1001, False)])
+def test_sign_arith_one_kernel_matches_generic(bits, n, mirror):
+    """rep.less_than_zero_arith (b2a of the sign bit) in one kernel (StackedSession
+    .p_sign_arith, k_bitdec3<SIGN>) gives bitwise the shares, nonce position and traffic
+    records of the generic decomposition + bit extraction + b2a steps; it opens to [x < 0]."""
+    from moose_amd.runtime.session import HV
+
+    plc = ReplicatedPlacement(owners=("a", "b", "c"))
+    outs = []
+    for whole in (True, False):
+        sess = StackedSession("cuda", seed=17)
+        if mirror:
+            sess.share_dirs = {"a": 2}
+        if not whole:
+            for name in ("p_sign_arith", "p_bit_decompose", "p_b2a", "p_b2a_prep"):
+                setattr(sess, name, lambda *a, **k: None)
+        xv = _rand((n,), bits, "cuda", 21)
+        x = rep.share(sess, plc, HV("c", xv))
+        y = rep.less_than_zero_arith(sess, x)
+        nxt = rep.share(sess, plc, HV("b", _rand((7,), bits, "cuda", 5)))  # next nonce
+        opened = rep.reveal(sess, y, "a").v
+        outs.append((y.s0.v, y.s1.v, nxt.s0.v, sess.stats.as_dict(), opened, xv))
+    for i in (0, 1, 2, 4):
+        _eq(outs[0][i], outs[1][i])
+    for k in ("rounds", "reshare_bytes", "bytes", "messages"):
+        assert outs[0][3][k] == outs[1][3][k], k
+    sign = [v >> (bits - 1) for v in R.to_ints(outs[0][5]).tolist()]
+    assert R.to_ints(outs[0][4]).tolist() == sign
