@@ -1002,6 +1002,69 @@ __global__ void __launch_bounds__(256) k_bitdec3(const T* __restrict__ x0, const
   }
 }
 
+// rep.mux(s, x, y) = s * (x - y) + y for arithmetic sharings, three stacked parties, ONE
+// launch: the share-wise differences, the RSS product with its zero share
+// PRF(k_p, nonce) - PRF(k_{p+1}, nonce) and reshare (as k_rss_cross_ring3_lat), and the
+// share-wise add of y -- bitwise the sub + mul + add kernels it replaces.  Latency form:
+// the block's 3 x EPB keystream chunks one per thread, then EPB threads finish.
+template <class T>
+__global__ void __launch_bounds__(256) k_mux3_lat(const T* __restrict__ s0, const T* __restrict__ s1,
+                                                  const T* __restrict__ x0, const T* __restrict__ x1,
+                                                  const T* __restrict__ y0, const T* __restrict__ y1,
+                                                  T* __restrict__ out0, T* __restrict__ out1,
+                                                  int64_t n, KeySrc keys, uint64_t nonce) {
+  constexpr int EPB = 256 / 3;
+  constexpr int P = Lane<T>::kPer;
+  __shared__ uint32_t rks[3][kKeyWords];
+  __shared__ uint64_t kl[3][EPB], kh[3][EPB];
+  stage_keys(rks, keys, 3);
+  const int64_t nb = (n + P - 1) / P;
+  const int tid = threadIdx.x, s = tid / EPB, lb = tid % EPB;
+  const bool r4 = out1 == out0 + n;  // 4-slot ring: out1's slots 0, 1 are out0's 1, 2
+  for (int64_t b0 = (int64_t)blockIdx.x * EPB; b0 < nb; b0 += (int64_t)gridDim.x * EPB) {
+    const bool fin = tid < EPB && b0 + tid < nb;
+    T v[3][P], ya[3][P], yb[3][P];  // operands first: their loads overlap the keystream work
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const int64_t e = (b0 + tid) * P + j, i = (int64_t)p * n + e;
+        if (fin && e < n) {
+          const T a0 = s0[i], a1 = s1[i], d0 = x0[i] - y0[i], d1 = x1[i] - y1[i];
+          v[p][j] = a0 * d0 + a0 * d1 + a1 * d0;
+          ya[p][j] = y0[i];
+          yb[p][j] = y1[i];
+        } else {
+          v[p][j] = ya[p][j] = yb[p][j] = 0;
+        }
+      }
+    }
+    if (s < 3 && b0 + lb < nb) {
+      uint64_t lo, hi;
+      prf_chunk(rks[s], nonce, (uint64_t)(b0 + lb), &lo, &hi);
+      kl[s][lb] = lo;
+      kh[s][lb] = hi;
+    }
+    __syncthreads();
+    if (fin) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const int q = p == 2 ? 0 : p + 1, pm = p == 0 ? 2 : p - 1;
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+          const int64_t e = (b0 + tid) * P + j;
+          if (e >= n) break;
+          const T z = v[p][j] + pick<T>(kl[p][tid], kh[p][tid], j) - pick<T>(kl[q][tid], kh[q][tid], j);
+          out0[(int64_t)p * n + e] = z + ya[p][j];
+          // z_p is party p-1's second share: out1[p-1] = z_p + y1[p-1]
+          if (!r4 || pm == 2) out1[(int64_t)pm * n + e] = z + yb[pm][j];
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // The adder's sum after the last level, both share components: p ^ ((g ^ t) << 1).
 template <class T>
 __global__ void __launch_bounds__(256) k_ks_sum2(const T* __restrict__ p0, const T* __restrict__ p1,
@@ -1951,6 +2014,24 @@ int mxh_ks_cross1(int words, const void* g0, const void* g1, const void* p0, con
   }
   MX_LAUNCH_CHECK();
   return 0;
+}
+
+// slots: k0, k1, k2 of the placement
+int mxh_mux3(int words, const void* s0, const void* s1, const void* x0, const void* x1,
+             const void* y0, const void* y1, void* out0, void* out1, int64_t n,
+             const uint32_t* slots, uint64_t nonce, void* stream) {
+  if (n == 0) return 0;
+  const uint32_t* ptrs[3];
+  for (int i = 0; i < 3; ++i) ptrs[i] = slots + MX_KEY_SLOT_WORDS * i;
+  DEV_DISPATCH(words, T, {
+    constexpr int P = 16 / (int)sizeof(T);
+    const int64_t g = std::min<int64_t>(((n + P - 1) / P + 84) / 85, 16384);
+    hipLaunchKernelGGL(k_mux3_lat<T>, dim3((unsigned)g), dim3(256), 0, S(stream), (const T*)s0,
+                       (const T*)s1, (const T*)x0, (const T*)x1, (const T*)y0, (const T*)y1,
+                       (T*)out0, (T*)out1, n, mxd::keysrc_slots(ptrs, 3), nonce);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
 }
 
 // slots: k0, k1, k2 of the placement; nonces: one per adder level (nlev <= 8)

@@ -1538,6 +1538,23 @@ def b2a3(b0: RT, b1: RT, ring_bits: int, slot_ptr: int, mir: bool, n1: int, nmul
     return o0, o1
 
 
+def mux3(s0: RT, s1: RT, x0: RT, x1: RT, y0: RT, y1: RT, slot_ptr: int, nonce: int):
+    """rep.mux(s, x, y) = s * (x - y) + y for arithmetic stacked sharings in one launch
+    (k_mux3_lat, zero-share nonce ``nonce``).  Returns (s0, s1), or None (host, shapes)."""
+    ts = (s0, s1, x0, x1, y0, y1)
+    bits = s0.bits
+    if not s0.data.is_cuda or bits not in (64, 128) or any(
+            t.bits != bits or t.shape != s0.shape for t in ts) or s0.shape[0] != 3:
+        return None
+    ds = [t.data.contiguous() for t in ts]
+    o0, o1 = ring4(s0.shape, bits, ds[0].device)
+    nat.check(nat.lib().mxh_mux3(_words(bits), *[nat.ptr(d) for d in ds], nat.ptr(o0.data),
+                                 nat.ptr(o1.data), math.prod(s0.shape[1:]),
+                                 ctypes.c_void_p(slot_ptr), nonce & MASK64,
+                                 nat.stream_of(ds[0])), "mux3")
+    return o0, o1
+
+
 def bitdec3(x0: RT, x1: RT, slot_ptr: int, mir: bool, n1: int, nmul: int, nonces,
             sign_nonces=None):
     """The whole of rep.bit_decompose for three stacked parties in one launch (k_bitdec3):

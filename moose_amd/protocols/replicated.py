@@ -812,6 +812,11 @@ def mux(sess, s: RepTensor, x: RepTensor, y: RepTensor) -> RepTensor:
     """s ? x : y ; s is an arithmetic 0/1 sharing or a boolean bit sharing."""
     if s.kind == "bool":
         s = b2a(sess, s, x.bits)
+    f = getattr(sess, "p_mux", None)
+    if f is not None and x.kind == "arith" and y.kind == "arith":
+        r = f(x.plc, s, x, y)  # the three steps in one kernel (same nonce, same shares)
+        if r is not None:
+            return RepTensor(x.plc, x.bits, "arith", r[0], r[1])
     return add(sess, mul(sess, s, sub(sess, x, y)), y)
 
 

@@ -426,3 +426,34 @@ def test_sign_arith_one_kernel_matches_generic(bits, n, mirror):
         assert outs[0][3][k] == outs[1][3][k], k
     sign = [v >> (bits - 1) for v in R.to_ints(outs[0][5]).tolist()]
     assert R.to_ints(outs[0][4]).tolist() == sign
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits,n", [(64, 301), (128, 300), (128, 70001)])
+def test_mux_one_kernel_matches_generic(bits, n):
+    """rep.mux(s, x, y) = s (x - y) + y in one kernel (StackedSession.p_mux, k_mux3_lat)
+    gives bitwise the shares, nonce position and traffic of the sub + mul + add steps, and
+    opens to the selection."""
+    from moose_amd.runtime.session import HV
+
+    plc = ReplicatedPlacement(owners=("a", "b", "c"))
+    outs = []
+    for whole in (True, False):
+        sess = StackedSession("cuda", seed=23)
+        if not whole:
+            sess.p_mux = lambda *a, **k: None
+        bit = R.from_ints(np.arange(n) % 2, bits, "cuda")
+        s = rep.share(sess, plc, HV("a", bit))
+        x = rep.share(sess, plc, HV("b", _rand((n,), bits, "cuda", 31)))
+        y = rep.share(sess, plc, HV("c", _rand((n,), bits, "cuda", 32)))
+        m = rep.mux(sess, s, x, y)
+        nxt = rep.share(sess, plc, HV("b", _rand((7,), bits, "cuda", 5)))  # next nonce
+        opened = rep.reveal(sess, m, "a").v
+        outs.append((m.s0.v, m.s1.v, nxt.s0.v, sess.stats.as_dict(), opened))
+    for i in (0, 1, 2, 4):
+        _eq(outs[0][i], outs[1][i])
+    for k in ("rounds", "reshare_bytes", "bytes", "messages"):
+        assert outs[0][3][k] == outs[1][3][k], k
+    xs, ys = R.to_ints(_rand((n,), bits, "cpu", 31)), R.to_ints(_rand((n,), bits, "cpu", 32))
+    want = [int(xs[i]) if i % 2 else int(ys[i]) for i in range(n)]
+    assert R.to_ints(outs[0][4]).tolist() == want
