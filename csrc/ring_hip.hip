@@ -351,12 +351,17 @@ __global__ void __launch_bounds__(256) k_b2a_prep3(const uint8_t* __restrict__ s
 // 0 the cross terms are c_0 = 0, c_1 = A_1 b_2, c_2 = A_0 b_2.  Four keystream chunks per
 // chunk position, one per thread into LDS (as k_rss_cross_ring3_lat), then EPB threads
 // finish the elements: bitwise the shares of b2a_prep3 + share3 + rss_mul3 + lincomb2.
+// With pw0 (k_b2a3 over bit planes): the bits are read from packed boolean share words
+// [3][m] (T) instead of bit tensors -- element e = j * m + i is bit start + j of word i (the
+// BitSplit planes [3][count][m] it replaces).
 template <class T>
 __global__ void __launch_bounds__(256) k_b2a3(const uint8_t* __restrict__ s0,
                                               const uint8_t* __restrict__ s1,
                                               T* __restrict__ out0, T* __restrict__ out1,
                                               int64_t n, mxd::KeySrc keys, int mir, uint64_t n1,
-                                              uint64_t nmul) {
+                                              uint64_t nmul, const T* __restrict__ pw0 = nullptr,
+                                              const T* __restrict__ pw1 = nullptr,
+                                              int start = 0, int64_t m = 1) {
   constexpr int EPB = 64;
   __shared__ uint32_t rks[3][mxd::kKeyWords];
   __shared__ uint64_t kl[4][EPB], kh[4][EPB];
@@ -375,9 +380,17 @@ __global__ void __launch_bounds__(256) k_b2a3(const uint8_t* __restrict__ s0,
     for (int j = 0; j < P; ++j) {
       const int64_t e = (b0 + tid) * P + j;
       const bool ok = fin && e < n;
-      ba[j] = ok ? (uint8_t)(s0[e] ^ s1[e]) : 0;
-      bx[j] = ok ? s0[2 * n + e] : 0;
-      by[j] = ok ? s1[n + e] : 0;
+      if (pw0 != nullptr) {  // bit start + e / m of packed word e % m
+        const int64_t pj = ok ? e / m : 0, pi = ok ? e - pj * m : 0;
+        const int sh = start + (int)pj;
+        ba[j] = ok ? (uint8_t)(((pw0[pi] ^ pw1[pi]) >> sh) & 1) : 0;
+        bx[j] = ok ? (uint8_t)((pw0[2 * m + pi] >> sh) & 1) : 0;
+        by[j] = ok ? (uint8_t)((pw1[m + pi] >> sh) & 1) : 0;
+      } else {
+        ba[j] = ok ? (uint8_t)(s0[e] ^ s1[e]) : 0;
+        bx[j] = ok ? s0[2 * n + e] : 0;
+        by[j] = ok ? s1[n + e] : 0;
+      }
     }
     if (b0 + lb < nb) {
       uint64_t lo, hi;
@@ -2014,6 +2027,27 @@ int mxh_ks_cross1(int words, const void* g0, const void* g1, const void* p0, con
   }
   MX_LAUNCH_CHECK();
   return 0;
+}
+
+// mxh_b2a3 over bit planes start..start+count-1 of packed boolean share words w0, w1
+// ([3][m] ring words): out [3][count * m] (plane-major per party, as BitSplit lays them)
+int mxh_b2a3_planes(int words, const void* w0, const void* w1, int64_t m, int start, int count,
+                    void* out0, void* out1, const uint32_t* slots, int mir, uint64_t n1,
+                    uint64_t nmul, void* stream) {
+  const int64_t n = m * count;
+  if (n == 0) return 0;
+  if (words != 1 && words != 2) return -2;
+  const uint32_t* ptrs[3];
+  for (int i = 0; i < 3; ++i) ptrs[i] = slots + MX_KEY_SLOT_WORDS * i;
+  DEV_DISPATCH(words, T, {
+    constexpr int P = 16 / (int)sizeof(T);
+    const int64_t g = std::min<int64_t>(((n + P - 1) / P + 63) / 64, 16384);
+    hipLaunchKernelGGL(k_b2a3<T>, dim3((unsigned)g), dim3(256), 0, S(stream), nullptr, nullptr,
+                       (T*)out0, (T*)out1, n, mxd::keysrc_slots(ptrs, 3), mir ? 1 : 0, n1, nmul,
+                       (const T*)w0, (const T*)w1, start, m);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
 }
 
 // slots: k0, k1, k2 of the placement

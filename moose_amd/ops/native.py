@@ -87,6 +87,10 @@ _SIGS = {
                 c_vp, c_vp],
     ),
     "mxh_b2a_prep3": (c_int, [c_int, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "mxh_b2a3_planes": (
+        c_int, [c_int, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_u64, c_u64,
+                c_vp],
+    ),
     "mxh_mux3": (
         c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_u64, c_vp],
     ),

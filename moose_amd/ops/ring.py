@@ -1538,6 +1538,26 @@ def b2a3(b0: RT, b1: RT, ring_bits: int, slot_ptr: int, mir: bool, n1: int, nmul
     return o0, o1
 
 
+def b2a3_planes(w0: RT, w1: RT, start: int, count: int, slot_ptr: int, mir: bool, n1: int,
+                nmul: int):
+    """b2a3 of BitSplit(start, count) of a packed boolean share pair (w0, w1: [3, ...] ring
+    words) in one launch, the planes never materialised: (s0, s1) arithmetic [3, count,
+    ...] pairs, or None (host)."""
+    d0, d1 = w0.data, w1.data
+    bits = w0.bits
+    if not d0.is_cuda or bits not in (64, 128) or w1.bits != bits or w0.shape != w1.shape \
+            or w0.shape[0] != 3 or start < 0 or count < 1 or start + count > bits:
+        return None
+    d0, d1 = d0.contiguous(), d1.contiguous()
+    rest = tuple(w0.shape[1:])
+    o0, o1 = ring4((3, count) + rest, bits, d0.device)
+    nat.check(nat.lib().mxh_b2a3_planes(
+        _words(bits), nat.ptr(d0), nat.ptr(d1), math.prod(rest), int(start), int(count),
+        nat.ptr(o0.data), nat.ptr(o1.data), ctypes.c_void_p(slot_ptr), int(bool(mir)),
+        n1 & MASK64, nmul & MASK64, nat.stream_of(d0)), "b2a3_planes")
+    return o0, o1
+
+
 def mux3(s0: RT, s1: RT, x0: RT, x1: RT, y0: RT, y1: RT, slot_ptr: int, nonce: int):
     """rep.mux(s, x, y) = s * (x - y) + y for arithmetic stacked sharings in one launch
     (k_mux3_lat, zero-share nonce ``nonce``).  Returns (s0, s1), or None (host, shapes)."""

@@ -350,10 +350,7 @@ def _top_bit_onehot(sess, x: RepTensor, lo: int, hi: int) -> RepTensor:
         p = _or(sess, p, rep.local(sess, p, "Shr", amount=d))
         d *= 2
     onehot = rep.xor(sess, p, rep.local(sess, p, "Shr", amount=1))
-    planes = RepTensor(x.plc, 1, "bool", *rep._sharewise(sess, "BitSplit", x.plc,
-                                                         (onehot.s0, onehot.s1), start=lo,
-                                                         count=hi - lo))
-    return rep.b2a(sess, planes, bits)
+    return rep.b2a_planes(sess, onehot, lo, hi - lo, bits)
 
 
 def _weighted(sess, t: RepTensor, weights, bits) -> RepTensor:
@@ -551,9 +548,7 @@ def _exp2_parts(sess, a: RepFixed, negative: bool):
               and getattr(sess, "party_dot_trunc", None) is not None
               and hasattr(sess, "p_cross_plain") and npad >= 2 and npad & (npad - 1) == 0)
     bd = rep.bit_decompose(sess, a.t)
-    planes = RepTensor(a.plc, 1, "bool", *rep._sharewise(sess, "BitSplit", a.plc, (bd.s0, bd.s1),
-                                                         start=0, count=f + npad))
-    ab = rep.b2a(sess, planes, bits)  # arithmetic bits, leading axis
+    ab = rep.b2a_planes(sess, bd, 0, f + npad, bits)  # arithmetic bits, leading axis
     frac_w = [(1 << j) for j in range(f)] + [0] * npad
     r = RepFixed(_weighted(sess, ab, frac_w, bits), f, integ)
     if negative:

@@ -768,6 +768,18 @@ def b2a(sess, b: RepTensor, ring_bits: int) -> RepTensor:
         return lincomb(sess, [(1, A), (1, B), (-2, AB)])
 
 
+def b2a_planes(sess, b: RepTensor, start: int, count: int, ring_bits: int) -> RepTensor:
+    """b2a of bit planes start..start+count-1 of a packed boolean sharing (a new leading
+    logical axis): BitSplit + b2a, one kernel on a stacked device session (same shares)."""
+    f = getattr(sess, "p_b2a_planes", None)
+    r = f(b.plc, b, start, count, ring_bits) if f is not None else None
+    if r is not None:
+        return RepTensor(b.plc, ring_bits, "arith", r[0], r[1])
+    planes = RepTensor(b.plc, 1, "bool", *_sharewise(sess, "BitSplit", b.plc, (b.s0, b.s1),
+                                                     start=start, count=count))
+    return b2a(sess, planes, ring_bits)
+
+
 def msb(sess, x: RepTensor) -> RepTensor:
     """Boolean sharing of the sign bit."""
     bd = bit_decompose(sess, x)

@@ -391,6 +391,26 @@ class StackedSession(Session):
         self.stats.record_round(3 * nb)
         return PV(plc, o0), PV(plc, o1)
 
+    def p_b2a_planes(self, plc, b, start, count, ring_bits):
+        """rep.b2a of the bit planes start..start+count-1 of the packed boolean sharing
+        ``b`` (BitSplit + b2a) in one kernel: the b2a's nonces and traffic records as
+        p_b2a draws and records them.  None -> the two steps."""
+        if self.device.type != "cuda" or not getattr(self, "fused", False) \
+                or os.environ.get("MOOSEX_B2A_FUSED", "1") == "0":
+            return None
+        v0, v1 = b.s0.v, b.s1.v
+        if not (isinstance(v0, R.RT) and isinstance(v1, R.RT)) or v0.bits != ring_bits \
+                or v0.bits not in (64, 128) or v1.shape != v0.shape or v0.shape[0] != 3 \
+                or start < 0 or count < 1 or start + count > v0.bits:
+            return None
+        d = self.share_dir(plc, 0)
+        n1, _na, nmul = self.nonce(plc), self.nonce(plc), self.nonce(plc)
+        o0, o1 = R.b2a3_planes(v0, v1, start, count, self.key_ptr(plc, 0), d == 2, n1, nmul)
+        nb = count * math.prod(v0.shape[1:]) * (ring_bits // 8)
+        self.stats.record_send(plc.owners[0], plc.owners[d % 3], nb)
+        self.stats.record_round(3 * nb)
+        return PV(plc, o0), PV(plc, o1)
+
     def p_mux(self, plc, s, x, y):
         """rep.mux(s, x, y) = s * (x - y) + y (arithmetic) in one kernel: the product's one
         nonce and its round as rep.mul draws and records them.  None -> the three steps."""

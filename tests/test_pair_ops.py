@@ -457,3 +457,36 @@ def test_mux_one_kernel_matches_generic(bits, n):
     xs, ys = R.to_ints(_rand((n,), bits, "cpu", 31)), R.to_ints(_rand((n,), bits, "cpu", 32))
     want = [int(xs[i]) if i % 2 else int(ys[i]) for i in range(n)]
     assert R.to_ints(outs[0][4]).tolist() == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits,start,count,mirror", [(64, 0, 30, False), (128, 3, 50, True),
+                                                     (128, 0, 128, False)])
+def test_b2a_planes_one_kernel_matches_generic(bits, start, count, mirror):
+    """rep.b2a_planes (BitSplit + b2a) in one kernel (k_b2a3 reading the packed words) gives
+    bitwise the shares, nonce position and traffic records of the two steps; it opens to
+    the bits of the decomposed value."""
+    from moose_amd.runtime.session import HV
+
+    plc = ReplicatedPlacement(owners=("a", "b", "c"))
+    outs = []
+    for whole in (True, False):
+        sess = StackedSession("cuda", seed=29)
+        if mirror:
+            sess.share_dirs = {"a": 2}
+        if not whole:
+            sess.p_b2a_planes = lambda *a, **k: None
+        xv = _rand((5, 41), bits, "cuda", 33)
+        bd = rep.bit_decompose(sess, rep.share(sess, plc, HV("b", xv)))
+        y = rep.b2a_planes(sess, bd, start, count, bits)
+        nxt = rep.share(sess, plc, HV("b", _rand((7,), bits, "cuda", 5)))  # next nonce
+        opened = rep.reveal(sess, y, "a").v
+        outs.append((y.s0.v, y.s1.v, nxt.s0.v, sess.stats.as_dict(), opened, xv))
+    for i in (0, 1, 2, 4):
+        _eq(outs[0][i], outs[1][i])
+    for k in ("rounds", "reshare_bytes", "bytes", "messages"):
+        assert outs[0][3][k] == outs[1][3][k], k
+    xs = R.to_ints(outs[0][5]).reshape(-1).tolist()
+    got = R.to_ints(outs[0][4]).reshape(count, -1)
+    for j in range(count):
+        assert got[j].tolist() == [(v >> (start + j)) & 1 for v in xs]
