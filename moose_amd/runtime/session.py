@@ -381,8 +381,10 @@ class StackedSession(Session):
             return None
         v0, v1 = b.s0.v, b.s1.v
         if not (isinstance(v0, R.RT) and isinstance(v1, R.RT)) or v0.bits != 1 \
-                or ring_bits not in (64, 128) or not v0.data.is_cuda:
-            return None
+                or ring_bits not in (64, 128) or not v0.data.is_cuda \
+                or v0.data.dtype != torch.uint8 or v1.data.dtype != torch.uint8 \
+                or v0.data.shape != v1.data.shape or v0.data.shape[0] != 3:
+            return None  # (R.b2a3's own conditions, checked before any nonce is drawn)
         d = self.share_dir(plc, 0)
         n1, _na, nmul = self.nonce(plc), self.nonce(plc), self.nonce(plc)
         o0, o1 = R.b2a3(v0, v1, ring_bits, self.key_ptr(plc, 0), d == 2, n1, nmul)
