@@ -1025,7 +1025,8 @@ __global__ void __launch_bounds__(256) k_mux3_lat(const T* __restrict__ s0, cons
                                                   const T* __restrict__ x0, const T* __restrict__ x1,
                                                   const T* __restrict__ y0, const T* __restrict__ y1,
                                                   T* __restrict__ out0, T* __restrict__ out1,
-                                                  int64_t n, KeySrc keys, uint64_t nonce) {
+                                                  int64_t n, KeySrc keys, uint64_t nonce,
+                                                  int absv = 0) {
   constexpr int EPB = 256 / 3;
   constexpr int P = Lane<T>::kPer;
   __shared__ uint32_t rks[3][kKeyWords];
@@ -1043,10 +1044,12 @@ __global__ void __launch_bounds__(256) k_mux3_lat(const T* __restrict__ s0, cons
       for (int j = 0; j < P; ++j) {
         const int64_t e = (b0 + tid) * P + j, i = (int64_t)p * n + e;
         if (fin && e < n) {
-          const T a0 = s0[i], a1 = s1[i], d0 = x0[i] - y0[i], d1 = x1[i] - y1[i];
+          // absv: x - 2 s x (rep.lincomb of x and the product) -- operand x, added x
+          const T a0 = s0[i], a1 = s1[i];
+          const T d0 = absv ? x0[i] : (T)(x0[i] - y0[i]), d1 = absv ? x1[i] : (T)(x1[i] - y1[i]);
           v[p][j] = a0 * d0 + a0 * d1 + a1 * d0;
-          ya[p][j] = y0[i];
-          yb[p][j] = y1[i];
+          ya[p][j] = absv ? x0[i] : y0[i];
+          yb[p][j] = absv ? x1[i] : y1[i];
         } else {
           v[p][j] = ya[p][j] = yb[p][j] = 0;
         }
@@ -1068,9 +1071,10 @@ __global__ void __launch_bounds__(256) k_mux3_lat(const T* __restrict__ s0, cons
           const int64_t e = (b0 + tid) * P + j;
           if (e >= n) break;
           const T z = v[p][j] + pick<T>(kl[p][tid], kh[p][tid], j) - pick<T>(kl[q][tid], kh[q][tid], j);
-          out0[(int64_t)p * n + e] = z + ya[p][j];
+          const T zz = absv ? (T)(0 - (z << 1)) : z;
+          out0[(int64_t)p * n + e] = zz + ya[p][j];
           // z_p is party p-1's second share: out1[p-1] = z_p + y1[p-1]
-          if (!r4 || pm == 2) out1[(int64_t)pm * n + e] = z + yb[pm][j];
+          if (!r4 || pm == 2) out1[(int64_t)pm * n + e] = zz + yb[pm][j];
         }
       }
     }
@@ -2051,9 +2055,10 @@ int mxh_b2a3_planes(int words, const void* w0, const void* w1, int64_t m, int st
 }
 
 // slots: k0, k1, k2 of the placement
+// absv: x - 2 s x instead (y unused)
 int mxh_mux3(int words, const void* s0, const void* s1, const void* x0, const void* x1,
              const void* y0, const void* y1, void* out0, void* out1, int64_t n,
-             const uint32_t* slots, uint64_t nonce, void* stream) {
+             const uint32_t* slots, uint64_t nonce, int absv, void* stream) {
   if (n == 0) return 0;
   const uint32_t* ptrs[3];
   for (int i = 0; i < 3; ++i) ptrs[i] = slots + MX_KEY_SLOT_WORDS * i;
@@ -2062,7 +2067,7 @@ int mxh_mux3(int words, const void* s0, const void* s1, const void* x0, const vo
     const int64_t g = std::min<int64_t>(((n + P - 1) / P + 84) / 85, 16384);
     hipLaunchKernelGGL(k_mux3_lat<T>, dim3((unsigned)g), dim3(256), 0, S(stream), (const T*)s0,
                        (const T*)s1, (const T*)x0, (const T*)x1, (const T*)y0, (const T*)y1,
-                       (T*)out0, (T*)out1, n, mxd::keysrc_slots(ptrs, 3), nonce);
+                       (T*)out0, (T*)out1, n, mxd::keysrc_slots(ptrs, 3), nonce, absv);
     MX_LAUNCH_CHECK();
     return 0;
   });

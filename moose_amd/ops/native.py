@@ -92,7 +92,8 @@ _SIGS = {
                 c_vp],
     ),
     "mxh_mux3": (
-        c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_u64, c_vp],
+        c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_u64, c_int,
+                c_vp],
     ),
     "mxh_bitdec3": (
         c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_u64, c_u64, c_vp,

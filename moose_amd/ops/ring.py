@@ -1558,9 +1558,11 @@ def b2a3_planes(w0: RT, w1: RT, start: int, count: int, slot_ptr: int, mir: bool
     return o0, o1
 
 
-def mux3(s0: RT, s1: RT, x0: RT, x1: RT, y0: RT, y1: RT, slot_ptr: int, nonce: int):
+def mux3(s0: RT, s1: RT, x0: RT, x1: RT, y0: RT, y1: RT, slot_ptr: int, nonce: int,
+         absv: bool = False):
     """rep.mux(s, x, y) = s * (x - y) + y for arithmetic stacked sharings in one launch
-    (k_mux3_lat, zero-share nonce ``nonce``).  Returns (s0, s1), or None (host, shapes)."""
+    (k_mux3_lat, zero-share nonce ``nonce``); ``absv``: x - 2 s x instead (y = x, unused).
+    Returns (s0, s1), or None (host, shapes)."""
     ts = (s0, s1, x0, x1, y0, y1)
     bits = s0.bits
     if not s0.data.is_cuda or bits not in (64, 128) or any(
@@ -1570,7 +1572,7 @@ def mux3(s0: RT, s1: RT, x0: RT, x1: RT, y0: RT, y1: RT, slot_ptr: int, nonce: i
     o0, o1 = ring4(s0.shape, bits, ds[0].device)
     nat.check(nat.lib().mxh_mux3(_words(bits), *[nat.ptr(d) for d in ds], nat.ptr(o0.data),
                                  nat.ptr(o1.data), math.prod(s0.shape[1:]),
-                                 ctypes.c_void_p(slot_ptr), nonce & MASK64,
+                                 ctypes.c_void_p(slot_ptr), nonce & MASK64, int(bool(absv)),
                                  nat.stream_of(ds[0])), "mux3")
     return o0, o1
 

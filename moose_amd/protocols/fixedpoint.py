@@ -300,7 +300,7 @@ def relu(sess, x: RepFixed) -> RepFixed:
 
 def abs_(sess, x: RepFixed) -> RepFixed:
     s = sign_bit(sess, x)
-    return _with(x, rep.lincomb(sess, [(1, x.t), (-2, rep.mul(sess, s, x.t))]))
+    return _with(x, rep.negate_where(sess, s, x.t))
 
 
 def _stack0(sess, xs):
@@ -486,7 +486,7 @@ def reciprocal_positive(sess, x: RepFixed) -> RepFixed:
 
 def reciprocal(sess, x: RepFixed) -> RepFixed:
     s = sign_bit(sess, x)
-    ax = _with(x, rep.lincomb(sess, [(1, x.t), (-2, rep.mul(sess, s, x.t))]))
+    ax = _with(x, rep.negate_where(sess, s, x.t))
     r = reciprocal_positive(sess, ax)
     return _with(r, rep.lincomb(sess, [(1, r.t), (-2, rep.mul(sess, s, r.t))]))
 
@@ -749,7 +749,7 @@ def _merged_exp_tail(sess, x: RepFixed, fac: RepTensor, npad: int) -> RepFixed:
 
 def exp2(sess, x: RepFixed) -> RepFixed:
     s = sign_bit(sess, x)
-    ax = _with(x, rep.lincomb(sess, [(1, x.t), (-2, rep.mul(sess, s, x.t))]))
+    ax = _with(x, rep.negate_where(sess, s, x.t))
     pos = _exp2_parts(sess, ax, negative=False)
     negv = _exp2_parts(sess, ax, negative=True)
     return _with(pos, rep.mux(sess, s, negv.t, pos.t))
@@ -769,7 +769,7 @@ def sigmoid(sess, x: RepFixed) -> RepFixed:
     """sigma(x) = 1 / (1 + e^-|x|) mirrored for x < 0; 1 + e^-|x| is in [1, 2] so the
     reciprocal needs no normalisation."""
     s = sign_bit(sess, x)
-    ax = _with(x, rep.lincomb(sess, [(1, x.t), (-2, rep.mul(sess, s, x.t))]))
+    ax = _with(x, rep.negate_where(sess, s, x.t))
     e = exp_nonpositive(sess, neg(sess, ax))
     d = add_const(sess, e, 1.0)  # in [1, 2]
     # 1/d = (1/h) / 2 with h = d / 2 in [0.5, 1]: the fit of 1/h evaluated at d directly

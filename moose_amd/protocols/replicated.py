@@ -832,10 +832,20 @@ def mux(sess, s: RepTensor, x: RepTensor, y: RepTensor) -> RepTensor:
     return add(sess, mul(sess, s, sub(sess, x, y)), y)
 
 
+def negate_where(sess, s: RepTensor, x: RepTensor) -> RepTensor:
+    """x - 2 s x for an arithmetic 0/1 sharing s (|x| when s = [x < 0]): the product and the
+    lincomb in one kernel on a stacked device session (same nonce, same shares)."""
+    f = getattr(sess, "p_mux", None)
+    if f is not None and s.kind == "arith" and x.kind == "arith":
+        r = f(x.plc, s, x, x, absv=True)
+        if r is not None:
+            return RepTensor(x.plc, x.bits, "arith", r[0], r[1])
+    return lincomb(sess, [(1, x), (-2, mul(sess, s, x))])
+
+
 def abs_(sess, x: RepTensor) -> RepTensor:
     s = less_than_zero_arith(sess, x)
-    # |x| = x - 2 s x
-    return lincomb(sess, [(1, x), (-2, mul(sess, s, x))])
+    return negate_where(sess, s, x)  # |x| = x - 2 s x
 
 
 def relu(sess, x: RepTensor) -> RepTensor:

@@ -413,16 +413,18 @@ class StackedSession(Session):
         self.stats.record_round(3 * nb)
         return PV(plc, o0), PV(plc, o1)
 
-    def p_mux(self, plc, s, x, y):
+    def p_mux(self, plc, s, x, y, absv=False):
         """rep.mux(s, x, y) = s * (x - y) + y (arithmetic) in one kernel: the product's one
-        nonce and its round as rep.mul draws and records them.  None -> the three steps."""
+        nonce and its round as rep.mul draws and records them.  ``absv``: x - 2 s x
+        (rep.lincomb of x and mul(s, x); y is x).  None -> the three steps."""
         if self.device.type != "cuda" or not getattr(self, "fused", False):
             return None
         vs = [t.v for t in (s.s0, s.s1, x.s0, x.s1, y.s0, y.s1)]
         if not all(isinstance(v, R.RT) for v in vs) or vs[0].bits not in (64, 128) or any(
-                v.bits != vs[0].bits or v.shape != vs[0].shape for v in vs):
+                v.bits != vs[0].bits or v.shape != vs[0].shape for v in vs) \
+                or len(vs[0].shape) < 1 or vs[0].shape[0] != 3 or not vs[0].data.is_cuda:
             return None
-        r = R.mux3(*vs, self.key_ptr(plc, 0), self.nonce(plc))
+        r = R.mux3(*vs, self.key_ptr(plc, 0), self.nonce(plc), absv=absv)
         if r is None:  # a nonce is drawn: never fall back silently
             raise RuntimeError("mux3 declined after its checks")
         self.stats.record_round(_nbytes(r[0]))

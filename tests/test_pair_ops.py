@@ -490,3 +490,32 @@ def test_b2a_planes_one_kernel_matches_generic(bits, start, count, mirror):
     got = R.to_ints(outs[0][4]).reshape(count, -1)
     for j in range(count):
         assert got[j].tolist() == [(v >> (start + j)) & 1 for v in xs]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits,n", [(64, 301), (128, 300)])
+def test_negate_where_one_kernel_matches_generic(bits, n):
+    """rep.negate_where(s, x) = x - 2 s x in one kernel (k_mux3_lat, absv) gives bitwise the
+    shares, nonce position and traffic of mul + lincomb, and opens to -x where s = 1."""
+    from moose_amd.runtime.session import HV
+
+    plc = ReplicatedPlacement(owners=("a", "b", "c"))
+    outs = []
+    for whole in (True, False):
+        sess = StackedSession("cuda", seed=37)
+        if not whole:
+            sess.p_mux = lambda *a, **k: None
+        bit = R.from_ints(np.arange(n) % 2, bits, "cuda")
+        s = rep.share(sess, plc, HV("a", bit))
+        x = rep.share(sess, plc, HV("b", _rand((n,), bits, "cuda", 41)))
+        m = rep.negate_where(sess, s, x)
+        nxt = rep.share(sess, plc, HV("b", _rand((7,), bits, "cuda", 5)))  # next nonce
+        opened = rep.reveal(sess, m, "a").v
+        outs.append((m.s0.v, m.s1.v, nxt.s0.v, sess.stats.as_dict(), opened))
+    for i in (0, 1, 2, 4):
+        _eq(outs[0][i], outs[1][i])
+    for k in ("rounds", "reshare_bytes", "bytes", "messages"):
+        assert outs[0][3][k] == outs[1][3][k], k
+    xs = R.to_ints(_rand((n,), bits, "cpu", 41))
+    want = [(-int(xs[i])) % (1 << bits) if i % 2 else int(xs[i]) for i in range(n)]
+    assert R.to_ints(outs[0][4]).tolist() == want
