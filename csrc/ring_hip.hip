@@ -1082,6 +1082,24 @@ __global__ void __launch_bounds__(256) k_mux3_lat(const T* __restrict__ s0, cons
   }
 }
 
+// a * f + (batch row in {ra, rb} ? c : 0), elementwise over a [rows][per] stack with f of
+// the same shape and c a scalar on the device: exp's integer-part factors (MulLeading by the
+// public vector's broadcast, then add_public of 1 on slot 0 of s0 and slot 2 of s1, here the
+// pair buffer's rows ra, rb) in one launch instead of two.
+template <class T>
+__global__ void __launch_bounds__(256) k_mul_rows_add(const T* __restrict__ a,
+                                                      const T* __restrict__ f,
+                                                      T* __restrict__ out, int64_t n,
+                                                      int64_t per, const T* __restrict__ c,
+                                                      int ra, int rb) {
+  const T cv = c[0];
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / per;
+    out[i] = a[i] * f[i] + ((r == ra || r == rb) ? cv : (T)0);
+  }
+}
+
 // The adder's sum after the last level, both share components: p ^ ((g ^ t) << 1).
 template <class T>
 __global__ void __launch_bounds__(256) k_ks_sum2(const T* __restrict__ p0, const T* __restrict__ p1,
@@ -2049,6 +2067,18 @@ int mxh_b2a3_planes(int words, const void* w0, const void* w1, int64_t m, int st
     hipLaunchKernelGGL(k_b2a3<T>, dim3((unsigned)g), dim3(256), 0, S(stream), nullptr, nullptr,
                        (T*)out0, (T*)out1, n, mxd::keysrc_slots(ptrs, 3), mir ? 1 : 0, n1, nmul,
                        (const T*)w0, (const T*)w1, start, m);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mxh_mul_rows_add(int words, const void* a, const void* f, void* out, int64_t n,
+                     int64_t per, const void* c, int ra, int rb, void* stream) {
+  if (n == 0) return 0;
+  if (words != 1 && words != 2) return -2;
+  DEV_DISPATCH(words, T, {
+    hipLaunchKernelGGL(k_mul_rows_add<T>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
+                       (const T*)a, (const T*)f, (T*)out, n, per, (const T*)c, ra, rb);
     MX_LAUNCH_CHECK();
     return 0;
   });

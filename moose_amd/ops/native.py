@@ -91,6 +91,7 @@ _SIGS = {
         c_int, [c_int, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_u64, c_u64,
                 c_vp],
     ),
+    "mxh_mul_rows_add": (c_int, [c_int, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_int, c_int, c_vp]),
     "mxh_mux3": (
         c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_u64, c_int,
                 c_vp],

@@ -1057,6 +1057,36 @@ def mul_leading(a: RT, c: RT, nb: int) -> RT:
     return binary("mul", a, full)
 
 
+def mul_leading_add(a: RT, c: RT, nb: int, cadd: RT, rows) -> RT:
+    """mul_leading(a, c, nb) plus the public scalar ``cadd`` on batch rows ``rows`` (two of
+    a's leading axis) in one launch (k_mul_rows_add); None when mul_leading would not use a
+    cached broadcast (then the caller runs the two steps)."""
+    if not (a.data.is_cuda and a.bits in (64, 128) and nb == 1 and isinstance(cadd, RT)
+            and cadd.bits == a.bits and cadd.numel() == 1):
+        return None
+    if not (c.data.is_cuda and _CONSTS.get(_const_key.get(id(c))) is c):
+        return None
+    k = len(a.shape) - nb - 1
+    cb = reshape(c, (c.shape[0],) + (1,) * k)
+    key = (id(c), tuple(a.shape))
+    full = _LEADING.get(key)
+    if full is None:
+        full = RT(expand(cb, tuple(a.shape)).data.contiguous(), a.bits)
+        if not torch.cuda.is_current_stream_capturing():
+            _cache_put(_LEADING, key, full, 1024)
+    ad = a.data.contiguous()
+    cd = cadd.data.contiguous()
+    if cd.device != ad.device:
+        cd = cd.to(ad.device)
+    out = empty(a.shape, a.bits, a.device)
+    n = a.numel()
+    nat.check(nat.lib().mxh_mul_rows_add(_words(a.bits), nat.ptr(ad), nat.ptr(full.data),
+                                         nat.ptr(out.data), n, n // a.shape[0], nat.ptr(cd),
+                                         int(rows[0]), int(rows[1]), nat.stream_of(ad)),
+              "mul_rows_add")
+    return out
+
+
 def weighted_sum(a: RT, weights, nb=0) -> RT:
     """sum_j weights[j] * a[.., j, ..] over the leading logical axis (public integer
     weights, e.g. bit composition).  One kernel."""

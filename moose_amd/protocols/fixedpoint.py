@@ -570,10 +570,16 @@ def _exp2_parts(sess, a: RepFixed, negative: bool):
     cs += [0] * (npad - nint)
     ints = local(sess, ab, "Slice", slice=(f, f + npad, None))
     cvec = R.const_ints(cs, bits, sess.device)
-    pc = sess.public(ints.plc, cvec)
-    fac = RepTensor(ints.plc, bits, "arith",
-                    *rep._sharewise(sess, "MulLeading", ints.plc, (ints.s0, ints.s1), (pc, pc)))
-    fac = rep.add_public(sess, fac, _encode_const(sess, 1.0, f, bits))
+    one = _encode_const(sess, 1.0, f, bits)
+    both = getattr(sess, "p_mul_leading_add", None)
+    r = both(ints.plc, ints.s0, ints.s1, cvec, one) if both is not None else None
+    if r is not None:  # the two steps below in one launch (same values)
+        fac = RepTensor(ints.plc, bits, "arith", r[0], r[1])
+    else:
+        pc = sess.public(ints.plc, cvec)
+        fac = RepTensor(ints.plc, bits, "arith", *rep._sharewise(
+            sess, "MulLeading", ints.plc, (ints.s0, ints.s1), (pc, pc)))
+        fac = rep.add_public(sess, fac, one)
     if merged:
         # parties on different processes: the polynomial's levels and the product tree's
         # levels are independent -- each round carries both (module doc: _merged_exp_tail)

@@ -413,6 +413,21 @@ class StackedSession(Session):
         self.stats.record_round(3 * nb)
         return PV(plc, o0), PV(plc, o1)
 
+    def p_mul_leading_add(self, plc, x0, x1, c, cadd):
+        """MulLeading of a share pair by the public vector ``c`` then add_public of the scalar
+        ``cadd`` (slot 0 of s0, slot 2 of s1), one launch over the pair buffer (no nonce, no
+        traffic).  None -> the two steps."""
+        if self.device.type != "cuda" or not getattr(self, "fused", False):
+            return None
+        pb = self._pair_base(x0.v, x1.v)
+        if pb is None:
+            return None
+        base, k, o = pb
+        r = R.mul_leading_add(base, c, 1, cadd, (0, o + 2))
+        if r is None:
+            return None
+        return PV(plc, R.RT(r.data[0:3], r.bits)), PV(plc, R.RT(r.data[o:o + 3], r.bits))
+
     def p_mux(self, plc, s, x, y, absv=False):
         """rep.mux(s, x, y) = s * (x - y) + y (arithmetic) in one kernel: the product's one
         nonce and its round as rep.mul draws and records them.  ``absv``: x - 2 s x

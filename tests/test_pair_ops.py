@@ -519,3 +519,26 @@ def test_negate_where_one_kernel_matches_generic(bits, n):
     xs = R.to_ints(_rand((n,), bits, "cpu", 41))
     want = [(-int(xs[i])) % (1 << bits) if i % 2 else int(xs[i]) for i in range(n)]
     assert R.to_ints(outs[0][4]).tolist() == want
+
+
+@pytest.mark.gpu
+def test_exp_factors_one_launch_matches_two_steps():
+    """exp's integer-part factors (MulLeading by the public vector, then + 1 on party 0's
+    share) in one launch (StackedSession.p_mul_leading_add, k_mul_rows_add) give bitwise the
+    shares of the two steps: whole exp(x) outputs equal with the same seed."""
+    from moose_amd.protocols import fixedpoint as fxp
+    from moose_amd.runtime.session import HV
+
+    plc = ReplicatedPlacement(owners=("a", "b", "c"))
+    vals = torch.linspace(-6, 3, 200, dtype=torch.float64, device="cuda")
+    outs = []
+    for whole in (True, False):
+        sess = StackedSession("cuda", seed=43)
+        if not whole:
+            sess.p_mul_leading_add = lambda *a, **k: None
+        x = rep.share(sess, plc, HV("a", R.encode(vals, 40, 128)))
+        y = fxp.exp(sess, fxp.RepFixed(x, 40, 24))
+        outs.append((y.t.s0.v, y.t.s1.v, sess.stats.as_dict()))
+    _eq(outs[0][0], outs[1][0])
+    _eq(outs[0][1], outs[1][1])
+    assert outs[0][2]["rounds"] == outs[1][2]["rounds"]
