@@ -44,6 +44,8 @@
 #include "hip_attr.h"
 #include "moosex.h"
 
+void mx_ws_note(int dev, int64_t want, bool ok);  // gemm_mfma.hip: workspace bookkeeping
+
 namespace {
 
 using u64 = uint64_t;
@@ -1221,7 +1223,9 @@ void* workspace(int64_t bytes, hipStream_t st) {
     int64_t want = 1 << 20;
     while (want < bytes) want <<= 1;
     void* q = nullptr;
-    if (hipMalloc(&q, want) != hipSuccess) return nullptr;
+    const bool ok = hipMalloc(&q, want) == hipSuccess;
+    mx_ws_note(dev, want, ok);
+    if (!ok) return nullptr;
     w.ptr = q;
     w.bytes = want;
   }

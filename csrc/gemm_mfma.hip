@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <mutex>
 
@@ -783,6 +784,32 @@ bool use_split_kernel() {
   return on;
 }
 
+}  // namespace
+
+// Workspace bookkeeping shared with gemm_crt.hip: the size of the last failed allocation
+// (reported by the Python wrapper when a GEMM returns -4) and the bytes held per device.
+std::atomic<int64_t> g_ws_failed{0};
+std::atomic<int64_t> g_ws_held[16];
+
+void mx_ws_note(int dev, int64_t want, bool ok) {
+  if (ok) {
+    if (dev >= 0 && dev < 16) g_ws_held[dev] += want;
+  } else {
+    g_ws_failed = want;
+    (void)hipGetLastError();  // do not leave the OOM as the sticky error of later launches
+  }
+}
+
+extern "C" int64_t mx_workspace_failed_bytes(void) { return g_ws_failed.exchange(0); }
+
+extern "C" int64_t mx_workspace_held_bytes(void) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 0;
+  return g_ws_held[dev].load();
+}
+
+namespace {
+
 struct Workspace {
   void* ptr = nullptr;
   int64_t bytes = 0;
@@ -816,7 +843,9 @@ void* get_workspace(int64_t bytes, hipStream_t st) {
     int64_t want = 1 << 20;
     while (want < bytes) want <<= 1;
     void* p = nullptr;
-    if (hipMalloc(&p, want) != hipSuccess) return nullptr;
+    const bool ok = hipMalloc(&p, want) == hipSuccess;
+    mx_ws_note(dev, want, ok);
+    if (!ok) return nullptr;
     w.ptr = p;  // the previous buffer (if any) stays allocated
     w.bytes = want;
   }

@@ -150,6 +150,11 @@ int mx_gemm(int dev, int words, int64_t batch, int64_t M, int64_t N, int64_t K,
 // Scratch for the MFMA GEMM (device only): bytes needed for the given problem
 int64_t mx_gemm_workspace_bytes(int words, int64_t batch, int64_t M, int64_t N,
                                 int64_t K, int mode);
+// Size (bytes) of the last GEMM workspace allocation that failed (the -4 return of the
+// GEMM entry points), 0 if none since the last call; reading it resets it.  Held
+// workspace bytes on the calling device (every stream's grow-only scratch).
+int64_t mx_workspace_failed_bytes(void);
+int64_t mx_workspace_held_bytes(void);
 // GEMM variant using caller-provided device workspace (graph-capture friendly)
 int mx_gemm_ws(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
                const void* A1, const void* B0, const void* B1, int mode, void* C,

@@ -58,7 +58,7 @@ _OPS = {
     "OutputOperation": ("Output", ["value"], lambda o: {"tag": o.tag}),
     "SigmoidOperation": ("Sigmoid", ["x"], None),
     "ReluOperation": ("Relu", ["x"], None),
-    "SelectOperation": ("Select", ["x", "index"], lambda o: {"axis": o.axis}),
+    "SelectOperation": ("Select", ["index", "x"], lambda o: {"axis": o.axis}),
     "SoftmaxOperation": ("Softmax", ["x"], lambda o: {"axis": o.axis, "upmost_index": o.upmost_index}),
     "ReshapeOperation": ("Reshape", ["x", "shape"], None),
     "SaveOperation": ("Save", ["key", "value"], None),

@@ -65,6 +65,8 @@ _SIGS = {
         [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp],
     ),
     "mx_gemm_workspace_bytes": (c_i64, [c_int, c_i64, c_i64, c_i64, c_i64, c_int]),
+    "mx_workspace_failed_bytes": (c_i64, []),
+    "mx_workspace_held_bytes": (c_i64, []),
     "mx_mfma_peak": (c_int, [c_int, c_int, c_vp, c_vp]),
     "mx_gemm_ws": (
         c_int,
@@ -258,7 +260,34 @@ def loaded_path():
 
 def check(rc, what):
     if rc != 0:
+        if rc == -4:
+            raise NativeError(workspace_error(what, _ws_failed_bytes(), _ws_held_bytes()))
         raise NativeError(f"{what} failed with code {rc}")
+
+
+def _ws_failed_bytes() -> int:
+    try:
+        return int(lib().mx_workspace_failed_bytes())
+    except Exception:  # noqa: BLE001 - an older library: no size known
+        return 0
+
+
+def _ws_held_bytes() -> int:
+    try:
+        return int(lib().mx_workspace_held_bytes())
+    except Exception:  # noqa: BLE001
+        return 0
+
+
+def workspace_error(what: str, failed: int, held: int) -> str:
+    """Message of a GEMM whose device scratch could not be allocated (return code -4)."""
+    gib = 1 << 30
+    size = f"{failed / gib:.2f} GiB" if failed else "an unknown size"
+    return (f"{what} failed with code -4: the device workspace allocation of {size} "
+            f"({failed} bytes) failed; {held / gib:.2f} GiB of GEMM workspace already held on "
+            "this device.  The scratch is grow-only per (device, stream) -- see docs/API.md "
+            "'Device memory' for the per-stream footprint; use fewer step streams or "
+            "processes per GPU, or smaller products")
 
 
 def dev_of(t: torch.Tensor) -> int:

@@ -21,6 +21,7 @@ from __future__ import annotations
 import ctypes
 import math
 import os
+import threading
 from typing import List
 from typing import Sequence
 
@@ -39,15 +40,30 @@ _CMP = {"lt": 0, "gt": 1, "eq": 2, "msb": 3}
 
 # Every host->device copy made while a computation runs goes through to_device, so that
 # hipGraph capture (runtime/graphs.py) can substitute copies staged before the capture.
-_UPLOAD_HOOK = None
+# The hook is per thread (in-process parties record and capture on their own threads).
+_UPLOAD_HOOK = None  # process-wide fallback
+_TLS = threading.local()
+
+
+def upload_hook():
+    h = getattr(_TLS, "hook", None)
+    return h if h is not None else _UPLOAD_HOOK
+
+
+def set_upload_hook(hook):
+    """Install ``hook`` for the calling thread; returns the previous one."""
+    prev = getattr(_TLS, "hook", None)
+    _TLS.hook = hook
+    return prev
 
 
 def to_device(t: torch.Tensor, device) -> torch.Tensor:
     device = torch.device(device)
     if device.type == "cpu" or t.device == device:
         return t
-    if _UPLOAD_HOOK is not None:
-        return _UPLOAD_HOOK(t, device)
+    hook = upload_hook()
+    if hook is not None:
+        return hook(t, device)
     return t.to(device)
 
 
@@ -170,9 +186,17 @@ def zeros(shape, bits, device) -> RT:
 
 
 _SCALARS = {}
-# set while several threads issue work on their own streams of one device (the in-process
-# parties, parallel/threads.py): a cached constant is then read by other streams too
-SHARED_STREAMS = False
+# > 0 while several threads issue work on their own streams of one device (the in-process
+# parties, parallel/threads.py): a cached constant is then read by other streams too.  A
+# count, so that overlapping evaluations of several runtimes do not clear it for each other
+SHARED_STREAMS = 0
+_SHARED_LOCK = threading.Lock()
+
+
+def shared_streams(delta: int):
+    global SHARED_STREAMS
+    with _SHARED_LOCK:
+        SHARED_STREAMS = max(0, SHARED_STREAMS + delta)
 
 
 def _cache_put(cache, key, t, limit):
@@ -1029,7 +1053,8 @@ def const_ints(values, bits, device) -> RT:
     t = from_ints(np.array(list(key[0]), dtype=object), bits, device)
     if torch.device(device).type == "cpu" or not torch.cuda.is_current_stream_capturing():
         _cache_put(_CONSTS, key, t, 4096)
-        _const_key[id(t)] = key
+        if _CONSTS.get(key) is t:  # only what the cache keeps (it is bounded)
+            _const_key[id(t)] = key
     return t
 
 

@@ -46,11 +46,15 @@ class Hub:
         self.failed: Optional[str] = None
         self.timeout = timeout
         self.lock = threading.Lock()
+        self.done = [False] * n  # party i's thread has returned (successfully or not)
 
     def fail(self, why: str):
         with self.lock:
             if self.failed is None:
                 self.failed = why
+
+    def finish(self, rank: int):
+        self.done[rank] = True
 
 
 class ThreadTransport:
@@ -114,6 +118,12 @@ class ThreadTransport:
                 if self.hub.failed is not None:
                     raise TransportError(f"rank {self.rank}: no message from rank {src}: "
                                          f"session failed ({self.hub.failed})") from None
+                if self.hub.done[src] and box.empty():
+                    # the sender returned without sending what this party expects (a
+                    # protocol desynchronisation): it never will
+                    why = f"rank {src} finished without sending to rank {self.rank}"
+                    self.hub.fail(why)
+                    raise TransportError(f"rank {self.rank}: {why}") from None
                 if self.hub.timeout is not None and waited >= self.hub.timeout:
                     self.hub.fail(f"rank {self.rank} timed out waiting for rank {src}")
                     raise TransportError(f"rank {self.rank}: no message from rank {src} "
@@ -240,16 +250,9 @@ class ThreadTransport:
         return None
 
 
-class _ThreadUploads:
-    """The ring module's upload hook while the party threads run a warm-up: each thread's
-    host->device copies go to that thread's recorder (runtime/graphs._Recorder)."""
-
-    def __init__(self):
-        self.by_thread = {}
-
-    def __call__(self, t, device):
-        rec = self.by_thread.get(threading.get_ident())
-        return rec(t, device) if rec is not None else t.to(device)
+# a party that waits this long for a message ends the evaluation (device_map runtimes
+# without an explicit timeout); a desynchronised peer that returned is detected at once
+DEFAULT_TIMEOUT_S = float(os.environ.get("MOOSEX_PARTY_TIMEOUT", "300"))
 
 
 def run_parties(comp, arguments: dict, identities: List[str], devices: List, storage: dict,
@@ -267,18 +270,19 @@ def run_parties(comp, arguments: dict, identities: List[str], devices: List, sto
     from moose_amd.runtime import graphs as G
     from moose_amd.runtime.interpreter import Interpreter
 
-    hub = Hub(devices, timeout=timeout)
+    hub = Hub(devices, timeout=DEFAULT_TIMEOUT_S if timeout is None else timeout)
     role_ranks = {r: i for i, r in enumerate(identities)}
     results, stats, elapsed, errors, warm = {}, {}, {}, {}, {}
     lowered = is_lowered(comp)
-    hooks = _ThreadUploads() if record else None
 
     def party(i):
         ident, dev = identities[i], hub.devices[i]
         tr = ThreadTransport(i, hub)
+        rec = None
         try:
-            if hooks is not None:
-                hooks.by_thread[threading.get_ident()] = rec = G._Recorder()
+            if record:  # this thread's host->device copies go to its recorder
+                rec = G._Recorder()
+                R.set_upload_hook(rec)
             if dev.type == "cuda":
                 torch.cuda.set_device(dev)
                 stream = torch.cuda.Stream(dev)
@@ -305,7 +309,7 @@ def run_parties(comp, arguments: dict, identities: List[str], devices: List, sto
                     out = {tag: interp.to_numpy(lv) for tag, lv in outs.items()
                            if lv.kind != "unit" and sess.materialized(lv.v)}
                     st = sess.stats
-                    if hooks is not None:
+                    if rec is not None:
                         warm[ident] = {"uploads": rec.items, "first": out, "stats": st,
                                        "keys_n": sess.keytable.n, "log": tr.log}
             if dev.type == "cuda":
@@ -315,20 +319,26 @@ def run_parties(comp, arguments: dict, identities: List[str], devices: List, sto
         except BaseException as e:  # noqa: BLE001 - reported after every party stopped
             errors[ident] = e
             hub.fail(f"{ident}: {type(e).__name__}: {e}")
+        finally:
+            if rec is not None:
+                R.set_upload_hook(None)
+            hub.finish(i)
 
     threads = [threading.Thread(target=party, args=(i,), name=f"moose-party-{identities[i]}",
                                 daemon=True) for i in range(len(identities))]
-    prev, prev_shared = R._UPLOAD_HOOK, R.SHARED_STREAMS
-    if hooks is not None:
-        R._UPLOAD_HOOK = hooks
-    R.SHARED_STREAMS = True  # shared device constants: their producer drains first
+    R.shared_streams(+1)  # shared device constants: their producer drains first
     try:
         for t in threads:
             t.start()
         for t in threads:
-            t.join()
+            # every blocked receive gives up within the hub's timeout (or at once when its
+            # sender has returned), so the joins end; the bound is a last resort
+            t.join(hub.timeout + 60.0)
+            if t.is_alive():
+                hub.fail(f"{t.name} did not finish")
+                raise TransportError(f"{t.name} did not finish within {hub.timeout + 60.0} s")
     finally:
-        R._UPLOAD_HOOK, R.SHARED_STREAMS = prev, prev_shared
+        R.shared_streams(-1)
     if errors:
         # the first party to fail is the cause; the others saw TransportError because of it
         first = next((e for e in errors.values() if not isinstance(e, TransportError)),

@@ -34,8 +34,13 @@ from moose_amd.runtime.prims import PRIMS
 _NEEDS_BITS = {"Fill", "AddConst", "SampleSeeded", "Sample", "RingFixedpointEncode",
                "RingInject", "RingCast"}
 _NEEDS_DEVICE = {"Fill", "SampleSeeded", "Sample", "Zeros", "Ones"}
+# torch dtype of each plaintext host tensor type: unsigned types wider than 8 bits travel in
+# a signed dtype (u16 -> i32 and u32 -> i64 widened, exact; u64 as its 64-bit pattern)
 _TY_DTYPE = {"HostFloat64Tensor": torch.float64, "HostFloat32Tensor": torch.float32,
              "HostUint64Tensor": torch.int64, "HostInt64Tensor": torch.int64,
+             "HostInt32Tensor": torch.int32, "HostInt16Tensor": torch.int16,
+             "HostInt8Tensor": torch.int8, "HostUint8Tensor": torch.uint8,
+             "HostUint16Tensor": torch.int32, "HostUint32Tensor": torch.int64,
              "HostBitTensor": torch.bool, "HostBoolTensor": torch.bool}
 
 
@@ -51,12 +56,10 @@ def constant_value(c: Constant, device):
         return R.from_ints(np.asarray(v, dtype=object), 128, device)
     if k == "HostBitTensor":
         return R.RT(torch.as_tensor(np.asarray(v, dtype=np.uint8), device=device), 1)
-    if k in ("HostFloat64Tensor", "HostFloat32Tensor", "HostInt64Tensor", "HostUint8Tensor",
-             "HostInt32Tensor", "HostUint64Tensor"):
-        a = np.asarray(v)
-        if a.dtype == np.uint64:
-            a = a.view(np.int64)
-        return torch.as_tensor(a, device=device)
+    if k in _TY_DTYPE and k not in ("HostBitTensor", "HostBoolTensor"):
+        from moose_amd.runtime.interpreter import numpy_to_torch
+
+        return numpy_to_torch(np.asarray(v), device).to(_TY_DTYPE[k])
     if k == "HostShape":
         return tuple(int(d) for d in v)
     if k in ("HostString", "HostSeed", "HostPrfKey"):
@@ -152,6 +155,8 @@ class GraphExecutor:
             return constant_value(op.attrs["value"], self.device)
         if kind == "Input":
             name = attrs["arg_name"]
+            if op.sig.ret.name == "HostUnit":
+                return None
             if name not in arguments:
                 raise GraphExecutionError(f"missing argument {name}")
             a = arguments[name]
@@ -195,6 +200,10 @@ def run_host_prim(op, vals, attrs, device):
     prim = PRIMS.get(kind)
     if prim is None:
         raise GraphExecutionError(f"no host kernel for {kind}")
+    if kind == "Select":  # IR operands (index, x); the primitive takes (x, index)
+        vals = [vals[1], vals[0]]
+    elif kind == "Broadcast" and len(vals) == 2 and isinstance(vals[0], tuple):
+        vals = [vals[1], vals[0]]  # IR (shape, x) as the reference's (kernels/mod.rs:230)
     return prim.impl(0, *vals, **prim_attrs(op, attrs, device))
 
 
@@ -209,8 +218,12 @@ def prim_attrs(op, attrs, device):
         attrs["bits"] = bits
     if kind in _NEEDS_DEVICE:
         attrs["device"] = device
-    if kind in ("Cast", "Zeros", "Ones"):
+    if kind in ("Cast", "Zeros", "Ones", "RingFixedpointDecode"):
         attrs["dtype"] = _TY_DTYPE.get(op.sig.ret.name, torch.float64)
+    if kind == "Cast":
+        attrs["ty"] = op.sig.ret.name
+    if kind in ("Reshape", "Broadcast") and len(op.inputs) == 2:
+        attrs.pop("shape", None)  # the shape is the operand
     if kind == "BitDecompose":
         attrs["to_bits"] = bits == 1
     params = _params(prim.impl)

@@ -78,11 +78,10 @@ class _Stager:
 def _upload_hook(hook):
     class _Ctx:
         def __enter__(self):
-            self.prev = R._UPLOAD_HOOK
-            R._UPLOAD_HOOK = hook
+            self.prev = R.set_upload_hook(hook)
 
         def __exit__(self, *exc):
-            R._UPLOAD_HOOK = self.prev
+            R.set_upload_hook(self.prev)
 
     return _Ctx()
 

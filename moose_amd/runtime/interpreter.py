@@ -101,6 +101,8 @@ def numpy_to_torch(a, device):
         return R.to_device(torch.from_numpy(a.view(np.int64).copy()), device)
     if a.dtype == np.uint32:
         a = a.astype(np.int64)
+    elif a.dtype == np.uint16:
+        a = a.astype(np.int32)
     if a.dtype == object:
         raise MooseRuntimeError("object arrays are not tensors")
     return R.to_device(torch.from_numpy(np.ascontiguousarray(a)), device)
@@ -1207,9 +1209,11 @@ class Interpreter:
         return self._shape_op(op, x, "StridedSlice", slices=py)
 
     def op_Select(self, op, ins):
-        mask = self.to_host(ins[1], self._some_host(op)) if not ins[1].is_host else ins[1]
+        # operands (index, x), as the reference's SelectOp (kernels/indexing.rs:60)
+        idx, x = ins[0], ins[1]
+        mask = self.to_host(idx, self._some_host(op)) if not idx.is_host else idx
         m = self._plain(mask)
-        return self._shape_op(op, ins[0], "Select", m, axis=op.attrs["axis"])
+        return self._shape_op(op, x, "Select", m, axis=op.attrs["axis"])
 
     def _some_host(self, op):
         plc = op.placement

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import os
 import time
+import weakref
 from typing import Dict
 from typing import List
 from typing import Optional
@@ -98,7 +99,9 @@ class LocalMooseRuntime:
             env = os.environ.get("MOOSEX_GRAPHS", "auto")
             use_graphs = {"1": True, "0": False}.get(env, "auto")
         self.use_graphs = use_graphs
-        self._seen = {}  # auto mode: (id(comp), signature) -> (comp, last eager seconds)
+        # auto mode: (id(comp), signature) -> (weak reference to comp, last eager seconds);
+        # weak, so the cache does not keep the user's computations alive
+        self._seen = {}
         # HIP streams for independent operations (runtime/lanes.py); MOOSEX_LANES=n
         self.lanes = lanes
         from moose_amd.runtime.graphs import GraphCache
@@ -172,7 +175,7 @@ class LocalMooseRuntime:
 
             akey = (id(comp), signature(arguments))
             seen = self._seen.get(akey)
-            graphs = (seen is not None and seen[0] is comp and seen[1] < AUTO_GRAPH_MS / 1e3)
+            graphs = (seen is not None and seen[0]() is comp and seen[1] < AUTO_GRAPH_MS / 1e3)
         if graphs:
             t0 = time.perf_counter()
             r = self._graphs.evaluate(comp, arguments, self.device, self.storage,
@@ -200,7 +203,7 @@ class LocalMooseRuntime:
         if akey is not None:
             if len(self._seen) >= 256:
                 self._seen.pop(next(iter(self._seen)))
-            self._seen[akey] = (comp, dt)
+            self._seen[akey] = (weakref.ref(comp), dt)
         elapsed = int(dt * 1e6)
         self.last_timings = {i: elapsed for i in self.identities}
         self.last_stats = sess.stats
@@ -237,7 +240,7 @@ class LocalMooseRuntime:
                     result.update(outs[i])
                 return result
         seen = self._seen.get(key) if key is not None else None
-        record = (tapeable and seen is not None and seen[0] is comp
+        record = (tapeable and seen is not None and seen[0]() is comp
                   and (self.use_graphs is True or seen[1] < PARTIES_AUTO_GRAPH_MS / 1e3)
                   and key not in self._party_tapes)
         t0 = time.perf_counter()
@@ -250,7 +253,7 @@ class LocalMooseRuntime:
         if key is not None:
             if len(self._seen) >= 256:
                 self._seen.pop(next(iter(self._seen)))
-            self._seen[key] = (comp, dt)
+            self._seen[key] = (weakref.ref(comp), dt)
         if record and warm is not None:
             try:
                 tapes = T.PartyTapes(comp, arguments, self.identities, devices, self.storage,

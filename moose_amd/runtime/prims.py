@@ -107,9 +107,25 @@ def _neg(nb, a):
 
 @prim("Div")
 def _div(nb, a, b):
+    if _is_rt(a):
+        return _ring_div(a, b)
     if a.dtype in (torch.float32, torch.float64):
         return a / b
     return torch.div(a, b, rounding_mode="trunc")
+
+
+def _ring_div(a, b):
+    """Unsigned integer division of ring tensors (``Wrapping<u64> / Wrapping<u128>``,
+    reference host/ops.rs:334-343).  A host-only kernel on python integers: no protocol
+    divides ring values, so it is never on a hot path."""
+    import numpy as np
+
+    x, y = R.to_ints(a), R.to_ints(b)
+    x, y = np.broadcast_arrays(x, y)
+    if any(int(v) == 0 for v in y.reshape(-1)):
+        raise ZeroDivisionError("ring division by zero")
+    q = np.vectorize(lambda u, v: int(u) // int(v), otypes=[object])(x, y)
+    return R.from_ints(q, a.bits, a.device)
 
 
 @prim("Shl")
@@ -167,6 +183,50 @@ def _mean(nb, a, axis=None):
     return a.mean(dim=_lax(a.dim(), axis, nb))
 
 
+@prim("RingFixedpointMean")
+def _ring_fixedpoint_mean(nb, a, axis=None, scaling_base=2, scaling_exp=0):
+    """Sum along ``axis`` (all entries when None) times the mean weight 1/n encoded with
+    scaling_base^scaling_exp -- the float product truncated toward zero, as the
+    reference's encode (host/fixedpoint.rs:66-76, 10-38).  No truncation of the product:
+    the result carries twice the fractional bits, as the reference's."""
+    shape = a.shape[nb:]
+    n = shape[axis] if axis is not None else math.prod(shape)
+    w = int((1.0 / n) * float(int(scaling_base) ** int(scaling_exp)))
+    s = R.sum(a, axis, nb)
+    return R.binary("mul", s, R.fill((), w % (1 << a.bits), a.bits, a.device))
+
+
+@prim("RingFixedpointArgmax", ty=lambda tys, **a: T.Ty("HostRing64Tensor"))
+def _ring_fixedpoint_argmax(nb, a, axis, upmost_index=None):
+    """Index of the first maximum along ``axis``, entries read as signed ring values; a
+    Z_2^64 tensor of indices (reference host/ops.rs:2374-2445)."""
+    ax = _lax(a.ndim, axis, nb)
+    d = a.data
+    n = d.shape[ax]
+    hi = d.select(ax, 0)
+    lo = None
+    if a.bits == 128:  # (lo, hi) words: signed high word, unsigned low word
+        lo = hi[..., 0] ^ _SIGN64
+        hi = hi[..., 1]
+    best_hi, best_lo = hi.clone(), None if lo is None else lo.clone()
+    idx = torch.zeros(best_hi.shape, dtype=torch.int64, device=d.device)
+    for i in range(1, n):
+        v = d.select(ax, i)
+        if a.bits == 128:
+            vl, vh = v[..., 0] ^ _SIGN64, v[..., 1]
+            gt = (vh > best_hi) | ((vh == best_hi) & (vl > best_lo))
+            best_lo = torch.where(gt, vl, best_lo)
+        else:
+            vh = v
+            gt = vh > best_hi
+        best_hi = torch.where(gt, vh, best_hi)
+        idx = torch.where(gt, torch.full_like(idx, i), idx)
+    return R.RT(idx.contiguous(), 64)
+
+
+_SIGN64 = -(1 << 63)
+
+
 # ---------------------------------------------------------------------------
 # shapes
 # ---------------------------------------------------------------------------
@@ -178,7 +238,7 @@ def _shape(nb, a):
 
 
 @prim("Reshape")
-def _reshape(nb, a, shape):
+def _reshape(nb, a, shape=None):
     if _is_rt(a):
         return R.reshape(a, shape, nb)
     return a.reshape(tuple(a.shape[:nb]) + tuple(shape))
@@ -262,6 +322,7 @@ def _strided_slice(nb, a, slices):
 
 @prim("Select")
 def _select(nb, a, mask, axis):
+    # session primitive order (x, index); the IR op is (index, x) (graph_executor swaps)
     m = mask.data if _is_rt(mask) else mask
     if _is_rt(a):
         return R.select_mask(a, axis, m, nb)
@@ -277,7 +338,7 @@ def _diag(nb, a):
 
 
 @prim("Broadcast")
-def _broadcast(nb, a, shape):
+def _broadcast(nb, a, shape=None):
     if _is_rt(a):
         return R.broadcast_to(a, shape, nb)
     lead = len(shape) - (a.dim() - nb)
@@ -365,12 +426,12 @@ def _sample(nb, shape, bits, device="cpu"):
 
 
 @prim("Zeros")
-def _zeros(nb, shape, dtype, device):
+def _zeros(nb, shape, dtype=torch.float64, device="cpu"):
     return torch.zeros(tuple(shape), dtype=dtype, device=device)
 
 
 @prim("Ones")
-def _ones(nb, shape, dtype, device):
+def _ones(nb, shape, dtype=torch.float64, device="cpu"):
     return torch.ones(tuple(shape), dtype=dtype, device=device)
 
 
@@ -384,8 +445,9 @@ def _encode(nb, x, scaling_exp, bits):
 
 
 @prim("RingFixedpointDecode")
-def _decode(nb, x, scaling_exp):
-    return R.decode(x, scaling_exp)
+def _decode(nb, x, scaling_exp, dtype=None):
+    out = R.decode(x, scaling_exp)
+    return out if dtype is None or out.dtype == dtype else out.to(dtype)
 
 
 @prim("BitExtract")
@@ -499,6 +561,8 @@ def _msb(nb, a):
 
 @prim("Mux")
 def _mux(nb, s, x, y):
+    if _is_rt(s) and not _is_rt(x):  # a bit selector over plaintext operands
+        s = s.data
     if _is_rt(x):
         sel = s if _is_rt(s) else R.RT(s.to(torch.uint8), 1)
         m = R.ring_inject(sel, 0, x.bits) if sel.bits == 1 else sel
@@ -523,7 +587,19 @@ prim("Sqrt")(_f(torch.sqrt))
 prim("Sigmoid")(_f(torch.sigmoid))
 prim("Relu")(_f(torch.relu))
 prim("Abs")(_f(torch.abs))
-prim("Sign")(_f(torch.sign))
+@prim("Sign")
+def _sign(nb, a):
+    """Plaintext: torch.sign.  Ring: -1 for negative (two's complement) entries, +1
+    otherwise -- zero included (reference host/ops.rs:1420-1452)."""
+    if not _is_rt(a):
+        return torch.sign(a)
+    d = a.data if a.bits == 64 else a.data[..., 1]
+    neg = d < 0
+    if a.bits == 64:
+        return R.RT(torch.where(neg, -1, 1).to(torch.int64), 64)
+    lo = torch.where(neg, -1, 1).to(torch.int64)
+    hi = torch.where(neg, -1, 0).to(torch.int64)
+    return R.RT(torch.stack([lo, hi], dim=-1), 128)
 prim("Inverse")(_f(torch.linalg.inv))
 
 
@@ -541,14 +617,45 @@ def _argmax(nb, a, axis, upmost_index):
 
 @prim("Maximum")
 def _maximum(nb, *xs):
+    if _is_rt(xs[0]):
+        return _ring_maximum(xs)
     acc = xs[0]
     for x in xs[1:]:
         acc = torch.maximum(acc, x)
     return acc
 
 
+def _ring_maximum(xs):
+    """Elementwise maximum of ring tensors compared as UNSIGNED integers -- the reference's
+    ring Maximum compares ``Wrapping<u64>`` / ``Wrapping<u128>`` (host/ops.rs:2475-2497)."""
+    bits = xs[0].bits
+    acc = xs[0].data
+    for x in xs[1:]:
+        d = x.data
+        if bits == 128:
+            ah, bh = acc[..., 1] ^ _SIGN64, d[..., 1] ^ _SIGN64
+            al, bl = acc[..., 0] ^ _SIGN64, d[..., 0] ^ _SIGN64
+            gt = (bh > ah) | ((bh == ah) & (bl > al))
+            acc = torch.where(gt.unsqueeze(-1), d, acc)
+        elif bits == 64:
+            acc = torch.where((d ^ _SIGN64) > (acc ^ _SIGN64), d, acc)
+        else:
+            acc = torch.maximum(acc, d)
+    return R.RT(acc.contiguous(), bits)
+
+
 @prim("Cast")
-def _cast(nb, x, dtype):
+def _cast(nb, x, dtype=torch.float64, ty=None):
+    """Host casts (reference kernels/conversion.rs:26-48).  ``ty`` is the result type name
+    when known (a lowered graph): rings and bits need it."""
+    if ty == "HostBitTensor":  # x != 0 (host/ops.rs:2334-2371)
+        d = x.data if _is_rt(x) else x
+        return R.RT((d != 0).to(torch.uint8), 1)
+    if ty in ("HostRing64Tensor", "HostRing128Tensor"):
+        bits = 64 if ty == "HostRing64Tensor" else 128
+        return x if x.bits == bits else R.cast(x, bits)
+    if _is_rt(x):  # bit -> float / u64 (0 / 1); Z_2^64 -> u64 (the same 64 bits)
+        return x.data.to(dtype)
     return x.to(dtype)
 
 

@@ -112,3 +112,19 @@ def test_error_model_variants():
     assert issubclass(TransportError, errors.Networking)
     assert issubclass(GraphExecutionError, errors.KernelError)
     assert issubclass(MooseRuntimeError, errors.KernelError)
+
+
+def test_gemm_workspace_failure_names_the_size(monkeypatch):
+    """a GEMM whose device workspace cannot be allocated (code -4)
+    raises an error that names the size it tried and what is already held."""
+    import pytest
+
+    from moose_amd.ops import native
+
+    monkeypatch.setattr(native, "_ws_failed_bytes", lambda: 8 << 30)
+    monkeypatch.setattr(native, "_ws_held_bytes", lambda: 24 << 30)
+    with pytest.raises(native.NativeError) as e:
+        native.check(-4, "ring gemm")
+    msg = str(e.value)
+    assert "8.00 GiB" in msg and "8589934592 bytes" in msg and "24.00 GiB" in msg
+    assert "docs/API.md" in msg

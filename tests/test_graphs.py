@@ -150,3 +150,24 @@ def test_small_constants_uploaded_and_encoded_once():
         assert (len(I._CONST_LV), len(R._ENCODED_CONSTS)) == n
         for o in outs:
             assert np.abs(np.asarray(o) - tm.proba).max() < 1e-4
+
+
+@pytest.mark.gpu
+def test_seeded_auto_replays_match_seeded_eager_bitwise():
+    """a seeded runtime in the default auto mode replays from its third
+    evaluation; every replay must equal a seeded eager evaluation bitwise (the replay
+    re-draws the seeded keys exactly as a fresh seeded session's setup would)."""
+    from moose_amd.models.predictors.tutorial import logistic_regression_tutorial
+
+    tm = logistic_regression_tutorial(128)
+    args = {"x": tm.x_test}
+    eager = pm.LocalMooseRuntime(["alice", "bob", "carole"], device="cuda", seed=11,
+                                 use_graphs=False)
+    want = np.asarray(list(eager.evaluate_computation(tm.computation, args).values())[0])
+    auto = pm.LocalMooseRuntime(["alice", "bob", "carole"], device="cuda", seed=11)
+    assert auto.use_graphs == "auto"
+    for i in range(5):
+        got = np.asarray(list(auto.evaluate_computation(tm.computation, args).values())[0])
+        assert np.array_equal(got, want), (i, np.abs(got - want).max())
+    plan = next(iter(auto._graphs.plans.values()))
+    assert plan.replays >= 3

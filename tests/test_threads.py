@@ -90,6 +90,28 @@ def test_thread_party_failure_raises_instead_of_hanging():
     np.testing.assert_allclose(out, [2.25, 4.0], atol=1e-5)
 
 
+def test_receive_from_a_finished_party_raises_at_once():
+    """a party that returns without sending what its peer expects (a protocol
+    desynchronisation) must not leave the peer polling forever -- with no timeout set the
+    receive raises as soon as the sender's thread has finished and its mailbox is empty."""
+    import time
+
+    from moose_amd.parallel.threads import Hub
+    from moose_amd.parallel.threads import ThreadTransport
+    from moose_amd.parallel.transport import TransportError
+
+    hub = Hub(["cpu", "cpu"], timeout=None)
+    a, b = ThreadTransport(0, hub), ThreadTransport(1, hub)
+    b.send(torch.arange(3), 0)  # one message, then party 1 returns
+    hub.finish(1)
+    assert torch.equal(a.recv(1), torch.arange(3))  # what was sent still arrives
+    t0 = time.perf_counter()
+    with pytest.raises(TransportError, match="finished without sending"):
+        a.recv(1)
+    assert time.perf_counter() - t0 < 5
+    assert hub.failed is not None
+
+
 def test_device_map_rejects_unknown_identity():
     with pytest.raises(ValueError):
         LocalMooseRuntime(IDS, device_map={"mallory": "cpu"})
