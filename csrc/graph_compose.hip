@@ -17,8 +17,13 @@
 
 extern "C" {
 
+void* mx_copy_many_fn(void);                                      // party_graph.hip
+int mx_copy_many_grid(int n, int64_t max_bytes, int* gx, int* gy);  // party_graph.hip
+
 // n nodes in a topological order.  kind[i] = 0: a child graph (child[i], a hipGraph_t);
-// kind[i] = 1: a device-to-device copy of bytes[i] from src[i] to dst[i].  The
+// kind[i] = 1: a device-to-device copy of bytes[i] from src[i] to dst[i]; kind[i] = 2: ONE
+// kernel copying several messages (party_graph.hip k_copy_many): dst[i] = its descriptor
+// table in device memory, child[i] = the number of entries, bytes[i] = the largest.  The
 // dependencies of node i are deps[dep_off[i] .. dep_off[i + 1]) (indices < i).
 // Returns 0 and the graph / its executable, or a negative code (nothing is leaked).
 int mx_graph_compose(int n, const int* kind, void* const* child, void* const* dst,
@@ -47,7 +52,22 @@ int mx_graph_compose(int n, const int* kind, void* const* child, void* const* ds
     else if (kind[i] == 0)
       rc = hipGraphAddChildGraphNode(&nodes[(size_t)i], g, d.data(), d.size(),
                                      (hipGraph_t)child[i]);
-    else
+    else if (kind[i] == 2) {
+      const int cnt = (int)(intptr_t)child[i];
+      int gx = 1, gy = 1;
+      mx_copy_many_grid(cnt, bytes[i], &gx, &gy);
+      void* desc = dst[i];
+      int count = cnt;
+      void* args[] = {&desc, &count};
+      hipKernelNodeParams kp = {};
+      kp.func = mx_copy_many_fn();
+      kp.gridDim = dim3(gx, gy, 1);
+      kp.blockDim = dim3(256, 1, 1);
+      kp.sharedMemBytes = 0;
+      kp.kernelParams = args;
+      kp.extra = nullptr;
+      rc = hipGraphAddKernelNode(&nodes[(size_t)i], g, d.data(), d.size(), &kp);
+    } else
       rc = hipGraphAddMemcpyNode1D(&nodes[(size_t)i], g, d.data(), d.size(), dst[i], src[i],
                                    (size_t)bytes[i], hipMemcpyDeviceToDevice);
     if (rc != hipSuccess) {

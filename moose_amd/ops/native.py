@@ -219,6 +219,9 @@ _SIGS = {
     "mx_stream_destroy": (c_int, [c_vp]),
     "mx_graph_compose": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mx_graph_launch": (c_int, [c_vp, c_vp]),
+    "mx_key_refresh": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp]),
+    "mx_key_refresh_host": (None, [c_vp, c_u64, c_int, c_vp]),
+    "mx_copy_many": (c_int, [c_vp, c_int, c_i64, c_vp]),
     "mx_graph_free": (c_int, [c_vp, c_vp]),
     "mx_gemm_roll": (
         c_int,

@@ -149,6 +149,9 @@ class SPMDTape:
         self.segments = len(self.steps) - self.rounds
         self.replays = 0
         self.issue_s = []  # host time per replay spent issuing (graphs + message calls)
+        if seed is None:  # unseeded replays draw their keys on the device (keys.py)
+            self.keys.enable_device_refresh()
+        self._pinned = {}  # argument name -> pinned host staging buffer
 
     # ------------------------------------------------------------------------------
     def _decode(self, interp, sess, outs) -> Dict[str, np.ndarray]:
@@ -164,7 +167,7 @@ class SPMDTape:
         overwrite the peers' slots with their keys.  Seeded: the draws a fresh seeded
         session makes in its setups (SPMDSession.setup), in the same order."""
         if self.seed is None:
-            self.keys.refresh(self.keys.n)
+            self.keys.refresh_device(self.keys.n)
             return
         rng = torch.Generator().manual_seed(self.seed)
         draw = lambda: bytes(torch.randint(0, 256, (16,), generator=rng,  # noqa: E731
@@ -176,15 +179,32 @@ class SPMDTape:
             allk[(idx + 2) % 3] = bytes(16)
             self.keys._write(base, allk)
 
+    def copy_arguments(self, arguments: dict):
+        """The new arguments into the static buffers, on the current stream: through a
+        pinned staging buffer per argument (an asynchronous DMA; a pageable copy would hold
+        the host until it ran).  The previous replay has completed (its outputs were
+        decoded), so the staging buffer is free."""
+        for k, v in arguments.items():
+            t = self.static.get(k)
+            if not isinstance(t, torch.Tensor):
+                continue
+            a = np.asarray(v)
+            a = a.view(np.int64) if a.dtype == np.uint64 else a
+            src = torch.from_numpy(np.ascontiguousarray(a).reshape(t.shape))
+            if src.dtype != t.dtype:
+                src = src.to(t.dtype)
+            if t.device.type != "cuda":
+                t.copy_(src)
+                continue
+            pin = self._pinned.get(k)
+            if pin is None or pin.shape != t.shape or pin.dtype != t.dtype:
+                pin = self._pinned[k] = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            pin.copy_(src)
+            t.copy_(pin, non_blocking=True)
+
     def replay(self, arguments: dict) -> Dict[str, np.ndarray]:
         with torch.cuda.stream(self.stream):
-            for k, v in arguments.items():
-                t = self.static.get(k)
-                if isinstance(t, torch.Tensor):
-                    a = np.asarray(v)
-                    a = a.view(np.int64) if a.dtype == np.uint64 else a
-                    src = torch.from_numpy(np.ascontiguousarray(a).reshape(t.shape))
-                    t.copy_(src if src.dtype == t.dtype else src.to(t.dtype))
+            self.copy_arguments(arguments)
             self._fill_keys()
             issue = 0.0
             tr = self.tr

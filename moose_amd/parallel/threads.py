@@ -392,70 +392,134 @@ class PartyTapes:
         self._composed = self._compose() if single else None
 
     def _compose(self):
-        """The schedule as ONE hipGraph (csrc/graph_compose.hip): each segment a child
-        graph, each message a device-to-device memcpy node, in the issue order of the
-        per-action replay (MOOSEX_PARTY_GRAPH_DAG=1: only program-order and send -> receive
-        edges).  None when the runtime declines (the per-action replay is used)."""
+        """The schedule as ONE hipGraph (csrc/graph_compose.hip) in a total order: each
+        segment a child graph; the messages of one round of all parties ONE batched copy
+        kernel (csrc/party_graph.hip k_copy_many; ``MOOSEX_PARTY_COPY_BATCH=0``: a copy node
+        per message).  None when the runtime declines (the per-action replay is used)."""
         import ctypes
 
         from moose_amd.ops import native as nat
 
-        n = len(self.tapes)
-        kinds, child, dst, src, nbytes, deps = [], [], [], [], [], []
-        last = [None] * n
-        sent_at = {}
-        # copies still reading a party's send buffers: that party's next segment waits for
-        # them (its graph pool may reuse a sent tensor's memory once the send is issued --
-        # write-after-read edges the send -> receive order alone does not give)
-        reading = [[] for _ in range(n)]
-        for a in self.actions:
-            p = a[1]
+        batched = os.environ.get("MOOSEX_PARTY_COPY_BATCH", "1") != "0"
+        acts = self._schedule_rounds() if batched else [
+            a if a[0] != "cp" else ("cpb", [(a[1], a[2], a[3], a[4])])
+            for a in self.actions if a[0] != "rec"]
+        kinds, child, dst, src, nbytes = [], [], [], [], []
+        descs = []
+        for a in acts:
             if a[0] == "g":
                 kinds.append(0)
                 child.append(a[2].raw_cuda_graph())
                 dst.append(0)
                 src.append(0)
                 nbytes.append(0)
-                deps.append(sorted(set(([last[p]] if last[p] is not None else []) + reading[p])))
-                reading[p] = []
-                last[p] = len(kinds) - 1
-            elif a[0] == "rec":
-                sent_at[id(a[2])] = (last[p], p)
-            else:
-                _, p, s, t, buf, ev = a
-                at, sender = sent_at.get(id(ev), (None, None))
-                d = [x for x in (last[p], at) if x is not None]
-                kinds.append(1)
-                child.append(0)
-                dst.append(buf.data_ptr())
-                src.append(t.data_ptr())
-                nbytes.append(t.numel() * t.element_size())
-                deps.append(sorted(set(d)))
-                last[p] = len(kinds) - 1
-                if sender is not None and sender != p:
-                    reading[sender].append(last[p])
+                continue
+            msgs = a[1]
+            if len(msgs) == 1 or not batched:
+                for _p, _s, t, buf in msgs:
+                    kinds.append(1)
+                    child.append(0)
+                    dst.append(buf.data_ptr())
+                    src.append(t.data_ptr())
+                    nbytes.append(t.numel() * t.element_size())
+                continue
+            descs.append([(t.data_ptr(), buf.data_ptr(), t.numel() * t.element_size())
+                          for _p, _s, t, buf in msgs])
+            kinds.append(2)
+            child.append(len(msgs))
+            dst.append(len(descs) - 1)  # the table's address is filled in below
+            src.append(0)
+            nbytes.append(max(b for _, _, b in descs[-1]))
+        if descs:
+            flat = [v for d in descs for e in d for v in e]
+            table = torch.tensor([x - (1 << 64) if x >= (1 << 63) else x for x in flat],
+                                 dtype=torch.int64, device=self.devices[0])
+            self._copy_table = table  # alive as long as the graph
+            offs, at = [], 0
+            for d in descs:
+                offs.append(table.data_ptr() + 8 * 3 * at)
+                at += len(d)
+            dst = [offs[d] if k == 2 else d for k, d in zip(kinds, dst)]
         m = len(kinds)
-        if os.environ.get("MOOSEX_PARTY_GRAPH_DAG") != "1":
-            # the issue order as a total order (profiles/r4_party_graph.md: on one device
-            # the branchy DAG ran slower -- 5.0 vs 3.2 ms per LR inference -- and its
-            # replays did not reproduce the eager values, so it stays a debugging option)
-            deps = [sorted(set(d) | ({i - 1} if i else set())) for i, d in enumerate(deps)]
+        deps = [[i - 1] if i else [] for i in range(m)]  # the total order
         off = [0]
-        flat = []
+        flat_deps = []
         for d in deps:
-            flat += d
-            off.append(len(flat))
+            flat_deps += d
+            off.append(len(flat_deps))
         arr = lambda ty, xs: (ty * max(1, len(xs)))(*xs)  # noqa: E731
         g, ex = ctypes.c_void_p(), ctypes.c_void_p()
         rc = nat.lib().mx_graph_compose(
             m, arr(ctypes.c_int, kinds), arr(ctypes.c_void_p, child),
             arr(ctypes.c_void_p, dst), arr(ctypes.c_void_p, src),
-            arr(ctypes.c_int64, nbytes), arr(ctypes.c_int, off), arr(ctypes.c_int, flat),
+            arr(ctypes.c_int64, nbytes), arr(ctypes.c_int, off), arr(ctypes.c_int, flat_deps),
             ctypes.byref(g), ctypes.byref(ex))
         if rc != 0:
             return None
         self._graph_handles = (g, ex)
+        self.graph_nodes = {"segments": kinds.count(0), "copy_nodes": kinds.count(1),
+                            "copy_batches": kinds.count(2)}
         return ex
+
+    def _schedule_rounds(self):
+        """The tapes as a round-synchronous total order: every party runs its segments up to
+        its next round, then the messages of all parties whose round can complete (every
+        sender has reached it) are copied together -- one batch per round instead of one
+        copy per message (the composed one-GPU replay).  Returns ("g", party, graph) and
+        ("cpb", [(receiver, sender, payload, landing buffer)]) actions."""
+        from moose_amd.parallel.transport import CommStep
+        from moose_amd.runtime.graphs import CaptureError
+
+        n = len(self.tapes)
+        steps = [t.steps for t in self.tapes]
+        ptr, sent_done = [0] * n, [False] * n
+        sent, recvd, pending = {}, {}, {}
+        acts = []
+        while any(ptr[p] < len(steps[p]) for p in range(n)):
+            progress = False
+            for p in range(n):  # every party up to its next round; its sends go out
+                while ptr[p] < len(steps[p]) and not isinstance(steps[p][ptr[p]], CommStep):
+                    acts.append(("g", p, steps[p][ptr[p]]))
+                    ptr[p] += 1
+                    progress = True
+                if ptr[p] < len(steps[p]) and not sent_done[p]:
+                    for t, dst in steps[p][ptr[p]].sends:
+                        k = sent.get((p, dst), 0)
+                        sent[(p, dst)] = k + 1
+                        pending[(p, dst, k)] = t
+                    sent_done[p] = True
+                    progress = True
+            batch = []
+            for p in range(n):  # every round whose messages have all been sent completes
+                if ptr[p] >= len(steps[p]) or not sent_done[p]:
+                    continue
+                s = steps[p][ptr[p]]
+                need = {}
+                for _, src in s.recvs:
+                    need[src] = need.get(src, 0) + 1
+                if any(sent.get((src, p), 0) < recvd.get((src, p), 0) + c
+                       for src, c in need.items()):
+                    continue
+                for buf, src in s.recvs:
+                    k = recvd.get((src, p), 0)
+                    recvd[(src, p)] = k + 1
+                    t = pending.pop((src, p, k))
+                    if t.numel() != buf.numel() or t.dtype != buf.dtype:
+                        raise CaptureError(f"message {k} from party {src} to {p}: "
+                                           f"{tuple(t.shape)} {t.dtype} sent, "
+                                           f"{tuple(buf.shape)} {buf.dtype} expected")
+                    batch.append((p, src, t.reshape(buf.shape), buf))
+                ptr[p] += 1
+                sent_done[p] = False
+                progress = True
+            if batch:
+                acts.append(("cpb", batch))
+            if not progress:
+                raise CaptureError("the parties' tapes do not pair up (a receive no party "
+                                   "sends)")
+        if pending:
+            raise CaptureError(f"{len(pending)} messages sent but never received")
+        return acts
 
     def __del__(self):
         h = getattr(self, "_graph_handles", None)
@@ -529,8 +593,6 @@ class PartyTapes:
     def replay(self, arguments: dict) -> Dict[str, dict]:
         import time
 
-        import numpy as np
-
         if self._composed is not None:
             return self._replay_composed(arguments)
         n = len(self.tapes)
@@ -545,13 +607,7 @@ class PartyTapes:
                     for q in range(n):
                         if q != p:
                             s.wait_event(self._ends[q])
-                for k, v in arguments.items():
-                    t = tape.static.get(k)
-                    if isinstance(t, torch.Tensor):
-                        a = np.asarray(v)
-                        a = a.view(np.int64) if a.dtype == np.uint64 else a
-                        src = torch.from_numpy(np.ascontiguousarray(a).reshape(t.shape))
-                        t.copy_(src if src.dtype == t.dtype else src.to(t.dtype))
+                tape.copy_arguments(arguments)
                 tape._fill_keys()
             cur = -1
             for a in self.actions:
@@ -605,7 +661,7 @@ class PartyTapes:
         t0 = time.perf_counter()
         with torch.cuda.stream(s):
             for tape in self.tapes:
-                _copy_arguments(tape, arguments)
+                tape.copy_arguments(arguments)
                 tape._fill_keys()
             nat.check(nat.lib().mx_graph_launch(self._composed, s.cuda_stream), "graph launch")
             self.issue_s.append(time.perf_counter() - t0)
@@ -614,15 +670,3 @@ class PartyTapes:
                 out[self.identities[p]] = tape._decode(tape.interp, tape.sess, tape.outs)
                 tape.replays += 1
         return out
-
-
-def _copy_arguments(tape, arguments):
-    import numpy as np
-
-    for k, v in arguments.items():
-        t = tape.static.get(k)
-        if isinstance(t, torch.Tensor):
-            a = np.asarray(v)
-            a = a.view(np.int64) if a.dtype == np.uint64 else a
-            src = torch.from_numpy(np.ascontiguousarray(a).reshape(t.shape))
-            t.copy_(src if src.dtype == t.dtype else src.to(t.dtype))

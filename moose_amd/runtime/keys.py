@@ -116,6 +116,26 @@ class KeyTable:
         raw = os.urandom(16 * n)
         self._write(0, [raw[16 * i:16 * i + 16] for i in range(n)])
 
+    def enable_device_refresh(self):
+        """Draw the keys of later :meth:`refresh_device` calls on the device: a master key
+        from the OS (16 bytes, uploaded once) and a replay counter in device memory
+        (csrc/party_graph.hip ``mx_key_refresh``)."""
+        raw = np.frombuffer(os.urandom(16), dtype=np.int32).copy()
+        self._master = torch.from_numpy(raw).to(self.device)
+        self._epoch = torch.zeros(1, dtype=torch.int64, device=self.device)
+
+    def refresh_device(self, upto: int = None):
+        """Fresh keys for slots ``[0, upto)`` drawn by ONE kernel on the current stream:
+        slot s of the e-th refresh = ChaCha12(master, nonce e, block s)'s first 16 bytes and
+        its AES-128 schedule.  No host work beyond the launch (a replay's key refresh was a
+        urandom call, the schedules and a pinned copy per table on the host)."""
+        n = self.capacity if upto is None else upto
+        if self.device.type != "cuda" or getattr(self, "_master", None) is None:
+            return self.refresh(n)
+        nat.check(nat.lib().mx_key_refresh(self.t.data_ptr(), n, self._master.data_ptr(),
+                                           self._epoch.data_ptr(), nat.stream_of(self.t)),
+                  "key refresh")
+
     def ptr(self, slot: int) -> int:
         return self.t.data_ptr() + slot * SLOT_WORDS * 4
 

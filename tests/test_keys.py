@@ -93,3 +93,37 @@ def test_fused_mul_reshare_matches_cross_then_shift(device, bits):
     s0, s1 = R.rss_mul3_k(kind, x0, x1, y0, y1, kt.ptr(0), 11)
     assert torch.equal(s0.data.cpu(), z.data.cpu())
     assert torch.equal(s1.data.cpu(), torch.roll(z.data, -1, dims=0).cpu())
+
+
+@pytest.mark.gpu
+def test_device_key_refresh_matches_host_derivation():
+    """KeyTable.refresh_device (csrc/party_graph.hip): slot s of the e-th refresh holds the
+    first 16 bytes of ChaCha12(master, nonce e, block s) and that key's AES-128 schedule --
+    the host derivation (mx_key_refresh_host) and the host slot image (mx_key_slots) of the
+    same key -- and every refresh gives new keys."""
+    import ctypes
+
+    import numpy as np
+
+    from moose_amd.ops import native as nat
+    from moose_amd.runtime.keys import slot_words
+
+    kt = KeyTable("cuda:0", capacity=40)
+    kt.enable_device_refresh()
+    master = kt._master.cpu().numpy().view(np.uint32).copy()
+    seen = set()
+    for e in range(3):
+        kt.refresh_device(37)
+        got = kt.t.cpu().numpy().view(np.uint32)
+        assert int(kt._epoch.item()) == e + 1
+        for s in (0, 1, 17, 36):
+            want = np.zeros(48, dtype=np.uint32)
+            nat.lib().mx_key_refresh_host(master.ctypes.data_as(ctypes.c_void_p), e, s,
+                                          want.ctypes.data_as(ctypes.c_void_p))
+            assert np.array_equal(got[s], want), (e, s)
+            raw = got[s, :4].tobytes()
+            assert np.array_equal(slot_words([raw])[0], want)  # the host AES schedule
+            seen.add(raw)
+        assert not got[37:].any()  # slots past the refreshed range untouched
+    assert len(seen) == 12
+    torch.cuda.synchronize()

@@ -160,22 +160,16 @@ def test_thread_parties_lr_inference_gpu(monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", [
-    "serial",
-    pytest.param("dag", marks=pytest.mark.xfail(
-        reason="the branch form of the composed graph still differs from eager on one device "
-               "after the write-after-read edges (debug option only; docs/NEXT.md)",
-        strict=False)),
-    "per-action"])
+@pytest.mark.parametrize("mode", ["serial", "copy-per-message", "per-action"])
 def test_thread_party_tapes_replay_bitwise_equal_eager(mode, monkeypatch):
     """Seeded sessions: a replay re-draws the seeded keys as a fresh eager evaluation does,
     so every replay's outputs equal the eager ones bitwise (parties on cuda:0): the tapes
-    composed into one hipGraph in issue order (default on one device) or as a DAG of
-    program-order, send -> receive and copy -> sender's-next-segment edges, and the
+    composed into one hipGraph in a round-synchronous total order (default on one device:
+    each round's messages one batched copy kernel, or one copy node per message), and the
     per-action replay."""
     composed = mode != "per-action"
     monkeypatch.setenv("MOOSEX_PARTY_GRAPH", "1" if composed else "0")
-    monkeypatch.setenv("MOOSEX_PARTY_GRAPH_DAG", "1" if mode == "dag" else "0")
+    monkeypatch.setenv("MOOSEX_PARTY_COPY_BATCH", "0" if mode == "copy-per-message" else "1")
     comp = _comp(False)
     args = _args()
     devs = {i: "cuda:0" for i in IDS}
@@ -228,6 +222,46 @@ def test_party_tapes_schedule_pairs_rounds():
     pt.tapes = [_T([CommStep([], [(e(1), 1)])]), _T(["x"])]
     with pytest.raises(CaptureError):
         pt._schedule()
+
+
+def test_party_tapes_round_schedule_batches_messages():
+    """The composed one-GPU order (PartyTapes._schedule_rounds, CPU mock tapes): every
+    party's segments stay in program order, each message is copied after its sender's
+    segment that produced it and before its receiver's next segment, and the messages of
+    one round of all parties form ONE batch."""
+    from moose_amd.parallel.threads import PartyTapes
+    from moose_amd.parallel.transport import CommStep
+    from moose_amd.runtime.graphs import CaptureError
+
+    class _T:
+        def __init__(self, steps):
+            self.steps = steps
+
+    def e(n):
+        return torch.zeros(n)
+
+    # round 1: a ring shift (3 messages); round 2: the dealer's two messages
+    tapes = [
+        ["a0", CommStep([(e(2), 1)], [(e(2), 2)]), "a1", CommStep([], [(e(3), 2)]), "a2"],
+        ["b0", CommStep([(e(2), 2)], [(e(2), 0)]), CommStep([], [(e(3), 2)]), "b1"],
+        ["c0", CommStep([(e(2), 0)], [(e(2), 1)]), "c1", CommStep([(e(3), 0), (e(3), 1)], [])],
+    ]
+    pt = PartyTapes.__new__(PartyTapes)
+    pt.tapes = [_T(s) for s in tapes]
+    acts = pt._schedule_rounds()
+    order = {p: [a[2] for a in acts if a[0] == "g" and a[1] == p] for p in range(3)}
+    assert order == {0: ["a0", "a1", "a2"], 1: ["b0", "b1"], 2: ["c0", "c1"]}
+    batches = [a[1] for a in acts if a[0] == "cpb"]
+    assert [len(b) for b in batches] == [3, 2]
+    pos = {a[2]: i for i, a in enumerate(acts) if a[0] == "g"}
+    first = acts.index(("cpb", batches[0]))
+    second = acts.index(("cpb", batches[1]))
+    assert max(pos["a0"], pos["b0"], pos["c0"]) < first < min(pos["a1"], pos["b1"], pos["c1"])
+    assert pos["c1"] < second < min(pos["a2"], pos["b1"])
+    assert {(r, s) for r, s, _, _ in batches[1]} == {(0, 2), (1, 2)}
+    pt.tapes = [_T([CommStep([], [(e(1), 1)])]), _T(["x"])]
+    with pytest.raises(CaptureError):
+        pt._schedule_rounds()
 
 
 @pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
