@@ -318,6 +318,24 @@ int mx_dot_tail_r1(int dev, int words, int64_t n, int m, int ncomp, const int* r
 int mx_dot_tail_r2(int dev, int words, int64_t n, int ncomp, const int* roles,
                    const void* const* a, const void* const* b, void* const* out, void* stream);
 
+// The same tail for ONE party over up to MX_MAX_JOBS products ("jobs", rss_jobs.hip): job q
+// is ptrs[8q..8q+7] = (x0, x1, y0, y1, a, a2, o0, o1) and dims[8q..8q+7] = (rows, sx, sy, sa,
+// sa2, ca, ca2, cb): value[r, e] = cb (x0 y0 + x0 y1 + x1 y0) + ca a + ca2 a2 (row r of x at
+// x + r sx, ...), for rows of length L; the new shares go to o0 / o1 (dense [rows, L]).
+// Messages are dense over the concatenation of the jobs' rows.  main: the values' messages;
+// dealer: P2's part.
+#define MX_MAX_JOBS 4
+int mx_jobs_r0(int dev, int words, int njobs, const void* const* ptrs, const int64_t* dims,
+               int64_t L, int m, int role, int main, int dealer, void* msg, void* msg_rt,
+               void* msg_rm, const uint32_t* const* slots, const uint64_t* nonces,
+               void* stream);
+int mx_jobs_r1(int dev, int words, int njobs, const void* const* ptrs, const int64_t* dims,
+               int64_t L, int m, int role, const void* msg, const void* rmk, const void* rz,
+               const void* rrt, const void* rrm, void* w, const uint32_t* const* slots,
+               const uint64_t* nonces, void* stream);
+int mx_jobs_r2(int dev, int words, int njobs, const void* const* ptrs, const int64_t* dims,
+               int64_t L, int role, const void* a, const void* b, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

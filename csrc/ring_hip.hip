@@ -1156,6 +1156,75 @@ __global__ void __launch_bounds__(256) k_ks_cross1(const T* __restrict__ g0, con
   }
 }
 
+// Latency form of k_ks_cross1 (a per-party level of the LR inference's adders: a few
+// hundred elements): the block's 2 x EPB keystream chunks (both keys, one nonce) one per
+// thread into LDS, then every thread finishes elements -- one ChaCha block on the critical
+// path instead of two (four with both ANDs) in sequence.  Same chunks, same values.
+template <class T>
+__global__ void __launch_bounds__(256)
+    k_ks_cross1_lat(const T* __restrict__ g0, const T* __restrict__ g1, const T* __restrict__ p0,
+                    const T* __restrict__ p1, T* __restrict__ z, int64_t n, int d, int both,
+                    KeySrc keys, uint64_t nonce, const T* __restrict__ t0, const T* __restrict__ t1,
+                    T* __restrict__ go0, T* __restrict__ go1) {
+  constexpr int EPB = 128;
+  __shared__ uint32_t rks[2][kKeyWords];
+  __shared__ uint64_t kl[2][EPB], kh[2][EPB];
+  stage_keys(rks, keys, 2);
+  constexpr int P = Lane<T>::kPer;
+  const int64_t ntot = both ? 2 * n : n;
+  const int64_t nb = (ntot + P - 1) / P;
+  const int tid = threadIdx.x, s = tid / EPB, lb = tid % EPB;
+  for (int64_t b0 = (int64_t)blockIdx.x * EPB; b0 < nb; b0 += (int64_t)gridDim.x * EPB) {
+    if (b0 + lb < nb) {
+      uint64_t lo, hi;
+      prf_chunk(rks[s], nonce, (uint64_t)(b0 + lb), &lo, &hi);
+      kl[s][lb] = lo;
+      kh[s][lb] = hi;
+    }
+    __syncthreads();
+    for (int q = tid; q < EPB * P; q += blockDim.x) {
+      const int64_t c = b0 * P + q;
+      if (c >= ntot) break;
+      const int lc = q / P, j = q % P;
+      const T k = pick<T>(kl[0][lc], kh[0][lc], j) ^ pick<T>(kl[1][lc], kh[1][lc], j);
+      const int64_t e = c < n ? c : c - n;
+      const T a0 = p0[e], a1 = p1[e];
+      if (c < n) {
+        T G0 = g0[e], G1 = g1[e];
+        if (t0 != nullptr) {
+          G0 ^= t0[e];
+          G1 ^= t1[e];
+          go0[e] = G0;
+          go1[e] = G1;
+        }
+        const T s0 = G0 << d, s1 = G1 << d;
+        z[c] = (a0 & s0) ^ (a0 & s1) ^ (a1 & s0) ^ k;
+      } else {
+        const T u0 = a0 << d, u1 = a1 << d;
+        z[c] = (a0 & u0) ^ (a0 & u1) ^ (a1 & u0) ^ k;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <class T>
+bool ks_lat_launch(const void* g0, const void* g1, const void* t0, const void* t1, void* go0,
+                   void* go1, const void* p0, const void* p1, void* z, int64_t n, int d, int both,
+                   const KeySrc& k, uint64_t nonce, hipStream_t st) {
+  constexpr int P = Lane<T>::kPer;
+  const int64_t nb = ((both ? 2 * n : n) + P - 1) / P;
+  static const bool on = [] {
+    const char* e = std::getenv("MOOSEX_KS_LAT");
+    return !(e && e[0] == '0');
+  }();
+  if (!on || nb > (1 << 14)) return false;
+  hipLaunchKernelGGL(k_ks_cross1_lat<T>, dim3((unsigned)((nb + 127) / 128)), dim3(256), 0, st,
+                     (const T*)g0, (const T*)g1, (const T*)p0, (const T*)p1, (T*)z, n, d, both, k,
+                     nonce, (const T*)t0, (const T*)t1, (T*)go0, (T*)go1);
+  return true;
+}
+
 // Latency variant for small launches (few keystream chunks): the block's 3 x EPB chunks are
 // computed one per thread into LDS, then EPB threads finish the elements -- one PRF on the
 // critical path instead of three.
@@ -2144,6 +2213,13 @@ int mxh_ks_cross1x_s(int words, const void* g0, const void* g1, const void* t0, 
                      void* stream) {
   if (n == 0) return 0;
   KeySrc k = mxd::keysrc_slots(slots, 2);
+  if ((words == 1 && ks_lat_launch<u64>(g0, g1, t0, t1, go0, go1, p0, p1, z, n, d, both, k,
+                                        nonce, S(stream))) ||
+      (words == 2 && ks_lat_launch<u128>(g0, g1, t0, t1, go0, go1, p0, p1, z, n, d, both, k,
+                                         nonce, S(stream)))) {
+    MX_LAUNCH_CHECK();
+    return 0;
+  }
   if (words == 1) {
     hipLaunchKernelGGL(k_ks_cross1<u64>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
                        (const u64*)g0, (const u64*)g1, (const u64*)p0, (const u64*)p1, (u64*)z,
@@ -2184,6 +2260,13 @@ int mxh_ks_cross1_s(int words, const void* g0, const void* g1, const void* p0, c
                     uint64_t nonce, void* stream) {
   if (n == 0) return 0;
   KeySrc k = mxd::keysrc_slots(slots, 2);
+  if ((words == 1 && ks_lat_launch<u64>(g0, g1, nullptr, nullptr, nullptr, nullptr, p0, p1, z,
+                                        n, d, both, k, nonce, S(stream))) ||
+      (words == 2 && ks_lat_launch<u128>(g0, g1, nullptr, nullptr, nullptr, nullptr, p0, p1, z,
+                                         n, d, both, k, nonce, S(stream)))) {
+    MX_LAUNCH_CHECK();
+    return 0;
+  }
   if (words == 1) {
     hipLaunchKernelGGL(k_ks_cross1<u64>, dim3(grid_for(n)), dim3(kBlock), 0, S(stream),
                        (const u64*)g0, (const u64*)g1, (const u64*)p0, (const u64*)p1, (u64*)z,

@@ -18,6 +18,7 @@ Parity: reference host ring kernels ``moose/src/host/ops.rs:1709-2036``.
 """
 from __future__ import annotations
 
+import builtins
 import ctypes
 import math
 import os
@@ -2026,3 +2027,85 @@ def dot_tail_r2(a, b, out, bits, roles, n):
     dev, st = _dev_stream([t for t in out if t is not None])
     nat.check(nat.lib().mx_dot_tail_r2(dev, _words(bits), n, len(roles), _roles_arr(roles),
                                        _vp(a), _vp(b), _vp(out), st), "dot_tail_r2")
+
+
+# ---------------------------------------------------------------------------
+# the per-party tail over several products at once (csrc/rss_jobs.hip)
+# ---------------------------------------------------------------------------
+MAX_JOBS = 4
+
+
+class MulJob:
+    """One product of a batched per-party tail: ``rows`` rows of length L (the call's row
+    length) with value[r] = cb (x0 y0 + x0 y1 + x1 y0)[r] + ca a[r] + ca2 a2[r], where
+    operand rows are read at ``r * stride`` (stride 0: one row broadcast to every row) and
+    a / a2 are additive shares (e.g. a party's first share component); the new shares are
+    written to the dense rows ``o0`` / ``o1``.  Operands are ring-tensor data (torch)."""
+
+    __slots__ = ("x0", "x1", "y0", "y1", "a", "a2", "o0", "o1", "rows", "sx", "sy", "sa",
+                 "sa2", "ca", "ca2", "cb")
+
+    def __init__(self, rows, o0, o1, x=None, y=None, sx=0, sy=0, a=None, sa=0, ca=1, cb=1,
+                 a2=None, sa2=0, ca2=1):
+        self.rows, self.o0, self.o1 = rows, o0, o1
+        self.x0, self.x1 = x if x is not None else (None, None)
+        self.y0, self.y1 = y if y is not None else (None, None)
+        self.sx, self.sy, self.a, self.sa, self.a2, self.sa2 = sx, sy, a, sa, a2, sa2
+        self.ca, self.ca2, self.cb = ca, ca2, (cb if x is not None else 0)
+
+
+def _jobs_abi(jobs):
+    if not 1 <= len(jobs) <= MAX_JOBS:
+        raise ValueError(f"1..{MAX_JOBS} jobs per call, got {len(jobs)}")
+    ptrs, dims = [], []
+    for j in jobs:
+        for t in (j.x0, j.x1, j.y0, j.y1, j.a, j.a2, j.o0, j.o1):
+            ptrs.append(None if t is None else t.data_ptr())
+        for v in (j.rows, j.sx, j.sy, j.sa, j.sa2, j.ca, j.ca2, j.cb):
+            v = int(v)
+            dims.append(v - (1 << 64) if v >= (1 << 63) else v)
+    return (ctypes.c_void_p * len(ptrs))(*ptrs), (ctypes.c_int64 * len(dims))(*dims)
+
+
+def jobs_r0(jobs, L, bits, m, role, slots, nonces, like, main=True, dealer=True):
+    """Round 0 of the batched per-party tail (mx_jobs_r0): the outgoing message over the
+    concatenation of the jobs' rows (P0 m0, P1 m1, P2 z2), the dealer's rt1 / rm1 (P2, when
+    ``dealer``), P2's new shares into the jobs' outputs.  ``like``: any tensor of the call's
+    device (allocation and stream)."""
+    n = builtins.sum(j.rows for j in jobs) * L
+    w = _words(bits)
+    shp = (n,) + ((2,) if bits == 128 else ())
+    msg = torch.empty(shp, dtype=torch.int64, device=like.device) if main else None
+    rt = torch.empty(shp, dtype=torch.int64, device=like.device) if role == 2 and dealer else None
+    rm = torch.empty((n,), dtype=torch.int64, device=like.device) if role == 2 and dealer else None
+    p, d = _jobs_abi(jobs)
+    nat.check(nat.lib().mx_jobs_r0(
+        nat.dev_of(like), w, len(jobs), p, d, L, m, role, int(main), int(dealer),
+        None if msg is None else msg.data_ptr(), None if rt is None else rt.data_ptr(),
+        None if rm is None else rm.data_ptr(), _slots_arr(slots), _nonces_arr(nonces),
+        nat.stream_of(like)), "jobs_r0")
+    return msg, rt, rm
+
+
+def jobs_r1(jobs, L, bits, m, role, slots, nonces, msg, rmk, rz, rrt, rrm):
+    """Round 1 (mx_jobs_r1): P0 / P1 open c from their message, the other's and z2; returns
+    w (P0 w0, P1 w1; None for P2) and writes P0's o0 = z0, P1's o1 = z2."""
+    if role == 2:
+        return None
+    w = torch.empty_like(msg)
+    p, d = _jobs_abi(jobs)
+    ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    nat.check(nat.lib().mx_jobs_r1(
+        nat.dev_of(msg), _words(bits), len(jobs), p, d, L, m, role, ptr(msg), ptr(rmk), ptr(rz),
+        ptr(rrt), ptr(rrm), w.data_ptr(), _slots_arr(slots), _nonces_arr(nonces),
+        nat.stream_of(msg)), "jobs_r1")
+    return w
+
+
+def jobs_r2(jobs, L, bits, role, a, b):
+    """Round 2 (mx_jobs_r2): P0's o1 / P1's o0 = w0 + w1."""
+    if role == 2:
+        return
+    p, d = _jobs_abi(jobs)
+    nat.check(nat.lib().mx_jobs_r2(nat.dev_of(a), _words(bits), len(jobs), p, d, L, role,
+                                   a.data_ptr(), b.data_ptr(), nat.stream_of(a)), "jobs_r2")

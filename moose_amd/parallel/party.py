@@ -192,3 +192,34 @@ def record_tail_traffic(stats, plc, nb, round_b=True):
     for a, b in ((0, 1), (1, 0)):
         stats.record_send(o[a], o[b], nb)
     stats.record_round(2 * nb)
+
+
+def jobs_tail(sess, plc, role, jobs, L, bits, m, nonces, slots):
+    """Zero share + reshare + TruncPr of the products ``jobs`` (ring.MulJob list) for ONE
+    party of role ``role``: the dot tail's two rounds and three kernels (csrc/rss_jobs.hip)
+    for all of them at once -- every job's cross terms computed inside round 0, the new
+    shares written straight to the jobs' output rows.  ``nonces`` = the dot tail's seven."""
+    like = next(t for j in jobs for t in (j.o0, j.x0, j.a) if t is not None)
+    msg, rt, rm = R.jobs_r0(jobs, L, bits, m, role, slots, nonces, like)
+    n_el = sum(j.rows for j in jobs) * L
+    like_t = ((n_el,) + ((2,) if bits == 128 else ()), torch.int64)
+    like_rm = ((n_el,), torch.int64)
+    payload = {"m0": msg if role == 0 else None, "m1": msg if role == 1 else None,
+               "z2_0": msg if role == 2 else None, "z2_1": msg if role == 2 else None,
+               "rt1": rt, "rm1": rm}
+    got = sess.party_exchange(plc, [(nm, a, b, payload[nm], like_rm if nm == "rm1" else like_t)
+                                    for nm, a, b in TAIL_A])
+    rmk = got.get("m1") if role == 0 else got.get("m0") if role == 1 else None
+    rz = got.get("z2_0") if role == 0 else got.get("z2_1") if role == 1 else None
+    w = R.jobs_r1(jobs, L, bits, m, role, slots, nonces, msg, rmk, rz, got.get("rt1"),
+                  got.get("rm1"))
+    nb = n_el * (16 if bits == 128 else 8)
+    record_tail_traffic(sess.stats, plc, nb, round_b=False)
+    got = sess.party_exchange(plc, [("w0", 0, 1, w if role == 0 else None, like_t),
+                                    ("w1", 1, 0, w if role == 1 else None, like_t)])
+    if role in (0, 1):
+        R.jobs_r2(jobs, L, bits, role, w, got["w1"] if role == 0 else got["w0"])
+    for a, b in ((0, 1), (1, 0)):
+        sess.stats.record_send(plc.owners[a], plc.owners[b], nb)
+    sess.stats.record_round(2 * nb)
+

@@ -389,6 +389,7 @@ class PartyTapes:
         self.segments = sum(t.segments for t in self.tapes)
         self._ends = None
         self.issue_s = []
+        self.issue_parts = []
         self._composed = self._compose() if single else None
 
     def _compose(self):
@@ -662,9 +663,15 @@ class PartyTapes:
         with torch.cuda.stream(s):
             for tape in self.tapes:
                 tape.copy_arguments(arguments)
+            t1 = time.perf_counter()
+            for tape in self.tapes:
                 tape._fill_keys()
+            t2 = time.perf_counter()
             nat.check(nat.lib().mx_graph_launch(self._composed, s.cuda_stream), "graph launch")
-            self.issue_s.append(time.perf_counter() - t0)
+            t3 = time.perf_counter()
+            self.issue_s.append(t3 - t0)
+            # host time per replay: arguments staged, keys refreshed, graph launched
+            self.issue_parts.append((t1 - t0, t2 - t1, t3 - t2))
             out = {}
             for p, tape in enumerate(self.tapes):
                 out[self.identities[p]] = tape._decode(tape.interp, tape.sess, tape.outs)

@@ -22,14 +22,17 @@ sequentially, exp.rs:155) and a polynomial for the fraction; negative inputs use
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from functools import lru_cache
 
 import numpy as np
+import torch
 
 from moose_amd.ops import ring as R
 from moose_amd.protocols import replicated as rep
 from moose_amd.protocols.replicated import RepTensor
+from moose_amd.runtime.session import PV
 from moose_amd.runtime.values import MV
 
 
@@ -106,6 +109,10 @@ def mul(sess, x, y, px=None, py=None, f=None):
 
 
 def dot(sess, x, y, px=None, py=None, f=None):
+    m = f if f is not None else (y.frac if px is not None else x.frac)
+    if (px is not None or py is not None) and 0 < m <= 63 and _jobs_ok(
+            sess, (y if px is not None else x).t):
+        return _dot_public_trunc_jobs(sess, x, y, px, py, m)
     if px is not None:
         z = rep.dot_public(sess, y.t, px, public_left=True)
         base = y
@@ -115,6 +122,22 @@ def dot(sess, x, y, px=None, py=None, f=None):
     else:
         return _with(x, rep.dot_trunc(sess, x.t, y.t, f if f is not None else x.frac))
     return _with(base, rep.trunc_pr(sess, z, f if f is not None else base.frac))
+
+
+def _dot_public_trunc_jobs(sess, x, y, px, py, m):
+    """A secret x public fixed-point product on a per-party session: the GEMM of this
+    party's FIRST share component only (an additive sharing of the product) and its TruncPr
+    through the batched tail -- one GEMM and 3 kernels (the generic path multiplies both
+    components, then runs TruncPr on the replicated product)."""
+    base = y if px is not None else x
+    t = base.t
+    plc, bits = t.plc, t.bits
+    pc = sess.public(plc, _pub(px if px is not None else py))
+    v0 = sess.p("Dot", plc, pc, t.s0) if px is not None else sess.p("Dot", plc, t.s0, pc)
+    nonces = _tail_nonces(sess, plc)
+    r = rep.tail_job(sess, plc, bits, m, nonces, v0,
+                     lambda o0, o1: R.MulJob(1, o0, o1, a=v0.v.data.contiguous()))
+    return _with(base, r)
 
 
 def dot_many(sess, pairs, f=None):
@@ -387,6 +410,8 @@ def poly_eval(sess, x: RepFixed, coeffs, shift: int = 0) -> RepFixed:
     f, bits = x.frac, x.bits
     if n > 1 and _rows_ok(sess, x):
         return _poly_eval_rows(sess, x, coeffs, shift)
+    if n > 1 and 0 < f + shift <= 63 and _jobs_ok(sess, x.t):
+        return _poly_eval_jobs(sess, x, coeffs, shift)
     P = local(sess, x, "ExpandDims", axis=[0])
     have = 1
     while have < n:
@@ -398,7 +423,55 @@ def poly_eval(sess, x: RepFixed, coeffs, shift: int = 0) -> RepFixed:
         P = concat(sess, [P, mul(sess, left, right)], 0)
         have += m
     acc = _weighted(sess, P.t, [int(round(c * (1 << f))) for c in coeffs[1:]], bits)
-    acc = rep.trunc_pr(sess, acc, f + shift)
+    if _party_tail(sess) and 0 < f + shift <= 63 and x.t.kind == "arith":
+        # per-party sessions: TruncPr of the weighted sum's additive shares (each party's
+        # first share component) with the dot's tail -- as _merged_exp_tail does, and
+        # bitwise what the batched form (_poly_eval_jobs) computes
+        ex = local(sess, RepFixed(acc, f, x.integ), "ExpandDims", axis=[0]).t
+        acc = local(sess, _tail_trunc(sess, x.t.plc, ex.s0, bits, f + shift), "IndexAxis",
+                    axis=0, index=0)
+    else:
+        acc = rep.trunc_pr(sess, acc, f + shift)
+    return add_const(sess, RepFixed(acc, f, x.integ), coeffs[0] / (1 << shift))
+
+
+def _party_tail(sess) -> bool:
+    """One party per process / thread (SPMD, in-process parties) with the dot's folded tail."""
+    return (not getattr(sess, "is_simulated", True) and getattr(sess, "party_dot_trunc", None)
+            is not None and os.environ.get("MOOSEX_DOT_TAIL", "1") != "0")
+
+
+def _poly_eval_jobs(sess, x: RepFixed, coeffs, shift: int = 0) -> RepFixed:
+    """poly_eval for one party on the batched tail (csrc/rss_jobs.hip): each power level is
+    the tail's three kernels reading and writing a preallocated power stack, and the
+    weighted sum's TruncPr one more (the weighted sum of the stack rows one kernel) --
+    bitwise the generic per-party levels (mul_trunc of the stacked operands) and final
+    TruncPr of the weighted sum's additive shares."""
+    from moose_amd.parallel.spmd import Remote
+
+    n = len(coeffs) - 1
+    f, bits, t = x.frac, x.bits, x.t
+    plc = t.plc
+    weights = [int(round(c * (1 << f))) for c in coeffs[1:]]
+    member = sess.party_index(plc) is not None
+    L = max(1, math.prod(sess.p_shape(t.s0))) if member else 1
+    st = _Stack(t.s0.v.data, t.s1.v.data, n - 1, bits) if member else None
+    have = 1
+    while have < n:
+        m = min(2 * have, n) - have
+        nonces = _tail_nonces(sess, plc)
+        if member:
+            sess.party_jobs(plc, _power_jobs(st, have, m, L), L, bits, f, nonces)
+        have += m
+    nonces = _tail_nonces(sess, plc)
+    if member:
+        acc0, acc1 = torch.empty_like(st.x0), torch.empty_like(st.x0)
+        sess.party_jobs(plc, [_acc_job(st, weights, n, L, acc0, acc1)], L, bits, f + shift,
+                        nonces)
+        acc = RepTensor(plc, bits, "arith", PV(plc, R.RT(acc0, bits)), PV(plc, R.RT(acc1, bits)))
+    else:
+        r = PV(plc, Remote(bits))
+        acc = RepTensor(plc, bits, "arith", r, r)
     return add_const(sess, RepFixed(acc, f, x.integ), coeffs[0] / (1 << shift))
 
 
@@ -693,6 +766,8 @@ def _merged_exp_tail(sess, x: RepFixed, fac: RepTensor, npad: int) -> RepFixed:
     and the polynomial's final TruncPr (its terms' additive shares) rides with a tree level
     too.  For the tutorial LR (fixed(24,40): 32 factors) 20 rounds become 12; the values
     are those of poly_eval + the tree up to TruncPr's probabilistic rounding."""
+    if _jobs_ok(sess, x.t, fac):
+        return _merged_exp_tail_jobs(sess, x, fac, npad)
     coeffs = _fit("exp2", 0.0, 1.0, 7)
     f, bits, t = x.frac, x.bits, x.t
     plc = t.plc
@@ -753,6 +828,151 @@ def _merged_exp_tail(sess, x: RepFixed, fac: RepTensor, npad: int) -> RepFixed:
                f=f + 1)
 
 
+def _jobs_ok(sess, *reps) -> bool:
+    """A per-party session whose products can run through the batched tail kernels
+    (csrc/rss_jobs.hip): same-shape dense shares within each operand."""
+    if getattr(sess, "party_jobs", None) is None or not rep.JOBS:
+        return False
+    if os.environ.get("MOOSEX_DOT_TAIL", "1") == "0" or reps[0].bits not in (64, 128):
+        return False
+    if sess.party_index(reps[0].plc) is None:
+        return True
+    return all(isinstance(t.v, R.RT) and t.v.data.is_contiguous()
+               and t.v.shape == r.s0.v.shape for r in reps for t in (r.s0, r.s1))
+
+
+def _abs_scaled_jobs(sess, s: RepTensor, x: RepFixed, c: float) -> RepFixed:
+    """|x| * c (one truncation) on a per-party session, for the arithmetic sign bit s of x:
+    trunc(c x - 2 c s x) -- the product s x, the public scaling and the truncation in ONE
+    batched tail (job value c x_p - 2c cross(s, x)_p): 2 rounds and 3 kernels instead of
+    negate_where's multiplication round plus mul_const's TruncPr (3 rounds, ~7 kernels)."""
+    cv = int(round(c * (1 << x.frac)))
+    t = x.t
+    nonces = _tail_nonces(sess, t.plc)
+    r = rep.tail_job(sess, t.plc, t.bits, x.frac, nonces, t.s0,
+                     lambda o0, o1: R.MulJob(1, o0, o1, x=(s.s0.v.data, s.s1.v.data),
+                                             y=(t.s0.v.data, t.s1.v.data), cb=-2 * cv,
+                                             a=t.s0.v.data, ca=cv))
+    return _with(x, r)
+
+
+class _Stack:
+    """A party's rows for the batched tails: ``x`` (the first power, its own tensors) and
+    a dense [k, ...] stack per share component for the rows after it."""
+
+    def __init__(self, x0, x1, rows, bits):
+        self.x0, self.x1, self.bits = x0, x1, bits
+        shp = (rows,) + tuple(x0.shape)
+        self.s0 = torch.empty(shp, dtype=x0.dtype, device=x0.device)
+        self.s1 = torch.empty(shp, dtype=x0.dtype, device=x0.device)
+
+    def power(self, k):
+        """(share0, share1) tensors of x^k (k >= 1)."""
+        return (self.x0, self.x1) if k == 1 else (self.s0[k - 2], self.s1[k - 2])
+
+
+def _power_jobs(st: _Stack, have: int, m: int, L: int):
+    """Jobs of one power level: x^(have+1 .. have+m) = x^have * [x, x^2, .., x^m], written
+    into the stack rows (as the generic level's concat of x^have copies times P[0:m])."""
+    left = st.power(have)
+    jobs = [R.MulJob(1, st.s0[have - 1], st.s1[have - 1], x=left, y=st.power(1))]
+    if m > 1:
+        jobs.append(R.MulJob(m - 1, st.s0[have:have + m - 1], st.s1[have:have + m - 1], x=left,
+                             y=(st.s0[0], st.s1[0]), sx=0, sy=L))
+    return jobs
+
+
+def _acc_job(st: _Stack, weights, n, L, o0, o1):
+    """The additive share sum_k w_k x^k (this party's first share components) as a value
+    job: the stack rows by one weighted-sum kernel, x^1 as the job's second term."""
+    rest = R.weighted_sum(R.RT(st.s0[:n - 1], st.bits), [w % (1 << st.bits) for w in weights[1:n]])
+    return R.MulJob(1, o0, o1, a=rest.data, sa=L, a2=st.x0, sa2=L, ca2=weights[0])
+
+
+def _tail_nonces(sess, plc):
+    return tuple(sess.nonce(plc) for _ in range(7))
+
+
+def _merged_exp_tail_jobs(sess, x: RepFixed, fac: RepTensor, npad: int) -> RepFixed:
+    """_merged_exp_tail on the batched per-party tail (csrc/rss_jobs.hip): every round is the
+    tail's three kernels for all of that round's products -- the polynomial level's (read
+    from and written into a preallocated power stack), the tree level's, and the
+    polynomial's weighted sum when it rides along -- with the same nonces, the same element
+    order and so bitwise the same shares as the generic rounds (cross terms per pair,
+    concatenation, tail, slices)."""
+    from moose_amd.parallel.spmd import Remote
+
+    coeffs = _fit("exp2", 0.0, 1.0, 7)
+    f, bits, t = x.frac, x.bits, x.t
+    plc = t.plc
+    n = len(coeffs) - 1
+    weights = [int(round(c * (1 << f))) for c in coeffs[1:]]
+    member = sess.party_index(plc) is not None
+    shape = sess.p_shape(t.s0) if member else None
+    L = max(1, math.prod(shape)) if member else 1
+    st = _Stack(t.s0.v.data, t.s1.v.data, n - 1, bits) if member else None
+    F0, F1 = (fac.s0.v.data, fac.s1.v.data) if member else (None, None)
+
+    def run(jobs):
+        nonces = _tail_nonces(sess, plc)
+        if member:
+            sess.party_jobs(plc, jobs, L, bits, f, nonces)
+
+    def tree_job(nf):
+        h = nf // 2
+        o0 = torch.empty_like(F0[0:h])
+        o1 = torch.empty_like(F0[0:h])
+        return R.MulJob(h, o0, o1, x=(F0[0:h], F1[0:h]), y=(F0[h:2 * h], F1[h:2 * h]), sx=L,
+                        sy=L), (o0, o1)
+
+    have, nf = 1, npad
+    while have < n:  # one polynomial level + one tree level per round
+        m = min(2 * have, n) - have
+        jobs = _power_jobs(st, have, m, L) if member else []
+        new = None
+        if nf > 1 and member:
+            tj, new = tree_job(nf)
+            jobs.append(tj)
+        run(jobs)
+        if nf > 1:
+            F0, F1 = new if member else (None, None)
+            nf //= 2
+        have += m
+    # the polynomial's weighted sum rides with the next tree level (its TruncPr)
+    acc0 = acc1 = None
+    jobs = []
+    new = None
+    if member and nf > 1:
+        tj, new = tree_job(nf)
+        jobs.append(tj)
+    if member:
+        acc0, acc1 = torch.empty_like(st.x0), torch.empty_like(st.x0)
+        jobs.append(_acc_job(st, weights, n, L, acc0, acc1))
+    run(jobs)
+    if nf > 1:
+        F0, F1 = new if member else (None, None)
+        nf //= 2
+    while nf > 1:
+        new = None
+        if member:
+            tj, new = tree_job(nf)
+            run([tj])
+        else:
+            run([])
+        F0, F1 = new if member else (None, None)
+        nf //= 2
+    if not member:
+        r = PV(plc, Remote(bits))
+        acc = RepTensor(plc, bits, "arith", r, r)
+        F = acc
+    else:
+        acc = RepTensor(plc, bits, "arith", PV(plc, R.RT(acc0, bits)), PV(plc, R.RT(acc1, bits)))
+        F = RepTensor(plc, bits, "arith", PV(plc, R.RT(F0[0], bits)), PV(plc, R.RT(F1[0], bits)))
+    p = add_const(sess, RepFixed(acc, f, x.integ), coeffs[0])
+    # 2^-a = p(1 - r) / 2 * prod: the halving is one more bit of the last TruncPr
+    return mul(sess, p, RepFixed(F, f, x.integ), f=f + 1)
+
+
 def exp2(sess, x: RepFixed) -> RepFixed:
     s = sign_bit(sess, x)
     ax = _with(x, rep.negate_where(sess, s, x.t))
@@ -775,8 +995,12 @@ def sigmoid(sess, x: RepFixed) -> RepFixed:
     """sigma(x) = 1 / (1 + e^-|x|) mirrored for x < 0; 1 + e^-|x| is in [1, 2] so the
     reciprocal needs no normalisation."""
     s = sign_bit(sess, x)
-    ax = _with(x, rep.negate_where(sess, s, x.t))
-    e = exp_nonpositive(sess, neg(sess, ax))
+    if _jobs_ok(sess, x.t, s):
+        # per-party: |x| / ln 2 in one tail (_abs_scaled_jobs), one round fewer
+        e = _exp2_parts(sess, _abs_scaled_jobs(sess, s, x, 1.0 / math.log(2.0)), negative=True)
+    else:
+        ax = _with(x, rep.negate_where(sess, s, x.t))
+        e = exp_nonpositive(sess, neg(sess, ax))
     d = add_const(sess, e, 1.0)  # in [1, 2]
     # 1/d = (1/h) / 2 with h = d / 2 in [0.5, 1]: the fit of 1/h evaluated at d directly
     # (coefficients c_k / 2^k), and both halvings folded into TruncPrs of one more bit --

@@ -380,7 +380,10 @@ def mul(sess, x: RepTensor, y: RepTensor) -> RepTensor:
 def mul_public_trunc(sess, x: RepTensor, c, m: int, value: int = None) -> RepTensor:
     """trunc_pr(mul_public(x, c), m); for a public scalar ring constant whose integer
     ``value`` the caller knows, on a fused stacked session, the multiplication runs inside the
-    TruncPr kernel (same shares)."""
+    TruncPr kernel (same shares); on a per-party session inside the batched tail."""
+    if (m and 0 < m <= 63 and value is not None and -(1 << 62) < value < (1 << 62)
+            and jobs_ok(sess, x)):
+        return mul_public_trunc_jobs(sess, x, value, m)
     if (m and value is not None and x.kind == "arith" and getattr(sess, "fused", False)
             and x.bits in (64, 128) and hasattr(sess, "fused_trunc_pr_premul")):
         with span("rep.trunc_pr"):
@@ -399,6 +402,15 @@ def mul_trunc(sess, x: RepTensor, y: RepTensor, m: int, out=None) -> RepTensor:
         r = f(x.plc, x.s0, x.s1, y.s0, y.s1, m, out=out)
         if r is not None:
             return RepTensor(x.plc, x.bits, "arith", r[0], r[1])
+    jobs = getattr(sess, "party_jobs", None)
+    if (jobs is not None and JOBS and 0 < m <= 63 and x.kind == "arith" and x.bits in (64, 128)
+            and os.environ.get("MOOSEX_DOT_TAIL", "1") != "0" and sess.jobs_shape_ok(x, y)):
+        # one party of a per-party session: the product's cross terms inside the batched
+        # tail's first kernel (csrc/rss_jobs.hip) -- 3 kernels, bitwise the shares of the
+        # cross-term kernel + dot tail below (same nonces, same element order)
+        with span("rep.mul_trunc_party"):
+            nonces = tuple(sess.nonce(x.plc) for _ in range(7))
+            return _mul_trunc_jobs(sess, x, y, m, nonces, out)
     party = getattr(sess, "party_dot_trunc", None)
     plain = getattr(sess, "p_cross_plain", None)
     if (party is not None and plain is not None and 0 < m <= 63 and x.kind == "arith"
@@ -412,6 +424,55 @@ def mul_trunc(sess, x: RepTensor, y: RepTensor, m: int, out=None) -> RepTensor:
             s0, s1 = party(x.plc, v, m, nonces, out=(out[0], out[1]) if out else None)
             return RepTensor(x.plc, x.bits, "arith", s0, s1)
     return trunc_pr(sess, mul(sess, x, y), m, out=out)
+
+
+# per-party sessions batch products into the tail kernels of csrc/rss_jobs.hip
+JOBS = os.environ.get("MOOSEX_PARTY_JOBS", "1") != "0"
+
+
+def _mul_trunc_jobs(sess, x: RepTensor, y: RepTensor, m: int, nonces, out=None) -> RepTensor:
+    return tail_job(sess, x.plc, x.bits, m, nonces, x.s0,
+                    lambda o0, o1: R.MulJob(1, o0, o1, x=(x.s0.v.data, x.s1.v.data),
+                                            y=(y.s0.v.data, y.s1.v.data)), out=out)
+
+
+def tail_job(sess, plc, bits, m, nonces, like: PV, make, out=None) -> RepTensor:
+    """One value through the per-party batched tail (csrc/rss_jobs.hip): ``make(o0, o1)``
+    builds its ring.MulJob (one row of ``like``'s size) writing the new shares to o0 / o1.
+    Non-members get placeholders."""
+    from moose_amd.parallel.spmd import Remote
+
+    if sess.party_index(plc) is None:
+        r = PV(plc, Remote(bits))
+        return RepTensor(plc, bits, "arith", r, r)
+    v = like.v
+    if out is not None:
+        o0, o1 = out[0].v.data, out[1].v.data
+    else:
+        o0, o1 = R.empty2(v.shape, bits, v.data.device)
+        o0, o1 = o0.data, o1.data
+    sess.party_jobs(plc, [make(o0, o1)], max(1, v.numel()), bits, m, nonces)
+    return RepTensor(plc, bits, "arith", PV(plc, R.RT(o0, bits)), PV(plc, R.RT(o1, bits)))
+
+
+def jobs_ok(sess, *reps) -> bool:
+    """A per-party session whose products run through the batched tail kernels: every share
+    of every operand one dense shape (members decide alike; non-members follow)."""
+    if getattr(sess, "party_jobs", None) is None or not JOBS:
+        return False
+    if os.environ.get("MOOSEX_DOT_TAIL", "1") == "0" or reps[0].bits not in (64, 128):
+        return False
+    return all(r.kind == "arith" for r in reps) and sess.jobs_shape_ok(*reps)
+
+
+def mul_public_trunc_jobs(sess, x: RepTensor, value: int, m: int) -> RepTensor:
+    """trunc_pr(x * c, m) for a public integer c = ``value`` on a per-party session: the
+    additive shares c x_p (each party's first share component scaled) through the batched
+    tail -- 3 kernels, 2 rounds (the generic path multiplies both components first)."""
+    with span("rep.trunc_pr"):
+        nonces = tuple(sess.nonce(x.plc) for _ in range(7))
+        return tail_job(sess, x.plc, x.bits, m, nonces, x.s0,
+                        lambda o0, o1: R.MulJob(1, o0, o1, a=x.s0.v.data, ca=value))
 
 
 def mul_trunc_many(sess, jobs):

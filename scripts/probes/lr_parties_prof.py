@@ -47,6 +47,22 @@ def main():
         rec["actions"] = {k: sum(1 for x in t.actions if x[0] == k) for k in ("g", "rec", "cp")}
         iss = sorted(t.issue_s)
         rec["host_issue_ms_p50"] = iss[len(iss) // 2] * 1e3 if iss else None
+        parts = getattr(t, "issue_parts", [])
+        if parts:
+            rec["issue_parts_ms_p50"] = [sorted(x)[len(x) // 2] * 1e3 for x in zip(*parts)]
+        rec["graph_nodes"] = getattr(t, "graph_nodes", None)
+        import time as _t
+        # the device time of one replay alone (launch -> synchronize), no decode
+        ts = []
+        for _ in range(10):
+            torch.cuda.synchronize()
+            t0 = _t.perf_counter()
+            from moose_amd.ops import native as nat
+            s = t.streams[0]
+            nat.lib().mx_graph_launch(t._composed, s.cuda_stream)
+            s.synchronize()
+            ts.append((_t.perf_counter() - t0) * 1e3)
+        rec["graph_only_ms_p50"] = sorted(ts)[5]
     print(json.dumps(rec), flush=True)
 
 

@@ -204,6 +204,32 @@ def test_ks_cross1_matches_host(bits, both):
 
 
 @pytest.mark.parametrize("bits", [64, 128])
+@pytest.mark.parametrize("both", [True, False])
+@pytest.mark.parametrize("n", [37, 3000])
+def test_ks_cross1_slots_latency_form_matches_host(bits, both, n):
+    """The key-slot Kogge-Stone level kernels of the per-party adders (ks_cross1_s and the
+    xor-folding ks_cross1x_s; small launches take the latency form k_ks_cross1_lat):
+    GPU == CPU bitwise, keys read from device / host key slots."""
+    from moose_amd.runtime.keys import KeyTable
+
+    xs = [rand_rt((n,), bits, 80 + i) for i in range(6)]
+    raw = [bytes(range(16)), bytes(range(16, 32))]
+    out = {}
+    for dev in ("cpu", "cuda"):
+        kt = KeyTable(dev, capacity=4)
+        kt._write(0, raw)
+        slots = [kt.ptr(0), kt.ptr(1)]
+        ys = [x if dev == "cpu" else gpu(x) for x in xs]
+        z = R.ks_cross1_s(*ys[:4], 5, both, slots, 23)
+        zx, (go0, go1) = R.ks_cross1x_s(ys[0], ys[1], ys[4], ys[5], ys[2], ys[3], 3, both, slots,
+                                        29)
+        out[dev] = [t.data.cpu() for t in (z, zx, go0, go1)]
+        torch.cuda.synchronize()
+    for a, b in zip(out["cpu"], out["cuda"]):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("bits", [64, 128])
 def test_binary_slot_matches_host(bits):
     """Public operand on one share slot in one kernel (k_binary_slot): GPU == CPU."""
     a = rand_rt((3, 5, 7), bits, 70)
