@@ -336,6 +336,20 @@ int mx_jobs_r1(int dev, int words, int njobs, const void* const* ptrs, const int
 int mx_jobs_r2(int dev, int words, int njobs, const void* const* ptrs, const int64_t* dims,
                int64_t L, int role, const void* a, const void* b, void* stream);
 
+// Per-party bit decomposition front and B2A (bits_party.h, rss_bits_party.hip): nonces
+// nn = (n1 of the sharing, n_g of the product).  front: this party's p pair and zero-shared
+// AND term z (P0 also the share message a1; P1 runs after receiving a1 in arecv).  b2a:
+// phase 0 (P0, P2) / 1 (P1, arecv = A1): message (P0's A1), z, base pair of bit planes
+// start.. start + count - 1 of src = (s0, s1, g0, g1, t0, t1) -- sum words (g0 = null) or
+// the adder's last (p, g, t); phase 2: out = base - 2 (z, zr).  Elements [count, S].
+int mx_bits_front(int dev, int words, int role, int64_t n, const void* xa, const void* xb,
+                  const void* arecv, void* msg, void* z, void* p0, void* p1,
+                  const uint32_t* const* slots, const uint64_t* nonces, void* stream);
+int mx_bits_b2a(int dev, int words, int phase, int role, int64_t S, int start, int count,
+                const void* const* src, const void* arecv, void* msg, void* z, void* base0,
+                void* base1, const void* zr, void* out0, void* out1,
+                const uint32_t* const* slots, const uint64_t* nonces, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

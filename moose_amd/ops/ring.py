@@ -2109,3 +2109,53 @@ def jobs_r2(jobs, L, bits, role, a, b):
     p, d = _jobs_abi(jobs)
     nat.check(nat.lib().mx_jobs_r2(nat.dev_of(a), _words(bits), len(jobs), p, d, L, role,
                                    a.data_ptr(), b.data_ptr(), nat.stream_of(a)), "jobs_r2")
+
+
+# ---------------------------------------------------------------------------
+# per-party bit decomposition front and B2A (csrc/rss_bits_party.hip, bits_party.h)
+# ---------------------------------------------------------------------------
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def bits_front(role, xa, xb, arecv, bits, slots, n1, ng):
+    """This party's adder inputs of the bit decomposition of (xa, xb) (its two arithmetic
+    components, torch data): (message a1 (P0) or None, z (its zero-shared AND term, the
+    reshare message), p0, p1)."""
+    like = next(t for t in (xa, xb, arecv) if t is not None)
+    n = like.numel() // (2 if bits == 128 else 1)
+    z, p0, p1 = (torch.empty_like(like) for _ in range(3))
+    msg = torch.empty_like(like) if role == 0 else None
+    nat.check(nat.lib().mx_bits_front(
+        nat.dev_of(like), _words(bits), role, n, _p(xa), _p(xb), _p(arecv), _p(msg), _p(z),
+        _p(p0), _p(p1), _slots_arr(slots), _nonces_arr((n1, ng)), nat.stream_of(like)),
+        "bits_front")
+    return msg, z, p0, p1
+
+
+def bits_b2a(phase, role, src, start, count, bits, slots, n1, ng, arecv=None, state=None):
+    """B2A of bit planes start.. of a boolean sharing (src = (s0, s1, g0, g1, t0, t1) torch
+    data of one party; g = None: s are the sum words), phases 0 / 1 / 2 (bits_party.h).
+    Phases 0 / 1 return state (msg, z, base0, base1); phase 2 (state + the received z in
+    ``arecv``) returns the result pair [count, ...]."""
+    like = next(t for t in src if t is not None) if src is not None else state[1]
+    per = tuple(like.shape[:-1] if bits == 128 else like.shape) if src is not None else None
+    if phase == 2:
+        msg, z, b0, b1 = state
+        S = z.numel() // (2 if bits == 128 else 1) // count
+        o0, o1 = torch.empty_like(z), torch.empty_like(z)
+        nat.check(nat.lib().mx_bits_b2a(
+            nat.dev_of(z), _words(bits), 2, role, S, start, count, None, None, None, _p(z),
+            _p(b0), _p(b1), _p(arecv), _p(o0), _p(o1), _slots_arr(slots), _nonces_arr((n1, ng)),
+            nat.stream_of(z)), "bits_b2a")
+        return o0, o1
+    S = math.prod(per)
+    shp = (count,) + per + ((2,) if bits == 128 else ())
+    z, b0, b1 = (torch.empty(shp, dtype=torch.int64, device=like.device) for _ in range(3))
+    msg = torch.empty_like(z) if role == 0 else None
+    srcs = (ctypes.c_void_p * 6)(*[_p(t) for t in src])
+    nat.check(nat.lib().mx_bits_b2a(
+        nat.dev_of(like), _words(bits), phase, role, S, start, count, srcs, _p(arecv), _p(msg),
+        _p(z), _p(b0), _p(b1), None, None, None, _slots_arr(slots), _nonces_arr((n1, ng)),
+        nat.stream_of(like)), "bits_b2a")
+    return msg, z, b0, b1

@@ -311,9 +311,19 @@ def mux(sess, s, x, y):
     return rep.mux(sess, s, x, y)
 
 
+# the sign of a fixed(i, f) value is bit i + f of its ring element (|x| < 2^i): per-party
+# sessions run the sign's adder over those low bits only (MOOSEX_SIGN_WIDTH=0: all bits)
+SIGN_WIDTH = os.environ.get("MOOSEX_SIGN_WIDTH", "1") != "0"
+
+
+def _value_width(x: RepFixed):
+    w = x.integ + x.frac + 1
+    return w if SIGN_WIDTH and 2 < w < x.bits else None
+
+
 def sign_bit(sess, x: RepFixed) -> RepTensor:
     """Arithmetic 0/1 sharing of [x < 0]."""
-    return rep.less_than_zero_arith(sess, x.t)
+    return rep.less_than_zero_arith(sess, x.t, width=_value_width(x))
 
 
 def relu(sess, x: RepFixed) -> RepFixed:
@@ -620,7 +630,9 @@ def _exp2_parts(sess, a: RepFixed, negative: bool):
     merged = (negative and not getattr(sess, "is_simulated", True)
               and getattr(sess, "party_dot_trunc", None) is not None
               and hasattr(sess, "p_cross_plain") and npad >= 2 and npad & (npad - 1) == 0)
-    bd = rep.bit_decompose(sess, a.t)
+    # only bits below f + nint are read with a nonzero weight (higher planes are padding
+    # whose factor is 1 whatever the bit): the adder need not carry beyond them
+    bd = rep.bit_decompose(sess, a.t, width=f + nint if SIGN_WIDTH and f + nint < bits else None)
     ab = rep.b2a_planes(sess, bd, 0, f + npad, bits)  # arithmetic bits, leading axis
     frac_w = [(1 << j) for j in range(f)] + [0] * npad
     r = RepFixed(_weighted(sess, ab, frac_w, bits), f, integ)

@@ -63,6 +63,43 @@ class RepTensor:
         return "Add" if self.kind == "arith" else "Xor"
 
 
+class RawBits(RepTensor):
+    """A boolean sharing of packed words held, for one party of a per-party session, as the
+    Kogge-Stone adder's raw state ``raw`` = (p0, p1, g0, g1, t0, t1) (parallel/spmd.py
+    p_bit_decompose): the sum words p ^ ((g ^ t) << 1) are computed when first read, and the
+    B2A of bit planes reads the raw state directly (no sum kernel)."""
+
+    def __init__(self, plc, bits, s0, s1, raw):
+        self.raw = raw
+        super().__init__(plc, bits, "bool", s0, s1)
+
+    def _sum(self):
+        if self._s0 is None:
+            p0, p1, g0, g1, t0, t1 = self.raw
+            zero0 = t0 if t0 is not None else R.zeros(g0.shape, g0.bits, g0.device)
+            zero1 = t1 if t1 is not None else R.zeros(g1.shape, g1.bits, g1.device)
+            o0, o1 = R.ks_sum2(p0, p1, g0, g1, zero0, zero1)
+            self._s0, self._s1 = PV(self.plc, o0), PV(self.plc, o1)
+
+    @property
+    def s0(self):
+        self._sum()
+        return self._s0
+
+    @s0.setter
+    def s0(self, v):
+        self._s0 = v
+
+    @property
+    def s1(self):
+        self._sum()
+        return self._s1
+
+    @s1.setter
+    def s1(self, v):
+        self._s1 = v
+
+
 class DeferredRep(RepTensor):
     """A product whose last reshare round has not run (parallel/party.py ``RoundB``): the
     shares are completed when first read, and a reveal to the dealer P2 merges that round
@@ -715,14 +752,20 @@ def trunc_pr(sess, x: RepTensor, m: int, out=None) -> RepTensor:
 # ---------------------------------------------------------------------------
 # bit decomposition & comparisons (packed boolean words)
 # ---------------------------------------------------------------------------
-def bit_decompose(sess, x: RepTensor) -> RepTensor:
+def bit_decompose(sess, x: RepTensor, width=None) -> RepTensor:
     """Arithmetic sharing of x in Z_2^k -> boolean sharing of its k bits packed in one
     word.  y = x_0 + x_1 is boolean-shared by P0, x_2 is a trivial boolean sharing
-    (slot 2), and a packed Kogge-Stone adder computes y + x_2 (log2 k AND rounds)."""
+    (slot 2), and a packed Kogge-Stone adder computes y + x_2 (log2 k AND rounds).
+    ``width``: only the low ``width`` bits are needed (the caller knows |x| < 2^(width-1)
+    or reads no higher bit); a per-party session then runs ceil(log2(width - 1)) levels."""
     with span("rep.bit_decompose"):
         plc, bits = x.plc, x.bits
         whole = getattr(sess, "p_bit_decompose", None)
-        r = whole(plc, x) if whole is not None and x.kind == "arith" else None
+        r = None
+        if whole is not None and x.kind == "arith":
+            r = whole(plc, x) if width is None else whole(plc, x, width=width)
+        if isinstance(r, RepTensor):  # a per-party session's raw adder state
+            return r
         if r is not None:  # every step below in one kernel (same nonces, same shares)
             return RepTensor(plc, bits, "bool", r[0], r[1])
         o = plc.owners
@@ -847,11 +890,15 @@ def msb(sess, x: RepTensor) -> RepTensor:
     return bit_extract(sess, bd, x.bits - 1)
 
 
-def less_than_zero_arith(sess, x: RepTensor) -> RepTensor:
+def less_than_zero_arith(sess, x: RepTensor, width=None) -> RepTensor:
     """Arithmetic 0/1 sharing of [x < 0]: b2a of the sign bit (one kernel for the whole of
-    it on a stacked device session, same shares)."""
+    it on a stacked device session, same shares).  ``width``: |x| < 2^(width - 1) is known
+    (a fixed-point type's bound), so the sign is bit width - 1 -- a per-party session's
+    adder then spans only the low ``width`` bits (fewer rounds)."""
     f = getattr(sess, "p_sign_arith", None)
-    r = f(x.plc, x) if f is not None and x.kind == "arith" else None
+    r = None
+    if f is not None and x.kind == "arith":
+        r = f(x.plc, x) if width is None else f(x.plc, x, width=width)
     if r is not None:
         return RepTensor(x.plc, x.bits, "arith", r[0], r[1])
     return b2a(sess, msb(sess, x), x.bits)

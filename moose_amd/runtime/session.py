@@ -445,13 +445,14 @@ class StackedSession(Session):
         self.stats.record_round(_nbytes(r[0]))
         return PV(plc, r[0]), PV(plc, r[1])
 
-    def p_sign_arith(self, plc, x):
+    def p_sign_arith(self, plc, x, width=None):
         """rep.b2a(rep.msb(x)) in one kernel: p_bit_decompose's work, then the top bit's
         b2a (its sharing nonces n1', na' and product nonce nmul' after the decomposition's,
-        as the two protocol steps draw them).  None -> the steps."""
+        as the two protocol steps draw them).  ``width`` (a bound on the value's bits) is
+        not needed here: the whole-word chain is one kernel.  None -> the steps."""
         return self.p_bit_decompose(plc, x, sign=True)
 
-    def p_bit_decompose(self, plc, x, sign=False):
+    def p_bit_decompose(self, plc, x, sign=False, width=None):
         """The whole of rep.bit_decompose in one kernel (device, fused session, latency
         sizes): the nonces in the generic order (share: n1, na; the adder's AND: nmul; one
         per level) and the same traffic records, so the same shares.  None -> the steps."""
