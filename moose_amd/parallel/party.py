@@ -223,3 +223,52 @@ def jobs_tail(sess, plc, role, jobs, L, bits, m, nonces, slots):
         sess.stats.record_send(plc.owners[a], plc.owners[b], nb)
     sess.stats.record_round(2 * nb)
 
+
+
+class MulAddTail:
+    """a * b + c for replicated a, b, c on a per-party session with the product's reshare
+    pending (protocols/replicated.py mul_add_deferred): this party holds z, its zero-shared
+    3-out-of-3 share of a * b.  :meth:`finish` is the reshare (z -> P_{p-1}) and the add;
+    :meth:`reveal_to` opens a * b + c to a member P_j in ONE round instead of the reshare
+    round plus the reveal: P_{j+1} sends z_{j+1} + c_{j+2}, P_{j+2} sends z_{j+2} + c_j
+    (each its own z plus its second component), P_j sums z_j + c_{j+1} + both."""
+
+    def __init__(self, sess, plc, z, c0, c1, bits):
+        self.sess, self.plc, self.z, self.c0, self.c1, self.bits = sess, plc, z, c0, c1, bits
+        self.done = False
+        self.rep = None  # the DeferredRep whose shares finish() completes
+
+    def finish(self):
+        if self.done:
+            return
+        self.done = True
+        from moose_amd.runtime.session import PV
+
+        zn = self.sess.shift(PV(self.plc, self.z), 1).v
+        o0, o1 = R.binary2("add", self.z, self.c0, zn, self.c1)
+        self.rep._s0, self.rep._s1 = PV(self.plc, o0), PV(self.plc, o1)
+
+    def reveal_to(self, host):
+        """The opened value at ``host`` (an Opened of four addends), None elsewhere; None
+        when ``host`` is not a member (the caller finishes and reveals generically)."""
+        plc = self.plc
+        if host not in plc.owners:
+            return False
+        self.done = True
+        sess = self.sess
+        j = plc.owners.index(host)
+        idx = sess.party_index(plc)
+        like = (tuple(self.z.data.shape), self.z.data.dtype) if idx is not None else None
+        mine = None
+        if idx is not None and idx != j:
+            mine = R.binary("add", self.z, self.c1).data  # z + this party's second component
+        got = sess.party_exchange(plc, [("m1", (j + 1) % 3, j, mine if idx == (j + 1) % 3 else None,
+                                         like),
+                                        ("m2", (j + 2) % 3, j, mine if idx == (j + 2) % 3 else None,
+                                         like)])
+        nb = self.z.data.numel() * self.z.data.element_size() if idx is not None else 0
+        for a in ((j + 1) % 3, (j + 2) % 3):
+            sess.stats.record_send(plc.owners[a], host, nb)
+        if idx != j:
+            return None
+        return R.opened(self.z, self.c1, R.RT(got["m1"], self.bits), R.RT(got["m2"], self.bits))

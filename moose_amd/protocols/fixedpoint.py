@@ -1007,7 +1007,8 @@ def sigmoid(sess, x: RepFixed) -> RepFixed:
     """sigma(x) = 1 / (1 + e^-|x|) mirrored for x < 0; 1 + e^-|x| is in [1, 2] so the
     reciprocal needs no normalisation."""
     s = sign_bit(sess, x)
-    if _jobs_ok(sess, x.t, s):
+    party = _jobs_ok(sess, x.t, s)
+    if party:
         # per-party: |x| / ln 2 in one tail (_abs_scaled_jobs), one round fewer
         e = _exp2_parts(sess, _abs_scaled_jobs(sess, s, x, 1.0 / math.log(2.0)), negative=True)
     else:
@@ -1017,12 +1018,31 @@ def sigmoid(sess, x: RepFixed) -> RepFixed:
     # 1/d = (1/h) / 2 with h = d / 2 in [0.5, 1]: the fit of 1/h evaluated at d directly
     # (coefficients c_k / 2^k), and both halvings folded into TruncPrs of one more bit --
     # no round spent on multiplying by 0.5
-    w = poly_eval(sess, d, tuple(c / (1 << k)
-                                 for k, c in enumerate(_fit("recip", 0.5, 1.0, 4))))  # ~ 1/h
-    hw = mul(sess, d, w, f=d.frac + 1)  # h w
-    pos = mul(sess, w, const_sub(sess, 2.0, hw), f=w.frac + 1)  # one Newton step, halved
+    if party and RECIP_DIRECT and d.frac >= 36:
+        # one party per process (rounds cost messages): a degree-8 fit of 1/h (max error
+        # 4.4e-7 on [0.5, 1], 2.2e-7 on the probability) has three power levels -- 8 rounds
+        # instead of 10 for the degree-4 fit and its Newton step.  Its coefficients alternate
+        # up to ~700 (sum of magnitudes ~2600), so it needs the fractional bits to absorb that
+        # cancellation: below 36 the Newton form is more accurate
+        pos = poly_eval(sess, d, tuple(c / (1 << k) for k, c in
+                                       enumerate(_fit("recip", 0.5, 1.0, 8))), shift=1)
+    else:
+        w = poly_eval(sess, d, tuple(c / (1 << k)
+                                     for k, c in enumerate(_fit("recip", 0.5, 1.0, 4))))
+        hw = mul(sess, d, w, f=d.frac + 1)  # h w
+        pos = mul(sess, w, const_sub(sess, 2.0, hw), f=w.frac + 1)  # one Newton step, halved
+    if party:
+        # sigma = pos + s (1 - 2 pos); the product's reshare waits for the reader (a reveal
+        # absorbs it: parallel/party.py MulAddTail)
+        diff = rep.lincomb(sess, [(-2, pos.t)], const=_encode_const(sess, 1.0, pos.frac,
+                                                                      pos.bits))
+        return _with(pos, rep.mul_add(sess, s, diff, pos.t))
     one_minus = const_sub(sess, 1.0, pos)
     return _with(pos, rep.mux(sess, s, one_minus.t, pos.t))
+
+
+# per-party sessions evaluate the sigmoid's reciprocal as one degree-8 polynomial
+RECIP_DIRECT = os.environ.get("MOOSEX_RECIP_DIRECT", "1") != "0"
 
 
 def softmax(sess, x: RepFixed, axis: int, upmost_index: int) -> RepFixed:

@@ -928,6 +928,17 @@ def equal(sess, x: RepTensor, y: RepTensor) -> RepTensor:
     return equal_zero(sess, sub(sess, x, y))
 
 
+def mul_add(sess, a: RepTensor, b: RepTensor, c: RepTensor) -> RepTensor:
+    """a * b + c.  On a per-party session the product's reshare round is deferred until the
+    shares are read -- a reveal of the result absorbs it (one round fewer)."""
+    f = getattr(sess, "p_mul_add_deferred", None)
+    if f is not None:
+        r = f(a.plc, a, b, c)
+        if r is not None:
+            return r
+    return add(sess, mul(sess, a, b), c)
+
+
 def mux(sess, s: RepTensor, x: RepTensor, y: RepTensor) -> RepTensor:
     """s ? x : y ; s is an arithmetic 0/1 sharing or a boolean bit sharing."""
     if s.kind == "bool":
@@ -937,7 +948,7 @@ def mux(sess, s: RepTensor, x: RepTensor, y: RepTensor) -> RepTensor:
         r = f(x.plc, s, x, y)  # the three steps in one kernel (same nonce, same shares)
         if r is not None:
             return RepTensor(x.plc, x.bits, "arith", r[0], r[1])
-    return add(sess, mul(sess, s, sub(sess, x, y)), y)
+    return mul_add(sess, s, sub(sess, x, y), y)
 
 
 def negate_where(sess, s: RepTensor, x: RepTensor) -> RepTensor:

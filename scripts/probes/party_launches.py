@@ -17,6 +17,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--depth", type=int, default=3)
     ap.add_argument("--party", default="alice")
+    ap.add_argument("--batch", type=int, default=16)
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -29,6 +30,7 @@ def main():
 
     tls = threading.local()
     acc = collections.defaultdict(collections.Counter)
+    rounds = collections.Counter()
     order = []
 
     def stack():
@@ -44,9 +46,19 @@ def main():
             if len(s) >= a.depth:
                 return fn(*args, **kw)
             s.append(f"{mod}.{name}")
+            key = tuple(s)
+            sess = args[0] if args else None
+            st = getattr(sess, "stats", None)
+            mine = threading.current_thread().name == f"moose-party-{a.party}"
+            r0 = st.rounds if st is not None else 0
             try:
                 return fn(*args, **kw)
             finally:
+                if st is not None and mine:
+                    if key not in acc:
+                        order.append(key)
+                        acc[key]  # noqa: B018 - create the row
+                    rounds[key] += st.rounds - r0
                 s.pop()
         return w
 
@@ -95,18 +107,19 @@ def main():
     torch.Tensor.copy_ = copy_
 
     ids = ["alice", "bob", "carole"]
-    tm = logistic_regression_tutorial(16)
+    tm = logistic_regression_tutorial(a.batch)
     rt = LocalMooseRuntime(ids, device_map={i: "cpu" for i in ids}, seed=1)
     r = list(rt.evaluate_computation(tm.computation, {"x": tm.x_test}).values())[0]
     err = float(np.abs(np.asarray(r) - tm.proba).max())
     total = sum(sum(c.values()) for c in acc.values())
-    print(f"# launches of party {a.party} per LR evaluation: {total} (err {err:.1e})\n")
-    print("| step | launches | by kernel |\n|---|---|---|")
+    print(f"# launches of party {a.party} per LR evaluation: {total} (err {err:.1e}); "
+          f"rounds {rt.last_stats.rounds}\n")
+    print("| step | rounds (incl.) | launches | by kernel |\n|---|---|---|---|")
     for key in order:
         c = acc[key]
         ind = "&nbsp;" * 4 * (len(key) - 1)
         top = ", ".join(f"{k.replace('mx_', '')} {v}" for k, v in c.most_common())
-        print(f"| {ind}{key[-1]} | {sum(c.values())} | {top} |")
+        print(f"| {ind}{key[-1]} | {rounds[key]} | {sum(c.values())} | {top} |")
 
 
 if __name__ == "__main__":
