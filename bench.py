@@ -326,11 +326,37 @@ def _link_probe(comm, world, rank, device, prog, dists, mib, reps=3):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return round(len(ds) * nbytes / t.item() / 1e9, 2)
 
+    def latency(d, nb, tick, reps=25):
+        """Median time of ONE grouped exchange of ``nb`` bytes to rank + d / from rank - d
+        (the shape of one protocol round), synchronised on both sides; max over ranks."""
+        s = torch.full((max(1, nb // 8),), rank, dtype=torch.int64, device=device)
+        b = torch.empty_like(s)
+        ts = []
+        for r in range(reps + 2):
+            prog.tick(tick)
+            dist.barrier(device_ids=bdev)
+            if device.type == "cuda":
+                torch.cuda.synchronize(device)
+            t0 = time.perf_counter()
+            comm.exchange([(s, (rank + d) % world)], [(b, (rank - d) % world)])
+            if device.type == "cuda":
+                torch.cuda.synchronize(device)
+            if r >= 2:
+                ts.append(time.perf_counter() - t0)
+        ts.sort()
+        t = torch.tensor([ts[len(ts) // 2]], dtype=torch.float64, device=tdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return round(t.item() * 1e6, 1)
+
     rec = {"mib": mib, "reps": reps, "backend": dist.get_backend(),
-           "gbs_per_rank_and_direction": {}}
+           "gbs_per_rank_and_direction": {}, "exchange_latency_us_p50": {}}
     for i, d in enumerate(dists):
         rec["gbs_per_rank_and_direction"][f"d{d}"] = timed([d], i)
     rec["gbs_per_rank_and_direction"]["all"] = timed(list(dists), len(dists))
+    # small messages: the LR inference's rounds carry 2-4 KB per message
+    for i, d in enumerate(dists):
+        for nb in (8, 4096, 65536):
+            rec["exchange_latency_us_p50"][f"d{d}_{nb}B"] = latency(d, nb, 100 + i)
     return rec
 
 
@@ -454,6 +480,7 @@ def _lr_stacked(runs, device, world=1):
 
 
 def _lr_spmd(runs, world, rank, device, prog):
+    os.environ.setdefault("MOOSEX_TAPE_TIMING", "1")  # per-round device time in the record
     """The tutorial model with one party per GPU (ranks 3s, 3s+1, 3s+2 = alice, bob,
     carole of session s): every reshare, dealer message and reveal an RCCL send/recv.
     Latency of an evaluation = max over its three ranks; p50 over ``runs``.  Two modes:
@@ -526,9 +553,18 @@ def _lr_spmd(runs, world, rank, device, prog):
             if mode == "tape":
                 m["replayed"] = tape is not None and tape.replays >= runs
                 if tape is not None and tape.issue_s:
-                    iss = sorted(tape.issue_s)
-                    m["host_issue_ms_p50"] = iss[len(iss) // 2] * 1e3
+                    med = lambda xs: sorted(xs)[len(xs) // 2]  # noqa: E731
+                    m["host_issue_ms_p50"] = med(tape.issue_s) * 1e3
                     m["tape_rounds"], m["tape_segments"] = tape.rounds, tape.segments
+                    # where a replay's time goes: host time inside the message rounds, and
+                    # (timed replays) the tape stream's time in them -- all rounds and the
+                    # longest -- so p50 ~ rounds x per-round latency + kernel time checks out
+                    m["comm_host_ms_p50"] = med(tape.comm_host_s) * 1e3
+                    if tape.round_device_ms:
+                        m["rounds_device_ms_p50"] = med(tape.round_device_ms)
+                        m["round_device_max_ms_p50"] = med(tape.round_device_max_ms)
+                        m["per_round_device_us"] = med(tape.round_device_ms) * 1e3 / max(
+                            1, tape.rounds)
             if rank % 3 == 1:  # bob holds the opened probabilities
                 m["max_abs_err_vs_sklearn"] = float(
                     np.abs(np.asarray(list(got.values())[0]) - tm.proba).max())

@@ -149,6 +149,12 @@ class SPMDTape:
         self.segments = len(self.steps) - self.rounds
         self.replays = 0
         self.issue_s = []  # host time per replay spent issuing (graphs + message calls)
+        self.comm_host_s = []  # host time per replay inside the message rounds
+        # per replay, with MOOSEX_TAPE_TIMING=1: the tape stream's time inside the message
+        # rounds (events around each round: transfer + waiting for the peers), summed and
+        # the longest round -- p50 ~ rounds x round latency + kernel time, from the record
+        self.timing = os.environ.get("MOOSEX_TAPE_TIMING") == "1"
+        self.round_device_ms, self.round_device_max_ms = [], []
         if seed is None:  # unseeded replays draw their keys on the device (keys.py)
             self.keys.enable_device_refresh()
         self._pinned = {}  # argument name -> pinned host staging buffer
@@ -209,21 +215,42 @@ class SPMDTape:
             issue = 0.0
             tr = self.tr
             staged = tr.stage
+            timing = self.timing and self.device.type == "cuda"
+            evs = []
+            comm_host = 0.0
             for s in self.steps:
                 t0 = time.perf_counter()
                 if isinstance(s, CommStep):
+                    if timing:
+                        e0 = torch.cuda.Event(enable_timing=True)
+                        e0.record(self.stream)
                     s.run(tr)
+                    if timing:
+                        e1 = torch.cuda.Event(enable_timing=True)
+                        e1.record(self.stream)
+                        evs.append((e0, e1))
+                    dt = time.perf_counter() - t0
+                    comm_host += dt
                     if not staged:  # a staged (gloo) round's time is host copies, not issue
-                        issue += time.perf_counter() - t0
+                        issue += dt
                 else:
                     s.replay()
                     issue += time.perf_counter() - t0
             self.issue_s.append(issue)
+            self.comm_host_s.append(comm_host)
             self.replays += 1
             out = self._decode(self.interp, self.sess, self.outs)
-        end = getattr(tr, "end_evaluation", None)
-        if end is not None:
-            end()
+            if timing:  # the decode synchronised the tape stream: the events are complete
+                ms = [a.elapsed_time(b) for a, b in evs]
+                self.round_device_ms.append(sum(ms))
+                self.round_device_max_ms.append(max(ms) if ms else 0.0)
+            # every send-only round of this replay confirmed ON THE TAPE STREAM: under RCCL
+            # a send's completion wait is a stream dependency, so the next replay's
+            # kernels -- which rewrite the static buffers those sends read -- are ordered
+            # after them by the tape itself, not by a caller's device-wide synchronize
+            end = getattr(tr, "end_evaluation", None)
+            if end is not None:
+                end()
         return out
 
 

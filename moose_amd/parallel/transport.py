@@ -398,6 +398,8 @@ class Transport:
             ops.append(dist.P2POp(dist.irecv, buf, src, group=self.group))
         if self._unwaited:
             self.reap()  # a failed earlier send surfaces at the sender's next round
+        if self.fault is not None and self.fault[0] == "delay":
+            time.sleep(self.fault[1])  # test-only: this rank joins every round late
         if self.fault is not None and self.fault[0] == "exit":
             self._sends += 1
             if self._sends == self.fault[1]:

@@ -113,6 +113,7 @@ class GraphPlan:
                  lanes=None):
         self.comp = comp
         self.device = torch.device(device)
+        self.seed = seed
         self.ring = fixedpoint_ring
         self.storage = storage
         self.static = {}
@@ -236,7 +237,10 @@ class GraphPlan:
                 # pinned buffer followed by a blit (0.321 ms; profiles/r3_graphs_vs_eager.md)
                 src = torch.from_numpy(np.ascontiguousarray(a).reshape(t.shape))
                 t.copy_(src if src.dtype == t.dtype else src.to(t.dtype))
-        self.keys.refresh(self.keys.n)  # fresh randomness for this replay (the used slots)
+        if self.seed is None:
+            self.keys.refresh(self.keys.n)  # fresh randomness for this replay (used slots)
+        else:  # a seeded evaluation: the seeded session's keys, as the eager run draws them
+            self.keys.refresh_seeded(self.seed)
         for g in self.graphs:
             g.replay()
         self.replays += 1

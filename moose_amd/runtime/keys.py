@@ -79,6 +79,7 @@ class KeyTable:
         self.n = 0
         self.frozen = False
         self._rand = random_bytes or os.urandom
+        self.allocs = []  # (base, n) of the allocations made while frozen, in order
 
     def alloc(self, n: int) -> int:
         base = self.n
@@ -94,6 +95,8 @@ class KeyTable:
         self.n = base + n
         if not self.frozen:
             self._write(base, [self._rand(16) for _ in range(n)])
+        else:
+            self.allocs.append((base, n))  # a replay refills these slots (refresh_seeded)
         return base
 
     def _write(self, base: int, keys):
@@ -115,6 +118,16 @@ class KeyTable:
         n = self.capacity if upto is None else upto
         raw = os.urandom(16 * n)
         self._write(0, [raw[16 * i:16 * i + 16] for i in range(n)])
+
+    def refresh_seeded(self, seed: int):
+        """The keys a fresh session seeded with ``seed`` draws, in the slots its allocations
+        get (the frozen table's recorded allocations): a replay of a seeded evaluation then
+        uses exactly the eager evaluation's keys (bitwise-equal replays)."""
+        rng = torch.Generator().manual_seed(seed)
+        for base, n in self.allocs:
+            self._write(base, [bytes(torch.randint(0, 256, (16,), generator=rng,
+                                                   dtype=torch.uint8).tolist())
+                               for _ in range(n)])
 
     def enable_device_refresh(self):
         """Draw the keys of later :meth:`refresh_device` calls on the device: a master key

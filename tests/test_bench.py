@@ -73,6 +73,10 @@ def test_bench_self_launch(n, layout, sessions):
         assert min(d["p2p_bytes_per_step"]) > 0 and d["step_streams"] == 2
         # after the headline: point-to-point GB/s of the layout's exchange pattern
         assert all(v > 0 for v in d["link_probe"]["gbs_per_rank_and_direction"].values())
+        # small-message latency of one grouped exchange per distance (8 B, 4 KB, 64 KB)
+        lat = d["link_probe"]["exchange_latency_us_p50"]
+        assert len(lat) == 3 * (len(d["link_probe"]["gbs_per_rank_and_direction"]) - 1)
+        assert all(v > 0 for v in lat.values())
 
 
 def test_bench_lr_inference_in_line():

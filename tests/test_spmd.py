@@ -308,3 +308,68 @@ def test_spmd_tape_replay_bitwise_equal_eager():
     issue = [e[3][2] for e in got[0][2:]]
     print(f"tape rounds {got[0][3][3][0]}, host issue per replay (rank 0) "
           f"{[round(i * 1e3, 3) for i in issue]} ms")
+
+
+def _tape_async_worker(rank, port, q):
+    """Back-to-back replays with send-only rounds left in flight (MOOSEX_ASYNC_SENDS=1) and a
+    late receiver (MOOSEX_FAULT delay on rank 2): no synchronize between the replays; the
+    eager references are computed afterwards."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MOOSEX_ASYNC_SENDS="1",
+                      MOOSEX_FAULT="delay:0.02@2")
+    dist.init_process_group("gloo", rank=rank, world_size=3)
+    from moose_amd.models.predictors.tutorial import logistic_regression_tutorial
+    from moose_amd.parallel import spmd_graphs
+    from moose_amd.parallel.spmd import SPMDSession
+    from moose_amd.parallel.transport import Transport
+    from moose_amd.runtime.interpreter import Interpreter
+    from moose_amd.runtime.local import to_native
+
+    dev = torch.device("cuda:0")
+    tm = logistic_regression_tutorial(128)
+    comp = to_native(tm.computation, 128)
+    roles = {"alice": 0, "bob": 1, "carole": 2}
+    me = ("alice", "bob", "carole")[rank]
+    tr = Transport(rank, 3, dev, plans=True)
+    assert tr.async_sends
+    rng = np.random.default_rng(1)
+    xs = [tm.x_test + rng.normal(0, 0.1, tm.x_test.shape) for _ in range(6)]
+    outs, modes = [], []
+    for x in xs:  # back to back: the tape orders itself, nothing synchronises the device
+        r = spmd_graphs.evaluate(comp, {"x": x}, me, roles, tr, dev, {}, 128, seed=7)
+        modes.append("eager" if r is None else "tape")
+        if r is None:
+            sess = SPMDSession(me, roles, tr, dev, seed=7)
+            interp = Interpreter(sess, {}, fixedpoint_ring=128)
+            o = interp.run(comp, {"x": x})
+            r = ({k: interp.to_numpy(v) for k, v in o.items() if sess.materialized(v.v)},)
+        outs.append({k: np.asarray(v) for k, v in r[0].items()})
+    same = []
+    for x, got in zip(xs, outs):
+        sess = SPMDSession(me, roles, tr, dev, seed=7)
+        interp = Interpreter(sess, {}, fixedpoint_ring=128)
+        o = interp.run(comp, {"x": x})
+        want = {k: interp.to_numpy(v) for k, v in o.items() if sess.materialized(v.v)}
+        same.append(all(np.array_equal(np.asarray(got[k]), np.asarray(want[k])) for k in want))
+    q.put((rank, (modes, same)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_spmd_tape_replays_self_ordering_with_async_sends():
+    """SPMD tape replays carry their own ordering -- each replay waits for
+    its send-only rounds on the tape stream -- so back-to-back replays with sends left in
+    flight and a late receiver stay bitwise equal to fresh seeded eager evaluations."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_tape_async_worker, args=(r, port, q)) for r in range(3)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(3))
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, (modes, same) in got.items():
+        assert modes == ["eager", "tape", "tape", "tape", "tape", "tape"], (rank, modes)
+        assert all(same), (rank, same)
