@@ -93,4 +93,17 @@ MX_HD inline T sum_bit(T p, T g, T t, int q) {
   return v;
 }
 
+// the bit plane of B2A row ``row``: plane start + row; with ``xbit`` >= 0 the rows before the
+// last are XORed (locally, share-wise) with plane xbit and the last row IS plane xbit -- the
+// planes of |x| (up to one ulp) and the sign bit of a two's-complement x from ONE adder
+MX_HD inline void plane_of(int row, int start, int count, int xbit, int* q, int* xq) {
+  if (xbit >= 0 && row == count - 1) {
+    *q = xbit;
+    *xq = -1;
+  } else {
+    *q = start + row;
+    *xq = xbit;
+  }
+}
+
 }  // namespace mxb

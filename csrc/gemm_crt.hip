@@ -45,6 +45,7 @@
 #include "moosex.h"
 
 void mx_ws_note(int dev, int64_t want, bool ok);  // gemm_mfma.hip: workspace bookkeeping
+void mx_ws_shared_note(void);
 
 namespace {
 
@@ -1195,14 +1196,15 @@ struct Ws {
   bool used = false;
 };
 std::mutex g_mu;
-constexpr int kWsPerDev = 8;
+constexpr int kWsPerDev = 128;
 Ws g_ws[16][kWsPerDev];
 
 // Grow-only scratch per (device, stream): GEMMs issued on different streams (dataflow lanes,
-// pipelined steps) may run concurrently and must not share residue buffers.  Up to
-// kWsPerDev streams per device get their own; further streams share the last slot (their
-// work is then ordered only by the caller).  Replaced buffers are retired, never freed (a
-// captured graph may hold them).
+// pipelined steps, the in-process parties' graphs replayed concurrently) may run at the same
+// time and must not share residue buffers.  kWsPerDev exceeds the streams a process can hold
+// (PyTorch's pools: 32 per priority, plus the null stream); past it streams would share the
+// last slot (ordered only by the caller) -- counted, mx_workspace_shared_count.  Replaced
+// buffers are retired, never freed (a captured graph may hold them).
 void* workspace(int64_t bytes, hipStream_t st) {
   int dev = 0;
   hipGetDevice(&dev);
@@ -1217,7 +1219,10 @@ void* workspace(int64_t bytes, hipStream_t st) {
       slot->used = true;
       slot->stream = st;
     }
-  if (!slot) slot = &g_ws[dev][kWsPerDev - 1];
+  if (!slot) {
+    slot = &g_ws[dev][kWsPerDev - 1];
+    mx_ws_shared_note();
+  }
   Ws& w = *slot;
   if (w.bytes < bytes) {
     int64_t want = 1 << 20;

@@ -790,6 +790,12 @@ bool use_split_kernel() {
 // (reported by the Python wrapper when a GEMM returns -4) and the bytes held per device.
 std::atomic<int64_t> g_ws_failed{0};
 std::atomic<int64_t> g_ws_held[16];
+std::atomic<int64_t> g_ws_shared{0};
+
+void mx_ws_shared_note(void) { ++g_ws_shared; }
+
+// lookups that found every per-stream slot taken and fell back to a shared one (0 expected)
+extern "C" int64_t mx_workspace_shared_count(void) { return g_ws_shared.load(); }
 
 void mx_ws_note(int dev, int64_t want, bool ok) {
   if (ok) {
@@ -817,7 +823,7 @@ struct Workspace {
   bool used = false;
 };
 std::mutex g_ws_mu;
-constexpr int kWsPerDev = 8;
+constexpr int kWsPerDev = 128;
 Workspace g_ws[16][kWsPerDev];
 
 // Grow-only scratch per (device, stream) -- see gemm_crt.hip workspace(): concurrent GEMMs
@@ -837,7 +843,10 @@ void* get_workspace(int64_t bytes, hipStream_t st) {
       slot->used = true;
       slot->stream = st;
     }
-  if (!slot) slot = &g_ws[dev][kWsPerDev - 1];
+  if (!slot) {
+    slot = &g_ws[dev][kWsPerDev - 1];
+    mx_ws_shared_note();
+  }
   Workspace& w = *slot;
   if (w.bytes < bytes) {
     int64_t want = 1 << 20;

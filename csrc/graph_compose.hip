@@ -85,6 +85,79 @@ int mx_graph_compose(int n, const int* kind, void* const* child, void* const* ds
   return 0;
 }
 
+void* mx_party_kernel_fn(int which);  // party_graph.hip
+
+// One party's replay as ONE graph, a chain of n nodes (threads.py PartyTapes, per-party
+// streams): kind 0 = a child graph (child[i]); 5 = advance the party's replay counter
+// (p0 = counter); 6 = push messages (p0 = PushDesc table, i0 = entries, i64 = largest
+// message bytes, p1 = counter); 7 = wait for flags (p0 = flags, i0 = count, p1 = counter,
+// p2 = error word).
+int mx_graph_build_chain(int n, const int* kind, void* const* child, void* const* p0,
+                         void* const* p1, void* const* p2, const int* i0, const int64_t* i64,
+                         void** graph_out, void** exec_out) {
+  if (n < 1) return -2;
+  hipGraph_t g = nullptr;
+  if (hipGraphCreate(&g, 0) != hipSuccess) return -3;
+  hipGraphNode_t prev = nullptr;
+  for (int i = 0; i < n; ++i) {
+    hipGraphNode_t node = nullptr;
+    const size_t nd = prev ? 1 : 0;
+    hipError_t rc = hipSuccess;
+    if (kind[i] == 0) {
+      size_t count = 0;
+      if (hipGraphGetNodes((hipGraph_t)child[i], nullptr, &count) == hipSuccess && count == 0)
+        rc = hipGraphAddEmptyNode(&node, g, &prev, nd);
+      else
+        rc = hipGraphAddChildGraphNode(&node, g, &prev, nd, (hipGraph_t)child[i]);
+    } else {
+      void* a0 = p0[i];
+      void* a1 = p1[i];
+      void* a2 = p2[i];
+      int cnt = i0[i];
+      hipKernelNodeParams kp = {};
+      kp.sharedMemBytes = 0;
+      kp.extra = nullptr;
+      void* args3[] = {&a0, &cnt, &a1};
+      void* args4[] = {&a0, &cnt, &a1, &a2};
+      void* args1[] = {&a0};
+      if (kind[i] == 5) {
+        kp.func = mx_party_kernel_fn(0);
+        kp.gridDim = dim3(1);
+        kp.blockDim = dim3(64);
+        kp.kernelParams = args1;
+      } else if (kind[i] == 6) {
+        kp.func = mx_party_kernel_fn(1);
+        int gx = (int)((i64[i] + 4095) / 4096);
+        kp.gridDim = dim3(gx < 1 ? 1 : gx, cnt < 1 ? 1 : cnt);
+        kp.blockDim = dim3(256);
+        kp.kernelParams = args3;
+      } else if (kind[i] == 7) {
+        kp.func = mx_party_kernel_fn(2);
+        kp.gridDim = dim3(1);
+        kp.blockDim = dim3(256);
+        kp.kernelParams = args4;
+      } else {
+        hipGraphDestroy(g);
+        return -4;
+      }
+      rc = hipGraphAddKernelNode(&node, g, &prev, nd, &kp);
+    }
+    if (rc != hipSuccess) {
+      hipGraphDestroy(g);
+      return -10 - i;
+    }
+    prev = node;
+  }
+  hipGraphExec_t ex = nullptr;
+  if (hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) != hipSuccess) {
+    hipGraphDestroy(g);
+    return -5;
+  }
+  *graph_out = (void*)g;
+  *exec_out = (void*)ex;
+  return 0;
+}
+
 int mx_graph_launch(void* exec, void* stream) {
   return hipGraphLaunch((hipGraphExec_t)exec, (hipStream_t)stream) == hipSuccess ? 0 : -1;
 }

@@ -155,6 +155,7 @@ int64_t mx_gemm_workspace_bytes(int words, int64_t batch, int64_t M, int64_t N,
 // workspace bytes on the calling device (every stream's grow-only scratch).
 int64_t mx_workspace_failed_bytes(void);
 int64_t mx_workspace_held_bytes(void);
+int64_t mx_workspace_shared_count(void);
 // GEMM variant using caller-provided device workspace (graph-capture friendly)
 int mx_gemm_ws(int words, int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
                const void* A1, const void* B0, const void* B1, int mode, void* C,
@@ -346,7 +347,7 @@ int mx_bits_front(int dev, int words, int role, int64_t n, const void* xa, const
                   const void* arecv, void* msg, void* z, void* p0, void* p1,
                   const uint32_t* const* slots, const uint64_t* nonces, void* stream);
 int mx_bits_b2a(int dev, int words, int phase, int role, int64_t S, int start, int count,
-                const void* const* src, const void* arecv, void* msg, void* z, void* base0,
+                int xbit, const void* const* src, const void* arecv, void* msg, void* z, void* base0,
                 void* base1, const void* zr, void* out0, void* out1,
                 const uint32_t* const* slots, const uint64_t* nonces, void* stream);
 

@@ -91,9 +91,111 @@ __global__ void __launch_bounds__(256) k_copy_many(const CopyDesc* __restrict__ 
   }
 }
 
+// ---- per-party graphs on separate streams / devices: device-side message signalling ----
+// A party's replay is ONE graph on its own stream (or GPU); a message is pushed by the
+// SENDER's graph into the receiver's landing buffer, then a flag is raised; the receiver's
+// graph waits for the flag before the segment that reads the buffer.  The flags carry the
+// replay number (each graph's first node advances its party's counter; all counters move
+// in lock step), so no flag needs resetting and no graph waits on another's launch order.
+struct PushDesc {
+  const uint8_t* src;
+  uint8_t* dst;
+  int64_t bytes;
+  uint32_t* flag;     // the receiver's flag of this message (its memory)
+  uint32_t* pieces;   // blocks of this message done (reset by the last one)
+};
+
+__global__ void __launch_bounds__(64) k_epoch_step(uint64_t* __restrict__ epoch) {
+  if (threadIdx.x == 0) *epoch = *epoch + 1;
+}
+
+// grid (pieces, messages): copy, then the message's last block raises the flag
+__global__ void __launch_bounds__(256)
+    k_push(const PushDesc* __restrict__ d, int n, const uint64_t* __restrict__ epoch) {
+  const int m = blockIdx.y;
+  if (m >= n) return;
+  const PushDesc c = d[m];
+  const int64_t lo = (int64_t)blockIdx.x * kPiece;
+  const int64_t hi = lo + kPiece < c.bytes ? lo + kPiece : c.bytes;
+  if (lo < c.bytes) {
+    const bool vec = ((((uintptr_t)c.src) | ((uintptr_t)c.dst)) & 15) == 0;
+    if (vec) {
+      const int64_t v0 = lo / 16, v1 = hi / 16;
+      for (int64_t i = v0 + threadIdx.x; i < v1; i += blockDim.x)
+        ((uint4*)c.dst)[i] = ((const uint4*)c.src)[i];
+      for (int64_t i = v1 * 16 + threadIdx.x; i < hi; i += blockDim.x) c.dst[i] = c.src[i];
+    } else {
+      for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) c.dst[i] = c.src[i];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();  // this block's bytes before the count / the flag
+    const uint32_t npieces = (uint32_t)gridDim.x;
+    const uint32_t done = atomicAdd(c.pieces, 1u) + 1u;
+    if (done == npieces) {
+      __hip_atomic_store(c.pieces, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence_system();
+      __hip_atomic_store(c.flag, (uint32_t)*epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+// one workgroup: thread i < n waits for flag i to reach this replay's number; bounded --
+// after ~kMaxPolls polls it records the flag index in err (read by the host) and returns, so
+// a lost message ends the replay instead of holding the GPU
+constexpr uint32_t kMaxPolls = 1u << 22;
+
+__global__ void __launch_bounds__(256)
+    k_wait(const uint32_t* __restrict__ flags, int n, const uint64_t* __restrict__ epoch,
+           uint32_t* __restrict__ err) {
+  const uint32_t want = (uint32_t)*epoch;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    uint32_t polls = 0;
+    while (__hip_atomic_load(flags + i, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != want) {
+      if (++polls >= kMaxPolls) {
+        __hip_atomic_store(err, 1u + (uint32_t)i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+}
+
 }  // namespace
 
 extern "C" {
+
+void* mx_party_kernel_fn(int which) {
+  switch (which) {
+    case 0:
+      return (void*)k_epoch_step;
+    case 1:
+      return (void*)k_push;
+    case 2:
+      return (void*)k_wait;
+    default:
+      return nullptr;
+  }
+}
+
+// Peer access from device dev to device peer's memory (the push kernels' writes into another
+// GPU's landing buffers and flags); already enabled is fine.
+int mx_enable_peer(int dev, int peer) {
+  int can = 0;
+  if (hipDeviceCanAccessPeer(&can, dev, peer) != hipSuccess || !can) return -1;
+  int cur = 0;
+  hipGetDevice(&cur);
+  hipSetDevice(dev);
+  hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+  hipSetDevice(cur);
+  if (e == hipErrorPeerAccessAlreadyEnabled) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return e == hipSuccess ? 0 : -2;
+}
 
 int mx_key_refresh(void* slots, int n, const void* master, void* epoch, void* stream) {
   if (n <= 0) return 0;

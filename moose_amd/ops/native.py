@@ -67,6 +67,7 @@ _SIGS = {
     "mx_gemm_workspace_bytes": (c_i64, [c_int, c_i64, c_i64, c_i64, c_i64, c_int]),
     "mx_workspace_failed_bytes": (c_i64, []),
     "mx_workspace_held_bytes": (c_i64, []),
+    "mx_workspace_shared_count": (c_i64, []),
     "mx_mfma_peak": (c_int, [c_int, c_int, c_vp, c_vp]),
     "mx_gemm_ws": (
         c_int,
@@ -219,6 +220,9 @@ _SIGS = {
     "mx_stream_destroy": (c_int, [c_vp]),
     "mx_graph_compose": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mx_graph_launch": (c_int, [c_vp, c_vp]),
+    "mx_enable_peer": (c_int, [c_int, c_int]),
+    "mx_graph_build_chain": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                     c_vp]),
     "mx_jobs_r0": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_int,
                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mx_jobs_r1": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp,
@@ -226,7 +230,8 @@ _SIGS = {
     "mx_jobs_r2": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp]),
     "mx_bits_front": (c_int, [c_int, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                               c_vp, c_vp, c_vp, c_vp]),
-    "mx_bits_b2a": (c_int, [c_int, c_int, c_int, c_int, c_i64, c_int, c_int, c_vp, c_vp, c_vp,
+    "mx_bits_b2a": (c_int, [c_int, c_int, c_int, c_int, c_i64, c_int, c_int, c_int, c_vp, c_vp,
+                            c_vp,
                             c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mx_key_refresh": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp]),
     "mx_key_refresh_host": (None, [c_vp, c_u64, c_int, c_vp]),

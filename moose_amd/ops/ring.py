@@ -2133,11 +2133,13 @@ def bits_front(role, xa, xb, arecv, bits, slots, n1, ng):
     return msg, z, p0, p1
 
 
-def bits_b2a(phase, role, src, start, count, bits, slots, n1, ng, arecv=None, state=None):
+def bits_b2a(phase, role, src, start, count, bits, slots, n1, ng, arecv=None, state=None,
+             xbit=-1):
     """B2A of bit planes start.. of a boolean sharing (src = (s0, s1, g0, g1, t0, t1) torch
     data of one party; g = None: s are the sum words), phases 0 / 1 / 2 (bits_party.h).
-    Phases 0 / 1 return state (msg, z, base0, base1); phase 2 (state + the received z in
-    ``arecv``) returns the result pair [count, ...]."""
+    ``xbit`` >= 0: rows 0..count-2 are planes start.. XORed with plane xbit, the last row is
+    plane xbit (bits_party.h plane_of).  Phases 0 / 1 return state (msg, z, base0, base1);
+    phase 2 (state + the received z in ``arecv``) returns the result pair [count, ...]."""
     like = next(t for t in src if t is not None) if src is not None else state[1]
     per = tuple(like.shape[:-1] if bits == 128 else like.shape) if src is not None else None
     if phase == 2:
@@ -2145,7 +2147,7 @@ def bits_b2a(phase, role, src, start, count, bits, slots, n1, ng, arecv=None, st
         S = z.numel() // (2 if bits == 128 else 1) // count
         o0, o1 = torch.empty_like(z), torch.empty_like(z)
         nat.check(nat.lib().mx_bits_b2a(
-            nat.dev_of(z), _words(bits), 2, role, S, start, count, None, None, None, _p(z),
+            nat.dev_of(z), _words(bits), 2, role, S, start, count, xbit, None, None, None, _p(z),
             _p(b0), _p(b1), _p(arecv), _p(o0), _p(o1), _slots_arr(slots), _nonces_arr((n1, ng)),
             nat.stream_of(z)), "bits_b2a")
         return o0, o1
@@ -2155,7 +2157,8 @@ def bits_b2a(phase, role, src, start, count, bits, slots, n1, ng, arecv=None, st
     msg = torch.empty_like(z) if role == 0 else None
     srcs = (ctypes.c_void_p * 6)(*[_p(t) for t in src])
     nat.check(nat.lib().mx_bits_b2a(
-        nat.dev_of(like), _words(bits), phase, role, S, start, count, srcs, _p(arecv), _p(msg),
+        nat.dev_of(like), _words(bits), phase, role, S, start, count, xbit, srcs, _p(arecv),
+        _p(msg),
         _p(z), _p(b0), _p(b1), None, None, None, _slots_arr(slots), _nonces_arr((n1, ng)),
         nat.stream_of(like)), "bits_b2a")
     return msg, z, b0, b1

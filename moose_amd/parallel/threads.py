@@ -372,7 +372,10 @@ class PartyTapes:
         n = len(identities)
         role_ranks = {r: i for i, r in enumerate(identities)}
         # every party on one device: the tapes are composed into ONE graph (below)
-        single = (len(set(self.devices)) == 1
+        # per-party graphs on their own streams / devices with device-side message flags
+        # (_build_streams): MOOSEX_PARTY_STREAMS=1
+        self.streams_mode = os.environ.get("MOOSEX_PARTY_STREAMS") == "1"
+        single = (len(set(self.devices)) == 1 and not self.streams_mode
                   and os.environ.get("MOOSEX_PARTY_GRAPH", "1") != "0")
         self.tapes = []
         for i, ident in enumerate(identities):
@@ -381,7 +384,8 @@ class PartyTapes:
             with torch.cuda.device(self.devices[i]):
                 self.tapes.append(SPMDTape(comp, arguments, ident, role_ranks, tr,
                                            self.devices[i], storage, ring, seed,
-                                           warm=warm[ident], keep_graph=single))
+                                           warm=warm[ident],
+                                           keep_graph=single or self.streams_mode))
         self.streams = [t.stream for t in self.tapes]
         self._copy_streams = {}
         self.actions = self._schedule()
@@ -391,6 +395,7 @@ class PartyTapes:
         self.issue_s = []
         self.issue_parts = []
         self._composed = self._compose() if single else None
+        self._party_graphs = self._build_streams() if self.streams_mode else None
 
     def _compose(self):
         """The schedule as ONE hipGraph (csrc/graph_compose.hip) in a total order: each
@@ -462,6 +467,137 @@ class PartyTapes:
                             "copy_batches": kinds.count(2)}
         return ex
 
+    def _build_streams(self):
+        """Every party's replay as ONE graph on its own stream (its own GPU when the parties
+        are on several): its segments in program order and, at each message round, a PUSH
+        node -- the round's payloads copied into the receivers' landing buffers (peer writes
+        over xGMI across GPUs), then each message's flag raised to the replay number -- and a
+        WAIT node for the flags of the round's receives (csrc/party_graph.hip).  The graphs
+        depend on each other only through the flags in device memory, so they are launched
+        independently (no host issue per message, no launch order) and run concurrently.
+        Returns the per-party (graph, exec) handles, or None when the runtime declines."""
+        import ctypes
+
+        from moose_amd.ops import native as nat
+        from moose_amd.parallel.transport import CommStep
+
+        n = len(self.tapes)
+        # the k-th message from party a to party b is the k-th receive at b from a
+        land, flag_of, nflags = {}, {}, [0] * n
+        for q, tape in enumerate(self.tapes):
+            cnt = {}
+            for st in tape.steps:
+                if isinstance(st, CommStep):
+                    for buf, src in st.recvs:
+                        k = cnt.get(src, 0)
+                        cnt[src] = k + 1
+                        land[(src, q, k)] = buf
+                        flag_of[(src, q, k)] = nflags[q]
+                        nflags[q] += 1
+        for p in range(n):
+            for q in range(n):
+                if p != q and self.devices[p] != self.devices[q]:
+                    nat.check(nat.lib().mx_enable_peer(self.devices[p].index,
+                                                       self.devices[q].index), "peer access")
+        self._flags = [torch.zeros(max(1, nflags[q]), dtype=torch.int32, device=self.devices[q])
+                       for q in range(n)]
+        self._epochs = [torch.zeros(1, dtype=torch.int64, device=d) for d in self.devices]
+        self._errs = [torch.zeros(1, dtype=torch.int32, device=d) for d in self.devices]
+        self._tables = []
+        handles = []
+        for p, tape in enumerate(self.tapes):
+            dev = self.devices[p]
+            kinds, child, p0, p1, p2, i0, i64 = [], [], [], [], [], [], []
+
+            def node(kind, ch=0, a=0, b=0, c=0, cnt=0, big=0):
+                kinds.append(kind)
+                child.append(ch)
+                p0.append(a)
+                p1.append(b)
+                p2.append(c)
+                i0.append(cnt)
+                i64.append(big)
+
+            epoch = self._epochs[p].data_ptr()
+            node(5, a=epoch)
+            sent = {}
+            fbase = 0
+            for st in tape.steps:
+                if not isinstance(st, CommStep):
+                    node(0, ch=st.raw_cuda_graph())
+                    continue
+                if st.sends:
+                    rows = []
+                    pieces = torch.zeros(len(st.sends), dtype=torch.int32, device=dev)
+                    for j, (t, dst) in enumerate(st.sends):
+                        k = sent.get(dst, 0)
+                        sent[dst] = k + 1
+                        buf = land[(p, dst, k)]
+                        if t.numel() != buf.numel() or t.dtype != buf.dtype:
+                            from moose_amd.runtime.graphs import CaptureError
+
+                            raise CaptureError(f"message {k} from party {p} to {dst}: sizes "
+                                               "differ")
+                        flag = self._flags[dst].data_ptr() + 4 * flag_of[(p, dst, k)]
+                        rows.append((t.data_ptr(), buf.data_ptr(),
+                                     t.numel() * t.element_size(), flag,
+                                     pieces.data_ptr() + 4 * j))
+                    flat = [x - (1 << 64) if x >= (1 << 63) else x for r in rows for x in r]
+                    table = torch.tensor(flat, dtype=torch.int64, device=dev)
+                    self._tables += [table, pieces]
+                    node(6, a=table.data_ptr(), b=epoch, cnt=len(rows),
+                         big=max(r[2] for r in rows))
+                if st.recvs:
+                    node(7, a=self._flags[p].data_ptr() + 4 * fbase, b=epoch,
+                         c=self._errs[p].data_ptr(), cnt=len(st.recvs))
+                    fbase += len(st.recvs)
+            m = len(kinds)
+            arr = lambda ty, xs: (ty * max(1, len(xs)))(*xs)  # noqa: E731
+            g, ex = ctypes.c_void_p(), ctypes.c_void_p()
+            with torch.cuda.device(dev):
+                rc = nat.lib().mx_graph_build_chain(
+                    m, arr(ctypes.c_int, kinds), arr(ctypes.c_void_p, child),
+                    arr(ctypes.c_void_p, p0), arr(ctypes.c_void_p, p1), arr(ctypes.c_void_p, p2),
+                    arr(ctypes.c_int, i0), arr(ctypes.c_int64, i64), ctypes.byref(g),
+                    ctypes.byref(ex))
+            if rc != 0:
+                for gh, eh in handles:
+                    nat.lib().mx_graph_free(gh, eh)
+                return None
+            handles.append((g, ex))
+        self.graph_nodes = {"per_party_nodes": [len(t.steps) for t in self.tapes]}
+        return handles
+
+    def _replay_streams(self, arguments: dict) -> Dict[str, dict]:
+        """One graph launch per party on its own stream, after its arguments and keys."""
+        import time
+
+        from moose_amd.ops import native as nat
+
+        t0 = time.perf_counter()
+        for p, tape in enumerate(self.tapes):
+            s = self.streams[p]
+            with torch.cuda.device(self.devices[p]), torch.cuda.stream(s):
+                tape.copy_arguments(arguments)
+                tape._fill_keys()
+                nat.check(nat.lib().mx_graph_launch(self._party_graphs[p][1], s.cuda_stream),
+                          "party graph launch")
+        self.issue_s.append(time.perf_counter() - t0)
+        out = {}
+        for p, tape in enumerate(self.tapes):
+            with torch.cuda.device(self.devices[p]), torch.cuda.stream(self.streams[p]):
+                out[self.identities[p]] = tape._decode(tape.interp, tape.sess, tape.outs)
+                tape.replays += 1
+        for p in range(len(self.tapes)):
+            self.streams[p].synchronize()
+        errs = [int(e.item()) for e in self._errs]
+        if any(errs):
+            from moose_amd.parallel.transport import TransportError
+
+            raise TransportError(f"party graphs: a message never arrived (flags {errs}); the "
+                                 "replay is void")
+        return out
+
     def _schedule_rounds(self):
         """The tapes as a round-synchronous total order: every party runs its segments up to
         its next round, then the messages of all parties whose round can complete (every
@@ -523,12 +659,15 @@ class PartyTapes:
         return acts
 
     def __del__(self):
+        hs = list(getattr(self, "_party_graphs", None) or [])
         h = getattr(self, "_graph_handles", None)
         if h is not None:
+            hs.append(h)
+        for g, ex in hs:
             try:
                 from moose_amd.ops import native as nat
 
-                nat.lib().mx_graph_free(h[0], h[1])
+                nat.lib().mx_graph_free(g, ex)
             except Exception:  # noqa: BLE001 - interpreter shutdown
                 pass
 
@@ -594,6 +733,8 @@ class PartyTapes:
     def replay(self, arguments: dict) -> Dict[str, dict]:
         import time
 
+        if self._party_graphs is not None:
+            return self._replay_streams(arguments)
         if self._composed is not None:
             return self._replay_composed(arguments)
         n = len(self.tapes)

@@ -634,6 +634,13 @@ def _exp2_parts(sess, a: RepFixed, negative: bool):
     # whose factor is 1 whatever the bit): the adder need not carry beyond them
     bd = rep.bit_decompose(sess, a.t, width=f + nint if SIGN_WIDTH and f + nint < bits else None)
     ab = rep.b2a_planes(sess, bd, 0, f + npad, bits)  # arithmetic bits, leading axis
+    return _exp2_from_planes(sess, ab, f, integ, bits, nint, npad, negative, merged)
+
+
+def _exp2_from_planes(sess, ab: RepTensor, f: int, integ: int, bits: int, nint: int,
+                      npad: int, negative: bool, merged: bool) -> RepFixed:
+    """2^a (2^-a) from the arithmetic bit planes ``ab`` of a >= 0 at ``f`` fractional bits:
+    rows 0..f-1 the fraction, rows f..f+npad-1 the integer part (rows from nint on weigh 0)."""
     frac_w = [(1 << j) for j in range(f)] + [0] * npad
     r = RepFixed(_weighted(sess, ab, frac_w, bits), f, integ)
     if negative:
@@ -1006,9 +1013,16 @@ def exp_nonpositive(sess, x: RepFixed) -> RepFixed:
 def sigmoid(sess, x: RepFixed) -> RepFixed:
     """sigma(x) = 1 / (1 + e^-|x|) mirrored for x < 0; 1 + e^-|x| is in [1, 2] so the
     reciprocal needs no normalisation."""
-    s = sign_bit(sess, x)
-    party = _jobs_ok(sess, x.t, s)
-    if party:
+    one = _sign_and_exp_party(sess, x) if _jobs_ok(sess, x.t) else None
+    if one is not None:
+        s, e = one
+        party = True
+    else:
+        s = sign_bit(sess, x)
+        party = _jobs_ok(sess, x.t, s)
+    if one is not None:
+        pass
+    elif party:
         # per-party: |x| / ln 2 in one tail (_abs_scaled_jobs), one round fewer
         e = _exp2_parts(sess, _abs_scaled_jobs(sess, s, x, 1.0 / math.log(2.0)), negative=True)
     else:
@@ -1043,6 +1057,44 @@ def sigmoid(sess, x: RepFixed) -> RepFixed:
 
 # per-party sessions evaluate the sigmoid's reciprocal as one degree-8 polynomial
 RECIP_DIRECT = os.environ.get("MOOSEX_RECIP_DIRECT", "1") != "0"
+# per-party sessions take the sigmoid's sign and e^-|x| from one bit decomposition
+ONE_DECOMPOSITION = os.environ.get("MOOSEX_SIGMOID_ONE_BITDEC", "1") != "0"
+ONE_DEC_WIDTH = True  # False (tests): its adder over all bits, as the generic steps
+
+def _sign_and_exp_party(sess, x: RepFixed):
+    """(s, e^-|x|) for a per-party session from ONE bit decomposition: z = x * C with C =
+    log2(e) at ``fc`` fractional bits is a LOCAL product (no truncation: z keeps f + fc
+    fractional bits, |z| < 2^(integ + 1 + f + fc)); its planes XORed with its sign plane are
+    the planes of |z| (up to one unit of z's last bit: ~z = -z - 1), so one adder gives the
+    sign s (arithmetic, for the final mirror) and, from the planes at and above f + fc - f,
+    |z| floored to f fractional bits -- the input of 2^-a (_exp2_from_planes).  Replaces the
+    sign's decomposition, the |x| / ln 2 tail and the second decomposition (8 + 2 + 8 rounds
+    become 9 for the tutorial LR).  The floor differs from TruncPr's rounding by < 2^-f.
+    None when the ring has too few bits for fc >= 20 (the caller uses the three steps)."""
+    if not (ONE_DECOMPOSITION and SIGN_WIDTH) or getattr(sess, "is_simulated", True):
+        return None
+    f, integ, bits = x.frac, x.integ, x.bits
+    fc = min(f, bits - 3 - integ - f)
+    if fc < 20:
+        return None
+    F = f + fc
+    q = integ + 1 + F  # the sign plane: |z| < 2^(q)
+    nint = max(1, min(bits - 2 - f, integ + 1))
+    npad = 1 << (nint - 1).bit_length()
+    if F + npad > bits:
+        npad = nint
+    if q > bits - 1 or F + nint > q:
+        return None
+    C = int(round(math.log2(math.e) * (1 << fc)))
+    z = rep.lincomb(sess, [(C, x.t)])
+    bd = rep.bit_decompose(sess, z, width=q + 1 if ONE_DEC_WIDTH else None)
+    ab = rep.b2a_planes_xor(sess, bd, F - f, f + npad, q, bits)  # f + npad planes, then s
+    rows = local(sess, ab, "Slice", slice=(0, f + npad, None))
+    s = local(sess, ab, "IndexAxis", axis=0, index=f + npad)
+    merged = (getattr(sess, "party_dot_trunc", None) is not None
+              and hasattr(sess, "p_cross_plain") and npad >= 2 and npad & (npad - 1) == 0)
+    e = _exp2_from_planes(sess, rows, f, integ, bits, nint, npad, True, merged)
+    return s, e
 
 
 def softmax(sess, x: RepFixed, axis: int, upmost_index: int) -> RepFixed:

@@ -884,6 +884,25 @@ def b2a_planes(sess, b: RepTensor, start: int, count: int, ring_bits: int) -> Re
     return b2a(sess, planes, ring_bits)
 
 
+def b2a_planes_xor(sess, b: RepTensor, start: int, count: int, xbit: int,
+                   ring_bits: int) -> RepTensor:
+    """b2a of bit planes start..start+count-1 of a packed boolean sharing, each XORed with
+    plane ``xbit``, followed by plane ``xbit`` itself: count + 1 rows on a new leading axis.
+    With xbit the sign of a two's-complement x, the rows are the planes of |x| (exactly:
+    ~x = -x - 1 for x < 0, so off by one unit of bit 0) and the sign -- ONE decomposition
+    serves both (the XOR is local on boolean shares).  One round pair on a per-party session
+    (parallel/spmd.py p_b2a_planes_xor, same shares); BitSplit + Xor + Concat + b2a otherwise."""
+    f = getattr(sess, "p_b2a_planes_xor", None)
+    r = f(b.plc, b, start, count, xbit, ring_bits) if f is not None else None
+    if r is not None:
+        return RepTensor(b.plc, ring_bits, "arith", r[0], r[1])
+    planes = _sharewise(sess, "BitSplit", b.plc, (b.s0, b.s1), start=start, count=count)
+    sgn = _sharewise(sess, "BitSplit", b.plc, (b.s0, b.s1), start=xbit, count=1)
+    xored = _sharewise(sess, "Xor", b.plc, planes, sgn)
+    both = [sess.p("Concat", b.plc, xored[i], sgn[i], axis=0) for i in range(2)]
+    return b2a(sess, RepTensor(b.plc, 1, "bool", both[0], both[1]), ring_bits)
+
+
 def msb(sess, x: RepTensor) -> RepTensor:
     """Boolean sharing of the sign bit."""
     bd = bit_decompose(sess, x)

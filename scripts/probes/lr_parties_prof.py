@@ -53,16 +53,18 @@ def main():
         rec["graph_nodes"] = getattr(t, "graph_nodes", None)
         import time as _t
         # the device time of one replay alone (launch -> synchronize), no decode
-        ts = []
-        for _ in range(10):
-            torch.cuda.synchronize()
-            t0 = _t.perf_counter()
-            from moose_amd.ops import native as nat
-            s = t.streams[0]
-            nat.lib().mx_graph_launch(t._composed, s.cuda_stream)
-            s.synchronize()
-            ts.append((_t.perf_counter() - t0) * 1e3)
-        rec["graph_only_ms_p50"] = sorted(ts)[5]
+        if t._composed is not None:
+            ts = []
+            for _ in range(10):
+                torch.cuda.synchronize()
+                t0 = _t.perf_counter()
+                from moose_amd.ops import native as nat
+                s = t.streams[0]
+                nat.lib().mx_graph_launch(t._composed, s.cuda_stream)
+                s.synchronize()
+                ts.append((_t.perf_counter() - t0) * 1e3)
+            rec["graph_only_ms_p50"] = sorted(ts)[5]
+        rec["streams_mode"] = t._party_graphs is not None
     print(json.dumps(rec), flush=True)
 
 

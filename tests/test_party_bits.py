@@ -13,11 +13,12 @@ from moose_amd.runtime.local import LocalMooseRuntime
 IDS = ["alice", "bob", "carole"]
 
 
-def _lr(device, monkeypatch, bits_on, width_on):
+def _lr(device, monkeypatch, bits_on, width_on, one_dec=False):
     from moose_amd.models.predictors.tutorial import logistic_regression_tutorial
 
     monkeypatch.setenv("MOOSEX_PARTY_BITS", "1" if bits_on else "0")
     monkeypatch.setattr(FP, "SIGN_WIDTH", width_on)
+    monkeypatch.setattr(FP, "ONE_DECOMPOSITION", one_dec)
     tm = logistic_regression_tutorial(16)
     rt = LocalMooseRuntime(IDS, device_map={i: device for i in IDS}, seed=5, use_graphs=False)
     r = np.asarray(list(rt.evaluate_computation(tm.computation, {"x": tm.x_test}).values())[0])
@@ -39,6 +40,55 @@ def test_width_bound_saves_adder_levels(device, monkeypatch):
     # sign (fixed(24, 40): bit 64) and exp's integer bits (below 65): 6 levels each, not 7
     assert r_narrow == r_full - 2
     assert e_narrow < 1e-6 and e_full < 1e-6
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_one_decomposition_sigmoid_fused_equals_generic(device, monkeypatch):
+    """The sigmoid's sign and e^-|x| from one adder: the fused B2A with the sign-plane XOR
+    (bits_party.h plane_of) gives bitwise the generic BitSplit + Xor + Concat + b2a shares."""
+    monkeypatch.setattr(FP, "ONE_DEC_WIDTH", False)  # both adders over all bits
+    fused, r_fused, e = _lr(device, monkeypatch, True, True, one_dec=True)
+    generic, r_gen, _ = _lr(device, monkeypatch, False, True, one_dec=True)
+    assert np.array_equal(fused, generic)
+    assert r_fused == r_gen and e < 1e-6
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_one_decomposition_sigmoid_saves_rounds(device, monkeypatch):
+    three, r_three, e_three = _lr(device, monkeypatch, True, True, one_dec=False)
+    one, r_one, e_one = _lr(device, monkeypatch, True, True, one_dec=True)
+    # sign adder and B2A (7-8) + |x| / ln 2 tail (2) + exp adder and B2A (7-8) -> one adder
+    # and B2A (7-9): 10 rounds fewer for this model's fixed(14, 23)
+    assert r_one <= r_three - 9
+    assert e_one < 1e-6 and e_three < 1e-6
+    assert np.abs(one - three).max() < 1e-6
+
+
+def test_b2a_planes_xor_rows_are_abs_and_sign():
+    """Generic b2a_planes_xor on a stacked session: rows = planes of |x| (x >= 0) or of
+    |x| - 1 (x < 0) from the given start, then the sign plane."""
+    import torch
+
+    from moose_amd.ir.computation import ReplicatedPlacement
+    from moose_amd.ops import ring as R
+    from moose_amd.protocols import replicated as rep
+    from moose_amd.runtime.session import HV
+    from moose_amd.runtime.session import StackedSession
+
+    sess = StackedSession("cpu", seed=3)
+    plc = ReplicatedPlacement(("a", "b", "c"))
+    vals = [5, -5, 0, 123456, -123456, 1]
+    raw = torch.tensor([v % (1 << 64) - (1 << 64) if v % (1 << 64) >= (1 << 63) else v
+                        for v in vals], dtype=torch.int64)
+    x = rep.share(sess, plc, HV("a", R.RT(raw, 64)))
+    bd = rep.bit_decompose(sess, x)
+    ab = rep.b2a_planes_xor(sess, bd, 2, 20, 63, 64)
+    got = rep.reveal(sess, ab, "c").v.data.numpy()
+    assert got.shape == (21, len(vals))
+    for j, v in enumerate(vals):
+        a = abs(v) if v >= 0 else abs(v) - 1
+        assert [int(got[r][j]) for r in range(20)] == [(a >> (r + 2)) & 1 for r in range(20)]
+        assert int(got[20][j]) == (1 if v < 0 else 0)
 
 
 def test_sign_bit_width_bound_is_exact_on_the_boundary(monkeypatch):

@@ -160,16 +160,17 @@ def test_thread_parties_lr_inference_gpu(monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["serial", "copy-per-message", "per-action"])
+@pytest.mark.parametrize("mode", ["serial", "copy-per-message", "per-action", "streams"])
 def test_thread_party_tapes_replay_bitwise_equal_eager(mode, monkeypatch):
     """Seeded sessions: a replay re-draws the seeded keys as a fresh eager evaluation does,
     so every replay's outputs equal the eager ones bitwise (parties on cuda:0): the tapes
     composed into one hipGraph in a round-synchronous total order (default on one device:
     each round's messages one batched copy kernel, or one copy node per message), and the
     per-action replay."""
-    composed = mode != "per-action"
+    composed = mode not in ("per-action", "streams")
     monkeypatch.setenv("MOOSEX_PARTY_GRAPH", "1" if composed else "0")
     monkeypatch.setenv("MOOSEX_PARTY_COPY_BATCH", "0" if mode == "copy-per-message" else "1")
+    monkeypatch.setenv("MOOSEX_PARTY_STREAMS", "1" if mode == "streams" else "0")
     comp = _comp(False)
     args = _args()
     devs = {i: "cuda:0" for i in IDS}
@@ -184,6 +185,7 @@ def test_thread_party_tapes_replay_bitwise_equal_eager(mode, monkeypatch):
     (c, tapes), = rt._party_tapes.values()
     assert tapes is not False and tapes.tapes[0].replays == 2
     assert (tapes._composed is not None) == composed
+    assert (tapes._party_graphs is not None) == (mode == "streams")
 
 
 def test_party_tapes_schedule_pairs_rounds():
