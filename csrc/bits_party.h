@@ -93,16 +93,28 @@ MX_HD inline T sum_bit(T p, T g, T t, int q) {
   return v;
 }
 
-// the bit plane of B2A row ``row``: plane start + row; with ``xbit`` >= 0 the rows before the
-// last are XORed (locally, share-wise) with plane xbit and the last row IS plane xbit -- the
-// planes of |x| (up to one ulp) and the sign bit of a two's-complement x from ONE adder
-MX_HD inline void plane_of(int row, int start, int count, int xbit, int* q, int* xq) {
-  if (xbit >= 0 && row == count - 1) {
-    *q = xbit;
-    *xq = -1;
-  } else {
+// the bit plane of B2A row ``row``: plane start + row of element block 0.  With ``xbit`` >= 0
+// the rows before the last ``blocks`` are XORed (locally, share-wise) with plane xbit of block
+// 0 -- the planes of |x| up to one ulp -- and the last rows are sign planes (plane xbit):
+// blocks == 1: the sign of x (block 0); blocks == 3 (the adder ran over x, x - T, x + T):
+// NOT sign(x - T) = [x >= T], sign(x + T) = [x < -T], then sign(x).  ``neg``: the row is
+// the complement (boolean NOT: share component 0 flipped).
+MX_HD inline void plane_of(int row, int start, int count, int xbit, int blocks, int* q, int* xq,
+                           int* blk, int* neg) {
+  *blk = 0;
+  *neg = 0;
+  const int tail = xbit >= 0 ? blocks : 0;
+  if (row < count - tail) {
     *q = start + row;
     *xq = xbit;
+    return;
+  }
+  *q = xbit;
+  *xq = -1;
+  const int k = row - (count - tail);  // 0 .. tail - 1
+  if (tail == 3) {
+    *blk = k == 0 ? 1 : (k == 1 ? 2 : 0);
+    *neg = k == 0;
   }
 }
 

@@ -347,7 +347,7 @@ int mx_bits_front(int dev, int words, int role, int64_t n, const void* xa, const
                   const void* arecv, void* msg, void* z, void* p0, void* p1,
                   const uint32_t* const* slots, const uint64_t* nonces, void* stream);
 int mx_bits_b2a(int dev, int words, int phase, int role, int64_t S, int start, int count,
-                int xbit, const void* const* src, const void* arecv, void* msg, void* z, void* base0,
+                int xbit, int blocks, const void* const* src, const void* arecv, void* msg, void* z, void* base0,
                 void* base1, const void* zr, void* out0, void* out1,
                 const uint32_t* const* slots, const uint64_t* nonces, void* stream);
 

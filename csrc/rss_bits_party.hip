@@ -76,7 +76,7 @@ __device__ __forceinline__ T src_bit(const T* s, const T* g, const T* t, int64_t
 
 template <class T>
 __global__ void __launch_bounds__(256)
-    k_b2a(int phase, int role, int64_t S, int start, int count, int xbit,
+    k_b2a(int phase, int role, int64_t S, int start, int count, int xbit, int blocks,
           const T* __restrict__ s0,
           const T* __restrict__ s1, const T* __restrict__ g0, const T* __restrict__ g1,
           const T* __restrict__ t0, const T* __restrict__ t1, const T* __restrict__ arecv,
@@ -105,18 +105,20 @@ __global__ void __launch_bounds__(256)
       if (i >= n) break;
       const int lc = q / P, j = q % P;
       const int64_t row = i / S, e = i - row * S;
-      int qbit, xq;
-      mxb::plane_of((int)row, start, count, xbit, &qbit, &xq);
+      int qbit, xq, blk, neg;
+      mxb::plane_of((int)row, start, count, xbit, blocks, &qbit, &xq, &blk, &neg);
+      const int64_t es = e + blk * S;  // the element in the adder's blocks
       const int o = role == 1 ? 0 : 1;
       const T fa = role == 1 ? (T)0 : mxd::pick<T>(kl[0][lc], kh[0][lc], j);
       const T fo = mxd::pick<T>(kl[o][lc], kh[o][lc], j);
       const T fn = mxd::pick<T>(kl[o + 1][lc], kh[o + 1][lc], j);
-      T c0 = role == 1 ? (T)0 : src_bit<T>(s0, g0, t0, e, qbit);
-      T c1 = role == 2 ? (T)0 : src_bit<T>(s1, g1, t1, e, qbit);
+      T c0 = role == 1 ? (T)0 : src_bit<T>(s0, g0, t0, es, qbit);
+      T c1 = role == 2 ? (T)0 : src_bit<T>(s1, g1, t1, es, qbit);
       if (xq >= 0) {  // share-wise XOR with plane xq (local on boolean shares)
-        if (role != 1) c0 ^= src_bit<T>(s0, g0, t0, e, xq);
-        if (role != 2) c1 ^= src_bit<T>(s1, g1, t1, e, xq);
+        if (role != 1) c0 ^= src_bit<T>(s0, g0, t0, es, xq);
+        if (role != 2) c1 ^= src_bit<T>(s1, g1, t1, es, xq);
       }
+      if (neg && role == 0) c0 ^= (T)1;  // NOT: component 0 (P0's first) flipped
       const mxb::B2a<T> r = mxb::b2a<T>(role, c0, c1, role == 1 ? arecv[i] : (T)0, fa, fo, fn);
       if (role == 0) msg[i] = r.msg;
       z[i] = r.z;
@@ -179,7 +181,7 @@ int mxh_bits_front(int words, int role, int64_t n, const void* xa, const void* x
 }
 
 int mxh_bits_b2a(int words, int phase, int role, int64_t S, int start, int count, int xbit,
-                 const void* const* src, const void* arecv, void* msg, void* z, void* base0,
+                 int blocks, const void* const* src, const void* arecv, void* msg, void* z, void* base0,
                  void* base1, const void* zr, void* out0, void* out1,
                  const uint32_t* const* slots, const uint64_t* nn, void* stream) {
   const int64_t n = S * count;
@@ -192,7 +194,7 @@ int mxh_bits_b2a(int words, int phase, int role, int64_t S, int start, int count
   if (src == nullptr) src = none;  // phase 2 reads no source
 #define MX_B2A_LAUNCH(T)                                                                   \
   hipLaunchKernelGGL(k_b2a<T>, dim3(phase == 2 ? g : grid_of<T>(n)), dim3(256), 0, st, phase, \
-                     role, S, start, count, xbit, (const T*)src[0], (const T*)src[1],            \
+                     role, S, start, count, xbit, blocks, (const T*)src[0], (const T*)src[1],            \
                      (const T*)src[2], (const T*)src[3], (const T*)src[4], (const T*)src[5], \
                      (const T*)arecv, (T*)msg, (T*)z, (T*)base0, (T*)base1, (const T*)zr,  \
                      (T*)out0, (T*)out1, k, ss)

@@ -15,7 +15,7 @@ int mxh_bits_front(int words, int role, int64_t n, const void* xa, const void* x
                    const void* arecv, void* msg, void* z, void* p0, void* p1,
                    const uint32_t* const* slots, const uint64_t* nn, void* stream);
 int mxh_bits_b2a(int words, int phase, int role, int64_t S, int start, int count, int xbit,
-                 const void* const* src, const void* arecv, void* msg, void* z, void* base0,
+                 int blocks, const void* const* src, const void* arecv, void* msg, void* z, void* base0,
                  void* base1, const void* zr, void* out0, void* out1,
                  const uint32_t* const* slots, const uint64_t* nn, void* stream);
 }
@@ -58,7 +58,8 @@ T src_bit(const T* s, const T* g, const T* t, int64_t e, int q) {
 }
 
 template <class T>
-int b2a(int phase, int role, int64_t S, int start, int count, int xbit, const void* const* src,
+int b2a(int phase, int role, int64_t S, int start, int count, int xbit, int blocks,
+        const void* const* src,
         const T* arecv, T* msg, T* z, T* base0, T* base1, const T* zr, T* out0, T* out1,
         const uint32_t* const* slots, const uint64_t* nn) {
   const int64_t n = S * count;
@@ -81,10 +82,12 @@ int b2a(int phase, int role, int64_t S, int start, int count, int xbit, const vo
   const T* t1 = (const T*)src[5];
   for (int64_t i = 0; i < n; ++i) {
     const int64_t row = i / S, e = i - row * S;
-    int q, xq;
-    mxb::plane_of((int)row, start, count, xbit, &q, &xq);
-    T c0 = role == 1 ? (T)0 : src_bit<T>(s0, g0, t0, e, q);
-    T c1 = role == 2 ? (T)0 : src_bit<T>(s1, g1, t1, e, q);
+    int q, xq, blk, neg;
+    mxb::plane_of((int)row, start, count, xbit, blocks, &q, &xq, &blk, &neg);
+    const int64_t es = e + blk * S;  // the element in the adder's blocks
+    T c0 = role == 1 ? (T)0 : src_bit<T>(s0, g0, t0, es, q);
+    T c1 = role == 2 ? (T)0 : src_bit<T>(s1, g1, t1, es, q);
+    if (neg && role == 0) c0 ^= (T)1;  // NOT: component 0 (P0's first) flipped
     if (xq >= 0) {
       if (role != 1) c0 ^= src_bit<T>(s0, g0, t0, e, xq);
       if (role != 2) c1 ^= src_bit<T>(s1, g1, t1, e, xq);
@@ -118,21 +121,23 @@ int mx_bits_front(int dev, int words, int role, int64_t n, const void* xa, const
 }
 
 int mx_bits_b2a(int dev, int words, int phase, int role, int64_t S, int start, int count,
-                int xbit, const void* const* src, const void* arecv, void* msg, void* z,
-                void* base0, void* base1, const void* zr, void* out0, void* out1,
+                int xbit, int blocks, const void* const* src, const void* arecv, void* msg,
+                void* z, void* base0, void* base1, const void* zr, void* out0, void* out1,
                 const uint32_t* const* slots, const uint64_t* nn, void* stream) {
-  const int planes = xbit >= 0 ? count - 1 : count;  // rows read from start..
+  if (xbit < 0) blocks = 1;
+  const int planes = xbit >= 0 ? count - blocks : count;  // rows read from start..
   if (role < 0 || role > 2 || phase < 0 || phase > 2 || start < 0 || count < 1 ||
-      start + planes > 64 * words || xbit >= 64 * words || (xbit >= 0 && count < 2))
+      start + planes > 64 * words || xbit >= 64 * words || (blocks != 1 && blocks != 3) ||
+      (xbit >= 0 && planes < 1))
     return -3;
   if (dev)
-    return mxh_bits_b2a(words, phase, role, S, start, count, xbit, src, arecv, msg, z, base0,
-                        base1, zr, out0, out1, slots, nn, stream);
+    return mxh_bits_b2a(words, phase, role, S, start, count, xbit, blocks, src, arecv, msg, z,
+                        base0, base1, zr, out0, out1, slots, nn, stream);
   if (words == 1)
-    return b2a<u64>(phase, role, S, start, count, xbit, src, (const u64*)arecv, (u64*)msg, (u64*)z,
+    return b2a<u64>(phase, role, S, start, count, xbit, blocks, src, (const u64*)arecv, (u64*)msg, (u64*)z,
                     (u64*)base0, (u64*)base1, (const u64*)zr, (u64*)out0, (u64*)out1, slots, nn);
   if (words == 2)
-    return b2a<u128>(phase, role, S, start, count, xbit, src, (const u128*)arecv, (u128*)msg,
+    return b2a<u128>(phase, role, S, start, count, xbit, blocks, src, (const u128*)arecv, (u128*)msg,
                      (u128*)z, (u128*)base0, (u128*)base1, (const u128*)zr, (u128*)out0,
                      (u128*)out1, slots, nn);
   return -2;

@@ -230,8 +230,8 @@ _SIGS = {
     "mx_jobs_r2": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp]),
     "mx_bits_front": (c_int, [c_int, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                               c_vp, c_vp, c_vp, c_vp]),
-    "mx_bits_b2a": (c_int, [c_int, c_int, c_int, c_int, c_i64, c_int, c_int, c_int, c_vp, c_vp,
-                            c_vp,
+    "mx_bits_b2a": (c_int, [c_int, c_int, c_int, c_int, c_i64, c_int, c_int, c_int, c_int,
+                            c_vp, c_vp, c_vp,
                             c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mx_key_refresh": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp]),
     "mx_key_refresh_host": (None, [c_vp, c_u64, c_int, c_vp]),

@@ -597,9 +597,10 @@ def decode(a: RT, frac: int) -> torch.Tensor:
         d = [t.data.contiguous() for t in a.parts]
         out = torch.empty(a.shape, dtype=torch.float64, device=a.device)
         ptrs = [nat.ptr(x) for x in d] + [None] * (4 - len(d))
+        # a deferred truncation (Opened.shift) is the decode's division by 2^shift more
         nat.check(nat.lib().mx_addn_decode(
-            nat.dev_of(d[0]), _words(a.bits), *ptrs, nat.ptr(out), a.numel(), int(frac),
-            nat.stream_of(d[0])), "addn_decode")
+            nat.dev_of(d[0]), _words(a.bits), *ptrs, nat.ptr(out), a.numel(),
+            int(frac) + a.shift, nat.stream_of(d[0])), "addn_decode")
         return out
     ad = a.data.contiguous()
     out = torch.empty(a.shape, dtype=torch.float64, device=a.device)
@@ -1439,14 +1440,18 @@ class Opened(RT):
     ``data``.  A decode of it runs one fused pass (mx_addn_decode) instead of add + decode:
     the ring-valued sum never goes to memory."""
 
-    __slots__ = ("parts", "stream")
+    __slots__ = ("parts", "stream", "shift")
 
-    def __init__(self, a: RT, b: RT, c: RT, d: RT = None):
+    def __init__(self, a: RT, b: RT, c: RT, d: RT = None, shift: int = 0):
+        """``shift``: the opened sum carries ``shift`` more fractional bits than its type (a
+        truncation deferred into the reveal): ``data`` is the sum shifted right
+        (arithmetic, exact floor) and a decode divides by 2^(frac + shift)."""
         _RT_DATA.__set__(self, None)
         self.bits = a.bits
         self._shape = a.shape
         self.parts = (a, b, c) if d is None else (a, b, c, d)
         self.stream = _stream_of(a.data)
+        self.shift = shift
 
     def pending(self) -> bool:
         return _RT_DATA.__get__(self) is None
@@ -1459,6 +1464,8 @@ class Opened(RT):
             s = add3(*self.parts[:3])
             if len(self.parts) == 4:
                 s = binary("add", s, self.parts[3])
+            if self.shift:
+                s = s.sar(self.shift)
             d = s.data
             _RT_DATA.__set__(self, d)
             self.parts = None
@@ -1473,13 +1480,15 @@ class Opened(RT):
         return self.parts[0].device if self.pending() else self.data.device
 
 
-def opened(a: RT, b: RT, c: RT, d: RT = None) -> RT:
-    """a + b + c [+ d] as an :class:`Opened` (lazy) when the fused decode applies."""
+def opened(a: RT, b: RT, c: RT, d: RT = None, shift: int = 0) -> RT:
+    """a + b + c [+ d] (shifted right by ``shift``: Opened) as an :class:`Opened` (lazy)
+    when the fused decode applies."""
     parts = (a, b, c) if d is None else (a, b, c, d)
     if a.bits in (64, 128) and all(t.shape == a.shape and t.bits == a.bits for t in parts):
-        return Opened(*parts)
+        return Opened(*parts, shift=shift)
     s = add3(a, b, c)
-    return s if d is None else binary("add", s, d)
+    s = s if d is None else binary("add", s, d)
+    return s.sar(shift) if shift else s
 
 
 def add3(a: RT, b: RT, c: RT) -> RT:
@@ -2134,11 +2143,13 @@ def bits_front(role, xa, xb, arecv, bits, slots, n1, ng):
 
 
 def bits_b2a(phase, role, src, start, count, bits, slots, n1, ng, arecv=None, state=None,
-             xbit=-1):
+             xbit=-1, blocks=1):
     """B2A of bit planes start.. of a boolean sharing (src = (s0, s1, g0, g1, t0, t1) torch
     data of one party; g = None: s are the sum words), phases 0 / 1 / 2 (bits_party.h).
     ``xbit`` >= 0: rows 0..count-2 are planes start.. XORed with plane xbit, the last row is
-    plane xbit (bits_party.h plane_of).  Phases 0 / 1 return state (msg, z, base0, base1);
+    plane xbit; ``blocks`` > 1: the source holds that many blocks of the output's elements and
+    the last ``blocks`` rows are plane xbit of each (bits_party.h plane_of).  Phases 0 / 1
+    return state (msg, z, base0, base1);
     phase 2 (state + the received z in ``arecv``) returns the result pair [count, ...]."""
     like = next(t for t in src if t is not None) if src is not None else state[1]
     per = tuple(like.shape[:-1] if bits == 128 else like.shape) if src is not None else None
@@ -2147,17 +2158,21 @@ def bits_b2a(phase, role, src, start, count, bits, slots, n1, ng, arecv=None, st
         S = z.numel() // (2 if bits == 128 else 1) // count
         o0, o1 = torch.empty_like(z), torch.empty_like(z)
         nat.check(nat.lib().mx_bits_b2a(
-            nat.dev_of(z), _words(bits), 2, role, S, start, count, xbit, None, None, None, _p(z),
+            nat.dev_of(z), _words(bits), 2, role, S, start, count, xbit, blocks, None, None,
+            None, _p(z),
             _p(b0), _p(b1), _p(arecv), _p(o0), _p(o1), _slots_arr(slots), _nonces_arr((n1, ng)),
             nat.stream_of(z)), "bits_b2a")
         return o0, o1
+    if blocks > 1:  # ``blocks`` copies concatenated on axis 0: the rows are one block's
+        per = (per[0] // blocks,) + per[1:]
     S = math.prod(per)
     shp = (count,) + per + ((2,) if bits == 128 else ())
     z, b0, b1 = (torch.empty(shp, dtype=torch.int64, device=like.device) for _ in range(3))
     msg = torch.empty_like(z) if role == 0 else None
     srcs = (ctypes.c_void_p * 6)(*[_p(t) for t in src])
     nat.check(nat.lib().mx_bits_b2a(
-        nat.dev_of(like), _words(bits), phase, role, S, start, count, xbit, srcs, _p(arecv),
+        nat.dev_of(like), _words(bits), phase, role, S, start, count, xbit, blocks, srcs,
+        _p(arecv),
         _p(msg),
         _p(z), _p(b0), _p(b1), None, None, None, _slots_arr(slots), _nonces_arr((n1, ng)),
         nat.stream_of(like)), "bits_b2a")

@@ -129,12 +129,18 @@ class RoundB:
 
 class NoRoundB:
     """The deferred round of a process that hosts no party of the placement (SPMD
-    outsiders): nothing to send, nothing to complete."""
+    outsiders): nothing to send, nothing to complete (a deferred truncation's nonces are
+    drawn in step with the members: ``nonce_draw``)."""
 
     done = True
 
+    def __init__(self, nonce_draw=None):
+        self.nonce_draw = nonce_draw
+
     def finish(self):
-        pass
+        if self.nonce_draw is not None:
+            draw, self.nonce_draw = self.nonce_draw, None
+            draw()
 
 
 def dot_trunc_tail(sess, plc, roles, cross, bits, m, nonces, out0, out1, slots, pre=None,
@@ -233,10 +239,13 @@ class MulAddTail:
     round plus the reveal: P_{j+1} sends z_{j+1} + c_{j+2}, P_{j+2} sends z_{j+2} + c_j
     (each its own z plus its second component), P_j sums z_j + c_{j+1} + both."""
 
-    def __init__(self, sess, plc, z, c0, c1, bits):
+    def __init__(self, sess, plc, z, c0, c1, bits, post_shift=0):
         self.sess, self.plc, self.z, self.c0, self.c1, self.bits = sess, plc, z, c0, c1, bits
         self.done = False
         self.rep = None  # the DeferredRep whose shares finish() completes
+        # a TruncPr by post_shift bits pending too (mul_add_trunc): a reveal opens the value
+        # and shifts it exactly; finish() runs it as the dot's tail on the additive shares
+        self.post_shift = post_shift
 
     def finish(self):
         if self.done:
@@ -244,6 +253,17 @@ class MulAddTail:
         self.done = True
         from moose_amd.runtime.session import PV
 
+        if self.post_shift:
+            # z + c0 is this party's 3-out-of-3 additive share of a * b + c: zero share +
+            # reshare + TruncPr in the dot tail's 2 rounds (instead of reshare + TruncPr)
+            sess, bits = self.sess, self.bits
+            v = R.binary("add", self.z, self.c0)
+            nonces = tuple(sess.nonce(self.plc) for _ in range(7))
+            s0, s1 = sess.party_dot_trunc(self.plc, PV(self.plc, R.RT(v.data.unsqueeze(0), bits)),
+                                          self.post_shift, nonces)
+            self.rep._s0 = PV(self.plc, R.RT(s0.v.data[0], bits))
+            self.rep._s1 = PV(self.plc, R.RT(s1.v.data[0], bits))
+            return
         zn = self.sess.shift(PV(self.plc, self.z), 1).v
         o0, o1 = R.binary2("add", self.z, self.c0, zn, self.c1)
         self.rep._s0, self.rep._s1 = PV(self.plc, o0), PV(self.plc, o1)
@@ -271,4 +291,5 @@ class MulAddTail:
             sess.stats.record_send(plc.owners[a], host, nb)
         if idx != j:
             return None
-        return R.opened(self.z, self.c1, R.RT(got["m1"], self.bits), R.RT(got["m2"], self.bits))
+        return R.opened(self.z, self.c1, R.RT(got["m1"], self.bits), R.RT(got["m2"], self.bits),
+                        shift=self.post_shift)

@@ -885,21 +885,35 @@ def b2a_planes(sess, b: RepTensor, start: int, count: int, ring_bits: int) -> Re
 
 
 def b2a_planes_xor(sess, b: RepTensor, start: int, count: int, xbit: int,
-                   ring_bits: int) -> RepTensor:
+                   ring_bits: int, blocks: int = 1) -> RepTensor:
     """b2a of bit planes start..start+count-1 of a packed boolean sharing, each XORed with
     plane ``xbit``, followed by plane ``xbit`` itself: count + 1 rows on a new leading axis.
     With xbit the sign of a two's-complement x, the rows are the planes of |x| (exactly:
     ~x = -x - 1 for x < 0, so off by one unit of bit 0) and the sign -- ONE decomposition
-    serves both (the XOR is local on boolean shares).  One round pair on a per-party session
-    (parallel/spmd.py p_b2a_planes_xor, same shares); BitSplit + Xor + Concat + b2a otherwise."""
+    serves both (the XOR is local on boolean shares).  ``blocks`` = 3: ``b`` holds x, x - T
+    and x + T concatenated on axis 0 (decomposed together); the planes are x's and the last
+    rows [x >= T] (NOT sign(x - T)), [x < -T] (sign(x + T)) and sign(x).  One round
+    pair on a per-party session (parallel/spmd.py p_b2a_planes_xor, same shares); Slice +
+    BitSplit + Xor + Concat + b2a otherwise."""
     f = getattr(sess, "p_b2a_planes_xor", None)
-    r = f(b.plc, b, start, count, xbit, ring_bits) if f is not None else None
+    r = f(b.plc, b, start, count, xbit, ring_bits, blocks=blocks) if f is not None else None
     if r is not None:
         return RepTensor(b.plc, ring_bits, "arith", r[0], r[1])
-    planes = _sharewise(sess, "BitSplit", b.plc, (b.s0, b.s1), start=start, count=count)
-    sgn = _sharewise(sess, "BitSplit", b.plc, (b.s0, b.s1), start=xbit, count=1)
-    xored = _sharewise(sess, "Xor", b.plc, planes, sgn)
-    both = [sess.p("Concat", b.plc, xored[i], sgn[i], axis=0) for i in range(2)]
+    if blocks > 1:
+        n = sess.p_shape(b.s0)[0] // blocks
+        parts = [_sharewise(sess, "Slice", b.plc, (b.s0, b.s1), slice=(k * n, (k + 1) * n, None))
+                 for k in range(blocks)]
+    else:
+        parts = [(b.s0, b.s1)]
+    planes = _sharewise(sess, "BitSplit", b.plc, parts[0], start=start, count=count)
+    sgns = [_sharewise(sess, "BitSplit", b.plc, p, start=xbit, count=1) for p in parts]
+    xored = _sharewise(sess, "Xor", b.plc, planes, sgns[0])
+    tail = [sgns[0]]
+    if blocks == 3:  # NOT sign(x - T), sign(x + T), sign(x)
+        nt = add_public(sess, RepTensor(b.plc, 1, "bool", *sgns[1]),
+                        R.fill((), 1, 1, getattr(sess, "device", "cpu")))
+        tail = [(nt.s0, nt.s1), sgns[2], sgns[0]]
+    both = [sess.p("Concat", b.plc, xored[i], *[g[i] for g in tail], axis=0) for i in range(2)]
     return b2a(sess, RepTensor(b.plc, 1, "bool", both[0], both[1]), ring_bits)
 
 
@@ -956,6 +970,19 @@ def mul_add(sess, a: RepTensor, b: RepTensor, c: RepTensor) -> RepTensor:
         if r is not None:
             return r
     return add(sess, mul(sess, a, b), c)
+
+
+def mul_add_trunc(sess, a: RepTensor, b: RepTensor, c: RepTensor, m: int) -> RepTensor:
+    """TruncPr(a * b + c, m).  On a per-party session both the product's reshare and the
+    truncation wait for the reader: a reveal opens the untruncated value in one round and
+    shifts it exactly (parallel/party.py MulAddTail.post_shift); any other reader gets the
+    dot tail's 2 rounds (zero share + reshare + TruncPr) instead of reshare + TruncPr."""
+    f = getattr(sess, "p_mul_add_deferred", None)
+    if f is not None and 0 < m <= 63:
+        r = f(a.plc, a, b, c, post_shift=m)
+        if r is not None:
+            return r
+    return trunc_pr(sess, add(sess, mul(sess, a, b), c), m)
 
 
 def mux(sess, s: RepTensor, x: RepTensor, y: RepTensor) -> RepTensor:

@@ -13,13 +13,13 @@ from moose_amd.runtime.local import LocalMooseRuntime
 IDS = ["alice", "bob", "carole"]
 
 
-def _lr(device, monkeypatch, bits_on, width_on, one_dec=False):
+def _lr(device, monkeypatch, bits_on, width_on, one_dec=False, ring=64):
     from moose_amd.models.predictors.tutorial import logistic_regression_tutorial
 
     monkeypatch.setenv("MOOSEX_PARTY_BITS", "1" if bits_on else "0")
     monkeypatch.setattr(FP, "SIGN_WIDTH", width_on)
     monkeypatch.setattr(FP, "ONE_DECOMPOSITION", one_dec)
-    tm = logistic_regression_tutorial(16)
+    tm = logistic_regression_tutorial(ring)
     rt = LocalMooseRuntime(IDS, device_map={i: device for i in IDS}, seed=5, use_graphs=False)
     r = np.asarray(list(rt.evaluate_computation(tm.computation, {"x": tm.x_test}).values())[0])
     return r, rt.last_stats.rounds, float(np.abs(r - tm.proba).max())
@@ -42,15 +42,57 @@ def test_width_bound_saves_adder_levels(device, monkeypatch):
     assert e_narrow < 1e-6 and e_full < 1e-6
 
 
+@pytest.mark.parametrize("ring", [64, 128])
 @pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
-def test_one_decomposition_sigmoid_fused_equals_generic(device, monkeypatch):
-    """The sigmoid's sign and e^-|x| from one adder: the fused B2A with the sign-plane XOR
-    (bits_party.h plane_of) gives bitwise the generic BitSplit + Xor + Concat + b2a shares."""
+def test_one_decomposition_sigmoid_fused_equals_generic(device, ring, monkeypatch):
+    """The sigmoid's sign and e^-|x| from one adder over x, x - T and x + T: the fused B2A
+    with the sign-plane XOR and the range rows (bits_party.h plane_of) gives bitwise the
+    generic Slice + BitSplit + Xor + NOT + Concat + b2a shares."""
     monkeypatch.setattr(FP, "ONE_DEC_WIDTH", False)  # both adders over all bits
-    fused, r_fused, e = _lr(device, monkeypatch, True, True, one_dec=True)
-    generic, r_gen, _ = _lr(device, monkeypatch, False, True, one_dec=True)
+    fused, r_fused, e = _lr(device, monkeypatch, True, True, one_dec=True, ring=ring)
+    generic, r_gen, _ = _lr(device, monkeypatch, False, True, one_dec=True, ring=ring)
     assert np.array_equal(fused, generic)
     assert r_fused == r_gen and e < 1e-6
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_range_split_and_deferred_truncation_save_rounds(device, monkeypatch):
+    """fixed(24, 40): the range split drops the exp tree from 32 to 8 factors (two levels
+    fewer; 2 rounds, the polynomial's levels run beside the tree's) and the reveal absorbs
+    the reciprocal's last truncation (2 rounds); the values stay within 1e-6 of sklearn."""
+    base, r_base, e_base = _lr(device, monkeypatch, True, True, one_dec=True, ring=128)
+    monkeypatch.setattr(FP, "RANGE_SPLIT", False)
+    monkeypatch.setattr(FP, "DEFER_OUTPUT_TRUNC", False)
+    old, r_old, e_old = _lr(device, monkeypatch, True, True, one_dec=True, ring=128)
+    assert r_base == r_old - 4
+    assert e_base < 1e-6 and e_old < 1e-6
+
+
+def test_deferred_truncation_read_by_another_op(monkeypatch):
+    """A sigmoid whose output is not revealed directly (here scaled by 2 and shifted first):
+    the pending mul_add + truncation complete through the dot tail's TruncPr when the shares
+    are read -- same values as the stacked simulation up to the truncation's rounding."""
+    import moose_amd as pm
+
+    alice, bob, carole = (pm.host_placement(n) for n in IDS)
+    rep = pm.replicated_placement("rep", players=[alice, bob, carole])
+    fx = pm.fixed(24, 40)
+
+    @pm.computation
+    def f(x: pm.Argument(placement=alice, vtype=pm.TensorType(pm.float64))):
+        with alice:
+            xf = pm.cast(x, dtype=fx)
+        with rep:
+            s = pm.sigmoid(xf)
+            y = pm.add(s, s)
+        with carole:
+            return pm.cast(y, dtype=pm.float64)
+
+    x = np.array([-9.0, -2.5, -0.3, 0.0, 0.7, 3.0, 12.0, 50.0, -60.0])
+    want = 2.0 / (1.0 + np.exp(-x))
+    rt = LocalMooseRuntime(IDS, device_map={i: "cpu" for i in IDS}, seed=4, use_graphs=False)
+    got = np.asarray(list(rt.evaluate_computation(f, {"x": x}).values())[0])
+    np.testing.assert_allclose(got, want, atol=2e-6)
 
 
 @pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
