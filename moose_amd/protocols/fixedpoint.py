@@ -962,10 +962,10 @@ def _merged_exp_tail_jobs(sess, x: RepFixed, fac: RepTensor, npad: int) -> RepFi
     st = _Stack(t.s0.v.data, t.s1.v.data, n - 1, bits) if member else None
     F0, F1 = (fac.s0.v.data, fac.s1.v.data) if member else (None, None)
 
-    def run(jobs):
+    def run(jobs, m=f):
         nonces = _tail_nonces(sess, plc)
         if member:
-            sess.party_jobs(plc, jobs, L, bits, f, nonces)
+            sess.party_jobs(plc, jobs, L, bits, m, nonces)
 
     def tree_job(nf):
         h = nf // 2
@@ -987,6 +987,31 @@ def _merged_exp_tail_jobs(sess, x: RepFixed, fac: RepTensor, npad: int) -> RepFi
             F0, F1 = new if member else (None, None)
             nf //= 2
         have += m
+    fw = 62 - f  # the polynomial's weights' fractional bits in the one-product finish
+    if EXP_ONE_PRODUCT and nf == 1 and bits == 128 and fw >= 20:
+        # the tree is done with the powers: e = p F / 2 as ONE product -- the polynomial's
+        # weighted sum ACC = sum_k w_k x^k (w_k at fw bits) is a local combination of the
+        # replicated powers, so cross(ACC, F) + c_0 2^(f+fw) F_first is an additive share
+        # of p F at scale 2^(2f+fw), truncated by f + fw + 1 = 63 bits in the same tail
+        # (instead of the weighted sum's TruncPr round pair, then the product's)
+        wts = [int(round(c * (1 << fw))) for c in coeffs[1:]]
+        c0 = int(round(coeffs[0] * (1 << (f + fw))))
+        if member:
+            mod = 1 << bits
+            acc = []
+            for X, rows in ((st.x0, st.s0), (st.x1, st.s1)):
+                rest = R.weighted_sum(R.RT(rows[:n - 1], bits), [w % mod for w in wts[1:]])
+                lin = R.binary("mul", R.RT(X, bits), R.fill((), wts[0], bits, X.device))
+                acc.append(R.binary("add", rest, lin).data)
+            o0, o1 = torch.empty_like(st.x0), torch.empty_like(st.x0)
+            run([R.MulJob(1, o0, o1, x=(acc[0], acc[1]), y=(F0[0], F1[0]), a=F0[0], ca=c0)],
+                m=f + fw + 1)
+            e = RepTensor(plc, bits, "arith", PV(plc, R.RT(o0, bits)), PV(plc, R.RT(o1, bits)))
+        else:
+            run([], m=f + fw + 1)
+            r = PV(plc, Remote(bits))
+            e = RepTensor(plc, bits, "arith", r, r)
+        return RepFixed(e, f, x.integ)
     # the polynomial's weighted sum rides with the next tree level (its TruncPr)
     acc0 = acc1 = None
     jobs = []
@@ -1097,6 +1122,8 @@ def sigmoid(sess, x: RepFixed) -> RepFixed:
     return _with(pos, rep.mux(sess, s, one_minus.t, pos.t))
 
 
+# per-party sessions finish 2^-a with one product (the polynomial's sum untruncated)
+EXP_ONE_PRODUCT = os.environ.get("MOOSEX_EXP_ONE_PRODUCT", "1") != "0"
 # per-party sessions evaluate the sigmoid's reciprocal as one degree-8 polynomial
 RECIP_DIRECT = os.environ.get("MOOSEX_RECIP_DIRECT", "1") != "0"
 # per-party sessions leave the sigmoid's last truncation to its reader (a reveal: exact)

@@ -61,11 +61,15 @@ def test_range_split_and_deferred_truncation_save_rounds(device, monkeypatch):
     fewer; 2 rounds, the polynomial's levels run beside the tree's) and the reveal absorbs
     the reciprocal's last truncation (2 rounds); the values stay within 1e-6 of sklearn."""
     base, r_base, e_base = _lr(device, monkeypatch, True, True, one_dec=True, ring=128)
+    monkeypatch.setattr(FP, "EXP_ONE_PRODUCT", False)
+    mid, r_mid, e_mid = _lr(device, monkeypatch, True, True, one_dec=True, ring=128)
     monkeypatch.setattr(FP, "RANGE_SPLIT", False)
     monkeypatch.setattr(FP, "DEFER_OUTPUT_TRUNC", False)
     old, r_old, e_old = _lr(device, monkeypatch, True, True, one_dec=True, ring=128)
-    assert r_base == r_old - 4
-    assert e_base < 1e-6 and e_old < 1e-6
+    assert r_mid == r_old - 4
+    # the exp's polynomial sum and final product as one truncated product: 2 rounds fewer
+    assert r_base == r_mid - 2
+    assert e_base < 1e-6 and e_mid < 1e-6 and e_old < 1e-6
 
 
 def test_deferred_truncation_read_by_another_op(monkeypatch):

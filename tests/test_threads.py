@@ -283,3 +283,73 @@ def test_party_ks_chain_matches_per_level(dev, monkeypatch):
     assert ra == rb
     for k in b:
         assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
+
+
+@pytest.mark.gpu
+def test_device_flag_push_wait_orders_two_streams():
+    """The per-party stream graphs' message signalling alone (csrc/party_graph.hip k_push /
+    k_wait under mx_graph_build_chain): graph A delays (a chain of GEMMs), writes a payload
+    and pushes it to a landing buffer with a flag; graph B, launched FIRST on another stream,
+    waits for the flag and copies the landing buffer out.  Every replay B must see A's
+    payload of that replay."""
+    import ctypes
+
+    from moose_amd.ops import native as nat
+
+    dev = torch.device("cuda:0")
+    sa, sb = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    n = 4096
+    val = torch.zeros(1, dtype=torch.int64, device=dev)
+    payload = torch.zeros(n, dtype=torch.int64, device=dev)
+    landing = torch.zeros(n, dtype=torch.int64, device=dev)
+    out = torch.zeros(n, dtype=torch.int64, device=dev)
+    m = torch.randn(2048, 2048, device=dev)
+    ga, gb = torch.cuda.CUDAGraph(keep_graph=True), torch.cuda.CUDAGraph(keep_graph=True)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(sa):
+        ga.capture_begin()
+        y = m
+        for _ in range(8):  # ~1 ms of work before the payload is written
+            y = y @ m
+        payload.copy_(val.expand(n) + (y[0, 0] * 0).to(torch.int64))
+        ga.capture_end()
+    with torch.cuda.stream(sb):
+        gb.capture_begin()
+        out.copy_(landing)
+        gb.capture_end()
+    ep_a = torch.zeros(1, dtype=torch.int64, device=dev)
+    ep_b = torch.zeros(1, dtype=torch.int64, device=dev)
+    flags = torch.zeros(1, dtype=torch.int32, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    pieces = torch.zeros(1, dtype=torch.int32, device=dev)
+    table = torch.tensor([payload.data_ptr(), landing.data_ptr(), n * 8, flags.data_ptr(),
+                          pieces.data_ptr()], dtype=torch.int64, device=dev)
+
+    def chain(kinds, child, p0, p1, p2, i0, i64):
+        k = len(kinds)
+        arr = lambda ty, xs: (ty * k)(*xs)  # noqa: E731
+        g, ex = ctypes.c_void_p(), ctypes.c_void_p()
+        rc = nat.lib().mx_graph_build_chain(
+            k, arr(ctypes.c_int, kinds), arr(ctypes.c_void_p, child), arr(ctypes.c_void_p, p0),
+            arr(ctypes.c_void_p, p1), arr(ctypes.c_void_p, p2), arr(ctypes.c_int, i0),
+            arr(ctypes.c_int64, i64), ctypes.byref(g), ctypes.byref(ex))
+        assert rc == 0, rc
+        return g, ex
+
+    A = chain([5, 0, 6], [0, ga.raw_cuda_graph(), 0], [ep_a.data_ptr(), 0, table.data_ptr()],
+              [0, 0, ep_a.data_ptr()], [0, 0, 0], [0, 0, 1], [0, 0, n * 8])
+    B = chain([5, 7, 0], [0, 0, gb.raw_cuda_graph()], [ep_b.data_ptr(), flags.data_ptr(), 0],
+              [0, ep_b.data_ptr(), 0], [0, err.data_ptr(), 0], [0, 1, 0], [0, 0, 0])
+    try:
+        for r in range(1, 6):
+            val.fill_(1000 + r)
+            torch.cuda.synchronize()
+            nat.check(nat.lib().mx_graph_launch(B[1], sb.cuda_stream), "launch B")
+            nat.check(nat.lib().mx_graph_launch(A[1], sa.cuda_stream), "launch A")
+            torch.cuda.synchronize()
+            assert int(err.item()) == 0
+            assert int(flags.item()) == r and int(ep_a.item()) == r and int(ep_b.item()) == r
+            assert bool((out == 1000 + r).all()), (r, out[:4].tolist())
+    finally:
+        for g, ex in (A, B):
+            nat.lib().mx_graph_free(g, ex)
