@@ -158,6 +158,11 @@ int mx_graph_build_chain(int n, const int* kind, void* const* child, void* const
   return 0;
 }
 
+// Diagnostics: the graph as a DOT file (hipGraphDebugDotPrint; flags 1 = verbose).
+int mx_graph_dot(void* graph, const char* path, unsigned int flags) {
+  return hipGraphDebugDotPrint((hipGraph_t)graph, path, flags) == hipSuccess ? 0 : -1;
+}
+
 int mx_graph_launch(void* exec, void* stream) {
   return hipGraphLaunch((hipGraphExec_t)exec, (hipStream_t)stream) == hipSuccess ? 0 : -1;
 }

@@ -219,6 +219,7 @@ _SIGS = {
     "mx_stream_cumask": (c_int, [c_vp, c_int, c_vp]),
     "mx_stream_destroy": (c_int, [c_vp]),
     "mx_graph_compose": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mx_graph_dot": (c_int, [c_vp, ctypes.c_char_p, ctypes.c_uint]),
     "mx_graph_launch": (c_int, [c_vp, c_vp]),
     "mx_enable_peer": (c_int, [c_int, c_int]),
     "mx_graph_build_chain": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,

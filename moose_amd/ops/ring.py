@@ -200,11 +200,15 @@ def shared_streams(delta: int):
         SHARED_STREAMS = max(0, SHARED_STREAMS + delta)
 
 
+# MOOSEX_CONST_CACHE=0: no shared device constants (every use makes its own; diagnostics)
+CONST_CACHE = os.environ.get("MOOSEX_CONST_CACHE", "1") != "0"
+
+
 def _cache_put(cache, key, t, limit):
     """Insert a freshly made device constant into a shared cache.  While dataflow lanes
     run (runtime/lanes.py) other streams may read it next, so the producing stream is
     drained first (once per constant)."""
-    if len(cache) >= limit:
+    if len(cache) >= limit or not CONST_CACHE:
         return
     from moose_amd.runtime import lanes
 

@@ -23,6 +23,7 @@ additionally be pinned to different MI355Xs (SURVEY §7.1 "3 parties on 1 or 3 G
 """
 from __future__ import annotations
 
+import math
 import os
 import queue
 import threading
@@ -76,6 +77,10 @@ class ThreadTransport:
         # tape mode: every message round goes to this callback as a CommStep
         self.tape = None
         self._cursor = {}
+        # per source, the landing buffers of the taped messages allocated OUTSIDE the graph
+        # pool (prepare_landing); None: receives land where the protocol allocated them
+        self.landing = None
+        self._land_cursor = {}
 
     # -- payload movement --------------------------------------------------------------
     def _ship(self, t: torch.Tensor, dst: int):
@@ -130,6 +135,32 @@ class ThreadTransport:
                                          f"within {self.hub.timeout} s") from None
 
     # -- tape mode ------------------------------------------------------------------------
+    def prepare_landing(self):
+        """Allocate, before a capture, one persistent landing buffer per tensor message of
+        the warm-up log.  Needed when a SENDER writes the message into the receiver's memory
+        at the sender's own pace (per-party graphs on separate streams / devices): a buffer
+        from the receiver's graph pool reuses blocks the receiver's EARLIER segments still
+        use (torch reuses pool blocks in the capturing stream's order, which a write from
+        another stream does not follow) -- the cause of the composed-as-DAG failures."""
+        self.landing = {}
+        for src, items in self.log.items():
+            bufs = []
+            for kind, shape, dtype, _bits in items:
+                if kind in ("rt", "t") and math.prod(shape) > 0:
+                    bufs.append(torch.empty(shape, dtype=dtype, device=self.device))
+            self.landing[src] = bufs
+        self._land_cursor = {}
+
+    def _take_landing(self, src, out):
+        k = self._land_cursor.get(src, 0)
+        self._land_cursor[src] = k + 1
+        bufs = self.landing.get(src, [])
+        if k >= len(bufs) or bufs[k].dtype != out.dtype or bufs[k].numel() != out.numel():
+            from moose_amd.runtime.graphs import CaptureError
+
+            raise CaptureError(f"message {k} from rank {src}: no landing buffer of its shape")
+        return bufs[k]
+
     def _taped(self, sends, recvs):
         from moose_amd.parallel.transport import CommStep
 
@@ -137,6 +168,17 @@ class ThreadTransport:
         land, after = [], []
         for out, src in recvs:
             if out.numel() == 0:
+                continue
+            if self.landing is not None:
+                buf = self._take_landing(src, out)
+                whole = (out._base is None and out.storage_offset() == 0 and out.is_contiguous()
+                         and out.untyped_storage().nbytes() == out.numel() * out.element_size())
+                if whole and tuple(buf.shape) == tuple(out.shape):
+                    out.set_(buf)  # the protocol's tensor now IS the persistent buffer
+                    land.append((buf, src))
+                else:  # a view: land in the persistent buffer, copy after the round
+                    land.append((buf, src))
+                    after.append((out, buf.view(out.shape) if out.is_contiguous() else buf))
                 continue
             if out.is_contiguous():
                 land.append((out, src))
@@ -146,7 +188,7 @@ class ThreadTransport:
                 after.append((out, buf))
         self.tape(CommStep(sends, land))
         for out, buf in after:  # captured in the segment after the round
-            out.copy_(buf)
+            out.copy_(buf.reshape(out.shape))
 
     def _next_logged(self, src: int):
         k = self._cursor.get(src, 0)
@@ -373,14 +415,19 @@ class PartyTapes:
         role_ranks = {r: i for i, r in enumerate(identities)}
         # every party on one device: the tapes are composed into ONE graph (below)
         # per-party graphs on their own streams / devices with device-side message flags
-        # (_build_streams): MOOSEX_PARTY_STREAMS=1
-        self.streams_mode = os.environ.get("MOOSEX_PARTY_STREAMS") == "1"
+        # (_build_streams): the default when the parties are on several devices (one GPU:
+        # the composed graph, unless MOOSEX_PARTY_STREAMS=1; =0 disables it everywhere)
+        env = os.environ.get("MOOSEX_PARTY_STREAMS")
+        self.streams_mode = env == "1" or (env is None and len(set(self.devices)) > 1)
         single = (len(set(self.devices)) == 1 and not self.streams_mode
                   and os.environ.get("MOOSEX_PARTY_GRAPH", "1") != "0")
         self.tapes = []
         for i, ident in enumerate(identities):
             tr = ThreadTransport(i, None, device=self.devices[i], world=n)
             tr.log = warm[ident]["log"]
+            if self.streams_mode:  # senders write landing buffers at their own pace
+                with torch.cuda.device(self.devices[i]):
+                    tr.prepare_landing()
             with torch.cuda.device(self.devices[i]):
                 self.tapes.append(SPMDTape(comp, arguments, ident, role_ranks, tr,
                                            self.devices[i], storage, ring, seed,
@@ -395,7 +442,15 @@ class PartyTapes:
         self.issue_s = []
         self.issue_parts = []
         self._composed = self._compose() if single else None
-        self._party_graphs = self._build_streams() if self.streams_mode else None
+        self._party_graphs = None
+        if self.streams_mode:
+            try:
+                self._party_graphs = self._build_streams()
+            except Exception as e:  # noqa: BLE001 - e.g. no peer access between the GPUs
+                import warnings
+
+                warnings.warn(f"per-party stream graphs unavailable ({e}); per-action replay",
+                              RuntimeWarning, stacklevel=2)
 
     def _compose(self):
         """The schedule as ONE hipGraph (csrc/graph_compose.hip) in a total order: each
@@ -504,6 +559,10 @@ class PartyTapes:
         self._epochs = [torch.zeros(1, dtype=torch.int64, device=d) for d in self.devices]
         self._errs = [torch.zeros(1, dtype=torch.int32, device=d) for d in self.devices]
         self._tables = []
+        # MOOSEX_PARTY_STREAMS_SHADOW=1 (probes): copies of the landing buffers after waits
+        shadow = os.environ.get("MOOSEX_PARTY_STREAMS_SHADOW") == "1"
+        self._shadows = []
+        self._dummy = torch.zeros(64, dtype=torch.int32, device=self.devices[0])
         handles = []
         for p, tape in enumerate(self.tapes):
             dev = self.devices[p]
@@ -551,6 +610,19 @@ class PartyTapes:
                     node(7, a=self._flags[p].data_ptr() + 4 * fbase, b=epoch,
                          c=self._errs[p].data_ptr(), cnt=len(st.recvs))
                     fbase += len(st.recvs)
+                    if shadow:  # debugging: each landing buffer as seen right after the wait
+                        rows = []
+                        for buf, _src in st.recvs:
+                            sh = torch.empty_like(buf)
+                            self._shadows.append((buf, sh))
+                            rows.append((buf.data_ptr(), sh.data_ptr(),
+                                         buf.numel() * buf.element_size(),
+                                         self._dummy.data_ptr(), self._dummy.data_ptr() + 4))
+                        flat = [x - (1 << 64) if x >= (1 << 63) else x for r in rows for x in r]
+                        table = torch.tensor(flat, dtype=torch.int64, device=dev)
+                        self._tables.append(table)
+                        node(6, a=table.data_ptr(), b=epoch, cnt=len(rows),
+                             big=max(r[2] for r in rows))
             m = len(kinds)
             arr = lambda ty, xs: (ty * max(1, len(xs)))(*xs)  # noqa: E731
             g, ex = ctypes.c_void_p(), ctypes.c_void_p()
@@ -658,6 +730,14 @@ class PartyTapes:
             raise CaptureError(f"{len(pending)} messages sent but never received")
         return acts
 
+    def _free_party_graphs(self):
+        from moose_amd.ops import native as nat
+
+        torch.cuda.synchronize()
+        for g, ex in self._party_graphs or []:
+            nat.lib().mx_graph_free(g, ex)
+        self._party_graphs = None
+
     def __del__(self):
         hs = list(getattr(self, "_party_graphs", None) or [])
         h = getattr(self, "_graph_handles", None)
@@ -734,7 +814,20 @@ class PartyTapes:
         import time
 
         if self._party_graphs is not None:
-            return self._replay_streams(arguments)
+            from moose_amd.parallel.transport import TransportError
+
+            try:
+                return self._replay_streams(arguments)
+            except TransportError as e:
+                # a message never arrived (peer writes refused, a flag lost): this replay is
+                # void -- redo it, and every later one, with the per-action replay
+                import warnings
+
+                warnings.warn(f"per-party stream graphs disabled: {e}", RuntimeWarning,
+                              stacklevel=2)
+                self._free_party_graphs()
+                for err in self._errs:
+                    err.zero_()
         if self._composed is not None:
             return self._replay_composed(arguments)
         n = len(self.tapes)

@@ -303,15 +303,16 @@ def test_device_flag_push_wait_orders_two_streams():
     payload = torch.zeros(n, dtype=torch.int64, device=dev)
     landing = torch.zeros(n, dtype=torch.int64, device=dev)
     out = torch.zeros(n, dtype=torch.int64, device=dev)
-    m = torch.randn(2048, 2048, device=dev)
+    m = torch.randn(1 << 24, device=dev)
+    torch.sin(m)  # library / kernel initialisation outside the capture
     ga, gb = torch.cuda.CUDAGraph(keep_graph=True), torch.cuda.CUDAGraph(keep_graph=True)
     torch.cuda.synchronize()
     with torch.cuda.stream(sa):
         ga.capture_begin()
         y = m
-        for _ in range(8):  # ~1 ms of work before the payload is written
-            y = y @ m
-        payload.copy_(val.expand(n) + (y[0, 0] * 0).to(torch.int64))
+        for _ in range(40):  # ~1 ms of work before the payload is written
+            y = torch.sin(y)
+        payload.copy_(val.expand(n) + (y[0] * 0).to(torch.int64))
         ga.capture_end()
     with torch.cuda.stream(sb):
         gb.capture_begin()
@@ -353,3 +354,37 @@ def test_device_flag_push_wait_orders_two_streams():
     finally:
         for g, ex in (A, B):
             nat.lib().mx_graph_free(g, ex)
+
+
+@pytest.mark.gpu
+def test_party_streams_fall_back_to_per_action_replay(monkeypatch):
+    """A per-party stream replay that reports a lost message (TransportError) is redone --
+    and every later replay runs -- with the per-action replay of the same tapes (captured
+    with their hipGraphs kept), still bitwise equal to eager."""
+    from moose_amd.parallel import threads as T
+    from moose_amd.parallel.transport import TransportError
+
+    monkeypatch.setenv("MOOSEX_PARTY_STREAMS", "1")
+    comp = _comp(False)
+    args = _args()
+    devs = {i: "cuda:0" for i in IDS}
+    want = LocalMooseRuntime(IDS, device_map=devs, seed=11, use_graphs=False
+                             ).evaluate_computation(comp, args)
+    calls = {"n": 0}
+    orig = T.PartyTapes._replay_streams
+
+    def flaky(self, arguments):
+        calls["n"] += 1
+        if calls["n"] == 2:
+            raise TransportError("injected: a message never arrived")
+        return orig(self, arguments)
+
+    monkeypatch.setattr(T.PartyTapes, "_replay_streams", flaky)
+    rt = LocalMooseRuntime(IDS, device_map=devs, seed=11, use_graphs=True)
+    with pytest.warns(RuntimeWarning, match="stream graphs disabled"):
+        for _ in range(5):
+            got = rt.evaluate_computation(comp, args)
+            for k in want:
+                assert np.array_equal(np.asarray(got[k]), np.asarray(want[k])), k
+    (_, tapes), = rt._party_tapes.values()
+    assert tapes._party_graphs is None and calls["n"] == 2
