@@ -45,6 +45,23 @@ from moose_amd.utils.telemetry import span
 _FLOAT = {"Float32": torch.float32, "Float64": torch.float64}
 # small numeric tensor constants of computations, uploaded once per (value, device)
 _CONST_LV = {}
+# multi-round elementwise ops merged across independent chains (Interpreter._merge_unary)
+_MERGE_KINDS = {"Sigmoid", "Exp", "Log", "Log2", "Sqrt", "Relu", "Abs"}
+_MERGE_FNS = {"Sigmoid": fxp.sigmoid, "Exp": fxp.exp, "Log": fxp.log, "Log2": fxp.log2,
+              "Sqrt": fxp.sqrt, "Relu": fxp.relu, "Abs": fxp.abs_}
+MERGE_ROUNDS = os.environ.get("MOOSEX_MERGE_ROUNDS", "1") != "0"
+
+
+def _by_depth(ops):
+    """A topological order by depth (longest path from a source), stable within a depth:
+    operations that do not depend on each other and sit at the same depth become adjacent,
+    so the merge of independent chains finds their inputs computed.  A deterministic
+    function of the computation: every process of an SPMD job runs the same order."""
+    depth = {}
+    for op in ops:  # ``ops`` is already topologically sorted
+        depth[op.name] = 1 + max((depth.get(n, 0) for n in op.inputs), default=0)
+    order = sorted(range(len(ops)), key=lambda i: (depth[ops[i].name], i))
+    return [ops[i] for i in order]
 
 
 # replicated dialect operators handled by Interpreter._rep_dialect (reference
@@ -134,6 +151,9 @@ class Interpreter:
         batch = getattr(self.sess, "batch_dots", False) and os.environ.get(
             "MOOSEX_BATCH_DOTS", "1") != "0"
         ops = comp.operations
+        if (MERGE_ROUNDS and getattr(self.sess, "merge_rounds", False)
+                and not any(op.kind in ("Save", "Load") for op in ops)):
+            ops = _by_depth(ops)  # independent ops of one depth adjacent (_merge_unary)
         lanes = self.lanes
         begin = getattr(self.sess, "begin_evaluation", None)
         if begin is not None:
@@ -168,6 +188,10 @@ class Interpreter:
         table = self._table_handler(op)
         if (table is None and batch and op.kind == "Dot"
                 and self._batch_dots(op, ops[idx + 1:])):
+            return
+        if (table is None and op.kind in _MERGE_KINDS and MERGE_ROUNDS
+                and getattr(self.sess, "merge_rounds", False)
+                and self._merge_unary(op, ops[idx + 1:])):
             return
         handler = table or getattr(self, f"op_{op.kind}", None) or self._dialect_handler(op)
         if handler is None:
@@ -237,6 +261,70 @@ class Interpreter:
             if self.on_op is not None and self.lanes is None:
                 self.on_op()
             self.env[o.name] = LV(x.plc, "tensor", dtype, r)
+        return True
+
+    def _merge_unary(self, op, later, limit: int = 16) -> bool:
+        """Intra-evaluation overlap for one-party-per-process / per-thread sessions (the
+        reference's async session overlaps independent operations,
+        execution/asynchronous.rs:456-530): a multi-round elementwise fixed-point op
+        (sigmoid, exp, log, sqrt, relu, ...) runs TOGETHER with every later op of the same
+        kind, placement, dtype and attributes whose input is already computed -- the inputs
+        flattened and concatenated, one protocol run, the result split back -- so k
+        independent chains cost the rounds (message latencies) of one instead of k.  The
+        grouping uses only the computation's structure, so every process of an SPMD job
+        forms the same groups.  Values: each element's protocol run is the same
+        computation; only the PRF streams and TruncPr's rounding draws differ from running
+        the ops one by one.  MOOSEX_MERGE_ROUNDS=0 disables it."""
+        def key(o):
+            if not isinstance(o.placement, ReplicatedPlacement) or len(o.inputs) != 1:
+                return None
+            if o.inputs[0] not in self.env:
+                return None
+            x = self._at_memo_put(o, self.env[o.inputs[0]])  # e.g. a host input shared
+            if (x.kind != "tensor" or x.dtype is None or not x.dtype.is_fixed or x.is_host
+                    or x.is_mir or not isinstance(x.v, fxp.RepFixed)
+                    or not isinstance(x.plc, ReplicatedPlacement) or x.plc != o.placement):
+                return None
+            return (o.kind, o.placement, x.dtype, repr(sorted(o.attrs.items()))), x
+
+        k0 = key(op)
+        if k0 is None:
+            return False
+        group = [(op, k0[1])]
+        for o in later:
+            if len(group) >= limit:
+                break
+            if o.kind != op.kind or o.name in self.env:
+                continue
+            if self._table_handler(o) is not None:
+                continue
+            k = key(o)
+            if k is not None and k[0] == k0[0]:
+                group.append((o, k[1]))
+        if len(group) == 1:
+            return False
+        sess = self.sess
+        flats, metas = [], []
+        for _o, x in group:
+            try:
+                shp = tuple(fxp.shape_of(sess, x.v))
+            except Exception:  # noqa: BLE001 - this process holds no share: all remote
+                shp = None
+            n = math.prod(shp) if shp is not None else 1
+            flats.append(fxp.local(sess, x.v, "Reshape", shape=(n,)))
+            metas.append((shp, n))
+        fn = _MERGE_FNS[op.kind]
+        with span(f"op.{op.kind}.merged", n=len(group)):
+            y = fn(sess, fxp.concat(sess, flats, 0))
+            at = 0
+            for (o, x), (shp, n) in zip(group, metas):
+                part = fxp.local(sess, y, "Slice", slice=(at, at + n, None))
+                at += n
+                if shp is not None:
+                    part = fxp.local(sess, part, "Reshape", shape=shp)
+                if self.on_op is not None and self.lanes is None:
+                    self.on_op()
+                self.env[o.name] = LV(x.plc, "tensor", x.dtype, part)
         return True
 
     # ------------------------------------------------------------------------

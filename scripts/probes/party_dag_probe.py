@@ -157,6 +157,26 @@ def main():
             res.append({"outputs_equal": same, "first_diff": first_diff(bufs, srcs)})
         rec[name] = res
         print(json.dumps({name: res}), flush=True)
+    # device time of one launch (launch -> synchronize), median of 20: serial vs DAG
+    import time
+
+    def timed(ex):
+        s = pt.streams[0]
+        ts = []
+        for _ in range(20):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            nat.check(nat.lib().mx_graph_launch(ex, s.cuda_stream), "launch")
+            s.synchronize()
+            ts.append((time.perf_counter() - t0) * 1e3)
+        return sorted(ts)[10]
+
+    ex_dag, m_dag = compose(pt, dag=True)
+    rec["launch_ms_serial"] = timed(ser)
+    rec["launch_ms_dag"] = timed(ex_dag)
+    rec["nodes"] = m_dag
+    print(json.dumps({k: rec[k] for k in ("launch_ms_serial", "launch_ms_dag", "nodes")}),
+          flush=True)
     print(json.dumps(rec), flush=True)
 
 
