@@ -471,6 +471,11 @@ def _lr_stacked(runs, device, world=1):
             if tapes:
                 iss = sorted(tapes[0].issue_s)
                 rec["host_issue_ms_p50"] = iss[len(iss) // 2] * 1e3
+                # one composed graph (one GPU), per-party graphs with device-side message
+                # flags (several GPUs), or per-action issue (the fallback)
+                rec["replay_form"] = ("party_graphs" if tapes[0]._party_graphs is not None
+                                      else "composed" if tapes[0]._composed is not None
+                                      else "per_action")
         elif mode != "eager":
             rec["captured"] = bool(rt._graphs.plans)
         out[mode] = rec
