@@ -443,6 +443,7 @@ class PartyTapes:
         self.issue_parts = []
         self._composed = self._compose() if single else None
         self._party_graphs = None
+        self._launchers = None  # host threads issuing the per-party graph launches
         if self.streams_mode:
             try:
                 self._party_graphs = self._build_streams()
@@ -646,14 +647,32 @@ class PartyTapes:
 
         from moose_amd.ops import native as nat
 
-        t0 = time.perf_counter()
-        for p, tape in enumerate(self.tapes):
-            s = self.streams[p]
+        def launch(p):
+            tape, s = self.tapes[p], self.streams[p]
             with torch.cuda.device(self.devices[p]), torch.cuda.stream(s):
                 tape.copy_arguments(arguments)
                 tape._fill_keys()
                 nat.check(nat.lib().mx_graph_launch(self._party_graphs[p][1], s.cuda_stream),
                           "party graph launch")
+
+        t0 = time.perf_counter()
+        if self._launchers is None and os.environ.get("MOOSEX_PARTY_LAUNCH_THREADS",
+                                                      "1") != "0":
+            from concurrent.futures import ThreadPoolExecutor
+
+            self._launchers = ThreadPoolExecutor(len(self.tapes) - 1,
+                                                 thread_name_prefix="moose-party-launch")
+        if self._launchers is not None:
+            # hipGraphLaunch enqueues every node from the host: the parties' launches go out
+            # concurrently, so a party's graph does not wait behind another's enqueue (its
+            # first receive would otherwise stall until then)
+            futs = [self._launchers.submit(launch, p) for p in range(1, len(self.tapes))]
+            launch(0)
+            for f in futs:
+                f.result()
+        else:
+            for p in range(len(self.tapes)):
+                launch(p)
         self.issue_s.append(time.perf_counter() - t0)
         out = {}
         for p, tape in enumerate(self.tapes):
@@ -739,6 +758,9 @@ class PartyTapes:
         self._party_graphs = None
 
     def __del__(self):
+        ex = getattr(self, "_launchers", None)
+        if ex is not None:
+            ex.shutdown(wait=False)
         hs = list(getattr(self, "_party_graphs", None) or [])
         h = getattr(self, "_graph_handles", None)
         if h is not None:
