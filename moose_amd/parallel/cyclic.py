@@ -207,6 +207,13 @@ def default_offsets(roles: Sequence[str], world: int = None) -> Dict[str, int]:
     return {r: o for r, o in zip(roles, off)}
 
 
+# MOOSEX_DEALER_SIDE=1: the dot tail's early dealer kernel on a side stream beside the GEMM
+# (one GPU).  Off: measured slower -- 16.68 -> 16.90-16.99 ms per cyclic step on one MI355X
+# (gpurun_out/r5v): the ChaCha kernel next to the power-bound GEMM costs it more clock than
+# it hides
+DEALER_SIDE = os.environ.get("MOOSEX_DEALER_SIDE", "0") == "1"
+
+
 class CyclicSession(StackedSession):
     """Stacked party vectors whose components belong to N different sessions (module
     doc).  Runs the generic (per-round) protocol code; every round's messages are one
@@ -476,9 +483,29 @@ class CyclicSession(StackedSession):
         shp = (3, xs[1], ys[2]) + ((2,) if bits == 128 else ())
         s0 = torch.empty(shp, dtype=torch.int64, device=self.device)
         s1 = torch.empty_like(s0)
-        pre = party.dealer_early(self, plc, [0, 1, 2], (shp[1:], torch.int64), bits, m, nonces,
-                                 [s0[c] for c in range(3)], [s1[c] for c in range(3)],
-                                 self._pair_ptrs(plc))
+
+        def run():
+            return party.dealer_early(self, plc, [0, 1, 2], (shp[1:], torch.int64), bits, m,
+                                      nonces, [s0[c] for c in range(3)],
+                                      [s1[c] for c in range(3)], self._pair_ptrs(plc))
+
+        # opt-in (DEALER_SIDE), one GPU: the dealer's keystream kernel needs nothing but
+        # keys, so it can run on a side stream beside the GEMM; across GPUs it stays on the
+        # step's stream (one RCCL communicator, one issue order)
+        side = (DEALER_SIDE and self.device.type == "cuda"
+                and getattr(self.comm, "world", 1) == 1)
+        if side:
+            main = torch.cuda.current_stream(self.device)
+            st = self.side_stream()
+            st.wait_stream(main)
+            with torch.cuda.stream(st):
+                pre = run()
+            pre.event = torch.cuda.Event()
+            pre.event.record(st)
+            for t in [s0, s1] + [t for t in pre.rrt + pre.rrm if t is not None]:
+                t.record_stream(main)
+        else:
+            pre = run()
         pre.stack = (s0, s1)
         return pre
 
@@ -504,6 +531,8 @@ class CyclicSession(StackedSession):
 
         bits = v.v.bits
         data = v.v.data.contiguous()
+        if pre is not None and pre.event is not None:  # the dealer part ran on a side stream
+            torch.cuda.current_stream(self.device).wait_event(pre.event)
         if pre is not None:
             s0, s1 = pre.stack
         else:

@@ -51,11 +51,12 @@ class DealerEarly:
     """The dealer's half of round A, done before the product exists (:func:`dealer_early`):
     P2's new shares already written into ``out0`` / ``out1``, P1's received rt1 / rm1."""
 
-    __slots__ = ("out0", "out1", "rrt", "rrm", "stack")
+    __slots__ = ("out0", "out1", "rrt", "rrm", "stack", "event")
 
     def __init__(self, out0, out1, rrt, rrm):
         self.out0, self.out1, self.rrt, self.rrm = out0, out1, rrt, rrm
         self.stack = None  # the session's (s0, s1) tensors that out0 / out1 are views of
+        self.event = None  # set when the dealer part ran on a side stream (wait before use)
 
 
 def dealer_early(sess, plc, roles, like, bits, m, nonces, out0, out1, slots):
