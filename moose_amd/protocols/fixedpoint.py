@@ -134,6 +134,10 @@ def _dot_public_trunc_jobs(sess, x, y, px, py, m):
     plc, bits = t.plc, t.bits
     pc = sess.public(plc, _pub(px if px is not None else py))
     v0 = sess.p("Dot", plc, pc, t.s0) if px is not None else sess.p("Dot", plc, t.s0, pc)
+    if DEFER_DOT_TRUNC:
+        # the tail waits for the reader: the shares complete with the same tail when read,
+        # the sigmoid's decomposition and a reveal take the untruncated value instead
+        return _with(base, rep.PendingTrunc(sess, plc, bits, v0.v, m))
     nonces = _tail_nonces(sess, plc)
     r = rep.tail_job(sess, plc, bits, m, nonces, v0,
                      lambda o0, o1: R.MulJob(1, o0, o1, a=v0.v.data.contiguous()))
@@ -254,6 +258,8 @@ def shape_of(sess, x):
     t = x.t if isinstance(x, RepFixed) else x
     if isinstance(t, MV):
         return tuple(t.v.shape)
+    if isinstance(t, rep.PendingTrunc) and not t.completed:  # without completing it
+        return sess.p_shape(PV(t.plc, t.v_add))
     return sess.p_shape(t.s0)
 
 
@@ -879,15 +885,21 @@ def _merged_exp_tail(sess, x: RepFixed, fac: RepTensor, npad: int) -> RepFixed:
 
 def _jobs_ok(sess, *reps) -> bool:
     """A per-party session whose products can run through the batched tail kernels
-    (csrc/rss_jobs.hip): same-shape dense shares within each operand."""
+    (csrc/rss_jobs.hip): same-shape dense shares within each operand (a pending dot is
+    judged by its additive share, without completing it)."""
     if getattr(sess, "party_jobs", None) is None or not rep.JOBS:
         return False
     if os.environ.get("MOOSEX_DOT_TAIL", "1") == "0" or reps[0].bits not in (64, 128):
         return False
     if sess.party_index(reps[0].plc) is None:
         return True
-    return all(isinstance(t.v, R.RT) and t.v.data.is_contiguous()
-               and t.v.shape == r.s0.v.shape for r in reps for t in (r.s0, r.s1))
+
+    def ok(r):
+        if isinstance(r, rep.PendingTrunc) and not r.completed:
+            return isinstance(r.v_add, R.RT) and r.v_add.data.is_contiguous()
+        return all(isinstance(t.v, R.RT) and t.v.data.is_contiguous()
+                   and t.v.shape == r.s0.v.shape for t in (r.s0, r.s1))
+    return all(ok(r) for r in reps)
 
 
 def _abs_scaled_jobs(sess, s: RepTensor, x: RepFixed, c: float) -> RepFixed:
@@ -1122,6 +1134,8 @@ def sigmoid(sess, x: RepFixed) -> RepFixed:
     return _with(pos, rep.mux(sess, s, one_minus.t, pos.t))
 
 
+# per-party sessions leave a public-operand dot's TruncPr pending until it is read
+DEFER_DOT_TRUNC = os.environ.get("MOOSEX_DEFER_DOT_TRUNC", "1") != "0"
 # per-party sessions finish 2^-a with one product (the polynomial's sum untruncated)
 EXP_ONE_PRODUCT = os.environ.get("MOOSEX_EXP_ONE_PRODUCT", "1") != "0"
 # per-party sessions evaluate the sigmoid's reciprocal as one degree-8 polynomial
@@ -1154,20 +1168,33 @@ def _sign_and_exp_party(sess, x: RepFixed):
     if not (ONE_DECOMPOSITION and SIGN_WIDTH) or getattr(sess, "is_simulated", True):
         return None
     f, integ, bits = x.frac, x.integ, x.bits
-    fc = min(f, bits - 3 - integ - f)
+    # a dot whose TruncPr is pending (rep.PendingTrunc): decompose its untruncated value
+    # (m more fractional bits) after ONE reshare round instead of the tail's two
+    pend = x.t if isinstance(x.t, rep.PendingTrunc) and not x.t.completed else None
+    extra = pend.m if pend is not None else 0
+    fc = min(f, bits - 3 - integ - f - extra)
+    if fc < 20 and pend is not None:
+        pend, extra = None, 0  # too few ring bits for both: complete the dot first
+        fc = min(f, bits - 3 - integ - f)
     if fc < 20:
         return None
-    F = f + fc
+    F = f + extra + fc
     q = integ + 1 + F  # the sign plane: |z| < 2^(q)
     nint = max(1, min(bits - 2 - f, integ + 1))
     if q > bits - 1 or F + nint > q:
         return None
-    C = int(round(math.log2(math.e) * (1 << fc)))
-    z = rep.lincomb(sess, [(C, x.t)])
     jn = 1
     while jn < nint and (1 << jn) <= f + 2:
         jn += 1
     split = RANGE_SPLIT and jn < nint and F + jn < q
+    if pend is not None and not split and F + (1 << (nint - 1).bit_length()) > bits:
+        # the full product tree's planes would not fit above the pending scale: complete
+        # the dot first (the tail's two rounds) and decompose at the type's scale
+        pend = None
+        F -= extra
+        q -= extra
+    C = int(round(math.log2(math.e) * (1 << fc)))
+    z = rep.lincomb(sess, [(C, pend.reshare_untruncated() if pend is not None else x.t)])
     if split:
         T = R.fill((), 1 << (F + jn), bits, sess.device)
         zs = concat(sess, [RepFixed(z, F, integ), RepFixed(rep.sub_public(sess, z, T), F, integ),

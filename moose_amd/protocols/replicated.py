@@ -44,6 +44,7 @@ from moose_amd.ir.computation import ReplicatedPlacement
 from moose_amd.ops import ring as R
 from moose_amd.runtime.session import HV
 from moose_amd.runtime.session import PV
+from moose_amd.runtime.session import Public
 from moose_amd.utils.telemetry import span
 
 
@@ -128,6 +129,106 @@ class DeferredRep(RepTensor):
         self._s1 = v
 
 
+class PendingTrunc(RepTensor):
+    """A fixed-point product still 2^m above its type, held as this party's 3-out-of-3
+    additive share ``v_add`` (a per-party dot before its tail:
+    fixedpoint._dot_public_trunc_jobs), plus public addends at the truncated scale
+    (``pubs``, party 0 adds them).  Reading the shares completes it with the batched tail
+    (zero share + reshare + TruncPr by m: the dot's 2 rounds, as before).  Aware readers
+    skip the truncation: the sigmoid's one bit decomposition takes the reshared
+    untruncated value (:meth:`reshare_untruncated`, 1 round), a reveal opens the masked
+    additive shares and shifts exactly (1 round instead of 3)."""
+
+    def __init__(self, sess, plc, bits, v_add, m, pubs=()):
+        self._sess, self.v_add, self.m, self.pubs = sess, v_add, m, list(pubs)
+        self.completed = False
+        super().__init__(plc, bits, "arith", None, None)
+
+    def with_public(self, c):
+        return PendingTrunc(self._sess, self.plc, self.bits, self.v_add, self.m,
+                            self.pubs + [c])
+
+    def additive(self):
+        """This party's additive share of 2^m (x + pubs) (members only)."""
+        v = self.v_add
+        if self._sess.party_index(self.plc) == 0 and self.pubs:
+            scale = R.fill((), 1 << self.m, self.bits, v.data.device)
+            for c in self.pubs:
+                cv = c.v if isinstance(c, Public) else c
+                v = R.binary("add", v, R.binary("mul", cv, scale))
+        return v
+
+    def _complete(self):
+        if self.completed:
+            return
+        self.completed = True
+        sess, plc, bits = self._sess, self.plc, self.bits
+        nonces = tuple(sess.nonce(plc) for _ in range(7))
+        member = sess.party_index(plc) is not None
+        v = self.additive() if member else self.v_add
+        like = PV(plc, v)
+        r = tail_job(sess, plc, bits, self.m, nonces, like,
+                     lambda o0, o1: R.MulJob(1, o0, o1, a=v.data.contiguous()))
+        self._s0, self._s1 = r.s0, r.s1
+
+    def reshare_untruncated(self):
+        """Replicated shares of 2^m (x + pubs): zero share + one reshare round."""
+        sess, plc = self._sess, self.plc
+        member = sess.party_index(plc) is not None
+        z = sess.p_add_zero_share(plc, PV(plc, self.additive() if member else self.v_add))
+        return _reshare(sess, plc, z, self.bits, "arith")
+
+    @property
+    def s0(self):
+        self._complete()
+        return self._s0
+
+    @s0.setter
+    def s0(self, v):
+        self._s0 = v
+
+    @property
+    def s1(self):
+        self._complete()
+        return self._s1
+
+    @s1.setter
+    def s1(self, v):
+        self._s1 = v
+
+
+def _reveal_pending(sess, x: PendingTrunc, host):
+    """Open a PendingTrunc to a member: the other two parties send their zero-share-masked
+    additive shares, the host sums them with its own and shifts by m (floor, exact): ONE
+    round instead of the tail's two plus the reveal.  None: the generic reveal."""
+    from moose_amd.parallel.spmd import Remote
+
+    plc = x.plc
+    if host not in plc.owners or not hasattr(sess, "party_exchange"):
+        return None
+    j = plc.owners.index(host)
+    idx = sess.party_index(plc)
+    x.completed = True  # its shares are never formed
+    z = sess.p_add_zero_share(plc, PV(plc, x.additive() if idx is not None else x.v_add))
+    like = (tuple(z.v.data.shape), z.v.data.dtype) if idx is not None else None
+    mine = z.v.data if idx is not None else None
+    got = sess.party_exchange(plc, [("a", (j + 1) % 3, j, mine if idx == (j + 1) % 3 else None,
+                                     like),
+                                    ("b", (j + 2) % 3, j, mine if idx == (j + 2) % 3 else None,
+                                     like)])
+    for a in ((j + 1) % 3, (j + 2) % 3):
+        sess.stats.record_send(plc.owners[a], host, payload_bytes_of(z.v) if idx is not None
+                               else 0)
+    if idx != j:
+        return HV(host, Remote(x.bits))
+    return HV(host, R.opened(z.v, R.RT(got["a"], x.bits), R.RT(got["b"], x.bits),
+                             shift=x.m))
+
+
+def payload_bytes_of(v):
+    return v.data.numel() * v.data.element_size()
+
+
 def _owner_index(plc, host):
     try:
         return plc.owners.index(host)
@@ -203,6 +304,10 @@ def _share_outsider(sess, plc, x, kind, bits, shape):
 def reveal(sess, x: RepTensor, host: str) -> HV:
     """Open x to ``host`` (a party of x.plc or an outsider)."""
     with span("rep.reveal"):
+        if isinstance(x, PendingTrunc) and not x.completed:
+            r = _reveal_pending(sess, x, host)
+            if r is not None:
+                return r
         tail = getattr(x, "_tail", None)
         if tail is not None and not tail.done:
             fast = getattr(sess, "p_reveal_deferred", None)
@@ -299,7 +404,10 @@ def neg(sess, x: RepTensor) -> RepTensor:
 
 
 def add_public(sess, x: RepTensor, c) -> RepTensor:
-    """x + c for a public c (added to slot 0 only)."""
+    """x + c for a public c (added to slot 0 only).  A PendingTrunc stays pending (the
+    addend rides into its tail)."""
+    if isinstance(x, PendingTrunc) and not x.completed:
+        return x.with_public(c)
     return _apply_public(sess, x, x.add_prim, c)
 
 

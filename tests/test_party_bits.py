@@ -61,6 +61,8 @@ def test_range_split_and_deferred_truncation_save_rounds(device, monkeypatch):
     fewer; 2 rounds, the polynomial's levels run beside the tree's) and the reveal absorbs
     the reciprocal's last truncation (2 rounds); the values stay within 1e-6 of sklearn."""
     base, r_base, e_base = _lr(device, monkeypatch, True, True, one_dec=True, ring=128)
+    monkeypatch.setattr(FP, "DEFER_DOT_TRUNC", False)
+    nodot, r_nodot, e_nodot = _lr(device, monkeypatch, True, True, one_dec=True, ring=128)
     monkeypatch.setattr(FP, "EXP_ONE_PRODUCT", False)
     mid, r_mid, e_mid = _lr(device, monkeypatch, True, True, one_dec=True, ring=128)
     monkeypatch.setattr(FP, "RANGE_SPLIT", False)
@@ -68,8 +70,57 @@ def test_range_split_and_deferred_truncation_save_rounds(device, monkeypatch):
     old, r_old, e_old = _lr(device, monkeypatch, True, True, one_dec=True, ring=128)
     assert r_mid == r_old - 4
     # the exp's polynomial sum and final product as one truncated product: 2 rounds fewer
-    assert r_base == r_mid - 2
-    assert e_base < 1e-6 and e_mid < 1e-6 and e_old < 1e-6
+    assert r_nodot == r_mid - 2
+    # the dot's TruncPr left to its reader: the decomposition takes the untruncated value
+    # after one reshare round instead of the tail's two
+    assert r_base == r_nodot - 1
+    assert max(e_base, e_nodot, e_mid, e_old) < 1e-6
+
+
+def test_pending_dot_revealed_directly_and_read_by_other_ops():
+    """A public-operand dot on per-party sessions keeps its TruncPr pending
+    (rep.PendingTrunc): revealed directly it opens in one round and shifts exactly; read
+    by another op (here a multiplication) it completes with the dot's tail -- both within
+    the fixed-point error of the plaintext result."""
+    import moose_amd as pm
+
+    alice, bob, carole = (pm.host_placement(n) for n in IDS)
+    rep = pm.replicated_placement("rep", players=[alice, bob, carole])
+    mir = pm.mirrored_placement(name="mir", players=[alice, bob, carole])
+    fx = pm.fixed(24, 40)
+    w = np.array([[0.5, -1.25], [2.0, 0.125], [-0.75, 1.0]])
+
+    @pm.computation
+    def f(x: pm.Argument(placement=alice, vtype=pm.TensorType(pm.float64))):
+        with alice:
+            xf = pm.cast(x, dtype=fx)
+        wf = pm.cast(pm.constant(w, dtype=pm.float64, placement=mir), dtype=fx, placement=mir)
+        with rep:
+            y = pm.dot(xf, wf)
+            z = pm.mul(pm.dot(xf, wf), pm.dot(xf, wf))
+        with carole:
+            return pm.cast(y, dtype=pm.float64), pm.cast(z, dtype=pm.float64)
+
+    from moose_amd.protocols import replicated as R_
+
+    x = np.array([[1.5, -2.0, 0.25], [3.0, 0.5, -1.0]])
+    seen = []
+    orig = R_._reveal_pending
+
+    def spy(sess, v, host):
+        seen.append(host)
+        return orig(sess, v, host)
+
+    R_._reveal_pending = spy
+    try:
+        rt = LocalMooseRuntime(IDS, device_map={i: "cpu" for i in IDS}, seed=4)
+        got = [np.asarray(v) for v in rt.evaluate_computation(f, {"x": x}).values()]
+    finally:
+        R_._reveal_pending = orig
+    p = x @ w
+    for want in (p, p * p):
+        assert any(g.shape == want.shape and np.abs(g - want).max() < 1e-9 for g in got)
+    assert seen  # the dot revealed directly was opened without its tail
 
 
 def test_deferred_truncation_read_by_another_op(monkeypatch):
