@@ -346,6 +346,13 @@ int mx_jobs_r2(int dev, int words, int njobs, const void* const* ptrs, const int
 int mx_bits_front(int dev, int words, int role, int64_t n, const void* xa, const void* xb,
                   const void* arecv, void* msg, void* z, void* p0, void* p1,
                   const uint32_t* const* slots, const uint64_t* nonces, void* stream);
+// Per-party fused weighted sums over both share components (wsum_pair.h): ring values as
+// ``words`` little-endian int64 each (w: nrows of them, cb: nblk).
+int mx_wsum_pair(int dev, int words, int nrows, int nblk, int has2, int pub0, int pub1,
+                 int64_t L, int64_t rs, const int64_t* w, const int64_t* wx, const int64_t* m2,
+                 const int64_t* c2, const int64_t* cb, const void* r0, const void* r1,
+                 const void* x0, const void* x1, void* o0, void* o1, void* q0, void* q1,
+                 void* stream);
 int mx_bits_b2a(int dev, int words, int phase, int role, int64_t S, int start, int count,
                 int xbit, int blocks, const void* const* src, const void* arecv, void* msg, void* z, void* base0,
                 void* base1, const void* zr, void* out0, void* out1,

@@ -231,6 +231,9 @@ _SIGS = {
     "mx_jobs_r2": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp]),
     "mx_bits_front": (c_int, [c_int, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                               c_vp, c_vp, c_vp, c_vp]),
+    "mx_wsum_pair": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_i64, c_i64,
+                             c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                             c_vp, c_vp, c_vp]),
     "mx_bits_b2a": (c_int, [c_int, c_int, c_int, c_int, c_i64, c_int, c_int, c_int, c_int,
                             c_vp, c_vp, c_vp,
                             c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

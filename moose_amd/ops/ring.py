@@ -2181,3 +2181,45 @@ def bits_b2a(phase, role, src, start, count, bits, slots, n1, ng, arecv=None, st
         _p(z), _p(b0), _p(b1), None, None, None, _slots_arr(slots), _nonces_arr((n1, ng)),
         nat.stream_of(like)), "bits_b2a")
     return msg, z, b0, b1
+
+
+def _ring_words(values, bits):
+    """Python ints -> a ctypes int64 array of their little-endian 64-bit words (mod 2^bits)."""
+    w = _words(bits)
+    out = []
+    for v in values:
+        v = int(v) % (1 << bits)
+        for j in range(w):
+            out.append(_to_i64((v >> (64 * j)) & MASK64))
+    return (ctypes.c_int64 * max(1, len(out)))(*out)
+
+
+def wsum_pair(bits, L, rows=None, weights=(), x=None, wx=0, pub=(False, False), cblk=(0,),
+              second=None, like=None):
+    """Per-party fused weighted sums over both share components (csrc/wsum_pair.h):
+    s_c = sum_k weights[k] rows_c[k] + wx x_c; returns (o0, o1) of nblk = len(cblk) blocks
+    of L elements, block b = s_c + cblk[b] on the public slots ``pub`` (this party's copies
+    of x_0), and with ``second`` = (m2, c2) also (q0, q1) = m2 s_c + c2 on those slots.
+    ``rows`` = (r0, r1) tensors holding len(weights) rows of L elements, contiguous."""
+    ref = like if like is not None else (rows[0] if rows is not None else x[0])
+    nrows = len(weights)
+    if nrows > 64 or not 1 <= len(cblk) <= 3:
+        raise ValueError("wsum_pair: at most 64 rows and 3 blocks")
+    dev = ref.device
+    shp = (len(cblk) * L,) + ((2,) if bits == 128 else ())
+    o0 = torch.empty(shp, dtype=torch.int64, device=dev)
+    o1 = torch.empty_like(o0)
+    q0 = q1 = None
+    if second is not None:
+        q0 = torch.empty(((L,) + ((2,) if bits == 128 else ())), dtype=torch.int64, device=dev)
+        q1 = torch.empty_like(q0)
+    r = [None, None] if rows is None else [t.contiguous() for t in rows]
+    xx = [None, None] if x is None else [t.contiguous() for t in x]
+    m2, c2 = second if second is not None else (0, 0)
+    nat.check(nat.lib().mx_wsum_pair(
+        nat.dev_of(o0), _words(bits), nrows, len(cblk), 1 if second is not None else 0,
+        1 if pub[0] else 0, 1 if pub[1] else 0, L, L, _ring_words(weights, bits),
+        _ring_words([wx], bits), _ring_words([m2], bits), _ring_words([c2], bits),
+        _ring_words(cblk, bits), _p(r[0]), _p(r[1]), _p(xx[0]), _p(xx[1]), _p(o0), _p(o1),
+        _p(q0), _p(q1), nat.stream_of(o0)), "wsum_pair")
+    return (o0, o1) if second is None else (o0, o1, q0, q1)

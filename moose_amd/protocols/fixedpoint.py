@@ -491,7 +491,7 @@ def _poly_eval_jobs(sess, x: RepFixed, coeffs, shift: int = 0) -> RepFixed:
     return add_const(sess, RepFixed(acc, f, x.integ), coeffs[0] / (1 << shift))
 
 
-def _poly_powers_sum(sess, x: RepFixed, coeffs) -> RepTensor:
+def _poly_powers_sum(sess, x: RepFixed, coeffs, finish=None):
     """sum_{k>=1} w_k x^k (w_k = c_k at x's fractional bits) WITHOUT truncation: the power
     levels of _poly_eval_jobs, then the weighted sum of the replicated powers -- both share
     components, so the result is replicated (scale 2^2f) and costs no round."""
@@ -516,8 +516,71 @@ def _poly_powers_sum(sess, x: RepFixed, coeffs) -> RepTensor:
 
         r = PV(plc, Remote(bits))
         rows = RepTensor(plc, bits, "arith", r, r)
+    if finish is not None:  # (c0, m2, c2): W + c0 and m2 (W + c0) + c2 in one launch
+        c0, m2, c2 = finish
+        got = _wsum(sess, rows, weights[1:], x=t, wx=weights[0], cblk=(c0,),
+                    second=(m2, (m2 * c0 + c2)))
+        if got is not None:
+            return got
+        big = rep.add_public(sess, rep.lincomb(sess, [(weights[0], t),
+                                                      (1, _weighted(sess, rows, weights[1:],
+                                                                    bits))]),
+                             R.fill((), c0, bits, sess.device))
+        return big, rep.lincomb(sess, [(m2, big)], const=R.fill((), c2, bits, sess.device))
     acc = _weighted(sess, rows, weights[1:], bits)
     return rep.lincomb(sess, [(weights[0], t), (1, acc)])
+
+
+def _wsum(sess, rows, weights, x=None, wx=0, cblk=(0,), second=None, nrows=None):
+    """Per-party fused local step (csrc/wsum_pair.h): s = sum_k weights[k] rows[k] + wx x
+    over both share components in ONE launch; returns the RepTensor s + cblk[b] (blocks on
+    a new leading axis when len(cblk) > 1, the public constants on this party's copies of
+    x_0) and, with ``second`` = (m2, c2), also m2 s + c2.  Bitwise the composition of the
+    separate weighted sum / multiply / add / lincomb steps (ring arithmetic).  None when
+    the session is not a per-party one (the caller runs those steps)."""
+    from moose_amd.parallel.spmd import Remote
+
+    if not WSUM_FUSED or getattr(sess, "party_jobs", None) is None:
+        return None
+    ref = rows if rows is not None else x
+    plc, bits = ref.plc, ref.bits
+    if bits not in (64, 128):
+        return None
+    idx = sess.party_index(plc)
+    nb = len(cblk)
+    if idx is None:
+        r = PV(plc, Remote(bits))
+        t = RepTensor(plc, bits, "arith", r, r)
+        return t if second is None else (t, t)
+    if rows is not None:
+        k = len(weights)
+        r0, r1 = rows.s0.v.data, rows.s1.v.data
+        if not (r0.is_contiguous() and r1.is_contiguous()):
+            return None
+        per = tuple(r0.shape[1:-1] if bits == 128 else r0.shape[1:])
+        r0, r1 = r0[:k], r1[:k]
+    else:
+        per = tuple(x.s0.v.data.shape[:-1] if bits == 128 else x.s0.v.data.shape)
+        r0 = r1 = None
+    L = max(1, math.prod(per))
+    xs = None
+    if x is not None:
+        xs = (x.s0.v.data, x.s1.v.data)
+    out = R.wsum_pair(bits, L, rows=None if r0 is None else (r0, r1), weights=weights, x=xs,
+                      wx=wx, pub=(idx == 0, idx == 2), cblk=cblk, second=second,
+                      like=(r0 if r0 is not None else xs[0]))
+    shp = ((nb * per[0],) + per[1:] if nb > 1 else per) + ((2,) if bits == 128 else ())
+    o = RepTensor(plc, bits, "arith", PV(plc, R.RT(out[0].reshape(shp), bits)),
+                  PV(plc, R.RT(out[1].reshape(shp), bits)))
+    if second is None:
+        return o
+    pshp = per + ((2,) if bits == 128 else ())
+    return o, RepTensor(plc, bits, "arith", PV(plc, R.RT(out[2].reshape(pshp), bits)),
+                        PV(plc, R.RT(out[3].reshape(pshp), bits)))
+
+
+# MOOSEX_WSUM_FUSED=0: per-party local weighted sums as separate launches
+WSUM_FUSED = os.environ.get("MOOSEX_WSUM_FUSED", "1") != "0"
 
 
 def _rows_ok(sess, x) -> bool:
@@ -678,12 +741,15 @@ def _exp2_from_planes(sess, ab: RepTensor, f: int, integ: int, bits: int, nint: 
     rows 0..f-1 the fraction, rows f..f+npad-1 the integer part (rows from nint on weigh 0).
     ``cs``: the factor rows' public weights (c_j - 1) 2^f when the caller chose them."""
     frac_w = [(1 << j) for j in range(f)] + [0] * npad
-    r = RepFixed(_weighted(sess, ab, frac_w, bits), f, integ)
-    if negative:
+    fused = _wsum(sess, ab, [-(1 << j) for j in range(f)], cblk=(1 << f,)) if negative else None
+    if fused is not None:  # 1 - r in one launch (weighted sum, negation, public 1)
+        px, shift = RepFixed(fused, f, integ), 1
+    elif negative:
+        r = RepFixed(_weighted(sess, ab, frac_w, bits), f, integ)
         # 2^-r for r in [0,1) = 2^(1-r) / 2 -> fit exp2 on [0, 1] of (1 - r)
         px, shift = const_sub(sess, 1.0, r), 1
     else:
-        px, shift = r, 0
+        px, shift = RepFixed(_weighted(sess, ab, frac_w, bits), f, integ), 0
     one_minus = px
     # integer part factors 1 + b_j (c_j - 1), c_j = 2^(+-2^j), for all j at once: the
     # integer bit planes stay stacked on the leading axis, scaled by a public vector
@@ -1010,11 +1076,18 @@ def _merged_exp_tail_jobs(sess, x: RepFixed, fac: RepTensor, npad: int) -> RepFi
         c0 = int(round(coeffs[0] * (1 << (f + fw))))
         if member:
             mod = 1 << bits
-            acc = []
-            for X, rows in ((st.x0, st.s0), (st.x1, st.s1)):
-                rest = R.weighted_sum(R.RT(rows[:n - 1], bits), [w % mod for w in wts[1:]])
-                lin = R.binary("mul", R.RT(X, bits), R.fill((), wts[0], bits, X.device))
-                acc.append(R.binary("add", rest, lin).data)
+            if WSUM_FUSED:  # both components' sums in one launch
+                L = max(1, math.prod(shape))
+                a0, a1 = R.wsum_pair(bits, L, rows=(st.s0[:n - 1], st.s1[:n - 1]),
+                                     weights=wts[1:], x=(st.x0, st.x1), wx=wts[0],
+                                     pub=(False, False))
+                acc = [a0.reshape(st.x0.shape), a1.reshape(st.x0.shape)]
+            else:
+                acc = []
+                for X, rows in ((st.x0, st.s0), (st.x1, st.s1)):
+                    rest = R.weighted_sum(R.RT(rows[:n - 1], bits), [w % mod for w in wts[1:]])
+                    lin = R.binary("mul", R.RT(X, bits), R.fill((), wts[0], bits, X.device))
+                    acc.append(R.binary("add", rest, lin).data)
             o0, o1 = torch.empty_like(st.x0), torch.empty_like(st.x0)
             run([R.MulJob(1, o0, o1, x=(acc[0], acc[1]), y=(F0[0], F1[0]), a=F0[0], ca=c0)],
                 m=f + fw + 1)
@@ -1113,10 +1186,9 @@ def sigmoid(sess, x: RepFixed) -> RepFixed:
             # round; sigma * 2^(2f+1) = pos' + s (2^(2f+1) - 2 pos') is one mul_add whose
             # reshare AND truncation by f + 1 wait for the reader -- the reveal opens it in
             # one round and shifts exactly (2 rounds fewer than TruncPr(W) then mul_add)
-            W = _poly_powers_sum(sess, d, coeffs)
-            big = rep.add_public(sess, W, _encode_const(sess, coeffs[0], 2 * f, bits))
-            diff = rep.lincomb(sess, [(-2, big)], const=_encode_const(sess, 1.0, 2 * f + 1,
-                                                                        bits))
+            c0 = int(round(coeffs[0] * (1 << (2 * f))))
+            big, diff = _poly_powers_sum(sess, d, coeffs,
+                                         finish=(c0, -2, int(round(1.0 * (1 << (2 * f + 1))))))
             return RepFixed(rep.mul_add_trunc(sess, s, diff, big, f + 1), f, d.integ)
         pos = poly_eval(sess, d, coeffs, shift=1)
     else:
@@ -1194,11 +1266,17 @@ def _sign_and_exp_party(sess, x: RepFixed):
         F -= extra
         q -= extra
     C = int(round(math.log2(math.e) * (1 << fc)))
-    z = rep.lincomb(sess, [(C, pend.reshare_untruncated() if pend is not None else x.t)])
+    xt = pend.reshare_untruncated() if pend is not None else x.t
+    z = None if split else rep.lincomb(sess, [(C, xt)])
     if split:
-        T = R.fill((), 1 << (F + jn), bits, sess.device)
-        zs = concat(sess, [RepFixed(z, F, integ), RepFixed(rep.sub_public(sess, z, T), F, integ),
-                           RepFixed(rep.add_public(sess, z, T), F, integ)], 0).t
+        Tv = 1 << (F + jn)
+        zs = _wsum(sess, None, (), x=xt, wx=C, cblk=(0, -Tv, Tv))  # the 3 blocks, 1 launch
+        if zs is None:
+            z = rep.lincomb(sess, [(C, xt)])
+            T = R.fill((), Tv, bits, sess.device)
+            zs = concat(sess, [RepFixed(z, F, integ),
+                               RepFixed(rep.sub_public(sess, z, T), F, integ),
+                               RepFixed(rep.add_public(sess, z, T), F, integ)], 0).t
         nfac = jn + 2
         npad = 1 << (nfac - 1).bit_length()
         extra = npad - nfac  # planes above jn whose factor is 1 (weight 0)

@@ -211,3 +211,16 @@ def test_sign_bit_width_bound_is_exact_on_the_boundary(monkeypatch):
     rt = LocalMooseRuntime(IDS, device_map={i: "cpu" for i in IDS}, seed=2)
     got = np.asarray(list(rt.evaluate_computation(f, {"x": x}).values())[0])
     np.testing.assert_allclose(got, np.maximum(x, 0), atol=1e-9)
+
+
+@pytest.mark.parametrize("ring", [64, 128])
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_fused_weighted_sums_bitwise_equal_separate_steps(device, ring, monkeypatch):
+    """csrc/wsum_pair: the per-party weighted sums with their public terms in one launch
+    (exp's 1 - r, the polynomial sums, the sigmoid's blocks and mirror operand) give
+    bitwise the shares of the separate weighted-sum / multiply / add / lincomb steps."""
+    monkeypatch.setattr(FP, "WSUM_FUSED", True)
+    fused, r_f, e = _lr(device, monkeypatch, True, True, one_dec=True, ring=ring)
+    monkeypatch.setattr(FP, "WSUM_FUSED", False)
+    sep, r_s, _ = _lr(device, monkeypatch, True, True, one_dec=True, ring=ring)
+    assert np.array_equal(fused, sep) and r_f == r_s and e < 1e-6
