@@ -212,9 +212,13 @@ def _cache_put(cache, key, t, limit):
         return
     from moose_amd.runtime import lanes
 
-    if (lanes.ACTIVE or SHARED_STREAMS) and t.data.is_cuda:
-        torch.cuda.current_stream(t.data.device).synchronize()
-    cache[key] = t
+    d = t[1].data if isinstance(t, tuple) else t.data
+    if (lanes.ACTIVE or SHARED_STREAMS) and d.is_cuda:
+        torch.cuda.current_stream(d.device).synchronize()
+    with _SHARED_LOCK:
+        # first in wins: parties on threads may make one constant at once, and an entry
+        # keyed by an object's id must keep that object alive (never replaced)
+        cache.setdefault(key, t)
 
 
 def fill(shape, value: int, bits, device) -> RT:
@@ -575,11 +579,13 @@ def encode_lazy(x: torch.Tensor, frac: int, bits: int) -> RT:
     if id(x) in CONST_IDS and x.is_cuda:
         key = (id(x), int(frac), bits)
         hit = _ENCODED_CONSTS.get(key)
-        if hit is not None:
-            return hit
+        # the entry holds its source tensor: an id is only ever matched while that very
+        # tensor lives (a freed tensor's id may come back as another tensor's)
+        if hit is not None and hit[0] is x:
+            return hit[1]
         if not torch.cuda.is_current_stream_capturing():
             e = encode(x, frac, bits)
-            _cache_put(_ENCODED_CONSTS, key, e, 4096)
+            _cache_put(_ENCODED_CONSTS, key, (x, e), 4096)
             return e
     if bits not in (64, 128):
         return encode(x, frac, bits)

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import math
 import os
+import threading
 from typing import Dict
 
 import numpy as np
@@ -45,6 +46,7 @@ from moose_amd.utils.telemetry import span
 _FLOAT = {"Float32": torch.float32, "Float64": torch.float64}
 # small numeric tensor constants of computations, uploaded once per (value, device)
 _CONST_LV = {}
+_CONST_LOCK = threading.Lock()
 # multi-round elementwise ops merged across independent chains (Interpreter._merge_unary)
 _MERGE_KINDS = {"Sigmoid", "Exp", "Log", "Log2", "Sqrt", "Relu", "Abs"}
 _MERGE_FNS = {"Sigmoid": fxp.sigmoid, "Exp": fxp.exp, "Log": fxp.log, "Log2": fxp.log2,
@@ -805,8 +807,14 @@ class Interpreter:
             if len(_CONST_LV) < 1024:  # public constants are never written
                 if _lanes.ACTIVE or R.SHARED_STREAMS:  # other streams read it next
                     torch.cuda.current_stream(lv.v.v.device).synchronize()
-                _CONST_LV[key] = lv
-                R.CONST_IDS.add(id(lv.v.v))  # kept alive by the cache: the id stays its own
+                with _CONST_LOCK:
+                    # parties on threads may make the same constant at once: the first in
+                    # stays cached and is used; an id is registered only for a tensor the
+                    # cache keeps alive (a dropped one's id could return as another's)
+                    kept = _CONST_LV.setdefault(key, lv)
+                    if kept is lv:
+                        R.CONST_IDS.add(id(lv.v.v))
+                lv = kept
         if isinstance(plc, HostPlacement):
             return lv
         # constants on replicated / mirrored placements are public

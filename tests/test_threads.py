@@ -388,3 +388,36 @@ def test_party_streams_fall_back_to_per_action_replay(monkeypatch):
                 assert np.array_equal(np.asarray(got[k]), np.asarray(want[k])), k
     (_, tapes), = rt._party_tapes.values()
     assert tapes._party_graphs is None and calls["n"] == 2
+
+
+def test_shared_constant_caches_first_in_wins():
+    """Parties on threads may make one constant at once: the shared caches keep the first
+    (an entry keyed by an object's id must keep that object alive), so a dropped second
+    copy's id can never alias a cached constant later."""
+    from moose_amd.ops import ring as R
+
+    cache = {}
+    a, b = R.fill((3,), 1, 64, "cpu"), R.fill((3,), 1, 64, "cpu")
+    R._cache_put(cache, "k", a, 10)
+    R._cache_put(cache, "k", b, 10)
+    assert cache["k"] is a
+
+
+@pytest.mark.gpu
+def test_encoded_constant_cache_checks_identity():
+    """An encoded-constant entry is only returned for the very tensor it was made from (a
+    freed constant's id may come back as another tensor's: the round-5 intermittent
+    'dot shape mismatch' of threaded parties on one GPU)."""
+    from moose_amd.ops import ring as R
+
+    x = torch.ones(3, 2, dtype=torch.float64, device="cuda:0")
+    y = torch.full((200, 10), 2.0, dtype=torch.float64, device="cuda:0")
+    R.CONST_IDS.add(id(y))
+    R._ENCODED_CONSTS[(id(y), 10, 128)] = (x, R.encode(x, 10, 128))  # a stale entry
+    try:
+        e = R.encode_lazy(y, 10, 128)
+        assert tuple(e.shape) == (200, 10)
+        assert np.allclose(R.decode(e, 10).cpu().numpy(), 2.0)
+    finally:
+        R.CONST_IDS.discard(id(y))
+        R._ENCODED_CONSTS.pop((id(y), 10, 128), None)
