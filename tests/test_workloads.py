@@ -19,14 +19,20 @@ def _load(name):
     return mod
 
 
-def test_logreg_training_matches_fp64():
+@pytest.mark.parametrize("layout", ["stacked", "parties"])
+def test_logreg_training_matches_fp64(layout):
+    """The reference's LogReg training workload; "parties": the three parties as threads
+    with their own per-party protocol code (the sigmoid's deferred mirror and truncation
+    then complete through the gradient's reads instead of a reveal)."""
     L = _load("logreg_train")
     bs, n_it, nf = 16, 3, 100
     rng = np.random.default_rng(1)
     x = rng.standard_normal((bs * n_it, nf))
     y = rng.integers(2, size=(bs * n_it, 1)).astype(np.float64)
     comp = L.build_training(bs, n_it, n_features=nf)
-    rt = pm.LocalMooseRuntime(["alice", "bob", "carole"], device="cpu")
+    ids = ["alice", "bob", "carole"]
+    kw = {"device_map": {i: "cpu" for i in ids}} if layout == "parties" else {}
+    rt = pm.LocalMooseRuntime(ids, device="cpu", **kw)
     outs = rt.evaluate_computation(comp, {"x": x, "y": y, "w_0": np.zeros((nf, 1)),
                                           "b_0": np.zeros((1, 1))})
     w_ref, b_ref = L.plaintext_training(x, y, bs, n_it)
