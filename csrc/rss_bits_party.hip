@@ -4,6 +4,8 @@
 // stream the role draws, are computed one per thread into LDS, then the elements finished.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "bits_party.h"
 #include "moosex.h"
 #include "prf_dev.h"
@@ -129,6 +131,66 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// Throughput form of phases 0 / 1 (larger B2As, e.g. all bit planes of a decomposition): one
+// thread per ChaCha block index of every stream the role draws, its 4 chunks' elements
+// finished from registers -- a quarter of the latency form's keystream work (which computes a
+// whole block for each chunk), the same chunk -> element mapping (so bitwise the same).
+template <class T>
+__global__ void __launch_bounds__(256)
+    k_b2a_tp(int role, int64_t S, int start, int count, int xbit, int blocks,
+             const T* __restrict__ s0, const T* __restrict__ s1, const T* __restrict__ g0,
+             const T* __restrict__ g1, const T* __restrict__ t0, const T* __restrict__ t1,
+             const T* __restrict__ arecv, T* __restrict__ msg, T* __restrict__ z,
+             T* __restrict__ base0, T* __restrict__ base1, mxd::KeySrc keys, Str ss) {
+  __shared__ uint32_t rks[2][mxd::kKeyWords];
+  mxd::stage_keys(rks, keys, 2);
+  constexpr int P = mxd::Lane<T>::kPer;
+  const int64_t n = S * count;
+  const int64_t nch = (n + P - 1) / P;
+  const int64_t nblk = (int64_t)mx::ks_blocks_for((uint64_t)nch);
+  const int o = role == 1 ? 0 : 1;
+  for (int64_t B = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; B < nblk;
+       B += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t w[3][16];
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      if (q < ss.n) mx::chacha_block(rks[ss.key[q]], ss.nonce[q], (uint64_t)B, w[q]);
+#pragma unroll
+    for (int part = 0; part < 4; ++part) {
+      const int64_t c = (int64_t)mx::ks_chunk((uint64_t)B, part);
+      if (c >= nch) break;
+      uint64_t lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        if (q < ss.n) mx::part_u64(w[q], part, &lo[q], &hi[q]);
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const int64_t i = c * P + j;
+        if (i >= n) break;
+        const int64_t row = i / S, e = i - row * S;
+        int qbit, xq, blk, neg;
+        mxb::plane_of((int)row, start, count, xbit, blocks, &qbit, &xq, &blk, &neg);
+        const int64_t es = e + blk * S;
+        const T fa = role == 1 ? (T)0 : mxd::pick<T>(lo[0], hi[0], j);
+        const T fo = mxd::pick<T>(lo[o], hi[o], j);
+        const T fn = mxd::pick<T>(lo[o + 1], hi[o + 1], j);
+        T c0 = role == 1 ? (T)0 : src_bit<T>(s0, g0, t0, es, qbit);
+        T c1 = role == 2 ? (T)0 : src_bit<T>(s1, g1, t1, es, qbit);
+        if (xq >= 0) {
+          if (role != 1) c0 ^= src_bit<T>(s0, g0, t0, es, xq);
+          if (role != 2) c1 ^= src_bit<T>(s1, g1, t1, es, xq);
+        }
+        if (neg && role == 0) c0 ^= (T)1;
+        const mxb::B2a<T> r = mxb::b2a<T>(role, c0, c1, role == 1 ? arecv[i] : (T)0, fa, fo, fn);
+        if (role == 0) msg[i] = r.msg;
+        z[i] = r.z;
+        base0[i] = r.base0;
+        base1[i] = r.base1;
+      }
+    }
+  }
+}
+
 Str streams(int role, const uint64_t* nn) {
   // nn = (n1, n_g); role 0: (own, n1), role 2: (next, n1); then (own, n_g), (next, n_g)
   Str s{};
@@ -192,6 +254,24 @@ int mxh_bits_b2a(int words, int phase, int role, int64_t S, int start, int count
   const unsigned g = phase == 2 ? (unsigned)mxd::grid_for(n) : 0;
   const void* none[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   if (src == nullptr) src = none;  // phase 2 reads no source
+  // phases 0 / 1 over more than a few thousand chunks: the throughput form
+  const int64_t nch_ = words == 2 ? n : (n + 1) / 2;
+  if (phase != 2 && nch_ >= 2048 && getenv("MOOSEX_B2A_TP") == nullptr) {
+#define MX_B2A_TP(T)                                                                         \
+  hipLaunchKernelGGL(k_b2a_tp<T>, dim3(mxd::grid_for_chunks(nch_)), dim3(256), 0, st, role, S, \
+                     start, count, xbit, blocks, (const T*)src[0], (const T*)src[1],          \
+                     (const T*)src[2], (const T*)src[3], (const T*)src[4], (const T*)src[5],  \
+                     (const T*)arecv, (T*)msg, (T*)z, (T*)base0, (T*)base1, k, ss)
+    if (words == 1)
+      MX_B2A_TP(u64);
+    else if (words == 2)
+      MX_B2A_TP(u128);
+    else
+      return -2;
+#undef MX_B2A_TP
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : -100 - (int)e;
+  }
 #define MX_B2A_LAUNCH(T)                                                                   \
   hipLaunchKernelGGL(k_b2a<T>, dim3(phase == 2 ? g : grid_of<T>(n)), dim3(256), 0, st, phase, \
                      role, S, start, count, xbit, blocks, (const T*)src[0], (const T*)src[1],            \

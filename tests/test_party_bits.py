@@ -224,3 +224,16 @@ def test_fused_weighted_sums_bitwise_equal_separate_steps(device, ring, monkeypa
     monkeypatch.setattr(FP, "WSUM_FUSED", False)
     sep, r_s, _ = _lr(device, monkeypatch, True, True, one_dec=True, ring=ring)
     assert np.array_equal(fused, sep) and r_f == r_s and e < 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ring", [64, 128])
+def test_b2a_throughput_form_bitwise_equal_latency_form(ring, monkeypatch):
+    """csrc/rss_bits_party.hip k_b2a_tp (one thread per ChaCha block, its 4 chunks'
+    elements) against the latency form (a block per chunk): the same keystream chunk per
+    element, so bitwise the same shares."""
+    monkeypatch.delenv("MOOSEX_B2A_TP", raising=False)
+    tp, r_tp, e = _lr("cuda:0", monkeypatch, True, True, one_dec=True, ring=ring)
+    monkeypatch.setenv("MOOSEX_B2A_TP", "0")  # set: the latency form everywhere
+    lat, r_lat, _ = _lr("cuda:0", monkeypatch, True, True, one_dec=True, ring=ring)
+    assert np.array_equal(tp, lat) and r_tp == r_lat and e < 1e-6
