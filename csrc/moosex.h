@@ -55,6 +55,10 @@ int mx_ew_unary(int dev, int op, int words, const void* a, void* out, int64_t n,
 int mx_ew_binary2(int dev, int op, int words, const void* a0, const void* b0, void* out0,
                   const void* a1, const void* b1, void* out1, int64_t na, int64_t nb, int64_t n,
                   void* stream);
+// o_y = a_y * f + (add_y ? c[0] : 0), y = 0, 1 (one party's two share components)
+int mx_mul_add2(int dev, int words, const void* a0, const void* a1, const void* f,
+                const void* c, int add0, int add1, void* out0, void* out1, int64_t n,
+                void* stream);
 int mx_ew_unary2(int dev, int op, int words, const void* a0, void* out0, const void* a1,
                  void* out1, int64_t n, int64_t param, void* stream);
 // mx_ew_binary_slot on a0 (slot which0) and a1 (slot which1) with one public b

@@ -202,6 +202,8 @@ int mxh_add_zs3(int words, const void* v, const void* r, void* out0, void* out1,
 int mxh_ew_binary2(int op, int words, const void* a0, const void* b0, void* out0,
                    const void* a1, const void* b1, void* out1, int64_t na, int64_t nb, int64_t n,
                    void* stream);
+int mxh_mul_add2(int words, const void* a0, const void* a1, const void* f, const void* c,
+                 int add0, int add1, void* out0, void* out1, int64_t n, void* stream);
 int mxh_ew_add3(int words, const void* a, const void* b, const void* c, void* out, int64_t n,
                 void* stream);
 int mxh_lincomb2(int words, int nin, const void* const* ins, const int64_t* coef, const void* b,

@@ -386,6 +386,23 @@ int mx_ew_binary2(int dev, int op, int words, const void* a0, const void* b0, vo
   return rc ? rc : mx_ew_binary(0, op, words, a1, na, b1, nb, out1, n, stream);
 }
 
+int mx_mul_add2(int dev, int words, const void* a0, const void* a1, const void* f,
+                const void* c, int add0, int add1, void* out0, void* out1, int64_t n,
+                void* stream) {
+  if (dev) return mxh_mul_add2(words, a0, a1, f, c, add0, add1, out0, out1, n, stream);
+  DISPATCH_WORDS(words, T, {
+    const T* fs = (const T*)f;
+    const T cv = *(const T*)c;
+    for (int y = 0; y < 2; ++y) {
+      const T* a = (const T*)(y ? a1 : a0);
+      T* o = (T*)(y ? out1 : out0);
+      const T add = (y ? add1 : add0) ? cv : (T)0;
+      for (int64_t i = 0; i < n; ++i) o[i] = a[i] * fs[i] + add;
+    }
+    return 0;
+  });
+}
+
 int mx_ew_unary2(int dev, int op, int words, const void* a0, void* out0, const void* a1,
                  void* out1, int64_t n, int64_t param, void* stream) {
   if (dev) return mxh_ew_unary2(op, words, a0, out0, a1, out1, n, param, stream);

@@ -1100,6 +1100,21 @@ __global__ void __launch_bounds__(256) k_mul_rows_add(const T* __restrict__ a,
   }
 }
 
+// Share-pair form of k_mul_rows_add for one party's two components (per-party sessions):
+// o_y = a_y * f + (which[y] ? c : 0) -- the scaled integer-part factors plus the public 1
+// on this party's copies of x_0, one launch instead of two multiplies and an add.
+template <class T>
+__global__ void __launch_bounds__(256) k_mul_add2(Pair<T> p, int64_t n, const T* __restrict__ c) {
+  const int y = blockIdx.y;
+  const T* __restrict__ a = p.a[y];
+  const T* __restrict__ f = p.b[0];
+  T* __restrict__ out = p.o[y];
+  const T cv = p.which[y] ? c[0] : (T)0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = a[i] * f[i] + cv;
+}
+
 // The adder's sum after the last level, both share components: p ^ ((g ^ t) << 1).
 template <class T>
 __global__ void __launch_bounds__(256) k_ks_sum2(const T* __restrict__ p0, const T* __restrict__ p1,
@@ -1628,6 +1643,19 @@ int mxh_ew_binary_slot2(int op, int words, const void* a0, const void* a1, const
               {which0, which1}};
     hipLaunchKernelGGL(k_binary_slot2<T>, dim3(grid_for(m * nparties), 2), dim3(kBlock), 0,
                        S(stream), op, p, nb, m, nparties);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mxh_mul_add2(int words, const void* a0, const void* a1, const void* f, const void* c,
+                 int add0, int add1, void* out0, void* out1, int64_t n, void* stream) {
+  if (n == 0) return 0;
+  DEV_DISPATCH(words, T, {
+    Pair<T> p{{(const T*)a0, (const T*)a1}, {(const T*)f, (const T*)f}, {(T*)out0, (T*)out1},
+              {add0, add1}};
+    hipLaunchKernelGGL(k_mul_add2<T>, dim3(grid_for(n), 2), dim3(kBlock), 0, S(stream), p, n,
+                       (const T*)c);
     MX_LAUNCH_CHECK();
     return 0;
   });

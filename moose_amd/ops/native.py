@@ -27,6 +27,8 @@ _SIGS = {
     "mx_device_count": (c_int, []),
     "mx_ew_binary": (c_int, [c_int, c_int, c_int, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "mx_ew_unary": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_i64, c_i64, c_vp]),
+    "mx_mul_add2": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp,
+                            c_i64, c_vp]),
     "mx_ew_binary2": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
                               c_i64, c_i64, c_vp]),
     "mx_ew_unary2": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp]),

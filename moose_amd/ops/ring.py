@@ -1094,6 +1094,37 @@ def mul_leading(a: RT, c: RT, nb: int) -> RT:
     return binary("mul", a, full)
 
 
+def mul_leading_add2(a0: RT, a1: RT, c: RT, cadd: RT, add0: bool, add1: bool):
+    """One party's two share components scaled by the public vector ``c`` along the leading
+    axis (mul_leading, nb = 1) plus the public scalar ``cadd`` on the components flagged
+    ``add0`` / ``add1`` (add_public on this party's copies of x_0), one launch
+    (mx_mul_add2).  None when the operands do not fit (then the caller runs the steps)."""
+    if not (a0.bits in (64, 128) and a1.bits == a0.bits and a1.shape == a0.shape
+            and isinstance(cadd, RT) and cadd.bits == a0.bits and cadd.numel() == 1
+            and c.bits == a0.bits and len(a0.shape) >= 1 and c.numel() == a0.shape[0]):
+        return None
+    k = len(a0.shape) - 1
+    # the broadcast is cached only for a shared constant (its id stays its own)
+    shared = _CONSTS.get(_const_key.get(id(c))) is c
+    key = (id(c), tuple(a0.shape), "pair")
+    full = _LEADING.get(key) if shared else None
+    if full is None:
+        full = RT(expand(reshape(c, (c.shape[0],) + (1,) * k), tuple(a0.shape)).data
+                  .contiguous(), a0.bits)
+        if shared and not (a0.data.is_cuda and torch.cuda.is_current_stream_capturing()):
+            _cache_put(_LEADING, key, full, 1024)
+    d0, d1 = a0.data.contiguous(), a1.data.contiguous()
+    cd = cadd.data.contiguous()
+    if cd.device != d0.device:
+        cd = cd.to(d0.device)
+    o0, o1 = empty2(a0.shape, a0.bits, a0.device)
+    nat.check(nat.lib().mx_mul_add2(
+        nat.dev_of(d0), _words(a0.bits), nat.ptr(d0), nat.ptr(d1), nat.ptr(full.data),
+        nat.ptr(cd), int(bool(add0)), int(bool(add1)), nat.ptr(o0.data), nat.ptr(o1.data),
+        a0.numel(), nat.stream_of(d0)), "mul_add2")
+    return o0, o1
+
+
 def mul_leading_add(a: RT, c: RT, nb: int, cadd: RT, rows) -> RT:
     """mul_leading(a, c, nb) plus the public scalar ``cadd`` on batch rows ``rows`` (two of
     a's leading axis) in one launch (k_mul_rows_add); None when mul_leading would not use a

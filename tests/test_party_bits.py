@@ -237,3 +237,17 @@ def test_b2a_throughput_form_bitwise_equal_latency_form(ring, monkeypatch):
     monkeypatch.setenv("MOOSEX_B2A_TP", "0")  # set: the latency form everywhere
     lat, r_lat, _ = _lr("cuda:0", monkeypatch, True, True, one_dec=True, ring=ring)
     assert np.array_equal(tp, lat) and r_tp == r_lat and e < 1e-6
+
+
+@pytest.mark.parametrize("ring", [64, 128])
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_party_mul_leading_add_bitwise_equal_steps(device, ring, monkeypatch):
+    """SPMDSession.p_mul_leading_add (ring.mul_leading_add2, one mx_mul_add2 launch): exp's
+    integer-part factors 1 + b_j (c_j - 1) give bitwise the shares of MulLeading on both
+    components and add_public of 1 as separate steps."""
+    from moose_amd.parallel.spmd import SPMDSession
+
+    fused, r_f, e = _lr(device, monkeypatch, True, True, one_dec=True, ring=ring)
+    monkeypatch.setattr(SPMDSession, "p_mul_leading_add", None)
+    sep, r_s, _ = _lr(device, monkeypatch, True, True, one_dec=True, ring=ring)
+    assert np.array_equal(fused, sep) and r_f == r_s and e < 1e-6
