@@ -736,10 +736,13 @@ def _exp2_parts(sess, a: RepFixed, negative: bool):
 
 
 def _exp2_from_planes(sess, ab: RepTensor, f: int, integ: int, bits: int, nint: int,
-                      npad: int, negative: bool, merged: bool, cs=None) -> RepFixed:
+                      npad: int, negative: bool, merged: bool, cs=None,
+                      plus: float = 0.0) -> RepFixed:
     """2^a (2^-a) from the arithmetic bit planes ``ab`` of a >= 0 at ``f`` fractional bits:
     rows 0..f-1 the fraction, rows f..f+npad-1 the integer part (rows from nint on weigh 0).
-    ``cs``: the factor rows' public weights (c_j - 1) 2^f when the caller chose them."""
+    ``cs``: the factor rows' public weights (c_j - 1) 2^f when the caller chose them.
+    ``plus``: a public constant added to the result (in the last product's tail when the
+    batched per-party tail runs it, else one add)."""
     frac_w = [(1 << j) for j in range(f)] + [0] * npad
     fused = _wsum(sess, ab, [-(1 << j) for j in range(f)], cblk=(1 << f,)) if negative else None
     if fused is not None:  # 1 - r in one launch (weighted sum, negation, public 1)
@@ -777,13 +780,14 @@ def _exp2_from_planes(sess, ab: RepTensor, f: int, integ: int, bits: int, nint: 
     if merged:
         # parties on different processes: the polynomial's levels and the product tree's
         # levels are independent -- each round carries both (module doc: _merged_exp_tail)
-        return _merged_exp_tail(sess, one_minus, fac, npad)
+        return _merged_exp_tail(sess, one_minus, fac, npad, plus=plus)
     # the polynomial's power levels and the product tree's levels (a log-depth product over
     # the leading axis) advance together: each round's two products run as one launch on a
     # stacked device session (rep.mul_trunc_many)
     p, F = _poly_and_tree(sess, px, _fit("exp2", 0.0, 1.0, 7), shift,
                           RepFixed(fac, f, integ), npad)
-    return mul(sess, p, local(sess, F, "IndexAxis", axis=0, index=0))
+    e = mul(sess, p, local(sess, F, "IndexAxis", axis=0, index=0))
+    return add_const(sess, e, plus) if plus else e
 
 
 def _poly_and_tree(sess, x: RepFixed, coeffs, shift: int, F: RepFixed, nf: int):
@@ -879,7 +883,8 @@ def _tail_trunc(sess, plc, v, bits, m) -> RepTensor:
     return RepTensor(plc, bits, "arith", s0, s1)
 
 
-def _merged_exp_tail(sess, x: RepFixed, fac: RepTensor, npad: int) -> RepFixed:
+def _merged_exp_tail(sess, x: RepFixed, fac: RepTensor, npad: int,
+                     plus: float = 0.0) -> RepFixed:
     """2^-a = p(1 - r) / 2 * prod(factors) with the polynomial p (degree 7) and the
     product tree over the ``npad`` integer-bit factors evaluated TOGETHER: every round's
     messages carry one level of each -- the level's products are ONE batched tail (local
@@ -888,7 +893,7 @@ def _merged_exp_tail(sess, x: RepFixed, fac: RepTensor, npad: int) -> RepFixed:
     too.  For the tutorial LR (fixed(24,40): 32 factors) 20 rounds become 12; the values
     are those of poly_eval + the tree up to TruncPr's probabilistic rounding."""
     if _jobs_ok(sess, x.t, fac):
-        return _merged_exp_tail_jobs(sess, x, fac, npad)
+        return _merged_exp_tail_jobs(sess, x, fac, npad, plus=plus)
     coeffs = _fit("exp2", 0.0, 1.0, 7)
     f, bits, t = x.frac, x.bits, x.t
     plc = t.plc
@@ -945,8 +950,9 @@ def _merged_exp_tail(sess, x: RepFixed, fac: RepTensor, npad: int) -> RepFixed:
     while nf > 1:
         F, nf = run([(sl(F, 0, nf // 2), sl(F, nf // 2, nf))])[0], nf // 2
     # 2^-a = p(1 - r) / 2 * prod: the halving is one more bit of the last TruncPr
-    return mul(sess, p, RepFixed(local(sess, F, "IndexAxis", axis=0, index=0), f, x.integ),
-               f=f + 1)
+    e = mul(sess, p, RepFixed(local(sess, F, "IndexAxis", axis=0, index=0), f, x.integ),
+            f=f + 1)
+    return add_const(sess, e, plus) if plus else e
 
 
 def _jobs_ok(sess, *reps) -> bool:
@@ -1020,7 +1026,8 @@ def _tail_nonces(sess, plc):
     return tuple(sess.nonce(plc) for _ in range(7))
 
 
-def _merged_exp_tail_jobs(sess, x: RepFixed, fac: RepTensor, npad: int) -> RepFixed:
+def _merged_exp_tail_jobs(sess, x: RepFixed, fac: RepTensor, npad: int,
+                          plus: float = 0.0) -> RepFixed:
     """_merged_exp_tail on the batched per-party tail (csrc/rss_jobs.hip): every round is the
     tail's three kernels for all of that round's products -- the polynomial level's (read
     from and written into a preallocated power stack), the tree level's, and the
@@ -1089,14 +1096,20 @@ def _merged_exp_tail_jobs(sess, x: RepFixed, fac: RepTensor, npad: int) -> RepFi
                     lin = R.binary("mul", R.RT(X, bits), R.fill((), wts[0], bits, X.device))
                     acc.append(R.binary("add", rest, lin).data)
             o0, o1 = torch.empty_like(st.x0), torch.empty_like(st.x0)
-            run([R.MulJob(1, o0, o1, x=(acc[0], acc[1]), y=(F0[0], F1[0]), a=F0[0], ca=c0)],
-                m=f + fw + 1)
+            # the public ``plus`` rides in the tail: party 0 adds it at the product's
+            # untruncated scale (a multiple of 2^m: the truncation carries it exactly)
+            pk = int(round(plus * (1 << f))) << (f + fw + 1) if PLUS_IN_TAIL else 0
+            a2 = (R.const_ints([pk % mod] * L, bits, st.x0.device).data
+                  if pk and sess.party_index(plc) == 0 else None)
+            run([R.MulJob(1, o0, o1, x=(acc[0], acc[1]), y=(F0[0], F1[0]), a=F0[0], ca=c0,
+                          a2=a2)], m=f + fw + 1)
             e = RepTensor(plc, bits, "arith", PV(plc, R.RT(o0, bits)), PV(plc, R.RT(o1, bits)))
         else:
             run([], m=f + fw + 1)
             r = PV(plc, Remote(bits))
             e = RepTensor(plc, bits, "arith", r, r)
-        return RepFixed(e, f, x.integ)
+        e = RepFixed(e, f, x.integ)
+        return add_const(sess, e, plus) if plus and not PLUS_IN_TAIL else e
     # the polynomial's weighted sum rides with the next tree level (its TruncPr)
     acc0 = acc1 = None
     jobs = []
@@ -1129,7 +1142,8 @@ def _merged_exp_tail_jobs(sess, x: RepFixed, fac: RepTensor, npad: int) -> RepFi
         F = RepTensor(plc, bits, "arith", PV(plc, R.RT(F0[0], bits)), PV(plc, R.RT(F1[0], bits)))
     p = add_const(sess, RepFixed(acc, f, x.integ), coeffs[0])
     # 2^-a = p(1 - r) / 2 * prod: the halving is one more bit of the last TruncPr
-    return mul(sess, p, RepFixed(F, f, x.integ), f=f + 1)
+    e = mul(sess, p, RepFixed(F, f, x.integ), f=f + 1)
+    return add_const(sess, e, plus) if plus else e
 
 
 def exp2(sess, x: RepFixed) -> RepFixed:
@@ -1153,9 +1167,10 @@ def exp_nonpositive(sess, x: RepFixed) -> RepFixed:
 def sigmoid(sess, x: RepFixed) -> RepFixed:
     """sigma(x) = 1 / (1 + e^-|x|) mirrored for x < 0; 1 + e^-|x| is in [1, 2] so the
     reciprocal needs no normalisation."""
-    one = _sign_and_exp_party(sess, x) if _jobs_ok(sess, x.t) else None
+    # (s, 1 + e^-|x|): the 1 rides in the exp's last tail
+    one = _sign_and_exp_party(sess, x, plus=1.0) if _jobs_ok(sess, x.t) else None
     if one is not None:
-        s, e = one
+        s, d = one
         party = True
     else:
         s = sign_bit(sess, x)
@@ -1168,7 +1183,8 @@ def sigmoid(sess, x: RepFixed) -> RepFixed:
     else:
         ax = _with(x, rep.negate_where(sess, s, x.t))
         e = exp_nonpositive(sess, neg(sess, ax))
-    d = add_const(sess, e, 1.0)  # in [1, 2]
+    if one is None:
+        d = add_const(sess, e, 1.0)  # in [1, 2]
     # 1/d = (1/h) / 2 with h = d / 2 in [0.5, 1]: the fit of 1/h evaluated at d directly
     # (coefficients c_k / 2^k), and both halvings folded into TruncPrs of one more bit --
     # no round spent on multiplying by 0.5
@@ -1208,6 +1224,8 @@ def sigmoid(sess, x: RepFixed) -> RepFixed:
 
 # per-party sessions leave a public-operand dot's TruncPr pending until it is read
 DEFER_DOT_TRUNC = os.environ.get("MOOSEX_DEFER_DOT_TRUNC", "1") != "0"
+# ... and add a public constant after it (the sigmoid's 1 + e^-|x|) inside its tail
+PLUS_IN_TAIL = True
 # per-party sessions finish 2^-a with one product (the polynomial's sum untruncated)
 EXP_ONE_PRODUCT = os.environ.get("MOOSEX_EXP_ONE_PRODUCT", "1") != "0"
 # per-party sessions evaluate the sigmoid's reciprocal as one degree-8 polynomial
@@ -1220,7 +1238,7 @@ ONE_DEC_WIDTH = True  # False (tests): its adder over all bits, as the generic s
 # ... with the integer bits whose factor underflows replaced by a range check (3 blocks)
 RANGE_SPLIT = os.environ.get("MOOSEX_EXP_RANGE_SPLIT", "1") != "0"
 
-def _sign_and_exp_party(sess, x: RepFixed):
+def _sign_and_exp_party(sess, x: RepFixed, plus: float = 0.0):
     """(s, e^-|x|) for a per-party session from ONE bit decomposition: z = x * C with C =
     log2(e) at ``fc`` fractional bits is a LOCAL product (no truncation: z keeps F = f + fc
     fractional bits, |z| < 2^(integ + 1 + F)); its planes XORed with its sign plane are the
@@ -1300,7 +1318,8 @@ def _sign_and_exp_party(sess, x: RepFixed):
         cs, nint_used = None, nint
     merged = (getattr(sess, "party_dot_trunc", None) is not None
               and hasattr(sess, "p_cross_plain") and npad >= 2 and npad & (npad - 1) == 0)
-    e = _exp2_from_planes(sess, rows, f, integ, bits, nint_used, npad, True, merged, cs=cs)
+    e = _exp2_from_planes(sess, rows, f, integ, bits, nint_used, npad, True, merged, cs=cs,
+                          plus=plus)
     return s, e
 
 def softmax(sess, x: RepFixed, axis: int, upmost_index: int) -> RepFixed:

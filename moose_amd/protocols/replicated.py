@@ -129,6 +129,25 @@ class DeferredRep(RepTensor):
         self._s1 = v
 
 
+# 2^m c of a public addend (a model bias): kept per (constant object, m) -- the constant's
+# encoding is the same object every evaluation (ring.encode_lazy), so an evaluation adds
+# it with one launch instead of a fill, a multiply and the add.  The entry holds the
+# constant itself, so its id cannot be reused while cached.
+_SCALED = {}
+
+
+def _scaled_public(cv, m: int, bits: int):
+    key = (id(cv), m, bits)
+    hit = _SCALED.get(key)
+    if hit is not None and hit[0] is cv:
+        return hit[1]
+    scaled = R.binary("mul", cv, R.fill((), 1 << m, bits, cv.data.device))
+    capturing = cv.data.is_cuda and torch.cuda.is_current_stream_capturing()
+    if len(_SCALED) < 1024 and not capturing and R.CONST_CACHE:
+        _SCALED.setdefault(key, (cv, scaled))
+    return scaled
+
+
 class PendingTrunc(RepTensor):
     """A fixed-point product still 2^m above its type, held as this party's 3-out-of-3
     additive share ``v_add`` (a per-party dot before its tail:
@@ -152,10 +171,9 @@ class PendingTrunc(RepTensor):
         """This party's additive share of 2^m (x + pubs) (members only)."""
         v = self.v_add
         if self._sess.party_index(self.plc) == 0 and self.pubs:
-            scale = R.fill((), 1 << self.m, self.bits, v.data.device)
             for c in self.pubs:
-                cv = c.v if isinstance(c, Public) else c
-                v = R.binary("add", v, R.binary("mul", cv, scale))
+                v = R.binary("add", v, _scaled_public(c.v if isinstance(c, Public) else c,
+                                                      self.m, self.bits))
         return v
 
     def _complete(self):

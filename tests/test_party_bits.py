@@ -251,3 +251,16 @@ def test_party_mul_leading_add_bitwise_equal_steps(device, ring, monkeypatch):
     monkeypatch.setattr(SPMDSession, "p_mul_leading_add", None)
     sep, r_s, _ = _lr(device, monkeypatch, True, True, one_dec=True, ring=ring)
     assert np.array_equal(fused, sep) and r_f == r_s and e < 1e-6
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_sigmoid_one_plus_exp_in_the_tail_equals_separate_add(device, monkeypatch):
+    """The sigmoid's 1 + e^-|x|: party 0 adds 2^m * 1 to the exp's last product before its
+    TruncPr (fixedpoint PLUS_IN_TAIL; a multiple of 2^m, so the truncation carries it
+    exactly) -- the revealed outputs equal those of add_const after the product, bitwise,
+    with no launch for the add."""
+    monkeypatch.setattr(FP, "PLUS_IN_TAIL", True)
+    tail, r_t, e = _lr(device, monkeypatch, True, True, one_dec=True, ring=128)
+    monkeypatch.setattr(FP, "PLUS_IN_TAIL", False)
+    sep, r_s, _ = _lr(device, monkeypatch, True, True, one_dec=True, ring=128)
+    assert np.array_equal(tail, sep) and r_t == r_s and e < 1e-6
