@@ -15,7 +15,14 @@ own session time, ``max(timings.values())``).
 Usage::
 
     python benchmarks/logreg_train.py --batch_size 128 --n_iter 10 --n_exp 3 \
-        [--runtime local|distributed] [--device cuda|cpu] [--json out.json]
+        [--runtime local|parties|distributed] [--device cuda|cpu] [--json out.json]
+
+``--runtime parties``: the three parties as threads of this process, each on its own HIP
+stream (``--devices``: one device per party, e.g. ``cuda:0,cuda:1,cuda:2``; default all on
+``--device``), every reshare / dealer message a device copy between them -- the
+per-party protocol the reference's three workers run (parallel/threads.py), instead of
+the stacked one-session simulation of ``local``.  With ``--graphs`` the parties' tapes are
+replayed as one composed graph (one device) or per-party graphs (several).
 """
 from __future__ import annotations
 
@@ -118,8 +125,10 @@ def main(argv=None):
     ap.add_argument("--batch_size", type=int, default=128)
     ap.add_argument("--n_iter", type=int, default=10)
     ap.add_argument("--n_exp", type=int, default=3)
-    ap.add_argument("--runtime", choices=["local", "distributed"], default="local")
+    ap.add_argument("--runtime", choices=["local", "parties", "distributed"], default="local")
     ap.add_argument("--device", default=None)
+    ap.add_argument("--devices", default=None,
+                    help="parties runtime: comma-separated device per party")
     ap.add_argument("--graphs", action="store_true",
                     help="replay each evaluation as a captured hipGraph (runtime/graphs.py)")
     ap.add_argument("--seed", type=int, default=0)
@@ -142,18 +151,32 @@ def main(argv=None):
     ids = ["alice", "bob", "carole"]
     if args.runtime == "local":
         runtime = pm.LocalMooseRuntime(ids, device=args.device, use_graphs=args.graphs)
+    elif args.runtime == "parties":
+        import torch
+
+        dev = args.device or ("cuda:0" if torch.cuda.is_available() else "cpu")
+        devs = args.devices.split(",") if args.devices else [dev] * 3
+        runtime = pm.LocalMooseRuntime(ids, device_map=dict(zip(ids, devs)),
+                                       use_graphs=args.graphs, timeout=1200)
     else:
         runtime = pm.DistributedMooseRuntime(ids, timeout=1200)
     arguments = {"x": x, "y": y, "w_0": w0, "b_0": b0}
 
     runtime.evaluate_computation(native, arguments)  # warm-up (kernels, allocator)
+    if args.runtime == "parties" and args.graphs:
+        # the parties' tapes are recorded the second time a computation is seen (then
+        # replayed): that evaluation is warm-up too
+        runtime.evaluate_computation(native, arguments)
     session_s, wall_s = [], []
     outs = None
     for _ in range(args.n_exp):
         t0 = time.perf_counter()
         outs = runtime.evaluate_computation(native, arguments)
         wall_s.append(time.perf_counter() - t0)
-        session_s.append(max(runtime.last_timings.values()) / 1e6)
+        if args.runtime == "parties":  # the parties' threads run inside this call
+            session_s.append(wall_s[-1])
+        else:
+            session_s.append(max(runtime.last_timings.values()) / 1e6)
     w_ref, b_ref = plaintext_training(x, y, args.batch_size, args.n_iter)
     vals = sorted(outs.values(), key=lambda v: -np.asarray(v).size)
     err = max(float(np.abs(np.asarray(vals[0]).reshape(w_ref.shape) - w_ref).max()),
@@ -162,7 +185,8 @@ def main(argv=None):
     res = {
         "bench": "logreg_train", "batch_size": args.batch_size, "n_iter": args.n_iter,
         "n_features": N_FEATURES, "dtype": "fixed(24,40)/ring128", "runtime": args.runtime + ("+graphs" if args.graphs else ""),
-        "device": str(getattr(runtime, "device", runtime.__class__.__name__)),
+        "device": (",".join(devs) if args.runtime == "parties"
+                   else str(getattr(runtime, "device", runtime.__class__.__name__))),
         "session_s": {"min": min(session_s), "max": max(session_s),
                       "mean": statistics.mean(session_s)},
         "wall_s_mean": statistics.mean(wall_s), "trace_s": t_trace,

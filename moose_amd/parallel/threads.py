@@ -37,11 +37,20 @@ from moose_amd.ops import ring as R
 from moose_amd.parallel.transport import TransportError
 
 
+def _indexed(d) -> torch.device:
+    """``d`` as a torch.device; a bare "cuda" is the current GPU (each party thread sets its
+    device, which needs the index)."""
+    d = torch.device(d)
+    if d.type == "cuda" and d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    return d
+
+
 class Hub:
     """The mailboxes of one evaluation's parties (ordered pairs), plus failure state."""
 
     def __init__(self, devices: List, timeout: Optional[float] = None):
-        self.devices = [torch.device(d) for d in devices]
+        self.devices = [_indexed(d) for d in devices]
         n = len(self.devices)
         self.boxes = {(s, d): queue.Queue() for s in range(n) for d in range(n) if s != d}
         self.failed: Optional[str] = None
@@ -410,7 +419,7 @@ class PartyTapes:
         from moose_amd.parallel.spmd_graphs import SPMDTape
 
         self.identities = list(identities)
-        self.devices = [torch.device(d) for d in devices]
+        self.devices = [_indexed(d) for d in devices]
         n = len(identities)
         role_ranks = {r: i for i, r in enumerate(identities)}
         # every party on one device: the tapes are composed into ONE graph (below)
