@@ -69,7 +69,7 @@ def build(mode: str, k: int):
     return comp
 
 
-def run_one(runtime, mode, n, k, n_iter):
+def run_one(runtime, mode, n, k, n_iter, parties=False):
     from moose_amd.runtime.local import to_native
 
     native = to_native(build(mode, k))
@@ -77,7 +77,10 @@ def run_one(runtime, mode, n, k, n_iter):
     y = np.identity(n)
     args = {"x_arg": x, "y_arg": y}
     runtime.evaluate_computation(native, args)  # warm-up
-    if getattr(runtime, "use_graphs", False):
+    if parties:
+        # the parties' tapes are recorded the second time a computation is seen
+        runtime.evaluate_computation(native, args)
+    elif getattr(runtime, "use_graphs", False):
         # hipGraph plans: capture, then the adaptive probes (runtime/graphs.py) decide
         # between replay and eager before the timed evaluations
         from moose_amd.runtime.graphs import PROBES
@@ -87,8 +90,12 @@ def run_one(runtime, mode, n, k, n_iter):
     times = []
     out = None
     for _ in range(n_iter):
+        t0 = time.perf_counter()
         out = runtime.evaluate_computation(native, args)
-        times.append(max(runtime.last_timings.values()) / 1e6)
+        if parties:  # the parties' threads (or replay) run inside this call
+            times.append(time.perf_counter() - t0)
+        else:
+            times.append(max(runtime.last_timings.values()) / 1e6)
     z = np.asarray(next(iter(out.values())))
     expect = x * (k if mode == "parallel" else 1)
     ref = REFERENCE_S.get((mode, k, n))
@@ -107,16 +114,27 @@ def main(argv=None):
     ap.add_argument("--n", dest="n_iter", type=int, default=3)
     ap.add_argument("--sweep", action="store_true")
     ap.add_argument("--max_n", type=int, default=1000)
-    ap.add_argument("--runtime", choices=["local", "distributed"], default="local")
+    ap.add_argument("--runtime", choices=["local", "parties", "distributed"], default="local",
+                    help="parties: each party a thread on its own HIP stream running the "
+                         "per-party protocol (--devices: one device per party)")
     ap.add_argument("--device", default=None)
+    ap.add_argument("--devices", default=None)
     ap.add_argument("--graphs", action="store_true",
                     help="replay each evaluation as a captured hipGraph (runtime/graphs.py)")
     ap.add_argument("--json", default=None)
     args = ap.parse_args(argv)
 
     ids = ["alice", "bob", "carole"]
+    devs = None
     if args.runtime == "local":
         runtime = pm.LocalMooseRuntime(ids, device=args.device, use_graphs=args.graphs)
+    elif args.runtime == "parties":
+        import torch
+
+        dev = args.device or ("cuda:0" if torch.cuda.is_available() else "cpu")
+        devs = args.devices.split(",") if args.devices else [dev] * 3
+        runtime = pm.LocalMooseRuntime(ids, device_map=dict(zip(ids, devs)),
+                                       use_graphs=args.graphs, timeout=1200)
     else:
         runtime = pm.DistributedMooseRuntime(ids, timeout=1800)
     if args.sweep:
@@ -126,9 +144,10 @@ def main(argv=None):
         cases = [(args.mode, args.k, args.n)]
     results = []
     for mode, k, n in cases:
-        res = run_one(runtime, mode, n, k, args.n_iter)
+        res = run_one(runtime, mode, n, k, args.n_iter, parties=args.runtime == "parties")
         res["runtime"] = args.runtime + ("+graphs" if args.graphs else "")
-        res["device"] = str(getattr(runtime, "device", "distributed"))
+        res["device"] = (",".join(devs) if devs else str(getattr(runtime, "device",
+                                                                 "distributed")))
         results.append(res)
         print(json.dumps(res), flush=True)
         if args.json:

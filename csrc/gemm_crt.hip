@@ -45,6 +45,7 @@
 #include "moosex.h"
 
 void mx_ws_note(int dev, int64_t want, bool ok);  // gemm_mfma.hip: workspace bookkeeping
+bool mx_ws_malloc(void** p, int64_t bytes);       // gemm_mfma.hip: allocation (capture-safe)
 void mx_ws_shared_note(void);
 
 namespace {
@@ -1228,7 +1229,7 @@ void* workspace(int64_t bytes, hipStream_t st) {
     int64_t want = 1 << 20;
     while (want < bytes) want <<= 1;
     void* q = nullptr;
-    const bool ok = hipMalloc(&q, want) == hipSuccess;
+    const bool ok = mx_ws_malloc(&q, want);
     mx_ws_note(dev, want, ok);
     if (!ok) return nullptr;
     w.ptr = q;

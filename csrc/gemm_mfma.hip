@@ -797,6 +797,19 @@ void mx_ws_shared_note(void) { ++g_ws_shared; }
 // lookups that found every per-stream slot taken and fell back to a shared one (0 expected)
 extern "C" int64_t mx_workspace_shared_count(void) { return g_ws_shared.load(); }
 
+// A workspace that grows while its stream is being captured (a taped evaluation's first
+// product of a size, on the tape's own stream): the allocation is not a stream operation,
+// so it runs in relaxed capture mode (as PyTorch's caching allocator allocates inside
+// captures); the buffer is never freed, so the captured kernels' pointer stays valid.
+bool mx_ws_malloc(void** p, int64_t bytes) {
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+  const bool swapped = hipThreadExchangeStreamCaptureMode(&mode) == hipSuccess;
+  const bool ok = hipMalloc(p, bytes) == hipSuccess;
+  if (swapped) hipThreadExchangeStreamCaptureMode(&mode);
+  if (!ok) (void)hipGetLastError();
+  return ok;
+}
+
 void mx_ws_note(int dev, int64_t want, bool ok) {
   if (ok) {
     if (dev >= 0 && dev < 16) g_ws_held[dev] += want;
@@ -852,7 +865,7 @@ void* get_workspace(int64_t bytes, hipStream_t st) {
     int64_t want = 1 << 20;
     while (want < bytes) want <<= 1;
     void* p = nullptr;
-    const bool ok = hipMalloc(&p, want) == hipSuccess;
+    const bool ok = mx_ws_malloc(&p, want);
     mx_ws_note(dev, want, ok);
     if (!ok) return nullptr;
     w.ptr = p;  // the previous buffer (if any) stays allocated

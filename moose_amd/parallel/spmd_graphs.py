@@ -107,13 +107,14 @@ class SPMDTape:
             state["g"], state["n"] = g, 0
 
         def end():
-            if state["g"] is not None:
+            g = state["g"]
+            if g is not None:
+                state["g"] = None  # ended once, also when the capture failed
                 with warnings.catch_warnings():  # a segment between two rounds may be empty
                     warnings.filterwarnings("ignore", message="The CUDA Graph is empty")
-                    state["g"].capture_end()
+                    g.capture_end()
                 if state["n"]:
-                    self.steps.append(state["g"])
-                state["g"] = None
+                    self.steps.append(g)
 
         def rotate():  # before each op: bounded segments
             if state["g"] is None:

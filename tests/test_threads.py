@@ -421,3 +421,30 @@ def test_encoded_constant_cache_checks_identity():
     finally:
         R.CONST_IDS.discard(id(y))
         R._ENCODED_CONSTS.pop((id(y), 10, 128), None)
+
+
+@pytest.mark.gpu
+def test_party_tapes_capture_a_large_product():
+    """A taped product large enough for the CRT GEMM (its per-stream workspace grows while
+    the tape's own stream is capturing: the allocation runs in relaxed capture mode) is
+    recorded and replayed -- before, the capture failed and the next eager evaluation hit
+    'operation not permitted when stream is capturing'."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)), "benchmarks"))
+    from dot_product import build
+
+    from moose_amd.runtime.local import to_native
+
+    native = to_native(build("seq", 1))
+    n = 512
+    args = {"x_arg": np.ones((n, n)), "y_arg": np.identity(n)}
+    rt = LocalMooseRuntime(IDS, device_map={i: "cuda:0" for i in IDS}, use_graphs=True,
+                           timeout=120)
+    for _ in range(4):
+        out = rt.evaluate_computation(native, args)
+        np.testing.assert_allclose(np.asarray(next(iter(out.values()))), args["x_arg"],
+                                   atol=1e-6)
+    (_, tapes), = rt._party_tapes.values()
+    assert tapes is not False and all(t.replays >= 1 for t in tapes.tapes)
