@@ -334,6 +334,13 @@ int mx_jobs_r0(int dev, int words, int njobs, const void* const* ptrs, const int
                int64_t L, int m, int role, int main, int dealer, void* msg, void* msg_rt,
                void* msg_rm, const uint32_t* const* slots, const uint64_t* nonces,
                void* stream);
+// mx_jobs_r0 with the previous level's round-2 sums pending: region k = (o, a, b) =
+// pend[3k .. 3k+2] of pend_len[k] elements, o = a + b; operands read through them, and the
+// regions written too (one launch instead of the previous round 2 plus this round 0)
+int mx_jobs_r0p(int dev, int words, int njobs, const void* const* ptrs, const int64_t* dims,
+                int64_t L, int m, int role, int main, int dealer, void* msg, void* msg_rt,
+                void* msg_rm, const uint32_t* const* slots, const uint64_t* nonces, int npend,
+                const void* const* pend, const int64_t* pend_len, void* stream);
 int mx_jobs_r1(int dev, int words, int njobs, const void* const* ptrs, const int64_t* dims,
                int64_t L, int m, int role, const void* msg, const void* rmk, const void* rz,
                const void* rrt, const void* rrm, void* w, const uint32_t* const* slots,

@@ -47,11 +47,53 @@ struct JobD {
   int64_t ca, ca2, cb;
 };
 
+// The previous level's round-2 sums, still pending (parallel/party.py jobs_tail, defer):
+// region k of this party's output rows o[k][0, len[k]) is a[k] + b[k] (its w and the
+// received w).  Round 0 of the next level reads its operands through them and also writes
+// them (so later readers find the rows materialised): one launch instead of two.
+struct Pend {
+  const void* o[kMaxJobs];
+  const void* a[kMaxJobs];
+  const void* b[kMaxJobs];
+  int64_t len[kMaxJobs];
+  int64_t total;
+  int n;
+};
+
 struct Jobs {
   JobD j[kMaxJobs];
   int n;
   int64_t L;
+  Pend pend;
 };
+
+// operand element p[idx], or its pending sum when it lies in a pending region
+template <class T>
+__device__ __forceinline__ T ld(const Jobs& js, const void* p, int64_t idx) {
+  const T* q = (const T*)p + idx;
+  for (int k = 0; k < js.pend.n; ++k) {
+    const T* o = (const T*)js.pend.o[k];
+    if (q >= o && q < o + js.pend.len[k]) {
+      const int64_t off = q - o;
+      return ((const T*)js.pend.a[k])[off] + ((const T*)js.pend.b[k])[off];
+    }
+  }
+  return *q;
+}
+
+// the pending regions' sums, written (grid-stride over all their elements)
+template <class T>
+__device__ __forceinline__ void fill_pending(const Jobs& js, int first = 0) {
+  // threads [first, blockDim.x) of every block; the others are not delayed by it
+  const int64_t per = blockDim.x - first;
+  for (int64_t g = blockIdx.x * per + (threadIdx.x - first); g < js.pend.total;
+       g += (int64_t)gridDim.x * per) {
+    int64_t i = g;
+    int k = 0;
+    while (k < js.pend.n - 1 && i >= js.pend.len[k]) i -= js.pend.len[k++];
+    ((T*)js.pend.o[k])[i] = ((const T*)js.pend.a[k])[i] + ((const T*)js.pend.b[k])[i];
+  }
+}
 
 template <class T>
 struct Loc {
@@ -73,12 +115,12 @@ __device__ __forceinline__ T job_value(const Jobs& js, const Loc<T>& l) {
   T v = 0;
   if (J.cb != 0) {
     const int64_t ix = l.r * J.sx + l.e, iy = l.r * J.sy + l.e;
-    const T x0 = ((const T*)J.x0)[ix], x1 = ((const T*)J.x1)[ix];
-    const T y0 = ((const T*)J.y0)[iy], y1 = ((const T*)J.y1)[iy];
+    const T x0 = ld<T>(js, J.x0, ix), x1 = ld<T>(js, J.x1, ix);
+    const T y0 = ld<T>(js, J.y0, iy), y1 = ld<T>(js, J.y1, iy);
     v = (T)J.cb * (x0 * y0 + x0 * y1 + x1 * y0);
   }
-  if (J.a != nullptr) v += (T)J.ca * ((const T*)J.a)[l.r * J.sa + l.e];
-  if (J.a2 != nullptr) v += (T)J.ca2 * ((const T*)J.a2)[l.r * J.sa2 + l.e];
+  if (J.a != nullptr) v += (T)J.ca * ld<T>(js, J.a, l.r * J.sa + l.e);
+  if (J.a2 != nullptr) v += (T)J.ca2 * ld<T>(js, J.a2, l.r * J.sa2 + l.e);
   return v;
 }
 
@@ -99,6 +141,7 @@ __global__ void __launch_bounds__(256)
               uint64_t n_z0, uint64_t n_z2) {
   __shared__ uint32_t rks[mxd::kMaxKeySlots][mxd::kKeyWords];
   mxd::stage_keys(rks, keys, 2);
+  fill_pending<T>(js);
   constexpr int P = mxd::Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;
   const uint32_t* own = rks[0];
@@ -256,6 +299,10 @@ __global__ void __launch_bounds__(256)
   __shared__ uint32_t rks[2][mxd::kKeyWords];
   __shared__ uint64_t kl[8][kLatEpb], kh[8][kLatEpb];
   mxd::stage_keys(rks, keys, 2);
+  // the pending sums by the waves that draw no keystream chunk (P0 / P1 draw 2 streams:
+  // waves 1-3), beside the finishing wave 0 instead of before it
+  const int fill_from = ss.n * kLatEpb < (int)blockDim.x ? ss.n * kLatEpb : 0;
+  if ((int)threadIdx.x >= fill_from) fill_pending<T>(js, fill_from);
   constexpr int P = mxd::Lane<T>::kPer;
   const int64_t nb = (n + P - 1) / P;
   const int tid = threadIdx.x, s = tid / kLatEpb, lb = tid % kLatEpb;
@@ -377,6 +424,7 @@ int make_jobs(int njobs, const void* const* ptrs, const int64_t* dims, int64_t L
   if (njobs < 1 || njobs > kMaxJobs || L < 1) return -3;
   js->n = njobs;
   js->L = L;
+  js->pend = Pend{};
   int64_t at = 0;
   for (int q = 0; q < kMaxJobs; ++q) {
     JobD& J = js->j[q];
@@ -414,13 +462,23 @@ int make_jobs(int njobs, const void* const* ptrs, const int64_t* dims, int64_t L
 
 extern "C" {
 
-int mxh_jobs_r0(int words, int njobs, const void* const* ptrs, const int64_t* dims, int64_t L,
-                int m, int role, int main, int dealer, void* msg, void* msg_rt, void* msg_rm,
-                const uint32_t* const* slots, const uint64_t* nn, void* stream) {
+int mxh_jobs_r0p(int words, int njobs, const void* const* ptrs, const int64_t* dims, int64_t L,
+                 int m, int role, int main, int dealer, void* msg, void* msg_rt, void* msg_rm,
+                 const uint32_t* const* slots, const uint64_t* nn, int npend,
+                 const void* const* pend, const int64_t* pend_len, void* stream) {
   Jobs js;
   int64_t n = 0;
   int rc = make_jobs(njobs, ptrs, dims, L, &js, &n);
   if (rc) return rc;
+  if (npend < 0 || npend > kMaxJobs) return -3;
+  js.pend.n = npend;
+  for (int k = 0; k < npend; ++k) {
+    js.pend.o[k] = pend[3 * k];
+    js.pend.a[k] = pend[3 * k + 1];
+    js.pend.b[k] = pend[3 * k + 2];
+    js.pend.len[k] = pend_len[k];
+    js.pend.total += pend_len[k];
+  }
   if (n == 0) return 0;
   const mxd::KeySrc k = mxd::keysrc_slots(slots, 2);
   hipStream_t st = (hipStream_t)stream;
@@ -467,6 +525,13 @@ int mxh_jobs_r0(int words, int njobs, const void* const* ptrs, const int64_t* di
     return -2;
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : -100 - (int)e;
+}
+
+int mxh_jobs_r0(int words, int njobs, const void* const* ptrs, const int64_t* dims, int64_t L,
+                int m, int role, int main, int dealer, void* msg, void* msg_rt, void* msg_rm,
+                const uint32_t* const* slots, const uint64_t* nn, void* stream) {
+  return mxh_jobs_r0p(words, njobs, ptrs, dims, L, m, role, main, dealer, msg, msg_rt, msg_rm,
+                      slots, nn, 0, nullptr, nullptr, stream);
 }
 
 int mxh_jobs_r1(int words, int njobs, const void* const* ptrs, const int64_t* dims, int64_t L,

@@ -18,6 +18,10 @@ extern "C" {
 int mxh_jobs_r0(int words, int njobs, const void* const* ptrs, const int64_t* dims, int64_t L,
                 int m, int role, int main, int dealer, void* msg, void* msg_rt, void* msg_rm,
                 const uint32_t* const* slots, const uint64_t* nn, void* stream);
+int mxh_jobs_r0p(int words, int njobs, const void* const* ptrs, const int64_t* dims, int64_t L,
+                 int m, int role, int main, int dealer, void* msg, void* msg_rt, void* msg_rm,
+                 const uint32_t* const* slots, const uint64_t* nn, int npend,
+                 const void* const* pend, const int64_t* pend_len, void* stream);
 int mxh_jobs_r1(int words, int njobs, const void* const* ptrs, const int64_t* dims, int64_t L,
                 int m, int role, const void* msg, const void* rmk, const void* rz,
                 const void* rrt, const void* rrm, void* w, const uint32_t* const* slots,
@@ -65,6 +69,28 @@ struct Loc {
   int64_t r, e;
 };
 
+// pending round-2 sums of the previous level (rss_jobs.hip Pend): o[k][i] = a[k][i] + b[k][i]
+struct Pending {
+  int n = 0;
+  const void* o[MX_MAX_JOBS];
+  const void* a[MX_MAX_JOBS];
+  const void* b[MX_MAX_JOBS];
+  int64_t len[MX_MAX_JOBS];
+};
+
+template <class T>
+T ld(const Pending& pd, const void* p, int64_t idx) {
+  const T* q = (const T*)p + idx;
+  for (int k = 0; k < pd.n; ++k) {
+    const T* o = (const T*)pd.o[k];
+    if (q >= o && q < o + pd.len[k]) {
+      const int64_t off = q - o;
+      return ((const T*)pd.a[k])[off] + ((const T*)pd.b[k])[off];
+    }
+  }
+  return *q;
+}
+
 Loc locate(const std::vector<Job>& js, int64_t L, int64_t i) {
   int q = (int)js.size() - 1;
   while (q > 0 && i < js[q].start) --q;
@@ -73,17 +99,17 @@ Loc locate(const std::vector<Job>& js, int64_t L, int64_t i) {
 }
 
 template <class T>
-T value(const std::vector<Job>& js, const Loc& l) {
+T value(const std::vector<Job>& js, const Loc& l, const Pending& pd) {
   const Job& J = js[l.q];
   T v = 0;
   if (J.cb != 0) {
     const int64_t ix = l.r * J.sx + l.e, iy = l.r * J.sy + l.e;
-    const T x0 = ((const T*)J.p[0])[ix], x1 = ((const T*)J.p[1])[ix];
-    const T y0 = ((const T*)J.p[2])[iy], y1 = ((const T*)J.p[3])[iy];
+    const T x0 = ld<T>(pd, J.p[0], ix), x1 = ld<T>(pd, J.p[1], ix);
+    const T y0 = ld<T>(pd, J.p[2], iy), y1 = ld<T>(pd, J.p[3], iy);
     v = (T)J.cb * (x0 * y0 + x0 * y1 + x1 * y0);
   }
-  if (J.p[4] != nullptr) v += (T)J.ca * ((const T*)J.p[4])[l.r * J.sa + l.e];
-  if (J.p[5] != nullptr) v += (T)J.ca2 * ((const T*)J.p[5])[l.r * J.sa2 + l.e];
+  if (J.p[4] != nullptr) v += (T)J.ca * ld<T>(pd, J.p[4], l.r * J.sa + l.e);
+  if (J.p[5] != nullptr) v += (T)J.ca2 * ld<T>(pd, J.p[5], l.r * J.sa2 + l.e);
   return v;
 }
 
@@ -107,7 +133,8 @@ void prf(const uint32_t* slot, uint64_t nonce, int64_t i0, int64_t len, T* o) {
 
 template <class T>
 int r0(const std::vector<Job>& js, int64_t L, int64_t n, int m, int role, int main, int dealer,
-       T* msg, T* msg_rt, u64* msg_rm, const uint32_t* const* slots, const uint64_t* nn) {
+       T* msg, T* msg_rt, u64* msg_rm, const uint32_t* const* slots, const uint64_t* nn,
+       const Pending& pd) {
   const uint32_t* own = slots[0];
   const uint32_t* nxt = slots[1];
   for_chunks(n, [&](int64_t i0, int64_t len) {
@@ -119,7 +146,7 @@ int r0(const std::vector<Job>& js, int64_t L, int64_t n, int m, int role, int ma
       if (role == 1) prf<T>(nxt, nn[2], i0, len, r.data());
       for (int64_t q = 0; q < len; ++q) {
         const int64_t i = i0 + q;
-        const T z = value<T>(js, locate(js, L, i)) + a[q] - b[q];
+        const T z = value<T>(js, locate(js, L, i), pd) + a[q] - b[q];
         msg[i] = role == 0 ? mxf::trunc_mask0<T>(z, (T)0, r[q]) : role == 1 ? (T)(z + r[q]) : z;
       }
     }
@@ -140,6 +167,10 @@ int r0(const std::vector<Job>& js, int64_t L, int64_t n, int m, int role, int ma
       }
     }
   });
+  // the pending sums, materialised after every read above went through ld()
+  for (int k = 0; k < pd.n; ++k)
+    for (int64_t i = 0; i < pd.len[k]; ++i)
+      ((T*)pd.o[k])[i] = ((const T*)pd.a[k])[i] + ((const T*)pd.b[k])[i];
   return 0;
 }
 
@@ -181,24 +212,41 @@ int r2(const std::vector<Job>& js, int64_t L, int64_t n, int role, const T* a, c
 
 extern "C" {
 
-int mx_jobs_r0(int dev, int words, int njobs, const void* const* ptrs, const int64_t* dims,
-               int64_t L, int m, int role, int main, int dealer, void* msg, void* msg_rt,
-               void* msg_rm, const uint32_t* const* slots, const uint64_t* nn, void* stream) {
+int mx_jobs_r0p(int dev, int words, int njobs, const void* const* ptrs, const int64_t* dims,
+                int64_t L, int m, int role, int main, int dealer, void* msg, void* msg_rt,
+                void* msg_rm, const uint32_t* const* slots, const uint64_t* nn, int npend,
+                const void* const* pend, const int64_t* pend_len, void* stream) {
   if (m < 1 || m > 63 || role < 0 || role > 2) return -3;
+  if (npend < 0 || npend > MX_MAX_JOBS) return -3;
   if (dev)
-    return mxh_jobs_r0(words, njobs, ptrs, dims, L, m, role, main, dealer, msg, msg_rt, msg_rm,
-                       slots, nn, stream);
+    return mxh_jobs_r0p(words, njobs, ptrs, dims, L, m, role, main, dealer, msg, msg_rt, msg_rm,
+                        slots, nn, npend, pend, pend_len, stream);
   std::vector<Job> js;
   int64_t n = 0;
   int rc = make(njobs, ptrs, dims, L, &js, &n);
   if (rc) return rc;
+  Pending pd;
+  pd.n = npend;
+  for (int k = 0; k < npend; ++k) {
+    pd.o[k] = pend[3 * k];
+    pd.a[k] = pend[3 * k + 1];
+    pd.b[k] = pend[3 * k + 2];
+    pd.len[k] = pend_len[k];
+  }
   if (words == 1)
     return r0<u64>(js, L, n, m, role, main, dealer, (u64*)msg, (u64*)msg_rt, (u64*)msg_rm, slots,
-                   nn);
+                   nn, pd);
   if (words == 2)
     return r0<u128>(js, L, n, m, role, main, dealer, (u128*)msg, (u128*)msg_rt, (u64*)msg_rm,
-                    slots, nn);
+                    slots, nn, pd);
   return -2;
+}
+
+int mx_jobs_r0(int dev, int words, int njobs, const void* const* ptrs, const int64_t* dims,
+               int64_t L, int m, int role, int main, int dealer, void* msg, void* msg_rt,
+               void* msg_rm, const uint32_t* const* slots, const uint64_t* nn, void* stream) {
+  return mx_jobs_r0p(dev, words, njobs, ptrs, dims, L, m, role, main, dealer, msg, msg_rt,
+                     msg_rm, slots, nn, 0, nullptr, nullptr, stream);
 }
 
 int mx_jobs_r1(int dev, int words, int njobs, const void* const* ptrs, const int64_t* dims,

@@ -228,6 +228,8 @@ _SIGS = {
                                      c_vp]),
     "mx_jobs_r0": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_int,
                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mx_jobs_r0p": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_int,
+                            c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp]),
     "mx_jobs_r1": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp,
                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mx_jobs_r2": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp]),

@@ -2117,11 +2117,13 @@ def _jobs_abi(jobs):
     return (ctypes.c_void_p * len(ptrs))(*ptrs), (ctypes.c_int64 * len(dims))(*dims)
 
 
-def jobs_r0(jobs, L, bits, m, role, slots, nonces, like, main=True, dealer=True):
+def jobs_r0(jobs, L, bits, m, role, slots, nonces, like, main=True, dealer=True, pend=None):
     """Round 0 of the batched per-party tail (mx_jobs_r0): the outgoing message over the
     concatenation of the jobs' rows (P0 m0, P1 m1, P2 z2), the dealer's rt1 / rm1 (P2, when
     ``dealer``), P2's new shares into the jobs' outputs.  ``like``: any tensor of the call's
-    device (allocation and stream)."""
+    device (allocation and stream).  ``pend``: the previous level's round-2 sums still
+    pending, [(o, a, b)] with o = a + b elementwise (flat tensors of equal size): operands
+    are read through them and they are written too (mx_jobs_r0p)."""
     n = builtins.sum(j.rows for j in jobs) * L
     w = _words(bits)
     shp = (n,) + ((2,) if bits == 128 else ())
@@ -2129,11 +2131,15 @@ def jobs_r0(jobs, L, bits, m, role, slots, nonces, like, main=True, dealer=True)
     rt = torch.empty(shp, dtype=torch.int64, device=like.device) if role == 2 and dealer else None
     rm = torch.empty((n,), dtype=torch.int64, device=like.device) if role == 2 and dealer else None
     p, d = _jobs_abi(jobs)
-    nat.check(nat.lib().mx_jobs_r0(
+    pend = pend or []
+    pp = (ctypes.c_void_p * max(1, 3 * len(pend)))(*[t.data_ptr() for r in pend for t in r])
+    pl = (ctypes.c_int64 * max(1, len(pend)))(*[r[0].numel() // (2 if bits == 128 else 1)
+                                                 for r in pend])
+    nat.check(nat.lib().mx_jobs_r0p(
         nat.dev_of(like), w, len(jobs), p, d, L, m, role, int(main), int(dealer),
         None if msg is None else msg.data_ptr(), None if rt is None else rt.data_ptr(),
         None if rm is None else rm.data_ptr(), _slots_arr(slots), _nonces_arr(nonces),
-        nat.stream_of(like)), "jobs_r0")
+        len(pend), pp, pl, nat.stream_of(like)), "jobs_r0")
     return msg, rt, rm
 
 

@@ -201,13 +201,45 @@ def record_tail_traffic(stats, plc, nb, round_b=True):
     stats.record_round(2 * nb)
 
 
-def jobs_tail(sess, plc, role, jobs, L, bits, m, nonces, slots):
+class PendingSums:
+    """A level's round-2 sums not yet written (jobs_tail with ``defer``): this party's
+    output rows o = w + received w, as regions the next level's round 0 reads through and
+    writes (rss_jobs.hip Pend), or :meth:`flush` runs the round-2 kernel itself."""
+
+    def __init__(self, jobs, L, bits, role, w, recv, regions):
+        self.jobs, self.L, self.bits, self.role = jobs, L, bits, role
+        self.w, self.recv, self.regions = w, recv, regions
+
+    def flush(self):
+        R.jobs_r2(self.jobs, self.L, self.bits, self.role, self.w, self.recv)
+
+
+def _pending_regions(jobs, L, role, w, recv):
+    """(o, a, b) flat views per job (o = P0's o1 / P1's o0 rows), or None when an output is
+    not a dense block (then round 2 runs as its own kernel)."""
+    regions, at = [], 0
+    for j in jobs:
+        o = j.o1 if role == 0 else j.o0
+        n = j.rows * L
+        per = w[0].numel()  # int64 words per element
+        if o is None or not o.is_contiguous() or o.numel() != n * per or o.dtype != w.dtype:
+            return None
+        regions.append((o.reshape((n,) + tuple(w.shape[1:])), w[at:at + n], recv[at:at + n]))
+        at += n
+    return regions
+
+
+def jobs_tail(sess, plc, role, jobs, L, bits, m, nonces, slots, pend=None, defer=False):
     """Zero share + reshare + TruncPr of the products ``jobs`` (ring.MulJob list) for ONE
     party of role ``role``: the dot tail's two rounds and three kernels (csrc/rss_jobs.hip)
     for all of them at once -- every job's cross terms computed inside round 0, the new
-    shares written straight to the jobs' output rows.  ``nonces`` = the dot tail's seven."""
+    shares written straight to the jobs' output rows.  ``nonces`` = the dot tail's seven.
+    ``pend``: the previous level's :class:`PendingSums` (this round 0 completes them);
+    ``defer``: return this level's round-2 sums as a PendingSums instead of running round 2
+    (the caller hands them to the next level or flushes them before anything else reads)."""
     like = next(t for j in jobs for t in (j.o0, j.x0, j.a) if t is not None)
-    msg, rt, rm = R.jobs_r0(jobs, L, bits, m, role, slots, nonces, like)
+    msg, rt, rm = R.jobs_r0(jobs, L, bits, m, role, slots, nonces, like,
+                            pend=pend.regions if pend is not None else None)
     n_el = sum(j.rows for j in jobs) * L
     like_t = ((n_el,) + ((2,) if bits == 128 else ()), torch.int64)
     like_rm = ((n_el,), torch.int64)
@@ -224,11 +256,18 @@ def jobs_tail(sess, plc, role, jobs, L, bits, m, nonces, slots):
     record_tail_traffic(sess.stats, plc, nb, round_b=False)
     got = sess.party_exchange(plc, [("w0", 0, 1, w if role == 0 else None, like_t),
                                     ("w1", 1, 0, w if role == 1 else None, like_t)])
+    out = None
     if role in (0, 1):
-        R.jobs_r2(jobs, L, bits, role, w, got["w1"] if role == 0 else got["w0"])
+        recv = got["w1"] if role == 0 else got["w0"]
+        regions = _pending_regions(jobs, L, role, w, recv) if defer else None
+        if regions is not None:
+            out = PendingSums(jobs, L, bits, role, w, recv, regions)
+        else:
+            R.jobs_r2(jobs, L, bits, role, w, recv)
     for a, b in ((0, 1), (1, 0)):
         sess.stats.record_send(plc.owners[a], plc.owners[b], nb)
     sess.stats.record_round(2 * nb)
+    return out
 
 
 

@@ -476,11 +476,12 @@ def _poly_eval_jobs(sess, x: RepFixed, coeffs, shift: int = 0) -> RepFixed:
     while have < n:
         m = min(2 * have, n) - have
         nonces = _tail_nonces(sess, plc)
-        if member:
-            sess.party_jobs(plc, _power_jobs(st, have, m, L), L, bits, f, nonces)
+        if member:  # each level's round-2 sums ride in the next level's round 0
+            sess.party_jobs(plc, _power_jobs(st, have, m, L), L, bits, f, nonces, defer=True)
         have += m
     nonces = _tail_nonces(sess, plc)
     if member:
+        sess.party_jobs_flush(plc)  # the acc job's weighted sum reads the rows directly
         acc0, acc1 = torch.empty_like(st.x0), torch.empty_like(st.x0)
         sess.party_jobs(plc, [_acc_job(st, weights, n, L, acc0, acc1)], L, bits, f + shift,
                         nonces)
@@ -506,10 +507,11 @@ def _poly_powers_sum(sess, x: RepFixed, coeffs, finish=None):
     while have < n:
         m = min(2 * have, n) - have
         nonces = _tail_nonces(sess, plc)
-        if member:
-            sess.party_jobs(plc, _power_jobs(st, have, m, L), L, bits, f, nonces)
+        if member:  # each level's round-2 sums ride in the next level's round 0
+            sess.party_jobs(plc, _power_jobs(st, have, m, L), L, bits, f, nonces, defer=True)
         have += m
     if member:
+        sess.party_jobs_flush(plc)  # the last level's sums, before the rows are read
         rows = RepTensor(plc, bits, "arith", PV(plc, R.RT(st.s0, bits)), PV(plc, R.RT(st.s1, bits)))
     else:
         from moose_amd.parallel.spmd import Remote
@@ -1047,10 +1049,10 @@ def _merged_exp_tail_jobs(sess, x: RepFixed, fac: RepTensor, npad: int,
     st = _Stack(t.s0.v.data, t.s1.v.data, n - 1, bits) if member else None
     F0, F1 = (fac.s0.v.data, fac.s1.v.data) if member else (None, None)
 
-    def run(jobs, m=f):
+    def run(jobs, m=f, defer=False):
         nonces = _tail_nonces(sess, plc)
         if member:
-            sess.party_jobs(plc, jobs, L, bits, m, nonces)
+            sess.party_jobs(plc, jobs, L, bits, m, nonces, defer=defer)
 
     def tree_job(nf):
         h = nf // 2
@@ -1067,11 +1069,13 @@ def _merged_exp_tail_jobs(sess, x: RepFixed, fac: RepTensor, npad: int,
         if nf > 1 and member:
             tj, new = tree_job(nf)
             jobs.append(tj)
-        run(jobs)
+        run(jobs, defer=True)  # its round-2 sums ride in the next level's round 0
         if nf > 1:
             F0, F1 = new if member else (None, None)
             nf //= 2
         have += m
+    if member:
+        sess.party_jobs_flush(plc)  # the power stack and the tree rows, before other reads
     fw = 62 - f  # the polynomial's weights' fractional bits in the one-product finish
     if EXP_ONE_PRODUCT and nf == 1 and bits == 128 and fw >= 20:
         # the tree is done with the powers: e = p F / 2 as ONE product -- the polynomial's

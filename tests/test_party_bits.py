@@ -264,3 +264,31 @@ def test_sigmoid_one_plus_exp_in_the_tail_equals_separate_add(device, monkeypatc
     monkeypatch.setattr(FP, "PLUS_IN_TAIL", False)
     sep, r_s, _ = _lr(device, monkeypatch, True, True, one_dec=True, ring=128)
     assert np.array_equal(tail, sep) and r_t == r_s and e < 1e-6
+
+
+@pytest.mark.parametrize("ring", [64, 128])
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_jobs_round2_folded_into_next_round0_bitwise_equal(device, ring, monkeypatch):
+    """parallel/party.py PendingSums: a batched tail level's round-2 sums (P0's o1, P1's o0)
+    written by the next level's round-0 kernel, which reads its operands through them
+    (rss_jobs.hip Pend) -- bitwise the shares of the separate round-2 kernel, fewer
+    launches."""
+    from moose_amd.ops import ring as Rg
+    from moose_amd.parallel import spmd
+
+    calls = {"r2": 0}
+    orig = Rg.jobs_r2
+
+    def count(*a, **k):
+        calls["r2"] += 1
+        return orig(*a, **k)
+
+    monkeypatch.setattr(Rg, "jobs_r2", count)
+    monkeypatch.setattr(spmd, "JOBS_FOLD", True)
+    fold, r_f, e = _lr(device, monkeypatch, True, True, one_dec=True, ring=ring)
+    n_fold = calls["r2"]
+    monkeypatch.setattr(spmd, "JOBS_FOLD", False)
+    calls["r2"] = 0
+    sep, r_s, _ = _lr(device, monkeypatch, True, True, one_dec=True, ring=ring)
+    assert np.array_equal(fold, sep) and r_f == r_s and e < 1e-6
+    assert n_fold < calls["r2"]
