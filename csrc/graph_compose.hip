@@ -13,7 +13,132 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
+#include <unordered_map>
 #include <vector>
+
+namespace {
+
+// Segments flattened into the composed / chained graphs (default; MOOSEX_PARTY_GRAPH_FLAT=0:
+// child-graph nodes).  Measured on one MI355X (LR parties, composed graph): a child-graph
+// node costs ~3 us of device time at its boundary -- 80 segments: p50 0.87 -> 0.65 ms flat.
+bool flat_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("MOOSEX_PARTY_GRAPH_FLAT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// A captured copy's node in another graph: its 3-D parameters as read back, or (when the
+// runtime does not take those back) the equivalent 1-D copy.
+hipError_t add_copy(hipGraphNode_t* out, hipGraph_t g, const hipGraphNode_t* deps, size_t nd,
+                    const hipMemcpy3DParms& mp) {
+  if (hipGraphAddMemcpyNode(out, g, deps, nd, &mp) == hipSuccess) return hipSuccess;
+  (void)hipGetLastError();
+  if (mp.srcArray != nullptr || mp.dstArray != nullptr || mp.extent.height > 1 ||
+      mp.extent.depth > 1)
+    return hipErrorInvalidValue;
+  char* dst = (char*)mp.dstPtr.ptr + mp.dstPos.x;
+  const char* src = (const char*)mp.srcPtr.ptr + mp.srcPos.x;
+  return hipGraphAddMemcpyNode1D(out, g, deps, nd, dst, src, mp.extent.width, mp.kind);
+}
+
+// Copy the nodes of a captured segment (kernel / memcpy / memset / empty nodes) into the
+// parent graph instead of adding it as a child-graph node: the instantiated executable then
+// holds one flat list of packets (no nested graph per segment).  ``deps``: what the
+// segment's roots wait for; ``leaves``: its last nodes, for the next node to wait for.
+// 1 (nothing added) when the segment holds another node type (the caller adds it as a
+// child graph), 0 when flattened, -1 when adding a node failed midway.
+int flatten_into(hipGraph_t g, hipGraph_t child, const std::vector<hipGraphNode_t>& deps,
+                  std::vector<hipGraphNode_t>* leaves) {
+  size_t n = 0;
+  if (hipGraphGetNodes(child, nullptr, &n) != hipSuccess) return 1;
+  std::vector<hipGraphNode_t> nodes(n);
+  if (n && hipGraphGetNodes(child, nodes.data(), &n) != hipSuccess) return 1;
+  size_t ne = 0;
+  if (hipGraphGetEdges(child, nullptr, nullptr, &ne) != hipSuccess) return 1;
+  std::vector<hipGraphNode_t> from(ne), to(ne);
+  if (ne && hipGraphGetEdges(child, from.data(), to.data(), &ne) != hipSuccess) return 1;
+  // every node's type and parameters read before anything is added (a node whose
+  // parameters cannot be read back -- e.g. some captured copies -- keeps the segment whole)
+  std::vector<hipGraphNodeType> types(n);
+  std::vector<hipKernelNodeParams> kps(n);
+  std::vector<hipMemcpy3DParms> mps(n);
+  std::vector<hipMemsetParams> mss(n);
+  for (size_t i = 0; i < n; ++i) {
+    hipGraphNodeType& t = types[i];
+    if (hipGraphNodeGetType(nodes[i], &t) != hipSuccess) return 1;
+    if (t == hipGraphNodeTypeKernel) {
+      if (hipGraphKernelNodeGetParams(nodes[i], &kps[i]) != hipSuccess) return 1;
+    } else if (t == hipGraphNodeTypeMemcpy) {
+      if (hipGraphMemcpyNodeGetParams(nodes[i], &mps[i]) != hipSuccess) return 1;
+      // can it be re-added?  Tried once in a scratch graph, before touching g
+      hipGraph_t scratch = nullptr;
+      if (hipGraphCreate(&scratch, 0) != hipSuccess) return 1;
+      hipGraphNode_t tmp = nullptr;
+      const bool ok = add_copy(&tmp, scratch, nullptr, 0, mps[i]) == hipSuccess;
+      hipGraphDestroy(scratch);
+      if (!ok) {
+        (void)hipGetLastError();
+        return 1;
+      }
+    } else if (t == hipGraphNodeTypeMemset) {
+      if (hipGraphMemsetNodeGetParams(nodes[i], &mss[i]) != hipSuccess) return 1;
+    } else if (t != hipGraphNodeTypeEmpty) {
+      return 1;
+    }
+  }
+  // topological order (Kahn) over the segment's edges
+  std::unordered_map<hipGraphNode_t, int> idx;
+  for (size_t i = 0; i < n; ++i) idx[nodes[i]] = (int)i;
+  std::vector<std::vector<int>> preds(n), succs(n);
+  for (size_t e = 0; e < ne; ++e) {
+    const int a = idx.at(from[e]), b = idx.at(to[e]);
+    preds[b].push_back(a);
+    succs[a].push_back(b);
+  }
+  std::vector<int> indeg(n), order;
+  std::vector<int> ready;
+  for (size_t i = 0; i < n; ++i)
+    if ((indeg[i] = (int)preds[i].size()) == 0) ready.push_back((int)i);
+  while (!ready.empty()) {
+    const int v = ready.back();
+    ready.pop_back();
+    order.push_back(v);
+    for (int w : succs[v])
+      if (--indeg[w] == 0) ready.push_back(w);
+  }
+  if (order.size() != n) return 1;
+  std::vector<hipGraphNode_t> made(n, nullptr);
+  std::vector<hipGraphNode_t> d;
+  for (int v : order) {
+    d.clear();
+    if (preds[v].empty())
+      d = deps;
+    else
+      for (int u : preds[v]) d.push_back(made[u]);
+    const hipGraphNodeType t = types[v];
+    hipError_t rc;
+    if (t == hipGraphNodeTypeKernel) {
+      rc = hipGraphAddKernelNode(&made[v], g, d.data(), d.size(), &kps[v]);
+    } else if (t == hipGraphNodeTypeMemcpy) {
+      rc = add_copy(&made[v], g, d.data(), d.size(), mps[v]);
+    } else if (t == hipGraphNodeTypeMemset) {
+      rc = hipGraphAddMemsetNode(&made[v], g, d.data(), d.size(), &mss[v]);
+    } else {
+      rc = hipGraphAddEmptyNode(&made[v], g, d.data(), d.size());
+    }
+    if (rc != hipSuccess) return -1 - (int)t;  // (the caller destroys the half-built graph)
+  }
+  leaves->clear();
+  for (size_t i = 0; i < n; ++i)
+    if (succs[i].empty()) leaves->push_back(made[i]);
+  if (leaves->empty()) *leaves = deps;
+  return 0;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -33,6 +158,9 @@ int mx_graph_compose(int n, const int* kind, void* const* child, void* const* ds
   hipGraph_t g = nullptr;
   if (hipGraphCreate(&g, 0) != hipSuccess) return -3;
   std::vector<hipGraphNode_t> nodes((size_t)n, nullptr);
+  // what a later node waits for to follow node i: node i, or a flattened segment's leaves
+  std::vector<std::vector<hipGraphNode_t>> exits((size_t)n);
+  const bool flat = flat_on();
   std::vector<hipGraphNode_t> d;
   for (int i = 0; i < n; ++i) {
     d.clear();
@@ -42,10 +170,24 @@ int mx_graph_compose(int n, const int* kind, void* const* child, void* const* ds
         hipGraphDestroy(g);
         return -4;
       }
-      d.push_back(nodes[(size_t)j]);
+      for (auto h : exits[(size_t)j]) d.push_back(h);
     }
-    hipError_t rc;
+    hipError_t rc = hipSuccess;
     size_t count = 0;
+    bool done = false;
+    if (kind[i] == 0 && flat && hipGraphGetNodes((hipGraph_t)child[i], nullptr, &count) ==
+                                    hipSuccess && count > 0) {
+      std::vector<hipGraphNode_t> lv;
+      const int fr = flatten_into(g, (hipGraph_t)child[i], d, &lv);
+      if (fr == 0) {
+        exits[(size_t)i] = lv;
+        done = true;
+      } else if (fr < 0) {
+        hipGraphDestroy(g);
+        return -6;
+      }  // fr == 1: other node types -- a child-graph node below
+    }
+    if (done) continue;
     if (kind[i] == 0 && hipGraphGetNodes((hipGraph_t)child[i], nullptr, &count) == hipSuccess &&
         count == 0)  // a segment that launched nothing: keep its place in the order
       rc = hipGraphAddEmptyNode(&nodes[(size_t)i], g, d.data(), d.size());
@@ -74,6 +216,7 @@ int mx_graph_compose(int n, const int* kind, void* const* child, void* const* ds
       hipGraphDestroy(g);
       return -10 - i;
     }
+    exits[(size_t)i].assign(1, nodes[(size_t)i]);
   }
   hipGraphExec_t ex = nullptr;
   if (hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) != hipSuccess) {
@@ -105,10 +248,25 @@ int mx_graph_build_chain(int n, const int* kind, void* const* child, void* const
     hipError_t rc = hipSuccess;
     if (kind[i] == 0) {
       size_t count = 0;
-      if (hipGraphGetNodes((hipGraph_t)child[i], nullptr, &count) == hipSuccess && count == 0)
+      if (hipGraphGetNodes((hipGraph_t)child[i], nullptr, &count) == hipSuccess && count == 0) {
         rc = hipGraphAddEmptyNode(&node, g, &prev, nd);
-      else
+      } else if (flat_on()) {
+        // the segment's nodes in the chain; the next node waits for its last one(s)
+        std::vector<hipGraphNode_t> dv(prev ? 1 : 0, prev), lv;
+        const int fr = flatten_into(g, (hipGraph_t)child[i], dv, &lv);
+        if (fr < 0) {
+          hipGraphDestroy(g);
+          return -100 + fr;  // -101 - node type: adding a copied node failed
+        }
+        if (fr == 1)  // other node types: a child-graph node
+          rc = hipGraphAddChildGraphNode(&node, g, &prev, nd, (hipGraph_t)child[i]);
+        else if (lv.size() == 1)
+          node = lv[0];
+        else  // several leaves: one empty node joins them
+          rc = hipGraphAddEmptyNode(&node, g, lv.data(), lv.size());
+      } else {
         rc = hipGraphAddChildGraphNode(&node, g, &prev, nd, (hipGraph_t)child[i]);
+      }
     } else {
       void* a0 = p0[i];
       void* a1 = p1[i];

@@ -645,6 +645,10 @@ class PartyTapes:
             if rc != 0:
                 for gh, eh in handles:
                     nat.lib().mx_graph_free(gh, eh)
+                import warnings
+
+                warnings.warn(f"per-party graph of party {p} not built (mx_graph_build_chain "
+                              f"{rc}); per-action replay", RuntimeWarning, stacklevel=2)
                 return None
             handles.append((g, ex))
         self.graph_nodes = {"per_party_nodes": [len(t.steps) for t in self.tapes]}
