@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <unordered_map>
 #include <vector>
@@ -62,29 +63,31 @@ int flatten_into(hipGraph_t g, hipGraph_t child, const std::vector<hipGraphNode_
   if (ne && hipGraphGetEdges(child, from.data(), to.data(), &ne) != hipSuccess) return 1;
   // every node's type and parameters read before anything is added (a node whose
   // parameters cannot be read back -- e.g. some captured copies -- keeps the segment whole)
+  // (parameters are read again right before each node is added: what a GetParams call
+  // returns may point into storage that the next call reuses)
   std::vector<hipGraphNodeType> types(n);
-  std::vector<hipKernelNodeParams> kps(n);
-  std::vector<hipMemcpy3DParms> mps(n);
-  std::vector<hipMemsetParams> mss(n);
   for (size_t i = 0; i < n; ++i) {
     hipGraphNodeType& t = types[i];
     if (hipGraphNodeGetType(nodes[i], &t) != hipSuccess) return 1;
     if (t == hipGraphNodeTypeKernel) {
-      if (hipGraphKernelNodeGetParams(nodes[i], &kps[i]) != hipSuccess) return 1;
+      hipKernelNodeParams kp;
+      if (hipGraphKernelNodeGetParams(nodes[i], &kp) != hipSuccess) return 1;
     } else if (t == hipGraphNodeTypeMemcpy) {
-      if (hipGraphMemcpyNodeGetParams(nodes[i], &mps[i]) != hipSuccess) return 1;
+      hipMemcpy3DParms mp;
+      if (hipGraphMemcpyNodeGetParams(nodes[i], &mp) != hipSuccess) return 1;
       // can it be re-added?  Tried once in a scratch graph, before touching g
       hipGraph_t scratch = nullptr;
       if (hipGraphCreate(&scratch, 0) != hipSuccess) return 1;
       hipGraphNode_t tmp = nullptr;
-      const bool ok = add_copy(&tmp, scratch, nullptr, 0, mps[i]) == hipSuccess;
+      const bool ok = add_copy(&tmp, scratch, nullptr, 0, mp) == hipSuccess;
       hipGraphDestroy(scratch);
       if (!ok) {
         (void)hipGetLastError();
         return 1;
       }
     } else if (t == hipGraphNodeTypeMemset) {
-      if (hipGraphMemsetNodeGetParams(nodes[i], &mss[i]) != hipSuccess) return 1;
+      hipMemsetParams ms;
+      if (hipGraphMemsetNodeGetParams(nodes[i], &ms) != hipSuccess) return 1;
     } else if (t != hipGraphNodeTypeEmpty) {
       return 1;
     }
@@ -112,7 +115,12 @@ int flatten_into(hipGraph_t g, hipGraph_t child, const std::vector<hipGraphNode_
   if (order.size() != n) return 1;
   std::vector<hipGraphNode_t> made(n, nullptr);
   std::vector<hipGraphNode_t> d;
+  static const bool dbg = std::getenv("MOOSEX_FLAT_DEBUG") != nullptr;
   for (int v : order) {
+    if (dbg) {
+      fprintf(stderr, "flat: node %d type %d\n", v, (int)types[v]);
+      fflush(stderr);
+    }
     d.clear();
     if (preds[v].empty())
       d = deps;
@@ -121,11 +129,17 @@ int flatten_into(hipGraph_t g, hipGraph_t child, const std::vector<hipGraphNode_
     const hipGraphNodeType t = types[v];
     hipError_t rc;
     if (t == hipGraphNodeTypeKernel) {
-      rc = hipGraphAddKernelNode(&made[v], g, d.data(), d.size(), &kps[v]);
+      hipKernelNodeParams kp;
+      rc = hipGraphKernelNodeGetParams(nodes[v], &kp);
+      if (rc == hipSuccess) rc = hipGraphAddKernelNode(&made[v], g, d.data(), d.size(), &kp);
     } else if (t == hipGraphNodeTypeMemcpy) {
-      rc = add_copy(&made[v], g, d.data(), d.size(), mps[v]);
+      hipMemcpy3DParms mp;
+      rc = hipGraphMemcpyNodeGetParams(nodes[v], &mp);
+      if (rc == hipSuccess) rc = add_copy(&made[v], g, d.data(), d.size(), mp);
     } else if (t == hipGraphNodeTypeMemset) {
-      rc = hipGraphAddMemsetNode(&made[v], g, d.data(), d.size(), &mss[v]);
+      hipMemsetParams ms;
+      rc = hipGraphMemsetNodeGetParams(nodes[v], &ms);
+      if (rc == hipSuccess) rc = hipGraphAddMemsetNode(&made[v], g, d.data(), d.size(), &ms);
     } else {
       rc = hipGraphAddEmptyNode(&made[v], g, d.data(), d.size());
     }
