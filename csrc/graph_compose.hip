@@ -31,6 +31,19 @@ bool flat_on() {
   return on;
 }
 
+constexpr int kFlatMaxSegments = 256;
+
+// Segments with copy / memset nodes too (MOOSEX_PARTY_GRAPH_FLAT=all); by default only
+// segments of kernel (and empty) nodes are flattened -- a large composed graph whose
+// segments held other node types crashed the runtime while their copies were added.
+bool flat_all() {
+  static const bool on = [] {
+    const char* e = std::getenv("MOOSEX_PARTY_GRAPH_FLAT");
+    return e && e[0] == 'a';
+  }();
+  return on;
+}
+
 // A captured copy's node in another graph: its 3-D parameters as read back, or (when the
 // runtime does not take those back) the equivalent 1-D copy.
 hipError_t add_copy(hipGraphNode_t* out, hipGraph_t g, const hipGraphNode_t* deps, size_t nd,
@@ -72,6 +85,8 @@ int flatten_into(hipGraph_t g, hipGraph_t child, const std::vector<hipGraphNode_
     if (t == hipGraphNodeTypeKernel) {
       hipKernelNodeParams kp;
       if (hipGraphKernelNodeGetParams(nodes[i], &kp) != hipSuccess) return 1;
+    } else if (!flat_all() && t != hipGraphNodeTypeEmpty) {
+      return 1;  // (a child-graph node keeps the segment whole)
     } else if (t == hipGraphNodeTypeMemcpy) {
       hipMemcpy3DParms mp;
       if (hipGraphMemcpyNodeGetParams(nodes[i], &mp) != hipSuccess) return 1;
@@ -174,7 +189,11 @@ int mx_graph_compose(int n, const int* kind, void* const* child, void* const* ds
   std::vector<hipGraphNode_t> nodes((size_t)n, nullptr);
   // what a later node waits for to follow node i: node i, or a flattened segment's leaves
   std::vector<std::vector<hipGraphNode_t>> exits((size_t)n);
-  const bool flat = flat_on();
+  // (composed graphs of up to kFlatMaxSegments segments: the larger ones -- a LogReg
+  // training run's thousands -- keep child-graph nodes until their flattening is verified)
+  int nseg = 0;
+  for (int i = 0; i < n; ++i) nseg += kind[i] == 0;
+  const bool flat = flat_on() && (flat_all() || nseg <= kFlatMaxSegments);
   std::vector<hipGraphNode_t> d;
   for (int i = 0; i < n; ++i) {
     d.clear();
