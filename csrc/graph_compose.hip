@@ -275,6 +275,9 @@ int mx_graph_build_chain(int n, const int* kind, void* const* child, void* const
   hipGraph_t g = nullptr;
   if (hipGraphCreate(&g, 0) != hipSuccess) return -3;
   hipGraphNode_t prev = nullptr;
+  int nseg = 0;
+  for (int i = 0; i < n; ++i) nseg += kind[i] == 0;
+  const bool flat_chain = flat_on() && (flat_all() || nseg <= kFlatMaxSegments);
   for (int i = 0; i < n; ++i) {
     hipGraphNode_t node = nullptr;
     const size_t nd = prev ? 1 : 0;
@@ -283,7 +286,7 @@ int mx_graph_build_chain(int n, const int* kind, void* const* child, void* const
       size_t count = 0;
       if (hipGraphGetNodes((hipGraph_t)child[i], nullptr, &count) == hipSuccess && count == 0) {
         rc = hipGraphAddEmptyNode(&node, g, &prev, nd);
-      } else if (flat_on()) {
+      } else if (flat_chain) {
         // the segment's nodes in the chain; the next node waits for its last one(s)
         std::vector<hipGraphNode_t> dv(prev ? 1 : 0, prev), lv;
         const int fr = flatten_into(g, (hipGraph_t)child[i], dv, &lv);
