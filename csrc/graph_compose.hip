@@ -83,8 +83,11 @@ int flatten_into(hipGraph_t g, hipGraph_t child, const std::vector<hipGraphNode_
     hipGraphNodeType& t = types[i];
     if (hipGraphNodeGetType(nodes[i], &t) != hipSuccess) return 1;
     if (t == hipGraphNodeTypeKernel) {
-      hipKernelNodeParams kp;
+      hipKernelNodeParams kp = {};
       if (hipGraphKernelNodeGetParams(nodes[i], &kp) != hipSuccess) return 1;
+      // arguments the runtime does not hand back (neither an argument array nor a packed
+      // buffer): the node cannot be re-created -- keep the segment whole
+      if (kp.func == nullptr || (kp.kernelParams == nullptr && kp.extra == nullptr)) return 1;
     } else if (!flat_all() && t != hipGraphNodeTypeEmpty) {
       return 1;  // (a child-graph node keeps the segment whole)
     } else if (t == hipGraphNodeTypeMemcpy) {
@@ -133,7 +136,10 @@ int flatten_into(hipGraph_t g, hipGraph_t child, const std::vector<hipGraphNode_
   static const bool dbg = std::getenv("MOOSEX_FLAT_DEBUG") != nullptr;
   for (int v : order) {
     if (dbg) {
-      fprintf(stderr, "flat: node %d type %d\n", v, (int)types[v]);
+      hipKernelNodeParams k = {};
+      if (types[v] == hipGraphNodeTypeKernel) hipGraphKernelNodeGetParams(nodes[v], &k);
+      fprintf(stderr, "flat: node %d type %d func %p params %p extra %p\n", v, (int)types[v],
+              k.func, (void*)k.kernelParams, (void*)k.extra);
       fflush(stderr);
     }
     d.clear();
@@ -144,7 +150,7 @@ int flatten_into(hipGraph_t g, hipGraph_t child, const std::vector<hipGraphNode_
     const hipGraphNodeType t = types[v];
     hipError_t rc;
     if (t == hipGraphNodeTypeKernel) {
-      hipKernelNodeParams kp;
+      hipKernelNodeParams kp = {};
       rc = hipGraphKernelNodeGetParams(nodes[v], &kp);
       if (rc == hipSuccess) rc = hipGraphAddKernelNode(&made[v], g, d.data(), d.size(), &kp);
     } else if (t == hipGraphNodeTypeMemcpy) {
