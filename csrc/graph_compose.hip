@@ -258,9 +258,19 @@ int mx_graph_compose(int n, const int* kind, void* const* child, void* const* ds
     exits[(size_t)i].assign(1, nodes[(size_t)i]);
   }
   hipGraphExec_t ex = nullptr;
+  if (std::getenv("MOOSEX_FLAT_DEBUG") != nullptr) {
+    size_t cnt = 0;
+    hipGraphGetNodes(g, nullptr, &cnt);
+    fprintf(stderr, "compose: instantiate %zu nodes\n", cnt);
+    fflush(stderr);
+  }
   if (hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) != hipSuccess) {
     hipGraphDestroy(g);
     return -5;
+  }
+  if (std::getenv("MOOSEX_FLAT_DEBUG") != nullptr) {
+    fprintf(stderr, "compose: instantiated\n");
+    fflush(stderr);
   }
   *graph_out = (void*)g;
   *exec_out = (void*)ex;
