@@ -304,6 +304,8 @@ class ThreadTransport:
 # a party that waits this long for a message ends the evaluation (device_map runtimes
 # without an explicit timeout); a desynchronised peer that returned is detected at once
 DEFAULT_TIMEOUT_S = float(os.environ.get("MOOSEX_PARTY_TIMEOUT", "300"))
+# segments per composed executable (a larger tape is replayed as several, back to back)
+CHUNK_SEGMENTS = int(os.environ.get("MOOSEX_PARTY_GRAPH_CHUNK", "200"))
 
 
 def run_parties(comp, arguments: dict, identities: List[str], devices: List, storage: dict,
@@ -511,26 +513,38 @@ class PartyTapes:
                 offs.append(table.data_ptr() + 8 * 3 * at)
                 at += len(d)
             dst = [offs[d] if k == 2 else d for k, d in zip(kinds, dst)]
-        m = len(kinds)
-        deps = [[i - 1] if i else [] for i in range(m)]  # the total order
-        off = [0]
-        flat_deps = []
-        for d in deps:
-            flat_deps += d
-            off.append(len(flat_deps))
+        # the total order in chunks of at most CHUNK_SEGMENTS segments, one executable each
+        # (launched back to back on one stream): every chunk is small enough for the
+        # composer to flatten its segments (csrc/graph_compose.hip kFlatMaxSegments)
+        bounds, start, nseg = [], 0, 0
+        for i, k in enumerate(kinds):
+            if k == 0:
+                if nseg == CHUNK_SEGMENTS:
+                    bounds.append((start, i))
+                    start, nseg = i, 0
+                nseg += 1
+        bounds.append((start, len(kinds)))
         arr = lambda ty, xs: (ty * max(1, len(xs)))(*xs)  # noqa: E731
-        g, ex = ctypes.c_void_p(), ctypes.c_void_p()
-        rc = nat.lib().mx_graph_compose(
-            m, arr(ctypes.c_int, kinds), arr(ctypes.c_void_p, child),
-            arr(ctypes.c_void_p, dst), arr(ctypes.c_void_p, src),
-            arr(ctypes.c_int64, nbytes), arr(ctypes.c_int, off), arr(ctypes.c_int, flat_deps),
-            ctypes.byref(g), ctypes.byref(ex))
-        if rc != 0:
-            return None
-        self._graph_handles = (g, ex)
+        handles = []
+        for a, b in bounds:
+            m = b - a
+            off = [0] + [max(0, i) for i in range(m)]  # node i > 0 waits for node i - 1
+            flat_deps = list(range(m - 1))
+            g, ex = ctypes.c_void_p(), ctypes.c_void_p()
+            rc = nat.lib().mx_graph_compose(
+                m, arr(ctypes.c_int, kinds[a:b]), arr(ctypes.c_void_p, child[a:b]),
+                arr(ctypes.c_void_p, dst[a:b]), arr(ctypes.c_void_p, src[a:b]),
+                arr(ctypes.c_int64, nbytes[a:b]), arr(ctypes.c_int, off),
+                arr(ctypes.c_int, flat_deps), ctypes.byref(g), ctypes.byref(ex))
+            if rc != 0:
+                for gh, eh in handles:
+                    nat.lib().mx_graph_free(gh, eh)
+                return None
+            handles.append((g, ex))
+        self._graph_handles = handles
         self.graph_nodes = {"segments": kinds.count(0), "copy_nodes": kinds.count(1),
-                            "copy_batches": kinds.count(2)}
-        return ex
+                            "copy_batches": kinds.count(2), "executables": len(handles)}
+        return [ex for _, ex in handles]
 
     def _build_streams(self):
         """Every party's replay as ONE graph on its own stream (its own GPU when the parties
@@ -775,9 +789,7 @@ class PartyTapes:
         if ex is not None:
             ex.shutdown(wait=False)
         hs = list(getattr(self, "_party_graphs", None) or [])
-        h = getattr(self, "_graph_handles", None)
-        if h is not None:
-            hs.append(h)
+        hs += list(getattr(self, "_graph_handles", None) or [])
         for g, ex in hs:
             try:
                 from moose_amd.ops import native as nat
@@ -936,7 +948,8 @@ class PartyTapes:
             for tape in self.tapes:
                 tape._fill_keys()
             t2 = time.perf_counter()
-            nat.check(nat.lib().mx_graph_launch(self._composed, s.cuda_stream), "graph launch")
+            for ex in self._composed:
+                nat.check(nat.lib().mx_graph_launch(ex, s.cuda_stream), "graph launch")
             t3 = time.perf_counter()
             self.issue_s.append(t3 - t0)
             # host time per replay: arguments staged, keys refreshed, graph launched

@@ -60,7 +60,8 @@ def main():
                 t0 = _t.perf_counter()
                 from moose_amd.ops import native as nat
                 s = t.streams[0]
-                nat.lib().mx_graph_launch(t._composed, s.cuda_stream)
+                for ex in t._composed:
+                    nat.lib().mx_graph_launch(ex, s.cuda_stream)
                 s.synchronize()
                 ts.append((_t.perf_counter() - t0) * 1e3)
             rec["graph_only_ms_p50"] = sorted(ts)[5]
