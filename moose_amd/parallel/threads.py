@@ -308,6 +308,21 @@ DEFAULT_TIMEOUT_S = float(os.environ.get("MOOSEX_PARTY_TIMEOUT", "300"))
 CHUNK_SEGMENTS = int(os.environ.get("MOOSEX_PARTY_GRAPH_CHUNK", "200"))
 
 
+def chunk_bounds(kinds, per: int):
+    """[(start, end)) node ranges of a composed schedule, each holding at most ``per``
+    segment nodes (kind 0); a chunk starts at a segment, so the copies after a chunk's last
+    segment stay in that chunk."""
+    bounds, start, nseg = [], 0, 0
+    for i, k in enumerate(kinds):
+        if k == 0:
+            if nseg == per:
+                bounds.append((start, i))
+                start, nseg = i, 0
+            nseg += 1
+    bounds.append((start, len(kinds)))
+    return bounds
+
+
 def run_parties(comp, arguments: dict, identities: List[str], devices: List, storage: dict,
                 fixedpoint_ring: int = 128, seed: Optional[int] = None,
                 timeout: Optional[float] = None, record: bool = False):
@@ -516,14 +531,7 @@ class PartyTapes:
         # the total order in chunks of at most CHUNK_SEGMENTS segments, one executable each
         # (launched back to back on one stream): every chunk is small enough for the
         # composer to flatten its segments (csrc/graph_compose.hip kFlatMaxSegments)
-        bounds, start, nseg = [], 0, 0
-        for i, k in enumerate(kinds):
-            if k == 0:
-                if nseg == CHUNK_SEGMENTS:
-                    bounds.append((start, i))
-                    start, nseg = i, 0
-                nseg += 1
-        bounds.append((start, len(kinds)))
+        bounds = chunk_bounds(kinds, CHUNK_SEGMENTS)
         arr = lambda ty, xs: (ty * max(1, len(xs)))(*xs)  # noqa: E731
         handles = []
         for a, b in bounds:

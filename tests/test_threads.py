@@ -448,3 +448,19 @@ def test_party_tapes_capture_a_large_product():
                                    atol=1e-6)
     (_, tapes), = rt._party_tapes.values()
     assert tapes is not False and all(t.replays >= 1 for t in tapes.tapes)
+
+
+def test_composed_schedule_chunks_keep_order_and_bound_segments():
+    """PartyTapes._compose splits the composed total order into executables of at most N
+    segments (threads.chunk_bounds): consecutive, covering every node once, copies kept
+    with the segments before them."""
+    from moose_amd.parallel.threads import chunk_bounds
+
+    kinds = [0, 2, 0, 0, 1, 2, 0, 0, 0, 2, 2, 0]
+    for per in (1, 2, 3, 5, 100):
+        b = chunk_bounds(kinds, per)
+        assert b[0][0] == 0 and b[-1][1] == len(kinds)
+        assert all(b[i][1] == b[i + 1][0] for i in range(len(b) - 1))
+        assert all(sum(k == 0 for k in kinds[s:e]) <= per for s, e in b)
+        assert all(kinds[s] == 0 for s, _ in b[1:])  # a new chunk starts at a segment
+    assert chunk_bounds(kinds, 100) == [(0, len(kinds))]
