@@ -180,6 +180,39 @@ void* mx_party_kernel_fn(int which) {
   }
 }
 
+// Uncached device memory for what another GPU writes while this GPU reads it (the per-party
+// graphs' message flags and landing buffers): the owner's L2 never holds a line of it, so a
+// peer's xGMI write followed by its system-scope release (k_push) is what the owner's next
+// load sees -- coarse-grained memory only guarantees that at kernel / queue boundaries
+// (RCCL allocates its cross-GPU flags the same way).  Zero-filled.
+int mx_alloc_uncached(int dev, int64_t bytes, void** out) {
+  *out = nullptr;
+  if (bytes <= 0) bytes = 1;
+  int cur = 0;
+  hipGetDevice(&cur);
+  hipSetDevice(dev);
+  hipError_t e = hipExtMallocWithFlags(out, (size_t)bytes, hipDeviceMallocUncached);
+  if (e == hipSuccess) e = hipMemset(*out, 0, (size_t)bytes);
+  hipSetDevice(cur);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    if (*out) hipFree(*out);
+    *out = nullptr;
+    return -(int)e;
+  }
+  return 0;
+}
+
+int mx_free_uncached(int dev, void* p) {
+  if (!p) return 0;
+  int cur = 0;
+  hipGetDevice(&cur);
+  hipSetDevice(dev);
+  hipError_t e = hipFree(p);
+  hipSetDevice(cur);
+  return e == hipSuccess ? 0 : -(int)e;
+}
+
 // Peer access from device dev to device peer's memory (the push kernels' writes into another
 // GPU's landing buffers and flags); already enabled is fine.
 int mx_enable_peer(int dev, int peer) {

@@ -224,6 +224,8 @@ _SIGS = {
     "mx_graph_dot": (c_int, [c_vp, ctypes.c_char_p, ctypes.c_uint]),
     "mx_graph_launch": (c_int, [c_vp, c_vp]),
     "mx_enable_peer": (c_int, [c_int, c_int]),
+    "mx_alloc_uncached": (c_int, [c_int, c_i64, c_vp]),
+    "mx_free_uncached": (c_int, [c_int, c_vp]),
     "mx_graph_build_chain": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                      c_vp]),
     "mx_jobs_r0": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_int,
@@ -341,3 +343,40 @@ def key_buffer(keys) -> ctypes.Array:
     """Pack a list of 16-byte keys into a C buffer."""
     raw = b"".join(bytes(k) for k in keys)
     return ctypes.create_string_buffer(raw, len(raw))
+
+
+class _UncachedBlock:
+    """``bytes`` of uncached device memory (mx_alloc_uncached), exposed to torch through
+    ``__cuda_array_interface__``; freed when the last tensor viewing it is gone (torch keeps
+    the exporting object alive for the storage's lifetime)."""
+
+    def __init__(self, dev: int, nbytes: int):
+        p = ctypes.c_void_p()
+        check(lib().mx_alloc_uncached(dev, int(nbytes), ctypes.byref(p)),
+              f"uncached device allocation of {nbytes} bytes")
+        self.dev, self.ptr, self.nbytes = dev, p.value, int(nbytes)
+        self.__cuda_array_interface__ = {"shape": (self.nbytes,), "typestr": "|u1",
+                                         "data": (self.ptr, False), "version": 2,
+                                         "strides": None}
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                lib().mx_free_uncached(self.dev, ctypes.c_void_p(self.ptr))
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+
+def uncached_zeros(shape, dtype, device) -> torch.Tensor:
+    """A zero-filled tensor in uncached device memory (csrc/party_graph.hip
+    mx_alloc_uncached): what a PEER GPU writes while this one polls or later reads it --
+    message flags and landing buffers of the per-party stream graphs (threads.py)."""
+    import math
+
+    device = torch.device(device)
+    el = torch.empty((), dtype=dtype).element_size()
+    n = math.prod(shape) if len(shape) else 1
+    blk = _UncachedBlock(device.index if device.index is not None else 0, max(1, n) * el)
+    with torch.cuda.device(device):
+        raw = torch.as_tensor(blk, device=device)
+    return raw[:n * el].view(dtype).reshape(tuple(shape))

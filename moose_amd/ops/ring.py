@@ -607,10 +607,9 @@ def decode(a: RT, frac: int) -> torch.Tensor:
         d = [t.data.contiguous() for t in a.parts]
         out = torch.empty(a.shape, dtype=torch.float64, device=a.device)
         ptrs = [nat.ptr(x) for x in d] + [None] * (4 - len(d))
-        # a deferred truncation (Opened.shift) is the decode's division by 2^shift more
         nat.check(nat.lib().mx_addn_decode(
             nat.dev_of(d[0]), _words(a.bits), *ptrs, nat.ptr(out), a.numel(),
-            int(frac) + a.shift, nat.stream_of(d[0])), "addn_decode")
+            int(frac), nat.stream_of(d[0])), "addn_decode")
         return out
     ad = a.data.contiguous()
     out = torch.empty(a.shape, dtype=torch.float64, device=a.device)
@@ -1406,6 +1405,24 @@ def zs_trunc3_k(z: RT, slot_ptr: int, nmul: int, m: int, nonces):
     return o0, o1
 
 
+def zs_trunc3_rows(z: RT, slot_ptr: int, nmul: int, m: int, nonces, buf4, r0: int):
+    """zs_trunc3_k for the row block [r0, r0 + rows) of a pipelined product: ``z`` =
+    [3, rows, N] local products, the shares written straight into rows of ``buf4`` (the
+    result's [4, M, N] share-pair ring buffer, slots x0, x1, x2, x0)."""
+    bits = z.bits
+    d = z.data.contiguous()
+    n = math.prod(z.shape) // 3  # ring elements per party in the block
+    el = 2 if bits == 128 else 1
+    os_ = math.prod(buf4.shape[1:]) // el  # party stride of the result (elements)
+    o0 = buf4.data_ptr() + r0 * math.prod(buf4.shape[2:]) * 8
+    nn = (ctypes.c_uint64 * 6)(*[v & MASK64 for v in nonces])
+    rc = nat.lib().mx_mul_trunc3_kv(
+        nat.dev_of(d), _words(bits), nat.ptr(d), None, None, None, ctypes.c_void_p(o0),
+        ctypes.c_void_p(o0 + os_ * el * 8), n, os_, ctypes.c_void_p(slot_ptr), nmul & MASK64,
+        int(m), nn, None, nat.stream_of(d))
+    nat.check(rc, "zs_trunc3_rows")
+
+
 def add_zs3(v: RT, r: RT):
     """Stacked arith zero share from precomputed keystreams ``r`` (= PRF(k_p) per party)
     plus the reshare: returns (s0, s1) exactly like ``rss_mul3_k(arith, v)``."""
@@ -1481,18 +1498,14 @@ class Opened(RT):
     ``data``.  A decode of it runs one fused pass (mx_addn_decode) instead of add + decode:
     the ring-valued sum never goes to memory."""
 
-    __slots__ = ("parts", "stream", "shift")
+    __slots__ = ("parts", "stream")
 
-    def __init__(self, a: RT, b: RT, c: RT, d: RT = None, shift: int = 0):
-        """``shift``: the opened sum carries ``shift`` more fractional bits than its type (a
-        truncation deferred into the reveal): ``data`` is the sum shifted right
-        (arithmetic, exact floor) and a decode divides by 2^(frac + shift)."""
+    def __init__(self, a: RT, b: RT, c: RT, d: RT = None):
         _RT_DATA.__set__(self, None)
         self.bits = a.bits
         self._shape = a.shape
         self.parts = (a, b, c) if d is None else (a, b, c, d)
         self.stream = _stream_of(a.data)
-        self.shift = shift
 
     def pending(self) -> bool:
         return _RT_DATA.__get__(self) is None
@@ -1505,8 +1518,6 @@ class Opened(RT):
             s = add3(*self.parts[:3])
             if len(self.parts) == 4:
                 s = binary("add", s, self.parts[3])
-            if self.shift:
-                s = s.sar(self.shift)
             d = s.data
             _RT_DATA.__set__(self, d)
             self.parts = None
@@ -1521,15 +1532,15 @@ class Opened(RT):
         return self.parts[0].device if self.pending() else self.data.device
 
 
-def opened(a: RT, b: RT, c: RT, d: RT = None, shift: int = 0) -> RT:
-    """a + b + c [+ d] (shifted right by ``shift``: Opened) as an :class:`Opened` (lazy)
-    when the fused decode applies."""
+def opened(a: RT, b: RT, c: RT, d: RT = None) -> RT:
+    """a + b + c [+ d] as an :class:`Opened` (lazy) when the fused decode applies.  The
+    addends are shares of the value at its own type's scale: a reveal never opens a value
+    with more fractional bits than its type (no truncation is ever deferred into a reveal)."""
     parts = (a, b, c) if d is None else (a, b, c, d)
     if a.bits in (64, 128) and all(t.shape == a.shape and t.bits == a.bits for t in parts):
-        return Opened(*parts, shift=shift)
+        return Opened(*parts)
     s = add3(a, b, c)
-    s = s if d is None else binary("add", s, d)
-    return s.sar(shift) if shift else s
+    return s if d is None else binary("add", s, d)
 
 
 def add3(a: RT, b: RT, c: RT) -> RT:

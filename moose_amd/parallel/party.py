@@ -127,6 +127,45 @@ class RoundB:
         return [(self.out0[c], self.out1[c], got["w0"], got["w1"]) if r == 2 else None
                 for c, r in enumerate(roles)]
 
+    def reveal_to_member(self, j):
+        """Open the (truncated) product to member P_j in ONE round after round A -- the
+        reveal's round and round B merged, and only the value's own shares on the wire:
+
+        * P2 (the dealer): P0 sends w0, P1 sends w1; P2 sums x2 + x0 + w0 + w1;
+        * P0: P1 sends w1 + x2 (its round-B message plus its reveal message, summed);
+          P0 sums x0 + w0 + (w1 + x2);
+        * P1: P0 sends w0 + x0; P1 sums x2 + w1 + (w0 + x0).
+
+        w0 + w1 = x1, so every receiver learns x0 + x1 + x2 -- the TruncPr'd value -- and
+        nothing it would not learn from round B followed by the reveal.  Returns, for each
+        hosted component playing P_j, the addends of the value; None for the others.  The
+        shares stay pending (:meth:`finish` runs the ordinary round B if something reads
+        them; the receiver already knows the value)."""
+        if j == 2:
+            return self.reveal_to_dealer()
+        sess, roles, like, bits = self.sess, self.roles, self.like, self.bits
+        R._join(self.stream)
+        src = 1 - j  # the other non-dealer party
+        mine = None
+        c_src = {r: c for c, r in enumerate(roles)}.get(src)
+        if c_src is not None:
+            # P1 adds its x2 (out1), P0 its x0 (out0)
+            own = self.out1[c_src] if src == 1 else self.out0[c_src]
+            mine = R.binary("add", R.RT(self.w[c_src], bits),
+                            R.RT(own.reshape(self.w[c_src].shape), bits)).data
+        got = sess.party_exchange(self.plc, [("wx", src, j, mine, like)])
+        nb = math.prod(like[0]) * 8
+        sess.stats.record_send(self.plc.owners[src], self.plc.owners[j], nb)
+        sess.stats.record_round(nb)
+        out = []
+        for c, r in enumerate(roles):
+            if r != j:
+                out.append(None)
+                continue
+            keep = self.out0[c] if j == 0 else self.out1[c]  # x0 at P0, x2 at P1
+            out.append((keep, self.w[c].reshape(keep.shape), got["wx"].reshape(keep.shape)))
+        return out
+
 
 class NoRoundB:
     """The deferred round of a process that hosts no party of the placement (SPMD
@@ -277,15 +316,35 @@ class MulAddTail:
     3-out-of-3 share of a * b.  :meth:`finish` is the reshare (z -> P_{p-1}) and the add;
     :meth:`reveal_to` opens a * b + c to a member P_j in ONE round instead of the reshare
     round plus the reveal: P_{j+1} sends z_{j+1} + c_{j+2}, P_{j+2} sends z_{j+2} + c_j
-    (each its own z plus its second component), P_j sums z_j + c_{j+1} + both."""
+    (each its own z plus its second component), P_j sums z_j + c_{j+1} + both.
+
+    ``post_shift`` = m > 0 (rep.mul_add_trunc): the value is TruncPr(a * b + c, m).  Then
+    z + c0 (an additive share of the untruncated value) goes through the dot tail -- zero
+    share + reshare + TruncPr, 2 rounds -- and a reveal merges the tail's round B with the
+    reveal (:meth:`RoundB.reveal_to_member`): 2 rounds, and the receiver only ever holds
+    shares of the TRUNCATED value (the reference reveals TruncPr'd shares too:
+    replicated/convert.rs:280-313 after replicated/fixedpoint.rs:80-103)."""
 
     def __init__(self, sess, plc, z, c0, c1, bits, post_shift=0):
         self.sess, self.plc, self.z, self.c0, self.c1, self.bits = sess, plc, z, c0, c1, bits
         self.done = False
         self.rep = None  # the DeferredRep whose shares finish() completes
-        # a TruncPr by post_shift bits pending too (mul_add_trunc): a reveal opens the value
-        # and shifts it exactly; finish() runs it as the dot's tail on the additive shares
         self.post_shift = post_shift
+        self._rb = None  # the truncating tail's round B (post_shift), once round A ran
+
+    def _tail_round_a(self):
+        """post_shift: the dot tail's round A on z + c0; the new shares land in the
+        DeferredRep, round B stays pending (self._rb)."""
+        from moose_amd.runtime.session import PV
+
+        sess, bits = self.sess, self.bits
+        v = R.binary("add", self.z, self.c0)
+        nonces = tuple(sess.nonce(self.plc) for _ in range(7))
+        s0, s1, self._rb = sess.party_dot_trunc(
+            self.plc, PV(self.plc, R.RT(v.data.unsqueeze(0), bits)), self.post_shift, nonces,
+            defer=True)
+        self.rep._s0 = PV(self.plc, R.RT(s0.v.data[0], bits))
+        self.rep._s1 = PV(self.plc, R.RT(s1.v.data[0], bits))
 
     def finish(self):
         if self.done:
@@ -294,30 +353,34 @@ class MulAddTail:
         from moose_amd.runtime.session import PV
 
         if self.post_shift:
-            # z + c0 is this party's 3-out-of-3 additive share of a * b + c: zero share +
-            # reshare + TruncPr in the dot tail's 2 rounds (instead of reshare + TruncPr)
-            sess, bits = self.sess, self.bits
-            v = R.binary("add", self.z, self.c0)
-            nonces = tuple(sess.nonce(self.plc) for _ in range(7))
-            s0, s1 = sess.party_dot_trunc(self.plc, PV(self.plc, R.RT(v.data.unsqueeze(0), bits)),
-                                          self.post_shift, nonces)
-            self.rep._s0 = PV(self.plc, R.RT(s0.v.data[0], bits))
-            self.rep._s1 = PV(self.plc, R.RT(s1.v.data[0], bits))
+            if self._rb is None:
+                self._tail_round_a()
+            self._rb.finish()
             return
         zn = self.sess.shift(PV(self.plc, self.z), 1).v
         o0, o1 = R.binary2("add", self.z, self.c0, zn, self.c1)
         self.rep._s0, self.rep._s1 = PV(self.plc, o0), PV(self.plc, o1)
 
     def reveal_to(self, host):
-        """The opened value at ``host`` (an Opened of four addends), None elsewhere; None
+        """The opened value at ``host`` (an Opened of its addends), None elsewhere; False
         when ``host`` is not a member (the caller finishes and reveals generically)."""
         plc = self.plc
         if host not in plc.owners:
             return False
-        self.done = True
         sess = self.sess
         j = plc.owners.index(host)
         idx = sess.party_index(plc)
+        if self.post_shift:
+            if self.done or self._rb is not None:
+                return False  # shares already formed (or round A ran): the generic reveal
+            self._tail_round_a()
+            parts = self._rb.reveal_to_member(j)[0]
+            # round B stays pending: a later reader runs it (finish)
+            if idx != j:
+                return None
+            shape = self.z.data.shape
+            return R.opened(*[R.RT(t.reshape(shape), self.bits) for t in parts])
+        self.done = True
         like = (tuple(self.z.data.shape), self.z.data.dtype) if idx is not None else None
         mine = None
         if idx is not None and idx != j:
@@ -331,5 +394,4 @@ class MulAddTail:
             sess.stats.record_send(plc.owners[a], host, nb)
         if idx != j:
             return None
-        return R.opened(self.z, self.c1, R.RT(got["m1"], self.bits), R.RT(got["m2"], self.bits),
-                        shift=self.post_shift)
+        return R.opened(self.z, self.c1, R.RT(got["m1"], self.bits), R.RT(got["m2"], self.bits))

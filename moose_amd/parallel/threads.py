@@ -31,10 +31,16 @@ from typing import Dict
 from typing import List
 from typing import Optional
 
+import numpy as np
 import torch
 
 from moose_amd.ops import ring as R
 from moose_amd.parallel.transport import TransportError
+
+
+def _host(v):
+    """A decoded output as something numpy compares (tensors to the host)."""
+    return v.detach().cpu().numpy() if isinstance(v, torch.Tensor) else v
 
 
 def _indexed(d) -> torch.device:
@@ -151,12 +157,18 @@ class ThreadTransport:
         from the receiver's graph pool reuses blocks the receiver's EARLIER segments still
         use (torch reuses pool blocks in the capturing stream's order, which a write from
         another stream does not follow) -- the cause of the composed-as-DAG failures."""
+        from moose_amd.ops import native as nat
+
         self.landing = {}
         for src, items in self.log.items():
             bufs = []
             for kind, shape, dtype, _bits in items:
                 if kind in ("rt", "t") and math.prod(shape) > 0:
-                    bufs.append(torch.empty(shape, dtype=dtype, device=self.device))
+                    # uncached device memory: the sender's peer writes are what this party's
+                    # later kernels read, with no stale line of an earlier replay in its L2
+                    bufs.append(nat.uncached_zeros(shape, dtype, self.device)
+                                if self.device.type == "cuda" and UNCACHED_LANDING
+                                else torch.empty(shape, dtype=dtype, device=self.device))
             self.landing[src] = bufs
         self._land_cursor = {}
 
@@ -306,6 +318,12 @@ class ThreadTransport:
 DEFAULT_TIMEOUT_S = float(os.environ.get("MOOSEX_PARTY_TIMEOUT", "300"))
 # segments per composed executable (a larger tape is replayed as several, back to back)
 CHUNK_SEGMENTS = int(os.environ.get("MOOSEX_PARTY_GRAPH_CHUNK", "200"))
+# per-party stream graphs: message flags and landing buffers in uncached device memory
+# (MOOSEX_PARTY_UNCACHED=0: PyTorch's allocator, coarse-grained -- probes only)
+UNCACHED_LANDING = os.environ.get("MOOSEX_PARTY_UNCACHED", "1") != "0"
+# per-party stream graphs are checked once at capture against the per-action replay of the
+# same tapes from the same key state (bitwise); a mismatch keeps the per-action replay
+VALIDATE_STREAMS = os.environ.get("MOOSEX_PARTY_STREAMS_VALIDATE", "1") != "0"
 
 
 def chunk_bounds(kinds, per: int):
@@ -470,14 +488,84 @@ class PartyTapes:
         self._composed = self._compose() if single else None
         self._party_graphs = None
         self._launchers = None  # host threads issuing the per-party graph launches
+        # how replays run, and whether the per-party graphs were checked at capture
+        self.validated = None
+        self.fallback = None
         if self.streams_mode:
             try:
                 self._party_graphs = self._build_streams()
             except Exception as e:  # noqa: BLE001 - e.g. no peer access between the GPUs
                 import warnings
 
-                warnings.warn(f"per-party stream graphs unavailable ({e}); per-action replay",
-                              RuntimeWarning, stacklevel=2)
+                self.fallback = f"per-party stream graphs unavailable: {e}"
+                warnings.warn(f"{self.fallback}; per-action replay", RuntimeWarning,
+                              stacklevel=2)
+            if self._party_graphs is not None and VALIDATE_STREAMS:
+                self._validate_streams(arguments)
+
+    @property
+    def replay_form(self) -> str:
+        if self._party_graphs is not None:
+            return "party_graphs"
+        return "composed" if self._composed is not None else "per_action"
+
+    def _key_state(self):
+        """Each tape's device key-refresh counter (unseeded tapes draw replay e's keys from
+        ChaCha12(master, e)): saved and restored around a validation replay so the
+        per-action replay runs from the same keys."""
+        return [t.keys._epoch.clone() if getattr(t.keys, "_epoch", None) is not None else None
+                for t in self.tapes]
+
+    def _set_key_state(self, state):
+        for t, e in zip(self.tapes, state):
+            if e is not None:
+                t.keys._epoch.copy_(e)
+
+    def _validate_streams(self, arguments: dict):
+        """Run the per-party graphs once and the per-action replay of the same tapes once,
+        from the same key state and arguments, and compare every party's outputs bitwise.
+        The per-action replay orders every message with stream events (no flags, no peer
+        writes of our own): if the graphs' device-side messaging misbehaves on this machine
+        (a lost or stale push, a flag seen before its payload), the outputs differ and the
+        runtime keeps the per-action replay -- recorded in ``fallback`` / ``validated`` --
+        instead of returning wrong values later."""
+        import warnings
+
+        from moose_amd.parallel.transport import TransportError
+
+        for d in set(self.devices):
+            torch.cuda.synchronize(d)
+        state = self._key_state()
+        why = None
+        try:
+            got = self._replay_streams(arguments)
+        except TransportError as e:
+            got, why = None, f"a message never arrived ({e})"
+        for d in set(self.devices):
+            torch.cuda.synchronize(d)
+        for err in self._errs:
+            err.zero_()
+        self._set_key_state(state)
+        want = self._replay_actions(arguments)
+        for d in set(self.devices):
+            torch.cuda.synchronize(d)
+        for t in self.tapes:
+            t.replays -= 2  # the two validation replays are not evaluations
+        if got is not None:
+            for ident in self.identities:
+                a, b = got.get(ident, {}), want.get(ident, {})
+                if set(a) != set(b) or any(
+                        not np.array_equal(np.asarray(_host(a[k])), np.asarray(_host(b[k])))
+                        for k in a):
+                    why = f"outputs of {ident} differ from the per-action replay"
+                    break
+        if why is None:
+            self.validated = True
+            return
+        self.validated = False
+        self.fallback = f"per-party stream graphs failed validation: {why}"
+        warnings.warn(f"{self.fallback}; per-action replay", RuntimeWarning, stacklevel=3)
+        self._free_party_graphs()
 
     def _compose(self):
         """The schedule as ONE hipGraph (csrc/graph_compose.hip) in a total order: each
@@ -586,7 +674,11 @@ class PartyTapes:
                 if p != q and self.devices[p] != self.devices[q]:
                     nat.check(nat.lib().mx_enable_peer(self.devices[p].index,
                                                        self.devices[q].index), "peer access")
-        self._flags = [torch.zeros(max(1, nflags[q]), dtype=torch.int32, device=self.devices[q])
+        # the flags a peer raises while this party polls: uncached device memory (coherent
+        # without kernel boundaries; csrc/party_graph.hip mx_alloc_uncached)
+        self._flags = [nat.uncached_zeros((max(1, nflags[q]),), torch.int32, self.devices[q])
+                       if UNCACHED_LANDING else
+                       torch.zeros(max(1, nflags[q]), dtype=torch.int32, device=self.devices[q])
                        for q in range(n)]
         self._epochs = [torch.zeros(1, dtype=torch.int64, device=d) for d in self.devices]
         self._errs = [torch.zeros(1, dtype=torch.int32, device=d) for d in self.devices]
@@ -595,6 +687,10 @@ class PartyTapes:
         shadow = os.environ.get("MOOSEX_PARTY_STREAMS_SHADOW") == "1"
         self._shadows = []
         self._dummy = torch.zeros(64, dtype=torch.int32, device=self.devices[0])
+        # test-only fault injection (MOOSEX_FAULT=party_landing): the first push writes a
+        # scratch buffer instead of its receiver's landing buffer -- the receiver reads a
+        # stale message, which the capture-time validation must catch
+        fault = os.environ.get("MOOSEX_FAULT") == "party_landing"
         handles = []
         for p, tape in enumerate(self.tapes):
             dev = self.devices[p]
@@ -630,6 +726,10 @@ class PartyTapes:
                             raise CaptureError(f"message {k} from party {p} to {dst}: sizes "
                                                "differ")
                         flag = self._flags[dst].data_ptr() + 4 * flag_of[(p, dst, k)]
+                        if fault:
+                            fault = False
+                            buf = torch.empty_like(buf)
+                            self._tables.append(buf)
                         rows.append((t.data_ptr(), buf.data_ptr(),
                                      t.numel() * t.element_size(), flag,
                                      pieces.data_ptr() + 4 * j))
@@ -885,6 +985,13 @@ class PartyTapes:
                     err.zero_()
         if self._composed is not None:
             return self._replay_composed(arguments)
+        return self._replay_actions(arguments)
+
+    def _replay_actions(self, arguments: dict) -> Dict[str, dict]:
+        """The per-action replay: one host thread issues every party's segments and the
+        message copies, interleaved, on the parties' streams (event edges only)."""
+        import time
+
         n = len(self.tapes)
         prev_dev = torch.cuda.current_device()
         prev = [torch.cuda.current_stream(d) for d in set(self.devices)]

@@ -456,6 +456,8 @@ class CommStep:
 def _parse_fault(spec, rank):
     if not spec:
         return None
+    if spec == "party_landing":  # parallel/threads.py: per-party stream graphs only
+        return None
     what, _, who = spec.partition("@")
     if who and int(who) != rank:
         return None

@@ -317,9 +317,16 @@ def mux(sess, s, x, y):
     return rep.mux(sess, s, x, y)
 
 
-# the sign of a fixed(i, f) value is bit i + f of its ring element (|x| < 2^i): per-party
-# sessions run the sign's adder over those low bits only (MOOSEX_SIGN_WIDTH=0: all bits)
-SIGN_WIDTH = os.environ.get("MOOSEX_SIGN_WIDTH", "1") != "0"
+# opt-in (MOOSEX_SIGN_WIDTH=1): take the sign of a fixed(i, f) value from bit i + f of its
+# ring element, running the sign's adder over those low bits only.  That is only right while
+# |x| < 2^i, and i is a NOMINAL bound (mul and dot keep it while the value grows), so by
+# default relu / abs / sign_bit use the ring's msb as the reference does
+# (replicated/exp.rs, fixedpoint ops: rep.msb over all bits).
+SIGN_WIDTH = os.environ.get("MOOSEX_SIGN_WIDTH", "0") == "1"
+
+
+# exp's adder carries only over the bits its planes read (MOOSEX_EXP_WIDTH=0: all bits)
+EXP_WIDTH = os.environ.get("MOOSEX_EXP_WIDTH", "1") != "0"
 
 
 def _value_width(x: RepFixed):
@@ -732,7 +739,9 @@ def _exp2_parts(sess, a: RepFixed, negative: bool):
               and hasattr(sess, "p_cross_plain") and npad >= 2 and npad & (npad - 1) == 0)
     # only bits below f + nint are read with a nonzero weight (higher planes are padding
     # whose factor is 1 whatever the bit): the adder need not carry beyond them
-    bd = rep.bit_decompose(sess, a.t, width=f + nint if SIGN_WIDTH and f + nint < bits else None)
+    # (bounded by construction, unlike a sign: planes above f + nint are never read, so a
+    # carry into them cannot change the result)
+    bd = rep.bit_decompose(sess, a.t, width=f + nint if EXP_WIDTH and f + nint < bits else None)
     ab = rep.b2a_planes(sess, bd, 0, f + npad, bits)  # arithmetic bits, leading axis
     return _exp2_from_planes(sess, ab, f, integ, bits, nint, npad, negative, merged)
 
@@ -1259,7 +1268,7 @@ def _sign_and_exp_party(sess, x: RepFixed, plus: float = 0.0):
     rounds).  Their factors 1 - [z >= T] and 1 - [z < -T] join the tree: jn + 2 factors
     (8 for fixed(24, 40)) instead of 25 -> 32, two tree levels (4 rounds) fewer.
     None when the ring has too few bits for fc >= 20 (the caller uses the three steps)."""
-    if not (ONE_DECOMPOSITION and SIGN_WIDTH) or getattr(sess, "is_simulated", True):
+    if not ONE_DECOMPOSITION or getattr(sess, "is_simulated", True):
         return None
     f, integ, bits = x.frac, x.integ, x.bits
     # a dot whose TruncPr is pending (rep.PendingTrunc): decompose its untruncated value

@@ -153,14 +153,16 @@ class PendingTrunc(RepTensor):
     additive share ``v_add`` (a per-party dot before its tail:
     fixedpoint._dot_public_trunc_jobs), plus public addends at the truncated scale
     (``pubs``, party 0 adds them).  Reading the shares completes it with the batched tail
-    (zero share + reshare + TruncPr by m: the dot's 2 rounds, as before).  Aware readers
-    skip the truncation: the sigmoid's one bit decomposition takes the reshared
-    untruncated value (:meth:`reshare_untruncated`, 1 round), a reveal opens the masked
-    additive shares and shifts exactly (1 round instead of 3)."""
+    (zero share + reshare + TruncPr by m: the dot's 2 rounds, as before).  The sigmoid's one
+    bit decomposition takes the reshared untruncated value (:meth:`reshare_untruncated`, 1
+    round -- it stays secret-shared); a reveal runs the dot tail and merges its round B with
+    the reveal (:func:`_reveal_pending`, 2 rounds): no receiver ever holds shares of the
+    untruncated value."""
 
     def __init__(self, sess, plc, bits, v_add, m, pubs=()):
         self._sess, self.v_add, self.m, self.pubs = sess, v_add, m, list(pubs)
         self.completed = False
+        self._rb = None  # round B of a tail a reveal ran (shares pending until read)
         super().__init__(plc, bits, "arith", None, None)
 
     def with_public(self, c):
@@ -178,6 +180,8 @@ class PendingTrunc(RepTensor):
 
     def _complete(self):
         if self.completed:
+            if self._rb is not None:
+                self._rb.finish()
             return
         self.completed = True
         sess, plc, bits = self._sess, self.plc, self.bits
@@ -216,31 +220,38 @@ class PendingTrunc(RepTensor):
 
 
 def _reveal_pending(sess, x: PendingTrunc, host):
-    """Open a PendingTrunc to a member: the other two parties send their zero-share-masked
-    additive shares, the host sums them with its own and shifts by m (floor, exact): ONE
-    round instead of the tail's two plus the reveal.  None: the generic reveal."""
+    """Open a PendingTrunc to a member P_j: the dot tail (zero share + reshare + TruncPr by
+    m, round A) and then its round B merged with the reveal (parallel/party.py
+    RoundB.reveal_to_member) -- 2 rounds instead of the tail's two plus the reveal, and the
+    receiver sums shares of the TRUNCATED value only (reference: replicated/convert.rs:
+    280-313 reveals the TruncPr'd tensor of replicated/fixedpoint.rs:80-103).  The shares
+    stay pending until something reads them (round B then runs as usual).  None: the
+    generic reveal."""
     from moose_amd.parallel.spmd import Remote
 
     plc = x.plc
-    if host not in plc.owners or not hasattr(sess, "party_exchange"):
+    if host not in plc.owners or getattr(sess, "party_dot_trunc", None) is None \
+            or not hasattr(sess, "party_exchange") or getattr(sess, "is_simulated", True):
         return None
     j = plc.owners.index(host)
     idx = sess.party_index(plc)
-    x.completed = True  # its shares are never formed
-    z = sess.p_add_zero_share(plc, PV(plc, x.additive() if idx is not None else x.v_add))
-    like = (tuple(z.v.data.shape), z.v.data.dtype) if idx is not None else None
-    mine = z.v.data if idx is not None else None
-    got = sess.party_exchange(plc, [("a", (j + 1) % 3, j, mine if idx == (j + 1) % 3 else None,
-                                     like),
-                                    ("b", (j + 2) % 3, j, mine if idx == (j + 2) % 3 else None,
-                                     like)])
-    for a in ((j + 1) % 3, (j + 2) % 3):
-        sess.stats.record_send(plc.owners[a], host, payload_bytes_of(z.v) if idx is not None
-                               else 0)
+    nonces = tuple(sess.nonce(plc) for _ in range(7))  # as _complete: members and others
+    x.completed = True
+    if idx is None:
+        r = PV(plc, Remote(x.bits))
+        x._s0, x._s1 = r, r
+        return HV(host, Remote(x.bits))
+    v = x.additive()
+    s0, s1, rb = sess.party_dot_trunc(plc, PV(plc, R.RT(v.data.contiguous().unsqueeze(0),
+                                                        x.bits)), x.m, nonces, defer=True)
+    x._s0 = PV(plc, R.RT(s0.v.data[0], x.bits))
+    x._s1 = PV(plc, R.RT(s1.v.data[0], x.bits))
+    x._rb = rb
+    parts = rb.reveal_to_member(j)[0]
     if idx != j:
         return HV(host, Remote(x.bits))
-    return HV(host, R.opened(z.v, R.RT(got["a"], x.bits), R.RT(got["b"], x.bits),
-                             shift=x.m))
+    shape = v.data.shape
+    return HV(host, R.opened(*[R.RT(t.reshape(shape), x.bits) for t in parts]))
 
 
 def payload_bytes_of(v):
@@ -802,10 +813,21 @@ def dot_trunc(sess, x: RepTensor, y: RepTensor, m: int) -> RepTensor:
         # every chunk's shares land in rows of the result (no concatenation afterwards)
         N = y.s0.v.shape[2]
         shp = (3, M, N) + ((2,) if bits == 128 else ())
-        out0 = torch.empty(shp, dtype=data.dtype, device=data.device)
-        out1 = torch.empty_like(out0)
+        # a stacked device session: each chunk's whole tail is one kernel writing its rows of
+        # the result's share-pair ring buffer
+        rows_fused = (cuda and getattr(sess, "fused", False) and m and kind == "arith"
+                      and bits in (64, 128) and getattr(sess, "p_zs_trunc_rows", None) is not None)
+        if rows_fused:
+            buf4 = torch.empty((4,) + shp[1:], dtype=data.dtype, device=data.device)
+            out0, out1 = buf4[0:3], buf4[1:4]
+        else:
+            out0 = torch.empty(shp, dtype=data.dtype, device=data.device)
+            out1 = torch.empty_like(out0)
 
         def tail(v, r0, r1):
+            if rows_fused:
+                sess.p_zs_trunc_rows(plc, v, m, buf4, r0)
+                return
             if use_party:
                 nonces = tuple(sess.nonce(plc) for _ in range(7))
                 party(plc, v, m, nonces, out=(out0[:, r0:r1], out1[:, r0:r1]))
@@ -1099,10 +1121,11 @@ def mul_add(sess, a: RepTensor, b: RepTensor, c: RepTensor) -> RepTensor:
 
 
 def mul_add_trunc(sess, a: RepTensor, b: RepTensor, c: RepTensor, m: int) -> RepTensor:
-    """TruncPr(a * b + c, m).  On a per-party session both the product's reshare and the
-    truncation wait for the reader: a reveal opens the untruncated value in one round and
-    shifts it exactly (parallel/party.py MulAddTail.post_shift); any other reader gets the
-    dot tail's 2 rounds (zero share + reshare + TruncPr) instead of reshare + TruncPr."""
+    """TruncPr(a * b + c, m).  On a per-party session the product's reshare is folded into
+    the truncation: a * b + c goes through the dot tail (zero share + reshare + TruncPr, 2
+    rounds instead of reshare + TruncPr's 2 after it), and a reveal merges the tail's
+    second round with the reveal (parallel/party.py MulAddTail) -- the receiver only sums
+    shares of the truncated value."""
     f = getattr(sess, "p_mul_add_deferred", None)
     if f is not None and 0 < m <= 63:
         r = f(a.plc, a, b, c, post_shift=m)

@@ -89,6 +89,7 @@ class LocalMooseRuntime:
         self.fixedpoint_ring = fixedpoint_ring
         self.seed = seed
         self.last_stats = None
+        self.last_replay = None  # parties on GPUs: how the last replay ran (PartyTapes)
         self.last_timings = None
         # replay whole evaluations as hipGraphs (runtime/graphs.py).  Default (None): on a
         # GPU, "auto" -- a computation evaluated a second time with the same argument
@@ -235,6 +236,11 @@ class LocalMooseRuntime:
                 self.last_stats_by_identity = {i: t.stats for i, t in
                                                zip(self.identities, tapes[1].tapes)}
                 self.last_stats = self.last_stats_by_identity[self.identities[0]]
+                # how this replay ran (per-party graphs / composed / per-action) and whether
+                # the per-party graphs passed their capture-time check
+                self.last_replay = {"form": tapes[1].replay_form,
+                                    "validated": tapes[1].validated,
+                                    "fallback": tapes[1].fallback}
                 result = {}
                 for i in self.identities:
                     result.update(outs[i])

@@ -146,7 +146,7 @@ class StackedSession(Session):
         self._keytable = kt
 
     # rows per pipelined dot+TruncPr (protocols/replicated.dot_trunc); 1 = no pipelining
-    pipeline_chunks = 1
+    pipeline_chunks = int(os.environ.get("MOOSEX_STACKED_CHUNKS", "1"))
     # the interpreter batches independent same-shape Dots into one launch sequence
     batch_dots = True
 
@@ -714,6 +714,18 @@ class StackedSession(Session):
         # the messages of the per-party protocol (reshare folded into TruncPr, 2 rounds)
         record_tail_traffic(self.stats, plc, _nbytes(r[0]) // 3)
         return PV(plc, r[0]), PV(plc, r[1])
+
+    def p_zs_trunc_rows(self, plc, z, m, buf4, r0):
+        """p_zs_trunc of a row block of a pipelined product (rep.dot_trunc with
+        ``pipeline_chunks`` > 1): the new shares written into rows [r0, r0 + rows) of the
+        result's [4, M, N] share-pair ring buffer ``buf4``.  The chunk is its own protocol
+        instance (its own nonces)."""
+        nmul = self.nonce(plc)
+        nonces = tuple(self.nonce(plc) for _ in range(6))
+        R.zs_trunc3_rows(z.v, self.key_ptr(plc, 0), nmul, m, nonces, buf4, r0)
+        from moose_amd.parallel.party import record_tail_traffic
+
+        record_tail_traffic(self.stats, plc, _nbytes(z.v) // 3)
 
     def party_exchange(self, plc, specs):
         """Every party is local: a per-party message is the sender's buffer."""

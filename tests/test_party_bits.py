@@ -18,6 +18,7 @@ def _lr(device, monkeypatch, bits_on, width_on, one_dec=False, ring=64):
 
     monkeypatch.setenv("MOOSEX_PARTY_BITS", "1" if bits_on else "0")
     monkeypatch.setattr(FP, "SIGN_WIDTH", width_on)
+    monkeypatch.setattr(FP, "EXP_WIDTH", width_on)
     monkeypatch.setattr(FP, "ONE_DECOMPOSITION", one_dec)
     tm = logistic_regression_tutorial(ring)
     rt = LocalMooseRuntime(IDS, device_map={i: device for i in IDS}, seed=5, use_graphs=False)
@@ -58,8 +59,10 @@ def test_one_decomposition_sigmoid_fused_equals_generic(device, ring, monkeypatc
 @pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
 def test_range_split_and_deferred_truncation_save_rounds(device, monkeypatch):
     """fixed(24, 40): the range split drops the exp tree from 32 to 8 factors (two levels
-    fewer; 2 rounds, the polynomial's levels run beside the tree's) and the reveal absorbs
-    the reciprocal's last truncation (2 rounds); the values stay within 1e-6 of sklearn."""
+    fewer; 2 rounds, the polynomial's levels run beside the tree's); the reciprocal's last
+    truncation as one dot tail whose second round merges with the reveal costs no more
+    rounds than TruncPr then the mirror (and the reveal opens the truncated value only:
+    tests/test_reveal_precision.py); the values stay within 1e-6 of sklearn."""
     base, r_base, e_base = _lr(device, monkeypatch, True, True, one_dec=True, ring=128)
     monkeypatch.setattr(FP, "DEFER_DOT_TRUNC", False)
     nodot, r_nodot, e_nodot = _lr(device, monkeypatch, True, True, one_dec=True, ring=128)
@@ -68,7 +71,7 @@ def test_range_split_and_deferred_truncation_save_rounds(device, monkeypatch):
     monkeypatch.setattr(FP, "RANGE_SPLIT", False)
     monkeypatch.setattr(FP, "DEFER_OUTPUT_TRUNC", False)
     old, r_old, e_old = _lr(device, monkeypatch, True, True, one_dec=True, ring=128)
-    assert r_mid == r_old - 4
+    assert r_mid == r_old - 2
     # the exp's polynomial sum and final product as one truncated product: 2 rounds fewer
     assert r_nodot == r_mid - 2
     # the dot's TruncPr left to its reader: the decomposition takes the untruncated value
@@ -79,9 +82,10 @@ def test_range_split_and_deferred_truncation_save_rounds(device, monkeypatch):
 
 def test_pending_dot_revealed_directly_and_read_by_other_ops():
     """A public-operand dot on per-party sessions keeps its TruncPr pending
-    (rep.PendingTrunc): revealed directly it opens in one round and shifts exactly; read
-    by another op (here a multiplication) it completes with the dot's tail -- both within
-    the fixed-point error of the plaintext result."""
+    (rep.PendingTrunc): revealed directly it runs the dot tail with its second round merged
+    into the reveal (2 rounds, the truncated value opened); read by another op (here a
+    multiplication) it completes with the dot's tail -- both within the fixed-point error of
+    the plaintext result."""
     import moose_amd as pm
 
     alice, bob, carole = (pm.host_placement(n) for n in IDS)
@@ -120,7 +124,7 @@ def test_pending_dot_revealed_directly_and_read_by_other_ops():
     p = x @ w
     for want in (p, p * p):
         assert any(g.shape == want.shape and np.abs(g - want).max() < 1e-9 for g in got)
-    assert seen  # the dot revealed directly was opened without its tail
+    assert seen  # the dot revealed directly took the merged tail + reveal
 
 
 def test_deferred_truncation_read_by_another_op(monkeypatch):
@@ -292,3 +296,37 @@ def test_jobs_round2_folded_into_next_round0_bitwise_equal(device, ring, monkeyp
     sep, r_s, _ = _lr(device, monkeypatch, True, True, one_dec=True, ring=ring)
     assert np.array_equal(fold, sep) and r_f == r_s and e < 1e-6
     assert n_fold < calls["r2"]
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_sign_beyond_the_nominal_integer_bound(device):
+    """fixed(8, 27): a product keeps the nominal 8 integer bits while its value grows past
+    2^8 (20 * 20 = 400).  relu / abs take the ring's msb by default (the width shortcut is
+    opt-in: MOOSEX_SIGN_WIDTH=1), so the per-party runtime agrees with the stacked one and
+    with the plaintext (relu(20 * 20) returned 0)."""
+    import moose_amd as pm
+
+    alice, bob, carole = (pm.host_placement(n) for n in IDS)
+    rep = pm.replicated_placement("rep", players=[alice, bob, carole])
+    fx = pm.fixed(8, 27)
+
+    @pm.computation
+    def f(x: pm.Argument(placement=alice, vtype=pm.TensorType(pm.float64))):
+        with alice:
+            xf = pm.cast(x, dtype=fx)
+        with rep:
+            sq = pm.mul(xf, xf)
+            r = pm.relu(pm.sub(sq, pm.constant(np.array([0.0]), dtype=fx)))
+            a = pm.abs(pm.mul(xf, pm.constant(np.array([-1.0]), dtype=fx)))
+        with carole:
+            return pm.cast(r, dtype=pm.float64), pm.cast(a, dtype=pm.float64)
+
+    x = np.array([20.0, -20.0, 21.0, 1.5, -0.25])  # x * x < 2^9: no wrap at 2^54
+    outs = {}
+    for name, kw in (("parties", {"device_map": {i: device for i in IDS}}),
+                     ("stacked", {"device": device})):
+        rt = LocalMooseRuntime(IDS, seed=2, use_graphs=False, fixedpoint_ring=64, **kw)
+        outs[name] = [np.asarray(v) for v in rt.evaluate_computation(f, {"x": x}).values()]
+    for name, got in outs.items():
+        for want in (x * x, np.abs(x)):
+            assert any(np.allclose(g, want, rtol=1e-6) for g in got), (name, got, want)

@@ -167,6 +167,11 @@ def test_thread_party_tapes_replay_bitwise_equal_eager(mode, monkeypatch):
     composed into one hipGraph in a round-synchronous total order (default on one device:
     each round's messages one batched copy kernel, or one copy node per message), and the
     per-action replay."""
+    if mode == "streams":
+        # per-party stream graphs need their streams on distinct hardware queues: a fresh
+        # child process with enough queues (tests/gpu_streams_child.py) -- no skip
+        _streams_child("replay")
+        return
     composed = mode not in ("per-action", "streams")
     monkeypatch.setenv("MOOSEX_PARTY_GRAPH", "1" if composed else "0")
     monkeypatch.setenv("MOOSEX_PARTY_COPY_BATCH", "0" if mode == "copy-per-message" else "1")
@@ -186,13 +191,7 @@ def test_thread_party_tapes_replay_bitwise_equal_eager(mode, monkeypatch):
             assert set(got) == set(want)
             for k in want:
                 assert np.array_equal(np.asarray(got[k]), np.asarray(want[k])), k
-    if mode == "streams" and any("stream graphs disabled" in str(w.message) for w in caught):
-        # one GPU only: the three party streams share the process's hardware queues, and a
-        # party's bounded flag wait can sit in front of its producer's kernels -- the wait
-        # times out, the replay is redone per action (values checked above).  On several
-        # GPUs each party's graph has its device to itself.
-        pytest.skip("party streams shared a hardware queue on one GPU (bounded wait fell "
-                    "back to the per-action replay; values were checked)")
+    assert not any("stream graphs" in str(w.message) for w in caught)
     (c, tapes), = rt._party_tapes.values()
     assert tapes is not False and tapes.tapes[0].replays == 2
     assert (tapes._composed is not None) == composed
@@ -299,76 +298,50 @@ def test_party_ks_chain_matches_per_level(dev, monkeypatch):
 @pytest.mark.gpu
 def test_device_flag_push_wait_orders_two_streams():
     """The per-party stream graphs' message signalling alone (csrc/party_graph.hip k_push /
-    k_wait under mx_graph_build_chain): graph A delays (a chain of GEMMs), writes a payload
-    and pushes it to a landing buffer with a flag; graph B, launched FIRST on another stream,
-    waits for the flag and copies the landing buffer out.  Every replay B must see A's
-    payload of that replay."""
-    import ctypes
+    k_wait under mx_graph_build_chain): graph A delays (a chain of kernels), writes a payload
+    and pushes it to an uncached landing buffer with a flag; graph B, launched FIRST on
+    another stream, waits for the flag and copies the landing buffer out.  Every replay B
+    must see A's payload of that replay.  Run in a fresh child process whose two streams
+    have hardware queues of their own (tests/gpu_streams_child.py): a timed-out wait FAILS."""
+    _streams_child("flag")
 
-    from moose_amd.ops import native as nat
 
-    dev = torch.device("cuda:0")
-    sa, sb = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
-    n = 4096
-    val = torch.zeros(1, dtype=torch.int64, device=dev)
-    payload = torch.zeros(n, dtype=torch.int64, device=dev)
-    landing = torch.zeros(n, dtype=torch.int64, device=dev)
-    out = torch.zeros(n, dtype=torch.int64, device=dev)
-    m = torch.randn(1 << 24, device=dev)
-    torch.sin(m)  # library / kernel initialisation outside the capture
-    ga, gb = torch.cuda.CUDAGraph(keep_graph=True), torch.cuda.CUDAGraph(keep_graph=True)
-    torch.cuda.synchronize()
-    with torch.cuda.stream(sa):
-        ga.capture_begin()
-        y = m
-        for _ in range(40):  # ~1 ms of work before the payload is written
-            y = torch.sin(y)
-        payload.copy_(val.expand(n) + (y[0] * 0).to(torch.int64))
-        ga.capture_end()
-    with torch.cuda.stream(sb):
-        gb.capture_begin()
-        out.copy_(landing)
-        gb.capture_end()
-    ep_a = torch.zeros(1, dtype=torch.int64, device=dev)
-    ep_b = torch.zeros(1, dtype=torch.int64, device=dev)
-    flags = torch.zeros(1, dtype=torch.int32, device=dev)
-    err = torch.zeros(1, dtype=torch.int32, device=dev)
-    pieces = torch.zeros(1, dtype=torch.int32, device=dev)
-    table = torch.tensor([payload.data_ptr(), landing.data_ptr(), n * 8, flags.data_ptr(),
-                          pieces.data_ptr()], dtype=torch.int64, device=dev)
+def _streams_child(case):
+    import os
+    import subprocess
+    import sys
 
-    def chain(kinds, child, p0, p1, p2, i0, i64):
-        k = len(kinds)
-        arr = lambda ty, xs: (ty * k)(*xs)  # noqa: E731
-        g, ex = ctypes.c_void_p(), ctypes.c_void_p()
-        rc = nat.lib().mx_graph_build_chain(
-            k, arr(ctypes.c_int, kinds), arr(ctypes.c_void_p, child), arr(ctypes.c_void_p, p0),
-            arr(ctypes.c_void_p, p1), arr(ctypes.c_void_p, p2), arr(ctypes.c_int, i0),
-            arr(ctypes.c_int64, i64), ctypes.byref(g), ctypes.byref(ex))
-        assert rc == 0, rc
-        return g, ex
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="16", PYTHONUNBUFFERED="1")
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(here, "gpu_streams_child.py"), case],
+                       env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, (r.stdout[-4000:], r.stderr[-4000:])
 
-    A = chain([5, 0, 6], [0, ga.raw_cuda_graph(), 0], [ep_a.data_ptr(), 0, table.data_ptr()],
-              [0, 0, ep_a.data_ptr()], [0, 0, 0], [0, 0, 1], [0, 0, n * 8])
-    B = chain([5, 7, 0], [0, 0, gb.raw_cuda_graph()], [ep_b.data_ptr(), flags.data_ptr(), 0],
-              [0, ep_b.data_ptr(), 0], [0, err.data_ptr(), 0], [0, 1, 0], [0, 0, 0])
-    try:
-        for r in range(1, 6):
-            val.fill_(1000 + r)
-            torch.cuda.synchronize()
-            nat.check(nat.lib().mx_graph_launch(B[1], sb.cuda_stream), "launch B")
-            nat.check(nat.lib().mx_graph_launch(A[1], sa.cuda_stream), "launch A")
-            torch.cuda.synchronize()
-            if int(err.item()) != 0 and r == 1:
-                # both streams on one hardware queue: B's wait sits in front of A's work,
-                # the bounded wait gives up -- the ordering cannot be exercised here
-                pytest.skip("the two streams share a hardware queue on this device")
-            assert int(err.item()) == 0
-            assert int(flags.item()) == r and int(ep_a.item()) == r and int(ep_b.item()) == r
-            assert bool((out == 1000 + r).all()), (r, out[:4].tolist())
-    finally:
-        for g, ex in (A, B):
-            nat.lib().mx_graph_free(g, ex)
+
+@pytest.mark.gpu
+def test_party_streams_validation_catches_a_corrupted_landing_buffer(monkeypatch):
+    """MOOSEX_FAULT=party_landing: the first message's push writes a scratch buffer, so its
+    receiver reads a stale landing buffer.  The capture-time validation (the per-party
+    graphs against the per-action replay of the same tapes and keys) must catch it: the
+    runtime records the failure and keeps the per-action replay, whose values stay bitwise
+    equal to eager."""
+    monkeypatch.setenv("MOOSEX_PARTY_STREAMS", "1")
+    monkeypatch.setenv("MOOSEX_FAULT", "party_landing")
+    comp = _comp(False)
+    args = _args()
+    devs = {i: "cuda:0" for i in IDS}
+    want = LocalMooseRuntime(IDS, device_map=devs, seed=11, use_graphs=False
+                             ).evaluate_computation(comp, args)
+    rt = LocalMooseRuntime(IDS, device_map=devs, seed=11, use_graphs=True)
+    with pytest.warns(RuntimeWarning, match="failed validation"):
+        for _ in range(4):
+            got = rt.evaluate_computation(comp, args)
+            for k in want:
+                assert np.array_equal(np.asarray(got[k]), np.asarray(want[k])), k
+    (_, tapes), = rt._party_tapes.values()
+    assert tapes.validated is False and tapes.replay_form == "per_action"
+    assert rt.last_replay["form"] == "per_action" and "validation" in rt.last_replay["fallback"]
+    assert tapes.tapes[0].replays == 2
 
 
 @pytest.mark.gpu
