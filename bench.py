@@ -431,7 +431,9 @@ def _lr_stacked(runs, device, world=1):
     # default with no flags (auto: captured at the second evaluation, replayed after), and
     # the three parties as threads of this process, each on its own HIP stream
     # (parallel/threads.py; per-party tapes replayed by one host thread)
-    modes = ["eager", "graphs", "default", "parties"]
+    # "storage" / "parties_storage": the same model with x read from alice's storage (a
+    # Load; replayed through runtime/storage_tap.py), runtime defaults
+    modes = ["eager", "graphs", "default", "storage", "parties", "parties_storage"]
     gpus3 = None
     if (device.type == "cuda" and world >= 3 and torch.cuda.device_count() >= 3
             and os.environ.get("MOOSEX_SHARED_GPU") != "1"):
@@ -440,23 +442,27 @@ def _lr_stacked(runs, device, world=1):
         modes.append("parties_3gpu")
     for mode in modes:
         flags = {"eager": {"use_graphs": False}, "graphs": {"use_graphs": True},
-                 "default": {},
+                 "default": {}, "storage": {},
                  "parties": {"device_map": {r: str(device) for r in ROLES}, "timeout": 30},
+                 "parties_storage": {"device_map": {r: str(device) for r in ROLES},
+                                     "timeout": 30},
                  "parties_3gpu": {"device_map": {r: str(d) for r, d in zip(ROLES, gpus3 or [])},
                                   "timeout": 30},
                  }[mode]
         try:
             rt = LocalMooseRuntime(list(ROLES), device=device, fixedpoint_ring=128, **flags)
-            args = {"x": tm.x_test}
+            comp, args = tm.computation, {"x": tm.x_test}
+            if mode.endswith("storage"):
+                comp, args = _storage_fed_lr(tm, rt)
             for _ in range(3):
-                r = rt.evaluate_computation(tm.computation, args)
+                r = rt.evaluate_computation(comp, args)
             lat = []
             for _ in range(runs):
                 t0 = time.perf_counter()
-                r = rt.evaluate_computation(tm.computation, args)  # synchronises the device
+                r = rt.evaluate_computation(comp, args)  # synchronises the device
                 lat.append((time.perf_counter() - t0) * 1e3)
         except Exception as e:  # noqa: BLE001 - an extra mode: record, keep the others
-            if not mode.startswith("parties"):
+            if not (mode.startswith("parties") or mode.endswith("storage")):
                 raise
             out[mode] = {"error": f"{type(e).__name__}: {e}"[:300]}
             continue
@@ -473,9 +479,12 @@ def _lr_stacked(runs, device, world=1):
                 rec["host_issue_ms_p50"] = iss[len(iss) // 2] * 1e3
                 # one composed graph (one GPU), per-party graphs with device-side message
                 # flags (several GPUs), or per-action issue (the fallback)
-                rec["replay_form"] = ("party_graphs" if tapes[0]._party_graphs is not None
-                                      else "composed" if tapes[0]._composed is not None
-                                      else "per_action")
+                rec["replay_form"] = tapes[0].replay_form
+                # per-party graphs are checked at capture against the per-action replay
+                # (bitwise); a failure keeps the per-action replay and is recorded here
+                rec["validated"] = tapes[0].validated
+                if tapes[0].fallback:
+                    rec["fallback"] = tapes[0].fallback[:200]
         elif mode != "eager":
             rec["captured"] = bool(rt._graphs.plans)
         out[mode] = rec
@@ -493,6 +502,21 @@ def _lr_stacked(runs, device, world=1):
                 os.environ.pop("MOOSEX_PARTY_STREAMS", None)
             out["parties_3gpu_per_action"] = alt
     return out
+
+
+def _storage_fed_lr(tm, rt):
+    """The tutorial model with its input Loaded from alice's storage (the reference's
+    storage-fed worker deployment): (computation, arguments) and x written to storage."""
+    from moose_amd.runtime import storage_tap
+    from moose_amd.runtime.local import to_native
+
+    native = to_native(tm.computation, 128)
+    inputs = [op for op in native.operations if op.kind == "Input"]
+    names = {op.attrs.get("arg_name") or op.name for op in inputs}
+    for op in inputs:
+        rt.write_value_to_storage(op.placement.owner, op.attrs.get("arg_name") or op.name,
+                                  tm.x_test)
+    return storage_tap.storage_fed(native, names), {}
 
 
 def _lr_stacked_mode(tm, device, flags, runs):
@@ -518,8 +542,8 @@ def _lr_stacked_mode(tm, device, flags, runs):
     return {"p50_ms": lat[len(lat) // 2], "p90_ms": lat[int(0.9 * (len(lat) - 1))],
             "max_abs_err_vs_sklearn": float(np.abs(np.asarray(list(r.values())[0])
                                                    - tm.proba).max()),
-            "replay_form": ("party_graphs" if tapes and tapes[0]._party_graphs is not None
-                            else "per_action"), "rounds": rt.last_stats.rounds}
+            "replay_form": tapes[0].replay_form if tapes else None,
+            "validated": tapes[0].validated if tapes else None, "rounds": rt.last_stats.rounds}
 
 
 def _lr_spmd(runs, world, rank, device, prog):

@@ -96,6 +96,13 @@ class SPMDTape:
         self.sess.use_keytable(self.keys)
         self.sess.key_setups = []
         self.interp = Interpreter(self.sess, storage, ring)
+        # this party's host Load / Save at the replay's edges (runtime/storage_tap.py)
+        from moose_amd.runtime.storage_tap import StorageTap
+
+        self.storage = storage
+        self.tap = StorageTap(comp, storage, self.device, hosts={identity},
+                              arguments=arguments)
+        self.interp.storage_tap = self.tap
         stager = G._Stager(uploads, self.device)
         self.steps = []  # CUDAGraph segments and CommSteps, in program order
         pool = torch.cuda.graph_pool_handle()
@@ -143,6 +150,7 @@ class SPMDTape:
         finally:
             tr.tape = None
             self.interp.on_op = None
+            self.interp.storage_tap = None
         torch.cuda.synchronize(self.device)
         self._stager = stager  # the staged constants stay alive with the graphs
         self.stream = stream
@@ -162,6 +170,8 @@ class SPMDTape:
 
     # ------------------------------------------------------------------------------
     def _decode(self, interp, sess, outs) -> Dict[str, np.ndarray]:
+        if interp is getattr(self, "interp", None) and self.tap.save_keys:
+            self.tap.write_saves(self.storage)  # a replay's saved values, into the storage
         res = {}
         for tag, lv in outs.items():
             if lv.kind == "unit" or not sess.materialized(lv.v):
@@ -208,6 +218,8 @@ class SPMDTape:
                 pin = self._pinned[k] = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
             pin.copy_(src)
             t.copy_(pin, non_blocking=True)
+        if self.tap.loads:  # the stored values this replay loads, as arguments
+            self.tap.refresh(self.storage)
 
     def replay(self, arguments: dict) -> Dict[str, np.ndarray]:
         with torch.cuda.stream(self.stream):
@@ -283,6 +295,29 @@ def _agree(tr, ok: bool) -> bool:
     return bool(t.item())
 
 
+def storage_key(comp, storage, identity: str, tr, arguments=None) -> Optional[int]:
+    """A key of what ``comp``'s Loads read from storage, the SAME on every rank: each rank
+    hashes the (key, shape, dtype) of the values its own identity loads
+    (runtime/storage_tap.signature) and the group sums the hashes.  A stored value only its
+    owner can see is then part of every rank's message-plan and tape key, so a changed shape
+    re-records the plan everywhere instead of desynchronising the replay.  None when
+    ``comp`` loads nothing or cannot be taped (the headers are sent)."""
+    import hashlib
+
+    import torch.distributed as dist
+
+    if not any(op.kind == "Load" for op in comp.operations) or not G.capturable(comp):
+        return None
+    sig = G.storage_signature(comp, storage, hosts={identity}, arguments=arguments)
+    h = int.from_bytes(hashlib.blake2b(repr(sig).encode(), digest_size=7).digest(), "little")
+    if tr.world <= 1:
+        return h
+    nccl = dist.get_backend(tr.group) == "nccl"
+    t = torch.tensor([h], dtype=torch.int64, device=tr.device if nccl else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=tr.group)
+    return int(t.item())
+
+
 def evaluate(comp, arguments: dict, identity: str, role_ranks: Dict[str, int], tr, device,
              storage, ring: int, seed: Optional[int] = None):
     """Evaluate ``comp`` as ``identity`` through the tape cache: the first evaluation of a
@@ -294,12 +329,13 @@ def evaluate(comp, arguments: dict, identity: str, role_ranks: Dict[str, int], t
     from moose_amd.parallel.spmd import _loads
     from moose_amd.parallel.spmd import _structure_key
 
-    if not enabled(device) or not getattr(tr, "plans", False) or _loads(comp) \
-            or not G.capturable(comp):
+    skey = getattr(tr, "storage_key", None)  # the caller's collective storage_key()
+    if not enabled(device) or not getattr(tr, "plans", False) \
+            or (_loads(comp) and skey is None) or not G.capturable(comp):
         return None
     key = (tr.plan_scope, tr.rank, tr.world, id(tr.group), identity,
            tuple(sorted(role_ranks.items())), _structure_key(comp), _argument_key(arguments),
-           G.signature(arguments), seed)
+           G.signature(arguments), seed, skey)
     tape = _TAPES.get(key)
     if tape is not None:
         if tape is False:

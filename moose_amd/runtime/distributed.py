@@ -109,6 +109,10 @@ def run_spmd(comp: Computation, arguments: dict, identities: List[str], *, rank:
     t0 = time.perf_counter()
     # a program evaluated again with the same argument signature replays its recorded
     # tape (captured kernel segments + prebuilt message rounds, parallel/spmd_graphs.py)
+    # a program that Loads: every rank agrees on what the owners' stored values look like
+    # (one small collective), so its message plan and tape are keyed on them
+    tr.storage_key = (spmd_graphs.storage_key(comp, store, identity, tr, arguments)
+                      if getattr(tr, "plans", False) else None)
     taped = spmd_graphs.evaluate(comp, arguments, identity, role_ranks, tr, device, store,
                                  fixedpoint_ring, seed)
     if taped is not None:

@@ -18,8 +18,12 @@ graph (``torch.cuda.CUDAGraph`` is hipGraph on ROCm) and afterwards replays it:
    with fresh random keys (so each replay draws independent randomness -- the nonce
    sequence is fixed, the keys are not), replay, decode the outputs.
 
-Anything that cannot be captured (host side effects such as Save/Load, data-dependent
-uploads, CPU devices) falls back to eager evaluation.
+Host ``Load`` / ``Save`` are served at the replay's edges by a
+:class:`~moose_amd.runtime.storage_tap.StorageTap` (loaded values are static buffers
+refreshed from the storage before each replay, saved values are read back after it); the
+plan is specialised on the stored values' shapes and dtypes as on the arguments'.  Anything
+else that cannot be captured (share checkpoints, data-dependent uploads, CPU devices) falls
+back to eager evaluation.
 """
 from __future__ import annotations
 
@@ -38,7 +42,6 @@ from moose_amd.runtime.interpreter import numpy_to_torch
 from moose_amd.runtime.keys import KeyTable
 from moose_amd.runtime.session import StackedSession
 
-_SIDE_EFFECTS = {"Save", "Load"}
 SEGMENT_OPS = int(os.environ.get("MOOSEX_GRAPH_SEGMENT_OPS", "32"))
 
 
@@ -103,7 +106,20 @@ def signature(arguments: dict):
 
 
 def capturable(comp) -> bool:
-    return not any(op.kind in _SIDE_EFFECTS for op in comp.operations)
+    """Can an evaluation of ``comp`` be replayed?  Host Load / Save go through a StorageTap;
+    share checkpoints and computed keys keep the computation eager."""
+    from moose_amd.runtime import storage_tap
+
+    return storage_tap.capturable(comp)
+
+
+def storage_signature(comp, storage, hosts=None, arguments=None):
+    """What ``comp``'s Loads read (runtime/storage_tap.signature): part of a plan's key."""
+    from moose_amd.runtime import storage_tap
+
+    if not any(op.kind == "Load" for op in comp.operations):
+        return ()
+    return storage_tap.signature(comp, storage, hosts, arguments)
 
 
 class GraphPlan:
@@ -138,6 +154,10 @@ class GraphPlan:
             self.first = self._decode(interp, outs)
         self.stats = sess.stats
         torch.cuda.synchronize(self.device)
+        # host Load / Save at the replay's edges (static buffers staged before the capture)
+        from moose_amd.runtime.storage_tap import StorageTap
+
+        self.tap = StorageTap(comp, storage, self.device, arguments=arguments)
         # 2. capture on a session with a frozen, refreshed key table
         self.keys = KeyTable(self.device, capacity=max(256, sess.keytable.n + 16))
         self.keys.refresh()
@@ -181,6 +201,7 @@ class GraphPlan:
             state["n"] += 1
 
         self.interp.on_op = rotate
+        self.interp.storage_tap = self.tap
         with _upload_hook(stager), torch.cuda.stream(stream):
             try:
                 self.outs = self.interp.run(comp, self.static)
@@ -196,6 +217,7 @@ class GraphPlan:
                 if state["g"] is not None:
                     end()
         self.interp.on_op = None
+        self.interp.storage_tap = None
         torch.cuda.synchronize(self.device)
         self._stager = stager  # keep the staged constants alive
         self.replays = 0
@@ -237,6 +259,7 @@ class GraphPlan:
                 # pinned buffer followed by a blit (0.321 ms; profiles/r3_graphs_vs_eager.md)
                 src = torch.from_numpy(np.ascontiguousarray(a).reshape(t.shape))
                 t.copy_(src if src.dtype == t.dtype else src.to(t.dtype))
+        self.tap.refresh(self.storage)  # the stored values this replay loads
         if self.seed is None:
             self.keys.refresh(self.keys.n)  # fresh randomness for this replay (used slots)
         else:  # a seeded evaluation: the seeded session's keys, as the eager run draws them
@@ -244,6 +267,7 @@ class GraphPlan:
         for g in self.graphs:
             g.replay()
         self.replays += 1
+        self.tap.write_saves(self.storage)  # what it saved, read back into the storage
         return self._decode(self.interp, self.outs)
 
 
@@ -267,7 +291,10 @@ class GraphCache:
         self._eager_key = None
 
     def evaluate(self, comp, arguments, device, storage, ring, seed=None, lanes=None):
-        key = (id(comp), signature(arguments))
+        if not capturable(comp):
+            return None
+        key = (id(comp), signature(arguments),
+               storage_signature(comp, storage, arguments=arguments))
         self._eager_key = None
         plan = self.plans.get(key)
         if plan is not None and plan.comp is comp:

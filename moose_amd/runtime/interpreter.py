@@ -135,6 +135,8 @@ class Interpreter:
         self.fixed_ring = fixedpoint_ring  # override Fixed128 -> Fixed64 if 64
         self.outputs = {}
         self.on_op = None
+        # replayed evaluations: Load / Save served by a runtime.storage_tap.StorageTap
+        self.storage_tap = None
         # independent operations on separate HIP streams (runtime/lanes.py)
         self.lanes = None
         dev = getattr(sess, "device", None)
@@ -878,7 +880,9 @@ class Interpreter:
             return LV(plc, "unit", None, MV(plc, None))
         host = op.placement.owner
         val = self.to_host(val, host)
-        if self.sess.materialized(val.v):
+        if self.storage_tap is not None:  # a capture: stored after each replay
+            self.storage_tap.record_save(host, k, self, val)
+        elif self.sess.materialized(val.v):
             self.storage.setdefault(host, {})[k] = self.to_numpy(val)
         return LV(op.placement, "unit", None, HV(host, None))
 
@@ -888,6 +892,9 @@ class Interpreter:
         if isinstance(op.placement, ReplicatedPlacement):
             return self._load_shares(op, k)
         host = op.placement.owner
+        if self.storage_tap is not None:  # a capture: a static buffer refreshed per replay
+            return self._host_value_from_python(host, self.storage_tap.load(host, k),
+                                                op.sig.ret)
         store = self.storage.get(host, {})
         if k not in store:
             from moose_amd.utils import storage as st

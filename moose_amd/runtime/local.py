@@ -224,7 +224,8 @@ class LocalMooseRuntime:
                     and G.capturable(comp) and not _is_lowered(comp))
         key = None
         if tapeable:
-            key = (id(comp), G.signature(arguments))
+            key = (id(comp), G.signature(arguments),
+                   G.storage_signature(comp, self.storage, arguments=arguments))
             tapes = self._party_tapes.get(key)
             if tapes is not None and tapes[0] is comp and tapes[1] is not False:
                 t0 = time.perf_counter()

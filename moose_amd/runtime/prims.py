@@ -600,7 +600,17 @@ def _sign(nb, a):
     lo = torch.where(neg, -1, 1).to(torch.int64)
     hi = torch.where(neg, -1, 0).to(torch.int64)
     return R.RT(torch.stack([lo, hi], dim=-1), 128)
-prim("Inverse")(_f(torch.linalg.inv))
+def _inverse(a):
+    """torch.linalg.inv without its error check on device tensors: the check reads the
+    solver's info flag back to the host, which a hipGraph capture cannot do (a singular
+    input gives inf/nan entries instead of an exception, like numpy's LinAlgError-free
+    paths; on the host the checked form runs)."""
+    if a.is_cuda:
+        return torch.linalg.inv_ex(a)[0]
+    return torch.linalg.inv(a)
+
+
+prim("Inverse")(_f(_inverse))
 
 
 @prim("Softmax")

@@ -10,9 +10,12 @@ process has streams: every party stream then has a queue to itself, and the chec
 (exit 1) instead of skipping when the wait times out.
 
 Cases:
-  flag     k_push / k_wait ordering of two graphs on two streams (5 replays)
-  replay   seeded per-party stream graphs: capture-time validation passes, every replay
-           bitwise equal to eager, no fallback
+  flag      k_push / k_wait ordering of two graphs on two streams (5 replays)
+  replay    seeded per-party stream graphs: capture-time validation passes, every replay
+            bitwise equal to eager, no fallback
+  fault     a corrupted landing buffer (MOOSEX_FAULT=party_landing) is caught by the
+            validation (wrong values, not a timeout) and the per-action replay is kept
+  fallback  a lost message after the validation: the per-action replay from then on
 """
 import ctypes
 import os
@@ -118,5 +121,79 @@ def replay_case():
     print("replay: validated, 3 replays bitwise equal to eager")
 
 
+def fault_case():
+    """MOOSEX_FAULT=party_landing: the first push writes a scratch buffer instead of its
+    receiver's landing buffer.  With the streams on queues of their own the flags all
+    arrive, so the capture-time validation must catch the wrong VALUES."""
+    import warnings
+
+    from moose_amd.runtime.local import LocalMooseRuntime
+    from test_spmd import _args
+    from test_spmd import _comp
+
+    os.environ["MOOSEX_PARTY_STREAMS"] = "1"
+    os.environ["MOOSEX_FAULT"] = "party_landing"
+    ids = ["alice", "bob", "carole"]
+    comp, args = _comp(False), _args()
+    devs = {i: "cuda:0" for i in ids}
+    want = LocalMooseRuntime(ids, device_map=devs, seed=11, use_graphs=False
+                             ).evaluate_computation(comp, args)
+    rt = LocalMooseRuntime(ids, device_map=devs, seed=11, use_graphs=True)
+    with warnings.catch_warnings(record=True) as caught:
+        warnings.simplefilter("always")
+        for _ in range(4):
+            got = rt.evaluate_computation(comp, args)
+            for k in want:
+                assert np.array_equal(np.asarray(got[k]), np.asarray(want[k])), k
+    (_, tapes), = rt._party_tapes.values()
+    assert tapes.validated is False and tapes.replay_form == "per_action"
+    assert "differ from the per-action replay" in tapes.fallback, tapes.fallback
+    assert any("failed validation" in str(w.message) for w in caught)
+    assert rt.last_replay["form"] == "per_action" and tapes.tapes[0].replays == 2
+    print("fault: caught by validation ->", tapes.fallback)
+
+
+def fallback_case():
+    """A per-party stream replay that reports a lost message (TransportError) AFTER the
+    validation passed is redone -- and every later replay runs -- per action, bitwise equal
+    to eager."""
+    import warnings
+
+    from moose_amd.parallel import threads as T
+    from moose_amd.parallel.transport import TransportError
+    from moose_amd.runtime.local import LocalMooseRuntime
+    from test_spmd import _args
+    from test_spmd import _comp
+
+    os.environ["MOOSEX_PARTY_STREAMS"] = "1"
+    ids = ["alice", "bob", "carole"]
+    comp, args = _comp(False), _args()
+    devs = {i: "cuda:0" for i in ids}
+    want = LocalMooseRuntime(ids, device_map=devs, seed=11, use_graphs=False
+                             ).evaluate_computation(comp, args)
+    calls = {"n": 0}
+    orig = T.PartyTapes._replay_streams
+
+    def flaky(self, arguments):
+        calls["n"] += 1
+        if calls["n"] == 3:  # 1: the validation, 2: the first replay, 3: the second
+            raise TransportError("injected: a message never arrived")
+        return orig(self, arguments)
+
+    T.PartyTapes._replay_streams = flaky
+    rt = LocalMooseRuntime(ids, device_map=devs, seed=11, use_graphs=True)
+    with warnings.catch_warnings(record=True) as caught:
+        warnings.simplefilter("always")
+        for _ in range(6):
+            got = rt.evaluate_computation(comp, args)
+            for k in want:
+                assert np.array_equal(np.asarray(got[k]), np.asarray(want[k])), k
+    assert any("stream graphs disabled" in str(w.message) for w in caught)
+    (_, tapes), = rt._party_tapes.values()
+    assert tapes.validated is True and tapes._party_graphs is None and calls["n"] == 3
+    print("fallback: per-action after the injected loss")
+
+
 if __name__ == "__main__":
-    {"flag": flag_case, "replay": replay_case}[sys.argv[1]]()
+    {"flag": flag_case, "replay": replay_case, "fault": fault_case,
+     "fallback": fallback_case}[sys.argv[1]]()

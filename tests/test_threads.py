@@ -319,63 +319,23 @@ def _streams_child(case):
 
 
 @pytest.mark.gpu
-def test_party_streams_validation_catches_a_corrupted_landing_buffer(monkeypatch):
+def test_party_streams_validation_catches_a_corrupted_landing_buffer():
     """MOOSEX_FAULT=party_landing: the first message's push writes a scratch buffer, so its
     receiver reads a stale landing buffer.  The capture-time validation (the per-party
-    graphs against the per-action replay of the same tapes and keys) must catch it: the
-    runtime records the failure and keeps the per-action replay, whose values stay bitwise
-    equal to eager."""
-    monkeypatch.setenv("MOOSEX_PARTY_STREAMS", "1")
-    monkeypatch.setenv("MOOSEX_FAULT", "party_landing")
-    comp = _comp(False)
-    args = _args()
-    devs = {i: "cuda:0" for i in IDS}
-    want = LocalMooseRuntime(IDS, device_map=devs, seed=11, use_graphs=False
-                             ).evaluate_computation(comp, args)
-    rt = LocalMooseRuntime(IDS, device_map=devs, seed=11, use_graphs=True)
-    with pytest.warns(RuntimeWarning, match="failed validation"):
-        for _ in range(4):
-            got = rt.evaluate_computation(comp, args)
-            for k in want:
-                assert np.array_equal(np.asarray(got[k]), np.asarray(want[k])), k
-    (_, tapes), = rt._party_tapes.values()
-    assert tapes.validated is False and tapes.replay_form == "per_action"
-    assert rt.last_replay["form"] == "per_action" and "validation" in rt.last_replay["fallback"]
-    assert tapes.tapes[0].replays == 2
+    graphs against the per-action replay of the same tapes and keys) catches the wrong
+    values, records the failure and keeps the per-action replay, bitwise equal to eager
+    (tests/gpu_streams_child.py fault: streams on queues of their own, so the flags all
+    arrive and only the values can give it away)."""
+    _streams_child("fault")
 
 
 @pytest.mark.gpu
-def test_party_streams_fall_back_to_per_action_replay(monkeypatch):
-    """A per-party stream replay that reports a lost message (TransportError) is redone --
-    and every later replay runs -- with the per-action replay of the same tapes (captured
-    with their hipGraphs kept), still bitwise equal to eager."""
-    from moose_amd.parallel import threads as T
-    from moose_amd.parallel.transport import TransportError
-
-    monkeypatch.setenv("MOOSEX_PARTY_STREAMS", "1")
-    comp = _comp(False)
-    args = _args()
-    devs = {i: "cuda:0" for i in IDS}
-    want = LocalMooseRuntime(IDS, device_map=devs, seed=11, use_graphs=False
-                             ).evaluate_computation(comp, args)
-    calls = {"n": 0}
-    orig = T.PartyTapes._replay_streams
-
-    def flaky(self, arguments):
-        calls["n"] += 1
-        if calls["n"] == 2:
-            raise TransportError("injected: a message never arrived")
-        return orig(self, arguments)
-
-    monkeypatch.setattr(T.PartyTapes, "_replay_streams", flaky)
-    rt = LocalMooseRuntime(IDS, device_map=devs, seed=11, use_graphs=True)
-    with pytest.warns(RuntimeWarning, match="stream graphs disabled"):
-        for _ in range(5):
-            got = rt.evaluate_computation(comp, args)
-            for k in want:
-                assert np.array_equal(np.asarray(got[k]), np.asarray(want[k])), k
-    (_, tapes), = rt._party_tapes.values()
-    assert tapes._party_graphs is None and calls["n"] == 2
+def test_party_streams_fall_back_to_per_action_replay():
+    """A per-party stream replay that reports a lost message (TransportError) after the
+    capture-time validation passed is redone -- and every later replay runs -- with the
+    per-action replay of the same tapes, still bitwise equal to eager
+    (tests/gpu_streams_child.py fallback)."""
+    _streams_child("fallback")
 
 
 def test_shared_constant_caches_first_in_wins():

@@ -135,8 +135,9 @@ def test_persistent_workers_serve_many_evaluations():
 
 def test_spmd_load_with_changing_stored_shape():
     """A computation that Loads from worker storage runs twice on the same workers with a
-    stored value of a different shape the second time (message plans would replay the
-    first shape's headers)."""
+    stored value of a different shape the second time, and back (message plans would replay
+    the first shape's headers).  The plans are keyed on the collective
+    storage key (spmd_graphs.storage_key), so each shape replays its own plan."""
     alice, bob, carole = (pm.host_placement(n) for n in IDS)
     rep = pm.replicated_placement("rep", players=[alice, bob, carole])
 
@@ -151,7 +152,7 @@ def test_spmd_load_with_changing_stored_shape():
             return pm.cast(y, dtype=pm.float64)
 
     with DistributedMooseRuntime(IDS, backend="gloo", timeout=180) as rt:
-        for shape in ((3,), (2, 5)):
+        for shape in ((3,), (2, 5), (3,), (3,), (2, 5)):
             x = np.arange(np.prod(shape), dtype=np.float64).reshape(shape) / 4
             rt.write_value_to_storage("alice", "x", x)
             out = rt.evaluate_computation(g, {})
