@@ -1,0 +1,276 @@
+"""Round-5 per-party kernels pinned GPU == CPU directly (VERDICT r5 "what's weak" 7).
+
+tests/test_party_jobs.py and test_party_bits.py compare these kernels with the generic
+protocol steps they replace on the SAME device; here each kernel's device form is compared
+bitwise with its host form (csrc/*_cpu.cpp) on identical inputs and key slots -- as
+tests/test_native_gpu.py does for the older kernels -- so a bug shared by a fused kernel and
+a generic GPU helper (PRF slot staging, chunk walking) cannot hide.  Sizes cover the latency
+forms (a block per keystream chunk group) and the throughput forms (a thread per ChaCha
+block), both ring widths:
+
+* rss_jobs.hip  k_jobs_r0 / k_jobs_r0_lat (+ the pending-sums form), k_jobs_r1 / _lat,
+  k_jobs_r2 -- every role, jobs with cross terms, additive terms, strides and scalings;
+* rss_bits_party.hip  k_front, k_b2a (phases 0 / 1 / 2) and k_b2a_tp, with the sign-plane
+  XOR and the three-block range rows;
+* wsum_pair.hip  k_wsum_pair and the group form k_wsum_pair_g;
+* ring_hip.hip  k_mul_add2 (mul_leading_add2);
+* party_graph.hip  k_copy_many (composed replays' batched copies) and k_push / k_wait
+  (payloads of several sizes and alignments through per-party graphs).
+"""
+import ctypes
+
+import pytest
+import torch
+
+from moose_amd.ops import native as nat
+from moose_amd.ops import ring as R
+from moose_amd.runtime.keys import KeyTable
+
+pytestmark = pytest.mark.gpu
+
+KEYS = [bytes(range(16)), bytes(range(16, 32)), bytes(range(32, 48))]
+NONCES = (101, 102, 103, 104, 105, 106, 107)
+
+
+def _rand(shape, bits, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randint(-(2**63), 2**63 - 1, tuple(shape) + ((2,) if bits == 128 else ()),
+                         generator=g, dtype=torch.int64)
+
+
+def _slots(dev):
+    kt = KeyTable(dev, capacity=4)
+    kt._write(0, KEYS)
+    return kt, [[kt.ptr(r), kt.ptr((r + 1) % 3)] for r in range(3)]
+
+
+def _to(t, dev):
+    return None if t is None else t.to(dev)
+
+
+def _eq(a, b, what):
+    if a is None or b is None:
+        assert a is None and b is None, what
+        return
+    assert torch.equal(a.cpu(), b.cpu()), what
+
+
+def _jobs_for(dev, bits, rows, L, seed):
+    """Three jobs of one call: a cross product with row strides, an additive share with a
+    scale, and cross + two additive terms; their outputs are fresh zero rows."""
+    n = rows * L
+    t = lambda s, r=rows: _rand((r * L,), bits, seed + s).to(dev)  # noqa: E731
+    out = lambda: torch.zeros(n * (2 if bits == 128 else 1), dtype=torch.int64,  # noqa: E731
+                              device=dev).reshape((n,) + ((2,) if bits == 128 else ()))
+    j1 = R.MulJob(rows, out(), out(), x=(t(1), t(2)), y=(t(3, 1), t(4, 1)), sx=L, sy=0)
+    j2 = R.MulJob(rows, out(), out(), a=t(5), sa=L, ca=3)
+    j3 = R.MulJob(rows, out(), out(), x=(t(6), t(7)), y=(t(8), t(9)), sx=L, sy=L, cb=5,
+                  a=t(10), sa=L, ca=-2, a2=t(11), sa2=L, ca2=7)
+    return [j1, j2, j3]
+
+
+def _jobs_protocol(dev, bits, rows, L, m, pend):
+    """The three roles' r0 / r1 / r2 kernels on ``dev`` with the real messages between them
+    (and, with ``pend``, round 0 reading through a previous level's pending sums)."""
+    kt, slots = _slots(dev)
+    jobs = [_jobs_for(dev, bits, rows, L, 10 * r) for r in range(3)]
+    outs = []
+    pends = [None] * 3
+    if pend:
+        n = rows * L
+        for r in range(2):  # P0 / P1 rows of job 0's operand x0 are a pending o = a + b
+            o = jobs[r][0].x0
+            a, b = _rand((n,), bits, 70 + r).to(dev), _rand((n,), bits, 80 + r).to(dev)
+            pends[r] = [(o, a, b)]
+    r0 = [R.jobs_r0(jobs[r], L, bits, m, r, slots[r], NONCES, jobs[r][0].o0, pend=pends[r])
+          for r in range(3)]
+    msg = [x[0] for x in r0]
+    rt, rm = r0[2][1], r0[2][2]
+    w0 = R.jobs_r1(jobs[0], L, bits, m, 0, slots[0], NONCES, msg[0], msg[1], msg[2], None, None)
+    w1 = R.jobs_r1(jobs[1], L, bits, m, 1, slots[1], NONCES, msg[1], msg[0], msg[2], rt, rm)
+    R.jobs_r2(jobs[0], L, bits, 0, w0, w1)
+    R.jobs_r2(jobs[1], L, bits, 1, w1, w0)
+    for r in range(3):
+        outs += [msg[r]] + [t for j in jobs[r] for t in (j.o0, j.o1, j.x0)]
+    outs += [rt, rm, w0, w1]
+    if dev != "cpu":
+        torch.cuda.synchronize()
+    del kt
+    return outs
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+@pytest.mark.parametrize("rows,L", [(3, 37), (3, 6400)])
+@pytest.mark.parametrize("pend", [False, True])
+def test_jobs_kernels_gpu_equal_cpu(bits, rows, L, pend):
+    """k_jobs_r0(_lat / pending-sums form), k_jobs_r1(_lat), k_jobs_r2: GPU == CPU."""
+    cpu = _jobs_protocol("cpu", bits, rows, L, 23, pend)
+    dev = _jobs_protocol("cuda", bits, rows, L, 23, pend)
+    for k, (a, b) in enumerate(zip(cpu, dev)):
+        _eq(a, b, k)
+
+
+def _bits_run(dev, bits, n, count, xbit, blocks, with_g):
+    kt, slots = _slots(dev)
+    res = []
+    for role in range(3):
+        xa, xb = _rand((n,), bits, 1 + role).to(dev), _rand((n,), bits, 4 + role).to(dev)
+        a1 = _rand((n,), bits, 9).to(dev) if role == 1 else None
+        res += list(R.bits_front(role, xa, xb, a1, bits, slots[role], 31, 32))
+        src = [_rand((n * blocks,), bits, 20 + 6 * role + i).to(dev) for i in range(6)]
+        if not with_g:
+            src[2:] = [None] * 4
+        arecv = _rand((count, n) if blocks == 1 else (count, n), bits, 40).to(dev)
+        phase = 0 if role == 0 else 1
+        st = R.bits_b2a(phase, role, src, 5, count, bits, slots[role], 33, 34,
+                        arecv=None if role == 0 else arecv.reshape(
+                            (count, n) + ((2,) if bits == 128 else ())),
+                        xbit=xbit, blocks=blocks)
+        res += list(st)
+        z2 = _rand((count, n), bits, 50 + role).to(dev)
+        res += list(R.bits_b2a(2, role, None, 5, count, bits, slots[role], 33, 34, arecv=z2,
+                               state=st, xbit=xbit, blocks=blocks))
+    if dev != "cpu":
+        torch.cuda.synchronize()
+    del kt
+    return res
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+@pytest.mark.parametrize("n,count", [(37, 3), (700, 8)])
+@pytest.mark.parametrize("form", ["planes", "xor_sign", "blocks3", "sums"])
+def test_bits_party_kernels_gpu_equal_cpu(bits, n, count, form):
+    """k_front and the B2A phases (k_b2a, and k_b2a_tp at >= 2048 chunks) for every role:
+    plain planes, planes XORed with a sign plane, the three-block range rows, and a source
+    given as sum words (no raw adder state): GPU == CPU."""
+    xbit, blocks, with_g = {"planes": (-1, 1, True), "xor_sign": (60, 1, True),
+                            "blocks3": (60, 3, True), "sums": (-1, 1, False)}[form]
+    cnt = count + (blocks if xbit >= 0 else 0)
+    cpu = _bits_run("cpu", bits, n, cnt, xbit, blocks, with_g)
+    dev = _bits_run("cuda", bits, n, cnt, xbit, blocks, with_g)
+    for k, (a, b) in enumerate(zip(cpu, dev)):
+        _eq(a, b, k)
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+@pytest.mark.parametrize("nrows,L", [(4, 37), (24, 300), (4, 9000)])
+def test_wsum_pair_gpu_equal_cpu(bits, nrows, L):
+    """k_wsum_pair (one thread per element) and k_wsum_pair_g (groups of rows, >= 16 rows):
+    weighted rows + a scaled x, three public blocks on slot 0, the second output."""
+    weights = [(-1) ** k * (k * 7919 + 3) << (k % 5) for k in range(nrows)]
+    res = {}
+    for dev in ("cpu", "cuda"):
+        rows = [_rand((nrows * L,), bits, 60 + c).to(dev) for c in range(2)]
+        x = [_rand((L,), bits, 62 + c).to(dev) for c in range(2)]
+        out = R.wsum_pair(bits, L, rows=rows, weights=weights, x=x, wx=-12345,
+                          pub=(True, False), cblk=(0, -(1 << 50), 1 << 50),
+                          second=(-2, 1 << 41))
+        out2 = R.wsum_pair(bits, L, rows=rows, weights=weights[:2], pub=(False, True),
+                           like=rows[0]) if nrows >= 2 else ()
+        if dev != "cpu":
+            torch.cuda.synchronize()
+        res[dev] = list(out) + list(out2)
+    for k, (a, b) in enumerate(zip(res["cpu"], res["cuda"])):
+        _eq(a, b, k)
+
+
+@pytest.mark.parametrize("bits", [64, 128])
+@pytest.mark.parametrize("flags", [(True, False), (False, True), (False, False)])
+def test_mul_add2_gpu_equal_cpu(bits, flags):
+    """k_mul_add2 (mul_leading_add2): both components scaled along the leading axis plus a
+    public scalar on the flagged ones: GPU == CPU."""
+    res = {}
+    for dev in ("cpu", "cuda"):
+        a0 = R.RT(_rand((8, 33), bits, 1).to(dev), bits)
+        a1 = R.RT(_rand((8, 33), bits, 2).to(dev), bits)
+        c = R.RT(_rand((8,), bits, 3).to(dev), bits)
+        cadd = R.RT(_rand((), bits, 4).to(dev), bits)
+        r = R.mul_leading_add2(a0, a1, c, cadd, *flags)
+        assert r is not None
+        res[dev] = [t.data.cpu() for t in r]
+    for a, b in zip(res["cpu"], res["cuda"]):
+        assert torch.equal(a, b)
+
+
+def test_copy_many_batch_copies_every_message():
+    """k_copy_many inside a composed graph (graph_compose.hip node kind 2): several messages
+    of different sizes and alignments (16-byte vector path and byte path, several 4 KiB
+    pieces) land byte-exact."""
+    dev = torch.device("cuda:0")
+    sizes = [8, 4096, 4104, 20000 + 3, 1 << 16]
+    srcs = [torch.randint(0, 255, (n + 3,), dtype=torch.uint8, device=dev) for n in sizes]
+    dsts = [torch.zeros(n + 3, dtype=torch.uint8, device=dev) for n in sizes]
+    offs = [0, 0, 1, 3, 0]  # byte offsets: misaligned sources / destinations take the byte path
+    desc = []
+    for s, d, n, o in zip(srcs, dsts, sizes, offs):
+        desc += [s.data_ptr() + o, d.data_ptr() + (o + 1 if o else 0), n]
+    table = torch.tensor([v - (1 << 64) if v >= (1 << 63) else v for v in desc],
+                         dtype=torch.int64, device=dev)
+    arr = lambda ty, xs: (ty * len(xs))(*xs)  # noqa: E731
+    g, ex = ctypes.c_void_p(), ctypes.c_void_p()
+    rc = nat.lib().mx_graph_compose(
+        1, arr(ctypes.c_int, [2]), arr(ctypes.c_void_p, [len(sizes)]),
+        arr(ctypes.c_void_p, [table.data_ptr()]), arr(ctypes.c_void_p, [0]),
+        arr(ctypes.c_int64, [max(sizes)]), arr(ctypes.c_int, [0, 0]), arr(ctypes.c_int, [0]),
+        ctypes.byref(g), ctypes.byref(ex))
+    assert rc == 0, rc
+    try:
+        s = torch.cuda.current_stream(dev)
+        nat.check(nat.lib().mx_graph_launch(ex, s.cuda_stream), "launch")
+        torch.cuda.synchronize()
+    finally:
+        nat.lib().mx_graph_free(g, ex)
+    for s, d, n, o in zip(srcs, dsts, sizes, offs):
+        do = o + 1 if o else 0
+        assert torch.equal(d[do:do + n].cpu(), s[o:o + n].cpu()), n
+
+
+def test_push_payloads_of_several_sizes():
+    """k_push of one round with several messages (sizes across 4 KiB pieces, a misaligned
+    one) into uncached landing buffers, then k_wait on all their flags in another graph on
+    the same stream (ordered: no concurrency needed): every payload byte-exact, every flag
+    at the replay number, over 3 replays."""
+    dev = torch.device("cuda:0")
+    sizes = [16, 4096, 12288 + 5, 100000]
+    srcs = [torch.randint(0, 255, (n,), dtype=torch.uint8, device=dev) for n in sizes]
+    lands = [nat.uncached_zeros((n,), torch.uint8, dev) for n in sizes]
+    flags = nat.uncached_zeros((len(sizes),), torch.int32, dev)
+    pieces = torch.zeros(len(sizes), dtype=torch.int32, device=dev)
+    ep_a = torch.zeros(1, dtype=torch.int64, device=dev)
+    ep_b = torch.zeros(1, dtype=torch.int64, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    rows = []
+    for j, (s, d, n) in enumerate(zip(srcs, lands, sizes)):
+        rows += [s.data_ptr(), d.data_ptr(), n, flags.data_ptr() + 4 * j, pieces.data_ptr() + 4 * j]
+    table = torch.tensor(rows, dtype=torch.int64, device=dev)
+
+    def chain(kinds, p0, p1, p2, i0, i64):
+        k = len(kinds)
+        arr = lambda ty, xs: (ty * k)(*xs)  # noqa: E731
+        g, ex = ctypes.c_void_p(), ctypes.c_void_p()
+        rc = nat.lib().mx_graph_build_chain(
+            k, arr(ctypes.c_int, kinds), arr(ctypes.c_void_p, [0] * k), arr(ctypes.c_void_p, p0),
+            arr(ctypes.c_void_p, p1), arr(ctypes.c_void_p, p2), arr(ctypes.c_int, i0),
+            arr(ctypes.c_int64, i64), ctypes.byref(g), ctypes.byref(ex))
+        assert rc == 0, rc
+        return g, ex
+
+    A = chain([5, 6], [ep_a.data_ptr(), table.data_ptr()], [0, ep_a.data_ptr()], [0, 0],
+              [0, len(sizes)], [0, max(sizes)])
+    B = chain([5, 7], [ep_b.data_ptr(), flags.data_ptr()], [0, ep_b.data_ptr()],
+              [0, err.data_ptr()], [0, len(sizes)], [0, 0])
+    s = torch.cuda.current_stream(dev)
+    try:
+        for r in range(1, 4):
+            for t in srcs:
+                t.random_(0, 255)
+            nat.check(nat.lib().mx_graph_launch(A[1], s.cuda_stream), "A")
+            nat.check(nat.lib().mx_graph_launch(B[1], s.cuda_stream), "B")
+            torch.cuda.synchronize()
+            assert int(err.item()) == 0
+            assert flags.cpu().tolist() == [r] * len(sizes)
+            for t, d in zip(srcs, lands):
+                assert torch.equal(t.cpu(), d.cpu())
+    finally:
+        for g, ex in (A, B):
+            nat.lib().mx_graph_free(g, ex)
