@@ -198,8 +198,8 @@ def test_copy_many_batch_copies_every_message():
     pieces) land byte-exact."""
     dev = torch.device("cuda:0")
     sizes = [8, 4096, 4104, 20000 + 3, 1 << 16]
-    srcs = [torch.randint(0, 255, (n + 3,), dtype=torch.uint8, device=dev) for n in sizes]
-    dsts = [torch.zeros(n + 3, dtype=torch.uint8, device=dev) for n in sizes]
+    srcs = [torch.randint(0, 255, (n + 8,), dtype=torch.uint8, device=dev) for n in sizes]
+    dsts = [torch.zeros(n + 8, dtype=torch.uint8, device=dev) for n in sizes]
     offs = [0, 0, 1, 3, 0]  # byte offsets: misaligned sources / destinations take the byte path
     desc = []
     for s, d, n, o in zip(srcs, dsts, sizes, offs):

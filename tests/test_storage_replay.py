@@ -128,7 +128,7 @@ def test_linreg_example_replays_bitwise_equal_eager(device, kind):
     -- also across a stored shape change (re-captured) and back."""
     eager = _mk(kind, device, False)
     rt = _mk(kind, device, True)
-    for n, seed in ((10, 1), (10, 2), (10, 3), (12, 4), (12, 5), (10, 6)):
+    for n, seed in ((10, 1), (10, 2), (10, 3), (12, 4), (12, 5), (12, 6), (10, 7)):
         want = _run_linreg(eager, None, n, seed)
         got = _run_linreg(rt, None, n, seed)
         for a, b in zip(got, want):
