@@ -154,8 +154,15 @@ def dot_many(sess, pairs, f=None):
     x0 = pairs[0][0]
     X = _stack_operands(sess, [x for x, _ in pairs])
     Y = _stack_operands(sess, [y for _, y in pairs])
-    Z = rep.dot(sess, X.t, Y.t, nbatch=1)
-    T = _with(x0, rep.trunc_pr(sess, Z, f if f is not None else x0.frac))
+    m = f if f is not None else x0.frac
+    if getattr(sess, "party_dot_trunc", None) is not None and not getattr(
+            sess, "is_simulated", True):
+        # one party per process / thread: the batched GEMM, then ONE dot tail (zero share
+        # + reshare folded into TruncPr: 2 rounds) for all k products
+        T = _with(x0, rep.dot_trunc(sess, X.t, Y.t, m, nbatch=1))
+    else:
+        Z = rep.dot(sess, X.t, Y.t, nbatch=1)
+        T = _with(x0, rep.trunc_pr(sess, Z, m))
     return [local(sess, T, "IndexAxis", axis=0, index=i) for i in range(len(pairs))]
 
 

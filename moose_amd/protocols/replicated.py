@@ -754,8 +754,9 @@ def _rows(pv: PV, r0: int, r1: int) -> PV:
     return PV(pv.plc, R.RT(v.data[:, r0:r1], v.bits))
 
 
-def dot_trunc(sess, x: RepTensor, y: RepTensor, m: int) -> RepTensor:
-    """trunc_pr(dot(x, y), m) -- the fixed-point matrix product.
+def dot_trunc(sess, x: RepTensor, y: RepTensor, m: int, nbatch: int = 0) -> RepTensor:
+    """trunc_pr(dot(x, y), m) -- the fixed-point matrix product.  ``nbatch`` leading axes of
+    x and y index independent products (one batched GEMM, one tail).
 
     Sessions whose reshares cross GPUs set ``pipeline_chunks`` > 1: the product of 2-D
     operands then runs as a row-chunked pipeline.  The GEMM of row chunk c+1 runs on the
@@ -767,6 +768,15 @@ def dot_trunc(sess, x: RepTensor, y: RepTensor, m: int) -> RepTensor:
     once (p_prepare_cross) and x row blocks are read in place."""
     chunks = getattr(sess, "pipeline_chunks", 1)
     nchunk = 1
+    if nbatch:
+        if not (getattr(sess, "party_dot_trunc", None) is not None and m and 0 < m <= 63
+                and x.kind == "arith" and x.bits in (64, 128)):
+            return trunc_pr(sess, dot(sess, x, y, nbatch=nbatch), m)
+        with span("rep.dot_trunc_party"):
+            nonces = tuple(sess.nonce(x.plc) for _ in range(7))
+            v = sess.p_dot_cross(x.plc, x.s0, x.s1, y.s0, y.s1, nbatch=nbatch)
+            s0, s1 = sess.party_dot_trunc(x.plc, v, m, nonces)
+            return RepTensor(x.plc, x.bits, "arith", s0, s1)
     if chunks > 1:
         xs, ys = x.s0.v.shape, y.s0.v.shape  # stacked: (3, M, K), (3, K, N)
         if len(xs) == 3 and len(ys) == 3:

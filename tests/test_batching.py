@@ -50,3 +50,51 @@ def test_independent_dots_batched(monkeypatch):
     out2 = np.asarray(next(iter(rt.evaluate_computation(_comp(4), {"x": x, "y": y}).values())))
     assert calls == []
     np.testing.assert_allclose(out, out2, atol=1e-4)
+
+
+def _distinct_dots(k):
+    alice, bob, carole = (pm.host_placement(n) for n in ("alice", "bob", "carole"))
+    rep = pm.replicated_placement("rep", players=[alice, bob, carole])
+    fx = pm.fixed(14, 23)
+
+    @pm.computation
+    def f(x: pm.Argument(alice, vtype=pm.TensorType(pm.float64)),
+          y: pm.Argument(bob, vtype=pm.TensorType(pm.float64))):
+        with alice:
+            xs = [pm.cast(pm.mul(x, pm.constant(np.array([float(i + 1)]))), dtype=fx)
+                  for i in range(k)]
+        with bob:
+            yf = pm.cast(y, dtype=fx)
+        with rep:
+            z = pm.add_n([pm.dot(xi, yf) for xi in xs])
+        with carole:
+            return pm.cast(z, dtype=pm.float64)
+
+    return f
+
+
+def test_independent_dots_batched_on_per_party_sessions():
+    """Parties as threads (one per-party SPMD session each): k independent Dots of distinct
+    operands (6x5 . 5x3) run as ONE batched product and ONE dot tail -- the rounds of one
+    product instead of k (BASELINE's "parallel" dot benchmark) -- with the plaintext
+    values; MOOSEX_BATCH_DOTS=0 gives k times the rounds."""
+    import os
+
+    from moose_amd.runtime.local import LocalMooseRuntime
+
+    ids = ["alice", "bob", "carole"]
+    rng = np.random.default_rng(1)
+    x, y = rng.uniform(-2, 2, (6, 5)), rng.uniform(-2, 2, (5, 3))
+    want = sum((i + 1) * x for i in range(4)) @ y
+    rounds = {}
+    for flag in ("1", "0"):
+        os.environ["MOOSEX_BATCH_DOTS"] = flag
+        try:
+            rt = LocalMooseRuntime(ids, device_map={i: "cpu" for i in ids}, seed=2)
+            got = np.asarray(list(rt.evaluate_computation(_distinct_dots(4),
+                                                          {"x": x, "y": y}).values())[0])
+        finally:
+            os.environ.pop("MOOSEX_BATCH_DOTS", None)
+        np.testing.assert_allclose(got, want, atol=1e-4)
+        rounds[flag] = rt.last_stats.rounds
+    assert rounds["0"] >= rounds["1"] + 6, rounds  # 4 tails of 2 rounds -> one
