@@ -12,6 +12,11 @@
 // concurrently inside it -- the dataflow the host-side interleaving only approximated.
 #include <hip/hip_runtime.h>
 
+#include <execinfo.h>
+#include <pthread.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -19,6 +24,55 @@
 #include <vector>
 
 namespace {
+
+// MOOSEX_FLAT_DEBUG: a SIGSEGV / SIGBUS handler on an alternate stack prints where the
+// builder was (segment, node, kernel), the fault address, this thread's stack range and a
+// native backtrace, then re-raises (the evidence of profiles/r6_graph_flatten_segfault.md).
+volatile int g_dbg_seg = -1, g_dbg_node = -1, g_dbg_added = 0;
+void* volatile g_dbg_func = nullptr;
+char* volatile g_stack_lo = nullptr;
+char* volatile g_stack_hi = nullptr;
+
+void fault_handler(int sig, siginfo_t* si, void*) {
+  char buf[512];
+  const int n = snprintf(buf, sizeof buf,
+                         "graph build fault: signal %d at %p; segment %d node %d (%d nodes "
+                         "added) func %p; builder stack [%p, %p)\n",
+                         sig, si->si_addr, g_dbg_seg, g_dbg_node, g_dbg_added, g_dbg_func,
+                         (void*)g_stack_lo, (void*)g_stack_hi);
+  if (n > 0) (void)!write(2, buf, (size_t)n);
+  void* bt[64];
+  const int k = backtrace(bt, 64);
+  backtrace_symbols_fd(bt, k, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
+void install_fault_handler() {
+  if (std::getenv("MOOSEX_FLAT_DEBUG") == nullptr) return;
+  static thread_local char* alt = nullptr;
+  if (alt == nullptr) {
+    alt = (char*)malloc(1 << 16);
+    stack_t ss = {};
+    ss.ss_sp = alt;
+    ss.ss_size = 1 << 16;
+    sigaltstack(&ss, nullptr);
+  }
+  struct sigaction sa = {};
+  sa.sa_sigaction = fault_handler;
+  sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+  sigaction(SIGSEGV, &sa, nullptr);
+  sigaction(SIGBUS, &sa, nullptr);
+  pthread_attr_t at;
+  if (pthread_getattr_np(pthread_self(), &at) == 0) {
+    void* lo = nullptr;
+    size_t sz = 0;
+    pthread_attr_getstack(&at, &lo, &sz);
+    g_stack_lo = (char*)lo;
+    g_stack_hi = (char*)lo + sz;
+    pthread_attr_destroy(&at);
+  }
+}
 
 // Segments flattened into the composed / chained graphs (default; MOOSEX_PARTY_GRAPH_FLAT=0:
 // child-graph nodes).  Measured on one MI355X (LR parties, composed graph): a child-graph
@@ -31,34 +85,18 @@ bool flat_on() {
   return on;
 }
 
-constexpr int kFlatMaxSegments = 256;
-
-// Segments with copy / memset nodes too (MOOSEX_PARTY_GRAPH_FLAT=all); by default only
-// segments of kernel (and empty) nodes are flattened -- a large composed graph whose
-// segments held other node types crashed the runtime while their copies were added.
-bool flat_all() {
-  static const bool on = [] {
-    const char* e = std::getenv("MOOSEX_PARTY_GRAPH_FLAT");
-    return e && e[0] == 'a';
+// composed / chained graphs with more segments than this keep child-graph nodes
+// (MOOSEX_FLAT_MAX_SEGMENTS; 0 = no limit, the default: the round-5 cap of 256 guarded
+// against the crash of flattening captured copies, which are no longer flattened)
+int flat_max_segments() {
+  static const int v = [] {
+    const char* e = std::getenv("MOOSEX_FLAT_MAX_SEGMENTS");
+    return e ? std::atoi(e) : 0;
   }();
-  return on;
+  return v;
 }
 
-// A captured copy's node in another graph: its 3-D parameters as read back, or (when the
-// runtime does not take those back) the equivalent 1-D copy.
-hipError_t add_copy(hipGraphNode_t* out, hipGraph_t g, const hipGraphNode_t* deps, size_t nd,
-                    const hipMemcpy3DParms& mp) {
-  if (hipGraphAddMemcpyNode(out, g, deps, nd, &mp) == hipSuccess) return hipSuccess;
-  (void)hipGetLastError();
-  if (mp.srcArray != nullptr || mp.dstArray != nullptr || mp.extent.height > 1 ||
-      mp.extent.depth > 1)
-    return hipErrorInvalidValue;
-  char* dst = (char*)mp.dstPtr.ptr + mp.dstPos.x;
-  const char* src = (const char*)mp.srcPtr.ptr + mp.srcPos.x;
-  return hipGraphAddMemcpyNode1D(out, g, deps, nd, dst, src, mp.extent.width, mp.kind);
-}
-
-// Copy the nodes of a captured segment (kernel / memcpy / memset / empty nodes) into the
+// Copy the nodes of a captured segment (kernel and empty nodes) into the
 // parent graph instead of adding it as a child-graph node: the instantiated executable then
 // holds one flat list of packets (no nested graph per segment).  ``deps``: what the
 // segment's roots wait for; ``leaves``: its last nodes, for the next node to wait for.
@@ -74,10 +112,9 @@ int flatten_into(hipGraph_t g, hipGraph_t child, const std::vector<hipGraphNode_
   if (hipGraphGetEdges(child, nullptr, nullptr, &ne) != hipSuccess) return 1;
   std::vector<hipGraphNode_t> from(ne), to(ne);
   if (ne && hipGraphGetEdges(child, from.data(), to.data(), &ne) != hipSuccess) return 1;
-  // every node's type and parameters read before anything is added (a node whose
-  // parameters cannot be read back -- e.g. some captured copies -- keeps the segment whole)
-  // (parameters are read again right before each node is added: what a GetParams call
-  // returns may point into storage that the next call reuses)
+  // every node's type and parameters read before anything is added (a node that cannot be
+  // re-created keeps the segment whole); parameters are read again right before each node
+  // is added: what a GetParams call returns may point into storage the next call reuses
   std::vector<hipGraphNodeType> types(n);
   for (size_t i = 0; i < n; ++i) {
     hipGraphNodeType& t = types[i];
@@ -88,25 +125,12 @@ int flatten_into(hipGraph_t g, hipGraph_t child, const std::vector<hipGraphNode_
       // arguments the runtime does not hand back (neither an argument array nor a packed
       // buffer): the node cannot be re-created -- keep the segment whole
       if (kp.func == nullptr || (kp.kernelParams == nullptr && kp.extra == nullptr)) return 1;
-    } else if (!flat_all() && t != hipGraphNodeTypeEmpty) {
-      return 1;  // (a child-graph node keeps the segment whole)
-    } else if (t == hipGraphNodeTypeMemcpy) {
-      hipMemcpy3DParms mp;
-      if (hipGraphMemcpyNodeGetParams(nodes[i], &mp) != hipSuccess) return 1;
-      // can it be re-added?  Tried once in a scratch graph, before touching g
-      hipGraph_t scratch = nullptr;
-      if (hipGraphCreate(&scratch, 0) != hipSuccess) return 1;
-      hipGraphNode_t tmp = nullptr;
-      const bool ok = add_copy(&tmp, scratch, nullptr, 0, mp) == hipSuccess;
-      hipGraphDestroy(scratch);
-      if (!ok) {
-        (void)hipGetLastError();
-        return 1;
-      }
-    } else if (t == hipGraphNodeTypeMemset) {
-      hipMemsetParams ms;
-      if (hipGraphMemsetNodeGetParams(nodes[i], &ms) != hipSuccess) return 1;
     } else if (t != hipGraphNodeTypeEmpty) {
+      // copies, memsets, child graphs: the segment stays a child-graph node.  What
+      // hipGraphMemcpyNodeGetParams reads back from a copy captured off a stream is not
+      // its parameters on this runtime (kind, extent and pointers are uninitialised
+      // memory), so such a node cannot be re-created -- the round-5 crash of
+      // MOOSEX_PARTY_GRAPH_FLAT=all (profiles/r6_graph_flatten_segfault.md)
       return 1;
     }
   }
@@ -135,6 +159,8 @@ int flatten_into(hipGraph_t g, hipGraph_t child, const std::vector<hipGraphNode_
   std::vector<hipGraphNode_t> d;
   static const bool dbg = std::getenv("MOOSEX_FLAT_DEBUG") != nullptr;
   for (int v : order) {
+    g_dbg_node = v;
+    ++g_dbg_added;
     if (dbg) {
       hipKernelNodeParams k = {};
       if (types[v] == hipGraphNodeTypeKernel) hipGraphKernelNodeGetParams(nodes[v], &k);
@@ -152,15 +178,8 @@ int flatten_into(hipGraph_t g, hipGraph_t child, const std::vector<hipGraphNode_
     if (t == hipGraphNodeTypeKernel) {
       hipKernelNodeParams kp = {};
       rc = hipGraphKernelNodeGetParams(nodes[v], &kp);
+      g_dbg_func = kp.func;
       if (rc == hipSuccess) rc = hipGraphAddKernelNode(&made[v], g, d.data(), d.size(), &kp);
-    } else if (t == hipGraphNodeTypeMemcpy) {
-      hipMemcpy3DParms mp;
-      rc = hipGraphMemcpyNodeGetParams(nodes[v], &mp);
-      if (rc == hipSuccess) rc = add_copy(&made[v], g, d.data(), d.size(), mp);
-    } else if (t == hipGraphNodeTypeMemset) {
-      hipMemsetParams ms;
-      rc = hipGraphMemsetNodeGetParams(nodes[v], &ms);
-      if (rc == hipSuccess) rc = hipGraphAddMemsetNode(&made[v], g, d.data(), d.size(), &ms);
     } else {
       rc = hipGraphAddEmptyNode(&made[v], g, d.data(), d.size());
     }
@@ -186,22 +205,36 @@ int mx_copy_many_grid(int n, int64_t max_bytes, int* gx, int* gy);  // party_gra
 // table in device memory, child[i] = the number of entries, bytes[i] = the largest.  The
 // dependencies of node i are deps[dep_off[i] .. dep_off[i + 1]) (indices < i).
 // Returns 0 and the graph / its executable, or a negative code (nothing is leaked).
+static int graph_compose_impl(int n, const int* kind, void* const* child, void* const* dst,
+                              void* const* src, const int64_t* bytes, const int* dep_off,
+                              const int* deps, void** graph_out, void** exec_out);
+
 int mx_graph_compose(int n, const int* kind, void* const* child, void* const* dst,
                      void* const* src, const int64_t* bytes, const int* dep_off,
                      const int* deps, void** graph_out, void** exec_out) {
+  install_fault_handler();
+  return graph_compose_impl(n, kind, child, dst, src, bytes, dep_off, deps, graph_out,
+                            exec_out);
+}
+
+static int graph_compose_impl(int n, const int* kind, void* const* child, void* const* dst,
+                              void* const* src, const int64_t* bytes, const int* dep_off,
+                              const int* deps, void** graph_out, void** exec_out) {
   if (n < 1) return -2;
   hipGraph_t g = nullptr;
   if (hipGraphCreate(&g, 0) != hipSuccess) return -3;
   std::vector<hipGraphNode_t> nodes((size_t)n, nullptr);
   // what a later node waits for to follow node i: node i, or a flattened segment's leaves
   std::vector<std::vector<hipGraphNode_t>> exits((size_t)n);
-  // (composed graphs of up to kFlatMaxSegments segments: the larger ones -- a LogReg
-  // training run's thousands -- keep child-graph nodes until their flattening is verified)
+  // (composed graphs of up to flat_max_segments() segments; the larger ones keep
+  // child-graph nodes)
   int nseg = 0;
   for (int i = 0; i < n; ++i) nseg += kind[i] == 0;
-  const bool flat = flat_on() && (flat_all() || nseg <= kFlatMaxSegments);
+  const bool flat = flat_on() && (flat_max_segments() <= 0 || nseg <= flat_max_segments());
   std::vector<hipGraphNode_t> d;
+  g_dbg_added = 0;
   for (int i = 0; i < n; ++i) {
+    g_dbg_seg = i;
     d.clear();
     for (int e = dep_off[i]; e < dep_off[i + 1]; ++e) {
       const int j = deps[e];
@@ -258,6 +291,7 @@ int mx_graph_compose(int n, const int* kind, void* const* child, void* const* ds
     exits[(size_t)i].assign(1, nodes[(size_t)i]);
   }
   hipGraphExec_t ex = nullptr;
+  g_dbg_seg = -2;  // instantiating
   if (std::getenv("MOOSEX_FLAT_DEBUG") != nullptr) {
     size_t cnt = 0;
     hipGraphGetNodes(g, nullptr, &cnt);
@@ -284,16 +318,31 @@ void* mx_party_kernel_fn(int which);  // party_graph.hip
 // (p0 = counter); 6 = push messages (p0 = PushDesc table, i0 = entries, i64 = largest
 // message bytes, p1 = counter); 7 = wait for flags (p0 = flags, i0 = count, p1 = counter,
 // p2 = error word).
+static int graph_build_chain_impl(int n, const int* kind, void* const* child,
+                                  void* const* p0, void* const* p1, void* const* p2,
+                                  const int* i0, const int64_t* i64, void** graph_out,
+                                  void** exec_out);
+
 int mx_graph_build_chain(int n, const int* kind, void* const* child, void* const* p0,
                          void* const* p1, void* const* p2, const int* i0, const int64_t* i64,
                          void** graph_out, void** exec_out) {
+  install_fault_handler();
+  g_dbg_seg = -1;
+  return graph_build_chain_impl(n, kind, child, p0, p1, p2, i0, i64, graph_out, exec_out);
+}
+
+static int graph_build_chain_impl(int n, const int* kind, void* const* child,
+                                  void* const* p0, void* const* p1, void* const* p2,
+                                  const int* i0, const int64_t* i64, void** graph_out,
+                                  void** exec_out) {
   if (n < 1) return -2;
   hipGraph_t g = nullptr;
   if (hipGraphCreate(&g, 0) != hipSuccess) return -3;
   hipGraphNode_t prev = nullptr;
   int nseg = 0;
   for (int i = 0; i < n; ++i) nseg += kind[i] == 0;
-  const bool flat_chain = flat_on() && (flat_all() || nseg <= kFlatMaxSegments);
+  const bool flat_chain = flat_on() && (flat_max_segments() <= 0 ||
+                                        nseg <= flat_max_segments());
   for (int i = 0; i < n; ++i) {
     hipGraphNode_t node = nullptr;
     const size_t nd = prev ? 1 : 0;

@@ -316,8 +316,12 @@ class ThreadTransport:
 # a party that waits this long for a message ends the evaluation (device_map runtimes
 # without an explicit timeout); a desynchronised peer that returned is detected at once
 DEFAULT_TIMEOUT_S = float(os.environ.get("MOOSEX_PARTY_TIMEOUT", "300"))
-# segments per composed executable (a larger tape is replayed as several, back to back)
-CHUNK_SEGMENTS = int(os.environ.get("MOOSEX_PARTY_GRAPH_CHUNK", "200"))
+# segments per composed executable (0: the whole tape is ONE executable; > 0: a larger tape
+# is replayed as several, back to back).  Round 5 chunked at 200 against a crash that was
+# the flattening of captured copy nodes, not the graph's size
+# (profiles/r6_graph_flatten_segfault.md): a 100-iteration LogReg tape is one 28,512-node
+# executable
+CHUNK_SEGMENTS = int(os.environ.get("MOOSEX_PARTY_GRAPH_CHUNK", "0"))
 # per-party stream graphs: message flags and landing buffers in uncached device memory
 # (MOOSEX_PARTY_UNCACHED=0: PyTorch's allocator, coarse-grained -- probes only)
 UNCACHED_LANDING = os.environ.get("MOOSEX_PARTY_UNCACHED", "1") != "0"
@@ -616,10 +620,10 @@ class PartyTapes:
                 offs.append(table.data_ptr() + 8 * 3 * at)
                 at += len(d)
             dst = [offs[d] if k == 2 else d for k, d in zip(kinds, dst)]
-        # the total order in chunks of at most CHUNK_SEGMENTS segments, one executable each
-        # (launched back to back on one stream): every chunk is small enough for the
-        # composer to flatten its segments (csrc/graph_compose.hip kFlatMaxSegments)
-        bounds = chunk_bounds(kinds, CHUNK_SEGMENTS)
+        # the total order as one executable, or in chunks of at most CHUNK_SEGMENTS
+        # segments launched back to back on one stream
+        bounds = (chunk_bounds(kinds, CHUNK_SEGMENTS) if CHUNK_SEGMENTS > 0
+                  else [(0, len(kinds))])
         arr = lambda ty, xs: (ty * max(1, len(xs)))(*xs)  # noqa: E731
         handles = []
         for a, b in bounds:

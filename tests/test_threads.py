@@ -412,3 +412,35 @@ def test_composed_schedule_chunks_keep_order_and_bound_segments():
         assert all(sum(k == 0 for k in kinds[s:e]) <= per for s, e in b)
         assert all(kinds[s] == 0 for s, _ in b[1:])  # a new chunk starts at a segment
     assert chunk_bounds(kinds, 100) == [(0, len(kinds))]
+
+
+@pytest.mark.gpu
+def test_large_party_tape_composes_into_one_flat_executable():
+    """A 40-iteration LogReg training tape of the parties (hundreds of segments): composed
+    into ONE executable with every kernel-only segment flattened (no 200-segment chunks, no
+    256-segment cap -- the round-5 crash was the flattening of captured copy nodes,
+    profiles/r6_graph_flatten_segfault.md), and its seeded replays bitwise equal to eager."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)), "benchmarks"))
+    from logreg_train import build_training
+
+    from moose_amd.runtime.local import to_native
+
+    native = to_native(build_training(16, 40, n_features=8))
+    rng = np.random.default_rng(0)
+    args = {"x": rng.standard_normal((640, 8)), "y": rng.integers(2, size=(640, 1)) * 1.0,
+            "w_0": np.zeros((8, 1)), "b_0": np.zeros((1, 1))}
+    devs = {i: "cuda:0" for i in IDS}
+    want = LocalMooseRuntime(IDS, device_map=devs, seed=5, use_graphs=False,
+                             timeout=300).evaluate_computation(native, args)
+    rt = LocalMooseRuntime(IDS, device_map=devs, seed=5, use_graphs=True, timeout=300)
+    for _ in range(4):
+        got = rt.evaluate_computation(native, args)
+        for k in want:
+            assert np.array_equal(np.asarray(got[k]), np.asarray(want[k])), k
+    (_, tapes), = rt._party_tapes.values()
+    assert tapes is not False and tapes.replay_form == "composed"
+    assert tapes.segments > 256 and tapes.graph_nodes["executables"] == 1, tapes.graph_nodes
+    assert tapes.tapes[0].replays == 2
