@@ -328,6 +328,12 @@ UNCACHED_LANDING = os.environ.get("MOOSEX_PARTY_UNCACHED", "1") != "0"
 # per-party stream graphs are checked once at capture against the per-action replay of the
 # same tapes from the same key state (bitwise); a mismatch keeps the per-action replay
 VALIDATE_STREAMS = os.environ.get("MOOSEX_PARTY_STREAMS_VALIDATE", "1") != "0"
+# the composed one-GPU graph as a DAG (each party's nodes in program order, a message copy
+# after its sender's segment and before its receiver's next one, and the sender's next
+# segment after the copy has read its buffer) instead of one total order: the parties'
+# branches may run concurrently inside the one launch.  Needs persistent landing buffers
+# (ThreadTransport.prepare_landing; profiles/r5_party_dag_hazard.md)
+DAG_COMPOSE = os.environ.get("MOOSEX_PARTY_GRAPH_DAG", "0") == "1"
 
 
 def chunk_bounds(kinds, per: int):
@@ -473,7 +479,9 @@ class PartyTapes:
         for i, ident in enumerate(identities):
             tr = ThreadTransport(i, None, device=self.devices[i], world=n)
             tr.log = warm[ident]["log"]
-            if self.streams_mode:  # senders write landing buffers at their own pace
+            if self.streams_mode or (DAG_COMPOSE and len(set(self.devices)) == 1):
+                # senders write landing buffers at their own pace (streams), or a copy
+                # runs when its sender's branch reaches it (DAG): persistent buffers
                 with torch.cuda.device(self.devices[i]):
                     tr.prepare_landing()
             with torch.cuda.device(self.devices[i]):
@@ -580,6 +588,8 @@ class PartyTapes:
 
         from moose_amd.ops import native as nat
 
+        if DAG_COMPOSE:
+            return self._compose_dag()
         batched = os.environ.get("MOOSEX_PARTY_COPY_BATCH", "1") != "0"
         acts = self._schedule_rounds() if batched else [
             a if a[0] != "cp" else ("cpb", [(a[1], a[2], a[3], a[4])])
@@ -645,6 +655,64 @@ class PartyTapes:
         self.graph_nodes = {"segments": kinds.count(0), "copy_nodes": kinds.count(1),
                             "copy_batches": kinds.count(2), "executables": len(handles)}
         return [ex for _, ex in handles]
+
+    def _compose_dag(self):
+        """The per-action schedule as ONE graph with only the protocol's edges
+        (MOOSEX_PARTY_GRAPH_DAG=1): a party's segments and receive copies in its program
+        order, a copy after the sender's segment that produced the message, and the sender's
+        next segment after every copy that read its buffer (write-after-read).  Returns
+        [exec] or None when the runtime declines."""
+        import ctypes
+
+        from moose_amd.ops import native as nat
+
+        n = len(self.tapes)
+        kinds, child, dst, src, nbytes, deps = [], [], [], [], [], []
+        last = [None] * n
+        sent_at = {}
+        reading = [[] for _ in range(n)]
+        for a in self.actions:
+            p = a[1]
+            if a[0] == "g":
+                kinds.append(0)
+                child.append(a[2].raw_cuda_graph())
+                dst.append(0)
+                src.append(0)
+                nbytes.append(0)
+                deps.append(sorted(set(([last[p]] if last[p] is not None else []) +
+                                       reading[p])))
+                reading[p] = []
+                last[p] = len(kinds) - 1
+            elif a[0] == "rec":
+                sent_at[id(a[2])] = (last[p], p)
+            else:
+                _, p, _s, t, buf, ev = a
+                at, sender = sent_at.get(id(ev), (None, None))
+                kinds.append(1)
+                child.append(0)
+                dst.append(buf.data_ptr())
+                src.append(t.data_ptr())
+                nbytes.append(t.numel() * t.element_size())
+                deps.append(sorted(set(x for x in (last[p], at) if x is not None)))
+                last[p] = len(kinds) - 1
+                if sender is not None and sender != p:
+                    reading[sender].append(last[p])
+        off, flat = [0], []
+        for d in deps:
+            flat += d
+            off.append(len(flat))
+        arr = lambda ty, xs: (ty * max(1, len(xs)))(*xs)  # noqa: E731
+        g, ex = ctypes.c_void_p(), ctypes.c_void_p()
+        rc = nat.lib().mx_graph_compose(
+            len(kinds), arr(ctypes.c_int, kinds), arr(ctypes.c_void_p, child),
+            arr(ctypes.c_void_p, dst), arr(ctypes.c_void_p, src), arr(ctypes.c_int64, nbytes),
+            arr(ctypes.c_int, off), arr(ctypes.c_int, flat), ctypes.byref(g), ctypes.byref(ex))
+        if rc != 0:
+            return None
+        self._graph_handles = [(g, ex)]
+        self.graph_nodes = {"segments": kinds.count(0), "copy_nodes": kinds.count(1),
+                            "copy_batches": 0, "executables": 1, "dag": True}
+        return [ex]
 
     def _build_streams(self):
         """Every party's replay as ONE graph on its own stream (its own GPU when the parties
