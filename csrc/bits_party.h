@@ -94,26 +94,46 @@ MX_HD inline T sum_bit(T p, T g, T t, int q) {
 }
 
 // the bit plane of B2A row ``row``: plane start + row of element block 0.  With ``xbit`` >= 0
-// the rows before the last ``blocks`` are XORed (locally, share-wise) with plane xbit of block
-// 0 -- the planes of |x| up to one ulp -- and the last rows are sign planes (plane xbit):
-// blocks == 1: the sign of x (block 0); blocks == 3 (the adder ran over x, x - T, x + T):
-// NOT sign(x - T) = [x >= T], sign(x + T) = [x < -T], then sign(x).  ``neg``: the row is
-// the complement (boolean NOT: share component 0 flipped).
+// the rows before the last tail rows are XORed (locally, share-wise) with plane xbit of block
+// 0 -- the planes of |z| up to one ulp -- and the tail rows are sign planes.  ``blocks``
+// packs the block layout: nb = blocks & 0xff blocks concatenated along the elements, and
+// sbit = blocks >> 8 the sign plane of the tail rows (0: xbit).
+//   nb == 1: one tail row, the sign of z (block 0);
+//   nb == 3 (the adder ran over z, z - T, z + T): NOT sign(z - T) = [z >= T],
+//            sign(z + T) = [z < -T], then sign(z);
+//   nb == 2 (z, x): one tail row, sign(x) at plane sbit -- the ring's msb when sbit is the
+//            top bit, so the sign holds for every representable x, whatever bound z's
+//            planes assume;
+//   nb == 4 (z, x - T', x + T', x): [x >= T'] = NOT sign(x - T'), [x < -T'] = sign(x + T'),
+//            sign(x), all at plane sbit.
+// ``neg``: the row is the complement (boolean NOT: share component 0 flipped).
+MX_HD inline int tail_rows(int xbit, int blocks) {
+  if (xbit < 0) return 0;
+  const int nb = blocks & 0xff;
+  return (nb == 2 || nb == 4) ? nb - 1 : nb;
+}
+
 MX_HD inline void plane_of(int row, int start, int count, int xbit, int blocks, int* q, int* xq,
                            int* blk, int* neg) {
   *blk = 0;
   *neg = 0;
-  const int tail = xbit >= 0 ? blocks : 0;
+  const int nb = blocks & 0xff, sbit = blocks >> 8;
+  const int tail = tail_rows(xbit, blocks);
   if (row < count - tail) {
     *q = start + row;
     *xq = xbit;
     return;
   }
-  *q = xbit;
+  *q = sbit > 0 ? sbit : xbit;
   *xq = -1;
   const int k = row - (count - tail);  // 0 .. tail - 1
-  if (tail == 3) {
+  if (nb == 3) {
     *blk = k == 0 ? 1 : (k == 1 ? 2 : 0);
+    *neg = k == 0;
+  } else if (nb == 2) {
+    *blk = 1;
+  } else if (nb == 4) {
+    *blk = k + 1;
     *neg = k == 0;
   }
 }

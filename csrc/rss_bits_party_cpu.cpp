@@ -125,10 +125,11 @@ int mx_bits_b2a(int dev, int words, int phase, int role, int64_t S, int start, i
                 void* z, void* base0, void* base1, const void* zr, void* out0, void* out1,
                 const uint32_t* const* slots, const uint64_t* nn, void* stream) {
   if (xbit < 0) blocks = 1;
-  const int planes = xbit >= 0 ? count - blocks : count;  // rows read from start..
+  const int nb = blocks & 0xff, sbit = blocks >> 8;
+  const int planes = count - mxb::tail_rows(xbit, blocks);  // rows read from start..
   if (role < 0 || role > 2 || phase < 0 || phase > 2 || start < 0 || count < 1 ||
-      start + planes > 64 * words || xbit >= 64 * words || (blocks != 1 && blocks != 3) ||
-      (xbit >= 0 && planes < 1))
+      start + planes > 64 * words || xbit >= 64 * words || nb < 1 || nb > 4 ||
+      sbit >= 64 * words || (sbit > 0) != (nb == 2 || nb == 4) || (xbit >= 0 && planes < 1))
     return -3;
   if (dev)
     return mxh_bits_b2a(words, phase, role, S, start, count, xbit, blocks, src, arecv, msg, z,

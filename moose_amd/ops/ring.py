@@ -2221,8 +2221,9 @@ def bits_b2a(phase, role, src, start, count, bits, slots, n1, ng, arecv=None, st
             _p(b0), _p(b1), _p(arecv), _p(o0), _p(o1), _slots_arr(slots), _nonces_arr((n1, ng)),
             nat.stream_of(z)), "bits_b2a")
         return o0, o1
-    if blocks > 1:  # ``blocks`` copies concatenated on axis 0: the rows are one block's
-        per = (per[0] // blocks,) + per[1:]
+    nb = blocks & 0xff  # bits_party.h plane_of: blocks >> 8 is the tail rows' sign plane
+    if nb > 1:  # ``nb`` copies concatenated on axis 0: the rows are one block's
+        per = (per[0] // nb,) + per[1:]
     S = math.prod(per)
     shp = (count,) + per + ((2,) if bits == 128 else ())
     z, b0, b1 = (torch.empty(shp, dtype=torch.int64, device=like.device) for _ in range(3))

@@ -1254,7 +1254,6 @@ RECIP_DIRECT = os.environ.get("MOOSEX_RECIP_DIRECT", "1") != "0"
 DEFER_OUTPUT_TRUNC = os.environ.get("MOOSEX_SIGMOID_DEFER_TRUNC", "1") != "0"
 # per-party sessions take the sigmoid's sign and e^-|x| from one bit decomposition
 ONE_DECOMPOSITION = os.environ.get("MOOSEX_SIGMOID_ONE_BITDEC", "1") != "0"
-ONE_DEC_WIDTH = True  # False (tests): its adder over all bits, as the generic steps
 # ... with the integer bits whose factor underflows replaced by a range check (3 blocks)
 RANGE_SPLIT = os.environ.get("MOOSEX_EXP_RANGE_SPLIT", "1") != "0"
 
@@ -1271,8 +1270,10 @@ def _sign_and_exp_party(sess, x: RepFixed, plus: float = 0.0):
     Only the integer bits j with a factor 2^-(2^j) that does not underflow at f bits
     (2^j <= f + 2: jn of them) are factors of their own; |z| >= T = 2^(F + jn) makes e^-|x|
     < 2^-(2^jn), zero at f bits, so the bits above are replaced by [z >= T] and [z < -T]:
-    the sign planes of z - T and z + T, decomposed in the SAME adder (three blocks, same
-    rounds).  Their factors 1 - [z >= T] and 1 - [z < -T] join the tree: jn + 2 factors
+    the sign planes of x - T' and x + T' (T' = T / C), decomposed in the SAME adder (the
+    blocks z, x - T', x + T', x; same rounds).  The mirror's sign and the range flags are
+    the ring's msb of x's blocks, so they are right for every representable x, not only
+    below the type's nominal 2^integ.  Their factors 1 - [z >= T] and 1 - [z < -T] join the tree: jn + 2 factors
     (8 for fixed(24, 40)) instead of 25 -> 32, two tree levels (4 rounds) fewer.
     None when the ring has too few bits for fc >= 20 (the caller uses the three steps)."""
     if not ONE_DECOMPOSITION or getattr(sess, "is_simulated", True):
@@ -1305,21 +1306,28 @@ def _sign_and_exp_party(sess, x: RepFixed, plus: float = 0.0):
         q -= extra
     C = int(round(math.log2(math.e) * (1 << fc)))
     xt = pend.reshare_untruncated() if pend is not None else x.t
-    z = None if split else rep.lincomb(sess, [(C, xt)])
+    z = rep.lincomb(sess, [(C, xt)])
+    fx = f + (pend.m if pend is not None else 0)  # x' = xt's fractional bits
     if split:
+        # blocks z, x' - T', x' + T', x' (T' = T / C in x's units): |z|'s planes come from
+        # z (plane q its sign), but the range flags and the mirror's sign come from x' at the
+        # ring's msb -- right for every representable x, not only |x| < 2^integ (a product
+        # keeps the nominal integ while its value grows)
         Tv = 1 << (F + jn)
-        zs = _wsum(sess, None, (), x=xt, wx=C, cblk=(0, -Tv, Tv))  # the 3 blocks, 1 launch
-        if zs is None:
-            z = rep.lincomb(sess, [(C, xt)])
-            T = R.fill((), Tv, bits, sess.device)
-            zs = concat(sess, [RepFixed(z, F, integ),
-                               RepFixed(rep.sub_public(sess, z, T), F, integ),
-                               RepFixed(rep.add_public(sess, z, T), F, integ)], 0).t
+        Tx = -(-Tv // C)  # z >= T  <=>  x' >= Tx (x' an integer at fx bits)
+        xs = _wsum(sess, None, (), x=xt, wx=1, cblk=(-Tx, Tx, 0))  # 3 blocks, 1 launch
+        if xs is None:
+            T = R.fill((), Tx, bits, sess.device)
+            xs = concat(sess, [RepFixed(rep.sub_public(sess, xt, T), fx, integ),
+                               RepFixed(rep.add_public(sess, xt, T), fx, integ),
+                               RepFixed(xt, fx, integ)], 0).t
+        zs = concat(sess, [RepFixed(z, F, integ), RepFixed(xs, fx, integ)], 0).t
         nfac = jn + 2
         npad = 1 << (nfac - 1).bit_length()
         extra = npad - nfac  # planes above jn whose factor is 1 (weight 0)
-        bd = rep.bit_decompose(sess, zs, width=q + 1 if ONE_DEC_WIDTH else None)
-        ab = rep.b2a_planes_xor(sess, bd, F - f, f + jn + extra, q, bits, blocks=3)
+        bd = rep.bit_decompose(sess, zs)  # all bits: the signs are the ring's msb
+        ab = rep.b2a_planes_xor(sess, bd, F - f, f + jn + extra, q, bits, blocks=4,
+                                sbit=bits - 1)
         cs = []
         for j in range(jn):
             cs.append(int(round((2.0 ** -(2 ** j) - 1.0) * (1 << f))))
@@ -1331,8 +1339,11 @@ def _sign_and_exp_party(sess, x: RepFixed, plus: float = 0.0):
         npad = 1 << (nint - 1).bit_length()
         if F + npad > bits:
             npad = nint
-        bd = rep.bit_decompose(sess, z, width=q + 1 if ONE_DEC_WIDTH else None)
-        ab = rep.b2a_planes_xor(sess, bd, F - f, f + npad, q, bits)  # f + npad planes, then s
+        # blocks z, x': |z|'s planes from z, the mirror's sign from x' at the ring's msb
+        zs = concat(sess, [RepFixed(z, F, integ), RepFixed(xt, fx, integ)], 0).t
+        bd = rep.bit_decompose(sess, zs)
+        ab = rep.b2a_planes_xor(sess, bd, F - f, f + npad, q, bits, blocks=2,
+                                sbit=bits - 1)  # f + npad planes, then s
         rows = local(sess, ab, "Slice", slice=(0, f + npad, None))
         s = local(sess, ab, "IndexAxis", axis=0, index=f + npad)
         cs, nint_used = None, nint

@@ -1043,18 +1043,27 @@ def b2a_planes(sess, b: RepTensor, start: int, count: int, ring_bits: int) -> Re
 
 
 def b2a_planes_xor(sess, b: RepTensor, start: int, count: int, xbit: int,
-                   ring_bits: int, blocks: int = 1) -> RepTensor:
+                   ring_bits: int, blocks: int = 1, sbit: int = 0) -> RepTensor:
     """b2a of bit planes start..start+count-1 of a packed boolean sharing, each XORed with
-    plane ``xbit``, followed by plane ``xbit`` itself: count + 1 rows on a new leading axis.
-    With xbit the sign of a two's-complement x, the rows are the planes of |x| (exactly:
-    ~x = -x - 1 for x < 0, so off by one unit of bit 0) and the sign -- ONE decomposition
-    serves both (the XOR is local on boolean shares).  ``blocks`` = 3: ``b`` holds x, x - T
-    and x + T concatenated on axis 0 (decomposed together); the planes are x's and the last
-    rows [x >= T] (NOT sign(x - T)), [x < -T] (sign(x + T)) and sign(x).  One round
-    pair on a per-party session (parallel/spmd.py p_b2a_planes_xor, same shares); Slice +
-    BitSplit + Xor + Concat + b2a otherwise."""
+    plane ``xbit``, followed by sign rows: count + tail rows on a new leading axis.  With
+    xbit the sign of a two's-complement z, the rows are the planes of |z| (exactly: ~z = -z
+    - 1 for z < 0, so off by one unit of bit 0) -- ONE decomposition serves planes and
+    signs (the XOR is local on boolean shares).  ``b`` holds ``blocks`` blocks concatenated
+    on axis 0 (decomposed together); the planes are block 0's, and the tail rows:
+
+    * blocks 1: sign(z) (plane xbit); blocks 3 (z, z - T, z + T): [z >= T] (NOT sign(z - T)),
+      [z < -T] (sign(z + T)), sign(z), all at plane xbit;
+    * ``sbit`` > 0 (the ring's msb): blocks 2 (z, x): sign(x); blocks 4 (z, x - T', x + T',
+      x): [x >= T'], [x < -T'], sign(x) -- signs of x at plane sbit, right for every
+      representable x whatever magnitude bound z's planes assume.
+
+    One round pair on a per-party session (parallel/spmd.py p_b2a_planes_xor, csrc/
+    bits_party.h plane_of, same shares); Slice + BitSplit + Xor + Concat + b2a otherwise."""
+    if (sbit > 0) != (blocks in (2, 4)):
+        raise ValueError("b2a_planes_xor: blocks 2 / 4 take a sign plane sbit, 1 / 3 do not")
     f = getattr(sess, "p_b2a_planes_xor", None)
-    r = f(b.plc, b, start, count, xbit, ring_bits, blocks=blocks) if f is not None else None
+    code = blocks | (sbit << 8)
+    r = f(b.plc, b, start, count, xbit, ring_bits, blocks=code) if f is not None else None
     if r is not None:
         return RepTensor(b.plc, ring_bits, "arith", r[0], r[1])
     if blocks > 1:
@@ -1064,13 +1073,24 @@ def b2a_planes_xor(sess, b: RepTensor, start: int, count: int, xbit: int,
     else:
         parts = [(b.s0, b.s1)]
     planes = _sharewise(sess, "BitSplit", b.plc, parts[0], start=start, count=count)
-    sgns = [_sharewise(sess, "BitSplit", b.plc, p, start=xbit, count=1) for p in parts]
-    xored = _sharewise(sess, "Xor", b.plc, planes, sgns[0])
-    tail = [sgns[0]]
-    if blocks == 3:  # NOT sign(x - T), sign(x + T), sign(x)
-        nt = add_public(sess, RepTensor(b.plc, 1, "bool", *sgns[1]),
+    xsg = _sharewise(sess, "BitSplit", b.plc, parts[0], start=xbit, count=1)
+    xored = _sharewise(sess, "Xor", b.plc, planes, xsg)
+    sp = sbit if sbit > 0 else xbit
+    sgns = [_sharewise(sess, "BitSplit", b.plc, p, start=sp, count=1) for p in parts]
+
+    def not_(sg):
+        nt = add_public(sess, RepTensor(b.plc, 1, "bool", *sg),
                         R.fill((), 1, 1, getattr(sess, "device", "cpu")))
-        tail = [(nt.s0, nt.s1), sgns[2], sgns[0]]
+        return (nt.s0, nt.s1)
+
+    if blocks == 1:
+        tail = [xsg]
+    elif blocks == 3:  # NOT sign(z - T), sign(z + T), sign(z)
+        tail = [not_(sgns[1]), sgns[2], xsg]
+    elif blocks == 2:  # sign(x)
+        tail = [sgns[1]]
+    else:  # NOT sign(x - T'), sign(x + T'), sign(x)
+        tail = [not_(sgns[1]), sgns[2], sgns[3]]
     both = [sess.p("Concat", b.plc, xored[i], *[g[i] for g in tail], axis=0) for i in range(2)]
     return b2a(sess, RepTensor(b.plc, 1, "bool", both[0], both[1]), ring_bits)
 

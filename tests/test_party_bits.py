@@ -49,7 +49,6 @@ def test_one_decomposition_sigmoid_fused_equals_generic(device, ring, monkeypatc
     """The sigmoid's sign and e^-|x| from one adder over x, x - T and x + T: the fused B2A
     with the sign-plane XOR and the range rows (bits_party.h plane_of) gives bitwise the
     generic Slice + BitSplit + Xor + NOT + Concat + b2a shares."""
-    monkeypatch.setattr(FP, "ONE_DEC_WIDTH", False)  # both adders over all bits
     fused, r_fused, e = _lr(device, monkeypatch, True, True, one_dec=True, ring=ring)
     generic, r_gen, _ = _lr(device, monkeypatch, False, True, one_dec=True, ring=ring)
     assert np.array_equal(fused, generic)
@@ -330,3 +329,33 @@ def test_sign_beyond_the_nominal_integer_bound(device):
     for name, got in outs.items():
         for want in (x * x, np.abs(x)):
             assert any(np.allclose(g, want, rtol=1e-6) for g in got), (name, got, want)
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_sigmoid_beyond_the_nominal_integer_bound(device):
+    """fixed(24, 40): inputs far beyond |x| < 2^24 (a product keeps the nominal integer bits
+    while its value grows).  The per-party one-decomposition sigmoid takes its mirror sign
+    and range flags from x itself at the ring's msb (blocks z, x - T', x + T', x), so it
+    saturates to 0 / 1 like the stacked session and the plaintext (the width-
+    bounded sign flipped such outputs)."""
+    import moose_amd as pm
+
+    alice, bob, carole = (pm.host_placement(n) for n in IDS)
+    rep = pm.replicated_placement("rep", players=[alice, bob, carole])
+    fx = pm.fixed(24, 40)
+
+    @pm.computation
+    def f(x: pm.Argument(placement=alice, vtype=pm.TensorType(pm.float64))):
+        with alice:
+            xf = pm.cast(x, dtype=fx)
+        with rep:
+            s = pm.sigmoid(xf)
+        with bob:
+            return pm.cast(s, dtype=pm.float64)
+
+    x = np.array([3e7, -3e7, 1e10, -1e10, 5e12, -5e12, 2.5, -0.5, 0.0])
+    want = 1.0 / (1.0 + np.exp(-np.clip(x, -500, 500)))
+    for kw in ({"device_map": {i: device for i in IDS}}, {"device": device}):
+        rt = LocalMooseRuntime(IDS, seed=3, use_graphs=False, **kw)
+        got = np.asarray(list(rt.evaluate_computation(f, {"x": x}).values())[0])
+        np.testing.assert_allclose(got, want, atol=1e-6, err_msg=str(kw))
