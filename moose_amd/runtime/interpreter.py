@@ -39,6 +39,7 @@ from moose_amd.protocols.fixedpoint import RepFixed
 from moose_amd.runtime import lanes as _lanes
 from moose_amd.runtime import shares
 from moose_amd.runtime.session import HV
+from moose_amd.runtime.session import nonce_scope
 from moose_amd.runtime.values import LV
 from moose_amd.runtime.values import MV
 from moose_amd.utils.telemetry import span
@@ -52,6 +53,9 @@ _MERGE_KINDS = {"Sigmoid", "Exp", "Log", "Log2", "Sqrt", "Relu", "Abs"}
 _MERGE_FNS = {"Sigmoid": fxp.sigmoid, "Exp": fxp.exp, "Log": fxp.log, "Log2": fxp.log2,
               "Sqrt": fxp.sqrt, "Relu": fxp.relu, "Abs": fxp.abs_}
 MERGE_ROUNDS = os.environ.get("MOOSEX_MERGE_ROUNDS", "1") != "0"
+# per-operation nonce scopes (runtime/session.py nonce_scope; MOOSEX_NONCE_SCOPES=0: one
+# session-wide counter, the round-5 numbering)
+NONCE_SCOPES = os.environ.get("MOOSEX_NONCE_SCOPES", "1") != "0"
 
 
 def _by_depth(ops):
@@ -151,6 +155,11 @@ class Interpreter:
         self.arguments = arguments or {}
         self._at_memo = {}
         comp = comp.toposorted()
+        # every non-host operation draws its PRF nonces from a scope of its own, numbered by
+        # its place among them in the toposorted program (the same on every party and in
+        # every layout; host operations -- which draw none -- do not shift the numbering)
+        self._scope = {op.name: i + 1 for i, op in enumerate(
+            o for o in comp.operations if not isinstance(o.placement, HostPlacement))}
         me = getattr(self.sess, "me", None)  # set for one-process-per-party sessions
         batch = getattr(self.sess, "batch_dots", False) and os.environ.get(
             "MOOSEX_BATCH_DOTS", "1") != "0"
@@ -189,6 +198,10 @@ class Interpreter:
         return self.outputs
 
     def _run_op(self, op, ops, idx, batch, me):
+        with nonce_scope(self._scope.get(op.name) if NONCE_SCOPES else None):
+            self._run_op_scoped(op, ops, idx, batch, me)
+
+    def _run_op_scoped(self, op, ops, idx, batch, me):
         table = self._table_handler(op)
         if (table is None and batch and op.kind == "Dot"
                 and self._batch_dots(op, ops[idx + 1:])):

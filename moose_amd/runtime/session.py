@@ -27,6 +27,8 @@ from __future__ import annotations
 
 import math
 import os
+import threading
+from contextlib import contextmanager
 from dataclasses import dataclass
 from typing import Any
 from typing import List
@@ -81,6 +83,21 @@ def _nbytes(v):
     return 8
 
 
+_SCOPE = threading.local()
+
+
+@contextmanager
+def nonce_scope(key: Optional[int]):
+    """PRF nonces drawn in this thread come from scope ``key``'s own counter (Session.nonce);
+    ``key`` >= 1 (None: the session-wide counter)."""
+    prev = getattr(_SCOPE, "key", None)
+    _SCOPE.key = key
+    try:
+        yield
+    finally:
+        _SCOPE.key = prev
+
+
 class Session:
     """Common bookkeeping; see subclasses."""
 
@@ -106,10 +123,17 @@ class Session:
         """Fresh PRF nonce of replicated placement ``plc``.  Every member of ``plc``
         executes every protocol step on ``plc`` in program order, so all members draw the
         same sequence; keeping one counter per placement keeps it aligned even when a
-        party also works on other placements (SPMD execution)."""
-        n = self._nonces.get(plc, 0) + 1
-        self._nonces[plc] = n
-        return n
+        party also works on other placements (SPMD execution).  Inside a
+        :func:`nonce_scope` (the interpreter opens one per operation) the counter is the
+        scope's own and the nonce is ``scope << 32 | n``: an operation's nonces do not
+        depend on what ran before it or beside it, so independent operations can run
+        interleaved (parallel/lockstep.py) with bitwise the shares of running them one by
+        one."""
+        sc = getattr(_SCOPE, "key", None)
+        k = plc if sc is None else (sc, plc)
+        n = self._nonces.get(k, 0) + 1
+        self._nonces[k] = n
+        return n if sc is None else (sc << 32) | n
 
     def _random_bytes(self, n=16) -> bytes:
         if self._rng is not None:

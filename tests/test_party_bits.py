@@ -320,11 +320,13 @@ def test_sign_beyond_the_nominal_integer_bound(device):
         with carole:
             return pm.cast(r, dtype=pm.float64), pm.cast(a, dtype=pm.float64)
 
-    x = np.array([20.0, -20.0, 21.0, 1.5, -0.25])  # x * x < 2^9: no wrap at 2^54
+    # Z_2^128: x * x at 2^54 stays far below TruncPr's 2^126 bound (on Z_2^64 a product
+    # past 2^8 would already exceed 2^62)
+    x = np.array([20.0, -20.0, 21.0, 1.5, -0.25])
     outs = {}
     for name, kw in (("parties", {"device_map": {i: device for i in IDS}}),
                      ("stacked", {"device": device})):
-        rt = LocalMooseRuntime(IDS, seed=2, use_graphs=False, fixedpoint_ring=64, **kw)
+        rt = LocalMooseRuntime(IDS, seed=2, use_graphs=False, fixedpoint_ring=128, **kw)
         outs[name] = [np.asarray(v) for v in rt.evaluate_computation(f, {"x": x}).values()]
     for name, got in outs.items():
         for want in (x * x, np.abs(x)):
