@@ -219,6 +219,22 @@ class PendingTrunc(RepTensor):
         self._s1 = v
 
 
+def lazy(x) -> bool:
+    """A replicated value with message rounds still pending (read-completed)."""
+    return ((isinstance(x, PendingTrunc) and (not x.completed or x._rb is not None))
+            or isinstance(x, DeferredRep))
+
+
+def settle(x):
+    """Run a lazy replicated value's pending rounds now (:func:`lazy`).  Lockstep groups
+    (parallel/lockstep.py) settle the lazy inputs their units share before the coroutines
+    start: a completion is not re-entrant, so two coroutines must not both run it."""
+    if isinstance(x, PendingTrunc):
+        x._complete()
+    elif isinstance(x, DeferredRep):
+        x._tail.finish()
+
+
 def _reveal_pending(sess, x: PendingTrunc, host):
     """Open a PendingTrunc to a member P_j: the dot tail (zero share + reshare + TruncPr by
     m, round A) and then its round B merged with the reveal (parallel/party.py

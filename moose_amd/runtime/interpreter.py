@@ -16,6 +16,7 @@ symbolic session.
 """
 from __future__ import annotations
 
+import functools
 import math
 import os
 import threading
@@ -50,6 +51,12 @@ _CONST_LV = {}
 _CONST_LOCK = threading.Lock()
 # multi-round elementwise ops merged across independent chains (Interpreter._merge_unary)
 _MERGE_KINDS = {"Sigmoid", "Exp", "Log", "Log2", "Sqrt", "Relu", "Abs"}
+# multi-round operations that independent ops of OTHER kinds may run beside in lockstep
+# (parallel/lockstep.py): their message rounds are merged
+_LOCKSTEP_KINDS = _MERGE_KINDS | {"Div", "Less", "Greater", "Softmax", "Argmax", "Maximum",
+                                  "Dot", "Mul", "Pow2", "Msb", "Equal", "Mux", "Sign",
+                                  "TruncPr", "BitDecompose", "Mean", "Sum", "AddN"}
+LOCKSTEP = os.environ.get("MOOSEX_LOCKSTEP", "1") != "0"
 _MERGE_FNS = {"Sigmoid": fxp.sigmoid, "Exp": fxp.exp, "Log": fxp.log, "Log2": fxp.log2,
               "Sqrt": fxp.sqrt, "Relu": fxp.relu, "Abs": fxp.abs_}
 MERGE_ROUNDS = os.environ.get("MOOSEX_MERGE_ROUNDS", "1") != "0"
@@ -206,6 +213,10 @@ class Interpreter:
         if (table is None and batch and op.kind == "Dot"
                 and self._batch_dots(op, ops[idx + 1:])):
             return
+        if (table is None and LOCKSTEP and op.kind in _LOCKSTEP_KINDS
+                and getattr(self.sess, "merge_rounds", False) and self.lanes is None
+                and self._lockstep(op, ops[idx + 1:], me)):
+            return
         if (table is None and op.kind in _MERGE_KINDS and MERGE_ROUNDS
                 and getattr(self.sess, "merge_rounds", False)
                 and self._merge_unary(op, ops[idx + 1:])):
@@ -280,6 +291,128 @@ class Interpreter:
             self.env[o.name] = LV(x.plc, "tensor", dtype, r)
         return True
 
+    def _lockstep(self, op, later, me, limit: int = 8) -> bool:
+        """Intra-evaluation overlap of DIFFERENT kinds (parallel/lockstep.py): a multi-round
+        replicated op runs as a coroutine beside the later ops of the lockstep kinds on the
+        same placement whose inputs are already computed (independent of it and of each
+        other); their message rounds go out merged, so the group costs the rounds of its
+        longest member.  Same-kind elementwise ops inside the group still run as ONE merged
+        protocol (a unit, as _merge_unary forms it).  Every unit's inputs are converted
+        (e.g. host inputs shared) before the coroutines start, in program order and each
+        under the nonce scope its one-by-one run uses, so the shares are bitwise those of
+        running the units one by one.  MOOSEX_LOCKSTEP=0 disables it."""
+        from moose_amd.parallel.lockstep import Lockstep
+
+        plc = op.placement
+        if not isinstance(plc, ReplicatedPlacement):
+            return False
+        # a process outside the placement forms the same units and converts the same inputs
+        # (it takes part in sharing its own), then runs the units one by one
+        member = me is None or me in _owners(plc)
+
+        def ready(o):
+            return (o.kind in _LOCKSTEP_KINDS and o.placement == plc and o.name not in self.env
+                    and all(n in self.env for n in o.inputs) and self._table_handler(o) is None)
+
+        if not ready(op):
+            return False
+        cands = [op]
+        for o in later:
+            if len(cands) >= limit:
+                break
+            if ready(o):
+                cands.append(o)
+        if len(cands) == 1:
+            return False
+
+        def mkey(o):  # _merge_unary's grouping, from the program's structure
+            if not (MERGE_ROUNDS and o.kind in _MERGE_KINDS and len(o.inputs) == 1):
+                return None
+            x = self.env[o.inputs[0]]
+            if x.kind != "tensor" or x.dtype is None or not x.dtype.is_fixed or x.is_mir:
+                return None
+            return (o.kind, x.dtype, repr(sorted(o.attrs.items())))
+
+        units, used = [], set()
+        for o in cands:
+            if o.name in used:
+                continue
+            k = mkey(o)
+            members = [o] + ([c for c in cands if c.name not in used and c is not o
+                              and mkey(c) == k] if k is not None else [])
+            used.update(m.name for m in members)
+            units.append(members)
+        if len(units) == 1:
+            return False  # one same-kind group: _merge_unary's
+        # a lazy replicated input (a product whose last rounds run when first read) that
+        # several units read is settled first, under the scope of the first of them
+        seen = {}
+        for u in units:
+            for o in u:
+                for n in o.inputs:
+                    if u[0].name not in seen.setdefault(n, []):
+                        seen[n].append(u[0].name)
+        for n, users in seen.items():
+            t = getattr(self.env[n].v, "t", self.env[n].v)
+            if len(users) > 1 and rep.lazy(t):
+                with nonce_scope(self._scope.get(users[0])):
+                    rep.settle(t)
+
+        # inputs converted in program order, as the units' one-by-one runs would: a merged
+        # unit through the batching memo (_merge_unary's probe: later units may reuse it), a
+        # single op as its handler's ``at`` (consuming a memo entry), kept for that handler
+        pre = self.__dict__.setdefault("_lockstep_pre", {})
+        for u in units:
+            with nonce_scope(self._scope.get(u[0].name)):
+                for o in u:
+                    for n in o.inputs:
+                        lv = self.env[n]
+                        if len(u) > 1:
+                            self._at_memo_put(o, lv)
+                            continue
+                        conv = self.at(o, lv)
+                        if conv is not lv:
+                            pre[(o.name, id(lv))] = (lv, conv)
+
+        def evaluate(o):
+            handler = getattr(self, f"op_{o.kind}", None) or self._dialect_handler(o)
+            if handler is None:
+                raise MooseRuntimeError(f"operator {o.kind} is not supported by the interpreter")
+            ins = [self.env[n] for n in o.inputs]
+            with span(f"op.{o.kind}", op=o.name):
+                try:
+                    if not member:
+                        return self._foreign_op(o, ins, me)
+                    return handler(o, ins)
+                except MooseRuntimeError:
+                    raise
+                except Exception as e:  # annotate with the failing op
+                    raise MooseRuntimeError(f"{o.name} = {o.kind} failed: {e}") from e
+
+        def run_unit(u):
+            if len(u) == 1:
+                return [(u[0], evaluate(u[0]))]
+            group = [(o, self._at_memo_put(o, self.env[o.inputs[0]])) for o in u]
+            return self._merge_compute(u[0].kind, group)
+
+        try:
+            with span("op.lockstep", n=len(units)):
+                if member:
+                    outs = Lockstep(self.sess).run(
+                        [functools.partial(run_unit, u) for u in units],
+                        [self._scope.get(u[0].name) for u in units])
+                else:
+                    outs = []
+                    for u in units:
+                        with nonce_scope(self._scope.get(u[0].name)):
+                            outs.append(run_unit(u))
+        finally:
+            pre.clear()
+        for res in outs:
+            for o, lv in res:
+                self.env[o.name] = lv
+        return True
+
     def _merge_unary(self, op, later, limit: int = 16) -> bool:
         """Intra-evaluation overlap for one-party-per-process / per-thread sessions (the
         reference's async session overlaps independent operations,
@@ -320,6 +453,15 @@ class Interpreter:
                 group.append((o, k[1]))
         if len(group) == 1:
             return False
+        for o, lv in self._merge_compute(op.kind, group):
+            if self.on_op is not None and self.lanes is None:
+                self.on_op()
+            self.env[o.name] = lv
+        return True
+
+    def _merge_compute(self, kind, group):
+        """One protocol run of ``kind`` over the concatenated inputs of ``group`` [(op,
+        converted input)]: [(op, its output LV)]."""
         sess = self.sess
         flats, metas = [], []
         for _o, x in group:
@@ -330,8 +472,9 @@ class Interpreter:
             n = math.prod(shp) if shp is not None else 1
             flats.append(fxp.local(sess, x.v, "Reshape", shape=(n,)))
             metas.append((shp, n))
-        fn = _MERGE_FNS[op.kind]
-        with span(f"op.{op.kind}.merged", n=len(group)):
+        fn = _MERGE_FNS[kind]
+        out = []
+        with span(f"op.{kind}.merged", n=len(group)):
             y = fn(sess, fxp.concat(sess, flats, 0))
             at = 0
             for (o, x), (shp, n) in zip(group, metas):
@@ -339,10 +482,8 @@ class Interpreter:
                 at += n
                 if shp is not None:
                     part = fxp.local(sess, part, "Reshape", shape=shp)
-                if self.on_op is not None and self.lanes is None:
-                    self.on_op()
-                self.env[o.name] = LV(x.plc, "tensor", x.dtype, part)
-        return True
+                out.append((o, LV(x.plc, "tensor", x.dtype, part)))
+        return out
 
     # ------------------------------------------------------------------------
     # dialect-level operations (textual computations below the logical level)
@@ -598,6 +739,11 @@ class Interpreter:
 
     def at(self, op, x: LV) -> LV:
         plc = op.placement
+        pre = self.__dict__.get("_lockstep_pre")
+        if pre:  # converted for this op before its lockstep group started (_lockstep)
+            hit = pre.pop((op.name, id(x)), None)
+            if hit is not None and hit[0] is x:
+                return hit[1]
         memo = self.__dict__.get("_at_memo")
         if memo:
             hit = memo.pop((id(x), plc), None)

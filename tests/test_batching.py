@@ -73,14 +73,17 @@ def _distinct_dots(k):
     return f
 
 
-def test_independent_dots_batched_on_per_party_sessions():
+def test_independent_dots_batched_on_per_party_sessions(monkeypatch):
     """Parties as threads (one per-party SPMD session each): k independent Dots of distinct
     operands (6x5 . 5x3) run as ONE batched product and ONE dot tail -- the rounds of one
     product instead of k (BASELINE's "parallel" dot benchmark) -- with the plaintext
-    values; MOOSEX_BATCH_DOTS=0 gives k times the rounds."""
+    values; MOOSEX_BATCH_DOTS=0 (and no lockstep) gives k times the rounds."""
     import os
 
+    from moose_amd.runtime import interpreter as I
     from moose_amd.runtime.local import LocalMooseRuntime
+
+    monkeypatch.setattr(I, "LOCKSTEP", False)
 
     ids = ["alice", "bob", "carole"]
     rng = np.random.default_rng(1)

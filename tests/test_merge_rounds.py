@@ -56,8 +56,10 @@ def _check(out, args):
 def test_independent_chains_share_rounds(monkeypatch):
     args = _args()
     monkeypatch.setattr(I, "MERGE_ROUNDS", False)
+    monkeypatch.setattr(I, "LOCKSTEP", False)
     rt = LocalMooseRuntime(IDS, device_map={i: "cpu" for i in IDS}, seed=3)
-    _check(rt.evaluate_computation(_comp(), args), args)
+    serial_out = rt.evaluate_computation(_comp(), args)
+    _check(serial_out, args)
     serial = rt.last_stats.rounds
     monkeypatch.setattr(I, "MERGE_ROUNDS", True)
     rt = LocalMooseRuntime(IDS, device_map={i: "cpu" for i in IDS}, seed=3)
@@ -65,6 +67,13 @@ def test_independent_chains_share_rounds(monkeypatch):
     merged = rt.last_stats.rounds
     # two sigmoids and two exps: each pair costs the rounds of one
     assert merged <= serial // 2 + 4, (merged, serial)
+    # ... and the sigmoid pair and the exp pair run side by side (parallel/lockstep.py): the
+    # rounds of the longer one
+    monkeypatch.setattr(I, "LOCKSTEP", True)
+    rt = LocalMooseRuntime(IDS, device_map={i: "cpu" for i in IDS}, seed=3)
+    _check(rt.evaluate_computation(_comp(), args), args)
+    both = rt.last_stats.rounds
+    assert both < merged - 15, (both, merged, serial)
 
 
 def test_merged_chains_across_processes_with_an_outsider():
@@ -75,7 +84,7 @@ def test_merged_chains_across_processes_with_an_outsider():
     comp = _comp(src="dave")
     local = LocalMooseRuntime(idents, device="cpu", seed=1).evaluate_computation(comp, args)
     got = DistributedMooseRuntime(idents, backend="gloo", seed=1,
-                                  timeout=300).evaluate_computation(comp, args)
+                                  timeout=60).evaluate_computation(comp, args)
     assert set(got) == set(local)
     for k in local:
         np.testing.assert_allclose(np.asarray(got[k], dtype=np.float64),
@@ -96,3 +105,69 @@ def test_merged_chains_graph_replays_bitwise_equal_eager():
         for k in want:
             assert np.array_equal(np.asarray(got[k]), np.asarray(want[k])), k
     _check(got, args)
+
+
+def _two_kinds():
+    alice, bob, carole = (pm.host_placement(n) for n in IDS)
+    rep = pm.replicated_placement("rep", players=[alice, bob, carole])
+    fx = pm.fixed(24, 40)
+
+    @pm.computation
+    def f(x: pm.Argument(placement=alice, vtype=pm.TensorType(pm.float64)),
+          y: pm.Argument(placement=bob, vtype=pm.TensorType(pm.float64))):
+        with alice:
+            xf = pm.cast(x, dtype=fx)
+        with bob:
+            yf = pm.cast(y, dtype=fx)
+        with rep:
+            c = pm.less(xf, yf)
+            e = pm.exp(yf)
+            d = pm.div(xf, yf)
+        with carole:
+            return pm.cast(e, dtype=pm.float64), c, pm.cast(d, dtype=pm.float64)
+
+    return f
+
+
+TWO_ARGS = {"x": np.array([1.0, -2.0, 3.5, 0.25]), "y": np.array([0.5, 1.5, 4.0, -1.25])}
+
+
+def _two_check(out):
+    x, y = TWO_ARGS["x"], TWO_ARGS["y"]
+    vals = [np.asarray(v) for v in out.values()]
+    assert any(v.dtype == bool and np.array_equal(v, x < y) for v in vals)
+    assert any(v.dtype != bool and np.allclose(v, np.exp(y), rtol=1e-6) for v in vals)
+    assert any(v.dtype != bool and np.allclose(v, x / y, atol=1e-5) for v in vals)
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_different_kinds_share_rounds_bitwise_equal_serial(device, monkeypatch):
+    """A comparison, an exponential and a division of the same inputs, independent of each
+    other (parallel/lockstep.py): run as coroutines whose message rounds go out together,
+    they cost the rounds of the longest instead of the sum -- and, every operation drawing
+    its nonces from its own scope, the outputs are bitwise those of the serial run."""
+    outs = {}
+    for flag in (False, True):
+        monkeypatch.setattr(I, "LOCKSTEP", flag)
+        rt = LocalMooseRuntime(IDS, device_map={i: device for i in IDS}, seed=7,
+                               use_graphs=False)
+        out = rt.evaluate_computation(_two_kinds(), TWO_ARGS)
+        _two_check(out)
+        outs[flag] = ([np.asarray(v) for v in out.values()], rt.last_stats.rounds)
+    (a, r_ls), (b, r_serial) = outs[True], outs[False]
+    assert all(np.array_equal(p, q) for p, q in zip(a, b))
+    assert r_ls < r_serial - 10, (r_ls, r_serial)
+
+
+def test_different_kinds_lockstep_across_processes():
+    """SPMD processes over gloo (message plans, grouped exchanges): the same lockstep groups
+    on every process, outputs bitwise equal to a serial run, fewer rounds."""
+    res = {}
+    for flag in ("0", "1"):
+        rt = DistributedMooseRuntime(IDS, backend="gloo", seed=3, timeout=60,
+                                     worker_env={"MOOSEX_LOCKSTEP": flag})
+        out = rt.evaluate_computation(_two_kinds(), TWO_ARGS)
+        _two_check(out)
+        res[flag] = [np.asarray(v) for v in out.values()]
+        rt.close()
+    assert all(np.array_equal(p, q) for p, q in zip(res["0"], res["1"]))
