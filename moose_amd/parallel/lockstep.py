@@ -46,15 +46,21 @@ class _TransportProxy:
     """The session's transport while a group runs.  A coroutine parks at the points EVERY
     member of the placement reaches alike -- ``SPMDSession.party_exchange`` (through
     :func:`current`, also when this party has nothing to send or receive there) and the ring
-    shift of a reshare -- so the parties' schedules stay identical; everything else (point-
-    to-point moves, role-dependent grouped exchanges) goes straight through, in that same
-    deterministic order on every party."""
+    shift of a reshare -- so the parties' schedules stay identical.  Every other transport
+    call (point-to-point moves, role-dependent grouped exchanges, key setup) runs at once,
+    in that same deterministic order on every party, but on the scheduler's thread: a taped
+    evaluation ends and restarts its capture segment at each message, and a thread-local
+    hipGraph capture may only be ended by the thread that began it."""
 
     def __init__(self, ls: "Lockstep", real):
         self._ls, self._real = ls, real
 
     def __getattr__(self, name):
-        return getattr(self._real, name)
+        attr = getattr(self._real, name)
+        w = getattr(_TLS, "worker", None)
+        if not callable(attr) or w is None or w[0] is not self._ls:
+            return attr
+        return lambda *a, **kw: self._ls.delegate(w[1], attr, a, kw)
 
     def shift(self, data, to_r, from_r):
         w = getattr(_TLS, "worker", None)
@@ -96,12 +102,40 @@ class Lockstep:
         if self.abort is not None:
             raise self.abort
 
+    def delegate(self, k, fn, args, kwargs):
+        """Called on coroutine k's thread: run ``fn`` on the scheduler's thread now (no
+        park: the coroutine continues right after) and return its result."""
+        self.calls[k] = (fn, args, kwargs)
+        self.back.release()
+        self.go[k].acquire()
+        if self.abort is not None:
+            raise self.abort
+        res, err = self.replies.pop(k)
+        if err is not None:
+            raise err
+        return res
+
+    def _resume(self, k):
+        """Run coroutine k until it parks or ends, serving its delegated calls."""
+        self.go[k].release()
+        while True:
+            self.back.acquire()
+            call = self.calls.pop(k, None)
+            if call is None:
+                return
+            fn, args, kwargs = call
+            try:
+                self.replies[k] = (fn(*args, **kwargs), None)
+            except BaseException as e:  # noqa: BLE001 - raised on the coroutine's thread
+                self.replies[k] = (None, e)
+            self.go[k].release()
+
     def run(self, fns: List[Callable], scopes: List[int]):
         n = len(fns)
         sess = self.sess
         self.go = [threading.Semaphore(0) for _ in range(n)]
         self.back = threading.Semaphore(0)
-        self.pending = {}
+        self.pending, self.calls, self.replies = {}, {}, {}
         self.abort = None
         self.stats = [SessionStats() for _ in range(n)]
         results, errors, done = [None] * n, [None] * n, [False] * n
@@ -136,8 +170,7 @@ class Lockstep:
             active = list(range(n))
             while active:
                 for k in list(active):
-                    self.go[k].release()  # coroutine k runs until it parks or ends
-                    self.back.acquire()
+                    self._resume(k)
                     if done[k]:
                         active.remove(k)
                 if any(e is not None for e in errors):
