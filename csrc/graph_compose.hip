@@ -20,8 +20,11 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <unordered_map>
 #include <vector>
+
+#include "party_batch.h"
 
 namespace {
 
@@ -192,7 +195,180 @@ int flatten_into(hipGraph_t g, hipGraph_t child, const std::vector<hipGraphNode_
   return 0;
 }
 
+// kernel -> its party-batched twin (party_batch.h); filled by static initialisers of the
+// kernels' translation units, read when a composed graph is built
+std::unordered_map<const void*, mxb::Entry>& x3_registry() {
+  static std::unordered_map<const void*, mxb::Entry> m;
+  return m;
+}
+
+// MOOSEX_PARTY_MERGE=0: no party-batched launches in composed graphs
+bool merge_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("MOOSEX_PARTY_MERGE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// One launch of a party's segment in a phase of the composed total order, or a whole
+// segment that cannot be taken apart (copies / memsets inside: kept as a child graph).
+struct Item {
+  bool opaque = false;
+  hipGraph_t child = nullptr;   // opaque: the segment
+  hipGraphNode_t node = nullptr;  // a kernel node of a segment
+  const void* func = nullptr;
+  dim3 grid, block;
+  unsigned shmem = 0;
+  const mxb::Entry* x3 = nullptr;  // the twin, when this launch can be batched
+};
+
+bool same_launch(const Item& a, const Item& b) {
+  return !a.opaque && !b.opaque && a.x3 != nullptr && a.func == b.func &&
+         a.grid.x == b.grid.x && a.grid.y == b.grid.y && a.block.x == b.block.x &&
+         a.block.y == b.block.y && a.block.z == b.block.z && a.shmem == b.shmem;
+}
+
+// The launches of one captured segment in a topological order; false when the segment
+// holds other node types (then it is one opaque item).
+bool segment_items(hipGraph_t child, std::vector<Item>* out) {
+  size_t n = 0;
+  if (hipGraphGetNodes(child, nullptr, &n) != hipSuccess) return false;
+  std::vector<hipGraphNode_t> nodes(n);
+  if (n && hipGraphGetNodes(child, nodes.data(), &n) != hipSuccess) return false;
+  size_t ne = 0;
+  if (hipGraphGetEdges(child, nullptr, nullptr, &ne) != hipSuccess) return false;
+  std::vector<hipGraphNode_t> from(ne), to(ne);
+  if (ne && hipGraphGetEdges(child, from.data(), to.data(), &ne) != hipSuccess) return false;
+  std::unordered_map<hipGraphNode_t, int> idx;
+  for (size_t i = 0; i < n; ++i) idx[nodes[i]] = (int)i;
+  std::vector<std::vector<int>> succs(n);
+  std::vector<int> indeg(n, 0);
+  for (size_t e = 0; e < ne; ++e) {
+    succs[idx.at(from[e])].push_back(idx.at(to[e]));
+    ++indeg[idx.at(to[e])];
+  }
+  std::vector<Item> items;
+  std::vector<int> ready;
+  for (size_t i = 0; i < n; ++i)
+    if (indeg[i] == 0) ready.push_back((int)i);
+  // FIFO over the ready set keeps a captured stream's order
+  for (size_t h = 0; h < ready.size(); ++h) {
+    const int v = ready[h];
+    hipGraphNodeType t;
+    if (hipGraphNodeGetType(nodes[v], &t) != hipSuccess) return false;
+    if (t == hipGraphNodeTypeKernel) {
+      hipKernelNodeParams kp = {};
+      if (hipGraphKernelNodeGetParams(nodes[v], &kp) != hipSuccess) return false;
+      if (kp.func == nullptr || (kp.kernelParams == nullptr && kp.extra == nullptr)) return false;
+      Item it;
+      it.node = nodes[v];
+      it.func = kp.func;
+      it.grid = kp.gridDim;
+      it.block = kp.blockDim;
+      it.shmem = kp.sharedMemBytes;
+      auto f = x3_registry().find(kp.func);
+      if (f != x3_registry().end() && kp.gridDim.z == 1 &&
+          kp.blockDim.x * kp.blockDim.y * kp.blockDim.z <= 256)
+        it.x3 = &f->second;
+      items.push_back(it);
+    } else if (t != hipGraphNodeTypeEmpty) {
+      return false;
+    }
+    for (int w : succs[v])
+      if (--indeg[w] == 0) ready.push_back(w);
+  }
+  if (ready.size() != n) return false;
+  out->insert(out->end(), items.begin(), items.end());
+  return true;
+}
+
+// One node per group of a phase's launches (1-3 parties' same launch, or one item) in an
+// order that keeps every party's own order, with the fewest nodes: a dynamic programme over
+// the three parties' positions (phases too long for it keep the segments' order, unbatched).
+struct Group {
+  int party[3];
+  int idx[3];
+  int k;
+};
+
+std::vector<Group> align3(const std::vector<Item>* L) {
+  const int a = (int)L[0].size(), b = (int)L[1].size(), c = (int)L[2].size();
+  std::vector<Group> out;
+  const int64_t states = (int64_t)(a + 1) * (b + 1) * (c + 1);
+  if (!merge_on() || states > (int64_t)4 << 20) {
+    for (int p = 0; p < 3; ++p)
+      for (int i = 0; i < (int)L[p].size(); ++i) out.push_back({{p, 0, 0}, {i, 0, 0}, 1});
+    return out;
+  }
+  auto at = [&](int i, int j, int k) { return ((int64_t)i * (b + 1) + j) * (c + 1) + k; };
+  std::vector<int32_t> cost((size_t)states, 0);
+  std::vector<uint8_t> pick((size_t)states, 0);  // bitmask of the parties advanced
+  for (int i = a; i >= 0; --i)
+    for (int j = b; j >= 0; --j)
+      for (int k = c; k >= 0; --k) {
+        if (i == a && j == b && k == c) continue;
+        int best = INT32_MAX;
+        uint8_t bm = 0;
+        const bool h0 = i < a, h1 = j < b, h2 = k < c;
+        auto consider = [&](uint8_t m) {
+          const int v = 1 + cost[(size_t)at(i + (m & 1), j + ((m >> 1) & 1), k + ((m >> 2) & 1))];
+          if (v < best) {
+            best = v;
+            bm = m;
+          }
+        };
+        if (h0 && h1 && h2 && same_launch(L[0][i], L[1][j]) && same_launch(L[0][i], L[2][k]))
+          consider(7);
+        if (h0 && h1 && same_launch(L[0][i], L[1][j])) consider(3);
+        if (h0 && h2 && same_launch(L[0][i], L[2][k])) consider(5);
+        if (h1 && h2 && same_launch(L[1][j], L[2][k])) consider(6);
+        if (h0) consider(1);
+        if (h1) consider(2);
+        if (h2) consider(4);
+        cost[(size_t)at(i, j, k)] = best;
+        pick[(size_t)at(i, j, k)] = bm;
+      }
+  int i = 0, j = 0, k = 0;
+  while (i < a || j < b || k < c) {
+    const uint8_t m = pick[(size_t)at(i, j, k)];
+    Group g{{0, 0, 0}, {0, 0, 0}, 0};
+    if (m & 1) g.party[g.k] = 0, g.idx[g.k++] = i++;
+    if (m & 2) g.party[g.k] = 1, g.idx[g.k++] = j++;
+    if (m & 4) g.party[g.k] = 2, g.idx[g.k++] = k++;
+    out.push_back(g);
+  }
+  return out;
+}
+
+// the twin's argument blocks from the members' captured arguments
+bool pack_args(const Group& g, const std::vector<Item>* L, const mxb::Entry& e,
+               unsigned char* blob) {
+  std::memset(blob, 0, 3 * e.stride);
+  for (int z = 0; z < g.k; ++z) {
+    hipKernelNodeParams kp = {};
+    if (hipGraphKernelNodeGetParams(L[g.party[z]][g.idx[z]].node, &kp) != hipSuccess)
+      return false;
+    unsigned char* dst = blob + z * e.stride;
+    if (kp.kernelParams != nullptr) {
+      for (int a = 0; a < e.nargs; ++a) std::memcpy(dst + e.off[a], kp.kernelParams[a], e.size[a]);
+    } else {
+      void* buf = nullptr;
+      size_t size = 0;
+      for (void** x = (void**)kp.extra; x != nullptr && *x != HIP_LAUNCH_PARAM_END; x += 2) {
+        if (x[0] == HIP_LAUNCH_PARAM_BUFFER_POINTER) buf = x[1];
+        if (x[0] == HIP_LAUNCH_PARAM_BUFFER_SIZE) size = *(size_t*)x[1];
+      }
+      if (buf == nullptr || size < e.off[e.nargs - 1] + e.size[e.nargs - 1]) return false;
+      std::memcpy(dst, buf, size < e.stride ? size : e.stride);
+    }
+  }
+  return true;
+}
+
 }  // namespace
+
+void mx_x3_add(const void* kernel, const mxb::Entry& e) { x3_registry()[kernel] = e; }
 
 extern "C" {
 
@@ -305,6 +481,139 @@ static int graph_compose_impl(int n, const int* kind, void* const* child, void* 
   if (std::getenv("MOOSEX_FLAT_DEBUG") != nullptr) {
     fprintf(stderr, "compose: instantiated\n");
     fflush(stderr);
+  }
+  *graph_out = (void*)g;
+  *exec_out = (void*)ex;
+  return 0;
+}
+
+// The composed total order as ONE chain with party-batched launches (party_batch.h):
+// kind / child / dst / src / bytes as mx_graph_compose, party[i] = the party of segment i
+// (kind 0).  Each maximal run of segments between two copy nodes is a phase: the parties'
+// launches in it are independent, so the same launch of 2-3 parties becomes one node.
+// stats[0..3] = nodes, launches merged away, batched nodes, phases.
+int mx_graph_compose_merged(int n, const int* kind, void* const* child, void* const* dst,
+                            void* const* src, const int64_t* bytes, const int* party,
+                            int64_t* stats, void** graph_out, void** exec_out) {
+  install_fault_handler();
+  if (n < 1) return -2;
+  hipGraph_t g = nullptr;
+  if (hipGraphCreate(&g, 0) != hipSuccess) return -3;
+  std::vector<hipGraphNode_t> prev;
+  int64_t nodes = 0, merged_away = 0, batched = 0, phases = 0;
+  auto add_after = [&](hipGraphNode_t node) {
+    prev.assign(1, node);
+    ++nodes;
+  };
+  alignas(16) static thread_local unsigned char blob[4096];
+  for (int i = 0; i < n;) {
+    if (kind[i] != 0) {
+      hipGraphNode_t node = nullptr;
+      hipError_t rc;
+      if (kind[i] == 2) {
+        const int cnt = (int)(intptr_t)child[i];
+        int gx = 1, gy = 1;
+        mx_copy_many_grid(cnt, bytes[i], &gx, &gy);
+        void* desc = dst[i];
+        int count = cnt;
+        void* args[] = {&desc, &count};
+        hipKernelNodeParams kp = {};
+        kp.func = mx_copy_many_fn();
+        kp.gridDim = dim3(gx, gy, 1);
+        kp.blockDim = dim3(256, 1, 1);
+        kp.kernelParams = args;
+        rc = hipGraphAddKernelNode(&node, g, prev.data(), prev.size(), &kp);
+      } else {
+        rc = hipGraphAddMemcpyNode1D(&node, g, prev.data(), prev.size(), dst[i], src[i],
+                                     (size_t)bytes[i], hipMemcpyDeviceToDevice);
+      }
+      if (rc != hipSuccess) {
+        hipGraphDestroy(g);
+        return -10 - i;
+      }
+      add_after(node);
+      ++i;
+      continue;
+    }
+    int j = i;
+    while (j < n && kind[j] == 0) ++j;
+    ++phases;
+    // the phase's items per party (parties beyond the third: unbatched, in segment order)
+    std::vector<Item> L[3];
+    bool many = false;
+    for (int s2 = i; s2 < j; ++s2)
+      if (party[s2] < 0 || party[s2] > 2) many = true;
+    if (!many) {
+      for (int s2 = i; s2 < j; ++s2) {
+        std::vector<Item> its;
+        if (segment_items((hipGraph_t)child[s2], &its)) {
+          L[party[s2]].insert(L[party[s2]].end(), its.begin(), its.end());
+        } else {
+          Item op;
+          op.opaque = true;
+          op.child = (hipGraph_t)child[s2];
+          L[party[s2]].push_back(op);
+        }
+      }
+    } else {
+      for (int s2 = i; s2 < j; ++s2) {
+        Item op;
+        op.opaque = true;
+        op.child = (hipGraph_t)child[s2];
+        L[0].push_back(op);
+      }
+    }
+    for (const Group& gr : align3(L)) {
+      const Item& it = L[gr.party[0]][gr.idx[0]];
+      hipGraphNode_t node = nullptr;
+      hipError_t rc = hipSuccess;
+      if (it.opaque) {
+        size_t count = 0;
+        if (hipGraphGetNodes(it.child, nullptr, &count) == hipSuccess && count == 0) continue;
+        rc = hipGraphAddChildGraphNode(&node, g, prev.data(), prev.size(), it.child);
+      } else if (gr.k == 1) {
+        hipKernelNodeParams kp = {};
+        rc = hipGraphKernelNodeGetParams(it.node, &kp);
+        if (rc == hipSuccess) rc = hipGraphAddKernelNode(&node, g, prev.data(), prev.size(), &kp);
+      } else {
+        const mxb::Entry& e = *it.x3;
+        if (!pack_args(gr, L, e, blob)) {
+          hipGraphDestroy(g);
+          return -7;
+        }
+        void* args[] = {blob};
+        hipKernelNodeParams kp = {};
+        kp.func = const_cast<void*>(e.x3);
+        kp.gridDim = dim3(it.grid.x, it.grid.y, (unsigned)gr.k);
+        kp.blockDim = it.block;
+        kp.sharedMemBytes = it.shmem;
+        kp.kernelParams = args;
+        rc = hipGraphAddKernelNode(&node, g, prev.data(), prev.size(), &kp);
+        merged_away += gr.k - 1;
+        ++batched;
+      }
+      if (rc != hipSuccess) {
+        hipGraphDestroy(g);
+        return -20 - i;
+      }
+      add_after(node);
+    }
+    i = j;
+  }
+  if (nodes == 0) {
+    hipGraphNode_t node = nullptr;
+    hipGraphAddEmptyNode(&node, g, nullptr, 0);
+  }
+  hipGraphExec_t ex = nullptr;
+  if (hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) != hipSuccess) {
+    hipGraphDestroy(g);
+    return -5;
+  }
+  if (stats) {
+    stats[0] = nodes;
+    stats[1] = merged_away;
+    stats[2] = batched;
+    stats[3] = phases;
   }
   *graph_out = (void*)g;
   *exec_out = (void*)ex;

@@ -20,6 +20,7 @@
 
 #include "aes_core.h"
 #include "moosex.h"
+#include "party_batch.h"
 #include "prf_core.h"
 
 namespace {
@@ -46,9 +47,9 @@ __device__ void expand_key_dev(const uint32_t key_le[4], uint32_t* rk) {
 }
 
 // one workgroup: every thread derives slots tid, tid + 256, ...; then the counter advances
-__global__ void __launch_bounds__(256)
-    k_key_refresh(uint32_t* __restrict__ slots, int n, const uint32_t* __restrict__ master,
-                  uint64_t* __restrict__ epoch) {
+__device__ __forceinline__ void d_key_refresh(uint32_t* __restrict__ slots, int n,
+                                              const uint32_t* __restrict__ master,
+                                              uint64_t* __restrict__ epoch) {
   const uint64_t e = *epoch;
   uint32_t mk[4] = {master[0], master[1], master[2], master[3]};
   for (int s = threadIdx.x; s < n; s += blockDim.x) {
@@ -63,6 +64,15 @@ __global__ void __launch_bounds__(256)
   __syncthreads();  // every thread has read e before it changes
   if (threadIdx.x == 0) *epoch = e + 1;
 }
+
+__global__ void __launch_bounds__(256) k_key_refresh(uint32_t* __restrict__ slots, int n,
+                                                     const uint32_t* __restrict__ master,
+                                                     uint64_t* __restrict__ epoch) {
+  d_key_refresh(slots, n, master, epoch);
+}
+
+// the parties' refreshes at the head of a composed replay: one party-batched node
+MX_X3(k_key_refresh, d_key_refresh);
 
 struct CopyDesc {
   const uint8_t* src;

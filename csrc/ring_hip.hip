@@ -18,6 +18,7 @@
 
 #include "prf_dev.h"
 #include "moosex.h"
+#include "party_batch.h"
 #include "ring_common.h"
 #include "rss_fused.h"
 
@@ -42,12 +43,20 @@ inline hipStream_t S(void* s) { return (hipStream_t)s; }
   } while (0)
 
 template <class T>
-__global__ void __launch_bounds__(256) k_binary(int op, const T* __restrict__ a, int64_t na, const T* __restrict__ b,
-                         int64_t nb, T* __restrict__ out, int64_t n) {
+__device__ __forceinline__ void d_binary(int op, const T* __restrict__ a, int64_t na,
+                                         const T* __restrict__ b, int64_t nb, T* __restrict__ out,
+                                         int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     out[i] = mxr::binop<T>(op, a[na == 1 ? 0 : i], b[nb == 1 ? 0 : i]);
   }
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) k_binary(int op, const T* __restrict__ a, int64_t na,
+                                                const T* __restrict__ b, int64_t nb,
+                                                T* __restrict__ out, int64_t n) {
+  d_binary<T>(op, a, na, b, nb, out, n);
 }
 
 template <class T>
@@ -133,8 +142,8 @@ struct Lin3 {
 };
 
 template <class T>
-__global__ void __launch_bounds__(256) k_lincomb2(Lin3<T> p, int nin, const T* __restrict__ b,
-                                                  int64_t nb, int64_t m, int np) {
+__device__ __forceinline__ void d_lincomb2(const Lin3<T>& p, int nin, const T* __restrict__ b,
+                                           int64_t nb, int64_t m, int np) {
   const int y = blockIdx.y;
   T* __restrict__ out = p.o[y];
   const int which = p.which[y];
@@ -150,6 +159,12 @@ __global__ void __launch_bounds__(256) k_lincomb2(Lin3<T> p, int nin, const T* _
     }
     out[g] = v;
   }
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) k_lincomb2(Lin3<T> p, int nin, const T* __restrict__ b,
+                                                  int64_t nb, int64_t m, int np) {
+  d_lincomb2<T>(p, nin, b, nb, m, np);
 }
 
 // AddN of k replicated values that are evenly spaced views of one stack (the products of a
@@ -213,14 +228,16 @@ __global__ void __launch_bounds__(256) k_add_zs3(const T* __restrict__ v, const 
 }
 
 template <class T>
-__global__ void __launch_bounds__(256) k_unary(int op, const T* __restrict__ a, T* __restrict__ out, int64_t n, int k) {
+__global__ void __launch_bounds__(256) k_unary(int op, const T* __restrict__ a, T* __restrict__ out,
+                                               int64_t n, int k) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
     out[i] = mxr::unop<T>(op, a[i], k);
 }
 
 template <class T>
-__global__ void __launch_bounds__(256) k_fill(T* __restrict__ out, int64_t n, uint64_t lo, uint64_t hi) {
+__global__ void __launch_bounds__(256) k_fill(T* __restrict__ out, int64_t n, uint64_t lo,
+                                              uint64_t hi) {
   T v;
   if constexpr (sizeof(T) == 16) {
     v = ((T)hi << 64) | (T)lo;
@@ -234,7 +251,8 @@ __global__ void __launch_bounds__(256) k_fill(T* __restrict__ out, int64_t n, ui
 
 // out[o, j, i] = bit (start + j) of a[o, i] as a 0/1 byte (bit decomposition / split)
 template <class T>
-__global__ void __launch_bounds__(256) k_bit_planes(const T* __restrict__ a, uint8_t* __restrict__ out, int64_t outer,
+__global__ void __launch_bounds__(256) k_bit_planes(const T* __restrict__ a,
+                                                    uint8_t* __restrict__ out, int64_t outer, 
                              int64_t inner, int start, int count) {
   const int64_t n = outer * inner;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < n;
@@ -248,7 +266,8 @@ __global__ void __launch_bounds__(256) k_bit_planes(const T* __restrict__ a, uin
 
 // out[o, i] = sum_j w[j] * a[o, j, i]  (public ring weights, bit composition)
 template <class T>
-__global__ void __launch_bounds__(256) k_weighted_sum(const T* __restrict__ a, const T* __restrict__ w,
+__global__ void __launch_bounds__(256) k_weighted_sum(const T* __restrict__ a,
+                                                      const T* __restrict__ w, 
                                T* __restrict__ out, int64_t outer, int64_t k, int64_t inner) {
   const int64_t n = outer * inner;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < n;
@@ -299,7 +318,8 @@ __global__ void __launch_bounds__(256) k_weighted_sum_wide(const T* __restrict__
 }
 
 template <class T>
-__global__ void __launch_bounds__(256) k_compare(int op, const T* __restrict__ a, int64_t na, const T* __restrict__ b,
+__global__ void __launch_bounds__(256) k_compare(int op, const T* __restrict__ a, int64_t na,
+                                                 const T* __restrict__ b, 
                           int64_t nb, uint8_t* __restrict__ out, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -307,7 +327,8 @@ __global__ void __launch_bounds__(256) k_compare(int op, const T* __restrict__ a
 }
 
 template <class T>
-__global__ void __launch_bounds__(256) k_bit_extract(const T* __restrict__ a, uint8_t* __restrict__ out, int64_t n,
+__global__ void __launch_bounds__(256) k_bit_extract(const T* __restrict__ a,
+                                                     uint8_t* __restrict__ out, int64_t n, 
                               int bit) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -315,7 +336,8 @@ __global__ void __launch_bounds__(256) k_bit_extract(const T* __restrict__ a, ui
 }
 
 template <class T>
-__global__ void __launch_bounds__(256) k_ring_inject(const uint8_t* __restrict__ bits, T* __restrict__ out, int64_t n,
+__global__ void __launch_bounds__(256) k_ring_inject(const uint8_t* __restrict__ bits,
+                                                     T* __restrict__ out, int64_t n, 
                               int bit) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -427,7 +449,8 @@ __global__ void __launch_bounds__(256) k_b2a3(const uint8_t* __restrict__ s0,
 }
 
 template <class T>
-__global__ void __launch_bounds__(256) k_encode(const double* __restrict__ x, T* __restrict__ out, int64_t n,
+__global__ void __launch_bounds__(256) k_encode(const double* __restrict__ x, T* __restrict__ out,
+                                                int64_t n, 
                          double scale) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -435,7 +458,8 @@ __global__ void __launch_bounds__(256) k_encode(const double* __restrict__ x, T*
 }
 
 template <class T>
-__global__ void __launch_bounds__(256) k_decode(const T* __restrict__ x, double* __restrict__ out, int64_t n,
+__global__ void __launch_bounds__(256) k_decode(const T* __restrict__ x, double* __restrict__ out,
+                                                int64_t n, 
                          double scale) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -449,10 +473,9 @@ __global__ void __launch_bounds__(256) k_decode(const T* __restrict__ x, double*
 // decode(a + b + c [+ d]): the reveal's add and the decode in one pass (no ring-valued sum in
 // HBM); d may be null
 template <class T>
-__global__ void __launch_bounds__(256) k_addn_decode(const T* __restrict__ a, const T* __restrict__ b,
-                                                     const T* __restrict__ c, const T* __restrict__ d,
-                                                     double* __restrict__ out, int64_t n,
-                                                     double scale) {
+__device__ __forceinline__ void d_addn_decode(const T* __restrict__ a, const T* __restrict__ b,
+                                              const T* __restrict__ c, const T* __restrict__ d,
+                                              double* __restrict__ out, int64_t n, double scale) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     T v = a[i] + b[i] + c[i];
@@ -464,9 +487,20 @@ __global__ void __launch_bounds__(256) k_addn_decode(const T* __restrict__ a, co
   }
 }
 
+template <class T>
+__global__ void __launch_bounds__(256) k_addn_decode(const T* __restrict__ a,
+                                                     const T* __restrict__ b,
+                                                     const T* __restrict__ c,
+                                                     const T* __restrict__ d,
+                                                     double* __restrict__ out, int64_t n,
+                                                     double scale) {
+  d_addn_decode<T>(a, b, c, d, out, n, scale);
+}
+
 // one thread per output when the reduced axis is short; a block per output otherwise
 template <class T>
-__global__ void __launch_bounds__(256) k_sum_axis(const T* __restrict__ a, T* __restrict__ out, int64_t outer,
+__global__ void __launch_bounds__(256) k_sum_axis(const T* __restrict__ a, T* __restrict__ out,
+                                                  int64_t outer, 
                            int64_t red, int64_t inner) {
   int64_t total = outer * inner;
   for (int64_t oi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; oi < total;
@@ -485,7 +519,8 @@ __global__ void __launch_bounds__(256) k_sum_axis(const T* __restrict__ a, T* __
 }
 
 template <class T>
-__global__ void __launch_bounds__(256) k_sum_axis_wide(const T* __restrict__ a, T* __restrict__ out, int64_t red,
+__global__ void __launch_bounds__(256) k_sum_axis_wide(const T* __restrict__ a, T* __restrict__ out,
+                                                       int64_t red, 
                                 int64_t inner) {
   __shared__ T part[kBlock];
   int64_t oi = blockIdx.x;
@@ -542,10 +577,11 @@ __global__ void __launch_bounds__(256) k_prg(RawKey key, uint64_t nonce, uint64_
 // (party, block).  Keys are staged in LDS (from launch parameters or from key slots in
 // device memory, see prf_dev.h).
 template <class T>
-__global__ void __launch_bounds__(256) k_rss_cross(int kind, const T* __restrict__ x0, const T* __restrict__ x1,
-                            const T* __restrict__ y0, const T* __restrict__ y1,
-                            T* __restrict__ out, int64_t n, int nparties, int has_keys,
-                            KeySrc keys, uint64_t nonce, int pairs) {
+__device__ __forceinline__ void d_rss_cross(int kind, const T* __restrict__ x0,
+                                            const T* __restrict__ x1, const T* __restrict__ y0,
+                                            const T* __restrict__ y1, T* __restrict__ out,
+                                            int64_t n, int nparties, int has_keys,
+                                            const KeySrc& keys, uint64_t nonce, int pairs) {
   // pairs == 0: party p uses keys p and p+1 (one session, shared ring of keys);
   // pairs == 1: party p uses keys 2p and 2p+1 (parties of independent sessions)
   __shared__ uint32_t rks[mxd::kMaxKeySlots][kKeyWords];
@@ -590,6 +626,16 @@ __global__ void __launch_bounds__(256) k_rss_cross(int kind, const T* __restrict
   }
 }
 
+template <class T>
+__global__ void __launch_bounds__(256) k_rss_cross(int kind, const T* __restrict__ x0,
+                                                   const T* __restrict__ x1,
+                                                   const T* __restrict__ y0,
+                                                   const T* __restrict__ y1, T* __restrict__ out,
+                                                   int64_t n, int nparties, int has_keys,
+                                                   KeySrc keys, uint64_t nonce, int pairs) {
+  d_rss_cross<T>(kind, x0, x1, y0, y1, out, n, nparties, has_keys, keys, nonce, pairs);
+}
+
 // Operand layouts of the stacked multiplication kernels: operand k of party p, element e is
 // ptr_k[p * ps[k] + e % per[k]] -- a slice along the first logical axis (party stride !=
 // n) or a broadcast of one row over it (per = row size) without materialising the view.
@@ -612,7 +658,8 @@ __device__ __forceinline__ T ld_view(const T* __restrict__ a, const Views& v, in
 // ChaCha block evaluates the three keys' blocks once and finishes all three parties'
 // elements of the block's chunks (the shares are identical to k_rss_cross).
 template <class T>
-__global__ void __launch_bounds__(256) k_rss_cross_ring3(int kind, const T* __restrict__ x0, const T* __restrict__ x1,
+__global__ void __launch_bounds__(256) k_rss_cross_ring3(int kind, const T* __restrict__ x0,
+                                                         const T* __restrict__ x1, 
                                   const T* __restrict__ y0, const T* __restrict__ y1,
                                   T* __restrict__ out, T* __restrict__ out1, int64_t n,
                                   KeySrc keys, uint64_t nonce, Views vw) {
@@ -652,7 +699,8 @@ __global__ void __launch_bounds__(256) k_rss_cross_ring3(int kind, const T* __re
 // computed one PRF chunk per thread into LDS (one PRF on the critical path), then EPB
 // threads finish all three parties' shares and write the reshared outputs directly.
 template <class T>
-__global__ void __launch_bounds__(256) k_ks_level3(const T* __restrict__ g0, const T* __restrict__ g1,
+__global__ void __launch_bounds__(256) k_ks_level3(const T* __restrict__ g0,
+                                                   const T* __restrict__ g1, 
                                                    const T* __restrict__ p0, const T* __restrict__ p1,
                                                    T* __restrict__ og0, T* __restrict__ og1,
                                                    T* __restrict__ op0, T* __restrict__ op1,
@@ -718,7 +766,8 @@ struct Nonces8 {
 };
 
 template <class T>
-__global__ void __launch_bounds__(256) k_ks_adder3(const T* __restrict__ g0, const T* __restrict__ g1,
+__global__ void __launch_bounds__(256) k_ks_adder3(const T* __restrict__ g0,
+                                                   const T* __restrict__ g1, 
                                                    const T* __restrict__ p0, const T* __restrict__ p1,
                                                    T* __restrict__ og0, T* __restrict__ og1,
                                                    int64_t n, int nlev, KeySrc keys, Nonces8 nn,
@@ -804,7 +853,8 @@ __global__ void __launch_bounds__(256) k_ks_adder3(const T* __restrict__ g0, con
 // and pk' through LDS) run the whole carry chain from LDS -- one keystream latency instead
 // of one per level.  Same masks, same logic: bitwise k_ks_adder3's result.
 template <class T>
-__global__ void __launch_bounds__(256) k_ks_adder3p(const T* __restrict__ g0, const T* __restrict__ g1,
+__global__ void __launch_bounds__(256) k_ks_adder3p(const T* __restrict__ g0,
+                                                    const T* __restrict__ g1, 
                                                     const T* __restrict__ p0, const T* __restrict__ p1,
                                                     T* __restrict__ og0, T* __restrict__ og1,
                                                     int64_t n, int nlev, KeySrc keys, Nonces8 nn,
@@ -1021,7 +1071,8 @@ __global__ void __launch_bounds__(256) k_bitdec3(const T* __restrict__ x0, const
 // share-wise add of y -- bitwise the sub + mul + add kernels it replaces.  Latency form:
 // the block's 3 x EPB keystream chunks one per thread, then EPB threads finish.
 template <class T>
-__global__ void __launch_bounds__(256) k_mux3_lat(const T* __restrict__ s0, const T* __restrict__ s1,
+__global__ void __launch_bounds__(256) k_mux3_lat(const T* __restrict__ s0,
+                                                  const T* __restrict__ s1, 
                                                   const T* __restrict__ x0, const T* __restrict__ x1,
                                                   const T* __restrict__ y0, const T* __restrict__ y1,
                                                   T* __restrict__ out0, T* __restrict__ out1,
@@ -1104,7 +1155,7 @@ __global__ void __launch_bounds__(256) k_mul_rows_add(const T* __restrict__ a,
 // o_y = a_y * f + (which[y] ? c : 0) -- the scaled integer-part factors plus the public 1
 // on this party's copies of x_0, one launch instead of two multiplies and an add.
 template <class T>
-__global__ void __launch_bounds__(256) k_mul_add2(Pair<T> p, int64_t n, const T* __restrict__ c) {
+__device__ __forceinline__ void d_mul_add2(const Pair<T>& p, int64_t n, const T* __restrict__ c) {
   const int y = blockIdx.y;
   const T* __restrict__ a = p.a[y];
   const T* __restrict__ f = p.b[0];
@@ -1113,6 +1164,11 @@ __global__ void __launch_bounds__(256) k_mul_add2(Pair<T> p, int64_t n, const T*
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
     out[i] = a[i] * f[i] + cv;
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) k_mul_add2(Pair<T> p, int64_t n, const T* __restrict__ c) {
+  d_mul_add2<T>(p, n, c);
 }
 
 // The adder's sum after the last level, both share components: p ^ ((g ^ t) << 1).
@@ -1133,7 +1189,8 @@ __global__ void __launch_bounds__(256) k_ks_sum2(const T* __restrict__ p0, const
 // t0 (mx_ks_cross1x_s) the level's g is g ^ t -- the previous level's xor, folded in --
 // and is written to go0 / go1 for the next level.
 template <class T>
-__global__ void __launch_bounds__(256) k_ks_cross1(const T* __restrict__ g0, const T* __restrict__ g1,
+__global__ void __launch_bounds__(256) k_ks_cross1(const T* __restrict__ g0,
+                                                   const T* __restrict__ g1, 
                                                    const T* __restrict__ p0, const T* __restrict__ p1,
                                                    T* __restrict__ z, int64_t n, int d, int both,
                                                    KeySrc keys, uint64_t nonce,
@@ -1176,11 +1233,12 @@ __global__ void __launch_bounds__(256) k_ks_cross1(const T* __restrict__ g0, con
 // thread into LDS, then every thread finishes elements -- one ChaCha block on the critical
 // path instead of two (four with both ANDs) in sequence.  Same chunks, same values.
 template <class T>
-__global__ void __launch_bounds__(256)
-    k_ks_cross1_lat(const T* __restrict__ g0, const T* __restrict__ g1, const T* __restrict__ p0,
-                    const T* __restrict__ p1, T* __restrict__ z, int64_t n, int d, int both,
-                    KeySrc keys, uint64_t nonce, const T* __restrict__ t0, const T* __restrict__ t1,
-                    T* __restrict__ go0, T* __restrict__ go1) {
+__device__ __forceinline__ void d_ks_cross1_lat(const T* __restrict__ g0, const T* __restrict__ g1,
+                                                const T* __restrict__ p0, const T* __restrict__ p1,
+                                                T* __restrict__ z, int64_t n, int d, int both,
+                                                const KeySrc& keys, uint64_t nonce,
+                                                const T* __restrict__ t0, const T* __restrict__ t1,
+                                                T* __restrict__ go0, T* __restrict__ go1) {
   constexpr int EPB = 128;
   __shared__ uint32_t rks[2][kKeyWords];
   __shared__ uint64_t kl[2][EPB], kh[2][EPB];
@@ -1222,6 +1280,32 @@ __global__ void __launch_bounds__(256)
     __syncthreads();
   }
 }
+
+template <class T>
+__global__ void __launch_bounds__(256) k_ks_cross1_lat(const T* __restrict__ g0,
+                                                       const T* __restrict__ g1,
+                                                       const T* __restrict__ p0,
+                                                       const T* __restrict__ p1, T* __restrict__ z,
+                                                       int64_t n, int d, int both, KeySrc keys,
+                                                       uint64_t nonce, const T* __restrict__ t0,
+                                                       const T* __restrict__ t1,
+                                                       T* __restrict__ go0, T* __restrict__ go1) {
+  d_ks_cross1_lat<T>(g0, g1, p0, p1, z, n, d, both, keys, nonce, t0, t1, go0, go1);
+}
+
+// party-batched twins for the composed one-GPU replay (party_batch.h)
+MX_X3(k_binary<u64>, d_binary<u64>);
+MX_X3(k_binary<u128>, d_binary<u128>);
+MX_X3(k_lincomb2<u64>, d_lincomb2<u64>);
+MX_X3(k_lincomb2<u128>, d_lincomb2<u128>);
+MX_X3(k_addn_decode<u64>, d_addn_decode<u64>);
+MX_X3(k_addn_decode<u128>, d_addn_decode<u128>);
+MX_X3(k_rss_cross<u64>, d_rss_cross<u64>);
+MX_X3(k_rss_cross<u128>, d_rss_cross<u128>);
+MX_X3(k_mul_add2<u64>, d_mul_add2<u64>);
+MX_X3(k_mul_add2<u128>, d_mul_add2<u128>);
+MX_X3(k_ks_cross1_lat<u64>, d_ks_cross1_lat<u64>);
+MX_X3(k_ks_cross1_lat<u128>, d_ks_cross1_lat<u128>);
 
 template <class T>
 bool ks_lat_launch(const void* g0, const void* g1, const void* t0, const void* t1, void* go0,
@@ -1486,7 +1570,8 @@ __global__ void __launch_bounds__(256) k_mul_trunc3(
 }
 
 template <class T>
-__global__ void __launch_bounds__(256) k_prf_expand(T* __restrict__ out, int64_t n, int nkeys, KeySrc keys,
+__global__ void __launch_bounds__(256) k_prf_expand(T* __restrict__ out, int64_t n, int nkeys,
+                                                    KeySrc keys, 
                              uint64_t nonce) {
   __shared__ uint32_t rks[4][kKeyWords];
   stage_keys(rks, keys, nkeys);
@@ -1517,7 +1602,8 @@ __global__ void __launch_bounds__(256) k_prf_expand(T* __restrict__ out, int64_t
 // Reference (VALU) ring GEMM: 16x16 output tile per block, K staged through LDS.
 // a_bs / b_bs: batch strides in elements (0: one operand broadcast over the batch).
 template <class T, int TS>
-__global__ void __launch_bounds__(256) k_gemm_valu(int64_t M, int64_t N, int64_t K, const T* __restrict__ A0,
+__global__ void __launch_bounds__(256) k_gemm_valu(int64_t M, int64_t N, int64_t K,
+                                                   const T* __restrict__ A0, 
                             const T* __restrict__ A1, const T* __restrict__ B0,
                             const T* __restrict__ B1, int mode, T* __restrict__ C,
                             int accumulate, int64_t a_bs, int64_t b_bs) {

@@ -8,6 +8,7 @@
 
 #include "bits_party.h"
 #include "moosex.h"
+#include "party_batch.h"
 #include "prf_dev.h"
 
 using u64 = uint64_t;
@@ -36,10 +37,11 @@ __device__ inline void stage(const uint32_t (*rks)[mxd::kKeyWords], const Str& s
 }
 
 template <class T>
-__global__ void __launch_bounds__(256)
-    k_front(int role, int64_t n, const T* __restrict__ xa, const T* __restrict__ xb,
-            const T* __restrict__ arecv, T* __restrict__ msg, T* __restrict__ z,
-            T* __restrict__ p0, T* __restrict__ p1, mxd::KeySrc keys, Str ss) {
+__device__ __forceinline__ void d_front(int role, int64_t n, const T* __restrict__ xa,
+                                        const T* __restrict__ xb, const T* __restrict__ arecv,
+                                        T* __restrict__ msg, T* __restrict__ z, T* __restrict__ p0,
+                                        T* __restrict__ p1, const mxd::KeySrc& keys,
+                                        const Str& ss) {
   __shared__ uint32_t rks[2][mxd::kKeyWords];
   __shared__ uint64_t kl[3][EPB], kh[3][EPB];
   mxd::stage_keys(rks, keys, 2);
@@ -68,6 +70,15 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+template <class T>
+__global__ void __launch_bounds__(256) k_front(int role, int64_t n, const T* __restrict__ xa,
+                                               const T* __restrict__ xb,
+                                               const T* __restrict__ arecv, T* __restrict__ msg,
+                                               T* __restrict__ z, T* __restrict__ p0,
+                                               T* __restrict__ p1, mxd::KeySrc keys, Str ss) {
+  d_front<T>(role, n, xa, xb, arecv, msg, z, p0, p1, keys, ss);
+}
+
 // source bit of component c at (plane row, element e): from the adder's sum words, or from
 // its raw (p, g, t) of the last level (g == null: s are sum words)
 template <class T>
@@ -77,14 +88,15 @@ __device__ __forceinline__ T src_bit(const T* s, const T* g, const T* t, int64_t
 }
 
 template <class T>
-__global__ void __launch_bounds__(256)
-    k_b2a(int phase, int role, int64_t S, int start, int count, int xbit, int blocks,
-          const T* __restrict__ s0,
-          const T* __restrict__ s1, const T* __restrict__ g0, const T* __restrict__ g1,
-          const T* __restrict__ t0, const T* __restrict__ t1, const T* __restrict__ arecv,
-          T* __restrict__ msg, T* __restrict__ z, T* __restrict__ base0, T* __restrict__ base1,
-          const T* __restrict__ zr, T* __restrict__ out0, T* __restrict__ out1,
-          mxd::KeySrc keys, Str ss) {
+__device__ __forceinline__ void d_b2a(int phase, int role, int64_t S, int start, int count,
+                                      int xbit, int blocks, const T* __restrict__ s0,
+                                      const T* __restrict__ s1, const T* __restrict__ g0,
+                                      const T* __restrict__ g1, const T* __restrict__ t0,
+                                      const T* __restrict__ t1, const T* __restrict__ arecv,
+                                      T* __restrict__ msg, T* __restrict__ z, T* __restrict__ base0,
+                                      T* __restrict__ base1, const T* __restrict__ zr,
+                                      T* __restrict__ out0, T* __restrict__ out1,
+                                      const mxd::KeySrc& keys, const Str& ss) {
   const int64_t n = S * count;
   if (phase == 2) {  // out = base - 2 (z, z_received)
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
@@ -131,17 +143,33 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+template <class T>
+__global__ void __launch_bounds__(256) k_b2a(int phase, int role, int64_t S, int start, int count,
+                                             int xbit, int blocks, const T* __restrict__ s0,
+                                             const T* __restrict__ s1, const T* __restrict__ g0,
+                                             const T* __restrict__ g1, const T* __restrict__ t0,
+                                             const T* __restrict__ t1, const T* __restrict__ arecv,
+                                             T* __restrict__ msg, T* __restrict__ z,
+                                             T* __restrict__ base0, T* __restrict__ base1,
+                                             const T* __restrict__ zr, T* __restrict__ out0,
+                                             T* __restrict__ out1, mxd::KeySrc keys, Str ss) {
+  d_b2a<T>(phase, role, S, start, count, xbit, blocks, s0, s1, g0, g1, t0, t1, arecv, msg, z, base0,
+           base1, zr, out0, out1, keys, ss);
+}
+
 // Throughput form of phases 0 / 1 (larger B2As, e.g. all bit planes of a decomposition): one
 // thread per ChaCha block index of every stream the role draws, its 4 chunks' elements
 // finished from registers -- a quarter of the latency form's keystream work (which computes a
 // whole block for each chunk), the same chunk -> element mapping (so bitwise the same).
 template <class T>
-__global__ void __launch_bounds__(256)
-    k_b2a_tp(int role, int64_t S, int start, int count, int xbit, int blocks,
-             const T* __restrict__ s0, const T* __restrict__ s1, const T* __restrict__ g0,
-             const T* __restrict__ g1, const T* __restrict__ t0, const T* __restrict__ t1,
-             const T* __restrict__ arecv, T* __restrict__ msg, T* __restrict__ z,
-             T* __restrict__ base0, T* __restrict__ base1, mxd::KeySrc keys, Str ss) {
+__device__ __forceinline__ void d_b2a_tp(int role, int64_t S, int start, int count, int xbit,
+                                         int blocks, const T* __restrict__ s0,
+                                         const T* __restrict__ s1, const T* __restrict__ g0,
+                                         const T* __restrict__ g1, const T* __restrict__ t0,
+                                         const T* __restrict__ t1, const T* __restrict__ arecv,
+                                         T* __restrict__ msg, T* __restrict__ z,
+                                         T* __restrict__ base0, T* __restrict__ base1,
+                                         const mxd::KeySrc& keys, const Str& ss) {
   __shared__ uint32_t rks[2][mxd::kKeyWords];
   mxd::stage_keys(rks, keys, 2);
   constexpr int P = mxd::Lane<T>::kPer;
@@ -190,6 +218,27 @@ __global__ void __launch_bounds__(256)
     }
   }
 }
+
+template <class T>
+__global__ void __launch_bounds__(256) k_b2a_tp(int role, int64_t S, int start, int count, int xbit,
+                                                int blocks, const T* __restrict__ s0,
+                                                const T* __restrict__ s1, const T* __restrict__ g0,
+                                                const T* __restrict__ g1, const T* __restrict__ t0,
+                                                const T* __restrict__ t1,
+                                                const T* __restrict__ arecv, T* __restrict__ msg,
+                                                T* __restrict__ z, T* __restrict__ base0,
+                                                T* __restrict__ base1, mxd::KeySrc keys, Str ss) {
+  d_b2a_tp<T>(role, S, start, count, xbit, blocks, s0, s1, g0, g1, t0, t1, arecv, msg, z, base0,
+              base1, keys, ss);
+}
+
+// party-batched twins for the composed one-GPU replay (party_batch.h)
+MX_X3(k_front<u64>, d_front<u64>);
+MX_X3(k_front<u128>, d_front<u128>);
+MX_X3(k_b2a<u64>, d_b2a<u64>);
+MX_X3(k_b2a<u128>, d_b2a<u128>);
+MX_X3(k_b2a_tp<u64>, d_b2a_tp<u64>);
+MX_X3(k_b2a_tp<u128>, d_b2a_tp<u128>);
 
 Str streams(int role, const uint64_t* nn) {
   // nn = (n1, n_g); role 0: (own, n1), role 2: (next, n1); then (own, n_g), (next, n_g)

@@ -23,6 +23,7 @@
 #include <cstdlib>
 
 #include "moosex.h"
+#include "party_batch.h"
 #include "prf_dev.h"
 #include "ring_common.h"
 #include "rss_fused.h"
@@ -134,9 +135,9 @@ __device__ __forceinline__ T* job_out(const Jobs& js, const Loc<T>& l, int which
 // z2 of the jobs' values (main != 0), and the dealer P2's rt1 / rm1 and its new shares
 // (dealer != 0; independent of the values, so it may run before they exist).
 template <class T>
-__global__ void __launch_bounds__(256)
-    k_jobs_r0(Jobs js, int64_t n, int m, int role, int main, int dealer, T* __restrict__ msg,
-              T* __restrict__ msg_rt, u64* __restrict__ msg_rm, mxd::KeySrc keys,
+__device__ __forceinline__ void
+    d_jobs_r0(const Jobs& js, int64_t n, int m, int role, int main, int dealer, T* __restrict__ msg,
+              T* __restrict__ msg_rt, u64* __restrict__ msg_rm, const mxd::KeySrc& keys,
               uint64_t n_a, uint64_t n_r0, uint64_t n_r1, uint64_t n_t, uint64_t n_m,
               uint64_t n_z0, uint64_t n_z2) {
   __shared__ uint32_t rks[mxd::kMaxKeySlots][mxd::kKeyWords];
@@ -214,13 +215,23 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+template <class T>
+__global__ void __launch_bounds__(256)
+    k_jobs_r0(Jobs js, int64_t n, int m, int role, int main, int dealer, T* __restrict__ msg,
+              T* __restrict__ msg_rt, u64* __restrict__ msg_rm, mxd::KeySrc keys,
+              uint64_t n_a, uint64_t n_r0, uint64_t n_r1, uint64_t n_t, uint64_t n_m,
+              uint64_t n_z0, uint64_t n_z2) {
+  d_jobs_r0<T>(js, n, m, role, main, dealer, msg, msg_rt, msg_rm, keys, n_a, n_r0, n_r1, n_t,
+               n_m, n_z0, n_z2);
+}
+
 // Round 1 (k_dot_tail_r1, one component): P0 / P1 open c, w = y - z; P0's o0 = z0, P1's
 // o1 = z2 at the jobs' output rows.
 template <class T>
-__global__ void __launch_bounds__(256)
-    k_jobs_r1(Jobs js, int64_t n, int m, int role, const T* __restrict__ mine,
+__device__ __forceinline__ void
+    d_jobs_r1(const Jobs& js, int64_t n, int m, int role, const T* __restrict__ mine,
               const T* __restrict__ other, const T* __restrict__ z2m, const T* __restrict__ rt,
-              const u64* __restrict__ rm, T* __restrict__ wo, mxd::KeySrc keys, uint64_t n_t,
+              const u64* __restrict__ rm, T* __restrict__ wo, const mxd::KeySrc& keys, uint64_t n_t,
               uint64_t n_m, uint64_t n_z0, uint64_t n_z2) {
   __shared__ uint32_t rks[mxd::kMaxKeySlots][mxd::kKeyWords];
   mxd::stage_keys(rks, keys, 2);
@@ -266,14 +277,29 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// Round 2 (k_dot_tail_r2, one component): P0's o1 / P1's o0 = w0 + w1.
 template <class T>
 __global__ void __launch_bounds__(256)
-    k_jobs_r2(Jobs js, int64_t n, int role, const T* __restrict__ a, const T* __restrict__ b) {
+    k_jobs_r1(Jobs js, int64_t n, int m, int role, const T* __restrict__ mine,
+              const T* __restrict__ other, const T* __restrict__ z2m, const T* __restrict__ rt,
+              const u64* __restrict__ rm, T* __restrict__ wo, mxd::KeySrc keys, uint64_t n_t,
+              uint64_t n_m, uint64_t n_z0, uint64_t n_z2) {
+  d_jobs_r1<T>(js, n, m, role, mine, other, z2m, rt, rm, wo, keys, n_t, n_m, n_z0, n_z2);
+}
+
+// Round 2 (k_dot_tail_r2, one component): P0's o1 / P1's o0 = w0 + w1.
+template <class T>
+__device__ __forceinline__ void
+    d_jobs_r2(const Jobs& js, int64_t n, int role, const T* __restrict__ a, const T* __restrict__ b) {
   if (role != 0 && role != 1) return;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
     *job_out<T>(js, locate<T>(js, i), role == 0 ? 1 : 0) = a[i] + b[i];
+}
+
+template <class T>
+__global__ void __launch_bounds__(256)
+    k_jobs_r2(Jobs js, int64_t n, int role, const T* __restrict__ a, const T* __restrict__ b) {
+  d_jobs_r2<T>(js, n, role, a, b);
 }
 
 
@@ -291,10 +317,10 @@ struct Streams {
 };
 
 template <class T>
-__global__ void __launch_bounds__(256)
-    k_jobs_r0_lat(Jobs js, int64_t n, int m, int role, int main, int dealer, T* __restrict__ msg,
-                  T* __restrict__ msg_rt, u64* __restrict__ msg_rm, mxd::KeySrc keys,
-                  Streams ss) {
+__device__ __forceinline__ void
+    d_jobs_r0_lat(const Jobs& js, int64_t n, int m, int role, int main, int dealer, T* __restrict__ msg,
+                  T* __restrict__ msg_rt, u64* __restrict__ msg_rm, const mxd::KeySrc& keys,
+                  const Streams& ss) {
   // streams: main 0..1 (P0: a, r; P1: b, r; P2: a, b), dealer 2..7 (P2: r0, r1, t, m, z0, z2)
   __shared__ uint32_t rks[2][mxd::kKeyWords];
   __shared__ uint64_t kl[8][kLatEpb], kh[8][kLatEpb];
@@ -358,10 +384,18 @@ __global__ void __launch_bounds__(256)
 
 template <class T>
 __global__ void __launch_bounds__(256)
-    k_jobs_r1_lat(Jobs js, int64_t n, int m, int role, const T* __restrict__ mine,
+    k_jobs_r0_lat(Jobs js, int64_t n, int m, int role, int main, int dealer, T* __restrict__ msg,
+                  T* __restrict__ msg_rt, u64* __restrict__ msg_rm, mxd::KeySrc keys,
+                  Streams ss) {
+  d_jobs_r0_lat<T>(js, n, m, role, main, dealer, msg, msg_rt, msg_rm, keys, ss);
+}
+
+template <class T>
+__device__ __forceinline__ void
+    d_jobs_r1_lat(const Jobs& js, int64_t n, int m, int role, const T* __restrict__ mine,
                   const T* __restrict__ other, const T* __restrict__ z2m,
                   const T* __restrict__ rt, const u64* __restrict__ rm, T* __restrict__ wo,
-                  mxd::KeySrc keys, Streams ss) {
+                  const mxd::KeySrc& keys, const Streams& ss) {
   // streams: P0 t, m, z0 (own); P1 z2 (next) -- at index 2
   __shared__ uint32_t rks[2][mxd::kKeyWords];
   __shared__ uint64_t kl[3][kLatEpb], kh[3][kLatEpb];
@@ -406,6 +440,26 @@ __global__ void __launch_bounds__(256)
     __syncthreads();
   }
 }
+
+template <class T>
+__global__ void __launch_bounds__(256)
+    k_jobs_r1_lat(Jobs js, int64_t n, int m, int role, const T* __restrict__ mine,
+                  const T* __restrict__ other, const T* __restrict__ z2m,
+                  const T* __restrict__ rt, const u64* __restrict__ rm, T* __restrict__ wo,
+                  mxd::KeySrc keys, Streams ss) {
+  d_jobs_r1_lat<T>(js, n, m, role, mine, other, z2m, rt, rm, wo, keys, ss);
+}
+
+// party-batched twins for the composed one-GPU replay (party_batch.h)
+MX_X3(k_jobs_r0<u128>, d_jobs_r0<u128>);
+MX_X3(k_jobs_r1<u64>, d_jobs_r1<u64>);
+MX_X3(k_jobs_r1<u128>, d_jobs_r1<u128>);
+MX_X3(k_jobs_r2<u64>, d_jobs_r2<u64>);
+MX_X3(k_jobs_r2<u128>, d_jobs_r2<u128>);
+MX_X3(k_jobs_r0_lat<u64>, d_jobs_r0_lat<u64>);
+MX_X3(k_jobs_r0_lat<u128>, d_jobs_r0_lat<u128>);
+MX_X3(k_jobs_r1_lat<u64>, d_jobs_r1_lat<u64>);
+MX_X3(k_jobs_r1_lat<u128>, d_jobs_r1_lat<u128>);
 
 // the latency forms run while the launch has at most this many chunk positions
 constexpr int64_t kLatMaxChunks = 1 << 14;

@@ -19,6 +19,7 @@
 
 #include "prf_dev.h"
 #include "moosex.h"
+#include "party_batch.h"
 #include "ring_common.h"
 #include "rss_fused.h"
 
@@ -39,12 +40,13 @@ struct Roles {
        g += (int64_t)gridDim.x * blockDim.x)
 
 template <class T>
-__global__ void __launch_bounds__(256)
-    k_trunc_party_r0(int64_t n, int m, Roles roles, const T* __restrict__ s0,
-                     const T* __restrict__ s1, T* __restrict__ msg, u64* __restrict__ msg_rm,
-                     T* __restrict__ out0, T* __restrict__ out1, mxd::KeySrc keys, uint64_t n_r0,
-                     uint64_t n_r1, uint64_t n_t, uint64_t n_m, uint64_t n_z0, uint64_t n_z2,
-                     int ncomp) {
+__device__ __forceinline__ void d_trunc_party_r0(int64_t n, int m, const Roles& roles,
+                                                 const T* __restrict__ s0, const T* __restrict__ s1,
+                                                 T* __restrict__ msg, u64* __restrict__ msg_rm,
+                                                 T* __restrict__ out0, T* __restrict__ out1,
+                                                 const mxd::KeySrc& keys, uint64_t n_r0,
+                                                 uint64_t n_r1, uint64_t n_t, uint64_t n_m,
+                                                 uint64_t n_z0, uint64_t n_z2, int ncomp) {
   __shared__ uint32_t rks[mxd::kMaxKeySlots][mxd::kKeyWords];
   mxd::stage_keys(rks, keys, 2 * ncomp);
   constexpr int P = mxd::Lane<T>::kPer;
@@ -124,12 +126,29 @@ __global__ void __launch_bounds__(256)
 }
 
 template <class T>
-__global__ void __launch_bounds__(256)
-    k_trunc_party_r1(int64_t n, int m, Roles roles, const T* __restrict__ msg,
-                     const T* __restrict__ rmk, const T* __restrict__ rrt,
-                     const u64* __restrict__ rrm, T* __restrict__ w, T* __restrict__ out0,
-                     T* __restrict__ out1, mxd::KeySrc keys, uint64_t n_t, uint64_t n_m,
-                     uint64_t n_z0, uint64_t n_z2, int ncomp) {
+__global__ void __launch_bounds__(256) k_trunc_party_r0(int64_t n, int m, Roles roles,
+                                                        const T* __restrict__ s0,
+                                                        const T* __restrict__ s1,
+                                                        T* __restrict__ msg,
+                                                        u64* __restrict__ msg_rm,
+                                                        T* __restrict__ out0, T* __restrict__ out1,
+                                                        mxd::KeySrc keys, uint64_t n_r0,
+                                                        uint64_t n_r1, uint64_t n_t, uint64_t n_m,
+                                                        uint64_t n_z0, uint64_t n_z2, int ncomp) {
+  d_trunc_party_r0<T>(n, m, roles, s0, s1, msg, msg_rm, out0, out1, keys, n_r0, n_r1, n_t, n_m,
+                      n_z0, n_z2, ncomp);
+}
+
+template <class T>
+__device__ __forceinline__ void d_trunc_party_r1(int64_t n, int m, const Roles& roles,
+                                                 const T* __restrict__ msg,
+                                                 const T* __restrict__ rmk,
+                                                 const T* __restrict__ rrt,
+                                                 const u64* __restrict__ rrm, T* __restrict__ w,
+                                                 T* __restrict__ out0, T* __restrict__ out1,
+                                                 const mxd::KeySrc& keys, uint64_t n_t,
+                                                 uint64_t n_m, uint64_t n_z0, uint64_t n_z2,
+                                                 int ncomp) {
   __shared__ uint32_t rks[mxd::kMaxKeySlots][mxd::kKeyWords];
   mxd::stage_keys(rks, keys, 2 * ncomp);
   constexpr int P = mxd::Lane<T>::kPer;
@@ -190,9 +209,24 @@ __global__ void __launch_bounds__(256)
 }
 
 template <class T>
-__global__ void __launch_bounds__(256)
-    k_share_party(int kind, int64_t n, Roles rel, const void* __restrict__ xv, T* __restrict__ out0,
-                  T* __restrict__ out1, mxd::KeySrc keys, uint64_t n1, uint64_t na, int ncomp) {
+__global__ void __launch_bounds__(256) k_trunc_party_r1(int64_t n, int m, Roles roles,
+                                                        const T* __restrict__ msg,
+                                                        const T* __restrict__ rmk,
+                                                        const T* __restrict__ rrt,
+                                                        const u64* __restrict__ rrm,
+                                                        T* __restrict__ w, T* __restrict__ out0,
+                                                        T* __restrict__ out1, mxd::KeySrc keys,
+                                                        uint64_t n_t, uint64_t n_m, uint64_t n_z0,
+                                                        uint64_t n_z2, int ncomp) {
+  d_trunc_party_r1<T>(n, m, roles, msg, rmk, rrt, rrm, w, out0, out1, keys, n_t, n_m, n_z0, n_z2,
+                      ncomp);
+}
+
+template <class T>
+__device__ __forceinline__ void d_share_party(int kind, int64_t n, const Roles& rel,
+                                              const void* __restrict__ xv, T* __restrict__ out0,
+                                              T* __restrict__ out1, const mxd::KeySrc& keys,
+                                              uint64_t n1, uint64_t na, int ncomp) {
   const bool mir = kind & MX_SHARE_MIRROR;
   kind &= ~MX_SHARE_MIRROR;
   const T* x = (const T*)xv;
@@ -250,6 +284,15 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+template <class T>
+__global__ void __launch_bounds__(256) k_share_party(int kind, int64_t n, Roles rel,
+                                                     const void* __restrict__ xv,
+                                                     T* __restrict__ out0, T* __restrict__ out1,
+                                                     mxd::KeySrc keys, uint64_t n1, uint64_t na,
+                                                     int ncomp) {
+  d_share_party<T>(kind, n, rel, xv, out0, out1, keys, n1, na, ncomp);
+}
+
 inline Roles roles_of(const int* r, int ncomp) {
   Roles o;
   for (int c = 0; c < 3; ++c) o.r[c] = c < ncomp ? r[c] : -1;
@@ -290,11 +333,12 @@ __device__ __forceinline__ T* wp(const WP3& a, int c) {
 }
 
 template <class T>
-__global__ void __launch_bounds__(256)
-    k_dot_tail_r0(int64_t n, int m, Roles roles, CP3 cross, WP3 msg, WP3 msg_rt, WP3 msg_rm,
-                  WP3 out0, WP3 out1, mxd::KeySrc keys, uint64_t n_a, uint64_t n_r0,
-                  uint64_t n_r1, uint64_t n_t, uint64_t n_m, uint64_t n_z0, uint64_t n_z2,
-                  int ncomp) {
+__device__ __forceinline__ void d_dot_tail_r0(int64_t n, int m, const Roles& roles,
+                                              const CP3& cross, const WP3& msg, const WP3& msg_rt,
+                                              const WP3& msg_rm, const WP3& out0, const WP3& out1,
+                                              const mxd::KeySrc& keys, uint64_t n_a, uint64_t n_r0,
+                                              uint64_t n_r1, uint64_t n_t, uint64_t n_m,
+                                              uint64_t n_z0, uint64_t n_z2, int ncomp) {
   __shared__ uint32_t rks[mxd::kMaxKeySlots][mxd::kKeyWords];
   mxd::stage_keys(rks, keys, 2 * ncomp);
   constexpr int P = mxd::Lane<T>::kPer;
@@ -380,13 +424,26 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+template <class T>
+__global__ void __launch_bounds__(256) k_dot_tail_r0(int64_t n, int m, Roles roles, CP3 cross,
+                                                     WP3 msg, WP3 msg_rt, WP3 msg_rm, WP3 out0,
+                                                     WP3 out1, mxd::KeySrc keys, uint64_t n_a,
+                                                     uint64_t n_r0, uint64_t n_r1, uint64_t n_t,
+                                                     uint64_t n_m, uint64_t n_z0, uint64_t n_z2,
+                                                     int ncomp) {
+  d_dot_tail_r0<T>(n, m, roles, cross, msg, msg_rt, msg_rm, out0, out1, keys, n_a, n_r0, n_r1, n_t,
+                   n_m, n_z0, n_z2, ncomp);
+}
+
 // P0 / P1: c = own message + the other's + z2 (rz may be null: the two-term opening of
 // k_trunc_party_r0's protocol), then y, w = y - z and the PRF share of the new sharing.
 template <class T>
-__global__ void __launch_bounds__(256)
-    k_dot_tail_r1(int64_t n, int m, Roles roles, CP3 msg, CP3 rmk, CP3 rz, CP3 rrt, CP3 rrm,
-                  WP3 w, WP3 out0, WP3 out1, mxd::KeySrc keys, uint64_t n_t, uint64_t n_m,
-                  uint64_t n_z0, uint64_t n_z2, int ncomp) {
+__device__ __forceinline__ void d_dot_tail_r1(int64_t n, int m, const Roles& roles, const CP3& msg,
+                                              const CP3& rmk, const CP3& rz, const CP3& rrt,
+                                              const CP3& rrm, const WP3& w, const WP3& out0,
+                                              const WP3& out1, const mxd::KeySrc& keys,
+                                              uint64_t n_t, uint64_t n_m, uint64_t n_z0,
+                                              uint64_t n_z2, int ncomp) {
   __shared__ uint32_t rks[mxd::kMaxKeySlots][mxd::kKeyWords];
   mxd::stage_keys(rks, keys, 2 * ncomp);
   constexpr int P = mxd::Lane<T>::kPer;
@@ -440,10 +497,20 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+template <class T>
+__global__ void __launch_bounds__(256) k_dot_tail_r1(int64_t n, int m, Roles roles, CP3 msg,
+                                                     CP3 rmk, CP3 rz, CP3 rrt, CP3 rrm, WP3 w,
+                                                     WP3 out0, WP3 out1, mxd::KeySrc keys,
+                                                     uint64_t n_t, uint64_t n_m, uint64_t n_z0,
+                                                     uint64_t n_z2, int ncomp) {
+  d_dot_tail_r1<T>(n, m, roles, msg, rmk, rz, rrt, rrm, w, out0, out1, keys, n_t, n_m, n_z0, n_z2,
+                   ncomp);
+}
+
 // out[c] = a[c] + b[c] for the components in role 0 or 1 (P0's s1, P1's s0 = w0 + w1)
 template <class T>
-__global__ void __launch_bounds__(256)
-    k_dot_tail_r2(int64_t n, Roles roles, CP3 a, CP3 b, WP3 out, int ncomp) {
+__device__ __forceinline__ void d_dot_tail_r2(int64_t n, const Roles& roles, const CP3& a,
+                                              const CP3& b, const WP3& out, int ncomp) {
   const int64_t total = n * ncomp;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total;
        g += (int64_t)gridDim.x * blockDim.x) {
@@ -454,6 +521,26 @@ __global__ void __launch_bounds__(256)
     wp<T>(out, c)[i] = cp<T>(a, c)[i] + cp<T>(b, c)[i];
   }
 }
+
+template <class T>
+__global__ void __launch_bounds__(256) k_dot_tail_r2(int64_t n, Roles roles, CP3 a, CP3 b, WP3 out,
+                                                     int ncomp) {
+  d_dot_tail_r2<T>(n, roles, a, b, out, ncomp);
+}
+
+// party-batched twins for the composed one-GPU replay (party_batch.h)
+MX_X3(k_trunc_party_r0<u64>, d_trunc_party_r0<u64>);
+MX_X3(k_trunc_party_r0<u128>, d_trunc_party_r0<u128>);
+MX_X3(k_trunc_party_r1<u64>, d_trunc_party_r1<u64>);
+MX_X3(k_trunc_party_r1<u128>, d_trunc_party_r1<u128>);
+MX_X3(k_share_party<u64>, d_share_party<u64>);
+MX_X3(k_share_party<u128>, d_share_party<u128>);
+MX_X3(k_dot_tail_r0<u64>, d_dot_tail_r0<u64>);
+MX_X3(k_dot_tail_r0<u128>, d_dot_tail_r0<u128>);
+MX_X3(k_dot_tail_r1<u64>, d_dot_tail_r1<u64>);
+MX_X3(k_dot_tail_r1<u128>, d_dot_tail_r1<u128>);
+MX_X3(k_dot_tail_r2<u64>, d_dot_tail_r2<u64>);
+MX_X3(k_dot_tail_r2<u128>, d_dot_tail_r2<u128>);
 
 inline CP3 cp3(const void* const* a, int ncomp) {
   CP3 o{{nullptr, nullptr, nullptr}};

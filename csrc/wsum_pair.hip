@@ -4,6 +4,7 @@
 #include <cstdlib>
 
 #include "moosex.h"
+#include "party_batch.h"
 #include "prf_dev.h"
 #include "wsum_pair.h"
 
@@ -13,10 +14,11 @@ using u128 = unsigned __int128;
 namespace {
 
 template <class T>
-__global__ void __launch_bounds__(256)
-    k_wsum_pair(mxw::WsumArgs<T> a, const T* __restrict__ r0, const T* __restrict__ r1,
-                const T* __restrict__ x0, const T* __restrict__ x1, T* __restrict__ o0,
-                T* __restrict__ o1, T* __restrict__ q0, T* __restrict__ q1) {
+__device__ __forceinline__ void d_wsum_pair(const mxw::WsumArgs<T>& a, const T* __restrict__ r0,
+                                            const T* __restrict__ r1, const T* __restrict__ x0,
+                                            const T* __restrict__ x1, T* __restrict__ o0,
+                                            T* __restrict__ o1, T* __restrict__ q0,
+                                            T* __restrict__ q1) {
   const int64_t n = 2 * a.L;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < n;
        g += (int64_t)gridDim.x * blockDim.x) {
@@ -28,6 +30,16 @@ __global__ void __launch_bounds__(256)
     for (int b = 0; b < a.nblk; ++b) o[(int64_t)b * a.L + i] = s + (pub ? a.cb[b] : (T)0);
     if (a.has2) (c ? q1 : q0)[i] = a.m2 * s + (pub ? a.c2 : (T)0);
   }
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) k_wsum_pair(mxw::WsumArgs<T> a, const T* __restrict__ r0,
+                                                   const T* __restrict__ r1,
+                                                   const T* __restrict__ x0,
+                                                   const T* __restrict__ x1, T* __restrict__ o0,
+                                                   T* __restrict__ o1, T* __restrict__ q0,
+                                                   T* __restrict__ q1) {
+  d_wsum_pair<T>(a, r0, r1, x0, x1, o0, o1, q0, q1);
 }
 
 // Group form: kGroup lanes per output element, lane j summing rows j, j + kGroup, ... (a
@@ -51,10 +63,11 @@ __device__ __forceinline__ T shfl_xor_ring(T v, int m) {
 }
 
 template <class T>
-__global__ void __launch_bounds__(256)
-    k_wsum_pair_g(mxw::WsumArgs<T> a, const T* __restrict__ r0, const T* __restrict__ r1,
-                  const T* __restrict__ x0, const T* __restrict__ x1, T* __restrict__ o0,
-                  T* __restrict__ o1, T* __restrict__ q0, T* __restrict__ q1) {
+__device__ __forceinline__ void d_wsum_pair_g(const mxw::WsumArgs<T>& a, const T* __restrict__ r0,
+                                              const T* __restrict__ r1, const T* __restrict__ x0,
+                                              const T* __restrict__ x1, T* __restrict__ o0,
+                                              T* __restrict__ o1, T* __restrict__ q0,
+                                              T* __restrict__ q1) {
   // the grid covers every element once (kGroup lanes each): no stride loop, so all lanes
   // of a group reach the butterfly
   const int64_t n = 2 * a.L;
@@ -79,6 +92,22 @@ __global__ void __launch_bounds__(256)
     if (a.has2) (c ? q1 : q0)[i] = a.m2 * s + (pub ? a.c2 : (T)0);
   }
 }
+
+template <class T>
+__global__ void __launch_bounds__(256) k_wsum_pair_g(mxw::WsumArgs<T> a, const T* __restrict__ r0,
+                                                     const T* __restrict__ r1,
+                                                     const T* __restrict__ x0,
+                                                     const T* __restrict__ x1, T* __restrict__ o0,
+                                                     T* __restrict__ o1, T* __restrict__ q0,
+                                                     T* __restrict__ q1) {
+  d_wsum_pair_g<T>(a, r0, r1, x0, x1, o0, o1, q0, q1);
+}
+
+// party-batched twins for the composed one-GPU replay (party_batch.h)
+MX_X3(k_wsum_pair<u64>, d_wsum_pair<u64>);
+MX_X3(k_wsum_pair<u128>, d_wsum_pair<u128>);
+MX_X3(k_wsum_pair_g<u64>, d_wsum_pair_g<u64>);
+MX_X3(k_wsum_pair_g<u128>, d_wsum_pair_g<u128>);
 
 }  // namespace
 

@@ -221,6 +221,9 @@ _SIGS = {
     "mx_stream_cumask": (c_int, [c_vp, c_int, c_vp]),
     "mx_stream_destroy": (c_int, [c_vp]),
     "mx_graph_compose": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    # (n, kind, child, dst, src, bytes, party, stats[4], graph*, exec*): party-batched chain
+    "mx_graph_compose_merged": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                        c_vp]),
     "mx_graph_dot": (c_int, [c_vp, ctypes.c_char_p, ctypes.c_uint]),
     "mx_graph_launch": (c_int, [c_vp, c_vp]),
     "mx_enable_peer": (c_int, [c_int, c_int]),

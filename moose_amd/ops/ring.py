@@ -2250,23 +2250,32 @@ def _ring_words(values, bits):
 
 
 def wsum_pair(bits, L, rows=None, weights=(), x=None, wx=0, pub=(False, False), cblk=(0,),
-              second=None, like=None):
+              second=None, like=None, lead=False):
     """Per-party fused weighted sums over both share components (csrc/wsum_pair.h):
     s_c = sum_k weights[k] rows_c[k] + wx x_c; returns (o0, o1) of nblk = len(cblk) blocks
     of L elements, block b = s_c + cblk[b] on the public slots ``pub`` (this party's copies
     of x_0), and with ``second`` = (m2, c2) also (q0, q1) = m2 s_c + c2 on those slots.
-    ``rows`` = (r0, r1) tensors holding len(weights) rows of L elements, contiguous."""
+    ``rows`` = (r0, r1) tensors holding len(weights) rows of L elements, contiguous.
+    ``lead``: (q0, q1) is block 0 of the outputs instead -- (o0, o1) of 1 + nblk blocks,
+    no concatenation afterwards."""
     ref = like if like is not None else (rows[0] if rows is not None else x[0])
     nrows = len(weights)
     if nrows > 64 or not 1 <= len(cblk) <= 3:
         raise ValueError("wsum_pair: at most 64 rows and 3 blocks")
     dev = ref.device
-    shp = (len(cblk) * L,) + ((2,) if bits == 128 else ())
-    o0 = torch.empty(shp, dtype=torch.int64, device=dev)
-    o1 = torch.empty_like(o0)
+    tail = (2,) if bits == 128 else ()
     q0 = q1 = None
-    if second is not None:
-        q0 = torch.empty(((L,) + ((2,) if bits == 128 else ())), dtype=torch.int64, device=dev)
+    if lead:
+        if second is None:
+            raise ValueError("wsum_pair: lead needs second")
+        b0 = torch.empty(((1 + len(cblk)) * L,) + tail, dtype=torch.int64, device=dev)
+        b1 = torch.empty_like(b0)
+        q0, q1, o0, o1 = b0[:L], b1[:L], b0[L:], b1[L:]
+    else:
+        o0 = torch.empty((len(cblk) * L,) + tail, dtype=torch.int64, device=dev)
+        o1 = torch.empty_like(o0)
+    if second is not None and not lead:
+        q0 = torch.empty(((L,) + tail), dtype=torch.int64, device=dev)
         q1 = torch.empty_like(q0)
     r = [None, None] if rows is None else [t.contiguous() for t in rows]
     xx = [None, None] if x is None else [t.contiguous() for t in x]
@@ -2277,4 +2286,6 @@ def wsum_pair(bits, L, rows=None, weights=(), x=None, wx=0, pub=(False, False), 
         _ring_words([wx], bits), _ring_words([m2], bits), _ring_words([c2], bits),
         _ring_words(cblk, bits), _p(r[0]), _p(r[1]), _p(xx[0]), _p(xx[1]), _p(o0), _p(o1),
         _p(q0), _p(q1), nat.stream_of(o0)), "wsum_pair")
+    if lead:
+        return b0, b1
     return (o0, o1) if second is None else (o0, o1, q0, q1)

@@ -54,23 +54,32 @@ class SPMDTape:
 
     def __init__(self, comp, arguments: dict, identity: str, role_ranks: Dict[str, int],
                  tr, device, storage, ring: int, seed: Optional[int] = None, warm=None,
-                 keep_graph: bool = False):
+                 keep_graph: bool = False, shared_static: Optional[dict] = None):
         """``warm``: the warm-up already ran elsewhere (the in-process parties of
         parallel/threads.py run it together, on threads) -- a dict with the recorded
         ``uploads``, the ``first`` outputs, the session ``stats`` and the number of key
         slots ``keys_n`` it used.  ``keep_graph``: the segments keep their hipGraph (not
-        instantiated until a replay) so a caller can compose them into a larger graph."""
+        instantiated until a replay) so a caller can compose them into a larger graph.
+        ``shared_static``: argument buffers shared by the tapes of one device (the graphs
+        only read them), so a replay uploads each argument once per device."""
         from moose_amd.parallel.spmd import SPMDSession
 
         self.comp, self.device, self.tr = comp, torch.device(device), tr
         self.identity, self.role_ranks, self.seed = identity, dict(role_ranks), seed
         self.static = {}
+        self.owns_static = set()  # the buffers this tape uploads (the others' are shared)
         for k, v in arguments.items():
             if isinstance(v, (np.ndarray, np.generic)) or (
                     isinstance(v, (list, tuple)) and v and not isinstance(v[0], (str, bytes))):
                 a = np.asarray(v)
-                t = numpy_to_torch(a, self.device)
-                t._moose_dtype = dtype_of_numpy(a)
+                t = shared_static.get(k) if shared_static is not None else None
+                if t is None or tuple(t.shape) != a.shape or \
+                        getattr(t, "_moose_dtype", None) != dtype_of_numpy(a):
+                    t = numpy_to_torch(a, self.device)
+                    t._moose_dtype = dtype_of_numpy(a)
+                    self.owns_static.add(k)
+                    if shared_static is not None:
+                        shared_static[k] = t
                 self.static[k] = t
             else:
                 self.static[k] = v
@@ -203,21 +212,20 @@ class SPMDTape:
         decoded), so the staging buffer is free."""
         for k, v in arguments.items():
             t = self.static.get(k)
-            if not isinstance(t, torch.Tensor):
+            if not isinstance(t, torch.Tensor) or k not in self.owns_static:
                 continue
             a = np.asarray(v)
             a = a.view(np.int64) if a.dtype == np.uint64 else a
-            src = torch.from_numpy(np.ascontiguousarray(a).reshape(t.shape))
-            if src.dtype != t.dtype:
-                src = src.to(t.dtype)
             if t.device.type != "cuda":
-                t.copy_(src)
+                src = torch.from_numpy(np.ascontiguousarray(a).reshape(t.shape))
+                t.copy_(src if src.dtype == t.dtype else src.to(t.dtype))
                 continue
             pin = self._pinned.get(k)
-            if pin is None or pin.shape != t.shape or pin.dtype != t.dtype:
-                pin = self._pinned[k] = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
-            pin.copy_(src)
-            t.copy_(pin, non_blocking=True)
+            if pin is None or pin[0].shape != t.shape or pin[0].dtype != t.dtype:
+                pt = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+                pin = self._pinned[k] = (pt, pt.numpy())
+            np.copyto(pin[1], a.reshape(t.shape), casting="unsafe")  # no torch dispatch
+            t.copy_(pin[0], non_blocking=True)
         if self.tap.loads:  # the stored values this replay loads, as arguments
             self.tap.refresh(self.storage)
 

@@ -334,6 +334,9 @@ VALIDATE_STREAMS = os.environ.get("MOOSEX_PARTY_STREAMS_VALIDATE", "1") != "0"
 # branches may run concurrently inside the one launch.  Needs persistent landing buffers
 # (ThreadTransport.prepare_landing; profiles/r5_party_dag_hazard.md)
 DAG_COMPOSE = os.environ.get("MOOSEX_PARTY_GRAPH_DAG", "0") == "1"
+# the composed chain batches the same launch of several parties into one node
+# (csrc/party_batch.h; MOOSEX_PARTY_MERGE=0: one node per launch)
+MERGE_PARTIES = os.environ.get("MOOSEX_PARTY_MERGE", "1") != "0"
 
 
 def chunk_bounds(kinds, per: int):
@@ -476,6 +479,10 @@ class PartyTapes:
         single = (len(set(self.devices)) == 1 and not self.streams_mode
                   and os.environ.get("MOOSEX_PARTY_GRAPH", "1") != "0")
         self.tapes = []
+        # the composed graph runs every party on one stream: the tapes share their argument
+        # buffers, uploaded once per replay
+        self.shared_static = single and not DAG_COMPOSE
+        shared = {}
         for i, ident in enumerate(identities):
             tr = ThreadTransport(i, None, device=self.devices[i], world=n)
             tr.log = warm[ident]["log"]
@@ -488,7 +495,10 @@ class PartyTapes:
                 self.tapes.append(SPMDTape(comp, arguments, ident, role_ranks, tr,
                                            self.devices[i], storage, ring, seed,
                                            warm=warm[ident],
-                                           keep_graph=single or self.streams_mode))
+                                           keep_graph=single or self.streams_mode,
+                                           shared_static=shared.setdefault(
+                                               self.devices[i], {})
+                                           if self.shared_static else None))
         self.streams = [t.stream for t in self.tapes]
         self._copy_streams = {}
         self.actions = self._schedule()
@@ -594,11 +604,17 @@ class PartyTapes:
         acts = self._schedule_rounds() if batched else [
             a if a[0] != "cp" else ("cpb", [(a[1], a[2], a[3], a[4])])
             for a in self.actions if a[0] != "rec"]
-        kinds, child, dst, src, nbytes = [], [], [], [], []
+        # the device key refresh of unseeded tapes as the head of the graph (one captured
+        # launch per party, batched into one node) instead of a host launch per replay
+        keyg = {p: g for p, g in ((p, self._key_graph(t)) for p, t in enumerate(self.tapes))
+                if g is not None} if batched and MERGE_PARTIES else {}
+        acts = [("g", p, g) for p, g in keyg.items()] + acts
+        kinds, child, dst, src, nbytes, party = [], [], [], [], [], []
         descs = []
         for a in acts:
             if a[0] == "g":
                 kinds.append(0)
+                party.append(a[1])
                 child.append(a[2].raw_cuda_graph())
                 dst.append(0)
                 src.append(0)
@@ -608,6 +624,7 @@ class PartyTapes:
             if len(msgs) == 1 or not batched:
                 for _p, _s, t, buf in msgs:
                     kinds.append(1)
+                    party.append(-1)
                     child.append(0)
                     dst.append(buf.data_ptr())
                     src.append(t.data_ptr())
@@ -616,6 +633,7 @@ class PartyTapes:
             descs.append([(t.data_ptr(), buf.data_ptr(), t.numel() * t.element_size())
                           for _p, _s, t, buf in msgs])
             kinds.append(2)
+            party.append(-1)
             child.append(len(msgs))
             dst.append(len(descs) - 1)  # the table's address is filled in below
             src.append(0)
@@ -630,11 +648,33 @@ class PartyTapes:
                 offs.append(table.data_ptr() + 8 * 3 * at)
                 at += len(d)
             dst = [offs[d] if k == 2 else d for k, d in zip(kinds, dst)]
+        arr = lambda ty, xs: (ty * max(1, len(xs)))(*xs)  # noqa: E731
+        if batched and CHUNK_SEGMENTS <= 0 and MERGE_PARTIES:
+            # one chain in which the same launch of 2-3 parties between two rounds is ONE
+            # party-batched node (csrc/party_batch.h)
+            g, ex = ctypes.c_void_p(), ctypes.c_void_p()
+            st = (ctypes.c_int64 * 4)()
+            rc = nat.lib().mx_graph_compose_merged(
+                len(kinds), arr(ctypes.c_int, kinds), arr(ctypes.c_void_p, child),
+                arr(ctypes.c_void_p, dst), arr(ctypes.c_void_p, src),
+                arr(ctypes.c_int64, nbytes), arr(ctypes.c_int, party), st, ctypes.byref(g),
+                ctypes.byref(ex))
+            if rc == 0:
+                self._keys_in_graph = set(keyg)
+                self._key_graphs = keyg  # alive as long as the composed graph
+                self._graph_handles = [(g, ex)]
+                self.graph_nodes = {"segments": kinds.count(0), "copy_nodes": kinds.count(1),
+                                    "copy_batches": kinds.count(2), "executables": 1,
+                                    "nodes": st[0], "merged_away": st[1],
+                                    "party_batched": st[2], "phases": st[3]}
+                return [ex]
+        if keyg:  # not composed with the merged chain: the host refreshes the keys
+            kinds, child, dst, src, nbytes, party = (
+                xs[len(keyg):] for xs in (kinds, child, dst, src, nbytes, party))
         # the total order as one executable, or in chunks of at most CHUNK_SEGMENTS
         # segments launched back to back on one stream
         bounds = (chunk_bounds(kinds, CHUNK_SEGMENTS) if CHUNK_SEGMENTS > 0
                   else [(0, len(kinds))])
-        arr = lambda ty, xs: (ty * max(1, len(xs)))(*xs)  # noqa: E731
         handles = []
         for a, b in bounds:
             m = b - a
@@ -655,6 +695,22 @@ class PartyTapes:
         self.graph_nodes = {"segments": kinds.count(0), "copy_nodes": kinds.count(1),
                             "copy_batches": kinds.count(2), "executables": len(handles)}
         return [ex for _, ex in handles]
+
+    def _key_graph(self, tape):
+        """The unseeded tape's device key refresh (runtime/keys.py refresh_device: the
+        replay counter lives in device memory, so a captured launch draws fresh keys at
+        every replay) captured on the tape's stream; None for seeded tapes."""
+        keys = tape.keys
+        if tape.seed is not None or getattr(keys, "_master", None) is None:
+            return None
+        g = torch.cuda.CUDAGraph(keep_graph=True)
+        with torch.cuda.device(tape.device), torch.cuda.stream(tape.stream):
+            g.capture_begin(capture_error_mode="thread_local")
+            try:
+                keys.refresh_device(keys.n)
+            finally:
+                g.capture_end()
+        return g
 
     def _compose_dag(self):
         """The per-action schedule as ONE graph with only the protocol's edges
@@ -1078,6 +1134,16 @@ class PartyTapes:
                             s.wait_event(self._ends[q])
                 tape.copy_arguments(arguments)
                 tape._fill_keys()
+            if self.shared_static:  # shared argument buffers: every upload before any reader
+                evs = []
+                for p in range(n):
+                    e = torch.cuda.Event()
+                    e.record(self.streams[p])
+                    evs.append(e)
+                for p in range(n):
+                    for q in range(n):
+                        if q != p:
+                            self.streams[p].wait_event(evs[q])
             cur = -1
             for a in self.actions:
                 p = a[1]
@@ -1132,8 +1198,10 @@ class PartyTapes:
             for tape in self.tapes:
                 tape.copy_arguments(arguments)
             t1 = time.perf_counter()
-            for tape in self.tapes:
-                tape._fill_keys()
+            in_graph = getattr(self, "_keys_in_graph", ())
+            for p, tape in enumerate(self.tapes):
+                if p not in in_graph:
+                    tape._fill_keys()
             t2 = time.perf_counter()
             for ex in self._composed:
                 nat.check(nat.lib().mx_graph_launch(ex, s.cuda_stream), "graph launch")

@@ -547,13 +547,15 @@ def _poly_powers_sum(sess, x: RepFixed, coeffs, finish=None):
     return rep.lincomb(sess, [(weights[0], t), (1, acc)])
 
 
-def _wsum(sess, rows, weights, x=None, wx=0, cblk=(0,), second=None, nrows=None):
+def _wsum(sess, rows, weights, x=None, wx=0, cblk=(0,), second=None, nrows=None,
+          lead=False):
     """Per-party fused local step (csrc/wsum_pair.h): s = sum_k weights[k] rows[k] + wx x
     over both share components in ONE launch; returns the RepTensor s + cblk[b] (blocks on
     a new leading axis when len(cblk) > 1, the public constants on this party's copies of
-    x_0) and, with ``second`` = (m2, c2), also m2 s + c2.  Bitwise the composition of the
-    separate weighted sum / multiply / add / lincomb steps (ring arithmetic).  None when
-    the session is not a per-party one (the caller runs those steps)."""
+    x_0) and, with ``second`` = (m2, c2), also m2 s + c2 -- with ``lead``, as block 0 of
+    ONE RepTensor of 1 + len(cblk) blocks.  Bitwise the composition of the separate
+    weighted sum / multiply / add / lincomb steps (ring arithmetic).  None when the session
+    is not a per-party one (the caller runs those steps)."""
     from moose_amd.parallel.spmd import Remote
 
     if not WSUM_FUSED or getattr(sess, "party_jobs", None) is None:
@@ -567,7 +569,7 @@ def _wsum(sess, rows, weights, x=None, wx=0, cblk=(0,), second=None, nrows=None)
     if idx is None:
         r = PV(plc, Remote(bits))
         t = RepTensor(plc, bits, "arith", r, r)
-        return t if second is None else (t, t)
+        return t if second is None or lead else (t, t)
     if rows is not None:
         k = len(weights)
         r0, r1 = rows.s0.v.data, rows.s1.v.data
@@ -584,11 +586,13 @@ def _wsum(sess, rows, weights, x=None, wx=0, cblk=(0,), second=None, nrows=None)
         xs = (x.s0.v.data, x.s1.v.data)
     out = R.wsum_pair(bits, L, rows=None if r0 is None else (r0, r1), weights=weights, x=xs,
                       wx=wx, pub=(idx == 0, idx == 2), cblk=cblk, second=second,
-                      like=(r0 if r0 is not None else xs[0]))
+                      like=(r0 if r0 is not None else xs[0]), lead=lead)
+    if lead:
+        nb += 1
     shp = ((nb * per[0],) + per[1:] if nb > 1 else per) + ((2,) if bits == 128 else ())
     o = RepTensor(plc, bits, "arith", PV(plc, R.RT(out[0].reshape(shp), bits)),
                   PV(plc, R.RT(out[1].reshape(shp), bits)))
-    if second is None:
+    if second is None or lead:
         return o
     pshp = per + ((2,) if bits == 128 else ())
     return o, RepTensor(plc, bits, "arith", PV(plc, R.RT(out[2].reshape(pshp), bits)),
@@ -1306,7 +1310,6 @@ def _sign_and_exp_party(sess, x: RepFixed, plus: float = 0.0):
         q -= extra
     C = int(round(math.log2(math.e) * (1 << fc)))
     xt = pend.reshare_untruncated() if pend is not None else x.t
-    z = rep.lincomb(sess, [(C, xt)])
     fx = f + (pend.m if pend is not None else 0)  # x' = xt's fractional bits
     if split:
         # blocks z, x' - T', x' + T', x' (T' = T / C in x's units): |z|'s planes come from
@@ -1315,13 +1318,15 @@ def _sign_and_exp_party(sess, x: RepFixed, plus: float = 0.0):
         # keeps the nominal integ while its value grows)
         Tv = 1 << (F + jn)
         Tx = -(-Tv // C)  # z >= T  <=>  x' >= Tx (x' an integer at fx bits)
-        xs = _wsum(sess, None, (), x=xt, wx=1, cblk=(-Tx, Tx, 0))  # 3 blocks, 1 launch
-        if xs is None:
+        # the four blocks in one launch (z = C x' as block 0), no concatenation
+        zs = _wsum(sess, None, (), x=xt, wx=1, cblk=(-Tx, Tx, 0), second=(C, 0), lead=True)
+        if zs is None:
+            z = rep.lincomb(sess, [(C, xt)])
             T = R.fill((), Tx, bits, sess.device)
             xs = concat(sess, [RepFixed(rep.sub_public(sess, xt, T), fx, integ),
                                RepFixed(rep.add_public(sess, xt, T), fx, integ),
                                RepFixed(xt, fx, integ)], 0).t
-        zs = concat(sess, [RepFixed(z, F, integ), RepFixed(xs, fx, integ)], 0).t
+            zs = concat(sess, [RepFixed(z, F, integ), RepFixed(xs, fx, integ)], 0).t
         nfac = jn + 2
         npad = 1 << (nfac - 1).bit_length()
         extra = npad - nfac  # planes above jn whose factor is 1 (weight 0)
@@ -1340,7 +1345,10 @@ def _sign_and_exp_party(sess, x: RepFixed, plus: float = 0.0):
         if F + npad > bits:
             npad = nint
         # blocks z, x': |z|'s planes from z, the mirror's sign from x' at the ring's msb
-        zs = concat(sess, [RepFixed(z, F, integ), RepFixed(xt, fx, integ)], 0).t
+        zs = _wsum(sess, None, (), x=xt, wx=1, cblk=(0,), second=(C, 0), lead=True)
+        if zs is None:
+            z = rep.lincomb(sess, [(C, xt)])
+            zs = concat(sess, [RepFixed(z, F, integ), RepFixed(xt, fx, integ)], 0).t
         bd = rep.bit_decompose(sess, zs)
         ab = rep.b2a_planes_xor(sess, bd, F - f, f + npad, q, bits, blocks=2,
                                 sbit=bits - 1)  # f + npad planes, then s
