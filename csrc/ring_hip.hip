@@ -60,16 +60,23 @@ __global__ void __launch_bounds__(256) k_binary(int op, const T* __restrict__ a,
 }
 
 template <class T>
-__global__ void __launch_bounds__(256) k_binary_slot(int op, const T* __restrict__ a,
-                                                     const T* __restrict__ b, int64_t nb,
-                                                     T* __restrict__ out, int64_t m, int np,
-                                                     int which) {
+__device__ __forceinline__ void d_binary_slot(int op, const T* __restrict__ a,
+                                              const T* __restrict__ b, int64_t nb,
+                                              T* __restrict__ out, int64_t m, int np, int which) {
   const int64_t n = m * np;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < n;
        g += (int64_t)gridDim.x * blockDim.x) {
     const int64_t p = g / m, i = g - p * m;
     out[g] = p == which ? mxr::binop<T>(op, a[g], b[nb == 1 ? 0 : i % nb]) : a[g];
   }
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) k_binary_slot(int op, const T* __restrict__ a,
+                                                     const T* __restrict__ b, int64_t nb,
+                                                     T* __restrict__ out, int64_t m, int np,
+                                                     int which) {
+  d_binary_slot<T>(op, a, b, nb, out, m, np, which);
 }
 
 // Share-pair forms: both replicated share vectors (s0, s1) of a share-wise op in ONE launch,
@@ -83,8 +90,8 @@ struct Pair {
 };
 
 template <class T>
-__global__ void __launch_bounds__(256) k_binary2(int op, Pair<T> p, int64_t na, int64_t nb,
-                                                 int64_t n) {
+__device__ __forceinline__ void d_binary2(int op, const Pair<T>& p, int64_t na, int64_t nb,
+                                          int64_t n) {
   const int y = blockIdx.y;
   const T* __restrict__ a = p.a[y];
   const T* __restrict__ b = p.b[y];
@@ -95,7 +102,13 @@ __global__ void __launch_bounds__(256) k_binary2(int op, Pair<T> p, int64_t na, 
 }
 
 template <class T>
-__global__ void __launch_bounds__(256) k_unary2(int op, Pair<T> p, int64_t n, int k) {
+__global__ void __launch_bounds__(256) k_binary2(int op, Pair<T> p, int64_t na, int64_t nb,
+                                                 int64_t n) {
+  d_binary2<T>(op, p, na, nb, n);
+}
+
+template <class T>
+__device__ __forceinline__ void d_unary2(int op, const Pair<T>& p, int64_t n, int k) {
   const int y = blockIdx.y;
   const T* __restrict__ a = p.a[y];
   T* __restrict__ out = p.o[y];
@@ -104,10 +117,15 @@ __global__ void __launch_bounds__(256) k_unary2(int op, Pair<T> p, int64_t n, in
     out[i] = mxr::unop<T>(op, a[i], k);
 }
 
+template <class T>
+__global__ void __launch_bounds__(256) k_unary2(int op, Pair<T> p, int64_t n, int k) {
+  d_unary2<T>(op, p, n, k);
+}
+
 // public b applied to party slot which[y] of stacked a[y] ([np, m]), other slots copied
 template <class T>
-__global__ void __launch_bounds__(256) k_binary_slot2(int op, Pair<T> p, int64_t nb, int64_t m,
-                                                      int np) {
+__device__ __forceinline__ void d_binary_slot2(int op, const Pair<T>& p, int64_t nb, int64_t m,
+                                               int np) {
   const int y = blockIdx.y;
   const T* __restrict__ a = p.a[y];
   const T* __restrict__ b = p.b[0];
@@ -119,6 +137,12 @@ __global__ void __launch_bounds__(256) k_binary_slot2(int op, Pair<T> p, int64_t
     const int64_t q = g / m, i = g - q * m;
     out[g] = q == which ? mxr::binop<T>(op, a[g], b[nb == 1 ? 0 : i % nb]) : a[g];
   }
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) k_binary_slot2(int op, Pair<T> p, int64_t nb, int64_t m,
+                                                      int np) {
+  d_binary_slot2<T>(op, p, nb, m, np);
 }
 
 // out = a + b + c (a reveal: the holder's two shares plus the received third)
@@ -179,7 +203,7 @@ struct SumViews {
 };
 
 template <class T>
-__global__ void __launch_bounds__(256) k_sum_views2(SumViews<T> p, int k, int64_t m, int np) {
+__device__ __forceinline__ void d_sum_views2(const SumViews<T>& p, int k, int64_t m, int np) {
   const int y = blockIdx.y;
   const T* __restrict__ base = p.base[y];
   T* __restrict__ out = p.o[y];
@@ -195,9 +219,14 @@ __global__ void __launch_bounds__(256) k_sum_views2(SumViews<T> p, int k, int64_
   }
 }
 
+template <class T>
+__global__ void __launch_bounds__(256) k_sum_views2(SumViews<T> p, int k, int64_t m, int np) {
+  d_sum_views2<T>(p, k, m, np);
+}
+
 // trivial sharings in the stacked layout: out_y[q, i] = q == which[y] ? a[y][i] : 0
 template <class T>
-__global__ void __launch_bounds__(256) k_slot_place2(Pair<T> p, int64_t m, int np) {
+__device__ __forceinline__ void d_slot_place2(const Pair<T>& p, int64_t m, int np) {
   const int y = blockIdx.y;
   const T* __restrict__ a = p.a[y];
   T* __restrict__ out = p.o[y];
@@ -208,6 +237,11 @@ __global__ void __launch_bounds__(256) k_slot_place2(Pair<T> p, int64_t m, int n
     const int64_t q = g / m, i = g - q * m;
     out[g] = q == which ? a[i] : (T)0;
   }
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) k_slot_place2(Pair<T> p, int64_t m, int np) {
+  d_slot_place2<T>(p, m, np);
 }
 
 template <class T>
@@ -228,16 +262,21 @@ __global__ void __launch_bounds__(256) k_add_zs3(const T* __restrict__ v, const 
 }
 
 template <class T>
-__global__ void __launch_bounds__(256) k_unary(int op, const T* __restrict__ a, T* __restrict__ out,
-                                               int64_t n, int k) {
+__device__ __forceinline__ void d_unary(int op, const T* __restrict__ a, T* __restrict__ out,
+                                        int64_t n, int k) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
     out[i] = mxr::unop<T>(op, a[i], k);
 }
 
 template <class T>
-__global__ void __launch_bounds__(256) k_fill(T* __restrict__ out, int64_t n, uint64_t lo,
-                                              uint64_t hi) {
+__global__ void __launch_bounds__(256) k_unary(int op, const T* __restrict__ a, T* __restrict__ out,
+                                               int64_t n, int k) {
+  d_unary<T>(op, a, out, n, k);
+}
+
+template <class T>
+__device__ __forceinline__ void d_fill(T* __restrict__ out, int64_t n, uint64_t lo, uint64_t hi) {
   T v;
   if constexpr (sizeof(T) == 16) {
     v = ((T)hi << 64) | (T)lo;
@@ -249,11 +288,16 @@ __global__ void __launch_bounds__(256) k_fill(T* __restrict__ out, int64_t n, ui
     out[i] = v;
 }
 
+template <class T>
+__global__ void __launch_bounds__(256) k_fill(T* __restrict__ out, int64_t n, uint64_t lo,
+                                              uint64_t hi) {
+  d_fill<T>(out, n, lo, hi);
+}
+
 // out[o, j, i] = bit (start + j) of a[o, i] as a 0/1 byte (bit decomposition / split)
 template <class T>
-__global__ void __launch_bounds__(256) k_bit_planes(const T* __restrict__ a,
-                                                    uint8_t* __restrict__ out, int64_t outer, 
-                             int64_t inner, int start, int count) {
+__device__ __forceinline__ void d_bit_planes(const T* __restrict__ a, uint8_t* __restrict__ out,
+                                             int64_t outer, int64_t inner, int start, int count) {
   const int64_t n = outer * inner;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < n;
        g += (int64_t)gridDim.x * blockDim.x) {
@@ -262,6 +306,13 @@ __global__ void __launch_bounds__(256) k_bit_planes(const T* __restrict__ a,
     uint8_t* dst = out + o * count * inner + i;
     for (int j = 0; j < count; ++j) dst[(int64_t)j * inner] = (uint8_t)((v >> (start + j)) & 1);
   }
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) k_bit_planes(const T* __restrict__ a,
+                                                    uint8_t* __restrict__ out, int64_t outer,
+                                                    int64_t inner, int start, int count) {
+  d_bit_planes<T>(a, out, outer, inner, start, count);
 }
 
 // out[o, i] = sum_j w[j] * a[o, j, i]  (public ring weights, bit composition)
@@ -318,30 +369,48 @@ __global__ void __launch_bounds__(256) k_weighted_sum_wide(const T* __restrict__
 }
 
 template <class T>
-__global__ void __launch_bounds__(256) k_compare(int op, const T* __restrict__ a, int64_t na,
-                                                 const T* __restrict__ b, 
-                          int64_t nb, uint8_t* __restrict__ out, int64_t n) {
+__device__ __forceinline__ void d_compare(int op, const T* __restrict__ a, int64_t na,
+                                          const T* __restrict__ b, int64_t nb,
+                                          uint8_t* __restrict__ out, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
     out[i] = mxr::cmpop<T>(op, a[na == 1 ? 0 : i], b ? b[nb == 1 ? 0 : i] : (T)0);
 }
 
 template <class T>
-__global__ void __launch_bounds__(256) k_bit_extract(const T* __restrict__ a,
-                                                     uint8_t* __restrict__ out, int64_t n, 
-                              int bit) {
+__global__ void __launch_bounds__(256) k_compare(int op, const T* __restrict__ a, int64_t na,
+                                                 const T* __restrict__ b, int64_t nb,
+                                                 uint8_t* __restrict__ out, int64_t n) {
+  d_compare<T>(op, a, na, b, nb, out, n);
+}
+
+template <class T>
+__device__ __forceinline__ void d_bit_extract(const T* __restrict__ a, uint8_t* __restrict__ out,
+                                              int64_t n, int bit) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
     out[i] = (uint8_t)((a[i] >> bit) & 1);
 }
 
 template <class T>
-__global__ void __launch_bounds__(256) k_ring_inject(const uint8_t* __restrict__ bits,
-                                                     T* __restrict__ out, int64_t n, 
-                              int bit) {
+__global__ void __launch_bounds__(256) k_bit_extract(const T* __restrict__ a,
+                                                     uint8_t* __restrict__ out, int64_t n,
+                                                     int bit) {
+  d_bit_extract<T>(a, out, n, bit);
+}
+
+template <class T>
+__device__ __forceinline__ void d_ring_inject(const uint8_t* __restrict__ bits, T* __restrict__ out,
+                                              int64_t n, int bit) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
     out[i] = ((T)(bits[i] & 1)) << bit;
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) k_ring_inject(const uint8_t* __restrict__ bits,
+                                                     T* __restrict__ out, int64_t n, int bit) {
+  d_ring_inject<T>(bits, out, n, bit);
 }
 
 // The local half of rep.b2a for three stacked parties, one launch: from the bit sharing
@@ -449,18 +518,22 @@ __global__ void __launch_bounds__(256) k_b2a3(const uint8_t* __restrict__ s0,
 }
 
 template <class T>
-__global__ void __launch_bounds__(256) k_encode(const double* __restrict__ x, T* __restrict__ out,
-                                                int64_t n, 
-                         double scale) {
+__device__ __forceinline__ void d_encode(const double* __restrict__ x, T* __restrict__ out,
+                                         int64_t n, double scale) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
     out[i] = (T)mxr::f64_to_i128(x[i] * scale);
 }
 
 template <class T>
-__global__ void __launch_bounds__(256) k_decode(const T* __restrict__ x, double* __restrict__ out,
-                                                int64_t n, 
-                         double scale) {
+__global__ void __launch_bounds__(256) k_encode(const double* __restrict__ x, T* __restrict__ out,
+                                                int64_t n, double scale) {
+  d_encode<T>(x, out, n, scale);
+}
+
+template <class T>
+__device__ __forceinline__ void d_decode(const T* __restrict__ x, double* __restrict__ out,
+                                         int64_t n, double scale) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     if constexpr (sizeof(T) == 8)
@@ -468,6 +541,12 @@ __global__ void __launch_bounds__(256) k_decode(const T* __restrict__ x, double*
     else
       out[i] = mxr::i128_to_f64(x[i]) * scale;
   }
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) k_decode(const T* __restrict__ x, double* __restrict__ out,
+                                                int64_t n, double scale) {
+  d_decode<T>(x, out, n, scale);
 }
 
 // decode(a + b + c [+ d]): the reveal's add and the decode in one pass (no ring-valued sum in
@@ -499,9 +578,8 @@ __global__ void __launch_bounds__(256) k_addn_decode(const T* __restrict__ a,
 
 // one thread per output when the reduced axis is short; a block per output otherwise
 template <class T>
-__global__ void __launch_bounds__(256) k_sum_axis(const T* __restrict__ a, T* __restrict__ out,
-                                                  int64_t outer, 
-                           int64_t red, int64_t inner) {
+__device__ __forceinline__ void d_sum_axis(const T* __restrict__ a, T* __restrict__ out,
+                                           int64_t outer, int64_t red, int64_t inner) {
   int64_t total = outer * inner;
   for (int64_t oi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; oi < total;
        oi += (int64_t)gridDim.x * blockDim.x) {
@@ -516,6 +594,12 @@ __global__ void __launch_bounds__(256) k_sum_axis(const T* __restrict__ a, T* __
     for (; r < red; ++r) acc[0] += p[r * inner];
     out[oi] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   }
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) k_sum_axis(const T* __restrict__ a, T* __restrict__ out,
+                                                  int64_t outer, int64_t red, int64_t inner) {
+  d_sum_axis<T>(a, out, outer, red, inner);
 }
 
 template <class T>
@@ -1173,11 +1257,10 @@ __global__ void __launch_bounds__(256) k_mul_add2(Pair<T> p, int64_t n, const T*
 
 // The adder's sum after the last level, both share components: p ^ ((g ^ t) << 1).
 template <class T>
-__global__ void __launch_bounds__(256) k_ks_sum2(const T* __restrict__ p0, const T* __restrict__ p1,
-                                                 const T* __restrict__ g0, const T* __restrict__ g1,
-                                                 const T* __restrict__ t0, const T* __restrict__ t1,
-                                                 T* __restrict__ o0, T* __restrict__ o1,
-                                                 int64_t n) {
+__device__ __forceinline__ void d_ks_sum2(const T* __restrict__ p0, const T* __restrict__ p1,
+                                          const T* __restrict__ g0, const T* __restrict__ g1,
+                                          const T* __restrict__ t0, const T* __restrict__ t1,
+                                          T* __restrict__ o0, T* __restrict__ o1, int64_t n) {
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
        e += (int64_t)gridDim.x * blockDim.x) {
     o0[e] = p0[e] ^ (T)((g0[e] ^ t0[e]) << 1);
@@ -1185,19 +1268,27 @@ __global__ void __launch_bounds__(256) k_ks_sum2(const T* __restrict__ p0, const
   }
 }
 
+template <class T>
+__global__ void __launch_bounds__(256) k_ks_sum2(const T* __restrict__ p0, const T* __restrict__ p1,
+                                                 const T* __restrict__ g0, const T* __restrict__ g1,
+                                                 const T* __restrict__ t0, const T* __restrict__ t1,
+                                                 T* __restrict__ o0, T* __restrict__ o1,
+                                                 int64_t n) {
+  d_ks_sum2<T>(p0, p1, g0, g1, t0, t1, o0, o1, n);
+}
+
 // One party's cross terms of a Kogge-Stone level (mx_ks_cross1): thread per element.  With
 // t0 (mx_ks_cross1x_s) the level's g is g ^ t -- the previous level's xor, folded in --
 // and is written to go0 / go1 for the next level.
 template <class T>
-__global__ void __launch_bounds__(256) k_ks_cross1(const T* __restrict__ g0,
-                                                   const T* __restrict__ g1, 
-                                                   const T* __restrict__ p0, const T* __restrict__ p1,
-                                                   T* __restrict__ z, int64_t n, int d, int both,
-                                                   KeySrc keys, uint64_t nonce,
-                                                   const T* __restrict__ t0 = nullptr,
-                                                   const T* __restrict__ t1 = nullptr,
-                                                   T* __restrict__ go0 = nullptr,
-                                                   T* __restrict__ go1 = nullptr) {
+__device__ __forceinline__ void d_ks_cross1(const T* __restrict__ g0, const T* __restrict__ g1,
+                                            const T* __restrict__ p0, const T* __restrict__ p1,
+                                            T* __restrict__ z, int64_t n, int d, int both,
+                                            const KeySrc& keys, uint64_t nonce,
+                                            const T* __restrict__ t0 = nullptr,
+                                            const T* __restrict__ t1 = nullptr,
+                                            T* __restrict__ go0 = nullptr,
+                                            T* __restrict__ go1 = nullptr) {
   __shared__ uint32_t rks[2][kKeyWords];
   stage_keys(rks, keys, 2);
   constexpr int P = Lane<T>::kPer;
@@ -1226,6 +1317,20 @@ __global__ void __launch_bounds__(256) k_ks_cross1(const T* __restrict__ g0,
              pick<T>(l1, h1, (int)(c % P));
     }
   }
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) k_ks_cross1(const T* __restrict__ g0,
+                                                   const T* __restrict__ g1,
+                                                   const T* __restrict__ p0,
+                                                   const T* __restrict__ p1, T* __restrict__ z,
+                                                   int64_t n, int d, int both, KeySrc keys,
+                                                   uint64_t nonce,
+                                                   const T* __restrict__ t0 = nullptr,
+                                                   const T* __restrict__ t1 = nullptr,
+                                                   T* __restrict__ go0 = nullptr,
+                                                   T* __restrict__ go1 = nullptr) {
+  d_ks_cross1<T>(g0, g1, p0, p1, z, n, d, both, keys, nonce, nullptr, nullptr, nullptr, nullptr);
 }
 
 // Latency form of k_ks_cross1 (a per-party level of the LR inference's adders: a few
@@ -1570,9 +1675,8 @@ __global__ void __launch_bounds__(256) k_mul_trunc3(
 }
 
 template <class T>
-__global__ void __launch_bounds__(256) k_prf_expand(T* __restrict__ out, int64_t n, int nkeys,
-                                                    KeySrc keys, 
-                             uint64_t nonce) {
+__device__ __forceinline__ void d_prf_expand(T* __restrict__ out, int64_t n, int nkeys,
+                                             const KeySrc& keys, uint64_t nonce) {
   __shared__ uint32_t rks[4][kKeyWords];
   stage_keys(rks, keys, nkeys);
   constexpr int P = Lane<T>::kPer;
@@ -1599,17 +1703,61 @@ __global__ void __launch_bounds__(256) k_prf_expand(T* __restrict__ out, int64_t
   }
 }
 
+template <class T>
+__global__ void __launch_bounds__(256) k_prf_expand(T* __restrict__ out, int64_t n, int nkeys,
+                                                    KeySrc keys, uint64_t nonce) {
+  d_prf_expand<T>(out, n, nkeys, keys, nonce);
+}
+
+// party-batched twins of the per-party sessions' local kernels (party_batch.h)
+MX_X3(k_binary2<u64>, d_binary2<u64>);
+MX_X3(k_binary2<u128>, d_binary2<u128>);
+MX_X3(k_unary2<u64>, d_unary2<u64>);
+MX_X3(k_unary2<u128>, d_unary2<u128>);
+MX_X3(k_unary<u64>, d_unary<u64>);
+MX_X3(k_unary<u128>, d_unary<u128>);
+MX_X3(k_binary_slot<u64>, d_binary_slot<u64>);
+MX_X3(k_binary_slot<u128>, d_binary_slot<u128>);
+MX_X3(k_binary_slot2<u64>, d_binary_slot2<u64>);
+MX_X3(k_binary_slot2<u128>, d_binary_slot2<u128>);
+MX_X3(k_sum_axis<u64>, d_sum_axis<u64>);
+MX_X3(k_sum_axis<u128>, d_sum_axis<u128>);
+MX_X3(k_fill<u64>, d_fill<u64>);
+MX_X3(k_fill<u128>, d_fill<u128>);
+MX_X3(k_encode<u64>, d_encode<u64>);
+MX_X3(k_encode<u128>, d_encode<u128>);
+MX_X3(k_decode<u64>, d_decode<u64>);
+MX_X3(k_decode<u128>, d_decode<u128>);
+MX_X3(k_ks_cross1<u64>, d_ks_cross1<u64>);
+MX_X3(k_ks_cross1<u128>, d_ks_cross1<u128>);
+MX_X3(k_ks_sum2<u64>, d_ks_sum2<u64>);
+MX_X3(k_ks_sum2<u128>, d_ks_sum2<u128>);
+MX_X3(k_slot_place2<u64>, d_slot_place2<u64>);
+MX_X3(k_slot_place2<u128>, d_slot_place2<u128>);
+MX_X3(k_sum_views2<u64>, d_sum_views2<u64>);
+MX_X3(k_sum_views2<u128>, d_sum_views2<u128>);
+MX_X3(k_bit_extract<u64>, d_bit_extract<u64>);
+MX_X3(k_bit_extract<u128>, d_bit_extract<u128>);
+MX_X3(k_bit_planes<u64>, d_bit_planes<u64>);
+MX_X3(k_bit_planes<u128>, d_bit_planes<u128>);
+MX_X3(k_compare<u64>, d_compare<u64>);
+MX_X3(k_compare<u128>, d_compare<u128>);
+MX_X3(k_prf_expand<u64>, d_prf_expand<u64>);
+MX_X3(k_prf_expand<u128>, d_prf_expand<u128>);
+MX_X3(k_ring_inject<u64>, d_ring_inject<u64>);
+MX_X3(k_ring_inject<u128>, d_ring_inject<u128>);
+
 // Reference (VALU) ring GEMM: 16x16 output tile per block, K staged through LDS.
 // a_bs / b_bs: batch strides in elements (0: one operand broadcast over the batch).
 template <class T, int TS>
-__global__ void __launch_bounds__(256) k_gemm_valu(int64_t M, int64_t N, int64_t K,
-                                                   const T* __restrict__ A0, 
-                            const T* __restrict__ A1, const T* __restrict__ B0,
-                            const T* __restrict__ B1, int mode, T* __restrict__ C,
-                            int accumulate, int64_t a_bs, int64_t b_bs) {
+__device__ __forceinline__ void d_gemm_valu(int64_t M, int64_t N, int64_t K,
+                                            const T* __restrict__ A0, const T* __restrict__ A1,
+                                            const T* __restrict__ B0, const T* __restrict__ B1,
+                                            int mode, T* __restrict__ C, int accumulate,
+                                            int64_t a_bs, int64_t b_bs, int zb) {
   __shared__ T As[TS][TS + 1];
   __shared__ T Bs[TS][TS + 1];
-  const int64_t b = blockIdx.z;
+  const int64_t b = zb >= 0 ? zb : blockIdx.z;  // zb >= 0: an unbatched launch's only product
   const int64_t row = blockIdx.y * TS + threadIdx.y;
   const int64_t col = blockIdx.x * TS + threadIdx.x;
   const T* a0 = A0 + b * a_bs;
@@ -1641,6 +1789,21 @@ __global__ void __launch_bounds__(256) k_gemm_valu(int64_t M, int64_t N, int64_t
   }
 }
 
+template <class T, int TS>
+__global__ void __launch_bounds__(256) k_gemm_valu(int64_t M, int64_t N, int64_t K,
+                                                   const T* __restrict__ A0,
+                                                   const T* __restrict__ A1,
+                                                   const T* __restrict__ B0,
+                                                   const T* __restrict__ B1, int mode,
+                                                   T* __restrict__ C, int accumulate,
+                                                   int64_t a_bs, int64_t b_bs, int zb) {
+  d_gemm_valu<T, TS>(M, N, K, A0, A1, B0, B1, mode, C, accumulate, a_bs, b_bs, zb);
+}
+
+// an unbatched product (grid z = 1, zb = 0) of several parties: one party-batched launch
+MX_X3((k_gemm_valu<u64, 16>), (d_gemm_valu<u64, 16>));
+MX_X3((k_gemm_valu<u128, 16>), (d_gemm_valu<u128, 16>));
+
 template <class T>
 int launch_gemm_valu(int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
                      const void* A1, const void* B0, const void* B1, int mode, void* C,
@@ -1650,7 +1813,7 @@ int launch_gemm_valu(int64_t batch, int64_t M, int64_t N, int64_t K, const void*
   dim3 block(TS, TS);
   hipLaunchKernelGGL((k_gemm_valu<T, TS>), grid, block, 0, st, M, N, K, (const T*)A0,
                      (const T*)A1, (const T*)B0, (const T*)B1, mode, (T*)C, accumulate,
-                     a_bs < 0 ? M * K : a_bs, b_bs < 0 ? K * N : b_bs);
+                     a_bs < 0 ? M * K : a_bs, b_bs < 0 ? K * N : b_bs, batch == 1 ? 0 : -1);
   MX_LAUNCH_CHECK();
   return 0;
 }

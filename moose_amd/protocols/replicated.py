@@ -593,6 +593,18 @@ def mul_trunc(sess, x: RepTensor, y: RepTensor, m: int, out=None) -> RepTensor:
         if r is not None:
             return RepTensor(x.plc, x.bits, "arith", r[0], r[1])
     jobs = getattr(sess, "party_jobs", None)
+    if jobs is not None and sess.party_index(x.plc) is not None:
+        one = [t for t in (x, y) if t.s0.v.numel() == 1]
+        if len(one) == 1 and x.s0.v.shape != y.s0.v.shape:
+            # a one-element factor (a learning rate, a momentum): broadcast inside the tail
+            # kernel as a stride-0 row when the product goes there, else materialised
+            r = _mul_trunc_bcast(sess, x, y, m, out)
+            if r is not None:
+                return r
+            small = one[0]
+            big = y if small is x else x
+            b = local(sess, small, "Broadcast", shape=tuple(big.s0.v.shape))
+            x, y = (b, y) if small is x else (x, b)
     if (jobs is not None and JOBS and 0 < m <= 63 and x.kind == "arith" and x.bits in (64, 128)
             and os.environ.get("MOOSEX_DOT_TAIL", "1") != "0" and sess.jobs_shape_ok(x, y)):
         # one party of a per-party session: the product's cross terms inside the batched
@@ -620,16 +632,38 @@ def mul_trunc(sess, x: RepTensor, y: RepTensor, m: int, out=None) -> RepTensor:
 JOBS = os.environ.get("MOOSEX_PARTY_JOBS", "1") != "0"
 
 
+def _mul_trunc_bcast(sess, x: RepTensor, y: RepTensor, m: int, out=None):
+    """mul_trunc of a dense operand by a one-element one on a per-party session, through
+    the batched tail with the small factor as a stride-0 row (rows of length 1): the same
+    elements in the same order as the product of the materialised broadcast, so the same
+    shares.  None when the tail cannot take it."""
+    big, small = (x, y) if y.s0.v.numel() == 1 else (y, x)
+    if not (JOBS and 0 < m <= 63 and x.kind == "arith" and y.kind == "arith"
+            and x.bits in (64, 128) and os.environ.get("MOOSEX_DOT_TAIL", "1") != "0"):
+        return None
+    shares = [t.v for r in (big, small) for t in (r.s0, r.s1)]
+    if not all(isinstance(t, R.RT) and t.data.is_contiguous() for t in shares):
+        return None
+    n = big.s0.v.numel()
+    with span("rep.mul_trunc_party"):
+        nonces = tuple(sess.nonce(x.plc) for _ in range(7))
+        return tail_job(sess, x.plc, x.bits, m, nonces, big.s0,
+                        lambda o0, o1: R.MulJob(n, o0, o1,
+                                                x=(big.s0.v.data, big.s1.v.data), sx=1,
+                                                y=(small.s0.v.data, small.s1.v.data), sy=0),
+                        out=out, L=1)
+
+
 def _mul_trunc_jobs(sess, x: RepTensor, y: RepTensor, m: int, nonces, out=None) -> RepTensor:
     return tail_job(sess, x.plc, x.bits, m, nonces, x.s0,
                     lambda o0, o1: R.MulJob(1, o0, o1, x=(x.s0.v.data, x.s1.v.data),
                                             y=(y.s0.v.data, y.s1.v.data)), out=out)
 
 
-def tail_job(sess, plc, bits, m, nonces, like: PV, make, out=None) -> RepTensor:
+def tail_job(sess, plc, bits, m, nonces, like: PV, make, out=None, L=None) -> RepTensor:
     """One value through the per-party batched tail (csrc/rss_jobs.hip): ``make(o0, o1)``
-    builds its ring.MulJob (one row of ``like``'s size) writing the new shares to o0 / o1.
-    Non-members get placeholders."""
+    builds its ring.MulJob (one row of ``like``'s size, or rows of length ``L``) writing
+    the new shares to o0 / o1.  Non-members get placeholders."""
     from moose_amd.parallel.spmd import Remote
 
     if sess.party_index(plc) is None:
@@ -641,7 +675,8 @@ def tail_job(sess, plc, bits, m, nonces, like: PV, make, out=None) -> RepTensor:
     else:
         o0, o1 = R.empty2(v.shape, bits, v.data.device)
         o0, o1 = o0.data, o1.data
-    sess.party_jobs(plc, [make(o0, o1)], max(1, v.numel()), bits, m, nonces)
+    sess.party_jobs(plc, [make(o0, o1)], L if L is not None else max(1, v.numel()), bits, m,
+                    nonces)
     return RepTensor(plc, bits, "arith", PV(plc, R.RT(o0, bits)), PV(plc, R.RT(o1, bits)))
 
 

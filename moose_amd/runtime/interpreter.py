@@ -63,6 +63,9 @@ MERGE_ROUNDS = os.environ.get("MOOSEX_MERGE_ROUNDS", "1") != "0"
 # per-operation nonce scopes (runtime/session.py nonce_scope; MOOSEX_NONCE_SCOPES=0: one
 # session-wide counter, the round-5 numbering)
 NONCE_SCOPES = os.environ.get("MOOSEX_NONCE_SCOPES", "1") != "0"
+# per-party sessions broadcast a one-element secret operand of add / sub / mul inside the
+# kernels instead of materialising it (MOOSEX_BCAST_IN_KERNEL=0: materialised)
+BCAST_IN_KERNEL = os.environ.get("MOOSEX_BCAST_IN_KERNEL", "1") != "0"
 
 
 def _by_depth(ops):
@@ -1188,7 +1191,7 @@ class Interpreter:
         r = self._host_binary(op, hx, hy, kind, dtype)
         return LV(x.plc, "tensor", r.dtype, MV(x.plc, r.v.v))
 
-    def _broadcast_secret(self, x, y, px, py):
+    def _broadcast_secret(self, x, y, px, py, kind=None):
         """Numpy-broadcast the secret operand(s) of an elementwise op to the common shape.
 
         Shares carry a leading party axis (stacked) or live per process (SPMD), so rank
@@ -1208,6 +1211,14 @@ class Interpreter:
         if sx is None or sy is None or sx == sy:
             return x, y
         target = tuple(np.broadcast_shapes(sx, sy))
+        if (BCAST_IN_KERNEL and kind in ("Add", "Sub", "Mul") and px is None and py is None
+                and getattr(self.sess, "party_jobs", None) is not None
+                and ((math.prod(sx) == 1 and sy == target)
+                     or (math.prod(sy) == 1 and sx == target))):
+            # a per-party session broadcasts a one-element operand inside its kernels
+            # (share-wise add / sub: ring.binary2; mul: a stride-0 row of the batched tail,
+            # rep.mul_trunc): no materialised copy
+            return x, y
         if px is None and sx != target:
             x = LV(x.plc, x.kind, x.dtype, fxp.broadcast_to(self.sess, x.v, target))
         if py is None and sy != target:
@@ -1222,7 +1233,7 @@ class Interpreter:
                                  LV(x.plc, "tensor", y.dtype, MV(x.plc, py)), kind, dtype)
             return LV(x.plc, "tensor", h.dtype, MV(x.plc, h.v.v))
         if kind != "Dot":
-            x, y = self._broadcast_secret(x, y, px, py)
+            x, y = self._broadcast_secret(x, y, px, py, kind)
         if kind in ("Less", "Greater"):
             a, b = x, y
             return LV(x.plc, "tensor", T.BOOL, fxp.compare(sess, kind, a.v, b.v, px, py))

@@ -2,6 +2,7 @@
 independent same-shape secret Dots run as ONE batched protocol instance
 (fixedpoint.dot_many), with the same results as one instance per Dot."""
 import numpy as np
+import pytest
 
 import moose_amd as pm
 from moose_amd.protocols import fixedpoint as fxp
@@ -101,3 +102,46 @@ def test_independent_dots_batched_on_per_party_sessions(monkeypatch):
         np.testing.assert_allclose(got, want, atol=1e-4)
         rounds[flag] = rt.last_stats.rounds
     assert rounds["0"] >= rounds["1"] + 6, rounds  # 4 tails of 2 rounds -> one
+
+
+def _scalar_factors():
+    alice, bob, carole = (pm.host_placement(n) for n in ("alice", "bob", "carole"))
+    rep = pm.replicated_placement("rep", players=[alice, bob, carole])
+    fx = pm.fixed(24, 40)
+
+    @pm.computation
+    def f(x: pm.Argument(placement=alice, vtype=pm.TensorType(pm.float64)),
+          c: pm.Argument(placement=bob, vtype=pm.TensorType(pm.float64))):
+        with alice:
+            xf = pm.cast(x, dtype=fx)
+        with bob:
+            cf = pm.cast(c, dtype=fx)
+        with rep:
+            a = pm.mul(xf, cf)
+            b = pm.add(pm.sub(a, cf), cf)
+            z = pm.mul(cf, b)
+        with carole:
+            return pm.cast(z, dtype=pm.float64)
+
+    return f
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_one_element_factors_broadcast_in_kernel(device, monkeypatch):
+    """A one-element secret factor (a learning rate) times / plus a (5, 3) secret on the
+    per-party sessions: broadcast inside the kernels (a stride-0 row of the batched tail,
+    ring.binary2) instead of materialised -- bitwise the same outputs, and the values."""
+    from moose_amd.runtime import interpreter as I
+    from moose_amd.runtime.local import LocalMooseRuntime
+
+    ids = ["alice", "bob", "carole"]
+    rng = np.random.default_rng(4)
+    args = {"x": rng.uniform(-3, 3, (5, 3)), "c": np.array(0.37)}
+    outs = {}
+    for flag in (False, True):
+        monkeypatch.setattr(I, "BCAST_IN_KERNEL", flag)
+        rt = LocalMooseRuntime(ids, device_map={i: device for i in ids}, seed=5,
+                               use_graphs=False)
+        outs[flag] = np.asarray(list(rt.evaluate_computation(_scalar_factors(), args).values())[0])
+    assert np.array_equal(outs[True], outs[False])
+    np.testing.assert_allclose(outs[True], 0.37 * 0.37 * args["x"], atol=1e-6)
