@@ -489,8 +489,9 @@ static int graph_compose_impl(int n, const int* kind, void* const* child, void* 
 
 // The composed total order as ONE chain with party-batched launches (party_batch.h):
 // kind / child / dst / src / bytes as mx_graph_compose, party[i] = the party of segment i
-// (kind 0).  Each maximal run of segments between two copy nodes is a phase: the parties'
-// launches in it are independent, so the same launch of 2-3 parties becomes one node.
+// (kind 0), or for a copy node the bitmask of the parties it reads from or writes to.
+// Each maximal run of segments between two copy nodes is a phase: the parties' launches in
+// it are independent, so the same launch of 2-3 parties becomes one node.
 // stats[0..3] = nodes, launches merged away, batched nodes, phases.
 int mx_graph_compose_merged(int n, const int* kind, void* const* child, void* const* dst,
                             void* const* src, const int64_t* bytes, const int* party,
@@ -506,6 +507,7 @@ int mx_graph_compose_merged(int n, const int* kind, void* const* child, void* co
     ++nodes;
   };
   alignas(16) static thread_local unsigned char blob[4096];
+  std::vector<Item> carry[3];  // a party's launches deferred to the next phase
   for (int i = 0; i < n;) {
     if (kind[i] != 0) {
       hipGraphNode_t node = nullptr;
@@ -538,8 +540,15 @@ int mx_graph_compose_merged(int n, const int* kind, void* const* child, void* co
     int j = i;
     while (j < n && kind[j] == 0) ++j;
     ++phases;
-    // the phase's items per party (parties beyond the third: unbatched, in segment order)
+    // the copies after the phase: the parties they read from or write to, and whether
+    // another phase follows them
+    int k2 = j, touched = 0;
+    while (k2 < n && kind[k2] != 0) touched |= party[k2++];
+    const bool next_phase = k2 < n;
+    // the phase's items per party (parties beyond the third: unbatched, in segment order),
+    // after the ones a previous phase deferred
     std::vector<Item> L[3];
+    for (int p = 0; p < 3; ++p) L[p].swap(carry[p]);
     bool many = false;
     for (int s2 = i; s2 < j; ++s2)
       if (party[s2] < 0 || party[s2] > 2) many = true;
@@ -563,7 +572,42 @@ int mx_graph_compose_merged(int n, const int* kind, void* const* child, void* co
         L[0].push_back(op);
       }
     }
-    for (const Group& gr : align3(L)) {
+    static const bool dbg = std::getenv("MOOSEX_MERGE_DEBUG") != nullptr;
+    std::vector<Group> groups = align3(L);
+    if (!many && next_phase && merge_on()) {
+      // A party whose launches merge with nobody here (it runs a round ahead: the dealer,
+      // a party with nothing to receive) waits for the next phase, where the others reach
+      // the same launches -- when the copies in between neither read its messages nor
+      // write its buffers, so its order against every copy it depends on is kept.
+      bool moved = false;
+      for (int p = 0; p < 3; ++p) {
+        if (L[p].empty() || ((touched >> p) & 1)) continue;
+        bool single = true;
+        for (const Group& gr : groups)
+          for (int z = 0; z < gr.k; ++z)
+            if (gr.party[z] == p && gr.k > 1) single = false;
+        if (single) {
+          carry[p].swap(L[p]);
+          moved = true;
+        }
+      }
+      if (moved) groups = align3(L);
+    }
+    if (dbg) {  // the phase's launches per party and the groups chosen
+      fprintf(stderr, "phase %lld:\n", (long long)phases);
+      for (int p = 0; p < 3; ++p) {
+        fprintf(stderr, "  party %d:", p);
+        for (const Item& it : L[p]) {
+          const char* nm = it.opaque ? "<segment>" : hipKernelNameRefByPtr(it.func, nullptr);
+          fprintf(stderr, " %.40s/%u%s", nm ? nm : "?", it.grid.x, it.x3 ? "" : "(no twin)");
+        }
+        fprintf(stderr, "\n");
+      }
+      fprintf(stderr, "  groups:");
+      for (const Group& gr : groups) fprintf(stderr, " %d", gr.k);
+      fprintf(stderr, "\n");
+    }
+    for (const Group& gr : groups) {
       const Item& it = L[gr.party[0]][gr.idx[0]];
       hipGraphNode_t node = nullptr;
       hipError_t rc = hipSuccess;

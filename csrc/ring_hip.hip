@@ -1804,10 +1804,93 @@ __global__ void __launch_bounds__(256) k_gemm_valu(int64_t M, int64_t N, int64_t
 MX_X3((k_gemm_valu<u64, 16>), (d_gemm_valu<u64, 16>));
 MX_X3((k_gemm_valu<u128, 16>), (d_gemm_valu<u128, 16>));
 
+// Skinny products (N <= 4: a matrix times a vector or a few columns -- the per-party
+// LogReg and LR dots): one wave per output row, its lanes splitting K, then a butterfly over
+// whole ring elements.  One pass of coalesced loads instead of the tiled kernel's serial
+// k-tiles with two barriers each (a 100 x 128 by 128 x 1 product: ~25 us there).  The same
+// ring sums (addition mod 2^w is associative), so the same products.
+template <class T>
+__device__ __forceinline__ T shfl_xor_wave(T v, int m) {
+  constexpr int W = (int)(sizeof(T) / 4);
+  uint32_t w[W];
+#pragma unroll
+  for (int q = 0; q < W; ++q) w[q] = (uint32_t)(v >> (32 * q));
+#pragma unroll
+  for (int q = 0; q < W; ++q) w[q] = (uint32_t)__shfl_xor((int)w[q], m, 64);
+  T r = 0;
+#pragma unroll
+  for (int q = 0; q < W; ++q) r |= (T)w[q] << (32 * q);
+  return r;
+}
+
+template <class T>
+__device__ __forceinline__ void d_gemv_valu(int64_t M, int64_t N, int64_t K,
+                                            const T* __restrict__ A0, const T* __restrict__ A1,
+                                            const T* __restrict__ B0, const T* __restrict__ B1,
+                                            int mode, T* __restrict__ C, int accumulate,
+                                            int64_t a_bs, int64_t b_bs, int zb) {
+  const int64_t b = zb >= 0 ? zb : blockIdx.z;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= M) return;  // uniform per wave: the butterfly below sees whole waves
+  const T* a0 = A0 + b * a_bs + row * K;
+  const T* a1 = mode ? A1 + b * a_bs + row * K : nullptr;
+  const T* b0 = B0 + b * b_bs;
+  const T* b1 = mode ? B1 + b * b_bs : nullptr;
+  for (int64_t n = 0; n < N; ++n) {
+    T acc = 0;
+    for (int64_t k = lane; k < K; k += 64) {
+      const T y0 = b0[k * N + n];
+      if (mode) {
+        acc += a0[k] * (y0 + b1[k * N + n]) + a1[k] * y0;
+      } else {
+        acc += a0[k] * y0;
+      }
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) acc += shfl_xor_wave(acc, m);
+    if (lane == 0) {
+      T* c = C + b * M * N + row * N + n;
+      *c = accumulate ? (T)(*c + acc) : acc;
+    }
+  }
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) k_gemv_valu(int64_t M, int64_t N, int64_t K,
+                                                   const T* __restrict__ A0,
+                                                   const T* __restrict__ A1,
+                                                   const T* __restrict__ B0,
+                                                   const T* __restrict__ B1, int mode,
+                                                   T* __restrict__ C, int accumulate,
+                                                   int64_t a_bs, int64_t b_bs, int zb) {
+  d_gemv_valu<T>(M, N, K, A0, A1, B0, B1, mode, C, accumulate, a_bs, b_bs, zb);
+}
+
+MX_X3(k_gemv_valu<u64>, d_gemv_valu<u64>);
+MX_X3(k_gemv_valu<u128>, d_gemv_valu<u128>);
+
+// MOOSEX_GEMV=0: skinny products on the tiled kernel too
+bool gemv_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("MOOSEX_GEMV");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <class T>
 int launch_gemm_valu(int64_t batch, int64_t M, int64_t N, int64_t K, const void* A0,
                      const void* A1, const void* B0, const void* B1, int mode, void* C,
                      int accumulate, hipStream_t st, int64_t a_bs = -1, int64_t b_bs = -1) {
+  if (N <= 4 && gemv_on()) {
+    const dim3 grid((unsigned)((M + 3) / 4), 1, (unsigned)batch);
+    hipLaunchKernelGGL((k_gemv_valu<T>), grid, dim3(256), 0, st, M, N, K, (const T*)A0,
+                       (const T*)A1, (const T*)B0, (const T*)B1, mode, (T*)C, accumulate,
+                       a_bs < 0 ? M * K : a_bs, b_bs < 0 ? K * N : b_bs, batch == 1 ? 0 : -1);
+    MX_LAUNCH_CHECK();
+    return 0;
+  }
   constexpr int TS = 16;
   dim3 grid((unsigned)((N + TS - 1) / TS), (unsigned)((M + TS - 1) / TS), (unsigned)batch);
   dim3 block(TS, TS);

@@ -339,6 +339,13 @@ DAG_COMPOSE = os.environ.get("MOOSEX_PARTY_GRAPH_DAG", "0") == "1"
 MERGE_PARTIES = os.environ.get("MOOSEX_PARTY_MERGE", "1") != "0"
 
 
+def _touch(dst: int, src: int) -> int:
+    """The parties a message copy writes to and reads from, as a bitmask (every party when
+    one is beyond the third): the composed graph's merging keeps each party's launches
+    on their side of every copy that touches the party (csrc/graph_compose.hip)."""
+    return 7 if dst > 2 or src > 2 else (1 << dst) | (1 << src)
+
+
 def chunk_bounds(kinds, per: int):
     """[(start, end)) node ranges of a composed schedule, each holding at most ``per``
     segment nodes (kind 0); a chunk starts at a segment, so the copies after a chunk's last
@@ -624,7 +631,7 @@ class PartyTapes:
             if len(msgs) == 1 or not batched:
                 for _p, _s, t, buf in msgs:
                     kinds.append(1)
-                    party.append(-1)
+                    party.append(_touch(_p, _s))
                     child.append(0)
                     dst.append(buf.data_ptr())
                     src.append(t.data_ptr())
@@ -633,7 +640,10 @@ class PartyTapes:
             descs.append([(t.data_ptr(), buf.data_ptr(), t.numel() * t.element_size())
                           for _p, _s, t, buf in msgs])
             kinds.append(2)
-            party.append(-1)
+            mask = 0
+            for _p, _s, _t, _b in msgs:
+                mask |= _touch(_p, _s)
+            party.append(mask)
             child.append(len(msgs))
             dst.append(len(descs) - 1)  # the table's address is filled in below
             src.append(0)

@@ -101,6 +101,23 @@ def test_gemm_matches_host(bits, shape):
 
 
 @pytest.mark.parametrize("bits", [64, 128])
+@pytest.mark.parametrize("shape", [(100, 128, 1), (128, 100, 1), (7, 300, 3), (129, 65, 4),
+                                   (1, 1, 1), (5, 1000, 2)])
+def test_skinny_gemm_matches_host(bits, shape):
+    """N <= 4: the wave-per-row product (k_gemv_valu), batched and single, plain and the
+    RSS cross form, equal to the host's."""
+    M, K, N = shape
+    a, b = rand_rt((2, M, K), bits, 12), rand_rt((2, K, N), bits, 13)
+    same(R.dot(a, b, nb=1), R.dot(gpu(a), gpu(b), nb=1))
+    a1, b1 = rand_rt((M, K), bits, 14), rand_rt((K, N), bits, 15)
+    same(R.dot(a1, b1), R.dot(gpu(a1), gpu(b1)))
+    xs = [rand_rt((3, M, K), bits, 40 + i) for i in range(2)]
+    ys = [rand_rt((3, K, N), bits, 50 + i) for i in range(2)]
+    same(R.dot_cross(xs[0], xs[1], ys[0], ys[1], nb=1),
+         R.dot_cross(*[gpu(t) for t in xs + ys], nb=1))
+
+
+@pytest.mark.parametrize("bits", [64, 128])
 def test_gemm_cross_matches_host(bits):
     M, K, N = 96, 160, 128
     xs = [rand_rt((3, M, K), bits, 20 + i) for i in range(2)]
