@@ -192,9 +192,7 @@ class ThreadTransport:
                 continue
             if self.landing is not None:
                 buf = self._take_landing(src, out)
-                whole = (out._base is None and out.storage_offset() == 0 and out.is_contiguous()
-                         and out.untyped_storage().nbytes() == out.numel() * out.element_size())
-                if whole and tuple(buf.shape) == tuple(out.shape):
+                if _whole(out) and tuple(buf.shape) == tuple(out.shape):
                     out.set_(buf)  # the protocol's tensor now IS the persistent buffer
                     land.append((buf, src))
                 else:  # a view: land in the persistent buffer, copy after the round
@@ -297,7 +295,16 @@ class ThreadTransport:
                 self.send(t, dst)
         for out, src in recvs:
             if out.numel():
-                out.copy_(self.recv(src).reshape(out.shape))
+                y = self.recv(src)
+                if isinstance(y, R.RT):
+                    y = y.data
+                if (_whole(out) and y.device == out.device and y.dtype == out.dtype
+                        and y.numel() == out.numel() and y.is_contiguous()):
+                    # the received tensor is a private copy already: adopt its storage
+                    # instead of copying it once more
+                    out.set_(y.view(out.shape))
+                else:
+                    out.copy_(y.reshape(out.shape))
 
     def end_evaluation(self):
         pass
@@ -337,6 +344,12 @@ DAG_COMPOSE = os.environ.get("MOOSEX_PARTY_GRAPH_DAG", "0") == "1"
 # the composed chain batches the same launch of several parties into one node
 # (csrc/party_batch.h; MOOSEX_PARTY_MERGE=0: one node per launch)
 MERGE_PARTIES = os.environ.get("MOOSEX_PARTY_MERGE", "1") != "0"
+
+
+def _whole(t: torch.Tensor) -> bool:
+    """``t`` is its storage's only view (not a slice or view of a larger tensor)."""
+    return (t._base is None and t.storage_offset() == 0 and t.is_contiguous()
+            and t.untyped_storage().nbytes() == t.numel() * t.element_size())
 
 
 def _touch(dst: int, src: int) -> int:

@@ -19,7 +19,8 @@ def main():
     from moose_amd.runtime.interpreter import Interpreter
     from moose_amd.runtime.local import LocalMooseRuntime, to_native
 
-    native = to_native(build("seq", 1))
+    k = int(os.environ.get("EAGER_K", "1"))
+    native = to_native(build("seq", k))
     args = {"x_arg": np.ones((1, 1)), "y_arg": np.identity(1)}
     ids = ["alice", "bob", "carole"]
     rt = LocalMooseRuntime(ids, device_map={i: "cuda:0" for i in ids}, use_graphs=False,
@@ -58,7 +59,8 @@ def main():
             st.add(p)
         s = io.StringIO()
         st.stream = s
-        st.sort_stats("tottime").print_stats(16)
+        st.sort_stats(os.environ.get("EAGER_SORT", "tottime")).print_stats(
+            int(os.environ.get("EAGER_TOP", "16")))
         print(f"== {name}\n" + s.getvalue(), flush=True)
 
 
