@@ -488,8 +488,9 @@ static int graph_compose_impl(int n, const int* kind, void* const* child, void* 
 }
 
 // The composed total order as ONE chain with party-batched launches (party_batch.h):
-// kind / child / dst / src / bytes as mx_graph_compose, party[i] = the party of segment i
-// (kind 0), or for a copy node the bitmask of the parties it reads from or writes to.
+// kind / child / dst / src / bytes as mx_graph_compose (and kind 3: an upload of bytes[i]
+// from pinned host memory src[i] to dst[i]), party[i] = the party of segment i (kind 0), or
+// for a copy node the bitmask of the parties it reads from or writes to.
 // Each maximal run of segments between two copy nodes is a phase: the parties' launches in
 // it are independent, so the same launch of 2-3 parties becomes one node.
 // stats[0..3] = nodes, launches merged away, batched nodes, phases.
@@ -525,9 +526,11 @@ int mx_graph_compose_merged(int n, const int* kind, void* const* child, void* co
         kp.blockDim = dim3(256, 1, 1);
         kp.kernelParams = args;
         rc = hipGraphAddKernelNode(&node, g, prev.data(), prev.size(), &kp);
-      } else {
+      } else {  // 1: a message copy; 3: an argument upload from pinned host memory
         rc = hipGraphAddMemcpyNode1D(&node, g, prev.data(), prev.size(), dst[i], src[i],
-                                     (size_t)bytes[i], hipMemcpyDeviceToDevice);
+                                     (size_t)bytes[i],
+                                     kind[i] == 3 ? hipMemcpyHostToDevice
+                                                  : hipMemcpyDeviceToDevice);
       }
       if (rc != hipSuccess) {
         hipGraphDestroy(g);

@@ -240,6 +240,16 @@ int mx_enable_peer(int dev, int peer) {
   return e == hipSuccess ? 0 : -2;
 }
 
+// An asynchronous copy on ``stream`` (a replay's argument upload from pinned host memory:
+// one call instead of a framework copy op)
+int mx_copy_async(void* dst, const void* src, int64_t bytes, void* stream) {
+  if (bytes <= 0) return 0;
+  return hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDefault, (hipStream_t)stream) ==
+                 hipSuccess
+             ? 0
+             : -1;
+}
+
 int mx_key_refresh(void* slots, int n, const void* master, void* epoch, void* stream) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(k_key_refresh, dim3(1), dim3(256), 0, (hipStream_t)stream,

@@ -289,7 +289,8 @@ __global__ void __launch_bounds__(256)
 // Round 2 (k_dot_tail_r2, one component): P0's o1 / P1's o0 = w0 + w1.
 template <class T>
 __device__ __forceinline__ void
-    d_jobs_r2(const Jobs& js, int64_t n, int role, const T* __restrict__ a, const T* __restrict__ b) {
+    d_jobs_r2(const Jobs& js, int64_t n, int role, const T* __restrict__ a,
+              const T* __restrict__ b) {
   if (role != 0 && role != 1) return;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -318,9 +319,9 @@ struct Streams {
 
 template <class T>
 __device__ __forceinline__ void
-    d_jobs_r0_lat(const Jobs& js, int64_t n, int m, int role, int main, int dealer, T* __restrict__ msg,
-                  T* __restrict__ msg_rt, u64* __restrict__ msg_rm, const mxd::KeySrc& keys,
-                  const Streams& ss) {
+    d_jobs_r0_lat(const Jobs& js, int64_t n, int m, int role, int main, int dealer,
+                  T* __restrict__ msg, T* __restrict__ msg_rt, u64* __restrict__ msg_rm,
+                  const mxd::KeySrc& keys, const Streams& ss) {
   // streams: main 0..1 (P0: a, r; P1: b, r; P2: a, b), dealer 2..7 (P2: r0, r1, t, m, z0, z2)
   __shared__ uint32_t rks[2][mxd::kKeyWords];
   __shared__ uint64_t kl[8][kLatEpb], kh[8][kLatEpb];

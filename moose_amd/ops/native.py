@@ -247,6 +247,7 @@ _SIGS = {
                             c_vp, c_vp, c_vp,
                             c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mx_key_refresh": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp]),
+    "mx_copy_async": (c_int, [c_vp, c_vp, ctypes.c_int64, c_vp]),
     "mx_key_refresh_host": (None, [c_vp, c_u64, c_int, c_vp]),
     "mx_copy_many": (c_int, [c_vp, c_int, c_i64, c_vp]),
     "mx_graph_free": (c_int, [c_vp, c_vp]),

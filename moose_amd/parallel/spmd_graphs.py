@@ -39,6 +39,7 @@ from typing import Optional
 import numpy as np
 import torch
 
+from moose_amd.ops import native as nat
 from moose_amd.parallel.transport import CommStep
 from moose_amd.runtime import graphs as G
 from moose_amd.runtime.interpreter import Interpreter
@@ -205,11 +206,27 @@ class SPMDTape:
             allk[(idx + 2) % 3] = bytes(16)
             self.keys._write(base, allk)
 
-    def copy_arguments(self, arguments: dict):
+    def pinned(self, k):
+        """(pinned host tensor, its numpy view): the staging buffer of argument ``k``."""
+        t = self.static[k]
+        pin = self._pinned.get(k)
+        if pin is None or pin[0].shape != t.shape or pin[0].dtype != t.dtype:
+            pt = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            pin = self._pinned[k] = (pt, pt.numpy())
+        return pin
+
+    def uploads(self):
+        """[(device buffer, pinned staging buffer)] of the arguments this tape uploads (a
+        composed graph copies them itself: PartyTapes._compose)."""
+        return [(self.static[k], self.pinned(k)[0]) for k in sorted(self.owns_static)
+                if isinstance(self.static.get(k), torch.Tensor) and self.static[k].is_cuda]
+
+    def copy_arguments(self, arguments: dict, upload: bool = True):
         """The new arguments into the static buffers, on the current stream: through a
         pinned staging buffer per argument (an asynchronous DMA; a pageable copy would hold
         the host until it ran).  The previous replay has completed (its outputs were
-        decoded), so the staging buffer is free."""
+        decoded), so the staging buffer is free.  ``upload=False``: only staged (the graph
+        holds the copies)."""
         for k, v in arguments.items():
             t = self.static.get(k)
             if not isinstance(t, torch.Tensor) or k not in self.owns_static:
@@ -220,12 +237,12 @@ class SPMDTape:
                 src = torch.from_numpy(np.ascontiguousarray(a).reshape(t.shape))
                 t.copy_(src if src.dtype == t.dtype else src.to(t.dtype))
                 continue
-            pin = self._pinned.get(k)
-            if pin is None or pin[0].shape != t.shape or pin[0].dtype != t.dtype:
-                pt = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
-                pin = self._pinned[k] = (pt, pt.numpy())
+            pin = self.pinned(k)
             np.copyto(pin[1], a.reshape(t.shape), casting="unsafe")  # no torch dispatch
-            t.copy_(pin[0], non_blocking=True)
+            if upload:
+                nat.check(nat.lib().mx_copy_async(t.data_ptr(), pin[0].data_ptr(),
+                    t.numel() * t.element_size(),
+                    torch.cuda.current_stream(t.device).cuda_stream), "argument upload")
         if self.tap.loads:  # the stored values this replay loads, as arguments
             self.tap.refresh(self.storage)
 

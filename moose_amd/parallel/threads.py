@@ -629,7 +629,18 @@ class PartyTapes:
         keyg = {p: g for p, g in ((p, self._key_graph(t)) for p, t in enumerate(self.tapes))
                 if g is not None} if batched and MERGE_PARTIES else {}
         acts = [("g", p, g) for p, g in keyg.items()] + acts
+        # the argument uploads (pinned staging -> static buffer) as the graph's first
+        # nodes: a replay only stages the new values on the host
+        ups = [(t, pin) for tape in self.tapes for t, pin in tape.uploads()] \
+            if batched and MERGE_PARTIES and CHUNK_SEGMENTS <= 0 else []
         kinds, child, dst, src, nbytes, party = [], [], [], [], [], []
+        for t, pin in ups:
+            kinds.append(3)
+            child.append(0)
+            dst.append(t.data_ptr())
+            src.append(pin.data_ptr())
+            nbytes.append(t.numel() * t.element_size())
+            party.append(7)
         descs = []
         for a in acts:
             if a[0] == "g":
@@ -683,6 +694,7 @@ class PartyTapes:
                 arr(ctypes.c_int64, nbytes), arr(ctypes.c_int, party), st, ctypes.byref(g),
                 ctypes.byref(ex))
             if rc == 0:
+                self._uploads_in_graph = bool(ups)
                 self._keys_in_graph = set(keyg)
                 self._key_graphs = keyg  # alive as long as the composed graph
                 self._graph_handles = [(g, ex)]
@@ -691,9 +703,9 @@ class PartyTapes:
                                     "nodes": st[0], "merged_away": st[1],
                                     "party_batched": st[2], "phases": st[3]}
                 return [ex]
-        if keyg:  # not composed with the merged chain: the host refreshes the keys
+        if keyg or ups:  # not composed with the merged chain: the host does these
             kinds, child, dst, src, nbytes, party = (
-                xs[len(keyg):] for xs in (kinds, child, dst, src, nbytes, party))
+                xs[len(ups) + len(keyg):] for xs in (kinds, child, dst, src, nbytes, party))
         # the total order as one executable, or in chunks of at most CHUNK_SEGMENTS
         # segments launched back to back on one stream
         bounds = (chunk_bounds(kinds, CHUNK_SEGMENTS) if CHUNK_SEGMENTS > 0
@@ -1218,8 +1230,9 @@ class PartyTapes:
         s = self.streams[0]
         t0 = time.perf_counter()
         with torch.cuda.stream(s):
+            upload = not getattr(self, "_uploads_in_graph", False)
             for tape in self.tapes:
-                tape.copy_arguments(arguments)
+                tape.copy_arguments(arguments, upload=upload)
             t1 = time.perf_counter()
             in_graph = getattr(self, "_keys_in_graph", ())
             for p, tape in enumerate(self.tapes):

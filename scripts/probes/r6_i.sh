@@ -3,7 +3,7 @@
 # broadcasts of one-element add / sub operands: replay tests, LR and LogReg parties
 cd "$(dirname "$0")/../.."
 export PYTHONPATH=$PWD TMPDIR=/tmp
-out=gpurun_out/r6m
+out=gpurun_out/r6r
 mkdir -p $out
 timeout -k 10 600 python -u -m pytest -v --timeout 120 --timeout-method thread -m gpu \
   tests/test_threads.py tests/test_storage_replay.py tests/test_merge_rounds.py \
