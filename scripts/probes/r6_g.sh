@@ -3,7 +3,7 @@
 # tape (composed, merged vs not; per-party chains), smoke, and the driver's bench command
 cd "$(dirname "$0")/../.."
 export PYTHONPATH=$PWD TMPDIR=/tmp
-out=gpurun_out/r6g
+out=gpurun_out/r6s
 mkdir -p $out
 timeout -k 10 1000 python -u -m pytest -v --timeout 120 --timeout-method thread -m gpu tests \
   > $out/pytest.log 2>&1
