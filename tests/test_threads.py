@@ -204,6 +204,45 @@ def test_thread_party_tapes_replay_bitwise_equal_eager(mode, monkeypatch):
         assert tapes.graph_nodes["merged_away"] > 0, tapes.graph_nodes
 
 
+@pytest.mark.gpu
+def test_composed_replay_with_an_outsider_bitwise_equal_eager():
+    """Four in-process parties on cuda:0, one output revealed to dave (outside the
+    replicated placement): the composed replay keeps the fourth party's segments unbatched
+    and in order, and every replay equals the eager seeded evaluation bitwise.  (An input
+    OWNED by an outsider is shared with host-drawn fresh seeds, which a tape does not
+    replay: such a computation stays eager.)"""
+    alice, bob, carole, dave = (pm.host_placement(n) for n in IDS + ["dave"])
+    rep = pm.replicated_placement("rep", players=[alice, bob, carole])
+    fp = pm.fixed(14, 23)
+
+    @pm.computation
+    def comp(x: pm.Argument(placement=alice, vtype=pm.TensorType(pm.float64)),
+             y: pm.Argument(placement=bob, vtype=pm.TensorType(pm.float64))):
+        with alice:
+            xf = pm.cast(x, dtype=fp)
+        with bob:
+            yf = pm.cast(y, dtype=fp)
+        with rep:
+            z = pm.dot(xf, yf)
+            s = pm.sigmoid(z)
+        with dave:
+            return pm.cast(s, dtype=pm.float64), pm.cast(z, dtype=pm.float64)
+
+    idents = IDS + ["dave"]
+    args = _args()
+    devs = {i: "cuda:0" for i in idents}
+    want = LocalMooseRuntime(idents, device_map=devs, seed=5,
+                             use_graphs=False).evaluate_computation(comp, args)
+    rt = LocalMooseRuntime(idents, device_map=devs, seed=5, use_graphs=True)
+    for _ in range(4):
+        got = rt.evaluate_computation(comp, args)
+        assert set(got) == set(want)
+        for k in want:
+            assert np.array_equal(np.asarray(got[k]), np.asarray(want[k])), k
+    (_, tapes), = rt._party_tapes.values()
+    assert tapes is not False and tapes.replay_form == "composed"
+
+
 def test_party_tapes_schedule_pairs_rounds():
     """The replay order of PartyTapes (CPU, mock tapes): a ring shift, then a dealer's
     send-only round to two receive-only parties.  Every receive is issued after its
