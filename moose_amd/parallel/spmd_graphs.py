@@ -200,9 +200,16 @@ class SPMDTape:
         draw = lambda: bytes(torch.randint(0, 256, (16,), generator=rng,  # noqa: E731
                                            dtype=torch.uint8).tolist())
         for base, idx in self.sess.key_setups:
+            if base == "seed":  # a fresh seed (SPMDSession.h_fresh_seed): one draw
+                b = draw()
+                if idx is not None:
+                    self.keys._write(idx, [b])
+                continue
             allk = [draw() for _ in range(4)]
             if idx is None:
                 continue
+            for _ in range(4):  # the member's alloc(4) draws too (SPMDSession.setup)
+                draw()
             allk[(idx + 2) % 3] = bytes(16)
             self.keys._write(base, allk)
 

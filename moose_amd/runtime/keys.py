@@ -48,6 +48,25 @@ class KeyRef:
         return 16
 
 
+class KeyBuf:
+    """A fresh seed received from its owner: the owner's key slot image (raw key and AES
+    schedule, SLOT_WORDS int32) in a buffer of the receiver (parallel/spmd.py move).  Like
+    :class:`KeyRef`, SampleSeeded expands it from ``ptr``."""
+
+    __slots__ = ("t",)
+    table = None  # SampleSeeded tells key-slot seeds from raw bytes by this attribute
+
+    def __init__(self, t: torch.Tensor):
+        self.t = t
+
+    @property
+    def ptr(self):
+        return self.t.data_ptr()
+
+    def __len__(self):
+        return 16
+
+
 def slot_words(keys) -> np.ndarray:
     """Host image of ``len(keys)`` slots."""
     raw = b"".join(bytes(k) for k in keys)

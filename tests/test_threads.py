@@ -205,12 +205,16 @@ def test_thread_party_tapes_replay_bitwise_equal_eager(mode, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_composed_replay_with_an_outsider_bitwise_equal_eager():
-    """Four in-process parties on cuda:0, one output revealed to dave (outside the
-    replicated placement): the composed replay keeps the fourth party's segments unbatched
-    and in order, and every replay equals the eager seeded evaluation bitwise.  (An input
-    OWNED by an outsider is shared with host-drawn fresh seeds, which a tape does not
-    replay: such a computation stays eager.)"""
+@pytest.mark.parametrize("where", ["output", "input"])
+def test_composed_replay_with_an_outsider_bitwise_equal_eager(where):
+    """Four in-process parties on cuda:0 and dave outside the replicated placement, who
+    receives an output or OWNS an input (shared with two fresh seeds: key slots the tape
+    refreshes at every replay and ships as slot images).  The composed replay keeps the
+    fourth party's segments unbatched and in order, and every replay equals the eager
+    seeded evaluation bitwise."""
+    if where == "input":
+        _replay_equals_eager(_comp(True), IDS + ["dave"], _args())
+        return
     alice, bob, carole, dave = (pm.host_placement(n) for n in IDS + ["dave"])
     rep = pm.replicated_placement("rep", players=[alice, bob, carole])
     fp = pm.fixed(14, 23)
@@ -228,8 +232,10 @@ def test_composed_replay_with_an_outsider_bitwise_equal_eager():
         with dave:
             return pm.cast(s, dtype=pm.float64), pm.cast(z, dtype=pm.float64)
 
-    idents = IDS + ["dave"]
-    args = _args()
+    _replay_equals_eager(comp, IDS + ["dave"], _args())
+
+
+def _replay_equals_eager(comp, idents, args):
     devs = {i: "cuda:0" for i in idents}
     want = LocalMooseRuntime(idents, device_map=devs, seed=5,
                              use_graphs=False).evaluate_computation(comp, args)
@@ -241,6 +247,7 @@ def test_composed_replay_with_an_outsider_bitwise_equal_eager():
             assert np.array_equal(np.asarray(got[k]), np.asarray(want[k])), k
     (_, tapes), = rt._party_tapes.values()
     assert tapes is not False and tapes.replay_form == "composed"
+    assert tapes.tapes[0].replays >= 2
 
 
 def test_party_tapes_schedule_pairs_rounds():
