@@ -63,6 +63,8 @@ MERGE_ROUNDS = os.environ.get("MOOSEX_MERGE_ROUNDS", "1") != "0"
 # per-operation nonce scopes (runtime/session.py nonce_scope; MOOSEX_NONCE_SCOPES=0: one
 # session-wide counter, the round-5 numbering)
 NONCE_SCOPES = os.environ.get("MOOSEX_NONCE_SCOPES", "1") != "0"
+# operand + output elements of one batched Dot call (Interpreter._batch_dots)
+BATCH_DOT_ELEMS = int(os.environ.get("MOOSEX_BATCH_DOT_ELEMS", str(1 << 25)))
 # per-party sessions broadcast a one-element secret operand of add / sub / mul inside the
 # kernels instead of materialising it (MOOSEX_BCAST_IN_KERNEL=0: materialised)
 BCAST_IN_KERNEL = os.environ.get("MOOSEX_BCAST_IN_KERNEL", "1") != "0"
@@ -270,6 +272,12 @@ class Interpreter:
         if k0 is None:
             return False
         group = [(op, k0[1], k0[2])]
+        # one batched product stays within a bounded operand + output size (the batched GEMM
+        # and its workspace grow with it: 100 products of 1000 x 1000 in one call asked for
+        # tens of GiB); the rest are batched by the next Dot's call
+        (_, _, sx, sy) = k0[0]
+        per = sx[0] * sx[1] + sy[0] * sy[1] + sx[0] * sy[1]
+        limit = max(1, min(limit, BATCH_DOT_ELEMS // max(1, per)))
         for o in later:
             if len(group) >= limit:
                 break
