@@ -63,6 +63,23 @@ class Hub:
         self.timeout = timeout
         self.lock = threading.Lock()
         self.done = [False] * n  # party i's thread has returned (successfully or not)
+        # the baton (BATON): one party thread runs Python at a time and hands over only
+        # while it waits for a message -- three threads trading the interpreter lock at
+        # every framework call cost each small op several times its own time
+        self.baton = threading.Lock() if BATON else None
+
+    def hold(self):
+        if self.baton is not None:
+            self.baton.acquire()
+            self._holder = threading.get_ident()
+
+    def release(self) -> bool:
+        """Hand the baton over if this thread holds it; True when it did."""
+        if self.baton is None or getattr(self, "_holder", None) != threading.get_ident():
+            return False
+        self._holder = None
+        self.baton.release()
+        return True
 
     def fail(self, why: str):
         with self.lock:
@@ -129,6 +146,18 @@ class ThreadTransport:
 
     def _get(self, src: int):
         box = self.hub.boxes[(src, self.rank)]
+        try:  # already there: no hand-over
+            return box.get_nowait()
+        except queue.Empty:
+            pass
+        handed = self.hub.release()  # another party runs while this one waits
+        try:
+            return self._wait(box, src)
+        finally:
+            if handed:
+                self.hub.hold()
+
+    def _wait(self, box, src: int):
         waited = 0.0
         while True:
             try:
@@ -341,6 +370,9 @@ VALIDATE_STREAMS = os.environ.get("MOOSEX_PARTY_STREAMS_VALIDATE", "1") != "0"
 # branches may run concurrently inside the one launch.  Needs persistent landing buffers
 # (ThreadTransport.prepare_landing; profiles/r5_party_dag_hazard.md)
 DAG_COMPOSE = os.environ.get("MOOSEX_PARTY_GRAPH_DAG", "0") == "1"
+# in-process parties run their Python one at a time, handing over while they wait for a
+# message (Hub.baton; MOOSEX_PARTY_BATON=0: free-running threads)
+BATON = os.environ.get("MOOSEX_PARTY_BATON", "1") != "0"
 # the composed chain batches the same launch of several parties into one node
 # (csrc/party_batch.h; MOOSEX_PARTY_MERGE=0: one node per launch)
 MERGE_PARTIES = os.environ.get("MOOSEX_PARTY_MERGE", "1") != "0"
@@ -398,6 +430,7 @@ def run_parties(comp, arguments: dict, identities: List[str], devices: List, sto
         ident, dev = identities[i], hub.devices[i]
         tr = ThreadTransport(i, hub)
         rec = None
+        hub.hold()
         try:
             if record:  # this thread's host->device copies go to its recorder
                 rec = G._Recorder()
@@ -442,6 +475,7 @@ def run_parties(comp, arguments: dict, identities: List[str], devices: List, sto
             if rec is not None:
                 R.set_upload_hook(None)
             hub.finish(i)
+            hub.release()
 
     threads = [threading.Thread(target=party, args=(i,), name=f"moose-party-{identities[i]}",
                                 daemon=True) for i in range(len(identities))]
