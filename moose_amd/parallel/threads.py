@@ -23,6 +23,7 @@ additionally be pinned to different MI355Xs (SURVEY §7.1 "3 parties on 1 or 3 G
 """
 from __future__ import annotations
 
+import functools
 import math
 import os
 import queue
@@ -406,6 +407,39 @@ def chunk_bounds(kinds, per: int):
     return bounds
 
 
+class _Workers:
+    """Party threads kept between evaluations: starting three threads per evaluation cost
+    ~0.8 ms of an eager one (the interpreter bootstraps each while the parties run).  A
+    worker runs one party at a time under that party's thread name; a worker still busy
+    (a party that never returned) is simply not reused -- a new one starts."""
+
+    def __init__(self):
+        self._idle = queue.SimpleQueue()
+
+    def run(self, fn, name: str) -> threading.Event:
+        done = threading.Event()
+        try:
+            inbox = self._idle.get_nowait()
+        except queue.Empty:
+            inbox = queue.SimpleQueue()
+            threading.Thread(target=self._loop, args=(inbox,), name=name, daemon=True).start()
+        inbox.put((fn, name, done))
+        return done
+
+    def _loop(self, inbox):
+        while True:
+            fn, name, done = inbox.get()
+            threading.current_thread().name = name
+            try:
+                fn()
+            finally:
+                done.set()
+                self._idle.put(inbox)
+
+
+_WORKERS = _Workers()
+
+
 def run_parties(comp, arguments: dict, identities: List[str], devices: List, storage: dict,
                 fixedpoint_ring: int = 128, seed: Optional[int] = None,
                 timeout: Optional[float] = None, record: bool = False):
@@ -477,19 +511,17 @@ def run_parties(comp, arguments: dict, identities: List[str], devices: List, sto
             hub.finish(i)
             hub.release()
 
-    threads = [threading.Thread(target=party, args=(i,), name=f"moose-party-{identities[i]}",
-                                daemon=True) for i in range(len(identities))]
     R.shared_streams(+1)  # shared device constants: their producer drains first
     try:
-        for t in threads:
-            t.start()
-        for t in threads:
+        names = [f"moose-party-{identities[i]}" for i in range(len(identities))]
+        done = [_WORKERS.run(functools.partial(party, i), names[i])
+                for i in range(len(identities))]
+        for name, ev in zip(names, done):
             # every blocked receive gives up within the hub's timeout (or at once when its
-            # sender has returned), so the joins end; the bound is a last resort
-            t.join(hub.timeout + 60.0)
-            if t.is_alive():
-                hub.fail(f"{t.name} did not finish")
-                raise TransportError(f"{t.name} did not finish within {hub.timeout + 60.0} s")
+            # sender has returned), so the waits end; the bound is a last resort
+            if not ev.wait(hub.timeout + 60.0):
+                hub.fail(f"{name} did not finish")
+                raise TransportError(f"{name} did not finish within {hub.timeout + 60.0} s")
     finally:
         R.shared_streams(-1)
     if errors:
