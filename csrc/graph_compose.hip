@@ -489,8 +489,9 @@ static int graph_compose_impl(int n, const int* kind, void* const* child, void* 
 
 // The composed total order as ONE chain with party-batched launches (party_batch.h):
 // kind / child / dst / src / bytes as mx_graph_compose (and kind 3: an upload of bytes[i]
-// from pinned host memory src[i] to dst[i]), party[i] = the party of segment i (kind 0), or
-// for a copy node the bitmask of the parties it reads from or writes to.
+// from pinned host memory src[i] to dst[i]; kind 4: no node, a round whose messages are all
+// read where their senders wrote them), party[i] = the party of segment i (kind 0), or for
+// a copy node / round boundary the bitmask of the parties it reads from or writes to.
 // Each maximal run of segments between two copy nodes is a phase: the parties' launches in
 // it are independent, so the same launch of 2-3 parties becomes one node.
 // stats[0..3] = nodes, launches merged away, batched nodes, phases.
@@ -510,6 +511,10 @@ int mx_graph_compose_merged(int n, const int* kind, void* const* child, void* co
   alignas(16) static thread_local unsigned char blob[4096];
   std::vector<Item> carry[3];  // a party's launches deferred to the next phase
   for (int i = 0; i < n;) {
+    if (kind[i] == 4) {  // a round whose messages are all read in place: a phase boundary
+      ++i;
+      continue;
+    }
     if (kind[i] != 0) {
       hipGraphNode_t node = nullptr;
       hipError_t rc;

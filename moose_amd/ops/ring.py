@@ -2128,7 +2128,8 @@ def _jobs_abi(jobs):
     return (ctypes.c_void_p * len(ptrs))(*ptrs), (ctypes.c_int64 * len(dims))(*dims)
 
 
-def jobs_r0(jobs, L, bits, m, role, slots, nonces, like, main=True, dealer=True, pend=None):
+def jobs_r0(jobs, L, bits, m, role, slots, nonces, like, main=True, dealer=True, pend=None,
+            alloc=None):
     """Round 0 of the batched per-party tail (mx_jobs_r0): the outgoing message over the
     concatenation of the jobs' rows (P0 m0, P1 m1, P2 z2), the dealer's rt1 / rm1 (P2, when
     ``dealer``), P2's new shares into the jobs' outputs.  ``like``: any tensor of the call's
@@ -2138,9 +2139,11 @@ def jobs_r0(jobs, L, bits, m, role, slots, nonces, like, main=True, dealer=True,
     n = builtins.sum(j.rows for j in jobs) * L
     w = _words(bits)
     shp = (n,) + ((2,) if bits == 128 else ())
-    msg = torch.empty(shp, dtype=torch.int64, device=like.device) if main else None
-    rt = torch.empty(shp, dtype=torch.int64, device=like.device) if role == 2 and dealer else None
-    rm = torch.empty((n,), dtype=torch.int64, device=like.device) if role == 2 and dealer else None
+    # ``alloc(shape)``: where the outgoing messages go (a session's outbox), else fresh
+    new = alloc or (lambda s: torch.empty(s, dtype=torch.int64, device=like.device))
+    msg = new(shp) if main else None
+    rt = new(shp) if role == 2 and dealer else None
+    rm = new((n,)) if role == 2 and dealer else None
     p, d = _jobs_abi(jobs)
     pend = pend or []
     pp = (ctypes.c_void_p * max(1, 3 * len(pend)))(*[t.data_ptr() for r in pend for t in r])
@@ -2154,12 +2157,13 @@ def jobs_r0(jobs, L, bits, m, role, slots, nonces, like, main=True, dealer=True,
     return msg, rt, rm
 
 
-def jobs_r1(jobs, L, bits, m, role, slots, nonces, msg, rmk, rz, rrt, rrm):
+def jobs_r1(jobs, L, bits, m, role, slots, nonces, msg, rmk, rz, rrt, rrm, alloc=None):
     """Round 1 (mx_jobs_r1): P0 / P1 open c from their message, the other's and z2; returns
-    w (P0 w0, P1 w1; None for P2) and writes P0's o0 = z0, P1's o1 = z2."""
+    w (P0 w0, P1 w1; None for P2) and writes P0's o0 = z0, P1's o1 = z2.  ``alloc``: where
+    w goes (the session's outbox)."""
     if role == 2:
         return None
-    w = torch.empty_like(msg)
+    w = alloc(tuple(msg.shape)) if alloc is not None else torch.empty_like(msg)
     p, d = _jobs_abi(jobs)
     ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
     nat.check(nat.lib().mx_jobs_r1(

@@ -277,8 +277,10 @@ def jobs_tail(sess, plc, role, jobs, L, bits, m, nonces, slots, pend=None, defer
     ``defer``: return this level's round-2 sums as a PendingSums instead of running round 2
     (the caller hands them to the next level or flushes them before anything else reads)."""
     like = next(t for j in jobs for t in (j.o0, j.x0, j.a) if t is not None)
+    box = getattr(sess, "outbox", None)
+    alloc = (lambda shp: box(shp)) if box is not None else None
     msg, rt, rm = R.jobs_r0(jobs, L, bits, m, role, slots, nonces, like,
-                            pend=pend.regions if pend is not None else None)
+                            pend=pend.regions if pend is not None else None, alloc=alloc)
     n_el = sum(j.rows for j in jobs) * L
     like_t = ((n_el,) + ((2,) if bits == 128 else ()), torch.int64)
     like_rm = ((n_el,), torch.int64)
@@ -290,7 +292,7 @@ def jobs_tail(sess, plc, role, jobs, L, bits, m, nonces, slots, pend=None, defer
     rmk = got.get("m1") if role == 0 else got.get("m0") if role == 1 else None
     rz = got.get("z2_0") if role == 0 else got.get("z2_1") if role == 1 else None
     w = R.jobs_r1(jobs, L, bits, m, role, slots, nonces, msg, rmk, rz, got.get("rt1"),
-                  got.get("rm1"))
+                  got.get("rm1"), alloc=alloc)
     nb = n_el * (16 if bits == 128 else 8)
     record_tail_traffic(sess.stats, plc, nb, round_b=False)
     got = sess.party_exchange(plc, [("w0", 0, 1, w if role == 0 else None, like_t),

@@ -91,6 +91,73 @@ class Hub:
         self.done[rank] = True
 
 
+class Mailbox:
+    """Messages read where their sender wrote them (the composed one-GPU replay).
+
+    A protocol step that produces a message for another party asks its transport for the
+    buffer first (``outbox``; ``SPMDSession.outbox``).  The tapes are captured twice:
+
+    * pass 1 (normal buffers) learns, for every such message, which send it became --
+      the k-th tensor from party s to party d is the sender's n-th outbox buffer;
+    * pass 2 allocates one persistent buffer per outbox call before capturing again: the
+      sender's kernels write the message straight into it, and the receiver -- knowing the
+      route -- lands the k-th message in it too.  The message round then needs no copy
+      (PartyTapes._compose keeps only a phase boundary).
+
+    Capture is deterministic (same program, same warm-up log), so pass 2 makes the same
+    outbox calls and sends in the same order as pass 1."""
+
+    def __init__(self):
+        self.pass_ = 1
+        self.calls = {}   # (rank, n) -> (shape, dtype) of the n-th outbox request
+        self.keep = {}    # pass 1: (rank, n) -> the tensor handed out (kept alive: unique ptr)
+        self.by_ptr = {}  # pass 1: data_ptr -> (rank, n)
+        self.route = {}   # (src, dst, k) -> n: the k-th message src -> dst is outbox call n
+        self.slots = {}   # pass 2: (rank, n) -> persistent buffer
+
+    def prepare(self, device):
+        """Pass 2's persistent buffers (before its capture: no allocation inside it)."""
+        self.pass_ = 2
+        self.keep, self.by_ptr = {}, {}
+        routed = {(s, n) for (s, _d, _k), n in self.route.items()}
+        for key in sorted(routed):
+            shape, dtype = self.calls[key]
+            self.slots[key] = torch.empty(shape, dtype=dtype, device=device)
+        for key, t in self.slots.items():
+            self.by_ptr[t.data_ptr()] = key
+
+    def outbox(self, rank, n, shape, dtype, device):
+        shape = tuple(shape)
+        if self.pass_ == 1:
+            self.calls[(rank, n)] = (shape, dtype)
+            t = torch.empty(shape, dtype=dtype, device=device)
+            self.keep[(rank, n)] = t
+            self.by_ptr[t.data_ptr()] = (rank, n)
+            return t
+        slot = self.slots.get((rank, n))
+        if slot is None or tuple(slot.shape) != shape or slot.dtype != dtype:
+            return None  # never sent in pass 1 (or a different request): a normal buffer
+        return slot
+
+    def sent(self, rank, dst, k, t):
+        """Pass 1: the k-th message rank -> dst was ``t``: an outbox buffer makes a route."""
+        key = self.by_ptr.get(t.data_ptr())
+        if self.pass_ == 1 and key is not None and key[0] == rank and \
+                t.numel() * t.element_size() == self.keep[key].numel() * \
+                self.keep[key].element_size():
+            self.route[(rank, dst, k)] = key[1]
+
+    def landing(self, src, dst, k, out):
+        """Pass 2: the sender's buffer of the k-th message src -> dst (None: a copy)."""
+        if self.pass_ != 2:
+            return None
+        n = self.route.get((src, dst, k))
+        slot = self.slots.get((src, n)) if n is not None else None
+        if slot is None or slot.numel() != out.numel() or slot.dtype != out.dtype:
+            return None
+        return slot
+
+
 class ThreadTransport:
     """Transport API of :class:`~moose_amd.parallel.transport.Transport` (send / recv /
     shift / exchange) between the threads of a :class:`Hub`."""
@@ -114,6 +181,19 @@ class ThreadTransport:
         # pool (prepare_landing); None: receives land where the protocol allocated them
         self.landing = None
         self._land_cursor = {}
+        # messages read where their sender wrote them (Mailbox; composed one-GPU replays)
+        self.mailbox = None
+        self._outbox_n = 0
+        self._send_k, self._recv_k = {}, {}
+
+    def outbox(self, shape, dtype):
+        """The buffer of a message this party is about to produce and send (Mailbox), or
+        None: the caller allocates it as usual."""
+        if self.mailbox is None or self.tape is None:
+            return None
+        n = self._outbox_n
+        self._outbox_n += 1
+        return self.mailbox.outbox(self.rank, n, shape, dtype, self.device)
 
     # -- payload movement --------------------------------------------------------------
     def _ship(self, t: torch.Tensor, dst: int):
@@ -216,9 +296,26 @@ class ThreadTransport:
         from moose_amd.parallel.transport import CommStep
 
         sends = [(t.contiguous(), dst) for t, dst in sends if t.numel()]
+        mb = self.mailbox
+        for t, dst in sends:
+            k = self._send_k.get(dst, 0)
+            self._send_k[dst] = k + 1
+            if mb is not None:
+                mb.sent(self.rank, dst, k, t)
         land, after = [], []
         for out, src in recvs:
             if out.numel() == 0:
+                continue
+            k = self._recv_k.get(src, 0)
+            self._recv_k[src] = k + 1
+            slot = mb.landing(src, self.rank, k, out) if mb is not None else None
+            if slot is not None:
+                if _whole(out) and out.dtype == slot.dtype:
+                    out.set_(slot.view(out.shape))  # read where the sender wrote it
+                    land.append((slot, src))
+                else:  # a view of something larger: copy after the round (own segment)
+                    land.append((slot, src))
+                    after.append((out, slot))
                 continue
             if self.landing is not None:
                 buf = self._take_landing(src, out)
@@ -371,6 +468,8 @@ VALIDATE_STREAMS = os.environ.get("MOOSEX_PARTY_STREAMS_VALIDATE", "1") != "0"
 # branches may run concurrently inside the one launch.  Needs persistent landing buffers
 # (ThreadTransport.prepare_landing; profiles/r5_party_dag_hazard.md)
 DAG_COMPOSE = os.environ.get("MOOSEX_PARTY_GRAPH_DAG", "0") == "1"
+# composed one-GPU replays: messages read where their senders wrote them (Mailbox)
+INPLACE = os.environ.get("MOOSEX_PARTY_INPLACE", "1") != "0"
 # in-process parties run their Python one at a time, handing over while they wait for a
 # message (Hub.baton; MOOSEX_PARTY_BATON=0: free-running threads)
 BATON = os.environ.get("MOOSEX_PARTY_BATON", "1") != "0"
@@ -564,27 +663,46 @@ class PartyTapes:
         self.streams_mode = env == "1" or (env is None and len(set(self.devices)) > 1)
         single = (len(set(self.devices)) == 1 and not self.streams_mode
                   and os.environ.get("MOOSEX_PARTY_GRAPH", "1") != "0")
-        self.tapes = []
         # the composed graph runs every party on one stream: the tapes share their argument
         # buffers, uploaded once per replay
         self.shared_static = single and not DAG_COMPOSE
-        shared = {}
-        for i, ident in enumerate(identities):
-            tr = ThreadTransport(i, None, device=self.devices[i], world=n)
-            tr.log = warm[ident]["log"]
-            if self.streams_mode or (DAG_COMPOSE and len(set(self.devices)) == 1):
-                # senders write landing buffers at their own pace (streams), or a copy
-                # runs when its sender's branch reaches it (DAG): persistent buffers
+        # ... and read their messages where the senders wrote them (Mailbox: two capture
+        # passes; MOOSEX_PARTY_INPLACE=0: every message copied)
+        mailbox = Mailbox() if (self.shared_static and INPLACE and MERGE_PARTIES
+                                and CHUNK_SEGMENTS <= 0) else None
+
+        def capture():
+            tapes, shared = [], {}
+            for i, ident in enumerate(identities):
+                tr = ThreadTransport(i, None, device=self.devices[i], world=n)
+                tr.log = warm[ident]["log"]
+                tr.mailbox = mailbox
+                if self.streams_mode or (DAG_COMPOSE and len(set(self.devices)) == 1):
+                    # senders write landing buffers at their own pace (streams), or a copy
+                    # runs when its sender's branch reaches it (DAG): persistent buffers
+                    with torch.cuda.device(self.devices[i]):
+                        tr.prepare_landing()
                 with torch.cuda.device(self.devices[i]):
-                    tr.prepare_landing()
-            with torch.cuda.device(self.devices[i]):
-                self.tapes.append(SPMDTape(comp, arguments, ident, role_ranks, tr,
-                                           self.devices[i], storage, ring, seed,
-                                           warm=warm[ident],
-                                           keep_graph=single or self.streams_mode,
-                                           shared_static=shared.setdefault(
-                                               self.devices[i], {})
-                                           if self.shared_static else None))
+                    tapes.append(SPMDTape(comp, arguments, ident, role_ranks, tr,
+                                          self.devices[i], storage, ring, seed,
+                                          warm=warm[ident],
+                                          keep_graph=single or self.streams_mode,
+                                          shared_static=shared.setdefault(
+                                              self.devices[i], {})
+                                          if self.shared_static else None))
+            return tapes
+
+        self.tapes = capture()
+        self.inplace_messages = 0
+        if mailbox is not None and mailbox.route:
+            # pass 2: the routed outbox buffers exist before the capture, senders write
+            # their messages into them and receivers read them there
+            self.tapes = None
+            torch.cuda.synchronize(self.devices[0])
+            mailbox.prepare(self.devices[0])
+            self.tapes = capture()
+            self.inplace_messages = len(mailbox.route)
+        self._mailbox = mailbox  # the persistent message buffers live with the graphs
         self.streams = [t.stream for t in self.tapes]
         self._copy_streams = {}
         self.actions = self._schedule()
@@ -717,7 +835,20 @@ class PartyTapes:
                 src.append(0)
                 nbytes.append(0)
                 continue
-            msgs = a[1]
+            mask = 0
+            for _p, _s, _t, _b in a[1]:
+                mask |= _touch(_p, _s)
+            # a message read where its sender wrote it (Mailbox) needs no copy; a round of
+            # only such messages is a phase boundary (kind 4, no node)
+            msgs = [m for m in a[1] if m[2].data_ptr() != m[3].data_ptr()]
+            if not msgs:
+                kinds.append(4)
+                party.append(mask)
+                child.append(0)
+                dst.append(0)
+                src.append(0)
+                nbytes.append(0)
+                continue
             if len(msgs) == 1 or not batched:
                 for _p, _s, t, buf in msgs:
                     kinds.append(1)
@@ -730,9 +861,6 @@ class PartyTapes:
             descs.append([(t.data_ptr(), buf.data_ptr(), t.numel() * t.element_size())
                           for _p, _s, t, buf in msgs])
             kinds.append(2)
-            mask = 0
-            for _p, _s, _t, _b in msgs:
-                mask |= _touch(_p, _s)
             party.append(mask)
             child.append(len(msgs))
             dst.append(len(descs) - 1)  # the table's address is filled in below
@@ -766,12 +894,17 @@ class PartyTapes:
                 self._graph_handles = [(g, ex)]
                 self.graph_nodes = {"segments": kinds.count(0), "copy_nodes": kinds.count(1),
                                     "copy_batches": kinds.count(2), "executables": 1,
+                                    "inplace_rounds": kinds.count(4),
+                                    "inplace_messages": self.inplace_messages,
                                     "nodes": st[0], "merged_away": st[1],
                                     "party_batched": st[2], "phases": st[3]}
                 return [ex]
         if keyg or ups:  # not composed with the merged chain: the host does these
             kinds, child, dst, src, nbytes, party = (
                 xs[len(ups) + len(keyg):] for xs in (kinds, child, dst, src, nbytes, party))
+        keep = [i for i, k in enumerate(kinds) if k != 4]  # a plain chain needs no boundary
+        kinds, child, dst, src, nbytes, party = (
+            [xs[i] for i in keep] for xs in (kinds, child, dst, src, nbytes, party))
         # the total order as one executable, or in chunks of at most CHUNK_SEGMENTS
         # segments launched back to back on one stream
         bounds = (chunk_bounds(kinds, CHUNK_SEGMENTS) if CHUNK_SEGMENTS > 0

@@ -161,15 +161,16 @@ def test_thread_parties_lr_inference_gpu(monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["serial", "unbatched-launches", "copy-per-message",
-                                  "per-action", "streams"])
+@pytest.mark.parametrize("mode", ["serial", "copied-messages", "unbatched-launches",
+                                  "copy-per-message", "per-action", "streams"])
 def test_thread_party_tapes_replay_bitwise_equal_eager(mode, monkeypatch):
     """Seeded sessions: a replay re-draws the seeded keys as a fresh eager evaluation does,
     so every replay's outputs equal the eager ones bitwise (parties on cuda:0): the tapes
     composed into one hipGraph in a round-synchronous total order (default on one device:
     each round's messages one batched copy kernel, or one copy node per message; the same
     launch of several parties between two rounds one party-batched node, csrc/
-    party_batch.h, or one node per launch), and the per-action replay."""
+    party_batch.h, or one node per launch; the jobs tails' messages read where their
+    senders wrote them, threads.Mailbox, or copied), and the per-action replay."""
     if mode == "streams":
         # per-party stream graphs need their streams on distinct hardware queues: a fresh
         # child process with enough queues (tests/gpu_streams_child.py) -- no skip
@@ -180,6 +181,7 @@ def test_thread_party_tapes_replay_bitwise_equal_eager(mode, monkeypatch):
     monkeypatch.setenv("MOOSEX_PARTY_COPY_BATCH", "0" if mode == "copy-per-message" else "1")
     monkeypatch.setenv("MOOSEX_PARTY_STREAMS", "1" if mode == "streams" else "0")
     monkeypatch.setattr(T, "MERGE_PARTIES", mode != "unbatched-launches")
+    monkeypatch.setattr(T, "INPLACE", mode != "copied-messages")
     comp = _comp(False)
     args = _args()
     devs = {i: "cuda:0" for i in IDS}
@@ -202,6 +204,9 @@ def test_thread_party_tapes_replay_bitwise_equal_eager(mode, monkeypatch):
     assert (tapes._party_graphs is not None) == (mode == "streams")
     if mode == "serial":  # the parties' protocol launches batched into shared nodes
         assert tapes.graph_nodes["merged_away"] > 0, tapes.graph_nodes
+        assert tapes.graph_nodes["inplace_messages"] > 0, tapes.graph_nodes
+    if mode == "copied-messages":
+        assert tapes.inplace_messages == 0
 
 
 @pytest.mark.gpu
