@@ -1757,14 +1757,25 @@ def ks_cross1(g0: RT, g1: RT, p0: RT, p1: RT, d: int, both: bool, keys, nonce: i
     return z
 
 
+def _empty_in(alloc, shape, bits, device) -> RT:
+    """``empty``, or from ``alloc(shape, dtype)`` (a session's outbox: a message)."""
+    if alloc is None:
+        return empty(shape, bits, device)
+    shape = tuple(shape)
+    if bits == 128:
+        return RT(alloc(shape + (2,), torch.int64), 128)
+    return RT(alloc(shape, torch.int64 if bits == 64 else torch.uint8), bits)
+
+
 def ks_cross1_s(g0: RT, g1: RT, p0: RT, p1: RT, d: int, both: bool, slot_ptrs,
-                nonce: int) -> RT:
-    """ks_cross1 with the keys (k_p, k_{p+1}) read from two device key slots."""
+                nonce: int, alloc=None) -> RT:
+    """ks_cross1 with the keys (k_p, k_{p+1}) read from two device key slots (``alloc``:
+    where z, the level's message, goes)."""
     bits = g0.bits
     shp = g0.shape
     datas = [x.data.contiguous() for x in (g0, g1, p0, p1)]
     n = math.prod(shp)
-    z = empty(((2,) + tuple(shp)) if both else tuple(shp), bits, g0.device)
+    z = _empty_in(alloc, ((2,) + tuple(shp)) if both else tuple(shp), bits, g0.device)
     nat.check(
         nat.lib().mx_ks_cross1_s(
             nat.dev_of(z.data), _words(bits), *[nat.ptr(x) for x in datas], nat.ptr(z.data),
@@ -1777,16 +1788,16 @@ def ks_cross1_s(g0: RT, g1: RT, p0: RT, p1: RT, d: int, both: bool, slot_ptrs,
 
 
 def ks_cross1x_s(g0: RT, g1: RT, t0, t1, p0: RT, p1: RT, d: int, both: bool, slot_ptrs,
-                 nonce: int):
+                 nonce: int, alloc=None):
     """ks_cross1_s on g ^ t (the previous level's xor folded into this level's launch;
     t0 = t1 = None: plain ks_cross1_s).  Returns (z, (g0 ^ t0, g1 ^ t1) or None)."""
     if t0 is None:
-        return ks_cross1_s(g0, g1, p0, p1, d, both, slot_ptrs, nonce), None
+        return ks_cross1_s(g0, g1, p0, p1, d, both, slot_ptrs, nonce, alloc=alloc), None
     bits = g0.bits
     shp = g0.shape
     datas = [x.data.contiguous() for x in (g0, g1, t0, t1, p0, p1)]
     n = math.prod(shp)
-    z = empty(((2,) + tuple(shp)) if both else tuple(shp), bits, g0.device)
+    z = _empty_in(alloc, ((2,) + tuple(shp)) if both else tuple(shp), bits, g0.device)
     go0, go1 = empty2(shp, bits, g0.device)
     nat.check(
         nat.lib().mx_ks_cross1x_s(
@@ -1968,16 +1979,17 @@ def _nonces_arr(nonces):
     return (ctypes.c_uint64 * len(nonces))(*[v & MASK64 for v in nonces])
 
 
-def trunc_party_r0(s0: RT, s1: RT, m: int, roles, slots, nonces):
+def trunc_party_r0(s0: RT, s1: RT, m: int, roles, slots, nonces, alloc=None):
     """Round 0 of the per-party TruncPr (mx_trunc_party_r0) on stacked [ncomp, ...] shares.
     Returns (msg, msg_rm, out0, out1): outgoing messages and the (partly filled) new
-    shares."""
+    shares.  ``alloc``: where the messages go."""
     ncomp = len(roles)
     d0 = s0.data.contiguous()
     d1 = s1.data.contiguous()
     n = math.prod(s0.shape) // ncomp
-    msg, out0, out1 = (torch.empty_like(d0) for _ in range(3))
-    msg_rm = torch.empty((ncomp, n), dtype=torch.int64, device=d0.device)
+    msg = _new(alloc, d0.shape, d0.dtype, d0.device)
+    out0, out1 = torch.empty_like(d0), torch.empty_like(d0)
+    msg_rm = _new(alloc, (ncomp, n), torch.int64, d0.device)
     nat.check(nat.lib().mx_trunc_party_r0(
         nat.dev_of(d0), _words(s0.bits), n, m, ncomp, _roles_arr(roles), nat.ptr(d0),
         nat.ptr(d1), nat.ptr(msg), nat.ptr(msg_rm), nat.ptr(out0), nat.ptr(out1),
@@ -1985,11 +1997,12 @@ def trunc_party_r0(s0: RT, s1: RT, m: int, roles, slots, nonces):
     return msg, msg_rm, out0, out1
 
 
-def trunc_party_r1(msg, rmk, rrt, rrm, out0, out1, bits, m, roles, slots, nonces):
+def trunc_party_r1(msg, rmk, rrt, rrm, out0, out1, bits, m, roles, slots, nonces,
+                   alloc=None):
     """Round 1 (mx_trunc_party_r1): returns w; writes P0's s0 / P1's s1 into out0/out1."""
     ncomp = len(roles)
     n = msg.numel() // ncomp // (2 if bits == 128 else 1)
-    w = torch.empty_like(msg)
+    w = _new(alloc, msg.shape, msg.dtype, msg.device)
     nat.check(nat.lib().mx_trunc_party_r1(
         nat.dev_of(msg), _words(bits), n, m, ncomp, _roles_arr(roles), nat.ptr(msg),
         nat.ptr(rmk), nat.ptr(rrt), nat.ptr(rrm), nat.ptr(w), nat.ptr(out0), nat.ptr(out1),
@@ -2031,14 +2044,24 @@ def _dev_stream(ts):
     return nat.dev_of(t), nat.stream_of(t)
 
 
-def dot_tail_r0(cross, bits, m, roles, slots, nonces, out0, out1, n, dealer=True):
+def _new(alloc, shape, dtype, device):
+    """A message buffer: from ``alloc(shape, dtype)`` (a session's outbox, where the
+    receiver reads it in place) or fresh."""
+    if alloc is not None:
+        return alloc(tuple(shape), dtype)
+    return torch.empty(tuple(shape), dtype=dtype, device=device)
+
+
+def dot_tail_r0(cross, bits, m, roles, slots, nonces, out0, out1, n, dealer=True,
+                alloc=None):
     """Round 0 of the per-party dot tail (mx_dot_tail_r0): returns the per-component
     outgoing messages (P0 m0, P1 m1, P2 z2), the dealer's rt1 and rm1 (P2 only); writes
     P2's new shares into out0 / out1.  ``dealer=False``: the dealer's part already ran
-    (:func:`dot_tail_dealer`), rt / rm are None."""
-    msg = [torch.empty_like(x) for x in cross]
-    rt = [torch.empty_like(x) if r == 2 and dealer else None for x, r in zip(cross, roles)]
-    rm = [torch.empty((n,), dtype=torch.int64, device=x.device) if r == 2 and dealer else None
+    (:func:`dot_tail_dealer`), rt / rm are None.  ``alloc``: where the messages go."""
+    msg = [_new(alloc, x.shape, x.dtype, x.device) for x in cross]
+    rt = [_new(alloc, x.shape, x.dtype, x.device) if r == 2 and dealer else None
+          for x, r in zip(cross, roles)]
+    rm = [_new(alloc, (n,), torch.int64, x.device) if r == 2 and dealer else None
           for x, r in zip(cross, roles)]
     dev, st = _dev_stream(cross)
     nat.check(nat.lib().mx_dot_tail_r0(
@@ -2048,15 +2071,14 @@ def dot_tail_r0(cross, bits, m, roles, slots, nonces, out0, out1, n, dealer=True
     return msg, rt, rm
 
 
-def dot_tail_dealer(bits, m, roles, slots, nonces, out0, out1, n):
+def dot_tail_dealer(bits, m, roles, slots, nonces, out0, out1, n, alloc=None):
     """The dealer P2's part of round 0 on its own (mx_dot_tail_r0 without the products):
     it depends on PRF keys and nonces only, so it runs before the product exists and its
     messages rt1 / rm1 travel while the GEMM runs.  Returns (rt, rm) per component (P2's
     components only); writes P2's new shares into out0 / out1."""
     like = [o if r == 2 else None for o, r in zip(out0, roles)]
-    rt = [torch.empty_like(o) if o is not None else None for o in like]
-    rm = [torch.empty((n,), dtype=torch.int64, device=o.device) if o is not None else None
-          for o in like]
+    rt = [_new(alloc, o.shape, o.dtype, o.device) if o is not None else None for o in like]
+    rm = [_new(alloc, (n,), torch.int64, o.device) if o is not None else None for o in like]
     if not any(o is not None for o in like):
         return rt, rm
     only = [r if r == 2 else -1 for r in roles]
@@ -2069,10 +2091,12 @@ def dot_tail_dealer(bits, m, roles, slots, nonces, out0, out1, n):
     return rt, rm
 
 
-def dot_tail_r1(msg, rmk, rz, rrt, rrm, bits, m, roles, slots, nonces, out0, out1, n):
+def dot_tail_r1(msg, rmk, rz, rrt, rrm, bits, m, roles, slots, nonces, out0, out1, n,
+                alloc=None):
     """Round 1 (mx_dot_tail_r1): returns w per component (P0, P1); writes P0's s0 and
     P1's s1 into out0 / out1."""
-    w = [torch.empty_like(x) if r in (0, 1) else None for x, r in zip(msg, roles)]
+    w = [_new(alloc, x.shape, x.dtype, x.device) if r in (0, 1) else None
+         for x, r in zip(msg, roles)]
     dev, st = _dev_stream(msg)
     nat.check(nat.lib().mx_dot_tail_r1(
         dev, _words(bits), n, m, len(roles), _roles_arr(roles), _vp(msg), _vp(rmk), _vp(rz),
@@ -2189,14 +2213,15 @@ def _p(t):
     return None if t is None else t.data_ptr()
 
 
-def bits_front(role, xa, xb, arecv, bits, slots, n1, ng):
+def bits_front(role, xa, xb, arecv, bits, slots, n1, ng, alloc=None):
     """This party's adder inputs of the bit decomposition of (xa, xb) (its two arithmetic
     components, torch data): (message a1 (P0) or None, z (its zero-shared AND term, the
-    reshare message), p0, p1)."""
+    reshare message), p0, p1.  ``alloc``: where the messages go)."""
     like = next(t for t in (xa, xb, arecv) if t is not None)
     n = like.numel() // (2 if bits == 128 else 1)
-    z, p0, p1 = (torch.empty_like(like) for _ in range(3))
-    msg = torch.empty_like(like) if role == 0 else None
+    p0, p1 = torch.empty_like(like), torch.empty_like(like)
+    msg = _new(alloc, like.shape, like.dtype, like.device) if role == 0 else None
+    z = _new(alloc, like.shape, like.dtype, like.device)
     nat.check(nat.lib().mx_bits_front(
         nat.dev_of(like), _words(bits), role, n, _p(xa), _p(xb), _p(arecv), _p(msg), _p(z),
         _p(p0), _p(p1), _slots_arr(slots), _nonces_arr((n1, ng)), nat.stream_of(like)),
@@ -2205,7 +2230,7 @@ def bits_front(role, xa, xb, arecv, bits, slots, n1, ng):
 
 
 def bits_b2a(phase, role, src, start, count, bits, slots, n1, ng, arecv=None, state=None,
-             xbit=-1, blocks=1):
+             xbit=-1, blocks=1, alloc=None):
     """B2A of bit planes start.. of a boolean sharing (src = (s0, s1, g0, g1, t0, t1) torch
     data of one party; g = None: s are the sum words), phases 0 / 1 / 2 (bits_party.h).
     ``xbit`` >= 0: rows 0..count-2 are planes start.. XORed with plane xbit, the last row is
@@ -2230,8 +2255,9 @@ def bits_b2a(phase, role, src, start, count, bits, slots, n1, ng, arecv=None, st
         per = (per[0] // nb,) + per[1:]
     S = math.prod(per)
     shp = (count,) + per + ((2,) if bits == 128 else ())
-    z, b0, b1 = (torch.empty(shp, dtype=torch.int64, device=like.device) for _ in range(3))
-    msg = torch.empty_like(z) if role == 0 else None
+    b0, b1 = (torch.empty(shp, dtype=torch.int64, device=like.device) for _ in range(2))
+    msg = _new(alloc, shp, torch.int64, like.device) if role == 0 else None
+    z = _new(alloc, shp, torch.int64, like.device)
     srcs = (ctypes.c_void_p * 6)(*[_p(t) for t in src])
     nat.check(nat.lib().mx_bits_b2a(
         nat.dev_of(like), _words(bits), phase, role, S, start, count, xbit, blocks, srcs,

@@ -66,7 +66,8 @@ def dealer_early(sess, plc, roles, like, bits, m, nonces, out0, out1, slots):
     instead of 2.5.  ``like`` = (shape, dtype) of one component's product."""
     comp = {r: c for c, r in enumerate(roles)}
     n_el = math.prod(like[0]) // (2 if bits == 128 else 1)
-    rt, rm = R.dot_tail_dealer(bits, m, roles, slots, nonces, out0, out1, n_el)
+    rt, rm = R.dot_tail_dealer(bits, m, roles, slots, nonces, out0, out1, n_el,
+                               alloc=getattr(sess, "outbox", None))
     c2 = comp.get(2)
     got = sess.party_exchange(plc, [
         ("rt1", 2, 1, None if c2 is None else rt[c2], like),
@@ -194,8 +195,9 @@ def dot_trunc_tail(sess, plc, roles, cross, bits, m, nonces, out0, out1, slots, 
     :class:`RoundB` instead of running it."""
     comp = {r: c for c, r in enumerate(roles)}
     n_el = math.prod(cross[0].shape) // (2 if bits == 128 else 1)
+    box = getattr(sess, "outbox", None)  # where a thread receiver reads the messages
     msg, rt, rm = R.dot_tail_r0(cross, bits, m, roles, slots, nonces, out0, out1, n_el,
-                                dealer=pre is None)
+                                dealer=pre is None, alloc=box)
 
     def mine(party, arrs):
         c = comp.get(party)
@@ -215,7 +217,8 @@ def dot_trunc_tail(sess, plc, roles, cross, bits, m, nonces, out0, out1, slots, 
         rrm = [got.get("rm1") if r == 1 else None for r in roles]
     else:
         rrt, rrm = pre.rrt, pre.rrm
-    w = R.dot_tail_r1(msg, rmk, rz, rrt, rrm, bits, m, roles, slots, nonces, out0, out1, n_el)
+    w = R.dot_tail_r1(msg, rmk, rz, rrt, rrm, bits, m, roles, slots, nonces, out0, out1, n_el,
+                      alloc=box)
     nb = cross[0].numel() * cross[0].element_size()
     record_tail_traffic(sess.stats, plc, nb, round_b=False)
     rb = RoundB(sess, plc, roles, w, out0, out1, bits, n_el, like)

@@ -3,7 +3,7 @@
 # with and without it
 cd "$(dirname "$0")/../.."
 export PYTHONPATH=$PWD TMPDIR=/tmp
-out=gpurun_out/r6z
+out=gpurun_out/${OUT:-r6z}
 mkdir -p $out
 timeout -k 10 600 python -u -m pytest -v --timeout 120 --timeout-method thread -m gpu \
   tests/test_threads.py tests/test_storage_replay.py tests/test_merge_rounds.py \
