@@ -324,7 +324,9 @@ def expand(a: RT, shape) -> RT:
     return RT(a.data.expand(shape), a.bits)
 
 
-def binary(op: str, a, b) -> RT:
+def binary(op: str, a, b, alloc=None) -> RT:
+    """a op b elementwise; ``alloc(shape, dtype)``: where the result goes (a session's
+    outbox when it is a message; Z_2^64 / Z_2^128 only)."""
     if not isinstance(a, RT):
         a = _as_rt(a, b)
     b = _as_rt(b, a)
@@ -347,7 +349,7 @@ def binary(op: str, a, b) -> RT:
         na = nb_ = a.numel()
     n = max(na, nb_)
     out_shape = a.shape if na >= nb_ else b.shape
-    out = empty(out_shape, bits, a.device)
+    out = _empty_in(alloc, out_shape, bits, a.device)
     ad, bd = a.data.contiguous(), b.data.contiguous()
     nat.check(
         nat.lib().mx_ew_binary(

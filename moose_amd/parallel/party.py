@@ -153,7 +153,8 @@ class RoundB:
             # P1 adds its x2 (out1), P0 its x0 (out0)
             own = self.out1[c_src] if src == 1 else self.out0[c_src]
             mine = R.binary("add", R.RT(self.w[c_src], bits),
-                            R.RT(own.reshape(self.w[c_src].shape), bits)).data
+                            R.RT(own.reshape(self.w[c_src].shape), bits),
+                            alloc=getattr(sess, "outbox", None)).data
         got = sess.party_exchange(self.plc, [("wx", src, j, mine, like)])
         nb = math.prod(like[0]) * 8
         sess.stats.record_send(self.plc.owners[src], self.plc.owners[j], nb)
@@ -389,7 +390,8 @@ class MulAddTail:
         like = (tuple(self.z.data.shape), self.z.data.dtype) if idx is not None else None
         mine = None
         if idx is not None and idx != j:
-            mine = R.binary("add", self.z, self.c1).data  # z + this party's second component
+            # z + this party's second component (a message: into the session's outbox)
+            mine = R.binary("add", self.z, self.c1, alloc=getattr(sess, "outbox", None)).data
         got = sess.party_exchange(plc, [("m1", (j + 1) % 3, j, mine if idx == (j + 1) % 3 else None,
                                          like),
                                         ("m2", (j + 2) % 3, j, mine if idx == (j + 2) % 3 else None,

@@ -113,6 +113,40 @@ def test_receive_from_a_finished_party_raises_at_once():
     assert hub.failed is not None
 
 
+def test_mailbox_routes_a_message_in_place_on_the_second_capture():
+    """threads.Mailbox: the first capture learns that party 0's first outbox buffer became
+    its first message to party 1; the second capture hands party 0 a persistent buffer for
+    it and lands party 1's receive in that same buffer (no copy).  An outbox buffer that is
+    never sent is not routed (the transport declines it the second time)."""
+    from moose_amd.parallel.transport import CommStep
+
+    mb = T.Mailbox()
+
+    def capture():
+        steps = {0: [], 1: []}
+        trs = [T.ThreadTransport(i, None, device="cpu", world=2) for i in range(2)]
+        for i, tr in enumerate(trs):
+            tr.mailbox = mb
+            tr.tape = steps[i].append
+            tr.log = {1 - i: [("t", (2, 2), torch.int64, None)]}
+        msg = trs[0].outbox((2, 2), torch.int64)
+        kept = trs[0].outbox((3,), torch.int64)  # this party's own: never sent
+        trs[0].exchange([(msg, 1)], [])
+        got = torch.empty((2, 2), dtype=torch.int64)
+        trs[1].exchange([], [(got, 0)])
+        return msg, kept, got, steps
+
+    msg, kept, got, steps = capture()
+    assert mb.route == {(0, 1, 0): 0}
+    assert got.data_ptr() != msg.data_ptr()  # pass 1: the receive is a copy target
+    mb.prepare("cpu")
+    msg, kept, got, steps = capture()
+    assert got.data_ptr() == msg.data_ptr() == mb.slots[(0, 0)].data_ptr()
+    assert kept is None and (0, 1) not in mb.slots  # the session allocates it as usual
+    (step,), = [steps[1]]
+    assert isinstance(step, CommStep) and step.recvs[0][0].data_ptr() == msg.data_ptr()
+
+
 def test_device_map_rejects_unknown_identity():
     with pytest.raises(ValueError):
         LocalMooseRuntime(IDS, device_map={"mallory": "cpu"})
