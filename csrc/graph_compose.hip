@@ -495,6 +495,16 @@ static int graph_compose_impl(int n, const int* kind, void* const* child, void* 
 // Each maximal run of segments between two copy nodes is a phase: the parties' launches in
 // it are independent, so the same launch of 2-3 parties becomes one node.
 // stats[0..3] = nodes, launches merged away, batched nodes, phases.
+// MOOSEX_PARTY_TAIL_DEFER=0: a party moves to the next phase only when none of its
+// launches merged here (the round-6 rule)
+static bool tail_defer_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("MOOSEX_PARTY_TAIL_DEFER");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int mx_graph_compose_merged(int n, const int* kind, void* const* child, void* const* dst,
                             void* const* src, const int64_t* bytes, const int* party,
                             int64_t* stats, void** graph_out, void** exec_out) {
@@ -587,14 +597,20 @@ int mx_graph_compose_merged(int n, const int* kind, void* const* child, void* co
       // a party with nothing to receive) waits for the next phase, where the others reach
       // the same launches -- when the copies in between neither read its messages nor
       // write its buffers, so its order against every copy it depends on is kept.
+      // Only the unmatched TAIL moves (the launches after the party's last merged one):
+      // the party's order is kept, and what merged here stays here.
       bool moved = false;
       for (int p = 0; p < 3; ++p) {
         if (L[p].empty() || ((touched >> p) & 1)) continue;
-        bool single = true;
+        int last = -1;  // the party's last launch in a merged group
         for (const Group& gr : groups)
           for (int z = 0; z < gr.k; ++z)
-            if (gr.party[z] == p && gr.k > 1) single = false;
-        if (single) {
+            if (gr.party[z] == p && gr.k > 1 && gr.idx[z] > last) last = gr.idx[z];
+        if (last + 1 < (int)L[p].size() && tail_defer_on()) {
+          carry[p].assign(L[p].begin() + last + 1, L[p].end());
+          L[p].resize(last + 1);
+          moved = true;
+        } else if (last < 0) {
           carry[p].swap(L[p]);
           moved = true;
         }

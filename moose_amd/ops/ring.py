@@ -2015,14 +2015,21 @@ def trunc_party_r1(msg, rmk, rrt, rrm, out0, out1, bits, m, roles, slots, nonces
 SHARE_MIRROR = 8  # MX_SHARE_MIRROR (moosex.h): the masked slot goes to P_{j+2}
 
 
-def share_party(kind: str, x: RT, ncomp: int, rel, slots, n1: int, na: int, mirror=False):
+def share_party(kind: str, x: RT, ncomp: int, rel, slots, n1: int, na: int, mirror=False,
+                alloc=None, msg_slot=None):
     """Per-component slots of a sharing by member j (mx_share_party); the owner's out1
     (slot x_{j+1}) is the message to P_{j+1} (whose out0 it becomes).  A pending
-    :class:`Encoded` input is encoded inside the kernel."""
+    :class:`Encoded` input is encoded inside the kernel.  ``alloc``: two separate buffers
+    (a receiver lands its slot whole), slot ``msg_slot`` (the owner's message) from
+    ``alloc(shape, dtype)``."""
     code, xd, aux = share_source(x, kind)
     na = na if aux is None else aux
-    out0, out1 = empty2((ncomp,) + tuple(x.shape), x.bits, xd.device)
-    out0, out1 = out0.data, out1.data
+    if alloc is None:
+        out0, out1 = empty2((ncomp,) + tuple(x.shape), x.bits, xd.device)
+        out0, out1 = out0.data, out1.data
+    else:
+        out0, out1 = (_empty_in(alloc if s == msg_slot else None, (ncomp,) + tuple(x.shape),
+                                x.bits, xd.device).data for s in (0, 1))
     nat.check(nat.lib().mx_share_party(
         nat.dev_of(xd), code | (SHARE_MIRROR if mirror else 0), _words(x.bits), x.numel(), ncomp,
         _roles_arr(rel), nat.ptr(xd), nat.ptr(out0), nat.ptr(out1), _slots_arr(slots),
