@@ -61,6 +61,9 @@ int mx_mul_add2(int dev, int words, const void* a0, const void* a1, const void* 
                 void* stream);
 int mx_ew_unary2(int dev, int op, int words, const void* a0, void* out0, const void* a1,
                  void* out1, int64_t n, int64_t param, void* stream);
+// out_y = a_y^T, y = 0, 1 ([rows, cols] ring matrices -> [cols, rows])
+int mx_transpose2(int dev, int words, const void* a0, void* out0, const void* a1, void* out1,
+                  int64_t rows, int64_t cols, void* stream);
 // mx_ew_binary_slot on a0 (slot which0) and a1 (slot which1) with one public b
 int mx_ew_binary_slot2(int dev, int op, int words, const void* a0, const void* a1,
                        const void* b, int64_t nb, void* out0, void* out1, int64_t m,

@@ -220,6 +220,8 @@ int mxh_mul_trunc3_kv(int words, const void* x0, const void* x1, const void* y0,
                       void* stream);
 int mxh_ew_unary2(int op, int words, const void* a0, void* out0, const void* a1, void* out1,
                   int64_t n, int64_t param, void* stream);
+int mxh_transpose2(int words, const void* a0, void* out0, const void* a1, void* out1,
+                   int64_t rows, int64_t cols, void* stream);
 int mxh_ew_binary_slot2(int op, int words, const void* a0, const void* a1, const void* b,
                         int64_t nb, void* out0, void* out1, int64_t m, int nparties, int which0,
                         int which1, void* stream);

@@ -403,6 +403,20 @@ int mx_mul_add2(int dev, int words, const void* a0, const void* a1, const void* 
   });
 }
 
+int mx_transpose2(int dev, int words, const void* a0, void* out0, const void* a1, void* out1,
+                  int64_t rows, int64_t cols, void* stream) {
+  if (dev) return mxh_transpose2(words, a0, out0, a1, out1, rows, cols, stream);
+  DISPATCH_WORDS(words, T, {
+    for (int y = 0; y < 2; ++y) {
+      const T* a = (const T*)(y ? a1 : a0);
+      T* o = (T*)(y ? out1 : out0);
+      for (int64_t i = 0; i < rows; ++i)
+        for (int64_t j = 0; j < cols; ++j) o[j * rows + i] = a[i * cols + j];
+    }
+    return 0;
+  });
+}
+
 int mx_ew_unary2(int dev, int op, int words, const void* a0, void* out0, const void* a1,
                  void* out1, int64_t n, int64_t param, void* stream) {
   if (dev) return mxh_ew_unary2(op, words, a0, out0, a1, out1, n, param, stream);

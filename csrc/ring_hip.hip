@@ -122,6 +122,29 @@ __global__ void __launch_bounds__(256) k_unary2(int op, Pair<T> p, int64_t n, in
   d_unary2<T>(op, p, n, k);
 }
 
+// out_y = a_y^T for a party's two share components ([rows, cols] -> [cols, rows]): 32 x 32
+// tiles through LDS (rows read and written whole); tile = blockIdx.x, component = blockIdx.y
+// (blockIdx.z stays free for the party-batched twin)
+template <class T>
+__device__ __forceinline__ void d_transpose2(const Pair<T>& p, int64_t rows, int64_t cols) {
+  __shared__ T tile[32][33];
+  const T* __restrict__ a = p.a[blockIdx.y];
+  T* __restrict__ out = p.o[blockIdx.y];
+  const int64_t tiles_c = (cols + 31) / 32;
+  const int64_t r0 = (blockIdx.x / tiles_c) * 32, c0 = (blockIdx.x % tiles_c) * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 lanes: 8 rows per pass
+  for (int r = ty; r < 32; r += 8)
+    if (r0 + r < rows && c0 + tx < cols) tile[r][tx] = a[(r0 + r) * cols + c0 + tx];
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8)
+    if (c0 + r < cols && r0 + tx < rows) out[(c0 + r) * rows + r0 + tx] = tile[tx][r];
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) k_transpose2(Pair<T> p, int64_t rows, int64_t cols) {
+  d_transpose2<T>(p, rows, cols);
+}
+
 // public b applied to party slot which[y] of stacked a[y] ([np, m]), other slots copied
 template <class T>
 __device__ __forceinline__ void d_binary_slot2(int op, const Pair<T>& p, int64_t nb, int64_t m,
@@ -1714,6 +1737,8 @@ MX_X3(k_binary2<u64>, d_binary2<u64>);
 MX_X3(k_binary2<u128>, d_binary2<u128>);
 MX_X3(k_unary2<u64>, d_unary2<u64>);
 MX_X3(k_unary2<u128>, d_unary2<u128>);
+MX_X3(k_transpose2<u64>, d_transpose2<u64>);
+MX_X3(k_transpose2<u128>, d_transpose2<u128>);
 MX_X3(k_unary<u64>, d_unary<u64>);
 MX_X3(k_unary<u128>, d_unary<u128>);
 MX_X3(k_binary_slot<u64>, d_binary_slot<u64>);
@@ -1961,6 +1986,20 @@ int mxh_ew_unary2(int op, int words, const void* a0, void* out0, const void* a1,
     Pair<T> p{{(const T*)a0, (const T*)a1}, {nullptr, nullptr}, {(T*)out0, (T*)out1}, {0, 0}};
     hipLaunchKernelGGL(k_unary2<T>, dim3(grid_for(n), 2), dim3(kBlock), 0, S(stream), op, p, n,
                        (int)param);
+    MX_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mxh_transpose2(int words, const void* a0, void* out0, const void* a1, void* out1,
+                   int64_t rows, int64_t cols, void* stream) {
+  if (rows <= 0 || cols <= 0) return 0;
+  const int64_t tiles = ((rows + 31) / 32) * ((cols + 31) / 32);
+  if (tiles > 0x7fffffff) return -3;
+  DEV_DISPATCH(words, T, {
+    Pair<T> p{{(const T*)a0, (const T*)a1}, {nullptr, nullptr}, {(T*)out0, (T*)out1}, {0, 0}};
+    hipLaunchKernelGGL(k_transpose2<T>, dim3((unsigned)tiles, 2), dim3(256), 0, S(stream), p,
+                       rows, cols);
     MX_LAUNCH_CHECK();
     return 0;
   });

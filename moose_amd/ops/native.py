@@ -32,6 +32,7 @@ _SIGS = {
     "mx_ew_binary2": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
                               c_i64, c_i64, c_vp]),
     "mx_ew_unary2": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp]),
+    "mx_transpose2": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp]),
     "mx_ew_binary_slot2": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
                                    c_i64, c_int, c_int, c_int, c_vp]),
     "mx_mul_trunc3_kv": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,

@@ -381,6 +381,19 @@ def unary(op: str, a: RT, k: int = 0) -> RT:
     return out
 
 
+def transpose2(a0: RT, a1: RT):
+    """(a0^T, a1^T) of two [rows, cols] ring matrices (a party's share components) in one
+    launch (mx_transpose2: 32 x 32 tiles through LDS) instead of two strided copies."""
+    rows, cols = a0.shape
+    bits = a0.bits
+    d0, d1 = a0.data.contiguous(), a1.data.contiguous()
+    o0, o1 = empty2((cols, rows), bits, d0.device)
+    nat.check(nat.lib().mx_transpose2(
+        nat.dev_of(d0), _words(bits), nat.ptr(d0), nat.ptr(o0.data), nat.ptr(d1),
+        nat.ptr(o1.data), rows, cols, nat.stream_of(d0)), "transpose2")
+    return o0, o1
+
+
 def binary2(op: str, a0: RT, b0: RT, a1: RT, b1: RT):
     """(a0 op b0, a1 op b1) -- both share vectors of a share-wise replicated op -- in one
     launch (mx_ew_binary2).  Operands of each pair have the same shapes as the other pair's;

@@ -118,6 +118,18 @@ def test_skinny_gemm_matches_host(bits, shape):
 
 
 @pytest.mark.parametrize("bits", [64, 128])
+@pytest.mark.parametrize("shape", [(128, 100), (1, 37), (33, 1), (65, 97)])
+def test_transpose2_matches_host(bits, shape):
+    """k_transpose2 (32 x 32 LDS tiles, ragged edges) equals the host's transposes."""
+    a0, a1 = rand_rt(shape, bits, 60), rand_rt(shape, bits, 61)
+    h0, h1 = R.transpose2(a0, a1)
+    d0, d1 = R.transpose2(gpu(a0), gpu(a1))
+    same(h0, d0)
+    same(h1, d1)
+    same(h0, R.transpose(a0))
+
+
+@pytest.mark.parametrize("bits", [64, 128])
 def test_gemm_cross_matches_host(bits):
     M, K, N = 96, 160, 128
     xs = [rand_rt((3, M, K), bits, 20 + i) for i in range(2)]

@@ -41,6 +41,16 @@ def test_binary2_matches_binary(dev, bits, op):
 
 @pytest.mark.parametrize("dev", DEVICES)
 @pytest.mark.parametrize("bits", [64, 128])
+@pytest.mark.parametrize("shape", [(128, 100), (1, 37), (65, 97)])
+def test_transpose2_matches_transpose(dev, bits, shape):
+    a0, a1 = _rand(shape, bits, dev, 5), _rand(shape, bits, dev, 6)
+    o0, o1 = R.transpose2(a0, a1)
+    _eq(o0, R.transpose(a0))
+    _eq(o1, R.transpose(a1))
+
+
+@pytest.mark.parametrize("dev", DEVICES)
+@pytest.mark.parametrize("bits", [64, 128])
 def test_unary2_and_slot2(dev, bits):
     a0, a1 = _rand((3, 5, 7), bits, dev, 1), _rand((3, 5, 7), bits, dev, 2)
     for op, k in (("neg", 0), ("shl", 5)):
