@@ -223,10 +223,21 @@ struct Item {
   const mxb::Entry* x3 = nullptr;  // the twin, when this launch can be batched
 };
 
+// MOOSEX_PARTY_GS_MERGE=0: grid-stride twins merge only at equal grids
+static bool gs_merge_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("MOOSEX_PARTY_GS_MERGE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 bool same_launch(const Item& a, const Item& b) {
+  // a grid-stride twin (MX_X3_GS) merges launches of different grid.x
   return !a.opaque && !b.opaque && a.x3 != nullptr && a.func == b.func &&
-         a.grid.x == b.grid.x && a.grid.y == b.grid.y && a.block.x == b.block.x &&
-         a.block.y == b.block.y && a.block.z == b.block.z && a.shmem == b.shmem;
+         (a.grid.x == b.grid.x || (a.x3->any_grid && gs_merge_on())) &&
+         a.grid.y == b.grid.y && a.block.x == b.block.x && a.block.y == b.block.y &&
+         a.block.z == b.block.z && a.shmem == b.shmem;
 }
 
 // The launches of one captured segment in a topological order; false when the segment
@@ -652,7 +663,10 @@ int mx_graph_compose_merged(int n, const int* kind, void* const* child, void* co
         void* args[] = {blob};
         hipKernelNodeParams kp = {};
         kp.func = const_cast<void*>(e.x3);
-        kp.gridDim = dim3(it.grid.x, it.grid.y, (unsigned)gr.k);
+        unsigned gx = it.grid.x;  // the largest (a grid-stride twin's parties may differ)
+        for (int z = 1; z < gr.k; ++z)
+          gx = std::max(gx, L[gr.party[z]][gr.idx[z]].grid.x);
+        kp.gridDim = dim3(gx, it.grid.y, (unsigned)gr.k);
         kp.blockDim = it.block;
         kp.sharedMemBytes = it.shmem;
         kp.kernelParams = args;

@@ -76,6 +76,8 @@ struct Entry {
   size_t off[kMaxArgs];
   size_t size[kMaxArgs];
   size_t stride;      // one argument block
+  int any_grid;       // the body is a pure grid-stride loop over its own n: the parties'
+                      // launches merge at different grid.x (the twin runs the largest)
 };
 
 }  // namespace mxb
@@ -86,10 +88,11 @@ void mx_x3_add(const void* kernel, const mxb::Entry& e);
 namespace mxb {
 
 template <auto Body, class... A>
-int x3_register(void (*k)(A...)) {
+int x3_register(void (*k)(A...), int any_grid = 0) {
   using L = Layout<A...>;
   if constexpr (3 * L::kSize <= kMaxBlob && L::N <= kMaxArgs) {
     Entry e{};
+    e.any_grid = any_grid;
     e.x3 = (const void*)&k_x3<Body, A...>;
     e.nargs = L::N;
     for (int i = 0; i < L::N; ++i) {
@@ -110,3 +113,7 @@ int x3_register(void (*k)(A...)) {
 // register kernel instance ``k`` (e.g. k_foo<u128>) with its body ``body`` (d_foo<u128>)
 #define MX_X3(k, body) \
   static const int MX_X3_CAT(mx_x3_reg_, __LINE__) = mxb::x3_register<&body>(&k)
+// ... whose body covers its elements with grid-stride loops only (any grid.x is correct:
+// no per-block partition, no block-count-sized workspace)
+#define MX_X3_GS(k, body) \
+  static const int MX_X3_CAT(mx_x3_reg_, __LINE__) = mxb::x3_register<&body>(&k, 1)

@@ -1422,8 +1422,8 @@ __global__ void __launch_bounds__(256) k_ks_cross1_lat(const T* __restrict__ g0,
 }
 
 // party-batched twins for the composed one-GPU replay (party_batch.h)
-MX_X3(k_binary<u64>, d_binary<u64>);
-MX_X3(k_binary<u128>, d_binary<u128>);
+MX_X3_GS(k_binary<u64>, d_binary<u64>);
+MX_X3_GS(k_binary<u128>, d_binary<u128>);
 MX_X3(k_lincomb2<u64>, d_lincomb2<u64>);
 MX_X3(k_lincomb2<u128>, d_lincomb2<u128>);
 MX_X3(k_addn_decode<u64>, d_addn_decode<u64>);
@@ -1733,14 +1733,14 @@ __global__ void __launch_bounds__(256) k_prf_expand(T* __restrict__ out, int64_t
 }
 
 // party-batched twins of the per-party sessions' local kernels (party_batch.h)
-MX_X3(k_binary2<u64>, d_binary2<u64>);
-MX_X3(k_binary2<u128>, d_binary2<u128>);
-MX_X3(k_unary2<u64>, d_unary2<u64>);
-MX_X3(k_unary2<u128>, d_unary2<u128>);
+MX_X3_GS(k_binary2<u64>, d_binary2<u64>);
+MX_X3_GS(k_binary2<u128>, d_binary2<u128>);
+MX_X3_GS(k_unary2<u64>, d_unary2<u64>);
+MX_X3_GS(k_unary2<u128>, d_unary2<u128>);
 MX_X3(k_transpose2<u64>, d_transpose2<u64>);
 MX_X3(k_transpose2<u128>, d_transpose2<u128>);
-MX_X3(k_unary<u64>, d_unary<u64>);
-MX_X3(k_unary<u128>, d_unary<u128>);
+MX_X3_GS(k_unary<u64>, d_unary<u64>);
+MX_X3_GS(k_unary<u128>, d_unary<u128>);
 MX_X3(k_binary_slot<u64>, d_binary_slot<u64>);
 MX_X3(k_binary_slot<u128>, d_binary_slot<u128>);
 MX_X3(k_binary_slot2<u64>, d_binary_slot2<u64>);

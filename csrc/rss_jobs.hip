@@ -452,15 +452,15 @@ __global__ void __launch_bounds__(256)
 }
 
 // party-batched twins for the composed one-GPU replay (party_batch.h)
-MX_X3(k_jobs_r0<u128>, d_jobs_r0<u128>);
-MX_X3(k_jobs_r1<u64>, d_jobs_r1<u64>);
-MX_X3(k_jobs_r1<u128>, d_jobs_r1<u128>);
-MX_X3(k_jobs_r2<u64>, d_jobs_r2<u64>);
-MX_X3(k_jobs_r2<u128>, d_jobs_r2<u128>);
-MX_X3(k_jobs_r0_lat<u64>, d_jobs_r0_lat<u64>);
-MX_X3(k_jobs_r0_lat<u128>, d_jobs_r0_lat<u128>);
-MX_X3(k_jobs_r1_lat<u64>, d_jobs_r1_lat<u64>);
-MX_X3(k_jobs_r1_lat<u128>, d_jobs_r1_lat<u128>);
+MX_X3_GS(k_jobs_r0<u128>, d_jobs_r0<u128>);
+MX_X3_GS(k_jobs_r1<u64>, d_jobs_r1<u64>);
+MX_X3_GS(k_jobs_r1<u128>, d_jobs_r1<u128>);
+MX_X3_GS(k_jobs_r2<u64>, d_jobs_r2<u64>);
+MX_X3_GS(k_jobs_r2<u128>, d_jobs_r2<u128>);
+MX_X3_GS(k_jobs_r0_lat<u64>, d_jobs_r0_lat<u64>);
+MX_X3_GS(k_jobs_r0_lat<u128>, d_jobs_r0_lat<u128>);
+MX_X3_GS(k_jobs_r1_lat<u64>, d_jobs_r1_lat<u64>);
+MX_X3_GS(k_jobs_r1_lat<u128>, d_jobs_r1_lat<u128>);
 
 // the latency forms run while the launch has at most this many chunk positions
 constexpr int64_t kLatMaxChunks = 1 << 14;
