@@ -281,20 +281,23 @@ __device__ __forceinline__ void residue2(const uint32_t (&xa)[NW], const uint32_
 }
 
 // One thread = (tile, k-step, image row r, 16-byte chunk c) of every residue plane.
-// TRANS = false: A' rows are M rows of [A0 | A1] (row-major [R][K] per batch, batch stride
-// xs elements).  TRANS = true: B' rows are the N columns of [B0 + B1 ; B0] ([K][R]).
+// TRANS = false: A' rows are M rows of A0 (mode 0), [A0 | A1] (mode 1) or A0 + A1 (mode 2)
+// (row-major [R][K] per batch, batch stride xs elements).  TRANS = true: B' rows are the N
+// columns ([K][R]) of B0 (mode 0), [B0 + B1 ; B0] (1), [B0 ; B1] (2) or B0 + B1 (3).
+// nkb k-steps are generated; the image is laid out with nkb_s k-steps per tile (>= nkb: a
+// shorter operand placed in a longer operand's slot).
 template <class T, bool TRANS, int ROWS, bool PK = true>
 __global__ void __launch_bounds__(256)
     k_crt_prep(const T* __restrict__ X0, const T* __restrict__ X1, int64_t R, int64_t K,
                int64_t xs, int mode, int8_t* __restrict__ out, int64_t tiles, int64_t nkb,
-               const PrepTab tab) {
+               int64_t nkb_s, const PrepTab tab) {
   constexpr int NW = Words<T>::N;
   const int64_t total = tiles * nkb * (ROWS * 4);
   const int64_t b = blockIdx.y;
   const T* x0 = X0 + b * xs;
   const T* x1 = mode ? X1 + b * xs : x0;
   const int n = tab.n;
-  const int64_t plane = tiles * nkb * (int64_t)(ROWS * BK);
+  const int64_t plane = tiles * nkb_s * (int64_t)(ROWS * BK);
   int8_t* ob = out + b * n * plane;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total;
        g += (int64_t)gridDim.x * blockDim.x) {
@@ -311,17 +314,19 @@ __global__ void __launch_bounds__(256)
       T e = 0;
       if (row < R) {
         if (!TRANS) {
-          if (k < K) e = x0[row * K + k];
-          else if (mode && k < 2 * K) e = x1[row * K + (k - K)];
+          if (k < K) e = mode == 2 ? (T)(x0[row * K + k] + x1[row * K + k]) : x0[row * K + k];
+          else if (mode == 1 && k < 2 * K) e = x1[row * K + (k - K)];
         } else {
-          if (k < K) e = mode ? (T)(x0[k * R + row] + x1[k * R + row]) : x0[k * R + row];
-          else if (mode && k < 2 * K) e = x0[(k - K) * R + row];
+          if (k < K)
+            e = (mode & 1) ? (T)(x0[k * R + row] + x1[k * R + row]) : x0[k * R + row];
+          else if (mode == 1 && k < 2 * K) e = x0[(k - K) * R + row];
+          else if (mode == 2 && k < 2 * K) e = x1[(k - K) * R + row];
         }
       }
 #pragma unroll
       for (int w = 0; w < NW; ++w) v[j][w] = (uint32_t)(e >> (32 * w));
     }
-    int8_t* base = ob + (t * nkb + kb) * (int64_t)(ROWS * BK) + img_off(r, c);
+    int8_t* base = ob + (t * nkb_s + kb) * (int64_t)(ROWS * BK) + img_off(r, c);
     {  // p = 256: the low byte (times the folded inverse)
       int rr[16];
 #pragma unroll
@@ -599,8 +604,8 @@ __global__ void __launch_bounds__(256)
 template <int WR, int WC, int BN, int MINW, int STG = kStages, int IL = 0>
 __global__ void __launch_bounds__(64 * WR * WC, MINW)
     k_crt_gemm16(const int8_t* __restrict__ RA, const int8_t* __restrict__ RB,
-                 int8_t* __restrict__ CR, int tiles_m, int tiles_n, int nkb, int gM,
-                 const EpiTab ep, int dma_mask, int bcast, int a_nkb, int roll) {
+                 int8_t* __restrict__ CR, int tiles_m, int tiles_n, int nkb_all, int gM,
+                 const EpiTab ep, int dma_mask, int bcast, int a_nkb, int roll, int amap) {
   constexpr int NW = WR * WC;
   constexpr int MI = BM / WR / 16, NJ = BN / WC / 16;
   constexpr int NM = MI * NJ;                    // MFMAs per wave per k-step
@@ -617,10 +622,13 @@ __global__ void __launch_bounds__(64 * WR * WC, MINW)
   const int gm = tiles_m - first_m < gM ? tiles_m - first_m : gM;
   const int in_group = tid_flat % (gM * tiles_n);
   const int tm = first_m + in_group % gm, tn = in_group / gm;
-  const int g = blockIdx.y;
+  // amap < 0 (bit 31): the asymmetric three-party product (run_crt_asym) -- the parties with
+  // the full K' (1 and 2) are dispatched first, party 0's half-length blocks fill the tail
+  const int g = amap < 0 ? (int)((blockIdx.y + ep.n) % gridDim.y) : (int)blockIdx.y;
   const int mi = g % ep.n;
+  int nkb = nkb_all;
   const int8_t* ga = RA + ((int64_t)((bcast & 1) ? mi : g) * tiles_m + tm) * a_nkb * (int64_t)kImg;
-  const int8_t* gb = RB + ((int64_t)((bcast & 2) ? mi : g) * tiles_n + tn) * nkb * (int64_t)kImgB;
+  const int8_t* gb = RB + ((int64_t)((bcast & 2) ? mi : g) * tiles_n + tn) * nkb_all * (int64_t)kImgB;
   // roll != 0: A' = [x_b | x_{b+roll}] (an RSS pair whose second share is the next party's
   // first) -- the image holds each batch entry's K residues once; k-blocks from a_nkb on
   // read entry b + roll's image (ga2 is biased so that ga2 + kb * kImg addresses it)
@@ -632,6 +640,16 @@ __global__ void __launch_bounds__(64 * WR * WC, MINW)
     ga2 = RA + ((int64_t)(b2 * ep.n + mi) * tiles_m + tm) * a_nkb * (int64_t)kImg -
           (int64_t)a_nkb * kImg;
     khalf = a_nkb;
+  } else if (amap < 0) {
+    // party b reads A' = [entry e1 | entry e2] of the K-residue image, or only e1's K
+    // (k-steps [0, a_nkb): party 0's one-GEMM product) when its half bit is set
+    const int sh = 8 * (g / ep.n);
+    const int e1 = (amap >> sh) & 7, e2 = (amap >> (sh + 3)) & 7;
+    ga = RA + ((int64_t)(e1 * ep.n + mi) * tiles_m + tm) * a_nkb * (int64_t)kImg;
+    ga2 = RA + ((int64_t)(e2 * ep.n + mi) * tiles_m + tm) * a_nkb * (int64_t)kImg -
+          (int64_t)a_nkb * kImg;
+    khalf = a_nkb;
+    if ((amap >> (sh + 6)) & 1) nkb = a_nkb;
   }
 
   const int lane = threadIdx.x & 63;
@@ -1083,8 +1101,9 @@ bool prep_packed() {
 template <class T>
 void launch_prep(const CPlan& p, const Tables& tb, bool is_b, int64_t batch, int64_t R,
                  int64_t K, int64_t xs, const T* X0, const T* X1, int mode, int8_t* out,
-                 hipStream_t st, int64_t nkb = -1) {
+                 hipStream_t st, int64_t nkb = -1, int64_t nkb_s = -1) {
   if (nkb < 0) nkb = p.nkb;
+  if (nkb_s < nkb) nkb_s = nkb;
   const int64_t tiles = is_b ? p.tiles_n : p.tiles_m;
   const int rows = is_b ? p.bn : BM;
   const int64_t work = tiles * nkb * (rows * 4);
@@ -1094,24 +1113,24 @@ void launch_prep(const CPlan& p, const Tables& tb, bool is_b, int64_t batch, int
   if (!prep_packed() || is_b) {  // MOOSEX_CRT_PACKED=0: one residue at a time everywhere
     if (!is_b)
       hipLaunchKernelGGL((k_crt_prep<T, false, BM, false>), grid, dim3(256), 0, st, X0, X1, R, K,
-                         xs, mode, out, tiles, nkb, tb.pa);
+                         xs, mode, out, tiles, nkb, nkb_s, tb.pa);
     else if (rows == 256)
       hipLaunchKernelGGL((k_crt_prep<T, true, 256, false>), grid, dim3(256), 0, st, X0, X1, R, K,
-                         xs, mode, out, tiles, nkb, tb.pb);
+                         xs, mode, out, tiles, nkb, nkb_s, tb.pb);
     else
       hipLaunchKernelGGL((k_crt_prep<T, true, 128, false>), grid, dim3(256), 0, st, X0, X1, R, K,
-                         xs, mode, out, tiles, nkb, tb.pb);
+                         xs, mode, out, tiles, nkb, nkb_s, tb.pb);
     return;
   }
   if (!is_b)
     hipLaunchKernelGGL((k_crt_prep<T, false, BM>), grid, dim3(256), 0, st, X0, X1, R, K, xs, mode,
-                       out, tiles, nkb, tb.pa);
+                       out, tiles, nkb, nkb_s, tb.pa);
   else if (rows == 256)
     hipLaunchKernelGGL((k_crt_prep<T, true, 256>), grid, dim3(256), 0, st, X0, X1, R, K, xs, mode,
-                       out, tiles, nkb, tb.pb);
+                       out, tiles, nkb, nkb_s, tb.pb);
   else
     hipLaunchKernelGGL((k_crt_prep<T, true, 128>), grid, dim3(256), 0, st, X0, X1, R, K, xs, mode,
-                       out, tiles, nkb, tb.pb);
+                       out, tiles, nkb, nkb_s, tb.pb);
 }
 
 // MOOSEX_CRT_DMA_MASK (timing experiments, wrong results): bit 0 = stream A, bit 1 = B,
@@ -1123,7 +1142,8 @@ int dma_mask() {
 
 template <int WR, int WC, int BN, int MINW, bool M16, int STG = kStages, int IL = 0>
 void launch_variant(const CPlan& p, const Tables& tb, int64_t batch, const int8_t* ra,
-                    const int8_t* rb, int8_t* cr, int bcast, int roll, hipStream_t st) {
+                    const int8_t* rb, int8_t* cr, int bcast, int roll, hipStream_t st,
+                    int amap = 0) {
   constexpr int lds = STG * (kImg + BN * BK);
   const void* fn = M16 ? (const void*)k_crt_gemm16<WR, WC, BN, MINW, STG, IL>
                        : (const void*)k_crt_gemm<WR, WC, BN, MINW>;
@@ -1132,7 +1152,7 @@ void launch_variant(const CPlan& p, const Tables& tb, int64_t batch, const int8_
   if constexpr (M16)
     hipLaunchKernelGGL((k_crt_gemm16<WR, WC, BN, MINW, STG, IL>), grid, dim3(64 * WR * WC), lds, st, ra,
                        rb, cr, (int)p.tiles_m, (int)p.tiles_n, (int)p.nkb, gemm_group_m(), tb.ep,
-                       dma_mask(), bcast, (int)p.a_nkb, roll);
+                       dma_mask(), bcast, (int)p.a_nkb, roll, amap);
   else
     hipLaunchKernelGGL((k_crt_gemm<WR, WC, BN, MINW>), grid, dim3(64 * WR * WC), lds, st, ra, rb,
                        cr, (int)p.tiles_m, (int)p.tiles_n, (int)p.nkb, gemm_group_m(), tb.ep,
@@ -1140,24 +1160,25 @@ void launch_variant(const CPlan& p, const Tables& tb, int64_t batch, const int8_
 }
 
 void launch_crt_gemm(const CPlan& p, const Tables& tb, int64_t batch, const int8_t* ra,
-                     const int8_t* rb, int8_t* cr, int bcast, int roll, hipStream_t st) {
-  switch (crt_kernel()) {  // roll: 16x16x64 kernels only (run_crt checks)
+                     const int8_t* rb, int8_t* cr, int bcast, int roll, hipStream_t st,
+                     int amap = 0) {
+  switch (crt_kernel()) {  // roll, amap: 16x16x64 kernels only (run_crt* check)
     case 1: launch_variant<2, 2, 256, 1, false>(p, tb, batch, ra, rb, cr, bcast, 0, st); break;
     case 2: launch_variant<2, 4, 256, 2, false>(p, tb, batch, ra, rb, cr, bcast, 0, st); break;
-    case 4: launch_variant<2, 2, 256, 1, true>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
+    case 4: launch_variant<2, 2, 256, 1, true>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
     case 3: launch_variant<2, 2, 128, 2, false>(p, tb, batch, ra, rb, cr, bcast, 0, st); break;
-    case 6: launch_variant<2, 4, 256, 2, true>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
-    case 7: launch_variant<2, 4, 256, 2, true, 4>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
-    case 8: launch_variant<2, 4, 256, 2, true, 3, 1>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
-    case 9: launch_variant<2, 4, 256, 2, true, 4, 1>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
-    case 10: launch_variant<2, 4, 256, 2, true, 3, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
-    case 11: launch_variant<2, 4, 256, 2, true, 4, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
-    case 12: launch_variant<2, 2, 256, 1, true, 3, 1>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
-    case 13: launch_variant<2, 2, 256, 1, true, 4, 1>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
-    case 14: launch_variant<2, 2, 256, 1, true, 3, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
-    case 15: launch_variant<2, 2, 256, 1, true, 4, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
-    case 16: launch_variant<2, 4, 256, 2, true, 5, 3>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
-    default: launch_variant<2, 2, 128, 2, true>(p, tb, batch, ra, rb, cr, bcast, roll, st); break;
+    case 6: launch_variant<2, 4, 256, 2, true>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
+    case 7: launch_variant<2, 4, 256, 2, true, 4>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
+    case 8: launch_variant<2, 4, 256, 2, true, 3, 1>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
+    case 9: launch_variant<2, 4, 256, 2, true, 4, 1>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
+    case 10: launch_variant<2, 4, 256, 2, true, 3, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
+    case 11: launch_variant<2, 4, 256, 2, true, 4, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
+    case 12: launch_variant<2, 2, 256, 1, true, 3, 1>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
+    case 13: launch_variant<2, 2, 256, 1, true, 4, 1>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
+    case 14: launch_variant<2, 2, 256, 1, true, 3, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
+    case 15: launch_variant<2, 2, 256, 1, true, 4, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
+    case 16: launch_variant<2, 4, 256, 2, true, 5, 3>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
+    default: launch_variant<2, 2, 128, 2, true>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
   }
 }
 
@@ -1277,9 +1298,85 @@ int run_crt(int64_t batch, int64_t M, int64_t N, int64_t K, const T* A0, const T
   return e != hipSuccess ? -100 - (int)e : 0;
 }
 
+// The three parties' local products of a replicated matrix product in the asymmetric
+// form: with party p holding (a, b) = (x_p, x_{p+1}) and (c, d) = (y_p, y_{p+1}),
+//   z_0 = (a + b)(c + d),   z_1 = b (c + d) + a d,   z_2 = a d + b c,
+// which sum to x.y (all nine x_i y_j exactly once) with five K-long GEMMs instead of the
+// symmetric form's six (z_p = a (c + d) + b c for every p).  S0/S1, T0/T1: [3][M][K] and
+// [3][K][N] share stacks; rolled: S1[p] = S0[p + 1] and T1[p] = T0[p + 1] (a stacked
+// session's pair; S1/T1 may be null) -- party 1's b and party 2's a are then the same
+// share x_2, whose residues are prepared once (four K-long A' images instead of five).
+template <class T>
+int run_crt_asym(int64_t M, int64_t N, int64_t K, const T* S0, const T* S1, const T* T0,
+                 const T* T1, int rolled, T* C, hipStream_t st) {
+  constexpr int words = sizeof(T) / 8;
+  if (K % BK || !crt_mfma16()) return -7;
+  if (2 * K > (1 << 15)) return -6;  // exact epilogue rounding bound
+  const CPlan p = make_cplan(words, 3, M, N, K, 1, true);  // nkb = 2K/64, a_nkb = K/64
+  if (p.n < 0) return -6;
+  const Tables& tb = tables_for(words, p.n);
+  const int64_t sa = M * K, sb = K * N;
+  const T* a[3];
+  const T* b[3];
+  const T* c[3];
+  const T* d[3];
+  for (int q = 0; q < 3; ++q) {
+    a[q] = S0 + q * sa;
+    b[q] = rolled ? S0 + ((q + 1) % 3) * sa : S1 + q * sa;
+    c[q] = T0 + q * sb;
+    d[q] = rolled ? T0 + ((q + 1) % 3) * sb : T1 + q * sb;
+  }
+  // A' images (K residues each): E0 = a_0 + b_0; party 1 reads [b_1 | a_1], party 2 [a_2 | b_2]
+  const T* ent[5] = {nullptr, b[1], a[1], a[2], b[2]};
+  int ne = 5, e21 = 3, e22 = 4;
+  if (rolled) {  // a_2 = b_1 = x_2
+    ne = 4;
+    ent[3] = b[2];  // x_0
+    e21 = 1;
+    e22 = 3;
+  }
+  const int64_t a_entry = p.n * p.tiles_m * p.a_nkb * (int64_t)kImg;
+  const int64_t ra_bytes = ne * a_entry;
+  const int64_t b_entry = p.rb_bytes / 3;
+  int8_t* ws = (int8_t*)workspace(ra_bytes + p.rb_bytes + p.cr_bytes, st);
+  if (!ws) return -4;
+  int8_t* ra = ws;
+  int8_t* cr = ra + ra_bytes;
+  int8_t* rb = cr + p.cr_bytes;
+  // B': party 0 (c + d) over K (in a 2K slot), party 1 [d + c ; d], party 2 [d ; c]
+  launch_prep<T>(p, tb, true, 1, N, K, 0, c[0], d[0], 3, rb, st, p.a_nkb, p.nkb);
+  launch_prep<T>(p, tb, true, 1, N, K, 0, d[1], c[1], 1, rb + b_entry, st);
+  launch_prep<T>(p, tb, true, 1, N, K, 0, d[2], c[2], 2, rb + 2 * b_entry, st);
+  launch_prep<T>(p, tb, false, 1, M, K, 0, a[0], b[0], 2, ra, st, p.a_nkb);
+  for (int e = 1; e < ne; ++e)
+    launch_prep<T>(p, tb, false, 1, M, K, 0, ent[e], ent[e], 0, ra + e * a_entry, st, p.a_nkb);
+  const int amap = (int)(0x80000000u | (1u << 6) | ((1u | (2u << 3)) << 8) |
+                         ((unsigned)(e21 | (e22 << 3)) << 16));
+  launch_crt_gemm(p, tb, 3, ra, rb, cr, 0, 0, st, amap);
+  launch_recon<T>(p, tb, 3, M, N, cr, C, 0, st);
+  const hipError_t e = hipGetLastError();
+  return e != hipSuccess ? -100 - (int)e : 0;
+}
+
 }  // namespace
 
 extern "C" {
+
+// Asymmetric three-party RSS product (run_crt_asym): C[p] = z_p for p = 0, 1, 2.  -7: not
+// applicable (the caller runs the generic form of the same z_p).
+int mx_gemm_asym(int words, int64_t M, int64_t N, int64_t K, const void* S0, const void* S1,
+                 const void* T0, const void* T1, int rolled, void* C, void* stream) {
+  if (M == 0 || N == 0) return 0;
+  if (!rolled && (!S1 || !T1)) return -2;
+  hipStream_t st = (hipStream_t)stream;
+  if (words == 1)
+    return run_crt_asym<u64>(M, N, K, (const u64*)S0, (const u64*)S1, (const u64*)T0,
+                             (const u64*)T1, rolled, (u64*)C, st);
+  if (words == 2)
+    return run_crt_asym<u128>(M, N, K, (const u128*)S0, (const u128*)S1, (const u128*)T0,
+                              (const u128*)T1, rolled, (u128*)C, st);
+  return -2;
+}
 
 // Moduli count for a K' (= K, or 2K in mode 1) inner dimension; -1 if out of range.
 int mx_crt_moduli(int words, int64_t kprime) {

@@ -252,6 +252,9 @@ _SIGS = {
     "mx_key_refresh_host": (None, [c_vp, c_u64, c_int, c_vp]),
     "mx_copy_many": (c_int, [c_vp, c_int, c_i64, c_vp]),
     "mx_graph_free": (c_int, [c_vp, c_vp]),
+    "mx_gemm_asym": (
+        c_int, [c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
+    ),
     "mx_gemm_roll": (
         c_int,
         [c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_int,

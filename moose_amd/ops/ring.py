@@ -968,6 +968,62 @@ def dot_cross_pair(x0: RT, y0: RT, y1: RT, roll: int, pb: PreparedCross = None, 
     return out
 
 
+def _asym_operands(x0: RT, x1: RT, y0: RT, y1: RT):
+    """Stacks (A0, A1, B0, B1) whose mode-1 cross GEMM A0.(B0 + B1) + A1.B0 is the
+    asymmetric z_p of dot_cross_asym, per party p with (a, b, c, d) = (x0, x1, y0, y1)[p]:
+    (a + b, 0, c, d), (b, a, d, c), (a, b, c, d - c)."""
+    def at(t, p):
+        return RT(t.data[p], t.bits)
+
+    a, b, c, d = ([at(t, p) for p in range(3)] for t in (x0, x1, y0, y1))
+    zero = zeros(tuple(x0.shape[1:]), x0.bits, x0.device)
+    stk = lambda ts: RT(torch.stack([t.data for t in ts]), x0.bits)  # noqa: E731
+    A0 = stk([binary("add", a[0], b[0]), b[1], a[2]])
+    A1 = stk([zero, a[1], b[2]])
+    B0 = stk([c[0], d[1], c[2]])
+    B1 = stk([d[0], c[1], binary("sub", d[2], c[2])])
+    return A0, A1, B0, B1
+
+
+def dot_cross_asym(x0: RT, x1: RT, y0: RT, y1: RT, rolled: bool = False) -> RT:
+    """The three parties' local products of a replicated matrix product, in the asymmetric
+    form (x0/x1: [3, M, K] first/second share stacks, y0/y1: [3, K, N]).  With party p
+    holding (a, b) = (x_p, x_{p+1}), (c, d) = (y_p, y_{p+1}):
+
+        z_0 = (a + b)(c + d),   z_1 = b (c + d) + a d,   z_2 = a d + b c.
+
+    Every x_i y_j appears exactly once over the three parties, so sum_p z_p = x.y as in the
+    symmetric form z_p = a (c + d) + b c (Araki et al.; the reference's
+    replicated/arith.rs:436-492), and each z_p is a function of party p's own shares only.
+    Party 0's product is one K-long GEMM instead of two: five K-long GEMMs per product
+    instead of six.  The zero share added before the reshare masks z_p exactly as before.
+    On the device the five run as one CRT GEMM launch (mx_gemm_asym; ``rolled``: x1/y1 are
+    x0/y0 rolled by one party, so x_2's residues are shared by parties 1 and 2); elsewhere
+    the same z_p by the generic cross GEMM of rearranged operands (_asym_operands)."""
+    bits = x0.bits
+    M, K = x0.shape[1], x0.shape[2]
+    N = y0.shape[2]
+    d = x0.data
+    if d.is_cuda and bits in (64, 128) and x0.shape[0] == 3 and y0.shape[0] == 3:
+        ts = [t.data if t is not None else None for t in (x0, x1, y0, y1)]
+        if rolled:
+            ts[1] = ts[3] = None
+        if all(t is None or t.is_contiguous() for t in ts):
+            out = empty((3, M, N), bits, d.device)
+            rc = nat.lib().mx_gemm_asym(
+                _words(bits), M, N, K, nat.ptr(ts[0]), None if ts[1] is None else nat.ptr(ts[1]),
+                nat.ptr(ts[2]), None if ts[3] is None else nat.ptr(ts[3]), 1 if rolled else 0,
+                nat.ptr(out.data), nat.stream_of(d))
+            if rc != -7:
+                nat.check(rc, "gemm_asym")
+                return out
+    if x1 is None or y1 is None:
+        x1 = RT(torch.roll(x0.data, -1, dims=0), bits)
+        y1 = RT(torch.roll(y0.data, -1, dims=0), bits)
+    A0, A1, B0, B1 = _asym_operands(x0, x1, y0, y1)
+    return dot_cross(A0, A1, B0, B1, nb=1)
+
+
 def _party_batch_strides(t: RT):
     """(party stride, batch stride) in ring elements of a [P, B, *inner] device tensor whose
     inner dims are contiguous (e.g. an expanded, stride-0 stack of one operand); None if

@@ -147,6 +147,14 @@ class Session:
         return attrs
 
 
+def _asym_applies(x, y) -> bool:
+    """Whether a stacked product [3, M, K] . [3, K, N] takes the asymmetric local products:
+    large products only (every dimension >= 256), a rule on the shape alone."""
+    xs, ys = x.shape, y.shape
+    return (len(xs) == 3 and len(ys) == 3 and xs[0] == 3 and ys[0] == 3 and x.bits in (64, 128)
+            and min(xs[1], xs[2], ys[2]) >= 256)
+
+
 class StackedSession(Session):
     """All three parties of every replicated placement on one device (module doc)."""
 
@@ -842,6 +850,9 @@ class StackedSession(Session):
     # every party of a session on this device: a pair's second share vector is its first
     # rolled by one party (s1[p] = s0[p + 1]), so the CRT GEMM needs the residues of s0 only
     pair_rolled = os.environ.get("MOOSEX_PAIR_ROLL", "1") != "0"
+    # products with every dimension >= 256 take the asymmetric local products
+    # (ops/ring.py dot_cross_asym) on every device, so CPU and GPU sessions agree bitwise
+    dot_asym = os.environ.get("MOOSEX_DOT_ASYM", "1") != "0"
 
     def p_dot_cross_rows(self, plc, x0, x1, r0, r1, prepared):
         if self.pair_rolled:
@@ -856,6 +867,9 @@ class StackedSession(Session):
         one evaluation (e.g. a chain z = z.y) has its GEMM operand image prepared once, from
         its second use on; every product is still computed."""
         yv0, yv1 = y0.v, y1.v
+        if nbatch == 0 and self.dot_asym and _asym_applies(x0.v, yv0):
+            # the asymmetric local products (five K-long GEMMs instead of six; same sum)
+            return PV(plc, R.dot_cross_asym(x0.v, x1.v, yv0, yv1, rolled=self.pair_rolled))
         # (not while dataflow lanes run: a prepared image produced on one lane would be
         # read by products on other lanes without an event)
         if (nbatch == 0 and self.device.type == "cuda" and len(yv0.shape) == 3
