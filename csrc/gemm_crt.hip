@@ -286,16 +286,26 @@ __device__ __forceinline__ void residue2(const uint32_t (&xa)[NW], const uint32_
 // columns ([K][R]) of B0 (mode 0), [B0 + B1 ; B0] (1), [B0 ; B1] (2) or B0 + B1 (3).
 // nkb k-steps are generated; the image is laid out with nkb_s k-steps per tile (>= nkb: a
 // shorter operand placed in a longer operand's slot).
+// src.n > 0: batch entry b takes its operands and mode from src instead (one launch for a
+// set of images of different forms, e.g. run_crt_asym's sums beside plain shares).
+struct PrepSrcs {
+  int n = 0;
+  int mode[6];
+  const void* x0[6];
+  const void* x1[6];
+};
+
 template <class T, bool TRANS, int ROWS, bool PK = true>
 __global__ void __launch_bounds__(256)
     k_crt_prep(const T* __restrict__ X0, const T* __restrict__ X1, int64_t R, int64_t K,
-               int64_t xs, int mode, int8_t* __restrict__ out, int64_t tiles, int64_t nkb,
-               int64_t nkb_s, const PrepTab tab) {
+               int64_t xs, int mode_all, int8_t* __restrict__ out, int64_t tiles, int64_t nkb,
+               int64_t nkb_s, const PrepTab tab, const PrepSrcs src) {
   constexpr int NW = Words<T>::N;
   const int64_t total = tiles * nkb * (ROWS * 4);
   const int64_t b = blockIdx.y;
-  const T* x0 = X0 + b * xs;
-  const T* x1 = mode ? X1 + b * xs : x0;
+  const int mode = src.n > 0 ? src.mode[b] : mode_all;
+  const T* x0 = src.n > 0 ? (const T*)src.x0[b] : X0 + b * xs;
+  const T* x1 = src.n > 0 ? (const T*)src.x1[b] : (mode ? X1 + b * xs : x0);
   const int n = tab.n;
   const int64_t plane = tiles * nkb_s * (int64_t)(ROWS * BK);
   int8_t* ob = out + b * n * plane;
@@ -605,7 +615,8 @@ template <int WR, int WC, int BN, int MINW, int STG = kStages, int IL = 0>
 __global__ void __launch_bounds__(64 * WR * WC, MINW)
     k_crt_gemm16(const int8_t* __restrict__ RA, const int8_t* __restrict__ RB,
                  int8_t* __restrict__ CR, int tiles_m, int tiles_n, int nkb_all, int gM,
-                 const EpiTab ep, int dma_mask, int bcast, int a_nkb, int roll, int amap) {
+                 const EpiTab ep, int dma_mask, int bcast, int a_nkb, int roll, int amap,
+                 int bmap) {
   constexpr int NW = WR * WC;
   constexpr int MI = BM / WR / 16, NJ = BN / WC / 16;
   constexpr int NM = MI * NJ;                    // MFMAs per wave per k-step
@@ -633,6 +644,7 @@ __global__ void __launch_bounds__(64 * WR * WC, MINW)
   // first) -- the image holds each batch entry's K residues once; k-blocks from a_nkb on
   // read entry b + roll's image (ga2 is biased so that ga2 + kb * kImg addresses it)
   const int8_t* ga2 = ga;
+  const int8_t* gb2 = gb;
   int khalf = 1 << 30;
   if (roll) {
     const int nbt = (int)gridDim.y / ep.n;
@@ -641,13 +653,18 @@ __global__ void __launch_bounds__(64 * WR * WC, MINW)
           (int64_t)a_nkb * kImg;
     khalf = a_nkb;
   } else if (amap < 0) {
-    // party b reads A' = [entry e1 | entry e2] of the K-residue image, or only e1's K
+    // party b reads A' = [entry e1 | entry e2] of the K-residue A image and
+    // B' = [entry f1 ; entry f2] of the K-residue B image (bmap), or only (e1, f1)'s K
     // (k-steps [0, a_nkb): party 0's one-GEMM product) when its half bit is set
     const int sh = 8 * (g / ep.n);
     const int e1 = (amap >> sh) & 7, e2 = (amap >> (sh + 3)) & 7;
+    const int f1 = (bmap >> sh) & 7, f2 = (bmap >> (sh + 3)) & 7;
     ga = RA + ((int64_t)(e1 * ep.n + mi) * tiles_m + tm) * a_nkb * (int64_t)kImg;
     ga2 = RA + ((int64_t)(e2 * ep.n + mi) * tiles_m + tm) * a_nkb * (int64_t)kImg -
           (int64_t)a_nkb * kImg;
+    gb = RB + ((int64_t)(f1 * ep.n + mi) * tiles_n + tn) * a_nkb * (int64_t)kImgB;
+    gb2 = RB + ((int64_t)(f2 * ep.n + mi) * tiles_n + tn) * a_nkb * (int64_t)kImgB -
+          (int64_t)a_nkb * kImgB;
     khalf = a_nkb;
     if ((amap >> (sh + 6)) & 1) nkb = a_nkb;
   }
@@ -668,7 +685,7 @@ __global__ void __launch_bounds__(64 * WR * WC, MINW)
     const bool is_b = pc >= 16;
     const int pp = is_b ? pc - 16 : pc;
     srcs[t] = (is_b ? gb : ga) + pp * 1024 + lane * 16;
-    srcs2[t] = (is_b ? gb : ga2) + pp * 1024 + lane * 16;
+    srcs2[t] = (is_b ? gb2 : ga2) + pp * 1024 + lane * 16;
     dsts[t] = (is_b ? kImg : 0) + pp * 1024;
     steps[t] = is_b ? kImgB : kImg;
   }
@@ -1101,7 +1118,8 @@ bool prep_packed() {
 template <class T>
 void launch_prep(const CPlan& p, const Tables& tb, bool is_b, int64_t batch, int64_t R,
                  int64_t K, int64_t xs, const T* X0, const T* X1, int mode, int8_t* out,
-                 hipStream_t st, int64_t nkb = -1, int64_t nkb_s = -1) {
+                 hipStream_t st, int64_t nkb = -1, int64_t nkb_s = -1,
+                 const PrepSrcs& src = PrepSrcs()) {
   if (nkb < 0) nkb = p.nkb;
   if (nkb_s < nkb) nkb_s = nkb;
   const int64_t tiles = is_b ? p.tiles_n : p.tiles_m;
@@ -1113,24 +1131,24 @@ void launch_prep(const CPlan& p, const Tables& tb, bool is_b, int64_t batch, int
   if (!prep_packed() || is_b) {  // MOOSEX_CRT_PACKED=0: one residue at a time everywhere
     if (!is_b)
       hipLaunchKernelGGL((k_crt_prep<T, false, BM, false>), grid, dim3(256), 0, st, X0, X1, R, K,
-                         xs, mode, out, tiles, nkb, nkb_s, tb.pa);
+                         xs, mode, out, tiles, nkb, nkb_s, tb.pa, src);
     else if (rows == 256)
       hipLaunchKernelGGL((k_crt_prep<T, true, 256, false>), grid, dim3(256), 0, st, X0, X1, R, K,
-                         xs, mode, out, tiles, nkb, nkb_s, tb.pb);
+                         xs, mode, out, tiles, nkb, nkb_s, tb.pb, src);
     else
       hipLaunchKernelGGL((k_crt_prep<T, true, 128, false>), grid, dim3(256), 0, st, X0, X1, R, K,
-                         xs, mode, out, tiles, nkb, nkb_s, tb.pb);
+                         xs, mode, out, tiles, nkb, nkb_s, tb.pb, src);
     return;
   }
   if (!is_b)
     hipLaunchKernelGGL((k_crt_prep<T, false, BM>), grid, dim3(256), 0, st, X0, X1, R, K, xs, mode,
-                       out, tiles, nkb, nkb_s, tb.pa);
+                       out, tiles, nkb, nkb_s, tb.pa, src);
   else if (rows == 256)
     hipLaunchKernelGGL((k_crt_prep<T, true, 256>), grid, dim3(256), 0, st, X0, X1, R, K, xs, mode,
-                       out, tiles, nkb, nkb_s, tb.pb);
+                       out, tiles, nkb, nkb_s, tb.pb, src);
   else
     hipLaunchKernelGGL((k_crt_prep<T, true, 128>), grid, dim3(256), 0, st, X0, X1, R, K, xs, mode,
-                       out, tiles, nkb, nkb_s, tb.pb);
+                       out, tiles, nkb, nkb_s, tb.pb, src);
 }
 
 // MOOSEX_CRT_DMA_MASK (timing experiments, wrong results): bit 0 = stream A, bit 1 = B,
@@ -1143,7 +1161,7 @@ int dma_mask() {
 template <int WR, int WC, int BN, int MINW, bool M16, int STG = kStages, int IL = 0>
 void launch_variant(const CPlan& p, const Tables& tb, int64_t batch, const int8_t* ra,
                     const int8_t* rb, int8_t* cr, int bcast, int roll, hipStream_t st,
-                    int amap = 0) {
+                    int amap = 0, int bmap = 0) {
   constexpr int lds = STG * (kImg + BN * BK);
   const void* fn = M16 ? (const void*)k_crt_gemm16<WR, WC, BN, MINW, STG, IL>
                        : (const void*)k_crt_gemm<WR, WC, BN, MINW>;
@@ -1152,7 +1170,7 @@ void launch_variant(const CPlan& p, const Tables& tb, int64_t batch, const int8_
   if constexpr (M16)
     hipLaunchKernelGGL((k_crt_gemm16<WR, WC, BN, MINW, STG, IL>), grid, dim3(64 * WR * WC), lds, st, ra,
                        rb, cr, (int)p.tiles_m, (int)p.tiles_n, (int)p.nkb, gemm_group_m(), tb.ep,
-                       dma_mask(), bcast, (int)p.a_nkb, roll, amap);
+                       dma_mask(), bcast, (int)p.a_nkb, roll, amap, bmap);
   else
     hipLaunchKernelGGL((k_crt_gemm<WR, WC, BN, MINW>), grid, dim3(64 * WR * WC), lds, st, ra, rb,
                        cr, (int)p.tiles_m, (int)p.tiles_n, (int)p.nkb, gemm_group_m(), tb.ep,
@@ -1161,24 +1179,24 @@ void launch_variant(const CPlan& p, const Tables& tb, int64_t batch, const int8_
 
 void launch_crt_gemm(const CPlan& p, const Tables& tb, int64_t batch, const int8_t* ra,
                      const int8_t* rb, int8_t* cr, int bcast, int roll, hipStream_t st,
-                     int amap = 0) {
+                     int amap = 0, int bmap = 0) {
   switch (crt_kernel()) {  // roll, amap: 16x16x64 kernels only (run_crt* check)
     case 1: launch_variant<2, 2, 256, 1, false>(p, tb, batch, ra, rb, cr, bcast, 0, st); break;
     case 2: launch_variant<2, 4, 256, 2, false>(p, tb, batch, ra, rb, cr, bcast, 0, st); break;
-    case 4: launch_variant<2, 2, 256, 1, true>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
+    case 4: launch_variant<2, 2, 256, 1, true>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap, bmap); break;
     case 3: launch_variant<2, 2, 128, 2, false>(p, tb, batch, ra, rb, cr, bcast, 0, st); break;
-    case 6: launch_variant<2, 4, 256, 2, true>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
-    case 7: launch_variant<2, 4, 256, 2, true, 4>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
-    case 8: launch_variant<2, 4, 256, 2, true, 3, 1>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
-    case 9: launch_variant<2, 4, 256, 2, true, 4, 1>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
-    case 10: launch_variant<2, 4, 256, 2, true, 3, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
-    case 11: launch_variant<2, 4, 256, 2, true, 4, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
-    case 12: launch_variant<2, 2, 256, 1, true, 3, 1>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
-    case 13: launch_variant<2, 2, 256, 1, true, 4, 1>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
-    case 14: launch_variant<2, 2, 256, 1, true, 3, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
-    case 15: launch_variant<2, 2, 256, 1, true, 4, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
-    case 16: launch_variant<2, 4, 256, 2, true, 5, 3>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
-    default: launch_variant<2, 2, 128, 2, true>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap); break;
+    case 6: launch_variant<2, 4, 256, 2, true>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap, bmap); break;
+    case 7: launch_variant<2, 4, 256, 2, true, 4>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap, bmap); break;
+    case 8: launch_variant<2, 4, 256, 2, true, 3, 1>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap, bmap); break;
+    case 9: launch_variant<2, 4, 256, 2, true, 4, 1>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap, bmap); break;
+    case 10: launch_variant<2, 4, 256, 2, true, 3, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap, bmap); break;
+    case 11: launch_variant<2, 4, 256, 2, true, 4, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap, bmap); break;
+    case 12: launch_variant<2, 2, 256, 1, true, 3, 1>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap, bmap); break;
+    case 13: launch_variant<2, 2, 256, 1, true, 4, 1>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap, bmap); break;
+    case 14: launch_variant<2, 2, 256, 1, true, 3, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap, bmap); break;
+    case 15: launch_variant<2, 2, 256, 1, true, 4, 2>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap, bmap); break;
+    case 16: launch_variant<2, 4, 256, 2, true, 5, 3>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap, bmap); break;
+    default: launch_variant<2, 2, 128, 2, true>(p, tb, batch, ra, rb, cr, bcast, roll, st, amap, bmap); break;
   }
 }
 
@@ -1326,33 +1344,61 @@ int run_crt_asym(int64_t M, int64_t N, int64_t K, const T* S0, const T* S1, cons
     c[q] = T0 + q * sb;
     d[q] = rolled ? T0 + ((q + 1) % 3) * sb : T1 + q * sb;
   }
-  // A' images (K residues each): E0 = a_0 + b_0; party 1 reads [b_1 | a_1], party 2 [a_2 | b_2]
-  const T* ent[5] = {nullptr, b[1], a[1], a[2], b[2]};
-  int ne = 5, e21 = 3, e22 = 4;
-  if (rolled) {  // a_2 = b_1 = x_2
-    ne = 4;
-    ent[3] = b[2];  // x_0
-    e21 = 1;
-    e22 = 3;
-  }
+  // K-residue images.  A: E0 = a_0 + b_0; party 1 reads [b_1 | a_1], party 2 [a_2 | b_2].
+  // B: F0 = c_0 + d_0, F1 = c_1 + d_1; party 1 reads [F1 ; d_1], party 2 [d_2 ; c_2].
+  // Rolled (a_p = x_p, b_p = x_{p+1}, c_p = y_p, d_p = y_{p+1}): b_1 = a_2 = x_2 and
+  // d_1 = c_2 = y_2 are one image each -- A = [x_0 + x_1, x_2, x_1, x_0], B = [y_0 + y_1,
+  // y_1 + y_2, y_2, y_0] -- and each image group is one batched launch.
+  int na, nb, amap, bmap;
   const int64_t a_entry = p.n * p.tiles_m * p.a_nkb * (int64_t)kImg;
-  const int64_t ra_bytes = ne * a_entry;
-  const int64_t b_entry = p.rb_bytes / 3;
-  int8_t* ws = (int8_t*)workspace(ra_bytes + p.rb_bytes + p.cr_bytes, st);
+  const int64_t b_entry = p.n * p.tiles_n * p.a_nkb * (int64_t)(p.bn * BK);
+  auto pmap = [](int e0, int e1, int e2, int e3, int e4) {  // party 0: (e0, -) half-length
+    return (int)(0x80000000u | (unsigned)e0 | (1u << 6) | ((unsigned)(e1 | (e2 << 3)) << 8) |
+                 ((unsigned)(e3 | (e4 << 3)) << 16));
+  };
+  if (rolled) {
+    na = 4;
+    nb = 4;
+    amap = pmap(0, 1, 2, 1, 3);
+    bmap = pmap(0, 1, 2, 3, 2);
+  } else {
+    na = 5;
+    nb = 5;
+    amap = pmap(0, 1, 2, 3, 4);
+    bmap = pmap(0, 1, 2, 3, 4);
+  }
+  const int64_t ra_bytes = na * a_entry, rb_bytes = nb * b_entry;
+  int8_t* ws = (int8_t*)workspace(ra_bytes + rb_bytes + p.cr_bytes, st);
   if (!ws) return -4;
   int8_t* ra = ws;
   int8_t* cr = ra + ra_bytes;
   int8_t* rb = cr + p.cr_bytes;
-  // B': party 0 (c + d) over K (in a 2K slot), party 1 [d + c ; d], party 2 [d ; c]
-  launch_prep<T>(p, tb, true, 1, N, K, 0, c[0], d[0], 3, rb, st, p.a_nkb, p.nkb);
-  launch_prep<T>(p, tb, true, 1, N, K, 0, d[1], c[1], 1, rb + b_entry, st);
-  launch_prep<T>(p, tb, true, 1, N, K, 0, d[2], c[2], 2, rb + 2 * b_entry, st);
-  launch_prep<T>(p, tb, false, 1, M, K, 0, a[0], b[0], 2, ra, st, p.a_nkb);
-  for (int e = 1; e < ne; ++e)
-    launch_prep<T>(p, tb, false, 1, M, K, 0, ent[e], ent[e], 0, ra + e * a_entry, st, p.a_nkb);
-  const int amap = (int)(0x80000000u | (1u << 6) | ((1u | (2u << 3)) << 8) |
-                         ((unsigned)(e21 | (e22 << 3)) << 16));
-  launch_crt_gemm(p, tb, 3, ra, rb, cr, 0, 0, st, amap);
+  const int64_t kn = p.a_nkb;
+  // every image of a side in one launch (a lone batch-1 launch of the sum ran at half the
+  // bandwidth of the batched images)
+  PrepSrcs sa_, sb_;
+  auto put = [](PrepSrcs& q, const T* x0, const T* x1, int mode) {
+    q.x0[q.n] = x0;
+    q.x1[q.n] = x1;
+    q.mode[q.n] = mode;
+    ++q.n;
+  };
+  put(sa_, a[0], b[0], 2);
+  put(sb_, c[0], d[0], 3);
+  put(sb_, c[1], d[1], 3);
+  if (rolled) {
+    put(sa_, a[2], a[2], 0);  // x_2
+    put(sa_, a[1], a[1], 0);  // x_1
+    put(sa_, a[0], a[0], 0);  // x_0
+    put(sb_, d[1], d[1], 0);  // y_2
+    put(sb_, d[2], d[2], 0);  // y_0
+  } else {
+    for (const T* e : {b[1], a[1], a[2], b[2]}) put(sa_, e, e, 0);
+    for (const T* f : {d[1], d[2], c[2]}) put(sb_, f, f, 0);
+  }
+  launch_prep<T>(p, tb, true, sb_.n, N, K, 0, nullptr, nullptr, 0, rb, st, kn, kn, sb_);
+  launch_prep<T>(p, tb, false, sa_.n, M, K, 0, nullptr, nullptr, 0, ra, st, kn, kn, sa_);
+  launch_crt_gemm(p, tb, 3, ra, rb, cr, 0, 0, st, amap, bmap);
   launch_recon<T>(p, tb, 3, M, N, cr, C, 0, st);
   const hipError_t e = hipGetLastError();
   return e != hipSuccess ? -100 - (int)e : 0;

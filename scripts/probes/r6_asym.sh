@@ -2,7 +2,7 @@
 # r6: asymmetric local products (five K-long GEMMs instead of six) -- tests, A/B bench, kernel table
 cd "$(dirname "$0")/../.."
 export PYTHONPATH=$PWD TMPDIR=/tmp
-out=gpurun_out/${OUT:-r6asym}
+out=gpurun_out/${OUT:-r6asym3}
 mkdir -p $out
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
   tests/test_dot_asym.py tests/test_gemm_crt.py > $out/pytest.log 2>&1
