@@ -114,3 +114,39 @@ def test_gpu_session_dot_asym_bitwise_cpu():
     assert torch.equal(zg.s1.v.data.cpu(), zc.s1.v.data)
     assert torch.equal(og, oc)
     assert (og - want).abs().max() < 1e-4
+
+
+def _cyclic_vs_stacked(device):
+    from moose_amd.parallel.cyclic import CyclicSession
+    from moose_amd.parallel.cyclic import RingComm
+
+    cyc = CyclicSession(RingComm(0, 1, device), {"a": 0, "b": 1, "c": 2}, device, seed=9,
+                        pipeline_chunks=1)
+    keys = cyc.session_keys(PLC, 0)
+    st = StackedSession("cpu", seed=9)
+    st.fused = False
+    st.keytable._write(st.setup(PLC), keys)
+    res = []
+    for sess, dev in ((cyc, device), (st, "cpu")):
+        g = torch.Generator().manual_seed(4)
+        a, b = (torch.rand(256, 256, generator=g, dtype=torch.float64) - 0.5 for _ in range(2))
+        X = rep.share(sess, PLC, HV("a", R.encode(a.to(dev), 23, 128)))
+        Y = rep.share(sess, PLC, HV("b", R.encode(b.to(dev), 23, 128)))
+        Z = rep.dot_trunc(sess, X, Y, 23)
+        out = R.decode(R.RT(rep.reveal(sess, Z, "c").v.data, 128), 23).cpu()
+        res.append((Z.s0.v.data.cpu(), Z.s1.v.data.cpu(), out, a @ b))
+    (c0, c1, co, want), (s0, s1, so, _) = res
+    assert torch.equal(c0, s0) and torch.equal(c1, s1) and torch.equal(co, so)
+    assert (co - want).abs().max() < 1e-4
+
+
+def test_cyclic_session_asym_bitwise_stacked():
+    """The cyclic layout's session (components of different sessions: the two-stack form)
+    takes the same asymmetric products as a stacked session: bitwise the same shares."""
+    _cyclic_vs_stacked("cpu")
+
+
+@pytest.mark.gpu
+def test_gpu_cyclic_session_asym_bitwise_cpu_stacked():
+    """On the device the cyclic session runs the one-launch five-image form (no roll)."""
+    _cyclic_vs_stacked("cuda:0")
