@@ -367,6 +367,16 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// o = a + b over n ring elements (run_crt_asym's party-0 A' sum, written once so that its
+// residue image streams one operand: the two-operand prep ran at ~2.4 plain images)
+template <class T>
+__global__ void __launch_bounds__(256)
+    k_add_pair(const T* __restrict__ a, const T* __restrict__ b, T* __restrict__ o, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    o[i] = a[i] + b[i];
+}
+
 // XCD-aware remap (as gemm_mfma.hip): consecutive tile ids land on one XCD
 __device__ inline int64_t xcd_remap(int64_t bid, int64_t nwg) {
   const int64_t q = nwg / 8, r = nwg % 8;
@@ -1368,11 +1378,20 @@ int run_crt_asym(int64_t M, int64_t N, int64_t K, const T* S0, const T* S1, cons
     bmap = pmap(0, 1, 2, 3, 4);
   }
   const int64_t ra_bytes = na * a_entry, rb_bytes = nb * b_entry;
-  int8_t* ws = (int8_t*)workspace(ra_bytes + rb_bytes + p.cr_bytes, st);
+  static const bool asum = [] {  // MOOSEX_CRT_ASUM=0: the sum inside the prep (mode 2)
+    const char* e = std::getenv("MOOSEX_CRT_ASUM");
+    return !(e && e[0] == '0');
+  }();
+  const int64_t sum_bytes = asum ? round_up(sa * (int64_t)sizeof(T), 256) : 0;
+  int8_t* ws = (int8_t*)workspace(ra_bytes + rb_bytes + p.cr_bytes + sum_bytes, st);
   if (!ws) return -4;
   int8_t* ra = ws;
   int8_t* cr = ra + ra_bytes;
   int8_t* rb = cr + p.cr_bytes;
+  T* a01 = asum ? (T*)(rb + rb_bytes) : nullptr;
+  if (asum)
+    hipLaunchKernelGGL((k_add_pair<T>), dim3((unsigned)std::min<int64_t>((sa + 255) / 256, 65536)),
+                       dim3(256), 0, st, a[0], b[0], a01, sa);
   const int64_t kn = p.a_nkb;
   // every image of a side in one launch (a lone batch-1 launch of the sum ran at half the
   // bandwidth of the batched images)
@@ -1383,7 +1402,10 @@ int run_crt_asym(int64_t M, int64_t N, int64_t K, const T* S0, const T* S1, cons
     q.mode[q.n] = mode;
     ++q.n;
   };
-  put(sa_, a[0], b[0], 2);
+  if (asum)
+    put(sa_, a01, a01, 0);
+  else
+    put(sa_, a[0], b[0], 2);
   put(sb_, c[0], d[0], 3);
   put(sb_, c[1], d[1], 3);
   if (rolled) {
