@@ -288,11 +288,15 @@ __device__ __forceinline__ void residue2(const uint32_t (&xa)[NW], const uint32_
 // shorter operand placed in a longer operand's slot).
 // src.n > 0: batch entry b takes its operands and mode from src instead (one launch for a
 // set of images of different forms, e.g. run_crt_asym's sums beside plain shares).
+// dual[b] != 0 (mode 0 only): the thread then adds x1 to the elements it holds and writes
+// the sum's image too, at byte offset dual[b] from entry b's own image -- a share's image
+// and the image of its sum with the next share from one read of the share.
 struct PrepSrcs {
   int n = 0;
   int mode[6];
   const void* x0[6];
   const void* x1[6];
+  int64_t dual[6];
 };
 
 template <class T, bool TRANS, int ROWS, bool PK = true>
@@ -336,7 +340,8 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
       for (int w = 0; w < NW; ++w) v[j][w] = (uint32_t)(e >> (32 * w));
     }
-    int8_t* base = ob + (t * nkb_s + kb) * (int64_t)(ROWS * BK) + img_off(r, c);
+    const int64_t boff = (t * nkb_s + kb) * (int64_t)(ROWS * BK) + img_off(r, c);
+    auto emit = [&](int8_t* base) __attribute__((always_inline)) {
     {  // p = 256: the low byte (times the folded inverse)
       int rr[16];
 #pragma unroll
@@ -363,6 +368,23 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
       for (int u = 0; u < 4; ++u) o[u] = (int)pack4(rr[4 * u], rr[4 * u + 1], rr[4 * u + 2], rr[4 * u + 3]);
       *(v4i*)(base + i * plane) = o;
+    }
+    };
+    emit(ob + boff);
+    if (src.n > 0 && src.dual[b]) {  // + x1: the sum's image from the same read of x0
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int64_t k = k0 + j;
+        if (row < R && k < K) {
+          T e = 0;
+#pragma unroll
+          for (int w = 0; w < NW; ++w) e |= (T)v[j][w] << (32 * w);
+          e += TRANS ? x1[k * R + row] : x1[row * K + k];
+#pragma unroll
+          for (int w = 0; w < NW; ++w) v[j][w] = (uint32_t)(e >> (32 * w));
+        }
+      }
+      emit(ob + src.dual[b] + boff);
     }
   }
 }
@@ -1138,7 +1160,11 @@ void launch_prep(const CPlan& p, const Tables& tb, bool is_b, int64_t batch, int
   const dim3 grid((unsigned)std::min<int64_t>((work + 255) / 256, 16384), (unsigned)batch);
   // packed residues pay on A' (0.626 -> 0.592 ms at 4096^2) but not on the B' image, which
   // streams 1.5x the bytes and loses more to the extra VGPRs (1.128 -> 1.163 ms)
-  if (!prep_packed() || is_b) {  // MOOSEX_CRT_PACKED=0: one residue at a time everywhere
+  static const bool packed_b = [] {  // MOOSEX_CRT_PACKED_B=1: packed residues on B' too
+    const char* e = std::getenv("MOOSEX_CRT_PACKED_B");
+    return e && e[0] == '1';
+  }();
+  if (!prep_packed() || (is_b && !packed_b)) {  // MOOSEX_CRT_PACKED=0: one at a time everywhere
     if (!is_b)
       hipLaunchKernelGGL((k_crt_prep<T, false, BM, false>), grid, dim3(256), 0, st, X0, X1, R, K,
                          xs, mode, out, tiles, nkb, nkb_s, tb.pa, src);
@@ -1382,44 +1408,63 @@ int run_crt_asym(int64_t M, int64_t N, int64_t K, const T* S0, const T* S1, cons
     const char* e = std::getenv("MOOSEX_CRT_ASUM");
     return !(e && e[0] == '0');
   }();
-  const int64_t sum_bytes = asum ? round_up(sa * (int64_t)sizeof(T), 256) : 0;
+  static const bool dual = [] {  // MOOSEX_CRT_DUAL=0: separate sum images
+    const char* e = std::getenv("MOOSEX_CRT_DUAL");
+    return !(e && e[0] == '0');
+  }();
+  // rolled: the sums ride on the share images' threads (dual) -- no separate sum pass
+  const bool duals = rolled && dual;
+  const int64_t sum_bytes = asum && !duals ? round_up(sa * (int64_t)sizeof(T), 256) : 0;
   int8_t* ws = (int8_t*)workspace(ra_bytes + rb_bytes + p.cr_bytes + sum_bytes, st);
   if (!ws) return -4;
   int8_t* ra = ws;
   int8_t* cr = ra + ra_bytes;
   int8_t* rb = cr + p.cr_bytes;
-  T* a01 = asum ? (T*)(rb + rb_bytes) : nullptr;
-  if (asum)
+  T* a01 = sum_bytes ? (T*)(rb + rb_bytes) : nullptr;
+  if (a01)
     hipLaunchKernelGGL((k_add_pair<T>), dim3((unsigned)std::min<int64_t>((sa + 255) / 256, 65536)),
                        dim3(256), 0, st, a[0], b[0], a01, sa);
   const int64_t kn = p.a_nkb;
   // every image of a side in one launch (a lone batch-1 launch of the sum ran at half the
   // bandwidth of the batched images)
   PrepSrcs sa_, sb_;
-  auto put = [](PrepSrcs& q, const T* x0, const T* x1, int mode) {
+  auto put = [](PrepSrcs& q, const T* x0, const T* x1, int mode, int64_t dual = 0) {
     q.x0[q.n] = x0;
     q.x1[q.n] = x1;
     q.mode[q.n] = mode;
+    q.dual[q.n] = dual;
     ++q.n;
   };
-  if (asum)
-    put(sa_, a01, a01, 0);
-  else
-    put(sa_, a[0], b[0], 2);
-  put(sb_, c[0], d[0], 3);
-  put(sb_, c[1], d[1], 3);
-  if (rolled) {
-    put(sa_, a[2], a[2], 0);  // x_2
-    put(sa_, a[1], a[1], 0);  // x_1
-    put(sa_, a[0], a[0], 0);  // x_0
-    put(sb_, d[1], d[1], 0);  // y_2
-    put(sb_, d[2], d[2], 0);  // y_0
+  if (duals) {
+    // A = [x0 + x1, x2, x1, x0]: the x0 thread writes E3 and then E0 = x0 + x1.
+    // B = [y0 + y1, y1 + y2, y2, y0]: the y2 thread writes F2 and then F1 = y2 + y1, the y0
+    // thread F3 and then F0 = y0 + y1.  Launched as entries 1..3 / 2..3 of the image.
+    put(sa_, a[2], a[2], 0);                  // E1 = x2
+    put(sa_, a[1], a[1], 0);                  // E2 = x1
+    put(sa_, a[0], b[0], 0, -3 * a_entry);    // E3 = x0, dual E0 = x0 + x1
+    put(sb_, d[1], c[1], 0, -b_entry);        // F2 = y2, dual F1 = y2 + y1
+    put(sb_, d[2], d[0], 0, -3 * b_entry);    // F3 = y0, dual F0 = y0 + y1
+    launch_prep<T>(p, tb, true, sb_.n, N, K, 0, nullptr, nullptr, 0, rb + 2 * b_entry, st, kn,
+                   kn, sb_);
+    launch_prep<T>(p, tb, false, sa_.n, M, K, 0, nullptr, nullptr, 0, ra + a_entry, st, kn, kn,
+                   sa_);
   } else {
-    for (const T* e : {b[1], a[1], a[2], b[2]}) put(sa_, e, e, 0);
-    for (const T* f : {d[1], d[2], c[2]}) put(sb_, f, f, 0);
+    if (a01)
+      put(sa_, a01, a01, 0);
+    else
+      put(sa_, a[0], b[0], 2);
+    put(sb_, c[0], d[0], 3);
+    put(sb_, c[1], d[1], 3);
+    if (rolled) {
+      for (const T* e : {a[2], a[1], a[0]}) put(sa_, e, e, 0);  // x2, x1, x0
+      for (const T* f : {d[1], d[2]}) put(sb_, f, f, 0);        // y2, y0
+    } else {
+      for (const T* e : {b[1], a[1], a[2], b[2]}) put(sa_, e, e, 0);
+      for (const T* f : {d[1], d[2], c[2]}) put(sb_, f, f, 0);
+    }
+    launch_prep<T>(p, tb, true, sb_.n, N, K, 0, nullptr, nullptr, 0, rb, st, kn, kn, sb_);
+    launch_prep<T>(p, tb, false, sa_.n, M, K, 0, nullptr, nullptr, 0, ra, st, kn, kn, sa_);
   }
-  launch_prep<T>(p, tb, true, sb_.n, N, K, 0, nullptr, nullptr, 0, rb, st, kn, kn, sb_);
-  launch_prep<T>(p, tb, false, sa_.n, M, K, 0, nullptr, nullptr, 0, ra, st, kn, kn, sa_);
   launch_crt_gemm(p, tb, 3, ra, rb, cr, 0, 0, st, amap, bmap);
   launch_recon<T>(p, tb, 3, M, N, cr, C, 0, st);
   const hipError_t e = hipGetLastError();
