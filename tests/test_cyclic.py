@@ -33,11 +33,13 @@ def _data(session, bits):
     return R.encode(v, 23, bits)
 
 
-def _mats(session, bits):
-    """(256 x 16) . (16 x 8) operands for the row-chunked dot+TruncPr pipeline."""
-    a = torch.linspace(-3, 3, 256 * 16, dtype=torch.float64).reshape(256, 16) + 0.1 * session
-    b = torch.linspace(-2, 2, 16 * 8, dtype=torch.float64).reshape(16, 8) - 0.05 * session
-    return R.encode(a, 23, bits), R.encode(b, 23, bits)
+def _mats(session, bits, big=False):
+    """(256 x 16) . (16 x 8) operands for the row-chunked dot+TruncPr pipeline; ``big``:
+    (256 x 256) . (256 x 256), large enough for the asymmetric local products."""
+    k, n = (256, 256) if big else (16, 8)
+    a = torch.linspace(-3, 3, 256 * k, dtype=torch.float64).reshape(256, k) + 0.1 * session
+    b = torch.linspace(-2, 2, k * n, dtype=torch.float64).reshape(k, n) - 0.05 * session
+    return R.encode(a / (k / 16), 23, bits), R.encode(b, 23, bits)
 
 
 def _program(sess, xb, ya, mb, ma):
@@ -60,7 +62,7 @@ def _program(sess, xb, ya, mb, ma):
 
 
 def _worker(rank, world, port, q, device="cpu", offsets=None, chunks=4, dirs=None,
-            backend="gloo"):
+            backend="gloo", big=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if backend == "nccl":  # one GPU per rank, every exchange an RCCL send/recv
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -79,8 +81,8 @@ def _worker(rank, world, port, q, device="cpu", offsets=None, chunks=4, dirs=Non
         xd, yd = _data(sess.session_of("b"), bits), _data(100 + sess.session_of("a"), bits)
         xb = HV("b", R.RT(R.to_device(xd.data, device), bits))
         ya = HV("a", R.RT(R.to_device(yd.data, device), bits))
-        ma_, _ = _mats(sess.session_of("b"), bits)
-        _, mb_ = _mats(sess.session_of("a"), bits)
+        ma_, _ = _mats(sess.session_of("b"), bits, big)
+        _, mb_ = _mats(sess.session_of("a"), bits, big)
         mb = HV("b", R.RT(R.to_device(ma_.data, device), bits))
         ma = HV("a", R.RT(R.to_device(mb_.data, device), bits))
         ts, outs = _program(sess, xb, ya, mb, ma)
@@ -92,7 +94,7 @@ def _worker(rank, world, port, q, device="cpu", offsets=None, chunks=4, dirs=Non
     dist.destroy_process_group()
 
 
-def _stacked_reference(keys, session, chunks=4, dirs=None):
+def _stacked_reference(keys, session, chunks=4, dirs=None, big=False):
     """The worker's program for both ring widths, in the same order (one nonce stream)."""
     from moose_amd.runtime.session import HV
     from moose_amd.runtime.session import StackedSession
@@ -108,17 +110,17 @@ def _stacked_reference(keys, session, chunks=4, dirs=None):
     for bits in (64, 128):
         xb = HV("b", _data(session, bits))
         ya = HV("a", _data(100 + session, bits))
-        ma_, mb_ = _mats(session, bits)
+        ma_, mb_ = _mats(session, bits, big)
         out[bits] = _program(s, xb, ya, HV("b", ma_), HV("a", mb_))
     return out
 
 
-def _run(world, device, offsets=None, chunks=4, dirs=None, backend="gloo"):
+def _run(world, device, offsets=None, chunks=4, dirs=None, backend="gloo", big=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     ps = [ctx.Process(target=_worker, args=(r, world, port, q, device, offsets, chunks, dirs,
-                                            backend)) for r in range(world)]
+                                            backend, big)) for r in range(world)]
     for p in ps:
         p.start()
     got = {}
@@ -139,7 +141,7 @@ def _run(world, device, offsets=None, chunks=4, dirs=None, backend="gloo"):
     keys = got[0][1]
     refs = {}
     for s in range(world):
-        r = _stacked_reference(keys[s], s, chunks, dirs)
+        r = _stacked_reference(keys[s], s, chunks, dirs, big)
         refs.update({(s, b): r[b] for b in (64, 128)})
     for g in range(world):
         res, _, msgs = got[g]
@@ -161,7 +163,7 @@ def _run(world, device, offsets=None, chunks=4, dirs=None, backend="gloo"):
             np.testing.assert_allclose(
                 R.decode(R.RT(torch.from_numpy(out[0]), bits), 23).numpy(), want.numpy(),
                 atol=1e-5)
-            ma_, mb_ = _mats(s_c, bits)
+            ma_, mb_ = _mats(s_c, bits, big)
             want = R.decode(ma_, 23).numpy() @ R.decode(mb_, 23).numpy()
             np.testing.assert_allclose(
                 R.decode(R.RT(torch.from_numpy(out[1]), bits), 23).numpy(), want, atol=1e-4)
@@ -170,6 +172,13 @@ def _run(world, device, offsets=None, chunks=4, dirs=None, backend="gloo"):
 @pytest.mark.parametrize("world", [2, 3, 4])
 def test_cyclic_bitwise_equals_stacked(world):
     _run(world, "cpu")
+
+
+def test_cyclic_asym_products_bitwise_equals_stacked():
+    """Three ranks, a 256^3 product unchunked: every component takes the asymmetric local
+    products of its party (two-stack form) and the shares still equal the stacked
+    session's bit for bit."""
+    _run(3, "cpu", chunks=1, big=True)
 
 
 def test_cyclic_unchunked_dealer_early():
