@@ -289,8 +289,13 @@ void TcpNetworking::accept_loop() {
     int one = 1;
     ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
     std::lock_guard<std::mutex> g(readers_mu_);
+    try {
+      readers_.emplace_back([this, fd] { read_loop(fd); });
+    } catch (const std::system_error&) {  // no thread for this peer: refuse the connection
+      ::close(fd);
+      continue;
+    }
     reader_fds_.push_back(fd);
-    readers_.emplace_back([this, fd] { read_loop(fd); });
   }
 }
 

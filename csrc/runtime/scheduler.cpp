@@ -134,7 +134,21 @@ RunStats Dataflow::run(const std::function<void(int32_t)>& callback, int workers
   };
 
   std::vector<std::thread> pool;
-  for (int w = 0; w < workers; ++w) pool.emplace_back(worker);
+  try {
+    for (int w = 0; w < workers; ++w) pool.emplace_back(worker);
+  } catch (...) {
+    // a thread that cannot be started (e.g. the process's thread limit under load): stop
+    // and join the workers already running -- destroying a joinable std::thread would
+    // terminate the process -- then report the error to the caller
+    {
+      std::lock_guard<std::mutex> g(mu);
+      stop = true;
+    }
+    cv_work.notify_all();
+    for (auto& t : pool) t.join();
+    if (mb_ && listener >= 0) mb_->remove_listener(listener);
+    throw;
+  }
 
   {
     std::unique_lock<std::mutex> lk(mu);

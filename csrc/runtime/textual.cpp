@@ -4,6 +4,7 @@
 #include <array>
 #include <climits>
 #include <cstring>
+#include <system_error>
 #include <thread>
 
 namespace moosert {
@@ -494,16 +495,22 @@ std::vector<OpRecord> parse_computation(std::string_view src, const Schema& sche
   }
   std::vector<std::vector<OpRecord>> results(parts.size());
   std::vector<std::string> errors(parts.size());
+  auto parse = [&](size_t p) {
+    try {
+      results[p] = parse_chunk(src.substr(parts[p].first, parts[p].second - parts[p].first),
+                               line_base[p], schema);
+    } catch (const std::exception& e) {
+      errors[p] = e.what();
+    }
+  };
   std::vector<std::thread> pool;
-  for (size_t p = 0; p < parts.size(); ++p) {
-    pool.emplace_back([&, p] {
-      try {
-        results[p] = parse_chunk(src.substr(parts[p].first, parts[p].second - parts[p].first),
-                                 line_base[p], schema);
-      } catch (const std::exception& e) {
-        errors[p] = e.what();
-      }
-    });
+  size_t started = 0;
+  try {
+    for (; started < parts.size(); ++started) pool.emplace_back(parse, started);
+  } catch (const std::system_error&) {
+    // no more threads (the process's limit under load): the rest parse on this thread
+    // (a joinable std::thread must never be destroyed)
+    for (size_t p = started; p < parts.size(); ++p) parse(p);
   }
   for (auto& th : pool) th.join();
   for (auto& e : errors)
