@@ -104,14 +104,8 @@ def _shares_worker(rank, port, q, device="cpu"):
         D = rep.dot(s, rep.local(s, X, "Reshape", shape=(1, 257)),
                     rep.local(s, X, "Reshape", shape=(257, 1)))
         B = rep.bit_decompose(s, X)  # per-party fused Kogge-Stone levels (SPMD p_ks_level)
-        # a 256^3 product: each party's asymmetric local product (ring.dot_cross_asym)
-        big = R.encode(torch.linspace(-1, 1, 256 * 256, dtype=torch.float64).reshape(256, 256),
-                       23, bits)
-        X2 = rep.share(s, plc, HV("b", R.RT(big.data.to(device), bits) if rank == 1
-                                   else _remote(bits)))
-        D2 = rep.dot(s, X2, X2)
-        out[bits] = ([t.s0.v.data.cpu().clone() for t in (X, Y, D, B, D2)]
-                     + [t.s1.v.data.cpu().clone() for t in (X, Y, D, B, D2)])
+        out[bits] = ([t.s0.v.data.cpu().clone() for t in (X, Y, D, B)]
+                     + [t.s1.v.data.cpu().clone() for t in (X, Y, D, B)])
     q.put((rank, {b: [t.numpy() for t in v] for b, v in out.items()}))
     dist.barrier()
     dist.destroy_process_group()
@@ -127,8 +121,7 @@ def _remote(bits):
 def test_spmd_shares_bitwise_equal_stacked(device):
     """One process per party (gloo; on the GPU all three share the test device and stage
     messages through the host): shares after Share / TruncPr (per-party kernels) / Dot /
-    BitDecompose, and a 256^3 Dot (asymmetric local products), equal the stacked generic
-    protocol bit for bit."""
+    BitDecompose equal the stacked generic protocol bit for bit."""
     from moose_amd.protocols import replicated as rep
     from moose_amd.runtime.session import HV
     from moose_amd.runtime.session import StackedSession
@@ -153,12 +146,7 @@ def test_spmd_shares_bitwise_equal_stacked(device):
         D = rep.dot(s, rep.local(s, X, "Reshape", shape=(1, 257)),
                     rep.local(s, X, "Reshape", shape=(257, 1)))
         B = rep.bit_decompose(s, X)  # generic per-step protocol (fused=False)
-        big = R.encode(torch.linspace(-1, 1, 256 * 256, dtype=torch.float64).reshape(256, 256),
-                       23, bits)
-        X2 = rep.share(s, plc, HV("b", big))
-        D2 = rep.dot(s, X2, X2)
-        stacked = ([t.s0.v.data for t in (X, Y, D, B, D2)]
-                   + [t.s1.v.data for t in (X, Y, D, B, D2)])
+        stacked = [t.s0.v.data for t in (X, Y, D, B)] + [t.s1.v.data for t in (X, Y, D, B)]
         for i, st in enumerate(stacked):
             for p in range(3):
                 assert np.array_equal(res[p][bits][i], st[p].numpy()), (bits, i, p)
